@@ -1,0 +1,79 @@
+// Shared device helpers for the gfx950 (MI355X / CDNA4) kernels of pyspark_tf_gke_amd.
+//
+// Conventions used by every kernel in csrc/kernels:
+//   * bf16 tensors are carried as raw uint16_t storage (bf16_t) and converted with
+//     bf2f / f2bf (f2bf lowers to v_cvt_pk_bf16_f32, round-to-nearest-even, NaN-preserving).
+//   * wave64: lane = threadIdx.x & 63, wave = threadIdx.x >> 6. Never 32.
+//   * every host entry point is `extern "C" int ptg_*(..., hipStream_t)` returning the
+//     hipError_t of the launch, so the Python side can fail loudly.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef uint16_t bf16_t;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;   // MFMA A/B fragment (4 VGPRs)
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;     // 16x16 MFMA accumulator
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;   // 32x32 MFMA accumulator
+
+struct alignas(16) U4 { uint32_t x, y, z, w; };
+struct alignas(8) U2 { uint32_t x, y; };
+
+#define PTG_DEV __device__ __forceinline__
+
+PTG_DEV float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+PTG_DEV bf16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(bf16_t, b);
+}
+PTG_DEV float lo_bf(uint32_t w) { return __uint_as_float(w << 16); }
+PTG_DEV float hi_bf(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+PTG_DEV uint32_t pack_bf(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+// unpack a 16-byte vector of 8 bf16 into floats
+PTG_DEV void unpack8(const U4& v, float* f) {
+  f[0] = lo_bf(v.x); f[1] = hi_bf(v.x); f[2] = lo_bf(v.y); f[3] = hi_bf(v.y);
+  f[4] = lo_bf(v.z); f[5] = hi_bf(v.z); f[6] = lo_bf(v.w); f[7] = hi_bf(v.w);
+}
+PTG_DEV U4 pack8(const float* f) {
+  U4 v;
+  v.x = pack_bf(f[0], f[1]); v.y = pack_bf(f[2], f[3]);
+  v.z = pack_bf(f[4], f[5]); v.w = pack_bf(f[6], f[7]);
+  return v;
+}
+PTG_DEV U4 zero4() { U4 z; z.x = z.y = z.z = z.w = 0u; return z; }
+
+PTG_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+PTG_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum for blockDim.x == 256 (4 waves). `scratch` must hold >= 4 floats.
+PTG_DEV float block_sum256(float v, float* scratch) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) scratch[w] = v;
+  __syncthreads();
+  float r = scratch[0] + scratch[1] + scratch[2] + scratch[3];
+  return r;
+}
+
+// XCD-aware, bijective remap of a linear workgroup id (cdna_hip_programming.md §5, T1):
+// blocks b and b+8 share an XCD under round-robin dispatch; give each XCD a contiguous
+// chunk of the tile space so neighbouring tiles share that XCD's L2.
+PTG_DEV int xcd_remap(int bid, int nwg) {
+  if (nwg < 16) return bid;
+  const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+}
+
+static inline int ptg_ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
+
+#define PTG_RETURN_LAUNCH() return (int)hipGetLastError()

@@ -1,0 +1,447 @@
+// MFMA GEMM engine for gfx950 + implicit-GEMM 2-D convolution (fwd / dgrad / wgrad).
+//
+// One templated main loop serves every matmul-shaped op of the training runtime:
+//   Dense fwd / dX / dW (TF `Dense`, reference train_tf_ps.py:332-335, :366-367) and
+//   Conv2D fwd / dgrad / wgrad (TF `Conv2D(k, 5, padding="same")`, train_tf_ps.py:351-363).
+// The reference gets these from cuBLAS/cuDNN inside TensorFlow; here they are hand-written
+// around v_mfma_f32_16x16x32_bf16 (bf16 in, fp32 accumulate).
+//
+// Structure (cdna_hip_programming.md §5 "standard MFMA GEMM main loop"):
+//   * 256 threads = 4 waves arranged WM x WN; each wave owns a (BM/WM) x (BN/WN) sub-tile made
+//     of 16x16 MFMA fragments; accumulators indexed by fragment repeat only.
+//   * BK = 32 K-step, two LDS buffers; the next tile's global loads are issued into registers
+//     before the MFMAs of the current tile and written to the other LDS buffer after them,
+//     one barrier per K-step.
+//   * LDS images are [rows][BK] with k contiguous (80-byte padded rows), so every A and B
+//     fragment is one 16-byte ds_read.  Operands whose source memory is k-contiguous are staged
+//     with 16-byte stores; operands whose source is row-contiguous (transposed use of a matrix,
+//     the im2col^T of wgrad) are loaded as 16-byte row vectors and scattered into the image.
+//   * Operand "loaders" turn (row, k) into a 16-byte vector: plain matrices, the implicit im2col
+//     gather of a NHWC activation, the flipped/transposed filter of dgrad, the im2col^T of wgrad.
+//     The convolution therefore never materialises its im2col matrix.
+//   * blockIdx.x is remapped XCD-aware (T1) so tiles that share operand panels share an L2;
+//     blockIdx.y indexes split-K slices (fp32 atomic epilogue).
+#include "common.h"
+
+namespace ptg {
+
+constexpr int BK = 32;
+constexpr int LDK = BK + 8;  // padded LDS row: 40 bf16 = 80 B (16-B aligned)
+
+// ------------------------------------------------------------------------------------------
+// Operand loaders. K_CONTIG loaders return elements (r, k..k+7); the others return
+// elements (r..r+7, k).  Ctx caches the per-row decode so the K loop only does k-math.
+// ------------------------------------------------------------------------------------------
+template <int VEC>
+struct MatK {  // element(r,k) = p[r*ld + k]; ld % VEC == 0, K % 8 == 0 or zero-padded rows
+  static constexpr bool K_CONTIG = true;
+  const bf16_t* p; long ld; int R; int K;
+  struct Ctx { const bf16_t* row; bool ok; };
+  PTG_DEV Ctx ctx(int r) const { Ctx c; c.ok = r < R; c.row = p + (long)(c.ok ? r : 0) * ld; return c; }
+  PTG_DEV U4 load(const Ctx& c, int k) const {
+    if (!c.ok || k >= K) return zero4();
+    if constexpr (VEC == 8) {
+      return *(const U4*)(c.row + k);
+    } else {
+      U2 a = *(const U2*)(c.row + k);
+      U2 b = (k + 4 < K) ? *(const U2*)(c.row + k + 4) : U2{0u, 0u};
+      U4 v; v.x = a.x; v.y = a.y; v.z = b.x; v.w = b.y; return v;
+    }
+  }
+};
+
+struct MatMN {  // element(r,k) = p[k*ld + r]; R % 8 == 0, ld % 8 == 0
+  static constexpr bool K_CONTIG = false;
+  const bf16_t* p; long ld; int R; int K;
+  struct Ctx { const bf16_t* col; bool ok; };
+  PTG_DEV Ctx ctx(int r0) const { Ctx c; c.ok = r0 < R; c.col = p + (c.ok ? r0 : 0); return c; }
+  PTG_DEV U4 load(const Ctx& c, int k) const {
+    if (!c.ok || k >= K) return zero4();
+    return *(const U4*)(c.col + (long)k * ld);
+  }
+};
+
+// Implicit im2col of an NHWC activation: row m = output pixel (n, oh, ow); k = (kh, kw, ci).
+// C is a power of two; CVEC = 8 (C % 8 == 0, one 16-B load) or 4 (C == 4, two 8-B loads).
+template <int CVEC>
+struct ConvFwdA {
+  static constexpr bool K_CONTIG = true;
+  const bf16_t* x; int H, W, C, logC, OH, OW, KW, stride, pad, M, Kc;
+  struct Ctx { const bf16_t* img; int ih0, iw0; bool ok; };
+  PTG_DEV Ctx ctx(int m) const {
+    Ctx c; c.ok = m < M; if (!c.ok) m = 0;
+    const int ohw = OH * OW;
+    const int n = m / ohw, rem = m - n * ohw, oh = rem / OW, ow = rem - oh * OW;
+    c.img = x + (long)n * H * W * C; c.ih0 = oh * stride - pad; c.iw0 = ow * stride - pad;
+    return c;
+  }
+  PTG_DEV const bf16_t* at(const Ctx& c, int k, bool& ok) const {
+    const int pos = k >> logC, ci = k & (C - 1);
+    const int kh = pos / KW, kw = pos - kh * KW;
+    const int ih = c.ih0 + kh, iw = c.iw0 + kw;
+    ok = (k < Kc) && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+    return c.img + ((long)ih * W + iw) * C + ci;
+  }
+  PTG_DEV U4 load(const Ctx& c, int k) const {
+    if (!c.ok) return zero4();
+    if constexpr (CVEC == 8) {
+      bool ok; const bf16_t* p = at(c, k, ok);
+      return ok ? *(const U4*)p : zero4();
+    } else {
+      bool ok0, ok1;
+      const bf16_t* p0 = at(c, k, ok0);
+      const bf16_t* p1 = at(c, k + 4, ok1);
+      U2 a = ok0 ? *(const U2*)p0 : U2{0u, 0u};
+      U2 b = ok1 ? *(const U2*)p1 : U2{0u, 0u};
+      U4 v; v.x = a.x; v.y = a.y; v.z = b.x; v.w = b.y; return v;
+    }
+  }
+};
+
+// dgrad filter: rows = input channel ci (8 at a time), k = (kh', kw', co) of the flipped filter
+// W'[ci][kh'][kw'][co] = W[co][KH-1-kh'][KW-1-kw'][ci]. W is stored [Cout][KH][KW][Cin].
+struct ConvDgradB {
+  static constexpr bool K_CONTIG = false;
+  const bf16_t* w; int Cin, Cout, logCout, KH, KW, Kc2;
+  struct Ctx { int ci0; bool ok; };
+  PTG_DEV Ctx ctx(int r0) const { Ctx c; c.ci0 = r0; c.ok = r0 < Cin; return c; }
+  PTG_DEV U4 load(const Ctx& c, int k) const {
+    if (!c.ok || k >= Kc2) return zero4();
+    const int pos = k >> logCout, co = k & (Cout - 1);
+    const int kh = pos / KW, kw = pos - kh * KW;
+    const long off = ((long)co * KH * KW + (KH - 1 - kh) * KW + (KW - 1 - kw)) * Cin + c.ci0;
+    return *(const U4*)(w + off);
+  }
+};
+
+// wgrad im2col^T: rows = kc = (kh, kw, ci) (8 at a time), k = output pixel (n, oh, ow).
+template <int CVEC>
+struct ConvWgradB {
+  static constexpr bool K_CONTIG = false;
+  const bf16_t* x; int H, W, C, logC, OH, OW, KW, stride, pad, P, Kc;
+  struct Ctx { int dh0, dw0, ci0, dh1, dw1, ci1; bool ok0, ok1; };
+  PTG_DEV Ctx ctx(int r0) const {
+    Ctx c;
+    int pos = r0 >> logC; c.ci0 = r0 & (C - 1);
+    c.dh0 = pos / KW - pad; c.dw0 = pos % KW - pad; c.ok0 = r0 < Kc;
+    int r1 = r0 + 4; pos = r1 >> logC; c.ci1 = r1 & (C - 1);
+    c.dh1 = pos / KW - pad; c.dw1 = pos % KW - pad; c.ok1 = r1 < Kc;
+    return c;
+  }
+  PTG_DEV U4 load(const Ctx& c, int k) const {
+    if (!c.ok0 || k >= P) return zero4();
+    const int ohw = OH * OW;
+    const int n = k / ohw, rem = k - n * ohw, oh = rem / OW, ow = rem - oh * OW;
+    const bf16_t* img = x + (long)n * H * W * C;
+    const int ih0 = oh * stride + c.dh0, iw0 = ow * stride + c.dw0;
+    if constexpr (CVEC == 8) {
+      if ((unsigned)ih0 >= (unsigned)H || (unsigned)iw0 >= (unsigned)W) return zero4();
+      return *(const U4*)(img + ((long)ih0 * W + iw0) * C + c.ci0);
+    } else {
+      U2 a = U2{0u, 0u}, b = U2{0u, 0u};
+      if ((unsigned)ih0 < (unsigned)H && (unsigned)iw0 < (unsigned)W)
+        a = *(const U2*)(img + ((long)ih0 * W + iw0) * C + c.ci0);
+      const int ih1 = oh * stride + c.dh1, iw1 = ow * stride + c.dw1;
+      if (c.ok1 && (unsigned)ih1 < (unsigned)H && (unsigned)iw1 < (unsigned)W)
+        b = *(const U2*)(img + ((long)ih1 * W + iw1) * C + c.ci1);
+      U4 v; v.x = a.x; v.y = a.y; v.z = b.x; v.w = b.y; return v;
+    }
+  }
+};
+
+// ------------------------------------------------------------------------------------------
+// Epilogues: called per accumulator element (m, n) inside bounds.
+// ------------------------------------------------------------------------------------------
+enum { ACT_NONE = 0, ACT_RELU = 1 };
+
+struct EpiBf16 {  // out[m*ldc+n] = act(acc + bias[n]) as bf16 (optionally also fp32)
+  bf16_t* out; long ldc; const float* bias; int act; float* out32;
+  PTG_DEV void operator()(int m, int n, float v) const {
+    if (bias) v += bias[n];
+    if (act == ACT_RELU) v = fmaxf(v, 0.f);
+    out[(long)m * ldc + n] = f2bf(v);
+    if (out32) out32[(long)m * ldc + n] = v;
+  }
+};
+struct EpiF32 {  // out[m*ldc+n] (=|+=) act(acc + bias)
+  float* out; long ldc; const float* bias; int act; int accumulate;
+  PTG_DEV void operator()(int m, int n, float v) const {
+    if (bias) v += bias[n];
+    if (act == ACT_RELU) v = fmaxf(v, 0.f);
+    float* p = out + (long)m * ldc + n;
+    if (accumulate) *p += v; else *p = v;
+  }
+};
+struct EpiAtomic {  // split-K: out[m*ldc+n] += acc  (device-scope fp32 atomic, no return)
+  float* out; long ldc;
+  PTG_DEV void operator()(int m, int n, float v) const { atomicAdd(out + (long)m * ldc + n, v); }
+};
+
+// ------------------------------------------------------------------------------------------
+// The main loop.
+// ------------------------------------------------------------------------------------------
+template <int BM, int BN, int WM, int WN, class LA, class LB, class EPI>
+__global__ __launch_bounds__(256) void gemm_kernel(LA la, LB lb, EPI epi, int M, int N, int K,
+                                                   int kchunk) {
+  constexpr int WTM = BM / WM, WTN = BN / WN, FM = WTM / 16, FN = WTN / 16;
+  static_assert(WM * WN == 4, "4 waves");
+  static_assert(FM >= 1 && FN >= 1, "wave tile >= 16x16");
+  constexpr int AV = BM * BK / 8, BV = BN * BK / 8;  // 16-B vectors per operand tile
+  constexpr int AI = (AV + 255) / 256, BI = (BV + 255) / 256;
+  // one LDS array (A and B images of both stages)
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * (BM + BN) * LDK];
+  bf16_t* sA0 = smem;
+  bf16_t* sB0 = smem + BM * LDK;
+  constexpr int STAGE = (BM + BN) * LDK;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int tiles_n = (N + BN - 1) / BN;
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = t / tiles_n, tn = t - tm * tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kb = blockIdx.y * kchunk;
+  const int ke = min(K, kb + kchunk);
+  if (kb >= ke) return;
+  const int nk = (ke - kb + BK - 1) / BK;
+
+  typename LA::Ctx ca[AI]; int akk[AI], aoff[AI]; bool aon[AI];
+  typename LB::Ctx cb[BI]; int bkk[BI], boff[BI]; bool bon[BI];
+#pragma unroll
+  for (int i = 0; i < AI; ++i) {
+    const int v = tid + i * 256;
+    aon[i] = v < AV;
+    if constexpr (LA::K_CONTIG) {
+      const int r = v / (BK / 8), kv = v % (BK / 8);
+      ca[i] = la.ctx(m0 + r); akk[i] = kv * 8; aoff[i] = r * LDK + kv * 8;
+    } else {
+      const int kk = v / (BM / 8), rv = v % (BM / 8);
+      ca[i] = la.ctx(m0 + rv * 8); akk[i] = kk; aoff[i] = rv * 8 * LDK + kk;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < BI; ++i) {
+    const int v = tid + i * 256;
+    bon[i] = v < BV;
+    if constexpr (LB::K_CONTIG) {
+      const int r = v / (BK / 8), kv = v % (BK / 8);
+      cb[i] = lb.ctx(n0 + r); bkk[i] = kv * 8; boff[i] = r * LDK + kv * 8;
+    } else {
+      const int kk = v / (BN / 8), rv = v % (BN / 8);
+      cb[i] = lb.ctx(n0 + rv * 8); bkk[i] = kk; boff[i] = rv * 8 * LDK + kk;
+    }
+  }
+
+  U4 ra[AI], rb[BI];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < AI; ++i) ra[i] = aon[i] ? la.load(ca[i], k0 + akk[i]) : zero4();
+#pragma unroll
+    for (int i = 0; i < BI; ++i) rb[i] = bon[i] ? lb.load(cb[i], k0 + bkk[i]) : zero4();
+  };
+  auto scatter = [](bf16_t* dst, const U4& v) {
+    dst[0 * LDK] = (bf16_t)(v.x & 0xffff); dst[1 * LDK] = (bf16_t)(v.x >> 16);
+    dst[2 * LDK] = (bf16_t)(v.y & 0xffff); dst[3 * LDK] = (bf16_t)(v.y >> 16);
+    dst[4 * LDK] = (bf16_t)(v.z & 0xffff); dst[5 * LDK] = (bf16_t)(v.z >> 16);
+    dst[6 * LDK] = (bf16_t)(v.w & 0xffff); dst[7 * LDK] = (bf16_t)(v.w >> 16);
+  };
+  auto sstore = [&](int stage) {
+    bf16_t* sA = sA0 + stage * STAGE;
+    bf16_t* sB = sB0 + stage * STAGE;
+#pragma unroll
+    for (int i = 0; i < AI; ++i)
+      if (aon[i]) {
+        if constexpr (LA::K_CONTIG) *(U4*)(sA + aoff[i]) = ra[i];
+        else scatter(sA + aoff[i], ra[i]);
+      }
+#pragma unroll
+    for (int i = 0; i < BI; ++i)
+      if (bon[i]) {
+        if constexpr (LB::K_CONTIG) *(U4*)(sB + boff[i]) = rb[i];
+        else scatter(sB + boff[i], rb[i]);
+      }
+  };
+
+  f32x4_t acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  gload(kb);
+  sstore(0);
+  __syncthreads();
+  const int frow = lane & 15, fk = 8 * (lane >> 4);
+  for (int it = 0; it < nk; ++it) {
+    const int cur = it & 1;
+    if (it + 1 < nk) gload(kb + (it + 1) * BK);
+    const bf16_t* sA = sA0 + cur * STAGE;
+    const bf16_t* sB = sB0 + cur * STAGE;
+    bf16x8_t af[FM], bfr[FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+      af[i] = *(const bf16x8_t*)(sA + (wm * WTM + i * 16 + frow) * LDK + fk);
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+      bfr[j] = *(const bf16x8_t*)(sB + (wn * WTN + j * 16 + frow) * LDK + fk);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    if (it + 1 < nk) sstore(cur ^ 1);
+    __syncthreads();
+  }
+
+  // C/D map of mfma_f32_16x16x32: col = lane&15, row = (lane>>4)*4 + r
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * WTM + i * 16 + (lane >> 4) * 4 + r;
+        const int n = n0 + wn * WTN + j * 16 + (lane & 15);
+        if (m < M && n < N) epi(m, n, acc[i][j][r]);
+      }
+}
+
+template <int BM, int BN, int WM, int WN, class LA, class LB, class EPI>
+static int launch_gemm(const LA& la, const LB& lb, const EPI& epi, int M, int N, int K, int splits,
+                       hipStream_t s) {
+  const int tiles = ptg_ceil_div(M, BM) * ptg_ceil_div(N, BN);
+  if (splits < 1) splits = 1;
+  int kchunk = ptg_ceil_div(ptg_ceil_div(K, splits), BK) * BK;
+  if (kchunk < BK) kchunk = BK;
+  splits = ptg_ceil_div(K, kchunk);
+  dim3 grid(tiles, splits);
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, LA, LB, EPI>), grid, dim3(256), 0, s, la, lb, epi, M,
+                     N, K, kchunk);
+  PTG_RETURN_LAUNCH();
+}
+
+// Tile-shape choice. N is the narrow dimension for convolutions (output channels).
+template <class LA, class LB, class EPI>
+static int dispatch_gemm(const LA& la, const LB& lb, const EPI& epi, int M, int N, int K, int splits,
+                         hipStream_t s) {
+  if (N <= 16) return launch_gemm<256, 16, 4, 1>(la, lb, epi, M, N, K, splits, s);
+  if (N <= 32) return launch_gemm<256, 32, 4, 1>(la, lb, epi, M, N, K, splits, s);
+  if (N <= 64) return launch_gemm<128, 64, 2, 2>(la, lb, epi, M, N, K, splits, s);
+  if (M <= 64) return launch_gemm<64, 128, 1, 4>(la, lb, epi, M, N, K, splits, s);
+  return launch_gemm<128, 128, 2, 2>(la, lb, epi, M, N, K, splits, s);
+}
+
+// Narrow-M variant (wgrad: M = output channels).
+template <class LA, class LB, class EPI>
+static int dispatch_gemm_narrow_m(const LA& la, const LB& lb, const EPI& epi, int M, int N, int K,
+                                  int splits, hipStream_t s) {
+  if (M <= 16) return launch_gemm<16, 128, 1, 4>(la, lb, epi, M, N, K, splits, s);
+  if (M <= 32) return launch_gemm<32, 128, 1, 4>(la, lb, epi, M, N, K, splits, s);
+  if (M <= 64) return launch_gemm<64, 128, 1, 4>(la, lb, epi, M, N, K, splits, s);
+  return launch_gemm<128, 128, 2, 2>(la, lb, epi, M, N, K, splits, s);
+}
+
+static int ilog2(int v) { int l = 0; while ((1 << l) < v) ++l; return l; }
+static bool is_pow2(int v) { return v > 0 && (v & (v - 1)) == 0; }
+
+}  // namespace ptg
+
+using namespace ptg;
+
+extern "C" {
+
+// Generic bf16 GEMM: C[M][N] = sum_k A(m,k) B(k,n).
+//   a_kcontig: A(m,k) = A[m*lda + k]  else A(m,k) = A[k*lda + m]
+//   b_kcontig: B(k,n) = B[n*ldb + k]  else B(k,n) = B[k*ldb + n]
+//   epi: 0 = bf16 store (+bias, act); 1 = fp32 store (+bias, act); 2 = fp32 accumulate (+=);
+//        3 = fp32 atomic add (split-K; caller zeroes C)
+int ptg_gemm_bf16(int M, int N, int K, const void* A, long lda, int a_kcontig, const void* B, long ldb,
+                  int b_kcontig, int epi, void* C, long ldc, const float* bias, int act, int splits,
+                  hipStream_t s) {
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  if (epi != 3) splits = 1;
+  const bf16_t* a = (const bf16_t*)A; const bf16_t* b = (const bf16_t*)B;
+#define PTG_EPI_SWITCH(LAX, LBX)                                                                 \
+  switch (epi) {                                                                                 \
+    case 0: return dispatch_gemm(LAX, LBX, EpiBf16{(bf16_t*)C, ldc, bias, act, nullptr}, M, N, K, \
+                                 1, s);                                                          \
+    case 1: return dispatch_gemm(LAX, LBX, EpiF32{(float*)C, ldc, bias, act, 0}, M, N, K, 1, s); \
+    case 2: return dispatch_gemm(LAX, LBX, EpiF32{(float*)C, ldc, bias, act, 1}, M, N, K, 1, s); \
+    case 3: return dispatch_gemm(LAX, LBX, EpiAtomic{(float*)C, ldc}, M, N, K, splits, s);       \
+    default: return (int)hipErrorInvalidValue;                                                   \
+  }
+  if (a_kcontig && b_kcontig) {
+    if (lda % 8 || ldb % 8 || K % 8) return (int)hipErrorInvalidValue;
+    MatK<8> la{a, lda, M, K}; MatK<8> lb{b, ldb, N, K};
+    PTG_EPI_SWITCH(la, lb)
+  } else if (a_kcontig && !b_kcontig) {
+    if (lda % 8 || ldb % 8 || K % 8 || N % 8) return (int)hipErrorInvalidValue;
+    MatK<8> la{a, lda, M, K}; MatMN lb{b, ldb, N, K};
+    PTG_EPI_SWITCH(la, lb)
+  } else if (!a_kcontig && !b_kcontig) {
+    if (lda % 8 || ldb % 8 || M % 8 || N % 8) return (int)hipErrorInvalidValue;
+    MatMN la{a, lda, M, K}; MatMN lb{b, ldb, N, K};
+    PTG_EPI_SWITCH(la, lb)
+  } else {
+    if (lda % 8 || ldb % 8 || M % 8 || K % 8) return (int)hipErrorInvalidValue;
+    MatMN la{a, lda, M, K}; MatK<8> lb{b, ldb, N, K};
+    PTG_EPI_SWITCH(la, lb)
+  }
+#undef PTG_EPI_SWITCH
+}
+
+// Conv2D forward, NHWC bf16: z[n][oh][ow][co] = bias[co] + sum_{kh,kw,ci} x[..] w[co][kh][kw][ci]
+// w is [Cout][KH*KW*C] bf16. C must be a power of two >= 4.
+int ptg_conv2d_fwd(const void* x, const void* w, const float* bias, void* z, int N, int H, int W, int C,
+                   int Cout, int KH, int KW, int stride, int pad, int OH, int OW, int act,
+                   hipStream_t s) {
+  if (!is_pow2(C) || C < 4) return (int)hipErrorInvalidValue;
+  const int M = N * OH * OW, Kc = KH * KW * C;
+  EpiBf16 epi{(bf16_t*)z, Cout, bias, act, nullptr};
+  if (C % 8 == 0) {
+    ConvFwdA<8> la{(const bf16_t*)x, H, W, C, ilog2(C), OH, OW, KW, stride, pad, M, Kc};
+    MatK<8> lb{(const bf16_t*)w, Kc, Cout, Kc};
+    return dispatch_gemm(la, lb, epi, M, Cout, Kc, 1, s);
+  } else {
+    ConvFwdA<4> la{(const bf16_t*)x, H, W, C, ilog2(C), OH, OW, KW, stride, pad, M, Kc};
+    MatK<4> lb{(const bf16_t*)w, Kc, Cout, Kc};
+    return dispatch_gemm(la, lb, epi, M, Cout, Kc, 1, s);
+  }
+}
+
+// Conv2D data gradient for stride-1 convolutions: dx = conv(dz, flip(w)^T, pad' = K-1-pad).
+// dz [N][H][W][Cout] (Cout power of two >= 8), dx [N][H][W][Cin] (Cin % 8 == 0).
+int ptg_conv2d_dgrad(const void* dz, const void* w, void* dx, int N, int H, int W, int Cin, int Cout,
+                     int KH, int KW, int pad, hipStream_t s) {
+  if (!is_pow2(Cout) || Cout < 8 || Cin % 8) return (int)hipErrorInvalidValue;
+  const int M = N * H * W, Kc2 = KH * KW * Cout;
+  ConvFwdA<8> la{(const bf16_t*)dz, H, W, Cout, ilog2(Cout), H, W, KW, 1, KH - 1 - pad, M, Kc2};
+  ConvDgradB lb{(const bf16_t*)w, Cin, Cout, ilog2(Cout), KH, KW, Kc2};
+  EpiBf16 epi{(bf16_t*)dx, Cin, nullptr, ACT_NONE, nullptr};
+  return dispatch_gemm(la, lb, epi, M, Cin, Kc2, 1, s);
+}
+
+// Conv2D weight gradient: dw[co][kc] (+)= sum_pixels dz[p][co] * im2col(x)[p][kc], fp32.
+// Split-K over output pixels with fp32 atomics; dw must be zeroed (or hold a sum to add to).
+int ptg_conv2d_wgrad(const void* x, const void* dz, float* dw, int N, int H, int W, int C, int Cout,
+                     int KH, int KW, int stride, int pad, int OH, int OW, int splits, hipStream_t s) {
+  if (!is_pow2(C) || C < 4 || Cout % 8) return (int)hipErrorInvalidValue;
+  const int P = N * OH * OW, Kc = KH * KW * C;
+  MatMN la{(const bf16_t*)dz, Cout, Cout, P};
+  EpiAtomic epi{dw, Kc};
+  if (splits <= 0) {
+    const int tiles = ptg_ceil_div(Cout, Cout <= 16 ? 16 : (Cout <= 32 ? 32 : 64)) * ptg_ceil_div(Kc, 128);
+    splits = ptg_ceil_div(1024, tiles);
+    const int max_splits = ptg_ceil_div(P, 4 * BK);
+    if (splits > max_splits) splits = max_splits;
+  }
+  if (C % 8 == 0) {
+    ConvWgradB<8> lb{(const bf16_t*)x, H, W, C, ilog2(C), OH, OW, KW, stride, pad, P, Kc};
+    return dispatch_gemm_narrow_m(la, lb, epi, Cout, Kc, P, splits, s);
+  } else {
+    ConvWgradB<4> lb{(const bf16_t*)x, H, W, C, ilog2(C), OH, OW, KW, stride, pad, P, Kc};
+    return dispatch_gemm_narrow_m(la, lb, epi, Cout, Kc, P, splits, s);
+  }
+}
+
+}  // extern "C"

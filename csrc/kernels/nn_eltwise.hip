@@ -1,0 +1,647 @@
+// Memory-bound kernels of the training runtime (gfx950): PReLU (+ fused 2x2 max-pool) forward and
+// backward, bias/activation epilogues, skinny dense layers, losses + metrics, fused flat Adam,
+// image resize/normalise.  Reference semantics (TF/Keras inside train_tf_ps.py):
+//   PReLU with per-element alpha (Keras default shared_axes=None)      train_tf_ps.py:352-364
+//   MaxPooling2D(2x2, stride 2, valid)                                  train_tf_ps.py:353-362
+//   Dense(relu/linear/softmax)                                          train_tf_ps.py:332-335,366-367
+//   MeanSquaredError + MAE/MSE metrics                                  train_tf_ps.py:375-376,729-731
+//   SparseCategoricalCrossentropy + accuracy                            train_tf_ps.py:340-341,607-608
+//   Adam (epsilon 1e-7, Keras bias-corrected form)                      train_tf_ps.py:339,374,606,728
+//   tf.image.resize bilinear (half-pixel centres) then /255             train_tf_ps.py:301-306
+// All bf16 traffic is 16 B per lane (8 channels); channel counts are multiples of 8 except the
+// 4-channel padded image.
+#include "common.h"
+
+// ----------------------------------------------------------------------------------------------
+// PReLU + 2x2 max-pool forward: p[n][ph][pw][c] = max_{2x2} prelu(z), prelu(z) = z>0 ? z : a*z.
+// ----------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void prelu_pool_fwd_k(const bf16_t* __restrict__ z,
+                                                        const float* __restrict__ alpha,
+                                                        bf16_t* __restrict__ p, int N, int H, int W,
+                                                        int C) {
+  const int PH = H >> 1, PW = W >> 1, C8 = C >> 3;
+  const long total = (long)N * PH * PW * C8;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int c8 = i % C8;
+    long t = i / C8;
+    const int pw = t % PW; t /= PW;
+    const int ph = t % PH; const int n = t / PH;
+    float best[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) best[j] = -INFINITY;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int h = 2 * ph + (q >> 1), w = 2 * pw + (q & 1);
+      const long off = (((long)n * H + h) * W + w) * C + c8 * 8;
+      const long aoff = ((long)h * W + w) * C + c8 * 8;
+      float zv[8];
+      unpack8(*(const U4*)(z + off), zv);
+      const float4 a0 = *(const float4*)(alpha + aoff), a1 = *(const float4*)(alpha + aoff + 4);
+      const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float y = zv[j] > 0.f ? zv[j] : av[j] * zv[j];
+        best[j] = fmaxf(best[j], y);
+      }
+    }
+    *(U4*)(p + i * 8) = pack8(best);
+  }
+}
+
+// Backward of prelu+pool. Grid: x over pooled (ph, pw, c8) vectors, y over batch chunks.
+// dz is written for every element (zero where not the window's first argmax).
+// dalpha[h][w][c] += sum_n dA * min(z,0)  (dA = routed pooled gradient), dbias[c] += sum dz.
+__global__ __launch_bounds__(256) void prelu_pool_bwd_k(const bf16_t* __restrict__ dp,
+                                                        const bf16_t* __restrict__ z,
+                                                        const float* __restrict__ alpha,
+                                                        bf16_t* __restrict__ dz, float* __restrict__ dalpha,
+                                                        float* __restrict__ dbias, int N, int H, int W,
+                                                        int C, int nper) {
+  __shared__ float sbias[256];
+  const int PH = H >> 1, PW = W >> 1, C8 = C >> 3;
+  const int npos = PH * PW * C8;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  sbias[threadIdx.x] = 0.f;
+  __syncthreads();
+  const int n0 = blockIdx.y * nper, n1 = min(N, n0 + nper);
+  if (i < npos) {
+    const int c8 = i % C8;
+    const int t = i / C8;
+    const int pw = t % PW, ph = t / PW;
+    float da[4][8], db[8];
+    float av[4][8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int h = 2 * ph + (q >> 1), w = 2 * pw + (q & 1);
+      const long aoff = ((long)h * W + w) * C + c8 * 8;
+      const float4 a0 = *(const float4*)(alpha + aoff), a1 = *(const float4*)(alpha + aoff + 4);
+      av[q][0] = a0.x; av[q][1] = a0.y; av[q][2] = a0.z; av[q][3] = a0.w;
+      av[q][4] = a1.x; av[q][5] = a1.y; av[q][6] = a1.z; av[q][7] = a1.w;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) da[q][j] = 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) db[j] = 0.f;
+    for (int n = n0; n < n1; ++n) {
+      float g[8];
+      unpack8(*(const U4*)(dp + (((long)n * PH + ph) * PW + pw) * C + c8 * 8), g);
+      float zv[4][8], y[4][8];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int h = 2 * ph + (q >> 1), w = 2 * pw + (q & 1);
+        unpack8(*(const U4*)(z + (((long)n * H + h) * W + w) * C + c8 * 8), zv[q]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) y[q][j] = zv[q][j] > 0.f ? zv[q][j] : av[q][j] * zv[q][j];
+      }
+      int arg[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        int a = 0; float b = y[0][j];
+#pragma unroll
+        for (int q = 1; q < 4; ++q)
+          if (y[q][j] > b) { b = y[q][j]; a = q; }
+        arg[j] = a;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int h = 2 * ph + (q >> 1), w = 2 * pw + (q & 1);
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float gq = (arg[j] == q) ? g[j] : 0.f;
+          const float zz = zv[q][j];
+          o[j] = zz > 0.f ? gq : gq * av[q][j];
+          da[q][j] += zz > 0.f ? 0.f : gq * zz;
+          db[j] += o[j];
+        }
+        *(U4*)(dz + (((long)n * H + h) * W + w) * C + c8 * 8) = pack8(o);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int h = 2 * ph + (q >> 1), w = 2 * pw + (q & 1);
+      const long aoff = ((long)h * W + w) * C + c8 * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) atomicAdd(dalpha + aoff + j, da[q][j]);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) atomicAdd(&sbias[c8 * 8 + j], db[j]);
+  }
+  __syncthreads();
+  if (threadIdx.x < C) atomicAdd(dbias + threadIdx.x, sbias[threadIdx.x]);
+}
+
+// Plain PReLU forward (no pool): a = z>0 ? z : alpha[hwc]*z ; HWC = per-sample element count.
+__global__ __launch_bounds__(256) void prelu_fwd_k(const bf16_t* __restrict__ z,
+                                                   const float* __restrict__ alpha,
+                                                   bf16_t* __restrict__ a, long total8, int HWC8) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total8; i += (long)gridDim.x * 256) {
+    const long e = (i % HWC8) * 8;
+    float zv[8];
+    unpack8(*(const U4*)(z + i * 8), zv);
+    const float4 a0 = *(const float4*)(alpha + e), a1 = *(const float4*)(alpha + e + 4);
+    const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) zv[j] = zv[j] > 0.f ? zv[j] : av[j] * zv[j];
+    *(U4*)(a + i * 8) = pack8(zv);
+  }
+}
+
+// PReLU backward (no pool). Grid x over per-sample 8-vectors, y over batch chunks.
+__global__ __launch_bounds__(256) void prelu_bwd_k(const bf16_t* __restrict__ da,
+                                                   const bf16_t* __restrict__ z,
+                                                   const float* __restrict__ alpha,
+                                                   bf16_t* __restrict__ dz, float* __restrict__ dalpha,
+                                                   float* __restrict__ dbias, int N, int HWC, int C,
+                                                   int nper) {
+  __shared__ float sbias[256];
+  sbias[threadIdx.x] = 0.f;
+  __syncthreads();
+  const int HWC8 = HWC >> 3;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int n0 = blockIdx.y * nper, n1 = min(N, n0 + nper);
+  if (i < HWC8) {
+    const long e = (long)i * 8;
+    const int c0 = (int)(e % C);
+    const float4 a0 = *(const float4*)(alpha + e), a1 = *(const float4*)(alpha + e + 4);
+    const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    float dal[8] = {0, 0, 0, 0, 0, 0, 0, 0}, db[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int n = n0; n < n1; ++n) {
+      const long off = (long)n * HWC + e;
+      float g[8], zv[8], o[8];
+      unpack8(*(const U4*)(da + off), g);
+      unpack8(*(const U4*)(z + off), zv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        o[j] = zv[j] > 0.f ? g[j] : g[j] * av[j];
+        dal[j] += zv[j] > 0.f ? 0.f : g[j] * zv[j];
+        db[j] += o[j];
+      }
+      *(U4*)(dz + off) = pack8(o);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      atomicAdd(dalpha + e + j, dal[j]);
+      atomicAdd(&sbias[c0 + j], db[j]);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < C) atomicAdd(dbias + threadIdx.x, sbias[threadIdx.x]);
+}
+
+// out_bf16[m][n] = act(acc[m][n] + bias[n])   (split-K GEMM finishing pass)
+__global__ __launch_bounds__(256) void bias_act_k(const float* __restrict__ acc,
+                                                  const float* __restrict__ bias, bf16_t* __restrict__ out,
+                                                  float* __restrict__ out32, long total, int N, int act) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    float v = acc[i] + (bias ? bias[i % N] : 0.f);
+    if (act == 1) v = fmaxf(v, 0.f);
+    if (out) out[i] = f2bf(v);
+    if (out32) out32[i] = v;
+  }
+}
+
+// db[n] += sum_m g[m][n] (g bf16 or f32). One thread per column, coalesced across n.
+template <typename T>
+__global__ __launch_bounds__(256) void col_sum_k(const T* __restrict__ g, float* __restrict__ db, int M,
+                                                 int N, int mper) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  const int m0 = blockIdx.y * mper, m1 = min(M, m0 + mper);
+  float s = 0.f;
+  for (int m = m0; m < m1; ++m) {
+    if constexpr (sizeof(T) == 2) s += bf2f(g[(long)m * N + n]);
+    else s += g[(long)m * N + n];
+  }
+  atomicAdd(db + n, s);
+}
+
+template <typename T> PTG_DEV float ldf(const T* p, long i) {
+  if constexpr (sizeof(T) == 2) return bf2f(p[i]); else return p[i];
+}
+
+// ----------------------------------------------------------------------------------------------
+// Skinny dense layers (N <= 64 outputs or tiny K): fp32 math, VALU.  Used by the CSV-MLP
+// (3->16->32->64->15, 3,695 params: launch-bound, not FLOP-bound) and the CNN's Dense(2) head.
+// ----------------------------------------------------------------------------------------------
+// act: 0 none, 1 relu, 2 softmax (row-wise over N)
+template <typename TX>
+__global__ __launch_bounds__(256) void dense_small_fwd_k(const TX* __restrict__ x, const float* __restrict__ w,
+                                                         const float* __restrict__ b, float* __restrict__ y,
+                                                         bf16_t* __restrict__ ybf, int M, int K, int N, int act) {
+  // one wave per row; lanes stride K; N accumulators reduced across the wave
+  const int lane = threadIdx.x & 63;
+  const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= M) return;
+  float out_keep = 0.f;
+  float rowmax = -INFINITY;
+  for (int n = 0; n < N; ++n) {
+    float s = 0.f;
+    for (int k = lane; k < K; k += 64) s += ldf(x, (long)m * K + k) * w[(long)n * K + k];
+    s = wave_sum(s) + (b ? b[n] : 0.f);
+    if (act == 1) s = fmaxf(s, 0.f);
+    if (lane == n) out_keep = s;
+    rowmax = fmaxf(rowmax, s);
+  }
+  if (act == 2) {
+    const float e = lane < N ? __expf(out_keep - rowmax) : 0.f;
+    const float tot = wave_sum(e);
+    out_keep = e / tot;
+  }
+  if (lane < N) {
+    y[(long)m * N + lane] = out_keep;
+    if (ybf) ybf[(long)m * N + lane] = f2bf(out_keep);
+  }
+}
+
+// dx[m][k] = (sum_n dy[m][n] w[n][k]) * (mask ? (mask[m][k] > 0) : 1)
+template <typename TM, typename TO>
+__global__ __launch_bounds__(256) void dense_small_dx_k(const float* __restrict__ dy, const float* __restrict__ w,
+                                                        const TM* __restrict__ mask, TO* __restrict__ dx, int M,
+                                                        int K, int N) {
+  const long i = blockIdx.x * 256L + threadIdx.x;
+  if (i >= (long)M * K) return;
+  const int m = i / K, k = i - (long)m * K;
+  float s = 0.f;
+  for (int n = 0; n < N; ++n) s += dy[(long)m * N + n] * w[(long)n * K + k];
+  if (mask && !(ldf(mask, i) > 0.f)) s = 0.f;
+  if constexpr (sizeof(TO) == 2) dx[i] = f2bf(s); else dx[i] = s;
+}
+
+// dw[n][k] += sum_m dy[m][n] x[m][k];  db[n] += sum_m dy[m][n]
+template <typename TX>
+__global__ __launch_bounds__(256) void dense_small_dw_k(const float* __restrict__ dy, const TX* __restrict__ x,
+                                                        float* __restrict__ dw, float* __restrict__ db, int M,
+                                                        int K, int N) {
+  const long i = blockIdx.x * 256L + threadIdx.x;
+  if (i < (long)N * K) {
+    const int n = i / K, k = i - (long)n * K;
+    float s = 0.f;
+    for (int m = 0; m < M; ++m) s += dy[(long)m * N + n] * ldf(x, (long)m * K + k);
+    dw[i] += s;
+  }
+  if (db && i < N) {
+    float s = 0.f;
+    for (int m = 0; m < M; ++m) s += dy[(long)m * N + i];
+    db[i] += s;
+  }
+}
+
+// ----------------------------------------------------------------------------------------------
+// Losses. Single workgroup (B*D is tiny). stats: [loss_sum, abs_sum, sq_sum, count] accumulate.
+// ----------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void mse_k(const float* __restrict__ pred, const float* __restrict__ y,
+                                             float* __restrict__ dpred, float* __restrict__ stats, int total,
+                                             int B, float gscale) {
+  __shared__ float scr[4];
+  float se = 0.f, ae = 0.f;
+  const float inv = 1.f / (float)total;
+  for (int i = threadIdx.x; i < total; i += 256) {
+    const float d = pred[i] - y[i];
+    se += d * d; ae += fabsf(d);
+    dpred[i] = 2.f * d * inv * gscale;
+  }
+  const float sse = block_sum256(se, scr);
+  __syncthreads();
+  const float sae = block_sum256(ae, scr);
+  if (threadIdx.x == 0) {
+    // Keras Mean tracker of per-batch loss (mean over batch of per-sample mean over D)
+    stats[0] += sse * inv * (float)B;   // loss_sum weighted by batch count
+    stats[1] += sae;                    // abs error sum (MAE metric numerator)
+    stats[2] += sse;                    // squared error sum (MSE metric numerator)
+    stats[3] += (float)total;           // element count
+    stats[4] += (float)B;               // sample count
+  }
+}
+
+// softmax + sparse categorical cross-entropy on logits (row per thread, C <= 64).
+// probs clipped to [1e-7, 1-1e-7] like Keras' backend.  dlogits = (p - onehot) / B * gscale.
+// stats: [loss_sum, correct, -, -, count]
+__global__ __launch_bounds__(256) void softmax_xent_k(const float* __restrict__ logits,
+                                                      const int* __restrict__ labels,
+                                                      float* __restrict__ dlogits, float* __restrict__ stats,
+                                                      int B, int C, float gscale) {
+  __shared__ float scr[4];
+  float loss = 0.f, corr = 0.f;
+  for (int b = threadIdx.x; b < B; b += 256) {
+    const float* r = logits + (long)b * C;
+    float mx = -INFINITY; int am = 0;
+    for (int c = 0; c < C; ++c) if (r[c] > mx) { mx = r[c]; am = c; }
+    float s = 0.f;
+    for (int c = 0; c < C; ++c) s += __expf(r[c] - mx);
+    const int lab = labels[b];
+    for (int c = 0; c < C; ++c) {
+      const float p = __expf(r[c] - mx) / s;
+      dlogits[(long)b * C + c] = (p - (c == lab ? 1.f : 0.f)) / (float)B * gscale;
+    }
+    const float pl = fminf(fmaxf(__expf(r[lab] - mx) / s, 1e-7f), 1.f - 1e-7f);
+    loss += -__logf(pl);
+    corr += (am == lab) ? 1.f : 0.f;
+  }
+  const float sl = block_sum256(loss, scr);
+  __syncthreads();
+  const float sc = block_sum256(corr, scr);
+  if (threadIdx.x == 0) { stats[0] += sl; stats[1] += sc; stats[4] += (float)B; }
+}
+
+// ----------------------------------------------------------------------------------------------
+// Fused flat Adam over the whole parameter buffer (one launch per step, float4 vectorised).
+// Writes the fp32 master weights and their bf16 compute copy.  gscale folds in the 1/world
+// averaging of all-reduced gradients.
+// ----------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void adam_k(float* __restrict__ p, const float* __restrict__ g,
+                                              float* __restrict__ m, float* __restrict__ v,
+                                              bf16_t* __restrict__ pbf, long n4, float lr_t, float b1,
+                                              float b2, float eps, float gscale) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    float4 pp = ((float4*)p)[i];
+    const float4 gg = ((const float4*)g)[i];
+    float4 mm = ((float4*)m)[i], vv = ((float4*)v)[i];
+    float* P = &pp.x; const float* G = &gg.x; float* Mm = &mm.x; float* V = &vv.x;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float gj = G[j] * gscale;
+      Mm[j] = b1 * Mm[j] + (1.f - b1) * gj;
+      V[j] = b2 * V[j] + (1.f - b2) * gj * gj;
+      P[j] -= lr_t * Mm[j] / (sqrtf(V[j]) + eps);
+    }
+    ((float4*)p)[i] = pp; ((float4*)m)[i] = mm; ((float4*)v)[i] = vv;
+    if (pbf) {
+      U2 o; o.x = pack_bf(pp.x, pp.y); o.y = pack_bf(pp.z, pp.w);
+      ((U2*)pbf)[i] = o;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void cast_f32_bf16_k(const float* __restrict__ x, bf16_t* __restrict__ y,
+                                                       long n) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) y[i] = f2bf(x[i]);
+}
+__global__ __launch_bounds__(256) void cast_bf16_f32_k(const bf16_t* __restrict__ x, float* __restrict__ y,
+                                                       long n) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) y[i] = bf2f(x[i]);
+}
+
+// Bilinear resize (tf.image.resize: half-pixel centres, no antialias) of uint8 NHWC (3 ch) images,
+// scaled by 1/255, written as 4-channel NHWC bf16 (4th channel 0 = MFMA-friendly padding).
+__global__ __launch_bounds__(256) void resize_norm_k(const uint8_t* __restrict__ in, bf16_t* __restrict__ out,
+                                                     int N, int Hin, int Win, int H, int W) {
+  const long total = (long)N * H * W;
+  const float sy = (float)Hin / H, sx = (float)Win / W;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int x = i % W; long t = i / W; const int y = t % H; const int n = t / H;
+    float fy = (y + 0.5f) * sy - 0.5f, fx = (x + 0.5f) * sx - 0.5f;
+    fy = fmaxf(fy, 0.f); fx = fmaxf(fx, 0.f);
+    int y0 = min((int)fy, Hin - 1), x0 = min((int)fx, Win - 1);
+    const int y1 = min(y0 + 1, Hin - 1), x1 = min(x0 + 1, Win - 1);
+    const float wy = fy - y0, wx = fx - x0;
+    const uint8_t* b = in + (long)n * Hin * Win * 3;
+    float o[4];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const float v00 = b[((long)y0 * Win + x0) * 3 + c], v01 = b[((long)y0 * Win + x1) * 3 + c];
+      const float v10 = b[((long)y1 * Win + x0) * 3 + c], v11 = b[((long)y1 * Win + x1) * 3 + c];
+      const float top = v00 + (v01 - v00) * wx, bot = v10 + (v11 - v10) * wx;
+      o[c] = (top + (bot - top) * wy) * (1.f / 255.f);
+    }
+    o[3] = 0.f;
+    U2 r; r.x = pack_bf(o[0], o[1]); r.y = pack_bf(o[2], o[3]);
+    *(U2*)(out + i * 4) = r;
+  }
+}
+
+// float images [N][H][W][3] in [0,1] -> 4-channel bf16
+__global__ __launch_bounds__(256) void pack_rgb4_k(const float* __restrict__ in, bf16_t* __restrict__ out,
+                                                   long npix) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < npix; i += (long)gridDim.x * 256) {
+    U2 r; r.x = pack_bf(in[i * 3], in[i * 3 + 1]); r.y = pack_bf(in[i * 3 + 2], 0.f);
+    *(U2*)(out + i * 4) = r;
+  }
+}
+
+// Global average pool: out[n][c] = mean_hw x[n][hw][c] (fp32 out); backward broadcasts dy/HW.
+__global__ __launch_bounds__(256) void gap_fwd_k(const bf16_t* __restrict__ x, float* __restrict__ out, int N,
+                                                 int HW, int C) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= N * C) return;
+  const int n = i / C, c = i - n * C;
+  float s = 0.f;
+  for (int p = 0; p < HW; ++p) s += bf2f(x[((long)n * HW + p) * C + c]);
+  out[i] = s / (float)HW;
+}
+__global__ __launch_bounds__(256) void gap_bwd_k(const float* __restrict__ dy, bf16_t* __restrict__ out, int N,
+                                                 int HW, int C) {
+  const long total = (long)N * HW * C;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int c = i % C; const long n = i / ((long)HW * C);
+    out[i] = f2bf(dy[n * C + c] / (float)HW);
+  }
+}
+
+// ReLU backward: dz = (y > 0) ? dy : 0   (dy fp32 or bf16, y bf16 or fp32, dz bf16 or fp32)
+template <typename TD, typename TY, typename TO>
+__global__ __launch_bounds__(256) void relu_bwd_k(const TD* __restrict__ dy, const TY* __restrict__ y,
+                                                  TO* __restrict__ dz, long n) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const float g = ldf(dy, i);
+    const float v = ldf(y, i) > 0.f ? g : 0.f;
+    if constexpr (sizeof(TO) == 2) dz[i] = f2bf(v); else dz[i] = v;
+  }
+}
+
+static inline int grid_for(long n, int per = 1) {
+  long g = (n / per + 255) / 256;
+  if (g < 1) g = 1;
+  if (g > 8192) g = 8192;
+  return (int)g;
+}
+
+extern "C" {
+
+int ptg_prelu_pool_fwd(const void* z, const float* alpha, void* p, int N, int H, int W, int C,
+                       hipStream_t s) {
+  if (C % 8 || (H & 1) || (W & 1)) return (int)hipErrorInvalidValue;
+  const long total = (long)N * (H / 2) * (W / 2) * (C / 8);
+  hipLaunchKernelGGL(prelu_pool_fwd_k, dim3(grid_for(total)), dim3(256), 0, s, (const bf16_t*)z, alpha,
+                     (bf16_t*)p, N, H, W, C);
+  PTG_RETURN_LAUNCH();
+}
+
+int ptg_prelu_pool_bwd(const void* dp, const void* z, const float* alpha, void* dz, float* dalpha,
+                       float* dbias, int N, int H, int W, int C, int nper, hipStream_t s) {
+  if (C % 8 || C > 256 || (H & 1) || (W & 1)) return (int)hipErrorInvalidValue;
+  const int npos = (H / 2) * (W / 2) * (C / 8);
+  if (nper <= 0) {
+    const int bx = (npos + 255) / 256;
+    int chunks = (1024 + bx - 1) / bx;
+    if (chunks > N) chunks = N;
+    nper = (N + chunks - 1) / chunks;
+  }
+  dim3 grid((npos + 255) / 256, (N + nper - 1) / nper);
+  hipLaunchKernelGGL(prelu_pool_bwd_k, grid, dim3(256), 0, s, (const bf16_t*)dp, (const bf16_t*)z, alpha,
+                     (bf16_t*)dz, dalpha, dbias, N, H, W, C, nper);
+  PTG_RETURN_LAUNCH();
+}
+
+int ptg_prelu_fwd(const void* z, const float* alpha, void* a, int N, int HWC, hipStream_t s) {
+  if (HWC % 8) return (int)hipErrorInvalidValue;
+  const long total8 = (long)N * HWC / 8;
+  hipLaunchKernelGGL(prelu_fwd_k, dim3(grid_for(total8)), dim3(256), 0, s, (const bf16_t*)z, alpha,
+                     (bf16_t*)a, total8, HWC / 8);
+  PTG_RETURN_LAUNCH();
+}
+
+int ptg_prelu_bwd(const void* da, const void* z, const float* alpha, void* dz, float* dalpha,
+                  float* dbias, int N, int HWC, int C, int nper, hipStream_t s) {
+  if (HWC % 8 || C % 8 || C > 256) return (int)hipErrorInvalidValue;
+  const int nvec = HWC / 8;
+  if (nper <= 0) {
+    const int bx = (nvec + 255) / 256;
+    int chunks = (1024 + bx - 1) / bx;
+    if (chunks > N) chunks = N;
+    nper = (N + chunks - 1) / chunks;
+  }
+  dim3 grid((nvec + 255) / 256, (N + nper - 1) / nper);
+  hipLaunchKernelGGL(prelu_bwd_k, grid, dim3(256), 0, s, (const bf16_t*)da, (const bf16_t*)z, alpha,
+                     (bf16_t*)dz, dalpha, dbias, N, HWC, C, nper);
+  PTG_RETURN_LAUNCH();
+}
+
+int ptg_bias_act(const float* acc, const float* bias, void* out_bf16, float* out32, long M, int N, int act,
+                 hipStream_t s) {
+  const long total = M * N;
+  hipLaunchKernelGGL(bias_act_k, dim3(grid_for(total)), dim3(256), 0, s, acc, bias, (bf16_t*)out_bf16, out32,
+                     total, N, act);
+  PTG_RETURN_LAUNCH();
+}
+
+int ptg_col_sum(const void* g, int g_is_bf16, float* db, int M, int N, hipStream_t s) {
+  const int bx = (N + 255) / 256;
+  int chunks = (512 + bx - 1) / bx;
+  if (chunks > M) chunks = M;
+  if (chunks < 1) chunks = 1;
+  const int mper = (M + chunks - 1) / chunks;
+  dim3 grid(bx, (M + mper - 1) / mper);
+  if (g_is_bf16)
+    hipLaunchKernelGGL(col_sum_k<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)g, db, M, N, mper);
+  else
+    hipLaunchKernelGGL(col_sum_k<float>, grid, dim3(256), 0, s, (const float*)g, db, M, N, mper);
+  PTG_RETURN_LAUNCH();
+}
+
+int ptg_dense_small_fwd(const void* x, int x_is_bf16, const float* w, const float* b, float* y, void* ybf,
+                        int M, int K, int N, int act, hipStream_t s) {
+  if (N > 64) return (int)hipErrorInvalidValue;
+  dim3 grid((M + 3) / 4);
+  if (x_is_bf16)
+    hipLaunchKernelGGL(dense_small_fwd_k<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, w, b, y,
+                       (bf16_t*)ybf, M, K, N, act);
+  else
+    hipLaunchKernelGGL(dense_small_fwd_k<float>, grid, dim3(256), 0, s, (const float*)x, w, b, y,
+                       (bf16_t*)ybf, M, K, N, act);
+  PTG_RETURN_LAUNCH();
+}
+
+// mask_kind: 0 none, 1 f32 mask, 2 bf16 mask. out_is_bf16 selects dx dtype.
+int ptg_dense_small_dx(const float* dy, const float* w, const void* mask, int mask_kind, void* dx,
+                       int out_is_bf16, int M, int K, int N, hipStream_t s) {
+  const long total = (long)M * K;
+  dim3 grid((total + 255) / 256);
+  if (mask_kind == 2) {
+    if (out_is_bf16)
+      hipLaunchKernelGGL((dense_small_dx_k<bf16_t, bf16_t>), grid, dim3(256), 0, s, dy, w,
+                         (const bf16_t*)mask, (bf16_t*)dx, M, K, N);
+    else
+      hipLaunchKernelGGL((dense_small_dx_k<bf16_t, float>), grid, dim3(256), 0, s, dy, w,
+                         (const bf16_t*)mask, (float*)dx, M, K, N);
+  } else {
+    const float* mk = mask_kind == 1 ? (const float*)mask : nullptr;
+    if (out_is_bf16)
+      hipLaunchKernelGGL((dense_small_dx_k<float, bf16_t>), grid, dim3(256), 0, s, dy, w, mk, (bf16_t*)dx,
+                         M, K, N);
+    else
+      hipLaunchKernelGGL((dense_small_dx_k<float, float>), grid, dim3(256), 0, s, dy, w, mk, (float*)dx, M,
+                         K, N);
+  }
+  PTG_RETURN_LAUNCH();
+}
+
+int ptg_dense_small_dw(const float* dy, const void* x, int x_is_bf16, float* dw, float* db, int M, int K,
+                       int N, hipStream_t s) {
+  long total = (long)N * K;
+  if (total < N) total = N;
+  dim3 grid((total + 255) / 256);
+  if (x_is_bf16)
+    hipLaunchKernelGGL(dense_small_dw_k<bf16_t>, grid, dim3(256), 0, s, dy, (const bf16_t*)x, dw, db, M, K, N);
+  else
+    hipLaunchKernelGGL(dense_small_dw_k<float>, grid, dim3(256), 0, s, dy, (const float*)x, dw, db, M, K, N);
+  PTG_RETURN_LAUNCH();
+}
+
+int ptg_mse(const float* pred, const float* y, float* dpred, float* stats, int B, int D, float gscale,
+            hipStream_t s) {
+  hipLaunchKernelGGL(mse_k, dim3(1), dim3(256), 0, s, pred, y, dpred, stats, B * D, B, gscale);
+  PTG_RETURN_LAUNCH();
+}
+
+int ptg_softmax_xent(const float* logits, const int* labels, float* dlogits, float* stats, int B, int C,
+                     float gscale, hipStream_t s) {
+  hipLaunchKernelGGL(softmax_xent_k, dim3(1), dim3(256), 0, s, logits, labels, dlogits, stats, B, C, gscale);
+  PTG_RETURN_LAUNCH();
+}
+
+int ptg_adam(float* p, const float* g, float* m, float* v, void* pbf, long n, float lr_t, float b1, float b2,
+             float eps, float gscale, hipStream_t s) {
+  if (n % 4) return (int)hipErrorInvalidValue;
+  const long n4 = n / 4;
+  hipLaunchKernelGGL(adam_k, dim3(grid_for(n4)), dim3(256), 0, s, p, g, m, v, (bf16_t*)pbf, n4, lr_t, b1, b2,
+                     eps, gscale);
+  PTG_RETURN_LAUNCH();
+}
+
+int ptg_cast_f32_bf16(const float* x, void* y, long n, hipStream_t s) {
+  hipLaunchKernelGGL(cast_f32_bf16_k, dim3(grid_for(n)), dim3(256), 0, s, x, (bf16_t*)y, n);
+  PTG_RETURN_LAUNCH();
+}
+int ptg_cast_bf16_f32(const void* x, float* y, long n, hipStream_t s) {
+  hipLaunchKernelGGL(cast_bf16_f32_k, dim3(grid_for(n)), dim3(256), 0, s, (const bf16_t*)x, y, n);
+  PTG_RETURN_LAUNCH();
+}
+int ptg_resize_norm(const void* in_u8, void* out, int N, int Hin, int Win, int H, int W, hipStream_t s) {
+  hipLaunchKernelGGL(resize_norm_k, dim3(grid_for((long)N * H * W)), dim3(256), 0, s, (const uint8_t*)in_u8,
+                     (bf16_t*)out, N, Hin, Win, H, W);
+  PTG_RETURN_LAUNCH();
+}
+int ptg_pack_rgb4(const float* in, void* out, long npix, hipStream_t s) {
+  hipLaunchKernelGGL(pack_rgb4_k, dim3(grid_for(npix)), dim3(256), 0, s, in, (bf16_t*)out, npix);
+  PTG_RETURN_LAUNCH();
+}
+
+// flags: bit0 dy is bf16, bit1 y is bf16, bit2 dz is bf16
+int ptg_relu_bwd(const void* dy, const void* y, void* dz, long n, int flags, hipStream_t s) {
+  dim3 g(grid_for(n)), b(256);
+#define PTG_RB(A, B, C) hipLaunchKernelGGL((relu_bwd_k<A, B, C>), g, b, 0, s, (const A*)dy, (const B*)y, (C*)dz, n)
+  switch (flags & 7) {
+    case 0: PTG_RB(float, float, float); break;
+    case 1: PTG_RB(bf16_t, float, float); break;
+    case 2: PTG_RB(float, bf16_t, float); break;
+    case 3: PTG_RB(bf16_t, bf16_t, float); break;
+    case 4: PTG_RB(float, float, bf16_t); break;
+    case 5: PTG_RB(bf16_t, float, bf16_t); break;
+    case 6: PTG_RB(float, bf16_t, bf16_t); break;
+    default: PTG_RB(bf16_t, bf16_t, bf16_t); break;
+  }
+#undef PTG_RB
+  PTG_RETURN_LAUNCH();
+}
+
+int ptg_gap_fwd(const void* x, float* out, int N, int HW, int C, hipStream_t s) {
+  hipLaunchKernelGGL(gap_fwd_k, dim3((N * C + 255) / 256), dim3(256), 0, s, (const bf16_t*)x, out, N, HW, C);
+  PTG_RETURN_LAUNCH();
+}
+int ptg_gap_bwd(const float* dy, void* out, int N, int HW, int C, hipStream_t s) {
+  hipLaunchKernelGGL(gap_bwd_k, dim3(grid_for((long)N * HW * C)), dim3(256), 0, s, dy, (bf16_t*)out, N, HW, C);
+  PTG_RETURN_LAUNCH();
+}
+
+}  // extern "C"

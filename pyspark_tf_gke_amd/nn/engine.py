@@ -1,0 +1,367 @@
+"""Fused execution plan for Sequential models (the training "step engine").
+
+Keras layers (:mod:`.layers`) are lowered to device ops that own their forward/backward:
+
+* ``ConvOp``   Conv2D [+ PReLU] [+ MaxPooling2D]: implicit-GEMM MFMA conv with bias in the
+  epilogue, then ONE fused PReLU+max-pool kernel; backward = fused PReLU/pool gradient (also
+  accumulating d(alpha) and d(bias)) -> MFMA wgrad (split-K) -> MFMA dgrad.
+* ``DenseOp``  Dense: MFMA GEMM with bias+ReLU epilogue for wide layers, a VALU "skinny" kernel
+  for narrow ones (N <= 64: the MLP and the 2-output regression head).  A narrow Dense also
+  applies the previous layer's ReLU mask inside its dX kernel.
+* ``FlattenOp`` (a view), ``GAPOp``, ``PReLUOp``/``PoolOp`` (unfused fallbacks).
+
+Activations live in a :class:`Workspace` keyed by op and shape, so every step reuses the same
+device buffers (stable addresses; capturable into a HIP graph).  Reference: the model builders of
+train_tf_ps.py:328-378 and the GradientTape step of :616-631 / :738-753.
+"""
+from __future__ import annotations
+
+import torch
+
+from ..ops import nn as K
+from . import layers as L
+
+
+class Workspace:
+    def __init__(self):
+        self.bufs: dict = {}
+
+    def get(self, key, shape, dtype, device, zero=False):
+        shape = tuple(int(s) for s in shape)
+        t = self.bufs.get(key)
+        if t is None or tuple(t.shape) != shape or t.dtype != dtype or t.device != torch.device(device):
+            t = (torch.zeros if zero else torch.empty)(shape, dtype=dtype, device=device)
+            self.bufs[key] = t
+        return t
+
+    def clear(self):
+        self.bufs.clear()
+
+
+class Op:
+    first = False  # no dX needed
+
+    def __init__(self):
+        self.params = []
+        self.mask_for_prev = False  # this op applies the previous op's ReLU mask in its dX
+        self.grad_masked_by_next = False  # our output gradient arrives already ReLU-masked
+
+    def forward(self, x, ws, training):
+        raise NotImplementedError
+
+    def backward(self, dy, ws):
+        raise NotImplementedError
+
+
+def _bf16(x, ws, key):
+    if x.dtype == torch.bfloat16:
+        return x
+    out = ws.get(key, x.shape, torch.bfloat16, x.device)
+    out.copy_(x)
+    return out
+
+
+class ConvOp(Op):
+    def __init__(self, conv: L.Conv2D, prelu: L.PReLU | None, pool: L.MaxPooling2D | None):
+        super().__init__()
+        self.conv, self.prelu, self.pool = conv, prelu, pool
+        self.params = list(conv.params) + (list(prelu.params) if prelu else [])
+        conv.kernel.overwrite_grad = True
+        self.stride = conv.strides[0]
+        self.pad = conv.pad_amount()
+        self.name = conv.name
+        if conv.activation not in ("linear", None, "relu"):
+            raise NotImplementedError(f"Conv2D activation {conv.activation}")
+        if conv.activation == "relu" and (prelu or pool):
+            raise NotImplementedError("Conv2D(activation='relu') followed by PReLU/pool")
+
+    def _prep_input(self, x, ws):
+        cp = self.conv.cin_p
+        if x.shape[-1] == cp and x.dtype == torch.bfloat16:
+            return x
+        if x.dtype == torch.uint8 and x.shape[-1] == 3 and cp == 4:
+            # raw decoded images: bilinear resize + /255 + channel pad in one device pass
+            H, W = self.conv.in_shape[0], self.conv.in_shape[1]
+            xi = ws.get(self.name + "/xin", (x.shape[0], H, W, cp), torch.bfloat16, x.device)
+            return K.resize_norm(x.contiguous(), xi, H, W)
+        xi = ws.get(self.name + "/xin", (*x.shape[:-1], cp), torch.bfloat16, x.device)
+        if x.shape[-1] == 3 and cp == 4 and x.dtype == torch.float32:
+            return K.pack_rgb4(x.contiguous(), xi)
+        xi.zero_()
+        xi[..., : x.shape[-1]] = x
+        return xi
+
+    def forward(self, x, ws, training):
+        x = self._prep_input(x, ws)
+        B = x.shape[0]
+        OH, OW, Co = self.conv.out_shape
+        dev = x.device
+        z = ws.get(self.name + "/z", (B, OH, OW, Co), torch.bfloat16, dev)
+        act = "relu" if self.conv.activation == "relu" else None
+        b = self.conv.bias.data if self.conv.bias is not None else None
+        K.conv2d_fwd(x, self.conv.kernel.bf16, b, self.stride, self.pad, z, act)
+        self._x, self._z = x, z
+        if self.prelu is not None and self.pool is not None:
+            p = ws.get(self.name + "/p", (B, OH // 2, OW // 2, Co), torch.bfloat16, dev)
+            return K.prelu_pool_fwd(z, self.prelu.alpha.data, p)
+        if self.prelu is not None:
+            a = ws.get(self.name + "/a", (B, OH, OW, Co), torch.bfloat16, dev)
+            return K.prelu_fwd(z, self.prelu.alpha.data, a)
+        if self.pool is not None:
+            ones = ws.get(self.name + "/ones", (OH, OW, Co), torch.float32, dev)
+            ones.fill_(1.0)
+            p = ws.get(self.name + "/p", (B, OH // 2, OW // 2, Co), torch.bfloat16, dev)
+            return K.prelu_pool_fwd(z, ones, p)
+        return z
+
+    def backward(self, dy, ws):
+        z, x = self._z, self._x
+        dev = z.device
+        dy = _bf16(dy, ws, self.name + "/dy16")
+        dz = ws.get(self.name + "/dz", z.shape, torch.bfloat16, dev)
+        bias_g = self.conv.bias.grad if self.conv.bias is not None else \
+            ws.get(self.name + "/nobias", (z.shape[-1],), torch.float32, dev)
+        if self.prelu is not None and self.pool is not None:
+            K.prelu_pool_bwd(dy, z, self.prelu.alpha.data, dz, self.prelu.alpha.grad, bias_g)
+        elif self.prelu is not None:
+            K.prelu_bwd(dy, z, self.prelu.alpha.data, dz, self.prelu.alpha.grad, bias_g)
+        elif self.pool is not None:
+            ones = ws.get(self.name + "/ones", z.shape[1:], torch.float32, dev)
+            dummy = ws.get(self.name + "/dalpha_dummy", z.shape[1:], torch.float32, dev)
+            K.prelu_pool_bwd(dy, z, ones, dz, dummy, bias_g)
+        elif self.conv.activation == "relu":
+            zeros = ws.get(self.name + "/zeros", z.shape[1:], torch.float32, dev, zero=True)
+            dummy = ws.get(self.name + "/dalpha_dummy", z.shape[1:], torch.float32, dev)
+            K.prelu_bwd(dy, z, zeros, dz, dummy, bias_g)
+        else:
+            dz = dy
+            K.col_sum(dz.reshape(-1, dz.shape[-1]), bias_g)
+        K.conv2d_wgrad(x, dz, self.stride, self.pad, self.conv.kernel.grad)
+        if self.first:
+            return None
+        if self.stride != 1:
+            raise NotImplementedError("dgrad for strided convolutions")
+        dx = ws.get(self.name + "/dx", x.shape, torch.bfloat16, dev)
+        K.conv2d_dgrad(dz, self.conv.kernel.bf16, self.pad, dx)
+        return dx
+
+
+class DenseOp(Op):
+    def __init__(self, dense: L.Dense):
+        super().__init__()
+        self.dense = dense
+        self.params = list(dense.params)
+        self.name = dense.name
+        N, Kd = dense.units, dense.fan_in
+        self.big = N > 64 and N % 8 == 0 and Kd % 8 == 0
+        if self.big:
+            dense.kernel.overwrite_grad = True
+        self.act = dense.activation
+        self.logits_only = False  # softmax folded into the loss
+
+    def forward(self, x, ws, training):
+        x = x.reshape(x.shape[0], -1)
+        B = x.shape[0]
+        N = self.dense.units
+        dev = x.device
+        b = self.dense.bias.data if self.dense.bias is not None else None
+        act = None if (self.logits_only and self.act == "softmax") else self.act
+        if self.big:
+            x = _bf16(x, ws, self.name + "/x16")
+            y = ws.get(self.name + "/y", (B, N), torch.bfloat16, dev)
+            wsp = ws.get(self.name + "/splitk", (B * N,), torch.float32, dev)
+            K.linear_fwd(x, self.dense.kernel.bf16, b, act, y, workspace=wsp)
+        else:
+            y = ws.get(self.name + "/y", (B, N), torch.float32, dev)
+            K.dense_small_fwd(x, self.dense.kernel.data, b, act, y)
+        self._x, self._y = x, y
+        return y
+
+    def backward(self, dy, ws):
+        x, y = self._x, self._y
+        dev = y.device
+        B, N = y.shape
+        if self.big:
+            if self.act == "relu" and not self.grad_masked_by_next:
+                dz = ws.get(self.name + "/dz", (B, N), torch.bfloat16, dev)
+                K.relu_bwd(dy, y, dz)
+            else:
+                dz = _bf16(dy, ws, self.name + "/dz16")
+            K.linear_dw(dz, x, self.dense.kernel.grad)
+            if self.dense.bias is not None:
+                K.col_sum(dz, self.dense.bias.grad)
+            if self.first:
+                return None
+            dx = ws.get(self.name + "/dx", x.shape, torch.bfloat16, dev)
+            K.linear_dx(dz, self.dense.kernel.bf16, dx)
+            return dx
+        # skinny path (fp32 math)
+        if self.act == "relu" and not self.grad_masked_by_next:
+            dz = ws.get(self.name + "/dz", (B, N), torch.float32, dev)
+            K.relu_bwd(dy, y, dz)
+        elif dy.dtype != torch.float32:
+            dz = dy.float()
+        else:
+            dz = dy
+        db = self.dense.bias.grad if self.dense.bias is not None else None
+        K.dense_small_dw(dz, x, self.dense.kernel.grad, db)
+        if self.first:
+            return None
+        mask = self._prev_y if self.mask_for_prev else None
+        out_dtype = torch.bfloat16 if getattr(self, "_prev_big", False) or x.dtype == torch.bfloat16 else torch.float32
+        dx = ws.get(self.name + "/dx", x.shape, out_dtype, dev)
+        K.dense_small_dx(dz, self.dense.kernel.data, mask, dx)
+        return dx
+
+
+class FlattenOp(Op):
+    def __init__(self, layer):
+        super().__init__()
+        self.name = layer.name
+
+    def forward(self, x, ws, training):
+        self._shape = x.shape
+        return x.reshape(x.shape[0], -1)
+
+    def backward(self, dy, ws):
+        return dy.reshape(self._shape)
+
+
+class GAPOp(Op):
+    def __init__(self, layer):
+        super().__init__()
+        self.name = layer.name
+
+    def forward(self, x, ws, training):
+        x = _bf16(x, ws, self.name + "/x16")
+        self._xshape = x.shape
+        out = ws.get(self.name + "/y", (x.shape[0], x.shape[-1]), torch.float32, x.device)
+        return K.gap_fwd(x, out)
+
+    def backward(self, dy, ws):
+        dx = ws.get(self.name + "/dx", self._xshape, torch.bfloat16, dy.device)
+        return K.gap_bwd(dy.float().contiguous(), dx)
+
+
+class PReLUOp(Op):
+    def __init__(self, layer: L.PReLU):
+        super().__init__()
+        self.layer = layer
+        self.params = list(layer.params)
+        self.name = layer.name
+
+    def forward(self, x, ws, training):
+        x = _bf16(x, ws, self.name + "/x16")
+        self._z = x
+        a = ws.get(self.name + "/a", x.shape, torch.bfloat16, x.device)
+        return K.prelu_fwd(x, self.layer.alpha.data, a)
+
+    def backward(self, dy, ws):
+        z = self._z
+        dy = _bf16(dy, ws, self.name + "/dy16")
+        dz = ws.get(self.name + "/dz", z.shape, torch.bfloat16, z.device)
+        dummy_b = ws.get(self.name + "/db", (z.shape[-1],), torch.float32, z.device)
+        return K.prelu_bwd(dy, z, self.layer.alpha.data, dz, self.layer.alpha.grad, dummy_b)
+
+
+class PoolOp(Op):
+    def __init__(self, layer):
+        super().__init__()
+        self.name = layer.name
+
+    def forward(self, x, ws, training):
+        x = _bf16(x, ws, self.name + "/x16")
+        self._z = x
+        B, H, W, C = x.shape
+        ones = ws.get(self.name + "/ones", (H, W, C), torch.float32, x.device)
+        ones.fill_(1.0)
+        p = ws.get(self.name + "/p", (B, H // 2, W // 2, C), torch.bfloat16, x.device)
+        return K.prelu_pool_fwd(x, ones, p)
+
+    def backward(self, dy, ws):
+        z = self._z
+        dy = _bf16(dy, ws, self.name + "/dy16")
+        ones = ws.get(self.name + "/ones", z.shape[1:], torch.float32, z.device)
+        dummy = ws.get(self.name + "/dalpha", z.shape[1:], torch.float32, z.device)
+        dummy_b = ws.get(self.name + "/db", (z.shape[-1],), torch.float32, z.device)
+        dz = ws.get(self.name + "/dz", z.shape, torch.bfloat16, z.device)
+        return K.prelu_pool_bwd(dy, z, ones, dz, dummy, dummy_b)
+
+
+class ReLUOp(Op):
+    def __init__(self, layer):
+        super().__init__()
+        self.name = layer.name
+
+    def forward(self, x, ws, training):
+        y = ws.get(self.name + "/y", x.shape, x.dtype, x.device)
+        y.copy_(torch.relu(x)) if not x.is_cuda else K.relu_bwd(x, x, y)
+        self._y = y
+        return y
+
+    def backward(self, dy, ws):
+        dz = ws.get(self.name + "/dz", dy.shape, dy.dtype, dy.device)
+        return K.relu_bwd(dy, self._y, dz)
+
+
+def lower(layers: list) -> list:
+    """Fuse a built layer list into device ops."""
+    ops = []
+    i = 0
+    seq = [l for l in layers if not isinstance(l, L.Input)]
+    while i < len(seq):
+        l = seq[i]
+        if isinstance(l, L.Conv2D):
+            prelu = pool = None
+            j = i + 1
+            if j < len(seq) and isinstance(seq[j], L.PReLU) and l.activation in ("linear", None):
+                prelu = seq[j]; j += 1
+            if j < len(seq) and isinstance(seq[j], L.MaxPooling2D) and l.activation in ("linear", None):
+                pool = seq[j]; j += 1
+            ops.append(ConvOp(l, prelu, pool))
+            i = j
+        elif isinstance(l, L.Dense):
+            ops.append(DenseOp(l)); i += 1
+        elif isinstance(l, L.Flatten):
+            ops.append(FlattenOp(l)); i += 1
+        elif isinstance(l, L.GlobalAveragePooling2D):
+            ops.append(GAPOp(l)); i += 1
+        elif isinstance(l, L.PReLU):
+            ops.append(PReLUOp(l)); i += 1
+        elif isinstance(l, L.MaxPooling2D):
+            ops.append(PoolOp(l)); i += 1
+        elif isinstance(l, L.ReLU):
+            ops.append(ReLUOp(l)); i += 1
+        else:
+            raise NotImplementedError(type(l).__name__)
+    if ops:
+        ops[0].first = True
+    # ReLU-mask hand-off: a skinny Dense applies the previous relu-Dense's mask in its dX
+    for k in range(1, len(ops)):
+        cur, prev = ops[k], ops[k - 1]
+        if isinstance(cur, DenseOp) and not cur.big and isinstance(prev, DenseOp) and prev.act == "relu":
+            cur.mask_for_prev = True
+            cur._prev_big = prev.big
+            prev.grad_masked_by_next = True
+            cur._prev_op = prev
+    return ops
+
+
+def run_forward(ops, x, ws, training=True):
+    for k, op in enumerate(ops):
+        if isinstance(op, DenseOp) and op.mask_for_prev:
+            op._prev_y = op._prev_op._y if hasattr(op, "_prev_op") else None
+        x = op.forward(x, ws, training)
+        if isinstance(op, DenseOp) and k + 1 < len(ops):
+            nxt = ops[k + 1]
+            if isinstance(nxt, DenseOp) and nxt.mask_for_prev:
+                nxt._prev_y = op._y
+    return x
+
+
+def run_backward(ops, dy, ws, on_op_done=None):
+    for op in reversed(ops):
+        dy = op.backward(dy, ws)
+        if on_op_done is not None:
+            on_op_done(op)
+    return dy

@@ -1,0 +1,66 @@
+"""Keras-compatible loss objects (train_tf_ps.py:340,375,607,729).
+
+In ``fit()`` the loss runs as one fused device kernel that also produces the output gradient and
+the metric sums (``ops.nn.mse`` / ``ops.nn.softmax_xent``).  Calling a loss object directly
+(custom training loops, :mod:`.tape`) returns the scalar loss and, under a GradientTape, records
+which fused kernel to run for the backward pass.
+"""
+from __future__ import annotations
+
+import torch
+
+
+class Loss:
+    name = "loss"
+    kind = "none"
+
+    def __call__(self, y_true, y_pred):
+        from .tape import _active_tape
+
+        y_true = torch.as_tensor(y_true, device=y_pred.device)
+        val = self.compute(y_true, y_pred)
+        tape = _active_tape()
+        if tape is not None:
+            tape.record_loss(self, y_true, y_pred, val)
+        return val
+
+    def compute(self, y_true, y_pred):
+        raise NotImplementedError
+
+    def get_config(self):
+        return {"name": self.name}
+
+
+class MeanSquaredError(Loss):
+    name = "mean_squared_error"
+    kind = "mse"
+
+    def compute(self, y_true, y_pred):
+        d = y_pred.float() - y_true.float()
+        return (d * d).mean()
+
+
+class SparseCategoricalCrossentropy(Loss):
+    name = "sparse_categorical_crossentropy"
+    kind = "sparse_xent"
+
+    def __init__(self, from_logits: bool = False):
+        self.from_logits = from_logits
+
+    def compute(self, y_true, y_pred):
+        p = y_pred.float()
+        if self.from_logits:
+            p = torch.softmax(p, -1)
+        p = p.gather(1, y_true.long().view(-1, 1)).clamp(1e-7, 1 - 1e-7)
+        return (-p.log()).mean()
+
+
+def get(identifier) -> Loss:
+    if isinstance(identifier, Loss):
+        return identifier
+    key = str(identifier).lower()
+    if key in ("mse", "mean_squared_error", "meansquarederror"):
+        return MeanSquaredError()
+    if key in ("sparse_categorical_crossentropy", "sparsecategoricalcrossentropy"):
+        return SparseCategoricalCrossentropy()
+    raise ValueError(f"unknown loss {identifier!r}")

@@ -1,0 +1,487 @@
+"""``Sequential`` model with the Keras surface the reference uses (train_tf_ps.py:328-378, :651-679,
+:773-814): ``compile / fit / evaluate / predict / summary / save``, History dicts, plus
+``train_on_batch`` and GradientTape-style custom loops (:mod:`.tape`).
+
+A training step is: zero the (accumulated) gradient ranges -> fused forward ops -> fused
+loss kernel (output gradient + metric sums) -> fused backward ops (the active distribution
+strategy gets a callback as each op's gradients complete, to launch bucketed RCCL collectives
+while the rest of backward runs) -> strategy gradient sync -> ONE fused Adam launch (or the
+strategy's sharded update).  Host syncs happen only at epoch boundaries (metric readout).
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+import sys
+import time
+import zipfile
+
+import numpy as np
+import torch
+
+from ..ops import nn as K
+from . import engine as E
+from . import layers as L
+from . import losses as LS
+from . import metrics as MT
+from . import optimizers as OPT
+from .params import ParamStore
+
+
+def default_device() -> torch.device:
+    from ..distribute import current_strategy
+
+    st = current_strategy()
+    if st is not None:
+        return st.device
+    if torch.cuda.is_available():
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+class History:
+    def __init__(self):
+        self.history: dict = {}
+        self.epoch: list = []
+
+
+class Variable:
+    """Handle on one parameter of the flat store (what ``model.trainable_variables`` returns)."""
+
+    def __init__(self, param, model=None):
+        self.param = param
+        self.model = model
+        self.name = param.name
+
+    @property
+    def shape(self):
+        return self.param.shape
+
+    def numpy(self):
+        return self.param.data.detach().cpu().numpy()
+
+    def assign(self, value):
+        self.param.data.copy_(torch.as_tensor(value, dtype=torch.float32))
+
+
+class Sequential:
+    def __init__(self, layers=None, name: str = "sequential"):
+        self.name = name
+        self._layers: list = []
+        self.input_shape = None
+        self.built = False
+        self.store: ParamStore | None = None
+        self.ops: list = []
+        self.ws = E.Workspace()
+        self.optimizer = None
+        self.loss = None
+        self.metric_names: list = []
+        self.device = None
+        self._stats = None
+        self._eval_stats = None
+        self.stop_training = False
+        self.strategy = None
+        for l in layers or []:
+            self.add(l)
+
+    # ---------------------------------------------------------------- structure
+    def add(self, layer) -> None:
+        if isinstance(layer, L.Input):
+            self.input_shape = layer.shape
+        self._layers.append(layer)
+
+    @property
+    def layers(self):
+        return [l for l in self._layers if not isinstance(l, L.Input)]
+
+    def build(self, input_shape=None, device=None, seed: int | None = None) -> None:
+        if self.built:
+            return
+        if input_shape is not None:
+            self.input_shape = tuple(int(s) for s in (input_shape[1:] if input_shape[0] is None else input_shape))
+        if self.input_shape is None:
+            raise ValueError("Sequential needs an Input layer or build(input_shape)")
+        self.device = torch.device(device) if device is not None else default_device()
+        self.store = ParamStore()
+        shape = self.input_shape
+        for l in self.layers:
+            shape = l.build(shape, self.store)
+        self.output_shape = shape
+        if seed is None:
+            seed = int(os.environ.get("PTG_SEED", "1337"))
+        self.store.finalize(self.device, seed=seed)
+        self.ops = E.lower(self._layers)
+        self.built = True
+        from ..distribute import current_strategy
+
+        st = current_strategy()
+        if st is not None:
+            st.register_model(self)
+
+    def count_params(self) -> int:
+        return self.store.num_params() if self.store else 0
+
+    @property
+    def trainable_variables(self):
+        return [Variable(p, self) for l in self.layers for p in l.params]
+
+    weights = trainable_variables
+
+    @property
+    def losses(self):
+        return []  # no regularizers (reference: `model.losses` is empty, train_tf_ps.py:624)
+
+    def get_weights(self):
+        return [w for l in self.layers for w in l.keras_weights()]
+
+    def set_weights(self, ws):
+        i = 0
+        for l in self.layers:
+            n = len(l.keras_weights())
+            if n:
+                l.set_keras_weights(ws[i:i + n])
+                i += n
+        self.store.refresh_bf16()
+
+    # ---------------------------------------------------------------- compile
+    def compile(self, optimizer="adam", loss=None, metrics=None) -> None:
+        self.optimizer = OPT.get(optimizer)
+        self.loss = LS.get(loss) if loss is not None else None
+        self.metric_names = [MT.canonical_name(m) for m in (metrics or [])]
+        if not self.built and self.input_shape is not None:
+            self.build()
+        self._configure_loss()
+
+    def _configure_loss(self):
+        if not self.built or self.loss is None:
+            return
+        last = self.ops[-1]
+        if isinstance(self.loss, LS.SparseCategoricalCrossentropy) and isinstance(last, E.DenseOp):
+            # softmax is folded into the fused softmax-crossentropy kernel
+            last.logits_only = last.act == "softmax" or self.loss.from_logits
+
+    # ---------------------------------------------------------------- device helpers
+    def _to_device(self, a, dtype=None):
+        if isinstance(a, torch.Tensor):
+            t = a
+        else:
+            a = np.asarray(a)
+            t = torch.from_numpy(np.ascontiguousarray(a))
+        if dtype is not None and t.dtype != dtype:
+            t = t.to(dtype)
+        if t.device != self.device:
+            if t.device.type == "cpu" and self.device.type == "cuda":
+                t = t.pin_memory().to(self.device, non_blocking=True)
+            else:
+                t = t.to(self.device)
+        return t
+
+    def _x_dtype(self, x):
+        if isinstance(x, torch.Tensor):
+            return None if x.dtype in (torch.uint8, torch.bfloat16, torch.float32) else torch.float32
+        a = np.asarray(x)
+        return None if a.dtype in (np.uint8, np.float32) else torch.float32
+
+    def _prep_batch(self, x, y):
+        xb = self._to_device(x, self._x_dtype(x))
+        yb = None
+        if y is not None:
+            if isinstance(self.loss, LS.SparseCategoricalCrossentropy):
+                yb = self._to_device(y, torch.int32).view(-1)
+            else:
+                yb = self._to_device(y, torch.float32)
+                if yb.dim() == 1:
+                    yb = yb.view(-1, 1)
+        return xb, yb
+
+    def _stats_buf(self, which="train"):
+        if which == "train":
+            if self._stats is None or self._stats.device != self.device:
+                self._stats = torch.zeros(8, dtype=torch.float32, device=self.device)
+            return self._stats
+        if self._eval_stats is None or self._eval_stats.device != self.device:
+            self._eval_stats = torch.zeros(8, dtype=torch.float32, device=self.device)
+        return self._eval_stats
+
+    # ---------------------------------------------------------------- forward / loss / step
+    def __call__(self, x, training: bool = False):
+        if not self.built:
+            self.build()
+        xb = self._to_device(x, self._x_dtype(x))
+        out = E.run_forward(self.ops, xb, self.ws, training)
+        from .tape import _active_tape
+
+        tape = _active_tape()
+        if tape is not None:
+            tape.record_forward(self, out)
+        if isinstance(self.ops[-1], E.DenseOp) and self.ops[-1].logits_only:
+            out = torch.softmax(out.float(), -1)
+        return out
+
+    def _loss_grad(self, out, yb, stats, gscale=1.0):
+        dev = out.device
+        pred = out if out.dtype == torch.float32 else out.float()
+        dpred = self.ws.get("__dpred", pred.shape, torch.float32, dev)
+        if isinstance(self.loss, LS.MeanSquaredError):
+            K.mse(pred.contiguous(), yb, dpred, stats, gscale)
+        elif isinstance(self.loss, LS.SparseCategoricalCrossentropy):
+            K.softmax_xent(pred.contiguous(), yb, dpred, stats, gscale)
+        else:
+            raise ValueError(f"unsupported loss {self.loss}")
+        return dpred
+
+    def _strategy(self):
+        if getattr(self, "strategy", None) is not None:
+            return self.strategy
+        from ..distribute import current_strategy
+
+        return current_strategy()
+
+    def backward_and_update(self, dpred, strategy=None) -> None:
+        """Backward from d(loss)/d(output) + gradient sync + optimizer update."""
+        st = strategy
+        hook = st.on_op_grads_ready if st is not None else None
+        E.run_backward(self.ops, dpred, self.ws, on_op_done=(lambda op: hook(self, op)) if hook else None)
+        if st is not None:
+            st.finish_gradients(self)
+            st.apply_update(self)
+        else:
+            self.optimizer.apply(self.store)
+
+    def train_step(self, xb, yb, stats=None) -> None:
+        st = self._strategy()
+        stats = self._stats_buf() if stats is None else stats
+        self.store.zero_grad()
+        out = E.run_forward(self.ops, xb, self.ws, True)
+        dpred = self._loss_grad(out, yb, stats)
+        self.backward_and_update(dpred, st)
+
+    def train_on_batch(self, x, y, return_dict: bool = False):
+        xb, yb = self._prep_batch(x, y)
+        stats = self._stats_buf()
+        stats.zero_()
+        self.train_step(xb, yb, stats)
+        logs = self._logs_from(stats)
+        return logs if return_dict else [logs["loss"]] + [logs[m] for m in self.metric_names if m in logs]
+
+    def test_step(self, xb, yb, stats) -> None:
+        out = E.run_forward(self.ops, xb, self.ws, False)
+        self._loss_grad(out, yb, stats)
+
+    # ---------------------------------------------------------------- logs
+    def _logs_from(self, stats, prefix="") -> dict:
+        s = stats.detach()
+        st = self._strategy()
+        if st is not None and st.world_size > 1:
+            s = st.all_reduce_sum(s.clone())
+        s = s.double().cpu().numpy()
+        logs = {}
+        nsamp = max(s[4], 1.0)
+        logs[prefix + "loss"] = float(s[0] / nsamp)
+        for m in self.metric_names:
+            if m == "accuracy":
+                logs[prefix + "accuracy"] = float(s[1] / nsamp)
+            elif m == "mae":
+                logs[prefix + "mae"] = float(s[1] / max(s[3], 1.0))
+            elif m == "mse":
+                logs[prefix + "mse"] = float(s[2] / max(s[3], 1.0))
+        return logs
+
+    # ---------------------------------------------------------------- fit / evaluate / predict
+    @staticmethod
+    def _iter_batches(x, y, batch_size, shuffle, seed=None):
+        from ..data.dataset import Dataset
+
+        if isinstance(x, Dataset) or hasattr(x, "__iter__") and not isinstance(x, (np.ndarray, torch.Tensor)):
+            return iter(x)
+        n = len(x)
+        bs = batch_size or 32
+        idx = np.arange(n)
+        if shuffle:
+            np.random.default_rng(seed).shuffle(idx)
+
+        def gen():
+            for i in range(0, n, bs):
+                j = idx[i:i + bs]
+                yield (x[j], None if y is None else y[j])
+
+        return gen()
+
+    def fit(self, x=None, y=None, batch_size=None, epochs: int = 1, verbose="auto", callbacks=None,
+            validation_data=None, shuffle: bool = True, steps_per_epoch=None, validation_steps=None,
+            initial_epoch: int = 0):
+        if not self.built:
+            self.build()
+        if self.optimizer is None:
+            raise RuntimeError("call compile() before fit()")
+        verbose = 1 if verbose == "auto" else verbose
+        st = self._strategy()
+        is_chief = st is None or st.is_chief
+        hist = History()
+        callbacks = list(callbacks or [])
+        for cb in callbacks:
+            if hasattr(cb, "set_model"):
+                cb.set_model(self)
+            if hasattr(cb, "on_train_begin"):
+                cb.on_train_begin()
+        persistent_it = None
+        if steps_per_epoch is not None:
+            persistent_it = self._iter_batches(x, y, batch_size, shuffle)
+        stats = self._stats_buf()
+        for epoch in range(initial_epoch, epochs):
+            if verbose and is_chief:
+                print(f"Epoch {epoch + 1}/{epochs}", flush=True)
+            stats.zero_()
+            t0 = time.perf_counter()
+            it = persistent_it if persistent_it is not None else self._iter_batches(x, y, batch_size, shuffle,
+                                                                                   seed=epoch)
+            nsteps = 0
+            while steps_per_epoch is None or nsteps < steps_per_epoch:
+                try:
+                    batch = next(it)
+                except StopIteration:
+                    break
+                xb, yb = self._prep_batch(batch[0], batch[1])
+                self.train_step(xb, yb, stats)
+                nsteps += 1
+            logs = self._logs_from(stats)
+            if validation_data is not None:
+                vlogs = self.evaluate(*(validation_data if isinstance(validation_data, tuple) else (validation_data,)),
+                                      batch_size=batch_size, steps=validation_steps, verbose=0, return_dict=True,
+                                      _prefix="val_")
+                logs.update(vlogs)
+            dt = time.perf_counter() - t0
+            for k_, v_ in logs.items():
+                hist.history.setdefault(k_, []).append(v_)
+            hist.epoch.append(epoch)
+            if verbose and is_chief:
+                per = dt / max(nsteps, 1)
+                body = " - ".join(f"{k_}: {v_:.4f}" for k_, v_ in sorted(logs.items()))
+                print(f"{nsteps}/{nsteps} - {dt:.0f}s {per * 1e3:.0f}ms/step - {body}", flush=True)
+            for cb in callbacks:
+                if hasattr(cb, "on_epoch_end"):
+                    cb.on_epoch_end(epoch, logs)
+            if self.stop_training:
+                break
+        for cb in callbacks:
+            if hasattr(cb, "on_train_end"):
+                cb.on_train_end()
+        self.history = hist
+        return hist
+
+    def evaluate(self, x=None, y=None, batch_size=None, steps=None, verbose="auto", return_dict=False,
+                 _prefix=""):
+        stats = self._stats_buf("eval")
+        stats.zero_()
+        it = self._iter_batches(x, y, batch_size, False)
+        n = 0
+        while steps is None or n < steps:
+            try:
+                batch = next(it)
+            except StopIteration:
+                break
+            xb, yb = self._prep_batch(batch[0], batch[1])
+            self.test_step(xb, yb, stats)
+            n += 1
+        logs = self._logs_from(stats, prefix=_prefix)
+        if return_dict:
+            return logs
+        vals = [logs[_prefix + "loss"]] + [logs[_prefix + m] for m in self.metric_names if _prefix + m in logs]
+        return vals if len(vals) > 1 else vals[0]
+
+    def predict(self, x, batch_size=None, verbose=0, steps=None):
+        outs = []
+        it = self._iter_batches(x, None, batch_size, False)
+        n = 0
+        for batch in it:
+            xb = batch[0] if isinstance(batch, (tuple, list)) else batch
+            outs.append(self(xb, training=False).float().cpu().numpy().copy())
+            n += 1
+            if steps is not None and n >= steps:
+                break
+        return np.concatenate(outs, 0) if outs else np.zeros((0,) + tuple(self.output_shape), np.float32)
+
+    # ---------------------------------------------------------------- summary / save
+    def summary(self, print_fn=None):
+        pf = print_fn or print
+        rows = []
+        for l in self.layers:
+            rows.append((f"{l.name} ({l.keras_class})", str((None, *l.out_shape)), f"{l.param_count():,}"))
+        w = [max(31, max(len(r[0]) for r in rows) + 1), 22, 13]
+        line = lambda a, b, c, d: a + b * (w[0] + 2) + c + b * (w[1] + 2) + c + b * (w[2] + 2) + d  # noqa: E731
+        pf(f'Model: "{self.name}"')
+        pf(line("┏", "━", "┳", "┓"))
+        pf(f"┃ {'Layer (type)':<{w[0]}} ┃ {'Output Shape':<{w[1]}} ┃ {'Param #':>{w[2]}} ┃")
+        pf(line("┡", "━", "╇", "┩"))
+        for i, r in enumerate(rows):
+            pf(f"│ {r[0]:<{w[0]}} │ {r[1]:<{w[1]}} │ {r[2]:>{w[2]}} │")
+            pf(line("├", "─", "┼", "┤") if i + 1 < len(rows) else line("└", "─", "┴", "┘"))
+        total = self.count_params()
+        mb = total * 4 / 2 ** 20
+        pf(f" Total params: {total:,} ({mb:.2f} MB)")
+        pf(f" Trainable params: {total:,} ({mb:.2f} MB)")
+        pf(" Non-trainable params: 0 (0.00 B)")
+
+    def get_config(self) -> dict:
+        layers = [{"class_name": "InputLayer",
+                   "config": {"name": "input_layer", "batch_shape": [None, *self.input_shape], "dtype": "float32"}}]
+        for l in self.layers:
+            layers.append({"class_name": l.keras_class, "config": l.get_config()})
+        return {"name": self.name, "layers": layers}
+
+    def save(self, filepath: str) -> None:
+        """Keras-v3-shaped zip: config.json + metadata.json + model.weights.safetensors (weights in Keras
+        layouts, keyed ``layers/<name>/vars/<i>``; safetensors instead of HDF5 because h5py is absent)."""
+        from safetensors.numpy import save as st_save
+
+        st = self._strategy()
+        if st is not None and not st.is_chief:
+            return
+        cfg = {"module": "pyspark_tf_gke_amd.nn", "class_name": "Sequential", "config": self.get_config(),
+               "compile_config": {"optimizer": self.optimizer.get_config() if self.optimizer else None,
+                                  "loss": self.loss.name if self.loss else None, "metrics": self.metric_names}}
+        meta = {"keras_version": "3-compatible", "framework": "pyspark_tf_gke_amd",
+                "date_saved": time.strftime("%Y-%m-%d@%H:%M:%S"), "weights_format": "safetensors"}
+        tensors = {}
+        for l in self.layers:
+            for i, w in enumerate(l.keras_weights()):
+                tensors[f"layers/{l.name}/vars/{i}"] = np.ascontiguousarray(w.astype(np.float32))
+        os.makedirs(os.path.dirname(os.path.abspath(filepath)) or ".", exist_ok=True)
+        tmp = filepath + ".tmp"
+        with zipfile.ZipFile(tmp, "w") as zf:
+            zf.writestr("config.json", json.dumps(cfg, indent=2))
+            zf.writestr("metadata.json", json.dumps(meta, indent=2))
+            zf.writestr("model.weights.safetensors", st_save(tensors))
+        os.replace(tmp, filepath)
+
+
+def load_model(filepath: str, compile: bool = True, device=None) -> Sequential:
+    from safetensors.numpy import load as st_load
+
+    with zipfile.ZipFile(filepath) as zf:
+        cfg = json.loads(zf.read("config.json"))
+        tensors = st_load(zf.read("model.weights.safetensors"))
+    L.reset_name_counters()
+    m = Sequential(name=cfg["config"].get("name", "sequential"))
+    for lc in cfg["config"]["layers"]:
+        m.add(L.layer_from_config(lc["class_name"], lc["config"]))
+    m.build(device=device)
+    for l in m.layers:
+        ws = []
+        i = 0
+        while f"layers/{l.name}/vars/{i}" in tensors:
+            ws.append(tensors[f"layers/{l.name}/vars/{i}"])
+            i += 1
+        if ws:
+            l.set_keras_weights(ws)
+    m.store.refresh_bf16()
+    cc = cfg.get("compile_config") or {}
+    if compile and cc.get("loss"):
+        opt = cc.get("optimizer") or {}
+        m.compile(optimizer=OPT.Adam(learning_rate=opt.get("learning_rate", 1e-3)), loss=cc["loss"],
+                  metrics=cc.get("metrics"))
+    return m
+
+
+_ = (math, sys)

@@ -1,0 +1,74 @@
+"""Optimizers over the flat parameter store.
+
+``Adam`` reproduces ``tf.keras.optimizers.Adam`` (train_tf_ps.py:339,374 with lr 1e-3; the PS
+loops use 1e-4, :606,728): m/v moments, epsilon 1e-7, bias correction folded into the step size
+lr_t = lr * sqrt(1 - b2^t) / (1 - b1^t).  The whole model is updated by ONE fused kernel launch
+(``ptg_adam``) that also refreshes the bf16 compute copy.  ``apply(lo, hi)`` updates a byte range
+only: that is how the sharded parameter-server strategy gives each rank its shard of the update.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from ..ops import nn as K
+
+
+class Optimizer:
+    def __init__(self, learning_rate: float):
+        self.learning_rate = float(learning_rate)
+        self.iterations = 0
+
+    def get_config(self) -> dict:
+        return {"name": type(self).__name__.lower(), "learning_rate": self.learning_rate}
+
+    def apply_gradients(self, grads_and_vars) -> None:
+        from .tape import apply_gradients
+
+        apply_gradients(self, grads_and_vars)
+
+
+class Adam(Optimizer):
+    def __init__(self, learning_rate: float = 1e-3, beta_1: float = 0.9, beta_2: float = 0.999,
+                 epsilon: float = 1e-7, name: str = "adam"):
+        super().__init__(learning_rate)
+        self.beta_1, self.beta_2, self.epsilon = beta_1, beta_2, epsilon
+        self.name = name
+        self.m = None
+        self.v = None
+
+    def build(self, store) -> None:
+        if self.m is None or self.m.numel() != store.total or self.m.device != store.flat.device:
+            self.m = torch.zeros(store.total, dtype=torch.float32, device=store.flat.device)
+            self.v = torch.zeros(store.total, dtype=torch.float32, device=store.flat.device)
+
+    def lr_t(self, step: int) -> float:
+        b1, b2 = self.beta_1, self.beta_2
+        return self.learning_rate * math.sqrt(1.0 - b2 ** step) / (1.0 - b1 ** step)
+
+    def apply(self, store, gscale: float = 1.0, lo: int = 0, hi: int | None = None, advance: bool = True) -> None:
+        self.build(store)
+        step = self.iterations + 1
+        hi = store.total if hi is None else hi
+        if hi > lo:
+            sl = slice(lo, hi)
+            K.adam(store.flat[sl], store.flat_grad[sl], self.m[sl], self.v[sl], store.flat_bf16[sl],
+                   self.lr_t(step), self.beta_1, self.beta_2, self.epsilon, gscale)
+        if advance:
+            self.iterations = step
+
+    def get_config(self):
+        return {"name": self.name, "learning_rate": self.learning_rate, "beta_1": self.beta_1,
+                "beta_2": self.beta_2, "epsilon": self.epsilon}
+
+    def state_tensors(self) -> dict:
+        return {"m": self.m, "v": self.v}
+
+
+def get(identifier) -> Optimizer:
+    if isinstance(identifier, Optimizer):
+        return identifier
+    if isinstance(identifier, str) and identifier.lower() == "adam":
+        return Adam()
+    raise ValueError(f"unknown optimizer {identifier!r}")

@@ -1,0 +1,140 @@
+"""Flat parameter store.
+
+All parameters of a model live in ONE fp32 master buffer (plus one fp32 gradient buffer and one
+bf16 compute mirror at identical offsets).  This is the MI355X-native layout for the reference's
+per-variable Keras weights (train_tf_ps.py:328-378): the fused Adam kernel updates every
+parameter in a single launch, the data-parallel strategies all-reduce / reduce-scatter
+contiguous byte ranges (a handful of large RCCL collectives instead of one per variable), and the
+parameter-server strategy shards the buffer by byte range (the role of TF's
+``MinSizePartitioner``, train_tf_ps.py:505-507).
+
+Parameters are laid out in *reverse* layer order, so gradients complete front-to-back of the
+buffer during backward and bucketed all-reduce can start on the head while the tail is still
+being computed.  Every parameter starts on a 64-element boundary (16-byte vector access for the
+fp32 and bf16 views).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Callable
+
+import numpy as np
+import torch
+
+ALIGN = 64
+
+
+def glorot_uniform(fan_in: int, fan_out: int):
+    def init(shape, rng: np.random.Generator):
+        limit = math.sqrt(6.0 / (fan_in + fan_out))
+        return rng.uniform(-limit, limit, size=shape).astype(np.float32)
+
+    return init
+
+
+def zeros(shape, rng):
+    return np.zeros(shape, np.float32)
+
+
+def ones(shape, rng):
+    return np.ones(shape, np.float32)
+
+
+@dataclass
+class Param:
+    name: str
+    shape: tuple
+    init: Callable
+    overwrite_grad: bool = False  # backward writes (not accumulates) this gradient
+    logical_numel: int | None = None  # count shown by summary() (padding excluded)
+    order: int = 0
+    offset: int = -1
+    data: torch.Tensor | None = None
+    grad: torch.Tensor | None = None
+    bf16: torch.Tensor | None = None
+    mask_fn: Callable | None = None  # zero padded entries after init (e.g. padded input channels)
+
+    @property
+    def numel(self) -> int:
+        return int(np.prod(self.shape))
+
+
+@dataclass
+class ParamStore:
+    params: list = field(default_factory=list)
+    flat: torch.Tensor | None = None
+    flat_grad: torch.Tensor | None = None
+    flat_bf16: torch.Tensor | None = None
+    total: int = 0
+    device: torch.device | None = None
+    _zero_ranges: list = field(default_factory=list)
+
+    def add(self, name: str, shape, init, overwrite_grad=False, logical_numel=None, mask_fn=None) -> Param:
+        p = Param(name, tuple(int(s) for s in shape), init, overwrite_grad, logical_numel, len(self.params),
+                  mask_fn=mask_fn)
+        self.params.append(p)
+        return p
+
+    def finalize(self, device, seed: int = 0) -> None:
+        rng = np.random.default_rng(seed)
+        host_vals = {}
+        for p in self.params:  # init in declaration order (deterministic)
+            v = p.init(p.shape, rng)
+            if p.mask_fn is not None:
+                v = p.mask_fn(v)
+            host_vals[p.name] = v
+        off = 0
+        for p in reversed(self.params):  # reverse layer order = backward completion order
+            p.offset = off
+            off += int(math.ceil(p.numel / ALIGN) * ALIGN)
+        self.total = max(off, ALIGN)
+        self.device = torch.device(device)
+        flat_host = np.zeros(self.total, np.float32)
+        for p in self.params:
+            flat_host[p.offset:p.offset + p.numel] = host_vals[p.name].reshape(-1)
+        self.flat = torch.from_numpy(flat_host).to(self.device)
+        self.flat_grad = torch.zeros(self.total, dtype=torch.float32, device=self.device)
+        self.flat_bf16 = self.flat.to(torch.bfloat16)
+        self._bind_views()
+        # contiguous ranges whose gradient must be zeroed before each backward
+        ranges = []
+        for p in sorted(self.params, key=lambda q: q.offset):
+            if p.overwrite_grad:
+                continue
+            lo, hi = p.offset, p.offset + int(math.ceil(p.numel / ALIGN) * ALIGN)
+            if ranges and ranges[-1][1] == lo:
+                ranges[-1][1] = hi
+            else:
+                ranges.append([lo, hi])
+        self._zero_ranges = [tuple(r) for r in ranges]
+
+    def _bind_views(self) -> None:
+        for p in self.params:
+            sl = slice(p.offset, p.offset + p.numel)
+            p.data = self.flat[sl].view(p.shape)
+            p.grad = self.flat_grad[sl].view(p.shape)
+            p.bf16 = self.flat_bf16[sl].view(p.shape)
+
+    def zero_grad(self) -> None:
+        for lo, hi in self._zero_ranges:
+            self.flat_grad[lo:hi].zero_()
+
+    def refresh_bf16(self) -> None:
+        self.flat_bf16.copy_(self.flat.to(torch.bfloat16))
+
+    def by_name(self, name: str) -> Param:
+        for p in self.params:
+            if p.name == name:
+                return p
+        raise KeyError(name)
+
+    def num_params(self) -> int:
+        return sum(p.logical_numel if p.logical_numel is not None else p.numel for p in self.params)
+
+    def to(self, device) -> None:
+        self.device = torch.device(device)
+        self.flat = self.flat.to(self.device)
+        self.flat_grad = self.flat_grad.to(self.device)
+        self.flat_bf16 = self.flat_bf16.to(self.device)
+        self._bind_views()

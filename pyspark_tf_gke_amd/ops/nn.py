@@ -1,0 +1,282 @@
+"""Neural-network ops: GPU tensors run the hand-written gfx950 kernels (csrc/kernels/*.hip);
+CPU tensors run the fp32 PyTorch reference in :mod:`.reference` (the ``local`` host path and
+the numerics oracle of the tests).  There is no silent fallback: a GPU tensor with the HIP
+library missing raises.
+
+Layouts: activations NHWC bf16; conv filters [Cout][KH][KW][Cin]; dense weights [out][in];
+master parameters / gradients fp32.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import reference as ref
+from ._util import hip, need, on_device, ptr
+
+ACT = {None: 0, "linear": 0, "none": 0, "relu": 1, "softmax": 2}
+
+
+def conv_out_size(h: int, k: int, stride: int, pad: int) -> int:
+    return (h + 2 * pad - k) // stride + 1
+
+
+# ----------------------------------------------------------------------------------------------
+# Convolution (implicit GEMM on MFMA)
+# ----------------------------------------------------------------------------------------------
+def conv2d_fwd(x, w, bias, stride: int, pad: int, out, act: str | None = None):
+    """out[N,OH,OW,Cout] (bf16) = act(conv(x, w) + bias)."""
+    if not on_device(x):
+        return ref.conv2d_fwd(x, w, bias, stride, pad, out, act)
+    N, H, W, C = x.shape
+    Cout, KH, KW, Cw = w.shape
+    assert Cw == C, (w.shape, x.shape)
+    OH, OW = conv_out_size(H, KH, stride, pad), conv_out_size(W, KW, stride, pad)
+    assert tuple(out.shape) == (N, OH, OW, Cout), (out.shape, (N, OH, OW, Cout))
+    need(x, torch.bfloat16, "conv2d_fwd.x"); need(w, torch.bfloat16, "conv2d_fwd.w")
+    need(out, torch.bfloat16, "conv2d_fwd.out")
+    hip("ptg_conv2d_fwd", ptr(x), ptr(w), ptr(bias), ptr(out), N, H, W, C, Cout, KH, KW, stride, pad,
+        OH, OW, ACT[act])
+    return out
+
+
+def conv2d_dgrad(dz, w, pad: int, out):
+    """out[N,H,W,Cin] = d(conv)/dx for a stride-1 convolution."""
+    if not on_device(dz):
+        return ref.conv2d_dgrad(dz, w, pad, out)
+    N, H, W, Cout = dz.shape
+    Cw, KH, KW, Cin = w.shape
+    assert Cw == Cout and tuple(out.shape) == (N, H, W, Cin)
+    need(dz, torch.bfloat16, "dgrad.dz"); need(out, torch.bfloat16, "dgrad.out")
+    hip("ptg_conv2d_dgrad", ptr(dz), ptr(w), ptr(out), N, H, W, Cin, Cout, KH, KW, pad)
+    return out
+
+
+def conv2d_wgrad(x, dz, stride: int, pad: int, out, accumulate: bool = False, splits: int = 0):
+    """out[Cout,KH,KW,C] (fp32) (+)= d(conv)/dw."""
+    if not on_device(x):
+        return ref.conv2d_wgrad(x, dz, stride, pad, out, accumulate)
+    N, H, W, C = x.shape
+    _, OH, OW, Cout = dz.shape
+    Co, KH, KW, Cw = out.shape
+    assert Co == Cout and Cw == C
+    need(out, torch.float32, "wgrad.out")
+    if not accumulate:
+        out.zero_()
+    hip("ptg_conv2d_wgrad", ptr(x), ptr(dz), ptr(out), N, H, W, C, Cout, KH, KW, stride, pad, OH, OW, splits)
+    return out
+
+
+# ----------------------------------------------------------------------------------------------
+# Dense (MFMA GEMM)
+# ----------------------------------------------------------------------------------------------
+def gemm(M, N, K, a, lda, a_kcontig, b, ldb, b_kcontig, epi, c, ldc, bias=None, act=0, splits=1):
+    hip("ptg_gemm_bf16", M, N, K, ptr(a), lda, int(a_kcontig), ptr(b), ldb, int(b_kcontig), epi, ptr(c), ldc,
+        ptr(bias), act, splits)
+
+
+def linear_fwd(x, w, bias, act, out, workspace=None, splits: int = 0):
+    """out[M,N] bf16 = act(x[M,K] @ w[N,K]^T + bias). Split-K with an fp32 workspace when the
+    output tile grid alone cannot fill the 256 CUs (e.g. M=batch, K=20480)."""
+    if not on_device(x):
+        return ref.linear_fwd(x, w, bias, act, out)
+    M, K = x.shape
+    N = w.shape[0]
+    if splits == 0:
+        tiles = math.ceil(M / 128) * math.ceil(N / 128)
+        splits = 1 if tiles >= 192 or K < 4096 else min(16, max(1, 512 // max(tiles, 1)), K // 1024)
+    if splits > 1:
+        if workspace is None or workspace.numel() < M * N:
+            workspace = torch.empty(M * N, device=x.device, dtype=torch.float32)
+        ws = workspace[: M * N]
+        ws.zero_()
+        gemm(M, N, K, x, K, 1, w, K, 1, 3, ws, N, None, 0, splits)
+        hip("ptg_bias_act", ptr(ws), ptr(bias), ptr(out), None, M, N, ACT[act])
+    else:
+        gemm(M, N, K, x, K, 1, w, K, 1, 0, out, N, bias, ACT[act], 1)
+    return out
+
+
+def linear_dx(dy, w, out):
+    """out[M,K] bf16 = dy[M,N] @ w[N,K]."""
+    if not on_device(dy):
+        return ref.linear_dx(dy, w, out)
+    M, N = dy.shape
+    K = w.shape[1]
+    gemm(M, K, N, dy, N, 1, w, K, 0, 0, out, K)
+    return out
+
+
+def linear_dw(dy, x, out, accumulate: bool = False):
+    """out[N,K] fp32 (+)= dy[M,N]^T @ x[M,K]."""
+    if not on_device(dy):
+        return ref.linear_dw(dy, x, out, accumulate)
+    M, N = dy.shape
+    K = x.shape[1]
+    gemm(N, K, M, dy, N, 0, x, K, 0, 2 if accumulate else 1, out, K)
+    return out
+
+
+def col_sum(g, out):
+    """out[N] += sum over rows of g[M,N]."""
+    if not on_device(g):
+        return ref.col_sum(g, out)
+    M, N = g.shape
+    hip("ptg_col_sum", ptr(g), int(g.dtype == torch.bfloat16), ptr(out), M, N)
+    return out
+
+
+def bias_act(acc, bias, act, out_bf16=None, out32=None):
+    if not on_device(acc):
+        return ref.bias_act(acc, bias, act, out_bf16, out32)
+    M, N = acc.shape
+    hip("ptg_bias_act", ptr(acc), ptr(bias), ptr(out_bf16), ptr(out32), M, N, ACT[act])
+
+
+def dense_small_fwd(x, w, b, act, out, out_bf16=None):
+    """out[M,N] fp32 = act(x[M,K] @ w[N,K]^T + b) for narrow layers (N <= 64)."""
+    if not on_device(x):
+        return ref.dense_small_fwd(x, w, b, act, out, out_bf16)
+    M, K = x.shape
+    N = w.shape[0]
+    hip("ptg_dense_small_fwd", ptr(x), int(x.dtype == torch.bfloat16), ptr(w), ptr(b), ptr(out), ptr(out_bf16),
+        M, K, N, ACT[act])
+    return out
+
+
+def dense_small_dx(dy, w, mask, out):
+    """out[M,K] = (dy[M,N] @ w[N,K]) * (mask > 0 if mask is given)."""
+    if not on_device(dy):
+        return ref.dense_small_dx(dy, w, mask, out)
+    M, N = dy.shape
+    K = w.shape[1]
+    mk = 0 if mask is None else (2 if mask.dtype == torch.bfloat16 else 1)
+    hip("ptg_dense_small_dx", ptr(dy), ptr(w), ptr(mask), mk, ptr(out), int(out.dtype == torch.bfloat16), M, K, N)
+    return out
+
+
+def dense_small_dw(dy, x, dw, db):
+    """dw[N,K] += dy^T x ; db[N] += sum_m dy (fp32)."""
+    if not on_device(dy):
+        return ref.dense_small_dw(dy, x, dw, db)
+    M, N = dy.shape
+    K = x.shape[1]
+    hip("ptg_dense_small_dw", ptr(dy), ptr(x), int(x.dtype == torch.bfloat16), ptr(dw), ptr(db), M, K, N)
+
+
+# ----------------------------------------------------------------------------------------------
+# PReLU / pooling
+# ----------------------------------------------------------------------------------------------
+def prelu_pool_fwd(z, alpha, out):
+    if not on_device(z):
+        return ref.prelu_pool_fwd(z, alpha, out)
+    N, H, W, C = z.shape
+    hip("ptg_prelu_pool_fwd", ptr(z), ptr(alpha), ptr(out), N, H, W, C)
+    return out
+
+
+def prelu_pool_bwd(dp, z, alpha, dz_out, dalpha, dbias):
+    """dz_out = d/dz of maxpool2x2(prelu(z)); dalpha, dbias accumulate (fp32)."""
+    if not on_device(z):
+        return ref.prelu_pool_bwd(dp, z, alpha, dz_out, dalpha, dbias)
+    N, H, W, C = z.shape
+    hip("ptg_prelu_pool_bwd", ptr(dp), ptr(z), ptr(alpha), ptr(dz_out), ptr(dalpha), ptr(dbias), N, H, W, C, 0)
+    return dz_out
+
+
+def prelu_fwd(z, alpha, out):
+    if not on_device(z):
+        return ref.prelu_fwd(z, alpha, out)
+    N = z.shape[0]
+    hip("ptg_prelu_fwd", ptr(z), ptr(alpha), ptr(out), N, z[0].numel())
+    return out
+
+
+def prelu_bwd(da, z, alpha, dz_out, dalpha, dbias):
+    if not on_device(z):
+        return ref.prelu_bwd(da, z, alpha, dz_out, dalpha, dbias)
+    N = z.shape[0]
+    C = z.shape[-1]
+    hip("ptg_prelu_bwd", ptr(da), ptr(z), ptr(alpha), ptr(dz_out), ptr(dalpha), ptr(dbias), N, z[0].numel(), C, 0)
+    return dz_out
+
+
+def gap_fwd(x, out):
+    """Global average pool NHWC -> [N, C] fp32."""
+    if not on_device(x):
+        return ref.gap_fwd(x, out)
+    N, H, W, C = x.shape
+    hip("ptg_gap_fwd", ptr(x), ptr(out), N, H * W, C)
+    return out
+
+
+def gap_bwd(dy, out):
+    if not on_device(dy):
+        return ref.gap_bwd(dy, out)
+    N, H, W, C = out.shape
+    hip("ptg_gap_bwd", ptr(dy), ptr(out), N, H * W, C)
+    return out
+
+
+# ----------------------------------------------------------------------------------------------
+# Losses, optimizer, conversions
+# ----------------------------------------------------------------------------------------------
+def mse(pred, y, dpred, stats, gscale: float = 1.0):
+    if not on_device(pred):
+        return ref.mse(pred, y, dpred, stats, gscale)
+    B, D = pred.shape
+    hip("ptg_mse", ptr(pred), ptr(y), ptr(dpred), ptr(stats), B, D, float(gscale))
+
+
+def softmax_xent(logits, labels, dlogits, stats, gscale: float = 1.0):
+    if not on_device(logits):
+        return ref.softmax_xent(logits, labels, dlogits, stats, gscale)
+    B, C = logits.shape
+    hip("ptg_softmax_xent", ptr(logits), ptr(labels), ptr(dlogits), ptr(stats), B, C, float(gscale))
+
+
+def adam(p, g, m, v, pbf, lr_t: float, b1: float, b2: float, eps: float, gscale: float = 1.0):
+    if not on_device(p):
+        return ref.adam(p, g, m, v, pbf, lr_t, b1, b2, eps, gscale)
+    hip("ptg_adam", ptr(p), ptr(g), ptr(m), ptr(v), ptr(pbf), p.numel(), float(lr_t), float(b1), float(b2),
+        float(eps), float(gscale))
+
+
+def cast_f32_bf16(x, out):
+    if not on_device(x):
+        out.copy_(x.to(torch.bfloat16))
+        return out
+    hip("ptg_cast_f32_bf16", ptr(x), ptr(out), x.numel())
+    return out
+
+
+def resize_norm(images_u8, out, H: int, W: int):
+    """uint8 [N,Hin,Win,3] -> bf16 [N,H,W,4] bilinear (half-pixel) resize, /255, zero 4th channel."""
+    if not on_device(images_u8):
+        return ref.resize_norm(images_u8, out, H, W)
+    N, Hin, Win, _ = images_u8.shape
+    hip("ptg_resize_norm", ptr(images_u8), ptr(out), N, Hin, Win, H, W)
+    return out
+
+
+def pack_rgb4(images_f32, out):
+    """float [N,H,W,3] -> bf16 [N,H,W,4]."""
+    if not on_device(images_f32):
+        out.zero_()
+        out[..., :3] = images_f32.to(torch.bfloat16)
+        return out
+    npix = images_f32.numel() // 3
+    hip("ptg_pack_rgb4", ptr(images_f32), ptr(out), npix)
+    return out
+
+
+def relu_bwd(dy, y, out):
+    """out = (y > 0) * dy."""
+    if not on_device(dy):
+        out.copy_((dy.float() * (y.float() > 0)).to(out.dtype))
+        return out
+    flags = int(dy.dtype == torch.bfloat16) | (int(y.dtype == torch.bfloat16) << 1) | \
+        (int(out.dtype == torch.bfloat16) << 2)
+    hip("ptg_relu_bwd", ptr(dy), ptr(y), ptr(out), out.numel(), flags)
+    return out

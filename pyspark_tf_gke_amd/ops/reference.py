@@ -1,0 +1,202 @@
+"""fp32 PyTorch reference implementations of every NN op (CPU).
+
+These serve two roles: the host execution path for CPU tensors (``local`` mode, the CPU test
+suite) and the numerics oracle the GPU tests compare the HIP kernels against.  Each function has
+the same in/out contract as its counterpart in :mod:`.nn` (NHWC activations, [Cout,KH,KW,Cin]
+filters, [out,in] dense weights, results written into the provided ``out`` tensors).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+
+def _f(t):
+    return t.float()
+
+
+def _act(y, act):
+    if act == "relu":
+        return torch.relu(y)
+    if act == "softmax":
+        return torch.softmax(y, dim=-1)
+    return y
+
+
+def conv2d_fwd(x, w, bias, stride, pad, out, act=None):
+    xn = _f(x).permute(0, 3, 1, 2)
+    wn = _f(w).permute(0, 3, 1, 2)
+    y = F.conv2d(xn, wn, None if bias is None else _f(bias), stride=stride, padding=pad)
+    out.copy_(_act(y.permute(0, 2, 3, 1), act).to(out.dtype))
+    return out
+
+
+def conv2d_dgrad(dz, w, pad, out):
+    N, H, W, Cin = out.shape
+    wn = _f(w).permute(0, 3, 1, 2)  # [Cout, Cin, KH, KW]
+    dx = torch.nn.grad.conv2d_input((N, Cin, H, W), wn, _f(dz).permute(0, 3, 1, 2), stride=1, padding=pad)
+    out.copy_(dx.permute(0, 2, 3, 1).to(out.dtype))
+    return out
+
+
+def conv2d_wgrad(x, dz, stride, pad, out, accumulate=False):
+    Cout, KH, KW, C = out.shape
+    xn = _f(x).permute(0, 3, 1, 2)
+    dw = torch.nn.grad.conv2d_weight(xn, (Cout, C, KH, KW), _f(dz).permute(0, 3, 1, 2), stride=stride,
+                                     padding=pad)
+    dw = dw.permute(0, 2, 3, 1)
+    if accumulate:
+        out.add_(dw)
+    else:
+        out.copy_(dw)
+    return out
+
+
+def linear_fwd(x, w, bias, act, out):
+    y = _f(x) @ _f(w).t()
+    if bias is not None:
+        y = y + _f(bias)
+    out.copy_(_act(y, act).to(out.dtype))
+    return out
+
+
+def linear_dx(dy, w, out):
+    out.copy_((_f(dy) @ _f(w)).to(out.dtype))
+    return out
+
+
+def linear_dw(dy, x, out, accumulate=False):
+    dw = _f(dy).t() @ _f(x)
+    if accumulate:
+        out.add_(dw)
+    else:
+        out.copy_(dw)
+    return out
+
+
+def col_sum(g, out):
+    out.add_(_f(g).sum(0))
+    return out
+
+
+def bias_act(acc, bias, act, out_bf16=None, out32=None):
+    y = _f(acc) + (0 if bias is None else _f(bias))
+    y = _act(y, act)
+    if out_bf16 is not None:
+        out_bf16.copy_(y.to(out_bf16.dtype))
+    if out32 is not None:
+        out32.copy_(y)
+
+
+def dense_small_fwd(x, w, b, act, out, out_bf16=None):
+    y = _f(x) @ _f(w).t()
+    if b is not None:
+        y = y + _f(b)
+    y = _act(y, act)
+    out.copy_(y)
+    if out_bf16 is not None:
+        out_bf16.copy_(y.to(out_bf16.dtype))
+    return out
+
+
+def dense_small_dx(dy, w, mask, out):
+    dx = _f(dy) @ _f(w)
+    if mask is not None:
+        dx = dx * (_f(mask) > 0)
+    out.copy_(dx.to(out.dtype))
+    return out
+
+
+def dense_small_dw(dy, x, dw, db):
+    dw.add_(_f(dy).t() @ _f(x))
+    if db is not None:
+        db.add_(_f(dy).sum(0))
+
+
+def _prelu(z, alpha):
+    return torch.where(z > 0, z, alpha * z)
+
+
+def prelu_pool_fwd(z, alpha, out):
+    y = _prelu(_f(z), _f(alpha))
+    p = F.max_pool2d(y.permute(0, 3, 1, 2), 2, 2).permute(0, 2, 3, 1)
+    out.copy_(p.to(out.dtype))
+    return out
+
+
+def prelu_pool_bwd(dp, z, alpha, dz_out, dalpha, dbias):
+    zf = _f(z).detach().requires_grad_(True)
+    af = _f(alpha).detach().requires_grad_(True)
+    p = F.max_pool2d(_prelu(zf, af).permute(0, 3, 1, 2), 2, 2).permute(0, 2, 3, 1)
+    p.backward(_f(dp))
+    dz_out.copy_(zf.grad.to(dz_out.dtype))
+    dalpha.add_(af.grad)
+    dbias.add_(zf.grad.sum((0, 1, 2)))
+    return dz_out
+
+
+def prelu_fwd(z, alpha, out):
+    out.copy_(_prelu(_f(z), _f(alpha)).to(out.dtype))
+    return out
+
+
+def prelu_bwd(da, z, alpha, dz_out, dalpha, dbias):
+    zf, af, g = _f(z), _f(alpha), _f(da)
+    dz = torch.where(zf > 0, g, g * af)
+    dz_out.copy_(dz.to(dz_out.dtype))
+    dalpha.add_(torch.where(zf > 0, torch.zeros_like(g), g * zf).sum(0))
+    dbias.add_(dz.reshape(-1, dz.shape[-1]).sum(0))
+    return dz_out
+
+
+def gap_fwd(x, out):
+    out.copy_(_f(x).mean((1, 2)))
+    return out
+
+
+def gap_bwd(dy, out):
+    N, H, W, C = out.shape
+    out.copy_((_f(dy) / (H * W)).reshape(N, 1, 1, C).expand(N, H, W, C).to(out.dtype))
+    return out
+
+
+def mse(pred, y, dpred, stats, gscale=1.0):
+    d = _f(pred) - _f(y)
+    B = pred.shape[0]
+    n = d.numel()
+    dpred.copy_(2.0 * d / n * gscale)
+    sse = (d * d).sum()
+    stats[0] += sse / n * B
+    stats[1] += d.abs().sum()
+    stats[2] += sse
+    stats[3] += n
+    stats[4] += B
+
+
+def softmax_xent(logits, labels, dlogits, stats, gscale=1.0):
+    lg = _f(logits)
+    B, C = lg.shape
+    p = torch.softmax(lg, dim=-1)
+    onehot = F.one_hot(labels.long(), C).float()
+    dlogits.copy_((p - onehot) / B * gscale)
+    pl = p.gather(1, labels.long().view(-1, 1)).clamp(1e-7, 1 - 1e-7)
+    stats[0] += (-pl.log()).sum()
+    stats[1] += (lg.argmax(-1) == labels.long()).float().sum()
+    stats[4] += B
+
+
+def adam(p, g, m, v, pbf, lr_t, b1, b2, eps, gscale=1.0):
+    gg = g * gscale
+    m.mul_(b1).add_(gg, alpha=1 - b1)
+    v.mul_(b2).addcmul_(gg, gg, value=1 - b2)
+    p.sub_(lr_t * m / (v.sqrt() + eps))
+    if pbf is not None:
+        pbf.copy_(p.to(pbf.dtype))
+
+
+def resize_norm(images_u8, out, H, W):
+    x = images_u8.float().permute(0, 3, 1, 2)
+    y = F.interpolate(x, size=(H, W), mode="bilinear", align_corners=False, antialias=False) / 255.0
+    out.zero_()
+    out[..., :3] = y.permute(0, 2, 3, 1).to(out.dtype)
+    return out

@@ -1,0 +1,129 @@
+"""Process-group bootstrap and the collectives the runtime uses (RCCL over xGMI on MI355X).
+
+One OS process per GPU.  Ranks are launched by ``torch.distributed.run`` or by our own launcher
+(:mod:`pyspark_tf_gke_amd.runtime.launcher`) and read RANK / LOCAL_RANK / WORLD_SIZE /
+MASTER_ADDR / MASTER_PORT.  On GPUs the backend is ``nccl`` (= RCCL on ROCm); on CPU it is ``gloo``
+(the multi-process CPU tests).
+
+This replaces the reference's transports: Spark Netty shuffle/RPC (ports 7077/7078/7079,
+spark_session.py:44-50) and TF gRPC between chief, workers and PS (train_tf_ps.py:501-504) —
+SURVEY §2.4.  Tensor payloads go through RCCL; control goes through the TCP store torch creates.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def env_rank() -> tuple[int, int, int]:
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    return rank, local, world
+
+
+def is_initialized() -> bool:
+    return dist.is_available() and dist.is_initialized()
+
+
+def init(backend: str | None = None, device_type: str | None = None, timeout_s: int = 600) -> tuple[int, int]:
+    """Initialise the default process group from the environment (idempotent).
+    Returns (rank, world_size)."""
+    rank, local, world = env_rank()
+    if is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    if world <= 1:
+        return 0, 1
+    if device_type is None:
+        device_type = "cuda" if torch.cuda.is_available() else "cpu"
+    if backend is None:
+        backend = "nccl" if device_type == "cuda" else "gloo"
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29500")
+    kw = {}
+    if device_type == "cuda":
+        torch.cuda.set_device(local)
+        kw["device_id"] = torch.device("cuda", local)
+    dist.init_process_group(backend=backend, rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    return rank, world
+
+
+def rank() -> int:
+    return dist.get_rank() if is_initialized() else 0
+
+
+def world_size() -> int:
+    return dist.get_world_size() if is_initialized() else 1
+
+
+def barrier() -> None:
+    if is_initialized():
+        if dist.get_backend() == "nccl":
+            dist.barrier(device_ids=[torch.cuda.current_device()])
+        else:
+            dist.barrier()
+
+
+def all_reduce_(t: torch.Tensor, op=dist.ReduceOp.SUM, async_op: bool = False):
+    if not is_initialized() or dist.get_world_size() == 1:
+        return None
+    return dist.all_reduce(t, op=op, async_op=async_op)
+
+
+def all_reduce_max_scalar(x: float) -> float:
+    if not is_initialized():
+        return x
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def broadcast_(t: torch.Tensor, src: int = 0):
+    if is_initialized() and dist.get_world_size() > 1:
+        dist.broadcast(t, src)
+    return t
+
+
+def reduce_scatter_flat(out_shard: torch.Tensor, full: torch.Tensor, async_op=False):
+    return dist.reduce_scatter_tensor(out_shard, full, op=dist.ReduceOp.SUM, async_op=async_op)
+
+
+def all_gather_flat(full: torch.Tensor, shard: torch.Tensor, async_op=False):
+    return dist.all_gather_into_tensor(full, shard, async_op=async_op)
+
+
+def all_to_all_v(send: torch.Tensor, send_counts: list[int], recv_counts: list[int] | None = None) -> torch.Tensor:
+    """Variable all-to-all of rows (dim 0).  Size exchange first (one int64 all_to_all), then the
+    payload with split sizes: the two-phase shuffle of SURVEY §5.8 / M12."""
+    if not is_initialized() or dist.get_world_size() == 1:
+        return send
+    world = dist.get_world_size()
+    dev = send.device
+    if recv_counts is None:
+        sc = torch.tensor(send_counts, dtype=torch.int64, device=dev)
+        rc = torch.empty(world, dtype=torch.int64, device=dev)
+        dist.all_to_all_single(rc, sc)
+        recv_counts = rc.cpu().tolist()
+    row = send.shape[1:]
+    out = torch.empty((int(sum(recv_counts)), *row), dtype=send.dtype, device=dev)
+    dist.all_to_all_single(out, send, output_split_sizes=[int(c) for c in recv_counts],
+                           input_split_sizes=[int(c) for c in send_counts])
+    return out
+
+
+def all_gather_object(obj):
+    if not is_initialized() or dist.get_world_size() == 1:
+        return [obj]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, obj)
+    return out
+
+
+def destroy() -> None:
+    if is_initialized():
+        dist.destroy_process_group()

@@ -1,0 +1,227 @@
+"""Numerics of every HIP training kernel vs the fp32 PyTorch reference of the same op (run on the
+MI355X box).  Inputs are bf16-rounded first, so the only differences are accumulation order and
+output rounding."""
+import pytest
+import torch
+
+from pyspark_tf_gke_amd.ops import nn as K
+from pyspark_tf_gke_amd.ops import reference as R
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _close(a, b, rtol=2e-2, atol=2e-2, name=""):
+    a, b = a.float().cpu(), b.float().cpu()
+    err = (a - b).abs().max().item()
+    scale = b.abs().max().item() + 1e-6
+    assert err <= atol + rtol * scale, f"{name}: max err {err:.4g} vs scale {scale:.4g}"
+
+
+def rnd(*shape, dtype=torch.bfloat16, scale=1.0):
+    return (torch.randn(*shape) * scale).to(dtype)
+
+
+@pytest.fixture(autouse=True)
+def _seed(hip_built):
+    torch.manual_seed(0)
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 2048, 1024), (100, 72, 40), (64, 256, 2048), (512, 16, 96)])
+@pytest.mark.parametrize("layout", ["kk", "kmn", "mnmn", "mnk"])
+def test_gemm_layouts(M, N, K, layout):
+    a = rnd(M, K) if layout in ("kk", "kmn") else rnd(K, M)
+    b = rnd(N, K) if layout in ("kk", "mnk") else rnd(K, N)
+    A = a.float() if layout in ("kk", "kmn") else a.float().t()
+    Bm = b.float().t() if layout in ("kk", "mnk") else b.float()
+    ref = A @ Bm
+    c = torch.empty(M, N, device=DEV, dtype=torch.float32)
+    ak = layout in ("kk", "kmn")
+    bk = layout in ("kk", "mnk")
+    K.gemm(M, N, K, a.to(DEV), K if ak else M, ak, b.to(DEV), K if bk else N, bk, 1, c, N)
+    _close(c, ref, 1e-3, 1e-3, "gemm")
+
+
+def test_gemm_splitk_atomic_and_bias_relu():
+    M, N, Kd = 64, 2048, 20480
+    x, w = rnd(M, Kd, scale=0.1), rnd(N, Kd, scale=0.1)
+    b = torch.randn(N)
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    K.linear_fwd(x.to(DEV), w.to(DEV), b.to(DEV), "relu", out)
+    ref = torch.relu(x.float() @ w.float().t() + b)
+    _close(out, ref, 2e-2, 2e-2, "linear_fwd")
+
+
+def test_linear_dx_dw():
+    M, N, Kd = 128, 2048, 20480 // 8
+    dy, w, x = rnd(M, N), rnd(N, Kd), rnd(M, Kd)
+    dx = torch.empty(M, Kd, device=DEV, dtype=torch.bfloat16)
+    K.linear_dx(dy.to(DEV), w.to(DEV), dx)
+    _close(dx, dy.float() @ w.float(), 2e-2, 2e-2, "dx")
+    dw = torch.empty(N, Kd, device=DEV)
+    K.linear_dw(dy.to(DEV), x.to(DEV), dw)
+    _close(dw, dy.float().t() @ x.float(), 1e-3, 1e-3, "dw")
+
+
+CONV_CASES = [(2, 16, 20, 4, 8, 5), (2, 16, 20, 8, 16, 5), (2, 12, 10, 16, 32, 5), (3, 8, 10, 32, 64, 5),
+              (2, 8, 8, 64, 64, 5), (2, 9, 7, 16, 64, 3), (1, 6, 6, 8, 128, 3)]
+
+
+@pytest.mark.parametrize("N,H,W,C,Co,KS", CONV_CASES)
+def test_conv_fwd(N, H, W, C, Co, KS):
+    x, w, b = rnd(N, H, W, C), rnd(Co, KS, KS, C, scale=0.2), torch.randn(Co)
+    pad = KS // 2
+    out = torch.empty(N, H, W, Co, device=DEV, dtype=torch.bfloat16)
+    K.conv2d_fwd(x.to(DEV), w.to(DEV), b.to(DEV), 1, pad, out)
+    ref = torch.empty(N, H, W, Co, dtype=torch.bfloat16)
+    R.conv2d_fwd(x, w, b, 1, pad, ref)
+    _close(out, ref, 2e-2, 2e-2, "conv_fwd")
+
+
+def test_conv_fwd_strided_valid():
+    x, w = rnd(2, 15, 13, 8), rnd(16, 3, 3, 8, scale=0.2)
+    out = torch.empty(2, 7, 6, 16, device=DEV, dtype=torch.bfloat16)
+    K.conv2d_fwd(x.to(DEV), w.to(DEV), None, 2, 0, out)
+    ref = torch.empty(2, 7, 6, 16, dtype=torch.bfloat16)
+    R.conv2d_fwd(x, w, None, 2, 0, ref)
+    _close(out, ref, 2e-2, 2e-2, "conv_fwd_s2")
+
+
+@pytest.mark.parametrize("N,H,W,C,Co,KS", [c for c in CONV_CASES if c[3] % 8 == 0])
+def test_conv_dgrad(N, H, W, C, Co, KS):
+    dz, w = rnd(N, H, W, Co), rnd(Co, KS, KS, C, scale=0.2)
+    pad = KS // 2
+    out = torch.empty(N, H, W, C, device=DEV, dtype=torch.bfloat16)
+    K.conv2d_dgrad(dz.to(DEV), w.to(DEV), pad, out)
+    ref = torch.empty(N, H, W, C, dtype=torch.bfloat16)
+    R.conv2d_dgrad(dz, w, pad, ref)
+    _close(out, ref, 2e-2, 2e-2, "dgrad")
+
+
+@pytest.mark.parametrize("N,H,W,C,Co,KS", CONV_CASES)
+def test_conv_wgrad(N, H, W, C, Co, KS):
+    x, dz = rnd(N, H, W, C), rnd(N, H, W, Co)
+    pad = KS // 2
+    out = torch.empty(Co, KS, KS, C, device=DEV)
+    K.conv2d_wgrad(x.to(DEV), dz.to(DEV), 1, pad, out)
+    ref = torch.empty(Co, KS, KS, C)
+    R.conv2d_wgrad(x, dz, 1, pad, ref)
+    _close(out, ref, 1e-3, 1e-3, "wgrad")
+
+
+def test_conv_wgrad_large_splitk():
+    x, dz = rnd(8, 64, 80, 16), rnd(8, 64, 80, 32, scale=0.1)
+    out = torch.empty(32, 5, 5, 16, device=DEV)
+    K.conv2d_wgrad(x.to(DEV), dz.to(DEV), 1, 2, out)
+    ref = torch.empty(32, 5, 5, 16)
+    R.conv2d_wgrad(x, dz, 1, 2, ref)
+    _close(out, ref, 1e-3, 1e-3, "wgrad_big")
+
+
+@pytest.mark.parametrize("C", [8, 16, 64, 128])
+def test_prelu_pool_fwd_bwd(C):
+    N, H, W = 3, 8, 12
+    z = rnd(N, H, W, C)
+    alpha = torch.randn(H, W, C) * 0.3
+    alpha[0, 0, :] = 0.0  # exercise ties of zeros
+    z[0, :2, :2, :] = -1.0
+    p = torch.empty(N, H // 2, W // 2, C, device=DEV, dtype=torch.bfloat16)
+    K.prelu_pool_fwd(z.to(DEV), alpha.to(DEV), p)
+    pr = torch.empty(N, H // 2, W // 2, C, dtype=torch.bfloat16)
+    R.prelu_pool_fwd(z, alpha, pr)
+    _close(p, pr, 1e-2, 1e-2, "prelu_pool_fwd")
+    dp = rnd(N, H // 2, W // 2, C)
+    dz = torch.empty(N, H, W, C, device=DEV, dtype=torch.bfloat16)
+    da = torch.zeros(H, W, C, device=DEV)
+    db = torch.zeros(C, device=DEV)
+    K.prelu_pool_bwd(dp.to(DEV), z.to(DEV), alpha.to(DEV), dz, da, db)
+    dzr = torch.empty(N, H, W, C, dtype=torch.bfloat16)
+    dar, dbr = torch.zeros(H, W, C), torch.zeros(C)
+    R.prelu_pool_bwd(dp, z, alpha, dzr, dar, dbr)
+    _close(dz, dzr, 1e-2, 1e-2, "dz")
+    _close(da, dar, 1e-2, 1e-2, "dalpha")
+    _close(db, dbr, 1e-2, 1e-2, "dbias")
+
+
+def test_prelu_fwd_bwd():
+    N, H, W, C = 4, 16, 20, 64
+    z, alpha, da = rnd(N, H, W, C), torch.randn(H, W, C) * 0.2, rnd(N, H, W, C)
+    a = torch.empty_like(z, device=DEV)
+    K.prelu_fwd(z.to(DEV), alpha.to(DEV), a)
+    ar = torch.empty_like(z)
+    R.prelu_fwd(z, alpha, ar)
+    _close(a, ar, 1e-2, 1e-2, "prelu_fwd")
+    dz = torch.empty_like(z, device=DEV)
+    dal, db = torch.zeros(H, W, C, device=DEV), torch.zeros(C, device=DEV)
+    K.prelu_bwd(da.to(DEV), z.to(DEV), alpha.to(DEV), dz, dal, db)
+    dzr, dalr, dbr = torch.empty_like(z), torch.zeros(H, W, C), torch.zeros(C)
+    R.prelu_bwd(da, z, alpha, dzr, dalr, dbr)
+    _close(dz, dzr, 1e-2, 1e-2, "dz")
+    _close(dal, dalr, 1e-2, 1e-2, "dalpha")
+    _close(db, dbr, 1e-2, 1e-2, "dbias")
+
+
+@pytest.mark.parametrize("M,Kd,N,act", [(32, 3, 16, "relu"), (64, 64, 15, "softmax"), (128, 2048, 2, None)])
+def test_dense_small(M, Kd, N, act):
+    x, w, b = torch.randn(M, Kd), torch.randn(N, Kd) * 0.1, torch.randn(N)
+    y = torch.empty(M, N, device=DEV)
+    K.dense_small_fwd(x.to(DEV), w.to(DEV), b.to(DEV), act, y)
+    yr = torch.empty(M, N)
+    R.dense_small_fwd(x, w, b, act, yr)
+    _close(y, yr, 1e-4, 1e-4, "small_fwd")
+    dy = torch.randn(M, N)
+    mask = torch.randn(M, Kd)
+    dx = torch.empty(M, Kd, device=DEV)
+    K.dense_small_dx(dy.to(DEV), w.to(DEV), mask.to(DEV), dx)
+    dxr = torch.empty(M, Kd)
+    R.dense_small_dx(dy, w, mask, dxr)
+    _close(dx, dxr, 1e-4, 1e-4, "small_dx")
+    dw, db = torch.zeros(N, Kd, device=DEV), torch.zeros(N, device=DEV)
+    K.dense_small_dw(dy.to(DEV), x.to(DEV), dw, db)
+    dwr, dbr = torch.zeros(N, Kd), torch.zeros(N)
+    R.dense_small_dw(dy, x, dwr, dbr)
+    _close(dw, dwr, 1e-4, 1e-4, "small_dw")
+    _close(db, dbr, 1e-4, 1e-4, "small_db")
+
+
+def test_losses_and_adam():
+    B = 64
+    pred, y = torch.randn(B, 2) * 10, torch.randn(B, 2) * 10
+    d = torch.empty(B, 2, device=DEV)
+    st = torch.zeros(8, device=DEV)
+    K.mse(pred.to(DEV), y.to(DEV), d, st)
+    dr, sr = torch.empty(B, 2), torch.zeros(8)
+    R.mse(pred, y, dr, sr)
+    _close(d, dr, 1e-5, 1e-5, "mse_grad")
+    _close(st[:5], sr[:5], 1e-4, 1e-4, "mse_stats")
+    logits, lab = torch.randn(B, 15), torch.randint(0, 15, (B,), dtype=torch.int32)
+    dl = torch.empty(B, 15, device=DEV)
+    st.zero_()
+    K.softmax_xent(logits.to(DEV), lab.to(DEV), dl, st)
+    dlr, sr = torch.empty(B, 15), torch.zeros(8)
+    R.softmax_xent(logits, lab, dlr, sr)
+    _close(dl, dlr, 1e-5, 1e-5, "xent_grad")
+    _close(st[:5], sr[:5], 1e-4, 1e-4, "xent_stats")
+    n = 4096
+    p, g, m, v = torch.randn(n), torch.randn(n), torch.randn(n).abs() * 0.1, torch.rand(n) * 0.1
+    P, G, Mm, V = (t.clone().to(DEV) for t in (p, g, m, v))
+    pb = torch.empty(n, device=DEV, dtype=torch.bfloat16)
+    K.adam(P, G, Mm, V, pb, 1e-3, 0.9, 0.999, 1e-7, 0.5)
+    R.adam(p, g, m, v, None, 1e-3, 0.9, 0.999, 1e-7, 0.5)
+    _close(P, p, 1e-6, 1e-6, "adam_p")
+    _close(V, v, 1e-6, 1e-6, "adam_v")
+    _close(pb, p, 1e-2, 1e-2, "adam_bf16")
+
+
+def test_resize_norm_and_gap():
+    imgs = torch.randint(0, 256, (2, 37, 45, 3), dtype=torch.uint8)
+    out = torch.empty(2, 32, 40, 4, device=DEV, dtype=torch.bfloat16)
+    K.resize_norm(imgs.to(DEV), out, 32, 40)
+    ref = torch.empty(2, 32, 40, 4, dtype=torch.bfloat16)
+    R.resize_norm(imgs, ref, 32, 40)
+    _close(out, ref, 1e-2, 1e-2, "resize")
+    x = rnd(3, 4, 5, 128)
+    g = torch.empty(3, 128, device=DEV)
+    K.gap_fwd(x.to(DEV), g)
+    _close(g, x.float().mean((1, 2)), 1e-3, 1e-3, "gap")
