@@ -116,6 +116,20 @@ __global__ __launch_bounds__(256) void prelu_pool_bwd_k(const bf16_t* __restrict
         }
         *(U4*)(dz + (((long)n * H + h) * W + w) * C + c8 * 8) = pack8(o);
       }
+      // odd H/W (floor pooling): the last row/column belongs to no window -> zero gradient
+      const bool lastw = (W & 1) && pw == PW - 1, lasth = (H & 1) && ph == PH - 1;
+      if (lastw || lasth) {
+        const U4 zz = zero4();
+        if (lastw) {
+          *(U4*)(dz + (((long)n * H + 2 * ph) * W + W - 1) * C + c8 * 8) = zz;
+          *(U4*)(dz + (((long)n * H + 2 * ph + 1) * W + W - 1) * C + c8 * 8) = zz;
+        }
+        if (lasth) {
+          *(U4*)(dz + (((long)n * H + H - 1) * W + 2 * pw) * C + c8 * 8) = zz;
+          *(U4*)(dz + (((long)n * H + H - 1) * W + 2 * pw + 1) * C + c8 * 8) = zz;
+        }
+        if (lastw && lasth) *(U4*)(dz + (((long)n * H + H - 1) * W + W - 1) * C + c8 * 8) = zz;
+      }
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -460,7 +474,7 @@ extern "C" {
 
 int ptg_prelu_pool_fwd(const void* z, const float* alpha, void* p, int N, int H, int W, int C,
                        hipStream_t s) {
-  if (C % 8 || (H & 1) || (W & 1)) return (int)hipErrorInvalidValue;
+  if (C % 8 || H < 2 || W < 2) return (int)hipErrorInvalidValue;
   const long total = (long)N * (H / 2) * (W / 2) * (C / 8);
   hipLaunchKernelGGL(prelu_pool_fwd_k, dim3(grid_for(total)), dim3(256), 0, s, (const bf16_t*)z, alpha,
                      (bf16_t*)p, N, H, W, C);
@@ -469,7 +483,7 @@ int ptg_prelu_pool_fwd(const void* z, const float* alpha, void* p, int N, int H,
 
 int ptg_prelu_pool_bwd(const void* dp, const void* z, const float* alpha, void* dz, float* dalpha,
                        float* dbias, int N, int H, int W, int C, int nper, hipStream_t s) {
-  if (C % 8 || C > 256 || (H & 1) || (W & 1)) return (int)hipErrorInvalidValue;
+  if (C % 8 || C > 256 || H < 2 || W < 2) return (int)hipErrorInvalidValue;
   const int npos = (H / 2) * (W / 2) * (C / 8);
   if (nper <= 0) {
     const int bx = (npos + 255) / 256;

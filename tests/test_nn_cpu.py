@@ -1,0 +1,112 @@
+"""Keras-surface behaviour of the training runtime on the CPU (reference) path."""
+import json
+import zipfile
+
+import numpy as np
+import torch
+
+from pyspark_tf_gke_amd import nn
+from pyspark_tf_gke_amd.data import Dataset
+from pyspark_tf_gke_amd.models import (CNN_A1_PARAMS, CNN_B1_PARAMS, build_cnn_a1, build_cnn_model,
+                                       build_deep_model, build_mnist_cnn)
+
+
+def test_param_counts_match_reference_summaries(capsys):
+    m = build_cnn_model((256, 320, 3), flat=True, summary=True, device="cpu")
+    assert m.count_params() == CNN_B1_PARAMS  # 150-320-by-256-B1-model.txt:38
+    out = capsys.readouterr().out
+    assert "p_re_lu_4 (PReLU)" in out and "41,945,088" in out and "Total params: 43,368,850" in out
+    a1 = build_cnn_a1((256, 320, 3), device="cpu")
+    assert a1.count_params() == CNN_A1_PARAMS  # 100-320-by-256-A1-model.txt:27
+    mlp = build_deep_model(3, 15, device="cpu")
+    assert mlp.count_params() == 3695  # SURVEY §2.1 derived facts
+
+
+def test_layer_names_follow_keras():
+    m = build_cnn_model((32, 40, 3), flat=False, summary=False, device="cpu")
+    names = [l.name for l in m.layers]
+    assert names[:3] == ["conv2d", "p_re_lu", "max_pooling2d"]
+    assert "global_average_pooling2d" in names and names[-1] == "dense_1"
+
+
+def test_mlp_fit_history_and_validation():
+    rng = np.random.default_rng(0)
+    X = rng.normal(size=(400, 3)).astype(np.float32)
+    y = (X[:, 0] > 0).astype(np.int32) + 2 * (X[:, 1] > 0).astype(np.int32)
+    m = build_deep_model(3, 4, device="cpu")
+    ds = Dataset.from_tensor_slices((X[:320], y[:320])).shuffle(300, seed=1).batch(32).repeat()
+    val = Dataset.from_tensor_slices((X[320:], y[320:])).batch(32)
+    h = m.fit(ds, epochs=8, steps_per_epoch=10, validation_data=val, verbose=0)
+    assert set(h.history) == {"loss", "accuracy", "val_loss", "val_accuracy"}
+    assert len(h.history["loss"]) == 8
+    assert h.history["loss"][-1] < h.history["loss"][0]
+    assert h.history["accuracy"][-1] > 0.5
+    p = m.predict(X[:5])
+    assert p.shape == (5, 4) and np.allclose(p.sum(1), 1.0, atol=1e-5)
+
+
+def test_cnn_fit_mse_metrics():
+    x = np.random.default_rng(0).random((16, 32, 40, 3)).astype(np.float32)
+    y = (np.random.default_rng(1).random((16, 2)) * 30).astype(np.float32)
+    m = build_cnn_model((32, 40, 3), flat=True, summary=False, device="cpu")
+    h = m.fit(x, y, batch_size=8, epochs=3, verbose=0)
+    assert set(h.history) == {"loss", "mae", "mse"}
+    assert abs(h.history["loss"][0] - h.history["mse"][0]) < 1e-3 * h.history["mse"][0]
+    assert h.history["loss"][-1] < h.history["loss"][0]
+
+
+def test_save_and_load_roundtrip(tmp_path):
+    m = build_cnn_model((32, 40, 3), flat=True, summary=False, device="cpu")
+    x = np.random.default_rng(0).random((4, 32, 40, 3)).astype(np.float32)
+    before = m.predict(x)
+    path = str(tmp_path / "model.keras")
+    m.save(path)
+    with zipfile.ZipFile(path) as zf:
+        cfg = json.loads(zf.read("config.json"))
+        assert {"config.json", "metadata.json", "model.weights.safetensors"} <= set(zf.namelist())
+    assert cfg["config"]["layers"][1]["class_name"] == "Conv2D"
+    m2 = nn.load_model(path, device="cpu")
+    after = m2.predict(x)
+    assert np.allclose(before, after, atol=1e-4)
+    w = m2.get_weights()
+    assert w[0].shape == (5, 5, 3, 8)  # Keras kernel layout [KH, KW, Cin, Cout]
+
+
+def test_gradient_tape_custom_loop_matches_fit_step():
+    """The reference's PS step body (train_tf_ps.py:616-631) runs unchanged on the engine."""
+    rng = np.random.default_rng(0)
+    X = rng.normal(size=(64, 3)).astype(np.float32)
+    y = rng.integers(0, 5, 64).astype(np.int32)
+    m1 = build_deep_model(3, 5, device="cpu")
+    m2 = build_deep_model(3, 5, device="cpu")
+    opt = nn.optimizers.Adam(learning_rate=1e-3)
+    loss_obj = nn.losses.SparseCategoricalCrossentropy()
+    acc = nn.metrics.SparseCategoricalAccuracy()
+    for _ in range(3):
+        with nn.GradientTape() as tape:
+            logits = m1(X, training=True)
+            loss = loss_obj(y, logits)
+        grads = tape.gradient(loss, m1.trainable_variables)
+        opt.apply_gradients(zip(grads, m1.trainable_variables))
+        acc.update_state(y, logits)
+        m2.train_on_batch(X, y)
+    assert torch.allclose(m1.store.flat, m2.store.flat, atol=1e-6)
+    assert 0.0 <= float(acc.result()) <= 1.0
+
+
+def test_mnist_cnn_cpu_learns():
+    m = build_mnist_cnn(device="cpu")
+    x = torch.rand(32, 28, 28, 1)
+    y = torch.randint(0, 10, (32,), dtype=torch.int32)
+    l0 = m.train_on_batch(x, y, return_dict=True)["loss"]
+    for _ in range(10):
+        l1 = m.train_on_batch(x, y, return_dict=True)["loss"]
+    assert l1 < l0
+
+
+def test_odd_spatial_pooling_floor():
+    m = build_cnn_model((36, 44, 3), flat=True, summary=False, device="cpu")
+    assert m.layers[-4].out_shape == (2, 2, 64)
+    x = torch.rand(2, 36, 44, 3)
+    y = torch.rand(2, 2)
+    assert np.isfinite(m.train_on_batch(x, y, return_dict=True)["loss"])

@@ -28,18 +28,18 @@ def _seed(hip_built):
     torch.manual_seed(0)
 
 
-@pytest.mark.parametrize("M,N,K", [(256, 2048, 1024), (100, 72, 40), (64, 256, 2048), (512, 16, 96)])
+@pytest.mark.parametrize("M,N,KD", [(256, 2048, 1024), (104, 72, 40), (64, 256, 2048), (512, 16, 96)])
 @pytest.mark.parametrize("layout", ["kk", "kmn", "mnmn", "mnk"])
-def test_gemm_layouts(M, N, K, layout):
-    a = rnd(M, K) if layout in ("kk", "kmn") else rnd(K, M)
-    b = rnd(N, K) if layout in ("kk", "mnk") else rnd(K, N)
+def test_gemm_layouts(M, N, KD, layout):
+    a = rnd(M, KD) if layout in ("kk", "kmn") else rnd(KD, M)
+    b = rnd(N, KD) if layout in ("kk", "mnk") else rnd(KD, N)
     A = a.float() if layout in ("kk", "kmn") else a.float().t()
     Bm = b.float().t() if layout in ("kk", "mnk") else b.float()
     ref = A @ Bm
     c = torch.empty(M, N, device=DEV, dtype=torch.float32)
     ak = layout in ("kk", "kmn")
     bk = layout in ("kk", "mnk")
-    K.gemm(M, N, K, a.to(DEV), K if ak else M, ak, b.to(DEV), K if bk else N, bk, 1, c, N)
+    K.gemm(M, N, KD, a.to(DEV), KD if ak else M, ak, b.to(DEV), KD if bk else N, bk, 1, c, N)
     _close(c, ref, 1e-3, 1e-3, "gemm")
 
 
