@@ -1,0 +1,747 @@
+// DataFrame / SQL kernels (gfx950) — the executor-side compute of the Spark workloads.
+//
+//   expr VM        fused evaluation of a Column expression tree per row (Catalyst codegen's role:
+//                  filter predicates, withColumn(when/otherwise), isnan/isNull, arithmetic;
+//                  k_means.py:23-51, spark_installation_check.py:37)
+//   compaction     predicate mask -> row indices (wave ballot + block prefix) -> row gather (filter)
+//   reduce_stats   sum/count/min/max with null and NaN skipping (count(), agg avg; k_means.py:47)
+//   hash agg       groupBy().agg(): LDS-resident open-addressing tables with a global overflow
+//                  table; radix-partitioned two-pass variant for high-cardinality keys (BASELINE
+//                  1B-row groupBy; StringIndexer's label count, k_means.py:34)
+//   partition      hash partition ids + counting scatter (shuffle write for RCCL all-to-all-v)
+//   histogram      dictionary-code counts (StringIndexer fit)
+//
+// Tables are sized to powers of two; keys are int64 with EMPTY = INT64_MIN.
+#include "common.h"
+#include <cstring>
+
+#define EMPTY_KEY ((long long)0x8000000000000000ULL)
+
+PTG_DEV unsigned long long mix64(unsigned long long x) {
+  x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL; x ^= x >> 33;
+  return x;
+}
+
+// ================================================================================================
+// Expression VM. Program lives in the kernel argument block (wave-uniform -> scalar branches,
+// registers stay in VGPRs: every register access is a compile-time-unrolled select).
+// ================================================================================================
+enum VmOp {
+  OP_LDCOL = 1, OP_LDC, OP_LDNULL, OP_ADD, OP_SUB, OP_MUL, OP_DIV, OP_MOD, OP_NEG, OP_ABS, OP_SQRT, OP_LOG,
+  OP_EXP, OP_POW, OP_FLOOR, OP_CEIL, OP_EQ, OP_NE, OP_LT, OP_LE, OP_GT, OP_GE, OP_AND, OP_OR, OP_NOT,
+  OP_ISNULL, OP_ISNOTNULL, OP_ISNAN, OP_SELECT, OP_COALESCE, OP_CAST_INT, OP_EQ_NULLSAFE, OP_MIN2, OP_MAX2,
+  OP_ROUND
+};
+enum ColType { CT_F32 = 0, CT_F64 = 1, CT_I32 = 2, CT_I64 = 3, CT_U8 = 4, CT_CODE = 5 };
+#define VM_INS 96
+#define VM_COLS 12
+#define VM_CONSTS 32
+struct VmProg {
+  int n_ins, out_reg, out_type, filter_mode;
+  int ins[VM_INS];
+  double consts[VM_CONSTS];
+  const void* cols[VM_COLS];
+  const uint8_t* valid[VM_COLS];
+  int col_type[VM_COLS];
+};
+
+PTG_DEV double rreg(const double (&R)[8], int i) {
+  double v = R[0];
+#pragma unroll
+  for (int j = 1; j < 8; ++j) v = (i == j) ? R[j] : v;
+  return v;
+}
+PTG_DEV void wreg(double (&R)[8], int i, double v) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) R[j] = (i == j) ? v : R[j];
+}
+PTG_DEV double load_col(const void* p, int t, long i, bool& valid) {
+  switch (t) {
+    case CT_F32: return (double)((const float*)p)[i];
+    case CT_F64: return ((const double*)p)[i];
+    case CT_I32: return (double)((const int*)p)[i];
+    case CT_I64: return (double)((const long long*)p)[i];
+    case CT_U8: return (double)((const uint8_t*)p)[i];
+    default: { const int c = ((const int*)p)[i]; if (c < 0) valid = false; return (double)c; }
+  }
+}
+
+__global__ __launch_bounds__(256) void expr_eval_k(VmProg P, long n, void* out, uint8_t* out_valid) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    double R[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned vm = 0;  // validity bit per register
+    for (int pc = 0; pc < P.n_ins; ++pc) {
+      const int w = P.ins[pc];
+      const int op = w & 0xff, d = (w >> 8) & 0xf, a = (w >> 12) & 0xf, b = (w >> 16) & 0xf, c = (w >> 20) & 0xf;
+      const int k = (w >> 24) & 0xff;
+      const double x = rreg(R, a), y = rreg(R, b);
+      const bool va = (vm >> a) & 1, vb = (vm >> b) & 1;
+      double r = 0.0; bool v = true;
+      switch (op) {
+        case OP_LDCOL: { bool ok = true; r = load_col(P.cols[k], P.col_type[k], i, ok);
+                         if (P.valid[k]) ok = ok && P.valid[k][i]; v = ok; break; }
+        case OP_LDC: r = P.consts[k]; break;
+        case OP_LDNULL: v = false; break;
+        case OP_ADD: r = x + y; v = va && vb; break;
+        case OP_SUB: r = x - y; v = va && vb; break;
+        case OP_MUL: r = x * y; v = va && vb; break;
+        case OP_DIV: r = x / y; v = va && vb && y != 0.0; break;
+        case OP_MOD: r = fmod(x, y); v = va && vb && y != 0.0; break;
+        case OP_NEG: r = -x; v = va; break;
+        case OP_ABS: r = fabs(x); v = va; break;
+        case OP_SQRT: r = sqrt(x); v = va; break;
+        case OP_LOG: r = log(x); v = va && x > 0.0; break;
+        case OP_EXP: r = exp(x); v = va; break;
+        case OP_POW: r = pow(x, y); v = va && vb; break;
+        case OP_FLOOR: r = floor(x); v = va; break;
+        case OP_CEIL: r = ceil(x); v = va; break;
+        case OP_ROUND: r = round(x); v = va; break;
+        case OP_EQ: r = (x == y || (isnan(x) && isnan(y))) ? 1.0 : 0.0; v = va && vb; break;
+        case OP_NE: r = (x == y || (isnan(x) && isnan(y))) ? 0.0 : 1.0; v = va && vb; break;
+        case OP_LT: r = x < y ? 1.0 : 0.0; v = va && vb; break;
+        case OP_LE: r = x <= y ? 1.0 : 0.0; v = va && vb; break;
+        case OP_GT: r = x > y ? 1.0 : 0.0; v = va && vb; break;
+        case OP_GE: r = x >= y ? 1.0 : 0.0; v = va && vb; break;
+        case OP_AND: {  // SQL three-valued logic
+          const bool fa = va && x == 0.0, fb = vb && y == 0.0;
+          if (fa || fb) { r = 0.0; v = true; } else if (va && vb) { r = 1.0; v = true; } else { v = false; }
+          break; }
+        case OP_OR: {
+          const bool ta = va && x != 0.0, tb = vb && y != 0.0;
+          if (ta || tb) { r = 1.0; v = true; } else if (va && vb) { r = 0.0; v = true; } else { v = false; }
+          break; }
+        case OP_NOT: r = x == 0.0 ? 1.0 : 0.0; v = va; break;
+        case OP_ISNULL: r = va ? 0.0 : 1.0; break;
+        case OP_ISNOTNULL: r = va ? 1.0 : 0.0; break;
+        case OP_ISNAN: r = (va && isnan(x)) ? 1.0 : 0.0; break;
+        case OP_SELECT: {  // d = (cond a) ? b : c
+          const double z = rreg(R, c); const bool vc = (vm >> c) & 1;
+          const bool t = va && x != 0.0;
+          r = t ? y : z; v = t ? vb : vc; break; }
+        case OP_COALESCE: r = va ? x : y; v = va || vb; break;
+        case OP_CAST_INT: r = trunc(x); v = va && !isnan(x); break;
+        case OP_EQ_NULLSAFE: r = (va && vb) ? (x == y ? 1.0 : 0.0) : ((va == vb) ? 1.0 : 0.0); break;
+        case OP_MIN2: r = fmin(x, y); v = va && vb; break;
+        case OP_MAX2: r = fmax(x, y); v = va && vb; break;
+        default: break;
+      }
+      wreg(R, d, r);
+      vm = v ? (vm | (1u << d)) : (vm & ~(1u << d));
+    }
+    const double r = rreg(R, P.out_reg);
+    const bool v = (vm >> P.out_reg) & 1;
+    if (P.filter_mode) {
+      ((uint8_t*)out)[i] = (v && r != 0.0) ? 1 : 0;
+    } else {
+      switch (P.out_type) {
+        case CT_F32: ((float*)out)[i] = v ? (float)r : __builtin_nanf(""); break;
+        case CT_F64: ((double*)out)[i] = v ? r : __builtin_nan(""); break;
+        case CT_I32: ((int*)out)[i] = v ? (int)r : 0; break;
+        case CT_I64: ((long long*)out)[i] = v ? (long long)r : 0; break;
+        case CT_U8: ((uint8_t*)out)[i] = (v && r != 0.0) ? 1 : 0; break;
+        default: ((int*)out)[i] = v ? (int)r : -1; break;
+      }
+      if (out_valid) out_valid[i] = v ? 1 : 0;
+    }
+  }
+}
+
+// ================================================================================================
+// Stream compaction: mask (u8) -> ascending indices of set rows.
+// ================================================================================================
+#define CPT_ITEMS 16
+#define CPT_TILE (256 * CPT_ITEMS)
+
+__global__ __launch_bounds__(256) void compact_count_k(const uint8_t* __restrict__ mask, long n,
+                                                       int* __restrict__ block_counts) {
+  __shared__ float scr[4];
+  const long base = (long)blockIdx.x * CPT_TILE;
+  int c = 0;
+#pragma unroll
+  for (int j = 0; j < CPT_ITEMS; ++j) {
+    const long i = base + j * 256 + threadIdx.x;
+    c += (i < n && mask[i]) ? 1 : 0;
+  }
+  const float s = block_sum256((float)c, scr);
+  if (threadIdx.x == 0) block_counts[blockIdx.x] = (int)s;
+}
+
+// exclusive scan of block counts (single workgroup, any length); total -> total_out
+__global__ __launch_bounds__(256) void scan_excl_k(const int* __restrict__ in, long long* __restrict__ out, int nb,
+                                                   long long* __restrict__ total_out) {
+  __shared__ long long part[256];
+  const int per = (nb + 255) / 256;
+  const int b0 = threadIdx.x * per, b1 = min(nb, b0 + per);
+  long long s = 0;
+  for (int b = b0; b < b1; ++b) s += in[b];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    long long run = 0;
+    for (int t = 0; t < 256; ++t) { const long long v = part[t]; part[t] = run; run += v; }
+    *total_out = run;
+  }
+  __syncthreads();
+  long long run = part[threadIdx.x];
+  for (int b = b0; b < b1; ++b) { out[b] = run; run += in[b]; }
+}
+
+__global__ __launch_bounds__(256) void compact_write_k(const uint8_t* __restrict__ mask, long n,
+                                                       const long long* __restrict__ block_off,
+                                                       long long* __restrict__ idx_out) {
+  __shared__ int wave_tot[4];
+  __shared__ int wave_base[4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long base = (long)blockIdx.x * CPT_TILE;
+  long long run = block_off[blockIdx.x];
+  for (int j = 0; j < CPT_ITEMS; ++j) {
+    const long i = base + j * 256 + threadIdx.x;
+    const bool f = i < n && mask[i];
+    const unsigned long long bal = __ballot(f);
+    const int pre = __popcll(bal & ((1ULL << lane) - 1ULL));
+    if (lane == 0) wave_tot[w] = __popcll(bal);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int r = 0;
+      for (int q = 0; q < 4; ++q) { wave_base[q] = r; r += wave_tot[q]; }
+      wave_tot[0] = r;  // reuse slot 0 as the chunk total after bases are read
+    }
+    __syncthreads();
+    if (f) idx_out[run + wave_base[w] + pre] = i;
+    run += wave_tot[0];
+    __syncthreads();
+  }
+}
+
+// rows gather: dst[r] = src[idx[r]] for rows of row_bytes (multiple of 4)
+__global__ __launch_bounds__(256) void gather_rows_k(const uint8_t* __restrict__ src, const long long* __restrict__ idx,
+                                                     long m, int row_words, uint8_t* __restrict__ dst) {
+  const long total = m * row_words;
+  for (long t = blockIdx.x * 256L + threadIdx.x; t < total; t += (long)gridDim.x * 256) {
+    const long r = t / row_words; const int w = t - r * row_words;
+    ((uint32_t*)dst)[t] = ((const uint32_t*)src)[idx[r] * row_words + w];
+  }
+}
+__global__ __launch_bounds__(256) void gather_bytes_k(const uint8_t* __restrict__ src, const long long* __restrict__ idx,
+                                                      long m, int row_bytes, uint8_t* __restrict__ dst) {
+  const long total = m * row_bytes;
+  for (long t = blockIdx.x * 256L + threadIdx.x; t < total; t += (long)gridDim.x * 256) {
+    const long r = t / row_bytes; const int b = t - r * row_bytes;
+    dst[t] = src[idx[r] * row_bytes + b];
+  }
+}
+
+// ================================================================================================
+// reduce_stats: out[0]=sum, out[1]=count(valid, non-NaN if skip_nan), out[2]=min, out[3]=max,
+// out[4]=count of nulls (+NaN when skip_nan)
+// ================================================================================================
+__global__ __launch_bounds__(256) void reduce_stats_k(const void* __restrict__ col, int type,
+                                                      const uint8_t* __restrict__ valid, long n, int skip_nan,
+                                                      double* __restrict__ partial) {
+  __shared__ double sh[5][256];
+  double s = 0, c = 0, mn = INFINITY, mx = -INFINITY, nul = 0;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    bool ok = true;
+    const double v = load_col(col, type, i, ok);
+    if (valid) ok = ok && valid[i];
+    if (ok && skip_nan && isnan(v)) ok = false;
+    if (ok) { s += v; c += 1; mn = fmin(mn, v); mx = fmax(mx, v); } else { nul += 1; }
+  }
+  sh[0][threadIdx.x] = s; sh[1][threadIdx.x] = c; sh[2][threadIdx.x] = mn; sh[3][threadIdx.x] = mx;
+  sh[4][threadIdx.x] = nul;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) {
+      sh[0][threadIdx.x] += sh[0][threadIdx.x + o]; sh[1][threadIdx.x] += sh[1][threadIdx.x + o];
+      sh[2][threadIdx.x] = fmin(sh[2][threadIdx.x], sh[2][threadIdx.x + o]);
+      sh[3][threadIdx.x] = fmax(sh[3][threadIdx.x], sh[3][threadIdx.x + o]);
+      sh[4][threadIdx.x] += sh[4][threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x < 5) partial[blockIdx.x * 5 + threadIdx.x] = sh[threadIdx.x][0];
+}
+__global__ void reduce_stats_final_k(const double* __restrict__ partial, int nb, double* __restrict__ out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  double s = 0, c = 0, mn = INFINITY, mx = -INFINITY, nul = 0;
+  for (int b = 0; b < nb; ++b) {
+    s += partial[b * 5]; c += partial[b * 5 + 1]; mn = fmin(mn, partial[b * 5 + 2]);
+    mx = fmax(mx, partial[b * 5 + 3]); nul += partial[b * 5 + 4];
+  }
+  out[0] = s; out[1] = c; out[2] = mn; out[3] = mx; out[4] = nul;
+}
+
+// ================================================================================================
+// Hash aggregation.  Aggregates are "slots": for every input value column j we keep
+// sum[j], cnt[j] (non-null count), min[j], max[j] (doubles) per group, plus rows (count(*)).
+// Global table layout (capacity cap, power of two):
+//   keys[cap] (i64), rows[cap] (f64), then per value column j: sum, cnt, min, max  [4*nv][cap] (f64)
+// ================================================================================================
+#define AGG_MAXV 4
+struct AggIn {
+  const void* vals[AGG_MAXV];
+  const uint8_t* valid[AGG_MAXV];
+  int types[AGG_MAXV];
+  int nv;
+  int minmax;  // also maintain min/max (global-table path for every row)
+};
+
+PTG_DEV void atomic_min_f64(double* p, double v) {
+  unsigned long long* a = (unsigned long long*)p;
+  unsigned long long old = *a;
+  while (__longlong_as_double(old) > v) {
+    const unsigned long long prev = atomicCAS(a, old, (unsigned long long)__double_as_longlong(v));
+    if (prev == old) break;
+    old = prev;
+  }
+}
+PTG_DEV void atomic_max_f64(double* p, double v) {
+  unsigned long long* a = (unsigned long long*)p;
+  unsigned long long old = *a;
+  while (__longlong_as_double(old) < v) {
+    const unsigned long long prev = atomicCAS(a, old, (unsigned long long)__double_as_longlong(v));
+    if (prev == old) break;
+    old = prev;
+  }
+}
+
+// find-or-insert slot in the global table; returns -1 if the table is full
+PTG_DEV long gtable_slot(long long* keys, long cap, long long key) {
+  long h = (long)(mix64((unsigned long long)key) & (unsigned long long)(cap - 1));
+  for (long probe = 0; probe < cap; ++probe) {
+    const long long cur = keys[h];
+    if (cur == key) return h;
+    if (cur == EMPTY_KEY) {
+      const long long prev = (long long)atomicCAS((unsigned long long*)&keys[h], (unsigned long long)EMPTY_KEY,
+                                                  (unsigned long long)key);
+      if (prev == EMPTY_KEY || prev == key) return h;
+    }
+    h = (h + 1) & (cap - 1);
+  }
+  return -1;
+}
+
+PTG_DEV void gtable_add(double* tab, long cap, long slot, double rows, const double* s, const double* c,
+                        const double* mn, const double* mx, int nv) {
+  atomicAdd(&tab[slot], rows);
+  for (int j = 0; j < nv; ++j) {
+    double* base = tab + cap * (1 + 4 * j);
+    if (c[j] > 0) {
+      atomicAdd(&base[slot], s[j]);
+      atomicAdd(&base[cap + slot], c[j]);
+      atomic_min_f64(&base[2 * cap + slot], mn[j]);
+      atomic_max_f64(&base[3 * cap + slot], mx[j]);
+    }
+  }
+}
+
+// LDS-first aggregation: each workgroup aggregates a contiguous chunk of rows into an LDS table
+// (LCAP slots), overflowing rows go straight to the global table; the LDS table is flushed with
+// one global update per distinct key per workgroup.  Low/moderate cardinality => global atomics
+// drop by the per-chunk reuse factor.
+#define LCAP 1024
+__global__ __launch_bounds__(256) void hash_agg_lds_k(const long long* __restrict__ keys, long n, AggIn in,
+                                                      long long* __restrict__ gkeys, double* __restrict__ gtab,
+                                                      long gcap, long rows_per_block, int* __restrict__ overflow) {
+  __shared__ long long lk[LCAP];
+  __shared__ double lrows[LCAP];
+  __shared__ double lacc[AGG_MAXV][2][LCAP];  // sum, cnt (min/max go global-direct)
+  for (int t = threadIdx.x; t < LCAP; t += 256) {
+    lk[t] = EMPTY_KEY; lrows[t] = 0;
+    for (int j = 0; j < AGG_MAXV; ++j) { lacc[j][0][t] = 0; lacc[j][1][t] = 0; }
+  }
+  __syncthreads();
+  const long r0 = (long)blockIdx.x * rows_per_block, r1 = min(n, r0 + rows_per_block);
+  const bool need_minmax = in.minmax != 0;
+  for (long i = r0 + threadIdx.x; i < r1; i += 256) {
+    const long long key = keys[i];
+    double s[AGG_MAXV], c[AGG_MAXV];
+    for (int j = 0; j < in.nv; ++j) {
+      bool ok = true;
+      const double v = load_col(in.vals[j], in.types[j], i, ok);
+      if (in.valid[j]) ok = ok && in.valid[j][i];
+      if (ok && isnan(v)) ok = false;
+      s[j] = ok ? v : 0.0; c[j] = ok ? 1.0 : 0.0;
+    }
+    int h = (int)(mix64((unsigned long long)key) & (LCAP - 1));
+    int slot = -1;
+    for (int probe = 0; probe < 32; ++probe) {
+      const long long cur = lk[h];
+      if (cur == key) { slot = h; break; }
+      if (cur == EMPTY_KEY) {
+        const long long prev = (long long)atomicCAS((unsigned long long*)&lk[h], (unsigned long long)EMPTY_KEY,
+                                                    (unsigned long long)key);
+        if (prev == EMPTY_KEY || prev == key) { slot = h; break; }
+      }
+      h = (h + 1) & (LCAP - 1);
+    }
+    if (slot >= 0) {
+      atomicAdd(&lrows[slot], 1.0);
+      for (int j = 0; j < in.nv; ++j) {
+        if (c[j] > 0) { atomicAdd(&lacc[j][0][slot], s[j]); atomicAdd(&lacc[j][1][slot], 1.0); }
+      }
+    }
+    if (slot < 0 || need_minmax) {
+      const long gs = gtable_slot(gkeys, gcap, key);
+      if (gs < 0) { atomicAdd(overflow, 1); continue; }
+      if (slot < 0) {
+        gtable_add(gtab, gcap, gs, 1.0, s, c, s, s, in.nv);
+      } else {
+        for (int j = 0; j < in.nv; ++j)
+          if (c[j] > 0) {
+            double* base = gtab + gcap * (1 + 4 * j);
+            atomic_min_f64(&base[2 * gcap + gs], s[j]);
+            atomic_max_f64(&base[3 * gcap + gs], s[j]);
+          }
+      }
+    }
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < LCAP; t += 256) {
+    const long long key = lk[t];
+    if (key == EMPTY_KEY) continue;
+    const long gs = gtable_slot(gkeys, gcap, key);
+    if (gs < 0) { atomicAdd(overflow, 1); continue; }
+    atomicAdd(&gtab[gs], lrows[t]);
+    for (int j = 0; j < in.nv; ++j) {
+      double* base = gtab + gcap * (1 + 4 * j);
+      if (lacc[j][1][t] > 0) { atomicAdd(&base[gs], lacc[j][0][t]); atomicAdd(&base[gcap + gs], lacc[j][1][t]); }
+    }
+  }
+}
+
+// table init: keys EMPTY, rows/sum/cnt 0, min +inf, max -inf
+__global__ __launch_bounds__(256) void hash_table_init_k(long long* keys, double* tab, long cap, int nv) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < cap; i += (long)gridDim.x * 256) {
+    keys[i] = EMPTY_KEY;
+    tab[i] = 0.0;
+    for (int j = 0; j < nv; ++j) {
+      double* base = tab + cap * (1 + 4 * j);
+      base[i] = 0.0; base[cap + i] = 0.0; base[2 * cap + i] = INFINITY; base[3 * cap + i] = -INFINITY;
+    }
+  }
+}
+
+// extract occupied slots into dense outputs: out_keys[m], out_tab[(1+4nv)][m]; count -> *m_out
+__global__ __launch_bounds__(256) void hash_extract_k(const long long* __restrict__ keys, const double* __restrict__ tab,
+                                                      long cap, int nv, long long* __restrict__ out_keys,
+                                                      double* __restrict__ out_tab, long out_cap,
+                                                      unsigned long long* __restrict__ m_out) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < cap; i += (long)gridDim.x * 256) {
+    const long long k = keys[i];
+    if (k == EMPTY_KEY) continue;
+    const unsigned long long p = atomicAdd(m_out, 1ULL);
+    if ((long)p >= out_cap) continue;
+    out_keys[p] = k;
+    for (int s = 0; s < 1 + 4 * nv; ++s) out_tab[s * out_cap + p] = tab[s * cap + i];
+  }
+}
+
+// ---- radix-partitioned aggregation (high cardinality) -------------------------------------------
+// pass 1: partition histogram over P = 2^pbits partitions by the high hash bits
+__global__ __launch_bounds__(256) void part_hist_k(const long long* __restrict__ keys, long n, int pbits,
+                                                   unsigned int* __restrict__ counts) {
+  __shared__ unsigned int h[4096];
+  const int P = 1 << pbits;
+  for (int t = threadIdx.x; t < P; t += 256) h[t] = 0;
+  __syncthreads();
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const unsigned p = (unsigned)(mix64((unsigned long long)keys[i]) >> (64 - pbits));
+    atomicAdd(&h[p], 1u);
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < P; t += 256)
+    if (h[t]) atomicAdd(&counts[t], h[t]);
+}
+// pass 2: scatter rows (key + one value column as f64) into partition order
+__global__ __launch_bounds__(256) void part_scatter_k(const long long* __restrict__ keys, const void* __restrict__ val,
+                                                      int vtype, long n, int pbits,
+                                                      unsigned long long* __restrict__ cursor,
+                                                      long long* __restrict__ okeys, double* __restrict__ ovals,
+                                                      long rows_per_block) {
+  __shared__ unsigned int lc[4096];
+  __shared__ unsigned long long lbase[4096];
+  const int P = 1 << pbits;
+  const long r0 = (long)blockIdx.x * rows_per_block, r1 = min(n, r0 + rows_per_block);
+  for (int t = threadIdx.x; t < P; t += 256) lc[t] = 0;
+  __syncthreads();
+  for (long i = r0 + threadIdx.x; i < r1; i += 256)
+    atomicAdd(&lc[(unsigned)(mix64((unsigned long long)keys[i]) >> (64 - pbits))], 1u);
+  __syncthreads();
+  for (int t = threadIdx.x; t < P; t += 256) {
+    lbase[t] = lc[t] ? atomicAdd(&cursor[t], (unsigned long long)lc[t]) : 0ULL;
+    lc[t] = 0;
+  }
+  __syncthreads();
+  for (long i = r0 + threadIdx.x; i < r1; i += 256) {
+    const long long k = keys[i];
+    const unsigned p = (unsigned)(mix64((unsigned long long)k) >> (64 - pbits));
+    const unsigned off = atomicAdd(&lc[p], 1u);
+    const unsigned long long dst = lbase[p] + off;
+    bool ok = true;
+    okeys[dst] = k;
+    ovals[dst] = load_col(val, vtype, i, ok);
+  }
+}
+// pass 3: one workgroup per partition segment aggregates in LDS (sum, count) — rows of a partition
+// never meet another partition's keys, so each partition's table is final: no merge needed.
+#define PCAP 4096
+__global__ __launch_bounds__(256) void part_agg_k(const long long* __restrict__ okeys, const double* __restrict__ ovals,
+                                                  const unsigned long long* __restrict__ pstart, int P,
+                                                  long long* __restrict__ out_keys, double* __restrict__ out_sum,
+                                                  double* __restrict__ out_cnt, unsigned long long* __restrict__ m_out,
+                                                  long long* __restrict__ gkeys, double* __restrict__ gtab, long gcap,
+                                                  int* __restrict__ overflow) {
+  __shared__ long long lk[PCAP];
+  __shared__ double ls[PCAP];
+  __shared__ double lcnt[PCAP];
+  for (int p = blockIdx.x; p < P; p += gridDim.x) {
+    for (int t = threadIdx.x; t < PCAP; t += 256) { lk[t] = EMPTY_KEY; ls[t] = 0; lcnt[t] = 0; }
+    __syncthreads();
+    const unsigned long long a = pstart[p], b = pstart[p + 1];
+    for (unsigned long long i = a + threadIdx.x; i < b; i += 256) {
+      const long long key = okeys[i];
+      const double v = ovals[i];
+      int h = (int)(mix64((unsigned long long)key) & (PCAP - 1));
+      int slot = -1;
+      for (int probe = 0; probe < 64; ++probe) {
+        const long long cur = lk[h];
+        if (cur == key) { slot = h; break; }
+        if (cur == EMPTY_KEY) {
+          const long long prev = (long long)atomicCAS((unsigned long long*)&lk[h], (unsigned long long)EMPTY_KEY,
+                                                      (unsigned long long)key);
+          if (prev == EMPTY_KEY || prev == key) { slot = h; break; }
+        }
+        h = (h + 1) & (PCAP - 1);
+      }
+      if (slot >= 0) {
+        atomicAdd(&ls[slot], v); atomicAdd(&lcnt[slot], 1.0);
+      } else {  // partition exceeds the LDS table: global overflow table
+        const long gs = gtable_slot(gkeys, gcap, key);
+        if (gs < 0) { atomicAdd(overflow, 1); continue; }
+        atomicAdd(&gtab[gs], 1.0);
+        atomicAdd(&gtab[gcap + gs], v);
+        atomicAdd(&gtab[2 * gcap + gs], 1.0);
+      }
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < PCAP; t += 256) {
+      if (lk[t] == EMPTY_KEY) continue;
+      const unsigned long long q = atomicAdd(m_out, 1ULL);
+      out_keys[q] = lk[t]; out_sum[q] = ls[t]; out_cnt[q] = lcnt[t];
+    }
+    __syncthreads();
+  }
+}
+
+// ================================================================================================
+// histogram of int32 codes (StringIndexer fit); codes < 0 (null) counted in bin nbins
+// ================================================================================================
+__global__ __launch_bounds__(256) void histogram_k(const int* __restrict__ codes, long n, unsigned long long* __restrict__ out,
+                                                   int nbins) {
+  __shared__ unsigned int h[4097];
+  const bool lds = nbins < 4096;
+  if (lds)
+    for (int t = threadIdx.x; t <= nbins; t += 256) h[t] = 0;
+  __syncthreads();
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    int c = codes[i];
+    if (c < 0 || c >= nbins) c = nbins;
+    if (lds) atomicAdd(&h[c], 1u); else atomicAdd(&out[c], 1ULL);
+  }
+  __syncthreads();
+  if (lds)
+    for (int t = threadIdx.x; t <= nbins; t += 256)
+      if (h[t]) atomicAdd(&out[t], (unsigned long long)h[t]);
+}
+
+// ================================================================================================
+// hash partitioning for shuffles: part[i] = hash(key) % P, counts[P] (int64)
+// ================================================================================================
+__global__ __launch_bounds__(256) void hash_partition_k(const long long* __restrict__ keys, long n, int P,
+                                                        int* __restrict__ part, unsigned long long* __restrict__ counts) {
+  __shared__ unsigned int h[1024];
+  for (int t = threadIdx.x; t < P; t += 256) h[t] = 0;
+  __syncthreads();
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const int p = (int)(mix64((unsigned long long)keys[i]) % (unsigned long long)P);
+    part[i] = p;
+    atomicAdd(&h[p], 1u);
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < P; t += 256)
+    if (h[t]) atomicAdd(&counts[t], (unsigned long long)h[t]);
+}
+// stable-by-block scatter of row indices into partition order (perm[dst] = i)
+__global__ __launch_bounds__(256) void partition_perm_k(const int* __restrict__ part, long n, int P,
+                                                        unsigned long long* __restrict__ cursor,
+                                                        long long* __restrict__ perm, long rows_per_block) {
+  __shared__ unsigned int lc[1024];
+  __shared__ unsigned long long lb[1024];
+  const long r0 = (long)blockIdx.x * rows_per_block, r1 = min(n, r0 + rows_per_block);
+  for (int t = threadIdx.x; t < P; t += 256) lc[t] = 0;
+  __syncthreads();
+  for (long i = r0 + threadIdx.x; i < r1; i += 256) atomicAdd(&lc[part[i]], 1u);
+  __syncthreads();
+  for (int t = threadIdx.x; t < P; t += 256) { lb[t] = lc[t] ? atomicAdd(&cursor[t], (unsigned long long)lc[t]) : 0; lc[t] = 0; }
+  __syncthreads();
+  for (long i = r0 + threadIdx.x; i < r1; i += 256) {
+    const int p = part[i];
+    perm[lb[p] + atomicAdd(&lc[p], 1u)] = i;
+  }
+}
+
+// ================================================================================================
+// synthetic (key, value) generator: key = hash(seed, row) % num_keys, value uniform [0,1)
+// ================================================================================================
+__global__ __launch_bounds__(256) void fill_kv_k(long long* __restrict__ keys, double* __restrict__ vals, long n,
+                                                 long offset, long num_keys, unsigned long long seed) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const unsigned long long h = mix64((unsigned long long)(i + offset) * 0x9E3779B97F4A7C15ULL + seed);
+    keys[i] = (long long)(h % (unsigned long long)num_keys);
+    vals[i] = (double)(mix64(h ^ 0x632BE59BD9B4E019ULL) >> 11) * (1.0 / 9007199254740992.0);
+  }
+}
+
+static inline int grid_n(long n) {
+  long g = (n + 255) / 256;
+  if (g < 1) g = 1;
+  if (g > 4096) g = 4096;
+  return (int)g;
+}
+
+extern "C" {
+
+// prog: packed VmProg bytes (host-built, sizeof must match ptg_vm_prog_size)
+int ptg_vm_prog_size() { return (int)sizeof(VmProg); }
+
+int ptg_expr_eval(const void* prog, long n, void* out, void* out_valid, hipStream_t s) {
+  VmProg P;
+  memcpy(&P, prog, sizeof(VmProg));
+  hipLaunchKernelGGL(expr_eval_k, dim3(grid_n(n)), dim3(256), 0, s, P, n, out, (uint8_t*)out_valid);
+  PTG_RETURN_LAUNCH();
+}
+
+// indices of set mask rows; block_counts: int[ceil(n/4096)], block_off: i64[same], total: i64[1]
+int ptg_compact(const void* mask, long n, void* block_counts, void* block_off, void* total, void* idx_out,
+                hipStream_t s) {
+  const int nb = (int)((n + CPT_TILE - 1) / CPT_TILE);
+  if (nb == 0) return (int)hipMemsetAsync(total, 0, 8, s);
+  hipLaunchKernelGGL(compact_count_k, dim3(nb), dim3(256), 0, s, (const uint8_t*)mask, n, (int*)block_counts);
+  hipLaunchKernelGGL(scan_excl_k, dim3(1), dim3(256), 0, s, (const int*)block_counts, (long long*)block_off, nb,
+                     (long long*)total);
+  if (idx_out)
+    hipLaunchKernelGGL(compact_write_k, dim3(nb), dim3(256), 0, s, (const uint8_t*)mask, n,
+                       (const long long*)block_off, (long long*)idx_out);
+  PTG_RETURN_LAUNCH();
+}
+
+int ptg_gather_rows(const void* src, const void* idx, long m, int row_bytes, void* dst, hipStream_t s) {
+  if (m <= 0) return 0;
+  if (row_bytes % 4 == 0) {
+    const int rw = row_bytes / 4;
+    hipLaunchKernelGGL(gather_rows_k, dim3(grid_n(m * rw)), dim3(256), 0, s, (const uint8_t*)src,
+                       (const long long*)idx, m, rw, (uint8_t*)dst);
+  } else {
+    hipLaunchKernelGGL(gather_bytes_k, dim3(grid_n(m * row_bytes)), dim3(256), 0, s, (const uint8_t*)src,
+                       (const long long*)idx, m, row_bytes, (uint8_t*)dst);
+  }
+  PTG_RETURN_LAUNCH();
+}
+
+// out: double[5] = {sum, count, min, max, nulls}; partial: double[5*1024]
+int ptg_reduce_stats(const void* col, int type, const void* valid, long n, int skip_nan, void* partial, void* out,
+                     hipStream_t s) {
+  int g = grid_n(n);
+  if (g > 1024) g = 1024;
+  hipLaunchKernelGGL(reduce_stats_k, dim3(g), dim3(256), 0, s, col, type, (const uint8_t*)valid, n, skip_nan,
+                     (double*)partial);
+  hipLaunchKernelGGL(reduce_stats_final_k, dim3(1), dim3(64), 0, s, (const double*)partial, g, (double*)out);
+  PTG_RETURN_LAUNCH();
+}
+
+int ptg_hash_table_init(void* keys, void* tab, long cap, int nv, hipStream_t s) {
+  hipLaunchKernelGGL(hash_table_init_k, dim3(grid_n(cap)), dim3(256), 0, s, (long long*)keys, (double*)tab, cap, nv);
+  PTG_RETURN_LAUNCH();
+}
+
+// vals/valids/types: host arrays of nv entries (device pointers inside)
+int ptg_hash_agg(const void* keys, long n, const void* const* vals, const void* const* valids, const int* types,
+                 int nv, int minmax, void* gkeys, void* gtab, long gcap, void* overflow, hipStream_t s) {
+  if (nv > AGG_MAXV) return (int)hipErrorInvalidValue;
+  AggIn in;
+  for (int j = 0; j < AGG_MAXV; ++j) {
+    in.vals[j] = j < nv ? vals[j] : nullptr;
+    in.valid[j] = j < nv ? (const uint8_t*)valids[j] : nullptr;
+    in.types[j] = j < nv ? types[j] : 0;
+  }
+  in.nv = nv;
+  in.minmax = minmax;
+  long rpb = 65536;
+  long nb = (n + rpb - 1) / rpb;
+  if (nb < 512) { rpb = (n + 511) / 512; if (rpb < 256) rpb = 256; nb = (n + rpb - 1) / rpb; }
+  if (nb < 1) nb = 1;
+  hipLaunchKernelGGL(hash_agg_lds_k, dim3((unsigned)nb), dim3(256), 0, s, (const long long*)keys, n, in,
+                     (long long*)gkeys, (double*)gtab, gcap, rpb, (int*)overflow);
+  PTG_RETURN_LAUNCH();
+}
+
+int ptg_hash_extract(const void* keys, const void* tab, long cap, int nv, void* out_keys, void* out_tab, long out_cap,
+                     void* m_out, hipStream_t s) {
+  hipLaunchKernelGGL(hash_extract_k, dim3(grid_n(cap)), dim3(256), 0, s, (const long long*)keys, (const double*)tab,
+                     cap, nv, (long long*)out_keys, (double*)out_tab, out_cap, (unsigned long long*)m_out);
+  PTG_RETURN_LAUNCH();
+}
+
+// Partitioned sum/count aggregation of (key, val).  Workspace (device):
+//   counts u32[P], cursor u64[P], pstart u64[P+1] (host computes from counts), okeys i64[n], ovals f64[n]
+int ptg_part_hist(const void* keys, long n, int pbits, void* counts, hipStream_t s) {
+  if (pbits > 12) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(part_hist_k, dim3(grid_n(n)), dim3(256), 0, s, (const long long*)keys, n, pbits,
+                     (unsigned int*)counts);
+  PTG_RETURN_LAUNCH();
+}
+int ptg_part_scatter(const void* keys, const void* val, int vtype, long n, int pbits, void* cursor, void* okeys,
+                     void* ovals, hipStream_t s) {
+  long rpb = 16384;
+  const long nb = (n + rpb - 1) / rpb;
+  hipLaunchKernelGGL(part_scatter_k, dim3((unsigned)(nb < 1 ? 1 : nb)), dim3(256), 0, s, (const long long*)keys, val,
+                     vtype, n, pbits, (unsigned long long*)cursor, (long long*)okeys, (double*)ovals, rpb);
+  PTG_RETURN_LAUNCH();
+}
+int ptg_part_agg(const void* okeys, const void* ovals, const void* pstart, int P, void* out_keys, void* out_sum,
+                 void* out_cnt, void* m_out, void* gkeys, void* gtab, long gcap, void* overflow, hipStream_t s) {
+  int g = P < 1024 ? P : 1024;
+  hipLaunchKernelGGL(part_agg_k, dim3(g), dim3(256), 0, s, (const long long*)okeys, (const double*)ovals,
+                     (const unsigned long long*)pstart, P, (long long*)out_keys, (double*)out_sum, (double*)out_cnt,
+                     (unsigned long long*)m_out, (long long*)gkeys, (double*)gtab, gcap, (int*)overflow);
+  PTG_RETURN_LAUNCH();
+}
+
+int ptg_histogram_i32(const void* codes, long n, void* out, int nbins, hipStream_t s) {
+  hipLaunchKernelGGL(histogram_k, dim3(grid_n(n)), dim3(256), 0, s, (const int*)codes, n, (unsigned long long*)out,
+                     nbins);
+  PTG_RETURN_LAUNCH();
+}
+
+int ptg_hash_partition(const void* keys, long n, int P, void* part, void* counts, hipStream_t s) {
+  if (P > 1024) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(hash_partition_k, dim3(grid_n(n)), dim3(256), 0, s, (const long long*)keys, n, P, (int*)part,
+                     (unsigned long long*)counts);
+  PTG_RETURN_LAUNCH();
+}
+int ptg_partition_perm(const void* part, long n, int P, void* cursor, void* perm, hipStream_t s) {
+  const long rpb = 16384;
+  const long nb = (n + rpb - 1) / rpb;
+  hipLaunchKernelGGL(partition_perm_k, dim3((unsigned)(nb < 1 ? 1 : nb)), dim3(256), 0, s, (const int*)part, n, P,
+                     (unsigned long long*)cursor, (long long*)perm, rpb);
+  PTG_RETURN_LAUNCH();
+}
+
+int ptg_fill_synthetic_kv(void* keys, void* vals, long n, long offset, long num_keys, long seed, hipStream_t s) {
+  hipLaunchKernelGGL(fill_kv_k, dim3(grid_n(n)), dim3(256), 0, s, (long long*)keys, (double*)vals, n, offset, num_keys,
+                     (unsigned long long)seed);
+  PTG_RETURN_LAUNCH();
+}
+
+}  // extern "C"

@@ -1,0 +1,371 @@
+"""DataFrame / ML device ops (wrappers over csrc/kernels/df.hip and ml.hip).
+
+GPU tensors go to the HIP kernels; CPU tensors use numpy/torch host code with the same
+semantics (the ``local[N]`` executor path).  Column type codes match ``ColType`` in df.hip.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import struct
+
+import numpy as np
+import torch
+
+from .. import _native
+from ._util import hip, on_device, ptr
+
+CT_F32, CT_F64, CT_I32, CT_I64, CT_U8, CT_CODE = range(6)
+TORCH_CT = {torch.float32: CT_F32, torch.float64: CT_F64, torch.int32: CT_I32, torch.int64: CT_I64,
+            torch.uint8: CT_U8, torch.bool: CT_U8}
+
+# VM opcodes (enum VmOp in df.hip)
+OPS = ["", "LDCOL", "LDC", "LDNULL", "ADD", "SUB", "MUL", "DIV", "MOD", "NEG", "ABS", "SQRT", "LOG", "EXP", "POW",
+       "FLOOR", "CEIL", "EQ", "NE", "LT", "LE", "GT", "GE", "AND", "OR", "NOT", "ISNULL", "ISNOTNULL", "ISNAN",
+       "SELECT", "COALESCE", "CAST_INT", "EQ_NULLSAFE", "MIN2", "MAX2", "ROUND"]
+OP = {n: i for i, n in enumerate(OPS) if n}
+VM_INS, VM_COLS, VM_CONSTS = 96, 12, 32
+
+
+def pack_ins(op: str, d: int, a: int = 0, b: int = 0, c: int = 0, k: int = 0) -> int:
+    w = OP[op] | (d << 8) | (a << 12) | (b << 16) | (c << 20) | (k << 24)
+    return w - (1 << 32) if w >= (1 << 31) else w
+
+
+def pack_vm_prog(ins, out_reg, out_type, filter_mode, consts, cols) -> bytes:
+    """cols: list of (tensor, valid_tensor_or_None, type_code)."""
+    if len(ins) > VM_INS or len(consts) > VM_CONSTS or len(cols) > VM_COLS:
+        raise ValueError("expression too large for the device VM")
+    buf = struct.pack("4i", len(ins), out_reg, out_type, int(filter_mode))
+    buf += struct.pack(f"{VM_INS}i", *(list(ins) + [0] * (VM_INS - len(ins))))
+    buf += struct.pack(f"{VM_CONSTS}d", *(list(consts) + [0.0] * (VM_CONSTS - len(consts))))
+    ptrs = [c[0].data_ptr() for c in cols] + [0] * (VM_COLS - len(cols))
+    vptr = [(c[1].data_ptr() if c[1] is not None else 0) for c in cols] + [0] * (VM_COLS - len(cols))
+    types = [c[2] for c in cols] + [0] * (VM_COLS - len(cols))
+    buf += struct.pack(f"{VM_COLS}Q", *ptrs) + struct.pack(f"{VM_COLS}Q", *vptr) + struct.pack(f"{VM_COLS}i", *types)
+    size = _native.hip_lib().ptg_vm_prog_size()
+    buf += b"\0" * (size - len(buf))
+    assert len(buf) == size, (len(buf), size)
+    return buf
+
+
+def expr_eval(prog: bytes, n: int, out, out_valid=None):
+    cbuf = ctypes.create_string_buffer(prog, len(prog))
+    hip("ptg_expr_eval", ctypes.addressof(cbuf), n, ptr(out), ptr(out_valid))
+
+
+# ------------------------------------------------------------------------------------------------
+def compact(mask: torch.Tensor) -> torch.Tensor:
+    """Ascending int64 indices of the non-zero entries of a uint8/bool mask."""
+    n = mask.numel()
+    if not on_device(mask):
+        return torch.nonzero(mask.view(-1).bool(), as_tuple=False).view(-1)
+    m = mask.view(torch.uint8) if mask.dtype == torch.bool else mask
+    nb = max(1, math.ceil(n / 4096))
+    dev = mask.device
+    bc = torch.empty(nb, dtype=torch.int32, device=dev)
+    bo = torch.empty(nb, dtype=torch.int64, device=dev)
+    tot = torch.zeros(1, dtype=torch.int64, device=dev)
+    hip("ptg_compact", ptr(m), n, ptr(bc), ptr(bo), ptr(tot), None)
+    total = int(tot.item())
+    idx = torch.empty(total, dtype=torch.int64, device=dev)
+    if total:
+        hip("ptg_compact", ptr(m), n, ptr(bc), ptr(bo), ptr(tot), ptr(idx))
+    return idx
+
+
+def gather_rows(t: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
+    if not on_device(t):
+        return t.index_select(0, idx)
+    m = idx.numel()
+    out = torch.empty((m, *t.shape[1:]), dtype=t.dtype, device=t.device)
+    if m == 0:
+        return out
+    row_bytes = t[0].numel() * t.element_size() if t.dim() > 0 and t.shape[0] > 0 else t.element_size()
+    src = t.contiguous()
+    hip("ptg_gather_rows", ptr(src), ptr(idx), m, row_bytes, ptr(out))
+    return out
+
+
+def reduce_stats(col: torch.Tensor, valid, skip_nan: bool = True):
+    """-> (sum, count, min, max, nulls) as Python floats."""
+    if not on_device(col):
+        x = col.double()
+        ok = torch.ones_like(x, dtype=torch.bool) if valid is None else valid.bool()
+        if skip_nan:
+            ok = ok & ~torch.isnan(x)
+        v = x[ok]
+        return (float(v.sum()) if v.numel() else 0.0, float(v.numel()),
+                float(v.min()) if v.numel() else math.inf, float(v.max()) if v.numel() else -math.inf,
+                float(x.numel() - v.numel()))
+    dev = col.device
+    part = torch.empty(5 * 1024, dtype=torch.float64, device=dev)
+    out = torch.empty(5, dtype=torch.float64, device=dev)
+    t = col if col.dtype != torch.bool else col.view(torch.uint8)
+    hip("ptg_reduce_stats", ptr(t), TORCH_CT[t.dtype], ptr(valid), col.numel(), int(skip_nan), ptr(part), ptr(out))
+    return tuple(float(x) for x in out.cpu().tolist())
+
+
+def histogram(codes: torch.Tensor, nbins: int) -> torch.Tensor:
+    """counts[nbins + 1] (int64); last bin = nulls / out-of-range."""
+    if not on_device(codes):
+        c = codes.long().clone()
+        c[(c < 0) | (c >= nbins)] = nbins
+        return torch.bincount(c, minlength=nbins + 1)
+    out = torch.zeros(nbins + 1, dtype=torch.int64, device=codes.device)
+    hip("ptg_histogram_i32", ptr(codes), codes.numel(), ptr(out), nbins)
+    return out
+
+
+# ------------------------------------------------------------------------------------------------
+# hash aggregation
+# ------------------------------------------------------------------------------------------------
+def _pow2(x: int) -> int:
+    return 1 << max(4, int(math.ceil(math.log2(max(x, 1)))))
+
+
+def hash_agg(keys: torch.Tensor, vals: list, valids: list, want_minmax: bool = False, cap_hint: int | None = None):
+    """groupBy(key).agg over int64 keys.  Returns (keys[m], rows[m], [(sum, cnt, min, max)] per value column)
+    as tensors on the keys' device."""
+    nv = len(vals)
+    n = keys.numel()
+    if not on_device(keys):
+        uk, inv = torch.unique(keys, return_inverse=True)
+        m = uk.numel()
+        rows = torch.bincount(inv, minlength=m).double()
+        outs = []
+        for v, vd in zip(vals, valids):
+            x = v.double()
+            ok = ~torch.isnan(x) if vd is None else (vd.bool() & ~torch.isnan(x))
+            xs = torch.where(ok, x, torch.zeros_like(x))
+            s = torch.zeros(m, dtype=torch.float64).index_add_(0, inv, xs)
+            c = torch.zeros(m, dtype=torch.float64).index_add_(0, inv, ok.double())
+            mn = torch.full((m,), math.inf, dtype=torch.float64).scatter_reduce_(0, inv, torch.where(ok, x, torch.full_like(x, math.inf)), "amin")
+            mx = torch.full((m,), -math.inf, dtype=torch.float64).scatter_reduce_(0, inv, torch.where(ok, x, torch.full_like(x, -math.inf)), "amax")
+            outs.append((s, c, mn, mx))
+        return uk, rows, outs
+    dev = keys.device
+    cap = _pow2(2 * (cap_hint if cap_hint else min(n, 1 << 22)) + 16)
+    gkeys = torch.empty(cap, dtype=torch.int64, device=dev)
+    gtab = torch.empty((1 + 4 * nv) * cap, dtype=torch.float64, device=dev)
+    overflow = torch.zeros(1, dtype=torch.int32, device=dev)
+    hip("ptg_hash_table_init", ptr(gkeys), ptr(gtab), cap, nv)
+    vptrs = (ctypes.c_void_p * 4)(*[v.data_ptr() for v in vals])
+    vvals = (ctypes.c_void_p * 4)(*[(vd.data_ptr() if vd is not None else 0) for vd in valids])
+    types = (ctypes.c_int * 4)(*[TORCH_CT[v.dtype] for v in vals])
+    hip("ptg_hash_agg", ptr(keys), n, ctypes.addressof(vptrs), ctypes.addressof(vvals), ctypes.addressof(types), nv,
+        int(want_minmax), ptr(gkeys), ptr(gtab), cap, ptr(overflow))
+    if int(overflow.item()):
+        # table too small for the key cardinality: retry with a larger table
+        return hash_agg(keys, vals, valids, want_minmax, cap_hint=cap * 2)
+    return _extract(gkeys, gtab, cap, nv)
+
+
+def _extract(gkeys, gtab, cap, nv):
+    dev = gkeys.device
+    mcount = torch.zeros(1, dtype=torch.int64, device=dev)
+    hip("ptg_hash_extract", ptr(gkeys), ptr(gtab), cap, nv, None, None, 0, ptr(mcount))
+    m = int(mcount.item())
+    ok = torch.empty(m, dtype=torch.int64, device=dev)
+    ot = torch.empty((1 + 4 * nv) * max(m, 1), dtype=torch.float64, device=dev)
+    mcount.zero_()
+    hip("ptg_hash_extract", ptr(gkeys), ptr(gtab), cap, nv, ptr(ok), ptr(ot), m, ptr(mcount))
+    ot = ot.view(1 + 4 * nv, max(m, 1))[:, :m]
+    outs = [(ot[1 + 4 * j], ot[2 + 4 * j], ot[3 + 4 * j], ot[4 + 4 * j]) for j in range(nv)]
+    return ok, ot[0], outs
+
+
+def hash_agg_partitioned(keys: torch.Tensor, val: torch.Tensor, pbits: int = 9, ws: dict | None = None):
+    """High-cardinality sum/count aggregation: radix-partition by key hash, then one LDS table per
+    partition.  Returns (keys[m], sum[m], cnt[m]).  ``ws`` caches scratch buffers across calls."""
+    dev = keys.device
+    n = keys.numel()
+    P = 1 << pbits
+    ws = ws if ws is not None else {}
+
+    def buf(name, shape, dtype):
+        t = ws.get(name)
+        if t is None or t.numel() < int(np.prod(shape)) or t.dtype != dtype:
+            t = torch.empty(shape, dtype=dtype, device=dev)
+            ws[name] = t
+        return t[: int(np.prod(shape))].view(shape)
+
+    counts = buf("counts", (P,), torch.int32)
+    counts.zero_()
+    hip("ptg_part_hist", ptr(keys), n, pbits, ptr(counts))
+    pstart = buf("pstart", (P + 1,), torch.int64)
+    pstart[0] = 0
+    torch.cumsum(counts.to(torch.int64), 0, out=pstart[1:])
+    cursor = buf("cursor", (P,), torch.int64)
+    cursor.copy_(pstart[:P])
+    okeys = buf("okeys", (n,), torch.int64)
+    ovals = buf("ovals", (n,), torch.float64)
+    hip("ptg_part_scatter", ptr(keys), ptr(val), TORCH_CT[val.dtype], n, pbits, ptr(cursor), ptr(okeys), ptr(ovals))
+    cap_out = n if n < (1 << 26) else (1 << 26)
+    out_keys = buf("out_keys", (cap_out,), torch.int64)
+    out_sum = buf("out_sum", (cap_out,), torch.float64)
+    out_cnt = buf("out_cnt", (cap_out,), torch.float64)
+    m_out = buf("m_out", (1,), torch.int64)
+    m_out.zero_()
+    gcap = 1 << 16
+    gkeys = buf("gkeys", (gcap,), torch.int64)
+    gtab = buf("gtab", (5 * gcap,), torch.float64)
+    hip("ptg_hash_table_init", ptr(gkeys), ptr(gtab), gcap, 1)
+    overflow = buf("overflow", (1,), torch.int32)
+    overflow.zero_()
+    hip("ptg_part_agg", ptr(okeys), ptr(ovals), ptr(pstart), P, ptr(out_keys), ptr(out_sum), ptr(out_cnt), ptr(m_out),
+        ptr(gkeys), ptr(gtab), gcap, ptr(overflow))
+    return out_keys, out_sum, out_cnt, m_out, (gkeys, gtab, gcap), overflow
+
+
+def hash_partition(keys: torch.Tensor, P: int):
+    """-> (perm[n] int64 rows grouped by destination partition, counts[P] int64)."""
+    n = keys.numel()
+    if not on_device(keys):
+        k = keys.numpy().astype(np.uint64)
+        h = _mix64_np(k) % np.uint64(P)
+        perm = np.argsort(h, kind="stable")
+        counts = np.bincount(h.astype(np.int64), minlength=P)
+        return torch.from_numpy(perm.astype(np.int64)), torch.from_numpy(counts.astype(np.int64))
+    dev = keys.device
+    part = torch.empty(n, dtype=torch.int32, device=dev)
+    counts = torch.zeros(P, dtype=torch.int64, device=dev)
+    hip("ptg_hash_partition", ptr(keys), n, P, ptr(part), ptr(counts))
+    cursor = torch.zeros(P, dtype=torch.int64, device=dev)
+    cursor[1:] = torch.cumsum(counts, 0)[:-1]
+    perm = torch.empty(n, dtype=torch.int64, device=dev)
+    hip("ptg_partition_perm", ptr(part), n, P, ptr(cursor), ptr(perm))
+    return perm, counts
+
+
+def _mix64_np(x: np.ndarray) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        x = x.copy()
+        x ^= x >> np.uint64(33)
+        x *= np.uint64(0xff51afd7ed558ccd)
+        x ^= x >> np.uint64(33)
+        x *= np.uint64(0xc4ceb9fe1a85ec53)
+        x ^= x >> np.uint64(33)
+    return x
+
+
+def fill_synthetic_kv(n: int, num_keys: int, device, offset: int = 0, seed: int = 42):
+    keys = torch.empty(n, dtype=torch.int64, device=device)
+    vals = torch.empty(n, dtype=torch.float64, device=device)
+    if torch.device(device).type != "cuda":
+        i = np.arange(offset, offset + n, dtype=np.uint64)
+        with np.errstate(over="ignore"):
+            h = _mix64_np(i * np.uint64(0x9E3779B97F4A7C15) + np.uint64(seed))
+            keys.copy_(torch.from_numpy((h % np.uint64(num_keys)).astype(np.int64)))
+            v = (_mix64_np(h ^ np.uint64(0x632BE59BD9B4E019)) >> np.uint64(11)).astype(np.float64) / 9007199254740992.0
+        vals.copy_(torch.from_numpy(v))
+        return keys, vals
+    hip("ptg_fill_synthetic_kv", ptr(keys), ptr(vals), n, offset, num_keys, seed)
+    return keys, vals
+
+
+# ------------------------------------------------------------------------------------------------
+# ML kernels
+# ------------------------------------------------------------------------------------------------
+def assemble_features(segments, n: int, D: int, device):
+    """segments: list of (kind, tensor, offset, V, R) with kind 'onehot' (int32 codes), 'f64', 'f32'."""
+    out = torch.empty((n, D), dtype=torch.float32, device=device)
+    if torch.device(device).type != "cuda":
+        out.zero_()
+        for kind, t, off, V, R in segments:
+            if kind == "onehot":
+                c = t.long()
+                ok = (c >= 0) & (c < V)
+                rows = torch.nonzero(ok).view(-1)
+                for r in range(R):
+                    out[rows, off + r * V + c[rows]] = 1.0
+            else:
+                out[:, off] = t.float()
+        return out
+    kinds = {"onehot": 0, "f64": 1, "f32": 2}
+    segs = list(segments)
+    if len(segs) > 8:
+        raise ValueError("at most 8 assembler segments per launch")
+    pad = lambda xs, v=0: list(xs) + [v] * (8 - len(xs))  # noqa: E731
+    buf = struct.pack("i", len(segs)) + struct.pack("8i", *pad([kinds[s[0]] for s in segs]))
+    buf += b"\0" * 4  # align pointer array to 8
+    buf += struct.pack("8Q", *pad([s[1].data_ptr() for s in segs]))
+    buf += struct.pack("8i", *pad([s[2] for s in segs])) + struct.pack("8i", *pad([s[3] for s in segs]))
+    buf += struct.pack("8i", *pad([s[4] for s in segs]))
+    size = _native.hip_lib().ptg_asm_desc_size()
+    buf += b"\0" * (size - len(buf))
+    cbuf = ctypes.create_string_buffer(buf, len(buf))
+    hip("ptg_assemble_features", ctypes.addressof(cbuf), n, D, ptr(out))
+    return out
+
+
+def kmeans_assign_accum(X, C, assign=None, sums=None, counts=None, cost=None, weights=None, mind=None):
+    n, D = X.shape
+    k = C.shape[0]
+    if not on_device(X):
+        Xd, Cd = X.double(), C.double()
+        d = (Xd * Xd).sum(1)[:, None] - 2 * Xd @ Cd.t() + (Cd * Cd).sum(1)[None, :]
+        d = d.clamp_min(0)
+        best, arg = d.min(1)
+        if assign is not None:
+            assign.copy_(arg.to(assign.dtype))
+        if mind is not None:
+            mind.copy_(best.to(mind.dtype))
+        w = torch.ones(n, dtype=torch.float64) if weights is None else weights.double()
+        if sums is not None:
+            sums.index_add_(0, arg, (X.double() * w[:, None]).to(sums.dtype))
+            counts.index_add_(0, arg, w.to(counts.dtype))
+        if cost is not None:
+            cost += (best * w).sum().to(cost.dtype)
+        return
+    hip("ptg_kmeans_assign_accum", ptr(X), ptr(C), n, D, k, ptr(assign), ptr(sums), ptr(counts), ptr(cost), ptr(weights),
+        ptr(mind))
+
+
+def kmeans_update(sums, counts, C, moved):
+    k, D = C.shape
+    if not on_device(C):
+        newc = torch.where(counts[:, None] > 0, sums / counts.clamp_min(1e-30)[:, None], C)
+        moved.fill_(float(((newc - C) ** 2).sum(1).max()))
+        C.copy_(newc)
+        return
+    hip("ptg_kmeans_update", ptr(sums), ptr(counts), ptr(C), k, D, ptr(moved))
+
+
+def silhouette_sum(X, assign, k: int):
+    """Sum over points of Spark's squared-Euclidean silhouette coefficient (+ per-cluster stats)."""
+    n, D = X.shape
+    dev = X.device
+    S = torch.zeros((k, D), dtype=torch.float32, device=dev)
+    Q = torch.zeros(k, dtype=torch.float32, device=dev)
+    cnt = torch.zeros(k, dtype=torch.float32, device=dev)
+    if not on_device(X):
+        a = assign.long()
+        S.index_add_(0, a, X.float())
+        Q.index_add_(0, a, (X.float() ** 2).sum(1))
+        cnt.index_add_(0, a, torch.ones(n))
+        return S, Q, cnt
+    hip("ptg_cluster_stats", ptr(X), ptr(assign), n, D, ptr(S), ptr(Q), ptr(cnt))
+    return S, Q, cnt
+
+
+def silhouette_points(X, assign, S, Q, cnt) -> float:
+    n, D = X.shape
+    k = S.shape[0]
+    if not on_device(X):
+        Xd = X.double()
+        xn = (Xd ** 2).sum(1)
+        tot = cnt.double()[None, :] * xn[:, None] - 2 * Xd @ S.double().t() + Q.double()[None, :]
+        a_idx = assign.long()
+        own_n = cnt.double()[a_idx]
+        a = torch.where(own_n > 1, tot.gather(1, a_idx[:, None]).squeeze(1) / (own_n - 1).clamp_min(1), torch.zeros(n, dtype=torch.float64))
+        other = tot / cnt.double().clamp_min(1)[None, :]
+        other[torch.arange(n), a_idx] = math.inf
+        other[:, cnt <= 0] = math.inf
+        b = other.min(1).values
+        m = torch.maximum(a, b)
+        s = torch.where((own_n > 1) & torch.isfinite(b) & (m > 0), (b - a) / m, torch.zeros_like(a))
+        return float(s.sum())
+    out = torch.zeros(1, dtype=torch.float64, device=X.device)
+    hip("ptg_silhouette", ptr(X), ptr(assign), ptr(S), ptr(Q), ptr(cnt), n, D, k, ptr(out))
+    return float(out.item())

@@ -1,0 +1,894 @@
+"""DataFrame, GroupedData and Row — the PySpark DataFrame surface of the reference workloads
+(k_means.py, spark_workload_to_cloud_k8s.py, spark_installation_check.py, google_health_SQL.py).
+
+Execution model: SPMD, one rank per GPU = one Spark executor.  Each rank holds its partition as a
+device-resident :class:`~.table.Table`; transformations run immediately on that partition with
+the HIP kernels (expression VM, compaction, hash aggregation) and keep their result resident
+(the reference re-reads its JDBC source on every action because nothing is cached, SURVEY §3.3;
+here nothing needs re-reading).  Actions combine ranks with RCCL (count/agg all-reduce, groupBy
+partial-aggregate -> hash shuffle -> final aggregate) and gather small results to the driver view
+(every rank, like a Spark driver) for ``collect``/``show``.
+"""
+from __future__ import annotations
+
+import math
+import re
+
+import numpy as np
+import torch
+
+from ..ops import df as D
+from ..parallel import comm
+from . import column as C
+from . import types as T
+from .column import Column, col, expr_name
+from .table import ColumnVector, Table, column_from_python
+
+
+class Row(tuple):
+    def __new__(cls, *args, **kwargs):
+        if kwargs:
+            r = tuple.__new__(cls, tuple(kwargs.values()))
+            r.__fields__ = list(kwargs.keys())
+            return r
+        r = tuple.__new__(cls, args)
+        r.__fields__ = None
+        return r
+
+    @classmethod
+    def _make(cls, fields, values):
+        r = tuple.__new__(cls, tuple(values))
+        r.__fields__ = list(fields)
+        return r
+
+    def asDict(self):  # noqa: N802
+        return dict(zip(self.__fields__ or [], self))
+
+    def __getattr__(self, item):
+        f = self.__dict__.get("__fields__") if "__fields__" in self.__dict__ else None
+        if f and item in f:
+            return self[f.index(item)]
+        raise AttributeError(item)
+
+    def __getitem__(self, k):
+        if isinstance(k, str):
+            return tuple.__getitem__(self, self.__fields__.index(k))
+        return tuple.__getitem__(self, k)
+
+    def __repr__(self):
+        if self.__fields__:
+            return "Row(" + ", ".join(f"{k}={v!r}" for k, v in zip(self.__fields__, self)) + ")"
+        return "<Row(" + ", ".join(repr(v) for v in self) + ")>"
+
+
+_VM_OUT = {T.BooleanType: D.CT_U8, T.IntegerType: D.CT_I32, T.LongType: D.CT_I64, T.DoubleType: D.CT_F64,
+           T.FloatType: D.CT_F32}
+_TORCH_OF = {T.BooleanType: torch.uint8, T.IntegerType: torch.int32, T.LongType: torch.int64,
+             T.DoubleType: torch.float64, T.FloatType: torch.float32}
+
+
+def _to_col(c) -> Column:
+    return col(c) if isinstance(c, str) else c
+
+
+class DataFrame:
+    def __init__(self, table: Table, session, replicated: bool = False):
+        self._t = table
+        self.sparkSession = session
+        self._num_partitions = session.default_parallelism if session is not None else 1
+
+    # ------------------------------------------------------------------ schema
+    @property
+    def columns(self):
+        return self._t.names
+
+    @property
+    def schema(self) -> T.StructType:
+        return self._t.schema()
+
+    @property
+    def dtypes(self):
+        return [(f.name, f.dataType.simple) for f in self.schema]
+
+    def printSchema(self):  # noqa: N802
+        if comm.rank() == 0:
+            print(self.schema.treeString(), end="", flush=True)
+
+    def __getitem__(self, item):
+        if isinstance(item, str):
+            return col(self._t.resolve(item))
+        if isinstance(item, Column):
+            return self.filter(item)
+        if isinstance(item, (list, tuple)):
+            return self.select(*item)
+        raise TypeError(item)
+
+    def __getattr__(self, item):
+        if item.startswith("_"):
+            raise AttributeError(item)
+        try:
+            return col(self._t.resolve(item))
+        except KeyError:
+            raise AttributeError(item) from None
+
+    # ------------------------------------------------------------------ expression evaluation
+    def _new(self, table: Table) -> "DataFrame":
+        d = DataFrame(table, self.sparkSession)
+        d._num_partitions = self._num_partitions
+        return d
+
+    def _eval(self, c: Column, name_hint=None) -> tuple:
+        node = c.node
+        name = name_hint or expr_name(node)
+        base = C.strip_alias(node)
+        t = self._t
+        if base[0] == "col":
+            return name, t.column(base[1])
+        if base[0] in ("split", "explode", "agg"):
+            raise TypeError(f"{base[0]} is only valid as a top-level select() expression / in agg()")
+        if base[0] == "strmap":
+            src = self._eval(Column(base[2]))[1]
+            f = {"lower": str.lower, "upper": str.upper, "trim": str.strip}[base[1]]
+            mapped = [f(s) for s in src.dictionary or []]
+            return name, _remap_dictionary(src, mapped)
+        if base[0] == "strlen":
+            src = self._eval(Column(base[1]))[1]
+            lens = torch.tensor([len(s) for s in (src.dictionary or [])] + [0], dtype=torch.int32, device=t.device)
+            codes = src.data.long()
+            codes = torch.where(codes < 0, torch.full_like(codes, len(src.dictionary or [])), codes)
+            return name, ColumnVector(D.gather_rows(lens, codes), T.IntegerType(), src.valid_u8() if src.valid is not None else (src.data >= 0).to(torch.uint8))
+        if base[0] == "rand":
+            g = torch.Generator(device=t.device)
+            g.manual_seed((base[1] or 0) * 1000003 + comm.rank())
+            return name, ColumnVector(torch.rand(t.num_rows, generator=g, dtype=torch.float64, device=t.device),
+                                      T.DoubleType())
+        if base[0] == "rowid":
+            off = comm.rank() << 33
+            return name, ColumnVector(torch.arange(t.num_rows, dtype=torch.int64, device=t.device) + off, T.LongType())
+        if base[0] == "lit" and isinstance(base[1], str):
+            return name, ColumnVector(torch.zeros(t.num_rows, dtype=torch.int32, device=t.device), T.StringType(),
+                                      None, [base[1]])
+        if base[0] == "bin" and base[1] == "coalesce":
+            a, b = self._eval(Column(base[2]))[1], self._eval(Column(base[3]))[1]
+            if isinstance(a.dtype, T.StringType) and isinstance(b.dtype, T.StringType):
+                return name, _coalesce_strings(a, b)
+        dtype = C.infer_type(node, t)
+        if isinstance(dtype, T.StringType):
+            raise TypeError(f"string-valued expression {name} is not supported")
+        n = t.num_rows
+        if t.device.type == "cuda":
+            ins, r, consts, cols = C.compile_vm(node, t)
+            out = torch.empty(n, dtype=_TORCH_OF[type(dtype)], device=t.device)
+            valid = torch.empty(n, dtype=torch.uint8, device=t.device)
+            if n:
+                prog = D.pack_vm_prog(ins, r, _VM_OUT[type(dtype)], 0, consts, cols)
+                D.expr_eval(prog, n, out, valid)
+            if isinstance(dtype, T.BooleanType):
+                out = out.bool()
+            return name, ColumnVector(out, dtype, valid)
+        v, ok = C.eval_host(node, t)
+        tdt = _TORCH_OF[type(dtype)]
+        if tdt == torch.uint8:
+            out = (v != 0) & ok
+            out = out.bool()
+        elif tdt in (torch.int32, torch.int64):
+            out = torch.where(ok, v, torch.zeros_like(v)).to(tdt)
+        else:
+            out = torch.where(ok, v, torch.full_like(v, math.nan)).to(tdt)
+        return name, ColumnVector(out, dtype, ok.to(torch.uint8))
+
+    def _mask(self, cond) -> torch.Tensor:
+        t = self._t
+        n = t.num_rows
+        if isinstance(cond, str):
+            cond = _parse_sql_predicate(cond)
+        if t.device.type == "cuda":
+            ins, r, consts, cols = C.compile_vm(cond.node, t)
+            mask = torch.empty(n, dtype=torch.uint8, device=t.device)
+            if n:
+                D.expr_eval(D.pack_vm_prog(ins, r, D.CT_U8, 1, consts, cols), n, mask)
+            return mask
+        v, ok = C.eval_host(cond.node, t)
+        return ((v != 0) & ok).to(torch.uint8)
+
+    # ------------------------------------------------------------------ transformations
+    def filter(self, condition) -> "DataFrame":
+        idx = D.compact(self._mask(condition))
+        return self._new(self._t.take(idx))
+
+    where = filter
+
+    def select(self, *cols) -> "DataFrame":
+        if len(cols) == 1 and isinstance(cols[0], (list, tuple)):
+            cols = tuple(cols[0])
+        if any(isinstance(c, str) and c == "*" for c in cols):
+            cols = tuple(x for c in cols for x in ([col(n) for n in self.columns] if c == "*" else [c]))
+        cs = [_to_col(c) for c in cols]
+        for c in cs:
+            base = C.strip_alias(c.node)
+            if base[0] == "explode":
+                if len(cs) != 1:
+                    raise NotImplementedError("explode() must be the only select expression")
+                name = c.node[1] if c.node[0] == "alias" else "col"
+                return self._explode(base, name)
+            if base[0] == "agg":
+                return self.agg(*cs)
+        out = {}
+        for c in cs:
+            name, cv = self._eval(c)
+            out[name] = cv
+        return self._new(Table(out, self._t.num_rows, self._t.device))
+
+    def selectExpr(self, *exprs):  # noqa: N802
+        return self.select(*[col(e) for e in exprs])
+
+    def withColumn(self, colName: str, c: Column) -> "DataFrame":  # noqa: N802, N803
+        _, cv = self._eval(c, colName)
+        return self._new(self._t.with_column(colName, cv))
+
+    def withColumnRenamed(self, existing: str, new: str) -> "DataFrame":  # noqa: N802
+        cols = {}
+        for n, cv in self._t.columns.items():
+            cols[new if n.lower() == existing.lower() else n] = cv
+        return self._new(Table(cols, self._t.num_rows, self._t.device))
+
+    def toDF(self, *names) -> "DataFrame":  # noqa: N802
+        return self._new(Table(dict(zip(names, self._t.columns.values())), self._t.num_rows, self._t.device))
+
+    def drop(self, *names) -> "DataFrame":
+        drop = {(n if isinstance(n, str) else expr_name(n.node)).lower() for n in names}
+        return self._new(Table({n: c for n, c in self._t.columns.items() if n.lower() not in drop},
+                               self._t.num_rows, self._t.device))
+
+    def limit(self, num: int) -> "DataFrame":
+        # global limit: ranks keep rows in rank order until `num` rows are taken
+        counts = comm.all_gather_object(self._t.num_rows)
+        before = sum(counts[: comm.rank()])
+        keep = max(0, min(self._t.num_rows, num - before))
+        return self._new(self._t.slice(0, keep))
+
+    def _explode(self, node, name) -> "DataFrame":
+        inner = node[1]
+        if inner[0] != "split":
+            raise NotImplementedError("explode() supports split(col, pattern)")
+        pattern, src_node = inner[1], inner[2]
+        _, src = self._eval(Column(src_node))
+        rx = re.compile(pattern)
+        toks = [[w for w in rx.split(s)] for s in (src.dictionary or [])]
+        words, widx = [], {}
+        tok_codes = []
+        for ts in toks:
+            cs = []
+            for w in ts:
+                if w not in widx:
+                    widx[w] = len(words)
+                    words.append(w)
+                cs.append(widx[w])
+            tok_codes.append(cs)
+        codes = src.data.cpu().numpy()
+        valid = codes >= 0
+        lens = np.array([len(x) for x in tok_codes] + [0], dtype=np.int64)
+        safe = np.where(valid, codes, len(tok_codes))
+        per_row = lens[safe]
+        flat = np.array([c for x in tok_codes for c in x] + [0], dtype=np.int32)
+        starts = np.concatenate([[0], np.cumsum(lens[:-1])])
+        row_rep = np.repeat(np.arange(len(codes)), per_row)
+        within = np.arange(per_row.sum()) - np.repeat(np.cumsum(per_row) - per_row, per_row)
+        out_codes = flat[starts[safe[row_rep]] + within] if len(row_rep) else np.zeros(0, np.int32)
+        cv = ColumnVector(torch.from_numpy(out_codes.astype(np.int32)).to(self._t.device), T.StringType(), None, words)
+        return self._new(Table({name: cv}, len(out_codes), self._t.device))
+
+    # ------------------------------------------------------------------ actions
+    def count(self) -> int:
+        n = torch.tensor([self._t.num_rows], dtype=torch.int64)
+        if comm.world_size() > 1:
+            return int(sum(comm.all_gather_object(self._t.num_rows)))
+        return int(n.item())
+
+    def collect(self) -> list:
+        names = self.columns
+        local = self._t.rows()
+        if comm.world_size() > 1:
+            parts = comm.all_gather_object(local)
+            local = [r for p in parts for r in p]
+        return [Row._make(names, r) for r in local]
+
+    def take(self, num: int) -> list:
+        return self.limit(num).collect()
+
+    def head(self, n: int | None = None):
+        if n is None:
+            rows = self.take(1)
+            return rows[0] if rows else None
+        return self.take(n)
+
+    def first(self):
+        return self.head()
+
+    def isEmpty(self) -> bool:  # noqa: N802
+        return self.count() == 0
+
+    def toPandas(self):  # noqa: N802
+        import pandas as pd
+
+        rows = self.collect()
+        return pd.DataFrame([tuple(r) for r in rows], columns=self.columns)
+
+    def show(self, n: int = 20, truncate=True, vertical: bool = False) -> None:
+        rows = self.limit(n + 1).collect()
+        more = len(rows) > n
+        rows = rows[:n]
+        if comm.rank() != 0:
+            return
+        width = 20 if truncate is True else (int(truncate) if truncate else 0)
+
+        def fmt(v):
+            if v is None:
+                s = "NULL"
+            elif isinstance(v, bool):
+                s = str(v).lower()
+            elif isinstance(v, float):
+                s = "NaN" if math.isnan(v) else repr(v)
+            else:
+                s = str(v)
+            if width and len(s) > width:
+                s = s[: width - 3] + "..."
+            return s
+
+        cells = [[fmt(v) for v in r] for r in rows]
+        names = self.columns
+        w = [max([len(h)] + [len(c[i]) for c in cells]) for i, h in enumerate(names)]
+        sep = "+" + "+".join("-" * x for x in w) + "+"
+        out = [sep, "|" + "|".join(h.rjust(x) for h, x in zip(names, w)) + "|", sep]
+        for c in cells:
+            out.append("|" + "|".join(v.rjust(x) for v, x in zip(c, w)) + "|")
+        out.append(sep)
+        if more:
+            out.append(f"only showing top {n} row{'s' if n != 1 else ''}")
+        print("\n".join(out) + "\n", flush=True)
+
+    # ------------------------------------------------------------------ aggregation
+    def groupBy(self, *cols) -> "GroupedData":  # noqa: N802
+        if len(cols) == 1 and isinstance(cols[0], (list, tuple)):
+            cols = tuple(cols[0])
+        return GroupedData(self, [_to_col(c) for c in cols])
+
+    groupby = groupBy
+
+    def agg(self, *exprs) -> "DataFrame":
+        return GroupedData(self, []).agg(*exprs)
+
+    def describe(self, *cols) -> "DataFrame":
+        names = list(cols) or [n for n, c in self._t.columns.items() if isinstance(c.dtype, T.NUMERIC)]
+        stats = {}
+        for n in names:
+            s, c, mn, mx, _ = _global_stats(self._t.column(n))
+            mean = s / c if c else None
+            # second pass for stddev
+            cv = self._t.column(n)
+            x = cv.data.double()
+            ok = cv.valid_bool() & ~torch.isnan(x)
+            dev2 = float(((x - (mean or 0.0)) ** 2)[ok].sum()) if c else 0.0
+            if comm.world_size() > 1:
+                dev2 = float(sum(comm.all_gather_object(dev2)))
+            sd = math.sqrt(dev2 / (c - 1)) if c > 1 else None
+            stats[n] = [str(int(c)), str(mean), str(sd), str(mn if c else None), str(mx if c else None)]
+        rows = [["count"], ["mean"], ["stddev"], ["min"], ["max"]]
+        for i in range(5):
+            rows[i] += [stats[n][i] for n in names]
+        data = rows if comm.rank() == 0 else []
+        return self.sparkSession.createDataFrame(data, ["summary"] + names, _local=True)
+
+    # ------------------------------------------------------------------ misc
+    def orderBy(self, *cols, ascending=True) -> "DataFrame":  # noqa: N802
+        if len(cols) == 1 and isinstance(cols[0], (list, tuple)):
+            cols = tuple(cols[0])
+        t = self._t
+        if comm.world_size() > 1:
+            # global order: gather to rank 0 (sort results are small in the workloads), rank 0 sorts
+            t = _gather_table_to_rank0(t)
+        if t.num_rows == 0:
+            return self._new(t)
+        asc = ascending if isinstance(ascending, (list, tuple)) else [ascending] * len(cols)
+        perm = torch.arange(t.num_rows, device=t.device)
+        for c, a in reversed(list(zip(cols, asc))):
+            c = _to_col(c)
+            if c.node[0] == "sort":
+                a = c.node[1]
+                c = Column(c.node[2])
+            _, cv = DataFrame(t, self.sparkSession)._eval(c)
+            key = cv.data.take(perm) if cv.data.dim() == 1 else cv.data[perm]
+            if isinstance(cv.dtype, T.StringType):
+                order = np.argsort(np.argsort(np.array(cv.dictionary or [], dtype=object)))
+                lut = torch.tensor(list(order) + [-1], dtype=torch.int64, device=t.device)
+                kk = key.long()
+                key = lut[torch.where(kk < 0, torch.full_like(kk, len(order)), kk)]
+            key = key.double() if key.dtype == torch.bool else key
+            idx = torch.argsort(key, stable=True, descending=not a)
+            perm = perm[idx]
+        return self._new(t.take(perm))
+
+    sort = orderBy
+
+    def distinct(self) -> "DataFrame":
+        return self.dropDuplicates()
+
+    def dropDuplicates(self, subset=None) -> "DataFrame":  # noqa: N802
+        names = subset or self.columns
+        g = GroupedData(self, [col(n) for n in names])
+        return g.agg(*[]) if set(names) == set(self.columns) else g._first_rows()
+
+    drop_duplicates = dropDuplicates
+
+    def union(self, other: "DataFrame") -> "DataFrame":
+        return self._new(Table.concat([self._t, other._t.select(self.columns) if other.columns != self.columns else other._t]))
+
+    unionAll = union
+
+    def unionByName(self, other: "DataFrame", allowMissingColumns=False) -> "DataFrame":  # noqa: N802, N803
+        return self._new(Table.concat([self._t, other._t.select(self.columns)]))
+
+    def repartition(self, numPartitions=None, *cols) -> "DataFrame":  # noqa: N803
+        if isinstance(numPartitions, (str, Column)):
+            cols = (numPartitions,) + cols
+            numPartitions = None
+        d = self._new(self._t)
+        if cols and comm.world_size() > 1:
+            d = self._new(_shuffle_by_key(self._t, _group_keys(self, [_to_col(c) for c in cols])[0]))
+        if numPartitions:
+            d._num_partitions = int(numPartitions)
+        return d
+
+    def coalesce(self, numPartitions: int) -> "DataFrame":  # noqa: N803
+        d = self._new(self._t)
+        d._num_partitions = min(self._num_partitions, int(numPartitions))
+        return d
+
+    def cache(self):
+        return self
+
+    persist = cache
+
+    def unpersist(self, blocking=False):
+        return self
+
+    @property
+    def rdd(self):
+        from .rdd import RDD
+
+        return RDD.from_rows(self.sparkSession.sparkContext, self.collect())
+
+    @property
+    def na(self):
+        return _NaFunctions(self)
+
+    def fillna(self, value, subset=None) -> "DataFrame":
+        d = self
+        items = value.items() if isinstance(value, dict) else [(n, value) for n in (subset or self.columns)]
+        for n, v in items:
+            cv = self._t.column(n)
+            if isinstance(cv.dtype, T.StringType) != isinstance(v, str):
+                continue
+            if isinstance(v, str):
+                d = d.withColumn(n, Column(("bin", "coalesce", col(n).node, ("lit", v))))
+            else:
+                d = d.withColumn(n, C.Column(("when", [((col(n).isNull() | C.Column(("un", "ISNAN", col(n).node))).node,
+                                                        ("lit", v))], col(n).node)))
+        return d
+
+    def dropna(self, how="any", thresh=None, subset=None) -> "DataFrame":
+        names = subset or self.columns
+        conds = [col(n).isNotNull() for n in names]
+        if how == "all" and thresh is None:
+            out = conds[0]
+            for c in conds[1:]:
+                out = out | c
+        else:
+            out = conds[0]
+            for c in conds[1:]:
+                out = out & c
+        return self.filter(out)
+
+    def randomSplit(self, weights, seed=None):  # noqa: N802
+        total = float(sum(weights))
+        g = torch.Generator()
+        g.manual_seed((seed or 0) + comm.rank())
+        u = torch.rand(self._t.num_rows, generator=g).to(self._t.device)
+        out, lo = [], 0.0
+        for w in weights:
+            hi = lo + w / total
+            idx = D.compact(((u >= lo) & (u < hi)).to(torch.uint8))
+            out.append(self._new(self._t.take(idx)))
+            lo = hi
+        return out
+
+    def sample(self, withReplacement=False, fraction=0.1, seed=None):  # noqa: N803
+        return self.randomSplit([fraction, 1 - fraction], seed)[0]
+
+    def createOrReplaceTempView(self, name: str) -> None:  # noqa: N802
+        self.sparkSession._views[name] = self
+
+    createTempView = createOrReplaceTempView
+
+    @property
+    def write(self):
+        from .readwriter import DataFrameWriter
+
+        return DataFrameWriter(self)
+
+    def __repr__(self):
+        return "DataFrame[" + ", ".join(f"{n}: {t}" for n, t in self.dtypes) + "]"
+
+
+class _NaFunctions:
+    def __init__(self, df):
+        self.df = df
+
+    def fill(self, value, subset=None):
+        return self.df.fillna(value, subset)
+
+    def drop(self, how="any", thresh=None, subset=None):
+        return self.df.dropna(how, thresh, subset)
+
+
+def _remap_dictionary(src: ColumnVector, mapped: list) -> ColumnVector:
+    new, idx, lut = [], {}, []
+    for s in mapped:
+        if s not in idx:
+            idx[s] = len(new)
+            new.append(s)
+        lut.append(idx[s])
+    lut_t = torch.tensor(lut + [-1], dtype=torch.int32, device=src.device)
+    codes = src.data.long()
+    codes = torch.where(codes < 0, torch.full_like(codes, len(lut)), codes)
+    return ColumnVector(D.gather_rows(lut_t, codes), T.StringType(), src.valid, new)
+
+
+def _coalesce_strings(a: ColumnVector, b: ColumnVector) -> ColumnVector:
+    from .table import concat_columns
+
+    merged = concat_columns([a, b])  # dictionary union + remap
+    n = len(a)
+    ca, cb = merged.data[:n], merged.data[n:]
+    va = a.valid_bool() & (a.data >= 0)
+    return ColumnVector(torch.where(va, ca, cb), T.StringType(), None, merged.dictionary)
+
+
+def _parse_sql_predicate(s: str) -> Column:
+    """Tiny SQL predicate parser for ``df.filter("Age > 30")``-style strings: <col> <op> <literal>
+    joined by AND/OR."""
+    parts = re.split(r"\s+(AND|OR)\s+", s.strip(), flags=re.I)
+    out, pending = None, None
+    for p in parts:
+        if p.upper() in ("AND", "OR"):
+            pending = p.upper()
+            continue
+        m = re.match(r"^\s*([A-Za-z_][\w]*)\s*(==|=|!=|<>|>=|<=|>|<)\s*(.+?)\s*$", p)
+        if m:
+            name, op, lit_s = m.groups()
+            if lit_s.startswith(("'", '"')):
+                lit_v = lit_s[1:-1]
+            else:
+                lit_v = float(lit_s) if any(ch in lit_s for ch in ".eE") else int(lit_s)
+            op = {"=": "==", "<>": "!="}.get(op, op)
+            c = col(name)._bin(op, lit_v)
+        else:
+            m = re.match(r"^\s*([A-Za-z_][\w]*)\s+IS\s+(NOT\s+)?NULL\s*$", p, flags=re.I)
+            if not m:
+                raise ValueError(f"unsupported predicate: {p!r}")
+            c = col(m.group(1)).isNotNull() if m.group(2) else col(m.group(1)).isNull()
+        out = c if out is None else (out & c if pending == "AND" else out | c)
+    return out
+
+
+def _global_stats(cv: ColumnVector):
+    s, c, mn, mx, nul = D.reduce_stats(cv.data if cv.data.dtype != torch.bool else cv.data.to(torch.uint8),
+                                       cv.valid_u8(), skip_nan=True)
+    if comm.world_size() > 1:
+        parts = comm.all_gather_object((s, c, mn, mx, nul))
+        s = sum(p[0] for p in parts); c = sum(p[1] for p in parts)
+        mn = min(p[2] for p in parts); mx = max(p[3] for p in parts); nul = sum(p[4] for p in parts)
+    return s, c, mn, mx, nul
+
+
+# ------------------------------------------------------------------------------------------------
+# grouping
+# ------------------------------------------------------------------------------------------------
+_NULL_KEY = -(2 ** 62)
+
+
+def _key_of(cv: ColumnVector) -> torch.Tensor:
+    """int64 grouping key of one column (nulls -> one dedicated key)."""
+    d = cv.data
+    if isinstance(cv.dtype, T.StringType):
+        k = d.long()
+        null = k < 0
+    elif d.dtype in (torch.float64, torch.float32):
+        x = d.double()
+        x = torch.where(torch.isnan(x), torch.full_like(x, math.nan), x) + 0.0  # canonical NaN, -0 -> +0
+        k = x.view(torch.int64)
+        null = torch.zeros_like(k, dtype=torch.bool)
+    else:
+        k = d.long()
+        null = torch.zeros_like(k, dtype=torch.bool)
+    if cv.valid is not None:
+        null = null | ~cv.valid.bool()
+    return torch.where(null, torch.full_like(k, _NULL_KEY), k)
+
+
+def _group_keys(df: "DataFrame", cols: list):
+    """-> (int64 combined key per row, [(name, ColumnVector source)]).  Multi-column keys are
+    combined through dense per-column codes (exact, no hash collisions)."""
+    srcs = []
+    for c in cols:
+        name, cv = df._eval(c)
+        srcs.append((name, cv))
+    if not srcs:
+        return torch.zeros(df._t.num_rows, dtype=torch.int64, device=df._t.device), srcs
+    if len(srcs) == 1:
+        return _key_of(srcs[0][1]), srcs
+    combined = None
+    for _, cv in srcs:
+        k = _key_of(cv)
+        if comm.world_size() > 1:
+            # globally consistent dense codes: union of distinct keys across ranks
+            uk = torch.unique(k)
+            allk = comm.all_gather_object(uk.cpu().numpy())
+            glob = torch.from_numpy(np.unique(np.concatenate(allk))).to(k.device)
+            code = torch.searchsorted(glob, k)
+            card = glob.numel()
+        else:
+            glob, code = torch.unique(k, return_inverse=True)
+            card = glob.numel()
+        combined = code.long() if combined is None else combined * card + code.long()
+    return combined, srcs
+
+
+def _shuffle_by_key(t: Table, key: torch.Tensor) -> Table:
+    """Hash-partition rows by key across ranks (RCCL all-to-all-v of every column)."""
+    world = comm.world_size()
+    perm, counts = D.hash_partition(key, world)
+    send = t.take(perm)
+    sc = [int(x) for x in counts.cpu().tolist()]
+    rc = None
+    cols = {}
+    for n, cv in send.columns.items():
+        data = comm.all_to_all_v(cv.data.contiguous(), sc, rc)
+        if rc is None:
+            rc = [int(x) for x in _recv_counts(sc)]
+        valid = comm.all_to_all_v(cv.valid_u8().contiguous(), sc, rc) if cv.valid is not None else None
+        cols[n] = ColumnVector(data, cv.dtype, valid, cv.dictionary)
+    nrows = sum(rc) if rc is not None else 0
+    return Table(cols, nrows, t.device)
+
+
+def _recv_counts(send_counts):
+    parts = comm.all_gather_object(send_counts)
+    r = comm.rank()
+    return [p[r] for p in parts]
+
+
+def _gather_table_to_rank0(t: Table) -> Table:
+    parts = comm.all_gather_object({n: (c.data.cpu(), None if c.valid is None else c.valid.cpu(), c.dtype,
+                                        c.dictionary) for n, c in t.columns.items()})
+    if comm.rank() != 0:
+        return t.slice(0, 0)
+    tables = [Table({n: ColumnVector(v[0].to(t.device), v[2], None if v[1] is None else v[1].to(t.device), v[3])
+                     for n, v in p.items()}) for p in parts]
+    return Table.concat(tables)
+
+
+class GroupedData:
+    def __init__(self, df: DataFrame, cols: list):
+        self.df = df
+        self.cols = cols
+
+    def _aggs_from(self, exprs):
+        aggs = []  # (out_name, fn, source column name or None)
+        if len(exprs) == 1 and isinstance(exprs[0], dict):
+            for cname, fn in exprs[0].items():
+                fn = {"mean": "avg", "average": "avg"}.get(fn, fn)
+                src = None if cname == "*" else cname
+                label = f"{fn}({'1' if src is None and fn == 'count' else (cname if src else '*')})"
+                aggs.append((label, fn, None if src is None else col(src)))
+            return aggs
+        for e in exprs:
+            node = e.node
+            name = node[1] if node[0] == "alias" else None
+            base = C.strip_alias(node)
+            if base[0] != "agg":
+                raise TypeError(f"not an aggregate expression: {expr_name(node)}")
+            fn, x = base[1], base[2]
+            aggs.append((name or expr_name(base), fn, None if x is None else Column(x)))
+        return aggs
+
+    def count(self) -> DataFrame:
+        return self.agg(Column(("alias", "count", ("agg", "count", None))))
+
+    def _simple(self, fn, cols):
+        df = self.df
+        names = cols or [n for n, c in df._t.columns.items() if isinstance(c.dtype, T.NUMERIC)
+                         and n not in {expr_name(c.node) for c in self.cols}]
+        return self.agg(*[Column(("alias", f"{fn}({n})", ("agg", fn, col(n).node))) for n in names])
+
+    def sum(self, *cols):
+        return self._simple("sum", cols)
+
+    def avg(self, *cols):
+        return self._simple("avg", cols)
+
+    mean = avg
+
+    def min(self, *cols):
+        return self._simple("min", cols)
+
+    def max(self, *cols):
+        return self._simple("max", cols)
+
+    def agg(self, *exprs) -> DataFrame:
+        df = self.df
+        t = df._t
+        aggs = self._aggs_from(exprs)
+        sess = df.sparkSession
+        world = comm.world_size()
+        if not self.cols:  # global aggregation -> one row on rank 0
+            vals = {}
+            for label, fn, src in aggs:
+                if src is None:
+                    vals[label] = df.count()
+                    continue
+                _, cv = df._eval(src)
+                if fn == "count_distinct":
+                    k = _key_of(cv)
+                    loc = torch.unique(k[k != _NULL_KEY]).cpu().numpy()
+                    vals[label] = int(np.unique(np.concatenate(comm.all_gather_object(loc))).size)
+                    continue
+                if fn == "first":
+                    vals[label] = df.select(src).first()[0] if df.count() else None
+                    continue
+                s, c, mn, mx, nul = _global_stats(cv)
+                if fn == "count":
+                    vals[label] = int(c + (nul if cv.data.dtype in (torch.float32, torch.float64) and False else 0))
+                    # Spark count(col) counts non-null values (NaN counts as a value)
+                    x = cv.data
+                    if x.dtype in (torch.float32, torch.float64):
+                        nn = int((cv.valid_bool()).sum())
+                        vals[label] = int(sum(comm.all_gather_object(nn))) if world > 1 else nn
+                elif fn == "sum":
+                    vals[label] = s if c else None
+                elif fn == "avg":
+                    vals[label] = s / c if c else None
+                elif fn == "min":
+                    vals[label] = mn if c else None
+                elif fn == "max":
+                    vals[label] = mx if c else None
+                elif fn == "stddev":
+                    mean = s / c if c else 0.0
+                    x = cv.data.double()
+                    ok = cv.valid_bool() & ~torch.isnan(x)
+                    d2 = float(((x - mean) ** 2)[ok].sum())
+                    if world > 1:
+                        d2 = float(sum(comm.all_gather_object(d2)))
+                    vals[label] = math.sqrt(d2 / (c - 1)) if c > 1 else None
+                else:
+                    raise ValueError(f"unsupported aggregate {fn}")
+            data = [tuple(vals.values())] if comm.rank() == 0 else []
+            schema = []
+            for (label, fn, src), v in zip(aggs, vals.values()):
+                dt = T.LongType() if fn in ("count", "count_distinct") else T.DoubleType()
+                if fn in ("min", "max", "sum") and src is not None:
+                    st = C.infer_type(src.node, t)
+                    dt = st if fn != "sum" or isinstance(st, (T.DoubleType, T.FloatType)) else T.LongType()
+                schema.append(T.StructField(label, dt))
+            return sess.createDataFrame(data, T.StructType(schema), _local=True)
+        # ---- keyed aggregation
+        key, srcs = _group_keys(df, self.cols)
+        value_cols = []
+        for label, fn, src in aggs:
+            if src is None:
+                continue
+            _, cv = df._eval(src)
+            value_cols.append(cv)
+        need_minmax = any(fn in ("min", "max") for _, fn, _ in aggs)
+        key_rep_idx = None
+        # partial aggregation (rank-local)
+        vdata = [_num(cv) for cv in value_cols]
+        vvalid = [cv.valid_u8() for cv in value_cols]
+        ukeys, rows, outs = _hash_agg_all(key, vdata, vvalid, need_minmax)
+        # representative row per group for the key columns (min row index via an index column)
+        ridx = torch.arange(t.num_rows, dtype=torch.float64, device=t.device)
+        _, _, rep = _hash_agg_all(key, [ridx], [None], True)
+        key_rep_idx = rep[0][2].long()  # min row index
+        key_tables = Table({name: cv.take(key_rep_idx) for name, cv in srcs}, ukeys.numel(), t.device)
+        if world > 1:
+            # shuffle partials to the key owner and merge
+            part_cols = {f"__k": ColumnVector(ukeys, T.LongType()), "__rows": ColumnVector(rows, T.DoubleType())}
+            for j, (s, c, mn, mx) in enumerate(outs):
+                part_cols[f"__s{j}"] = ColumnVector(s, T.DoubleType())
+                part_cols[f"__c{j}"] = ColumnVector(c, T.DoubleType())
+                part_cols[f"__mn{j}"] = ColumnVector(mn, T.DoubleType())
+                part_cols[f"__mx{j}"] = ColumnVector(mx, T.DoubleType())
+            for name, cv in key_tables.columns.items():
+                part_cols["__key_" + name] = cv
+            pt = _shuffle_by_key(Table(part_cols, ukeys.numel(), t.device), ukeys)
+            k2 = pt.column("__k").data
+            vals2 = [pt.column("__rows").data]
+            for j in range(len(outs)):
+                vals2 += [pt.column(f"__s{j}").data, pt.column(f"__c{j}").data, pt.column(f"__mn{j}").data,
+                          pt.column(f"__mx{j}").data]
+            uk2, _, o2 = _hash_agg_all(k2, vals2, [None] * len(vals2), True)
+            ridx2 = torch.arange(pt.num_rows, dtype=torch.float64, device=t.device)
+            _, _, rep2 = _hash_agg_all(k2, [ridx2], [None], True)
+            rep_i = rep2[0][2].long()
+            ukeys = uk2
+            rows = o2[0][0]
+            outs = [(o2[1 + 4 * j][0], o2[2 + 4 * j][0], o2[3 + 4 * j][2], o2[4 + 4 * j][3]) for j in range(len(outs))]
+            key_tables = Table({name: pt.column("__key_" + name).take(rep_i) for name, _ in srcs}, ukeys.numel(),
+                               t.device)
+        cols = dict(key_tables.columns)
+        j = 0
+        for label, fn, src in aggs:
+            if src is None:
+                cols[label] = ColumnVector(rows.round().long(), T.LongType())
+                continue
+            s, c, mn, mx = outs[j]
+            srct = value_cols[j].dtype
+            j += 1
+            has = c > 0
+            if fn == "count":
+                cols[label] = ColumnVector(c.round().long(), T.LongType())
+            elif fn == "sum":
+                integral = isinstance(srct, (T.IntegerType, T.LongType, T.BooleanType))
+                cols[label] = ColumnVector(s.round().long() if integral else s, T.LongType() if integral else T.DoubleType(),
+                                           has.to(torch.uint8))
+            elif fn == "avg":
+                cols[label] = ColumnVector(s / c.clamp_min(1.0), T.DoubleType(), has.to(torch.uint8))
+            elif fn in ("min", "max"):
+                v = mn if fn == "min" else mx
+                if isinstance(srct, (T.IntegerType, T.LongType)):
+                    cols[label] = ColumnVector(torch.where(has, v, torch.zeros_like(v)).to(_TORCH_OF[type(srct)]), srct,
+                                               has.to(torch.uint8))
+                else:
+                    cols[label] = ColumnVector(v, T.DoubleType(), has.to(torch.uint8))
+            else:
+                raise ValueError(f"unsupported grouped aggregate {fn}")
+        return df._new(Table(cols, ukeys.numel(), t.device))
+
+    def _first_rows(self) -> DataFrame:
+        df = self.df
+        t = df._t
+        key, _ = _group_keys(df, self.cols)
+        if comm.world_size() > 1:
+            t = _shuffle_by_key(t, key)
+            df = df._new(t)
+            key, _ = _group_keys(df, self.cols)
+        ridx = torch.arange(t.num_rows, dtype=torch.float64, device=t.device)
+        _, _, rep = _hash_agg_all(key, [ridx], [None], True)
+        idx = torch.sort(rep[0][2].long()).values
+        return df._new(t.take(idx))
+
+
+def _num(cv: ColumnVector) -> torch.Tensor:
+    d = cv.data
+    if d.dtype == torch.bool:
+        return d.to(torch.uint8)
+    if isinstance(cv.dtype, T.StringType):
+        raise TypeError("cannot aggregate a string column numerically")
+    return d
+
+
+def _hash_agg_all(key, vals, valids, want_minmax):
+    """hash_agg with any number of value columns (chunks of 4 re-aligned by key order)."""
+    if len(vals) <= 4:
+        return D.hash_agg(key, vals, valids, want_minmax)
+    uk = rows = None
+    outs = []
+    for i in range(0, len(vals), 4):
+        k, r, o = D.hash_agg(key, vals[i:i + 4], valids[i:i + 4], want_minmax)
+        order = torch.argsort(k)
+        k, r = k[order], r[order]
+        o = [tuple(x[order] for x in q) for q in o]
+        if uk is None:
+            uk, rows = k, r
+        outs += o
+    return uk, rows, outs
