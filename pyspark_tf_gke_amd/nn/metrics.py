@@ -11,9 +11,12 @@ import torch
 
 class Metric:
     def __init__(self, name: str):
+        from ..distribute import current_strategy
+
         self.name = name
         self._total = None
         self._count = None
+        self._strategy = current_strategy()  # metrics created under strategy.scope() stay bound to it
 
     def _ensure(self, device):
         if self._total is None or self._total.device != torch.device(device):
@@ -32,11 +35,11 @@ class Metric:
 
     def result(self):
         if self._total is None:
-            return torch.tensor(0.0)
+            self._ensure("cpu" if self._strategy is None else self._strategy.device)
         from ..distribute import current_strategy
 
         t = torch.stack([self._total, self._count])
-        st = current_strategy()
+        st = self._strategy or current_strategy()
         if st is not None:
             t = st.all_reduce_sum(t)
         tot, cnt = t[0].item(), t[1].item()

@@ -21,6 +21,7 @@ import numpy as np
 import torch
 
 from ..ops import nn as K
+from ..runtime import fault as _fault
 from . import engine as E
 from . import layers as L
 from . import losses as LS
@@ -250,6 +251,7 @@ class Sequential:
             self.optimizer.apply(self.store)
 
     def train_step(self, xb, yb, stats=None) -> None:
+        _fault.maybe_fail()
         st = self._strategy()
         stats = self._stats_buf() if stats is None else stats
         self.store.zero_grad()
@@ -325,6 +327,7 @@ class Sequential:
                 cb.set_model(self)
             if hasattr(cb, "on_train_begin"):
                 cb.on_train_begin()
+            initial_epoch = max(initial_epoch, int(getattr(cb, "start_epoch", 0) or 0))
         persistent_it = None
         if steps_per_epoch is not None:
             persistent_it = self._iter_batches(x, y, batch_size, shuffle)

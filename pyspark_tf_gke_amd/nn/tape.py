@@ -86,7 +86,7 @@ def apply_gradients(optimizer, grads_and_vars) -> None:
     model = gv[0][1].model
     from ..distribute import current_strategy
 
-    st = current_strategy()
+    st = getattr(model, "strategy", None) or current_strategy()
     if st is not None:
         st.finish_gradients(model)
         st.apply_update(model, optimizer)

@@ -49,6 +49,9 @@ def init(backend: str | None = None, device_type: str | None = None, timeout_s: 
         kw["device_id"] = torch.device("cuda", local)
     dist.init_process_group(backend=backend, rank=rank, world_size=world,
                             timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    from ..runtime import heartbeat
+
+    heartbeat.start()
     return rank, world
 
 

@@ -1,0 +1,60 @@
+"""BASELINE config "raw-spark DataFrame groupBy-aggregate over 1B synthetic rows on 1 MI355X".
+
+The DataFrame is ``(key bigint, value double)`` with ``rows_per_gpu`` rows resident in HBM on every
+rank (weak scaling: 1B rows per GPU, 16 GB); keys are hash(row) % num_keys.  One timed step is the
+full ``df.groupBy("key").agg(sum("value"), count("*"))`` through the DataFrame API: rank-local
+radix-partitioned LDS aggregation -> hash shuffle of the partial aggregates over RCCL ->
+final merge.  rows/s = total rows aggregated per second over all GPUs.
+"""
+from __future__ import annotations
+
+import time
+
+import torch
+
+from ..parallel import comm
+
+
+def run(total_rows: int = 1_000_000_000, num_keys: int = 1_000_000, steps: int = 5, warmup: int = 1, device=None,
+        rows_per_gpu: int | None = None) -> dict:
+    from ..ops import df as D
+    from . import functions as F
+    from .dataframe import DataFrame
+    from .session import SparkSession
+    from .table import ColumnVector, Table
+    from . import types as T
+
+    world, rank = comm.world_size(), comm.rank()
+    n = rows_per_gpu or total_rows
+    spark = SparkSession.builder.master("mi355x").getOrCreate()
+    dev = spark.device if device is None else torch.device(device)
+    keys, vals = D.fill_synthetic_kv(n, num_keys, dev, offset=rank * n, seed=42)
+    df = DataFrame(Table({"key": ColumnVector(keys, T.LongType()), "value": ColumnVector(vals, T.DoubleType())}, n, dev),
+                   spark)
+
+    def step():
+        return df.groupBy("key").agg(F.sum("value").alias("s"), F.count("*").alias("c"))
+
+    out = None
+    for _ in range(warmup):
+        out = step()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    comm.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        out = step()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    comm.barrier()
+    dt = comm.all_reduce_max_scalar(time.perf_counter() - t0)
+    groups = out.count()
+    total_c = int(out._t.column("c").data.sum().item())
+    if world > 1:
+        total_c = int(sum(comm.all_gather_object(total_c)))
+    ok = total_c == n * world
+    return {"metric": "rows/sec Spark groupBy-aggregate", "value": round(n * world * steps / dt, 1), "unit": "rows/s",
+            "ms_per_step": round(dt / steps * 1e3, 3),
+            "config": {"model": "groupBy(key).agg(sum(value), count(*)) on (bigint key, double value)",
+                       "rows_per_gpu": n, "global_rows": n * world, "distinct_keys": num_keys, "groups_out": groups,
+                       "counts_check": ok, "parallelism": f"{world} executors (1 per GPU), RCCL all-to-all-v shuffle"}}

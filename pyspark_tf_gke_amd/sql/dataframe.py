@@ -616,18 +616,35 @@ def _key_of(cv: ColumnVector) -> torch.Tensor:
     return torch.where(null, torch.full_like(k, _NULL_KEY), k)
 
 
+def _decode_key(k: torch.Tensor, src: ColumnVector) -> ColumnVector:
+    """Inverse of :func:`_key_of`: group key -> key column value (so grouped outputs need no
+    representative-row lookup)."""
+    null = k == _NULL_KEY
+    valid = None if not bool(null.any()) else (~null).to(torch.uint8)
+    if isinstance(src.dtype, T.StringType):
+        return ColumnVector(torch.where(null, torch.full_like(k, -1), k).to(torch.int32), src.dtype, None,
+                            src.dictionary)
+    if src.data.dtype in (torch.float64, torch.float32):
+        v = torch.where(null, torch.zeros_like(k), k).view(torch.float64)
+        return ColumnVector(v.to(src.data.dtype), src.dtype, valid)
+    v = torch.where(null, torch.zeros_like(k), k)
+    return ColumnVector(v.to(src.data.dtype), src.dtype, valid)
+
+
 def _group_keys(df: "DataFrame", cols: list):
-    """-> (int64 combined key per row, [(name, ColumnVector source)]).  Multi-column keys are
-    combined through dense per-column codes (exact, no hash collisions)."""
+    """-> (int64 combined key per row, decode(keys) -> {name: ColumnVector}).  Multi-column keys
+    are combined through dense per-column codes (exact, no hash collisions)."""
     srcs = []
     for c in cols:
         name, cv = df._eval(c)
         srcs.append((name, cv))
     if not srcs:
-        return torch.zeros(df._t.num_rows, dtype=torch.int64, device=df._t.device), srcs
+        return torch.zeros(df._t.num_rows, dtype=torch.int64, device=df._t.device), lambda kk: {}
     if len(srcs) == 1:
-        return _key_of(srcs[0][1]), srcs
+        name, cv = srcs[0]
+        return _key_of(cv), lambda kk: {name: _decode_key(kk, cv)}
     combined = None
+    globs = []
     for _, cv in srcs:
         k = _key_of(cv)
         if comm.world_size() > 1:
@@ -636,12 +653,24 @@ def _group_keys(df: "DataFrame", cols: list):
             allk = comm.all_gather_object(uk.cpu().numpy())
             glob = torch.from_numpy(np.unique(np.concatenate(allk))).to(k.device)
             code = torch.searchsorted(glob, k)
-            card = glob.numel()
         else:
             glob, code = torch.unique(k, return_inverse=True)
-            card = glob.numel()
-        combined = code.long() if combined is None else combined * card + code.long()
-    return combined, srcs
+        globs.append(glob)
+        combined = code.long() if combined is None else combined * glob.numel() + code.long()
+
+    def decode(kk):
+        out = {}
+        rem = kk.clone()
+        codes = []
+        for g in reversed(globs):
+            codes.append(rem % g.numel())
+            rem = rem // g.numel()
+        codes.reverse()
+        for (name, cv), g, c in zip(srcs, globs, codes):
+            out[name] = _decode_key(g[c], cv)
+        return out
+
+    return combined, decode
 
 
 def _shuffle_by_key(t: Table, key: torch.Tensor) -> Table:
@@ -782,7 +811,7 @@ class GroupedData:
                 schema.append(T.StructField(label, dt))
             return sess.createDataFrame(data, T.StructType(schema), _local=True)
         # ---- keyed aggregation
-        key, srcs = _group_keys(df, self.cols)
+        key, decode = _group_keys(df, self.cols)
         value_cols = []
         for label, fn, src in aggs:
             if src is None:
@@ -790,42 +819,29 @@ class GroupedData:
             _, cv = df._eval(src)
             value_cols.append(cv)
         need_minmax = any(fn in ("min", "max") for _, fn, _ in aggs)
-        key_rep_idx = None
         # partial aggregation (rank-local)
         vdata = [_num(cv) for cv in value_cols]
         vvalid = [cv.valid_u8() for cv in value_cols]
         ukeys, rows, outs = _hash_agg_all(key, vdata, vvalid, need_minmax)
-        # representative row per group for the key columns (min row index via an index column)
-        ridx = torch.arange(t.num_rows, dtype=torch.float64, device=t.device)
-        _, _, rep = _hash_agg_all(key, [ridx], [None], True)
-        key_rep_idx = rep[0][2].long()  # min row index
-        key_tables = Table({name: cv.take(key_rep_idx) for name, cv in srcs}, ukeys.numel(), t.device)
         if world > 1:
-            # shuffle partials to the key owner and merge
-            part_cols = {f"__k": ColumnVector(ukeys, T.LongType()), "__rows": ColumnVector(rows, T.DoubleType())}
+            # shuffle partials to the key owner (RCCL all-to-all-v) and merge them
+            part_cols = {"__k": ColumnVector(ukeys, T.LongType()), "__rows": ColumnVector(rows, T.DoubleType())}
             for j, (s, c, mn, mx) in enumerate(outs):
                 part_cols[f"__s{j}"] = ColumnVector(s, T.DoubleType())
                 part_cols[f"__c{j}"] = ColumnVector(c, T.DoubleType())
                 part_cols[f"__mn{j}"] = ColumnVector(mn, T.DoubleType())
                 part_cols[f"__mx{j}"] = ColumnVector(mx, T.DoubleType())
-            for name, cv in key_tables.columns.items():
-                part_cols["__key_" + name] = cv
             pt = _shuffle_by_key(Table(part_cols, ukeys.numel(), t.device), ukeys)
             k2 = pt.column("__k").data
             vals2 = [pt.column("__rows").data]
             for j in range(len(outs)):
                 vals2 += [pt.column(f"__s{j}").data, pt.column(f"__c{j}").data, pt.column(f"__mn{j}").data,
                           pt.column(f"__mx{j}").data]
-            uk2, _, o2 = _hash_agg_all(k2, vals2, [None] * len(vals2), True)
-            ridx2 = torch.arange(pt.num_rows, dtype=torch.float64, device=t.device)
-            _, _, rep2 = _hash_agg_all(k2, [ridx2], [None], True)
-            rep_i = rep2[0][2].long()
+            uk2, _, o2 = _hash_agg_all(k2, vals2, [None] * len(vals2), need_minmax)
             ukeys = uk2
             rows = o2[0][0]
             outs = [(o2[1 + 4 * j][0], o2[2 + 4 * j][0], o2[3 + 4 * j][2], o2[4 + 4 * j][3]) for j in range(len(outs))]
-            key_tables = Table({name: pt.column("__key_" + name).take(rep_i) for name, _ in srcs}, ukeys.numel(),
-                               t.device)
-        cols = dict(key_tables.columns)
+        cols = dict(decode(ukeys))
         j = 0
         for label, fn, src in aggs:
             if src is None:
@@ -868,6 +884,35 @@ class GroupedData:
         return df._new(t.take(idx))
 
 
+_PART_WS: dict = {}
+
+
+def _partitioned_agg(key: torch.Tensor, val):
+    n = key.numel()
+    v = val if val is not None else torch.zeros(1, dtype=torch.float64, device=key.device).expand(n)
+    if val is None:
+        v = torch.zeros(n, dtype=torch.float64, device=key.device)
+    pbits = 12 if n >= (1 << 28) else 10
+    ok, osum, ocnt, m, (gk, gt, gcap), overflow = D.hash_agg_partitioned(key, v, pbits=pbits, ws=_PART_WS)
+    m = int(m.item())
+    keys, sums, cnts = ok[:m], osum[:m], ocnt[:m]
+    # rows that overflowed their partition's LDS table went to the global table
+    ek, erows, eo = D._extract(gk, gt, gcap, 1)
+    if ek.numel():
+        keys = torch.cat([keys, ek])
+        sums = torch.cat([sums, eo[0][0]])
+        cnts = torch.cat([cnts, erows])
+        k2, r2, o2 = D.hash_agg(keys, [sums, cnts], [None, None], False)
+        keys, sums, cnts = k2, o2[0][0], o2[1][0]
+    rows = cnts
+    outs = [(sums, cnts, sums, sums)] if val is not None else []
+    return keys, rows, outs
+
+
+def _unused():
+    return Table
+
+
 def _num(cv: ColumnVector) -> torch.Tensor:
     d = cv.data
     if d.dtype == torch.bool:
@@ -879,6 +924,14 @@ def _num(cv: ColumnVector) -> torch.Tensor:
 
 def _hash_agg_all(key, vals, valids, want_minmax):
     """hash_agg with any number of value columns (chunks of 4 re-aligned by key order)."""
+    n = key.numel()
+    if (key.is_cuda and n >= (1 << 23) and len(vals) <= 1 and not want_minmax
+            and all(v is None for v in valids)):
+        # large inputs: estimate the cardinality on a prefix; high-cardinality keys take the
+        # radix-partitioned LDS aggregation (one LDS table per partition, no global atomics)
+        sk, _, _ = D.hash_agg(key[: 1 << 20], [], [], False)
+        if sk.numel() > (1 << 15):
+            return _partitioned_agg(key, vals[0] if vals else None)
     if len(vals) <= 4:
         return D.hash_agg(key, vals, valids, want_minmax)
     uk = rows = None

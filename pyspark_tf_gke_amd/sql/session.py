@@ -85,6 +85,11 @@ class SparkSession:
             self._conf = {}
             self._app = "pyspark_tf_gke_amd"
             self._master = None
+            submitted = os.environ.get("PTG_SPARK_CONF")  # confs passed by cli.spark_submit
+            if submitted:
+                import json
+
+                self._conf.update(json.loads(submitted))
 
         def appName(self, name):  # noqa: N802
             self._app = name

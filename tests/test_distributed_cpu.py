@@ -1,0 +1,151 @@
+"""Multi-process correctness on the CPU with the gloo backend (2 ranks): the same code paths the
+8-GPU node runs over RCCL — MWMS gradient all-reduce, sharded parameter-server updates with the
+ClusterCoordinator, DataFrame shuffles (groupBy), distributed KMeans, launcher failure handling."""
+import json
+import os
+import subprocess
+import sys
+import textwrap
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run_ranks(body: str, nproc: int = 2, timeout: int = 300, extra_env=None):
+    script = textwrap.dedent(body)
+    env = dict(os.environ)
+    env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    env["PTG_DEVICE"] = "cpu"
+    env.update(extra_env or {})
+    cmd = [sys.executable, "-m", "pyspark_tf_gke_amd.runtime.launcher", "--nproc", str(nproc), "--",
+           sys.executable, "-c", script]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout, cwd=ROOT)
+    return r
+
+
+def _results(out: str):
+    res = {}
+    for line in out.splitlines():
+        if "RESULT " in line:
+            rank = int(line.split("]")[0].replace("[rank", ""))
+            res[rank] = json.loads(line.split("RESULT ", 1)[1])
+    return res
+
+
+def test_mirrored_matches_single_process_global_batch():
+    body = """
+    import json, torch, numpy as np
+    from pyspark_tf_gke_amd.distribute import MultiWorkerMirroredStrategy
+    from pyspark_tf_gke_amd.models import build_deep_model
+    st = MultiWorkerMirroredStrategy(device="cpu")
+    rng = np.random.default_rng(0)
+    X = rng.normal(size=(64, 3)).astype(np.float32); y = rng.integers(0, 5, 64).astype(np.int32)
+    with st.scope():
+        m = build_deep_model(3, 5, device="cpu")
+    half = 32 * st.rank
+    for _ in range(3):
+        m.train_on_batch(X[half:half+32], y[half:half+32])
+    ref = build_deep_model(3, 5, device="cpu")
+    for _ in range(3):
+        ref.store.zero_grad()
+        # single-process equivalent: mean of the two half-batch gradients
+        from pyspark_tf_gke_amd.nn import engine as E
+        gs = []
+        for h in (0, 32):
+            ref.store.zero_grad()
+            out = E.run_forward(ref.ops, torch.from_numpy(X[h:h+32]), ref.ws, True)
+            d = ref._loss_grad(out, torch.from_numpy(y[h:h+32]), torch.zeros(8))
+            E.run_backward(ref.ops, d, ref.ws)
+            gs.append(ref.store.flat_grad.clone())
+        ref.store.flat_grad.copy_(gs[0] + gs[1])
+        ref.optimizer.apply(ref.store, gscale=0.5)
+    diff = float((m.store.flat - ref.store.flat).abs().max())
+    print("RESULT", json.dumps({"diff": diff}), flush=True)
+    """
+    r = _run_ranks(body)
+    assert r.returncode == 0, r.stdout + r.stderr
+    res = _results(r.stdout)
+    assert len(res) == 2 and all(v["diff"] < 1e-5 for v in res.values()), res
+
+
+def test_parameter_server_coordinator_flow():
+    body = """
+    import json, numpy as np
+    from pyspark_tf_gke_amd import nn
+    from pyspark_tf_gke_amd.cli.train import make_parameter_server_strategy, _ps_loop
+    from pyspark_tf_gke_amd.data import Dataset
+    from pyspark_tf_gke_amd.models import build_deep_model
+    st = make_parameter_server_strategy(2, 1, chief_addr="127.0.0.1")
+    rng = np.random.default_rng(0)
+    X = rng.normal(size=(256, 3)).astype(np.float32); y = (X[:, 0] > 0).astype(np.int32)
+    def ds_fn(ctx=None):
+        ds = Dataset.from_tensor_slices((X, y))
+        if ctx is not None:
+            ds = ds.shard(ctx.num_input_pipelines, ctx.input_pipeline_id)
+        return ds.shuffle(100, seed=1).batch(16).repeat()
+    with st.scope():
+        m = build_deep_model(3, 2, device="cpu")
+        opt = nn.optimizers.Adam(1e-2)
+        metrics = [nn.metrics.Mean("loss"), nn.metrics.SparseCategoricalAccuracy("accuracy")]
+    h = _ps_loop(m, st, ds_fn, 7, 3, nn.losses.SparseCategoricalCrossentropy(), opt, metrics, lambda e, v: str(v))
+    print("RESULT", json.dumps({"acc": h["accuracy"], "loss": h["loss"], "sum": float(m.store.flat.sum())}), flush=True)
+    """
+    r = _run_ranks(body)
+    assert r.returncode == 0, r.stdout + r.stderr
+    res = _results(r.stdout)
+    assert len(res) == 2
+    assert res[0]["sum"] == res[1]["sum"]  # parameters identical on every rank after all-gather
+    assert res[0]["loss"] == res[1]["loss"]  # metrics all-reduced
+    assert res[0]["loss"][-1] < res[0]["loss"][0]
+
+
+def test_distributed_dataframe_groupby_and_kmeans():
+    body = """
+    import json, os
+    from pyspark_tf_gke_amd.sql import SparkSession
+    from pyspark_tf_gke_amd.sql.functions import avg, count, col
+    from pyspark_tf_gke_amd.ml import KMeans, VectorAssembler
+    s = SparkSession.builder.master("spark://127.0.0.1:7077").getOrCreate()
+    df = s.read.csv(os.path.join("tests", "data", "health.csv"), header=True, inferSchema=True)
+    n = df.count()
+    g = {r["measure_name"]: (r["n"], r["m"]) for r in df.groupBy("measure_name").agg(count("*").alias("n"), avg("value").alias("m")).collect()}
+    f = df.na.fill(0)
+    X = VectorAssembler(inputCols=["value", "lower_ci", "upper_ci"], outputCol="features").transform(f)
+    km = KMeans(k=3, seed=1, maxIter=20).fit(X)
+    top = [r["measure_name"] for r in df.groupBy("measure_name").count().orderBy(col("count").desc(), "measure_name").limit(3).collect()]
+    print("RESULT", json.dumps({"n": n, "groups": len(g), "ab": g["Able-Bodied"], "cost": km.summary.trainingCost, "top": top}), flush=True)
+    """
+    r = _run_ranks(body)
+    assert r.returncode == 0, r.stdout + r.stderr
+    res = _results(r.stdout)
+    import pandas as pd
+
+    pdf = pd.read_csv(os.path.join(ROOT, "tests", "data", "health.csv"))
+    ref = pdf.groupby("measure_name")["value"].agg(["size", "mean"])
+    for v in res.values():
+        assert v["n"] == 18155 and v["groups"] == 30
+        assert v["ab"][0] == ref.loc["Able-Bodied", "size"]
+        assert abs(v["ab"][1] - ref.loc["Able-Bodied", "mean"]) < 1e-6 * ref.loc["Able-Bodied", "mean"]
+    assert res[0]["cost"] == res[1]["cost"] and res[0]["top"] == res[1]["top"]
+
+
+def test_launcher_fails_fast_and_restarts():
+    body = """
+    import os, sys, time
+    from pyspark_tf_gke_amd.parallel import comm
+    comm.init()
+    if os.environ["RANK"] == "1" and os.environ.get("PTG_RESTART_COUNT") == "0":
+        sys.exit(3)
+    comm.barrier()
+    print("RESULT {\\"ok\\": 1}", flush=True)
+    """
+    r = _run_ranks(body, timeout=120)
+    assert r.returncode == 3 and "stopping the other ranks" in r.stderr
+    env = dict(os.environ)
+    env["PYTHONPATH"] = ROOT
+    cmd = [sys.executable, "-m", "pyspark_tf_gke_amd.runtime.launcher", "--nproc", "2", "--max-restarts", "1", "--",
+           sys.executable, "-c", textwrap.dedent(body)]
+    r2 = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=180, cwd=ROOT)
+    assert r2.returncode == 0, r2.stderr
+    assert len(_results(r2.stdout)) == 2

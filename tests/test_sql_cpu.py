@@ -1,0 +1,115 @@
+"""DataFrame API semantics on the host executor (local[N])."""
+import math
+import os
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from pyspark_tf_gke_amd.sql import Row, SparkSession
+from pyspark_tf_gke_amd.sql.functions import avg, col, count, isnan, lit, max as fmax, sum as fsum, when
+
+HEALTH = os.path.join(os.path.dirname(__file__), "data", "health.csv")
+
+
+@pytest.fixture(scope="module")
+def spark():
+    s = SparkSession.builder.appName("t").master("local[2]").config("spark.sql.shuffle.partitions", "2").getOrCreate()
+    yield s
+    s.stop()
+
+
+def test_installation_check_flow(spark, capsys):
+    """spark_installation_check.py:27-37 — createDataFrame, show, filter Age > 30."""
+    df = spark.createDataFrame([("Alice", 34), ("Bob", 45), ("Charlie", 29)], ["Name", "Age"])
+    df.show()
+    out = capsys.readouterr().out
+    assert "|  Alice| 34|" in out
+    assert [r.Name for r in df.filter(df.Age > 30).collect()] == ["Alice", "Bob"]
+    assert df.filter("Age > 30").count() == 2
+    assert spark.sparkContext.applicationId.startswith("app-")
+
+
+def test_csv_infer_schema_matches_pandas(spark):
+    df = spark.read.csv(HEALTH, header=True, inferSchema=True)
+    pdf = pd.read_csv(HEALTH)
+    assert df.count() == len(pdf) == 18155
+    assert df.columns == list(pdf.columns)
+    types = dict(df.dtypes)
+    assert types["measure_name"] == "string" and types["edition"] == "int"
+    assert types["value"] in ("int", "double")
+    # quoted commas in `source` survive tokenization
+    src = [r["source"] for r in df.select("source").limit(50).collect()]
+    assert src == list(pdf["source"].iloc[:50])
+    v = df.select("value").filter(~isnan(col("value")) & col("value").isNotNull()).agg({"value": "avg"}).collect()[0][0]
+    assert abs(v - pdf["value"].mean()) < 1e-6 * abs(v)
+
+
+def test_null_handling_and_when(spark):
+    df = spark.createDataFrame([(1, 2.0), (2, None), (3, float("nan")), (None, 4.0)], ["a", "b"])
+    assert df.filter(col("b").isNull()).count() == 1
+    assert df.filter(isnan(col("b"))).count() == 1
+    f = df.withColumn("b", when(col("b").isNull() | isnan(col("b")), 9.0).otherwise(col("b")))
+    assert [r.b for r in f.collect()] == [2.0, 9.0, 9.0, 4.0]
+    g = df.withColumn("c", col("a") * 2 + 1)
+    assert [r.c for r in g.collect()] == [3, 5, 7, None]
+    h = df.withColumn("d", col("a") / lit(0))
+    assert all(r.d is None for r in h.collect())
+
+
+def test_groupby_agg_vs_pandas(spark):
+    df = spark.read.csv(HEALTH, header=True, inferSchema=True)
+    g = df.groupBy("measure_name").agg(count("*").alias("n"), avg("value").alias("m"), fmax("upper_ci").alias("mx"))
+    got = {r["measure_name"]: (r["n"], r["m"], r["mx"]) for r in g.collect()}
+    pdf = pd.read_csv(HEALTH)
+    ref = pdf.groupby("measure_name").agg(n=("value", "size"), m=("value", "mean"), mx=("upper_ci", "max"))
+    assert len(got) == len(ref) == 30
+    for k, row in ref.iterrows():
+        n, m, mx = got[k]
+        assert n == row.n
+        assert (m is None and math.isnan(row.m)) or abs(m - row.m) < 1e-6 * max(1, abs(row.m))
+        assert (mx is None and math.isnan(row.mx)) or mx == row.mx
+
+
+def test_multi_key_groupby_orderby_distinct(spark):
+    df = spark.createDataFrame([("a", 1, 1.0), ("a", 1, 2.0), ("b", 2, 3.0), ("a", 2, 4.0)], ["k", "j", "v"])
+    g = df.groupBy("k", "j").agg(fsum("v").alias("s")).orderBy("k", "j").collect()
+    assert [(r.k, r.j, r.s) for r in g] == [("a", 1, 3.0), ("a", 2, 4.0), ("b", 2, 3.0)]
+    assert df.select("k").distinct().count() == 2
+    top = df.orderBy(col("v").desc()).first()
+    assert top.v == 4.0
+    assert df.groupBy("k").count().orderBy("k").collect()[0]["count"] == 3
+
+
+def test_parquet_roundtrip(spark, tmp_path):
+    df = spark.createDataFrame([("x", 1, 0.5), ("y", None, 1.5)], ["s", "i", "d"])
+    p = str(tmp_path / "out.parquet")
+    df.write.mode("overwrite").parquet(p)
+    assert os.path.exists(os.path.join(p, "_SUCCESS"))
+    back = spark.read.parquet(p)
+    assert sorted(map(tuple, back.collect()), key=str) == sorted([("x", 1, 0.5), ("y", None, 1.5)], key=str)
+
+
+def test_rdd_and_dataframe_wordcount(spark, tmp_path):
+    p = tmp_path / "t.txt"
+    p.write_text("a b a\nc a b\n\nd\n")
+    sc = spark.sparkContext
+    rdd = sc.textFile(str(p)).flatMap(lambda l: l.split()).map(lambda w: (w, 1)).reduceByKey(lambda a, b: a + b)
+    assert dict(rdd.collect()) == {"a": 3, "b": 2, "c": 1, "d": 1}
+    from pyspark_tf_gke_amd.sql.functions import explode, split
+
+    words = spark.read.text(str(p)).select(explode(split(col("value"), r"\s+")).alias("word")).filter(col("word") != "")
+    wc = {r.word: r["count"] for r in words.groupBy("word").count().collect()}
+    assert wc == {"a": 3, "b": 2, "c": 1, "d": 1}
+    from pyspark_tf_gke_amd.sql.rdd import word_count_native
+
+    assert dict(word_count_native(p.read_bytes(), 2)) == {"a": 3, "b": 2, "c": 1, "d": 1}
+
+
+def test_row_and_describe(spark):
+    r = Row(name="x", v=1)
+    assert r.name == "x" and r["v"] == 1 and r.asDict() == {"name": "x", "v": 1}
+    df = spark.createDataFrame([(1.0,), (3.0,)], ["v"])
+    d = {row["summary"]: row["v"] for row in df.describe().collect()}
+    assert float(d["mean"]) == 2.0 and d["count"] == "2"
+    _ = np
