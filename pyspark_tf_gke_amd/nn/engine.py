@@ -91,16 +91,34 @@ class ConvOp(Op):
         xi[..., : x.shape[-1]] = x
         return xi
 
+    def _halo(self):
+        """(fwd/wgrad eligible, dgrad eligible) for the halo-tiled direct-conv kernels."""
+        H, W, _ = self.conv.in_shape
+        OH, OW, Co = self.conv.out_shape
+        KS = self.conv.kernel_size[0]
+        same = (OH, OW) == (H, W) and self.conv.kernel_size[0] == self.conv.kernel_size[1] and self.pad == KS // 2
+        fwd = K.halo_eligible(self.conv.cin_p, Co, KS, self.stride, same)
+        dgrad = K.halo_eligible(Co, self.conv.cin_p, KS, self.stride, same)
+        return fwd, dgrad
+
+    def _alpha_const(self, ws, value, dev):
+        key = self.name + ("/ones" if value else "/zeros")
+        t = ws.get(key, self.conv.out_shape, torch.float32, dev)
+        t.fill_(value)
+        return t
+
     def forward(self, x, ws, training):
         x = self._prep_input(x, ws)
         B = x.shape[0]
         OH, OW, Co = self.conv.out_shape
         dev = x.device
         z = ws.get(self.name + "/z", (B, OH, OW, Co), torch.bfloat16, dev)
-        act = "relu" if self.conv.activation == "relu" else None
         b = self.conv.bias.data if self.conv.bias is not None else None
-        K.conv2d_fwd(x, self.conv.kernel.bf16, b, self.stride, self.pad, z, act)
         self._x, self._z = x, z
+        if self._halo()[0] and not (self.pool is not None and (OH % 2 or OW % 2)):
+            return self._forward_halo(x, z, b, ws, B, OH, OW, Co, dev)
+        act = "relu" if self.conv.activation == "relu" else None
+        K.conv2d_fwd(x, self.conv.kernel.bf16, b, self.stride, self.pad, z, act)
         if self.prelu is not None and self.pool is not None:
             p = ws.get(self.name + "/p", (B, OH // 2, OW // 2, Co), torch.bfloat16, dev)
             return K.prelu_pool_fwd(z, self.prelu.alpha.data, p)
@@ -113,6 +131,25 @@ class ConvOp(Op):
             p = ws.get(self.name + "/p", (B, OH // 2, OW // 2, Co), torch.bfloat16, dev)
             return K.prelu_pool_fwd(z, ones, p)
         return z
+
+    def _forward_halo(self, x, z, b, ws, B, OH, OW, Co, dev):
+        """One kernel: conv + bias, and the PReLU/ReLU (+ 2x2 max-pool) epilogue fused in."""
+        w = self.conv.kernel.bf16
+        if self.prelu is not None:
+            alpha = self.prelu.alpha.data
+        elif self.conv.activation == "relu":
+            alpha = self._alpha_const(ws, 0.0, dev)  # ReLU == PReLU with alpha 0
+        elif self.pool is not None:
+            alpha = self._alpha_const(ws, 1.0, dev)  # identity
+        else:
+            return K.conv2d_fwd_fused(x, w, b, self.pad, z)
+        if self.pool is not None:
+            p = ws.get(self.name + "/p", (B, OH // 2, OW // 2, Co), torch.bfloat16, dev)
+            K.conv2d_fwd_fused(x, w, b, self.pad, z, alpha, p, "pool")
+            return p
+        a = ws.get(self.name + "/a", (B, OH, OW, Co), torch.bfloat16, dev)
+        K.conv2d_fwd_fused(x, w, b, self.pad, z, alpha, a, "prelu")
+        return a
 
     def backward(self, dy, ws):
         z, x = self._z, self._x
@@ -136,13 +173,22 @@ class ConvOp(Op):
         else:
             dz = dy
             K.col_sum(dz.reshape(-1, dz.shape[-1]), bias_g)
-        K.conv2d_wgrad(x, dz, self.stride, self.pad, self.conv.kernel.grad)
+        halo_fwd, halo_dgrad = self._halo()
+        if halo_fwd:
+            K.conv2d_wgrad_halo(x, dz, self.pad, self.conv.kernel.grad)
+        else:
+            K.conv2d_wgrad(x, dz, self.stride, self.pad, self.conv.kernel.grad)
         if self.first:
             return None
         if self.stride != 1:
             raise NotImplementedError("dgrad for strided convolutions")
         dx = ws.get(self.name + "/dx", x.shape, torch.bfloat16, dev)
-        K.conv2d_dgrad(dz, self.conv.kernel.bf16, self.pad, dx)
+        if halo_dgrad:
+            KS, Co = self.conv.kernel_size[0], z.shape[-1]
+            wf = ws.get(self.name + "/wflip", (self.conv.cin_p, KS, KS, Co), torch.bfloat16, dev)
+            K.conv2d_dgrad_halo(dz, self.conv.kernel.bf16, self.pad, dx, wf)
+        else:
+            K.conv2d_dgrad(dz, self.conv.kernel.bf16, self.pad, dx)
         return dx
 
 

@@ -68,6 +68,66 @@ def conv2d_wgrad(x, dz, stride: int, pad: int, out, accumulate: bool = False, sp
     return out
 
 
+HALO_C = (4, 8, 16, 32, 64)
+
+
+def halo_eligible(C: int, Cout: int, KS: int, stride: int, same: bool) -> bool:
+    """Shapes served by the halo-tiled direct-conv kernels (csrc/kernels/conv.hip)."""
+    return same and stride == 1 and KS in (3, 5) and C in HALO_C and Cout % 8 == 0 and Cout <= 64
+
+
+EPI = {None: 0, "pool": 1, "prelu": 2}
+
+
+def conv2d_fwd_fused(x, w, bias, pad: int, z_out, alpha=None, aux_out=None, epi=None):
+    """Halo-tiled 'same' conv: z = conv(x, w) + bias; epi='pool' also writes
+    aux = maxpool2x2(prelu(z, alpha)); epi='prelu' writes aux = prelu(z, alpha)."""
+    if not on_device(x):
+        ref.conv2d_fwd(x, w, bias, 1, pad, z_out, None)
+        if epi == "pool":
+            ref.prelu_pool_fwd(z_out, alpha, aux_out)
+        elif epi == "prelu":
+            ref.prelu_fwd(z_out, alpha, aux_out)
+        return z_out
+    N, H, W, C = x.shape
+    Cout, KS, _, Cw = w.shape
+    assert Cw == C and tuple(z_out.shape) == (N, H, W, Cout)
+    need(x, torch.bfloat16, "conv_halo.x"); need(w, torch.bfloat16, "conv_halo.w")
+    hip("ptg_conv2d_fwd_halo", ptr(x), ptr(w), ptr(bias), ptr(alpha), ptr(z_out), ptr(aux_out), N, H, W, C, Cout, KS,
+        pad, EPI[epi])
+    return z_out
+
+
+def conv2d_wgrad_halo(x, dz, pad: int, out):
+    """out[Cout,KS,KS,C] (fp32) = d(conv)/dw for a stride-1 'same' conv (halo-tiled MFMA)."""
+    if not on_device(x):
+        return ref.conv2d_wgrad(x, dz, 1, pad, out, False)
+    N, H, W, C = x.shape
+    Cout, KS, _, _ = out.shape
+    out.zero_()
+    hip("ptg_conv2d_wgrad_halo", ptr(x), ptr(dz), ptr(out), N, H, W, C, Cout, KS, pad)
+    return out
+
+
+def conv_flip_weights(w, out):
+    """out[Cin][KS][KS][Cout] = w[Cout][KS-1-kh][KS-1-kw][Cin] (dgrad filter)."""
+    Cout, KS, _, Cin = w.shape
+    if not on_device(w):
+        out.copy_(torch.flip(w, dims=(1, 2)).permute(3, 1, 2, 0))
+        return out
+    hip("ptg_conv_flip_weights", ptr(w), ptr(out), Cout, KS, Cin)
+    return out
+
+
+def conv2d_dgrad_halo(dz, w, pad: int, out, wflip_buf):
+    """dx = d(conv)/dx (stride-1 'same') via the halo fwd kernel on flipped weights."""
+    if not on_device(dz):
+        return ref.conv2d_dgrad(dz, w, pad, out)
+    conv_flip_weights(w, wflip_buf)
+    KS = w.shape[1]
+    return conv2d_fwd_fused(dz, wflip_buf, None, KS - 1 - pad, out)
+
+
 # ----------------------------------------------------------------------------------------------
 # Dense (MFMA GEMM)
 # ----------------------------------------------------------------------------------------------

@@ -119,6 +119,62 @@ def test_conv_wgrad_large_splitk():
     _close(out, ref, 1e-3, 1e-3, "wgrad_big")
 
 
+HALO_CASES = [(2, 16, 20, 4, 8, 5), (2, 18, 22, 8, 16, 5), (2, 12, 10, 16, 32, 5), (3, 8, 10, 32, 64, 5),
+              (2, 8, 8, 64, 64, 5), (2, 10, 14, 64, 24, 3), (2, 6, 70, 4, 8, 3), (1, 64, 80, 16, 32, 5),
+              (2, 256, 320, 4, 8, 5), (2, 9, 7, 16, 64, 3)]
+
+
+@pytest.mark.parametrize("N,H,W,C,Co,KS", HALO_CASES)
+@pytest.mark.parametrize("epi", [None, "pool", "prelu"])
+def test_conv_halo_fwd(N, H, W, C, Co, KS, epi):
+    if epi == "pool" and (H % 2 or W % 2):
+        pytest.skip("fused pool epilogue needs even H, W (engine falls back)")
+    x, w, b = rnd(N, H, W, C), rnd(Co, KS, KS, C, scale=0.2), torch.randn(Co)
+    alpha = torch.rand(H, W, Co) * 0.5
+    pad = KS // 2
+    z = torch.empty(N, H, W, Co, device=DEV, dtype=torch.bfloat16)
+    aux = None
+    if epi == "pool":
+        aux = torch.empty(N, H // 2, W // 2, Co, device=DEV, dtype=torch.bfloat16)
+    elif epi == "prelu":
+        aux = torch.empty(N, H, W, Co, device=DEV, dtype=torch.bfloat16)
+    K.conv2d_fwd_fused(x.to(DEV), w.to(DEV), b.to(DEV), pad, z, alpha.to(DEV), aux, epi)
+    zr = torch.empty(N, H, W, Co, dtype=torch.bfloat16)
+    R.conv2d_fwd(x, w, b, 1, pad, zr)
+    _close(z, zr, 2e-2, 2e-2, "halo_z")
+    if epi == "pool":
+        pr = torch.empty(N, H // 2, W // 2, Co, dtype=torch.bfloat16)
+        R.prelu_pool_fwd(zr, alpha, pr)
+        _close(aux, pr, 2e-2, 2e-2, "halo_pool")
+    elif epi == "prelu":
+        ar = torch.empty(N, H, W, Co, dtype=torch.bfloat16)
+        R.prelu_fwd(zr, alpha, ar)
+        _close(aux, ar, 2e-2, 2e-2, "halo_prelu")
+
+
+@pytest.mark.parametrize("N,H,W,C,Co,KS", HALO_CASES)
+def test_conv_halo_wgrad(N, H, W, C, Co, KS):
+    x, dz = rnd(N, H, W, C), rnd(N, H, W, Co, scale=0.1)
+    pad = KS // 2
+    out = torch.empty(Co, KS, KS, C, device=DEV)
+    K.conv2d_wgrad_halo(x.to(DEV), dz.to(DEV), pad, out)
+    ref = torch.empty(Co, KS, KS, C)
+    R.conv2d_wgrad(x, dz, 1, pad, ref)
+    _close(out, ref, 1e-3, 1e-3, "halo_wgrad")
+
+
+@pytest.mark.parametrize("N,H,W,C,Co,KS", [c for c in HALO_CASES if c[4] in K.HALO_C and c[3] % 8 == 0])
+def test_conv_halo_dgrad(N, H, W, C, Co, KS):
+    dz, w = rnd(N, H, W, Co), rnd(Co, KS, KS, C, scale=0.2)
+    pad = KS // 2
+    out = torch.empty(N, H, W, C, device=DEV, dtype=torch.bfloat16)
+    wf = torch.empty(C, KS, KS, Co, device=DEV, dtype=torch.bfloat16)
+    K.conv2d_dgrad_halo(dz.to(DEV), w.to(DEV), pad, out, wf)
+    ref = torch.empty(N, H, W, C, dtype=torch.bfloat16)
+    R.conv2d_dgrad(dz, w, pad, ref)
+    _close(out, ref, 2e-2, 2e-2, "halo_dgrad")
+
+
 @pytest.mark.parametrize("C", [8, 16, 64, 128])
 def test_prelu_pool_fwd_bwd(C):
     N, H, W = 3, 8, 12
