@@ -48,7 +48,35 @@ __global__ __launch_bounds__(256) void prelu_pool_fwd_k(const bf16_t* __restrict
   }
 }
 
-// Backward of prelu+pool. Grid: x over pooled (ph, pw, c8) vectors, y over batch chunks.
+// Per-channel reduction of db[8] (channels c8*8..+7) over a 256-thread block whose threads hold
+// channel group (tid % C8): xor-shuffles over the lanes that share a channel group (strides >= C8),
+// then one LDS slot per (wave, channel) and one global atomic per channel per block.
+PTG_DEV void bias_reduce_atomic(float db[8], int c8, int C8, float* sred, float* dbias) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, C = C8 * 8;
+  if (C8 & (C8 - 1)) {  // channel groups not a power of two: LDS atomics
+    if ((int)threadIdx.x < C) sred[threadIdx.x] = 0.f;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) atomicAdd(&sred[c8 * 8 + j], db[j]);
+    __syncthreads();
+    if ((int)threadIdx.x < C) atomicAdd(dbias + threadIdx.x, sred[threadIdx.x]);
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    for (int o = 32; o >= C8; o >>= 1) db[j] += __shfl_xor(db[j], o, 64);
+  if (lane < C8) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sred[wid * 256 + lane * 8 + j] = db[j];
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < C)
+    atomicAdd(dbias + threadIdx.x,
+              sred[threadIdx.x] + sred[256 + threadIdx.x] + sred[512 + threadIdx.x] + sred[768 + threadIdx.x]);
+}
+
+// Backward of prelu+pool. Grid: x over pooled (ph, pw, c8) vectors, y over batch chunks; samples
+// are processed two at a time so 10 independent 16-byte loads are in flight per lane.
 // dz is written for every element (zero where not the window's first argmax).
 // dalpha[h][w][c] += sum_n dA * min(z,0)  (dA = routed pooled gradient), dbias[c] += sum dz.
 __global__ __launch_bounds__(256) void prelu_pool_bwd_k(const bf16_t* __restrict__ dp,
@@ -57,92 +85,110 @@ __global__ __launch_bounds__(256) void prelu_pool_bwd_k(const bf16_t* __restrict
                                                         bf16_t* __restrict__ dz, float* __restrict__ dalpha,
                                                         float* __restrict__ dbias, int N, int H, int W,
                                                         int C, int nper) {
-  __shared__ float sbias[256];
+  __shared__ float sred[4 * 256];
+  __shared__ float sda[256 * 32];
   const int PH = H >> 1, PW = W >> 1, C8 = C >> 3;
   const int npos = PH * PW * C8;
   const int i = blockIdx.x * 256 + threadIdx.x;
-  sbias[threadIdx.x] = 0.f;
-  __syncthreads();
   const int n0 = blockIdx.y * nper, n1 = min(N, n0 + nper);
-  if (i < npos) {
-    const int c8 = i % C8;
-    const int t = i / C8;
-    const int pw = t % PW, ph = t / PW;
-    float da[4][8], db[8];
-    float av[4][8];
+  float db[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const bool active = i < npos;
+  const int c8 = active ? i % C8 : 0;
+  const int t = active ? i / C8 : 0;
+  const int pw = t % PW, ph = t / PW;
+  long zoff[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) zoff[q] = ((long)(2 * ph + (q >> 1)) * W + 2 * pw + (q & 1)) * C + c8 * 8;
+  const long HWC = (long)H * W * C, PHWC = (long)PH * PW * C;
+  const long poff = ((long)ph * PW + pw) * C + c8 * 8;
+  if (active) {
+    float da[4][8], av[4][8];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int h = 2 * ph + (q >> 1), w = 2 * pw + (q & 1);
-      const long aoff = ((long)h * W + w) * C + c8 * 8;
-      const float4 a0 = *(const float4*)(alpha + aoff), a1 = *(const float4*)(alpha + aoff + 4);
+      const float4 a0 = *(const float4*)(alpha + zoff[q]), a1 = *(const float4*)(alpha + zoff[q] + 4);
       av[q][0] = a0.x; av[q][1] = a0.y; av[q][2] = a0.z; av[q][3] = a0.w;
       av[q][4] = a1.x; av[q][5] = a1.y; av[q][6] = a1.z; av[q][7] = a1.w;
 #pragma unroll
       for (int j = 0; j < 8; ++j) da[q][j] = 0.f;
     }
+    const bool lastw = (W & 1) && pw == PW - 1, lasth = (H & 1) && ph == PH - 1;
+    for (int n = n0; n < n1; n += 2) {
+      const bool two = n + 1 < n1;
+      U4 graw[2], zraw[2][4];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) db[j] = 0.f;
-    for (int n = n0; n < n1; ++n) {
-      float g[8];
-      unpack8(*(const U4*)(dp + (((long)n * PH + ph) * PW + pw) * C + c8 * 8), g);
-      float zv[4][8], y[4][8];
+      for (int u = 0; u < 2; ++u) {
+        const int nn = (u == 0 || two) ? n + u : n;
+        graw[u] = *(const U4*)(dp + nn * PHWC + poff);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int h = 2 * ph + (q >> 1), w = 2 * pw + (q & 1);
-        unpack8(*(const U4*)(z + (((long)n * H + h) * W + w) * C + c8 * 8), zv[q]);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) y[q][j] = zv[q][j] > 0.f ? zv[q][j] : av[q][j] * zv[q][j];
-      }
-      int arg[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        int a = 0; float b = y[0][j];
-#pragma unroll
-        for (int q = 1; q < 4; ++q)
-          if (y[q][j] > b) { b = y[q][j]; a = q; }
-        arg[j] = a;
+        for (int q = 0; q < 4; ++q) zraw[u][q] = *(const U4*)(z + nn * HWC + zoff[q]);
       }
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int h = 2 * ph + (q >> 1), w = 2 * pw + (q & 1);
-        float o[8];
+      for (int u = 0; u < 2; ++u) {
+        if (u == 1 && !two) break;
+        const long nb = (long)(n + u) * HWC;
+        float g[8], zv[4][8], y[4][8];
+        unpack8(graw[u], g);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          unpack8(zraw[u][q], zv[q]);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) y[q][j] = zv[q][j] > 0.f ? zv[q][j] : av[q][j] * zv[q][j];
+        }
+        int arg[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float gq = (arg[j] == q) ? g[j] : 0.f;
-          const float zz = zv[q][j];
-          o[j] = zz > 0.f ? gq : gq * av[q][j];
-          da[q][j] += zz > 0.f ? 0.f : gq * zz;
-          db[j] += o[j];
+          int a = 0; float b = y[0][j];
+#pragma unroll
+          for (int q = 1; q < 4; ++q)
+            if (y[q][j] > b) { b = y[q][j]; a = q; }
+          arg[j] = a;
         }
-        *(U4*)(dz + (((long)n * H + h) * W + w) * C + c8 * 8) = pack8(o);
-      }
-      // odd H/W (floor pooling): the last row/column belongs to no window -> zero gradient
-      const bool lastw = (W & 1) && pw == PW - 1, lasth = (H & 1) && ph == PH - 1;
-      if (lastw || lasth) {
-        const U4 zz = zero4();
-        if (lastw) {
-          *(U4*)(dz + (((long)n * H + 2 * ph) * W + W - 1) * C + c8 * 8) = zz;
-          *(U4*)(dz + (((long)n * H + 2 * ph + 1) * W + W - 1) * C + c8 * 8) = zz;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float o[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float gq = (arg[j] == q) ? g[j] : 0.f;
+            const float zz = zv[q][j];
+            o[j] = zz > 0.f ? gq : gq * av[q][j];
+            da[q][j] += zz > 0.f ? 0.f : gq * zz;
+            db[j] += o[j];
+          }
+          *(U4*)(dz + nb + zoff[q]) = pack8(o);
         }
-        if (lasth) {
-          *(U4*)(dz + (((long)n * H + H - 1) * W + 2 * pw) * C + c8 * 8) = zz;
-          *(U4*)(dz + (((long)n * H + H - 1) * W + 2 * pw + 1) * C + c8 * 8) = zz;
+        // odd H/W (floor pooling): the last row/column belongs to no window -> zero gradient
+        if (lastw || lasth) {
+          const U4 zz = zero4();
+          bf16_t* d = dz + nb + c8 * 8;
+          if (lastw) {
+            *(U4*)(d + ((long)(2 * ph) * W + W - 1) * C) = zz;
+            *(U4*)(d + ((long)(2 * ph + 1) * W + W - 1) * C) = zz;
+          }
+          if (lasth) {
+            *(U4*)(d + ((long)(H - 1) * W + 2 * pw) * C) = zz;
+            *(U4*)(d + ((long)(H - 1) * W + 2 * pw + 1) * C) = zz;
+          }
+          if (lastw && lasth) *(U4*)(d + ((long)(H - 1) * W + W - 1) * C) = zz;
         }
-        if (lastw && lasth) *(U4*)(dz + (((long)n * H + H - 1) * W + W - 1) * C + c8 * 8) = zz;
       }
     }
+    // stage in LDS ordered (qh, thread, qw, j) ~ global order, so each atomic wave-instruction
+    // below covers ~256 contiguous bytes instead of 64 scattered 32-byte runs
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int h = 2 * ph + (q >> 1), w = 2 * pw + (q & 1);
-      const long aoff = ((long)h * W + w) * C + c8 * 8;
+    for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) atomicAdd(dalpha + aoff + j, da[q][j]);
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) atomicAdd(&sbias[c8 * 8 + j], db[j]);
+      for (int j = 0; j < 8; ++j) sda[(((q >> 1) * 256 + threadIdx.x) * 2 + (q & 1)) * 8 + j] = da[q][j];
   }
   __syncthreads();
-  if (threadIdx.x < C) atomicAdd(dbias + threadIdx.x, sbias[threadIdx.x]);
+  for (int k = 0; k < 32; ++k) {
+    const int L = k * 256 + threadIdx.x;
+    const int j = L & 7, qw = (L >> 3) & 1, tt = (L >> 4) & 255, qh = L >> 12;
+    const int ii = blockIdx.x * 256 + tt;
+    if (ii >= npos) continue;
+    const int cc = ii % C8, tq = ii / C8, pww = tq % PW, phh = tq / PW;
+    atomicAdd(dalpha + ((long)(2 * phh + qh) * W + 2 * pww + qw) * C + cc * 8 + j, sda[L]);
+  }
+  bias_reduce_atomic(db, c8, C8, sred, dbias);
 }
 
 // Plain PReLU forward (no pool): a = z>0 ? z : alpha[hwc]*z ; HWC = per-sample element count.
@@ -161,46 +207,57 @@ __global__ __launch_bounds__(256) void prelu_fwd_k(const bf16_t* __restrict__ z,
   }
 }
 
-// PReLU backward (no pool). Grid x over per-sample 8-vectors, y over batch chunks.
+// PReLU backward (no pool). Grid x over per-sample 8-vectors, y over batch chunks (two samples
+// in flight per iteration).
 __global__ __launch_bounds__(256) void prelu_bwd_k(const bf16_t* __restrict__ da,
                                                    const bf16_t* __restrict__ z,
                                                    const float* __restrict__ alpha,
                                                    bf16_t* __restrict__ dz, float* __restrict__ dalpha,
                                                    float* __restrict__ dbias, int N, int HWC, int C,
                                                    int nper) {
-  __shared__ float sbias[256];
-  sbias[threadIdx.x] = 0.f;
-  __syncthreads();
+  __shared__ float sred[4 * 256];
+  __shared__ float sda[2048];
   const int HWC8 = HWC >> 3;
   const int i = blockIdx.x * 256 + threadIdx.x;
   const int n0 = blockIdx.y * nper, n1 = min(N, n0 + nper);
+  float db[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (i < HWC8) {
     const long e = (long)i * 8;
-    const int c0 = (int)(e % C);
     const float4 a0 = *(const float4*)(alpha + e), a1 = *(const float4*)(alpha + e + 4);
     const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-    float dal[8] = {0, 0, 0, 0, 0, 0, 0, 0}, db[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int n = n0; n < n1; ++n) {
-      const long off = (long)n * HWC + e;
-      float g[8], zv[8], o[8];
-      unpack8(*(const U4*)(da + off), g);
-      unpack8(*(const U4*)(z + off), zv);
+    float dal[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int n = n0; n < n1; n += 2) {
+      const bool two = n + 1 < n1;
+      const long off0 = (long)n * HWC + e, off1 = two ? off0 + HWC : off0;
+      const U4 g0 = *(const U4*)(da + off0), z0 = *(const U4*)(z + off0);
+      const U4 g1 = *(const U4*)(da + off1), z1 = *(const U4*)(z + off1);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        o[j] = zv[j] > 0.f ? g[j] : g[j] * av[j];
-        dal[j] += zv[j] > 0.f ? 0.f : g[j] * zv[j];
-        db[j] += o[j];
+      for (int u = 0; u < 2; ++u) {
+        if (u == 1 && !two) break;
+        float g[8], zv[8], o[8];
+        unpack8(u ? g1 : g0, g);
+        unpack8(u ? z1 : z0, zv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          o[j] = zv[j] > 0.f ? g[j] : g[j] * av[j];
+          dal[j] += zv[j] > 0.f ? 0.f : g[j] * zv[j];
+          db[j] += o[j];
+        }
+        *(U4*)(dz + (u ? off1 : off0)) = pack8(o);
       }
-      *(U4*)(dz + off) = pack8(o);
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      atomicAdd(dalpha + e + j, dal[j]);
-      atomicAdd(&sbias[c0 + j], db[j]);
-    }
+    for (int j = 0; j < 8; ++j) sda[threadIdx.x * 8 + j] = dal[j];
   }
   __syncthreads();
-  if (threadIdx.x < C) atomicAdd(dbias + threadIdx.x, sbias[threadIdx.x]);
+  // the block's 2048 dalpha values are contiguous: coalesced atomics
+  for (int k = 0; k < 8; ++k) {
+    const int L = k * 256 + threadIdx.x;
+    const long e = (long)blockIdx.x * 2048 + L;
+    if (e < HWC) atomicAdd(dalpha + e, sda[L]);
+  }
+  // channel group of this thread: i % (C/8) (== tid % (C/8) when C/8 is a power of two)
+  bias_reduce_atomic(db, i % (C >> 3), C >> 3, sred, dbias);
 }
 
 // out_bf16[m][n] = act(acc[m][n] + bias[n])   (split-K GEMM finishing pass)
@@ -487,7 +544,7 @@ int ptg_prelu_pool_bwd(const void* dp, const void* z, const float* alpha, void* 
   const int npos = (H / 2) * (W / 2) * (C / 8);
   if (nper <= 0) {
     const int bx = (npos + 255) / 256;
-    int chunks = (1024 + bx - 1) / bx;
+    int chunks = (2048 + bx - 1) / bx;
     if (chunks > N) chunks = N;
     nper = (N + chunks - 1) / chunks;
   }
@@ -511,7 +568,7 @@ int ptg_prelu_bwd(const void* da, const void* z, const float* alpha, void* dz, f
   const int nvec = HWC / 8;
   if (nper <= 0) {
     const int bx = (nvec + 255) / 256;
-    int chunks = (1024 + bx - 1) / bx;
+    int chunks = (2048 + bx - 1) / bx;
     if (chunks > N) chunks = N;
     nper = (N + chunks - 1) / chunks;
   }

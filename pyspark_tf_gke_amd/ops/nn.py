@@ -236,12 +236,13 @@ def prelu_pool_fwd(z, alpha, out):
     return out
 
 
-def prelu_pool_bwd(dp, z, alpha, dz_out, dalpha, dbias):
-    """dz_out = d/dz of maxpool2x2(prelu(z)); dalpha, dbias accumulate (fp32)."""
+def prelu_pool_bwd(dp, z, alpha, dz_out, dalpha, dbias, nper: int = 0):
+    """dz_out = d/dz of maxpool2x2(prelu(z)); dalpha, dbias accumulate (fp32).  ``nper``: samples
+    per workgroup (0 = auto)."""
     if not on_device(z):
         return ref.prelu_pool_bwd(dp, z, alpha, dz_out, dalpha, dbias)
     N, H, W, C = z.shape
-    hip("ptg_prelu_pool_bwd", ptr(dp), ptr(z), ptr(alpha), ptr(dz_out), ptr(dalpha), ptr(dbias), N, H, W, C, 0)
+    hip("ptg_prelu_pool_bwd", ptr(dp), ptr(z), ptr(alpha), ptr(dz_out), ptr(dalpha), ptr(dbias), N, H, W, C, nper)
     return dz_out
 
 
@@ -253,12 +254,12 @@ def prelu_fwd(z, alpha, out):
     return out
 
 
-def prelu_bwd(da, z, alpha, dz_out, dalpha, dbias):
+def prelu_bwd(da, z, alpha, dz_out, dalpha, dbias, nper: int = 0):
     if not on_device(z):
         return ref.prelu_bwd(da, z, alpha, dz_out, dalpha, dbias)
     N = z.shape[0]
     C = z.shape[-1]
-    hip("ptg_prelu_bwd", ptr(da), ptr(z), ptr(alpha), ptr(dz_out), ptr(dalpha), ptr(dbias), N, z[0].numel(), C, 0)
+    hip("ptg_prelu_bwd", ptr(da), ptr(z), ptr(alpha), ptr(dz_out), ptr(dalpha), ptr(dbias), N, z[0].numel(), C, nper)
     return dz_out
 
 

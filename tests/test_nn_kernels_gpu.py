@@ -175,9 +175,9 @@ def test_conv_halo_dgrad(N, H, W, C, Co, KS):
     _close(out, ref, 2e-2, 2e-2, "halo_dgrad")
 
 
-@pytest.mark.parametrize("C", [8, 16, 64, 128])
-def test_prelu_pool_fwd_bwd(C):
-    N, H, W = 3, 8, 12
+@pytest.mark.parametrize("C,N,H,W,nper", [(8, 3, 8, 12, 0), (16, 3, 8, 12, 0), (64, 3, 8, 12, 0), (128, 3, 8, 12, 0),
+                                          (24, 7, 10, 14, 3), (8, 9, 7, 9, 4), (32, 5, 6, 6, 2)])
+def test_prelu_pool_fwd_bwd(C, N, H, W, nper):
     z = rnd(N, H, W, C)
     alpha = torch.randn(H, W, C) * 0.3
     alpha[0, 0, :] = 0.0  # exercise ties of zeros
@@ -191,7 +191,7 @@ def test_prelu_pool_fwd_bwd(C):
     dz = torch.empty(N, H, W, C, device=DEV, dtype=torch.bfloat16)
     da = torch.zeros(H, W, C, device=DEV)
     db = torch.zeros(C, device=DEV)
-    K.prelu_pool_bwd(dp.to(DEV), z.to(DEV), alpha.to(DEV), dz, da, db)
+    K.prelu_pool_bwd(dp.to(DEV), z.to(DEV), alpha.to(DEV), dz, da, db, nper)
     dzr = torch.empty(N, H, W, C, dtype=torch.bfloat16)
     dar, dbr = torch.zeros(H, W, C), torch.zeros(C)
     R.prelu_pool_bwd(dp, z, alpha, dzr, dar, dbr)
@@ -200,8 +200,8 @@ def test_prelu_pool_fwd_bwd(C):
     _close(db, dbr, 1e-2, 1e-2, "dbias")
 
 
-def test_prelu_fwd_bwd():
-    N, H, W, C = 4, 16, 20, 64
+@pytest.mark.parametrize("N,H,W,C,nper", [(4, 16, 20, 64, 0), (7, 5, 6, 24, 3), (5, 4, 4, 8, 2)])
+def test_prelu_fwd_bwd(N, H, W, C, nper):
     z, alpha, da = rnd(N, H, W, C), torch.randn(H, W, C) * 0.2, rnd(N, H, W, C)
     a = torch.empty_like(z, device=DEV)
     K.prelu_fwd(z.to(DEV), alpha.to(DEV), a)
@@ -210,7 +210,7 @@ def test_prelu_fwd_bwd():
     _close(a, ar, 1e-2, 1e-2, "prelu_fwd")
     dz = torch.empty_like(z, device=DEV)
     dal, db = torch.zeros(H, W, C, device=DEV), torch.zeros(C, device=DEV)
-    K.prelu_bwd(da.to(DEV), z.to(DEV), alpha.to(DEV), dz, dal, db)
+    K.prelu_bwd(da.to(DEV), z.to(DEV), alpha.to(DEV), dz, dal, db, nper)
     dzr, dalr, dbr = torch.empty_like(z), torch.zeros(H, W, C), torch.zeros(C)
     R.prelu_bwd(da, z, alpha, dzr, dalr, dbr)
     _close(dz, dzr, 1e-2, 1e-2, "dz")
