@@ -21,6 +21,8 @@
 //   conv_flip_k       W'[ci][kh][kw][co] = W[co][KS-1-kh][KS-1-kw][ci] (dgrad weights), bf16.
 #include "common.h"
 
+#include <algorithm>
+
 typedef __attribute__((ext_vector_type(4))) short s16x4_t;
 typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
 
@@ -63,164 +65,354 @@ PTG_DEV void stage_halo(bf16_t* __restrict__ hs, const bf16_t* __restrict__ img,
 }
 
 // ================================================================================================
-// forward / dgrad
+// forward / dgrad: persistent column-strip kernel, transposed MFMA (D = W * X^T)
 // ================================================================================================
-template <int C, int KS, int NF, int TW, int TH, int EPI>
-__global__ __launch_bounds__(256) void conv_fwd_halo_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
-                                                       const float* __restrict__ bias, const float* __restrict__ alpha,
-                                                       bf16_t* __restrict__ z, bf16_t* __restrict__ aux, int H, int W,
-                                                       int Cout, int pad, int tiles_h, int tiles_w) {
+// A workgroup owns a contiguous range of TH x TW output tiles, strip-major: it walks a vertical
+// strip (n, tw) top to bottom.
+//  * RING: the halo lives in a mirrored ring of 2*HR LDS rows; moving down one tile only loads the
+//    TH new input rows.  Without RING (TH >= 2*(KS-1)) each tile reloads its HR rows.
+//  * the next tile's rows are prefetched into registers before this tile's MFMAs and written to
+//    LDS after them, so HBM latency hides behind compute.
+//  * MFMA computes D[co][pixel] (weights are the A operand, the halo the B operand), so every lane
+//    ends with 4 consecutive output channels of one pixel: bias, bf16 rounding, per-element PReLU
+//    (one float4 alpha load) and 8-byte stores straight from registers - no LDS staging.
+//  * the 2x2 max-pool runs in registers: horizontal neighbours are adjacent lanes (xor 1); vertical
+//    neighbours are the paired fragment of the same wave (TW >= 16) or lanes xor TW (TW < 16).
+//  * PReLU is applied to the bf16-rounded z, exactly what the backward recomputes.
+typedef __attribute__((ext_vector_type(4))) unsigned int vu4_t;   // register-friendly (SROA-able)
+typedef __attribute__((ext_vector_type(2))) unsigned int vu2_t;
+template <int C> struct HVec { using T = vu4_t; static constexpr int per_pix = C / 8; };
+template <> struct HVec<4> { using T = vu2_t; static constexpr int per_pix = 1; };
+
+// dpp row_shl:n - lane l receives lane l+n of its 16-lane row (others keep their own value)
+template <int NSH>
+PTG_DEV float row_shl(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), 0x100 | NSH, 0xF, 0xF, false));
+}
+
+template <int C, int KS, int NF, int TW, int TH, int EPI, bool RING, bool KSPLIT>
+__global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
+                                                        const float* __restrict__ bias, const float* __restrict__ alpha,
+                                                        bf16_t* __restrict__ z, bf16_t* __restrict__ aux, int N, int H,
+                                                        int W, int Cout, int pad, int tiles_h, int tiles_w) {
+  using VT = typename HVec<C>::T;
+  constexpr int VPP = HVec<C>::per_pix;      // vectors per pixel
+  constexpr int VE = C == 4 ? 4 : 8;          // elements per vector
   constexpr int KWP = Kwp<C, KS>::v;
   constexpr int PIX = PixPitch<C>::v;
   constexpr int HR = TH + KS - 1, HC = TW + KWP - 1;
-  constexpr int KROW = KWP * C;         // flattened k per kernel row
+  constexpr int ROWE = HC * PIX;
+  constexpr int NROWS = RING ? 2 * HR : HR;
+  constexpr int KROW = KWP * C;
   constexpr int KTOT = KS * KROW;
   constexpr int KSTEPS = (KTOT + 31) / 32;
   constexpr int M = TH * TW;
-  constexpr int MFR = M / 16;           // 16-pixel fragments per tile
-  constexpr int FM = MFR / 4;           // fragments per wave
-  static_assert(MFR % 4 == 0, "tile must give 4 waves equal work");
-  constexpr int HALO_ELEMS = HR * HC * PIX;
-  constexpr int ZPITCH = NF * 16 + 8;   // staged output pixel pitch (bf16), padded
-  constexpr int ZELEMS = M * ZPITCH;
-  constexpr int LDS_ELEMS = (HALO_ELEMS + 8 > ZELEMS ? HALO_ELEMS + 8 : ZELEMS);
-  __shared__ __attribute__((aligned(16))) bf16_t smem[LDS_ELEMS];
+  constexpr int MFR = M / 16;
+  constexpr int FM = MFR / 4;
+  constexpr bool WIDE = TW >= 16;             // fragment = 16 pixels of one row
+  static_assert(MFR % 4 == 0 && TH % 2 == 0, "tile shape");
+  static_assert(WIDE ? (TW % 16 == 0 && (FM % 2 == 0 || EPI != EPI_POOL)) : (TW == 4 || TW == 8), "pool pairing");
+  constexpr int SEG = WIDE ? TW / 16 : 1;
+  constexpr int HALO_ELEMS = NROWS * ROWE;
+  constexpr int PFN = (HR * HC * VPP + 255) / 256;   // prefetch vectors per thread (worst case: HR rows)
+  constexpr bool WREG = !KSPLIT && KSTEPS * NF <= 8;   // all weight fragments resident in VGPRs
+  // KSPLIT: each wave runs every pixel fragment of the tile over a quarter of the K-steps, then
+  // the partial sums are reduce-scattered through LDS (more MFMAs per weight fetch when FM is small)
+  constexpr int AF = KSPLIT ? MFR : FM;                // fragments a wave accumulates
+  constexpr int RED_F4 = KSPLIT ? 4 * 3 * FM * NF * 64 : 1;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[HALO_ELEMS + 8];
+  __shared__ __attribute__((aligned(16))) float4 sred[RED_F4];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  int t = blockIdx.x;
-  const int tw_i = t % tiles_w; t /= tiles_w;
-  const int th_i = t % tiles_h; const int n = t / tiles_h;
-  const int oh0 = th_i * TH, ow0 = tw_i * TW;
-  const bf16_t* img = x + (long)n * H * W * C;
+  const int px = lane & 15, g = lane >> 4;
+  const int S = N * tiles_w;
+  if (tid < 8) smem[HALO_ELEMS + tid] = 0;  // zero guard for padded K groups
 
-  stage_halo<C, PIX>(smem, img, H, W, oh0 - pad, ow0 - pad, HR, HC);
-  // zero guard pixel used by padded K groups (k >= KTOT)
-  if (tid < 8) smem[HALO_ELEMS + tid] = 0;
-  __syncthreads();
-
-  // per-lane fragment rows (pixels)
-  const int frow = lane & 15, g = lane >> 4;
-  int pbase[FM];
-#pragma unroll
-  for (int i = 0; i < FM; ++i) {
-    const int m = (wid * FM + i) * 16 + frow;
-    const int r = m / TW, c = m % TW;
-    pbase[i] = (r * HC + c) * PIX;
-  }
-  f32x4_t acc[FM][NF];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < NF; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-  const int co_l = lane & 15;
-  for (int ks = 0; ks < KSTEPS; ++ks) {
-    const int kf = ks * 32 + 8 * g;   // this lane group's first k
-    const bool kval = kf < KTOT;
+  // ---- weight fragments (MFMA A operand: row = co, 8 k per lane group): w [Cout][KS][KS][C] ----
+  auto load_w = [&](int ks, int j) -> bf16x8_t {
+    const int kf = ks * 32 + 8 * g;
     const int kh = kf / KROW, rem = kf - kh * KROW;
     const int kw = rem / C, ci = rem - kw * C;
-    // B fragments (weights, from global / L1): w layout [Cout][KS][KS][C]
-    bf16x8_t bf[NF];
+    const int co = j * 16 + px;
+    U4 v = zero4();
+    if constexpr (C >= 8) {  // KWP == KS: flattened K is the memory order of a filter
+      (void)kh; (void)kw; (void)ci;
+      if (kf < KTOT && co < Cout) v = *(const U4*)(w + (long)co * KTOT + kf);
+    } else if (kf < KTOT && co < Cout) {
+      const bf16_t* wp = w + ((long)co * KS * KS + kh * KS) * C;
+      {
+        U2 a = U2{0u, 0u}, b = U2{0u, 0u};
+        if (kw < KS) a = *(const U2*)(wp + kw * 4);
+        if (kw + 1 < KS) b = *(const U2*)(wp + (kw + 1) * 4);
+        v.x = a.x; v.y = a.y; v.z = b.x; v.w = b.y;
+      }
+    }
+    return __builtin_bit_cast(bf16x8_t, v);
+  };
+  bf16x8_t wreg[WREG ? KSTEPS : 1][NF];
+  if constexpr (WREG) {
 #pragma unroll
-    for (int j = 0; j < NF; ++j) {
-      const int co = j * 16 + co_l;
-      U4 v = zero4();
-      if (kval && co < Cout) {
-        const bf16_t* wp = w + ((long)co * KS * KS + kh * KS) * C;
-        if constexpr (C >= 8) {
-          if (kw < KS) v = *(const U4*)(wp + kw * C + ci);
-        } else {  // C == 4: two pixels (kw, kw+1), pad columns are zero
-          U2 a = U2{0u, 0u}, b = U2{0u, 0u};
-          if (kw < KS) a = *(const U2*)(wp + kw * 4);
-          if (kw + 1 < KS) b = *(const U2*)(wp + (kw + 1) * 4);
-          v.x = a.x; v.y = a.y; v.z = b.x; v.w = b.y;
+    for (int ks = 0; ks < KSTEPS; ++ks)
+#pragma unroll
+      for (int j = 0; j < NF; ++j) wreg[ks][j] = load_w(ks, j);
+  }
+  // bias for this lane's 4 channels of each co fragment
+  float bv[NF][4];
+#pragma unroll
+  for (int j = 0; j < NF; ++j) {
+    const int co0 = j * 16 + g * 4;
+    float4 b4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (bias && co0 < Cout) b4 = *(const float4*)(bias + co0);
+    bv[j][0] = b4.x; bv[j][1] = b4.y; bv[j][2] = b4.z; bv[j][3] = b4.w;
+  }
+
+  // ---- halo rows: per-thread fixed (row, col, vector) slots, global -> registers -> LDS ring ----
+  int pr_r[PFN], pr_c[PFN], pr_l[PFN];
+#pragma unroll
+  for (int p = 0; p < PFN; ++p) {
+    const int idx = tid + p * 256;
+    const int pix = idx / VPP, vv = idx - pix * VPP;
+    pr_r[p] = pix / HC;
+    pr_c[p] = pix - pr_r[p] * HC;
+    pr_l[p] = pr_c[p] * PIX + vv * VE;   // LDS offset inside a halo row
+  }
+  VT pf[PFN];
+  auto load_rows = [&](int n, int iw0, int ih_first, int nrows) {
+    const bf16_t* img = x + (long)n * H * W * C;
+#pragma unroll
+    for (int p = 0; p < PFN; ++p) {
+      VT v = (VT)0u;
+      const int ih = ih_first + pr_r[p], iw = iw0 + pr_c[p];
+      if (pr_r[p] < nrows && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
+        v = *(const VT*)(img + ((long)ih * W + iw) * C + (pr_l[p] - pr_c[p] * PIX));
+      pf[p] = v;
+    }
+  };
+  auto store_rows = [&](int nrows, int slot_first) {
+#pragma unroll
+    for (int p = 0; p < PFN; ++p) {
+      if (pr_r[p] < nrows) {
+        int slot = slot_first + pr_r[p];
+        if constexpr (RING) slot = slot >= HR ? slot - HR : slot;
+        bf16_t* dst = smem + slot * ROWE + pr_l[p];
+        *(VT*)dst = pf[p];
+        if constexpr (RING) *(VT*)(dst + HR * ROWE) = pf[p];
+      }
+    }
+  };
+
+  // ---- this lane's pixel of each fragment (tile coordinates): owned fragments first ----
+  auto frag_rc = [&](int f, int& rr, int& cc) {
+    if constexpr (WIDE) {
+      const int pi = f >> 1, sub = f & 1;
+      rr = 2 * (pi / SEG) + sub;
+      cc = (pi % SEG) * 16 + px;
+    } else {
+      rr = (f * 16 + px) / TW;
+      cc = (f * 16 + px) % TW;
+    }
+  };
+  int f_r[FM], f_c[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int f = wid * FM + i;
+    if constexpr (WIDE) {
+      const int pi = f >> 1, sub = f & 1;  // fragment pairs = vertically adjacent rows
+      f_r[i] = 2 * (pi / SEG) + sub;
+      f_c[i] = (pi % SEG) * 16 + px;
+    } else {
+      f_r[i] = (f * 16 + px) / TW;
+      f_c[i] = (f * 16 + px) % TW;
+    }
+  }
+
+  // this workgroup's contiguous range of tiles, strip-major (balanced to within one tile)
+  const long T = (long)S * tiles_h;
+  const int t0 = (int)(T * blockIdx.x / gridDim.x), t1 = (int)(T * (blockIdx.x + 1) / gridDim.x);
+  if (t0 >= t1) return;
+  int s = t0 / tiles_h, th = t0 - s * tiles_h;
+  {  // first tile: synchronous fill of its HR rows
+    const int n = s / tiles_w, ow0 = (s - n * tiles_w) * TW;
+    load_rows(n, ow0 - pad, th * TH - pad, HR);
+    store_rows(HR, RING ? (th * TH) % HR : 0);
+  }
+  __syncthreads();
+
+  const int PH = H >> 1, PW = W >> 1;
+  for (int t = t0; t < t1; ++t) {
+    const int n = s / tiles_w, ow0 = (s - n * tiles_w) * TW, oh0 = th * TH;
+    // next tile of the range and the rows it needs that are not resident
+    int s2 = s, th2 = th + 1;
+    if (th2 >= tiles_h) { s2 = s + 1; th2 = 0; }
+    const bool has_next = t + 1 < t1;
+    const bool same_strip = s2 == s;
+    const int n2 = s2 / tiles_w, ow02 = (s2 - n2 * tiles_w) * TW;
+    const int nrows2 = (RING && same_strip) ? TH : HR;
+    const int ih2 = (RING && same_strip) ? th2 * TH - pad + HR - TH : th2 * TH - pad;
+    const int slot2 = !RING ? 0 : same_strip ? (th2 * TH + HR - TH) % HR : (th2 * TH) % HR;
+    if (has_next) load_rows(n2, ow02 - pad, ih2, nrows2);
+
+    // alpha for this lane's (pixel, 4 channels) of every fragment, needed after the MFMAs
+    float4 al[EPI != EPI_Z ? FM : 1][NF];
+    if constexpr (EPI != EPI_Z) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < NF; ++j) {
+          const int oh = oh0 + f_r[i], ow = ow0 + f_c[i], co0 = j * 16 + g * 4;
+          al[i][j] = (co0 < Cout && oh < H && ow < W) ? *(const float4*)(alpha + ((long)oh * W + ow) * Cout + co0)
+                                                      : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    }
+
+    // ---- MFMA main loop over the flattened K = (kh, kw', ci) ----
+    const int wstart = RING ? (oh0 % HR) : 0;
+    int pbase[AF];
+#pragma unroll
+    for (int i = 0; i < AF; ++i) {
+      int rr, cc;
+      if constexpr (KSPLIT) frag_rc(i, rr, cc);
+      else { rr = f_r[i]; cc = f_c[i]; }
+      pbase[i] = ((wstart + rr) * HC + cc) * PIX;
+    }
+    f32x4_t acc[AF][NF];
+#pragma unroll
+    for (int i = 0; i < AF; ++i)
+#pragma unroll
+      for (int j = 0; j < NF; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    constexpr int KS0 = 0, KSTEP = KSPLIT ? 4 : 1;
+    const int ks_begin = KSPLIT ? wid : KS0;
+    bf16x8_t wnext[NF];
+    if constexpr (!WREG) {
+#pragma unroll
+      for (int j = 0; j < NF; ++j) wnext[j] = load_w(ks_begin, j);
+    }
+#pragma unroll(WREG ? KSTEPS : 1)
+    for (int ks = ks_begin; ks < KSTEPS; ks += KSTEP) {
+      bf16x8_t wf[NF];
+      if constexpr (WREG) {
+#pragma unroll
+        for (int j = 0; j < NF; ++j) wf[j] = wreg[WREG ? ks : 0][j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < NF; ++j) wf[j] = wnext[j];
+        if (ks + KSTEP < KSTEPS) {
+#pragma unroll
+          for (int j = 0; j < NF; ++j) wnext[j] = load_w(ks + KSTEP, j);
         }
       }
-      bf[j] = __builtin_bit_cast(bf16x8_t, v);
-    }
-    // A fragments from the halo: pixel (r + kh, c + kw), channels ci..ci+7
-    const int koff = (kh * HC + kw) * PIX + ci;
+      const int kf = ks * 32 + 8 * g;
+      const bool kval = kf < KTOT;
+      const int kh = kf / KROW, rem = kf - kh * KROW;
+      const int kw = rem / C, ci = rem - kw * C;
+      const int koff = (kh * HC + kw) * PIX + ci;
 #pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      bf16x8_t af;
-      if constexpr (C >= 8) {
+      for (int i = 0; i < AF; ++i) {
+        bf16x8_t xf;
         const int off = kval ? pbase[i] + koff : HALO_ELEMS;
-        af = *(const bf16x8_t*)(smem + off);
-      } else {
-        const int off = kval ? pbase[i] + koff : HALO_ELEMS;
-        U2 lo = *(const U2*)(smem + off);
-        U2 hi = kval ? *(const U2*)(smem + off + 4) : U2{0u, 0u};
-        U4 v; v.x = lo.x; v.y = lo.y; v.z = hi.x; v.w = hi.y;
-        af = __builtin_bit_cast(bf16x8_t, v);
+        if constexpr (C >= 8) {
+          xf = *(const bf16x8_t*)(smem + off);
+        } else {
+          const U2 lo = *(const U2*)(smem + off);
+          const U2 hi = kval ? *(const U2*)(smem + off + 4) : U2{0u, 0u};
+          U4 v; v.x = lo.x; v.y = lo.y; v.z = hi.x; v.w = hi.y;
+          xf = __builtin_bit_cast(bf16x8_t, v);
+        }
+#pragma unroll
+        for (int j = 0; j < NF; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf, acc[i][j], 0, 0, 0);
       }
-#pragma unroll
-      for (int j = 0; j < NF; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[j], acc[i][j], 0, 0, 0);
     }
-  }
-  __syncthreads();  // halo no longer needed: reuse LDS for the output tile
-
-  // epilogue: + bias -> bf16 -> staged [pixel][co] tile
-  bf16_t* zs = smem;
+    f32x4_t res[FM][NF];
+    if constexpr (KSPLIT) {
+      // reduce-scatter: fragment f belongs to wave f / FM; partials go to that owner's slots
 #pragma unroll
-  for (int i = 0; i < FM; ++i)
+      for (int f = 0; f < MFR; ++f) {
+        const int o = f / FM, q = f % FM;
+        if (o != wid) {
+          const int src = wid < o ? wid : wid - 1;  // 0..2 among the non-owners
+#pragma unroll
+          for (int j = 0; j < NF; ++j)
+            sred[(((o * 3 + src) * FM + q) * NF + j) * 64 + lane] =
+                make_float4(acc[f][j][0], acc[f][j][1], acc[f][j][2], acc[f][j][3]);
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < FM; ++q)
+#pragma unroll
+        for (int j = 0; j < NF; ++j) {
+          f32x4_t a = acc[0][j];
+          // own partial (static index: select among fragments)
+#pragma unroll
+          for (int f = 0; f < MFR; ++f)
+            if (f == wid * FM + q) a = acc[f][j];
+#pragma unroll
+          for (int src = 0; src < 3; ++src) {
+            const float4 v = sred[(((wid * 3 + src) * FM + q) * NF + j) * 64 + lane];
+            a[0] += v.x; a[1] += v.y; a[2] += v.z; a[3] += v.w;
+          }
+          res[q][j] = a;
+        }
+    } else {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < NF; ++j) res[i][j] = acc[i][j];
+    }
+    __syncthreads();  // every wave is done reading the halo window
+    if (has_next) store_rows(nrows2, slot2);
+
+    // ---- epilogue from registers ----
 #pragma unroll
     for (int j = 0; j < NF; ++j) {
-      const int co = j * 16 + co_l;
-      const float b = (bias && co < Cout) ? bias[co] : 0.f;
+      const int co0 = j * 16 + g * 4;
+      const bool cval = co0 < Cout;
+      float y[FM][4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = (wid * FM + i) * 16 + g * 4 + r;
-        zs[m * ZPITCH + co] = f2bf(acc[i][j][r] + b);
+      for (int i = 0; i < FM; ++i) {
+        const int oh = oh0 + f_r[i], ow = ow0 + f_c[i];
+        float zr[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) zr[r] = bf2f(f2bf(res[i][j][r] + bv[j][r]));
+        const bool in = cval && oh < H && ow < W;
+        const long o = (((long)n * H + oh) * W + ow) * Cout + co0;
+        if (in) *(U2*)(z + o) = U2{pack_bf(zr[0], zr[1]), pack_bf(zr[2], zr[3])};
+        if constexpr (EPI != EPI_Z) {
+          const float a4[4] = {al[i][j].x, al[i][j].y, al[i][j].z, al[i][j].w};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) y[i][r] = zr[r] > 0.f ? zr[r] : a4[r] * zr[r];
+          if constexpr (EPI == EPI_PRELU) {
+            if (in) *(U2*)(aux + o) = U2{pack_bf(y[i][0], y[i][1]), pack_bf(y[i][2], y[i][3])};
+          }
+        }
+      }
+      if constexpr (EPI == EPI_POOL) {
+        // horizontal pair: lanes px, px^1; vertical pair: fragment i^1 (WIDE) or lanes px^TW
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) y[i][r] = fmaxf(y[i][r], row_shl<1>(y[i][r]));  // lead lanes: even column
+#pragma unroll
+        for (int i = 0; i < FM; i += (WIDE ? 2 : 1)) {
+          float pm[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            if constexpr (WIDE) pm[r] = fmaxf(y[i][r], y[i + 1][r]);
+            else pm[r] = fmaxf(y[i][r], row_shl<(WIDE ? 1 : TW)>(y[i][r]));
+          }
+          const int rr = f_r[i], cc = f_c[i];
+          const bool lead = ((cc & 1) == 0) && ((rr & 1) == 0);
+          const int ph = (oh0 + rr) >> 1, pw = (ow0 + cc) >> 1;
+          if (cval && lead && ph < PH && pw < PW)
+            *(U2*)(aux + (((long)n * PH + ph) * PW + pw) * Cout + co0) =
+                U2{pack_bf(pm[0], pm[1]), pack_bf(pm[2], pm[3])};
+        }
       }
     }
-  __syncthreads();
-  // z: 16-byte vectors, channels fastest
-  const int CV = Cout / 8;
-  for (int v = tid; v < M * CV; v += 256) {
-    const int m = v / CV, cv = v - m * CV;
-    const int oh = oh0 + m / TW, ow = ow0 + m % TW;
-    if (oh < H && ow < W)
-      *(U4*)(z + (((long)n * H + oh) * W + ow) * Cout + cv * 8) = *(const U4*)(zs + m * ZPITCH + cv * 8);
-  }
-  if constexpr (EPI == EPI_PRELU) {
-    for (int v = tid; v < M * CV; v += 256) {
-      const int m = v / CV, cv = v - m * CV;
-      const int oh = oh0 + m / TW, ow = ow0 + m % TW;
-      if (oh >= H || ow >= W) continue;
-      float zf[8];
-      unpack8(*(const U4*)(zs + m * ZPITCH + cv * 8), zf);
-      const float* al = alpha + ((long)oh * W + ow) * Cout + cv * 8;
-      const float4 a0 = *(const float4*)al, a1 = *(const float4*)(al + 4);
-      const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-#pragma unroll
-      for (int q = 0; q < 8; ++q) zf[q] = zf[q] > 0.f ? zf[q] : av[q] * zf[q];
-      *(U4*)(aux + (((long)n * H + oh) * W + ow) * Cout + cv * 8) = pack8(zf);
-    }
-  }
-  if constexpr (EPI == EPI_POOL) {
-    const int PH = H >> 1, PW = W >> 1;
-    constexpr int PM = (TH / 2) * (TW / 2);
-    for (int v = tid; v < PM * CV; v += 256) {
-      const int pm = v / CV, cv = v - pm * CV;
-      const int pr = pm / (TW / 2), pc = pm - pr * (TW / 2);
-      const int ph = (oh0 >> 1) + pr, pw = (ow0 >> 1) + pc;
-      if (ph >= PH || pw >= PW) continue;
-      float best[8];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) best[q] = -INFINITY;
-#pragma unroll
-      for (int qq = 0; qq < 4; ++qq) {
-        const int lr = 2 * pr + (qq >> 1), lc = 2 * pc + (qq & 1);
-        float zf[8];
-        unpack8(*(const U4*)(zs + (lr * TW + lc) * ZPITCH + cv * 8), zf);
-        const float* al = alpha + ((long)(oh0 + lr) * W + (ow0 + lc)) * Cout + cv * 8;
-        const float4 a0 = *(const float4*)al, a1 = *(const float4*)(al + 4);
-        const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-#pragma unroll
-        for (int q = 0; q < 8; ++q) best[q] = fmaxf(best[q], zf[q] > 0.f ? zf[q] : av[q] * zf[q]);
-      }
-      *(U4*)(aux + (((long)n * PH + ph) * PW + pw) * Cout + cv * 8) = pack8(best);
-    }
+    if (!has_next) break;
+    __syncthreads();  // next tile's halo rows visible
+    s = s2;
+    th = th2;
   }
 }
 
@@ -352,19 +544,44 @@ __global__ __launch_bounds__(256) void conv_flip_k(const bf16_t* __restrict__ w,
 // ------------------------------------------------------------------------------------------------
 // host dispatch
 // ------------------------------------------------------------------------------------------------
+// workgroups of `kernel` (256 threads) that fit on the device at once (cached per kernel)
+static int resident_blocks(const void* kernel) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess || per_cu <= 0) per_cu = 2;
+  return cus * per_cu;
+}
+
+template <int C, int KS, int NF, int TW, int TH, int E>
+static int launch_fwd_e(const void* x, const void* w, const float* bias, const float* alpha, void* z, void* aux, int N,
+                        int H, int W, int Cout, int pad, hipStream_t s) {
+  constexpr bool RING = TH < 2 * (KS - 1);
+  constexpr int KTOT = KS * Kwp<C, KS>::v * C, KSTEPS = (KTOT + 31) / 32, MFR = TH * TW / 16;
+  constexpr bool WREG = KSTEPS * NF <= 8;
+  constexpr bool KSPLIT = !WREG && MFR / 4 <= 2 && MFR * NF <= 16;
+  const auto kern = conv_fwd_strip_k<C, KS, NF, TW, TH, E, RING, KSPLIT>;
+  static const int resident = resident_blocks((const void*)kern);
+  const int th = (H + TH - 1) / TH, tw = (W + TW - 1) / TW;
+  const long tiles = (long)N * tw * th;
+  // persistent: one wave of resident workgroups, each walking a contiguous range of tiles
+  const int grid = (int)std::min<long>(tiles, resident);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, (const bf16_t*)x, (const bf16_t*)w, bias, alpha, (bf16_t*)z,
+                     (bf16_t*)aux, N, H, W, Cout, pad, th, tw);
+  PTG_RETURN_LAUNCH();
+}
+
 template <int C, int KS, int NF, int TW, int TH>
 static int launch_fwd(const void* x, const void* w, const float* bias, const float* alpha, void* z, void* aux, int N,
                       int H, int W, int Cout, int pad, int epi, hipStream_t s) {
-  const int th = (H + TH - 1) / TH, tw = (W + TW - 1) / TW;
-  dim3 grid(N * th * tw);
-#define PTG_FWD(E)                                                                                               \
-  hipLaunchKernelGGL((conv_fwd_halo_k<C, KS, NF, TW, TH, E>), grid, dim3(256), 0, s, (const bf16_t*)x,          \
-                     (const bf16_t*)w, bias, alpha, (bf16_t*)z, (bf16_t*)aux, H, W, Cout, pad, th, tw)
-  if (epi == EPI_POOL) PTG_FWD(EPI_POOL);
-  else if (epi == EPI_PRELU) PTG_FWD(EPI_PRELU);
-  else PTG_FWD(EPI_Z);
-#undef PTG_FWD
-  PTG_RETURN_LAUNCH();
+  if (epi == EPI_POOL) return launch_fwd_e<C, KS, NF, TW, TH, EPI_POOL>(x, w, bias, alpha, z, aux, N, H, W, Cout, pad, s);
+  if (epi == EPI_PRELU) return launch_fwd_e<C, KS, NF, TW, TH, EPI_PRELU>(x, w, bias, alpha, z, aux, N, H, W, Cout, pad, s);
+  return launch_fwd_e<C, KS, NF, TW, TH, EPI_Z>(x, w, bias, alpha, z, aux, N, H, W, Cout, pad, s);
 }
 
 template <int C, int KS, int NF>

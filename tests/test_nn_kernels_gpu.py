@@ -124,7 +124,13 @@ HALO_CASES = [(2, 16, 20, 4, 8, 5), (2, 18, 22, 8, 16, 5), (2, 12, 10, 16, 32, 5
               (2, 256, 320, 4, 8, 5), (2, 9, 7, 16, 64, 3)]
 
 
-@pytest.mark.parametrize("N,H,W,C,Co,KS", HALO_CASES)
+# more tiles than resident workgroups: exercises the persistent tile ranges, the ring-buffer halo
+# reuse across tiles of a strip and strip changes inside one workgroup's range
+BIG_HALO = [(16, 256, 320, 4, 8, 5), (32, 128, 160, 8, 16, 5), (64, 64, 80, 16, 32, 5), (128, 32, 40, 32, 64, 5),
+            (256, 16, 20, 64, 64, 5), (160, 32, 40, 64, 32, 5), (40, 66, 70, 16, 16, 3)]
+
+
+@pytest.mark.parametrize("N,H,W,C,Co,KS", HALO_CASES + BIG_HALO)
 @pytest.mark.parametrize("epi", [None, "pool", "prelu"])
 def test_conv_halo_fwd(N, H, W, C, Co, KS, epi):
     if epi == "pool" and (H % 2 or W % 2):
