@@ -13,7 +13,7 @@
 //                     LDS and written with 16-byte stores; optional fused epilogue
 //                     EPI_POOL  -> also writes maxpool2x2(prelu(z, alpha))  (PReLU + MaxPooling2D)
 //                     EPI_PRELU -> also writes prelu(z, alpha)                (last conv block)
-//   conv_wgrad_halo_k dW[co][kh][kw][ci] = sum_pixels dZ[pix][co] * x[pix + (kh,kw)][ci]:
+//   conv_wgrad_strip_k dW[co][kh][kw][ci] = sum_pixels dZ[pix][co] * x[pix + (kh,kw)][ci]:
 //                     M = Cout, N = 128-wide slice of (kh,kw,ci), K = pixels; dZ tile and x halo
 //                     staged in LDS, both MFMA operands read with ds_read_b64_tr_b16 (gfx950
 //                     transposed LDS read, cdna_hip_programming.md T10), partial sums of a whole
@@ -425,70 +425,134 @@ PTG_DEV s16x4_t tr_read(const bf16_t* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(p));
 }
 
-template <int C, int KS, int TW, int TH, int MF>
-__global__ __launch_bounds__(256) void conv_wgrad_halo_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dz,
-                                                         float* __restrict__ dw, int N, int H, int W, int Cout, int pad,
-                                                         int tiles_h, int tiles_w, int tiles_per_block, int nslices) {
+// Persistent: a workgroup owns one 64*NB-wide kflat slice and a contiguous strip-major range of
+// tiles; the next tile's halo rows (RING: only the TH new ones) and dZ tile are prefetched into
+// registers during this tile's MFMAs.  Partial sums stay in registers for the whole range and are
+// flushed with one fp32 atomic per output.
+template <int C, int KS, int TW, int TH, int MF, int NB, bool RING>
+__global__ __launch_bounds__(256) void conv_wgrad_strip_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dz,
+                                                          float* __restrict__ dw, int N, int H, int W, int Cout, int pad,
+                                                          int tiles_h, int tiles_w, int nslices) {
+  using VT = typename HVec<C>::T;
+  constexpr int VPP = HVec<C>::per_pix, VE = C == 4 ? 4 : 8;
   constexpr int PIX = PixPitch<C>::v;
   constexpr int HR = TH + KS - 1, HC = TW + KS - 1;
+  constexpr int ROWE = HC * PIX;
+  constexpr int NROWS = RING ? 2 * HR : HR;
   constexpr int M = TH * TW;              // pixels per tile (K of this GEMM)
   static_assert(M % 32 == 0 && TW % 4 == 0, "tile shape");
   constexpr int KF = KS * KS * C;         // output columns (kh, kw, ci)
-  constexpr int DPITCH = MF * 16 + 4;     // dz tile pixel pitch (bf16): 8-byte aligned, bank-shifted
-  constexpr int HALO_ELEMS = HR * HC * PIX;
+  constexpr int SLICE = 64 * NB;
+  constexpr int DPITCH = MF * 16 + 4;     // dZ tile pixel pitch (bf16): 8-byte aligned, bank-shifted
+  constexpr int HALO_ELEMS = NROWS * ROWE;
   constexpr int DZ_ELEMS = M * DPITCH;
+  constexpr int PFN = (HR * HC * VPP + 255) / 256;
+  constexpr int DV = M * MF * 4;          // 8-byte dZ vectors per tile (upper bound: Cout <= MF*16)
+  constexpr int PFD = (DV + 255) / 256;
   __shared__ __attribute__((aligned(16))) bf16_t smem[HALO_ELEMS + DZ_ELEMS + 8];
-  bf16_t* hs = smem;
-  bf16_t* ds = smem + HALO_ELEMS;
+  bf16_t* const ds = smem + HALO_ELEMS;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int slice = blockIdx.x % nslices;
-  const int chunk = blockIdx.x / nslices;
-  const int total_tiles = N * tiles_h * tiles_w;
-  const int t0 = chunk * tiles_per_block, t1 = min(total_tiles, t0 + tiles_per_block);
+  const int slice = blockIdx.x % nslices, chunk = blockIdx.x / nslices, nchunks = gridDim.x / nslices;
+  const long T = (long)N * tiles_w * tiles_h;
+  const int t0 = (int)(T * chunk / nchunks), t1 = (int)(T * (chunk + 1) / nchunks);
   if (t0 >= t1) return;
 
-  // each wave owns 2 of the slice's 8 column fragments (16 kflat each)
   const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
-  int bcol[2];   // per-lane column base (kflat) for the B tr-read, or -1 if out of range
-  int boff[2];   // halo offset of that kflat for pixel (0,0)
+  // per-lane B column (kflat) base of each of this wave's NB fragments
+  int boff[NB];
+  bool bval[NB];
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int kf = slice * 128 + (wid * 2 + j) * 16 + 4 * p;
-    bcol[j] = kf < KF ? kf : -1;
-    const int kk = kf < KF ? kf : 0;
+  for (int j = 0; j < NB; ++j) {
+    const int kf = slice * SLICE + (wid * NB + j) * 16 + 4 * p;
+    bval[j] = kf < KF;
+    const int kk = bval[j] ? kf : 0;
     const int kh = kk / (KS * C), rem = kk - kh * KS * C, kw = rem / C, ci = rem - kw * C;
     boff[j] = (kh * HC + kw) * PIX + ci;
   }
-  f32x4_t acc[MF][2];
+  f32x4_t acc[MF][NB];
 #pragma unroll
   for (int i = 0; i < MF; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NB; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  for (int t = t0; t < t1; ++t) {
-    int tt = t;
-    const int tw_i = tt % tiles_w; tt /= tiles_w;
-    const int th_i = tt % tiles_h; const int n = tt / tiles_h;
-    const int oh0 = th_i * TH, ow0 = tw_i * TW;
-    __syncthreads();  // previous tile's reads done
-    stage_halo<C, PIX>(hs, x + (long)n * H * W * C, H, W, oh0 - pad, ow0 - pad, HR, HC);
-    // dz tile [M][Cout] (zero for pixels outside the image)
-    {
-      const int CV = Cout / 4;  // 8-byte vectors
-      for (int v = tid; v < M * CV; v += 256) {
+  // halo slots of this thread
+  int pr_r[PFN], pr_c[PFN], pr_l[PFN];
+#pragma unroll
+  for (int k = 0; k < PFN; ++k) {
+    const int idx = tid + k * 256;
+    const int pix = idx / VPP, vv = idx - pix * VPP;
+    pr_r[k] = pix / HC;
+    pr_c[k] = pix - pr_r[k] * HC;
+    pr_l[k] = pr_c[k] * PIX + vv * VE;
+  }
+  VT pf[PFN];
+  U2 pd[PFD];
+  const int CV = Cout / 4;
+  auto load_tile = [&](int s_, int th_, int nrows, int ih_first) {
+    const int n = s_ / tiles_w, ow0 = (s_ - n * tiles_w) * TW, oh0 = th_ * TH;
+    const bf16_t* img = x + (long)n * H * W * C;
+#pragma unroll
+    for (int k = 0; k < PFN; ++k) {
+      VT v = (VT)0u;
+      const int ih = ih_first + pr_r[k], iw = ow0 - pad + pr_c[k];
+      if (pr_r[k] < nrows && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
+        v = *(const VT*)(img + ((long)ih * W + iw) * C + (pr_l[k] - pr_c[k] * PIX));
+      pf[k] = v;
+    }
+#pragma unroll
+    for (int k = 0; k < PFD; ++k) {
+      const int v = tid + k * 256;
+      U2 val = U2{0u, 0u};
+      if (v < M * CV) {
         const int m = v / CV, cv = v - m * CV;
         const int oh = oh0 + m / TW, ow = ow0 + m % TW;
-        U2 val = U2{0u, 0u};
         if (oh < H && ow < W) val = *(const U2*)(dz + (((long)n * H + oh) * W + ow) * Cout + cv * 4);
-        *(U2*)(ds + m * DPITCH + cv * 4) = val;
+      }
+      pd[k] = val;
+    }
+  };
+  auto store_tile = [&](int nrows, int slot_first) {
+#pragma unroll
+    for (int k = 0; k < PFN; ++k) {
+      if (pr_r[k] < nrows) {
+        int slot = slot_first + pr_r[k];
+        if constexpr (RING) slot = slot >= HR ? slot - HR : slot;
+        bf16_t* dst = smem + slot * ROWE + pr_l[k];
+        *(VT*)dst = pf[k];
+        if constexpr (RING) *(VT*)(dst + HR * ROWE) = pf[k];
       }
     }
-    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < PFD; ++k) {
+      const int v = tid + k * 256;
+      if (v < M * CV) {
+        const int m = v / CV, cv = v - m * CV;
+        *(U2*)(ds + m * DPITCH + cv * 4) = pd[k];
+      }
+    }
+  };
+
+  int s = t0 / tiles_h, th = t0 - s * tiles_h;
+  load_tile(s, th, HR, th * TH - pad);
+  store_tile(HR, RING ? (th * TH) % HR : 0);
+  __syncthreads();
+  for (int t = t0; t < t1; ++t) {
+    int s2 = s, th2 = th + 1;
+    if (th2 >= tiles_h) { s2 = s + 1; th2 = 0; }
+    const bool has_next = t + 1 < t1;
+    const bool same_strip = s2 == s;
+    const int nrows2 = (RING && same_strip) ? TH : HR;
+    const int ih2 = (RING && same_strip) ? th2 * TH - pad + HR - TH : th2 * TH - pad;
+    const int slot2 = !RING ? 0 : same_strip ? (th2 * TH + HR - TH) % HR : (th2 * TH) % HR;
+    if (has_next) load_tile(s2, th2, nrows2, ih2);
+
+    const int wrow = RING ? (th * TH) % HR : 0;
+#pragma unroll 2
     for (int k0 = 0; k0 < M; k0 += 32) {
       // rows of the two tr-reads of this lane group: pixels k0 + 8g + q and k0 + 8g + 4 + q
       const int m0 = k0 + 8 * g + q, m1 = m0 + 4;
-      const int r0 = m0 / TW, c0 = m0 % TW, r1 = m1 / TW, c1 = m1 % TW;
+      const int r0 = m0 / TW + wrow, c0 = m0 % TW, r1 = m1 / TW + wrow, c1 = m1 % TW;
       bf16x8_t af[MF];
 #pragma unroll
       for (int i = 0; i < MF; ++i) {
@@ -499,10 +563,11 @@ __global__ __launch_bounds__(256) void conv_wgrad_halo_k(const bf16_t* __restric
         U4 v; v.x = a.x; v.y = a.y; v.z = b.x; v.w = b.y;
         af[i] = __builtin_bit_cast(bf16x8_t, v);
       }
+      const int h0 = (r0 * HC + c0) * PIX, h1 = (r1 * HC + c1) * PIX;
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int o0 = bcol[j] >= 0 ? (r0 * HC + c0) * PIX + boff[j] : HALO_ELEMS + DZ_ELEMS;
-        const int o1 = bcol[j] >= 0 ? (r1 * HC + c1) * PIX + boff[j] : HALO_ELEMS + DZ_ELEMS;
+      for (int j = 0; j < NB; ++j) {
+        const int o0 = bval[j] ? h0 + boff[j] : HALO_ELEMS + DZ_ELEMS;
+        const int o1 = bval[j] ? h1 + boff[j] : HALO_ELEMS + DZ_ELEMS;
         const s16x4_t lo = tr_read(smem + o0);
         const s16x4_t hi = tr_read(smem + o1);
         const U2 a = __builtin_bit_cast(U2, lo), b = __builtin_bit_cast(U2, hi);
@@ -512,13 +577,19 @@ __global__ __launch_bounds__(256) void conv_wgrad_halo_k(const bf16_t* __restric
         for (int i = 0; i < MF; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[i][j], 0, 0, 0);
       }
     }
+    if (!has_next) break;
+    __syncthreads();  // all reads of this tile done
+    store_tile(nrows2, slot2);
+    __syncthreads();
+    s = s2;
+    th = th2;
   }
   // epilogue: rows = co ((lane>>4)*4 + r), cols = kflat (lane & 15)
 #pragma unroll
   for (int i = 0; i < MF; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int kf = slice * 128 + (wid * 2 + j) * 16 + li;
+    for (int j = 0; j < NB; ++j) {
+      const int kf = slice * SLICE + (wid * NB + j) * 16 + li;
       if (kf >= KF) continue;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -619,16 +690,18 @@ static int fwd_by_cin(const void* x, const void* w, const float* bias, const flo
 
 template <int C, int KS, int TW, int TH, int MF>
 static int launch_wgrad(const void* x, const void* dz, float* dw, int N, int H, int W, int Cout, int pad, hipStream_t s) {
+  constexpr bool RING = TH < 2 * (KS - 1);
+  constexpr int KF = KS * KS * C;
+  constexpr int NB = KF > 512 ? 4 : 2;
+  const auto kern = conv_wgrad_strip_k<C, KS, TW, TH, MF, NB, RING>;
+  static const int resident = resident_blocks((const void*)kern);
   const int th = (H + TH - 1) / TH, tw = (W + TW - 1) / TW;
-  const int tiles = N * th * tw;
-  const int KF = KS * KS * C;
-  const int nslices = (KF + 127) / 128;
-  int chunks = (1024 + nslices - 1) / nslices;
-  if (chunks > tiles) chunks = tiles;
-  const int tpb = (tiles + chunks - 1) / chunks;
-  chunks = (tiles + tpb - 1) / tpb;
-  hipLaunchKernelGGL((conv_wgrad_halo_k<C, KS, TW, TH, MF>), dim3(chunks * nslices), dim3(256), 0, s,
-                     (const bf16_t*)x, (const bf16_t*)dz, dw, N, H, W, Cout, pad, th, tw, tpb, nslices);
+  const long tiles = (long)N * tw * th;
+  const int nslices = (KF + 64 * NB - 1) / (64 * NB);
+  int chunks = (resident + nslices - 1) / nslices;
+  if (chunks > tiles) chunks = (int)tiles;
+  hipLaunchKernelGGL(kern, dim3(chunks * nslices), dim3(256), 0, s, (const bf16_t*)x, (const bf16_t*)dz, dw, N, H, W,
+                     Cout, pad, th, tw, nslices);
   PTG_RETURN_LAUNCH();
 }
 

@@ -158,7 +158,7 @@ def test_conv_halo_fwd(N, H, W, C, Co, KS, epi):
         _close(aux, ar, 2e-2, 2e-2, "halo_prelu")
 
 
-@pytest.mark.parametrize("N,H,W,C,Co,KS", HALO_CASES)
+@pytest.mark.parametrize("N,H,W,C,Co,KS", HALO_CASES + BIG_HALO)
 def test_conv_halo_wgrad(N, H, W, C, Co, KS):
     x, dz = rnd(N, H, W, C), rnd(N, H, W, Co, scale=0.1)
     pad = KS // 2
@@ -169,7 +169,7 @@ def test_conv_halo_wgrad(N, H, W, C, Co, KS):
     _close(out, ref, 1e-3, 1e-3, "halo_wgrad")
 
 
-@pytest.mark.parametrize("N,H,W,C,Co,KS", [c for c in HALO_CASES if c[4] in K.HALO_C and c[3] % 8 == 0])
+@pytest.mark.parametrize("N,H,W,C,Co,KS", [c for c in HALO_CASES + BIG_HALO if c[4] in K.HALO_C and c[3] % 8 == 0])
 def test_conv_halo_dgrad(N, H, W, C, Co, KS):
     dz, w = rnd(N, H, W, Co), rnd(Co, KS, KS, C, scale=0.2)
     pad = KS // 2
