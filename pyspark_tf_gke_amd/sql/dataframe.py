@@ -456,7 +456,7 @@ class DataFrame:
     def rdd(self):
         from .rdd import RDD
 
-        return RDD.from_rows(self.sparkSession.sparkContext, self.collect())
+        return RDD.from_list(self.sparkSession.sparkContext, self.collect(), max(1, self._num_partitions))
 
     @property
     def na(self):

@@ -4,10 +4,15 @@
   parses only its contiguous range of records (parallel ingest), string columns are
   dictionary-encoded and the dictionaries unified across ranks (spark_workload_to_cloud_k8s.py:48).
 * ``format("jdbc")``: the reference reads MySQL over JDBC with
-  partitionColumn/lowerBound/upperBound/numPartitions (google_health_SQL.py:26-37).  There is no
-  database here; the JDBC source resolves ``dbtable`` to a CSV/Parquet file (``url`` =
-  ``file:<dir>`` or option ``path``) and keeps the range-partition semantics — partitioned on the
-  column's real min/max, which fixes the reference's all-rows-in-partition-0 skew.
+  partitionColumn/lowerBound/upperBound/numPartitions (google_health_SQL.py:26-37).  The runtime
+  ships no MySQL; a real SQL source is SQLite (stdlib): ``jdbc:sqlite:<file>``, or a
+  ``jdbc:mysql://host:port/<db>`` URL resolved to ``$PTG_JDBC_ROOT/<db>.sqlite`` (written by
+  ``workloads/raw-spark/load_csv.py``).  Partitioned reads follow Spark's JDBC column partitioning
+  exactly (stride from the bounds; the first partition also takes ``< lower`` and NULLs, the last
+  ``>= upper``) and the partitions are read in parallel, round-robin over the executor ranks.  Option
+  ``adaptiveBounds=true`` uses the column's real min/max instead (fixes the reference's
+  all-rows-in-partition-0 skew).  Without a database file, ``dbtable`` resolves to an
+  exported CSV/Parquet file (``url`` = ``file:<dir>`` or option ``path``).
 * Parquet (pyarrow for the file format only), text, JSON lines.
 * Writer: one ``part-<rank>-<uuid>.parquet`` / ``.csv`` per rank + ``_SUCCESS``; modes
   overwrite / append / error / ignore.
@@ -257,6 +262,9 @@ class DataFrameReader:
     def _jdbc(self):
         url = str(self._opts.get("url", ""))
         table = self._opts.get("dbtable")
+        db = _sqlite_for_url(url)
+        if db is not None:
+            return self._jdbc_sqlite(db, table)
         base = self._opts.get("path") or os.environ.get("PTG_JDBC_ROOT")
         if url.startswith("file:"):
             base = url[5:]
@@ -279,6 +287,82 @@ class DataFrameReader:
         if pc:
             df._num_partitions = int(self._opts.get("numPartitions") or df._num_partitions)
         return df
+
+
+    def _jdbc_sqlite(self, path, table):
+        import sqlite3
+
+        from .session import SparkSession  # noqa: F401  (type context)
+
+        con = sqlite3.connect(f"file:{path}?mode=ro", uri=True)
+        try:
+            src = table if str(table).lstrip().startswith("(") else f'"{table}"'
+            cur = con.execute(f"SELECT * FROM {src} LIMIT 0")
+            names = [d[0] for d in cur.description]
+            decl = {}
+            if not str(table).lstrip().startswith("("):
+                decl = {r[1]: r[2] for r in con.execute(f'PRAGMA table_info("{table}")')}
+            types = [T.from_sql_decl(decl.get(n, "")) for n in names]
+            pc = self._opts.get("partitionColumn")
+            w, r = comm.world_size(), comm.rank()
+            if pc:
+                n = max(1, int(self._opts.get("numPartitions") or 1))
+                lo, hi = int(self._opts.get("lowerBound")), int(self._opts.get("upperBound"))
+                if self._truthy(self._opts.get("adaptiveBounds", False)):
+                    mn, mx = con.execute(f'SELECT MIN("{pc}"), MAX("{pc}") FROM {src}').fetchone()
+                    if mn is not None:
+                        lo, hi = int(mn), int(mx) + 1
+                wheres = jdbc_partition_predicates(pc, lo, hi, n)
+                mine = [wh for i, wh in enumerate(wheres) if i % w == r]
+            else:
+                n = 1
+                mine = ["1=1"] if r == 0 else []
+            rows = []
+            for wh in mine:
+                rows += con.execute(f"SELECT * FROM {src} WHERE {wh}").fetchall()
+        finally:
+            con.close()
+        schema = T.StructType([T.StructField(nm, tp) for nm, tp in zip(names, types)])
+        df = self._s.createDataFrame(rows, schema, _local=True)
+        t = df._t
+        df = DataFrame(Table({nm: unify_dictionary(c) for nm, c in t.columns.items()}, t.num_rows, t.device), self._s)
+        df._num_partitions = n
+        return df
+
+
+def jdbc_partition_predicates(column: str, lower: int, upper: int, n: int) -> list:
+    """WHERE clauses of Spark's JDBC column partitioning (JDBCRelation.columnPartition)."""
+    if n <= 1 or upper - lower < 1:
+        return ["1=1"]
+    n = min(n, upper - lower)
+    stride = upper // n - lower // n
+    cur, out = lower, []
+    for i in range(n):
+        lb = f'"{column}" >= {cur}' if i != 0 else None
+        cur += stride
+        ub = f'"{column}" < {cur}' if i != n - 1 else None
+        if ub is None:
+            out.append(lb)
+        elif lb is None:
+            out.append(f'{ub} OR "{column}" IS NULL')
+        else:
+            out.append(f"{lb} AND {ub}")
+    return out
+
+
+def _sqlite_for_url(url: str):
+    """jdbc:sqlite:<file> -> file; jdbc:mysql://host:port/<db> -> $PTG_JDBC_ROOT/<db>.sqlite if present."""
+    if url.startswith("jdbc:sqlite:"):
+        return url[len("jdbc:sqlite:"):]
+    if url.startswith("jdbc:mysql://"):
+        rest = url[len("jdbc:mysql://"):]
+        dbname = rest.split("/", 1)[1].split("?", 1)[0] if "/" in rest else ""
+        root = os.environ.get("PTG_JDBC_ROOT")
+        if root and dbname:
+            cand = os.path.join(root, f"{dbname}.sqlite")
+            if os.path.exists(cand):
+                return cand
+    return None
 
 
 def _expand(path, exts=None):

@@ -78,6 +78,8 @@ class ColumnVector:
         out = []
         if isinstance(self.dtype, T.BooleanType):
             return [bool(x) if v else None for x, v in zip(arr, valid)]
+        if isinstance(self.dtype, T.TimestampType):
+            return [T.micros_to_datetime(int(x)) if v else None for x, v in zip(arr, valid)]
         if isinstance(self.dtype, (T.IntegerType, T.LongType)):
             return [int(x) if v else None for x, v in zip(arr, valid)]
         for x, v in zip(arr, valid):
@@ -208,8 +210,10 @@ def column_from_python(values: list, dtype: T.DataType | None, device) -> Column
     if isinstance(dtype, T.VectorUDT):
         arr = np.stack([np.asarray(getattr(v, "toArray", lambda: v)(), dtype=np.float32) for v in values])
         return ColumnVector(torch.from_numpy(arr).to(device), dtype)
+    if isinstance(dtype, T.TimestampType):
+        values = [T.to_micros(v) for v in values]
     npdt = {T.IntegerType: np.int32, T.LongType: np.int64, T.DoubleType: np.float64, T.FloatType: np.float32,
-            T.BooleanType: np.bool_}[type(dtype)]
+            T.BooleanType: np.bool_, T.TimestampType: np.int64}[type(dtype)]
     arr = np.array([(v if v is not None else 0) for v in values], dtype=npdt)
     v = torch.from_numpy(valid).to(device) if not valid.all() else None
     return ColumnVector(torch.from_numpy(arr).to(device), dtype, v)

@@ -2,6 +2,8 @@
 strings, integers/longs and doubles; ML adds vectors)."""
 from __future__ import annotations
 
+import datetime
+
 import torch
 
 
@@ -56,8 +58,32 @@ class BooleanType(DataType):
 
 
 class TimestampType(DataType):
+    """Microseconds since the Unix epoch (UTC), int64 on device (Spark's internal representation)."""
     simple = "timestamp"
     torch_dtype = torch.int64
+
+
+_EPOCH = datetime.datetime(1970, 1, 1)
+
+
+def to_micros(v):
+    """datetime / ISO string ('YYYY-MM-DD HH:MM:SS[.ffffff]') / number -> epoch microseconds."""
+    if v is None:
+        return None
+    if isinstance(v, (int, float)):
+        return int(v)
+    if isinstance(v, str):
+        v = datetime.datetime.fromisoformat(v.strip())
+    if isinstance(v, datetime.datetime):
+        if v.tzinfo is not None:
+            v = v.astimezone(datetime.timezone.utc).replace(tzinfo=None)
+        d = v - _EPOCH
+        return (d.days * 86400 + d.seconds) * 1_000_000 + d.microseconds
+    raise TypeError(f"cannot convert {v!r} to a timestamp")
+
+
+def micros_to_datetime(us: int) -> datetime.datetime:
+    return _EPOCH + datetime.timedelta(microseconds=int(us))
 
 
 class VectorUDT(DataType):
@@ -113,6 +139,26 @@ class StructType:
 
 
 NUMERIC = (IntegerType, LongType, DoubleType, FloatType, BooleanType)
+
+
+def from_sql_decl(decl: str) -> DataType:
+    """SQL column declaration -> Spark type, following Spark's JDBC type mapping
+    (INT -> int, BIGINT -> bigint, FLOAT/REAL -> float, DOUBLE -> double, DECIMAL -> double here,
+    VARCHAR/TEXT -> string, TIMESTAMP/DATETIME -> timestamp, BOOLEAN -> boolean)."""
+    d = (decl or "").upper()
+    if "BIGINT" in d:
+        return LongType()
+    if "INT" in d:
+        return IntegerType()
+    if "DOUBLE" in d or "DEC" in d or "NUMERIC" in d:
+        return DoubleType()
+    if "FLOAT" in d or "REAL" in d:
+        return FloatType()
+    if "BOOL" in d:
+        return BooleanType()
+    if "TIMESTAMP" in d or "DATETIME" in d:
+        return TimestampType()
+    return StringType()
 
 
 def from_torch(dt: torch.dtype) -> DataType:
