@@ -31,7 +31,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="cnn_b1", choices=["cnn_b1", "groupby", "mlp", "cnn_a1", "mnist"])
-    ap.add_argument("--batch-size", type=int, default=int(os.environ.get("PTG_BENCH_BATCH", "128")),
+    ap.add_argument("--batch-size", type=int, default=int(os.environ.get("PTG_BENCH_BATCH", "256")),
                     help="per-GPU batch (weak scaling)")
     ap.add_argument("--rows", type=int, default=1_000_000_000, help="groupby: total rows")
     ap.add_argument("--keys", type=int, default=1_000_000, help="groupby: distinct keys")
