@@ -30,7 +30,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="cnn_b1", choices=["cnn_b1", "groupby", "mlp", "cnn_a1", "mnist"])
+    ap.add_argument("--workload", default="cnn_b1", choices=["cnn_b1", "groupby", "mlp", "cnn_a1", "mnist", "resnet50"])
     ap.add_argument("--batch-size", type=int, default=int(os.environ.get("PTG_BENCH_BATCH", "256")),
                     help="per-GPU batch (weak scaling)")
     ap.add_argument("--rows", type=int, default=1_000_000_000, help="groupby: total rows")
@@ -47,6 +47,7 @@ def _sync():
 
 def bench_cnn(args, strategy, rank, world):
     from pyspark_tf_gke_amd.models import build_cnn_a1, build_cnn_model, build_mnist_cnn
+    from pyspark_tf_gke_amd.models.resnet import build_resnet50
     from pyspark_tf_gke_amd.parallel import comm
 
     dev = strategy.device
@@ -64,6 +65,11 @@ def bench_cnn(args, strategy, rank, world):
             name, cfg_model = "samples/sec TF CNN train", "CNN-A1 (3-conv 32/64/128 + GAP, 4.86M params)"
             xs = [torch.rand((B, 256, 320, 3), generator=g, device=dev) for _ in range(2)]
             ys = [torch.rand((B, 2), generator=g, device=dev) * 256 for _ in range(2)]
+        elif args.workload == "resnet50":
+            model = build_resnet50()
+            name, cfg_model = "samples/sec TF ResNet-50 train", "ResNet-50 (keras.applications v1, 224x224x3, 1000 classes, 25.6M params)"
+            xs = [torch.rand((B, 224, 224, 3), generator=g, device=dev) for _ in range(2)]
+            ys = [torch.randint(0, 1000, (B,), generator=g, device=dev).to(torch.int32) for _ in range(2)]
         else:
             model = build_mnist_cnn()
             name, cfg_model = "samples/sec TF CNN train", "MNIST CNN (28x28x1, conv32/conv64/dense128)"
@@ -71,7 +77,7 @@ def bench_cnn(args, strategy, rank, world):
             ys = [torch.randint(0, 10, (B,), generator=g, device=dev).to(torch.int32) for _ in range(2)]
     # pre-pack the images once into the device input format (bf16 NHWC, channel-padded) so the
     # timed loop measures the training step, as a prefetching input pipeline would present it
-    first = model.ops[0]
+    first = model.first_op()
     xs = [first._prep_input(x, model.ws).clone() if args.workload != "mnist" else x for x in xs]
     stats = model._stats_buf()
 
@@ -97,9 +103,10 @@ def bench_cnn(args, strategy, rank, world):
     return {
         "metric": name, "value": round(value, 2), "unit": "samples/s", "ms_per_step": round(ms, 4),
         "config": {"model": cfg_model, "global_batch": B * world, "per_gpu_batch": B,
-                   "input": "256x320x3" if args.workload != "mnist" else "28x28x1",
+                   "input": {"mnist": "28x28x1", "resnet50": "224x224x3"}.get(args.workload, "256x320x3"),
                    "parallelism": f"dp{world}" + (" (MultiWorkerMirroredStrategy, RCCL all-reduce)" if world > 1 else ""),
-                   "optimizer": "Adam(1e-3) fused flat", "final_loss": round(logs["loss"], 4)},
+                   "optimizer": ("SGD(0.1, momentum 0.9)" if args.workload == "resnet50" else "Adam(1e-3)") + " fused flat",
+                   "final_loss": round(logs["loss"], 4)},
     }
 
 

@@ -1,0 +1,406 @@
+// BatchNormalization (training batch statistics and inference moving statistics), the
+// MaxPooling2D k x k / stride s / zero-padding pair of ResNet's stem, and bf16 tensor add.
+//
+// Keras ResNet-50 (BASELINE.json "raw-tf ResNet-50 MultiWorkerMirroredStrategy") is a chain of
+// Conv2D -> BatchNormalization -> ReLU blocks with a residual Add before the last ReLU of each
+// bottleneck.  The conv itself is an MFMA GEMM (gemm.hip); everything here is bandwidth-bound and
+// written for HBM3E: 16-byte bf16x8 vectors, per-channel coefficients computed ONCE by a tiny
+// finalize kernel so the big passes are a single FMA per element, and batch statistics reduced
+// block-locally (LDS) before a few spread-out fp32 atomics ([BN_G groups][C] partial sums) so no
+// channel address sees more than ~M/(rows_per_block * BN_G) atomics.
+//
+//   bn_stats_k        part[g][0|1][c] += sum z, sum z^2      (z = conv output, [M][C] bf16)
+//   bn_finalize_k     mean/var (or moving stats) -> scale = gamma*rstd, shift = beta - mean*scale;
+//                     moving-average update (Keras momentum convention, biased batch variance)
+//   bn_apply_k        y = act(z*scale + shift (+ residual))                      (bf16 out)
+//   bn_bwd_reduce_k   part[g][0|1][c] += sum g, sum g*z with g = dy * relu'(y)
+//   bn_bwd_finalize_k dgamma, dbeta (+= into the fp32 gradient buffer) and the per-channel affine
+//                     form dz = a*g + c1*z + c0 of the BN input gradient
+//   bn_bwd_apply_k    dz (bf16) and, for a fused residual Add, d(residual) = g
+//   maxpool_fwd_k     out = max over the k x k window of the zero-padded input; stores the argmax
+//                     window position (uint8) for the backward
+//   maxpool_bwd_k     gather form (each input pixel sums the dy of the <= ceil(k/s)^2 windows
+//                     whose argmax it is): deterministic, no atomics
+//   add_bf16_k        out = a + b
+#include "common.h"
+
+namespace {
+
+constexpr int BN_G = 64;
+
+// rows per block so that the grid has ~2048 blocks (>= 8 per CU) and every block has work
+inline int bn_rows_per_block(long M, int rpi) {
+  long r = (M + 2047) / 2048;
+  if (r < rpi) r = rpi;
+  r = (r + rpi - 1) / rpi * rpi;
+  return (int)r;
+}
+
+// Shared LDS reduction of per-thread [8] partials over the `rpi` row slots of each channel slot,
+// then one atomic per (channel, array) into the block's partial group.
+PTG_DEV void bn_flush(float (*red)[256][8], const float* s, const float* q, int tid, int cpt, int rpi,
+                      float* part, int C) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { red[0][tid][j] = s[j]; red[1][tid][j] = q[j]; }
+  __syncthreads();
+  if (tid < cpt) {
+    float as[8], aq[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { as[j] = 0.f; aq[j] = 0.f; }
+    for (int r = 0; r < rpi; ++r) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { as[j] += red[0][r * cpt + tid][j]; aq[j] += red[1][r * cpt + tid][j]; }
+    }
+    float* p = part + (long)(blockIdx.x % BN_G) * 2 * C;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      atomicAdd(p + tid * 8 + j, as[j]);
+      atomicAdd(p + C + tid * 8 + j, aq[j]);
+    }
+  }
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(256) void bn_stats_k(const bf16_t* __restrict__ z, long M, int C, int rpb,
+                                                  float* __restrict__ part) {
+  __shared__ float red[2][256][8];
+  const int tid = threadIdx.x, cpt = C >> 3, rpi = 256 / cpt;
+  const int slot = tid % cpt, rsub = tid / cpt;
+  float s[8], q[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { s[j] = 0.f; q[j] = 0.f; }
+  const long r0 = (long)blockIdx.x * rpb, r1 = min(M, r0 + rpb);
+  if (rsub < rpi) {
+    for (long r = r0 + rsub; r < r1; r += rpi) {
+      float f[8];
+      unpack8(*(const U4*)(z + r * C + slot * 8), f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { s[j] += f[j]; q[j] = fmaf(f[j], f[j], q[j]); }
+    }
+  }
+  bn_flush(red, s, q, tid, cpt, rpi, part, C);
+}
+
+__global__ __launch_bounds__(256) void bn_finalize_k(float* __restrict__ part, int C, long M,
+                                                     const float* __restrict__ gamma,
+                                                     const float* __restrict__ beta, float eps, float momentum,
+                                                     float* __restrict__ mmean, float* __restrict__ mvar,
+                                                     float* __restrict__ scale, float* __restrict__ shift,
+                                                     float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                     int training) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  float mean, var;
+  if (training) {
+    double s = 0.0, q = 0.0;
+    for (int g = 0; g < BN_G; ++g) {  // read and re-zero (the buffer is reused by the next pass)
+      float* p = part + (long)g * 2 * C;
+      s += p[c]; q += p[C + c]; p[c] = 0.f; p[C + c] = 0.f;
+    }
+    const double m = s / (double)M;
+    double v = q / (double)M - m * m;
+    mean = (float)m; var = (float)(v > 0.0 ? v : 0.0);
+    if (momentum >= 0.f && mmean) {
+      mmean[c] = mmean[c] * momentum + mean * (1.f - momentum);
+      mvar[c] = mvar[c] * momentum + var * (1.f - momentum);
+    }
+  } else {
+    mean = mmean[c]; var = mvar[c];
+  }
+  const float rstd = rsqrtf(var + eps);
+  const float sc = (gamma ? gamma[c] : 1.f) * rstd;
+  scale[c] = sc;
+  shift[c] = (beta ? beta[c] : 0.f) - mean * sc;
+  if (mean_out) { mean_out[c] = mean; rstd_out[c] = rstd; }
+}
+
+__global__ __launch_bounds__(256) void bn_apply_k(const bf16_t* __restrict__ z, const float* __restrict__ scale,
+                                                  const float* __restrict__ shift, const bf16_t* __restrict__ res,
+                                                  int relu, bf16_t* __restrict__ y, long n8, int C) {
+  const long stride = (long)gridDim.x * 256;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n8; i += stride) {
+    const int c0 = (int)((i * 8) % C);
+    float f[8], r[8];
+    unpack8(*(const U4*)(z + i * 8), f);
+    const float4 s0 = *(const float4*)(scale + c0), s1 = *(const float4*)(scale + c0 + 4);
+    const float4 h0 = *(const float4*)(shift + c0), h1 = *(const float4*)(shift + c0 + 4);
+    const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+    const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+    if (res) unpack8(*(const U4*)(res + i * 8), r);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float v = fmaf(f[j], sc[j], sh[j]);
+      if (res) v += r[j];
+      f[j] = relu ? fmaxf(v, 0.f) : v;
+    }
+    *(U4*)(y + i * 8) = pack8(f);
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_reduce_k(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
+                                                       const bf16_t* __restrict__ z, long M, int C, int rpb,
+                                                       int relu, float* __restrict__ part) {
+  __shared__ float red[2][256][8];
+  const int tid = threadIdx.x, cpt = C >> 3, rpi = 256 / cpt;
+  const int slot = tid % cpt, rsub = tid / cpt;
+  float s[8], q[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { s[j] = 0.f; q[j] = 0.f; }
+  const long r0 = (long)blockIdx.x * rpb, r1 = min(M, r0 + rpb);
+  if (rsub < rpi) {
+    for (long r = r0 + rsub; r < r1; r += rpi) {
+      const long off = r * C + slot * 8;
+      float g[8], zz[8];
+      unpack8(*(const U4*)(dy + off), g);
+      unpack8(*(const U4*)(z + off), zz);
+      if (relu) {
+        float yy[8];
+        unpack8(*(const U4*)(y + off), yy);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[j] = yy[j] > 0.f ? g[j] : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { s[j] += g[j]; q[j] = fmaf(g[j], zz[j], q[j]); }
+    }
+  }
+  bn_flush(red, s, q, tid, cpt, rpi, part, C);
+}
+
+// dz = gamma*rstd*(g - mean(g) - xhat*mean(g*xhat)) = a*g + c1*z + c0.
+// The preceding conv's bias gradient, sum(dz) = a*dbeta + M*(c1*mean + c0), is identically zero.
+__global__ __launch_bounds__(256) void bn_bwd_finalize_k(float* __restrict__ part, int C, long M,
+                                                         const float* __restrict__ gamma,
+                                                         const float* __restrict__ mean,
+                                                         const float* __restrict__ rstd,
+                                                         float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                         float* __restrict__ coef) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  double sg = 0.0, sgz = 0.0;
+  for (int g = 0; g < BN_G; ++g) {
+    float* p = part + (long)g * 2 * C;
+    sg += p[c]; sgz += p[C + c]; p[c] = 0.f; p[C + c] = 0.f;
+  }
+  const float m = mean[c], rs = rstd[c];
+  const float db = (float)sg;
+  const float dg = (float)((sgz - (double)m * sg) * rs);
+  if (dgamma) dgamma[c] += dg;
+  if (dbeta) dbeta[c] += db;
+  const float a = (gamma ? gamma[c] : 1.f) * rs;
+  const float invM = 1.f / (float)M;
+  const float c1 = -a * dg * rs * invM;
+  const float c0 = -a * db * invM - c1 * m;
+  coef[c] = a; coef[C + c] = c1; coef[2 * C + c] = c0;
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_apply_k(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
+                                                      const bf16_t* __restrict__ z, const float* __restrict__ coef,
+                                                      int relu, bf16_t* __restrict__ dz, bf16_t* __restrict__ dres,
+                                                      long n8, int C) {
+  const long stride = (long)gridDim.x * 256;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n8; i += stride) {
+    const int c0 = (int)((i * 8) % C);
+    float g[8], zz[8];
+    unpack8(*(const U4*)(dy + i * 8), g);
+    unpack8(*(const U4*)(z + i * 8), zz);
+    if (relu) {
+      float yy[8];
+      unpack8(*(const U4*)(y + i * 8), yy);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = yy[j] > 0.f ? g[j] : 0.f;
+    }
+    if (dres) *(U4*)(dres + i * 8) = pack8(g);
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = fmaf(coef[c0 + j], g[j], fmaf(coef[C + c0 + j], zz[j], coef[2 * C + c0 + j]));
+    *(U4*)(dz + i * 8) = pack8(o);
+  }
+}
+
+// -------------------------------------------------------------------------------------------------
+// MaxPooling2D(k, stride s) on a zero-padded (pad p each side) NHWC input; C % 8 == 0.
+// -------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void maxpool_fwd_k(const bf16_t* __restrict__ x, bf16_t* __restrict__ out,
+                                                     uint8_t* __restrict__ arg, int N, int H, int W, int C, int OH,
+                                                     int OW, int k, int s, int p) {
+  const int cv = C >> 3;
+  const long total = (long)N * OH * OW * cv;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int c8 = (int)(i % cv);
+    long t = i / cv;
+    const int ow = (int)(t % OW); t /= OW;
+    const int oh = (int)(t % OH);
+    const int n = (int)(t / OH);
+    float best[8];
+    int bi[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; bi[j] = 0; }
+    for (int kh = 0; kh < k; ++kh) {
+      const int ih = oh * s - p + kh;
+      for (int kw = 0; kw < k; ++kw) {
+        const int iw = ow * s - p + kw;
+        float f[8];
+        if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W) {
+          unpack8(*(const U4*)(x + (((long)n * H + ih) * W + iw) * C + c8 * 8), f);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] = 0.f;  // ZeroPadding2D semantics
+        }
+        const int pos = kh * k + kw;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (f[j] > best[j]) { best[j] = f[j]; bi[j] = pos; }
+      }
+    }
+    const long o = (((long)n * OH + oh) * OW + ow) * C + c8 * 8;
+    *(U4*)(out + o) = pack8(best);
+    if (arg) {
+      uint32_t lo = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((uint32_t)bi[3] << 24);
+      uint32_t hi = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((uint32_t)bi[7] << 24);
+      *(U2*)(arg + o) = U2{lo, hi};
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void maxpool_bwd_k(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ arg,
+                                                     bf16_t* __restrict__ dx, int N, int H, int W, int C, int OH,
+                                                     int OW, int k, int s, int p, int accum) {
+  const int cv = C >> 3;
+  const long total = (long)N * H * W * cv;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int c8 = (int)(i % cv);
+    long t = i / cv;
+    const int w = (int)(t % W); t /= W;
+    const int h = (int)(t % H);
+    const int n = (int)(t / H);
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    int oh_lo = h + p - k + 1; oh_lo = oh_lo <= 0 ? 0 : (oh_lo + s - 1) / s;
+    int oh_hi = (h + p) / s; if (oh_hi > OH - 1) oh_hi = OH - 1;
+    int ow_lo = w + p - k + 1; ow_lo = ow_lo <= 0 ? 0 : (ow_lo + s - 1) / s;
+    int ow_hi = (w + p) / s; if (ow_hi > OW - 1) ow_hi = OW - 1;
+    for (int oh = oh_lo; oh <= oh_hi; ++oh)
+      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+        const int pos = (h + p - oh * s) * k + (w + p - ow * s);
+        const long o = (((long)n * OH + oh) * OW + ow) * C + c8 * 8;
+        const U2 a = *(const U2*)(arg + o);
+        float g[8];
+        unpack8(*(const U4*)(dy + o), g);
+        const uint8_t* ab = (const uint8_t*)&a;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (ab[j] == pos) acc[j] += g[j];
+      }
+    const long xo = (((long)n * H + h) * W + w) * C + c8 * 8;
+    if (accum) {
+      float e[8];
+      unpack8(*(const U4*)(dx + xo), e);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += e[j];
+    }
+    *(U4*)(dx + xo) = pack8(acc);
+  }
+}
+
+__global__ __launch_bounds__(256) void add_bf16_k(const bf16_t* __restrict__ a, const bf16_t* __restrict__ b,
+                                                  bf16_t* __restrict__ out, long n8) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
+    float fa[8], fb[8];
+    unpack8(*(const U4*)(a + i * 8), fa);
+    unpack8(*(const U4*)(b + i * 8), fb);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) fa[j] += fb[j];
+    *(U4*)(out + i * 8) = pack8(fa);
+  }
+}
+
+static inline int ew_grid(long n8) {
+  long g = (n8 + 255) / 256;
+  if (g > 8192) g = 8192;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+extern "C" {
+
+// part: fp32 [BN_G][2][C], zero on entry (the finalize kernels re-zero it after reading).  C % 8 == 0 and C <= 2048.
+int ptg_bn_stats(const void* z, long M, int C, float* part, hipStream_t s) {
+  if (C % 8 || C > 2048 || M <= 0) return (int)hipErrorInvalidValue;
+  const int rpi = 256 / (C / 8);
+  const int rpb = bn_rows_per_block(M, rpi);
+  const int grid = ptg_ceil_div(M, rpb);
+  hipLaunchKernelGGL(bn_stats_k, dim3(grid), dim3(256), 0, s, (const bf16_t*)z, M, C, rpb, part);
+  PTG_RETURN_LAUNCH();
+}
+
+int ptg_bn_finalize(float* part, int C, long M, const float* gamma, const float* beta, float eps,
+                    float momentum, float* mmean, float* mvar, float* scale, float* shift, float* mean_out,
+                    float* rstd_out, int training, hipStream_t s) {
+  hipLaunchKernelGGL(bn_finalize_k, dim3(ptg_ceil_div(C, 256)), dim3(256), 0, s, part, C, M, gamma, beta, eps,
+                     momentum, mmean, mvar, scale, shift, mean_out, rstd_out, training);
+  PTG_RETURN_LAUNCH();
+}
+
+int ptg_bn_apply(const void* z, const float* scale, const float* shift, const void* res, int relu, void* y,
+                 long M, int C, hipStream_t s) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+  const long n8 = M * C / 8;
+  hipLaunchKernelGGL(bn_apply_k, dim3(ew_grid(n8)), dim3(256), 0, s, (const bf16_t*)z, scale, shift,
+                     (const bf16_t*)res, relu, (bf16_t*)y, n8, C);
+  PTG_RETURN_LAUNCH();
+}
+
+int ptg_bn_bwd_reduce(const void* dy, const void* y, const void* z, long M, int C, int relu, float* part,
+                      hipStream_t s) {
+  if (C % 8 || C > 2048 || M <= 0) return (int)hipErrorInvalidValue;
+  const int rpi = 256 / (C / 8);
+  const int rpb = bn_rows_per_block(M, rpi);
+  hipLaunchKernelGGL(bn_bwd_reduce_k, dim3(ptg_ceil_div(M, rpb)), dim3(256), 0, s, (const bf16_t*)dy,
+                     (const bf16_t*)y, (const bf16_t*)z, M, C, rpb, relu, part);
+  PTG_RETURN_LAUNCH();
+}
+
+int ptg_bn_bwd_finalize(float* part, int C, long M, const float* gamma, const float* mean, const float* rstd,
+                        float* dgamma, float* dbeta, float* coef, hipStream_t s) {
+  hipLaunchKernelGGL(bn_bwd_finalize_k, dim3(ptg_ceil_div(C, 256)), dim3(256), 0, s, part, C, M, gamma, mean, rstd,
+                     dgamma, dbeta, coef);
+  PTG_RETURN_LAUNCH();
+}
+
+int ptg_bn_bwd_apply(const void* dy, const void* y, const void* z, const float* coef, int relu, void* dz, void* dres,
+                     long M, int C, hipStream_t s) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+  const long n8 = M * C / 8;
+  hipLaunchKernelGGL(bn_bwd_apply_k, dim3(ew_grid(n8)), dim3(256), 0, s, (const bf16_t*)dy, (const bf16_t*)y,
+                     (const bf16_t*)z, coef, relu, (bf16_t*)dz, (bf16_t*)dres, n8, C);
+  PTG_RETURN_LAUNCH();
+}
+
+int ptg_maxpool_fwd(const void* x, void* out, void* arg, int N, int H, int W, int C, int OH, int OW, int k, int st,
+                    int p, hipStream_t s) {
+  if (C % 8 || k > 15) return (int)hipErrorInvalidValue;
+  const long n8 = (long)N * OH * OW * C / 8;
+  hipLaunchKernelGGL(maxpool_fwd_k, dim3(ew_grid(n8)), dim3(256), 0, s, (const bf16_t*)x, (bf16_t*)out,
+                     (uint8_t*)arg, N, H, W, C, OH, OW, k, st, p);
+  PTG_RETURN_LAUNCH();
+}
+
+int ptg_maxpool_bwd(const void* dy, const void* arg, void* dx, int N, int H, int W, int C, int OH, int OW, int k,
+                    int st, int p, int accum, hipStream_t s) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+  const long n8 = (long)N * H * W * C / 8;
+  hipLaunchKernelGGL(maxpool_bwd_k, dim3(ew_grid(n8)), dim3(256), 0, s, (const bf16_t*)dy, (const uint8_t*)arg,
+                     (bf16_t*)dx, N, H, W, C, OH, OW, k, st, p, accum);
+  PTG_RETURN_LAUNCH();
+}
+
+int ptg_add_bf16(const void* a, const void* b, void* out, long n, hipStream_t s) {
+  if (n % 8) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(add_bf16_k, dim3(ew_grid(n / 8)), dim3(256), 0, s, (const bf16_t*)a, (const bf16_t*)b,
+                     (bf16_t*)out, n / 8);
+  PTG_RETURN_LAUNCH();
+}
+
+}  // extern "C"

@@ -154,13 +154,26 @@ struct ConvWgradB {
 // ------------------------------------------------------------------------------------------
 enum { ACT_NONE = 0, ACT_RELU = 1 };
 
-struct EpiBf16 {  // out[m*ldc+n] = act(acc + bias[n]) as bf16 (optionally also fp32)
-  bf16_t* out; long ldc; const float* bias; int act; float* out32;
+struct EpiBf16 {  // out[m*ldc+n] = act(acc + bias[n]) (+ out if accum) as bf16 (optionally also fp32)
+  bf16_t* out; long ldc; const float* bias; int act; float* out32; int accum;
   PTG_DEV void operator()(int m, int n, float v) const {
     if (bias) v += bias[n];
     if (act == ACT_RELU) v = fmaxf(v, 0.f);
-    out[(long)m * ldc + n] = f2bf(v);
+    bf16_t* p = out + (long)m * ldc + n;
+    if (accum) v += bf2f(*p);
+    *p = f2bf(v);
     if (out32) out32[(long)m * ldc + n] = v;
+  }
+};
+// Strided scatter (dgrad of a 1x1 stride-s conv): GEMM row m = output pixel (n, oh, ow) lands on
+// input pixel (n, oh*s, ow*s) of an [N][H][W][ldc] tensor; the other input pixels are untouched.
+struct EpiBf16Remap {
+  bf16_t* out; long ldc; int OH, OW, H, W, s, accum;
+  PTG_DEV void operator()(int m, int n, float v) const {
+    const int ohw = OH * OW, b = m / ohw, rem = m - b * ohw, oh = rem / OW, ow = rem - oh * OW;
+    bf16_t* p = out + (((long)b * H + oh * s) * W + ow * s) * ldc + n;
+    if (accum) v += bf2f(*p);
+    *p = f2bf(v);
   }
 };
 struct EpiF32 {  // out[m*ldc+n] (=|+=) act(acc + bias)
@@ -354,7 +367,7 @@ extern "C" {
 //   a_kcontig: A(m,k) = A[m*lda + k]  else A(m,k) = A[k*lda + m]
 //   b_kcontig: B(k,n) = B[n*ldb + k]  else B(k,n) = B[k*ldb + n]
 //   epi: 0 = bf16 store (+bias, act); 1 = fp32 store (+bias, act); 2 = fp32 accumulate (+=);
-//        3 = fp32 atomic add (split-K; caller zeroes C)
+//        3 = fp32 atomic add (split-K; caller zeroes C); 4 = bf16 accumulate (C += A.B)
 int ptg_gemm_bf16(int M, int N, int K, const void* A, long lda, int a_kcontig, const void* B, long ldb,
                   int b_kcontig, int epi, void* C, long ldc, const float* bias, int act, int splits,
                   hipStream_t s) {
@@ -363,8 +376,10 @@ int ptg_gemm_bf16(int M, int N, int K, const void* A, long lda, int a_kcontig, c
   const bf16_t* a = (const bf16_t*)A; const bf16_t* b = (const bf16_t*)B;
 #define PTG_EPI_SWITCH(LAX, LBX)                                                                 \
   switch (epi) {                                                                                 \
-    case 0: return dispatch_gemm(LAX, LBX, EpiBf16{(bf16_t*)C, ldc, bias, act, nullptr}, M, N, K, \
-                                 1, s);                                                          \
+    case 0: return dispatch_gemm(LAX, LBX, EpiBf16{(bf16_t*)C, ldc, bias, act, nullptr, 0}, M, N, \
+                                 K, 1, s);                                                       \
+    case 4: return dispatch_gemm(LAX, LBX, EpiBf16{(bf16_t*)C, ldc, bias, act, nullptr, 1}, M, N, \
+                                 K, 1, s);                                                       \
     case 1: return dispatch_gemm(LAX, LBX, EpiF32{(float*)C, ldc, bias, act, 0}, M, N, K, 1, s); \
     case 2: return dispatch_gemm(LAX, LBX, EpiF32{(float*)C, ldc, bias, act, 1}, M, N, K, 1, s); \
     case 3: return dispatch_gemm(LAX, LBX, EpiAtomic{(float*)C, ldc}, M, N, K, splits, s);       \
@@ -397,7 +412,7 @@ int ptg_conv2d_fwd(const void* x, const void* w, const float* bias, void* z, int
                    hipStream_t s) {
   if (!is_pow2(C) || C < 4) return (int)hipErrorInvalidValue;
   const int M = N * OH * OW, Kc = KH * KW * C;
-  EpiBf16 epi{(bf16_t*)z, Cout, bias, act, nullptr};
+  EpiBf16 epi{(bf16_t*)z, Cout, bias, act, nullptr, 0};
   if (C % 8 == 0) {
     ConvFwdA<8> la{(const bf16_t*)x, H, W, C, ilog2(C), OH, OW, KW, stride, pad, M, Kc};
     MatK<8> lb{(const bf16_t*)w, Kc, Cout, Kc};
@@ -412,13 +427,30 @@ int ptg_conv2d_fwd(const void* x, const void* w, const float* bias, void* z, int
 // Conv2D data gradient for stride-1 convolutions: dx = conv(dz, flip(w)^T, pad' = K-1-pad).
 // dz [N][H][W][Cout] (Cout power of two >= 8), dx [N][H][W][Cin] (Cin % 8 == 0).
 int ptg_conv2d_dgrad(const void* dz, const void* w, void* dx, int N, int H, int W, int Cin, int Cout,
-                     int KH, int KW, int pad, hipStream_t s) {
+                     int KH, int KW, int pad, int accum, hipStream_t s) {
   if (!is_pow2(Cout) || Cout < 8 || Cin % 8) return (int)hipErrorInvalidValue;
   const int M = N * H * W, Kc2 = KH * KW * Cout;
   ConvFwdA<8> la{(const bf16_t*)dz, H, W, Cout, ilog2(Cout), H, W, KW, 1, KH - 1 - pad, M, Kc2};
   ConvDgradB lb{(const bf16_t*)w, Cin, Cout, ilog2(Cout), KH, KW, Kc2};
-  EpiBf16 epi{(bf16_t*)dx, Cin, nullptr, ACT_NONE, nullptr};
+  EpiBf16 epi{(bf16_t*)dx, Cin, nullptr, ACT_NONE, nullptr, accum};
   return dispatch_gemm(la, lb, epi, M, Cin, Kc2, 1, s);
+}
+
+// Data gradient of a 1x1 convolution with stride s (pad 0): dx[n][oh*s][ow*s][ci] (+)= sum_co
+// dz[n][oh][ow][co] w[co][ci]; input pixels off the stride lattice get no contribution (the caller
+// zeroes dx once when s > 1 and this is the first gradient written into it).
+int ptg_conv1x1_dgrad(const void* dz, const void* w, void* dx, int N, int OH, int OW, int H, int W, int Cin,
+                      int Cout, int stride, int accum, hipStream_t s) {
+  if (Cin % 8 || Cout % 8) return (int)hipErrorInvalidValue;
+  const int M = N * OH * OW;
+  MatK<8> la{(const bf16_t*)dz, Cout, M, Cout};
+  MatMN lb{(const bf16_t*)w, Cin, Cin, Cout};
+  if (stride == 1) {
+    EpiBf16 epi{(bf16_t*)dx, Cin, nullptr, ACT_NONE, nullptr, accum};
+    return dispatch_gemm(la, lb, epi, M, Cin, Cout, 1, s);
+  }
+  EpiBf16Remap epi{(bf16_t*)dx, Cin, OH, OW, H, W, stride, accum};
+  return dispatch_gemm(la, lb, epi, M, Cin, Cout, 1, s);
 }
 
 // Conv2D weight gradient: dw[co][kc] (+)= sum_pixels dz[p][co] * im2col(x)[p][kc], fp32.

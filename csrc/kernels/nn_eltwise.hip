@@ -444,6 +444,31 @@ __global__ __launch_bounds__(256) void adam_k(float* __restrict__ p, const float
   }
 }
 
+// Fused flat SGD (+momentum, optional Nesterov), Keras convention:
+//   v = momentum*v - lr*g ; p += v            (nesterov: p += momentum*v - lr*g)
+__global__ __launch_bounds__(256) void sgd_k(float* __restrict__ p, const float* __restrict__ g,
+                                             float* __restrict__ vel, bf16_t* __restrict__ pbf, long n4, float lr,
+                                             float momentum, int nesterov, float gscale) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    float4 pp = ((float4*)p)[i];
+    const float4 gg = ((const float4*)g)[i];
+    float4 vv = vel ? ((float4*)vel)[i] : float4{0.f, 0.f, 0.f, 0.f};
+    float* P = &pp.x; const float* G = &gg.x; float* V = &vv.x;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float gj = G[j] * gscale;
+      V[j] = momentum * V[j] - lr * gj;
+      P[j] += nesterov ? momentum * V[j] - lr * gj : V[j];
+    }
+    ((float4*)p)[i] = pp;
+    if (vel) ((float4*)vel)[i] = vv;
+    if (pbf) {
+      U2 o; o.x = pack_bf(pp.x, pp.y); o.y = pack_bf(pp.z, pp.w);
+      ((U2*)pbf)[i] = o;
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void cast_f32_bf16_k(const float* __restrict__ x, bf16_t* __restrict__ y,
                                                        long n) {
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) y[i] = f2bf(x[i]);
@@ -667,6 +692,15 @@ int ptg_adam(float* p, const float* g, float* m, float* v, void* pbf, long n, fl
   const long n4 = n / 4;
   hipLaunchKernelGGL(adam_k, dim3(grid_for(n4)), dim3(256), 0, s, p, g, m, v, (bf16_t*)pbf, n4, lr_t, b1, b2,
                      eps, gscale);
+  PTG_RETURN_LAUNCH();
+}
+
+int ptg_sgd(float* p, const float* g, float* vel, void* pbf, long n, float lr, float momentum, int nesterov,
+            float gscale, hipStream_t s) {
+  if (n % 4) return (int)hipErrorInvalidValue;
+  const long n4 = n / 4;
+  hipLaunchKernelGGL(sgd_k, dim3(grid_for(n4)), dim3(256), 0, s, p, g, vel, (bf16_t*)pbf, n4, lr, momentum,
+                     nesterov, gscale);
   PTG_RETURN_LAUNCH();
 }
 

@@ -211,12 +211,8 @@ class ParameterServerStrategy(Strategy):
             return
         from ..ops import nn as K
 
-        opt.build(st)
         lo, hi = self.shard_range(model)
-        step = opt.iterations + 1
-        K.adam(st.flat[lo:hi], self._gshard, opt.m[lo:hi], opt.v[lo:hi], st.flat_bf16[lo:hi], opt.lr_t(step),
-               opt.beta_1, opt.beta_2, opt.epsilon, 1.0 / self.world_size)
-        opt.iterations = step
+        opt.apply_shard(st, self._gshard, lo, hi, 1.0 / self.world_size)
         comm.all_gather_flat(st.flat, st.flat[lo:hi].clone())
         K.cast_f32_bf16(st.flat, st.flat_bf16)
 

@@ -16,10 +16,24 @@ train_tf_ps.py:328-378 and the GradientTape step of :616-631 / :738-753.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from ..ops import nn as K
 from . import layers as L
+
+
+# Host-path debug precision: with PTG_HOST_FP32=1 (or ``host_fp32(True)``) CPU models keep their
+# "bf16" activations and compute-weight mirror in fp32, so the CPU engine can be checked against
+# an fp32 autograd oracle exactly (the GPU path is always bf16).
+_HOST_FP32 = [os.environ.get("PTG_HOST_FP32") == "1"]
+
+
+def host_fp32(enabled: bool | None = None) -> bool:
+    if enabled is not None:
+        _HOST_FP32[0] = bool(enabled)
+    return _HOST_FP32[0]
 
 
 class Workspace:
@@ -28,6 +42,8 @@ class Workspace:
 
     def get(self, key, shape, dtype, device, zero=False):
         shape = tuple(int(s) for s in shape)
+        if dtype == torch.bfloat16 and _HOST_FP32[0] and torch.device(device).type == "cpu":
+            dtype = torch.float32
         t = self.bufs.get(key)
         if t is None or tuple(t.shape) != shape or t.dtype != dtype or t.device != torch.device(device):
             t = (torch.zeros if zero else torch.empty)(shape, dtype=dtype, device=device)
@@ -54,7 +70,7 @@ class Op:
 
 
 def _bf16(x, ws, key):
-    if x.dtype == torch.bfloat16:
+    if x.dtype == torch.bfloat16 or (_HOST_FP32[0] and x.device.type == "cpu"):
         return x
     out = ws.get(key, x.shape, torch.bfloat16, x.device)
     out.copy_(x)

@@ -1,0 +1,342 @@
+"""Fused device ops of the functional-graph engine (:mod:`.functional`).
+
+* :class:`ConvBNOp` — ``Conv2D -> BatchNormalization [-> Add(residual)] [-> ReLU]`` (ResNet's
+  unit).  Forward: conv into bf16 ``z`` (1x1/stride-1 = plain MFMA GEMM over the NHWC pixel rows;
+  3x3 with C <= 64 = halo-tiled direct conv; otherwise implicit GEMM), batch statistics of ``z``
+  (``bn_stats``, training) or moving statistics (inference), then ONE apply pass
+  ``y = relu(z*scale + shift + residual)``.  Backward: one reduction pass (sum g, sum g*z with the
+  ReLU mask applied on the fly), a per-channel finalize that also writes d(gamma)/d(beta), one
+  apply pass producing ``dz`` and ``d(residual)``, then MFMA wgrad and dgrad of the conv.  The conv
+  bias gradient of a conv feeding a training-mode BN is identically zero (BN removes the mean), so
+  it is never computed.
+* :class:`BNOp`, :class:`MaxPoolOp` (k x k / stride s / folded zero padding), :class:`AddOp`.
+* :class:`Adapter` runs the Sequential engine's single-input ops (Dense, GAP, Flatten, PReLU...)
+  inside a graph.
+
+Gradient accumulation: ``backward(dy, ws, existing)`` receives the gradient buffers already
+produced for each input (a tensor with several consumers); the 1x1 and implicit-GEMM dgrads add
+into them inside the GEMM epilogue instead of running a separate add.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from ..ops import bn as KB
+from ..ops import nn as K
+from . import engine as E
+from . import layers as L
+
+
+def _bf16(x, ws, key):
+    return E._bf16(x, ws, key)
+
+
+class Adapter:
+    """Graph node around a single-input Sequential-engine op."""
+
+    def __init__(self, inner, inputs, output):
+        self.inner = inner
+        self.inputs = inputs
+        self.output = output
+        self.params = inner.params
+        self.name = inner.name
+
+    @property
+    def first(self):
+        return self.inner.first
+
+    @first.setter
+    def first(self, v):
+        self.inner.first = v
+
+    def forward(self, xs, ws, training):
+        inner = self.inner
+        if isinstance(inner, E.DenseOp) and inner.mask_for_prev:
+            inner._prev_y = inner._prev_op._y
+        return inner.forward(xs[0], ws, training)
+
+    def backward(self, dy, ws, existing):
+        return [self.inner.backward(dy, ws)]
+
+
+class GraphOp:
+    """Graph node around a multi-input fused op."""
+
+    def __init__(self, op, inputs, output):
+        self.op = op
+        self.inputs = inputs
+        self.output = output
+        self.params = op.params
+        self.name = op.name
+
+    @property
+    def first(self):
+        return self.op.first
+
+    @first.setter
+    def first(self, v):
+        self.op.first = v
+
+    def forward(self, xs, ws, training):
+        return self.op.forward(xs, ws, training)
+
+    def backward(self, dy, ws, existing):
+        return self.op.backward(dy, ws, existing)
+
+    def _prep_input(self, x, ws):
+        return self.op._prep_input(x, ws)
+
+
+# ------------------------------------------------------------------------------------------------
+# convolution dispatch (shared by ConvBNOp)
+# ------------------------------------------------------------------------------------------------
+def conv_forward(x, w, bias, stride, pad, z):
+    N, H, W, C = x.shape
+    Co, KH, KW, _ = w.shape
+    if not K.on_device(x):
+        return K.conv2d_fwd(x, w, bias, stride, pad, z, None)
+    if KH == KW == 1 and stride == 1 and pad == 0:
+        M = N * H * W
+        K.gemm(M, Co, C, x, C, 1, w, C, 1, 0, z, Co, bias, 0, 1)
+        return z
+    same = pad == KH // 2 and KH == KW and stride == 1
+    if K.halo_eligible(C, Co, KH, stride, same):
+        return K.conv2d_fwd_fused(x, w, bias, pad, z)
+    return K.conv2d_fwd(x, w, bias, stride, pad, z, None)
+
+
+def conv_wgrad(x, dz, stride, pad, dw):
+    """dw (fp32, already zeroed by the store) += d(conv)/dw."""
+    N, H, W, C = x.shape
+    _, OH, OW, Co = dz.shape
+    _, KH, KW, _ = dw.shape
+    if not K.on_device(x):
+        return K.conv2d_wgrad(x, dz, stride, pad, dw, accumulate=True)
+    if KH == KW == 1 and stride == 1 and pad == 0:
+        M = N * H * W
+        tiles = math.ceil(Co / 128) * math.ceil(C / 128)
+        splits = max(1, min(math.ceil(2048 / tiles), M // 256))
+        K.gemm(Co, C, M, dz, Co, 0, x, C, 0, 3, dw, C, None, 0, splits)
+        return dw
+    same = pad == KH // 2 and KH == KW and stride == 1
+    if K.halo_eligible(C, Co, KH, stride, same):
+        tmp = dw  # halo wgrad overwrites; dw was zeroed by the store for this step
+        return K.conv2d_wgrad_halo(x, dz, pad, tmp)
+    return K.conv2d_wgrad(x, dz, stride, pad, dw, accumulate=True)
+
+
+def conv_dgrad(dz, w, stride, pad, dx, accumulate, ws, key):
+    """dx (+)= d(conv)/dx.  Returns True when the result was accumulated into ``dx`` in place."""
+    Co, KH, KW, Cin = w.shape
+    if KH == KW == 1 and pad == 0:
+        K.conv1x1_dgrad(dz, w, stride, dx, accumulate)
+        return True
+    if stride != 1:
+        raise NotImplementedError("dgrad of a strided KxK (K > 1) convolution that is not the first layer")
+    same = pad == KH // 2 and KH == KW
+    if K.on_device(dz) and K.halo_eligible(Co, Cin, KH, 1, same) and not accumulate:
+        wf = ws.get(key + "/wflip", (Cin, KH, KW, Co), torch.bfloat16, dz.device)
+        K.conv2d_dgrad_halo(dz, w, pad, dx, wf)
+        return True
+    K.conv2d_dgrad(dz, w, pad, dx, accumulate)
+    return True
+
+
+class _BNState:
+    """Per-op BN scratch: statistics, coefficients, partial sums (zeroed by the finalize kernels)."""
+
+    def __init__(self, bn: L.BatchNormalization, name: str):
+        self.bn = bn
+        self.name = name
+
+    def bufs(self, ws, C, dev):
+        f = torch.float32
+        return (ws.get(self.name + "/bn_part", (KB.BN_G, 2, C), f, dev, zero=True),
+                ws.get(self.name + "/bn_scale", (C,), f, dev), ws.get(self.name + "/bn_shift", (C,), f, dev),
+                ws.get(self.name + "/bn_mean", (C,), f, dev), ws.get(self.name + "/bn_rstd", (C,), f, dev),
+                ws.get(self.name + "/bn_coef", (3, C), f, dev))
+
+    def forward(self, z, res, relu, y, ws, training):
+        bn = self.bn
+        C = z.shape[-1]
+        M = z.numel() // C
+        part, scale, shift, mean, rstd, _ = self.bufs(ws, C, z.device)
+        g = bn.gamma.data if bn.gamma is not None else None
+        b = bn.beta.data if bn.beta is not None else None
+        if training:
+            KB.bn_stats(z, part)
+        KB.bn_finalize(part, M, g, b, bn.epsilon, bn.momentum if training else -1.0, bn.moving_mean,
+                       bn.moving_variance, scale, shift, mean, rstd, training)
+        if not K.on_device(z) and training:
+            part.zero_()
+        return KB.bn_apply(z, scale, shift, res, relu, y)
+
+    def backward(self, dy, y, z, relu, dz, dres, ws):
+        bn = self.bn
+        C = z.shape[-1]
+        M = z.numel() // C
+        part, _, _, mean, rstd, coef = self.bufs(ws, C, z.device)
+        KB.bn_bwd_reduce(dy, y, z, relu, part)
+        KB.bn_bwd_finalize(part, M, bn.gamma.data if bn.gamma is not None else None, mean, rstd,
+                           bn.gamma.grad if bn.gamma is not None else None,
+                           bn.beta.grad if bn.beta is not None else None, coef)
+        if not K.on_device(z):
+            part.zero_()
+        return KB.bn_bwd_apply(dy, y, z, coef, relu, dz, dres)
+
+
+class ConvBNOp:
+    first = False
+
+    def __init__(self, conv: L.Conv2D, bn: L.BatchNormalization, relu: bool, residual: bool, extra_pad: int = 0):
+        self.conv, self.bn, self.relu, self.residual = conv, bn, relu, residual
+        self.params = list(conv.params) + list(bn.params)
+        self.stride = conv.strides[0]
+        if conv.strides[0] != conv.strides[1]:
+            raise NotImplementedError("non-square strides")
+        self.pad = conv.pad_amount() + extra_pad
+        self.name = conv.name
+        self.state = _BNState(bn, conv.name)
+        if conv.activation not in ("linear", None):
+            raise NotImplementedError("Conv2D(activation=...) followed by BatchNormalization")
+
+    def _prep_input(self, x, ws):
+        cp = self.conv.cin_p
+        if x.shape[-1] == cp and (x.dtype == torch.bfloat16 or (E.host_fp32() and not x.is_cuda)):
+            return x
+        xi = ws.get(self.name + "/xin", (*x.shape[:-1], cp), torch.bfloat16, x.device)
+        if x.shape[-1] == 3 and cp == 4 and x.dtype == torch.float32:
+            return K.pack_rgb4(x.contiguous(), xi)
+        xi.zero_()
+        xi[..., : x.shape[-1]] = x
+        return xi
+
+    def forward(self, xs, ws, training):
+        x = self._prep_input(xs[0], ws)
+        res = xs[1] if self.residual else None
+        if res is not None:
+            res = _bf16(res, ws, self.name + "/res16")
+        B = x.shape[0]
+        OH, OW, Co = self.conv.out_shape
+        dev = x.device
+        z = ws.get(self.name + "/z", (B, OH, OW, Co), torch.bfloat16, dev)
+        b = self.conv.bias.data if self.conv.bias is not None else None
+        conv_forward(x, self.conv.kernel.bf16, b, self.stride, self.pad, z)
+        y = ws.get(self.name + "/y", z.shape, torch.bfloat16, dev)
+        self.state.forward(z, res, self.relu, y, ws, training)
+        self._x, self._z, self._y = x, z, y
+        return y
+
+    def backward(self, dy, ws, existing):
+        x, z, y = self._x, self._z, self._y
+        dev = z.device
+        dy = _bf16(dy, ws, self.name + "/dy16")
+        dz = ws.get(self.name + "/dz", z.shape, torch.bfloat16, dev)
+        dres = ws.get(self.name + "/dres", z.shape, torch.bfloat16, dev) if self.residual else None
+        self.state.backward(dy, y, z, self.relu, dz, dres, ws)
+        conv_wgrad(x, dz, self.stride, self.pad, self.conv.kernel.grad)
+        dx = None
+        if not self.first:
+            ex = existing[0]
+            if ex is not None and ex.dtype == x.dtype and tuple(ex.shape) == tuple(x.shape):
+                conv_dgrad(dz, self.conv.kernel.bf16, self.stride, self.pad, ex, True, ws, self.name)
+                dx = ex
+            else:
+                dx = ws.get(self.name + "/dx", x.shape, torch.bfloat16, dev)
+                conv_dgrad(dz, self.conv.kernel.bf16, self.stride, self.pad, dx, False, ws, self.name)
+        return [dx] + ([dres] if self.residual else [])
+
+
+class BNOp:
+    """Standalone BatchNormalization [+ residual Add] [+ ReLU] (input not produced by a Conv2D)."""
+
+    first = False
+
+    def __init__(self, bn: L.BatchNormalization, relu: bool, residual: bool):
+        self.bn, self.relu, self.residual = bn, relu, residual
+        self.params = list(bn.params)
+        self.name = bn.name
+        self.state = _BNState(bn, bn.name)
+
+    def _prep_input(self, x, ws):
+        return _bf16(x, ws, self.name + "/x16")
+
+    def forward(self, xs, ws, training):
+        z = self._prep_input(xs[0], ws)
+        res = _bf16(xs[1], ws, self.name + "/res16") if self.residual else None
+        y = ws.get(self.name + "/y", z.shape, torch.bfloat16, z.device)
+        self.state.forward(z, res, self.relu, y, ws, training)
+        self._z, self._y = z, y
+        return y
+
+    def backward(self, dy, ws, existing):
+        z, y = self._z, self._y
+        dy = _bf16(dy, ws, self.name + "/dy16")
+        dz = ws.get(self.name + "/dz", z.shape, torch.bfloat16, z.device)
+        dres = ws.get(self.name + "/dres", z.shape, torch.bfloat16, z.device) if self.residual else None
+        self.state.backward(dy, y, z, self.relu, dz, dres, ws)
+        return [None if self.first else dz] + ([dres] if self.residual else [])
+
+
+class MaxPoolOp:
+    first = False
+
+    def __init__(self, layer: L.MaxPooling2D, pad: int = 0):
+        self.layer = layer
+        self.k, self.s, self.p = layer.pool_size[0], layer.strides[0], pad
+        self.params = []
+        self.name = layer.name
+
+    def forward(self, xs, ws, training):
+        x = _bf16(xs[0], ws, self.name + "/x16")
+        B, H, W, C = x.shape
+        OH, OW = KB.pool_out_size(H, self.k, self.s, self.p), KB.pool_out_size(W, self.k, self.s, self.p)
+        out = ws.get(self.name + "/y", (B, OH, OW, C), torch.bfloat16, x.device)
+        arg = ws.get(self.name + "/arg", (B, OH, OW, C), torch.uint8, x.device)
+        KB.maxpool_fwd(x, out, arg, self.k, self.s, self.p)
+        self._xshape, self._arg = x.shape, arg
+        return out
+
+    def backward(self, dy, ws, existing):
+        if self.first:
+            return [None]
+        dy = _bf16(dy, ws, self.name + "/dy16")
+        ex = existing[0]
+        if ex is not None and ex.dtype == dy.dtype and tuple(ex.shape) == tuple(self._xshape):
+            KB.maxpool_bwd(dy, self._arg, ex, self.k, self.s, self.p, accumulate=True)
+            return [ex]
+        dx = ws.get(self.name + "/dx", self._xshape, torch.bfloat16, dy.device)
+        KB.maxpool_bwd(dy, self._arg, dx, self.k, self.s, self.p)
+        return [dx]
+
+
+class AddOp:
+    first = False
+
+    def __init__(self, layer: L.Add, relu: bool):
+        self.layer, self.relu = layer, relu
+        self.params = []
+        self.name = layer.name
+
+    def forward(self, xs, ws, training):
+        a = _bf16(xs[0], ws, self.name + "/a16")
+        b = _bf16(xs[1], ws, self.name + "/b16")
+        y = ws.get(self.name + "/y", a.shape, torch.bfloat16, a.device)
+        KB.add_(a, b, y)
+        if self.relu:
+            K.relu_bwd(y, y, y)
+        self._y = y
+        return y
+
+    def backward(self, dy, ws, existing):
+        dy = _bf16(dy, ws, self.name + "/dy16")
+        if self.relu:
+            g = ws.get(self.name + "/g", dy.shape, torch.bfloat16, dy.device)
+            K.relu_bwd(dy, self._y, g)
+        else:
+            g = dy
+        g2 = ws.get(self.name + "/g2", g.shape, torch.bfloat16, g.device)
+        g2.copy_(g)  # each branch owns its gradient buffer (it may be accumulated into)
+        return [g, g2]

@@ -16,7 +16,7 @@ import re
 
 import numpy as np
 
-from .params import ParamStore, glorot_uniform, zeros
+from .params import ParamStore, glorot_uniform, ones, zeros
 
 _counters: dict = {}
 
@@ -52,6 +52,21 @@ class Layer:
         self.out_shape = self.compute_output_shape(self.in_shape)
         return self.out_shape
 
+    def __call__(self, inputs):
+        """Functional API: ``y = layer(x)`` records a graph node (see :class:`.functional.Model`)."""
+        from .functional import KerasTensor
+
+        ins = list(inputs) if isinstance(inputs, (list, tuple)) else [inputs]
+        ins = [t.output if isinstance(t, Input) else t for t in ins]
+        for t in ins:
+            if not isinstance(t, KerasTensor):
+                raise TypeError(f"{self.name}: functional call expects KerasTensors, got {type(t).__name__}")
+        if getattr(self, "_inbound", None) is not None:
+            raise NotImplementedError(f"layer {self.name} is already connected (shared layers are not supported)")
+        self._inbound = ins
+        shape = self.compute_output_shape(ins[0].shape if len(ins) == 1 else tuple(t.shape for t in ins))
+        return KerasTensor(tuple(shape), self, ins)
+
     def compute_output_shape(self, s):
         return s
 
@@ -73,9 +88,12 @@ class Input(Layer):
     keras_class = "InputLayer"
 
     def __init__(self, shape, name=None, dtype="float32"):
-        super().__init__(name or "input_layer")
+        super().__init__(name or _auto_name("input_layer"))
         self.shape = tuple(int(s) for s in shape)
         self.dtype = dtype
+        from .functional import KerasTensor
+
+        self.output = KerasTensor(self.shape, self, [])
 
     def get_config(self):
         return {"name": self.name, "batch_shape": [None, *self.shape], "dtype": self.dtype}
@@ -232,22 +250,137 @@ class PReLU(Layer):
         self.alpha.data.copy_(torch.from_numpy(ws[0]))
 
 
+def _pair(v):
+    return (int(v[0]), int(v[1])) if isinstance(v, (tuple, list)) else (int(v), int(v))
+
+
 class MaxPooling2D(Layer):
+    """Square windows, 'valid' padding (Keras pads explicitly with ZeroPadding2D, which the engine
+    folds into the pooling kernel).  2x2/stride 2 is the reference CNN's configuration
+    (train_tf_ps.py:353); 3x3/stride 2 is ResNet-50's stem."""
+
     kind = "MaxPooling2D"
     keras_class = "MaxPooling2D"
 
-    def __init__(self, pool_size=2, strides=None, name=None):
+    def __init__(self, pool_size=2, strides=None, padding="valid", name=None):
         super().__init__(name)
-        if pool_size not in (2, (2, 2)) or strides not in (None, 2, (2, 2)):
-            raise NotImplementedError("MaxPooling2D supports 2x2 / stride 2 (the reference's configuration)")
-        self.pool_size = (2, 2)
+        self.pool_size = _pair(pool_size)
+        self.strides = _pair(strides) if strides is not None else self.pool_size
+        if self.pool_size[0] != self.pool_size[1] or self.strides[0] != self.strides[1] or padding != "valid":
+            raise NotImplementedError("MaxPooling2D: square windows/strides with padding='valid'")
+        self.padding = padding
 
     def compute_output_shape(self, s):
         H, W, C = s
-        return (H // 2, W // 2, C)
+        k, st = self.pool_size[0], self.strides[0]
+        return ((H - k) // st + 1, (W - k) // st + 1, C)
 
     def get_config(self):
-        return {"name": self.name, "pool_size": [2, 2], "strides": [2, 2], "padding": "valid"}
+        return {"name": self.name, "pool_size": list(self.pool_size), "strides": list(self.strides),
+                "padding": "valid"}
+
+
+class ZeroPadding2D(Layer):
+    kind = "ZeroPadding2D"
+    keras_class = "ZeroPadding2D"
+
+    def __init__(self, padding=1, name=None):
+        super().__init__(name)
+        if isinstance(padding, (tuple, list)):
+            a, b = padding
+            if isinstance(a, (tuple, list)) or isinstance(b, (tuple, list)) or a != b:
+                raise NotImplementedError("ZeroPadding2D: symmetric padding only")
+            padding = a
+        self.pad = int(padding)
+
+    def compute_output_shape(self, s):
+        H, W, C = s
+        return (H + 2 * self.pad, W + 2 * self.pad, C)
+
+    def get_config(self):
+        return {"name": self.name, "padding": [[self.pad, self.pad], [self.pad, self.pad]]}
+
+
+class BatchNormalization(Layer):
+    """Keras BatchNormalization over the last (channel) axis.  gamma/beta are trainable parameters of
+    the flat store; moving_mean/moving_variance are non-trainable device buffers (updated during
+    training steps with ``momentum``)."""
+
+    kind = "BatchNormalization"
+    keras_class = "BatchNormalization"
+
+    def __init__(self, axis=-1, momentum=0.99, epsilon=1e-3, center=True, scale=True, name=None):
+        super().__init__(name)
+        if axis not in (-1, 3):
+            raise NotImplementedError("BatchNormalization over the channel (last) axis only")
+        self.momentum, self.epsilon = float(momentum), float(epsilon)
+        self.center, self.scale = center, scale
+        self.moving_mean = self.moving_variance = None
+
+    def build(self, in_shape, store):
+        super().build(in_shape, store)
+        C = int(in_shape[-1])
+        self.channels = C
+        self.params = []
+        self.gamma = store.add(f"{self.name}/gamma", (C,), ones) if self.scale else None
+        self.beta = store.add(f"{self.name}/beta", (C,), zeros) if self.center else None
+        self.params = [p for p in (self.gamma, self.beta) if p is not None]
+        return self.out_shape
+
+    def init_state(self, device) -> None:
+        import torch
+
+        if self.moving_mean is None or self.moving_mean.device != torch.device(device):
+            self.moving_mean = torch.zeros(self.channels, dtype=torch.float32, device=device)
+            self.moving_variance = torch.ones(self.channels, dtype=torch.float32, device=device)
+
+    def param_count(self) -> int:
+        return super().param_count() + 2 * self.channels
+
+    def non_trainable_count(self) -> int:
+        return 2 * self.channels
+
+    def get_config(self):
+        return {"name": self.name, "axis": -1, "momentum": self.momentum, "epsilon": self.epsilon,
+                "center": self.center, "scale": self.scale}
+
+    def keras_weights(self):
+        out = [p.data.detach().float().cpu().numpy().copy() for p in self.params]
+        out += [self.moving_mean.detach().cpu().numpy().copy(), self.moving_variance.detach().cpu().numpy().copy()]
+        return out
+
+    def set_keras_weights(self, ws):
+        import torch
+
+        for p, w in zip(self.params, ws):
+            p.data.copy_(torch.from_numpy(np.ascontiguousarray(w)))
+        self.moving_mean.copy_(torch.from_numpy(np.ascontiguousarray(ws[-2])))
+        self.moving_variance.copy_(torch.from_numpy(np.ascontiguousarray(ws[-1])))
+
+
+class Activation(Layer):
+    kind = "Activation"
+    keras_class = "Activation"
+
+    def __init__(self, activation, name=None):
+        super().__init__(name)
+        if activation not in ("relu", "linear", "softmax"):
+            raise NotImplementedError(f"Activation({activation!r})")
+        self.activation = activation
+
+    def get_config(self):
+        return {"name": self.name, "activation": self.activation}
+
+
+class Add(Layer):
+    kind = "Add"
+    keras_class = "Add"
+
+    def compute_output_shape(self, s):
+        shapes = s if isinstance(s[0], tuple) else (s,)
+        if any(tuple(x) != tuple(shapes[0]) for x in shapes):
+            raise ValueError(f"Add: shape mismatch {shapes}")
+        return tuple(shapes[0])
 
 
 class Flatten(Layer):
@@ -272,7 +405,8 @@ class ReLU(Layer):
 
 
 LAYER_CLASSES = {c.keras_class: c for c in (Input, Dense, Conv2D, PReLU, MaxPooling2D, Flatten,
-                                              GlobalAveragePooling2D, ReLU)}
+                                              GlobalAveragePooling2D, ReLU, ZeroPadding2D, BatchNormalization,
+                                              Activation, Add)}
 
 
 def layer_from_config(cls_name: str, cfg: dict) -> Layer:
@@ -287,10 +421,20 @@ def layer_from_config(cls_name: str, cfg: dict) -> Layer:
                       cfg.get("padding", "valid"), cfg.get("activation"), cfg.get("use_bias", True),
                       name=cfg.get("name"))
     if cls is MaxPooling2D:
-        return MaxPooling2D(name=cfg.get("name"))
+        return MaxPooling2D(tuple(cfg.get("pool_size", (2, 2))), tuple(cfg.get("strides", cfg.get("pool_size", (2, 2)))),
+                            name=cfg.get("name"))
+    if cls is ZeroPadding2D:
+        pad = cfg.get("padding", 1)
+        return ZeroPadding2D(pad[0][0] if isinstance(pad, (list, tuple)) else pad, name=cfg.get("name"))
+    if cls is BatchNormalization:
+        return BatchNormalization(momentum=cfg.get("momentum", 0.99), epsilon=cfg.get("epsilon", 1e-3),
+                                  center=cfg.get("center", True), scale=cfg.get("scale", True), name=cfg.get("name"))
+    if cls is Activation:
+        return Activation(cfg["activation"], name=cfg.get("name"))
     return cls(name=cfg.get("name"))
 
 
 __all__ = ["Layer", "Input", "Dense", "Conv2D", "PReLU", "MaxPooling2D", "Flatten", "GlobalAveragePooling2D",
-           "ReLU", "layer_from_config", "reset_name_counters"]
+           "ReLU", "ZeroPadding2D", "BatchNormalization", "Activation", "Add", "layer_from_config",
+           "reset_name_counters"]
 

@@ -157,10 +157,23 @@ class Sequential:
     def _configure_loss(self):
         if not self.built or self.loss is None:
             return
-        last = self.ops[-1]
+        last = self._last_op()
         if isinstance(self.loss, LS.SparseCategoricalCrossentropy) and isinstance(last, E.DenseOp):
             # softmax is folded into the fused softmax-crossentropy kernel
             last.logits_only = last.act == "softmax" or self.loss.from_logits
+
+    # ---------------------------------------------------------------- execution plan hooks
+    def _run_forward(self, xb, training: bool):
+        return E.run_forward(self.ops, xb, self.ws, training)
+
+    def _run_backward(self, dpred, on_op_done=None):
+        return E.run_backward(self.ops, dpred, self.ws, on_op_done=on_op_done)
+
+    def _last_op(self):
+        return self.ops[-1]
+
+    def first_op(self):
+        return self.ops[0]
 
     # ---------------------------------------------------------------- device helpers
     def _to_device(self, a, dtype=None):
@@ -210,13 +223,13 @@ class Sequential:
         if not self.built:
             self.build()
         xb = self._to_device(x, self._x_dtype(x))
-        out = E.run_forward(self.ops, xb, self.ws, training)
+        out = self._run_forward(xb, training)
         from .tape import _active_tape
 
         tape = _active_tape()
         if tape is not None:
             tape.record_forward(self, out)
-        if isinstance(self.ops[-1], E.DenseOp) and self.ops[-1].logits_only:
+        if isinstance(self._last_op(), E.DenseOp) and self._last_op().logits_only:
             out = torch.softmax(out.float(), -1)
         return out
 
@@ -243,7 +256,7 @@ class Sequential:
         """Backward from d(loss)/d(output) + gradient sync + optimizer update."""
         st = strategy
         hook = st.on_op_grads_ready if st is not None else None
-        E.run_backward(self.ops, dpred, self.ws, on_op_done=(lambda op: hook(self, op)) if hook else None)
+        self._run_backward(dpred, on_op_done=(lambda op: hook(self, op)) if hook else None)
         if st is not None:
             st.finish_gradients(self)
             st.apply_update(self)
@@ -255,7 +268,7 @@ class Sequential:
         st = self._strategy()
         stats = self._stats_buf() if stats is None else stats
         self.store.zero_grad()
-        out = E.run_forward(self.ops, xb, self.ws, True)
+        out = self._run_forward(xb, True)
         dpred = self._loss_grad(out, yb, stats)
         self.backward_and_update(dpred, st)
 
@@ -268,7 +281,7 @@ class Sequential:
         return logs if return_dict else [logs["loss"]] + [logs[m] for m in self.metric_names if m in logs]
 
     def test_step(self, xb, yb, stats) -> None:
-        out = E.run_forward(self.ops, xb, self.ws, False)
+        out = self._run_forward(xb, False)
         self._loss_grad(out, yb, stats)
 
     # ---------------------------------------------------------------- logs
@@ -433,6 +446,9 @@ class Sequential:
             layers.append({"class_name": l.keras_class, "config": l.get_config()})
         return {"name": self.name, "layers": layers}
 
+    def _save_class_name(self) -> str:
+        return "Sequential"
+
     def save(self, filepath: str) -> None:
         """Keras-v3-shaped zip: config.json + metadata.json + model.weights.safetensors (weights in Keras
         layouts, keyed ``layers/<name>/vars/<i>``; safetensors instead of HDF5 because h5py is absent)."""
@@ -441,7 +457,7 @@ class Sequential:
         st = self._strategy()
         if st is not None and not st.is_chief:
             return
-        cfg = {"module": "pyspark_tf_gke_amd.nn", "class_name": "Sequential", "config": self.get_config(),
+        cfg = {"module": "pyspark_tf_gke_amd.nn", "class_name": self._save_class_name(), "config": self.get_config(),
                "compile_config": {"optimizer": self.optimizer.get_config() if self.optimizer else None,
                                   "loss": self.loss.name if self.loss else None, "metrics": self.metric_names}}
         meta = {"keras_version": "3-compatible", "framework": "pyspark_tf_gke_amd",
@@ -465,10 +481,15 @@ def load_model(filepath: str, compile: bool = True, device=None) -> Sequential:
     with zipfile.ZipFile(filepath) as zf:
         cfg = json.loads(zf.read("config.json"))
         tensors = st_load(zf.read("model.weights.safetensors"))
-    L.reset_name_counters()
-    m = Sequential(name=cfg["config"].get("name", "sequential"))
-    for lc in cfg["config"]["layers"]:
-        m.add(L.layer_from_config(lc["class_name"], lc["config"]))
+    if cfg.get("class_name") == "Functional":
+        from .functional import model_from_config
+
+        m = model_from_config(cfg["config"])
+    else:
+        L.reset_name_counters()
+        m = Sequential(name=cfg["config"].get("name", "sequential"))
+        for lc in cfg["config"]["layers"]:
+            m.add(L.layer_from_config(lc["class_name"], lc["config"]))
     m.build(device=device)
     for l in m.layers:
         ws = []

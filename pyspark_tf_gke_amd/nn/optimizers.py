@@ -58,6 +58,14 @@ class Adam(Optimizer):
         if advance:
             self.iterations = step
 
+    def apply_shard(self, store, grad_shard, lo: int, hi: int, gscale: float = 1.0) -> None:
+        """Update params[lo:hi] from an already-reduced gradient shard (sharded PS strategy)."""
+        self.build(store)
+        step = self.iterations + 1
+        K.adam(store.flat[lo:hi], grad_shard, self.m[lo:hi], self.v[lo:hi], store.flat_bf16[lo:hi],
+               self.lr_t(step), self.beta_1, self.beta_2, self.epsilon, gscale)
+        self.iterations = step
+
     def get_config(self):
         return {"name": self.name, "learning_rate": self.learning_rate, "beta_1": self.beta_1,
                 "beta_2": self.beta_2, "epsilon": self.epsilon}
@@ -66,9 +74,49 @@ class Adam(Optimizer):
         return {"m": self.m, "v": self.v}
 
 
+class SGD(Optimizer):
+    """``tf.keras.optimizers.SGD(learning_rate, momentum, nesterov)`` as one fused flat kernel
+    (the usual ResNet-50 optimizer)."""
+
+    def __init__(self, learning_rate: float = 0.01, momentum: float = 0.0, nesterov: bool = False, name: str = "SGD"):
+        super().__init__(learning_rate)
+        self.momentum, self.nesterov, self.name = float(momentum), bool(nesterov), name
+        self.velocity = None
+
+    def build(self, store) -> None:
+        if self.momentum > 0 and (self.velocity is None or self.velocity.numel() != store.total
+                                  or self.velocity.device != store.flat.device):
+            self.velocity = torch.zeros(store.total, dtype=torch.float32, device=store.flat.device)
+
+    def apply(self, store, gscale: float = 1.0, lo: int = 0, hi: int | None = None, advance: bool = True) -> None:
+        self.build(store)
+        hi = store.total if hi is None else hi
+        if hi > lo:
+            sl = slice(lo, hi)
+            K.sgd(store.flat[sl], store.flat_grad[sl], self.velocity[sl] if self.velocity is not None else None,
+                  store.flat_bf16[sl], self.learning_rate, self.momentum, self.nesterov, gscale)
+        if advance:
+            self.iterations += 1
+
+    def apply_shard(self, store, grad_shard, lo: int, hi: int, gscale: float = 1.0) -> None:
+        self.build(store)
+        K.sgd(store.flat[lo:hi], grad_shard, self.velocity[lo:hi] if self.velocity is not None else None,
+              store.flat_bf16[lo:hi], self.learning_rate, self.momentum, self.nesterov, gscale)
+        self.iterations += 1
+
+    def get_config(self):
+        return {"name": self.name, "learning_rate": self.learning_rate, "momentum": self.momentum,
+                "nesterov": self.nesterov}
+
+    def state_tensors(self) -> dict:
+        return {"velocity": self.velocity} if self.velocity is not None else {}
+
+
 def get(identifier) -> Optimizer:
     if isinstance(identifier, Optimizer):
         return identifier
     if isinstance(identifier, str) and identifier.lower() == "adam":
         return Adam()
+    if isinstance(identifier, str) and identifier.lower() == "sgd":
+        return SGD()
     raise ValueError(f"unknown optimizer {identifier!r}")

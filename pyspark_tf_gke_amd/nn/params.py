@@ -95,7 +95,10 @@ class ParamStore:
             flat_host[p.offset:p.offset + p.numel] = host_vals[p.name].reshape(-1)
         self.flat = torch.from_numpy(flat_host).to(self.device)
         self.flat_grad = torch.zeros(self.total, dtype=torch.float32, device=self.device)
-        self.flat_bf16 = self.flat.to(torch.bfloat16)
+        from .engine import host_fp32
+
+        mirror = torch.float32 if (host_fp32() and self.device.type == "cpu") else torch.bfloat16
+        self.flat_bf16 = self.flat.to(mirror)
         self._bind_views()
         # contiguous ranges whose gradient must be zeroed before each backward
         ranges = []
@@ -121,7 +124,7 @@ class ParamStore:
             self.flat_grad[lo:hi].zero_()
 
     def refresh_bf16(self) -> None:
-        self.flat_bf16.copy_(self.flat.to(torch.bfloat16))
+        self.flat_bf16.copy_(self.flat.to(self.flat_bf16.dtype))
 
     def by_name(self, name: str) -> Param:
         for p in self.params:

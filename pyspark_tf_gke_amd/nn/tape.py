@@ -55,7 +55,7 @@ class GradientTape:
         if m is None or self.loss_obj is None:
             raise RuntimeError("GradientTape.gradient: no model forward / loss recorded")
         out = self.out
-        last = m.ops[-1]
+        last = m._last_op()
         if isinstance(self.loss_obj, LS.SparseCategoricalCrossentropy) and isinstance(last, E.DenseOp) \
                 and last.act == "softmax" and not last.logits_only:
             raise RuntimeError("compile() the model with the loss (or build with from_logits) before a tape loop")
@@ -74,7 +74,7 @@ class GradientTape:
             dpred = m._loss_grad(out, yb, stats)
         finally:
             m.loss = saved_loss
-        E.run_backward(m.ops, dpred, m.ws)
+        m._run_backward(dpred)
         m._pending_grads = True
         return [v.param.grad for v in sources]
 

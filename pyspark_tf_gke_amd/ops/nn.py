@@ -41,16 +41,47 @@ def conv2d_fwd(x, w, bias, stride: int, pad: int, out, act: str | None = None):
     return out
 
 
-def conv2d_dgrad(dz, w, pad: int, out):
-    """out[N,H,W,Cin] = d(conv)/dx for a stride-1 convolution."""
+def conv2d_dgrad(dz, w, pad: int, out, accumulate: bool = False):
+    """out[N,H,W,Cin] (+)= d(conv)/dx for a stride-1 convolution."""
     if not on_device(dz):
+        if accumulate:
+            tmp = torch.empty_like(out, dtype=torch.float32)
+            ref.conv2d_dgrad(dz, w, pad, tmp)
+            out.copy_((out.float() + tmp).to(out.dtype))
+            return out
         return ref.conv2d_dgrad(dz, w, pad, out)
     N, H, W, Cout = dz.shape
     Cw, KH, KW, Cin = w.shape
     assert Cw == Cout and tuple(out.shape) == (N, H, W, Cin)
     need(dz, torch.bfloat16, "dgrad.dz"); need(out, torch.bfloat16, "dgrad.out")
-    hip("ptg_conv2d_dgrad", ptr(dz), ptr(w), ptr(out), N, H, W, Cin, Cout, KH, KW, pad)
+    hip("ptg_conv2d_dgrad", ptr(dz), ptr(w), ptr(out), N, H, W, Cin, Cout, KH, KW, pad, int(accumulate))
     return out
+
+
+def conv1x1_dgrad(dz, w, stride: int, out, accumulate: bool = False):
+    """out[N,H,W,Cin] (+)= d/dx of a 1x1 convolution with stride ``stride`` (pad 0).  With
+    stride > 1 and accumulate=False the off-lattice pixels are zeroed here."""
+    N, OH, OW, Cout = dz.shape
+    Cw, KH, KW, Cin = w.shape
+    _, H, W, _ = out.shape
+    assert KH == KW == 1 and Cw == Cout and out.shape[-1] == Cin
+    if not on_device(dz):
+        g = (_f32(dz).reshape(-1, Cout) @ _f32(w).reshape(Cout, Cin)).reshape(N, OH, OW, Cin)
+        full = torch.zeros(out.shape, dtype=torch.float32)
+        full[:, : OH * stride: stride, : OW * stride: stride] = g
+        if accumulate:
+            full += out.float()
+        out.copy_(full.to(out.dtype))
+        return out
+    need(dz, torch.bfloat16, "dgrad1x1.dz"); need(out, torch.bfloat16, "dgrad1x1.out")
+    if stride > 1 and not accumulate:
+        out.zero_()  # the remapped epilogue then writes only the stride lattice
+    hip("ptg_conv1x1_dgrad", ptr(dz), ptr(w), ptr(out), N, OH, OW, H, W, Cin, Cout, stride, int(accumulate))
+    return out
+
+
+def _f32(t):
+    return t.float()
 
 
 def conv2d_wgrad(x, dz, stride: int, pad: int, out, accumulate: bool = False, splits: int = 0):
@@ -304,6 +335,22 @@ def adam(p, g, m, v, pbf, lr_t: float, b1: float, b2: float, eps: float, gscale:
         float(eps), float(gscale))
 
 
+def sgd(p, g, vel, pbf, lr: float, momentum: float, nesterov: bool, gscale: float = 1.0):
+    """Keras SGD: v = momentum*v - lr*g; p += v (Nesterov: p += momentum*v - lr*g); refreshes pbf."""
+    if not on_device(p):
+        gg = g * gscale
+        if vel is not None:
+            vel.mul_(momentum).sub_(lr * gg)
+            p.add_(momentum * vel - lr * gg if nesterov else vel)
+        else:
+            p.sub_(lr * gg)
+        if pbf is not None:
+            pbf.copy_(p.to(pbf.dtype))
+        return
+    hip("ptg_sgd", ptr(p), ptr(g), ptr(vel), ptr(pbf), p.numel(), float(lr), float(momentum), int(nesterov),
+        float(gscale))
+
+
 def cast_f32_bf16(x, out):
     if not on_device(x):
         out.copy_(x.to(torch.bfloat16))
@@ -325,7 +372,7 @@ def pack_rgb4(images_f32, out):
     """float [N,H,W,3] -> bf16 [N,H,W,4]."""
     if not on_device(images_f32):
         out.zero_()
-        out[..., :3] = images_f32.to(torch.bfloat16)
+        out[..., :3] = images_f32.to(out.dtype)
         return out
     npix = images_f32.numel() // 3
     hip("ptg_pack_rgb4", ptr(images_f32), ptr(out), npix)

@@ -1,5 +1,6 @@
 """Checkpoint / resume.  The reference only saves the final ``model.keras``; here a
-checkpoint holds the flat fp32 parameters, the Adam moments and step, the epoch, and the RNG
+checkpoint holds the flat fp32 parameters, the optimizer state (Adam moments / SGD velocity) and
+step, the BatchNormalization moving statistics, the epoch, and the RNG
 state, written atomically with safetensors + a JSON manifest.  Parameters/moments are identical
 on every rank for mirrored training (rank 0 writes), while the sharded parameter-server strategy
 writes one shard file per rank (its slice of the optimizer state) plus the gathered parameters.
@@ -29,11 +30,16 @@ def save_checkpoint(model, path: str, epoch: int, extra: dict | None = None) -> 
             lo, hi = model.strategy.shard_range(model)
         else:
             lo, hi = 0, st.total
-        if opt is not None and opt.m is not None:
-            tensors["adam_m"] = opt.m[lo:hi].detach().cpu().contiguous()
-            tensors["adam_v"] = opt.v[lo:hi].detach().cpu().contiguous()
+        if opt is not None:
+            for k, t in opt.state_tensors().items():
+                if t is not None:
+                    tensors["opt_" + k] = t[lo:hi].detach().cpu().contiguous()
         if rank == 0:
             tensors["params"] = st.flat.detach().cpu().contiguous()
+            for l in model.layers:  # non-trainable BatchNormalization state
+                if getattr(l, "moving_mean", None) is not None:
+                    tensors[f"bn/{l.name}/moving_mean"] = l.moving_mean.detach().cpu().contiguous()
+                    tensors[f"bn/{l.name}/moving_variance"] = l.moving_variance.detach().cpu().contiguous()
         tmp = os.path.join(path, f"shard-{rank:05d}.safetensors.tmp")
         save_file(tensors, tmp, metadata={"lo": str(lo), "hi": str(hi)})
         os.replace(tmp, os.path.join(path, f"shard-{rank:05d}.safetensors"))
@@ -58,20 +64,27 @@ def load_checkpoint(model, path: str) -> dict:
     opt = model.optimizer
     if opt is not None:
         opt.build(st)
+    state = opt.state_tensors() if opt is not None else {}
     with safe_open(os.path.join(path, "shard-00000.safetensors"), "pt") as f:
+        keys = set(f.keys())
         st.flat.copy_(f.get_tensor("params").to(st.flat.device))
-        if not manifest["sharded"] and opt is not None and "adam_m" in f.keys():
-            opt.m.copy_(f.get_tensor("adam_m").to(opt.m.device))
-            opt.v.copy_(f.get_tensor("adam_v").to(opt.v.device))
+        if not manifest["sharded"]:
+            for k, t in state.items():
+                if t is not None and "opt_" + k in keys:
+                    t.copy_(f.get_tensor("opt_" + k).to(t.device))
+        for l in model.layers:
+            if getattr(l, "moving_mean", None) is not None and f"bn/{l.name}/moving_mean" in keys:
+                l.moving_mean.copy_(f.get_tensor(f"bn/{l.name}/moving_mean").to(l.moving_mean.device))
+                l.moving_variance.copy_(f.get_tensor(f"bn/{l.name}/moving_variance").to(l.moving_variance.device))
     if manifest["sharded"] and opt is not None:
         for r in range(manifest["world_size"]):
             fn = os.path.join(path, f"shard-{r:05d}.safetensors")
             with safe_open(fn, "pt") as f:
                 md = f.metadata()
                 lo, hi = int(md["lo"]), int(md["hi"])
-                if "adam_m" in f.keys():
-                    opt.m[lo:hi].copy_(f.get_tensor("adam_m").to(opt.m.device))
-                    opt.v[lo:hi].copy_(f.get_tensor("adam_v").to(opt.v.device))
+                for k, t in state.items():
+                    if t is not None and "opt_" + k in f.keys():
+                        t[lo:hi].copy_(f.get_tensor("opt_" + k).to(t.device))
     if opt is not None:
         opt.iterations = int(manifest["step"])
     st.refresh_bf16()

@@ -1,0 +1,119 @@
+"""Functional-graph engine (ResNet family) on the CPU host path vs an fp32 torch-autograd oracle."""
+import numpy as np
+import pytest
+import torch
+
+from graph_oracle import oracle_grads
+from pyspark_tf_gke_amd import nn
+from pyspark_tf_gke_amd.models.resnet import RESNET50_PARAMS, RESNET50_TRAINABLE, ResNet, ResNet50
+
+
+def _engine_grads(m, x, y):
+    stats = m._stats_buf()
+    stats.zero_()
+    m.store.zero_grad()
+    xb, yb = m._prep_batch(x, y)
+    out = m._run_forward(xb, True)
+    dpred = m._loss_grad(out, yb, stats)
+    m._run_backward(dpred)
+    return m._logs_from(stats)["loss"], {p.name: p.grad.detach().float().clone() for p in m.store.params}
+
+
+def _rel(a, b):
+    return float((a - b).norm() / max(b.norm(), 1e-6))
+
+
+def test_resnet50_param_count_matches_keras():
+    m = ResNet50(device="cpu")
+    assert m.count_params() == RESNET50_PARAMS
+    assert m.store.num_params() == RESNET50_TRAINABLE
+    names = [l.name for l in m.layers]
+    assert "conv2_block1_0_conv" in names and "conv5_block3_out" in names and names[-1] == "predictions"
+    # every Conv2D+BN(+Add)(+ReLU) unit is one fused op; stem pool + GAP + Dense are the others
+    assert len(m.ops) == 53 + 3
+
+
+@pytest.fixture
+def fp32_host():
+    from pyspark_tf_gke_amd.nn import engine
+
+    old = engine.host_fp32()
+    engine.host_fp32(True)
+    yield
+    engine.host_fp32(old)
+
+
+@pytest.mark.parametrize("blocks", [(1, 1), (2, 1)])
+def test_resnet_small_grads_match_autograd(blocks, fp32_host):
+    """Engine plumbing + BN/pool/residual math, exact up to fp32 rounding (host fp32 mode)."""
+    torch.manual_seed(0)
+    m = ResNet(blocks, input_shape=(32, 32, 3), classes=10, width=8, device="cpu")
+    m.compile(optimizer=nn.optimizers.SGD(0.0), loss="sparse_categorical_crossentropy", metrics=["accuracy"])
+    x = torch.rand(4, 32, 32, 3)
+    y = torch.randint(0, 10, (4,))
+    loss, g = _engine_grads(m, x, y)
+    ref_loss, ref = oracle_grads(m, x, y)
+    assert abs(loss - ref_loss) < 1e-4 * max(1.0, abs(ref_loss))
+    for name, rg in ref.items():
+        if name.endswith("_conv/bias") and "predictions" not in name:
+            # conv bias before a training-mode BN: analytically zero gradient (the engine skips it)
+            assert float(rg.abs().max()) < 1e-4
+            continue
+        eg = g[name].reshape(rg.shape)
+        assert _rel(eg, rg) < 1e-3, (name, _rel(eg, rg))
+
+
+def test_resnet_small_bf16_close_to_autograd():
+    """The real (bf16-activation) host path: same directions, bf16-level deviations."""
+    torch.manual_seed(0)
+    m = ResNet((1, 1), input_shape=(32, 32, 3), classes=10, width=8, device="cpu")
+    m.compile(optimizer=nn.optimizers.SGD(0.0), loss="sparse_categorical_crossentropy")
+    x = torch.rand(16, 32, 32, 3)
+    y = torch.randint(0, 10, (16,))
+    loss, g = _engine_grads(m, x, y)
+    ref_loss, ref = oracle_grads(m, x, y)
+    assert abs(loss - ref_loss) < 2e-2 * max(1.0, abs(ref_loss))
+    for name, rg in ref.items():
+        if name.endswith("kernel"):
+            eg = g[name].reshape(rg.shape).flatten()
+            cos = float(torch.dot(eg, rg.flatten()) / (eg.norm() * rg.norm()))
+            assert cos > 0.9, (name, cos)
+
+
+def test_resnet_train_loss_decreases_and_saves(tmp_path):
+    torch.manual_seed(0)
+    m = ResNet((1, 1), input_shape=(32, 32, 3), classes=4, width=8, device="cpu")
+    m.compile(optimizer=nn.optimizers.Adam(1e-2), loss="sparse_categorical_crossentropy", metrics=["accuracy"])
+    x = torch.rand(8, 32, 32, 3)
+    y = torch.randint(0, 4, (8,))
+    first = m.train_on_batch(x, y, return_dict=True)["loss"]
+    for _ in range(15):
+        last = m.train_on_batch(x, y, return_dict=True)["loss"]
+    assert last < first
+    # moving statistics moved away from their (0, 1) init
+    bn = [l for l in m.layers if isinstance(l, nn.BatchNormalization)][0]
+    assert float(bn.moving_mean.abs().sum()) > 0
+    p_train = m.predict(x.numpy(), batch_size=8)
+    path = str(tmp_path / "model.keras")
+    m.save(path)
+    m2 = nn.load_model(path, device="cpu")
+    assert m2.count_params() == m.count_params()
+    p_load = m2.predict(x.numpy(), batch_size=8)
+    np.testing.assert_allclose(p_load, p_train, atol=2e-2)
+
+
+def test_functional_mlp_and_sgd():
+    inp = nn.Input((3,))
+    h = nn.Dense(16, activation="relu")(inp)
+    h = nn.Dense(8, activation="relu")(h)
+    out = nn.Dense(3, activation="softmax")(h)
+    m = nn.Model(inp, out)
+    m.build(device="cpu")
+    m.compile(optimizer=nn.optimizers.SGD(0.1, momentum=0.9, nesterov=True), loss="sparse_categorical_crossentropy",
+              metrics=["accuracy"])
+    rng = np.random.default_rng(0)
+    x = rng.normal(size=(64, 3)).astype(np.float32)
+    y = (x[:, 0] > 0).astype(np.int32) + (x[:, 1] > 0)
+    h0 = m.fit(x, y, batch_size=16, epochs=1, verbose=0).history["loss"][0]
+    h1 = m.fit(x, y, batch_size=16, epochs=10, verbose=0).history["loss"][-1]
+    assert h1 < h0

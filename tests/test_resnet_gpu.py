@@ -1,0 +1,164 @@
+"""ResNet-family kernels (bn.hip, strided/accumulating dgrad, SGD) and the functional graph engine on
+the MI355X, each compared against the fp32 PyTorch reference of the same op."""
+import pytest
+import torch
+
+from graph_oracle import oracle_grads
+from pyspark_tf_gke_amd import nn
+from pyspark_tf_gke_amd.ops import bn as KB
+from pyspark_tf_gke_amd.ops import nn as K
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rel(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    return float((a - b).norm() / max(float(b.norm()), 1e-12))
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib(hip_built):
+    return hip_built
+
+
+@pytest.mark.parametrize("M,C", [(4096, 64), (1000, 256), (392, 2048), (50176, 128)])
+def test_bn_forward_backward(M, C):
+    torch.manual_seed(0)
+    z = (torch.randn(M, C) * 2 + 0.5).to(torch.bfloat16)
+    res = torch.randn(M, C).to(torch.bfloat16)
+    dy = torch.randn(M, C).to(torch.bfloat16)
+    gamma, beta = torch.rand(C) + 0.5, torch.randn(C)
+    out = {}
+    for dev in ("cpu", DEV):
+        zz, rr, dd = z.to(dev), res.to(dev), dy.to(dev)
+        g, b = gamma.to(dev), beta.to(dev)
+        part = KB.part_buffer(C, dev)
+        f = lambda: torch.empty(C, device=dev)  # noqa: E731
+        scale, shift, mean, rstd = f(), f(), f(), f()
+        mm, mv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+        KB.bn_stats(zz, part)
+        KB.bn_finalize(part, M, g, b, 1e-3, 0.9, mm, mv, scale, shift, mean, rstd, True)
+        if dev == "cpu":
+            part.zero_()
+        assert float(part.abs().sum()) == 0.0  # finalize re-zeroes the partial sums
+        y = torch.empty(M, C, dtype=torch.bfloat16, device=dev)
+        KB.bn_apply(zz, scale, shift, rr, True, y)
+        dg, db = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+        coef = torch.empty(3, C, device=dev)
+        KB.bn_bwd_reduce(dd, y, zz, True, part)
+        KB.bn_bwd_finalize(part, M, g, mean, rstd, dg, db, coef)
+        dz = torch.empty_like(zz)
+        dres = torch.empty_like(zz)
+        KB.bn_bwd_apply(dd, y, zz, coef, True, dz, dres)
+        out[dev] = dict(y=y, mm=mm, mv=mv, dg=dg, db=db, dz=dz, dres=dres, scale=scale)
+    for k in out["cpu"]:
+        assert _rel(out[DEV][k], out["cpu"][k]) < 2e-2, k
+
+
+@pytest.mark.parametrize("shape,k,s,p", [((2, 112, 112, 64), 3, 2, 1), ((3, 17, 19, 16), 3, 2, 0),
+                                         ((2, 32, 40, 8), 2, 2, 0)])
+def test_maxpool(shape, k, s, p):
+    torch.manual_seed(1)
+    x = torch.randn(shape).to(torch.bfloat16)
+    N, H, W, C = shape
+    OH, OW = KB.pool_out_size(H, k, s, p), KB.pool_out_size(W, k, s, p)
+    dy = torch.randn(N, OH, OW, C).to(torch.bfloat16)
+    res = {}
+    for dev in ("cpu", DEV):
+        o = torch.empty(N, OH, OW, C, dtype=torch.bfloat16, device=dev)
+        a = torch.empty(N, OH, OW, C, dtype=torch.uint8, device=dev)
+        KB.maxpool_fwd(x.to(dev), o, a, k, s, p)
+        dx = torch.empty(shape, dtype=torch.bfloat16, device=dev)
+        KB.maxpool_bwd(dy.to(dev), a, dx, k, s, p)
+        res[dev] = (o, a, dx)
+    assert torch.equal(res[DEV][0].cpu(), res["cpu"][0])
+    assert torch.equal(res[DEV][1].cpu(), res["cpu"][1])
+    assert _rel(res[DEV][2], res["cpu"][2]) < 1e-2
+
+
+@pytest.mark.parametrize("stride,acc", [(1, False), (2, False), (2, True), (1, True)])
+def test_conv1x1_dgrad(stride, acc):
+    torch.manual_seed(2)
+    N, H, W, Cin, Cout = 4, 28, 28, 64, 128
+    OH, OW = (H - 1) // stride + 1, (W - 1) // stride + 1
+    dz = torch.randn(N, OH, OW, Cout).to(torch.bfloat16)
+    w = (torch.randn(Cout, 1, 1, Cin) * 0.1).to(torch.bfloat16)
+    init = torch.randn(N, H, W, Cin).to(torch.bfloat16)
+    res = {}
+    for dev in ("cpu", DEV):
+        dx = init.clone().to(dev)
+        K.conv1x1_dgrad(dz.to(dev), w.to(dev), stride, dx, acc)
+        res[dev] = dx
+    assert _rel(res[DEV], res["cpu"]) < 1e-2
+
+
+def test_conv3x3_dgrad_accumulate():
+    torch.manual_seed(3)
+    N, H, W, Cin, Cout = 2, 14, 14, 128, 128
+    dz = torch.randn(N, H, W, Cout).to(torch.bfloat16)
+    w = (torch.randn(Cout, 3, 3, Cin) * 0.05).to(torch.bfloat16)
+    init = torch.randn(N, H, W, Cin).to(torch.bfloat16)
+    res = {}
+    for dev in ("cpu", DEV):
+        dx = init.clone().to(dev)
+        K.conv2d_dgrad(dz.to(dev), w.to(dev), 1, dx, accumulate=True)
+        res[dev] = dx
+    assert _rel(res[DEV], res["cpu"]) < 1e-2
+
+
+@pytest.mark.parametrize("nesterov", [False, True])
+def test_sgd_kernel(nesterov):
+    torch.manual_seed(4)
+    n = 10_000
+    p, g, v = torch.randn(n), torch.randn(n), torch.randn(n)
+    res = {}
+    for dev in ("cpu", DEV):
+        pp, vv = p.clone().to(dev), v.clone().to(dev)
+        pb = torch.empty(n, dtype=torch.bfloat16, device=dev)
+        K.sgd(pp, g.to(dev), vv, pb, 0.1, 0.9, nesterov, 0.5)
+        res[dev] = (pp, vv, pb)
+    for a, b in zip(res[DEV], res["cpu"]):
+        assert _rel(a, b) < 1e-5 or a.dtype == torch.bfloat16 and _rel(a, b) < 1e-2
+
+
+def test_small_resnet_grads_vs_autograd():
+    from pyspark_tf_gke_amd.models.resnet import ResNet
+
+    torch.manual_seed(0)
+    m = ResNet((1, 1), input_shape=(64, 64, 3), classes=10, width=16, device=DEV)
+    m.compile(optimizer=nn.optimizers.SGD(0.0), loss="sparse_categorical_crossentropy")
+    x = torch.rand(16, 64, 64, 3)
+    y = torch.randint(0, 10, (16,))
+    stats = m._stats_buf()
+    stats.zero_()
+    m.store.zero_grad()
+    xb, yb = m._prep_batch(x, y)
+    out = m._run_forward(xb, True)
+    dpred = m._loss_grad(out, yb, stats)
+    m._run_backward(dpred)
+    torch.cuda.synchronize()
+    loss = m._logs_from(stats)["loss"]
+    ref_loss, ref = oracle_grads(m, x, y)
+    assert abs(loss - ref_loss) < 3e-2 * max(1.0, abs(ref_loss))
+    g = {p.name: p.grad.detach().float().cpu() for p in m.store.params}
+    for name, rg in ref.items():
+        if name.endswith("kernel"):
+            eg = g[name].reshape(rg.shape).flatten()
+            cos = float(torch.dot(eg, rg.flatten()) / (eg.norm() * rg.norm()))
+            assert cos > 0.9, (name, cos)
+
+
+def test_resnet50_train_steps():
+    from pyspark_tf_gke_amd.models.resnet import build_resnet50
+
+    torch.manual_seed(0)
+    m = build_resnet50(device=DEV, optimizer=nn.optimizers.SGD(0.01, momentum=0.9))
+    x = torch.rand(8, 224, 224, 3, device=DEV)
+    y = torch.randint(0, 1000, (8,), device=DEV).to(torch.int32)
+    l0 = m.train_on_batch(x, y, return_dict=True)["loss"]
+    for _ in range(3):
+        l1 = m.train_on_batch(x, y, return_dict=True)["loss"]
+    assert l0 == l0 and l1 == l1 and l1 < l0  # fits the fixed batch
+    p = m.predict(x[:2].cpu().numpy(), batch_size=2)
+    assert p.shape == (2, 1000) and abs(float(p.sum()) - 2.0) < 1e-2
