@@ -28,10 +28,13 @@ namespace {
 
 constexpr int BN_G = 64;
 
-// rows per block so that the grid has ~2048 blocks (>= 8 per CU) and every block has work
+// Rows per block: ~1024 blocks for big tensors, but at least 16 rows per thread (memory-level
+// parallelism) and at least 64 rows per block, so the 2*C partial-sum atomics a block flushes stay
+// small next to the 2*C*rows bytes it reads (C = 2048 layers have only a few thousand rows).
 inline int bn_rows_per_block(long M, int rpi) {
-  long r = (M + 2047) / 2048;
-  if (r < rpi) r = rpi;
+  long r = (M + 1023) / 1024;
+  if (r < 16L * rpi) r = 16L * rpi;
+  if (r < 64) r = 64;
   r = (r + rpi - 1) / rpi * rpi;
   return (int)r;
 }
@@ -72,7 +75,20 @@ __global__ __launch_bounds__(256) void bn_stats_k(const bf16_t* __restrict__ z, 
   for (int j = 0; j < 8; ++j) { s[j] = 0.f; q[j] = 0.f; }
   const long r0 = (long)blockIdx.x * rpb, r1 = min(M, r0 + rpb);
   if (rsub < rpi) {
-    for (long r = r0 + rsub; r < r1; r += rpi) {
+    long r = r0 + rsub;
+    for (; r + 3L * rpi < r1; r += 4L * rpi) {  // 4 independent 16-B loads in flight per thread
+      U4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = *(const U4*)(z + (r + (long)u * rpi) * C + slot * 8);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float f[8];
+        unpack8(v[u], f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { s[j] += f[j]; q[j] = fmaf(f[j], f[j], q[j]); }
+      }
+    }
+    for (; r < r1; r += rpi) {
       float f[8];
       unpack8(*(const U4*)(z + r * C + slot * 8), f);
 #pragma unroll
@@ -148,20 +164,37 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_k(const bf16_t* __restrict_
 #pragma unroll
   for (int j = 0; j < 8; ++j) { s[j] = 0.f; q[j] = 0.f; }
   const long r0 = (long)blockIdx.x * rpb, r1 = min(M, r0 + rpb);
-  if (rsub < rpi) {
-    for (long r = r0 + rsub; r < r1; r += rpi) {
-      const long off = r * C + slot * 8;
-      float g[8], zz[8];
-      unpack8(*(const U4*)(dy + off), g);
-      unpack8(*(const U4*)(z + off), zz);
-      if (relu) {
-        float yy[8];
-        unpack8(*(const U4*)(y + off), yy);
+  auto acc_row = [&](const U4& vd, const U4& vz, const U4& vy) {
+    float g[8], zz[8];
+    unpack8(vd, g);
+    unpack8(vz, zz);
+    if (relu) {
+      float yy[8];
+      unpack8(vy, yy);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) g[j] = yy[j] > 0.f ? g[j] : 0.f;
+      for (int j = 0; j < 8; ++j) g[j] = yy[j] > 0.f ? g[j] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { s[j] += g[j]; q[j] = fmaf(g[j], zz[j], q[j]); }
+  };
+  if (rsub < rpi) {
+    long r = r0 + rsub;
+    for (; r + 3L * rpi < r1; r += 4L * rpi) {  // 8-12 independent 16-B loads in flight per thread
+      U4 vd[4], vz[4], vy[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const long off = (r + (long)u * rpi) * C + slot * 8;
+        vd[u] = *(const U4*)(dy + off);
+        vz[u] = *(const U4*)(z + off);
+        vy[u] = relu ? *(const U4*)(y + off) : vd[u];
       }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { s[j] += g[j]; q[j] = fmaf(g[j], zz[j], q[j]); }
+      for (int u = 0; u < 4; ++u) acc_row(vd[u], vz[u], vy[u]);
+    }
+    for (; r < r1; r += rpi) {
+      const long off = r * C + slot * 8;
+      const U4 vd = *(const U4*)(dy + off);
+      acc_row(vd, *(const U4*)(z + off), relu ? *(const U4*)(y + off) : vd);
     }
   }
   bn_flush(red, s, q, tid, cpt, rpi, part, C);

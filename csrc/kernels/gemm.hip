@@ -9,13 +9,14 @@
 // Structure (cdna_hip_programming.md §5 "standard MFMA GEMM main loop"):
 //   * 256 threads = 4 waves arranged WM x WN; each wave owns a (BM/WM) x (BN/WN) sub-tile made
 //     of 16x16 MFMA fragments; accumulators indexed by fragment repeat only.
-//   * BK = 32 K-step, two LDS buffers; the next tile's global loads are issued into registers
+//   * BK = 64 K-step, two LDS buffers; the next tile's global loads are issued into registers
 //     before the MFMAs of the current tile and written to the other LDS buffer after them,
 //     one barrier per K-step.
-//   * LDS images are [rows][BK] with k contiguous (80-byte padded rows), so every A and B
-//     fragment is one 16-byte ds_read.  Operands whose source memory is k-contiguous are staged
-//     with 16-byte stores; operands whose source is row-contiguous (transposed use of a matrix,
-//     the im2col^T of wgrad) are loaded as 16-byte row vectors and scattered into the image.
+//   * Operands whose source memory is k-contiguous are staged as [rows][BK] images (fragment =
+//     one 16-byte ds_read); operands whose source is row-contiguous (transposed use of a matrix,
+//     the im2col^T of wgrad, the dgrad filter) are staged k-major exactly as they sit in memory
+//     and read with the transposed LDS read ds_read_b64_tr_b16 - every LDS store is a 16-byte
+//     vector in both cases.
 //   * Operand "loaders" turn (row, k) into a 16-byte vector: plain matrices, the implicit im2col
 //     gather of a NHWC activation, the flipped/transposed filter of dgrad, the im2col^T of wgrad.
 //     The convolution therefore never materialises its im2col matrix.
@@ -25,8 +26,7 @@
 
 namespace ptg {
 
-constexpr int BK = 32;
-constexpr int LDK = BK + 8;  // padded LDS row: 40 bf16 = 80 B (16-B aligned)
+constexpr int BK = 64;
 
 // ------------------------------------------------------------------------------------------
 // Operand loaders. K_CONTIG loaders return elements (r, k..k+7); the others return
@@ -193,19 +193,42 @@ struct EpiAtomic {  // split-K: out[m*ldc+n] += acc  (device-scope fp32 atomic, 
 // ------------------------------------------------------------------------------------------
 // The main loop.
 // ------------------------------------------------------------------------------------------
+// LDS images (one __shared__ array, two stages):
+//   K_CONTIG operand: [rows][LDK] (k contiguous, 16-B padded rows): 16-B vector stores, fragment
+//     reads of 8 (or 2 x 4) consecutive k.
+//   row-contiguous operand: [BK][rows + 16] (k-major, exactly the global layout of a transposed
+//     use): 16-B vector stores of 8 consecutive rows, fragments read with the gfx950 transposed
+//     LDS read ds_read_b64_tr_b16 (cdna_hip_programming.md T10).  The +16 row padding makes the
+//     8 k-rows a half-wave touches land on distinct 8-dword bank groups.
+// When either operand is row-contiguous both use the k order in which lane group g holds
+// k = {4g..4g+3, 16+4g..16+4g+3} of each 32-wide MFMA step (any k permutation shared by A and B
+// leaves the product unchanged); the tr-read half-wave then reads 8 consecutive k-rows.
+typedef __attribute__((ext_vector_type(4))) short gs16x4_t;
+typedef __attribute__((address_space(3))) gs16x4_t glds_s16x4_t;
+
+PTG_DEV U2 gtr_read(const bf16_t* p) {
+  return __builtin_bit_cast(U2, __builtin_amdgcn_ds_read_tr16_b64_v4i16((glds_s16x4_t*)(p)));
+}
+
+template <class L, int R>
+struct LdsImg {
+  static constexpr int LD = L::K_CONTIG ? BK + 8 : R + 16;
+  static constexpr int ELEMS = L::K_CONTIG ? R * LD : BK * LD;
+};
+
 template <int BM, int BN, int WM, int WN, class LA, class LB, class EPI>
 __global__ __launch_bounds__(256) void gemm_kernel(LA la, LB lb, EPI epi, int M, int N, int K,
                                                    int kchunk) {
   constexpr int WTM = BM / WM, WTN = BN / WN, FM = WTM / 16, FN = WTN / 16;
   static_assert(WM * WN == 4, "4 waves");
   static_assert(FM >= 1 && FN >= 1, "wave tile >= 16x16");
+  constexpr bool PERM = !LA::K_CONTIG || !LB::K_CONTIG;
+  using IA = LdsImg<LA, BM>;
+  using IB = LdsImg<LB, BN>;
   constexpr int AV = BM * BK / 8, BV = BN * BK / 8;  // 16-B vectors per operand tile
   constexpr int AI = (AV + 255) / 256, BI = (BV + 255) / 256;
-  // one LDS array (A and B images of both stages)
-  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * (BM + BN) * LDK];
-  bf16_t* sA0 = smem;
-  bf16_t* sB0 = smem + BM * LDK;
-  constexpr int STAGE = (BM + BN) * LDK;
+  constexpr int STAGE = IA::ELEMS + IB::ELEMS;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
@@ -226,10 +249,10 @@ __global__ __launch_bounds__(256) void gemm_kernel(LA la, LB lb, EPI epi, int M,
     aon[i] = v < AV;
     if constexpr (LA::K_CONTIG) {
       const int r = v / (BK / 8), kv = v % (BK / 8);
-      ca[i] = la.ctx(m0 + r); akk[i] = kv * 8; aoff[i] = r * LDK + kv * 8;
+      ca[i] = la.ctx(m0 + r); akk[i] = kv * 8; aoff[i] = r * IA::LD + kv * 8;
     } else {
       const int kk = v / (BM / 8), rv = v % (BM / 8);
-      ca[i] = la.ctx(m0 + rv * 8); akk[i] = kk; aoff[i] = rv * 8 * LDK + kk;
+      ca[i] = la.ctx(m0 + rv * 8); akk[i] = kk; aoff[i] = kk * IA::LD + rv * 8;
     }
   }
 #pragma unroll
@@ -238,10 +261,10 @@ __global__ __launch_bounds__(256) void gemm_kernel(LA la, LB lb, EPI epi, int M,
     bon[i] = v < BV;
     if constexpr (LB::K_CONTIG) {
       const int r = v / (BK / 8), kv = v % (BK / 8);
-      cb[i] = lb.ctx(n0 + r); bkk[i] = kv * 8; boff[i] = r * LDK + kv * 8;
+      cb[i] = lb.ctx(n0 + r); bkk[i] = kv * 8; boff[i] = r * IB::LD + kv * 8;
     } else {
       const int kk = v / (BN / 8), rv = v % (BN / 8);
-      cb[i] = lb.ctx(n0 + rv * 8); bkk[i] = kk; boff[i] = rv * 8 * LDK + kk;
+      cb[i] = lb.ctx(n0 + rv * 8); bkk[i] = kk; boff[i] = kk * IB::LD + rv * 8;
     }
   }
 
@@ -252,27 +275,34 @@ __global__ __launch_bounds__(256) void gemm_kernel(LA la, LB lb, EPI epi, int M,
 #pragma unroll
     for (int i = 0; i < BI; ++i) rb[i] = bon[i] ? lb.load(cb[i], k0 + bkk[i]) : zero4();
   };
-  auto scatter = [](bf16_t* dst, const U4& v) {
-    dst[0 * LDK] = (bf16_t)(v.x & 0xffff); dst[1 * LDK] = (bf16_t)(v.x >> 16);
-    dst[2 * LDK] = (bf16_t)(v.y & 0xffff); dst[3 * LDK] = (bf16_t)(v.y >> 16);
-    dst[4 * LDK] = (bf16_t)(v.z & 0xffff); dst[5 * LDK] = (bf16_t)(v.z >> 16);
-    dst[6 * LDK] = (bf16_t)(v.w & 0xffff); dst[7 * LDK] = (bf16_t)(v.w >> 16);
-  };
   auto sstore = [&](int stage) {
-    bf16_t* sA = sA0 + stage * STAGE;
-    bf16_t* sB = sB0 + stage * STAGE;
+    bf16_t* sA = smem + stage * STAGE;
+    bf16_t* sB = sA + IA::ELEMS;
 #pragma unroll
     for (int i = 0; i < AI; ++i)
-      if (aon[i]) {
-        if constexpr (LA::K_CONTIG) *(U4*)(sA + aoff[i]) = ra[i];
-        else scatter(sA + aoff[i], ra[i]);
-      }
+      if (aon[i]) *(U4*)(sA + aoff[i]) = ra[i];
 #pragma unroll
     for (int i = 0; i < BI; ++i)
-      if (bon[i]) {
-        if constexpr (LB::K_CONTIG) *(U4*)(sB + boff[i]) = rb[i];
-        else scatter(sB + boff[i], rb[i]);
-      }
+      if (bon[i]) *(U4*)(sB + boff[i]) = rb[i];
+  };
+  // fragment (16 rows x 32 k at k-offset kk) of an LDS image; rows start at `row0`
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p4 = (li & 3) * 4;
+  auto frag_k = [&](const bf16_t* img, int ld, int row0, int kk) -> bf16x8_t {  // [rows][k] image
+    const bf16_t* r = img + (row0 + li) * ld + kk;
+    U4 v;
+    if constexpr (PERM) {
+      const U2 a = *(const U2*)(r + 4 * g), b = *(const U2*)(r + 16 + 4 * g);
+      v.x = a.x; v.y = a.y; v.z = b.x; v.w = b.y;
+    } else {
+      v = *(const U4*)(r + 8 * g);
+    }
+    return __builtin_bit_cast(bf16x8_t, v);
+  };
+  auto frag_t = [&](const bf16_t* img, int ld, int row0, int kk) -> bf16x8_t {  // [k][rows] image
+    const U2 a = gtr_read(img + (kk + 4 * g + q) * ld + row0 + p4);
+    const U2 b = gtr_read(img + (kk + 16 + 4 * g + q) * ld + row0 + p4);
+    U4 v; v.x = a.x; v.y = a.y; v.z = b.x; v.w = b.y;
+    return __builtin_bit_cast(bf16x8_t, v);
   };
 
   f32x4_t acc[FM][FN];
@@ -284,24 +314,31 @@ __global__ __launch_bounds__(256) void gemm_kernel(LA la, LB lb, EPI epi, int M,
   gload(kb);
   sstore(0);
   __syncthreads();
-  const int frow = lane & 15, fk = 8 * (lane >> 4);
   for (int it = 0; it < nk; ++it) {
     const int cur = it & 1;
     if (it + 1 < nk) gload(kb + (it + 1) * BK);
-    const bf16_t* sA = sA0 + cur * STAGE;
-    const bf16_t* sB = sB0 + cur * STAGE;
-    bf16x8_t af[FM], bfr[FN];
+    const bf16_t* sA = smem + cur * STAGE;
+    const bf16_t* sB = sA + IA::ELEMS;
 #pragma unroll
-    for (int i = 0; i < FM; ++i)
-      af[i] = *(const bf16x8_t*)(sA + (wm * WTM + i * 16 + frow) * LDK + fk);
+    for (int kk = 0; kk < BK; kk += 32) {
+      bf16x8_t af[FM], bfr[FN];
 #pragma unroll
-    for (int j = 0; j < FN; ++j)
-      bfr[j] = *(const bf16x8_t*)(sB + (wn * WTN + j * 16 + frow) * LDK + fk);
+      for (int i = 0; i < FM; ++i) {
+        if constexpr (LA::K_CONTIG) af[i] = frag_k(sA, IA::LD, wm * WTM + i * 16, kk);
+        else af[i] = frag_t(sA, IA::LD, wm * WTM + i * 16, kk);
+      }
 #pragma unroll
-    for (int i = 0; i < FM; ++i)
+      for (int j = 0; j < FN; ++j) {
+        if constexpr (LB::K_CONTIG) bfr[j] = frag_k(sB, IB::LD, wn * WTN + j * 16, kk);
+        else bfr[j] = frag_t(sB, IB::LD, wn * WTN + j * 16, kk);
+      }
 #pragma unroll
-      for (int j = 0; j < FN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    // the other stage was last read in step it-1, which ended with a barrier
     if (it + 1 < nk) sstore(cur ^ 1);
     __syncthreads();
   }
