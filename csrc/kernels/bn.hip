@@ -227,6 +227,11 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_k(float* __restrict__ par
   coef[c] = a; coef[C + c] = c1; coef[2 * C + c] = c0;
 }
 
+PTG_DEV void load8f(const float* p, float* f) {
+  const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+  f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+}
+
 __global__ __launch_bounds__(256) void bn_bwd_apply_k(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
                                                       const bf16_t* __restrict__ z, const float* __restrict__ coef,
                                                       int relu, bf16_t* __restrict__ dz, bf16_t* __restrict__ dres,
@@ -234,19 +239,24 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(const bf16_t* __restrict__
   const long stride = (long)gridDim.x * 256;
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n8; i += stride) {
     const int c0 = (int)((i * 8) % C);
-    float g[8], zz[8];
-    unpack8(*(const U4*)(dy + i * 8), g);
-    unpack8(*(const U4*)(z + i * 8), zz);
+    const U4 vd = *(const U4*)(dy + i * 8), vz = *(const U4*)(z + i * 8);
+    const U4 vy = relu ? *(const U4*)(y + i * 8) : vd;
+    float g[8], zz[8], a[8], c1[8], c0v[8];
+    unpack8(vd, g);
+    unpack8(vz, zz);
+    load8f(coef + c0, a);
+    load8f(coef + C + c0, c1);
+    load8f(coef + 2 * C + c0, c0v);
     if (relu) {
       float yy[8];
-      unpack8(*(const U4*)(y + i * 8), yy);
+      unpack8(vy, yy);
 #pragma unroll
       for (int j = 0; j < 8; ++j) g[j] = yy[j] > 0.f ? g[j] : 0.f;
     }
     if (dres) *(U4*)(dres + i * 8) = pack8(g);
     float o[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = fmaf(coef[c0 + j], g[j], fmaf(coef[C + c0 + j], zz[j], coef[2 * C + c0 + j]));
+    for (int j = 0; j < 8; ++j) o[j] = fmaf(a[j], g[j], fmaf(c1[j], zz[j], c0v[j]));
     *(U4*)(dz + i * 8) = pack8(o);
   }
 }

@@ -154,7 +154,27 @@ struct ConvWgradB {
 // ------------------------------------------------------------------------------------------
 enum { ACT_NONE = 0, ACT_RELU = 1 };
 
+// Every epilogue has a per-element operator() and vec8(m, n, v, cnt) for the 8 consecutive
+// columns n..n+cnt-1 of row m (the kernel stages the tile through LDS so each lane owns 8
+// consecutive outputs: 16-byte stores instead of 2-byte ones).
+PTG_DEV bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+PTG_DEV void bf16_store8(bf16_t* p, float* v, int cnt, bool accum) {
+  if (cnt == 8 && al16(p)) {
+    if (accum) {
+      float e[8];
+      unpack8(*(const U4*)p, e);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += e[j];
+    }
+    *(U4*)p = pack8(v);
+    return;
+  }
+  for (int j = 0; j < cnt; ++j) p[j] = f2bf(accum ? v[j] + bf2f(p[j]) : v[j]);
+}
+
 struct EpiBf16 {  // out[m*ldc+n] = act(acc + bias[n]) (+ out if accum) as bf16 (optionally also fp32)
+  static constexpr bool VEC = true;
   bf16_t* out; long ldc; const float* bias; int act; float* out32; int accum;
   PTG_DEV void operator()(int m, int n, float v) const {
     if (bias) v += bias[n];
@@ -164,10 +184,26 @@ struct EpiBf16 {  // out[m*ldc+n] = act(acc + bias[n]) (+ out if accum) as bf16 
     *p = f2bf(v);
     if (out32) out32[(long)m * ldc + n] = v;
   }
+  PTG_DEV void vec8(int m, int n, float* v, int cnt) const {
+    if (bias && cnt == 8 && al16(bias + n)) {
+      const float4 b0 = *(const float4*)(bias + n), b1 = *(const float4*)(bias + n + 4);
+      v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
+      v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+    } else if (bias) {
+      for (int j = 0; j < cnt; ++j) v[j] += bias[n + j];
+    }
+    if (act == ACT_RELU)
+      for (int j = 0; j < cnt; ++j) v[j] = fmaxf(v[j], 0.f);
+    if (out32) {
+      for (int j = 0; j < cnt; ++j) out32[(long)m * ldc + n + j] = accum ? v[j] + bf2f(out[(long)m * ldc + n + j]) : v[j];
+    }
+    bf16_store8(out + (long)m * ldc + n, v, cnt, accum);
+  }
 };
 // Strided scatter (dgrad of a 1x1 stride-s conv): GEMM row m = output pixel (n, oh, ow) lands on
 // input pixel (n, oh*s, ow*s) of an [N][H][W][ldc] tensor; the other input pixels are untouched.
 struct EpiBf16Remap {
+  static constexpr bool VEC = true;
   bf16_t* out; long ldc; int OH, OW, H, W, s, accum;
   PTG_DEV void operator()(int m, int n, float v) const {
     const int ohw = OH * OW, b = m / ohw, rem = m - b * ohw, oh = rem / OW, ow = rem - oh * OW;
@@ -175,8 +211,13 @@ struct EpiBf16Remap {
     if (accum) v += bf2f(*p);
     *p = f2bf(v);
   }
+  PTG_DEV void vec8(int m, int n, float* v, int cnt) const {
+    const int ohw = OH * OW, b = m / ohw, rem = m - b * ohw, oh = rem / OW, ow = rem - oh * OW;
+    bf16_store8(out + (((long)b * H + oh * s) * W + ow * s) * ldc + n, v, cnt, accum);
+  }
 };
 struct EpiF32 {  // out[m*ldc+n] (=|+=) act(acc + bias)
+  static constexpr bool VEC = false;  // fp32 rows: 16 lanes already cover 64 contiguous bytes
   float* out; long ldc; const float* bias; int act; int accumulate;
   PTG_DEV void operator()(int m, int n, float v) const {
     if (bias) v += bias[n];
@@ -184,10 +225,18 @@ struct EpiF32 {  // out[m*ldc+n] (=|+=) act(acc + bias)
     float* p = out + (long)m * ldc + n;
     if (accumulate) *p += v; else *p = v;
   }
+  PTG_DEV void vec8(int m, int n, float* v, int cnt) const {
+    for (int j = 0; j < cnt; ++j) (*this)(m, n + j, v[j]);
+  }
 };
 struct EpiAtomic {  // split-K: out[m*ldc+n] += acc  (device-scope fp32 atomic, no return)
+  static constexpr bool VEC = false;  // lane-consecutive atomics coalesce; 8-per-lane runs do not
   float* out; long ldc;
   PTG_DEV void operator()(int m, int n, float v) const { atomicAdd(out + (long)m * ldc + n, v); }
+  PTG_DEV void vec8(int m, int n, float* v, int cnt) const {
+    float* p = out + (long)m * ldc + n;
+    for (int j = 0; j < cnt; ++j) atomicAdd(p + j, v[j]);
+  }
 };
 
 // ------------------------------------------------------------------------------------------
@@ -344,16 +393,44 @@ __global__ __launch_bounds__(256) void gemm_kernel(LA la, LB lb, EPI epi, int M,
   }
 
   // C/D map of mfma_f32_16x16x32: col = lane&15, row = (lane>>4)*4 + r
+  if constexpr (!EPI::VEC) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm * WTM + i * 16 + (lane >> 4) * 4 + r;
+          const int n = n0 + wn * WTN + j * 16 + (lane & 15);
+          if (m < M && n < N) epi(m, n, acc[i][j][r]);
+        }
+    return;
+  }
+  // bf16 outputs: stage the fp32 tile through LDS, then every thread hands 8 consecutive columns
+  // of a row to the epilogue (one 16-byte store instead of eight 2-byte ones).
+  constexpr int CP = BN + 4;
+  static_assert(BM * CP * 4 <= 2 * STAGE * 2, "C tile must fit in the staging LDS");
+  float* cs = reinterpret_cast<float*>(smem);
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < FN; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * WTM + i * 16 + (lane >> 4) * 4 + r;
-        const int n = n0 + wn * WTN + j * 16 + (lane & 15);
-        if (m < M && n < N) epi(m, n, acc[i][j][r]);
-      }
+      for (int r = 0; r < 4; ++r)
+        cs[(wm * WTM + i * 16 + (lane >> 4) * 4 + r) * CP + wn * WTN + j * 16 + (lane & 15)] = acc[i][j][r];
+  __syncthreads();
+  constexpr int NV = BM * BN / 8;
+#pragma unroll
+  for (int v0 = 0; v0 < NV; v0 += 256) {
+    const int v = v0 + tid;
+    if (NV % 256 != 0 && v >= NV) break;
+    const int row = v / (BN / 8), c8 = v - row * (BN / 8);
+    const int m = m0 + row, n = n0 + c8 * 8;
+    if (m >= M || n >= N) continue;
+    const float4 a = *(const float4*)(cs + row * CP + c8 * 8), b = *(const float4*)(cs + row * CP + c8 * 8 + 4);
+    float vals[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    epi.vec8(m, n, vals, min(8, N - n));
+  }
 }
 
 template <int BM, int BN, int WM, int WN, class LA, class LB, class EPI>

@@ -388,31 +388,42 @@ __global__ __launch_bounds__(256) void mse_k(const float* __restrict__ pred, con
 // softmax + sparse categorical cross-entropy on logits (row per thread, C <= 64).
 // probs clipped to [1e-7, 1-1e-7] like Keras' backend.  dlogits = (p - onehot) / B * gscale.
 // stats: [loss_sum, correct, -, -, count]
+// One wave per row (ResNet-50's 1000-class head: B rows x 1000 logits); lanes stride the classes.
 __global__ __launch_bounds__(256) void softmax_xent_k(const float* __restrict__ logits,
                                                       const int* __restrict__ labels,
                                                       float* __restrict__ dlogits, float* __restrict__ stats,
                                                       int B, int C, float gscale) {
-  __shared__ float scr[4];
-  float loss = 0.f, corr = 0.f;
-  for (int b = threadIdx.x; b < B; b += 256) {
-    const float* r = logits + (long)b * C;
-    float mx = -INFINITY; int am = 0;
-    for (int c = 0; c < C; ++c) if (r[c] > mx) { mx = r[c]; am = c; }
-    float s = 0.f;
-    for (int c = 0; c < C; ++c) s += __expf(r[c] - mx);
-    const int lab = labels[b];
-    for (int c = 0; c < C; ++c) {
-      const float p = __expf(r[c] - mx) / s;
-      dlogits[(long)b * C + c] = (p - (c == lab ? 1.f : 0.f)) / (float)B * gscale;
-    }
-    const float pl = fminf(fmaxf(__expf(r[lab] - mx) / s, 1e-7f), 1.f - 1e-7f);
-    loss += -__logf(pl);
-    corr += (am == lab) ? 1.f : 0.f;
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const float* r = logits + (long)b * C;
+  float mx = -INFINITY;
+  int am = 0x7fffffff;
+  for (int c = lane; c < C; c += 64) {
+    const float v = r[c];
+    if (v > mx) { mx = v; am = c; }
   }
-  const float sl = block_sum256(loss, scr);
-  __syncthreads();
-  const float sc = block_sum256(corr, scr);
-  if (threadIdx.x == 0) { stats[0] += sl; stats[1] += sc; stats[4] += (float)B; }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {  // arg-max, lowest index on ties
+    const float om = __shfl_xor(mx, o, 64);
+    const int oa = __shfl_xor(am, o, 64);
+    if (om > mx || (om == mx && oa < am)) { mx = om; am = oa; }
+  }
+  float s = 0.f;
+  for (int c = lane; c < C; c += 64) s += __expf(r[c] - mx);
+  s = wave_sum(s);
+  const int lab = labels[b];
+  const float inv = 1.f / s, scale = gscale / (float)B;
+  for (int c = lane; c < C; c += 64) {
+    const float pr = __expf(r[c] - mx) * inv;
+    dlogits[(long)b * C + c] = (pr - (c == lab ? 1.f : 0.f)) * scale;
+  }
+  if (lane == 0) {
+    const float pl = fminf(fmaxf(__expf(r[lab] - mx) * inv, 1e-7f), 1.f - 1e-7f);
+    atomicAdd(stats + 0, -__logf(pl));
+    atomicAdd(stats + 1, am == lab ? 1.f : 0.f);
+    atomicAdd(stats + 4, 1.f);
+  }
 }
 
 // ----------------------------------------------------------------------------------------------
@@ -682,7 +693,8 @@ int ptg_mse(const float* pred, const float* y, float* dpred, float* stats, int B
 
 int ptg_softmax_xent(const float* logits, const int* labels, float* dlogits, float* stats, int B, int C,
                      float gscale, hipStream_t s) {
-  hipLaunchKernelGGL(softmax_xent_k, dim3(1), dim3(256), 0, s, logits, labels, dlogits, stats, B, C, gscale);
+  hipLaunchKernelGGL(softmax_xent_k, dim3(ptg_ceil_div(B, 4)), dim3(256), 0, s, logits, labels, dlogits, stats, B, C,
+                     gscale);
   PTG_RETURN_LAUNCH();
 }
 

@@ -9,6 +9,14 @@ parallel on a thread pool, ``num_parallel_calls=AUTOTUNE``), ``filter``, ``shard
 Elements are tuples of numpy arrays (or a single array).  Batches stay on the host; the trainer
 uploads them with pinned, non-blocking copies (and raw uint8 images are resized/normalised on the
 GPU by the first conv op).
+
+Columnar fast path: a ``from_tensor_slices`` source followed only by ``shard`` / ``shuffle`` /
+``batch`` / ``repeat`` / ``prefetch`` never iterates elements in Python: it builds index
+permutations and gathers whole batches (``index_select`` on device tensors, fancy indexing on host
+arrays).  Device tensors stay on the device, so a DataFrame column handed over by the ETL stage
+(the joint Spark -> TF pipeline) feeds the trainer without a host round trip.  ``shuffle`` with
+``buffer_size >= cardinality`` is an exact uniform shuffle; a smaller buffer is emulated by
+shuffling within consecutive windows of ``buffer_size`` elements and then shuffling window order.
 """
 from __future__ import annotations
 
@@ -35,44 +43,134 @@ def _np(x):
     return np.asarray(x)
 
 
+class _ColPlan:
+    """Vectorised plan of an array-backed dataset (see module docstring)."""
+
+    def __init__(self, arrays, kind, keys=None):
+        self.arrays, self.kind, self.keys = arrays, kind, keys
+        self.n = len(arrays[0])
+        self.ops: list = []  # ("shard", n, i) | ("shuffle", buf, seed, reshuffle) | ("batch", bs, drop) | ("repeat", c)
+        self.epoch = 0
+
+    def extend(self, op) -> "_ColPlan":
+        p = _ColPlan(self.arrays, self.kind, self.keys)
+        p.ops = self.ops + [op]
+        return p
+
+    def names(self):
+        return [o[0] for o in self.ops]
+
+    def _is_torch(self, a):
+        return type(a).__module__.startswith("torch")
+
+    def _gather(self, sel):
+        out = []
+        for a in self.arrays:
+            if self._is_torch(a):
+                import torch
+
+                out.append(a.index_select(0, torch.as_tensor(sel, device=a.device)))
+            else:
+                out.append(a[sel])
+        return self._pack(out)
+
+    def _pack(self, cols):
+        if self.kind == "tuple":
+            return tuple(cols)
+        if self.kind == "dict":
+            return dict(zip(self.keys, cols))
+        return cols[0]
+
+    def _order(self, base, shuffle, epoch):
+        if shuffle is None:
+            return base
+        _, buf, seed, reshuffle = shuffle
+        s = seed if seed is not None else 0x5EED
+        rng = np.random.default_rng((s, epoch) if reshuffle else s)
+        if buf >= len(base):
+            return base[rng.permutation(len(base))]
+        w = max(1, int(buf))
+        chunks = [base[i:i + w] for i in range(0, len(base), w)]
+        chunks = [c[rng.permutation(len(c))] for c in chunks]
+        return np.concatenate([chunks[i] for i in rng.permutation(len(chunks))]) if chunks else base
+
+    def __iter__(self):
+        base = np.arange(self.n)
+        shuffle, batch, repeat, batch_before_repeat = None, None, None, True
+        for op in self.ops:
+            if op[0] == "shard":
+                base = base[op[2]::op[1]]
+            elif op[0] == "shuffle":
+                shuffle = op
+            elif op[0] == "batch":
+                batch = op
+            elif op[0] == "repeat":
+                repeat = op[1]
+                batch_before_repeat = batch is not None
+        epochs = itertools.count() if (repeat is not None and repeat < 0) else range(1 if repeat is None else repeat)
+
+        def epoch_orders():
+            for _ in epochs:
+                e = self.epoch
+                self.epoch += 1
+                yield self._order(base, shuffle, e)
+
+        if batch is None:
+            for order in epoch_orders():
+                for i in order:
+                    yield self._pack([a[int(i)] for a in self.arrays])
+            return
+        bs, drop = batch[1], batch[2]
+        if batch_before_repeat:
+            for order in epoch_orders():
+                for st in range(0, len(order), bs):
+                    sel = order[st:st + bs]
+                    if drop and len(sel) < bs:
+                        break
+                    yield self._gather(sel)
+            return
+        pending = np.zeros(0, dtype=np.int64)
+        for order in epoch_orders():
+            pending = np.concatenate([pending, order])
+            while len(pending) >= bs:
+                yield self._gather(pending[:bs])
+                pending = pending[bs:]
+        if len(pending) and not drop:
+            yield self._gather(pending)
+
+
+def _keep(a):
+    """Array-like for the columnar path: GPU tensors stay on the device, the rest become numpy."""
+    if type(a).__module__.startswith("torch") and a.is_cuda:
+        return a
+    return _np(a)
+
+
 class Dataset:
-    def __init__(self, gen_fn, card: int = UNKNOWN):
+    def __init__(self, gen_fn, card: int = UNKNOWN, plan: _ColPlan | None = None):
         self._gen_fn = gen_fn
         self._card = card
+        self._plan = plan
+
+    @staticmethod
+    def _from_plan(plan: _ColPlan, card: int) -> "Dataset":
+        return Dataset(lambda: iter(plan), card, plan)
 
     # ------------------------------------------------------------------ sources
     @staticmethod
     def from_tensor_slices(tensors) -> "Dataset":
         if isinstance(tensors, dict):
             keys = list(tensors)
-            arrs = [_np(tensors[k]) for k in keys]
-            n = len(arrs[0])
-
-            def gen():
-                for i in range(n):
-                    yield {k: a[i] for k, a in zip(keys, arrs)}
-
-            return Dataset(gen, n)
-        if isinstance(tensors, (tuple, list)):
-            arrs = [_np(t) for t in tensors]
-            n = len(arrs[0])
-            if any(len(a) != n for a in arrs):
+            arrs = [_keep(tensors[k]) for k in keys]
+            plan = _ColPlan(arrs, "dict", keys)
+        elif isinstance(tensors, (tuple, list)):
+            arrs = [_keep(t) for t in tensors]
+            if any(len(a) != len(arrs[0]) for a in arrs):
                 raise ValueError("from_tensor_slices: components differ in length")
-
-            def gen():
-                for i in range(n):
-                    yield tuple(a[i] for a in arrs)
-
-            ds = Dataset(gen, n)
-            ds._arrays = arrs  # fast path for index-based batching
-            return ds
-        arr = _np(tensors)
-
-        def gen1():
-            for i in range(len(arr)):
-                yield arr[i]
-
-        return Dataset(gen1, len(arr))
+            plan = _ColPlan(arrs, "tuple")
+        else:
+            plan = _ColPlan([_keep(tensors)], "single")
+        return Dataset._from_plan(plan, plan.n)
 
     @staticmethod
     def from_generator(generator, output_signature=None, output_types=None) -> "Dataset":
@@ -121,13 +219,15 @@ class Dataset:
     def shard(self, num_shards: int, index: int) -> "Dataset":
         src = self
         card = UNKNOWN if self._card < 0 else (self._card - index + num_shards - 1) // num_shards
-        ds = Dataset(lambda: itertools.islice(iter(src), index, None, num_shards), card)
-        if hasattr(self, "_arrays"):
-            ds._arrays = [a[index::num_shards] for a in self._arrays]
-        return ds
+        if self._plan is not None and self._plan.ops == []:
+            return Dataset._from_plan(self._plan.extend(("shard", num_shards, index)), card)
+        return Dataset(lambda: itertools.islice(iter(src), index, None, num_shards), card)
 
     def shuffle(self, buffer_size: int, seed=None, reshuffle_each_iteration: bool = True) -> "Dataset":
         src = self
+        if self._plan is not None and set(self._plan.names()) <= {"shard"}:
+            return Dataset._from_plan(self._plan.extend(("shuffle", int(buffer_size), seed, reshuffle_each_iteration)),
+                                      self._card)
         state = {"epoch": 0}
 
         def gen():
@@ -150,6 +250,12 @@ class Dataset:
 
     def batch(self, batch_size: int, drop_remainder: bool = False) -> "Dataset":
         src = self
+        if self._plan is not None and "batch" not in self._plan.names():
+            if self._card >= 0:
+                card = self._card // batch_size if drop_remainder else -(-self._card // batch_size)
+            else:
+                card = self._card
+            return Dataset._from_plan(self._plan.extend(("batch", int(batch_size), bool(drop_remainder))), card)
 
         def stack(items):
             if isinstance(items[0], tuple):
@@ -187,6 +293,10 @@ class Dataset:
 
     def repeat(self, count=None) -> "Dataset":
         src = self
+        if self._plan is not None and "repeat" not in self._plan.names():
+            c = -1 if count is None else int(count)
+            card = INFINITE if c < 0 else (self._card * c if self._card >= 0 else UNKNOWN)
+            return Dataset._from_plan(self._plan.extend(("repeat", c)), card)
 
         def gen():
             n = 0
@@ -214,6 +324,8 @@ class Dataset:
 
     def prefetch(self, buffer_size=1) -> "Dataset":
         src = self
+        if self._plan is not None:
+            return self  # batches are gathered on demand (device-side for device tensors)
         depth = 2 if buffer_size in (None, AUTOTUNE) else max(1, int(buffer_size))
 
         def gen():

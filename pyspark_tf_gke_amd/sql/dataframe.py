@@ -152,6 +152,9 @@ class DataFrame:
             a, b = self._eval(Column(base[2]))[1], self._eval(Column(base[3]))[1]
             if isinstance(a.dtype, T.StringType) and isinstance(b.dtype, T.StringType):
                 return name, _coalesce_strings(a, b)
+        # rand()/monotonically_increasing_id() nested inside an expression: materialise them as
+        # temporary columns so the device expression VM only sees column/literal leaves
+        node, t = self._materialize_leaves(node, t)
         dtype = C.infer_type(node, t)
         if isinstance(dtype, T.StringType):
             raise TypeError(f"string-valued expression {name} is not supported")
@@ -176,6 +179,27 @@ class DataFrame:
         else:
             out = torch.where(ok, v, torch.full_like(v, math.nan)).to(tdt)
         return name, ColumnVector(out, dtype, ok.to(torch.uint8))
+
+    def _materialize_leaves(self, node, t):
+        tmp = {}
+
+        def walk(nd):
+            if isinstance(nd, tuple) and nd and nd[0] in ("rand", "rowid"):
+                key = f"__leaf{len(tmp)}"
+                tmp[key] = self._eval(Column(nd))[1]
+                return ("col", key)
+            if isinstance(nd, tuple):
+                return tuple(walk(x) if isinstance(x, tuple) else (
+                    [tuple(walk(y) for y in pair) if isinstance(pair, tuple) else pair for pair in x]
+                    if isinstance(x, list) else x) for x in nd)
+            return nd
+
+        new = walk(node)
+        if not tmp:
+            return node, t
+        for k, cv in tmp.items():
+            t = t.with_column(k, cv)
+        return new, t
 
     def _mask(self, cond) -> torch.Tensor:
         t = self._t

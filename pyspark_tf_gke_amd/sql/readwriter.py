@@ -407,6 +407,8 @@ def _arrow_to_table(at, device) -> Table:
                                       T.BooleanType(), valid)
         else:
             np_arr = np.asarray(arr.fill_null(0) if arr.null_count else arr)
+            if not np_arr.flags.writeable:  # arrow buffers are read-only; torch needs a writable array
+                np_arr = np_arr.copy()
             tt = torch.from_numpy(np.ascontiguousarray(np_arr))
             if tt.dtype == torch.int32:
                 dt = T.IntegerType()
