@@ -483,9 +483,150 @@ __global__ __launch_bounds__(256) void part_scatter_k(const long long* __restric
     ovals[dst] = load_col(val, vtype, i, ok);
   }
 }
+// Block-private partitioning (replaces the global-cursor scatter above for large inputs):
+// pass A counts each block's rows per partition into hist[p][block] (partition-major), an
+// exclusive scan over that array gives every (partition, block) pair its own contiguous output run,
+// and pass B scatters: a block's rows of partition p land in one run of ~rows_per_block/P rows
+// written by one CU, instead of single 8-byte stores spread over P global cursors (which leave
+// partially written lines in the L2s of all 8 XCDs).
+__global__ __launch_bounds__(256) void part_count_k(const long long* __restrict__ keys, long n, int pbits,
+                                                    long rows_per_block, unsigned int* __restrict__ hist, int nb) {
+  __shared__ unsigned int h[4096];
+  const int P = 1 << pbits;
+  for (int t = threadIdx.x; t < P; t += 256) h[t] = 0;
+  __syncthreads();
+  const long r0 = (long)blockIdx.x * rows_per_block, r1 = min(n, r0 + rows_per_block);
+  for (long i = r0 + threadIdx.x; i < r1; i += 256)
+    atomicAdd(&h[(unsigned)(mix64((unsigned long long)keys[i]) >> (64 - pbits))], 1u);
+  __syncthreads();
+  for (int t = threadIdx.x; t < P; t += 256) hist[(long)t * nb + blockIdx.x] = h[t];
+}
+__global__ __launch_bounds__(256) void part_scatter_runs_k(const long long* __restrict__ keys,
+                                                           const void* __restrict__ val, int vtype, long n, int pbits,
+                                                           long rows_per_block, const long long* __restrict__ offs,
+                                                           int nb, long long* __restrict__ okeys,
+                                                           double* __restrict__ ovals) {
+  __shared__ unsigned long long base[4096];
+  __shared__ unsigned int lc[4096];
+  const int P = 1 << pbits;
+  for (int t = threadIdx.x; t < P; t += 256) {
+    base[t] = (unsigned long long)offs[(long)t * nb + blockIdx.x];
+    lc[t] = 0;
+  }
+  __syncthreads();
+  const long r0 = (long)blockIdx.x * rows_per_block, r1 = min(n, r0 + rows_per_block);
+  for (long i = r0 + threadIdx.x; i < r1; i += 256) {
+    const long long k = keys[i];
+    const unsigned p = (unsigned)(mix64((unsigned long long)k) >> (64 - pbits));
+    bool ok = true;
+    const double v = load_col(val, vtype, i, ok);
+    const unsigned long long dst = base[p] + atomicAdd(&lc[p], 1u);
+    okeys[dst] = k;
+    ovals[dst] = v;
+  }
+}
+
+// Two-level LSD-free radix partitioning with LDS staging (the groupBy hot path at 1B rows).
+// Element-granular scatter is uncoalesced (cdna_hip_programming.md App. B "Scatter"), so each level
+// moves tiles of RT rows: a tile is counting-sorted by a 6-bit hash digit in LDS and then written
+// as 64 contiguous runs (~RT/64 rows = 512 B of keys per run).  Output offsets come from an
+// exclusive scan over per-tile digit counts laid out [segment][digit][tile]: one global scan gives
+// every (segment, digit, tile) its run.  Level 1 splits the input into 64 segments by hash bits
+// 58..63, level 2 splits each segment by bits 52..57 -> 4096 partitions of ~n/4096 rows and
+// ~keys/4096 distinct keys, small enough for one LDS hash table each (part_agg_k).
+#define RT 2048
+#define RB 64
+__global__ __launch_bounds__(256) void radix_count_k(const long long* __restrict__ keys,
+                                                     const long long* __restrict__ tstart,
+                                                     const int* __restrict__ trows,
+                                                     const long long* __restrict__ thbase,
+                                                     const long long* __restrict__ thstride, int shift,
+                                                     unsigned int* __restrict__ hist) {
+  __shared__ unsigned int h[RB];
+  const int tid = threadIdx.x, b = blockIdx.x;
+  if (tid < RB) h[tid] = 0;
+  __syncthreads();
+  const long long s0 = tstart[b];
+  const int nr = trows[b];
+  for (int i = tid; i < nr; i += 256)
+    atomicAdd(&h[(unsigned)(mix64((unsigned long long)keys[s0 + i]) >> shift) & (RB - 1)], 1u);
+  __syncthreads();
+  if (tid < RB) hist[thbase[b] + (long long)tid * thstride[b]] = h[tid];
+}
+
+__global__ __launch_bounds__(256) void radix_scatter_k(const long long* __restrict__ keys,
+                                                       const void* __restrict__ val, int vtype,
+                                                       const long long* __restrict__ tstart,
+                                                       const int* __restrict__ trows,
+                                                       const long long* __restrict__ thbase,
+                                                       const long long* __restrict__ thstride, int shift,
+                                                       const long long* __restrict__ offs,
+                                                       long long* __restrict__ okeys, double* __restrict__ ovals) {
+  constexpr int RPT = RT / 256;
+  __shared__ long long sk[RT];
+  __shared__ double sv[RT];
+  __shared__ unsigned char sd[RT];
+  __shared__ unsigned int cnt[RB];
+  __shared__ unsigned int lstart[RB];
+  __shared__ long long goff[RB];
+  const int tid = threadIdx.x, b = blockIdx.x;
+  const long long s0 = tstart[b];
+  const int nr = trows[b];
+  if (tid < RB) {
+    cnt[tid] = 0;
+    goff[tid] = offs[thbase[b] + (long long)tid * thstride[b]];
+  }
+  __syncthreads();
+  long long k[RPT];
+  double v[RPT];
+  int d[RPT];
+#pragma unroll
+  for (int j = 0; j < RPT; ++j) {
+    const int i = tid + j * 256;
+    d[j] = -1;
+    if (i < nr) {
+      bool ok = true;
+      k[j] = keys[s0 + i];
+      v[j] = load_col(val, vtype, s0 + i, ok);
+      d[j] = (int)((mix64((unsigned long long)k[j]) >> shift) & (RB - 1));
+      atomicAdd(&cnt[d[j]], 1u);
+    }
+  }
+  __syncthreads();
+  if (tid < RB) {  // exclusive scan of the 64 digit counts within one wave
+    const unsigned c = cnt[tid];
+    unsigned incl = c;
+#pragma unroll
+    for (int o = 1; o < RB; o <<= 1) {
+      const unsigned t = __shfl_up(incl, o, 64);
+      if (tid >= o) incl += t;
+    }
+    lstart[tid] = incl - c;
+    cnt[tid] = 0;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < RPT; ++j) {
+    if (d[j] < 0) continue;
+    const unsigned pos = lstart[d[j]] + atomicAdd(&cnt[d[j]], 1u);
+    sk[pos] = k[j];
+    sv[pos] = v[j];
+    sd[pos] = (unsigned char)d[j];
+  }
+  __syncthreads();
+  for (int i = tid; i < nr; i += 256) {  // consecutive rows of a digit run -> consecutive addresses
+    const int dd = sd[i];
+    const long long dst = goff[dd] + (i - (int)lstart[dd]);
+    okeys[dst] = sk[i];
+    ovals[dst] = sv[i];
+  }
+}
+
 // pass 3: one workgroup per partition segment aggregates in LDS (sum, count) — rows of a partition
 // never meet another partition's keys, so each partition's table is final: no merge needed.
-#define PCAP 4096
+// PCAP = LDS table slots: 1024 for the 4096-partition path (~keys/4096 distinct keys per partition,
+// 244 at 1M keys: <25 % load, 20 KB LDS -> several blocks per CU), 4096 for coarser partitionings.
+template <int PCAP>
 __global__ __launch_bounds__(256) void part_agg_k(const long long* __restrict__ okeys, const double* __restrict__ ovals,
                                                   const unsigned long long* __restrict__ pstart, int P,
                                                   long long* __restrict__ out_keys, double* __restrict__ out_sum,
@@ -494,41 +635,45 @@ __global__ __launch_bounds__(256) void part_agg_k(const long long* __restrict__ 
                                                   int* __restrict__ overflow) {
   __shared__ long long lk[PCAP];
   __shared__ double ls[PCAP];
-  __shared__ double lcnt[PCAP];
+  __shared__ unsigned int lcnt[PCAP];
+  auto insert = [&](long long key, double v) {
+    int h = (int)(mix64((unsigned long long)key) & (PCAP - 1));
+    for (int probe = 0; probe < 64; ++probe) {
+      const long long cur = lk[h];
+      if (cur == key) { atomicAdd(&ls[h], v); atomicAdd(&lcnt[h], 1u); return; }
+      if (cur == EMPTY_KEY) {
+        const long long prev = (long long)atomicCAS((unsigned long long*)&lk[h], (unsigned long long)EMPTY_KEY,
+                                                    (unsigned long long)key);
+        if (prev == EMPTY_KEY || prev == key) { atomicAdd(&ls[h], v); atomicAdd(&lcnt[h], 1u); return; }
+      }
+      h = (h + 1) & (PCAP - 1);
+    }
+    // partition exceeds the LDS table: global overflow table
+    const long gs = gtable_slot(gkeys, gcap, key);
+    if (gs < 0) { atomicAdd(overflow, 1); return; }
+    atomicAdd(&gtab[gs], 1.0);
+    atomicAdd(&gtab[gcap + gs], v);
+    atomicAdd(&gtab[2 * gcap + gs], 1.0);
+  };
   for (int p = blockIdx.x; p < P; p += gridDim.x) {
     for (int t = threadIdx.x; t < PCAP; t += 256) { lk[t] = EMPTY_KEY; ls[t] = 0; lcnt[t] = 0; }
     __syncthreads();
     const unsigned long long a = pstart[p], b = pstart[p + 1];
-    for (unsigned long long i = a + threadIdx.x; i < b; i += 256) {
-      const long long key = okeys[i];
-      const double v = ovals[i];
-      int h = (int)(mix64((unsigned long long)key) & (PCAP - 1));
-      int slot = -1;
-      for (int probe = 0; probe < 64; ++probe) {
-        const long long cur = lk[h];
-        if (cur == key) { slot = h; break; }
-        if (cur == EMPTY_KEY) {
-          const long long prev = (long long)atomicCAS((unsigned long long*)&lk[h], (unsigned long long)EMPTY_KEY,
-                                                      (unsigned long long)key);
-          if (prev == EMPTY_KEY || prev == key) { slot = h; break; }
-        }
-        h = (h + 1) & (PCAP - 1);
-      }
-      if (slot >= 0) {
-        atomicAdd(&ls[slot], v); atomicAdd(&lcnt[slot], 1.0);
-      } else {  // partition exceeds the LDS table: global overflow table
-        const long gs = gtable_slot(gkeys, gcap, key);
-        if (gs < 0) { atomicAdd(overflow, 1); continue; }
-        atomicAdd(&gtab[gs], 1.0);
-        atomicAdd(&gtab[gcap + gs], v);
-        atomicAdd(&gtab[2 * gcap + gs], 1.0);
-      }
+    unsigned long long i = a + threadIdx.x;
+    for (; i + 3 * 256 < b; i += 4 * 256) {  // 4 rows in flight per thread
+      long long k4[4];
+      double v4[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) { k4[u] = okeys[i + u * 256]; v4[u] = ovals[i + u * 256]; }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) insert(k4[u], v4[u]);
     }
+    for (; i < b; i += 256) insert(okeys[i], ovals[i]);
     __syncthreads();
     for (int t = threadIdx.x; t < PCAP; t += 256) {
       if (lk[t] == EMPTY_KEY) continue;
       const unsigned long long q = atomicAdd(m_out, 1ULL);
-      out_keys[q] = lk[t]; out_sum[q] = ls[t]; out_cnt[q] = lcnt[t];
+      out_keys[q] = lk[t]; out_sum[q] = ls[t]; out_cnt[q] = (double)lcnt[t];
     }
     __syncthreads();
   }
@@ -709,12 +854,47 @@ int ptg_part_scatter(const void* keys, const void* val, int vtype, long n, int p
                      vtype, n, pbits, (unsigned long long*)cursor, (long long*)okeys, (double*)ovals, rpb);
   PTG_RETURN_LAUNCH();
 }
+int ptg_part_count(const void* keys, long n, int pbits, long rows_per_block, void* hist, int nb, hipStream_t s) {
+  if (pbits > 12) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(part_count_k, dim3(nb), dim3(256), 0, s, (const long long*)keys, n, pbits, rows_per_block,
+                     (unsigned int*)hist, nb);
+  PTG_RETURN_LAUNCH();
+}
+int ptg_part_scatter_runs(const void* keys, const void* val, int vtype, long n, int pbits, long rows_per_block,
+                          const void* offs, int nb, void* okeys, void* ovals, hipStream_t s) {
+  if (pbits > 12) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(part_scatter_runs_k, dim3(nb), dim3(256), 0, s, (const long long*)keys, val, vtype, n, pbits,
+                     rows_per_block, (const long long*)offs, nb, (long long*)okeys, (double*)ovals);
+  PTG_RETURN_LAUNCH();
+}
+int ptg_radix_count(const void* keys, const void* tstart, const void* trows, const void* thbase,
+                    const void* thstride, int ntiles, int shift, void* hist, hipStream_t s) {
+  if (ntiles <= 0) return 0;
+  hipLaunchKernelGGL(radix_count_k, dim3(ntiles), dim3(256), 0, s, (const long long*)keys,
+                     (const long long*)tstart, (const int*)trows, (const long long*)thbase,
+                     (const long long*)thstride, shift, (unsigned int*)hist);
+  PTG_RETURN_LAUNCH();
+}
+int ptg_radix_scatter(const void* keys, const void* val, int vtype, const void* tstart, const void* trows,
+                      const void* thbase, const void* thstride, int ntiles, int shift, const void* offs, void* okeys,
+                      void* ovals, hipStream_t s) {
+  if (ntiles <= 0) return 0;
+  hipLaunchKernelGGL(radix_scatter_k, dim3(ntiles), dim3(256), 0, s, (const long long*)keys, val, vtype,
+                     (const long long*)tstart, (const int*)trows, (const long long*)thbase,
+                     (const long long*)thstride, shift, (const long long*)offs, (long long*)okeys, (double*)ovals);
+  PTG_RETURN_LAUNCH();
+}
 int ptg_part_agg(const void* okeys, const void* ovals, const void* pstart, int P, void* out_keys, void* out_sum,
                  void* out_cnt, void* m_out, void* gkeys, void* gtab, long gcap, void* overflow, hipStream_t s) {
-  int g = P < 1024 ? P : 1024;
-  hipLaunchKernelGGL(part_agg_k, dim3(g), dim3(256), 0, s, (const long long*)okeys, (const double*)ovals,
-                     (const unsigned long long*)pstart, P, (long long*)out_keys, (double*)out_sum, (double*)out_cnt,
-                     (unsigned long long*)m_out, (long long*)gkeys, (double*)gtab, gcap, (int*)overflow);
+  int g = P < 2048 ? P : 2048;
+  if (P >= 4096)
+    hipLaunchKernelGGL(part_agg_k<1024>, dim3(g), dim3(256), 0, s, (const long long*)okeys, (const double*)ovals,
+                       (const unsigned long long*)pstart, P, (long long*)out_keys, (double*)out_sum, (double*)out_cnt,
+                       (unsigned long long*)m_out, (long long*)gkeys, (double*)gtab, gcap, (int*)overflow);
+  else
+    hipLaunchKernelGGL(part_agg_k<4096>, dim3(g), dim3(256), 0, s, (const long long*)okeys, (const double*)ovals,
+                       (const unsigned long long*)pstart, P, (long long*)out_keys, (double*)out_sum, (double*)out_cnt,
+                       (unsigned long long*)m_out, (long long*)gkeys, (double*)gtab, gcap, (int*)overflow);
   PTG_RETURN_LAUNCH();
 }
 

@@ -325,6 +325,22 @@ __global__ __launch_bounds__(256) void dense_small_fwd_k(const TX* __restrict__ 
   }
 }
 
+// Narrow-K forward (K <= 64, e.g. the CSV MLP's 3 -> 16 -> 32 -> 64 layers at large batch): one
+// thread per output element, no softmax (act 0/1).
+template <typename TX>
+__global__ __launch_bounds__(256) void dense_small_fwd_t_k(const TX* __restrict__ x, const float* __restrict__ w,
+                                                           const float* __restrict__ b, float* __restrict__ y,
+                                                           bf16_t* __restrict__ ybf, int M, int K, int N, int act) {
+  const long i = blockIdx.x * 256L + threadIdx.x;
+  if (i >= (long)M * N) return;
+  const int m = i / N, n = i - (long)m * N;
+  float s = b ? b[n] : 0.f;
+  for (int k = 0; k < K; ++k) s += ldf(x, (long)m * K + k) * w[(long)n * K + k];
+  if (act == 1) s = fmaxf(s, 0.f);
+  y[i] = s;
+  if (ybf) ybf[i] = f2bf(s);
+}
+
 // dx[m][k] = (sum_n dy[m][n] w[n][k]) * (mask ? (mask[m][k] > 0) : 1)
 template <typename TM, typename TO>
 __global__ __launch_bounds__(256) void dense_small_dx_k(const float* __restrict__ dy, const float* __restrict__ w,
@@ -341,20 +357,25 @@ __global__ __launch_bounds__(256) void dense_small_dx_k(const float* __restrict_
 
 // dw[n][k] += sum_m dy[m][n] x[m][k];  db[n] += sum_m dy[m][n]
 template <typename TX>
+// dW[N][K] += dy^T x, db[N] += colsum(dy): thread per output, blockIdx.y = slice of the M rows
+// (split-M with fp32 atomics, so a large batch - the joint pipeline's 8192-row MLP batches - is not
+// a serial loop per thread).
 __global__ __launch_bounds__(256) void dense_small_dw_k(const float* __restrict__ dy, const TX* __restrict__ x,
                                                         float* __restrict__ dw, float* __restrict__ db, int M,
-                                                        int K, int N) {
+                                                        int K, int N, int rows_per_slice) {
   const long i = blockIdx.x * 256L + threadIdx.x;
+  const int m0 = blockIdx.y * rows_per_slice, m1 = min(M, m0 + rows_per_slice);
+  const bool single = gridDim.y == 1;
   if (i < (long)N * K) {
     const int n = i / K, k = i - (long)n * K;
     float s = 0.f;
-    for (int m = 0; m < M; ++m) s += dy[(long)m * N + n] * ldf(x, (long)m * K + k);
-    dw[i] += s;
+    for (int m = m0; m < m1; ++m) s += dy[(long)m * N + n] * ldf(x, (long)m * K + k);
+    if (single) dw[i] += s; else atomicAdd(dw + i, s);
   }
   if (db && i < N) {
     float s = 0.f;
-    for (int m = 0; m < M; ++m) s += dy[(long)m * N + i];
-    db[i] += s;
+    for (int m = m0; m < m1; ++m) s += dy[(long)m * N + i];
+    if (single) db[i] += s; else atomicAdd(db + i, s);
   }
 }
 
@@ -639,6 +660,16 @@ int ptg_col_sum(const void* g, int g_is_bf16, float* db, int M, int N, hipStream
 int ptg_dense_small_fwd(const void* x, int x_is_bf16, const float* w, const float* b, float* y, void* ybf,
                         int M, int K, int N, int act, hipStream_t s) {
   if (N > 64) return (int)hipErrorInvalidValue;
+  if (K <= 64 && act != 2 && M >= 256) {
+    const dim3 g(ptg_ceil_div((long)M * N, 256));
+    if (x_is_bf16)
+      hipLaunchKernelGGL(dense_small_fwd_t_k<bf16_t>, g, dim3(256), 0, s, (const bf16_t*)x, w, b, y, (bf16_t*)ybf, M,
+                         K, N, act);
+    else
+      hipLaunchKernelGGL(dense_small_fwd_t_k<float>, g, dim3(256), 0, s, (const float*)x, w, b, y, (bf16_t*)ybf, M,
+                         K, N, act);
+    PTG_RETURN_LAUNCH();
+  }
   dim3 grid((M + 3) / 4);
   if (x_is_bf16)
     hipLaunchKernelGGL(dense_small_fwd_k<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, w, b, y,
@@ -677,11 +708,16 @@ int ptg_dense_small_dw(const float* dy, const void* x, int x_is_bf16, float* dw,
                        int N, hipStream_t s) {
   long total = (long)N * K;
   if (total < N) total = N;
-  dim3 grid((total + 255) / 256);
+  const int bx = (int)((total + 255) / 256);
+  // split the rows so the grid has >= ~512 blocks, each slice >= 64 rows
+  int slices = 1;
+  while (bx * slices < 512 && M / (slices * 2) >= 64) slices *= 2;
+  const int rps = ptg_ceil_div(M, slices);
+  dim3 grid(bx, slices);
   if (x_is_bf16)
-    hipLaunchKernelGGL(dense_small_dw_k<bf16_t>, grid, dim3(256), 0, s, dy, (const bf16_t*)x, dw, db, M, K, N);
+    hipLaunchKernelGGL(dense_small_dw_k<bf16_t>, grid, dim3(256), 0, s, dy, (const bf16_t*)x, dw, db, M, K, N, rps);
   else
-    hipLaunchKernelGGL(dense_small_dw_k<float>, grid, dim3(256), 0, s, dy, (const float*)x, dw, db, M, K, N);
+    hipLaunchKernelGGL(dense_small_dw_k<float>, grid, dim3(256), 0, s, dy, (const float*)x, dw, db, M, K, N, rps);
   PTG_RETURN_LAUNCH();
 }
 

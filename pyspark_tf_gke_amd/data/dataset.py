@@ -63,15 +63,23 @@ class _ColPlan:
     def _is_torch(self, a):
         return type(a).__module__.startswith("torch")
 
+    def _device(self):
+        """Device of the GPU-resident columns (index math then stays on the GPU), else None."""
+        for a in self.arrays:
+            if self._is_torch(a):
+                return a.device
+        return None
+
     def _gather(self, sel):
         out = []
         for a in self.arrays:
             if self._is_torch(a):
                 import torch
 
-                out.append(a.index_select(0, torch.as_tensor(sel, device=a.device)))
+                idx = sel if isinstance(sel, torch.Tensor) else torch.as_tensor(sel, device=a.device)
+                out.append(a.index_select(0, idx))
             else:
-                out.append(a[sel])
+                out.append(a[sel.cpu().numpy() if hasattr(sel, "cpu") else sel])
         return self._pack(out)
 
     def _pack(self, cols):
@@ -86,6 +94,15 @@ class _ColPlan:
             return base
         _, buf, seed, reshuffle = shuffle
         s = seed if seed is not None else 0x5EED
+        dev = self._device()
+        if dev is not None and buf >= len(base):
+            import torch
+
+            g = torch.Generator(device=dev)
+            g.manual_seed(int(s) * 1000003 + (epoch if reshuffle else 0))
+            return base[torch.randperm(len(base), generator=g, device=dev)]
+        if dev is not None:
+            base = base.cpu().numpy()
         rng = np.random.default_rng((s, epoch) if reshuffle else s)
         if buf >= len(base):
             return base[rng.permutation(len(base))]
@@ -95,7 +112,13 @@ class _ColPlan:
         return np.concatenate([chunks[i] for i in rng.permutation(len(chunks))]) if chunks else base
 
     def __iter__(self):
-        base = np.arange(self.n)
+        dev = self._device()
+        if dev is not None:
+            import torch
+
+            base = torch.arange(self.n, device=dev)
+        else:
+            base = np.arange(self.n)
         shuffle, batch, repeat, batch_before_repeat = None, None, None, True
         for op in self.ops:
             if op[0] == "shard":
@@ -129,13 +152,20 @@ class _ColPlan:
                         break
                     yield self._gather(sel)
             return
-        pending = np.zeros(0, dtype=np.int64)
+        pending = None
         for order in epoch_orders():
-            pending = np.concatenate([pending, order])
+            if pending is None:
+                pending = order
+            elif dev is not None:
+                import torch
+
+                pending = torch.cat([pending, order])
+            else:
+                pending = np.concatenate([pending, order])
             while len(pending) >= bs:
                 yield self._gather(pending[:bs])
                 pending = pending[bs:]
-        if len(pending) and not drop:
+        if pending is not None and len(pending) and not drop:
             yield self._gather(pending)
 
 

@@ -175,6 +175,41 @@ def _extract(gkeys, gtab, cap, nv):
     return ok, ot[0], outs
 
 
+RADIX_TILE = 2048  # rows per tile of radix_scatter_k (RT in df.hip)
+
+
+def _radix_level(keys, val, seg_start, seg_len, shift, buf, tag):
+    """One radix level over segments [seg_start, seg_start+seg_len): returns (okeys, ovals f64, offs)
+    where offs[(hb[s] + d*ntiles[s] + t)] is the output offset of tile t's digit-d run and
+    ``offs[-1] == n``, plus (hb, ntiles) per segment."""
+    dev = keys.device
+    n = keys.numel()
+    T = RADIX_TILE
+    nseg = seg_start.numel()
+    ntiles_s = (seg_len + T - 1) // T
+    first = torch.cumsum(ntiles_s, 0) - ntiles_s
+    total = int(ntiles_s.sum().item())
+    tile_seg = torch.repeat_interleave(torch.arange(nseg, device=dev), ntiles_s, output_size=total)
+    tl = torch.arange(total, device=dev) - first[tile_seg]
+    tstart = seg_start[tile_seg] + tl * T
+    seg_end = seg_start + seg_len
+    trows = torch.minimum(torch.full_like(tstart, T), seg_end[tile_seg] - tstart).to(torch.int32)
+    hb = 64 * first
+    thbase = hb[tile_seg] + tl
+    thstride = ntiles_s[tile_seg]
+    hist = buf(tag + "hist", (64 * total,), torch.int32)
+    hip("ptg_radix_count", ptr(keys), ptr(tstart), ptr(trows), ptr(thbase), ptr(thstride), total, shift, ptr(hist))
+    offs = buf(tag + "offs", (64 * total + 1,), torch.int64)
+    torch.cumsum(hist, 0, dtype=torch.int64, out=offs[1:])
+    offs[0] = 0
+    excl = offs[:-1]  # exclusive scan; offs[-1] = n is the sentinel for empty trailing segments
+    okeys = buf(tag + "okeys", (n,), torch.int64)
+    ovals = buf(tag + "ovals", (n,), torch.float64)
+    hip("ptg_radix_scatter", ptr(keys), ptr(val), TORCH_CT[val.dtype], ptr(tstart), ptr(trows), ptr(thbase),
+        ptr(thstride), total, shift, ptr(excl), ptr(okeys), ptr(ovals))
+    return okeys, ovals, offs, hb, ntiles_s
+
+
 def hash_agg_partitioned(keys: torch.Tensor, val: torch.Tensor, pbits: int = 9, ws: dict | None = None):
     """High-cardinality sum/count aggregation: radix-partition by key hash, then one LDS table per
     partition.  Returns (keys[m], sum[m], cnt[m]).  ``ws`` caches scratch buffers across calls."""
@@ -190,17 +225,34 @@ def hash_agg_partitioned(keys: torch.Tensor, val: torch.Tensor, pbits: int = 9, 
             ws[name] = t
         return t[: int(np.prod(shape))].view(shape)
 
-    counts = buf("counts", (P,), torch.int32)
-    counts.zero_()
-    hip("ptg_part_hist", ptr(keys), n, pbits, ptr(counts))
-    pstart = buf("pstart", (P + 1,), torch.int64)
-    pstart[0] = 0
-    torch.cumsum(counts.to(torch.int64), 0, out=pstart[1:])
-    cursor = buf("cursor", (P,), torch.int64)
-    cursor.copy_(pstart[:P])
-    okeys = buf("okeys", (n,), torch.int64)
-    ovals = buf("ovals", (n,), torch.float64)
-    hip("ptg_part_scatter", ptr(keys), ptr(val), TORCH_CT[val.dtype], n, pbits, ptr(cursor), ptr(okeys), ptr(ovals))
+    if pbits == 12 and n >= (1 << 22):
+        # two 6-bit radix levels with LDS-staged, run-coalesced scatters (tiles of 4096 rows)
+        z = torch.zeros(1, dtype=torch.int64, device=dev)
+        k1, v1, offs1, hb1, nt1 = _radix_level(keys, val, z, torch.full((1,), n, dtype=torch.int64, device=dev),
+                                                58, buf, "l1")
+        seg_start = offs1[(hb1.view(-1, 1) + torch.arange(64, device=dev).view(1, -1) * nt1.view(-1, 1)).view(-1)]
+        seg_end = torch.cat([seg_start[1:], torch.full((1,), n, dtype=torch.int64, device=dev)])
+        okeys, ovals, offs2, hb2, nt2 = _radix_level(k1, v1, seg_start, seg_end - seg_start, 52, buf, "l2")
+        idx = (hb2.view(-1, 1) + torch.arange(64, device=dev).view(1, -1) * nt2.view(-1, 1)).view(-1)
+        pstart = buf("pstart", (P + 1,), torch.int64)
+        pstart[:P].copy_(offs2[idx])
+        pstart[P] = n
+    else:
+        # block-private partition runs: per-block histograms -> exclusive scan -> run scatter
+        rpb = 1 << 17 if n >= (1 << 26) else 1 << 14
+        nb = max(1, -(-n // rpb))
+        hist = buf("hist", (P * nb,), torch.int32)
+        hip("ptg_part_count", ptr(keys), n, pbits, rpb, ptr(hist), nb)
+        offs = buf("offs", (P * nb,), torch.int64)
+        torch.cumsum(hist, 0, dtype=torch.int64, out=offs)
+        offs.sub_(hist)
+        pstart = buf("pstart", (P + 1,), torch.int64)
+        pstart[:P].copy_(offs.view(P, nb)[:, 0])
+        pstart[P] = n
+        okeys = buf("okeys", (n,), torch.int64)
+        ovals = buf("ovals", (n,), torch.float64)
+        hip("ptg_part_scatter_runs", ptr(keys), ptr(val), TORCH_CT[val.dtype], n, pbits, rpb, ptr(offs), nb,
+            ptr(okeys), ptr(ovals))
     cap_out = n if n < (1 << 26) else (1 << 26)
     out_keys = buf("out_keys", (cap_out,), torch.int64)
     out_sum = buf("out_sum", (cap_out,), torch.float64)

@@ -634,6 +634,8 @@ def _key_of(cv: ColumnVector) -> torch.Tensor:
         null = torch.zeros_like(k, dtype=torch.bool)
     else:
         k = d.long()
+        if cv.valid is None:
+            return k  # integral key without nulls: used as is (no copy of a 1B-row column)
         null = torch.zeros_like(k, dtype=torch.bool)
     if cv.valid is not None:
         null = null | ~cv.valid.bool()
@@ -953,8 +955,8 @@ def _hash_agg_all(key, vals, valids, want_minmax):
             and all(v is None for v in valids)):
         # large inputs: estimate the cardinality on a prefix; high-cardinality keys take the
         # radix-partitioned LDS aggregation (one LDS table per partition, no global atomics)
-        sk, _, _ = D.hash_agg(key[: 1 << 20], [], [], False)
-        if sk.numel() > (1 << 15):
+        sk, _, _ = D.hash_agg(key[: 1 << 16], [], [], False)
+        if sk.numel() > (1 << 12):
             return _partitioned_agg(key, vals[0] if vals else None)
     if len(vals) <= 4:
         return D.hash_agg(key, vals, valids, want_minmax)

@@ -63,10 +63,13 @@ def test_hash_agg_matches_host(hip_built, nkeys):
     assert torch.allclose(og[0][3].cpu()[order], oh[0][3])
 
 
-def test_partitioned_agg(hip_built):
-    n, nkeys = 4_000_000, 1_000_000
+@pytest.mark.parametrize("n,nkeys,pbits", [(4_000_000, 1_000_000, 9), (8_388_608, 1_000_000, 12),
+                                           (5_000_000, 3_000, 12)])
+def test_partitioned_agg(hip_built, n, nkeys, pbits):
+    """pbits=12 with n >= 2^22 takes the two-level LDS-staged radix partitioning; 3,000 keys leave
+    most of the 4,096 partitions (and some level-1 segments' tiles) empty."""
     k, v = D.fill_synthetic_kv(n, nkeys, "cuda")
-    ok, osum, ocnt, m, _, overflow = D.hash_agg_partitioned(k, v, pbits=9)
+    ok, osum, ocnt, m, _, overflow = D.hash_agg_partitioned(k, v, pbits=pbits)
     m = int(m.item())
     assert int(overflow.item()) == 0
     kh, rh, oh = D.hash_agg(k.cpu(), [v.cpu()], [None], False)
