@@ -99,6 +99,7 @@ def main(argv=None) -> int:
     if rank == 0:
         os.makedirs(args.output_dir, exist_ok=True)
         model.save(os.path.join(args.output_dir, "model.keras"))
+        model.export(os.path.join(args.output_dir, "saved_model"))
         with open(os.path.join(args.output_dir, "history.json"), "w") as fh:
             json.dump(hist.history, fh)
         with open(os.path.join(args.output_dir, "train_report.json"), "w") as fh:

@@ -449,6 +449,12 @@ class Sequential:
     def _save_class_name(self) -> str:
         return "Sequential"
 
+    def export(self, filepath: str, assets: dict | None = None) -> str:
+        """Keras-3 ``model.export``: write the SavedModel-layout directory (:mod:`.saved_model`)."""
+        from . import saved_model
+
+        return saved_model.save(self, filepath, assets=assets)
+
     def save(self, filepath: str) -> None:
         """Keras-v3-shaped zip: config.json + metadata.json + model.weights.safetensors (weights in Keras
         layouts, keyed ``layers/<name>/vars/<i>``; safetensors instead of HDF5 because h5py is absent)."""

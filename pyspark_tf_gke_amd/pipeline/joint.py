@@ -19,7 +19,7 @@ GPU:
    train_tf_ps.py:328-343) with MultiWorkerMirroredStrategy (RCCL all-reduce) through the
    columnar ``Dataset`` fast path (shuffle/batch gathered on the device).  ``handoff="device"``
    additionally skips the Parquet read-back and trains straight from the ETL's device columns.
-Artifacts: ``<out>/etl.parquet/``, ``<out>/model.keras``, ``<out>/history.json``,
+Artifacts: ``<out>/etl.parquet/``, ``<out>/model.keras``, ``<out>/saved_model/``, ``<out>/history.json``,
 ``<out>/label_map.json``, ``<out>/joint_report.json``.
 """
 from __future__ import annotations
@@ -139,6 +139,8 @@ def run_joint(rows_per_executor: int = 1_000_000, out_dir: str = "./joint-out", 
               "wall_seconds": round(time.perf_counter() - t_all, 3)}
     if rank == 0:
         model.save(os.path.join(out_dir, "model.keras"))
+        model.export(os.path.join(out_dir, "saved_model"),
+                     assets={"label_map.json": {f"class_{i}": i for i in range(NUM_CLASSES)}})
         with open(os.path.join(out_dir, "history.json"), "w") as fh:
             json.dump({k: [float(v) for v in vs] for k, vs in hist.history.items()}, fh)
         with open(os.path.join(out_dir, "label_map.json"), "w") as fh:

@@ -1,4 +1,6 @@
 """Functional-graph engine (ResNet family) on the CPU host path vs an fp32 torch-autograd oracle."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -117,3 +119,21 @@ def test_functional_mlp_and_sgd():
     h0 = m.fit(x, y, batch_size=16, epochs=1, verbose=0).history["loss"][0]
     h1 = m.fit(x, y, batch_size=16, epochs=10, verbose=0).history["loss"][-1]
     assert h1 < h0
+
+
+def test_saved_model_export_load(tmp_path):
+    from pyspark_tf_gke_amd.models import build_cnn_model
+
+    torch.manual_seed(0)
+    for m, x in ((ResNet((1, 1), input_shape=(32, 32, 3), classes=4, width=8, device="cpu"),
+                  np.random.rand(3, 32, 32, 3).astype(np.float32)),
+                 (build_cnn_model((32, 40, 3), flat=True, summary=False, device="cpu"),
+                  np.random.rand(3, 32, 40, 3).astype(np.float32))):
+        d = str(tmp_path / m.name)
+        m.export(d, assets={"label_map.json": {"0": "a"}})
+        for f in ("saved_model.json", "fingerprint.json", "variables/variables.safetensors",
+                  "variables/variables.index.json", "assets/label_map.json"):
+            assert os.path.exists(os.path.join(d, f)), f
+        loaded = nn.saved_model.load(d, device="cpu")
+        out = loaded.signatures["serving_default"](input_layer=x)["output_0"]
+        np.testing.assert_allclose(out, m.predict(x), atol=1e-2)

@@ -27,6 +27,7 @@ def test_joint_single_rank(tmp_path, handoff):
     hist = json.load(open(os.path.join(out, "history.json")))
     assert hist["loss"][-1] < hist["loss"][0]
     assert os.path.exists(os.path.join(out, "model.keras"))
+    assert os.path.exists(os.path.join(out, "saved_model", "saved_model.json"))
 
 
 def test_joint_two_ranks(tmp_path):

@@ -224,7 +224,8 @@ def test_prelu_fwd_bwd(N, H, W, C, nper):
     _close(db, dbr, 1e-2, 1e-2, "dbias")
 
 
-@pytest.mark.parametrize("M,Kd,N,act", [(32, 3, 16, "relu"), (64, 64, 15, "softmax"), (128, 2048, 2, None)])
+@pytest.mark.parametrize("M,Kd,N,act", [(32, 3, 16, "relu"), (64, 64, 15, "softmax"), (128, 2048, 2, None),
+                                        (8192, 3, 16, "relu"), (8192, 32, 64, "relu"), (20000, 64, 15, None)])
 def test_dense_small(M, Kd, N, act):
     x, w, b = torch.randn(M, Kd), torch.randn(N, Kd) * 0.1, torch.randn(N)
     y = torch.empty(M, N, device=DEV)
@@ -243,8 +244,9 @@ def test_dense_small(M, Kd, N, act):
     K.dense_small_dw(dy.to(DEV), x.to(DEV), dw, db)
     dwr, dbr = torch.zeros(N, Kd), torch.zeros(N)
     R.dense_small_dw(dy, x, dwr, dbr)
-    _close(dw, dwr, 1e-4, 1e-4, "small_dw")
-    _close(db, dbr, 1e-4, 1e-4, "small_db")
+    tol = 1e-4 if M <= 1024 else 2e-3  # split-M atomics: different summation order over 8k+ rows
+    _close(dw, dwr, tol, tol, "small_dw")
+    _close(db, dbr, tol, tol, "small_db")
 
 
 def test_losses_and_adam():
