@@ -455,6 +455,10 @@ static int dispatch_gemm(const LA& la, const LB& lb, const EPI& epi, int M, int 
   if (N <= 32) return launch_gemm<256, 32, 4, 1>(la, lb, epi, M, N, K, splits, s);
   if (N <= 64) return launch_gemm<128, 64, 2, 2>(la, lb, epi, M, N, K, splits, s);
   if (M <= 64) return launch_gemm<64, 128, 1, 4>(la, lb, epi, M, N, K, splits, s);
+  // fewer 128x128 tiles than CUs (late ResNet stages: M = batch*7*7): halve the M tile so the grid
+  // covers the 256 CUs (measured: helps below one tile per CU, hurts at 1.5 per CU)
+  if ((long)ptg_ceil_div(M, 128) * ptg_ceil_div(N, 128) * splits < 256)
+    return launch_gemm<64, 128, 1, 4>(la, lb, epi, M, N, K, splits, s);
   return launch_gemm<128, 128, 2, 2>(la, lb, epi, M, N, K, splits, s);
 }
 
@@ -577,7 +581,9 @@ int ptg_conv2d_wgrad(const void* x, const void* dz, float* dw, int N, int H, int
   EpiAtomic epi{dw, Kc};
   if (splits <= 0) {
     const int tiles = ptg_ceil_div(Cout, Cout <= 16 ? 16 : (Cout <= 32 ? 32 : 64)) * ptg_ceil_div(Kc, 128);
-    splits = ptg_ceil_div(1024, tiles);
+    // ~2 blocks per CU: more K slices only add fp32 atomic traffic (which runs at ~1.3 TB/s of
+    // added bytes, MI355X_MICROARCH.md "Global float atomics") without adding useful overlap
+    splits = ptg_ceil_div(512, tiles);
     const int max_splits = ptg_ceil_div(P, 4 * BK);
     if (splits > max_splits) splits = max_splits;
   }

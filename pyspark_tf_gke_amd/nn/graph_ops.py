@@ -92,6 +92,10 @@ class GraphOp:
 # ------------------------------------------------------------------------------------------------
 # convolution dispatch (shared by ConvBNOp)
 # ------------------------------------------------------------------------------------------------
+# The halo-tiled direct conv (csrc/kernels/conv.hip) is tuned for the reference CNN's 5x5 layers
+# with 4-64 channels; measured on ResNet-50's 3x3/64-channel layers (56x56, batch 128) the
+# implicit-GEMM path is faster, so graph ops use the halo kernels for 5x5 only.
+HALO_KS = (5,)
 def conv_forward(x, w, bias, stride, pad, z):
     N, H, W, C = x.shape
     Co, KH, KW, _ = w.shape
@@ -102,7 +106,7 @@ def conv_forward(x, w, bias, stride, pad, z):
         K.gemm(M, Co, C, x, C, 1, w, C, 1, 0, z, Co, bias, 0, 1)
         return z
     same = pad == KH // 2 and KH == KW and stride == 1
-    if K.halo_eligible(C, Co, KH, stride, same):
+    if KH in HALO_KS and K.halo_eligible(C, Co, KH, stride, same):
         return K.conv2d_fwd_fused(x, w, bias, pad, z)
     return K.conv2d_fwd(x, w, bias, stride, pad, z, None)
 
@@ -117,11 +121,11 @@ def conv_wgrad(x, dz, stride, pad, dw):
     if KH == KW == 1 and stride == 1 and pad == 0:
         M = N * H * W
         tiles = math.ceil(Co / 128) * math.ceil(C / 128)
-        splits = max(1, min(math.ceil(2048 / tiles), M // 256))
+        splits = max(1, min(math.ceil(512 / tiles), M // 512))  # ~2 blocks/CU; atomics cost bytes
         K.gemm(Co, C, M, dz, Co, 0, x, C, 0, 3, dw, C, None, 0, splits)
         return dw
     same = pad == KH // 2 and KH == KW and stride == 1
-    if K.halo_eligible(C, Co, KH, stride, same):
+    if KH in HALO_KS and K.halo_eligible(C, Co, KH, stride, same):
         tmp = dw  # halo wgrad overwrites; dw was zeroed by the store for this step
         return K.conv2d_wgrad_halo(x, dz, pad, tmp)
     return K.conv2d_wgrad(x, dz, stride, pad, dw, accumulate=True)
@@ -136,7 +140,7 @@ def conv_dgrad(dz, w, stride, pad, dx, accumulate, ws, key):
     if stride != 1:
         raise NotImplementedError("dgrad of a strided KxK (K > 1) convolution that is not the first layer")
     same = pad == KH // 2 and KH == KW
-    if K.on_device(dz) and K.halo_eligible(Co, Cin, KH, 1, same) and not accumulate:
+    if K.on_device(dz) and KH in HALO_KS and K.halo_eligible(Co, Cin, KH, 1, same) and not accumulate:
         wf = ws.get(key + "/wflip", (Cin, KH, KW, Co), torch.bfloat16, dz.device)
         K.conv2d_dgrad_halo(dz, w, pad, dx, wf)
         return True
