@@ -28,7 +28,12 @@ typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
 
 namespace ptgc {
 
-enum { EPI_Z = 0, EPI_POOL = 1, EPI_PRELU = 2 };
+// EPI_POOLS ("sparse pool"): like EPI_POOL but instead of the full-resolution z it stores, per
+// pooled output and channel, only what the backward needs: the z of the window's argmax (bf16, into
+// `z`, shaped like the pooled output) and the argmax position q = 2*dh + dw (uint8, `argout`) -
+// 2.5 bytes per pooled element instead of 8 bytes of z (the first conv layer writes 335 MB less per
+// step at batch 256 and its backward reads 335 MB less).
+enum { EPI_Z = 0, EPI_POOL = 1, EPI_PRELU = 2, EPI_POOLS = 3 };
 
 template <int C> struct PixPitch { static constexpr int v = C >= 16 ? C + 8 : C; };  // bank-conflict pad
 template <int C, int KS> struct Kwp { static constexpr int v = (KS * C) % 8 == 0 ? KS : ((KS + 1) * C) % 8 == 0 ? KS + 1 : KS + 3; };
@@ -93,7 +98,8 @@ PTG_DEV float row_shl(float v) {
 template <int C, int KS, int NF, int TW, int TH, int EPI, bool RING, bool KSPLIT>
 __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
                                                         const float* __restrict__ bias, const float* __restrict__ alpha,
-                                                        bf16_t* __restrict__ z, bf16_t* __restrict__ aux, int N, int H,
+                                                        bf16_t* __restrict__ z, bf16_t* __restrict__ aux,
+                                                        uint8_t* __restrict__ argout, int N, int H,
                                                         int W, int Cout, int pad, int tiles_h, int tiles_w) {
   using VT = typename HVec<C>::T;
   constexpr int VPP = HVec<C>::per_pix;      // vectors per pixel
@@ -111,7 +117,8 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
   constexpr int FM = MFR / 4;
   constexpr bool WIDE = TW >= 16;             // fragment = 16 pixels of one row
   static_assert(MFR % 4 == 0 && TH % 2 == 0, "tile shape");
-  static_assert(WIDE ? (TW % 16 == 0 && (FM % 2 == 0 || EPI != EPI_POOL)) : (TW == 4 || TW == 8), "pool pairing");
+  static_assert(WIDE ? (TW % 16 == 0 && (FM % 2 == 0 || (EPI != EPI_POOL && EPI != EPI_POOLS))) : (TW == 4 || TW == 8),
+                "pool pairing");
   constexpr int SEG = WIDE ? TW / 16 : 1;
   constexpr int HALO_ELEMS = NROWS * ROWE;
   constexpr int PFN = (HR * HC * VPP + 255) / 256;   // prefetch vectors per thread (worst case: HR rows)
@@ -363,6 +370,60 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
     if (has_next) store_rows(nrows2, slot2);
 
     // ---- epilogue from registers ----
+    if constexpr (EPI == EPI_POOLS) {
+      // sparse pool record, one vertical fragment pair (WIDE) / one fragment at a time to keep the
+      // live register set small; the first maximum in q order (0,1,2,3) wins, as in the dense
+      // backward
+      constexpr int STEP = WIDE ? 2 : 1;
+#pragma unroll
+      for (int j = 0; j < NF; ++j) {
+        const int co0 = j * 16 + g * 4;
+        const bool cval = co0 < Cout;
+#pragma unroll
+        for (int i = 0; i < FM; i += STEP) {
+          float yy[STEP][4], zz[STEP][4], qq[STEP][4];
+#pragma unroll
+          for (int u = 0; u < STEP; ++u) {
+            const float a4[4] = {al[i + u][j].x, al[i + u][j].y, al[i + u][j].z, al[i + u][j].w};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float zr = bf2f(f2bf(res[i + u][j][r] + bv[j][r]));
+              const float yv = zr > 0.f ? zr : a4[r] * zr;
+              const float yn = row_shl<1>(yv), zn = row_shl<1>(zr);
+              const bool right = yn > yv;
+              yy[u][r] = right ? yn : yv;
+              zz[u][r] = right ? zn : zr;
+              qq[u][r] = right ? 1.f : 0.f;
+            }
+          }
+          float pm[4], pz[4], pq[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float yb, zb, qb;
+            if constexpr (WIDE) { yb = yy[STEP - 1][r]; zb = zz[STEP - 1][r]; qb = qq[STEP - 1][r]; }
+            else {
+              yb = row_shl<(WIDE ? 1 : TW)>(yy[0][r]);
+              zb = row_shl<(WIDE ? 1 : TW)>(zz[0][r]);
+              qb = row_shl<(WIDE ? 1 : TW)>(qq[0][r]);
+            }
+            const bool down = yb > yy[0][r];
+            pm[r] = down ? yb : yy[0][r];
+            pz[r] = down ? zb : zz[0][r];
+            pq[r] = down ? qb + 2.f : qq[0][r];
+          }
+          const int rr = f_r[i], cc = f_c[i];
+          const bool lead = ((cc & 1) == 0) && ((rr & 1) == 0);
+          const int ph = (oh0 + rr) >> 1, pw = (ow0 + cc) >> 1;
+          if (cval && lead && ph < PH && pw < PW) {
+            const long po = (((long)n * PH + ph) * PW + pw) * Cout + co0;
+            *(U2*)(aux + po) = U2{pack_bf(pm[0], pm[1]), pack_bf(pm[2], pm[3])};
+            *(U2*)(z + po) = U2{pack_bf(pz[0], pz[1]), pack_bf(pz[2], pz[3])};
+            *(uint32_t*)(argout + po) = (uint32_t)pq[0] | ((uint32_t)pq[1] << 8) | ((uint32_t)pq[2] << 16) |
+                                        ((uint32_t)pq[3] << 24);
+          }
+        }
+      }
+    } else
 #pragma unroll
     for (int j = 0; j < NF; ++j) {
       const int co0 = j * 16 + g * 4;
@@ -630,7 +691,7 @@ static int resident_blocks(const void* kernel) {
 }
 
 template <int C, int KS, int NF, int TW, int TH, int E>
-static int launch_fwd_e(const void* x, const void* w, const float* bias, const float* alpha, void* z, void* aux, int N,
+static int launch_fwd_e(const void* x, const void* w, const float* bias, const float* alpha, void* z, void* aux, void* arg, int N,
                         int H, int W, int Cout, int pad, hipStream_t s) {
   constexpr bool RING = TH < 2 * (KS - 1);
   constexpr int KTOT = KS * Kwp<C, KS>::v * C, KSTEPS = (KTOT + 31) / 32, MFR = TH * TW / 16;
@@ -643,47 +704,48 @@ static int launch_fwd_e(const void* x, const void* w, const float* bias, const f
   // persistent: one wave of resident workgroups, each walking a contiguous range of tiles
   const int grid = (int)std::min<long>(tiles, resident);
   hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, (const bf16_t*)x, (const bf16_t*)w, bias, alpha, (bf16_t*)z,
-                     (bf16_t*)aux, N, H, W, Cout, pad, th, tw);
+                     (bf16_t*)aux, (uint8_t*)arg, N, H, W, Cout, pad, th, tw);
   PTG_RETURN_LAUNCH();
 }
 
 template <int C, int KS, int NF, int TW, int TH>
-static int launch_fwd(const void* x, const void* w, const float* bias, const float* alpha, void* z, void* aux, int N,
+static int launch_fwd(const void* x, const void* w, const float* bias, const float* alpha, void* z, void* aux, void* arg, int N,
                       int H, int W, int Cout, int pad, int epi, hipStream_t s) {
-  if (epi == EPI_POOL) return launch_fwd_e<C, KS, NF, TW, TH, EPI_POOL>(x, w, bias, alpha, z, aux, N, H, W, Cout, pad, s);
-  if (epi == EPI_PRELU) return launch_fwd_e<C, KS, NF, TW, TH, EPI_PRELU>(x, w, bias, alpha, z, aux, N, H, W, Cout, pad, s);
-  return launch_fwd_e<C, KS, NF, TW, TH, EPI_Z>(x, w, bias, alpha, z, aux, N, H, W, Cout, pad, s);
+  if (epi == EPI_POOL) return launch_fwd_e<C, KS, NF, TW, TH, EPI_POOL>(x, w, bias, alpha, z, aux, arg, N, H, W, Cout, pad, s);
+  if (epi == EPI_POOLS) return launch_fwd_e<C, KS, NF, TW, TH, EPI_POOLS>(x, w, bias, alpha, z, aux, arg, N, H, W, Cout, pad, s);
+  if (epi == EPI_PRELU) return launch_fwd_e<C, KS, NF, TW, TH, EPI_PRELU>(x, w, bias, alpha, z, aux, arg, N, H, W, Cout, pad, s);
+  return launch_fwd_e<C, KS, NF, TW, TH, EPI_Z>(x, w, bias, alpha, z, aux, arg, N, H, W, Cout, pad, s);
 }
 
 template <int C, int KS, int NF>
-static int fwd_by_c(const void* x, const void* w, const float* bias, const float* alpha, void* z, void* aux, int N,
+static int fwd_by_c(const void* x, const void* w, const float* bias, const float* alpha, void* z, void* aux, void* arg, int N,
                     int H, int W, int Cout, int pad, int epi, hipStream_t s) {
   // tile shapes: TH x TW pixels, halo fits LDS, 4 waves with equal fragment counts
-  if constexpr (C == 4) return launch_fwd<C, KS, NF, 64, 4>(x, w, bias, alpha, z, aux, N, H, W, Cout, pad, epi, s);
-  else if constexpr (C == 8) return launch_fwd<C, KS, NF, 32, 8>(x, w, bias, alpha, z, aux, N, H, W, Cout, pad, epi, s);
-  else if constexpr (C == 16) return launch_fwd<C, KS, NF, 16, 8>(x, w, bias, alpha, z, aux, N, H, W, Cout, pad, epi, s);
-  else if constexpr (C == 32) return launch_fwd<C, KS, NF, 8, 16>(x, w, bias, alpha, z, aux, N, H, W, Cout, pad, epi, s);
-  else return launch_fwd<C, KS, NF, 4, 16>(x, w, bias, alpha, z, aux, N, H, W, Cout, pad, epi, s);
+  if constexpr (C == 4) return launch_fwd<C, KS, NF, 64, 4>(x, w, bias, alpha, z, aux, arg, N, H, W, Cout, pad, epi, s);
+  else if constexpr (C == 8) return launch_fwd<C, KS, NF, 32, 8>(x, w, bias, alpha, z, aux, arg, N, H, W, Cout, pad, epi, s);
+  else if constexpr (C == 16) return launch_fwd<C, KS, NF, 16, 8>(x, w, bias, alpha, z, aux, arg, N, H, W, Cout, pad, epi, s);
+  else if constexpr (C == 32) return launch_fwd<C, KS, NF, 8, 16>(x, w, bias, alpha, z, aux, arg, N, H, W, Cout, pad, epi, s);
+  else return launch_fwd<C, KS, NF, 4, 16>(x, w, bias, alpha, z, aux, arg, N, H, W, Cout, pad, epi, s);
 }
 
 template <int C, int KS>
-static int fwd_by_nf(const void* x, const void* w, const float* bias, const float* alpha, void* z, void* aux, int N,
+static int fwd_by_nf(const void* x, const void* w, const float* bias, const float* alpha, void* z, void* aux, void* arg, int N,
                      int H, int W, int Cout, int pad, int epi, hipStream_t s) {
-  if (Cout <= 16) return fwd_by_c<C, KS, 1>(x, w, bias, alpha, z, aux, N, H, W, Cout, pad, epi, s);
-  if (Cout <= 32) return fwd_by_c<C, KS, 2>(x, w, bias, alpha, z, aux, N, H, W, Cout, pad, epi, s);
-  if (Cout <= 64) return fwd_by_c<C, KS, 4>(x, w, bias, alpha, z, aux, N, H, W, Cout, pad, epi, s);
+  if (Cout <= 16) return fwd_by_c<C, KS, 1>(x, w, bias, alpha, z, aux, arg, N, H, W, Cout, pad, epi, s);
+  if (Cout <= 32) return fwd_by_c<C, KS, 2>(x, w, bias, alpha, z, aux, arg, N, H, W, Cout, pad, epi, s);
+  if (Cout <= 64) return fwd_by_c<C, KS, 4>(x, w, bias, alpha, z, aux, arg, N, H, W, Cout, pad, epi, s);
   return (int)hipErrorInvalidValue;
 }
 
 template <int KS>
-static int fwd_by_cin(const void* x, const void* w, const float* bias, const float* alpha, void* z, void* aux, int N,
+static int fwd_by_cin(const void* x, const void* w, const float* bias, const float* alpha, void* z, void* aux, void* arg, int N,
                       int H, int W, int C, int Cout, int pad, int epi, hipStream_t s) {
   switch (C) {
-    case 4: return fwd_by_nf<4, KS>(x, w, bias, alpha, z, aux, N, H, W, Cout, pad, epi, s);
-    case 8: return fwd_by_nf<8, KS>(x, w, bias, alpha, z, aux, N, H, W, Cout, pad, epi, s);
-    case 16: return fwd_by_nf<16, KS>(x, w, bias, alpha, z, aux, N, H, W, Cout, pad, epi, s);
-    case 32: return fwd_by_nf<32, KS>(x, w, bias, alpha, z, aux, N, H, W, Cout, pad, epi, s);
-    case 64: return fwd_by_nf<64, KS>(x, w, bias, alpha, z, aux, N, H, W, Cout, pad, epi, s);
+    case 4: return fwd_by_nf<4, KS>(x, w, bias, alpha, z, aux, arg, N, H, W, Cout, pad, epi, s);
+    case 8: return fwd_by_nf<8, KS>(x, w, bias, alpha, z, aux, arg, N, H, W, Cout, pad, epi, s);
+    case 16: return fwd_by_nf<16, KS>(x, w, bias, alpha, z, aux, arg, N, H, W, Cout, pad, epi, s);
+    case 32: return fwd_by_nf<32, KS>(x, w, bias, alpha, z, aux, arg, N, H, W, Cout, pad, epi, s);
+    case 64: return fwd_by_nf<64, KS>(x, w, bias, alpha, z, aux, arg, N, H, W, Cout, pad, epi, s);
     default: return (int)hipErrorInvalidValue;
   }
 }
@@ -734,13 +796,14 @@ using namespace ptgc;
 extern "C" {
 
 // stride-1 'same'-style conv with halo tiling. C in {4,8,16,32,64}, Cout % 8 == 0 and <= 64, KS in {3,5}.
-// epi: 0 = z only, 1 = z + maxpool2x2(prelu(z)) into aux (H, W even), 2 = z + prelu(z) into aux.
-int ptg_conv2d_fwd_halo(const void* x, const void* w, const float* bias, const float* alpha, void* z, void* aux, int N,
+// epi: 0 = z only, 1 = z + maxpool2x2(prelu(z)) into aux (H, W even), 2 = z + prelu(z) into aux,
+// 3 = maxpool2x2(prelu(z)) into aux + argmax z into z ([N][H/2][W/2][Cout]) + argmax q into arg.
+int ptg_conv2d_fwd_halo(const void* x, const void* w, const float* bias, const float* alpha, void* z, void* aux, void* arg, int N,
                         int H, int W, int C, int Cout, int KS, int pad, int epi, hipStream_t s) {
   if (Cout % 8 || Cout > 64) return (int)hipErrorInvalidValue;
-  if (epi == EPI_POOL && ((H & 1) || (W & 1))) return (int)hipErrorInvalidValue;
-  if (KS == 5) return fwd_by_cin<5>(x, w, bias, alpha, z, aux, N, H, W, C, Cout, pad, epi, s);
-  if (KS == 3) return fwd_by_cin<3>(x, w, bias, alpha, z, aux, N, H, W, C, Cout, pad, epi, s);
+  if ((epi == EPI_POOL || epi == EPI_POOLS) && ((H & 1) || (W & 1))) return (int)hipErrorInvalidValue;
+  if (KS == 5) return fwd_by_cin<5>(x, w, bias, alpha, z, aux, arg, N, H, W, C, Cout, pad, epi, s);
+  if (KS == 3) return fwd_by_cin<3>(x, w, bias, alpha, z, aux, arg, N, H, W, C, Cout, pad, epi, s);
   return (int)hipErrorInvalidValue;
 }
 

@@ -191,6 +191,93 @@ __global__ __launch_bounds__(256) void prelu_pool_bwd_k(const bf16_t* __restrict
   bias_reduce_atomic(db, c8, C8, sred, dbias);
 }
 
+// Backward of prelu+pool from the sparse forward record (conv.hip EPI_POOLS): per pooled element the
+// argmax position q (uint8) and the z there (bf16).  dz is dense (zero off the argmax), dalpha and
+// dbias as in prelu_pool_bwd_k.  Reads dp + zsel + arg (2.5 B per pooled element) instead of the
+// four z values of each window (8 B).
+__global__ __launch_bounds__(256) void prelu_pool_bwd_sparse_k(const bf16_t* __restrict__ dp,
+                                                               const bf16_t* __restrict__ zs,
+                                                               const uint8_t* __restrict__ arg,
+                                                               const float* __restrict__ alpha,
+                                                               bf16_t* __restrict__ dz, float* __restrict__ dalpha,
+                                                               float* __restrict__ dbias, int N, int H, int W, int C,
+                                                               int nper) {
+  __shared__ float sred[4 * 256];
+  __shared__ float sda[256 * 32];
+  const int PH = H >> 1, PW = W >> 1, C8 = C >> 3;
+  const int npos = PH * PW * C8;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int n0 = blockIdx.y * nper, n1 = min(N, n0 + nper);
+  float db[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const bool active = i < npos;
+  const int c8 = active ? i % C8 : 0;
+  const int t = active ? i / C8 : 0;
+  const int pw = t % PW, ph = t / PW;
+  long zoff[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) zoff[q] = ((long)(2 * ph + (q >> 1)) * W + 2 * pw + (q & 1)) * C + c8 * 8;
+  const long HWC = (long)H * W * C, PHWC = (long)PH * PW * C;
+  const long poff = ((long)ph * PW + pw) * C + c8 * 8;
+  if (active) {
+    float da[4][8], av[4][8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 a0 = *(const float4*)(alpha + zoff[q]), a1 = *(const float4*)(alpha + zoff[q] + 4);
+      av[q][0] = a0.x; av[q][1] = a0.y; av[q][2] = a0.z; av[q][3] = a0.w;
+      av[q][4] = a1.x; av[q][5] = a1.y; av[q][6] = a1.z; av[q][7] = a1.w;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) da[q][j] = 0.f;
+    }
+    for (int n = n0; n < n1; n += 4) {  // 4 samples in flight: 12 independent loads per lane
+      U4 graw[4], zraw[4];
+      U2 araw[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int nn = min(n + u, n1 - 1);
+        graw[u] = *(const U4*)(dp + nn * PHWC + poff);
+        zraw[u] = *(const U4*)(zs + nn * PHWC + poff);
+        araw[u] = *(const U2*)(arg + nn * PHWC + poff);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (n + u >= n1) break;
+        const long nb = (long)(n + u) * HWC;
+        float g[8], zv[8];
+        unpack8(graw[u], g);
+        unpack8(zraw[u], zv);
+        const uint8_t* ab = (const uint8_t*)&araw[u];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float o[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const bool hit = ab[j] == q;
+            const float gq = hit ? g[j] : 0.f;
+            o[j] = zv[j] > 0.f ? gq : gq * av[q][j];
+            da[q][j] += (hit && !(zv[j] > 0.f)) ? gq * zv[j] : 0.f;
+            db[j] += o[j];
+          }
+          *(U4*)(dz + nb + zoff[q]) = pack8(o);
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sda[(((q >> 1) * 256 + threadIdx.x) * 2 + (q & 1)) * 8 + j] = da[q][j];
+  }
+  __syncthreads();
+  for (int k = 0; k < 32; ++k) {
+    const int L = k * 256 + threadIdx.x;
+    const int j = L & 7, qw = (L >> 3) & 1, tt = (L >> 4) & 255, qh = L >> 12;
+    const int ii = blockIdx.x * 256 + tt;
+    if (ii >= npos) continue;
+    const int cc = ii % C8, tq = ii / C8, pww = tq % PW, phh = tq / PW;
+    atomicAdd(dalpha + ((long)(2 * phh + qh) * W + 2 * pww + qw) * C + cc * 8 + j, sda[L]);
+  }
+  bias_reduce_atomic(db, c8, C8, sred, dbias);
+}
+
 // Plain PReLU forward (no pool): a = z>0 ? z : alpha[hwc]*z ; HWC = per-sample element count.
 __global__ __launch_bounds__(256) void prelu_fwd_k(const bf16_t* __restrict__ z,
                                                    const float* __restrict__ alpha,
@@ -608,6 +695,22 @@ int ptg_prelu_pool_bwd(const void* dp, const void* z, const float* alpha, void* 
   dim3 grid((npos + 255) / 256, (N + nper - 1) / nper);
   hipLaunchKernelGGL(prelu_pool_bwd_k, grid, dim3(256), 0, s, (const bf16_t*)dp, (const bf16_t*)z, alpha,
                      (bf16_t*)dz, dalpha, dbias, N, H, W, C, nper);
+  PTG_RETURN_LAUNCH();
+}
+
+int ptg_prelu_pool_bwd_sparse(const void* dp, const void* zs, const void* arg, const float* alpha, void* dz,
+                              float* dalpha, float* dbias, int N, int H, int W, int C, int nper, hipStream_t s) {
+  if (C % 8 || C > 256 || (H & 1) || (W & 1) || H < 2 || W < 2) return (int)hipErrorInvalidValue;
+  const int npos = (H / 2) * (W / 2) * (C / 8);
+  if (nper <= 0) {
+    const int bx = (npos + 255) / 256;
+    int chunks = (2048 + bx - 1) / bx;
+    if (chunks > N) chunks = N;
+    nper = (N + chunks - 1) / chunks;
+  }
+  dim3 grid((npos + 255) / 256, (N + nper - 1) / nper);
+  hipLaunchKernelGGL(prelu_pool_bwd_sparse_k, grid, dim3(256), 0, s, (const bf16_t*)dp, (const bf16_t*)zs,
+                     (const uint8_t*)arg, alpha, (bf16_t*)dz, dalpha, dbias, N, H, W, C, nper);
   PTG_RETURN_LAUNCH();
 }
 

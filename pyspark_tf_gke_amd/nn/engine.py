@@ -29,6 +29,12 @@ from . import layers as L
 # an fp32 autograd oracle exactly (the GPU path is always bf16).
 _HOST_FP32 = [os.environ.get("PTG_HOST_FP32") == "1"]
 
+# Sparse PReLU+pool record (conv.hip EPI_POOLS: z at the argmax + argmax index instead of the full
+# z).  Opt-in: on CNN-B1 (batch 256, MI355X) it moves 0.8 GB less per step but its longer epilogue
+# makes the latency-bound layer-1/2 forward kernels slower than the backward saves (98.1k vs 99.2k
+# samples/s measured), so the dense record stays the default.
+SPARSE_POOL = os.environ.get("PTG_SPARSE_POOL", "0") == "1"
+
 
 def host_fp32(enabled: bool | None = None) -> bool:
     if enabled is not None:
@@ -128,10 +134,16 @@ class ConvOp(Op):
         B = x.shape[0]
         OH, OW, Co = self.conv.out_shape
         dev = x.device
-        z = ws.get(self.name + "/z", (B, OH, OW, Co), torch.bfloat16, dev)
         b = self.conv.bias.data if self.conv.bias is not None else None
+        self._sparse = False
+        halo_ok = self._halo()[0] and not (self.pool is not None and (OH % 2 or OW % 2))
+        if halo_ok and self.pool is not None and x.is_cuda and SPARSE_POOL:
+            # sparse pool record: pooled output + z at the argmax + argmax position (no full z)
+            self._x, self._sparse = x, True
+            return self._forward_pool_sparse(x, b, ws, B, OH, OW, Co, dev)
+        z = ws.get(self.name + "/z", (B, OH, OW, Co), torch.bfloat16, dev)
         self._x, self._z = x, z
-        if self._halo()[0] and not (self.pool is not None and (OH % 2 or OW % 2)):
+        if halo_ok:
             return self._forward_halo(x, z, b, ws, B, OH, OW, Co, dev)
         act = "relu" if self.conv.activation == "relu" else None
         K.conv2d_fwd(x, self.conv.kernel.bf16, b, self.stride, self.pad, z, act)
@@ -147,6 +159,22 @@ class ConvOp(Op):
             p = ws.get(self.name + "/p", (B, OH // 2, OW // 2, Co), torch.bfloat16, dev)
             return K.prelu_pool_fwd(z, ones, p)
         return z
+
+    def _pool_alpha(self, ws, dev):
+        if self.prelu is not None:
+            return self.prelu.alpha.data
+        if self.conv.activation == "relu":
+            return self._alpha_const(ws, 0.0, dev)  # ReLU == PReLU with alpha 0
+        return self._alpha_const(ws, 1.0, dev)  # identity
+
+    def _forward_pool_sparse(self, x, b, ws, B, OH, OW, Co, dev):
+        shp = (B, OH // 2, OW // 2, Co)
+        p = ws.get(self.name + "/p", shp, torch.bfloat16, dev)
+        zs = ws.get(self.name + "/zsel", shp, torch.bfloat16, dev)
+        arg = ws.get(self.name + "/arg", shp, torch.uint8, dev)
+        K.conv2d_fwd_fused(x, self.conv.kernel.bf16, b, self.pad, zs, self._pool_alpha(ws, dev), p, "pools", arg)
+        self._zs, self._arg, self._zshape = zs, arg, (B, OH, OW, Co)
+        return p
 
     def _forward_halo(self, x, z, b, ws, B, OH, OW, Co, dev):
         """One kernel: conv + bias, and the PReLU/ReLU (+ 2x2 max-pool) epilogue fused in."""
@@ -168,13 +196,21 @@ class ConvOp(Op):
         return a
 
     def backward(self, dy, ws):
-        z, x = self._z, self._x
-        dev = z.device
+        x = self._x
+        dev = x.device
         dy = _bf16(dy, ws, self.name + "/dy16")
-        dz = ws.get(self.name + "/dz", z.shape, torch.bfloat16, dev)
+        zshape = self._zshape if self._sparse else self._z.shape
+        dz = ws.get(self.name + "/dz", zshape, torch.bfloat16, dev)
         bias_g = self.conv.bias.grad if self.conv.bias is not None else \
-            ws.get(self.name + "/nobias", (z.shape[-1],), torch.float32, dev)
-        if self.prelu is not None and self.pool is not None:
+            ws.get(self.name + "/nobias", (zshape[-1],), torch.float32, dev)
+        z = self._z if not self._sparse else None
+        if self._sparse:
+            if self.prelu is not None:
+                dalpha = self.prelu.alpha.grad
+            else:
+                dalpha = ws.get(self.name + "/dalpha_dummy", zshape[1:], torch.float32, dev)
+            K.prelu_pool_bwd_sparse(dy, self._zs, self._arg, self._pool_alpha(ws, dev), dz, dalpha, bias_g)
+        elif self.prelu is not None and self.pool is not None:
             K.prelu_pool_bwd(dy, z, self.prelu.alpha.data, dz, self.prelu.alpha.grad, bias_g)
         elif self.prelu is not None:
             K.prelu_bwd(dy, z, self.prelu.alpha.data, dz, self.prelu.alpha.grad, bias_g)
@@ -200,7 +236,7 @@ class ConvOp(Op):
             raise NotImplementedError("dgrad for strided convolutions")
         dx = ws.get(self.name + "/dx", x.shape, torch.bfloat16, dev)
         if halo_dgrad:
-            KS, Co = self.conv.kernel_size[0], z.shape[-1]
+            KS, Co = self.conv.kernel_size[0], zshape[-1]
             wf = ws.get(self.name + "/wflip", (self.conv.cin_p, KS, KS, Co), torch.bfloat16, dev)
             K.conv2d_dgrad_halo(dz, self.conv.kernel.bf16, self.pad, dx, wf)
         else:

@@ -107,12 +107,19 @@ def halo_eligible(C: int, Cout: int, KS: int, stride: int, same: bool) -> bool:
     return same and stride == 1 and KS in (3, 5) and C in HALO_C and Cout % 8 == 0 and Cout <= 64
 
 
-EPI = {None: 0, "pool": 1, "prelu": 2}
+EPI = {None: 0, "pool": 1, "prelu": 2, "pools": 3}
 
 
-def conv2d_fwd_fused(x, w, bias, pad: int, z_out, alpha=None, aux_out=None, epi=None):
+def conv2d_fwd_fused(x, w, bias, pad: int, z_out, alpha=None, aux_out=None, epi=None, arg_out=None):
     """Halo-tiled 'same' conv: z = conv(x, w) + bias; epi='pool' also writes
-    aux = maxpool2x2(prelu(z, alpha)); epi='prelu' writes aux = prelu(z, alpha)."""
+    aux = maxpool2x2(prelu(z, alpha)); epi='prelu' writes aux = prelu(z, alpha).  epi='pools'
+    (sparse pool, GPU only) writes aux = the pooled output, z_out = z at each window's argmax
+    ([N,H/2,W/2,C]) and arg_out = the argmax position q = 2*dh + dw (uint8) instead of full z."""
+    if not on_device(x) and epi == "pools":
+        N, H, W, _ = x.shape
+        full = torch.empty((N, H, W, w.shape[0]), dtype=z_out.dtype)
+        ref.conv2d_fwd(x, w, bias, 1, pad, full, None)
+        return ref.prelu_pool_fwd_sparse(full, alpha, aux_out, z_out, arg_out)
     if not on_device(x):
         ref.conv2d_fwd(x, w, bias, 1, pad, z_out, None)
         if epi == "pool":
@@ -122,10 +129,16 @@ def conv2d_fwd_fused(x, w, bias, pad: int, z_out, alpha=None, aux_out=None, epi=
         return z_out
     N, H, W, C = x.shape
     Cout, KS, _, Cw = w.shape
-    assert Cw == C and tuple(z_out.shape) == (N, H, W, Cout)
+    if epi == "pools":
+        assert tuple(z_out.shape) == (N, H // 2, W // 2, Cout) and arg_out is not None
+        assert arg_out.dtype == torch.uint8 and tuple(arg_out.shape) == tuple(z_out.shape)
+        assert tuple(aux_out.shape) == tuple(z_out.shape)
+    else:
+        assert tuple(z_out.shape) == (N, H, W, Cout)
+    assert Cw == C
     need(x, torch.bfloat16, "conv_halo.x"); need(w, torch.bfloat16, "conv_halo.w")
-    hip("ptg_conv2d_fwd_halo", ptr(x), ptr(w), ptr(bias), ptr(alpha), ptr(z_out), ptr(aux_out), N, H, W, C, Cout, KS,
-        pad, EPI[epi])
+    hip("ptg_conv2d_fwd_halo", ptr(x), ptr(w), ptr(bias), ptr(alpha), ptr(z_out), ptr(aux_out), ptr(arg_out), N, H, W,
+        C, Cout, KS, pad, EPI[epi])
     return z_out
 
 
@@ -274,6 +287,16 @@ def prelu_pool_bwd(dp, z, alpha, dz_out, dalpha, dbias, nper: int = 0):
         return ref.prelu_pool_bwd(dp, z, alpha, dz_out, dalpha, dbias)
     N, H, W, C = z.shape
     hip("ptg_prelu_pool_bwd", ptr(dp), ptr(z), ptr(alpha), ptr(dz_out), ptr(dalpha), ptr(dbias), N, H, W, C, nper)
+    return dz_out
+
+
+def prelu_pool_bwd_sparse(dp, zsel, arg, alpha, dz_out, dalpha, dbias, nper: int = 0):
+    """Backward of maxpool2x2(prelu(z)) from the sparse forward record (zsel, arg)."""
+    if not on_device(dp):
+        return ref.prelu_pool_bwd_sparse(dp, zsel, arg, alpha, dz_out, dalpha, dbias)
+    N, H, W, C = dz_out.shape
+    hip("ptg_prelu_pool_bwd_sparse", ptr(dp), ptr(zsel), ptr(arg), ptr(alpha), ptr(dz_out), ptr(dalpha), ptr(dbias),
+        N, H, W, C, nper)
     return dz_out
 
 

@@ -135,6 +135,41 @@ def prelu_pool_bwd(dp, z, alpha, dz_out, dalpha, dbias):
     return dz_out
 
 
+def _windows(t):
+    """[N,H,W,C] -> [N,H/2,W/2,4,C] with window position q = 2*dh + dw."""
+    N, H, W, C = t.shape
+    return t.reshape(N, H // 2, 2, W // 2, 2, C).permute(0, 1, 3, 2, 4, 5).reshape(N, H // 2, W // 2, 4, C)
+
+
+def prelu_pool_fwd_sparse(z, alpha, pout, zsel_out, arg_out):
+    zf = _f(z)
+    y = _prelu(zf, _f(alpha))
+    yw, zw = _windows(y), _windows(zf)
+    q = torch.argmax(yw, dim=3)  # first maximum in q order
+    pout.copy_(torch.gather(yw, 3, q.unsqueeze(3)).squeeze(3).to(pout.dtype))
+    zsel_out.copy_(torch.gather(zw, 3, q.unsqueeze(3)).squeeze(3).to(zsel_out.dtype))
+    arg_out.copy_(q.to(torch.uint8))
+    return zsel_out
+
+
+def prelu_pool_bwd_sparse(dp, zsel, arg, alpha, dz_out, dalpha, dbias):
+    N, H, W, C = dz_out.shape
+    g, zs, q = _f(dp), _f(zsel), arg.long()
+    aw = _windows(_f(alpha).unsqueeze(0).expand(N, H, W, C))       # [N,PH,PW,4,C]
+    hit = torch.nn.functional.one_hot(q, 4).permute(0, 1, 2, 4, 3).bool()  # [N,PH,PW,4,C]
+    gq = torch.where(hit, g.unsqueeze(3), torch.zeros_like(aw))
+    pos = (zs > 0).unsqueeze(3)
+    dzw = torch.where(pos, gq, gq * aw)
+    daw = torch.where(pos, torch.zeros_like(gq), gq * zs.unsqueeze(3))
+    def unw(t):
+        return t.reshape(N, H // 2, W // 2, 2, 2, C).permute(0, 1, 3, 2, 4, 5).reshape(N, H, W, C)
+    dz = unw(dzw)
+    dz_out.copy_(dz.to(dz_out.dtype))
+    dalpha.add_(unw(daw).sum(0))
+    dbias.add_(dz.reshape(-1, C).sum(0))
+    return dz_out
+
+
 def prelu_fwd(z, alpha, out):
     out.copy_(_prelu(_f(z), _f(alpha)).to(out.dtype))
     return out

@@ -158,6 +158,51 @@ def test_conv_halo_fwd(N, H, W, C, Co, KS, epi):
         _close(aux, ar, 2e-2, 2e-2, "halo_prelu")
 
 
+@pytest.mark.parametrize("N,H,W,C,Co,KS", [c for c in HALO_CASES + BIG_HALO if c[1] % 2 == 0 and c[2] % 2 == 0])
+def test_conv_halo_pool_sparse(N, H, W, C, Co, KS):
+    """epi='pools': pooled output + z at the argmax + argmax position instead of the full z."""
+    x, w, b = rnd(N, H, W, C), rnd(Co, KS, KS, C, scale=0.2), torch.randn(Co)
+    alpha = torch.rand(H, W, Co) * 0.5
+    pad = KS // 2
+    shp = (N, H // 2, W // 2, Co)
+    zs = torch.empty(shp, device=DEV, dtype=torch.bfloat16)
+    p = torch.empty(shp, device=DEV, dtype=torch.bfloat16)
+    arg = torch.full(shp, 255, device=DEV, dtype=torch.uint8)
+    K.conv2d_fwd_fused(x.to(DEV), w.to(DEV), b.to(DEV), pad, zs, alpha.to(DEV), p, "pools", arg)
+    zr = torch.empty(N, H, W, Co, dtype=torch.bfloat16)
+    R.conv2d_fwd(x, w, b, 1, pad, zr)
+    pr = torch.empty(shp, dtype=torch.bfloat16)
+    R.prelu_pool_fwd(zr, alpha, pr)
+    _close(p, pr, 2e-2, 2e-2, "pools_p")
+    q = arg.cpu().long()
+    assert int(q.max()) <= 3
+    zw = R._windows(zr.float())
+    z_at = torch.gather(zw, 3, q.unsqueeze(3)).squeeze(3)
+    _close(zs, z_at, 2e-2, 2e-2, "pools_zsel")  # zsel is z at the reported argmax
+    yw = R._windows(torch.where(zr.float() > 0, zr.float(), zr.float() * alpha))
+    y_at = torch.gather(yw, 3, q.unsqueeze(3)).squeeze(3)
+    _close(y_at, yw.max(3).values, 2e-2, 2e-2, "pools_argmax_is_max")
+
+
+@pytest.mark.parametrize("C,N,H,W,nper", [(8, 3, 8, 12, 0), (16, 5, 16, 20, 2), (64, 3, 8, 12, 0), (32, 9, 6, 6, 4)])
+def test_prelu_pool_bwd_sparse(C, N, H, W, nper):
+    z = rnd(N, H, W, C)
+    alpha = torch.randn(H, W, C) * 0.3
+    shp = (N, H // 2, W // 2, C)
+    pr, zs, arg = torch.empty(shp), torch.empty(shp, dtype=torch.bfloat16), torch.empty(shp, dtype=torch.uint8)
+    R.prelu_pool_fwd_sparse(z, alpha, pr, zs, arg)
+    dp = rnd(*shp)
+    dz = torch.empty(N, H, W, C, device=DEV, dtype=torch.bfloat16)
+    da, db = torch.zeros(H, W, C, device=DEV), torch.zeros(C, device=DEV)
+    K.prelu_pool_bwd_sparse(dp.to(DEV), zs.to(DEV), arg.to(DEV), alpha.to(DEV), dz, da, db, nper)
+    dzr = torch.empty(N, H, W, C, dtype=torch.bfloat16)
+    dar, dbr = torch.zeros(H, W, C), torch.zeros(C)
+    R.prelu_pool_bwd_sparse(dp, zs, arg, alpha, dzr, dar, dbr)
+    _close(dz, dzr, 1e-2, 1e-2, "sparse_dz")
+    _close(da, dar, 1e-2, 1e-2, "sparse_dalpha")
+    _close(db, dbr, 1e-2, 1e-2, "sparse_dbias")
+
+
 @pytest.mark.parametrize("N,H,W,C,Co,KS", HALO_CASES + BIG_HALO)
 def test_conv_halo_wgrad(N, H, W, C, Co, KS):
     x, dz = rnd(N, H, W, C), rnd(N, H, W, Co, scale=0.1)
