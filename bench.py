@@ -84,8 +84,11 @@ def bench_cnn(args, strategy, rank, world):
     xs = [first._prep_input(x, model.ws).clone() if args.workload != "mnist" else x for x in xs]
     stats = model._stats_buf()
 
+    if args.graph:
+        model.jit_compile = True
+
     def step(i):
-        model.train_step(xs[i % 2], ys[i % 2], stats)
+        model.train_step_fast(xs[i % 2], ys[i % 2], stats)
 
     for i in range(args.warmup):
         step(i)

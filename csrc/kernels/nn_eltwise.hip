@@ -539,10 +539,21 @@ __global__ __launch_bounds__(256) void softmax_xent_k(const float* __restrict__ 
 // Writes the fp32 master weights and their bf16 compute copy.  gscale folds in the 1/world
 // averaging of all-reduced gradients.
 // ----------------------------------------------------------------------------------------------
+// Device-resident optimizer step state (HIP-graph capturable update): st[0] = step count t (as
+// float), st[1] = lr_t = lr * sqrt(1 - b2^t) / (1 - b1^t) for the step about to run.
+__global__ void adam_step_k(float* st, float lr, float b1, float b2) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    const float t = st[0] + 1.f;
+    st[0] = t;
+    st[1] = lr * sqrtf(1.f - powf(b2, t)) / (1.f - powf(b1, t));
+  }
+}
+
 __global__ __launch_bounds__(256) void adam_k(float* __restrict__ p, const float* __restrict__ g,
                                               float* __restrict__ m, float* __restrict__ v,
                                               bf16_t* __restrict__ pbf, long n4, float lr_t, float b1,
-                                              float b2, float eps, float gscale) {
+                                              float b2, float eps, float gscale, const float* __restrict__ lr_dev) {
+  if (lr_dev) lr_t = lr_dev[1];
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
     float4 pp = ((float4*)p)[i];
     const float4 gg = ((const float4*)g)[i];
@@ -838,11 +849,16 @@ int ptg_softmax_xent(const float* logits, const int* labels, float* dlogits, flo
 }
 
 int ptg_adam(float* p, const float* g, float* m, float* v, void* pbf, long n, float lr_t, float b1, float b2,
-             float eps, float gscale, hipStream_t s) {
+             float eps, float gscale, const float* lr_dev, hipStream_t s) {
   if (n % 4) return (int)hipErrorInvalidValue;
   const long n4 = n / 4;
   hipLaunchKernelGGL(adam_k, dim3(grid_for(n4)), dim3(256), 0, s, p, g, m, v, (bf16_t*)pbf, n4, lr_t, b1, b2,
-                     eps, gscale);
+                     eps, gscale, lr_dev);
+  PTG_RETURN_LAUNCH();
+}
+
+int ptg_adam_step(float* st, float lr, float b1, float b2, hipStream_t s) {
+  hipLaunchKernelGGL(adam_step_k, dim3(1), dim3(64), 0, s, st, lr, b1, b2);
   PTG_RETURN_LAUNCH();
 }
 

@@ -252,6 +252,8 @@ class Model(Sequential):
         from .model import default_device
 
         self.device = torch.device(device) if device is not None else default_device()
+        if self.device.type == "cuda" and self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
         self.store = ParamStore()
         shapes = {}
         for t in self.nodes:

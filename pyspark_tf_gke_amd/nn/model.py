@@ -104,6 +104,8 @@ class Sequential:
         if self.input_shape is None:
             raise ValueError("Sequential needs an Input layer or build(input_shape)")
         self.device = torch.device(device) if device is not None else default_device()
+        if self.device.type == "cuda" and self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
         self.store = ParamStore()
         shape = self.input_shape
         for l in self.layers:
@@ -146,7 +148,16 @@ class Sequential:
         self.store.refresh_bf16()
 
     # ---------------------------------------------------------------- compile
-    def compile(self, optimizer="adam", loss=None, metrics=None) -> None:
+    def compile(self, optimizer="adam", loss=None, metrics=None, jit_compile=None) -> None:
+        """``jit_compile=True`` (or env PTG_HIP_GRAPH=1) captures the whole training step - forward,
+        loss, backward, optimizer - into one HIP graph after two eager warm-up steps and replays it
+        (single-GPU training; multi-rank strategies stay eager because their collectives are
+        launched from host hooks)."""
+        if jit_compile is None:
+            jit_compile = os.environ.get("PTG_HIP_GRAPH", "0") == "1"
+        self.jit_compile = bool(jit_compile)
+        self._graphs = {}
+        self._graph_warm = {}
         self.optimizer = OPT.get(optimizer)
         self.loss = LS.get(loss) if loss is not None else None
         self.metric_names = [MT.canonical_name(m) for m in (metrics or [])]
@@ -272,6 +283,41 @@ class Sequential:
         dpred = self._loss_grad(out, yb, stats)
         self.backward_and_update(dpred, st)
 
+    # ---------------------------------------------------------------- HIP-graph step
+    def _graph_usable(self, xb) -> bool:
+        if not getattr(self, "jit_compile", False) or not xb.is_cuda:
+            return False
+        st = self._strategy()
+        return st is None or st.world_size == 1
+
+    def train_step_fast(self, xb, yb, stats=None) -> None:
+        """One training step; replays a captured HIP graph when ``jit_compile`` is on (same batch
+        shape/dtype as the captured step), otherwise runs eagerly."""
+        stats = self._stats_buf() if stats is None else stats
+        if not self._graph_usable(xb):
+            return self.train_step(xb, yb, stats)
+        key = (tuple(xb.shape), xb.dtype, tuple(yb.shape), yb.dtype, stats.data_ptr())
+        ent = self._graphs.get(key)
+        if ent is None:
+            n = self._graph_warm.get(key, 0)
+            if n < 2:  # eager warm-up: kernels selected, workspace buffers allocated
+                self._graph_warm[key] = n + 1
+                return self.train_step(xb, yb, stats)
+            self.optimizer.use_device_step(self.store)
+            sx, sy = xb.clone(), yb.clone()
+            torch.cuda.synchronize(xb.device)
+            graph = torch.cuda.CUDAGraph()
+            it0 = self.optimizer.iterations
+            with torch.cuda.graph(graph):
+                self.train_step(sx, sy, stats)  # recorded, not executed
+            self.optimizer.iterations = it0
+            ent = self._graphs[key] = (graph, sx, sy)
+        graph, sx, sy = ent
+        sx.copy_(xb, non_blocking=True)
+        sy.copy_(yb, non_blocking=True)
+        graph.replay()
+        self.optimizer.iterations += 1
+
     def train_on_batch(self, x, y, return_dict: bool = False):
         xb, yb = self._prep_batch(x, y)
         stats = self._stats_buf()
@@ -359,7 +405,7 @@ class Sequential:
                 except StopIteration:
                     break
                 xb, yb = self._prep_batch(batch[0], batch[1])
-                self.train_step(xb, yb, stats)
+                self.train_step_fast(xb, yb, stats)
                 nsteps += 1
             logs = self._logs_from(stats)
             if validation_data is not None:

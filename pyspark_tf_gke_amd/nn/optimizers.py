@@ -42,6 +42,13 @@ class Adam(Optimizer):
         if self.m is None or self.m.numel() != store.total or self.m.device != store.flat.device:
             self.m = torch.zeros(store.total, dtype=torch.float32, device=store.flat.device)
             self.v = torch.zeros(store.total, dtype=torch.float32, device=store.flat.device)
+            self.dev_state = None
+
+    def use_device_step(self, store) -> None:
+        """Keep the step counter / bias-corrected step size on the device (HIP-graph capture)."""
+        self.build(store)
+        if getattr(self, "dev_state", None) is None:
+            self.dev_state = torch.tensor([float(self.iterations), 0.0], dtype=torch.float32, device=store.flat.device)
 
     def lr_t(self, step: int) -> float:
         b1, b2 = self.beta_1, self.beta_2
@@ -51,10 +58,13 @@ class Adam(Optimizer):
         self.build(store)
         step = self.iterations + 1
         hi = store.total if hi is None else hi
+        ds = getattr(self, "dev_state", None)
+        if ds is not None and advance:
+            K.adam_step(ds, self.learning_rate, self.beta_1, self.beta_2)
         if hi > lo:
             sl = slice(lo, hi)
             K.adam(store.flat[sl], store.flat_grad[sl], self.m[sl], self.v[sl], store.flat_bf16[sl],
-                   self.lr_t(step), self.beta_1, self.beta_2, self.epsilon, gscale)
+                   self.lr_t(step), self.beta_1, self.beta_2, self.epsilon, gscale, lr_dev=ds)
         if advance:
             self.iterations = step
 
@@ -72,6 +82,8 @@ class Adam(Optimizer):
 
     def state_tensors(self) -> dict:
         return {"m": self.m, "v": self.v}
+
+
 
 
 class SGD(Optimizer):
@@ -110,6 +122,9 @@ class SGD(Optimizer):
 
     def state_tensors(self) -> dict:
         return {"velocity": self.velocity} if self.velocity is not None else {}
+
+    def use_device_step(self, store) -> None:
+        self.build(store)  # SGD has no step-dependent scalars: its launch is capturable as is
 
 
 def get(identifier) -> Optimizer:

@@ -351,11 +351,26 @@ def softmax_xent(logits, labels, dlogits, stats, gscale: float = 1.0):
     hip("ptg_softmax_xent", ptr(logits), ptr(labels), ptr(dlogits), ptr(stats), B, C, float(gscale))
 
 
-def adam(p, g, m, v, pbf, lr_t: float, b1: float, b2: float, eps: float, gscale: float = 1.0):
+def adam(p, g, m, v, pbf, lr_t: float, b1: float, b2: float, eps: float, gscale: float = 1.0, lr_dev=None):
+    """Fused Adam; with ``lr_dev`` (the device step state of :func:`adam_step`) the step size is read
+    on the device, so the launch can be captured once into a HIP graph and replayed every step."""
     if not on_device(p):
+        if lr_dev is not None:
+            lr_t = float(lr_dev[1])
         return ref.adam(p, g, m, v, pbf, lr_t, b1, b2, eps, gscale)
     hip("ptg_adam", ptr(p), ptr(g), ptr(m), ptr(v), ptr(pbf), p.numel(), float(lr_t), float(b1), float(b2),
-        float(eps), float(gscale))
+        float(eps), float(gscale), ptr(lr_dev))
+
+
+def adam_step(state, lr: float, b1: float, b2: float):
+    """state[0] += 1; state[1] = bias-corrected step size (on the device)."""
+    if not on_device(state):
+        t = float(state[0]) + 1.0
+        state[0] = t
+        state[1] = lr * math.sqrt(1.0 - b2 ** t) / (1.0 - b1 ** t)
+        return state
+    hip("ptg_adam_step", ptr(state), float(lr), float(b1), float(b2))
+    return state
 
 
 def sgd(p, g, vel, pbf, lr: float, momentum: float, nesterov: bool, gscale: float = 1.0):
