@@ -35,7 +35,11 @@ namespace ptgc {
 // step at batch 256 and its backward reads 335 MB less).
 enum { EPI_Z = 0, EPI_POOL = 1, EPI_PRELU = 2, EPI_POOLS = 3 };
 
-template <int C> struct PixPitch { static constexpr int v = C >= 16 ? C + 8 : C; };  // bank-conflict pad
+template <int C> struct PixPitch { static constexpr int v = C >= 16 ? C + 8 : C; };  // bank-conflict pad (wgrad)
+// forward halo: pixel pitch and per-row pad (elements) chosen with tools/lds_bank_sim.py so the
+// ds_read_b128 A-fragment reads of every (fragment, k-step) are conflict-free on gfx950's lane
+// groups (4 LDS cycles per read; C=16 was 7.9, C=32 12, C=64 8 with the uniform C+8 pitch).
+template <int C> struct FwdPitch { static constexpr int pix = C == 64 ? 96 : C, rowpad = (C == 32 || C == 64) ? 16 : 0; };
 template <int C, int KS> struct Kwp { static constexpr int v = (KS * C) % 8 == 0 ? KS : ((KS + 1) * C) % 8 == 0 ? KS + 1 : KS + 3; };
 
 // ------------------------------------------------------------------------------------------------
@@ -105,9 +109,9 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
   constexpr int VPP = HVec<C>::per_pix;      // vectors per pixel
   constexpr int VE = C == 4 ? 4 : 8;          // elements per vector
   constexpr int KWP = Kwp<C, KS>::v;
-  constexpr int PIX = PixPitch<C>::v;
+  constexpr int PIX = FwdPitch<C>::pix;
   constexpr int HR = TH + KS - 1, HC = TW + KWP - 1;
-  constexpr int ROWE = HC * PIX;
+  constexpr int ROWE = HC * PIX + FwdPitch<C>::rowpad;
   constexpr int NROWS = RING ? 2 * HR : HR;
   constexpr int KROW = KWP * C;
   constexpr int KTOT = KS * KROW;
@@ -280,7 +284,7 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
       int rr, cc;
       if constexpr (KSPLIT) frag_rc(i, rr, cc);
       else { rr = f_r[i]; cc = f_c[i]; }
-      pbase[i] = ((wstart + rr) * HC + cc) * PIX;
+      pbase[i] = (wstart + rr) * ROWE + cc * PIX;
     }
     f32x4_t acc[AF][NF];
 #pragma unroll
@@ -312,7 +316,7 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
       const bool kval = kf < KTOT;
       const int kh = kf / KROW, rem = kf - kh * KROW;
       const int kw = rem / C, ci = rem - kw * C;
-      const int koff = (kh * HC + kw) * PIX + ci;
+      const int koff = kh * ROWE + kw * PIX + ci;
 #pragma unroll
       for (int i = 0; i < AF; ++i) {
         bf16x8_t xf;

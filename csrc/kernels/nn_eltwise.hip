@@ -191,6 +191,141 @@ __global__ __launch_bounds__(256) void prelu_pool_bwd_k(const bf16_t* __restrict
   bias_reduce_atomic(db, c8, C8, sred, dbias);
 }
 
+// Backward of prelu+pool, sample-parallel inside the block: 256 threads = 16 pooled positions x 16
+// sample groups, so a block owns its 16 positions over a whole batch chunk and reduces dalpha over
+// the sample groups in LDS.  Large layers run one chunk (dalpha += without atomics: no other block
+// touches those elements); small layers split the batch over a few chunks and add with atomics.
+// (prelu_pool_bwd_k adds every block's dalpha partial with fp32 atomics: ~17M per layer at batch 256.)
+__global__ __launch_bounds__(256) void prelu_pool_bwd_sg_k(const bf16_t* __restrict__ dp,
+                                                           const bf16_t* __restrict__ z,
+                                                           const float* __restrict__ alpha,
+                                                           bf16_t* __restrict__ dz, float* __restrict__ dalpha,
+                                                           float* __restrict__ dbias, int N, int H, int W,
+                                                           int C, int nper) {
+  constexpr int PB = 16, SG = 16, RP = 33;  // RP: padded LDS row (bank-conflict free writes)
+  __shared__ float sda[SG * PB * RP];
+  __shared__ float sdb[256];
+  const int PH = H >> 1, PW = W >> 1, C8 = C >> 3;
+  const int npos = PH * PW * C8;
+  const int pl = threadIdx.x & (PB - 1), sg = threadIdx.x / PB;
+  const int i = blockIdx.x * PB + pl;
+  const int n0 = blockIdx.y * nper, n1 = min(N, n0 + nper);
+  const bool active = i < npos;
+  const int c8 = active ? i % C8 : 0;
+  const int t = active ? i / C8 : 0;
+  const int pw = t % PW, ph = t / PW;
+  long zoff[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) zoff[q] = ((long)(2 * ph + (q >> 1)) * W + 2 * pw + (q & 1)) * C + c8 * 8;
+  const long HWC = (long)H * W * C, PHWC = (long)PH * PW * C;
+  const long poff = ((long)ph * PW + pw) * C + c8 * 8;
+  float da[4][8], db[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) db[j] = 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) da[q][j] = 0.f;
+  if ((int)threadIdx.x < C) sdb[threadIdx.x] = 0.f;
+  if (active) {
+    float av[4][8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 a0 = *(const float4*)(alpha + zoff[q]), a1 = *(const float4*)(alpha + zoff[q] + 4);
+      av[q][0] = a0.x; av[q][1] = a0.y; av[q][2] = a0.z; av[q][3] = a0.w;
+      av[q][4] = a1.x; av[q][5] = a1.y; av[q][6] = a1.z; av[q][7] = a1.w;
+    }
+    const bool lastw = (W & 1) && pw == PW - 1, lasth = (H & 1) && ph == PH - 1;
+    for (int n = n0 + sg; n < n1; n += 2 * SG) {
+      const bool two = n + SG < n1;
+      U4 graw[2], zraw[2][4];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int nn = (u == 0 || two) ? n + u * SG : n;
+        graw[u] = *(const U4*)(dp + nn * PHWC + poff);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) zraw[u][q] = *(const U4*)(z + nn * HWC + zoff[q]);
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        if (u == 1 && !two) break;
+        const long nb = (long)(n + u * SG) * HWC;
+        float g[8], zv[4][8], y[4][8];
+        unpack8(graw[u], g);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          unpack8(zraw[u][q], zv[q]);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) y[q][j] = zv[q][j] > 0.f ? zv[q][j] : av[q][j] * zv[q][j];
+        }
+        int arg[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          int a = 0; float b = y[0][j];
+#pragma unroll
+          for (int q = 1; q < 4; ++q)
+            if (y[q][j] > b) { b = y[q][j]; a = q; }
+          arg[j] = a;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float o[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float gq = (arg[j] == q) ? g[j] : 0.f;
+            const float zz = zv[q][j];
+            o[j] = zz > 0.f ? gq : gq * av[q][j];
+            da[q][j] += zz > 0.f ? 0.f : gq * zz;
+            db[j] += o[j];
+          }
+          *(U4*)(dz + nb + zoff[q]) = pack8(o);
+        }
+        if (lastw || lasth) {
+          const U4 zz = zero4();
+          bf16_t* d = dz + nb + c8 * 8;
+          if (lastw) {
+            *(U4*)(d + ((long)(2 * ph) * W + W - 1) * C) = zz;
+            *(U4*)(d + ((long)(2 * ph + 1) * W + W - 1) * C) = zz;
+          }
+          if (lasth) {
+            *(U4*)(d + ((long)(H - 1) * W + 2 * pw) * C) = zz;
+            *(U4*)(d + ((long)(H - 1) * W + 2 * pw + 1) * C) = zz;
+          }
+          if (lastw && lasth) *(U4*)(d + ((long)(H - 1) * W + W - 1) * C) = zz;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sda[(sg * PB + pl) * RP + q * 8 + j] = da[q][j];
+  __syncthreads();
+  // bias: LDS atomics per channel, then one global atomic per channel and block
+  if (active) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) atomicAdd(&sdb[c8 * 8 + j], db[j]);
+  }
+  // dalpha: 16 positions x 32 values per block; thread handles 2 of the 512 sums over sample groups
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int o = h * 256 + threadIdx.x;
+    const int p = o >> 5, k = o & 31, q = k >> 3, j = k & 7;
+    float sum = 0.f;
+#pragma unroll
+    for (int gsg = 0; gsg < SG; ++gsg) sum += sda[(gsg * PB + p) * RP + k];
+    const int ii = blockIdx.x * PB + p;
+    if (ii < npos) {
+      const int cc = ii % C8, tq = ii / C8, pww = tq % PW, phh = tq / PW;
+      float* dst = dalpha + ((long)(2 * phh + (q >> 1)) * W + 2 * pww + (q & 1)) * C + cc * 8 + j;
+      if (gridDim.y == 1) *dst += sum;
+      else atomicAdd(dst, sum);
+    }
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < C) atomicAdd(dbias + threadIdx.x, sdb[threadIdx.x]);
+}
+
 // Backward of prelu+pool from the sparse forward record (conv.hip EPI_POOLS): per pooled element the
 // argmax position q (uint8) and the z there (bf16).  dz is dense (zero off the argmax), dalpha and
 // dbias as in prelu_pool_bwd_k.  Reads dp + zsel + arg (2.5 B per pooled element) instead of the
@@ -705,6 +840,22 @@ int ptg_prelu_pool_bwd(const void* dp, const void* z, const float* alpha, void* 
   }
   dim3 grid((npos + 255) / 256, (N + nper - 1) / nper);
   hipLaunchKernelGGL(prelu_pool_bwd_k, grid, dim3(256), 0, s, (const bf16_t*)dp, (const bf16_t*)z, alpha,
+                     (bf16_t*)dz, dalpha, dbias, N, H, W, C, nper);
+  PTG_RETURN_LAUNCH();
+}
+
+int ptg_prelu_pool_bwd2(const void* dp, const void* z, const float* alpha, void* dz, float* dalpha,
+                        float* dbias, int N, int H, int W, int C, int nper, hipStream_t s) {
+  if (C % 8 || C > 256 || H < 2 || W < 2) return (int)hipErrorInvalidValue;
+  const int npos = (H / 2) * (W / 2) * (C / 8);
+  const int bx = (npos + 15) / 16;
+  if (nper <= 0) {  // >= ~1024 blocks, but at least 64 samples (4 per sample group) per chunk
+    int chunks = (1024 + bx - 1) / bx;
+    chunks = std::max(1, std::min(chunks, N / 64));
+    nper = (N + chunks - 1) / chunks;
+  }
+  dim3 grid(bx, (N + nper - 1) / nper);
+  hipLaunchKernelGGL(prelu_pool_bwd_sg_k, grid, dim3(256), 0, s, (const bf16_t*)dp, (const bf16_t*)z, alpha,
                      (bf16_t*)dz, dalpha, dbias, N, H, W, C, nper);
   PTG_RETURN_LAUNCH();
 }

@@ -9,11 +9,16 @@ master parameters / gradients fp32.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
 from . import reference as ref
 from ._util import hip, need, on_device, ptr
+
+# prelu+pool backward kernel: "sg" = sample-parallel blocks with an in-LDS dalpha reduction
+# (prelu_pool_bwd_sg_k), "chunk" = position-parallel blocks adding dalpha partials with atomics
+PPBWD_KERNEL = os.environ.get("PTG_PPBWD", "sg")
 
 ACT = {None: 0, "linear": 0, "none": 0, "relu": 1, "softmax": 2}
 
@@ -286,7 +291,7 @@ def prelu_pool_bwd(dp, z, alpha, dz_out, dalpha, dbias, nper: int = 0):
     if not on_device(z):
         return ref.prelu_pool_bwd(dp, z, alpha, dz_out, dalpha, dbias)
     N, H, W, C = z.shape
-    hip("ptg_prelu_pool_bwd", ptr(dp), ptr(z), ptr(alpha), ptr(dz_out), ptr(dalpha), ptr(dbias), N, H, W, C, nper)
+    hip("ptg_prelu_pool_bwd2" if PPBWD_KERNEL == "sg" else "ptg_prelu_pool_bwd", ptr(dp), ptr(z), ptr(alpha), ptr(dz_out), ptr(dalpha), ptr(dbias), N, H, W, C, nper)
     return dz_out
 
 
