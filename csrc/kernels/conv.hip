@@ -99,7 +99,11 @@ PTG_DEV float row_shl(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), 0x100 | NSH, 0xF, 0xF, false));
 }
 
-template <int C, int KS, int NF, int TW, int TH, int EPI, bool RING, bool KSPLIT>
+// WLDS: the block's weight slice [NF*16 co][KSTEPS*32 k] is staged in LDS once (persistent
+// workgroup) and every A fragment is an LDS read instead of a per-wave global load per k-step
+// (for C >= 16 those loads were L2-latency bound).  COS > 1 splits Cout over COS workgroup groups
+// (blockIdx % COS), each holding NF*16 channels, when the whole filter does not fit LDS.
+template <int C, int KS, int NF, int TW, int TH, int EPI, bool RING, bool KSPLIT, bool WLDS = false, int COS = 1>
 __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
                                                         const float* __restrict__ bias, const float* __restrict__ alpha,
                                                         bf16_t* __restrict__ z, bf16_t* __restrict__ aux,
@@ -131,22 +135,41 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
   // the partial sums are reduce-scattered through LDS (more MFMAs per weight fetch when FM is small)
   constexpr int AF = KSPLIT ? MFR : FM;                // fragments a wave accumulates
   constexpr int RED_F4 = KSPLIT ? 4 * 3 * FM * NF * 64 : 1;
+  constexpr int WP = KSTEPS * 32 + 8;                  // LDS weight row pitch: odd multiple of 16 B
+  constexpr int WL_ELEMS = WLDS ? NF * 16 * WP : 8;
+  static_assert(!WLDS || (C >= 8 && !KSPLIT), "WLDS: contiguous filter rows, no k-split");
   __shared__ __attribute__((aligned(16))) bf16_t smem[HALO_ELEMS + 8];
   __shared__ __attribute__((aligned(16))) float4 sred[RED_F4];
+  __shared__ __attribute__((aligned(16))) bf16_t wlds[WL_ELEMS];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int px = lane & 15, g = lane >> 4;
   const int S = N * tiles_w;
+  const int cb = COS > 1 ? (int)(blockIdx.x % COS) * NF * 16 : 0;   // first output channel of this block
+  const int bid = COS > 1 ? (int)(blockIdx.x / COS) : (int)blockIdx.x;
+  const int nblk = COS > 1 ? (int)(gridDim.x / COS) : (int)gridDim.x;
   if (tid < 8) smem[HALO_ELEMS + tid] = 0;  // zero guard for padded K groups
+  if constexpr (WLDS) {
+    constexpr int VR = KSTEPS * 4;  // 16-byte vectors per weight row
+    for (int idx = tid; idx < NF * 16 * VR; idx += 256) {
+      const int r = idx / VR, v = idx - r * VR, co = cb + r, kf = v * 8;
+      U4 val = zero4();
+      if (co < Cout && kf < KTOT) val = *(const U4*)(w + (long)co * KTOT + kf);
+      *(U4*)(wlds + r * WP + kf) = val;
+    }
+  }
 
   // ---- weight fragments (MFMA A operand: row = co, 8 k per lane group): w [Cout][KS][KS][C] ----
   auto load_w = [&](int ks, int j) -> bf16x8_t {
     const int kf = ks * 32 + 8 * g;
     const int kh = kf / KROW, rem = kf - kh * KROW;
     const int kw = rem / C, ci = rem - kw * C;
-    const int co = j * 16 + px;
+    const int co = cb + j * 16 + px;
     U4 v = zero4();
-    if constexpr (C >= 8) {  // KWP == KS: flattened K is the memory order of a filter
+    if constexpr (WLDS) {
+      (void)kh; (void)kw; (void)ci; (void)co;
+      return *(const bf16x8_t*)(wlds + (j * 16 + px) * WP + kf);
+    } else if constexpr (C >= 8) {  // KWP == KS: flattened K is the memory order of a filter
       (void)kh; (void)kw; (void)ci;
       if (kf < KTOT && co < Cout) v = *(const U4*)(w + (long)co * KTOT + kf);
     } else if (kf < KTOT && co < Cout) {
@@ -171,7 +194,7 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
   float bv[NF][4];
 #pragma unroll
   for (int j = 0; j < NF; ++j) {
-    const int co0 = j * 16 + g * 4;
+    const int co0 = cb + j * 16 + g * 4;
     float4 b4 = make_float4(0.f, 0.f, 0.f, 0.f);
     if (bias && co0 < Cout) b4 = *(const float4*)(bias + co0);
     bv[j][0] = b4.x; bv[j][1] = b4.y; bv[j][2] = b4.z; bv[j][3] = b4.w;
@@ -239,7 +262,7 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
 
   // this workgroup's contiguous range of tiles, strip-major (balanced to within one tile)
   const long T = (long)S * tiles_h;
-  const int t0 = (int)(T * blockIdx.x / gridDim.x), t1 = (int)(T * (blockIdx.x + 1) / gridDim.x);
+  const int t0 = (int)(T * bid / nblk), t1 = (int)(T * (bid + 1) / nblk);
   if (t0 >= t1) return;
   int s = t0 / tiles_h, th = t0 - s * tiles_h;
   {  // first tile: synchronous fill of its HR rows
@@ -270,7 +293,7 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < NF; ++j) {
-          const int oh = oh0 + f_r[i], ow = ow0 + f_c[i], co0 = j * 16 + g * 4;
+          const int oh = oh0 + f_r[i], ow = ow0 + f_c[i], co0 = cb + j * 16 + g * 4;
           al[i][j] = (co0 < Cout && oh < H && ow < W) ? *(const float4*)(alpha + ((long)oh * W + ow) * Cout + co0)
                                                       : make_float4(0.f, 0.f, 0.f, 0.f);
         }
@@ -381,7 +404,7 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
       constexpr int STEP = WIDE ? 2 : 1;
 #pragma unroll
       for (int j = 0; j < NF; ++j) {
-        const int co0 = j * 16 + g * 4;
+        const int co0 = cb + j * 16 + g * 4;
         const bool cval = co0 < Cout;
 #pragma unroll
         for (int i = 0; i < FM; i += STEP) {
@@ -430,7 +453,7 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
     } else
 #pragma unroll
     for (int j = 0; j < NF; ++j) {
-      const int co0 = j * 16 + g * 4;
+      const int co0 = cb + j * 16 + g * 4;
       const bool cval = co0 < Cout;
       float y[FM][4];
 #pragma unroll
@@ -664,6 +687,173 @@ __global__ __launch_bounds__(256) void conv_wgrad_strip_k(const bf16_t* __restri
     }
 }
 
+// ================================================================================================
+// first layer: C=4 (packed RGB), Cout=8, fused bias + PReLU + 2x2 max-pool, pixel-pair MFMA
+// ================================================================================================
+// With Cout=8 the generic kernel wastes half of every 16-row MFMA (and half of the epilogue lanes).
+// Here the A operand's rows 0-7 are the 8 filters and rows 8-15 the same filters shifted one
+// column right - they fit the spare kw'=KS column of the KWP=KS+1 padded K for free - so with the
+// B columns at even pixels p, one v_mfma_f32_16x16x32_bf16 yields all 8 channels of pixels p and
+// p+1: 32 output pixels per MFMA, every lane busy in the epilogue, and each B fragment is one
+// aligned 16-byte LDS read (the pair (p+kw, p+kw+1) starts on an even pixel).  Lane (px, g) owns
+// pixel 2*px + (g>>1) of its 32-pixel fragment, channels 4*(g&1)..+3: z stores cover 512
+// contiguous bytes per wave instruction; the horizontal pool partner is lane ^ 32, the vertical one
+// the wave's other fragment (rows 2*rp, 2*rp+1).
+// Layout: 256x4-pixel... tiles of TW=64 x TH=4 pixels, mirrored ring of 2*HR halo rows walked
+// down a column strip, next rows prefetched into registers during the MFMAs (as conv_fwd_strip_k).
+template <int KS>
+__global__ __launch_bounds__(256) void conv1_pair_pool_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
+                                                         const float* __restrict__ bias, const float* __restrict__ alpha,
+                                                         bf16_t* __restrict__ z, bf16_t* __restrict__ pooled, int N, int H,
+                                                         int W, int pad, int tiles_h, int tiles_w) {
+  constexpr int C = 4, TW = 64, TH = 4;
+  constexpr int KWP = KS + 1;
+  static_assert((KWP * C) % 8 == 0 && TH < 2 * (KS - 1), "pair layout needs KS odd >= 5");
+  constexpr int HR = TH + KS - 1, HC = TW + KWP - 1;
+  constexpr int HP = (HC + 1) / 2;      // 16-byte pixel pairs per halo row
+  constexpr int ROWE = HP * 8;          // halo row pitch (elements), 16-byte aligned
+  constexpr int KROW = KWP * C, KTOT = KS * KROW, KSTEPS = (KTOT + 31) / 32;
+  constexpr int HALO = 2 * HR * ROWE;   // mirrored ring
+  constexpr int PFN = (HR * HP + 255) / 256;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[HALO + 8];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int px = lane & 15, g = lane >> 4;
+  if (tid < 8) smem[HALO + tid] = 0;
+
+  // A operand: row px = filter (px & 7), shifted one column right when px >= 8
+  bf16x8_t wreg[KSTEPS];
+  {
+    const int co = px & 7, sh = px >> 3;
+#pragma unroll
+    for (int ks = 0; ks < KSTEPS; ++ks) {
+      const int kf = ks * 32 + 8 * g;
+      U4 v = zero4();
+      if (kf < KTOT) {
+        const int kh = kf / KROW, kw = (kf - kh * KROW) / C;   // kw even
+        const bf16_t* wp = w + ((long)co * KS + kh) * KS * C;
+        const int a = kw - sh, b = kw + 1 - sh;
+        if (a >= 0 && a < KS) { const U2 t = *(const U2*)(wp + a * C); v.x = t.x; v.y = t.y; }
+        if (b >= 0 && b < KS) { const U2 t = *(const U2*)(wp + b * C); v.z = t.x; v.w = t.y; }
+      }
+      wreg[ks] = __builtin_bit_cast(bf16x8_t, v);
+    }
+  }
+  const int cc = 4 * (g & 1);
+  float bv[4] = {0.f, 0.f, 0.f, 0.f};
+  if (bias) { const float4 b4 = *(const float4*)(bias + cc); bv[0] = b4.x; bv[1] = b4.y; bv[2] = b4.z; bv[3] = b4.w; }
+
+  // halo slots: (row, pixel pair) per thread
+  int pr_r[PFN], pr_c[PFN];
+#pragma unroll
+  for (int p = 0; p < PFN; ++p) {
+    const int idx = tid + p * 256;
+    pr_r[p] = idx / HP;
+    pr_c[p] = idx - pr_r[p] * HP;
+  }
+  U4 pf[PFN];
+  auto load_rows = [&](int n, int iw0, int ih_first, int nrows) {
+    const bf16_t* img = x + (long)n * H * W * C;
+#pragma unroll
+    for (int p = 0; p < PFN; ++p) {
+      U4 v = zero4();
+      const int ih = ih_first + pr_r[p], iw = iw0 + 2 * pr_c[p];
+      if (pr_r[p] < nrows && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
+        v = *(const U4*)(img + ((long)ih * W + iw) * C);
+      pf[p] = v;
+    }
+  };
+  auto store_rows = [&](int nrows, int slot_first) {
+#pragma unroll
+    for (int p = 0; p < PFN; ++p) {
+      if (pr_r[p] < nrows) {
+        int slot = slot_first + pr_r[p];
+        slot = slot >= HR ? slot - HR : slot;
+        bf16_t* dst = smem + slot * ROWE + pr_c[p] * 8;
+        *(U4*)dst = pf[p];
+        *(U4*)(dst + HR * ROWE) = pf[p];
+      }
+    }
+  };
+
+  const int hf = wid & 1, rp = wid >> 1;   // this wave: columns hf*32.., rows 2*rp, 2*rp+1
+  const int S = N * tiles_w;
+  const long T = (long)S * tiles_h;
+  const int t0 = (int)(T * blockIdx.x / gridDim.x), t1 = (int)(T * (blockIdx.x + 1) / gridDim.x);
+  if (t0 >= t1) return;
+  int s = t0 / tiles_h, th = t0 - s * tiles_h;
+  {
+    const int n = s / tiles_w, ow0 = (s - n * tiles_w) * TW;
+    load_rows(n, ow0 - pad, th * TH - pad, HR);
+    store_rows(HR, (th * TH) % HR);
+  }
+  __syncthreads();
+  const int PH = H >> 1, PW = W >> 1;
+  for (int t = t0; t < t1; ++t) {
+    const int n = s / tiles_w, ow0 = (s - n * tiles_w) * TW, oh0 = th * TH;
+    int s2 = s, th2 = th + 1;
+    if (th2 >= tiles_h) { s2 = s + 1; th2 = 0; }
+    const bool has_next = t + 1 < t1;
+    const bool same_strip = s2 == s;
+    const int n2 = s2 / tiles_w, ow02 = (s2 - n2 * tiles_w) * TW;
+    const int nrows2 = same_strip ? TH : HR;
+    const int ih2 = same_strip ? th2 * TH - pad + HR - TH : th2 * TH - pad;
+    const int slot2 = same_strip ? (th2 * TH + HR - TH) % HR : (th2 * TH) % HR;
+    if (has_next) load_rows(n2, ow02 - pad, ih2, nrows2);
+
+    const int ow = ow0 + hf * 32 + 2 * px + (g >> 1);
+    float4 al[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int oh = oh0 + 2 * rp + i;
+      al[i] = (oh < H && ow < W) ? *(const float4*)(alpha + ((long)oh * W + ow) * 8 + cc) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    const int wstart = oh0 % HR;
+    f32x4_t acc[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int ks = 0; ks < KSTEPS; ++ks) {
+      const int kf = ks * 32 + 8 * g;
+      const int kh = kf / KROW, kw = (kf - kh * KROW) / C;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int off = kf < KTOT ? (wstart + 2 * rp + i + kh) * ROWE + (hf * 32 + 2 * px + kw) * C : HALO;
+        const bf16x8_t xf = *(const bf16x8_t*)(smem + off);
+        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wreg[ks], xf, acc[i], 0, 0, 0);
+      }
+    }
+    __syncthreads();  // every wave is done reading the halo window
+    if (has_next) store_rows(nrows2, slot2);
+
+    float y[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int oh = oh0 + 2 * rp + i;
+      const float a4[4] = {al[i].x, al[i].y, al[i].z, al[i].w};
+      float zr[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        zr[r] = bf2f(f2bf(acc[i][r] + bv[r]));
+        y[i][r] = zr[r] > 0.f ? zr[r] : a4[r] * zr[r];
+      }
+      if (oh < H && ow < W)
+        *(U2*)(z + (((long)n * H + oh) * W + ow) * 8 + cc) = U2{pack_bf(zr[0], zr[1]), pack_bf(zr[2], zr[3])};
+    }
+    float pm[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float v = fmaxf(y[0][r], y[1][r]);
+      pm[r] = fmaxf(v, __shfl_xor(v, 32, 64));
+    }
+    const int ph = (oh0 >> 1) + rp, pw = (ow0 >> 1) + hf * 16 + px;
+    if (g < 2 && ph < PH && pw < PW)
+      *(U2*)(pooled + (((long)n * PH + ph) * PW + pw) * 8 + cc) = U2{pack_bf(pm[0], pm[1]), pack_bf(pm[2], pm[3])};
+    if (!has_next) break;
+    __syncthreads();  // next tile's halo rows visible
+    s = s2;
+    th = th2;
+  }
+}
+
 // W'[ci][kh][kw][co] = W[co][KS-1-kh][KS-1-kw][ci]
 __global__ __launch_bounds__(256) void conv_flip_k(const bf16_t* __restrict__ w, bf16_t* __restrict__ wf, int Cout, int KS,
                                                    int Cin) {
@@ -694,22 +884,63 @@ static int resident_blocks(const void* kernel) {
   return cus * per_cu;
 }
 
-template <int C, int KS, int NF, int TW, int TH, int E>
-static int launch_fwd_e(const void* x, const void* w, const float* bias, const float* alpha, void* z, void* aux, void* arg, int N,
-                        int H, int W, int Cout, int pad, hipStream_t s) {
+template <int C, int KS, int NF, int TW, int TH, int E, bool WLDS, int COS>
+static int launch_fwd_k(const void* x, const void* w, const float* bias, const float* alpha, void* z, void* aux, void* arg,
+                        int N, int H, int W, int Cout, int pad, hipStream_t s) {
   constexpr bool RING = TH < 2 * (KS - 1);
   constexpr int KTOT = KS * Kwp<C, KS>::v * C, KSTEPS = (KTOT + 31) / 32, MFR = TH * TW / 16;
   constexpr bool WREG = KSTEPS * NF <= 8;
-  constexpr bool KSPLIT = !WREG && MFR / 4 <= 2 && MFR * NF <= 16;
-  const auto kern = conv_fwd_strip_k<C, KS, NF, TW, TH, E, RING, KSPLIT>;
+  constexpr bool KSPLIT = !WLDS && !WREG && MFR / 4 <= 2 && MFR * NF <= 16;
+  const auto kern = conv_fwd_strip_k<C, KS, NF, TW, TH, E, RING, KSPLIT, WLDS, COS>;
   static const int resident = resident_blocks((const void*)kern);
   const int th = (H + TH - 1) / TH, tw = (W + TW - 1) / TW;
   const long tiles = (long)N * tw * th;
   // persistent: one wave of resident workgroups, each walking a contiguous range of tiles
-  const int grid = (int)std::min<long>(tiles, resident);
+  // (COS groups of workgroups each cover all tiles for their slice of output channels)
+  const int grid = (int)std::min<long>(tiles * COS, resident / COS * COS);
   hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, (const bf16_t*)x, (const bf16_t*)w, bias, alpha, (bf16_t*)z,
                      (bf16_t*)aux, (uint8_t*)arg, N, H, W, Cout, pad, th, tw);
   PTG_RETURN_LAUNCH();
+}
+
+// PTG_CONV1_PAIR=0 routes the first layer (C=4, Cout=8) through the generic strip kernel
+static bool conv1_pair_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("PTG_CONV1_PAIR");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// PTG_CONV_WLDS=0 keeps the per-wave global weight loads (A/B switch for the LDS-resident path)
+static bool conv_wlds_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("PTG_CONV_WLDS");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+template <int C, int KS, int NF, int TW, int TH, int E>
+static int launch_fwd_e(const void* x, const void* w, const float* bias, const float* alpha, void* z, void* aux, void* arg, int N,
+                        int H, int W, int Cout, int pad, hipStream_t s) {
+  constexpr int KTOT = KS * Kwp<C, KS>::v * C, KSTEPS = (KTOT + 31) / 32;
+  constexpr bool WREG = KSTEPS * NF <= 8;
+  // measured on CNN-B1 shapes: C=16/32 gain 10-37 %; C=64 (4x16 tiles, one fragment per wave) is
+  // LDS-read bound at one workgroup per CU and loses to the k-split global-weight path
+  if constexpr (C >= 8 && C <= 32 && !WREG) {
+    // LDS budget: halo rows + weight slice must leave the block resident (160 KiB per CU)
+    constexpr int HR = TH + KS - 1, HC = TW + Kwp<C, KS>::v - 1;
+    constexpr int HALO_B = (HR < 2 * (KS - 1) ? 2 : 1) * HR * (HC * FwdPitch<C>::pix + FwdPitch<C>::rowpad) * 2;
+    constexpr int WB = NF * 16 * (KSTEPS * 32 + 8) * 2;
+    if (conv_wlds_enabled()) {
+      if constexpr (HALO_B + WB <= 150 * 1024)
+        return launch_fwd_k<C, KS, NF, TW, TH, E, true, 1>(x, w, bias, alpha, z, aux, arg, N, H, W, Cout, pad, s);
+      else if constexpr (NF % 2 == 0 && HALO_B + WB / 2 <= 150 * 1024)
+        return launch_fwd_k<C, KS, NF / 2, TW, TH, E, true, 2>(x, w, bias, alpha, z, aux, arg, N, H, W, Cout, pad, s);
+    }
+  }
+  return launch_fwd_k<C, KS, NF, TW, TH, E, false, 1>(x, w, bias, alpha, z, aux, arg, N, H, W, Cout, pad, s);
 }
 
 template <int C, int KS, int NF, int TW, int TH>
@@ -806,6 +1037,16 @@ int ptg_conv2d_fwd_halo(const void* x, const void* w, const float* bias, const f
                         int H, int W, int C, int Cout, int KS, int pad, int epi, hipStream_t s) {
   if (Cout % 8 || Cout > 64) return (int)hipErrorInvalidValue;
   if ((epi == EPI_POOL || epi == EPI_POOLS) && ((H & 1) || (W & 1))) return (int)hipErrorInvalidValue;
+  if (C == 4 && Cout == 8 && KS == 5 && epi == EPI_POOL && pad == 2 && conv1_pair_enabled()) {
+    const auto kern = conv1_pair_pool_k<5>;
+    static const int resident = resident_blocks((const void*)kern);
+    const int th = (H + 3) / 4, tw = (W + 63) / 64;
+    const long tiles = (long)N * th * tw;
+    const int grid = (int)std::min<long>(tiles, resident);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, (const bf16_t*)x, (const bf16_t*)w, bias, alpha, (bf16_t*)z,
+                       (bf16_t*)aux, N, H, W, pad, th, tw);
+    PTG_RETURN_LAUNCH();
+  }
   if (KS == 5) return fwd_by_cin<5>(x, w, bias, alpha, z, aux, arg, N, H, W, C, Cout, pad, epi, s);
   if (KS == 3) return fwd_by_cin<3>(x, w, bias, alpha, z, aux, arg, N, H, W, C, Cout, pad, epi, s);
   return (int)hipErrorInvalidValue;

@@ -121,7 +121,8 @@ def test_conv_wgrad_large_splitk():
 
 HALO_CASES = [(2, 16, 20, 4, 8, 5), (2, 18, 22, 8, 16, 5), (2, 12, 10, 16, 32, 5), (3, 8, 10, 32, 64, 5),
               (2, 8, 8, 64, 64, 5), (2, 10, 14, 64, 24, 3), (2, 6, 70, 4, 8, 3), (1, 64, 80, 16, 32, 5),
-              (2, 256, 320, 4, 8, 5), (2, 9, 7, 16, 64, 3)]
+              (2, 256, 320, 4, 8, 5), (2, 9, 7, 16, 64, 3),
+              (3, 18, 70, 4, 8, 5), (5, 30, 130, 4, 8, 5)]  # first-layer pair kernel: partial tiles
 
 
 # more tiles than resident workgroups: exercises the persistent tile ranges, the ring-buffer halo
