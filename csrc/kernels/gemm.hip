@@ -217,7 +217,7 @@ struct EpiBf16Remap {
   }
 };
 struct EpiF32 {  // out[m*ldc+n] (=|+=) act(acc + bias)
-  static constexpr bool VEC = false;  // fp32 rows: 16 lanes already cover 64 contiguous bytes
+  static constexpr bool VEC = true;  // staged through LDS: each lane stores 8 consecutive fp32 (2 x 16 B)
   float* out; long ldc; const float* bias; int act; int accumulate;
   PTG_DEV void operator()(int m, int n, float v) const {
     if (bias) v += bias[n];
@@ -226,6 +226,25 @@ struct EpiF32 {  // out[m*ldc+n] (=|+=) act(acc + bias)
     if (accumulate) *p += v; else *p = v;
   }
   PTG_DEV void vec8(int m, int n, float* v, int cnt) const {
+    float* p = out + (long)m * ldc + n;
+    if (cnt == 8 && al16(p) && (!bias || al16(bias + n))) {
+      float4 a = make_float4(v[0], v[1], v[2], v[3]), b = make_float4(v[4], v[5], v[6], v[7]);
+      if (bias) {
+        const float4 b0 = *(const float4*)(bias + n), b1 = *(const float4*)(bias + n + 4);
+        a.x += b0.x; a.y += b0.y; a.z += b0.z; a.w += b0.w; b.x += b1.x; b.y += b1.y; b.z += b1.z; b.w += b1.w;
+      }
+      if (act == ACT_RELU) {
+        a.x = fmaxf(a.x, 0.f); a.y = fmaxf(a.y, 0.f); a.z = fmaxf(a.z, 0.f); a.w = fmaxf(a.w, 0.f);
+        b.x = fmaxf(b.x, 0.f); b.y = fmaxf(b.y, 0.f); b.z = fmaxf(b.z, 0.f); b.w = fmaxf(b.w, 0.f);
+      }
+      if (accumulate) {
+        const float4 e0 = *(const float4*)p, e1 = *(const float4*)(p + 4);
+        a.x += e0.x; a.y += e0.y; a.z += e0.z; a.w += e0.w; b.x += e1.x; b.y += e1.y; b.z += e1.z; b.w += e1.w;
+      }
+      *(float4*)p = a;
+      *(float4*)(p + 4) = b;
+      return;
+    }
     for (int j = 0; j < cnt; ++j) (*this)(m, n + j, v[j]);
   }
 };

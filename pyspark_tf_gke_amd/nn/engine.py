@@ -88,7 +88,9 @@ class ConvOp(Op):
         super().__init__()
         self.conv, self.prelu, self.pool = conv, prelu, pool
         self.params = list(conv.params) + (list(prelu.params) if prelu else [])
-        conv.kernel.overwrite_grad = True
+        conv.kernel.fwd_bf16 = True
+        # the kernel gradient is NOT overwrite_grad: the store's single per-step fill zeroes it
+        # together with the biases/alphas, and the wgrad kernels accumulate onto it
         self.stride = conv.strides[0]
         self.pad = conv.pad_amount()
         self.name = conv.name
@@ -227,9 +229,9 @@ class ConvOp(Op):
             K.col_sum(dz.reshape(-1, dz.shape[-1]), bias_g)
         halo_fwd, halo_dgrad = self._halo()
         if halo_fwd:
-            K.conv2d_wgrad_halo(x, dz, self.pad, self.conv.kernel.grad)
+            K.conv2d_wgrad_halo(x, dz, self.pad, self.conv.kernel.grad, zeroed=True)
         else:
-            K.conv2d_wgrad(x, dz, self.stride, self.pad, self.conv.kernel.grad)
+            K.conv2d_wgrad(x, dz, self.stride, self.pad, self.conv.kernel.grad, accumulate=True)
         if self.first:
             return None
         if self.stride != 1:
@@ -254,6 +256,7 @@ class DenseOp(Op):
         self.big = N > 64 and N % 8 == 0 and Kd % 8 == 0
         if self.big:
             dense.kernel.overwrite_grad = True
+            dense.kernel.fwd_bf16 = True
         self.act = dense.activation
         self.logits_only = False  # softmax folded into the loss
 
@@ -445,8 +448,10 @@ def lower(layers: list) -> list:
     return ops
 
 
-def run_forward(ops, x, ws, training=True):
+def run_forward(ops, x, ws, training=True, pre_op=None):
     for k, op in enumerate(ops):
+        if pre_op is not None:
+            pre_op(op)  # e.g. wait for this op's parameter all-gather (sharded data-parallel update)
         if isinstance(op, DenseOp) and op.mask_for_prev:
             op._prev_y = op._prev_op._y if hasattr(op, "_prev_op") else None
         x = op.forward(x, ws, training)

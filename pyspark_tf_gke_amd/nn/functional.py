@@ -74,9 +74,11 @@ class GraphPlan:
         for op in self.ops:
             op.first = all(i == input_idx for i in op.inputs)
 
-    def forward(self, x, ws, training):
+    def forward(self, x, ws, training, pre_op=None):
         vals = {self.input_idx: x}
         for op in self.ops:
+            if pre_op is not None:
+                pre_op(op)
             vals[op.output] = op.forward([vals[i] for i in op.inputs], ws, training)
         return vals[self.output_idx]
 
@@ -271,6 +273,7 @@ class Model(Sequential):
                 l.init_state(self.device)
         self.plan = GraphPlan(self.nodes, self.nodes.index(self._in), self.nodes.index(self._out))
         self.ops = self.plan.ops
+        self.store.update_zero_ranges()
         self.built = True
         from ..distribute import current_strategy
 
@@ -280,7 +283,7 @@ class Model(Sequential):
 
     # ---- execution plan hooks
     def _run_forward(self, xb, training: bool):
-        return self.plan.forward(xb, self.ws, training)
+        return self.plan.forward(xb, self.ws, training, pre_op=self._pre_op_hook())
 
     def _run_backward(self, dpred, on_op_done=None):
         return self.plan.backward(dpred, self.ws, on_op_done=on_op_done)

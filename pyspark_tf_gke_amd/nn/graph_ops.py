@@ -126,8 +126,7 @@ def conv_wgrad(x, dz, stride, pad, dw):
         return dw
     same = pad == KH // 2 and KH == KW and stride == 1
     if KH in HALO_KS and K.halo_eligible(C, Co, KH, stride, same):
-        tmp = dw  # halo wgrad overwrites; dw was zeroed by the store for this step
-        return K.conv2d_wgrad_halo(x, dz, pad, tmp)
+        return K.conv2d_wgrad_halo(x, dz, pad, dw, zeroed=True)  # dw zeroed by the store
     return K.conv2d_wgrad(x, dz, stride, pad, dw, accumulate=True)
 
 
@@ -197,6 +196,7 @@ class ConvBNOp:
     def __init__(self, conv: L.Conv2D, bn: L.BatchNormalization, relu: bool, residual: bool, extra_pad: int = 0):
         self.conv, self.bn, self.relu, self.residual = conv, bn, relu, residual
         self.params = list(conv.params) + list(bn.params)
+        conv.kernel.fwd_bf16 = True
         self.stride = conv.strides[0]
         if conv.strides[0] != conv.strides[1]:
             raise NotImplementedError("non-square strides")

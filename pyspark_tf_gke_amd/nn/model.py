@@ -115,6 +115,7 @@ class Sequential:
             seed = int(os.environ.get("PTG_SEED", "1337"))
         self.store.finalize(self.device, seed=seed)
         self.ops = E.lower(self._layers)
+        self.store.update_zero_ranges()
         self.built = True
         from ..distribute import current_strategy
 
@@ -136,6 +137,7 @@ class Sequential:
         return []  # no regularizers (reference: `model.losses` is empty, train_tf_ps.py:624)
 
     def get_weights(self):
+        self._check_master()
         return [w for l in self.layers for w in l.keras_weights()]
 
     def set_weights(self, ws):
@@ -175,7 +177,27 @@ class Sequential:
 
     # ---------------------------------------------------------------- execution plan hooks
     def _run_forward(self, xb, training: bool):
-        return E.run_forward(self.ops, xb, self.ws, training)
+        return E.run_forward(self.ops, xb, self.ws, training, pre_op=self._pre_op_hook())
+
+    def _pre_op_hook(self):
+        """Per-op forward hook of the sharded data-parallel update (waits for the op's parameter
+        all-gather right before the op runs); None when the model is not sharded."""
+        if getattr(self, "_shard_plan", None) is None:
+            return None
+        st = self.strategy
+        return lambda op: st.before_forward_op(self, op)
+
+    def _sync_master(self) -> None:
+        """Collective: make the fp32 master weights current on every rank (sharded update)."""
+        st = getattr(self, "strategy", None)
+        if st is not None and hasattr(st, "synchronize_master"):
+            st.synchronize_master(self)
+
+    def _check_master(self) -> None:
+        if getattr(self.store, "master_stale", False):
+            raise RuntimeError("after sharded data-parallel steps only this rank's slice of the fp32 master "
+                               "weights is current: call strategy.synchronize_master(model) on every rank "
+                               "first (fit() and train_on_batch() do it for you)")
 
     def _run_backward(self, dpred, on_op_done=None):
         return E.run_backward(self.ops, dpred, self.ws, on_op_done=on_op_done)
@@ -323,6 +345,7 @@ class Sequential:
         stats = self._stats_buf()
         stats.zero_()
         self.train_step(xb, yb, stats)
+        self._sync_master()
         logs = self._logs_from(stats)
         return logs if return_dict else [logs["loss"]] + [logs[m] for m in self.metric_names if m in logs]
 
@@ -408,6 +431,7 @@ class Sequential:
                 self.train_step_fast(xb, yb, stats)
                 nsteps += 1
             logs = self._logs_from(stats)
+            self._sync_master()  # every rank is here: the full fp32 master for callbacks / saving
             if validation_data is not None:
                 vlogs = self.evaluate(*(validation_data if isinstance(validation_data, tuple) else (validation_data,)),
                                       batch_size=batch_size, steps=validation_steps, verbose=0, return_dict=True,
@@ -509,6 +533,7 @@ class Sequential:
         st = self._strategy()
         if st is not None and not st.is_chief:
             return
+        self._check_master()
         cfg = {"module": "pyspark_tf_gke_amd.nn", "class_name": self._save_class_name(), "config": self.get_config(),
                "compile_config": {"optimizer": self.optimizer.get_config() if self.optimizer else None,
                                   "loss": self.loss.name if self.loss else None, "metrics": self.metric_names}}

@@ -68,13 +68,16 @@ class Adam(Optimizer):
         if advance:
             self.iterations = step
 
-    def apply_shard(self, store, grad_shard, lo: int, hi: int, gscale: float = 1.0) -> None:
-        """Update params[lo:hi] from an already-reduced gradient shard (sharded PS strategy)."""
+    def apply_shard(self, store, grad_shard, lo: int, hi: int, gscale: float = 1.0, advance: bool = True) -> None:
+        """Update params[lo:hi] from an already-reduced gradient shard (sharded PS / sharded
+        data-parallel update).  ``advance=False`` lets one step update several shards."""
         self.build(store)
         step = self.iterations + 1
-        K.adam(store.flat[lo:hi], grad_shard, self.m[lo:hi], self.v[lo:hi], store.flat_bf16[lo:hi],
-               self.lr_t(step), self.beta_1, self.beta_2, self.epsilon, gscale)
-        self.iterations = step
+        if hi > lo:
+            K.adam(store.flat[lo:hi], grad_shard, self.m[lo:hi], self.v[lo:hi], store.flat_bf16[lo:hi],
+                   self.lr_t(step), self.beta_1, self.beta_2, self.epsilon, gscale)
+        if advance:
+            self.iterations = step
 
     def get_config(self):
         return {"name": self.name, "learning_rate": self.learning_rate, "beta_1": self.beta_1,
@@ -110,11 +113,13 @@ class SGD(Optimizer):
         if advance:
             self.iterations += 1
 
-    def apply_shard(self, store, grad_shard, lo: int, hi: int, gscale: float = 1.0) -> None:
+    def apply_shard(self, store, grad_shard, lo: int, hi: int, gscale: float = 1.0, advance: bool = True) -> None:
         self.build(store)
-        K.sgd(store.flat[lo:hi], grad_shard, self.velocity[lo:hi] if self.velocity is not None else None,
-              store.flat_bf16[lo:hi], self.learning_rate, self.momentum, self.nesterov, gscale)
-        self.iterations += 1
+        if hi > lo:
+            K.sgd(store.flat[lo:hi], grad_shard, self.velocity[lo:hi] if self.velocity is not None else None,
+                  store.flat_bf16[lo:hi], self.learning_rate, self.momentum, self.nesterov, gscale)
+        if advance:
+            self.iterations += 1
 
     def get_config(self):
         return {"name": self.name, "learning_rate": self.learning_rate, "momentum": self.momentum,

@@ -54,6 +54,8 @@ class Param:
     grad: torch.Tensor | None = None
     bf16: torch.Tensor | None = None
     mask_fn: Callable | None = None  # zero padded entries after init (e.g. padded input channels)
+    fwd_bf16: bool = False  # forward reads only the bf16 mirror (matmul/conv weights): the sharded
+    #                         update may all-gather just the bf16 copy of it
 
     @property
     def numel(self) -> int:
@@ -100,7 +102,12 @@ class ParamStore:
         mirror = torch.float32 if (host_fp32() and self.device.type == "cpu") else torch.bfloat16
         self.flat_bf16 = self.flat.to(mirror)
         self._bind_views()
-        # contiguous ranges whose gradient must be zeroed before each backward
+        self.update_zero_ranges()
+
+    def update_zero_ranges(self) -> None:
+        """Contiguous ranges whose gradient must be zeroed before each backward (every parameter
+        whose backward accumulates).  Re-run after the engine lowers the model, since lowering
+        decides which gradients are written whole (``overwrite_grad``)."""
         ranges = []
         for p in sorted(self.params, key=lambda q: q.offset):
             if p.overwrite_grad:
@@ -111,6 +118,38 @@ class ParamStore:
             else:
                 ranges.append([lo, hi])
         self._zero_ranges = [tuple(r) for r in ranges]
+
+    def relayout(self, groups: list, align: int) -> list:
+        """Re-place the parameters: ``groups`` (lists of Params, each in the order wanted) are laid
+        out one after another, every group starting on and padded to a multiple of ``align``
+        elements.  Values (fp32 master and bf16 mirror) move with their parameters; gradients are
+        zero.  Returns the [lo, hi) element range of each group.  Used by the sharded data-parallel
+        update, whose reduce-scatter / all-gather buckets need world-divisible ranges."""
+        seen = {id(p) for g in groups for p in g}
+        assert len(seen) == len(self.params), "relayout must place every parameter exactly once"
+        old = {id(p): (p.offset, p.numel) for p in self.params}
+        ranges, off = [], 0
+        for g in groups:
+            off = int(math.ceil(off / align) * align)
+            lo = off
+            for p in g:
+                p.offset = off
+                off += int(math.ceil(p.numel / ALIGN) * ALIGN)
+            off = int(math.ceil(off / align) * align)
+            ranges.append((lo, off))
+        total = max(off, ALIGN)
+        flat = torch.zeros(total, dtype=self.flat.dtype, device=self.flat.device)
+        mirror = torch.zeros(total, dtype=self.flat_bf16.dtype, device=self.flat.device)
+        for p in self.params:
+            o, n = old[id(p)]
+            flat[p.offset:p.offset + n] = self.flat[o:o + n]
+            mirror[p.offset:p.offset + n] = self.flat_bf16[o:o + n]
+        self.flat, self.flat_bf16 = flat, mirror
+        self.flat_grad = torch.zeros(total, dtype=torch.float32, device=flat.device)
+        self.total = total
+        self._bind_views()
+        self.update_zero_ranges()
+        return ranges
 
     def _bind_views(self) -> None:
         for p in self.params:

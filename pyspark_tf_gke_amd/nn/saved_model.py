@@ -57,6 +57,8 @@ def save(model, export_dir: str, signatures=None, assets: dict | None = None) ->
     st = model._strategy() if hasattr(model, "_strategy") else None
     if st is not None and not st.is_chief:
         return export_dir
+    if hasattr(model, "_check_master"):
+        model._check_master()
     tmp = export_dir.rstrip("/") + ".tmp"
     shutil.rmtree(tmp, ignore_errors=True)
     os.makedirs(os.path.join(tmp, "variables"))

@@ -147,13 +147,16 @@ def conv2d_fwd_fused(x, w, bias, pad: int, z_out, alpha=None, aux_out=None, epi=
     return z_out
 
 
-def conv2d_wgrad_halo(x, dz, pad: int, out):
-    """out[Cout,KS,KS,C] (fp32) = d(conv)/dw for a stride-1 'same' conv (halo-tiled MFMA)."""
+def conv2d_wgrad_halo(x, dz, pad: int, out, zeroed: bool = False):
+    """out[Cout,KS,KS,C] (fp32) = d(conv)/dw for a stride-1 'same' conv (halo-tiled MFMA).
+    ``zeroed``: ``out`` already holds zeros (the parameter store's one per-step gradient fill), so
+    the kernel's atomic partial sums land on it directly."""
     if not on_device(x):
         return ref.conv2d_wgrad(x, dz, 1, pad, out, False)
     N, H, W, C = x.shape
     Cout, KS, _, _ = out.shape
-    out.zero_()
+    if not zeroed:
+        out.zero_()
     hip("ptg_conv2d_wgrad_halo", ptr(x), ptr(dz), ptr(out), N, H, W, C, Cout, KS, pad)
     return out
 

@@ -1,5 +1,5 @@
 """Checkpoint / resume.  The reference only saves the final ``model.keras``; here a
-checkpoint holds the flat fp32 parameters, the optimizer state (Adam moments / SGD velocity) and
+checkpoint holds the fp32 parameters (per parameter name), the optimizer state (Adam moments / SGD velocity) and
 step, the BatchNormalization moving statistics, the epoch, and the RNG
 state, written atomically with safetensors + a JSON manifest.  Parameters/moments are identical
 on every rank for mirrored training (rank 0 writes), while the sharded parameter-server strategy
@@ -16,26 +16,41 @@ import torch
 from ..parallel import comm
 
 
+def _ps_sharded(model) -> bool:
+    st = getattr(model, "strategy", None)
+    return st is not None and hasattr(st, "shard_range") and comm.world_size() > 1
+
+
 def save_checkpoint(model, path: str, epoch: int, extra: dict | None = None) -> str:
+    """Collective (every rank calls it).  Parameters and mirrored optimizer state are stored per
+    parameter name (``param/<name>``, ``opt_<slot>/<name>``), so a checkpoint loads into any
+    flat-buffer layout (1 GPU, or N GPUs with the sharded data-parallel update's re-laid-out store).
+    The parameter-server strategy keeps its per-rank flat optimizer shards (``opt_<slot>`` + lo/hi)."""
     from safetensors.torch import save_file
 
     os.makedirs(path, exist_ok=True)
     opt = model.optimizer
     st = model.store
+    strat = getattr(model, "strategy", None)
+    if strat is not None and hasattr(strat, "synchronize_state"):
+        strat.synchronize_state(model)  # sharded update: full fp32 master + optimizer moments
     rank = comm.rank()
     tensors = {}
-    sharded = hasattr(model.strategy, "shard_range") if getattr(model, "strategy", None) is not None else False
+    sharded = _ps_sharded(model)
     if rank == 0 or sharded:
-        if sharded and comm.world_size() > 1:
-            lo, hi = model.strategy.shard_range(model)
-        else:
-            lo, hi = 0, st.total
+        lo, hi = model.strategy.shard_range(model) if sharded else (0, st.total)
         if opt is not None:
             for k, t in opt.state_tensors().items():
-                if t is not None:
+                if t is None:
+                    continue
+                if sharded:
                     tensors["opt_" + k] = t[lo:hi].detach().cpu().contiguous()
+                elif rank == 0:
+                    for p in st.params:
+                        tensors[f"opt_{k}/{p.name}"] = t[p.offset:p.offset + p.numel].detach().cpu().contiguous()
         if rank == 0:
-            tensors["params"] = st.flat.detach().cpu().contiguous()
+            for p in st.params:
+                tensors["param/" + p.name] = p.data.detach().reshape(-1).cpu().contiguous()
             for l in model.layers:  # non-trainable BatchNormalization state
                 if getattr(l, "moving_mean", None) is not None:
                     tensors[f"bn/{l.name}/moving_mean"] = l.moving_mean.detach().cpu().contiguous()
@@ -46,8 +61,8 @@ def save_checkpoint(model, path: str, epoch: int, extra: dict | None = None) -> 
     comm.barrier()
     if rank == 0:
         manifest = {"epoch": epoch, "step": opt.iterations if opt else 0, "world_size": comm.world_size(),
-                    "sharded": sharded, "time": time.time(), "torch_rng": torch.get_rng_state().tolist()[:16],
-                    **(extra or {})}
+                    "sharded": sharded, "layout": "per-param", "time": time.time(),
+                    "torch_rng": torch.get_rng_state().tolist()[:16], **(extra or {})}
         with open(os.path.join(path, "manifest.json.tmp"), "w") as fh:
             json.dump(manifest, fh)
         os.replace(os.path.join(path, "manifest.json.tmp"), os.path.join(path, "manifest.json"))
@@ -60,6 +75,9 @@ def load_checkpoint(model, path: str) -> dict:
 
     with open(os.path.join(path, "manifest.json")) as fh:
         manifest = json.load(fh)
+    strat = getattr(model, "strategy", None)
+    if strat is not None and hasattr(strat, "wait_parameters"):
+        strat.wait_parameters(model)  # no parameter gather still in flight may land on the loaded values
     st = model.store
     opt = model.optimizer
     if opt is not None:
@@ -67,11 +85,15 @@ def load_checkpoint(model, path: str) -> dict:
     state = opt.state_tensors() if opt is not None else {}
     with safe_open(os.path.join(path, "shard-00000.safetensors"), "pt") as f:
         keys = set(f.keys())
-        st.flat.copy_(f.get_tensor("params").to(st.flat.device))
-        if not manifest["sharded"]:
-            for k, t in state.items():
-                if t is not None and "opt_" + k in keys:
-                    t.copy_(f.get_tensor("opt_" + k).to(t.device))
+        for p in st.params:
+            key = "param/" + p.name
+            if key not in keys:
+                raise KeyError(f"checkpoint {path} has no parameter {p.name!r}")
+            p.data.copy_(f.get_tensor(key).to(st.flat.device).view(p.shape))
+            if not manifest["sharded"]:
+                for k, t in state.items():
+                    if t is not None and f"opt_{k}/{p.name}" in keys:
+                        t[p.offset:p.offset + p.numel].copy_(f.get_tensor(f"opt_{k}/{p.name}").to(t.device))
         for l in model.layers:
             if getattr(l, "moving_mean", None) is not None and f"bn/{l.name}/moving_mean" in keys:
                 l.moving_mean.copy_(f.get_tensor(f"bn/{l.name}/moving_mean").to(l.moving_mean.device))
@@ -88,6 +110,7 @@ def load_checkpoint(model, path: str) -> dict:
     if opt is not None:
         opt.iterations = int(manifest["step"])
     st.refresh_bf16()
+    st.master_stale = False
     return manifest
 
 

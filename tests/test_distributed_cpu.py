@@ -60,13 +60,69 @@ def test_mirrored_matches_single_process_global_batch():
             gs.append(ref.store.flat_grad.clone())
         ref.store.flat_grad.copy_(gs[0] + gs[1])
         ref.optimizer.apply(ref.store, gscale=0.5)
-    diff = float((m.store.flat - ref.store.flat).abs().max())
+    st.synchronize_master(m)
+    diff = max(float((p.data - ref.store.by_name(p.name).data).abs().max()) for p in m.store.params)
     print("RESULT", json.dumps({"diff": diff}), flush=True)
     """
     r = _run_ranks(body)
     assert r.returncode == 0, r.stdout + r.stderr
     res = _results(r.stdout)
     assert len(res) == 2 and all(v["diff"] < 1e-5 for v in res.values()), res
+
+
+SHARDED_BODY = """
+import json, os, tempfile, torch, numpy as np
+from pyspark_tf_gke_amd.distribute import MultiWorkerMirroredStrategy
+from pyspark_tf_gke_amd.models import build_cnn_model
+from pyspark_tf_gke_amd.utils import checkpoint as C
+from pyspark_tf_gke_amd.parallel import comm
+st_s = MultiWorkerMirroredStrategy(device="cpu", sharded_update=True, bucket_mb=0.5)
+st_p = MultiWorkerMirroredStrategy(device="cpu", sharded_update=False)
+rng = np.random.default_rng(st_s.rank)
+X = torch.from_numpy(rng.random((3, 4, 32, 32, 3)).astype(np.float32))
+Y = torch.from_numpy((rng.random((3, 4, 2)) * 30).astype(np.float32))
+models = {}
+for name, st in (("sharded", st_s), ("plain", st_p)):
+    with st.scope():
+        models[name] = build_cnn_model((32, 32, 3), flat=True, summary=False, device="cpu")
+ms, mp = models["sharded"], models["plain"]
+plan = ms._shard_plan
+kinds = sorted({b.fp32 for b in plan.buckets})
+for i in range(3):
+    for m in (ms, mp):
+        stats = m._stats_buf(); stats.zero_()
+        m.train_step_fast(X[i], Y[i], stats)
+stale = bool(ms.store.master_stale)
+st_s.synchronize_master(ms)
+diff = max(float((p.data - mp.store.by_name(p.name).data).abs().max()) for p in ms.store.params)
+ref = max(float(p.data.abs().max()) for p in mp.store.params)
+# checkpoint written from the sharded layout loads into the plain layout
+d = os.environ["PTG_TEST_CKPT"]
+C.save_checkpoint(ms, d, 0)
+with st_p.scope():
+    m2 = build_cnn_model((32, 32, 3), flat=True, summary=False, device="cpu")
+C.load_checkpoint(m2, d)
+cdiff = max(float((p.data - ms.store.by_name(p.name).data).abs().max()) for p in m2.store.params)
+mdiff = max(float((m2.optimizer.m[p.offset:p.offset + p.numel] - mp.optimizer.m[mp.store.by_name(p.name).offset:
+             mp.store.by_name(p.name).offset + p.numel]).abs().max()) for p in m2.store.params)
+print("RESULT", json.dumps({"diff": diff, "ref": ref, "stale": stale, "kinds": kinds, "nb": len(plan.buckets),
+                            "cdiff": cdiff, "mdiff": mdiff, "iters": ms.optimizer.iterations}), flush=True)
+"""
+
+
+@pytest.mark.parametrize("nproc", [2, 3])
+def test_sharded_update_matches_allreduce(nproc, tmp_path):
+    """Reduce-scatter + sharded Adam + (bf16/fp32) all-gather == all-reduce + replicated Adam, with
+    several buckets of both kinds; checkpoints are layout-independent and carry the gathered
+    optimizer moments."""
+    r = _run_ranks(SHARDED_BODY, nproc=nproc, extra_env={"PTG_HOST_FP32": "1", "PTG_TEST_CKPT": str(tmp_path / "ck")})
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    res = _results(r.stdout)
+    assert len(res) == nproc, r.stdout[-2000:]
+    for v in res.values():
+        assert v["stale"] and v["kinds"] == [False, True] and v["nb"] >= 3, v
+        assert v["diff"] <= 1e-5 * max(1.0, v["ref"]), v
+        assert v["cdiff"] == 0.0 and v["mdiff"] <= 1e-6 and v["iters"] == 3, v
 
 
 def test_parameter_server_coordinator_flow():
