@@ -517,10 +517,16 @@ PTG_DEV s16x4_t tr_read(const bf16_t* p) {
 // tiles; the next tile's halo rows (RING: only the TH new ones) and dZ tile are prefetched into
 // registers during this tile's MFMAs.  Partial sums stay in registers for the whole range and are
 // flushed with one fp32 atomic per output.
-template <int C, int KS, int TW, int TH, int MF, int NB, bool RING>
+//
+// SPARSE: dZ comes as the sparse pool record of its prelu+pool backward (dzsel [N][H/2][W/2][Cout]
+// = dZ at each window's argmax, argq = the argmax position q = 2*dh + dw; dZ is zero elsewhere in
+// the window): each thread loads 4 channels of one pooled pixel (8 + 4 bytes instead of the 32
+// bytes of the dense 2x2 window) and expands them into the same dense LDS dZ tile.
+template <int C, int KS, int TW, int TH, int MF, int NB, bool RING, bool SPARSE = false>
 __global__ __launch_bounds__(256) void conv_wgrad_strip_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dz,
                                                           float* __restrict__ dw, int N, int H, int W, int Cout, int pad,
-                                                          int tiles_h, int tiles_w, int nslices) {
+                                                          int tiles_h, int tiles_w, int nslices,
+                                                          const uint8_t* __restrict__ argq = nullptr) {
   using VT = typename HVec<C>::T;
   constexpr int VPP = HVec<C>::per_pix, VE = C == 4 ? 4 : 8;
   constexpr int PIX = PixPitch<C>::v;
@@ -535,8 +541,9 @@ __global__ __launch_bounds__(256) void conv_wgrad_strip_k(const bf16_t* __restri
   constexpr int HALO_ELEMS = NROWS * ROWE;
   constexpr int DZ_ELEMS = M * DPITCH;
   constexpr int PFN = (HR * HC * VPP + 255) / 256;
-  constexpr int DV = M * MF * 4;          // 8-byte dZ vectors per tile (upper bound: Cout <= MF*16)
+  constexpr int DV = (SPARSE ? M / 4 : M) * MF * 4;  // 8-byte dZ vectors per tile (upper bound: Cout <= MF*16)
   constexpr int PFD = (DV + 255) / 256;
+  static_assert(!SPARSE || (TH % 2 == 0 && TW % 2 == 0), "sparse dZ needs whole 2x2 windows per tile");
   __shared__ __attribute__((aligned(16))) bf16_t smem[HALO_ELEMS + DZ_ELEMS + 8];
   bf16_t* const ds = smem + HALO_ELEMS;
 
@@ -576,7 +583,9 @@ __global__ __launch_bounds__(256) void conv_wgrad_strip_k(const bf16_t* __restri
   }
   VT pf[PFN];
   U2 pd[PFD];
+  uint32_t pq[SPARSE ? PFD : 1];
   const int CV = Cout / 4;
+  const int PH = H >> 1, PW = W >> 1;
   auto load_tile = [&](int s_, int th_, int nrows, int ih_first) {
     const int n = s_ / tiles_w, ow0 = (s_ - n * tiles_w) * TW, oh0 = th_ * TH;
     const bf16_t* img = x + (long)n * H * W * C;
@@ -592,10 +601,24 @@ __global__ __launch_bounds__(256) void conv_wgrad_strip_k(const bf16_t* __restri
     for (int k = 0; k < PFD; ++k) {
       const int v = tid + k * 256;
       U2 val = U2{0u, 0u};
-      if (v < M * CV) {
-        const int m = v / CV, cv = v - m * CV;
-        const int oh = oh0 + m / TW, ow = ow0 + m % TW;
-        if (oh < H && ow < W) val = *(const U2*)(dz + (((long)n * H + oh) * W + ow) * Cout + cv * 4);
+      if constexpr (SPARSE) {
+        uint32_t qv = 0;
+        if (v < (M / 4) * CV) {
+          const int m = v / CV, cv = v - m * CV;
+          const int ph = (oh0 >> 1) + m / (TW / 2), pw = (ow0 >> 1) + m % (TW / 2);
+          if (ph < PH && pw < PW) {
+            const long o = (((long)n * PH + ph) * PW + pw) * Cout + cv * 4;
+            val = *(const U2*)(dz + o);
+            qv = *(const uint32_t*)(argq + o);
+          }
+        }
+        pq[k] = qv;
+      } else {
+        if (v < M * CV) {
+          const int m = v / CV, cv = v - m * CV;
+          const int oh = oh0 + m / TW, ow = ow0 + m % TW;
+          if (oh < H && ow < W) val = *(const U2*)(dz + (((long)n * H + oh) * W + ow) * Cout + cv * 4);
+        }
       }
       pd[k] = val;
     }
@@ -614,7 +637,22 @@ __global__ __launch_bounds__(256) void conv_wgrad_strip_k(const bf16_t* __restri
 #pragma unroll
     for (int k = 0; k < PFD; ++k) {
       const int v = tid + k * 256;
-      if (v < M * CV) {
+      if constexpr (SPARSE) {
+        if (v < (M / 4) * CV) {
+          const int m = v / CV, cv = v - m * CV;
+          const int m00 = (2 * (m / (TW / 2))) * TW + 2 * (m % (TW / 2));
+          const uint32_t lo = pd[k].x, hi = pd[k].y, qv = pq[k];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            // keep channel c's bf16 where its argmax byte equals q
+            const uint32_t h0 = ((qv & 0xffu) == (uint32_t)q ? 0x0000ffffu : 0u) |
+                                (((qv >> 8) & 0xffu) == (uint32_t)q ? 0xffff0000u : 0u);
+            const uint32_t h1 = (((qv >> 16) & 0xffu) == (uint32_t)q ? 0x0000ffffu : 0u) |
+                                (((qv >> 24) & 0xffu) == (uint32_t)q ? 0xffff0000u : 0u);
+            *(U2*)(ds + (m00 + (q >> 1) * TW + (q & 1)) * DPITCH + cv * 4) = U2{lo & h0, hi & h1};
+          }
+        }
+      } else if (v < M * CV) {
         const int m = v / CV, cv = v - m * CV;
         *(U2*)(ds + m * DPITCH + cv * 4) = pd[k];
       }
@@ -701,10 +739,14 @@ __global__ __launch_bounds__(256) void conv_wgrad_strip_k(const bf16_t* __restri
 // the wave's other fragment (rows 2*rp, 2*rp+1).
 // Layout: 256x4-pixel... tiles of TW=64 x TH=4 pixels, mirrored ring of 2*HR halo rows walked
 // down a column strip, next rows prefetched into registers during the MFMAs (as conv_fwd_strip_k).
-template <int KS>
-__global__ __launch_bounds__(256) void conv1_pair_pool_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
+// SPARSE: the sparse pool record (EPI_POOLS) instead of the full-resolution z: `z` receives, per
+// pooled element, the z of the window's argmax ([N][H/2][W/2][8]) and `argout` its position
+// q = 2*dh + dw (first maximum in q order wins, as in the dense backward).
+template <int KS, bool SPARSE>
+__global__ __launch_bounds__(256, 5) void conv1_pair_pool_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
                                                          const float* __restrict__ bias, const float* __restrict__ alpha,
-                                                         bf16_t* __restrict__ z, bf16_t* __restrict__ pooled, int N, int H,
+                                                         bf16_t* __restrict__ z, bf16_t* __restrict__ pooled,
+                                                         uint8_t* __restrict__ argout, int N, int H,
                                                          int W, int pad, int tiles_h, int tiles_w) {
   constexpr int C = 4, TW = 64, TH = 4;
   constexpr int KWP = KS + 1;
@@ -824,29 +866,57 @@ __global__ __launch_bounds__(256) void conv1_pair_pool_k(const bf16_t* __restric
     __syncthreads();  // every wave is done reading the halo window
     if (has_next) store_rows(nrows2, slot2);
 
-    float y[2][4];
+    float y[2][4], zr[2][4];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int oh = oh0 + 2 * rp + i;
       const float a4[4] = {al[i].x, al[i].y, al[i].z, al[i].w};
-      float zr[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        zr[r] = bf2f(f2bf(acc[i][r] + bv[r]));
-        y[i][r] = zr[r] > 0.f ? zr[r] : a4[r] * zr[r];
+        zr[i][r] = bf2f(f2bf(acc[i][r] + bv[r]));
+        y[i][r] = zr[i][r] > 0.f ? zr[i][r] : a4[r] * zr[i][r];
       }
-      if (oh < H && ow < W)
-        *(U2*)(z + (((long)n * H + oh) * W + ow) * 8 + cc) = U2{pack_bf(zr[0], zr[1]), pack_bf(zr[2], zr[3])};
-    }
-    float pm[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float v = fmaxf(y[0][r], y[1][r]);
-      pm[r] = fmaxf(v, __shfl_xor(v, 32, 64));
+      if (!SPARSE && oh < H && ow < W)
+        *(U2*)(z + (((long)n * H + oh) * W + ow) * 8 + cc) =
+            U2{pack_bf(zr[i][0], zr[i][1]), pack_bf(zr[i][2], zr[i][3])};
     }
     const int ph = (oh0 >> 1) + rp, pw = (ow0 >> 1) + hf * 16 + px;
-    if (g < 2 && ph < PH && pw < PW)
-      *(U2*)(pooled + (((long)n * PH + ph) * PW + pw) * 8 + cc) = U2{pack_bf(pm[0], pm[1]), pack_bf(pm[2], pm[3])};
+    float pm[4];
+    if constexpr (SPARSE) {
+      // window (dh, dw): this lane holds dw = g >> 1 for dh = 0, 1; the partner lane ^ 32 the other dw
+      float zs[4];
+      uint32_t qs = 0;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float py0 = __shfl_xor(y[0][r], 32, 64), py1 = __shfl_xor(y[1][r], 32, 64);
+        const float pz0 = __shfl_xor(zr[0][r], 32, 64), pz1 = __shfl_xor(zr[1][r], 32, 64);
+        const bool odd = g >= 2;
+        const float yq[4] = {odd ? py0 : y[0][r], odd ? y[0][r] : py0, odd ? py1 : y[1][r], odd ? y[1][r] : py1};
+        const float zq[4] = {odd ? pz0 : zr[0][r], odd ? zr[0][r] : pz0, odd ? pz1 : zr[1][r], odd ? zr[1][r] : pz1};
+        float b = yq[0], bz = zq[0];
+        uint32_t a = 0;
+#pragma unroll
+        for (int q = 1; q < 4; ++q)
+          if (yq[q] > b) { b = yq[q]; bz = zq[q]; a = q; }
+        pm[r] = b;
+        zs[r] = bz;
+        qs |= a << (8 * r);
+      }
+      if (g < 2 && ph < PH && pw < PW) {
+        const long po = (((long)n * PH + ph) * PW + pw) * 8 + cc;
+        *(U2*)(pooled + po) = U2{pack_bf(pm[0], pm[1]), pack_bf(pm[2], pm[3])};
+        *(U2*)(z + po) = U2{pack_bf(zs[0], zs[1]), pack_bf(zs[2], zs[3])};
+        *(uint32_t*)(argout + po) = qs;
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = fmaxf(y[0][r], y[1][r]);
+        pm[r] = fmaxf(v, __shfl_xor(v, 32, 64));
+      }
+      if (g < 2 && ph < PH && pw < PW)
+        *(U2*)(pooled + (((long)n * PH + ph) * PW + pw) * 8 + cc) = U2{pack_bf(pm[0], pm[1]), pack_bf(pm[2], pm[3])};
+    }
     if (!has_next) break;
     __syncthreads();  // next tile's halo rows visible
     s = s2;
@@ -985,12 +1055,13 @@ static int fwd_by_cin(const void* x, const void* w, const float* bias, const flo
   }
 }
 
-template <int C, int KS, int TW, int TH, int MF>
-static int launch_wgrad(const void* x, const void* dz, float* dw, int N, int H, int W, int Cout, int pad, hipStream_t s) {
+template <int C, int KS, int TW, int TH, int MF, bool SPARSE = false>
+static int launch_wgrad(const void* x, const void* dz, float* dw, int N, int H, int W, int Cout, int pad, hipStream_t s,
+                        const void* argq = nullptr) {
   constexpr bool RING = TH < 2 * (KS - 1);
   constexpr int KF = KS * KS * C;
   constexpr int NB = KF > 512 ? 4 : 2;
-  const auto kern = conv_wgrad_strip_k<C, KS, TW, TH, MF, NB, RING>;
+  const auto kern = conv_wgrad_strip_k<C, KS, TW, TH, MF, NB, RING, SPARSE>;
   static const int resident = resident_blocks((const void*)kern);
   const int th = (H + TH - 1) / TH, tw = (W + TW - 1) / TW;
   const long tiles = (long)N * tw * th;
@@ -998,28 +1069,29 @@ static int launch_wgrad(const void* x, const void* dz, float* dw, int N, int H, 
   int chunks = (resident + nslices - 1) / nslices;
   if (chunks > tiles) chunks = (int)tiles;
   hipLaunchKernelGGL(kern, dim3(chunks * nslices), dim3(256), 0, s, (const bf16_t*)x, (const bf16_t*)dz, dw, N, H, W,
-                     Cout, pad, th, tw, nslices);
+                     Cout, pad, th, tw, nslices, (const uint8_t*)argq);
   PTG_RETURN_LAUNCH();
 }
 
-template <int C, int KS, int MF>
-static int wgrad_by_c(const void* x, const void* dz, float* dw, int N, int H, int W, int Cout, int pad, hipStream_t s) {
-  if constexpr (C == 4) return launch_wgrad<C, KS, 64, 4, MF>(x, dz, dw, N, H, W, Cout, pad, s);
-  else if constexpr (C == 8) return launch_wgrad<C, KS, 32, 8, MF>(x, dz, dw, N, H, W, Cout, pad, s);
-  else if constexpr (C == 16) return launch_wgrad<C, KS, 16, 8, MF>(x, dz, dw, N, H, W, Cout, pad, s);
-  else if constexpr (C == 32) return launch_wgrad<C, KS, 8, 8, MF>(x, dz, dw, N, H, W, Cout, pad, s);
-  else return launch_wgrad<C, KS, 4, 16, MF>(x, dz, dw, N, H, W, Cout, pad, s);
+template <int C, int KS, int MF, bool SPARSE>
+static int wgrad_by_c(const void* x, const void* dz, float* dw, int N, int H, int W, int Cout, int pad, hipStream_t s,
+                      const void* argq) {
+  if constexpr (C == 4) return launch_wgrad<C, KS, 64, 4, MF, SPARSE>(x, dz, dw, N, H, W, Cout, pad, s, argq);
+  else if constexpr (C == 8) return launch_wgrad<C, KS, 32, 8, MF, SPARSE>(x, dz, dw, N, H, W, Cout, pad, s, argq);
+  else if constexpr (C == 16) return launch_wgrad<C, KS, 16, 8, MF, SPARSE>(x, dz, dw, N, H, W, Cout, pad, s, argq);
+  else if constexpr (C == 32) return launch_wgrad<C, KS, 8, 8, MF, SPARSE>(x, dz, dw, N, H, W, Cout, pad, s, argq);
+  else return launch_wgrad<C, KS, 4, 16, MF, SPARSE>(x, dz, dw, N, H, W, Cout, pad, s, argq);
 }
 
-template <int KS, int MF>
+template <int KS, int MF, bool SPARSE = false>
 static int wgrad_by_cin(const void* x, const void* dz, float* dw, int N, int H, int W, int C, int Cout, int pad,
-                        hipStream_t s) {
+                        hipStream_t s, const void* argq = nullptr) {
   switch (C) {
-    case 4: return wgrad_by_c<4, KS, MF>(x, dz, dw, N, H, W, Cout, pad, s);
-    case 8: return wgrad_by_c<8, KS, MF>(x, dz, dw, N, H, W, Cout, pad, s);
-    case 16: return wgrad_by_c<16, KS, MF>(x, dz, dw, N, H, W, Cout, pad, s);
-    case 32: return wgrad_by_c<32, KS, MF>(x, dz, dw, N, H, W, Cout, pad, s);
-    case 64: return wgrad_by_c<64, KS, MF>(x, dz, dw, N, H, W, Cout, pad, s);
+    case 4: return wgrad_by_c<4, KS, MF, SPARSE>(x, dz, dw, N, H, W, Cout, pad, s, argq);
+    case 8: return wgrad_by_c<8, KS, MF, SPARSE>(x, dz, dw, N, H, W, Cout, pad, s, argq);
+    case 16: return wgrad_by_c<16, KS, MF, SPARSE>(x, dz, dw, N, H, W, Cout, pad, s, argq);
+    case 32: return wgrad_by_c<32, KS, MF, SPARSE>(x, dz, dw, N, H, W, Cout, pad, s, argq);
+    case 64: return wgrad_by_c<64, KS, MF, SPARSE>(x, dz, dw, N, H, W, Cout, pad, s, argq);
     default: return (int)hipErrorInvalidValue;
   }
 }
@@ -1037,14 +1109,16 @@ int ptg_conv2d_fwd_halo(const void* x, const void* w, const float* bias, const f
                         int H, int W, int C, int Cout, int KS, int pad, int epi, hipStream_t s) {
   if (Cout % 8 || Cout > 64) return (int)hipErrorInvalidValue;
   if ((epi == EPI_POOL || epi == EPI_POOLS) && ((H & 1) || (W & 1))) return (int)hipErrorInvalidValue;
-  if (C == 4 && Cout == 8 && KS == 5 && epi == EPI_POOL && pad == 2 && conv1_pair_enabled()) {
-    const auto kern = conv1_pair_pool_k<5>;
-    static const int resident = resident_blocks((const void*)kern);
+  if (C == 4 && Cout == 8 && KS == 5 && (epi == EPI_POOL || epi == EPI_POOLS) && pad == 2 && conv1_pair_enabled()) {
+    const auto kern = epi == EPI_POOLS ? conv1_pair_pool_k<5, true> : conv1_pair_pool_k<5, false>;
+    static const int res_dense = resident_blocks((const void*)conv1_pair_pool_k<5, false>);
+    static const int res_sparse = resident_blocks((const void*)conv1_pair_pool_k<5, true>);
+    const int resident = epi == EPI_POOLS ? res_sparse : res_dense;
     const int th = (H + 3) / 4, tw = (W + 63) / 64;
     const long tiles = (long)N * th * tw;
     const int grid = (int)std::min<long>(tiles, resident);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, (const bf16_t*)x, (const bf16_t*)w, bias, alpha, (bf16_t*)z,
-                       (bf16_t*)aux, N, H, W, pad, th, tw);
+                       (bf16_t*)aux, (uint8_t*)arg, N, H, W, pad, th, tw);
     PTG_RETURN_LAUNCH();
   }
   if (KS == 5) return fwd_by_cin<5>(x, w, bias, alpha, z, aux, arg, N, H, W, C, Cout, pad, epi, s);
@@ -1062,6 +1136,17 @@ int ptg_conv2d_wgrad_halo(const void* x, const void* dz, float* dw, int N, int H
   if (KS == 3) { if (MF == 1) PTG_WG(3, 1); if (MF == 2) PTG_WG(3, 2); PTG_WG(3, 4); }
 #undef PTG_WG
   return (int)hipErrorInvalidValue;
+}
+
+// Weight gradient from the sparse pool record of dZ: dzsel / argq are [N][H/2][W/2][Cout] (H, W even);
+// only the 5x5 layers of the reference CNN (first layer: no dgrad needs a dense dZ) are instantiated.
+int ptg_conv2d_wgrad_halo_sparse(const void* x, const void* dzsel, const void* argq, float* dw, int N, int H, int W,
+                                 int C, int Cout, int KS, int pad, hipStream_t s) {
+  if (Cout % 8 || Cout > 64 || KS != 5 || (H & 1) || (W & 1)) return (int)hipErrorInvalidValue;
+  const int MF = Cout <= 16 ? 1 : (Cout <= 32 ? 2 : 4);
+  if (MF == 1) return wgrad_by_cin<5, 1, true>(x, dzsel, dw, N, H, W, C, Cout, pad, s, argq);
+  if (MF == 2) return wgrad_by_cin<5, 2, true>(x, dzsel, dw, N, H, W, C, Cout, pad, s, argq);
+  return wgrad_by_cin<5, 4, true>(x, dzsel, dw, N, H, W, C, Cout, pad, s, argq);
 }
 
 int ptg_conv_flip_weights(const void* w, void* wf, int Cout, int KS, int Cin, hipStream_t s) {

@@ -413,6 +413,114 @@ __global__ __launch_bounds__(256) void prelu_pool_bwd_sparse_k(const bf16_t* __r
   bias_reduce_atomic(db, c8, C8, sred, dbias);
 }
 
+// Sparse in, sparse out (the first conv layer, whose dZ only feeds the sparse-dZ weight gradient):
+// from the forward's record (zsel = z at each window's argmax, arg = its position q) it writes
+// dzsel = d(prelu)/dz at the argmax, i.e. dZ's only non-zero of the window, in the pooled layout.
+// Sample-parallel like prelu_pool_bwd_sg_k (16 pooled positions x 16 sample groups per block,
+// dalpha reduced over the sample groups in LDS); per pooled element of 8 channels it moves
+// dp + zsel + arg + dzsel = 56 bytes instead of the dense backward's 144.
+__global__ __launch_bounds__(256) void prelu_pool_bwd_sel_k(const bf16_t* __restrict__ dp,
+                                                            const bf16_t* __restrict__ zs,
+                                                            const uint8_t* __restrict__ arg,
+                                                            const float* __restrict__ alpha,
+                                                            bf16_t* __restrict__ dzs, float* __restrict__ dalpha,
+                                                            float* __restrict__ dbias, int N, int H, int W,
+                                                            int C, int nper) {
+  constexpr int PB = 16, SG = 16, RP = 33;
+  __shared__ float sda[SG * PB * RP];
+  __shared__ float sdb[256];
+  const int PH = H >> 1, PW = W >> 1, C8 = C >> 3;
+  const int npos = PH * PW * C8;
+  const int pl = threadIdx.x & (PB - 1), sg = threadIdx.x / PB;
+  const int i = blockIdx.x * PB + pl;
+  const int n0 = blockIdx.y * nper, n1 = min(N, n0 + nper);
+  const bool active = i < npos;
+  const int c8 = active ? i % C8 : 0;
+  const int t = active ? i / C8 : 0;
+  const int pw = t % PW, ph = t / PW;
+  long zoff[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) zoff[q] = ((long)(2 * ph + (q >> 1)) * W + 2 * pw + (q & 1)) * C + c8 * 8;
+  const long PHWC = (long)PH * PW * C;
+  const long poff = ((long)ph * PW + pw) * C + c8 * 8;
+  float da[4][8], db[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) db[j] = 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) da[q][j] = 0.f;
+  if ((int)threadIdx.x < C) sdb[threadIdx.x] = 0.f;
+  if (active) {
+    float av[4][8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 a0 = *(const float4*)(alpha + zoff[q]), a1 = *(const float4*)(alpha + zoff[q] + 4);
+      av[q][0] = a0.x; av[q][1] = a0.y; av[q][2] = a0.z; av[q][3] = a0.w;
+      av[q][4] = a1.x; av[q][5] = a1.y; av[q][6] = a1.z; av[q][7] = a1.w;
+    }
+    constexpr int U = 4;  // samples in flight per thread: 12 independent loads
+    for (int n = n0 + sg; n < n1; n += U * SG) {
+      U4 graw[U], zraw[U];
+      U2 araw[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int nn = n + u * SG < n1 ? n + u * SG : n;
+        const long o = (long)nn * PHWC + poff;
+        graw[u] = *(const U4*)(dp + o);
+        zraw[u] = *(const U4*)(zs + o);
+        araw[u] = *(const U2*)(arg + o);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (n + u * SG >= n1) break;
+        float g[8], zv[8], o[8];
+        unpack8(graw[u], g);
+        unpack8(zraw[u], zv);
+        const uint32_t aw[2] = {araw[u].x, araw[u].y};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int q = (aw[j >> 2] >> (8 * (j & 3))) & 3;
+          const float a = q == 0 ? av[0][j] : q == 1 ? av[1][j] : q == 2 ? av[2][j] : av[3][j];
+          const bool pos = zv[j] > 0.f;
+          o[j] = pos ? g[j] : g[j] * a;
+          const float d = pos ? 0.f : g[j] * zv[j];
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) da[qq][j] += q == qq ? d : 0.f;
+          db[j] += o[j];
+        }
+        *(U4*)(dzs + (long)(n + u * SG) * PHWC + poff) = pack8(o);
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sda[(sg * PB + pl) * RP + q * 8 + j] = da[q][j];
+  __syncthreads();
+  if (active) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) atomicAdd(&sdb[c8 * 8 + j], db[j]);
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int o = h * 256 + threadIdx.x;
+    const int p = o >> 5, k = o & 31, q = k >> 3, j = k & 7;
+    float sum = 0.f;
+#pragma unroll
+    for (int gsg = 0; gsg < SG; ++gsg) sum += sda[(gsg * PB + p) * RP + k];
+    const int ii = blockIdx.x * PB + p;
+    if (ii < npos) {
+      const int cc = ii % C8, tq = ii / C8, pww = tq % PW, phh = tq / PW;
+      float* dst = dalpha + ((long)(2 * phh + (q >> 1)) * W + 2 * pww + (q & 1)) * C + cc * 8 + j;
+      if (gridDim.y == 1) *dst += sum;
+      else atomicAdd(dst, sum);
+    }
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < C) atomicAdd(dbias + threadIdx.x, sdb[threadIdx.x]);
+}
+
 // Plain PReLU forward (no pool): a = z>0 ? z : alpha[hwc]*z ; HWC = per-sample element count.
 __global__ __launch_bounds__(256) void prelu_fwd_k(const bf16_t* __restrict__ z,
                                                    const float* __restrict__ alpha,
@@ -873,6 +981,23 @@ int ptg_prelu_pool_bwd_sparse(const void* dp, const void* zs, const void* arg, c
   dim3 grid((npos + 255) / 256, (N + nper - 1) / nper);
   hipLaunchKernelGGL(prelu_pool_bwd_sparse_k, grid, dim3(256), 0, s, (const bf16_t*)dp, (const bf16_t*)zs,
                      (const uint8_t*)arg, alpha, (bf16_t*)dz, dalpha, dbias, N, H, W, C, nper);
+  PTG_RETURN_LAUNCH();
+}
+
+int ptg_prelu_pool_bwd_sel(const void* dp, const void* zs, const void* arg, const float* alpha, void* dzs,
+                           float* dalpha, float* dbias, int N, int H, int W, int C, int nper, hipStream_t s) {
+  if (C % 8 || C > 256 || (H & 1) || (W & 1) || H < 2 || W < 2) return (int)hipErrorInvalidValue;
+  const int npos = (H / 2) * (W / 2) * (C / 8);
+  const int bx = (npos + 15) / 16;
+  if (nper <= 0) {  // as prelu_pool_bwd_sg_k: >= ~1024 blocks, >= 64 samples per chunk (4 chunks of
+    //                 64 samples for the first layer were slower: 173 vs 134 us, dalpha atomics)
+    int chunks = (1024 + bx - 1) / bx;
+    chunks = std::max(1, std::min(chunks, N / 64));
+    nper = (N + chunks - 1) / chunks;
+  }
+  dim3 grid(bx, (N + nper - 1) / nper);
+  hipLaunchKernelGGL(prelu_pool_bwd_sel_k, grid, dim3(256), 0, s, (const bf16_t*)dp, (const bf16_t*)zs,
+                     (const uint8_t*)arg, alpha, (bf16_t*)dzs, dalpha, dbias, N, H, W, C, nper);
   PTG_RETURN_LAUNCH();
 }
 

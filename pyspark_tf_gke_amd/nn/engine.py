@@ -34,6 +34,11 @@ _HOST_FP32 = [os.environ.get("PTG_HOST_FP32") == "1"]
 # makes the latency-bound layer-1/2 forward kernels slower than the backward saves (98.1k vs 99.2k
 # samples/s measured), so the dense record stays the default.
 SPARSE_POOL = os.environ.get("PTG_SPARSE_POOL", "0") == "1"
+# The FIRST conv layer (no data gradient) keeps its whole backward sparse: forward writes the record,
+# prelu_pool_bwd_sel turns it into dZ's record (dZ at the argmax) and the weight gradient expands it in
+# LDS, so the full-resolution z and dZ (335 MB each for CNN-B1 at batch 256) never exist.  Measured
+# on CNN-B1 b256: 118.6k vs 116.6k samples/s with the dense first-layer record.
+SPARSE_FIRST = os.environ.get("PTG_SPARSE_FIRST", "1") == "1"
 
 
 def host_fp32(enabled: bool | None = None) -> bool:
@@ -139,7 +144,9 @@ class ConvOp(Op):
         b = self.conv.bias.data if self.conv.bias is not None else None
         self._sparse = False
         halo_ok = self._halo()[0] and not (self.pool is not None and (OH % 2 or OW % 2))
-        if halo_ok and self.pool is not None and x.is_cuda and SPARSE_POOL:
+        self._sel = halo_ok and self.pool is not None and x.is_cuda and self.first and SPARSE_FIRST \
+            and self.conv.kernel_size[0] == 5
+        if halo_ok and self.pool is not None and x.is_cuda and (SPARSE_POOL or self._sel):
             # sparse pool record: pooled output + z at the argmax + argmax position (no full z)
             self._x, self._sparse = x, True
             return self._forward_pool_sparse(x, b, ws, B, OH, OW, Co, dev)
@@ -178,6 +185,18 @@ class ConvOp(Op):
         self._zs, self._arg, self._zshape = zs, arg, (B, OH, OW, Co)
         return p
 
+    def _backward_sel(self, x, dy, ws, dev):
+        """First layer: sparse record -> dZ record -> weight gradient (no dense z / dZ, no dgrad)."""
+        C = self._zshape[-1]
+        bias_g = self.conv.bias.grad if self.conv.bias is not None else \
+            ws.get(self.name + "/nobias", (C,), torch.float32, dev)
+        dalpha = self.prelu.alpha.grad if self.prelu is not None else \
+            ws.get(self.name + "/dalpha_dummy", self._zshape[1:], torch.float32, dev)
+        dzs = ws.get(self.name + "/dzsel", self._zs.shape, torch.bfloat16, dev)
+        K.prelu_pool_bwd_sel(dy, self._zs, self._arg, self._pool_alpha(ws, dev), dzs, dalpha, bias_g)
+        K.conv2d_wgrad_halo_sparse(x, dzs, self._arg, self.pad, self.conv.kernel.grad, zeroed=True)
+        return None
+
     def _forward_halo(self, x, z, b, ws, B, OH, OW, Co, dev):
         """One kernel: conv + bias, and the PReLU/ReLU (+ 2x2 max-pool) epilogue fused in."""
         w = self.conv.kernel.bf16
@@ -201,6 +220,8 @@ class ConvOp(Op):
         x = self._x
         dev = x.device
         dy = _bf16(dy, ws, self.name + "/dy16")
+        if getattr(self, "_sel", False):
+            return self._backward_sel(x, dy, ws, dev)
         zshape = self._zshape if self._sparse else self._z.shape
         dz = ws.get(self.name + "/dz", zshape, torch.bfloat16, dev)
         bias_g = self.conv.bias.grad if self.conv.bias is not None else \

@@ -161,6 +161,23 @@ def conv2d_wgrad_halo(x, dz, pad: int, out, zeroed: bool = False):
     return out
 
 
+def conv2d_wgrad_halo_sparse(x, dzsel, arg, pad: int, out, zeroed: bool = False):
+    """out[Cout,KS,KS,C] (fp32) = d(conv)/dw with dZ given as its sparse pool record (dzsel / arg of
+    shape [N,H/2,W/2,Cout]: dZ at each 2x2 window's argmax, zero elsewhere)."""
+    N, H, W, C = x.shape
+    Cout, KS, _, _ = out.shape
+    if not on_device(x):
+        dz = ref.expand_pool_record(dzsel, arg, (N, H, W, Cout)).to(dzsel.dtype)
+        return ref.conv2d_wgrad(x, dz, 1, pad, out, zeroed)
+    assert tuple(dzsel.shape) == (N, H // 2, W // 2, Cout) and tuple(arg.shape) == tuple(dzsel.shape)
+    need(x, torch.bfloat16, "wgrad_sparse.x"); need(dzsel, torch.bfloat16, "wgrad_sparse.dzsel")
+    need(arg, torch.uint8, "wgrad_sparse.arg"); need(out, torch.float32, "wgrad_sparse.out")
+    if not zeroed:
+        out.zero_()
+    hip("ptg_conv2d_wgrad_halo_sparse", ptr(x), ptr(dzsel), ptr(arg), ptr(out), N, H, W, C, Cout, KS, pad)
+    return out
+
+
 def conv_flip_weights(w, out):
     """out[Cin][KS][KS][Cout] = w[Cout][KS-1-kh][KS-1-kw][Cin] (dgrad filter)."""
     Cout, KS, _, Cin = w.shape
@@ -306,6 +323,22 @@ def prelu_pool_bwd_sparse(dp, zsel, arg, alpha, dz_out, dalpha, dbias, nper: int
     hip("ptg_prelu_pool_bwd_sparse", ptr(dp), ptr(zsel), ptr(arg), ptr(alpha), ptr(dz_out), ptr(dalpha), ptr(dbias),
         N, H, W, C, nper)
     return dz_out
+
+
+def prelu_pool_bwd_sel(dp, zsel, arg, alpha, dzsel_out, dalpha, dbias, nper: int = 0):
+    """Sparse-in / sparse-out backward of maxpool2x2(prelu(z)): from the forward record (zsel, arg)
+    write dzsel = dZ at each window's argmax ([N,H/2,W/2,C]); dalpha, dbias accumulate."""
+    if not on_device(dp):
+        return ref.prelu_pool_bwd_sel(dp, zsel, arg, alpha, dzsel_out, dalpha, dbias)
+    N, PH, PW, C = dzsel_out.shape
+    for t, nm in ((dp, "dp"), (zsel, "zsel"), (dzsel_out, "dzsel")):
+        need(t, torch.bfloat16, "prelu_pool_bwd_sel." + nm)
+        assert tuple(t.shape) == (N, PH, PW, C), (nm, t.shape)
+    need(arg, torch.uint8, "prelu_pool_bwd_sel.arg")
+    assert tuple(alpha.shape) == (2 * PH, 2 * PW, C) and tuple(dalpha.shape) == tuple(alpha.shape)
+    hip("ptg_prelu_pool_bwd_sel", ptr(dp), ptr(zsel), ptr(arg), ptr(alpha), ptr(dzsel_out), ptr(dalpha), ptr(dbias),
+        N, 2 * PH, 2 * PW, C, nper)
+    return dzsel_out
 
 
 def prelu_fwd(z, alpha, out):

@@ -170,6 +170,31 @@ def prelu_pool_bwd_sparse(dp, zsel, arg, alpha, dz_out, dalpha, dbias):
     return dz_out
 
 
+def expand_pool_record(vsel, arg, out_shape):
+    """Dense [N,H,W,C] tensor holding vsel[n,ph,pw,c] at window position arg (q = 2*dh + dw) and
+    zero elsewhere in each 2x2 window (the sparse pool record's dense form)."""
+    N, H, W, C = out_shape
+    hit = torch.nn.functional.one_hot(arg.long(), 4).permute(0, 1, 2, 4, 3)  # [N,PH,PW,4,C]
+    vw = _f(vsel).unsqueeze(3) * hit.float()
+    return vw.reshape(N, H // 2, W // 2, 2, 2, C).permute(0, 1, 3, 2, 4, 5).reshape(N, H, W, C)
+
+
+def prelu_pool_bwd_sel(dp, zsel, arg, alpha, dzsel_out, dalpha, dbias):
+    """Sparse-in / sparse-out backward of maxpool2x2(prelu(z)): dzsel = dZ at each window's argmax."""
+    N, PH, PW, C = dzsel_out.shape
+    H, W = 2 * PH, 2 * PW
+    g, zs, q = _f(dp), _f(zsel), arg.long()
+    aw = _windows(_f(alpha).unsqueeze(0).expand(N, H, W, C))  # [N,PH,PW,4,C]
+    a = torch.gather(aw, 3, q.unsqueeze(3)).squeeze(3)
+    pos = zs > 0
+    o = torch.where(pos, g, g * a)
+    dzsel_out.copy_(o.to(dzsel_out.dtype))
+    d = torch.where(pos, torch.zeros_like(g), g * zs)
+    dalpha.add_(expand_pool_record(d, arg, (N, H, W, C)).sum(0))
+    dbias.add_(o.reshape(-1, C).sum(0))
+    return dzsel_out
+
+
 def prelu_fwd(z, alpha, out):
     out.copy_(_prelu(_f(z), _f(alpha)).to(out.dtype))
     return out

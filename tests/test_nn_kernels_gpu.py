@@ -204,6 +204,69 @@ def test_prelu_pool_bwd_sparse(C, N, H, W, nper):
     _close(db, dbr, 1e-2, 1e-2, "sparse_dbias")
 
 
+@pytest.mark.parametrize("C,N,H,W,nper", [(8, 3, 8, 12, 0), (16, 5, 16, 20, 2), (64, 3, 8, 12, 0), (8, 130, 6, 10, 0),
+                                          (32, 9, 6, 6, 4)])
+def test_prelu_pool_bwd_sel(C, N, H, W, nper):
+    """Sparse record in, dZ record out (first conv layer): dzsel, dalpha, dbias vs the fp32 reference,
+    and dzsel expanded == the dense sparse-record backward's dZ."""
+    z = rnd(N, H, W, C)
+    alpha = torch.randn(H, W, C) * 0.3
+    shp = (N, H // 2, W // 2, C)
+    pr, zs, arg = torch.empty(shp), torch.empty(shp, dtype=torch.bfloat16), torch.empty(shp, dtype=torch.uint8)
+    R.prelu_pool_fwd_sparse(z, alpha, pr, zs, arg)
+    dp = rnd(*shp)
+    dzs = torch.empty(shp, device=DEV, dtype=torch.bfloat16)
+    da, db = torch.zeros(H, W, C, device=DEV), torch.zeros(C, device=DEV)
+    K.prelu_pool_bwd_sel(dp.to(DEV), zs.to(DEV), arg.to(DEV), alpha.to(DEV), dzs, da, db, nper)
+    dzr = torch.empty(N, H, W, C, dtype=torch.bfloat16)
+    dar, dbr = torch.zeros(H, W, C), torch.zeros(C)
+    R.prelu_pool_bwd_sparse(dp, zs, arg, alpha, dzr, dar, dbr)
+    _close(R.expand_pool_record(dzs.cpu(), arg, (N, H, W, C)), dzr, 1e-2, 1e-2, "sel_dz")
+    _close(da, dar, 1e-2, 1e-2, "sel_dalpha")
+    _close(db, dbr, 1e-2, 1e-2, "sel_dbias")
+
+
+@pytest.mark.parametrize("N,H,W,C,Co", [(2, 16, 20, 4, 8), (3, 18, 70, 4, 8), (16, 256, 320, 4, 8),
+                                        (2, 18, 22, 8, 16), (4, 12, 10, 16, 32), (3, 8, 10, 32, 64)])
+def test_conv_halo_wgrad_sparse(N, H, W, C, Co):
+    """Weight gradient from dZ's sparse pool record == the dense weight gradient of the expanded dZ."""
+    x = rnd(N, H, W, C)
+    shp = (N, H // 2, W // 2, Co)
+    dzs = rnd(*shp, scale=0.1)
+    arg = torch.randint(0, 4, shp, dtype=torch.uint8)
+    out = torch.full((Co, 5, 5, C), 7.0, device=DEV)
+    K.conv2d_wgrad_halo_sparse(x.to(DEV), dzs.to(DEV), arg.to(DEV), 2, out)
+    dz = R.expand_pool_record(dzs, arg, (N, H, W, Co)).to(torch.bfloat16)
+    ref = torch.empty(Co, 5, 5, C)
+    R.conv2d_wgrad(x, dz, 1, 2, ref)
+    _close(out, ref, 1e-3, 1e-3, "wgrad_sparse")
+
+
+def test_first_layer_sparse_chain_matches_dense(monkeypatch):
+    """CNN first layer end to end: sparse forward record + sel backward + sparse wgrad give the same
+    pooled output and gradients (weights, bias, alpha) as the dense path."""
+    from pyspark_tf_gke_amd.models import build_cnn_model
+    from pyspark_tf_gke_amd.nn import engine as E
+
+    torch.manual_seed(3)
+    x = torch.rand(4, 64, 80, 3)
+    y = torch.rand(4, 2) * 50
+    grads = {}
+    for mode in (False, True):
+        monkeypatch.setattr(E, "SPARSE_FIRST", mode)
+        m = build_cnn_model((64, 80, 3), flat=True, summary=False, device=DEV)
+        xb, yb = m._prep_batch(x, y)
+        m.store.zero_grad()
+        out = m._run_forward(xb, True)
+        d = m._loss_grad(out, yb, m._stats_buf())
+        m._run_backward(d)
+        torch.cuda.synchronize()
+        assert m.ops[0]._sel == mode
+        grads[mode] = {p.name: p.grad.detach().float().cpu().clone() for p in m.store.params}
+    for name, g in grads[False].items():
+        _close(grads[True][name], g, 2e-2, 1e-3, "sel_grad_" + name)
+
+
 @pytest.mark.parametrize("N,H,W,C,Co,KS", HALO_CASES + BIG_HALO)
 def test_conv_halo_wgrad(N, H, W, C, Co, KS):
     x, dz = rnd(N, H, W, C), rnd(N, H, W, Co, scale=0.1)
