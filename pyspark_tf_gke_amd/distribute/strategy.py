@@ -135,20 +135,38 @@ class _Bucket:
 class _ShardPlan:
     """Per-model state of the sharded data-parallel update (ZeRO-1 style).
 
-    The flat store is re-laid out as [weights read as bf16 in forward][everything else], each group
-    in backward-completion order and padded to ``world * 64`` elements, then cut into buckets of at
-    most ``bucket_elems``.  Rank r owns slice r of every bucket: it keeps the optimizer moments and
+    The flat store is re-laid out as [weights read as bf16 in forward][everything else], each part
+    in backward-completion order, grouped into buckets (closed at ``bucket_elems`` or after any
+    weight of >= ``BIG`` elements), every bucket padded to ``world * 64`` elements and split
+    further when larger than ``bucket_elems``.  Rank r owns slice r of every bucket: it keeps the optimizer moments and
     the fp32 master for that slice current, the rest of its fp32 copy of a bf16-group bucket goes
     stale between :meth:`MultiWorkerMirroredStrategy.synchronize_master` calls (``store.master_stale``)."""
+
+    BIG = 4 << 20  # elements
 
     def __init__(self, model, world, rank, bucket_elems):
         from ..nn.params import ALIGN
 
         st = model.store
-        ps = sorted(st.params, key=lambda p: p.offset)
-        g16 = [p for p in ps if p.fwd_bf16]
-        g32 = [p for p in ps if not p.fwd_bf16]
-        groups = [(g, fp32) for g, fp32 in ((g16, False), (g32, True)) if g]
+        ps = sorted(st.params, key=lambda p: p.offset)  # backward-completion order
+        groups = []
+        for fp32 in (False, True):
+            cur, size = [], 0
+            for p in ps:
+                if p.fwd_bf16 == fp32:
+                    continue
+                if cur and size >= bucket_elems:
+                    groups.append((cur, fp32))
+                    cur, size = [], 0
+                cur.append(p)
+                size += p.numel
+                if p.numel >= self.BIG:
+                    # a large weight closes its bucket: its reduce-scatter starts as soon as its own
+                    # gradient exists instead of waiting for the (later) gradients of the layers below
+                    groups.append((cur, fp32))
+                    cur, size = [], 0
+            if cur:
+                groups.append((cur, fp32))
         q = world * ALIGN
         ranges = st.relayout([g for g, _ in groups], q)
         self.buckets: list[_Bucket] = []
@@ -202,8 +220,7 @@ class MultiWorkerMirroredStrategy(Strategy):
 
     def register_model(self, model) -> None:
         if self.sharded_update:
-            # buckets of up to 4x the all-reduce bucket: a reduce-scatter moves half the bytes
-            model._shard_plan = _ShardPlan(model, self.world_size, self.rank, 4 * self.bucket_elems)
+            model._shard_plan = _ShardPlan(model, self.world_size, self.rank, self.bucket_elems)
         super().register_model(model)
 
     # ---- replicated update: bucketed all-reduce

@@ -40,13 +40,17 @@ def init(backend: str | None = None, device_type: str | None = None, timeout_s: 
     if device_type is None:
         device_type = "cuda" if torch.cuda.is_available() else "cpu"
     if backend is None:
-        backend = "nccl" if device_type == "cuda" else "gloo"
+        # PTG_DIST_BACKEND=gloo: host-staged collectives even for GPU tensors (lets several ranks share
+        # one GPU, e.g. a multi-rank rehearsal on a 1-GPU box; RCCL refuses duplicate devices)
+        backend = os.environ.get("PTG_DIST_BACKEND") or ("nccl" if device_type == "cuda" else "gloo")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29500")
     kw = {}
     if device_type == "cuda":
-        torch.cuda.set_device(local)
-        kw["device_id"] = torch.device("cuda", local)
+        dev = local % max(torch.cuda.device_count(), 1)
+        torch.cuda.set_device(dev)
+        if backend == "nccl":
+            kw["device_id"] = torch.device("cuda", dev)
     dist.init_process_group(backend=backend, rank=rank, world_size=world,
                             timeout=datetime.timedelta(seconds=timeout_s), **kw)
     from ..runtime import heartbeat
