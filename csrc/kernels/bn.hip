@@ -63,6 +63,28 @@ PTG_DEV void bn_flush(float (*red)[256][8], const float* s, const float* q, int 
   }
 }
 
+// Totals over the BN_G partial groups of channel c, read and re-zeroed (the buffer is reused).  Loads
+// first, 8 groups at a time: with the `p[c] = 0` stores interleaved the compiler serialised every
+// load behind the previous store (possible aliasing) - ~9 us per finalize launch.
+PTG_DEV void bn_part_sums(float* part, int C, int c, double& s, double& q) {
+  s = 0.0; q = 0.0;
+  for (int g = 0; g < BN_G; g += 8) {
+    float a[8], b[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const float* p = part + (long)(g + u) * 2 * C;
+      a[u] = p[c];
+      b[u] = p[C + c];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      float* p = part + (long)(g + u) * 2 * C;
+      s += a[u]; q += b[u];
+      p[c] = 0.f; p[C + c] = 0.f;
+    }
+  }
+}
+
 }  // namespace
 
 __global__ __launch_bounds__(256) void bn_stats_k(const bf16_t* __restrict__ z, long M, int C, int rpb,
@@ -109,11 +131,8 @@ __global__ __launch_bounds__(256) void bn_finalize_k(float* __restrict__ part, i
   if (c >= C) return;
   float mean, var;
   if (training) {
-    double s = 0.0, q = 0.0;
-    for (int g = 0; g < BN_G; ++g) {  // read and re-zero (the buffer is reused by the next pass)
-      float* p = part + (long)g * 2 * C;
-      s += p[c]; q += p[C + c]; p[c] = 0.f; p[C + c] = 0.f;
-    }
+    double s, q;
+    bn_part_sums(part, C, c, s, q);
     const double m = s / (double)M;
     double v = q / (double)M - m * m;
     mean = (float)m; var = (float)(v > 0.0 ? v : 0.0);
@@ -210,11 +229,8 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_k(float* __restrict__ par
                                                          float* __restrict__ coef) {
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= C) return;
-  double sg = 0.0, sgz = 0.0;
-  for (int g = 0; g < BN_G; ++g) {
-    float* p = part + (long)g * 2 * C;
-    sg += p[c]; sgz += p[C + c]; p[c] = 0.f; p[C + c] = 0.f;
-  }
+  double sg, sgz;
+  bn_part_sums(part, C, c, sg, sgz);
   const float m = mean[c], rs = rstd[c];
   const float db = (float)sg;
   const float dg = (float)((sgz - (double)m * sg) * rs);
