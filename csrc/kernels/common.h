@@ -76,4 +76,26 @@ PTG_DEV int xcd_remap(int bid, int nwg) {
 
 static inline int ptg_ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
 
+// Division by a runtime-invariant divisor without the ~30-instruction integer division sequence:
+// round-up multiply-high (Granlund-Montgomery / libdivide "branchfree" u32), exact for every 32-bit
+// dividend: q = (t + ((n - t) >> 1)) >> s with t = mulhi(n, m).  d == 1 is selected explicitly (its
+// magic would need 33 bits).  Built on the host with fastdiv(d).
+struct FastDiv {
+  uint32_t d, m, s;
+  __device__ __forceinline__ uint32_t div(uint32_t n) const {
+    const uint32_t t = __umulhi(n, m);
+    const uint32_t q = (t + ((n - t) >> 1)) >> s;
+    return d == 1u ? n : q;
+  }
+};
+static inline FastDiv fastdiv(uint32_t d) {
+  FastDiv f{d, 0u, 0u};
+  if (d <= 1) return f;
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;  // l = ceil(log2 d) >= 1
+  f.m = (uint32_t)(((((unsigned __int128)1) << 32) * ((1ull << l) - d)) / d + 1);
+  f.s = l - 1;
+  return f;
+}
+
 #define PTG_RETURN_LAUNCH() return (int)hipGetLastError()

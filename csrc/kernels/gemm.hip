@@ -67,17 +67,19 @@ template <int CVEC>
 struct ConvFwdA {
   static constexpr bool K_CONTIG = true;
   const bf16_t* x; int H, W, C, logC, OH, OW, KW, stride, pad, M, Kc;
+  FastDiv fKW, fOHW, fOW;  // set by init(): the per-load (kh, kw) and per-row pixel decodes without idiv
+  ConvFwdA& init() { fKW = fastdiv(KW); fOHW = fastdiv(OH * OW); fOW = fastdiv(OW); return *this; }
   struct Ctx { const bf16_t* img; int ih0, iw0; bool ok; };
   PTG_DEV Ctx ctx(int m) const {
     Ctx c; c.ok = m < M; if (!c.ok) m = 0;
     const int ohw = OH * OW;
-    const int n = m / ohw, rem = m - n * ohw, oh = rem / OW, ow = rem - oh * OW;
+    const int n = (int)fOHW.div(m), rem = m - n * ohw, oh = (int)fOW.div(rem), ow = rem - oh * OW;
     c.img = x + (long)n * H * W * C; c.ih0 = oh * stride - pad; c.iw0 = ow * stride - pad;
     return c;
   }
   PTG_DEV const bf16_t* at(const Ctx& c, int k, bool& ok) const {
     const int pos = k >> logC, ci = k & (C - 1);
-    const int kh = pos / KW, kw = pos - kh * KW;
+    const int kh = (int)fKW.div(pos), kw = pos - kh * KW;
     const int ih = c.ih0 + kh, iw = c.iw0 + kw;
     ok = (k < Kc) && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
     return c.img + ((long)ih * W + iw) * C + ci;
@@ -103,12 +105,14 @@ struct ConvFwdA {
 struct ConvDgradB {
   static constexpr bool K_CONTIG = false;
   const bf16_t* w; int Cin, Cout, logCout, KH, KW, Kc2;
+  FastDiv fKW;
+  ConvDgradB& init() { fKW = fastdiv(KW); return *this; }
   struct Ctx { int ci0; bool ok; };
   PTG_DEV Ctx ctx(int r0) const { Ctx c; c.ci0 = r0; c.ok = r0 < Cin; return c; }
   PTG_DEV U4 load(const Ctx& c, int k) const {
     if (!c.ok || k >= Kc2) return zero4();
     const int pos = k >> logCout, co = k & (Cout - 1);
-    const int kh = pos / KW, kw = pos - kh * KW;
+    const int kh = (int)fKW.div(pos), kw = pos - kh * KW;
     const long off = ((long)co * KH * KW + (KH - 1 - kh) * KW + (KW - 1 - kw)) * Cin + c.ci0;
     return *(const U4*)(w + off);
   }
@@ -119,19 +123,23 @@ template <int CVEC>
 struct ConvWgradB {
   static constexpr bool K_CONTIG = false;
   const bf16_t* x; int H, W, C, logC, OH, OW, KW, stride, pad, P, Kc;
+  FastDiv fKW, fOHW, fOW;  // the per-load pixel decode (k -> n, oh, ow) is the loader's hot path
+  ConvWgradB& init() { fKW = fastdiv(KW); fOHW = fastdiv(OH * OW); fOW = fastdiv(OW); return *this; }
   struct Ctx { int dh0, dw0, ci0, dh1, dw1, ci1; bool ok0, ok1; };
   PTG_DEV Ctx ctx(int r0) const {
     Ctx c;
     int pos = r0 >> logC; c.ci0 = r0 & (C - 1);
-    c.dh0 = pos / KW - pad; c.dw0 = pos % KW - pad; c.ok0 = r0 < Kc;
+    int q = (int)fKW.div(pos);
+    c.dh0 = q - pad; c.dw0 = pos - q * KW - pad; c.ok0 = r0 < Kc;
     int r1 = r0 + 4; pos = r1 >> logC; c.ci1 = r1 & (C - 1);
-    c.dh1 = pos / KW - pad; c.dw1 = pos % KW - pad; c.ok1 = r1 < Kc;
+    q = (int)fKW.div(pos);
+    c.dh1 = q - pad; c.dw1 = pos - q * KW - pad; c.ok1 = r1 < Kc;
     return c;
   }
   PTG_DEV U4 load(const Ctx& c, int k) const {
     if (!c.ok0 || k >= P) return zero4();
     const int ohw = OH * OW;
-    const int n = k / ohw, rem = k - n * ohw, oh = rem / OW, ow = rem - oh * OW;
+    const int n = (int)fOHW.div(k), rem = k - n * ohw, oh = (int)fOW.div(rem), ow = rem - oh * OW;
     const bf16_t* img = x + (long)n * H * W * C;
     const int ih0 = oh * stride + c.dh0, iw0 = ow * stride + c.dw0;
     if constexpr (CVEC == 8) {
@@ -552,10 +560,12 @@ int ptg_conv2d_fwd(const void* x, const void* w, const float* bias, void* z, int
   EpiBf16 epi{(bf16_t*)z, Cout, bias, act, nullptr, 0};
   if (C % 8 == 0) {
     ConvFwdA<8> la{(const bf16_t*)x, H, W, C, ilog2(C), OH, OW, KW, stride, pad, M, Kc};
+    la.init();
     MatK<8> lb{(const bf16_t*)w, Kc, Cout, Kc};
     return dispatch_gemm(la, lb, epi, M, Cout, Kc, 1, s);
   } else {
     ConvFwdA<4> la{(const bf16_t*)x, H, W, C, ilog2(C), OH, OW, KW, stride, pad, M, Kc};
+    la.init();
     MatK<4> lb{(const bf16_t*)w, Kc, Cout, Kc};
     return dispatch_gemm(la, lb, epi, M, Cout, Kc, 1, s);
   }
@@ -569,6 +579,8 @@ int ptg_conv2d_dgrad(const void* dz, const void* w, void* dx, int N, int H, int 
   const int M = N * H * W, Kc2 = KH * KW * Cout;
   ConvFwdA<8> la{(const bf16_t*)dz, H, W, Cout, ilog2(Cout), H, W, KW, 1, KH - 1 - pad, M, Kc2};
   ConvDgradB lb{(const bf16_t*)w, Cin, Cout, ilog2(Cout), KH, KW, Kc2};
+  la.init();
+  lb.init();
   EpiBf16 epi{(bf16_t*)dx, Cin, nullptr, ACT_NONE, nullptr, accum};
   return dispatch_gemm(la, lb, epi, M, Cin, Kc2, 1, s);
 }
@@ -608,9 +620,11 @@ int ptg_conv2d_wgrad(const void* x, const void* dz, float* dw, int N, int H, int
   }
   if (C % 8 == 0) {
     ConvWgradB<8> lb{(const bf16_t*)x, H, W, C, ilog2(C), OH, OW, KW, stride, pad, P, Kc};
+    lb.init();
     return dispatch_gemm_narrow_m(la, lb, epi, Cout, Kc, P, splits, s);
   } else {
     ConvWgradB<4> lb{(const bf16_t*)x, H, W, C, ilog2(C), OH, OW, KW, stride, pad, P, Kc};
+    lb.init();
     return dispatch_gemm_narrow_m(la, lb, epi, Cout, Kc, P, splits, s);
   }
 }
