@@ -31,33 +31,52 @@ constexpr int BK = 64;
 // ------------------------------------------------------------------------------------------
 // Operand loaders. K_CONTIG loaders return elements (r, k..k+7); the others return
 // elements (r..r+7, k).  Ctx caches the per-row decode so the K loop only does k-math.
+//
+// Every operand is read with buffer loads (cdna_hip_programming.md T8) through a descriptor built
+// once per workgroup from the kernel arguments: a 32-bit byte offset per lane, and every element
+// the GEMM must see as zero (rows past M/N, k past K, the convolution's zero padding) gets the
+// offset OOB, which the hardware range check returns as 0 - no branch per load, no 64-bit address
+// arithmetic.  Operands must be smaller than 2 GiB (checked on the host).
 // ------------------------------------------------------------------------------------------
+constexpr uint32_t OOB = 0x80000000u;
+typedef __amdgpu_buffer_rsrc_t Rsrc;
+
+PTG_DEV Rsrc make_rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+PTG_DEV U4 bload16(Rsrc r, uint32_t off) {
+  return __builtin_bit_cast(U4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+PTG_DEV U2 bload8(Rsrc r, uint32_t off) {
+  return __builtin_bit_cast(U2, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+}
+PTG_DEV U4 join(U2 a, U2 b) { U4 v; v.x = a.x; v.y = a.y; v.z = b.x; v.w = b.y; return v; }
+
 template <int VEC>
 struct MatK {  // element(r,k) = p[r*ld + k]; ld % VEC == 0, K % 8 == 0 or zero-padded rows
   static constexpr bool K_CONTIG = true;
-  const bf16_t* p; long ld; int R; int K;
-  struct Ctx { const bf16_t* row; bool ok; };
-  PTG_DEV Ctx ctx(int r) const { Ctx c; c.ok = r < R; c.row = p + (long)(c.ok ? r : 0) * ld; return c; }
-  PTG_DEV U4 load(const Ctx& c, int k) const {
-    if (!c.ok || k >= K) return zero4();
+  const bf16_t* p; long ld; int R; int K; uint32_t bytes;
+  struct Ctx { uint32_t row; };
+  PTG_DEV Rsrc rsrc() const { return make_rsrc(p, bytes); }
+  PTG_DEV Ctx ctx(int r) const { Ctx c; c.row = r < R ? (uint32_t)(r * ld) * 2u : OOB; return c; }
+  PTG_DEV U4 load(Rsrc rs, const Ctx& c, int k) const {
+    const uint32_t off = k < K ? c.row + 2u * k : OOB;
     if constexpr (VEC == 8) {
-      return *(const U4*)(c.row + k);
+      return bload16(rs, off);
     } else {
-      U2 a = *(const U2*)(c.row + k);
-      U2 b = (k + 4 < K) ? *(const U2*)(c.row + k + 4) : U2{0u, 0u};
-      U4 v; v.x = a.x; v.y = a.y; v.z = b.x; v.w = b.y; return v;
+      return join(bload8(rs, off), bload8(rs, k + 4 < K ? off + 8u : OOB));
     }
   }
 };
 
 struct MatMN {  // element(r,k) = p[k*ld + r]; R % 8 == 0, ld % 8 == 0
   static constexpr bool K_CONTIG = false;
-  const bf16_t* p; long ld; int R; int K;
-  struct Ctx { const bf16_t* col; bool ok; };
-  PTG_DEV Ctx ctx(int r0) const { Ctx c; c.ok = r0 < R; c.col = p + (c.ok ? r0 : 0); return c; }
-  PTG_DEV U4 load(const Ctx& c, int k) const {
-    if (!c.ok || k >= K) return zero4();
-    return *(const U4*)(c.col + (long)k * ld);
+  const bf16_t* p; long ld; int R; int K; uint32_t bytes;
+  struct Ctx { uint32_t col; };
+  PTG_DEV Rsrc rsrc() const { return make_rsrc(p, bytes); }
+  PTG_DEV Ctx ctx(int r0) const { Ctx c; c.col = r0 < R ? 2u * r0 : OOB; return c; }
+  PTG_DEV U4 load(Rsrc rs, const Ctx& c, int k) const {
+    return bload16(rs, k < K ? c.col + (uint32_t)(k * ld) * 2u : OOB);
   }
 };
 
@@ -66,37 +85,35 @@ struct MatMN {  // element(r,k) = p[k*ld + r]; R % 8 == 0, ld % 8 == 0
 template <int CVEC>
 struct ConvFwdA {
   static constexpr bool K_CONTIG = true;
-  const bf16_t* x; int H, W, C, logC, OH, OW, KW, stride, pad, M, Kc;
+  const bf16_t* x; int H, W, C, logC, OH, OW, KW, stride, pad, M, Kc; uint32_t bytes;
   FastDiv fKW, fOHW, fOW;  // set by init(): the per-load (kh, kw) and per-row pixel decodes without idiv
-  ConvFwdA& init() { fKW = fastdiv(KW); fOHW = fastdiv(OH * OW); fOW = fastdiv(OW); return *this; }
-  struct Ctx { const bf16_t* img; int ih0, iw0; bool ok; };
+  ConvFwdA& init() {
+    fKW = fastdiv(KW); fOHW = fastdiv(OH * OW); fOW = fastdiv(OW);
+    bytes = (uint32_t)((long)(M / (OH * OW)) * H * W * C * 2);
+    return *this;
+  }
+  struct Ctx { uint32_t img; int ih0, iw0; };
+  PTG_DEV Rsrc rsrc() const { return make_rsrc(x, bytes); }
   PTG_DEV Ctx ctx(int m) const {
-    Ctx c; c.ok = m < M; if (!c.ok) m = 0;
+    Ctx c;
+    const bool ok = m < M;
+    if (!ok) m = 0;
     const int ohw = OH * OW;
     const int n = (int)fOHW.div(m), rem = m - n * ohw, oh = (int)fOW.div(rem), ow = rem - oh * OW;
-    c.img = x + (long)n * H * W * C; c.ih0 = oh * stride - pad; c.iw0 = ow * stride - pad;
+    c.img = ok ? (uint32_t)(n * H * W * C) * 2u : OOB;
+    c.ih0 = oh * stride - pad; c.iw0 = ow * stride - pad;
     return c;
   }
-  PTG_DEV const bf16_t* at(const Ctx& c, int k, bool& ok) const {
+  PTG_DEV uint32_t at(const Ctx& c, int k) const {
     const int pos = k >> logC, ci = k & (C - 1);
     const int kh = (int)fKW.div(pos), kw = pos - kh * KW;
     const int ih = c.ih0 + kh, iw = c.iw0 + kw;
-    ok = (k < Kc) && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
-    return c.img + ((long)ih * W + iw) * C + ci;
+    const bool ok = (k < Kc) && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+    return ok ? c.img + (uint32_t)((ih * W + iw) * C + ci) * 2u : OOB;
   }
-  PTG_DEV U4 load(const Ctx& c, int k) const {
-    if (!c.ok) return zero4();
-    if constexpr (CVEC == 8) {
-      bool ok; const bf16_t* p = at(c, k, ok);
-      return ok ? *(const U4*)p : zero4();
-    } else {
-      bool ok0, ok1;
-      const bf16_t* p0 = at(c, k, ok0);
-      const bf16_t* p1 = at(c, k + 4, ok1);
-      U2 a = ok0 ? *(const U2*)p0 : U2{0u, 0u};
-      U2 b = ok1 ? *(const U2*)p1 : U2{0u, 0u};
-      U4 v; v.x = a.x; v.y = a.y; v.z = b.x; v.w = b.y; return v;
-    }
+  PTG_DEV U4 load(Rsrc rs, const Ctx& c, int k) const {
+    if constexpr (CVEC == 8) return bload16(rs, at(c, k));
+    else return join(bload8(rs, at(c, k)), bload8(rs, at(c, k + 4)));
   }
 };
 
@@ -104,17 +121,17 @@ struct ConvFwdA {
 // W'[ci][kh'][kw'][co] = W[co][KH-1-kh'][KW-1-kw'][ci]. W is stored [Cout][KH][KW][Cin].
 struct ConvDgradB {
   static constexpr bool K_CONTIG = false;
-  const bf16_t* w; int Cin, Cout, logCout, KH, KW, Kc2;
+  const bf16_t* w; int Cin, Cout, logCout, KH, KW, Kc2; uint32_t bytes;
   FastDiv fKW;
-  ConvDgradB& init() { fKW = fastdiv(KW); return *this; }
-  struct Ctx { int ci0; bool ok; };
-  PTG_DEV Ctx ctx(int r0) const { Ctx c; c.ci0 = r0; c.ok = r0 < Cin; return c; }
-  PTG_DEV U4 load(const Ctx& c, int k) const {
-    if (!c.ok || k >= Kc2) return zero4();
+  ConvDgradB& init() { fKW = fastdiv(KW); bytes = (uint32_t)((long)Cout * KH * KW * Cin * 2); return *this; }
+  struct Ctx { uint32_t ci0; };
+  PTG_DEV Rsrc rsrc() const { return make_rsrc(w, bytes); }
+  PTG_DEV Ctx ctx(int r0) const { Ctx c; c.ci0 = r0 < Cin ? 2u * r0 : OOB; return c; }
+  PTG_DEV U4 load(Rsrc rs, const Ctx& c, int k) const {
     const int pos = k >> logCout, co = k & (Cout - 1);
     const int kh = (int)fKW.div(pos), kw = pos - kh * KW;
-    const long off = ((long)co * KH * KW + (KH - 1 - kh) * KW + (KW - 1 - kw)) * Cin + c.ci0;
-    return *(const U4*)(w + off);
+    const uint32_t off = c.ci0 + (uint32_t)((co * KH * KW + (KH - 1 - kh) * KW + (KW - 1 - kw)) * Cin) * 2u;
+    return bload16(rs, k < Kc2 ? off : OOB);
   }
 };
 
@@ -122,37 +139,38 @@ struct ConvDgradB {
 template <int CVEC>
 struct ConvWgradB {
   static constexpr bool K_CONTIG = false;
-  const bf16_t* x; int H, W, C, logC, OH, OW, KW, stride, pad, P, Kc;
+  const bf16_t* x; int H, W, C, logC, OH, OW, KW, stride, pad, P, Kc; uint32_t bytes;
   FastDiv fKW, fOHW, fOW;  // the per-load pixel decode (k -> n, oh, ow) is the loader's hot path
-  ConvWgradB& init() { fKW = fastdiv(KW); fOHW = fastdiv(OH * OW); fOW = fastdiv(OW); return *this; }
-  struct Ctx { int dh0, dw0, ci0, dh1, dw1, ci1; bool ok0, ok1; };
+  ConvWgradB& init() {
+    fKW = fastdiv(KW); fOHW = fastdiv(OH * OW); fOW = fastdiv(OW);
+    bytes = (uint32_t)((long)(P / (OH * OW)) * H * W * C * 2);
+    return *this;
+  }
+  struct Ctx { int dh0, dw0, dh1, dw1; uint32_t ci0, ci1; };
+  PTG_DEV Rsrc rsrc() const { return make_rsrc(x, bytes); }
   PTG_DEV Ctx ctx(int r0) const {
     Ctx c;
-    int pos = r0 >> logC; c.ci0 = r0 & (C - 1);
+    int pos = r0 >> logC;
     int q = (int)fKW.div(pos);
-    c.dh0 = q - pad; c.dw0 = pos - q * KW - pad; c.ok0 = r0 < Kc;
-    int r1 = r0 + 4; pos = r1 >> logC; c.ci1 = r1 & (C - 1);
+    c.dh0 = q - pad; c.dw0 = pos - q * KW - pad; c.ci0 = r0 < Kc ? 2u * (r0 & (C - 1)) : OOB;
+    const int r1 = r0 + 4;
+    pos = r1 >> logC;
     q = (int)fKW.div(pos);
-    c.dh1 = q - pad; c.dw1 = pos - q * KW - pad; c.ok1 = r1 < Kc;
+    c.dh1 = q - pad; c.dw1 = pos - q * KW - pad; c.ci1 = r1 < Kc ? 2u * (r1 & (C - 1)) : OOB;
     return c;
   }
-  PTG_DEV U4 load(const Ctx& c, int k) const {
-    if (!c.ok0 || k >= P) return zero4();
+  PTG_DEV uint32_t at(int k, int n, int oh, int ow, int dh, int dw, uint32_t ci) const {
+    const int ih = oh * stride + dh, iw = ow * stride + dw;
+    const bool ok = k < P && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+    return ok ? ci + (uint32_t)(((n * H + ih) * W + iw) * C) * 2u : OOB;
+  }
+  PTG_DEV U4 load(Rsrc rs, const Ctx& c, int k) const {
     const int ohw = OH * OW;
     const int n = (int)fOHW.div(k), rem = k - n * ohw, oh = (int)fOW.div(rem), ow = rem - oh * OW;
-    const bf16_t* img = x + (long)n * H * W * C;
-    const int ih0 = oh * stride + c.dh0, iw0 = ow * stride + c.dw0;
     if constexpr (CVEC == 8) {
-      if ((unsigned)ih0 >= (unsigned)H || (unsigned)iw0 >= (unsigned)W) return zero4();
-      return *(const U4*)(img + ((long)ih0 * W + iw0) * C + c.ci0);
+      return bload16(rs, at(k, n, oh, ow, c.dh0, c.dw0, c.ci0));
     } else {
-      U2 a = U2{0u, 0u}, b = U2{0u, 0u};
-      if ((unsigned)ih0 < (unsigned)H && (unsigned)iw0 < (unsigned)W)
-        a = *(const U2*)(img + ((long)ih0 * W + iw0) * C + c.ci0);
-      const int ih1 = oh * stride + c.dh1, iw1 = ow * stride + c.dw1;
-      if (c.ok1 && (unsigned)ih1 < (unsigned)H && (unsigned)iw1 < (unsigned)W)
-        b = *(const U2*)(img + ((long)ih1 * W + iw1) * C + c.ci1);
-      U4 v; v.x = a.x; v.y = a.y; v.z = b.x; v.w = b.y; return v;
+      return join(bload8(rs, at(k, n, oh, ow, c.dh0, c.dw0, c.ci0)), bload8(rs, at(k, n, oh, ow, c.dh1, c.dw1, c.ci1)));
     }
   }
 };
@@ -345,21 +363,24 @@ __global__ __launch_bounds__(256) void gemm_kernel(LA la, LB lb, EPI epi, int M,
   }
 
   U4 ra[AI], rb[BI];
+  const Rsrc rsA = la.rsrc(), rsB = lb.rsrc();
+  // slots past the tile (AV or BV not a multiple of 256) exist only in the last unrolled slot
+  constexpr bool AFULL = AV % 256 == 0, BFULL = BV % 256 == 0;
   auto gload = [&](int k0) {
 #pragma unroll
-    for (int i = 0; i < AI; ++i) ra[i] = aon[i] ? la.load(ca[i], k0 + akk[i]) : zero4();
+    for (int i = 0; i < AI; ++i) ra[i] = la.load(rsA, ca[i], k0 + akk[i]);
 #pragma unroll
-    for (int i = 0; i < BI; ++i) rb[i] = bon[i] ? lb.load(cb[i], k0 + bkk[i]) : zero4();
+    for (int i = 0; i < BI; ++i) rb[i] = lb.load(rsB, cb[i], k0 + bkk[i]);
   };
   auto sstore = [&](int stage) {
     bf16_t* sA = smem + stage * STAGE;
     bf16_t* sB = sA + IA::ELEMS;
 #pragma unroll
     for (int i = 0; i < AI; ++i)
-      if (aon[i]) *(U4*)(sA + aoff[i]) = ra[i];
+      if (AFULL || aon[i]) *(U4*)(sA + aoff[i]) = ra[i];
 #pragma unroll
     for (int i = 0; i < BI; ++i)
-      if (bon[i]) *(U4*)(sB + boff[i]) = rb[i];
+      if (BFULL || bon[i]) *(U4*)(sB + boff[i]) = rb[i];
   };
   // fragment (16 rows x 32 k at k-offset kk) of an LDS image; rows start at `row0`
   const int g = lane >> 4, li = lane & 15, q = li >> 2, p4 = (li & 3) * 4;
@@ -500,6 +521,11 @@ static int dispatch_gemm_narrow_m(const LA& la, const LB& lb, const EPI& epi, in
 }
 
 static int ilog2(int v) { int l = 0; while ((1 << l) < v) ++l; return l; }
+// byte extents of the operand views (the buffer descriptors' range); the engine's operands are far
+// below the 2 GiB the 32-bit offsets (and the OOB sentinel above them) allow
+static long matk_bytes(long ld, int R, int K) { return ((long)(R - 1) * ld + K) * 2; }
+static long matmn_bytes(long ld, int R, int K) { return ((long)(K - 1) * ld + R) * 2; }
+static bool fits(long bytes) { return bytes > 0 && bytes < (long)OOB; }
 static bool is_pow2(int v) { return v > 0 && (v & (v - 1)) == 0; }
 
 }  // namespace ptg
@@ -517,6 +543,9 @@ int ptg_gemm_bf16(int M, int N, int K, const void* A, long lda, int a_kcontig, c
                   int b_kcontig, int epi, void* C, long ldc, const float* bias, int act, int splits,
                   hipStream_t s) {
   if (M <= 0 || N <= 0 || K <= 0) return 0;
+  if (!fits(a_kcontig ? matk_bytes(lda, M, K) : matmn_bytes(lda, M, K)) ||
+      !fits(b_kcontig ? matk_bytes(ldb, N, K) : matmn_bytes(ldb, N, K)))
+    return (int)hipErrorInvalidValue;
   if (epi != 3) splits = 1;
   const bf16_t* a = (const bf16_t*)A; const bf16_t* b = (const bf16_t*)B;
 #define PTG_EPI_SWITCH(LAX, LBX)                                                                 \
@@ -532,19 +561,19 @@ int ptg_gemm_bf16(int M, int N, int K, const void* A, long lda, int a_kcontig, c
   }
   if (a_kcontig && b_kcontig) {
     if (lda % 8 || ldb % 8 || K % 8) return (int)hipErrorInvalidValue;
-    MatK<8> la{a, lda, M, K}; MatK<8> lb{b, ldb, N, K};
+    MatK<8> la{a, lda, M, K, (uint32_t)matk_bytes(lda, M, K)}; MatK<8> lb{b, ldb, N, K, (uint32_t)matk_bytes(ldb, N, K)};
     PTG_EPI_SWITCH(la, lb)
   } else if (a_kcontig && !b_kcontig) {
     if (lda % 8 || ldb % 8 || K % 8 || N % 8) return (int)hipErrorInvalidValue;
-    MatK<8> la{a, lda, M, K}; MatMN lb{b, ldb, N, K};
+    MatK<8> la{a, lda, M, K, (uint32_t)matk_bytes(lda, M, K)}; MatMN lb{b, ldb, N, K, (uint32_t)matmn_bytes(ldb, N, K)};
     PTG_EPI_SWITCH(la, lb)
   } else if (!a_kcontig && !b_kcontig) {
     if (lda % 8 || ldb % 8 || M % 8 || N % 8) return (int)hipErrorInvalidValue;
-    MatMN la{a, lda, M, K}; MatMN lb{b, ldb, N, K};
+    MatMN la{a, lda, M, K, (uint32_t)matmn_bytes(lda, M, K)}; MatMN lb{b, ldb, N, K, (uint32_t)matmn_bytes(ldb, N, K)};
     PTG_EPI_SWITCH(la, lb)
   } else {
     if (lda % 8 || ldb % 8 || M % 8 || K % 8) return (int)hipErrorInvalidValue;
-    MatMN la{a, lda, M, K}; MatK<8> lb{b, ldb, N, K};
+    MatMN la{a, lda, M, K, (uint32_t)matmn_bytes(lda, M, K)}; MatK<8> lb{b, ldb, N, K, (uint32_t)matk_bytes(ldb, N, K)};
     PTG_EPI_SWITCH(la, lb)
   }
 #undef PTG_EPI_SWITCH
@@ -557,16 +586,17 @@ int ptg_conv2d_fwd(const void* x, const void* w, const float* bias, void* z, int
                    hipStream_t s) {
   if (!is_pow2(C) || C < 4) return (int)hipErrorInvalidValue;
   const int M = N * OH * OW, Kc = KH * KW * C;
+  if (!fits((long)N * H * W * C * 2) || !fits((long)Cout * Kc * 2)) return (int)hipErrorInvalidValue;
   EpiBf16 epi{(bf16_t*)z, Cout, bias, act, nullptr, 0};
   if (C % 8 == 0) {
     ConvFwdA<8> la{(const bf16_t*)x, H, W, C, ilog2(C), OH, OW, KW, stride, pad, M, Kc};
     la.init();
-    MatK<8> lb{(const bf16_t*)w, Kc, Cout, Kc};
+    MatK<8> lb{(const bf16_t*)w, Kc, Cout, Kc, (uint32_t)matk_bytes(Kc, Cout, Kc)};
     return dispatch_gemm(la, lb, epi, M, Cout, Kc, 1, s);
   } else {
     ConvFwdA<4> la{(const bf16_t*)x, H, W, C, ilog2(C), OH, OW, KW, stride, pad, M, Kc};
     la.init();
-    MatK<4> lb{(const bf16_t*)w, Kc, Cout, Kc};
+    MatK<4> lb{(const bf16_t*)w, Kc, Cout, Kc, (uint32_t)matk_bytes(Kc, Cout, Kc)};
     return dispatch_gemm(la, lb, epi, M, Cout, Kc, 1, s);
   }
 }
@@ -577,6 +607,7 @@ int ptg_conv2d_dgrad(const void* dz, const void* w, void* dx, int N, int H, int 
                      int KH, int KW, int pad, int accum, hipStream_t s) {
   if (!is_pow2(Cout) || Cout < 8 || Cin % 8) return (int)hipErrorInvalidValue;
   const int M = N * H * W, Kc2 = KH * KW * Cout;
+  if (!fits((long)M * Cout * 2) || !fits((long)Kc2 * Cin * 2)) return (int)hipErrorInvalidValue;
   ConvFwdA<8> la{(const bf16_t*)dz, H, W, Cout, ilog2(Cout), H, W, KW, 1, KH - 1 - pad, M, Kc2};
   ConvDgradB lb{(const bf16_t*)w, Cin, Cout, ilog2(Cout), KH, KW, Kc2};
   la.init();
@@ -592,8 +623,9 @@ int ptg_conv1x1_dgrad(const void* dz, const void* w, void* dx, int N, int OH, in
                       int Cout, int stride, int accum, hipStream_t s) {
   if (Cin % 8 || Cout % 8) return (int)hipErrorInvalidValue;
   const int M = N * OH * OW;
-  MatK<8> la{(const bf16_t*)dz, Cout, M, Cout};
-  MatMN lb{(const bf16_t*)w, Cin, Cin, Cout};
+  if (!fits((long)M * Cout * 2)) return (int)hipErrorInvalidValue;
+  MatK<8> la{(const bf16_t*)dz, Cout, M, Cout, (uint32_t)matk_bytes(Cout, M, Cout)};
+  MatMN lb{(const bf16_t*)w, Cin, Cin, Cout, (uint32_t)matmn_bytes(Cin, Cin, Cout)};
   if (stride == 1) {
     EpiBf16 epi{(bf16_t*)dx, Cin, nullptr, ACT_NONE, nullptr, accum};
     return dispatch_gemm(la, lb, epi, M, Cin, Cout, 1, s);
@@ -608,7 +640,8 @@ int ptg_conv2d_wgrad(const void* x, const void* dz, float* dw, int N, int H, int
                      int KH, int KW, int stride, int pad, int OH, int OW, int splits, hipStream_t s) {
   if (!is_pow2(C) || C < 4 || Cout % 8) return (int)hipErrorInvalidValue;
   const int P = N * OH * OW, Kc = KH * KW * C;
-  MatMN la{(const bf16_t*)dz, Cout, Cout, P};
+  if (!fits((long)N * H * W * C * 2) || !fits((long)P * Cout * 2)) return (int)hipErrorInvalidValue;
+  MatMN la{(const bf16_t*)dz, Cout, Cout, P, (uint32_t)matmn_bytes(Cout, Cout, P)};
   EpiAtomic epi{dw, Kc};
   if (splits <= 0) {
     const int tiles = ptg_ceil_div(Cout, Cout <= 16 ? 16 : (Cout <= 32 ? 32 : 64)) * ptg_ceil_div(Kc, 128);
