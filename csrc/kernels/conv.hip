@@ -937,6 +937,20 @@ __global__ __launch_bounds__(256) void conv_flip_k(const bf16_t* __restrict__ w,
   }
 }
 
+// Up to four flips in one launch: job j covers elements [off[j], off[j+1]) of the concatenated range.
+struct FlipJobs { const bf16_t* w[4]; bf16_t* wf[4]; int Cout[4], KS[4], Cin[4], off[5]; };
+__global__ __launch_bounds__(256) void conv_flip4_k(FlipJobs J) {
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < J.off[4]; i += gridDim.x * 256) {
+    const int j = i < J.off[1] ? 0 : i < J.off[2] ? 1 : i < J.off[3] ? 2 : 3;
+    const int e = i - J.off[j], Cout = J.Cout[j], KS = J.KS[j], Cin = J.Cin[j];
+    const int co = e % Cout;
+    int t = e / Cout;
+    const int kw = t % KS; t /= KS;
+    const int kh = t % KS; const int ci = t / KS;
+    J.wf[j][e] = J.w[j][(((long)co * KS + (KS - 1 - kh)) * KS + (KS - 1 - kw)) * Cin + ci];
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
 // host dispatch
 // ------------------------------------------------------------------------------------------------
@@ -1147,6 +1161,26 @@ int ptg_conv2d_wgrad_halo_sparse(const void* x, const void* dzsel, const void* a
   if (MF == 1) return wgrad_by_cin<5, 1, true>(x, dzsel, dw, N, H, W, C, Cout, pad, s, argq);
   if (MF == 2) return wgrad_by_cin<5, 2, true>(x, dzsel, dw, N, H, W, C, Cout, pad, s, argq);
   return wgrad_by_cin<5, 4, true>(x, dzsel, dw, N, H, W, C, Cout, pad, s, argq);
+}
+
+int ptg_conv_flip_weights4(int n, const void* w0, void* wf0, int Cout0, int KS0, int Cin0, const void* w1, void* wf1,
+                           int Cout1, int KS1, int Cin1, const void* w2, void* wf2, int Cout2, int KS2, int Cin2,
+                           const void* w3, void* wf3, int Cout3, int KS3, int Cin3, hipStream_t s) {
+  if (n < 1 || n > 4) return (int)hipErrorInvalidValue;
+  FlipJobs J{};
+  const void* ws[4] = {w0, w1, w2, w3};
+  void* wfs[4] = {wf0, wf1, wf2, wf3};
+  const int co[4] = {Cout0, Cout1, Cout2, Cout3}, ks[4] = {KS0, KS1, KS2, KS3}, ci[4] = {Cin0, Cin1, Cin2, Cin3};
+  J.off[0] = 0;
+  for (int j = 0; j < 4; ++j) {
+    const bool on = j < n;
+    J.w[j] = (const bf16_t*)ws[j]; J.wf[j] = (bf16_t*)wfs[j];
+    J.Cout[j] = on ? co[j] : 1; J.KS[j] = on ? ks[j] : 1; J.Cin[j] = on ? ci[j] : 1;
+    J.off[j + 1] = J.off[j] + (on ? co[j] * ks[j] * ks[j] * ci[j] : 0);
+  }
+  const int blocks = std::min(1024, (J.off[4] + 255) / 256);
+  hipLaunchKernelGGL(conv_flip4_k, dim3(std::max(blocks, 1)), dim3(256), 0, s, J);
+  PTG_RETURN_LAUNCH();
 }
 
 int ptg_conv_flip_weights(const void* w, void* wf, int Cout, int KS, int Cin, hipStream_t s) {

@@ -590,6 +590,79 @@ __global__ __launch_bounds__(256) void prelu_bwd_k(const bf16_t* __restrict__ da
   bias_reduce_atomic(db, i % (C >> 3), C >> 3, sred, dbias);
 }
 
+// PReLU backward, sample-parallel (the prelu_pool_bwd_sg_k layout without the pool): a block owns
+// 16 8-element positions over a batch chunk split into 16 sample groups and reduces dalpha over the
+// groups in LDS - one dalpha add per element and chunk instead of one fp32 atomic per element and
+// sample pair (prelu_bwd_k: 2.6M contended atomics for CNN-B1's last conv layer at batch 256).
+__global__ __launch_bounds__(256) void prelu_bwd_sg_k(const bf16_t* __restrict__ da, const bf16_t* __restrict__ z,
+                                                      const float* __restrict__ alpha, bf16_t* __restrict__ dz,
+                                                      float* __restrict__ dalpha, float* __restrict__ dbias, int N,
+                                                      int HWC, int C, int nper) {
+  constexpr int PB = 16, SG = 16, RP = 9, U = 4;
+  __shared__ float sda[SG * PB * RP];
+  __shared__ float sdb[256];
+  const int HWC8 = HWC >> 3, C8 = C >> 3;
+  const int pl = threadIdx.x & (PB - 1), sg = threadIdx.x / PB;
+  const int i = blockIdx.x * PB + pl;
+  const int n0 = blockIdx.y * nper, n1 = min(N, n0 + nper);
+  const bool active = i < HWC8;
+  const long e = (long)(active ? i : 0) * 8;
+  float dal[8], db[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { dal[j] = 0.f; db[j] = 0.f; }
+  if ((int)threadIdx.x < C) sdb[threadIdx.x] = 0.f;
+  if (active) {
+    const float4 a0 = *(const float4*)(alpha + e), a1 = *(const float4*)(alpha + e + 4);
+    const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    for (int n = n0 + sg; n < n1; n += U * SG) {
+      U4 graw[U], zraw[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const long o = (long)(n + u * SG < n1 ? n + u * SG : n) * HWC + e;
+        graw[u] = *(const U4*)(da + o);
+        zraw[u] = *(const U4*)(z + o);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (n + u * SG >= n1) break;
+        float g[8], zv[8], o[8];
+        unpack8(graw[u], g);
+        unpack8(zraw[u], zv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const bool pos = zv[j] > 0.f;
+          o[j] = pos ? g[j] : g[j] * av[j];
+          dal[j] += pos ? 0.f : g[j] * zv[j];
+          db[j] += o[j];
+        }
+        *(U4*)(dz + (long)(n + u * SG) * HWC + e) = pack8(o);
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sda[(sg * PB + pl) * RP + j] = dal[j];
+  __syncthreads();
+  if (active) {
+    const int c8 = i % C8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) atomicAdd(&sdb[c8 * 8 + j], db[j]);
+  }
+  if (threadIdx.x < PB * 8) {
+    const int p = threadIdx.x >> 3, j = threadIdx.x & 7;
+    float sum = 0.f;
+#pragma unroll
+    for (int gsg = 0; gsg < SG; ++gsg) sum += sda[(gsg * PB + p) * RP + j];
+    const int ii = blockIdx.x * PB + p;
+    if (ii < HWC8) {
+      float* dst = dalpha + (long)ii * 8 + j;
+      if (gridDim.y == 1) *dst += sum;
+      else atomicAdd(dst, sum);
+    }
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < C) atomicAdd(dbias + threadIdx.x, sdb[threadIdx.x]);
+}
+
 // out_bf16[m][n] = act(acc[m][n] + bias[n])   (split-K GEMM finishing pass)
 __global__ __launch_bounds__(256) void bias_act_k(const float* __restrict__ acc,
                                                   const float* __restrict__ bias, bf16_t* __restrict__ out,
@@ -1021,6 +1094,21 @@ int ptg_prelu_bwd(const void* da, const void* z, const float* alpha, void* dz, f
   }
   dim3 grid((nvec + 255) / 256, (N + nper - 1) / nper);
   hipLaunchKernelGGL(prelu_bwd_k, grid, dim3(256), 0, s, (const bf16_t*)da, (const bf16_t*)z, alpha,
+                     (bf16_t*)dz, dalpha, dbias, N, HWC, C, nper);
+  PTG_RETURN_LAUNCH();
+}
+
+int ptg_prelu_bwd2(const void* da, const void* z, const float* alpha, void* dz, float* dalpha,
+                   float* dbias, int N, int HWC, int C, int nper, hipStream_t s) {
+  if (HWC % 8 || C % 8 || C > 256) return (int)hipErrorInvalidValue;
+  const int bx = (HWC / 8 + 15) / 16;
+  if (nper <= 0) {  // >= ~512 blocks, >= 32 samples per chunk
+    int chunks = (512 + bx - 1) / bx;
+    chunks = std::max(1, std::min(chunks, N / 32));
+    nper = (N + chunks - 1) / chunks;
+  }
+  dim3 grid(bx, (N + nper - 1) / nper);
+  hipLaunchKernelGGL(prelu_bwd_sg_k, grid, dim3(256), 0, s, (const bf16_t*)da, (const bf16_t*)z, alpha,
                      (bf16_t*)dz, dalpha, dbias, N, HWC, C, nper);
   PTG_RETURN_LAUNCH();
 }

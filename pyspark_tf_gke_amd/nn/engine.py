@@ -185,6 +185,16 @@ class ConvOp(Op):
         self._zs, self._arg, self._zshape = zs, arg, (B, OH, OW, Co)
         return p
 
+    def _wflip_buf(self, ws, dev):
+        KS, Co = self.conv.kernel_size[0], self.conv.out_shape[-1]
+        return ws.get(self.name + "/wflip", (self.conv.cin_p, KS, KS, Co), torch.bfloat16, dev)
+
+    def dgrad_flip_job(self, ws):
+        """(weights, flip buffer) when this op's backward runs the halo dgrad on the GPU, else None."""
+        if self.first or self.stride != 1 or not self.conv.kernel.bf16.is_cuda or not self._halo()[1]:
+            return None
+        return self.conv.kernel.bf16, self._wflip_buf(ws, self.conv.kernel.bf16.device)
+
     def _backward_sel(self, x, dy, ws, dev):
         """First layer: sparse record -> dZ record -> weight gradient (no dense z / dZ, no dgrad)."""
         C = self._zshape[-1]
@@ -259,9 +269,9 @@ class ConvOp(Op):
             raise NotImplementedError("dgrad for strided convolutions")
         dx = ws.get(self.name + "/dx", x.shape, torch.bfloat16, dev)
         if halo_dgrad:
-            KS, Co = self.conv.kernel_size[0], zshape[-1]
-            wf = ws.get(self.name + "/wflip", (self.conv.cin_p, KS, KS, Co), torch.bfloat16, dev)
-            K.conv2d_dgrad_halo(dz, self.conv.kernel.bf16, self.pad, dx, wf)
+            wf = self._wflip_buf(ws, dev)
+            K.conv2d_dgrad_halo(dz, self.conv.kernel.bf16, self.pad, dx, wf,
+                                flipped=getattr(self, "_wf_ready", False))
         else:
             K.conv2d_dgrad(dz, self.conv.kernel.bf16, self.pad, dx)
         return dx
@@ -484,6 +494,17 @@ def run_forward(ops, x, ws, training=True, pre_op=None):
 
 
 def run_backward(ops, dy, ws, on_op_done=None):
+    # every halo dgrad filter of this pass flipped by one launch up front (weights are fixed until
+    # the optimizer step that follows the backward)
+    jobs = []
+    for op in ops:
+        if isinstance(op, ConvOp):
+            job = op.dgrad_flip_job(ws)
+            op._wf_ready = job is not None
+            if job is not None:
+                jobs.append(job)
+    if jobs:
+        K.conv_flip_weights_multi(jobs)
     for op in reversed(ops):
         dy = op.backward(dy, ws)
         if on_op_done is not None:

@@ -188,11 +188,36 @@ def conv_flip_weights(w, out):
     return out
 
 
-def conv2d_dgrad_halo(dz, w, pad: int, out, wflip_buf):
-    """dx = d(conv)/dx (stride-1 'same') via the halo fwd kernel on flipped weights."""
+def conv_flip_weights_multi(jobs):
+    """conv_flip_weights for up to 4 (w, out) pairs in ONE launch (every dgrad filter of a backward
+    pass is flipped up front instead of by one ~5 us launch per layer)."""
+    jobs = list(jobs)
+    if not jobs:
+        return
+    if not on_device(jobs[0][0]):
+        for w, out in jobs:
+            conv_flip_weights(w, out)
+        return
+    for k in range(0, len(jobs), 4):
+        args = []
+        part = jobs[k:k + 4]
+        for w, out in part:
+            need(w, torch.bfloat16, "flip.w"); need(out, torch.bfloat16, "flip.out")
+            Cout, KS, _, Cin = w.shape
+            assert tuple(out.shape) == (Cin, KS, KS, Cout)
+            args += [ptr(w), ptr(out), Cout, KS, Cin]
+        for _ in range(4 - len(part)):
+            args += [None, None, 0, 0, 0]
+        hip("ptg_conv_flip_weights4", len(part), *args)
+
+
+def conv2d_dgrad_halo(dz, w, pad: int, out, wflip_buf, flipped: bool = False):
+    """dx = d(conv)/dx (stride-1 'same') via the halo fwd kernel on flipped weights (``flipped``:
+    ``wflip_buf`` already holds them, see conv_flip_weights_multi)."""
     if not on_device(dz):
         return ref.conv2d_dgrad(dz, w, pad, out)
-    conv_flip_weights(w, wflip_buf)
+    if not flipped:
+        conv_flip_weights(w, wflip_buf)
     KS = w.shape[1]
     return conv2d_fwd_fused(dz, wflip_buf, None, KS - 1 - pad, out)
 
@@ -354,7 +379,8 @@ def prelu_bwd(da, z, alpha, dz_out, dalpha, dbias, nper: int = 0):
         return ref.prelu_bwd(da, z, alpha, dz_out, dalpha, dbias)
     N = z.shape[0]
     C = z.shape[-1]
-    hip("ptg_prelu_bwd", ptr(da), ptr(z), ptr(alpha), ptr(dz_out), ptr(dalpha), ptr(dbias), N, z[0].numel(), C, nper)
+    hip("ptg_prelu_bwd2" if PPBWD_KERNEL == "sg" else "ptg_prelu_bwd", ptr(da), ptr(z), ptr(alpha), ptr(dz_out),
+        ptr(dalpha), ptr(dbias), N, z[0].numel(), C, nper)
     return dz_out
 
 

@@ -13,11 +13,11 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def test_two_rank_sharded_update_on_gpu(hip_built):
-    env = dict(os.environ, PTG_DIST_BACKEND="gloo", PYTHONPATH=ROOT)
+def test_two_rank_sharded_update_on_gpu(hip_built, tmp_path):
+    env = dict(os.environ, PTG_DIST_BACKEND="gloo", PYTHONPATH=ROOT, PTG_REHEARSE_OUT=str(tmp_path))
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", "29617", os.path.join(ROOT, "tools", "rehearse_multirank.py")]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
-    res = [json.loads(l.split("REHEARSAL ", 1)[1]) for l in r.stdout.splitlines() if "REHEARSAL " in l]
+    res = [json.loads((tmp_path / f"rank{k}.json").read_text()) for k in range(2)]
     assert len(res) == 2 and all(v["ok"] and v["buckets"] > 2 for v in res), res

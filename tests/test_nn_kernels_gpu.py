@@ -267,6 +267,17 @@ def test_first_layer_sparse_chain_matches_dense(monkeypatch):
         _close(grads[True][name], g, 2e-2, 1e-3, "sel_grad_" + name)
 
 
+def test_conv_flip_weights_multi():
+    """One launch flipping several dgrad filters == the per-layer flip (and the reference permute)."""
+    shapes = [(8, 5, 5, 4), (16, 5, 5, 8), (32, 5, 5, 16), (64, 5, 5, 32), (64, 3, 3, 64)]
+    ws = [rnd(*s_).to(DEV) for s_ in shapes]
+    outs = [torch.empty(s_[3], s_[1], s_[2], s_[0], device=DEV, dtype=torch.bfloat16) for s_ in shapes]
+    K.conv_flip_weights_multi(list(zip(ws, outs)))
+    for w, o in zip(ws, outs):
+        ref = torch.flip(w.cpu(), dims=(1, 2)).permute(3, 1, 2, 0)
+        assert torch.equal(o.cpu(), ref)
+
+
 @pytest.mark.parametrize("N,H,W,C,Co,KS", HALO_CASES + BIG_HALO)
 def test_conv_halo_wgrad(N, H, W, C, Co, KS):
     x, dz = rnd(N, H, W, C), rnd(N, H, W, Co, scale=0.1)
@@ -318,7 +329,7 @@ def test_prelu_pool_fwd_bwd(C, N, H, W, nper, kernel, monkeypatch):
     _close(db, dbr, 1e-2, 1e-2, "dbias")
 
 
-@pytest.mark.parametrize("N,H,W,C,nper", [(4, 16, 20, 64, 0), (7, 5, 6, 24, 3), (5, 4, 4, 8, 2)])
+@pytest.mark.parametrize("N,H,W,C,nper", [(4, 16, 20, 64, 0), (7, 5, 6, 24, 3), (5, 4, 4, 8, 2), (96, 16, 20, 64, 0)])
 def test_prelu_fwd_bwd(N, H, W, C, nper):
     z, alpha, da = rnd(N, H, W, C), torch.randn(H, W, C) * 0.2, rnd(N, H, W, C)
     a = torch.empty_like(z, device=DEV)

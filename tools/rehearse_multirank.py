@@ -8,6 +8,7 @@ the real HIP kernels in the loop.  Launch:
         tools/rehearse_multirank.py
 """
 import json
+import os
 import sys
 from pathlib import Path
 
@@ -44,6 +45,10 @@ def main():
     out = {"rank": st_s.rank, "world": st_s.world_size, "buckets": len(ms._shard_plan.buckets), "diff": diff,
            "bf16_diff": bdiff, "scale": scale, "ok": diff <= 1e-4 * max(1.0, scale)}
     print("REHEARSAL " + json.dumps(out), flush=True)
+    out_dir = os.environ.get("PTG_REHEARSE_OUT")
+    if out_dir:  # ranks share stdout: lines can interleave, so the test reads one file per rank
+        with open(os.path.join(out_dir, f"rank{st_s.rank}.json"), "w") as fh:
+            json.dump(out, fh)
     return 0 if out["ok"] else 1
 
 
