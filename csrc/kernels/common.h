@@ -74,6 +74,23 @@ PTG_DEV int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
 }
 
+// Buffer loads (cdna_hip_programming.md T8): 32-bit byte offsets against a descriptor built once
+// from kernel arguments; every offset >= the descriptor's byte count (use PTG_OOB) reads as zero
+// through the hardware range check, so zero padding / tails need no branch.  Operands < 2 GiB.
+constexpr uint32_t PTG_OOB = 0x80000000u;
+typedef __amdgpu_buffer_rsrc_t Rsrc;
+PTG_DEV Rsrc make_rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+PTG_DEV U4 bload16(Rsrc r, uint32_t off) {
+  return __builtin_bit_cast(U4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+PTG_DEV U2 bload8(Rsrc r, uint32_t off) {
+  return __builtin_bit_cast(U2, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+}
+PTG_DEV uint32_t bload4(Rsrc r, uint32_t off) { return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0); }
+static inline bool ptg_fits_2g(long bytes) { return bytes > 0 && bytes < (long)PTG_OOB; }
+
 static inline int ptg_ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
 
 // Division by a runtime-invariant divisor without the ~30-instruction integer division sequence:

@@ -93,6 +93,14 @@ typedef __attribute__((ext_vector_type(2))) unsigned int vu2_t;
 template <int C> struct HVec { using T = vu4_t; static constexpr int per_pix = C / 8; };
 template <> struct HVec<4> { using T = vu2_t; static constexpr int per_pix = 1; };
 
+template <class VT> PTG_DEV VT bload_vt(Rsrc r, uint32_t off);
+template <> PTG_DEV vu4_t bload_vt<vu4_t>(Rsrc r, uint32_t off) {
+  return __builtin_bit_cast(vu4_t, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+template <> PTG_DEV vu2_t bload_vt<vu2_t>(Rsrc r, uint32_t off) {
+  return __builtin_bit_cast(vu2_t, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+}
+
 // dpp row_shl:n - lane l receives lane l+n of its 16-lane row (others keep their own value)
 template <int NSH>
 PTG_DEV float row_shl(float v) {
@@ -211,15 +219,15 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
     pr_l[p] = pr_c[p] * PIX + vv * VE;   // LDS offset inside a halo row
   }
   VT pf[PFN];
+  // halo loads: buffer loads, the zero padding / rows past the image come back as 0 (PTG_OOB)
+  const Rsrc xr = make_rsrc(x, (uint32_t)((long)N * H * W * C * 2));
   auto load_rows = [&](int n, int iw0, int ih_first, int nrows) {
-    const bf16_t* img = x + (long)n * H * W * C;
+    const uint32_t img = (uint32_t)(n * H * W * C) * 2u;
 #pragma unroll
     for (int p = 0; p < PFN; ++p) {
-      VT v = (VT)0u;
       const int ih = ih_first + pr_r[p], iw = iw0 + pr_c[p];
-      if (pr_r[p] < nrows && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
-        v = *(const VT*)(img + ((long)ih * W + iw) * C + (pr_l[p] - pr_c[p] * PIX));
-      pf[p] = v;
+      const bool ok = pr_r[p] < nrows && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+      pf[p] = bload_vt<VT>(xr, ok ? img + (uint32_t)((ih * W + iw) * C + (pr_l[p] - pr_c[p] * PIX)) * 2u : PTG_OOB);
     }
   };
   auto store_rows = [&](int nrows, int slot_first) {
@@ -586,41 +594,35 @@ __global__ __launch_bounds__(256) void conv_wgrad_strip_k(const bf16_t* __restri
   uint32_t pq[SPARSE ? PFD : 1];
   const int CV = Cout / 4;
   const int PH = H >> 1, PW = W >> 1;
+  // buffer loads: halo padding, pixels past the image and unused slots read as 0 (PTG_OOB)
+  const Rsrc xr = make_rsrc(x, (uint32_t)((long)N * H * W * C * 2));
+  const Rsrc dr = make_rsrc(dz, (uint32_t)(SPARSE ? (long)N * PH * PW * Cout * 2 : (long)N * H * W * Cout * 2));
+  const Rsrc qr = make_rsrc(argq, SPARSE ? (uint32_t)((long)N * PH * PW * Cout) : 0u);
   auto load_tile = [&](int s_, int th_, int nrows, int ih_first) {
     const int n = s_ / tiles_w, ow0 = (s_ - n * tiles_w) * TW, oh0 = th_ * TH;
-    const bf16_t* img = x + (long)n * H * W * C;
+    const uint32_t img = (uint32_t)(n * H * W * C) * 2u;
 #pragma unroll
     for (int k = 0; k < PFN; ++k) {
-      VT v = (VT)0u;
       const int ih = ih_first + pr_r[k], iw = ow0 - pad + pr_c[k];
-      if (pr_r[k] < nrows && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
-        v = *(const VT*)(img + ((long)ih * W + iw) * C + (pr_l[k] - pr_c[k] * PIX));
-      pf[k] = v;
+      const bool ok = pr_r[k] < nrows && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+      pf[k] = bload_vt<VT>(xr, ok ? img + (uint32_t)((ih * W + iw) * C + (pr_l[k] - pr_c[k] * PIX)) * 2u : PTG_OOB);
     }
 #pragma unroll
     for (int k = 0; k < PFD; ++k) {
       const int v = tid + k * 256;
-      U2 val = U2{0u, 0u};
       if constexpr (SPARSE) {
-        uint32_t qv = 0;
-        if (v < (M / 4) * CV) {
-          const int m = v / CV, cv = v - m * CV;
-          const int ph = (oh0 >> 1) + m / (TW / 2), pw = (ow0 >> 1) + m % (TW / 2);
-          if (ph < PH && pw < PW) {
-            const long o = (((long)n * PH + ph) * PW + pw) * Cout + cv * 4;
-            val = *(const U2*)(dz + o);
-            qv = *(const uint32_t*)(argq + o);
-          }
-        }
-        pq[k] = qv;
+        const int m = v / CV, cv = v - m * CV;
+        const int ph = (oh0 >> 1) + m / (TW / 2), pw = (ow0 >> 1) + m % (TW / 2);
+        const bool ok = v < (M / 4) * CV && ph < PH && pw < PW;
+        const uint32_t o = (uint32_t)(((n * PH + ph) * PW + pw) * Cout + cv * 4);
+        pd[k] = bload8(dr, ok ? 2u * o : PTG_OOB);
+        pq[k] = bload4(qr, ok ? o : PTG_OOB);
       } else {
-        if (v < M * CV) {
-          const int m = v / CV, cv = v - m * CV;
-          const int oh = oh0 + m / TW, ow = ow0 + m % TW;
-          if (oh < H && ow < W) val = *(const U2*)(dz + (((long)n * H + oh) * W + ow) * Cout + cv * 4);
-        }
+        const int m = v / CV, cv = v - m * CV;
+        const int oh = oh0 + m / TW, ow = ow0 + m % TW;
+        const bool ok = v < M * CV && oh < H && ow < W;
+        pd[k] = bload8(dr, ok ? (uint32_t)((((n * H + oh) * W + ow) * Cout + cv * 4) * 2) : PTG_OOB);
       }
-      pd[k] = val;
     }
   };
   auto store_tile = [&](int nrows, int slot_first) {
@@ -794,15 +796,14 @@ __global__ __launch_bounds__(256, 5) void conv1_pair_pool_k(const bf16_t* __rest
     pr_c[p] = idx - pr_r[p] * HP;
   }
   U4 pf[PFN];
-  auto load_rows = [&](int n, int iw0, int ih_first, int nrows) {
-    const bf16_t* img = x + (long)n * H * W * C;
+  const Rsrc xr = make_rsrc(x, (uint32_t)((long)N * H * W * C * 2));
+  auto load_rows = [&](int n, int iw0, int ih_first, int nrows) {  // padding reads 0 (PTG_OOB)
+    const uint32_t img = (uint32_t)(n * H * W * C) * 2u;
 #pragma unroll
     for (int p = 0; p < PFN; ++p) {
-      U4 v = zero4();
       const int ih = ih_first + pr_r[p], iw = iw0 + 2 * pr_c[p];
-      if (pr_r[p] < nrows && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
-        v = *(const U4*)(img + ((long)ih * W + iw) * C);
-      pf[p] = v;
+      const bool ok = pr_r[p] < nrows && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+      pf[p] = bload16(xr, ok ? img + (uint32_t)((ih * W + iw) * C) * 2u : PTG_OOB);
     }
   };
   auto store_rows = [&](int nrows, int slot_first) {
@@ -1121,7 +1122,7 @@ extern "C" {
 // 3 = maxpool2x2(prelu(z)) into aux + argmax z into z ([N][H/2][W/2][Cout]) + argmax q into arg.
 int ptg_conv2d_fwd_halo(const void* x, const void* w, const float* bias, const float* alpha, void* z, void* aux, void* arg, int N,
                         int H, int W, int C, int Cout, int KS, int pad, int epi, hipStream_t s) {
-  if (Cout % 8 || Cout > 64) return (int)hipErrorInvalidValue;
+  if (Cout % 8 || Cout > 64 || !ptg_fits_2g((long)N * H * W * C * 2)) return (int)hipErrorInvalidValue;
   if ((epi == EPI_POOL || epi == EPI_POOLS) && ((H & 1) || (W & 1))) return (int)hipErrorInvalidValue;
   if (C == 4 && Cout == 8 && KS == 5 && (epi == EPI_POOL || epi == EPI_POOLS) && pad == 2 && conv1_pair_enabled()) {
     const auto kern = epi == EPI_POOLS ? conv1_pair_pool_k<5, true> : conv1_pair_pool_k<5, false>;
@@ -1143,7 +1144,8 @@ int ptg_conv2d_fwd_halo(const void* x, const void* w, const float* bias, const f
 // dw (fp32, [Cout][KS][KS][C]) += weight gradient; caller zeroes dw.
 int ptg_conv2d_wgrad_halo(const void* x, const void* dz, float* dw, int N, int H, int W, int C, int Cout, int KS,
                           int pad, hipStream_t s) {
-  if (Cout % 8 || Cout > 64) return (int)hipErrorInvalidValue;
+  if (Cout % 8 || Cout > 64 || !ptg_fits_2g((long)N * H * W * C * 2) || !ptg_fits_2g((long)N * H * W * Cout * 2))
+    return (int)hipErrorInvalidValue;
   const int MF = Cout <= 16 ? 1 : (Cout <= 32 ? 2 : 4);
 #define PTG_WG(KSV, MFV) return wgrad_by_cin<KSV, MFV>(x, dz, dw, N, H, W, C, Cout, pad, s)
   if (KS == 5) { if (MF == 1) PTG_WG(5, 1); if (MF == 2) PTG_WG(5, 2); PTG_WG(5, 4); }
@@ -1156,7 +1158,8 @@ int ptg_conv2d_wgrad_halo(const void* x, const void* dz, float* dw, int N, int H
 // only the 5x5 layers of the reference CNN (first layer: no dgrad needs a dense dZ) are instantiated.
 int ptg_conv2d_wgrad_halo_sparse(const void* x, const void* dzsel, const void* argq, float* dw, int N, int H, int W,
                                  int C, int Cout, int KS, int pad, hipStream_t s) {
-  if (Cout % 8 || Cout > 64 || KS != 5 || (H & 1) || (W & 1)) return (int)hipErrorInvalidValue;
+  if (Cout % 8 || Cout > 64 || KS != 5 || (H & 1) || (W & 1) || !ptg_fits_2g((long)N * H * W * C * 2))
+    return (int)hipErrorInvalidValue;
   const int MF = Cout <= 16 ? 1 : (Cout <= 32 ? 2 : 4);
   if (MF == 1) return wgrad_by_cin<5, 1, true>(x, dzsel, dw, N, H, W, C, Cout, pad, s, argq);
   if (MF == 2) return wgrad_by_cin<5, 2, true>(x, dzsel, dw, N, H, W, C, Cout, pad, s, argq);

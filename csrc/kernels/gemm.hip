@@ -38,18 +38,7 @@ constexpr int BK = 64;
 // offset OOB, which the hardware range check returns as 0 - no branch per load, no 64-bit address
 // arithmetic.  Operands must be smaller than 2 GiB (checked on the host).
 // ------------------------------------------------------------------------------------------
-constexpr uint32_t OOB = 0x80000000u;
-typedef __amdgpu_buffer_rsrc_t Rsrc;
-
-PTG_DEV Rsrc make_rsrc(const void* p, uint32_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
-}
-PTG_DEV U4 bload16(Rsrc r, uint32_t off) {
-  return __builtin_bit_cast(U4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
-}
-PTG_DEV U2 bload8(Rsrc r, uint32_t off) {
-  return __builtin_bit_cast(U2, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
-}
+constexpr uint32_t OOB = PTG_OOB;
 PTG_DEV U4 join(U2 a, U2 b) { U4 v; v.x = a.x; v.y = a.y; v.z = b.x; v.w = b.y; return v; }
 
 template <int VEC>
