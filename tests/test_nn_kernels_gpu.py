@@ -401,6 +401,18 @@ def test_losses_and_adam():
     _close(pb, p, 1e-2, 1e-2, "adam_bf16")
 
 
+@pytest.mark.parametrize("N,H,W,C", [(5, 64, 80, 128), (3, 7, 7, 2048), (256, 16, 20, 64), (2, 3, 5, 8)])
+def test_gap_fwd_bwd(N, H, W, C):
+    x = rnd(N, H, W, C)
+    g = torch.full((N, C), 3.0, device=DEV)
+    K.gap_fwd(x.to(DEV), g)
+    _close(g, x.float().mean((1, 2)), 1e-3, 1e-3, "gap_fwd")
+    dy = torch.randn(N, C)
+    dx = torch.empty(N, H, W, C, device=DEV, dtype=torch.bfloat16)
+    K.gap_bwd(dy.to(DEV), dx)
+    _close(dx, (dy / (H * W)).view(N, 1, 1, C).expand(N, H, W, C), 1e-2, 1e-6, "gap_bwd")
+
+
 def test_resize_norm_and_gap():
     imgs = torch.randint(0, 256, (2, 37, 45, 3), dtype=torch.uint8)
     out = torch.empty(2, 32, 40, 4, device=DEV, dtype=torch.bfloat16)
