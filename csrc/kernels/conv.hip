@@ -93,6 +93,27 @@ typedef __attribute__((ext_vector_type(2))) unsigned int vu2_t;
 template <int C> struct HVec { using T = vu4_t; static constexpr int per_pix = C / 8; };
 template <> struct HVec<4> { using T = vu2_t; static constexpr int per_pix = 1; };
 
+// Work queue of the persistent kernels: round 0 takes chunk `b` (the workgroup's own, no atomic: a
+// launch-wide burst of claims on one address serialises for tens of us), later rounds claim chunk
+// nb + counter++ once the previous chunk is done.  Every workgroup claims until it draws a chunk
+// >= nch: (nch - nb) successful claims + one failing claim per workgroup that owns a chunk = nch
+// claims in total, so the workgroup drawing the value nch - 1 re-arms the counter to 0 for the next
+// launch (graph replays included).  Returns the chunk (>= nch: done).
+PTG_DEV long wq_next(int* cnt, int round, int b, int nb, int nch, int* s_slot) {
+  if (round == 0) return b;
+  if (b >= nch) return nch;  // no own chunk: never claimed (keeps the claim count at nch)
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int v = atomicAdd(cnt, 1);
+    if (v == nch - 1) atomicExch(cnt, 0);
+    *s_slot = v;
+  }
+  __syncthreads();
+  const long c = (long)nb + *s_slot;
+  __syncthreads();
+  return c;
+}
+
 template <class VT> PTG_DEV VT bload_vt(Rsrc r, uint32_t off);
 template <> PTG_DEV vu4_t bload_vt<vu4_t>(Rsrc r, uint32_t off) {
   return __builtin_bit_cast(vu4_t, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
@@ -116,7 +137,8 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
                                                         const float* __restrict__ bias, const float* __restrict__ alpha,
                                                         bf16_t* __restrict__ z, bf16_t* __restrict__ aux,
                                                         uint8_t* __restrict__ argout, int N, int H,
-                                                        int W, int Cout, int pad, int tiles_h, int tiles_w) {
+                                                        int W, int Cout, int pad, int tiles_h, int tiles_w,
+                                                        int* __restrict__ wq, int wchunk) {
   using VT = typename HVec<C>::T;
   constexpr int VPP = HVec<C>::per_pix;      // vectors per pixel
   constexpr int VE = C == 4 ? 4 : 8;          // elements per vector
@@ -268,10 +290,24 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
     }
   }
 
-  // this workgroup's contiguous range of tiles, strip-major (balanced to within one tile)
+  // Tile ranges, strip-major: static (this workgroup's contiguous 1/nblk of the tiles) or, with a
+  // work queue `wq`, chunks of `wchunk` tiles claimed until none is left - a workgroup that starts
+  // late (CUs held by a concurrent RCCL kernel) then takes less work instead of a full range.
   const long T = (long)S * tiles_h;
-  const int t0 = (int)(T * bid / nblk), t1 = (int)(T * (bid + 1) / nblk);
-  if (t0 >= t1) return;
+  __shared__ int s_wq;
+  for (int round = 0;; ++round) {
+  int t0, t1;
+  if (wq) {
+    const long c = wq_next(wq + (COS > 1 ? (int)(blockIdx.x % COS) : 0), round, bid, nblk, (int)((T + wchunk - 1) / wchunk),
+                           &s_wq);
+    t0 = (int)min(T, c * wchunk);
+    t1 = (int)min(T, (c + 1) * wchunk);
+  } else {
+    if (round) break;
+    t0 = (int)(T * bid / nblk);
+    t1 = (int)(T * (bid + 1) / nblk);
+  }
+  if (t0 >= t1) break;
   int s = t0 / tiles_h, th = t0 - s * tiles_h;
   {  // first tile: synchronous fill of its HR rows
     const int n = s / tiles_w, ow0 = (s - n * tiles_w) * TW;
@@ -510,6 +546,7 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
     s = s2;
     th = th2;
   }
+  }  // work rounds
 }
 
 // ================================================================================================
@@ -534,7 +571,8 @@ template <int C, int KS, int TW, int TH, int MF, int NB, bool RING, bool SPARSE 
 __global__ __launch_bounds__(256) void conv_wgrad_strip_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dz,
                                                           float* __restrict__ dw, int N, int H, int W, int Cout, int pad,
                                                           int tiles_h, int tiles_w, int nslices,
-                                                          const uint8_t* __restrict__ argq = nullptr) {
+                                                          const uint8_t* __restrict__ argq, int* __restrict__ wq,
+                                                          int wchunk) {
   using VT = typename HVec<C>::T;
   constexpr int VPP = HVec<C>::per_pix, VE = C == 4 ? 4 : 8;
   constexpr int PIX = PixPitch<C>::v;
@@ -558,8 +596,6 @@ __global__ __launch_bounds__(256) void conv_wgrad_strip_k(const bf16_t* __restri
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int slice = blockIdx.x % nslices, chunk = blockIdx.x / nslices, nchunks = gridDim.x / nslices;
   const long T = (long)N * tiles_w * tiles_h;
-  const int t0 = (int)(T * chunk / nchunks), t1 = (int)(T * (chunk + 1) / nchunks);
-  if (t0 >= t1) return;
 
   const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
   // per-lane B column (kflat) base of each of this wave's NB fragments
@@ -661,6 +697,22 @@ __global__ __launch_bounds__(256) void conv_wgrad_strip_k(const bf16_t* __restri
     }
   };
 
+  // static range or work-queue chunks (see conv_fwd_strip_k); partial sums stay in registers across
+  // every chunk this workgroup claims and are flushed once
+  __shared__ int s_wq;
+  for (int round = 0;; ++round) {
+  int t0, t1;
+  if (wq) {
+    __syncthreads();  // the previous chunk's LDS reads are done before its refill
+    const long c = wq_next(wq + slice, round, chunk, nchunks, (int)((T + wchunk - 1) / wchunk), &s_wq);
+    t0 = (int)min(T, c * wchunk);
+    t1 = (int)min(T, (c + 1) * wchunk);
+  } else {
+    if (round) break;
+    t0 = (int)(T * chunk / nchunks);
+    t1 = (int)(T * (chunk + 1) / nchunks);
+  }
+  if (t0 >= t1) break;
   int s = t0 / tiles_h, th = t0 - s * tiles_h;
   load_tile(s, th, HR, th * TH - pad);
   store_tile(HR, RING ? (th * TH) % HR : 0);
@@ -712,6 +764,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_strip_k(const bf16_t* __restri
     s = s2;
     th = th2;
   }
+  }  // work rounds
   // epilogue: rows = co ((lane>>4)*4 + r), cols = kflat (lane & 15)
 #pragma unroll
   for (int i = 0; i < MF; ++i)
@@ -749,7 +802,8 @@ __global__ __launch_bounds__(256, 5) void conv1_pair_pool_k(const bf16_t* __rest
                                                          const float* __restrict__ bias, const float* __restrict__ alpha,
                                                          bf16_t* __restrict__ z, bf16_t* __restrict__ pooled,
                                                          uint8_t* __restrict__ argout, int N, int H,
-                                                         int W, int pad, int tiles_h, int tiles_w) {
+                                                         int W, int pad, int tiles_h, int tiles_w,
+                                                         int* __restrict__ wq, int wchunk) {
   constexpr int C = 4, TW = 64, TH = 4;
   constexpr int KWP = KS + 1;
   static_assert((KWP * C) % 8 == 0 && TH < 2 * (KS - 1), "pair layout needs KS odd >= 5");
@@ -822,8 +876,19 @@ __global__ __launch_bounds__(256, 5) void conv1_pair_pool_k(const bf16_t* __rest
   const int hf = wid & 1, rp = wid >> 1;   // this wave: columns hf*32.., rows 2*rp, 2*rp+1
   const int S = N * tiles_w;
   const long T = (long)S * tiles_h;
-  const int t0 = (int)(T * blockIdx.x / gridDim.x), t1 = (int)(T * (blockIdx.x + 1) / gridDim.x);
-  if (t0 >= t1) return;
+  __shared__ int s_wq;
+  for (int round = 0;; ++round) {  // static range, or work-queue chunks (see conv_fwd_strip_k)
+  int t0, t1;
+  if (wq) {
+    const long c = wq_next(wq, round, blockIdx.x, gridDim.x, (int)((T + wchunk - 1) / wchunk), &s_wq);
+    t0 = (int)min(T, c * wchunk);
+    t1 = (int)min(T, (c + 1) * wchunk);
+  } else {
+    if (round) break;
+    t0 = (int)(T * blockIdx.x / gridDim.x);
+    t1 = (int)(T * (blockIdx.x + 1) / gridDim.x);
+  }
+  if (t0 >= t1) break;
   int s = t0 / tiles_h, th = t0 - s * tiles_h;
   {
     const int n = s / tiles_w, ow0 = (s - n * tiles_w) * TW;
@@ -923,6 +988,7 @@ __global__ __launch_bounds__(256, 5) void conv1_pair_pool_k(const bf16_t* __rest
     s = s2;
     th = th2;
   }
+  }  // work rounds
 }
 
 // W'[ci][kh][kw][co] = W[co][KS-1-kh][KS-1-kw][ci]
@@ -956,6 +1022,47 @@ __global__ __launch_bounds__(256) void conv_flip4_k(FlipJobs J) {
 // host dispatch
 // ------------------------------------------------------------------------------------------------
 // workgroups of `kernel` (256 threads) that fit on the device at once (cached per kernel)
+// Persistent grids are sized to OVERSUB x the resident workgroups: when another stream's kernel (an
+// RCCL collective overlapping the backward on a multi-GPU node) holds some CUs, the workgroups that
+// cannot start until a slot frees carry 1/OVERSUB of a full range instead of a whole one, bounding
+// the tail.  PTG_PERSIST_OVERSUB (default 1: measured 122.7k vs 117.3k samples/s at 2 on an idle GPU) sets it.
+static int persist_oversub() {
+  static const int v = [] {
+    const char* e = getenv("PTG_PERSIST_OVERSUB");
+    const int k = e ? atoi(e) : 1;
+    return k < 1 ? 1 : (k > 8 ? 8 : k);
+  }();
+  return v;
+}
+
+// Work-queue mode of the persistent kernels (off: static ranges; on: the data-parallel strategies
+// switch it on when RCCL collectives overlap the backward).  The queue counters live in one small
+// device buffer allocated and zeroed on the first (eager) launch; kernels re-arm them (wq_next).
+static int g_persist_dynamic = -1;
+static bool persist_dynamic() {
+  if (g_persist_dynamic < 0) {
+    const char* e = getenv("PTG_PERSIST_DYNAMIC");
+    g_persist_dynamic = (e && e[0] == '1') ? 1 : 0;
+  }
+  return g_persist_dynamic == 1;
+}
+// queue counters (one per channel group / weight slice), zeroed once; every launch leaves them at 0
+static int* work_queue(int slots, hipStream_t s) {
+  (void)s;
+  static int* buf = nullptr;
+  if (!buf) {
+    if (hipMalloc(&buf, 64 * sizeof(int)) != hipSuccess || hipMemset(buf, 0, 64 * sizeof(int)) != hipSuccess)
+      buf = nullptr;
+  }
+  return (buf && slots <= 64) ? buf : nullptr;
+}
+// tiles per claimed chunk: ~4 chunks per workgroup, at least 4 tiles (each chunk restarts the halo;
+// 8 per workgroup cost 14% on CNN-B1 with the claim not yet prefetched)
+static int wq_chunk(long tiles, int groups) {
+  long c = tiles / ((long)groups * 4);
+  return (int)(c < 4 ? 4 : c);
+}
+
 static int resident_blocks(const void* kernel) {
   static int cus = 0;
   if (!cus) {
@@ -982,9 +1089,10 @@ static int launch_fwd_k(const void* x, const void* w, const float* bias, const f
   const long tiles = (long)N * tw * th;
   // persistent: one wave of resident workgroups, each walking a contiguous range of tiles
   // (COS groups of workgroups each cover all tiles for their slice of output channels)
-  const int grid = (int)std::min<long>(tiles * COS, resident / COS * COS);
+  const int grid = (int)std::min<long>(tiles * COS, (long)resident * persist_oversub() / COS * COS);
+  int* wq = persist_dynamic() ? work_queue(COS, s) : nullptr;
   hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, (const bf16_t*)x, (const bf16_t*)w, bias, alpha, (bf16_t*)z,
-                     (bf16_t*)aux, (uint8_t*)arg, N, H, W, Cout, pad, th, tw);
+                     (bf16_t*)aux, (uint8_t*)arg, N, H, W, Cout, pad, th, tw, wq, wq_chunk(tiles, grid / COS));
   PTG_RETURN_LAUNCH();
 }
 
@@ -1081,10 +1189,11 @@ static int launch_wgrad(const void* x, const void* dz, float* dw, int N, int H, 
   const int th = (H + TH - 1) / TH, tw = (W + TW - 1) / TW;
   const long tiles = (long)N * tw * th;
   const int nslices = (KF + 64 * NB - 1) / (64 * NB);
-  int chunks = (resident + nslices - 1) / nslices;
+  int chunks = (resident * persist_oversub() + nslices - 1) / nslices;
   if (chunks > tiles) chunks = (int)tiles;
+  int* wq = persist_dynamic() ? work_queue(nslices, s) : nullptr;
   hipLaunchKernelGGL(kern, dim3(chunks * nslices), dim3(256), 0, s, (const bf16_t*)x, (const bf16_t*)dz, dw, N, H, W,
-                     Cout, pad, th, tw, nslices, (const uint8_t*)argq);
+                     Cout, pad, th, tw, nslices, (const uint8_t*)argq, wq, wq_chunk(tiles, chunks));
   PTG_RETURN_LAUNCH();
 }
 
@@ -1131,9 +1240,10 @@ int ptg_conv2d_fwd_halo(const void* x, const void* w, const float* bias, const f
     const int resident = epi == EPI_POOLS ? res_sparse : res_dense;
     const int th = (H + 3) / 4, tw = (W + 63) / 64;
     const long tiles = (long)N * th * tw;
-    const int grid = (int)std::min<long>(tiles, resident);
+    const int grid = (int)std::min<long>(tiles, (long)resident * persist_oversub());
+    int* wq = persist_dynamic() ? work_queue(1, s) : nullptr;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, (const bf16_t*)x, (const bf16_t*)w, bias, alpha, (bf16_t*)z,
-                       (bf16_t*)aux, (uint8_t*)arg, N, H, W, pad, th, tw);
+                       (bf16_t*)aux, (uint8_t*)arg, N, H, W, pad, th, tw, wq, wq_chunk(tiles, grid));
     PTG_RETURN_LAUNCH();
   }
   if (KS == 5) return fwd_by_cin<5>(x, w, bias, alpha, z, aux, arg, N, H, W, C, Cout, pad, epi, s);
@@ -1164,6 +1274,14 @@ int ptg_conv2d_wgrad_halo_sparse(const void* x, const void* dzsel, const void* a
   if (MF == 1) return wgrad_by_cin<5, 1, true>(x, dzsel, dw, N, H, W, C, Cout, pad, s, argq);
   if (MF == 2) return wgrad_by_cin<5, 2, true>(x, dzsel, dw, N, H, W, C, Cout, pad, s, argq);
   return wgrad_by_cin<5, 4, true>(x, dzsel, dw, N, H, W, C, Cout, pad, s, argq);
+}
+
+// dynamic: 1 = persistent conv kernels claim tile chunks from a work queue, 0 = static ranges,
+// -1 = PTG_PERSIST_DYNAMIC (default static).
+int ptg_set_persist_mode(int dynamic, hipStream_t s) {
+  (void)s;
+  g_persist_dynamic = dynamic < 0 ? -1 : (dynamic ? 1 : 0);
+  return 0;
 }
 
 int ptg_conv_flip_weights4(int n, const void* w0, void* wf0, int Cout0, int KS0, int Cin0, const void* w1, void* wf1,

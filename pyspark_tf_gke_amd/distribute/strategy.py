@@ -217,6 +217,11 @@ class MultiWorkerMirroredStrategy(Strategy):
         self.sharded_update = bool(sharded_update) and self.world_size > 1
         self._works: list = []
         self._launched = 0
+        if self.world_size > 1 and self.device.type == "cuda" and os.environ.get("PTG_PERSIST_DYNAMIC") is None:
+            # reduce-scatter / all-gather kernels run beside the backward: work-queue conv kernels
+            from ..ops import nn as K
+
+            K.set_persist_mode(True)
 
     def register_model(self, model) -> None:
         if self.sharded_update:

@@ -178,6 +178,15 @@ def conv2d_wgrad_halo_sparse(x, dzsel, arg, pad: int, out, zeroed: bool = False)
     return out
 
 
+def set_persist_mode(dynamic: bool | None) -> None:
+    """Persistent conv kernels: True = claim tile chunks from a work queue (robust when another
+    stream's kernels, e.g. RCCL collectives overlapping the backward, hold CUs), False = static
+    per-workgroup ranges (fastest on an idle GPU), None = the PTG_PERSIST_DYNAMIC default."""
+    if not torch.cuda.is_available():
+        return
+    hip("ptg_set_persist_mode", -1 if dynamic is None else int(bool(dynamic)))
+
+
 def conv_flip_weights(w, out):
     """out[Cin][KS][KS][Cout] = w[Cout][KS-1-kh][KS-1-kw][Cin] (dgrad filter)."""
     Cout, KS, _, Cin = w.shape

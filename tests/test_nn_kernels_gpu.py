@@ -267,6 +267,33 @@ def test_first_layer_sparse_chain_matches_dense(monkeypatch):
         _close(grads[True][name], g, 2e-2, 1e-3, "sel_grad_" + name)
 
 
+@pytest.mark.parametrize("N,H,W,C,Co,epi", [(16, 256, 320, 4, 8, "pools"), (32, 128, 160, 8, 16, "pool"),
+                                             (64, 64, 80, 16, 32, "pool"), (256, 16, 20, 64, 64, "prelu")])
+def test_persistent_work_queue_matches_static(N, H, W, C, Co, epi):
+    """Work-queue (dynamic chunk) mode of the persistent conv kernels == static ranges: identical
+    forward outputs, weight gradients equal up to summation order."""
+    x, w, b = rnd(N, H, W, C).to(DEV), rnd(Co, 5, 5, C, scale=0.2).to(DEV), torch.randn(Co).to(DEV)
+    alpha = (torch.rand(H, W, Co) * 0.3).to(DEV)
+    dz = rnd(N, H, W, Co, scale=0.1).to(DEV)
+    outs = {}
+    try:
+        for dyn in (False, True):
+            K.set_persist_mode(dyn)
+            shp = (N, H // 2, W // 2, Co) if epi in ("pool", "pools") else (N, H, W, Co)
+            zs = torch.empty(shp if epi == "pools" else (N, H, W, Co), device=DEV, dtype=torch.bfloat16)
+            aux = torch.empty(shp, device=DEV, dtype=torch.bfloat16)
+            arg = torch.empty(shp, device=DEV, dtype=torch.uint8) if epi == "pools" else None
+            K.conv2d_fwd_fused(x, w, b, 2, zs, alpha, aux, epi, arg)
+            dw = torch.zeros(Co, 5, 5, C, device=DEV)
+            K.conv2d_wgrad_halo(x, dz, 2, dw)
+            torch.cuda.synchronize()
+            outs[dyn] = (zs.cpu(), aux.cpu(), dw.cpu())
+    finally:
+        K.set_persist_mode(None)
+    assert torch.equal(outs[False][0], outs[True][0]) and torch.equal(outs[False][1], outs[True][1])
+    _close(outs[True][2], outs[False][2], 1e-4, 1e-4, "wq_wgrad")
+
+
 def test_conv_flip_weights_multi():
     """One launch flipping several dgrad filters == the per-layer flip (and the reference permute)."""
     shapes = [(8, 5, 5, 4), (16, 5, 5, 8), (32, 5, 5, 16), (64, 5, 5, 32), (64, 3, 3, 64)]
