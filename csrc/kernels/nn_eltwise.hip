@@ -12,6 +12,8 @@
 // 4-channel padded image.
 #include "common.h"
 
+#include <type_traits>
+
 // ----------------------------------------------------------------------------------------------
 // PReLU + 2x2 max-pool forward: p[n][ph][pw][c] = max_{2x2} prelu(z), prelu(z) = z>0 ? z : a*z.
 // ----------------------------------------------------------------------------------------------
@@ -196,128 +198,146 @@ __global__ __launch_bounds__(256) void prelu_pool_bwd_k(const bf16_t* __restrict
 // the sample groups in LDS.  Large layers run one chunk (dalpha += without atomics: no other block
 // touches those elements); small layers split the batch over a few chunks and add with atomics.
 // (prelu_pool_bwd_k adds every block's dalpha partial with fp32 atomics: ~17M per layer at batch 256.)
-__global__ __launch_bounds__(256) void prelu_pool_bwd_sg_k(const bf16_t* __restrict__ dp,
+template <int CH>
+__global__ __launch_bounds__(256, 4) void prelu_pool_bwd_sg_k(const bf16_t* __restrict__ dp,
                                                            const bf16_t* __restrict__ z,
                                                            const float* __restrict__ alpha,
                                                            bf16_t* __restrict__ dz, float* __restrict__ dalpha,
                                                            float* __restrict__ dbias, int N, int H, int W,
                                                            int C, int nper) {
-  constexpr int PB = 16, SG = 16, RP = 33;  // RP: padded LDS row (bank-conflict free writes)
+  // CH channels per thread (4: every per-thread array halves - 4 window positions x CH alphas and
+  // dalpha sums - so the kernel runs 4 waves per SIMD instead of 2 at CH = 8 with 255 VGPRs)
+  constexpr int PB = 16, SG = 16, NV = 4 * CH, RP = NV + 1;
+  using V = typename std::conditional<CH == 8, U4, U2>::type;
   __shared__ float sda[SG * PB * RP];
   __shared__ float sdb[256];
-  const int PH = H >> 1, PW = W >> 1, C8 = C >> 3;
-  const int npos = PH * PW * C8;
+  const int PH = H >> 1, PW = W >> 1, CG = C / CH;
+  const int npos = PH * PW * CG;
   const int pl = threadIdx.x & (PB - 1), sg = threadIdx.x / PB;
   const int i = blockIdx.x * PB + pl;
   const int n0 = blockIdx.y * nper, n1 = min(N, n0 + nper);
   const bool active = i < npos;
-  const int c8 = active ? i % C8 : 0;
-  const int t = active ? i / C8 : 0;
+  const int cg = active ? i % CG : 0;
+  const int t = active ? i / CG : 0;
   const int pw = t % PW, ph = t / PW;
-  long zoff[4];
+  uint32_t zoff[4];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) zoff[q] = ((long)(2 * ph + (q >> 1)) * W + 2 * pw + (q & 1)) * C + c8 * 8;
-  const long HWC = (long)H * W * C, PHWC = (long)PH * PW * C;
-  const long poff = ((long)ph * PW + pw) * C + c8 * 8;
-  float da[4][8], db[8];
+  for (int q = 0; q < 4; ++q) zoff[q] = (uint32_t)(((2 * ph + (q >> 1)) * W + 2 * pw + (q & 1)) * C + cg * CH);
+  const uint32_t HWC = (uint32_t)(H * W * C), PHWC = (uint32_t)(PH * PW * C);
+  const uint32_t poff = (uint32_t)((ph * PW + pw) * C + cg * CH);
+  float da[4][CH], db[CH];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) db[j] = 0.f;
+  for (int j = 0; j < CH; ++j) db[j] = 0.f;
 #pragma unroll
   for (int q = 0; q < 4; ++q)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) da[q][j] = 0.f;
+    for (int j = 0; j < CH; ++j) da[q][j] = 0.f;
   if ((int)threadIdx.x < C) sdb[threadIdx.x] = 0.f;
+  auto bload = [](Rsrc r, uint32_t off) -> V {
+    if constexpr (CH == 8) return bload16(r, off); else return bload8(r, off);
+  };
   if (active) {
-    float av[4][8];
+    float av[4][CH];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float4 a0 = *(const float4*)(alpha + zoff[q]), a1 = *(const float4*)(alpha + zoff[q] + 4);
-      av[q][0] = a0.x; av[q][1] = a0.y; av[q][2] = a0.z; av[q][3] = a0.w;
-      av[q][4] = a1.x; av[q][5] = a1.y; av[q][6] = a1.z; av[q][7] = a1.w;
-    }
-    const bool lastw = (W & 1) && pw == PW - 1, lasth = (H & 1) && ph == PH - 1;
-    for (int n = n0 + sg; n < n1; n += 2 * SG) {
-      const bool two = n + SG < n1;
-      U4 graw[2], zraw[2][4];
+    for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int nn = (u == 0 || two) ? n + u * SG : n;
-        graw[u] = *(const U4*)(dp + nn * PHWC + poff);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) zraw[u][q] = *(const U4*)(z + nn * HWC + zoff[q]);
+      for (int j = 0; j < CH; j += 4) {
+        const float4 a4 = *(const float4*)(alpha + zoff[q] + j);
+        av[q][j] = a4.x; av[q][j + 1] = a4.y; av[q][j + 2] = a4.z; av[q][j + 3] = a4.w;
       }
+    const bool lastw = (W & 1) && pw == PW - 1, lasth = (H & 1) && ph == PH - 1;
+    const Rsrc dpr = make_rsrc(dp, (uint32_t)N * PHWC * 2u), zr = make_rsrc(z, (uint32_t)N * HWC * 2u);
+    // one sample per iteration with the next sample's 5 loads in flight during this one's math
+    V gc, zc[4];
+    auto ld = [&](int nn, V& gq, V* zq) {
+      gq = bload(dpr, ((uint32_t)nn * PHWC + poff) * 2u);
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        if (u == 1 && !two) break;
-        const long nb = (long)(n + u * SG) * HWC;
-        float g[8], zv[4][8], y[4][8];
-        unpack8(graw[u], g);
+      for (int q = 0; q < 4; ++q) zq[q] = bload(zr, ((uint32_t)nn * HWC + zoff[q]) * 2u);
+    };
+    if (n0 + sg < n1) ld(n0 + sg, gc, zc);
+    for (int n = n0 + sg; n < n1; n += SG) {
+      V gn, zn[4];
+      ld(min(n + SG, n1 - 1), gn, zn);
+      const uint32_t* gw = (const uint32_t*)&gc;
+      uint32_t ow[4][CH / 2];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          unpack8(zraw[u][q], zv[q]);
+      for (int w = 0; w < CH / 2; ++w) {
+        float ov[2][4];
 #pragma unroll
-          for (int j = 0; j < 8; ++j) y[q][j] = zv[q][j] > 0.f ? zv[q][j] : av[q][j] * zv[q][j];
-        }
-        int arg[8];
+        for (int h = 0; h < 2; ++h) {
+          const int jj = 2 * w + h;
+          const float gj = h ? hi_bf(gw[w]) : lo_bf(gw[w]);
+          float zq[4], yq[4];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          int a = 0; float b = y[0][j];
+          for (int q = 0; q < 4; ++q) {
+            const uint32_t word = ((const uint32_t*)&zc[q])[w];
+            zq[q] = h ? hi_bf(word) : lo_bf(word);
+            yq[q] = zq[q] > 0.f ? zq[q] : av[q][jj] * zq[q];
+          }
+          int a = 0;
+          float b = yq[0];
 #pragma unroll
           for (int q = 1; q < 4; ++q)
-            if (y[q][j] > b) { b = y[q][j]; a = q; }
-          arg[j] = a;
+            if (yq[q] > b) { b = yq[q]; a = q; }  // first maximum in q order, as the forward's pool
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float gq = a == q ? gj : 0.f;
+            const bool pos = zq[q] > 0.f;
+            ov[h][q] = pos ? gq : gq * av[q][jj];
+            da[q][jj] += pos ? 0.f : gq * zq[q];
+            db[jj] += ov[h][q];
+          }
         }
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          float o[8];
+        for (int q = 0; q < 4; ++q) ow[q][w] = pack_bf(ov[0][q], ov[1][q]);
+      }
+      const long nb = (long)n * HWC;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float gq = (arg[j] == q) ? g[j] : 0.f;
-            const float zz = zv[q][j];
-            o[j] = zz > 0.f ? gq : gq * av[q][j];
-            da[q][j] += zz > 0.f ? 0.f : gq * zz;
-            db[j] += o[j];
-          }
-          *(U4*)(dz + nb + zoff[q]) = pack8(o);
+      for (int q = 0; q < 4; ++q) {
+        V o;
+#pragma unroll
+        for (int w = 0; w < CH / 2; ++w) ((uint32_t*)&o)[w] = ow[q][w];
+        *(V*)(dz + nb + zoff[q]) = o;
+      }
+      gc = gn;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) zc[q] = zn[q];
+      if (lastw || lasth) {  // odd H / W: the row / column outside every window gets zero gradient
+        V zz;
+#pragma unroll
+        for (int w = 0; w < CH / 2; ++w) ((uint32_t*)&zz)[w] = 0u;
+        bf16_t* d = dz + nb + cg * CH;
+        if (lastw) {
+          *(V*)(d + ((long)(2 * ph) * W + W - 1) * C) = zz;
+          *(V*)(d + ((long)(2 * ph + 1) * W + W - 1) * C) = zz;
         }
-        if (lastw || lasth) {
-          const U4 zz = zero4();
-          bf16_t* d = dz + nb + c8 * 8;
-          if (lastw) {
-            *(U4*)(d + ((long)(2 * ph) * W + W - 1) * C) = zz;
-            *(U4*)(d + ((long)(2 * ph + 1) * W + W - 1) * C) = zz;
-          }
-          if (lasth) {
-            *(U4*)(d + ((long)(H - 1) * W + 2 * pw) * C) = zz;
-            *(U4*)(d + ((long)(H - 1) * W + 2 * pw + 1) * C) = zz;
-          }
-          if (lastw && lasth) *(U4*)(d + ((long)(H - 1) * W + W - 1) * C) = zz;
+        if (lasth) {
+          *(V*)(d + ((long)(H - 1) * W + 2 * pw) * C) = zz;
+          *(V*)(d + ((long)(H - 1) * W + 2 * pw + 1) * C) = zz;
         }
+        if (lastw && lasth) *(V*)(d + ((long)(H - 1) * W + W - 1) * C) = zz;
       }
     }
   }
 #pragma unroll
   for (int q = 0; q < 4; ++q)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) sda[(sg * PB + pl) * RP + q * 8 + j] = da[q][j];
+    for (int j = 0; j < CH; ++j) sda[(sg * PB + pl) * RP + q * CH + j] = da[q][j];
   __syncthreads();
-  // bias: LDS atomics per channel, then one global atomic per channel and block
-  if (active) {
+  if (active) {  // bias: LDS atomics per channel, then one global atomic per channel and block
 #pragma unroll
-    for (int j = 0; j < 8; ++j) atomicAdd(&sdb[c8 * 8 + j], db[j]);
+    for (int j = 0; j < CH; ++j) atomicAdd(&sdb[cg * CH + j], db[j]);
   }
-  // dalpha: 16 positions x 32 values per block; thread handles 2 of the 512 sums over sample groups
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int o = h * 256 + threadIdx.x;
-    const int p = o >> 5, k = o & 31, q = k >> 3, j = k & 7;
+  // dalpha: PB positions x NV values per block, summed over the sample groups
+  for (int o = threadIdx.x; o < PB * NV; o += 256) {
+    const int p = o / NV, k = o % NV, q = k / CH, j = k % CH;
     float sum = 0.f;
 #pragma unroll
     for (int gsg = 0; gsg < SG; ++gsg) sum += sda[(gsg * PB + p) * RP + k];
     const int ii = blockIdx.x * PB + p;
     if (ii < npos) {
-      const int cc = ii % C8, tq = ii / C8, pww = tq % PW, phh = tq / PW;
-      float* dst = dalpha + ((long)(2 * phh + (q >> 1)) * W + 2 * pww + (q & 1)) * C + cc * 8 + j;
+      const int cc = ii % CG, tq = ii / CG, pww = tq % PW, phh = tq / PW;
+      float* dst = dalpha + ((long)(2 * phh + (q >> 1)) * W + 2 * pww + (q & 1)) * C + cc * CH + j;
       if (gridDim.y == 1) *dst += sum;
       else atomicAdd(dst, sum);
     }
@@ -1069,8 +1089,8 @@ int ptg_prelu_pool_bwd(const void* dp, const void* z, const float* alpha, void* 
 
 int ptg_prelu_pool_bwd2(const void* dp, const void* z, const float* alpha, void* dz, float* dalpha,
                         float* dbias, int N, int H, int W, int C, int nper, hipStream_t s) {
-  if (C % 8 || C > 256 || H < 2 || W < 2) return (int)hipErrorInvalidValue;
-  const int npos = (H / 2) * (W / 2) * (C / 8);
+  if (C % 8 || C > 256 || H < 2 || W < 2 || !ptg_fits_2g((long)N * H * W * C * 2)) return (int)hipErrorInvalidValue;
+  const int npos = (H / 2) * (W / 2) * (C / 4);
   const int bx = (npos + 15) / 16;
   if (nper <= 0) {  // >= ~1024 blocks, but at least 64 samples (4 per sample group) per chunk
     int chunks = (1024 + bx - 1) / bx;
@@ -1078,7 +1098,7 @@ int ptg_prelu_pool_bwd2(const void* dp, const void* z, const float* alpha, void*
     nper = (N + chunks - 1) / chunks;
   }
   dim3 grid(bx, (N + nper - 1) / nper);
-  hipLaunchKernelGGL(prelu_pool_bwd_sg_k, grid, dim3(256), 0, s, (const bf16_t*)dp, (const bf16_t*)z, alpha,
+  hipLaunchKernelGGL(prelu_pool_bwd_sg_k<4>, grid, dim3(256), 0, s, (const bf16_t*)dp, (const bf16_t*)z, alpha,
                      (bf16_t*)dz, dalpha, dbias, N, H, W, C, nper);
   PTG_RETURN_LAUNCH();
 }
