@@ -180,14 +180,16 @@ class _BNState:
         bn = self.bn
         C = z.shape[-1]
         M = z.numel() // C
-        part, _, _, mean, rstd, coef = self.bufs(ws, C, z.device)
-        KB.bn_bwd_reduce(dy, y, z, relu, part)
+        part, scale, shift, mean, rstd, coef = self.bufs(ws, C, z.device)
+        # no residual was added before the ReLU: its mask is z*scale+shift > 0, y need not be read
+        sc, sh = (scale, shift) if (relu and dres is None) else (None, None)
+        KB.bn_bwd_reduce(dy, y, z, relu, part, sc, sh)
         KB.bn_bwd_finalize(part, M, bn.gamma.data if bn.gamma is not None else None, mean, rstd,
                            bn.gamma.grad if bn.gamma is not None else None,
                            bn.beta.grad if bn.beta is not None else None, coef)
         if not K.on_device(z):
             part.zero_()
-        return KB.bn_bwd_apply(dy, y, z, coef, relu, dz, dres)
+        return KB.bn_bwd_apply(dy, y, z, coef, relu, dz, dres, sc, sh)
 
 
 class ConvBNOp:

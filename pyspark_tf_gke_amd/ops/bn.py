@@ -77,17 +77,28 @@ def bn_apply(z, scale, shift, res, relu: bool, y):
     return y
 
 
-def bn_bwd_reduce(dy, y, z, relu: bool, part):
+def _relu_mask(y, z, scale, shift, M, C):
+    """ReLU mask of the BN output: from y, or (mask_from_z) recomputed as z*scale+shift > 0."""
+    if scale is not None:
+        zf = z.float().reshape(M, C)
+        return torch.addcmul(shift.view(1, C), zf, scale.view(1, C)) > 0
+    return y.float().reshape(M, C) > 0
+
+
+def bn_bwd_reduce(dy, y, z, relu: bool, part, scale=None, shift=None):
+    """part += (sum g, sum g*z) with g = dy masked by the ReLU.  With ``scale``/``shift`` (a BN with
+    no residual input) the mask is recomputed from z and ``y`` is not read."""
     C = z.shape[-1]
     M = z.numel() // C
     if not on_device(z):
         g = dy.float().reshape(M, C)
         if relu:
-            g = g * (y.float().reshape(M, C) > 0)
+            g = g * _relu_mask(y, z, scale, shift, M, C)
         part[0, 0] += g.sum(0)
         part[0, 1] += (g * z.float().reshape(M, C)).sum(0)
         return part
-    hip("ptg_bn_bwd_reduce", ptr(dy), ptr(y), ptr(z), M, C, int(relu), ptr(part))
+    mode = 0 if not relu else (2 if scale is not None else 1)
+    hip("ptg_bn_bwd_reduce", ptr(dy), ptr(y), ptr(z), M, C, mode, ptr(part), ptr(scale), ptr(shift))
     return part
 
 
@@ -114,18 +125,20 @@ def bn_bwd_finalize(part, M: int, gamma, mean, rstd, dgamma, dbeta, coef):
     return coef
 
 
-def bn_bwd_apply(dy, y, z, coef, relu: bool, dz, dres=None):
+def bn_bwd_apply(dy, y, z, coef, relu: bool, dz, dres=None, scale=None, shift=None):
     C = z.shape[-1]
     M = z.numel() // C
     if not on_device(z):
         g = dy.float()
         if relu:
-            g = g * (y.float() > 0)
+            g = g * _relu_mask(y, z, scale, shift, M, C).reshape(g.shape)
         if dres is not None:
             dres.copy_(g.to(dres.dtype))
         dz.copy_((coef[0] * g + coef[1] * z.float() + coef[2]).to(dz.dtype))
         return dz
-    hip("ptg_bn_bwd_apply", ptr(dy), ptr(y), ptr(z), ptr(coef), int(relu), ptr(dz), ptr(dres), M, C)
+    mode = 0 if not relu else (2 if scale is not None else 1)
+    hip("ptg_bn_bwd_apply", ptr(dy), ptr(y), ptr(z), ptr(coef), mode, ptr(dz), ptr(dres), M, C, ptr(scale),
+        ptr(shift))
     return dz
 
 

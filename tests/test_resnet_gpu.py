@@ -56,6 +56,33 @@ def test_bn_forward_backward(M, C):
         assert _rel(out[DEV][k], out["cpu"][k]) < 2e-2, k
 
 
+@pytest.mark.parametrize("M,C", [(4096, 64), (1000, 256), (392, 2048)])
+def test_bn_backward_mask_from_z(M, C):
+    """BN without a residual: the ReLU mask recomputed from z (y not read) == the mask from y."""
+    torch.manual_seed(5)
+    z = (torch.randn(M, C) * 2 + 0.3).to(torch.bfloat16).to(DEV)
+    dy = torch.randn(M, C).to(torch.bfloat16).to(DEV)
+    gamma, beta = (torch.rand(C) + 0.5).to(DEV), torch.randn(C).to(DEV)
+    f = lambda: torch.empty(C, device=DEV)  # noqa: E731
+    part = KB.part_buffer(C, DEV)
+    scale, shift, mean, rstd = f(), f(), f(), f()
+    KB.bn_stats(z, part)
+    KB.bn_finalize(part, M, gamma, beta, 1e-3, -1.0, None, None, scale, shift, mean, rstd, True)
+    y = torch.empty_like(z)
+    KB.bn_apply(z, scale, shift, None, True, y)
+    outs = []
+    for sc, sh in ((None, None), (scale, shift)):
+        coef = torch.empty(3, C, device=DEV)
+        dg, db = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+        KB.bn_bwd_reduce(dy, y, z, True, part, sc, sh)
+        KB.bn_bwd_finalize(part, M, gamma, mean, rstd, dg, db, coef)
+        dz = torch.empty_like(z)
+        KB.bn_bwd_apply(dy, y if sc is None else None, z, coef, True, dz, None, sc, sh)
+        outs.append((dz.cpu(), dg.cpu(), db.cpu()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("shape,k,s,p", [((2, 112, 112, 64), 3, 2, 1), ((3, 17, 19, 16), 3, 2, 0),
                                          ((2, 32, 40, 8), 2, 2, 0)])
 def test_maxpool(shape, k, s, p):
