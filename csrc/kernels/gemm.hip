@@ -263,6 +263,51 @@ struct EpiF32 {  // out[m*ldc+n] (=|+=) act(acc + bias)
     for (int j = 0; j < cnt; ++j) (*this)(m, n + j, v[j]);
   }
 };
+// Adam applied in the epilogue of the weight-gradient GEMM (1-GPU training): the gradient tile
+// never goes to HBM - each lane reads its 8 parameters' p/m/v, updates them and writes p, m, v and
+// the bf16 mirror (26 bytes per parameter instead of the 4-byte gradient store + the 30-byte
+// adam_k pass).  Same arithmetic as adam_k (nn_eltwise.hip); lr_dev[1] (device step state, HIP
+// graphs) overrides lr_t.
+struct EpiAdam {
+  static constexpr bool VEC = true;
+  float* p; float* mo; float* ve; bf16_t* pbf; long ldc; float lr_t, b1, b2, eps, gscale; const float* lr_dev;
+  PTG_DEV float lr() const { return lr_dev ? lr_dev[1] : lr_t; }
+  PTG_DEV void upd(float& pp, float& mm, float& vv, float g, float l) const {
+    const float gj = g * gscale;
+    mm = b1 * mm + (1.f - b1) * gj;
+    vv = b2 * vv + (1.f - b2) * gj * gj;
+    pp -= l * mm / (sqrtf(vv) + eps);
+  }
+  PTG_DEV void operator()(int m, int n, float v) const {
+    const long i = (long)m * ldc + n;
+    float pp = p[i], mm = mo[i], vv = ve[i];
+    upd(pp, mm, vv, v, lr());
+    p[i] = pp; mo[i] = mm; ve[i] = vv;
+    pbf[i] = f2bf(pp);
+  }
+  PTG_DEV void vec8(int m, int n, float* v, int cnt) const {
+    const long i = (long)m * ldc + n;
+    if (cnt == 8 && (i & 7) == 0) {
+      float4 P[2] = {*(const float4*)(p + i), *(const float4*)(p + i + 4)};
+      float4 Mm[2] = {*(const float4*)(mo + i), *(const float4*)(mo + i + 4)};
+      float4 V[2] = {*(const float4*)(ve + i), *(const float4*)(ve + i + 4)};
+      const float l = lr();
+      float o[8];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        float* pp = &P[h].x; float* mm = &Mm[h].x; float* vv = &V[h].x;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { upd(pp[j], mm[j], vv[j], v[4 * h + j], l); o[4 * h + j] = pp[j]; }
+      }
+      *(float4*)(p + i) = P[0]; *(float4*)(p + i + 4) = P[1];
+      *(float4*)(mo + i) = Mm[0]; *(float4*)(mo + i + 4) = Mm[1];
+      *(float4*)(ve + i) = V[0]; *(float4*)(ve + i + 4) = V[1];
+      *(U4*)(pbf + i) = pack8(o);
+      return;
+    }
+    for (int j = 0; j < cnt; ++j) (*this)(m, n + j, v[j]);
+  }
+};
 struct EpiAtomic {  // split-K: out[m*ldc+n] += acc  (device-scope fp32 atomic, no return)
   static constexpr bool VEC = false;  // lane-consecutive atomics coalesce; 8-per-lane runs do not
   float* out; long ldc;
@@ -566,6 +611,19 @@ int ptg_gemm_bf16(int M, int N, int K, const void* A, long lda, int a_kcontig, c
     PTG_EPI_SWITCH(la, lb)
   }
 #undef PTG_EPI_SWITCH
+}
+
+// Weight gradient with Adam fused into the epilogue (EpiAdam): G[M][N] = A^T-style product as in
+// ptg_gemm_bf16 (same operand conventions, no split-K), then p/m/v/pbf[m*ldc+n] updated in place.
+int ptg_gemm_adam(int M, int N, int K, const void* A, long lda, int a_kcontig, const void* B, long ldb,
+                  int b_kcontig, float* p, float* m, float* v, void* pbf, long ldc, float lr_t, float b1,
+                  float b2, float eps, float gscale, const float* lr_dev, hipStream_t s) {
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  if (a_kcontig || b_kcontig || lda % 8 || ldb % 8 || M % 8 || N % 8 || ldc % 8) return (int)hipErrorInvalidValue;
+  if (!fits(matmn_bytes(lda, M, K)) || !fits(matmn_bytes(ldb, N, K))) return (int)hipErrorInvalidValue;
+  const bf16_t* a = (const bf16_t*)A; const bf16_t* b = (const bf16_t*)B;
+  MatMN la{a, lda, M, K, (uint32_t)matmn_bytes(lda, M, K)}; MatMN lb{b, ldb, N, K, (uint32_t)matmn_bytes(ldb, N, K)};
+  return dispatch_gemm(la, lb, EpiAdam{p, m, v, (bf16_t*)pbf, ldc, lr_t, b1, b2, eps, gscale, lr_dev}, M, N, K, 1, s);
 }
 
 // Conv2D forward, NHWC bf16: z[n][oh][ow][co] = bias[co] + sum_{kh,kw,ci} x[..] w[co][kh][kw][ci]

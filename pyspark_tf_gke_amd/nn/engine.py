@@ -290,6 +290,7 @@ class DenseOp(Op):
             dense.kernel.fwd_bf16 = True
         self.act = dense.activation
         self.logits_only = False  # softmax folded into the loss
+        self.fused_update = None  # optimizers.FusedAdamStep during a fused-update training step
 
     def forward(self, x, ws, training):
         x = x.reshape(x.shape[0], -1)
@@ -319,13 +320,18 @@ class DenseOp(Op):
                 K.relu_bwd(dy, y, dz)
             else:
                 dz = _bf16(dy, ws, self.name + "/dz16")
-            K.linear_dw(dz, x, self.dense.kernel.grad)
             if self.dense.bias is not None:
                 K.col_sum(dz, self.dense.bias.grad)
-            if self.first:
-                return None
-            dx = ws.get(self.name + "/dx", x.shape, torch.bfloat16, dev)
-            K.linear_dx(dz, self.dense.kernel.bf16, dx)
+            fused = self.fused_update
+            dx = None
+            if not self.first:
+                # before the weight update below: dX reads this step's (pre-update) bf16 weights
+                dx = ws.get(self.name + "/dx", x.shape, torch.bfloat16, dev)
+                K.linear_dx(dz, self.dense.kernel.bf16, dx)
+            if fused is not None and dz.is_cuda:
+                fused.linear_dw(dz, x, self.dense.kernel)  # Adam in the wgrad epilogue
+            else:
+                K.linear_dw(dz, x, self.dense.kernel.grad)
             return dx
         # skinny path (fp32 math)
         if self.act == "relu" and not self.grad_masked_by_next:

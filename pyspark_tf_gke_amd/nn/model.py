@@ -29,6 +29,10 @@ from . import metrics as MT
 from . import optimizers as OPT
 from .params import ParamStore
 
+# Adam fused into the weight-gradient GEMM of big Dense layers on one replica (gemm.hip EpiAdam):
+# the 168 MB CNN-B1 Dense kernel gradient is never written or re-read.  PTG_FUSED_ADAM=0 disables.
+FUSED_ADAM = os.environ.get("PTG_FUSED_ADAM", "1") != "0"
+
 
 def default_device() -> torch.device:
     from ..distribute import current_strategy
@@ -288,6 +292,17 @@ class Sequential:
     def backward_and_update(self, dpred, strategy=None) -> None:
         """Backward from d(loss)/d(output) + gradient sync + optimizer update."""
         st = strategy
+        fused = self._begin_fused_update(st)
+        if fused is not None:
+            # one local replica: big Dense layers apply Adam in their weight-gradient epilogue,
+            # the rest of the flat store gets the usual fused Adam pass afterwards
+            try:
+                self._run_backward(dpred)
+            finally:
+                for op in self._fusable_ops:
+                    op.fused_update = None
+            self.optimizer.finish_fused(fused)
+            return
         hook = st.on_op_grads_ready if st is not None else None
         self._run_backward(dpred, on_op_done=(lambda op: hook(self, op)) if hook else None)
         if st is not None:
@@ -295,6 +310,25 @@ class Sequential:
             st.apply_update(self)
         else:
             self.optimizer.apply(self.store)
+
+    def _begin_fused_update(self, st):
+        """FusedAdamStep when this step can update big Dense kernels inside their wgrad GEMM: Adam,
+        one replica (no gradient collective between backward and update), GPU, PTG_FUSED_ADAM != 0."""
+        if not FUSED_ADAM or not isinstance(self.optimizer, OPT.Adam) or not self.store.flat.is_cuda:
+            return None
+        if st is not None and st.world_size != 1:
+            return None
+        all_ops = getattr(self, "ops", None) or []
+        if getattr(self, "_fusable_key", None) is not all_ops:
+            self._fusable_key = all_ops
+            self._fusable_ops = [op for op in all_ops if isinstance(op, E.DenseOp) and op.big]
+        ops = self._fusable_ops
+        if not ops:
+            return None
+        ctx = self.optimizer.begin_fused(self.store)
+        for op in ops:
+            op.fused_update = ctx
+        return ctx
 
     def train_step(self, xb, yb, stats=None) -> None:
         _fault.maybe_fail()

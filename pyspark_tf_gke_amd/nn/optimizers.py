@@ -79,6 +79,23 @@ class Adam(Optimizer):
         if advance:
             self.iterations = step
 
+    # ---- fused update: the gradient producer applies Adam in its epilogue (one local replica) ----
+    def begin_fused(self, store) -> "FusedAdamStep":
+        self.build(store)
+        ds = getattr(self, "dev_state", None)
+        if ds is not None:
+            K.adam_step(ds, self.learning_rate, self.beta_1, self.beta_2)
+        return FusedAdamStep(self, store, self.iterations + 1, ds)
+
+    def finish_fused(self, ctx: "FusedAdamStep") -> None:
+        """Plain fused-flat Adam over every range no gradient producer has updated."""
+        lo = 0
+        for a, b in sorted(ctx.done) + [(ctx.store.total, ctx.store.total)]:
+            if a > lo:
+                self.apply(ctx.store, lo=lo, hi=a, advance=False)
+            lo = max(lo, b)
+        self.iterations = ctx.step
+
     def get_config(self):
         return {"name": self.name, "learning_rate": self.learning_rate, "beta_1": self.beta_1,
                 "beta_2": self.beta_2, "epsilon": self.epsilon}
@@ -87,6 +104,22 @@ class Adam(Optimizer):
         return {"m": self.m, "v": self.v}
 
 
+class FusedAdamStep:
+    """One training step's Adam state for gradient producers that update their own parameter
+    (``DenseOp`` runs :func:`ops.nn.linear_dw_adam`); ``done`` collects the flat ranges they took."""
+
+    def __init__(self, opt: Adam, store, step: int, lr_dev):
+        self.opt, self.store, self.step, self.lr_dev = opt, store, step, lr_dev
+        self.done: list = []
+
+    def linear_dw(self, dz, x, param) -> None:
+        o, n = param.offset, param.numel
+        st, opt = self.store, self.opt
+        shp = param.grad.shape
+        K.linear_dw_adam(dz, x, st.flat[o:o + n].view(shp), opt.m[o:o + n].view(shp), opt.v[o:o + n].view(shp),
+                         st.flat_bf16[o:o + n].view(shp), opt.lr_t(self.step), opt.beta_1, opt.beta_2, opt.epsilon,
+                         1.0, lr_dev=self.lr_dev)
+        self.done.append((o, o + n))
 
 
 class SGD(Optimizer):

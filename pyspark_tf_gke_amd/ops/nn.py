@@ -281,6 +281,23 @@ def linear_dw(dy, x, out, accumulate: bool = False):
     return out
 
 
+def linear_dw_adam(dy, x, p, m, v, pbf, lr_t: float, b1: float, b2: float, eps: float, gscale: float = 1.0,
+                   lr_dev=None):
+    """Adam step on a Dense kernel straight from its gradient dy[M,N]^T @ x[M,K]: p/m/v ([N,K] fp32)
+    and the bf16 mirror pbf are updated in the GEMM epilogue; the gradient is never stored."""
+    if not on_device(dy):
+        g = torch.zeros(p.shape, dtype=torch.float32, device=p.device)
+        ref.linear_dw(dy, x, g, False)
+        return adam(p, g, m, v, pbf, lr_t, b1, b2, eps, gscale, lr_dev=lr_dev)
+    M, N = dy.shape
+    K = x.shape[1]
+    for t in (p, m, v, pbf):
+        if t.numel() != N * K or not t.is_contiguous():
+            raise ValueError("linear_dw_adam: optimizer state must be contiguous [N, K]")
+    hip("ptg_gemm_adam", N, K, M, ptr(dy), N, 0, ptr(x), K, 0, ptr(p), ptr(m), ptr(v), ptr(pbf), K,
+        float(lr_t), float(b1), float(b2), float(eps), float(gscale), ptr(lr_dev))
+
+
 def col_sum(g, out):
     """out[N] += sum over rows of g[M,N]."""
     if not on_device(g):

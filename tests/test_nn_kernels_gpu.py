@@ -451,3 +451,51 @@ def test_resize_norm_and_gap():
     g = torch.empty(3, 128, device=DEV)
     K.gap_fwd(x.to(DEV), g)
     _close(g, x.float().mean((1, 2)), 1e-3, 1e-3, "gap")
+
+
+@pytest.mark.parametrize("B,N,Kd", [(256, 2048, 1024), (64, 136, 40), (32, 72, 200)])
+def test_linear_dw_adam(B, N, Kd):
+    """Adam in the wgrad epilogue == wgrad GEMM + adam_k (fp32 reference of both)."""
+    dy, x = rnd(B, N), rnd(B, Kd)
+    p, m, v = torch.randn(N, Kd), torch.randn(N, Kd) * 0.01, torch.rand(N, Kd) * 0.01
+    P, Mm, V = (t.clone().to(DEV) for t in (p, m, v))
+    pb = torch.empty(N, Kd, device=DEV, dtype=torch.bfloat16)
+    K.linear_dw_adam(dy.to(DEV), x.to(DEV), P, Mm, V, pb, 1e-3, 0.9, 0.999, 1e-7, 0.5)
+    g = dy.float().t() @ x.float()
+    R.adam(p, g, m, v, None, 1e-3, 0.9, 0.999, 1e-7, 0.5)
+    _close(Mm, m, 1e-4, 1e-6, "m")
+    _close(V, v, 1e-4, 1e-8, "v")
+    _close(P, p, 1e-5, 1e-5, "p")
+    _close(pb, p, 1e-2, 1e-2, "p_bf16")
+    # device step state overrides the host step size
+    lr_dev = torch.tensor([0.0, 0.0], device=DEV)
+    P2 = p.clone().to(DEV)
+    K.linear_dw_adam(dy.to(DEV), x.to(DEV), P2, m.clone().to(DEV), v.clone().to(DEV), pb, 5.0, 0.9, 0.999, 1e-7,
+                     0.5, lr_dev=lr_dev)
+    _close(P2, p, 0, 0, "lr_dev_zero_step")
+
+
+def test_fused_adam_training_matches_unfused(monkeypatch):
+    """A few Adam steps of an MLP with big Dense layers: fused-epilogue update == plain fused-flat
+    Adam pass (same weights, moments and bf16 mirror)."""
+    from pyspark_tf_gke_amd.nn import layers as L
+    from pyspark_tf_gke_amd.nn import model as MD
+
+    torch.manual_seed(5)
+    x = torch.randn(64, 256)
+    y = torch.randn(64, 2)
+    res = {}
+    for fused in (False, True):
+        monkeypatch.setattr(MD, "FUSED_ADAM", fused)
+        m = MD.Sequential([L.Input((256,)), L.Dense(512, activation="relu"), L.Dense(128, activation="relu"),
+                           L.Dense(2)])
+        m.build(device=DEV, seed=11)
+        m.compile(optimizer="adam", loss="mse")
+        for _ in range(3):
+            m.train_on_batch(x, y)
+        torch.cuda.synchronize()
+        assert bool(getattr(m, "_fusable_ops", None)) == fused
+        res[fused] = (m.store.flat.cpu().clone(), m.optimizer.m.cpu().clone(), m.optimizer.v.cpu().clone(),
+                      m.store.flat_bf16.float().cpu().clone())
+    for i, name in enumerate(("p", "m", "v", "pbf")):
+        _close(res[True][i], res[False][i], 1e-4, 1e-6, "fused_" + name)
