@@ -24,6 +24,8 @@
 //     blockIdx.y indexes split-K slices (fp32 atomic epilogue).
 #include "common.h"
 
+#include <type_traits>
+
 namespace ptg {
 
 constexpr int BK = 64;
@@ -270,8 +272,13 @@ struct EpiF32 {  // out[m*ldc+n] (=|+=) act(acc + bias)
 // graphs) overrides lr_t.
 struct EpiAdam {
   static constexpr bool VEC = true;
+  // the kernel issues PRE lanes' worth of p/m/v loads before any update is stored (the epilogue's
+  // stores could alias later loads, so the compiler would otherwise serialise 8 HBM round trips)
+  static constexpr int PRE = 4;
+  struct Pre { float4 P[2], Mm[2], V[2]; };
   float* p; float* mo; float* ve; bf16_t* pbf; long ldc; float lr_t, b1, b2, eps, gscale; const float* lr_dev;
   PTG_DEV float lr() const { return lr_dev ? lr_dev[1] : lr_t; }
+  PTG_DEV static bool fast(long i, int cnt) { return cnt == 8 && (i & 7) == 0; }
   PTG_DEV void upd(float& pp, float& mm, float& vv, float g, float l) const {
     const float gj = g * gscale;
     mm = b1 * mm + (1.f - b1) * gj;
@@ -285,29 +292,40 @@ struct EpiAdam {
     p[i] = pp; mo[i] = mm; ve[i] = vv;
     pbf[i] = f2bf(pp);
   }
-  PTG_DEV void vec8(int m, int n, float* v, int cnt) const {
+  PTG_DEV void preload(int m, int n, int cnt, Pre& r) const {
     const long i = (long)m * ldc + n;
-    if (cnt == 8 && (i & 7) == 0) {
-      float4 P[2] = {*(const float4*)(p + i), *(const float4*)(p + i + 4)};
-      float4 Mm[2] = {*(const float4*)(mo + i), *(const float4*)(mo + i + 4)};
-      float4 V[2] = {*(const float4*)(ve + i), *(const float4*)(ve + i + 4)};
-      const float l = lr();
-      float o[8];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        float* pp = &P[h].x; float* mm = &Mm[h].x; float* vv = &V[h].x;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) { upd(pp[j], mm[j], vv[j], v[4 * h + j], l); o[4 * h + j] = pp[j]; }
-      }
-      *(float4*)(p + i) = P[0]; *(float4*)(p + i + 4) = P[1];
-      *(float4*)(mo + i) = Mm[0]; *(float4*)(mo + i + 4) = Mm[1];
-      *(float4*)(ve + i) = V[0]; *(float4*)(ve + i + 4) = V[1];
-      *(U4*)(pbf + i) = pack8(o);
+    if (!fast(i, cnt)) return;
+    r.P[0] = *(const float4*)(p + i); r.P[1] = *(const float4*)(p + i + 4);
+    r.Mm[0] = *(const float4*)(mo + i); r.Mm[1] = *(const float4*)(mo + i + 4);
+    r.V[0] = *(const float4*)(ve + i); r.V[1] = *(const float4*)(ve + i + 4);
+  }
+  PTG_DEV void vec8_pre(int m, int n, float* v, int cnt, Pre& r) const {
+    const long i = (long)m * ldc + n;
+    if (!fast(i, cnt)) {
+      for (int j = 0; j < cnt; ++j) (*this)(m, n + j, v[j]);
       return;
     }
-    for (int j = 0; j < cnt; ++j) (*this)(m, n + j, v[j]);
+    const float l = lr();
+    float o[8];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      float* pp = &r.P[h].x; float* mm = &r.Mm[h].x; float* vv = &r.V[h].x;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { upd(pp[j], mm[j], vv[j], v[4 * h + j], l); o[4 * h + j] = pp[j]; }
+    }
+    *(float4*)(p + i) = r.P[0]; *(float4*)(p + i + 4) = r.P[1];
+    *(float4*)(mo + i) = r.Mm[0]; *(float4*)(mo + i + 4) = r.Mm[1];
+    *(float4*)(ve + i) = r.V[0]; *(float4*)(ve + i + 4) = r.V[1];
+    *(U4*)(pbf + i) = pack8(o);
+  }
+  PTG_DEV void vec8(int m, int n, float* v, int cnt) const {
+    Pre r;
+    preload(m, n, cnt, r);
+    vec8_pre(m, n, v, cnt, r);
   }
 };
+template <class E, class = void> struct EpiPre { static constexpr int v = 0; };
+template <class E> struct EpiPre<E, std::void_t<decltype(E::PRE)>> { static constexpr int v = E::PRE; };
 struct EpiAtomic {  // split-K: out[m*ldc+n] += acc  (device-scope fp32 atomic, no return)
   static constexpr bool VEC = false;  // lane-consecutive atomics coalesce; 8-per-lane runs do not
   float* out; long ldc;
@@ -491,7 +509,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(LA la, LB lb, EPI epi, int M,
   // bf16 outputs: stage the fp32 tile through LDS, then every thread hands 8 consecutive columns
   // of a row to the epilogue (one 16-byte store instead of eight 2-byte ones).
   constexpr int CP = BN + 4;
-  static_assert(BM * CP * 4 <= 2 * STAGE * 2, "C tile must fit in the staging LDS");
+  static_assert(!EPI::VEC || BM * CP * 4 <= 2 * STAGE * 2, "C tile must fit in the staging LDS");
   float* cs = reinterpret_cast<float*>(smem);
 #pragma unroll
   for (int i = 0; i < FM; ++i)
@@ -502,6 +520,32 @@ __global__ __launch_bounds__(256) void gemm_kernel(LA la, LB lb, EPI epi, int M,
         cs[(wm * WTM + i * 16 + (lane >> 4) * 4 + r) * CP + wn * WTN + j * 16 + (lane & 15)] = acc[i][j][r];
   __syncthreads();
   constexpr int NV = BM * BN / 8;
+  if constexpr (EpiPre<EPI>::v > 0 && NV % 256 == 0) {
+    // read-modify-write epilogue: a batch of lanes' operand loads first, then the updates
+    constexpr int NIT = NV / 256, B = EpiPre<EPI>::v < NIT ? EpiPre<EPI>::v : NIT;
+#pragma unroll
+    for (int b0 = 0; b0 < NIT; b0 += B) {
+      typename EPI::Pre pre[B];
+      int mm[B], nn[B];
+#pragma unroll
+      for (int u = 0; u < B; ++u) {
+        const int v = (b0 + u) * 256 + tid;
+        const int row = v / (BN / 8), c8 = v - row * (BN / 8);
+        mm[u] = m0 + row; nn[u] = n0 + c8 * 8;
+        if (mm[u] < M && nn[u] < N) epi.preload(mm[u], nn[u], min(8, N - nn[u]), pre[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < B; ++u) {
+        if (mm[u] >= M || nn[u] >= N) continue;
+        const int v = (b0 + u) * 256 + tid;
+        const int row = v / (BN / 8), c8 = v - row * (BN / 8);
+        const float4 a = *(const float4*)(cs + row * CP + c8 * 8), b = *(const float4*)(cs + row * CP + c8 * 8 + 4);
+        float vals[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        epi.vec8_pre(mm[u], nn[u], vals, min(8, N - nn[u]), pre[u]);
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int v0 = 0; v0 < NV; v0 += 256) {
     const int v = v0 + tid;
