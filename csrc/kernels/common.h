@@ -116,3 +116,18 @@ static inline FastDiv fastdiv(uint32_t d) {
 }
 
 #define PTG_RETURN_LAUNCH() return (int)hipGetLastError()
+
+// Workgroups of `kernel` (256 threads) resident at once on the whole device: the grid of a
+// persistent kernel (more would queue behind workgroups that only exit at the end).
+static inline int ptg_resident_blocks(const void* kernel) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess || per_cu <= 0) per_cu = 2;
+  return cus * per_cu;
+}

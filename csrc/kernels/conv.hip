@@ -1063,19 +1063,6 @@ static int wq_chunk(long tiles, int groups) {
   return (int)(c < 4 ? 4 : c);
 }
 
-static int resident_blocks(const void* kernel) {
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    hipGetDevice(&dev);
-    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (cus <= 0) cus = 256;
-  }
-  int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess || per_cu <= 0) per_cu = 2;
-  return cus * per_cu;
-}
-
 template <int C, int KS, int NF, int TW, int TH, int E, bool WLDS, int COS>
 static int launch_fwd_k(const void* x, const void* w, const float* bias, const float* alpha, void* z, void* aux, void* arg,
                         int N, int H, int W, int Cout, int pad, hipStream_t s) {
@@ -1084,7 +1071,7 @@ static int launch_fwd_k(const void* x, const void* w, const float* bias, const f
   constexpr bool WREG = KSTEPS * NF <= 8;
   constexpr bool KSPLIT = !WLDS && !WREG && MFR / 4 <= 2 && MFR * NF <= 16;
   const auto kern = conv_fwd_strip_k<C, KS, NF, TW, TH, E, RING, KSPLIT, WLDS, COS>;
-  static const int resident = resident_blocks((const void*)kern);
+  static const int resident = ptg_resident_blocks((const void*)kern);
   const int th = (H + TH - 1) / TH, tw = (W + TW - 1) / TW;
   const long tiles = (long)N * tw * th;
   // persistent: one wave of resident workgroups, each walking a contiguous range of tiles
@@ -1185,7 +1172,7 @@ static int launch_wgrad(const void* x, const void* dz, float* dw, int N, int H, 
   constexpr int KF = KS * KS * C;
   constexpr int NB = KF > 512 ? 4 : 2;
   const auto kern = conv_wgrad_strip_k<C, KS, TW, TH, MF, NB, RING, SPARSE>;
-  static const int resident = resident_blocks((const void*)kern);
+  static const int resident = ptg_resident_blocks((const void*)kern);
   const int th = (H + TH - 1) / TH, tw = (W + TW - 1) / TW;
   const long tiles = (long)N * tw * th;
   const int nslices = (KF + 64 * NB - 1) / (64 * NB);
@@ -1235,8 +1222,8 @@ int ptg_conv2d_fwd_halo(const void* x, const void* w, const float* bias, const f
   if ((epi == EPI_POOL || epi == EPI_POOLS) && ((H & 1) || (W & 1))) return (int)hipErrorInvalidValue;
   if (C == 4 && Cout == 8 && KS == 5 && (epi == EPI_POOL || epi == EPI_POOLS) && pad == 2 && conv1_pair_enabled()) {
     const auto kern = epi == EPI_POOLS ? conv1_pair_pool_k<5, true> : conv1_pair_pool_k<5, false>;
-    static const int res_dense = resident_blocks((const void*)conv1_pair_pool_k<5, false>);
-    static const int res_sparse = resident_blocks((const void*)conv1_pair_pool_k<5, true>);
+    static const int res_dense = ptg_resident_blocks((const void*)conv1_pair_pool_k<5, false>);
+    static const int res_sparse = ptg_resident_blocks((const void*)conv1_pair_pool_k<5, true>);
     const int resident = epi == EPI_POOLS ? res_sparse : res_dense;
     const int th = (H + 3) / 4, tw = (W + 63) / 64;
     const long tiles = (long)N * th * tw;
