@@ -483,3 +483,5 @@ int ptg_add_bf16(const void* a, const void* b, void* out, long n, hipStream_t s)
 }
 
 }  // extern "C"
+
+PTG_CHECK_STATUS(bn)

@@ -131,3 +131,29 @@ static inline int ptg_resident_blocks(const void* kernel) {
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess || per_cu <= 0) per_cu = 2;
   return cus * per_cu;
 }
+
+// ---- checked builds (-DPTG_CHECKED -> libptg_hip_checked.so, selected with PTG_CHECKED=1) ----
+// PTG_CHECKED_IDX(i, n) is i when 0 <= i < n.  Otherwise it records the source line in this
+// translation unit's ptg_check_line (first failure wins) and yields 0, so the access stays in
+// bounds and the kernel never faults; the host reads and clears the line after every launch
+// (PTG_CHECK_STATUS -> ptg_check_status_<tu>, polled by pyspark_tf_gke_amd._native).  Unchecked
+// builds compile the macro to plain i.
+#ifdef PTG_CHECKED
+static __device__ unsigned int ptg_check_line;
+PTG_DEV long long ptg_checked_idx(long long i, long long n, int line) {
+  if ((unsigned long long)i < (unsigned long long)n) return i;
+  atomicCAS(&ptg_check_line, 0u, (unsigned)line);
+  return 0;
+}
+#define PTG_CHECKED_IDX(i, n) ptg_checked_idx((long long)(i), (long long)(n), __LINE__)
+#define PTG_CHECK_STATUS(tu)                                                      \
+  extern "C" int ptg_check_status_##tu() {                                        \
+    unsigned int v = 0, z = 0;                                                    \
+    if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(ptg_check_line), sizeof(v)) != hipSuccess) return -1; \
+    if (v) hipMemcpyToSymbol(HIP_SYMBOL(ptg_check_line), &z, sizeof(z));          \
+    return (int)v;                                                                \
+  }
+#else
+#define PTG_CHECKED_IDX(i, n) (i)
+#define PTG_CHECK_STATUS(tu)
+#endif

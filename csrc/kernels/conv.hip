@@ -486,7 +486,7 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
           const bool lead = ((cc & 1) == 0) && ((rr & 1) == 0);
           const int ph = (oh0 + rr) >> 1, pw = (ow0 + cc) >> 1;
           if (cval && lead && ph < PH && pw < PW) {
-            const long po = (((long)n * PH + ph) * PW + pw) * Cout + co0;
+            const long po = PTG_CHECKED_IDX((((long)n * PH + ph) * PW + pw) * Cout + co0, (long)N * PH * PW * Cout);
             *(U2*)(aux + po) = U2{pack_bf(pm[0], pm[1]), pack_bf(pm[2], pm[3])};
             *(U2*)(z + po) = U2{pack_bf(pz[0], pz[1]), pack_bf(pz[2], pz[3])};
             *(uint32_t*)(argout + po) = (uint32_t)pq[0] | ((uint32_t)pq[1] << 8) | ((uint32_t)pq[2] << 16) |
@@ -508,7 +508,7 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
         for (int r = 0; r < 4; ++r) zr[r] = bf2f(f2bf(res[i][j][r] + bv[j][r]));
         const bool in = cval && oh < H && ow < W;
         const long o = (((long)n * H + oh) * W + ow) * Cout + co0;
-        if (in) *(U2*)(z + o) = U2{pack_bf(zr[0], zr[1]), pack_bf(zr[2], zr[3])};
+        if (in) *(U2*)(z + PTG_CHECKED_IDX(o, (long)N * H * W * Cout)) = U2{pack_bf(zr[0], zr[1]), pack_bf(zr[2], zr[3])};
         if constexpr (EPI != EPI_Z) {
           const float a4[4] = {al[i][j].x, al[i][j].y, al[i][j].z, al[i][j].w};
 #pragma unroll
@@ -536,7 +536,7 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
           const bool lead = ((cc & 1) == 0) && ((rr & 1) == 0);
           const int ph = (oh0 + rr) >> 1, pw = (ow0 + cc) >> 1;
           if (cval && lead && ph < PH && pw < PW)
-            *(U2*)(aux + (((long)n * PH + ph) * PW + pw) * Cout + co0) =
+            *(U2*)(aux + PTG_CHECKED_IDX((((long)n * PH + ph) * PW + pw) * Cout + co0, (long)N * PH * PW * Cout)) =
                 U2{pack_bf(pm[0], pm[1]), pack_bf(pm[2], pm[3])};
         }
       }
@@ -1299,3 +1299,5 @@ int ptg_conv_flip_weights(const void* w, void* wf, int Cout, int KS, int Cin, hi
 }
 
 }  // extern "C"
+
+PTG_CHECK_STATUS(conv)

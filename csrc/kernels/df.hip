@@ -215,20 +215,22 @@ __global__ __launch_bounds__(256) void compact_write_k(const uint8_t* __restrict
 
 // rows gather: dst[r] = src[idx[r]] for rows of row_bytes (multiple of 4)
 __global__ __launch_bounds__(256) void gather_rows_k(const uint8_t* __restrict__ src, const long long* __restrict__ idx,
-                                                     long m, int row_words, uint8_t* __restrict__ dst) {
+                                                     long m, int row_words, long nsrc, uint8_t* __restrict__ dst) {
   const long total = m * row_words;
   for (long t = blockIdx.x * 256L + threadIdx.x; t < total; t += (long)gridDim.x * 256) {
     const long r = t / row_words; const int w = t - r * row_words;
-    ((uint32_t*)dst)[t] = ((const uint32_t*)src)[idx[r] * row_words + w];
+    ((uint32_t*)dst)[t] = ((const uint32_t*)src)[PTG_CHECKED_IDX(idx[r], nsrc) * row_words + w];
   }
+  (void)nsrc;
 }
 __global__ __launch_bounds__(256) void gather_bytes_k(const uint8_t* __restrict__ src, const long long* __restrict__ idx,
-                                                      long m, int row_bytes, uint8_t* __restrict__ dst) {
+                                                      long m, int row_bytes, long nsrc, uint8_t* __restrict__ dst) {
   const long total = m * row_bytes;
   for (long t = blockIdx.x * 256L + threadIdx.x; t < total; t += (long)gridDim.x * 256) {
     const long r = t / row_bytes; const int b = t - r * row_bytes;
-    dst[t] = src[idx[r] * row_bytes + b];
+    dst[t] = src[PTG_CHECKED_IDX(idx[r], nsrc) * row_bytes + b];
   }
+  (void)nsrc;
 }
 
 // ================================================================================================
@@ -560,8 +562,9 @@ __global__ __launch_bounds__(256) void radix_scatter_k(const long long* __restri
                                                        const int* __restrict__ trows,
                                                        const long long* __restrict__ thbase,
                                                        const long long* __restrict__ thstride, int shift,
-                                                       const long long* __restrict__ offs,
+                                                       const long long* __restrict__ offs, long n_out,
                                                        long long* __restrict__ okeys, double* __restrict__ ovals) {
+  (void)n_out;
   constexpr int RPT = RT / 256;
   __shared__ long long sk[RT];
   __shared__ double sv[RT];
@@ -616,7 +619,7 @@ __global__ __launch_bounds__(256) void radix_scatter_k(const long long* __restri
   __syncthreads();
   for (int i = tid; i < nr; i += 256) {  // consecutive rows of a digit run -> consecutive addresses
     const int dd = sd[i];
-    const long long dst = goff[dd] + (i - (int)lstart[dd]);
+    const long long dst = PTG_CHECKED_IDX(goff[dd] + (i - (int)lstart[dd]), n_out);
     okeys[dst] = sk[i];
     ovals[dst] = sv[i];
   }
@@ -781,15 +784,16 @@ int ptg_compact(const void* mask, long n, void* block_counts, void* block_off, v
   PTG_RETURN_LAUNCH();
 }
 
-int ptg_gather_rows(const void* src, const void* idx, long m, int row_bytes, void* dst, hipStream_t s) {
+// nsrc: rows of src (checked builds verify every idx against it)
+int ptg_gather_rows(const void* src, const void* idx, long m, int row_bytes, long nsrc, void* dst, hipStream_t s) {
   if (m <= 0) return 0;
   if (row_bytes % 4 == 0) {
     const int rw = row_bytes / 4;
     hipLaunchKernelGGL(gather_rows_k, dim3(grid_n(m * rw)), dim3(256), 0, s, (const uint8_t*)src,
-                       (const long long*)idx, m, rw, (uint8_t*)dst);
+                       (const long long*)idx, m, rw, nsrc, (uint8_t*)dst);
   } else {
     hipLaunchKernelGGL(gather_bytes_k, dim3(grid_n(m * row_bytes)), dim3(256), 0, s, (const uint8_t*)src,
-                       (const long long*)idx, m, row_bytes, (uint8_t*)dst);
+                       (const long long*)idx, m, row_bytes, nsrc, (uint8_t*)dst);
   }
   PTG_RETURN_LAUNCH();
 }
@@ -876,12 +880,13 @@ int ptg_radix_count(const void* keys, const void* tstart, const void* trows, con
   PTG_RETURN_LAUNCH();
 }
 int ptg_radix_scatter(const void* keys, const void* val, int vtype, const void* tstart, const void* trows,
-                      const void* thbase, const void* thstride, int ntiles, int shift, const void* offs, void* okeys,
-                      void* ovals, hipStream_t s) {
+                      const void* thbase, const void* thstride, int ntiles, int shift, const void* offs, long n_out,
+                      void* okeys, void* ovals, hipStream_t s) {
   if (ntiles <= 0) return 0;
   hipLaunchKernelGGL(radix_scatter_k, dim3(ntiles), dim3(256), 0, s, (const long long*)keys, val, vtype,
                      (const long long*)tstart, (const int*)trows, (const long long*)thbase,
-                     (const long long*)thstride, shift, (const long long*)offs, (long long*)okeys, (double*)ovals);
+                     (const long long*)thstride, shift, (const long long*)offs, n_out, (long long*)okeys,
+                     (double*)ovals);
   PTG_RETURN_LAUNCH();
 }
 int ptg_part_agg(const void* okeys, const void* ovals, const void* pstart, int P, void* out_keys, void* out_sum,
@@ -925,3 +930,5 @@ int ptg_fill_synthetic_kv(void* keys, void* vals, long n, long offset, long num_
 }
 
 }  // extern "C"
+
+PTG_CHECK_STATUS(df)

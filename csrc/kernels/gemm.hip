@@ -754,3 +754,5 @@ int ptg_conv2d_wgrad(const void* x, const void* dz, float* dw, int N, int H, int
 }
 
 }  // extern "C"
+
+PTG_CHECK_STATUS(gemm)

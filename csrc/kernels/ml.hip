@@ -220,3 +220,5 @@ int ptg_silhouette(const void* X, const void* assign, const void* S, const void*
 }
 
 }  // extern "C"
+
+PTG_CHECK_STATUS(ml)

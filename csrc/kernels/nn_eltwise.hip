@@ -509,7 +509,7 @@ __global__ __launch_bounds__(256) void prelu_pool_bwd_sel_k(const bf16_t* __rest
           for (int qq = 0; qq < 4; ++qq) da[qq][j] += q == qq ? d : 0.f;
           db[j] += o[j];
         }
-        *(U4*)(dzs + (long)(n + u * SG) * PHWC + poff) = pack8(o);
+        *(U4*)(dzs + PTG_CHECKED_IDX((long)(n + u * SG) * PHWC + poff, (long)N * PHWC)) = pack8(o);
       }
     }
   }
@@ -1351,3 +1351,5 @@ int ptg_gap_bwd(const float* dy, void* out, int N, int HW, int C, hipStream_t s)
 }
 
 }  // extern "C"
+
+PTG_CHECK_STATUS(nn_eltwise)

@@ -15,7 +15,11 @@ import threading
 from pathlib import Path
 
 HERE = Path(__file__).resolve().parent
-HIP_LIB_PATH = HERE / "libptg_hip.so"
+# PTG_CHECKED=1 loads the bounds-checked kernel build (build.py ``checked``): every launch is
+# followed by a poll of the per-source-file check words, and a bad index raises with its line
+CHECKED = os.environ.get("PTG_CHECKED") == "1"
+HIP_LIB_PATH = HERE / ("libptg_hip_checked.so" if CHECKED else "libptg_hip.so")
+_CHECK_TUS = ("conv", "gemm", "nn_eltwise", "bn", "df", "ml")
 HOST_LIB_PATH = HERE / "libptg_host.so"
 
 _lock = threading.Lock()
@@ -126,8 +130,24 @@ def check(rc: int, name: str) -> None:
 
 def call(name: str, *args) -> None:
     """Invoke a HIP entry point and raise on error."""
-    fn = getattr(hip_lib(), name)
+    lib = hip_lib()
+    fn = getattr(lib, name)
     check(fn(*args), name)
+    if CHECKED:
+        check_kernels(name)
+
+
+def check_kernels(after: str = "") -> None:
+    """Checked builds: raise if any kernel clamped an out-of-range index (file and line)."""
+    lib = hip_lib()
+    for tu in _CHECK_TUS:
+        f = getattr(lib, "ptg_check_status_" + tu, None)
+        if f is None:
+            continue
+        line = f()
+        if line:
+            raise RuntimeError(f"native kernel index out of bounds at csrc/kernels/{tu}.hip:{line}"
+                               + (f" (detected after {after})" if after else ""))
 
 
 def loaded_paths() -> list[str]:

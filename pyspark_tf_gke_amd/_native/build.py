@@ -28,6 +28,7 @@ BUILD = ROOT / "build" / "native"
 ARCH = os.environ.get("PTG_OFFLOAD_ARCH", "gfx950")
 
 HIP_LIB = HERE / "libptg_hip.so"
+HIP_LIB_CHECKED = HERE / "libptg_hip_checked.so"  # -DPTG_CHECKED: index-checked kernels (PTG_CHECKED=1)
 HOST_LIB = HERE / "libptg_host.so"
 
 
@@ -51,16 +52,20 @@ def _run(cmd: list[str]) -> None:
         raise RuntimeError(f"command failed ({r.returncode}): {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
 
 
-def build_hip(force: bool = False, jobs: int = 8, verbose: bool = True) -> Path:
+def build_hip(force: bool = False, jobs: int = 8, verbose: bool = True, checked: bool = False) -> Path:
+    """``checked``: the bounds-checked variant - every PTG_CHECKED_IDX site verifies its
+    index, clamps it in range and reports the source line instead of faulting."""
     srcs = sorted((CSRC / "kernels").glob("*.hip"))
     headers = sorted((CSRC / "kernels").glob("*.h"))
-    BUILD.mkdir(parents=True, exist_ok=True)
+    bdir = BUILD / "checked" if checked else BUILD
+    out_lib = HIP_LIB_CHECKED if checked else HIP_LIB
+    bdir.mkdir(parents=True, exist_ok=True)
     hipcc = _hipcc()
     flags = ["--offload-arch=" + ARCH, "-O3", "-fPIC", "-std=c++17", "-munsafe-fp-atomics",
-             "-Wno-unused-result", "-I", str(CSRC / "kernels")]
+             "-Wno-unused-result", "-I", str(CSRC / "kernels")] + (["-DPTG_CHECKED"] if checked else [])
     objs, todo = [], []
     for s in srcs:
-        o = BUILD / (s.stem + ".o")
+        o = bdir / (s.stem + ".o")
         objs.append(o)
         if force or not o.exists() or o.stat().st_mtime < _newest_dep(s, headers):
             todo.append((s, o))
@@ -68,19 +73,19 @@ def build_hip(force: bool = False, jobs: int = 8, verbose: bool = True) -> Path:
     def compile_one(so):
         s, o = so
         if verbose:
-            print(f"[build] hipcc {s.name}", flush=True)
+            print(f"[build] hipcc {s.name}" + (" (checked)" if checked else ""), flush=True)
         _run([hipcc, *flags, "-c", str(s), "-o", str(o)])
         return o
 
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         list(ex.map(compile_one, todo))
-    if force or todo or not HIP_LIB.exists() or any(HIP_LIB.stat().st_mtime < o.stat().st_mtime for o in objs):
-        tmp = HIP_LIB.with_suffix(".so.tmp")
+    if force or todo or not out_lib.exists() or any(out_lib.stat().st_mtime < o.stat().st_mtime for o in objs):
+        tmp = out_lib.with_suffix(".so.tmp")
         _run([hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", *map(str, objs), "-o", str(tmp)])
-        os.replace(tmp, HIP_LIB)
+        os.replace(tmp, out_lib)
         if verbose:
-            print(f"[build] linked {HIP_LIB}", flush=True)
-    return HIP_LIB
+            print(f"[build] linked {out_lib}", flush=True)
+    return out_lib
 
 
 def build_host(force: bool = False, verbose: bool = True) -> Path:
@@ -107,6 +112,8 @@ def build_host(force: bool = False, verbose: bool = True) -> Path:
 def build_all(force: bool = False, jobs: int = 8, verbose: bool = True) -> None:
     build_host(force=force, verbose=verbose)
     build_hip(force=force, jobs=jobs, verbose=verbose)
+    if os.environ.get("PTG_BUILD_CHECKED", "1") != "0":
+        build_hip(force=force, jobs=jobs, verbose=verbose, checked=True)
 
 
 def main(argv=None) -> int:

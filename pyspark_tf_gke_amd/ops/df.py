@@ -83,7 +83,7 @@ def gather_rows(t: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
         return out
     row_bytes = t[0].numel() * t.element_size() if t.dim() > 0 and t.shape[0] > 0 else t.element_size()
     src = t.contiguous()
-    hip("ptg_gather_rows", ptr(src), ptr(idx), m, row_bytes, ptr(out))
+    hip("ptg_gather_rows", ptr(src), ptr(idx), m, row_bytes, t.shape[0] if t.dim() > 0 else 1, ptr(out))
     return out
 
 
@@ -206,7 +206,7 @@ def _radix_level(keys, val, seg_start, seg_len, shift, buf, tag):
     okeys = buf(tag + "okeys", (n,), torch.int64)
     ovals = buf(tag + "ovals", (n,), torch.float64)
     hip("ptg_radix_scatter", ptr(keys), ptr(val), TORCH_CT[val.dtype], ptr(tstart), ptr(trows), ptr(thbase),
-        ptr(thstride), total, shift, ptr(excl), ptr(okeys), ptr(ovals))
+        ptr(thstride), total, shift, ptr(excl), n, ptr(okeys), ptr(ovals))
     return okeys, ovals, offs, hb, ntiles_s
 
 
