@@ -294,6 +294,21 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
   // work queue `wq`, chunks of `wchunk` tiles claimed until none is left - a workgroup that starts
   // late (CUs held by a concurrent RCCL kernel) then takes less work instead of a full range.
   const long T = (long)S * tiles_h;
+  // SMAJ (no halo ring, PReLU epilogue): tiles are ordered position-major, sample-minor, so the
+  // consecutive tiles of a workgroup share one output position and the per-element PReLU alphas
+  // (for CNN-B1 layer 2 16 KB per tile, more than its halo) stay in registers across samples
+  constexpr bool SMAJ = !RING && EPI != EPI_Z;
+  auto decode = [&](int tt, int& s_, int& th_) {
+    if constexpr (SMAJ) {
+      const int nn = tt % N, pos = tt / N;
+      th_ = pos % tiles_h;
+      s_ = nn * tiles_w + pos / tiles_h;
+    } else {
+      s_ = tt / tiles_h;
+      th_ = tt - s_ * tiles_h;
+    }
+  };
+  float4 al[EPI != EPI_Z ? FM : 1][NF];
   __shared__ int s_wq;
   for (int round = 0;; ++round) {
   int t0, t1;
@@ -308,7 +323,9 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
     t1 = (int)(T * (bid + 1) / nblk);
   }
   if (t0 >= t1) break;
-  int s = t0 / tiles_h, th = t0 - s * tiles_h;
+  int s, th;
+  decode(t0, s, th);
+  int apos = -1;  // output position whose alphas are in al (SMAJ)
   {  // first tile: synchronous fill of its HR rows
     const int n = s / tiles_w, ow0 = (s - n * tiles_w) * TW;
     load_rows(n, ow0 - pad, th * TH - pad, HR);
@@ -321,9 +338,13 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
     const int n = s / tiles_w, ow0 = (s - n * tiles_w) * TW, oh0 = th * TH;
     // next tile of the range and the rows it needs that are not resident
     int s2 = s, th2 = th + 1;
-    if (th2 >= tiles_h) { s2 = s + 1; th2 = 0; }
+    if constexpr (SMAJ) {
+      decode(t + 1, s2, th2);
+    } else if (th2 >= tiles_h) {
+      s2 = s + 1; th2 = 0;
+    }
     const bool has_next = t + 1 < t1;
-    const bool same_strip = s2 == s;
+    const bool same_strip = !SMAJ && s2 == s;
     const int n2 = s2 / tiles_w, ow02 = (s2 - n2 * tiles_w) * TW;
     const int nrows2 = (RING && same_strip) ? TH : HR;
     const int ih2 = (RING && same_strip) ? th2 * TH - pad + HR - TH : th2 * TH - pad;
@@ -331,16 +352,19 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
     if (has_next) load_rows(n2, ow02 - pad, ih2, nrows2);
 
     // alpha for this lane's (pixel, 4 channels) of every fragment, needed after the MFMAs
-    float4 al[EPI != EPI_Z ? FM : 1][NF];
+    const int pos = SMAJ ? t / N : t;
     if constexpr (EPI != EPI_Z) {
+      if (pos != apos) {
+        apos = pos;
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
+        for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < NF; ++j) {
-          const int oh = oh0 + f_r[i], ow = ow0 + f_c[i], co0 = cb + j * 16 + g * 4;
-          al[i][j] = (co0 < Cout && oh < H && ow < W) ? *(const float4*)(alpha + ((long)oh * W + ow) * Cout + co0)
-                                                      : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
+          for (int j = 0; j < NF; ++j) {
+            const int oh = oh0 + f_r[i], ow = ow0 + f_c[i], co0 = cb + j * 16 + g * 4;
+            al[i][j] = (co0 < Cout && oh < H && ow < W) ? *(const float4*)(alpha + ((long)oh * W + ow) * Cout + co0)
+                                                        : make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+      }
     }
 
     // ---- MFMA main loop over the flattened K = (kh, kw', ci) ----
