@@ -544,16 +544,27 @@ __global__ __launch_bounds__(256) void radix_count_k(const long long* __restrict
                                                      const long long* __restrict__ thbase,
                                                      const long long* __restrict__ thstride, int shift,
                                                      unsigned int* __restrict__ hist) {
-  __shared__ unsigned int h[RB];
-  const int tid = threadIdx.x, b = blockIdx.x;
-  if (tid < RB) h[tid] = 0;
-  __syncthreads();
+  // All RT/256 keys of a thread are loaded before the first LDS atomic (8 independent 8-B loads in
+  // flight instead of a load->atomic chain per row), and each wave counts into its own 64-bin
+  // histogram so the 4 waves never contend on a bin; trows <= RT by construction (_radix_level).
+  constexpr int RPT = RT / 256;
+  __shared__ unsigned int h[4][RB];
+  const int tid = threadIdx.x, b = blockIdx.x, w = tid >> 6;
+  h[w][tid & (RB - 1)] = 0;
   const long long s0 = tstart[b];
   const int nr = trows[b];
-  for (int i = tid; i < nr; i += 256)
-    atomicAdd(&h[(unsigned)(mix64((unsigned long long)keys[s0 + i]) >> shift) & (RB - 1)], 1u);
+  unsigned long long k[RPT];
+#pragma unroll
+  for (int j = 0; j < RPT; ++j) {
+    const int i = tid + j * 256;
+    k[j] = i < nr ? (unsigned long long)keys[s0 + i] : 0ull;
+  }
   __syncthreads();
-  if (tid < RB) hist[thbase[b] + (long long)tid * thstride[b]] = h[tid];
+#pragma unroll
+  for (int j = 0; j < RPT; ++j)
+    if (tid + j * 256 < nr) atomicAdd(&h[w][(unsigned)(mix64(k[j]) >> shift) & (RB - 1)], 1u);
+  __syncthreads();
+  if (tid < RB) hist[thbase[b] + (long long)tid * thstride[b]] = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
 }
 
 __global__ __launch_bounds__(256) void radix_scatter_k(const long long* __restrict__ keys,
