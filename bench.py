@@ -3,16 +3,21 @@
 
 Default workload = the reference's CNN-B1 regressor (train_tf_ps.py:346-378 with flat=True, the
 model ``__main__`` trains, :883): 256x320x3 input, 5 x [Conv5x5 + PReLU (+ MaxPool)], Dense(2048,
-relu), Dense(2); MSE + MAE/MSE metrics; Adam.  Synthetic data of that shape (random images in
-[0,1], random pixel targets), random-init weights, bf16 compute / fp32 master weights.  N>1 ranks
-run MultiWorkerMirroredStrategy (bucketed RCCL all-reduce overlapped with backward) with a fixed
-per-GPU batch (weak scaling).  Every timed step is a full train step: forward, loss, backward,
-gradient all-reduce, Adam update.
+relu), Dense(2); MSE + MAE/MSE metrics; Adam.  Synthetic data of that shape (random uint8 images,
+random pixel targets), random-init weights, bf16 compute / fp32 master weights.  N>1 ranks run
+MultiWorkerMirroredStrategy (gradient buckets reduce-scattered over RCCL during backward, sharded
+Adam, bf16 all-gather overlapped with the next forward) with a fixed per-GPU batch (weak scaling).
+Every timed step is a full train step: input pack (decoded uint8 images resident in HBM ->
+normalised, channel-padded bf16), forward, loss, backward, gradient reduce-scatter / all-gather,
+Adam update.
 
-``--workload groupby`` measures the Spark DataFrame groupBy-aggregate over 1B synthetic rows
-instead (rows/s).
+``--gpus N`` without a torch.distributed launcher (no ``WORLD_SIZE`` in the environment) spawns N
+fresh rank processes through :func:`pyspark_tf_gke_amd.runtime.launcher.launch` before anything
+touches the GPU; under ``torch.distributed.run`` the ranks come from the environment.  Either way
+the job asserts ``world_size == --gpus``.
 
-Rank 0 prints ONE JSON line.
+``--workload groupby`` measures the Spark DataFrame groupBy-aggregate over 1B synthetic rows per
+GPU instead (rows/s).  Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -25,22 +30,28 @@ import time
 import torch
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="cnn_b1", choices=["cnn_b1", "groupby", "mlp", "cnn_a1", "mnist", "resnet50"])
-    ap.add_argument("--batch-size", type=int, default=int(os.environ.get("PTG_BENCH_BATCH", "256")),
-                    help="per-GPU batch (weak scaling)")
-    ap.add_argument("--rows", type=int, default=1_000_000_000, help="groupby: total rows")
+    ap.add_argument("--batch-size", type=int, default=int(os.environ.get("PTG_BENCH_BATCH", "0")),
+                    help="per-GPU batch (weak scaling); 0 = the workload default")
+    ap.add_argument("--rows", type=int, default=1_000_000_000, help="groupby: rows per GPU")
     ap.add_argument("--keys", type=int, default=1_000_000, help="groupby: distinct keys")
     ap.add_argument("--graph", type=int, default=int(os.environ.get("PTG_BENCH_GRAPH", "0")),
                     help="capture the train step in a HIP graph")
     ap.add_argument("--groupby-extra", type=int, default=int(os.environ.get("PTG_BENCH_GROUPBY", "1")),
                     help="after the CNN timing, also time the Spark groupBy half of the BASELINE metric and "
                          "report it under extra.groupby (1B rows per GPU)")
-    return ap.parse_args()
+    ap.add_argument("--extra-batches", default=os.environ.get("PTG_BENCH_EXTRA_BATCHES", "32,64"),
+                    help="cnn_b1: also time these per-GPU batches (the reference's 32 and 64) into extra")
+    ap.add_argument("--seed", type=int, default=1234)
+    return ap.parse_args(argv)
+
+
+DEFAULT_BATCH = {"cnn_b1": 256, "cnn_a1": 256, "resnet50": 128, "mnist": 512, "mlp": 4096}
 
 
 def _sync():
@@ -48,96 +59,178 @@ def _sync():
         torch.cuda.synchronize()
 
 
-def bench_cnn(args, strategy, rank, world):
-    from pyspark_tf_gke_amd.models import build_cnn_a1, build_cnn_model, build_mnist_cnn
+def _build(workload, B, dev, seed, rank, world):
+    """Model + two synthetic global batches; this rank keeps its [rank*B, (rank+1)*B) slice, so a
+    1-rank run at batch B*world sees exactly the union of what the N ranks see."""
+    from pyspark_tf_gke_amd.models import build_cnn_a1, build_cnn_model, build_deep_model, build_mnist_cnn
     from pyspark_tf_gke_amd.models.resnet import build_resnet50
+
+    torch.manual_seed(seed)  # identical initial weights on every rank and every world size
+    G = B * world
+    g = torch.Generator(device="cpu")
+    g.manual_seed(seed)
+    sl = slice(rank * B, (rank + 1) * B)
+
+    def img(h, w, c):
+        return [torch.randint(0, 256, (G, h, w, c), generator=g, dtype=torch.uint8)[sl].to(dev) for _ in range(2)]
+
+    if workload == "cnn_b1":
+        model = build_cnn_model((256, 320, 3), flat=True, summary=False)
+        meta = ("samples/sec TF CNN train", "CNN-B1 (train_tf_ps.py build_cnn_model flat=True, 256x320x3, 43.37M params)",
+                "256x320x3")
+        xs = img(256, 320, 3)
+        ys = [(torch.rand((G, 2), generator=g) * torch.tensor([320.0, 256.0]))[sl].to(dev) for _ in range(2)]
+    elif workload == "cnn_a1":
+        model = build_cnn_a1((256, 320, 3))
+        meta = ("samples/sec TF CNN train", "CNN-A1 (3-conv 32/64/128 + GAP, 4.86M params)", "256x320x3")
+        xs = img(256, 320, 3)
+        ys = [(torch.rand((G, 2), generator=g) * 256)[sl].to(dev) for _ in range(2)]
+    elif workload == "resnet50":
+        model = build_resnet50()
+        meta = ("samples/sec TF ResNet-50 train",
+                "ResNet-50 (keras.applications v1, 224x224x3, 1000 classes, 25.6M params)", "224x224x3")
+        xs = img(224, 224, 3)
+        ys = [torch.randint(0, 1000, (G,), generator=g)[sl].to(torch.int32).to(dev) for _ in range(2)]
+    elif workload == "mnist":
+        model = build_mnist_cnn()
+        meta = ("samples/sec TF CNN train", "MNIST CNN (28x28x1, conv32/conv64/dense128)", "28x28x1")
+        xs = [torch.rand((G, 28, 28, 1), generator=g)[sl].to(dev) for _ in range(2)]
+        ys = [torch.randint(0, 10, (G,), generator=g)[sl].to(torch.int32).to(dev) for _ in range(2)]
+    else:  # mlp: the reference's CSV MLP (train_tf_ps.py:328-343), 3 features -> 15 classes
+        model = build_deep_model(3, 15)
+        meta = ("samples/sec TF MLP train", "CSV-MLP (train_tf_ps.py build_deep_model 3->16->32->64->15, 3,695 params)",
+                "3 features")
+        xs = [torch.randn((G, 3), generator=g)[sl].to(dev) for _ in range(2)]
+        ys = [torch.randint(0, 15, (G,), generator=g)[sl].to(torch.int32).to(dev) for _ in range(2)]
+    return model, meta, xs, ys
+
+
+def _time_steps(model, xs, ys, steps, warmup):
     from pyspark_tf_gke_amd.parallel import comm
 
-    dev = strategy.device
-    B = args.batch_size
-    g = torch.Generator(device=dev)
-    g.manual_seed(1234 + rank)
-    with strategy.scope():
-        if args.workload == "cnn_b1":
-            model = build_cnn_model((256, 320, 3), flat=True, summary=False)
-            name, cfg_model = "samples/sec TF CNN train", "CNN-B1 (train_tf_ps.py build_cnn_model flat=True, 256x320x3, 43.37M params)"
-            xs = [torch.rand((B, 256, 320, 3), generator=g, device=dev) for _ in range(2)]
-            ys = [torch.rand((B, 2), generator=g, device=dev) * torch.tensor([320.0, 256.0], device=dev) for _ in range(2)]
-        elif args.workload == "cnn_a1":
-            model = build_cnn_a1((256, 320, 3))
-            name, cfg_model = "samples/sec TF CNN train", "CNN-A1 (3-conv 32/64/128 + GAP, 4.86M params)"
-            xs = [torch.rand((B, 256, 320, 3), generator=g, device=dev) for _ in range(2)]
-            ys = [torch.rand((B, 2), generator=g, device=dev) * 256 for _ in range(2)]
-        elif args.workload == "resnet50":
-            model = build_resnet50()
-            name, cfg_model = "samples/sec TF ResNet-50 train", "ResNet-50 (keras.applications v1, 224x224x3, 1000 classes, 25.6M params)"
-            xs = [torch.rand((B, 224, 224, 3), generator=g, device=dev) for _ in range(2)]
-            ys = [torch.randint(0, 1000, (B,), generator=g, device=dev).to(torch.int32) for _ in range(2)]
-        else:
-            model = build_mnist_cnn()
-            name, cfg_model = "samples/sec TF CNN train", "MNIST CNN (28x28x1, conv32/conv64/dense128)"
-            xs = [torch.rand((B, 28, 28, 1), generator=g, device=dev) for _ in range(2)]
-            ys = [torch.randint(0, 10, (B,), generator=g, device=dev).to(torch.int32) for _ in range(2)]
-    # pre-pack the images once into the device input format (bf16 NHWC, channel-padded) so the
-    # timed loop measures the training step, as a prefetching input pipeline would present it
-    first = model.first_op()
-    xs = [first._prep_input(x, model.ws).clone() if args.workload != "mnist" else x for x in xs]
     stats = model._stats_buf()
+    for i in range(warmup):
+        model.train_step_fast(xs[i % 2], ys[i % 2], stats)
+    _sync()
+    comm.barrier()
+    _sync()
+    stats.zero_()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        model.train_step_fast(xs[i % 2], ys[i % 2], stats)
+    _sync()
+    comm.barrier()
+    _sync()
+    dt = comm.all_reduce_max_scalar(time.perf_counter() - t0)
+    return dt, model._logs_from(stats)
 
+
+def _comm_probe(model, strategy, reps=5):
+    """The collectives of one training step (every gradient bucket's reduce-scatter and every
+    parameter bucket's all-gather, the exact sizes and dtypes of the step), timed alone: an upper
+    bound on the step's exposed communication (in the real step they overlap backward/forward)."""
+    from pyspark_tf_gke_amd.parallel import comm
+
+    plan = getattr(model, "_shard_plan", None)
+    if plan is None or strategy.world_size == 1:
+        return None
+    st = model.store
+    outs = {b.idx: torch.empty(b.shi - b.slo, dtype=torch.float32, device=st.flat.device) for b in plan.buckets}
+    strategy.wait_parameters(model)
+
+    def once():
+        for b in plan.buckets:
+            comm.reduce_scatter_flat(outs[b.idx], st.flat_grad[b.lo:b.hi])
+        for b in plan.buckets:
+            buf = st.flat if b.fp32 else st.flat_bf16
+            comm.all_gather_flat(buf[b.lo:b.hi], buf[b.slo:b.shi].clone())
+
+    once()
+    _sync()
+    comm.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        once()
+    _sync()
+    dt = comm.all_reduce_max_scalar(time.perf_counter() - t0) / reps
+    nbytes = sum((b.hi - b.lo) * 4 + (b.hi - b.lo) * (4 if b.fp32 else 2) for b in plan.buckets)
+    return {"comm_ms_isolated": round(dt * 1e3, 4), "buckets": len(plan.buckets),
+            "bytes_per_step": int(nbytes), "note": "reduce-scatter + all-gather of one step run alone"}
+
+
+def bench_train(args, strategy, rank, world):
+    dev = strategy.device
+    B = args.batch_size or DEFAULT_BATCH[args.workload]
+    with strategy.scope():
+        model, (name, cfg_model, shape), xs, ys = _build(args.workload, B, dev, args.seed, rank, world)
     if args.graph:
         model.jit_compile = True
-
-    def step(i):
-        model.train_step_fast(xs[i % 2], ys[i % 2], stats)
-
-    for i in range(args.warmup):
-        step(i)
-    _sync()
-    comm.barrier()
-    _sync()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(i)
-    _sync()
-    comm.barrier()
-    _sync()
-    dt = time.perf_counter() - t0
-    dt = comm.all_reduce_max_scalar(dt)
-    logs = model._logs_from(stats)
+    dt, logs = _time_steps(model, xs, ys, args.steps, args.warmup)
     ms = dt / args.steps * 1e3
-    value = B * world * args.steps / dt
-    return {
-        "metric": name, "value": round(value, 2), "unit": "samples/s", "ms_per_step": round(ms, 4),
-        "config": {"model": cfg_model, "global_batch": B * world, "per_gpu_batch": B,
-                   "input": {"mnist": "28x28x1", "resnet50": "224x224x3"}.get(args.workload, "256x320x3"),
-                   "parallelism": f"dp{world}" + (" (MultiWorkerMirroredStrategy, RCCL all-reduce)" if world > 1 else ""),
-                   "optimizer": ("SGD(0.1, momentum 0.9)" if args.workload == "resnet50" else "Adam(1e-3)") + " fused flat",
-                   "final_loss": round(logs["loss"], 4)},
-    }
+    opt = {"resnet50": "SGD(0.1, momentum 0.9)"}.get(args.workload, "Adam(1e-3)") + " fused flat"
+    res = {"metric": name, "value": round(B * world * args.steps / dt, 2), "unit": "samples/s",
+           "ms_per_step": round(ms, 4),
+           "config": {"model": cfg_model, "global_batch": B * world, "per_gpu_batch": B, "input": shape,
+                      "parallelism": f"dp{world}" + (" (MultiWorkerMirroredStrategy, RCCL reduce-scatter/all-gather)"
+                                                     if world > 1 else ""),
+                      "optimizer": opt, "final_loss": round(logs["loss"], 6),
+                      "input_pipeline": ("in the timed step: uint8 NHWC images resident in HBM -> /255, "
+                                         "channel-padded bf16 (pack_u8rgb4_k)") if args.workload != "mlp"
+                      else "fp32 features resident in HBM"}}
+    probe = _comm_probe(model, strategy)
+    if probe is not None:
+        res["comm"] = probe
+    del model, xs, ys
+    return res
 
 
 def bench_groupby(args, strategy, rank, world):
     from pyspark_tf_gke_amd.sql import bench_groupby as bg
 
-    res = bg.run(total_rows=args.rows, num_keys=args.keys, steps=args.steps, warmup=args.warmup,
-                 device=strategy.device)
-    return res
+    return bg.run(rows_per_gpu=args.rows, num_keys=args.keys, steps=args.steps, warmup=args.warmup,
+                  device=strategy.device)
+
+
+def _self_launch(args) -> int | None:
+    """``--gpus N`` with no launcher around us: run N fresh ranks and return their exit code."""
+    if "WORLD_SIZE" in os.environ or args.gpus <= 1:
+        return None
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from pyspark_tf_gke_amd.runtime.launcher import launch
+
+    cmd = [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
+    return launch(cmd, args.gpus, master_addr="127.0.0.1", prefix_output=False)
 
 
 def main():
     args = parse()
-    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    rc = _self_launch(args)
+    if rc is not None:
+        return rc
     from pyspark_tf_gke_amd.distribute import MultiWorkerMirroredStrategy
+    from pyspark_tf_gke_amd.parallel import comm
 
     strategy = MultiWorkerMirroredStrategy()
     rank, world = strategy.rank, strategy.world_size
-    if world != world_env:
-        raise RuntimeError(f"world mismatch {world} vs {world_env}")
+    if world != args.gpus:
+        raise RuntimeError(f"--gpus {args.gpus} but the job has {world} ranks (WORLD_SIZE="
+                           f"{os.environ.get('WORLD_SIZE')})")
     extra = {}
     if args.workload == "groupby":
         res = bench_groupby(args, strategy, rank, world)
+        dtype, data = "fp64", "synthetic (bigint keys = hash(row) % keys, double values), resident in HBM"
     else:
-        res = bench_cnn(args, strategy, rank, world)
+        res = bench_train(args, strategy, rank, world)
+        dtype = "bf16" if strategy.device.type == "cuda" else "fp32 (host reference path, no GPU)"
+        data = ("synthetic (random features / labels of the reference shape; random-init weights)"
+                if args.workload == "mlp" else
+                "synthetic (random uint8 images / targets of the reference shape; random-init weights)")
+        if args.workload == "cnn_b1" and args.extra_batches:
+            for b in [int(x) for x in args.extra_batches.split(",") if x.strip()]:
+                a2 = argparse.Namespace(**{**vars(args), "batch_size": b})
+                r2 = bench_train(a2, strategy, rank, world)
+                extra[f"batch{b}"] = {"value": r2["value"], "unit": "samples/s", "ms_per_step": r2["ms_per_step"],
+                                      "per_gpu_batch": b, "global_batch": b * world}
         if args.workload == "cnn_b1" and args.groupby_extra and torch.cuda.is_available():
             # second half of BASELINE.json's metric ("rows/sec Spark groupBy + samples/sec TF CNN
             # train"); timed separately, after the CNN steps, so it cannot perturb them
@@ -151,20 +244,19 @@ def main():
                 extra["groupby"] = {"metric": gb["metric"], "value": gb["value"], "unit": gb["unit"],
                                     "ms_per_step": gb["ms_per_step"], "rows_per_gpu": gb["config"]["rows_per_gpu"],
                                     "distinct_keys": gb["config"]["distinct_keys"],
-                                    "counts_check": gb["config"]["counts_check"]}
+                                    "counts_check": gb["config"]["counts_check"], "dtype": "fp64"}
             except Exception as e:  # noqa: BLE001 - never lose the headline line
                 extra["groupby"] = {"error": repr(e)[:300]}
     out = {"metric": res["metric"], "value": res["value"], "unit": res["unit"], "n_gpus": world,
            "steps": args.steps, "warmup": args.warmup, "ms_per_step": res["ms_per_step"],
-           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
-           "data": "synthetic (random images/targets of the reference shape; random-init weights)",
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": dtype, "data": data,
            "config": res["config"]}
+    if "comm" in res:
+        out["comm"] = res["comm"]
     if extra:
         out["extra"] = extra
     if rank == 0:
         print(json.dumps(out), flush=True)
-    from pyspark_tf_gke_amd.parallel import comm
-
     comm.destroy()
     return 0
 

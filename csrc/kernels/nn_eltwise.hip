@@ -972,6 +972,26 @@ __global__ __launch_bounds__(256) void resize_norm_k(const uint8_t* __restrict__
   }
 }
 
+// Same-size uint8 images [N][H][W][3] -> bf16 [N][H][W][4] / 255 (the decoded-image input pipeline
+// when no resize is needed): 4 pixels per thread = three 4-byte loads in, two 16-byte stores out.
+__global__ __launch_bounds__(256) void pack_u8rgb4_k(const uint32_t* __restrict__ in, U4* __restrict__ out,
+                                                     long nquad) {
+  constexpr float s = 1.f / 255.f;
+  for (long q = blockIdx.x * 256L + threadIdx.x; q < nquad; q += (long)gridDim.x * 256) {
+    const uint32_t a = in[q * 3], b = in[q * 3 + 1], c = in[q * 3 + 2];
+    const uint32_t by[12] = {a & 255, (a >> 8) & 255, (a >> 16) & 255, a >> 24,
+                             b & 255, (b >> 8) & 255, (b >> 16) & 255, b >> 24,
+                             c & 255, (c >> 8) & 255, (c >> 16) & 255, c >> 24};
+    U4 o0, o1;
+    o0.x = pack_bf(by[0] * s, by[1] * s); o0.y = pack_bf(by[2] * s, 0.f);
+    o0.z = pack_bf(by[3] * s, by[4] * s); o0.w = pack_bf(by[5] * s, 0.f);
+    o1.x = pack_bf(by[6] * s, by[7] * s); o1.y = pack_bf(by[8] * s, 0.f);
+    o1.z = pack_bf(by[9] * s, by[10] * s); o1.w = pack_bf(by[11] * s, 0.f);
+    out[q * 2] = o0;
+    out[q * 2 + 1] = o1;
+  }
+}
+
 // float images [N][H][W][3] in [0,1] -> 4-channel bf16
 __global__ __launch_bounds__(256) void pack_rgb4_k(const float* __restrict__ in, bf16_t* __restrict__ out,
                                                    long npix) {
@@ -1308,6 +1328,12 @@ int ptg_cast_bf16_f32(const void* x, float* y, long n, hipStream_t s) {
 int ptg_resize_norm(const void* in_u8, void* out, int N, int Hin, int Win, int H, int W, hipStream_t s) {
   hipLaunchKernelGGL(resize_norm_k, dim3(grid_for((long)N * H * W)), dim3(256), 0, s, (const uint8_t*)in_u8,
                      (bf16_t*)out, N, Hin, Win, H, W);
+  PTG_RETURN_LAUNCH();
+}
+int ptg_pack_u8rgb4(const void* in_u8, void* out, long npix, hipStream_t s) {
+  if (npix % 4 || ((uintptr_t)in_u8 & 3) || ((uintptr_t)out & 15)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(pack_u8rgb4_k, dim3(grid_for(npix / 4)), dim3(256), 0, s, (const uint32_t*)in_u8, (U4*)out,
+                     npix / 4);
   PTG_RETURN_LAUNCH();
 }
 int ptg_pack_rgb4(const float* in, void* out, long npix, hipStream_t s) {

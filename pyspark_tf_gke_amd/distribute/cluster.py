@@ -9,6 +9,8 @@ only: the roles map onto local ranks (rank r = worker r = PS shard r) and tensor
 """
 from __future__ import annotations
 
+import math
+
 import json
 import os
 from dataclasses import dataclass
@@ -106,22 +108,30 @@ class InputContext:
 
 class MinSizePartitioner:
     """``tf.distribute.experimental.partitioners.MinSizePartitioner`` (train_tf_ps.py:505-507):
-    shards of at least ``min_shard_bytes``, at most ``max_shards``.  Here it decides how the flat
-    parameter buffer is cut into PS shards (byte ranges owned by ranks)."""
+    a variable is cut along axis 0 into as many shards as keep every shard >= ``min_shard_bytes``
+    (whole rows per shard), at most ``max_shards``.  TF's rule (min_max_variable_partitioner):
+    slices_per_shard = max(1, ceil(min_shard_bytes / bytes_per_row)); shards = min(max_shards,
+    ceil(rows / slices_per_shard)).  :class:`~.strategy.ParameterServerStrategy` places each shard
+    on a PS task round-robin, the way TF's variable placement does."""
 
     def __init__(self, min_shard_bytes: int = 256 << 10, max_shards: int = 1, bytes_per_string: int = 16):
         self.min_shard_bytes = int(min_shard_bytes)
         self.max_shards = max(1, int(max_shards))
 
-    def num_shards(self, nbytes: int) -> int:
-        return max(1, min(self.max_shards, nbytes // max(self.min_shard_bytes, 1)))
-
-    def __call__(self, shape, dtype_size: int = 4):
+    def num_shards(self, shape, dtype_size: int = 4) -> int:
+        shape = tuple(int(s) for s in shape) or (1,)
+        rows = max(shape[0], 1)
         n = 1
         for s in shape:
-            n *= int(s)
-        k = self.num_shards(n * dtype_size)
-        return [k] + [1] * (len(shape) - 1)
+            n *= s
+        bytes_per_row = n * dtype_size / rows
+        if bytes_per_row <= 0:
+            return 1
+        slices_per_shard = max(1, math.ceil(self.min_shard_bytes / bytes_per_row))
+        return max(1, min(self.max_shards, math.ceil(rows / slices_per_shard)))
+
+    def __call__(self, shape, dtype_size: int = 4):
+        return [self.num_shards(shape, dtype_size)] + [1] * (len(tuple(shape)) - 1)
 
 
 class Server:

@@ -44,6 +44,10 @@ class Strategy:
         else:
             self.device = torch.device("cpu")
         self.models: list = []
+        self.optimizers: list = []
+        self._in_round = False
+        self._pending = None
+        self._commit_scale = 1.0
 
     @property
     def num_replicas_in_sync(self) -> int:
@@ -104,13 +108,62 @@ class Strategy:
         pass
 
     def apply_update(self, model, optimizer=None) -> None:
-        (optimizer or model.optimizer).apply(model.store)
+        if self.in_round():
+            self._defer(model, optimizer)
+            return
+        (optimizer or model.optimizer).apply(model.store, gscale=self._commit_scale)
 
-    def null_step(self, model, optimizer=None) -> None:
-        """Take part in a step's collectives with a zero gradient (coordinator rounds)."""
-        model.store.flat_grad.zero_()
-        self.finish_gradients(model)
-        self.apply_update(model, optimizer)
+    # ---- ClusterCoordinator rounds (see coordinator.py): inside a round the gradient sync and the
+    # update are deferred; after every rank ran (or failed, or had no) closure, the ranks agree on
+    # who contributed and commit the round together, so every rank issues the same collectives.
+    def begin_round(self) -> None:
+        self._in_round = True
+        self._pending = None
+
+    def end_round_local(self) -> None:
+        self._in_round = False
+
+    def in_round(self) -> bool:
+        return getattr(self, "_in_round", False)
+
+    def _defer(self, model, optimizer) -> None:
+        opt = optimizer or model.optimizer
+        if getattr(self, "_pending", None) not in (None, (model, opt)):
+            raise RuntimeError("a coordinator closure may update only one (model, optimizer) pair")
+        self._pending = (model, opt)
+
+    def pending_ids(self) -> tuple[int, int]:
+        """(model index, optimizer index) of this rank's deferred update, or (-1, -1)."""
+        pend = getattr(self, "_pending", None)
+        if pend is None:
+            return -1, -1
+        model, opt = pend
+        if opt not in self.optimizers:
+            self.optimizers.append(opt)
+        return self.models.index(model), self.optimizers.index(opt)
+
+    def abort_round(self) -> None:
+        pend = getattr(self, "_pending", None)
+        if pend is not None:
+            pend[0].store.flat_grad.zero_()
+        self._pending = None
+
+    def commit_round(self, model, optimizer, contributed: list) -> None:
+        """Collective.  Apply one round: ``contributed[r]`` says whether rank r holds a gradient.
+        Default (mirrored): average over the contributors; a rank without one pushes zeros; no
+        update at all when nobody contributed (the optimizer does not advance)."""
+        n_ok = sum(bool(c) for c in contributed)
+        if not contributed[self.rank]:
+            model.store.flat_grad.zero_()
+        if n_ok == 0:
+            return
+        self._commit_scale = float(self.world_size) / n_ok
+        try:
+            self.finish_gradients(model)
+            self.apply_update(model, optimizer)
+        finally:
+            self._commit_scale = 1.0
+        self._pending = None
 
 
 class OneDeviceStrategy(Strategy):
@@ -303,7 +356,7 @@ class MultiWorkerMirroredStrategy(Strategy):
 
     # ---- engine hooks
     def on_op_grads_ready(self, model, op) -> None:
-        if self.world_size == 1 or not op.params:
+        if self.world_size == 1 or not op.params or self.in_round():
             return
         plan = getattr(model, "_shard_plan", None)
         if plan is not None:
@@ -323,7 +376,7 @@ class MultiWorkerMirroredStrategy(Strategy):
             self._launch(model, hi)
 
     def finish_gradients(self, model) -> None:
-        if self.world_size == 1:
+        if self.world_size == 1 or self.in_round():
             return
         plan = getattr(model, "_shard_plan", None)
         if plan is not None:
@@ -345,15 +398,19 @@ class MultiWorkerMirroredStrategy(Strategy):
         self._launched = 0
 
     def apply_update(self, model, optimizer=None) -> None:
+        if self.in_round():
+            self._defer(model, optimizer)
+            return
         opt = optimizer or model.optimizer
         plan = getattr(model, "_shard_plan", None)
+        gs = self._commit_scale / self.world_size
         if plan is None:
-            opt.apply(model.store, gscale=1.0 / self.world_size)
+            opt.apply(model.store, gscale=gs)
             return
         st = model.store
         self.wait_parameters(model)  # (no-op in steady state: the forward waited for every bucket)
         for b in plan.buckets:
-            opt.apply_shard(st, b.gshard, b.slo, b.shi, gscale=1.0 / self.world_size, advance=False)
+            opt.apply_shard(st, b.gshard, b.slo, b.shi, gscale=gs, advance=False)
         opt.iterations += 1
         for b in plan.buckets:
             buf = st.flat if b.fp32 else st.flat_bf16
@@ -365,66 +422,238 @@ class MultiWorkerMirroredStrategy(Strategy):
 MirroredStrategy = MultiWorkerMirroredStrategy
 
 
-class ParameterServerStrategy(Strategy):
-    """Synchronous sharded parameter server.  ``mode='sync'`` is the only mode: the reference's
-    asynchronous PS has every worker apply updates to PS variables independently; on one xGMI node
-    the sharded synchronous form moves the same bytes per step as collectives (reduce-scatter +
-    all-gather of the flat buffer) without a central bottleneck."""
+class _Piece:
+    __slots__ = ("param", "lo", "n", "owner", "xlo", "task")
 
-    def __init__(self, cluster_resolver=None, variable_partitioner=None, device=None):
+    def __init__(self, param, lo, n, owner, task):
+        self.param, self.lo, self.n, self.owner, self.task = param, lo, n, owner, task
+        self.xlo = -1
+
+
+class _PSPlan:
+    """Variable placement of one model: every parameter is cut by the partitioner along axis 0
+    (whole rows per shard, TF's MinSizePartitioner rule) and shard i of the running count goes to
+    PS task ``i % num_ps`` (TF's round-robin variable placement); PS task t lives on rank
+    ``t % world``.  An owner's shards are packed into its segment of an exchange buffer of
+    ``world * seg`` elements, so "push" is ONE reduce-scatter (sync) or one send per owner (async)
+    and "pull" is ONE all-gather, whatever the placement.  The owner keeps its shards' fp32 values
+    and optimizer moments in packed form: the variables live on the PS."""
+
+    def __init__(self, model, partitioner, num_ps: int, world: int, rank: int):
+        from ..nn.params import ALIGN
+
+        st = model.store
+        self.pieces: list[_Piece] = []
+        task = 0
+        for p in sorted(st.params, key=lambda q: q.order):  # variable creation order
+            k = partitioner.num_shards(p.shape, 4) if partitioner is not None else 1
+            rows = p.shape[0] if p.shape else 1
+            row_elems = p.numel // max(rows, 1)
+            k = max(1, min(k, rows))
+            base, rem = divmod(rows, k)
+            r0 = 0
+            for j in range(k):
+                nr = base + (1 if j < rem else 0)
+                t = task % num_ps
+                self.pieces.append(_Piece(p, p.offset + r0 * row_elems, nr * row_elems, t % world, t))
+                r0 += nr
+                task += 1
+        per_owner = [0] * world
+        for pc in self.pieces:
+            pc.xlo = per_owner[pc.owner]
+            per_owner[pc.owner] += pc.n
+        self.owner_elems = per_owner
+        self.seg = max(ALIGN, int(math.ceil(max(per_owner) / ALIGN) * ALIGN))
+        for pc in self.pieces:
+            pc.xlo += pc.owner * self.seg
+        self.world, self.rank = world, rank
+        self.mine = [pc for pc in self.pieces if pc.owner == rank]
+        dev = st.flat.device
+        self.xbuf = torch.zeros(world * self.seg, dtype=torch.float32, device=dev)  # exchange buffer
+        self.gshard = torch.zeros(self.seg, dtype=torch.float32, device=dev)
+        self.master = torch.zeros(self.seg, dtype=torch.float32, device=dev)  # owned values
+        self.master_bf = torch.zeros(self.seg, dtype=st.flat_bf16.dtype, device=dev)
+        self.slots: dict[str, torch.Tensor] = {}  # packed optimizer moments of the owned shards
+        self.pack_params(st)
+
+    def placement(self) -> list:
+        """[(param name, row range, ps task, owner rank)] — the variable-to-PS map."""
+        out = []
+        for pc in self.pieces:
+            rows = pc.param.shape[0] if pc.param.shape else 1
+            re = pc.param.numel // max(rows, 1)
+            r0 = (pc.lo - pc.param.offset) // max(re, 1)
+            out.append((pc.param.name, (r0, r0 + pc.n // max(re, 1)), pc.task, pc.owner))
+        return out
+
+    def pack(self, src: torch.Tensor, dst: torch.Tensor, only_mine: bool = False) -> None:
+        for pc in (self.mine if only_mine else self.pieces):
+            x0 = pc.xlo - (self.rank * self.seg if only_mine else 0)
+            dst[x0:x0 + pc.n].copy_(src[pc.lo:pc.lo + pc.n])
+
+    def unpack(self, src: torch.Tensor, dst: torch.Tensor) -> None:
+        for pc in self.pieces:
+            dst[pc.lo:pc.lo + pc.n].copy_(src[pc.xlo:pc.xlo + pc.n])
+
+    def pack_params(self, st) -> None:
+        self.pack(st.flat, self.master, only_mine=True)
+
+    def slot(self, name: str) -> torch.Tensor:
+        t = self.slots.get(name)
+        if t is None:
+            t = self.slots[name] = torch.zeros(self.seg, dtype=torch.float32, device=self.master.device)
+        return t
+
+
+class ParameterServerStrategy(Strategy):
+    """The reference's strategy (train_tf_ps.py:440-511) on GPU ranks: every rank is a worker and
+    hosts PS tasks.  Variables are placed per shard by ``variable_partitioner`` (default
+    ``MinSizePartitioner(256 KiB, max_shards=#ps)``, :505-507) round-robin over the PS tasks; PS
+    task t lives on rank ``t % world`` (``num_ps`` from the cluster spec, or one per rank).
+
+    ``mode="sync"`` (default): a step pushes gradients with one reduce-scatter of the packed
+    exchange buffer (owners receive the sum), owners apply the optimizer to the shards they host
+    with the gradient averaged over the workers that contributed, and every worker pulls the new
+    values with one all-gather (M1/M2 of SURVEY §2.2.c).
+
+    ``mode="async"`` (TF's asynchronous PS semantics): each worker's gradient is sent point-to-point
+    to the owner of every shard (``batch_isend_irecv``; RCCL runs it on its own stream) and the
+    owner applies it as its own optimizer step, in worker order, without averaging; workers pull the
+    values after all pushes of the round were applied, so a worker's gradient is up to
+    ``workers - 1`` updates stale, as under TF's asynchronous PS with that many concurrent workers.
+
+    Under :class:`~.coordinator.ClusterCoordinator` the push/apply is committed per round after the
+    ranks agree who contributed: no zero-gradient pushes, no optimizer step when nobody did."""
+
+    def __init__(self, cluster_resolver=None, variable_partitioner=None, device=None, mode: str | None = None):
         super().__init__(device)
         self.cluster_resolver = cluster_resolver or TFConfigClusterResolver()
         spec = self.cluster_resolver.cluster_spec() if hasattr(self.cluster_resolver, "cluster_spec") else ClusterSpec({})
         self.cluster_spec = ClusterSpec(spec)
         self.num_workers = max(self.cluster_spec.num_tasks("worker"), self.world_size)
-        self.num_ps = self.cluster_spec.num_tasks("ps")
+        self.num_ps = self.cluster_spec.num_tasks("ps") or self.world_size
         self.variable_partitioner = variable_partitioner or MinSizePartitioner(256 << 10, max(self.num_ps, 1))
-        self._gshard = None
-
-    def shard_range(self, model) -> tuple[int, int]:
-        total = model.store.total
-        per = total // self.world_size
-        return self.rank * per, (self.rank + 1) * per
+        self.mode = (mode or os.environ.get("PTG_PS_MODE", "sync")).lower()
+        if self.mode not in ("sync", "async"):
+            raise ValueError(f"ParameterServerStrategy mode must be 'sync' or 'async', not {self.mode!r}")
 
     def register_model(self, model) -> None:
-        st = model.store
-        pad = 1024
-        if st.total % pad:
-            # pad the flat buffers so the byte range splits evenly over the PS shards
-            new_total = int(math.ceil(st.total / pad) * pad)
-            for name in ("flat", "flat_grad", "flat_bf16"):
-                t = getattr(st, name)
-                nt = torch.zeros(new_total, dtype=t.dtype, device=t.device)
-                nt[: st.total] = t
-                setattr(st, name, nt)
-            st.total = new_total
-            st._bind_views()
-        super().register_model(model)
+        super().register_model(model)  # broadcast rank 0's initial values first
+        model._ps_plan = _PSPlan(model, self.variable_partitioner, self.num_ps, self.world_size, self.rank)
 
-    def finish_gradients(self, model) -> None:
-        if self.world_size == 1:
+    def placement(self, model) -> list:
+        return model._ps_plan.placement()
+
+    # ---- optimizer on the owned (packed) shards
+    def _apply_owned(self, model, opt, grad: torch.Tensor, gscale: float) -> None:
+        from ..nn import optimizers as OPT
+        from ..ops import nn as K
+
+        plan = model._ps_plan
+        n = plan.seg
+        if isinstance(opt, OPT.Adam):
+            step = opt.iterations + 1
+            K.adam(plan.master[:n], grad[:n], plan.slot("m"), plan.slot("v"), plan.master_bf[:n], opt.lr_t(step),
+                   opt.beta_1, opt.beta_2, opt.epsilon, gscale)
+        elif isinstance(opt, OPT.SGD):
+            vel = plan.slot("velocity") if opt.momentum > 0 else None
+            K.sgd(plan.master[:n], grad[:n], vel, plan.master_bf[:n], opt.learning_rate, opt.momentum, opt.nesterov,
+                  gscale)
+        else:
+            raise TypeError(f"unsupported optimizer {type(opt).__name__}")
+        opt.iterations += 1
+
+    def _pull(self, model) -> None:
+        from ..ops import nn as K
+
+        plan = model._ps_plan
+        st = model.store
+        comm.all_gather_flat(plan.xbuf, plan.master)
+        plan.unpack(plan.xbuf, st.flat)
+        K.cast_f32_bf16(st.flat, st.flat_bf16)
+
+    def _push_apply(self, model, opt, contributed: list) -> None:
+        plan = model._ps_plan
+        st = model.store
+        n_ok = sum(bool(c) for c in contributed)
+        if n_ok == 0:
             return
-        lo, hi = self.shard_range(model)
-        if self._gshard is None or self._gshard.numel() != hi - lo or self._gshard.device != model.store.flat.device:
-            self._gshard = torch.empty(hi - lo, dtype=torch.float32, device=model.store.flat.device)
-        comm.reduce_scatter_flat(self._gshard, model.store.flat_grad)
-
-    def apply_update(self, model, optimizer=None) -> None:
-        opt = optimizer or model.optimizer
-        st = model.store
         if self.world_size == 1:
             opt.apply(st)
             return
-        from ..ops import nn as K
+        if self.mode == "sync":
+            if contributed[self.rank]:
+                plan.pack(st.flat_grad, plan.xbuf)
+            else:
+                plan.xbuf.zero_()
+            comm.reduce_scatter_flat(plan.gshard, plan.xbuf)
+            self._apply_owned(model, opt, plan.gshard, 1.0 / n_ok)
+        else:
+            import torch.distributed as dist
 
-        lo, hi = self.shard_range(model)
-        opt.apply_shard(st, self._gshard, lo, hi, 1.0 / self.world_size)
-        comm.all_gather_flat(st.flat, st.flat[lo:hi].clone())
-        K.cast_f32_bf16(st.flat, st.flat_bf16)
+            if contributed[self.rank]:
+                plan.pack(st.flat_grad, plan.xbuf)
+            ops, recv = [], {}
+            for w in range(self.world_size):
+                if w == self.rank or not contributed[w]:
+                    continue
+                recv[w] = torch.empty(plan.seg, dtype=torch.float32, device=plan.xbuf.device)
+                ops.append(dist.P2POp(dist.irecv, recv[w], w))
+            if contributed[self.rank]:
+                for r in range(self.world_size):
+                    if r != self.rank:
+                        ops.append(dist.P2POp(dist.isend, plan.xbuf[r * plan.seg:(r + 1) * plan.seg], r))
+            if ops:
+                for req in dist.batch_isend_irecv(ops):
+                    req.wait()
+            for w in range(self.world_size):  # apply each worker's push as its own step, in order
+                if not contributed[w]:
+                    continue
+                g = plan.xbuf[self.rank * plan.seg:(self.rank + 1) * plan.seg] if w == self.rank else recv[w]
+                self._apply_owned(model, opt, g, 1.0)
+        self._pull(model)
 
-    def null_step(self, model, optimizer=None) -> None:
-        """Participate in a step's collectives with zero gradient (ranks without a scheduled closure
-        in the last round of ``ClusterCoordinator.join``)."""
-        model.store.flat_grad.zero_()
-        self.finish_gradients(model)
-        self.apply_update(model, optimizer)
+    # ---- engine hooks
+    def finish_gradients(self, model) -> None:
+        pass  # the push happens in apply_update (after the whole backward)
+
+    def apply_update(self, model, optimizer=None) -> None:
+        if self.in_round():
+            self._defer(model, optimizer)
+            return
+        self._push_apply(model, optimizer or model.optimizer, [True] * self.world_size)
+
+    def commit_round(self, model, optimizer, contributed: list) -> None:
+        self._push_apply(model, optimizer or model.optimizer, contributed)
+        self._pending = None
+
+    # ---- checkpoint support: the canonical optimizer state is per parameter (full layout)
+    def synchronize_state(self, model) -> None:
+        """Collective: unpack every owner's moments into the optimizer's full-layout slots (and the
+        values into the store) on every rank, so checkpoints are stored per parameter name."""
+        plan = getattr(model, "_ps_plan", None)
+        opt = model.optimizer
+        if plan is None or self.world_size == 1:
+            return
+        self._pull(model)
+        if opt is None:
+            return
+        opt.build(model.store)
+        for name, full in opt.state_tensors().items():
+            if full is None or full.numel() != model.store.total:
+                continue
+            comm.all_gather_flat(plan.xbuf, plan.slot(name))
+            plan.unpack(plan.xbuf, full)
+
+    def on_state_loaded(self, model) -> None:
+        """After a checkpoint load into the full layout: re-pack the owned shards."""
+        plan = getattr(model, "_ps_plan", None)
+        if plan is None:
+            return
+        plan.pack_params(model.store)
+        opt = model.optimizer
+        if opt is None:
+            return
+        for name, full in opt.state_tensors().items():
+            if full is not None and full.numel() == model.store.total:
+                plan.pack(full, plan.slot(name), only_mine=True)

@@ -22,6 +22,7 @@ import torch
 
 from ..ops import nn as K
 from ..runtime import fault as _fault
+from ..runtime import heartbeat as _heartbeat
 from . import engine as E
 from . import layers as L
 from . import losses as LS
@@ -332,6 +333,7 @@ class Sequential:
 
     def train_step(self, xb, yb, stats=None) -> None:
         _fault.maybe_fail()
+        _heartbeat.progress()
         st = self._strategy()
         stats = self._stats_buf() if stats is None else stats
         self.store.zero_grad()

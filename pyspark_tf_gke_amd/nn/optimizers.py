@@ -19,9 +19,24 @@ class Optimizer:
     def __init__(self, learning_rate: float):
         self.learning_rate = float(learning_rate)
         self.iterations = 0
+        from ..distribute.strategy import current_strategy
+
+        st = current_strategy()
+        if st is not None:
+            # created under strategy.scope(): every rank registers its optimizers in the same
+            # order, so coordinator rounds can name the optimizer of an update by index
+            st.optimizers.append(self)
 
     def get_config(self) -> dict:
         return {"name": type(self).__name__.lower(), "learning_rate": self.learning_rate}
+
+    def set_iterations(self, n: int) -> None:
+        """Set the step counter everywhere it lives: the host count and, after HIP-graph capture,
+        the on-device counter the replayed graphs read for Adam's bias correction."""
+        self.iterations = int(n)
+        ds = getattr(self, "dev_state", None)
+        if ds is not None:
+            ds[0] = float(self.iterations)
 
     def apply_gradients(self, grads_and_vars) -> None:
         from .tape import apply_gradients

@@ -484,7 +484,9 @@ def sgd(p, g, vel, pbf, lr: float, momentum: float, nesterov: bool, gscale: floa
 
 def cast_f32_bf16(x, out):
     if not on_device(x):
-        out.copy_(x.to(torch.bfloat16))
+        # host mode: the "bf16" mirror may be fp32 (PTG_HOST_FP32, possibly aliasing ``x``)
+        if out.data_ptr() != x.data_ptr():
+            out.copy_(x.to(out.dtype))
         return out
     hip("ptg_cast_f32_bf16", ptr(x), ptr(out), x.numel())
     return out
@@ -495,6 +497,10 @@ def resize_norm(images_u8, out, H: int, W: int):
     if not on_device(images_u8):
         return ref.resize_norm(images_u8, out, H, W)
     N, Hin, Win, _ = images_u8.shape
+    if (Hin, Win) == (H, W) and (N * H * W) % 4 == 0:
+        # no resize: a pure byte -> bf16 pack (bilinear weights would all be 0/1)
+        hip("ptg_pack_u8rgb4", ptr(images_u8), ptr(out), N * H * W)
+        return out
     hip("ptg_resize_norm", ptr(images_u8), ptr(out), N, Hin, Win, H, W)
     return out
 

@@ -29,9 +29,13 @@ def is_initialized() -> bool:
     return dist.is_available() and dist.is_initialized()
 
 
-def init(backend: str | None = None, device_type: str | None = None, timeout_s: int = 600) -> tuple[int, int]:
+def init(backend: str | None = None, device_type: str | None = None, timeout_s: int | None = None) -> tuple[int, int]:
     """Initialise the default process group from the environment (idempotent).
-    Returns (rank, world_size)."""
+    Returns (rank, world_size).  ``timeout_s`` (default ``PTG_PG_TIMEOUT`` or 600 s) bounds every
+    collective: a rank whose peer died or hung gets an error (gloo) or is aborted by the RCCL
+    watchdog instead of blocking forever, exits non-zero, and the launcher restarts the group."""
+    if timeout_s is None:
+        timeout_s = int(float(os.environ.get("PTG_PG_TIMEOUT", "600")))
     rank, local, world = env_rank()
     if is_initialized():
         return dist.get_rank(), dist.get_world_size()
@@ -53,8 +57,11 @@ def init(backend: str | None = None, device_type: str | None = None, timeout_s: 
             kw["device_id"] = torch.device("cuda", dev)
     dist.init_process_group(backend=backend, rank=rank, world_size=world,
                             timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    import atexit
+
     from ..runtime import heartbeat
 
+    atexit.register(destroy)  # orderly teardown: no backend threads left running at interpreter exit
     heartbeat.start()
     return rank, world
 
@@ -121,6 +128,76 @@ def all_to_all_v(send: torch.Tensor, send_counts: list[int], recv_counts: list[i
     dist.all_to_all_single(out, send, output_split_sizes=[int(c) for c in recv_counts],
                            input_split_sizes=[int(c) for c in send_counts])
     return out
+
+
+# ---- tensor control plane: small scalars / vectors travel as tensors (one collective each), never as
+# pickled Python objects (no host serialisation, no extra all_gather of byte sizes)
+def _ctl_device() -> torch.device:
+    if is_initialized() and dist.get_backend() == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def all_reduce_int(values, op=dist.ReduceOp.SUM) -> list:
+    """All-reduce a short list of Python ints (int64) -> list of ints."""
+    vals = [int(v) for v in values]
+    if not is_initialized() or dist.get_world_size() == 1:
+        return vals
+    t = torch.tensor(vals, dtype=torch.int64, device=_ctl_device())
+    dist.all_reduce(t, op=op)
+    return [int(x) for x in t.cpu().tolist()]
+
+
+def all_reduce_float(values, op=dist.ReduceOp.SUM) -> list:
+    """All-reduce a short list of Python floats (fp64) -> list of floats."""
+    vals = [float(v) for v in values]
+    if not is_initialized() or dist.get_world_size() == 1:
+        return vals
+    t = torch.tensor(vals, dtype=torch.float64, device=_ctl_device())
+    dist.all_reduce(t, op=op)
+    return [float(x) for x in t.cpu().tolist()]
+
+
+def all_reduce_tensor_(t: torch.Tensor, op=dist.ReduceOp.SUM) -> torch.Tensor:
+    """In-place all-reduce of a tensor on whatever device it lives (staged through the control
+    device when the backend cannot reach it, e.g. CPU tensors under RCCL)."""
+    if not is_initialized() or dist.get_world_size() == 1:
+        return t
+    dev = _ctl_device()
+    if t.device == dev or (dev.type == "cuda" and t.is_cuda):
+        dist.all_reduce(t, op=op)
+        return t
+    s = t.to(dev)
+    dist.all_reduce(s, op=op)
+    t.copy_(s.to(t.device))
+    return t
+
+
+def all_gather_v(t: torch.Tensor) -> list:
+    """Variable-length all-gather along dim 0 -> list of per-rank tensors (on ``t``'s device).
+    One int64 all-gather of the lengths, then one all_gather_into_tensor of the padded rows."""
+    if not is_initialized() or dist.get_world_size() == 1:
+        return [t]
+    world = dist.get_world_size()
+    dev = _ctl_device()
+    n = torch.tensor([t.shape[0]], dtype=torch.int64, device=dev)
+    ns = torch.empty(world, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(ns, n)
+    lens = [int(x) for x in ns.cpu().tolist()]
+    mx = max(lens)
+    row = t.shape[1:]
+    src = torch.zeros((mx, *row), dtype=t.dtype, device=dev)
+    if t.shape[0]:
+        src[: t.shape[0]] = t.to(dev)
+    out = torch.empty((world * mx, *row), dtype=t.dtype, device=dev)
+    dist.all_gather_into_tensor(out, src)
+    return [out[r * mx: r * mx + lens[r]].to(t.device) for r in range(world)]
+
+
+def all_gather_unique(t: torch.Tensor) -> torch.Tensor:
+    """Sorted union of the per-rank distinct values of a 1-D tensor."""
+    parts = all_gather_v(t)
+    return torch.unique(torch.cat(parts))
 
 
 def all_gather_object(obj):

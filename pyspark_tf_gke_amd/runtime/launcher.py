@@ -5,8 +5,9 @@ Deployments, TF worker/PS StatefulSets, MetalLB/headless-service discovery; SURV
 Failure detection / elastic recovery:
   * a rank that exits non-zero makes the launcher stop the others (SIGTERM, then SIGKILL after a
     grace period) — no rank is left blocked in a collective;
-  * ranks heartbeat through files in ``PTG_HEARTBEAT_DIR`` (:mod:`.heartbeat`); a rank silent for
-    ``hang_timeout`` seconds is treated as hung;
+  * ranks report a progress counter through files in ``PTG_HEARTBEAT_DIR`` (:mod:`.heartbeat`); a
+    rank whose counter has not moved for ``hang_timeout`` seconds (e.g. blocked in a collective) is
+    treated as hung (before its first step the limit is ``startup_timeout``);
   * ``max_restarts`` relaunches the whole group (applications resume from their checkpoint, e.g.
     ``train --checkpoint-every 1 --resume``);
   * fault injection for tests: ``PTG_FAULT_RANK`` / ``PTG_FAULT_STEP`` (:mod:`.fault`).
@@ -90,7 +91,7 @@ def _terminate(procs, grace: float = 10.0):
 
 def launch(cmd: list, nprocs: int, master_addr: str = "127.0.0.1", master_port: int | None = None,
            env_extra: dict | None = None, max_restarts: int = 0, hang_timeout: float = 0.0, prefix_output: bool = True,
-           poll: float = 0.2) -> int:
+           poll: float = 0.2, startup_timeout: float | None = None) -> int:
     """Run ``cmd`` on ``nprocs`` ranks; return 0 or the first failing rank's exit code."""
     attempt = 0
     while True:
@@ -112,10 +113,10 @@ def launch(cmd: list, nprocs: int, master_addr: str = "127.0.0.1", master_port: 
                 if hang_timeout > 0:
                     from .heartbeat import stale_ranks
 
-                    stale = stale_ranks(hb_dir, nprocs, hang_timeout)
+                    stale = stale_ranks(hb_dir, nprocs, hang_timeout, startup_timeout)
                     if stale:
                         failed, rc = stale[0], 124
-                        sys.stderr.write(f"[launcher] rank {failed} heartbeat stale > {hang_timeout}s: treating as hung\n")
+                        sys.stderr.write(f"[launcher] rank {failed} made no progress for > {hang_timeout}s: treating as hung\n")
                         break
                 time.sleep(poll)
         except KeyboardInterrupt:
@@ -141,6 +142,7 @@ def main(argv=None) -> int:
     ap.add_argument("--master-port", type=int, default=0)
     ap.add_argument("--max-restarts", type=int, default=0)
     ap.add_argument("--hang-timeout", type=float, default=0.0)
+    ap.add_argument("--startup-timeout", type=float, default=None)
     ap.add_argument("cmd", nargs=argparse.REMAINDER)
     a = ap.parse_args(argv)
     cmd = a.cmd[1:] if a.cmd and a.cmd[0] == "--" else a.cmd
@@ -148,7 +150,7 @@ def main(argv=None) -> int:
         ap.error("missing command")
     n = a.nproc or _gpu_count() or 1
     return launch(cmd, n, a.master_addr, a.master_port or None, max_restarts=a.max_restarts,
-                  hang_timeout=a.hang_timeout)
+                  hang_timeout=a.hang_timeout, startup_timeout=a.startup_timeout)
 
 
 def _gpu_count() -> int:

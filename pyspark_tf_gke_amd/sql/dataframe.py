@@ -618,11 +618,10 @@ def _global_stats(cv: ColumnVector):
 # ------------------------------------------------------------------------------------------------
 # grouping
 # ------------------------------------------------------------------------------------------------
-_NULL_KEY = -(2 ** 62)
-
-
-def _key_of(cv: ColumnVector) -> torch.Tensor:
-    """int64 grouping key of one column (nulls -> one dedicated key)."""
+def _key_of(cv: ColumnVector):
+    """int64 grouping key of one column -> (key, null mask or None).  Null rows carry key 0; the
+    mask keeps them in their own group, outside the key domain (no sentinel value can collide with
+    a real key: every int64 and every double bit pattern is a legal key)."""
     d = cv.data
     if isinstance(cv.dtype, T.StringType):
         k = d.long()
@@ -631,22 +630,26 @@ def _key_of(cv: ColumnVector) -> torch.Tensor:
         x = d.double()
         x = torch.where(torch.isnan(x), torch.full_like(x, math.nan), x) + 0.0  # canonical NaN, -0 -> +0
         k = x.view(torch.int64)
-        null = torch.zeros_like(k, dtype=torch.bool)
+        null = None
     else:
         k = d.long()
-        if cv.valid is None:
-            return k  # integral key without nulls: used as is (no copy of a 1B-row column)
-        null = torch.zeros_like(k, dtype=torch.bool)
+        null = None
     if cv.valid is not None:
-        null = null | ~cv.valid.bool()
-    return torch.where(null, torch.full_like(k, _NULL_KEY), k)
+        inv = ~cv.valid.bool()
+        null = inv if null is None else (null | inv)
+    if null is not None:
+        if not bool(null.any()):
+            return k, None
+        k = torch.where(null, torch.zeros_like(k), k)
+    return k, null
 
 
-def _decode_key(k: torch.Tensor, src: ColumnVector) -> ColumnVector:
-    """Inverse of :func:`_key_of`: group key -> key column value (so grouped outputs need no
-    representative-row lookup)."""
-    null = k == _NULL_KEY
-    valid = None if not bool(null.any()) else (~null).to(torch.uint8)
+def _decode_key(k: torch.Tensor, src: ColumnVector, null: torch.Tensor | None = None) -> ColumnVector:
+    """Inverse of :func:`_key_of`: group key (+ null flag) -> key column value (so grouped outputs
+    need no representative-row lookup)."""
+    valid = None if null is None or not bool(null.any()) else (~null).to(torch.uint8)
+    if null is None:
+        null = torch.zeros_like(k, dtype=torch.bool)
     if isinstance(src.dtype, T.StringType):
         return ColumnVector(torch.where(null, torch.full_like(k, -1), k).to(torch.int32), src.dtype, None,
                             src.dictionary)
@@ -657,43 +660,56 @@ def _decode_key(k: torch.Tensor, src: ColumnVector) -> ColumnVector:
     return ColumnVector(v.to(src.data.dtype), src.dtype, valid)
 
 
+def _any_rank(flag: bool) -> bool:
+    if comm.world_size() == 1:
+        return flag
+    return bool(comm.all_reduce_int([int(flag)])[0])
+
+
 def _group_keys(df: "DataFrame", cols: list):
-    """-> (int64 combined key per row, decode(keys) -> {name: ColumnVector}).  Multi-column keys
-    are combined through dense per-column codes (exact, no hash collisions)."""
+    """-> (int64 combined key per row, decode(keys) -> {name: ColumnVector}).  A single non-null
+    column is its own key; otherwise (several columns, or nulls) every column is mapped to a dense
+    code over the global set of its distinct values (+1 code for null), and the codes are combined
+    mixed-radix (exact, no hash collisions)."""
     srcs = []
     for c in cols:
         name, cv = df._eval(c)
         srcs.append((name, cv))
     if not srcs:
         return torch.zeros(df._t.num_rows, dtype=torch.int64, device=df._t.device), lambda kk: {}
-    if len(srcs) == 1:
-        name, cv = srcs[0]
-        return _key_of(cv), lambda kk: {name: _decode_key(kk, cv)}
+    keyed = [(name, cv) + _key_of(cv) for name, cv in srcs]
+    if len(keyed) == 1 and not _any_rank(keyed[0][3] is not None):
+        name, cv, k, _ = keyed[0]
+        return k, lambda kk: {name: _decode_key(kk, cv)}
     combined = None
     globs = []
-    for _, cv in srcs:
-        k = _key_of(cv)
+    for _, cv, k, null in keyed:
+        has_null = _any_rank(null is not None)
+        kv = k if null is None else k[~null]
         if comm.world_size() > 1:
             # globally consistent dense codes: union of distinct keys across ranks
-            uk = torch.unique(k)
-            allk = comm.all_gather_object(uk.cpu().numpy())
-            glob = torch.from_numpy(np.unique(np.concatenate(allk))).to(k.device)
-            code = torch.searchsorted(glob, k)
+            glob = comm.all_gather_unique(torch.unique(kv))
         else:
-            glob, code = torch.unique(k, return_inverse=True)
-        globs.append(glob)
-        combined = code.long() if combined is None else combined * glob.numel() + code.long()
+            glob = torch.unique(kv)
+        code = torch.searchsorted(glob, k) if glob.numel() else torch.zeros_like(k)
+        if null is not None:
+            code = torch.where(null, torch.full_like(code, glob.numel()), code)
+        card = glob.numel() + int(has_null)
+        globs.append((glob, card))
+        combined = code.long() if combined is None else combined * card + code.long()
 
     def decode(kk):
         out = {}
         rem = kk.clone()
         codes = []
-        for g in reversed(globs):
-            codes.append(rem % g.numel())
-            rem = rem // g.numel()
+        for _, card in reversed(globs):
+            codes.append(rem % card)
+            rem = rem // card
         codes.reverse()
-        for (name, cv), g, c in zip(srcs, globs, codes):
-            out[name] = _decode_key(g[c], cv)
+        for (name, cv, _, _), (g, card), c in zip(keyed, globs, codes):
+            isnull = c >= g.numel()
+            gv = g[c.clamp_max(max(g.numel() - 1, 0))] if g.numel() else torch.zeros_like(c)
+            out[name] = _decode_key(gv, cv, isnull)
         return out
 
     return combined, decode
@@ -794,9 +810,9 @@ class GroupedData:
                     continue
                 _, cv = df._eval(src)
                 if fn == "count_distinct":
-                    k = _key_of(cv)
-                    loc = torch.unique(k[k != _NULL_KEY]).cpu().numpy()
-                    vals[label] = int(np.unique(np.concatenate(comm.all_gather_object(loc))).size)
+                    k, null = _key_of(cv)
+                    loc = torch.unique(k if null is None else k[~null])
+                    vals[label] = int(comm.all_gather_unique(loc).numel()) if world > 1 else int(loc.numel())
                     continue
                 if fn == "first":
                     vals[label] = df.select(src).first()[0] if df.count() else None

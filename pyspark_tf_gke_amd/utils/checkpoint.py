@@ -108,7 +108,7 @@ def load_checkpoint(model, path: str) -> dict:
                     if t is not None and "opt_" + k in f.keys():
                         t[lo:hi].copy_(f.get_tensor("opt_" + k).to(t.device))
     if opt is not None:
-        opt.iterations = int(manifest["step"])
+        opt.set_iterations(int(manifest["step"]))
     st.refresh_bf16()
     st.master_stale = False
     return manifest

@@ -1,0 +1,311 @@
+"""Fault tolerance and parameter-server fidelity on CPU ranks (gloo) — SURVEY §5.3, T14/T15:
+
+* a coordinator closure that raises on one rank is retried as a whole round: final parameters are
+  bit-identical to a fault-free run;
+* rounds with fewer closures than ranks average over the contributors only and never advance the
+  optimizer on zero pushes;
+* ``MinSizePartitioner`` placement (per-variable shards round-robin over PS tasks) at 2/3/5 ranks,
+  including world sizes that do not divide the parameter count;
+* sync PS == single-process mean gradient; async PS == each worker's gradient applied as its own
+  optimizer step, in worker order;
+* process fault at step s -> launcher restart -> resume from the last checkpoint == uninterrupted;
+* a rank that stops making progress (blocked in a collective) is detected and the group restarted.
+"""
+import json
+import os
+import subprocess
+import sys
+import textwrap
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _launch(body: str, nproc: int, extra_env=None, launcher_args=(), timeout=300):
+    env = dict(os.environ)
+    env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    env["PTG_DEVICE"] = "cpu"
+    env["PTG_HOST_FP32"] = "1"
+    env.pop("WORLD_SIZE", None)
+    env.update(extra_env or {})
+    cmd = [sys.executable, "-m", "pyspark_tf_gke_amd.runtime.launcher", "--nproc", str(nproc), *launcher_args, "--",
+           sys.executable, "-c", textwrap.dedent(body)]
+    return subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout, cwd=ROOT)
+
+
+def _results(out: str):
+    res = {}
+    for line in out.splitlines():
+        if "RESULT " in line:
+            rank = int(line.split("]")[0].replace("[rank", ""))
+            res[rank] = json.loads(line.split("RESULT ", 1)[1])
+    return res
+
+
+COMMON = """
+import json, os, torch, numpy as np
+from pyspark_tf_gke_amd import nn
+from pyspark_tf_gke_amd.distribute import ParameterServerStrategy, MultiWorkerMirroredStrategy, ClusterCoordinator
+from pyspark_tf_gke_amd.distribute.cluster import MinSizePartitioner
+from pyspark_tf_gke_amd.models import build_deep_model
+from pyspark_tf_gke_amd.nn.tape import GradientTape
+rng = np.random.default_rng(0)
+X = rng.normal(size=(16, 32, 3)).astype(np.float32)
+Y = rng.integers(0, 4, size=(16, 32)).astype(np.int32)
+loss_fn = nn.losses.SparseCategoricalCrossentropy()
+
+def make(st, lr=1e-2):
+    with st.scope():
+        m = build_deep_model(3, 4, device="cpu")
+        opt = nn.optimizers.Adam(lr)
+    return m, opt
+
+def step_fn(m, opt, i, fail_box=None, rank=None):
+    if fail_box is not None and fail_box.get(i, 0) > 0 and rank in fail_box.get("ranks", ()):
+        fail_box[i] -= 1
+        raise RuntimeError(f"injected closure failure {i}")
+    with GradientTape() as tape:
+        out = m(torch.from_numpy(X[i]), training=True)
+        loss = loss_fn(torch.from_numpy(Y[i]), out)
+    grads = tape.gradient(loss, m.trainable_variables)
+    opt.apply_gradients(zip(grads, m.trainable_variables))
+    return 1
+
+def flat(m):
+    return m.store.flat.clone()
+"""
+
+
+def test_coordinator_retry_is_bit_identical():
+    body = COMMON + """
+st = ParameterServerStrategy()
+m_ok, o_ok = make(st)
+m_ft, o_ft = make(st)
+co = ClusterCoordinator(st)
+for i in range(6):
+    co.schedule(step_fn, args=(m_ok, o_ok, i))
+co.join()
+fail = {3: 1, 5: 2, "ranks": (1,)}   # closure 3 fails once, closure 5 twice, both on rank 1
+co2 = ClusterCoordinator(st, max_retries=2)
+rvs = [co2.schedule(step_fn, args=(m_ft, o_ft, i, fail, st.rank)) for i in range(6)]
+co2.join()
+same = bool(torch.equal(flat(m_ok), flat(m_ft)))
+print("RESULT", json.dumps({"same": same, "retries": co2.retries, "it_ok": o_ok.iterations,
+                            "it_ft": o_ft.iterations, "vals": [rv.fetch() for rv in rvs]}), flush=True)
+"""
+    r = _launch(body, 2)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    res = _results(r.stdout)
+    assert len(res) == 2
+    for v in res.values():
+        assert v["same"], v
+        assert v["retries"] == 3 and v["it_ok"] == v["it_ft"] == 3 and v["vals"] == [1] * 6, v
+
+
+def test_coordinator_exhausted_retries_and_partial_rounds():
+    """A closure failing more than max_retries is dropped (error on every rank); a round with one
+    closure on two ranks averages over that one worker; no optimizer step without contributors."""
+    body = COMMON + """
+st = ParameterServerStrategy()
+m, o = make(st)
+ref, ro = make(st)
+co = ClusterCoordinator(st, max_retries=1)
+fail = {1: 5, "ranks": (1,)}
+rvs = [co.schedule(step_fn, args=(m, o, i, fail, st.rank)) for i in range(3)]
+co.join()
+errs = []
+for rv in rvs:
+    try:
+        rv.fetch(); errs.append(None)
+    except RuntimeError as e:
+        errs.append("failed")
+# emulate: round 1 = {0, 1}: closure 1 dropped after 2 attempts -> round re-run as {0, 2}?
+# requeue keeps order: [0, 2] form the next round (rank 0 runs 0, rank 1 runs 2): mean of both.
+from pyspark_tf_gke_amd.nn import engine as E
+def grad(model, i):
+    model.store.zero_grad()
+    out = E.run_forward(model.ops, torch.from_numpy(X[i]), model.ws, True)
+    d = model._loss_grad(out, torch.from_numpy(Y[i]), torch.zeros(8))
+    E.run_backward(model.ops, d, model.ws)
+    return model.store.flat_grad.clone()
+g0, g2 = grad(ref, 0), grad(ref, 2)
+ref.store.flat_grad.copy_(g0 + g2)
+ro.apply(ref.store, gscale=0.5)
+diff = float((m.store.flat - ref.store.flat).abs().max())
+# a 3-closure queue on 2 ranks with no failures: last round has one contributor
+m2, o2 = make(st)
+r2, ro2 = make(st)
+co3 = ClusterCoordinator(st)
+for i in range(3):
+    co3.schedule(step_fn, args=(m2, o2, i))
+co3.join()
+ga, gb = grad(r2, 0), grad(r2, 1)
+r2.store.flat_grad.copy_(ga + gb); ro2.apply(r2.store, gscale=0.5)
+gc = grad(r2, 2)
+r2.store.flat_grad.copy_(gc); ro2.apply(r2.store, gscale=1.0)
+diff2 = float((m2.store.flat - r2.store.flat).abs().max())
+print("RESULT", json.dumps({"errs": errs, "diff": diff, "it": o.iterations, "diff2": diff2, "it2": o2.iterations}),
+      flush=True)
+"""
+    r = _launch(body, 2)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    res = _results(r.stdout)
+    assert len(res) == 2
+    for v in res.values():
+        assert v["errs"] == [None, "failed", None], v
+        assert v["it"] == 1 and v["diff"] < 1e-6, v
+        assert v["it2"] == 2 and v["diff2"] < 1e-6, v
+
+
+@pytest.mark.parametrize("nproc", [2, 3, 5])
+def test_ps_partitioner_placement_and_sync_update(nproc):
+    body = COMMON + """
+st = ParameterServerStrategy(variable_partitioner=MinSizePartitioner(min_shard_bytes=256, max_shards=4))
+m, o = make(st)
+ref, ro = make(st)
+W = st.world_size
+for it in range(2):
+    step_fn(m, o, st.rank + W * it)
+from pyspark_tf_gke_amd.nn import engine as E
+for it in range(2):
+    acc = None
+    for w in range(W):
+        ref.store.zero_grad()
+        out = E.run_forward(ref.ops, torch.from_numpy(X[w + W * it]), ref.ws, True)
+        d = ref._loss_grad(out, torch.from_numpy(Y[w + W * it]), torch.zeros(8))
+        E.run_backward(ref.ops, d, ref.ws)
+        g = ref.store.flat_grad.clone()
+        acc = g if acc is None else acc + g
+    ref.store.flat_grad.copy_(acc)
+    ro.apply(ref.store, gscale=1.0 / W)
+diff = float((m.store.flat - ref.store.flat).abs().max())
+pl = st.placement(m)
+print("RESULT", json.dumps({"diff": diff, "placement": pl, "W": W}), flush=True)
+"""
+    r = _launch(body, nproc)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    res = _results(r.stdout)
+    assert len(res) == nproc
+    for v in res.values():
+        assert v["diff"] < 1e-6, v
+    pl = res[0]["placement"]
+    # Dense kernels (rows x cols fp32): shards of whole rows, >= 256 B each unless the variable is
+    # smaller, at most 4 per variable; PS tasks assigned round-robin in creation order
+    by_var = {}
+    for name, (r0, r1), task, owner in pl:
+        by_var.setdefault(name, []).append((r0, r1, task, owner))
+        assert owner == task % nproc
+    assert [p[2] for p in pl] == [i % nproc for i in range(len(pl))]
+    assert max(len(v) for v in by_var.values()) == 4
+    for shards in by_var.values():
+        assert shards[0][0] == 0 and all(a[1] == b[0] for a, b in zip(shards, shards[1:]))
+
+
+def test_ps_single_ps_task_lives_on_rank0():
+    """The reference's launcher config (1 PS): every variable unsplit, on PS task 0 = rank 0."""
+    body = COMMON + """
+from pyspark_tf_gke_amd.distribute.cluster import SimpleClusterResolver, ClusterSpec
+spec = ClusterSpec({"worker": ["127.0.0.1:2222", "127.0.0.1:2223"], "ps": ["127.0.0.1:2224"]})
+st = ParameterServerStrategy(SimpleClusterResolver(spec))
+m, o = make(st)
+step_fn(m, o, st.rank)
+print("RESULT", json.dumps({"owners": sorted({p[3] for p in st.placement(m)}), "n": len(st.placement(m)),
+                            "sum": float(m.store.flat.sum())}), flush=True)
+"""
+    r = _launch(body, 2)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    res = _results(r.stdout)
+    assert res[0]["owners"] == [0] and res[0]["sum"] == res[1]["sum"]
+
+
+def test_ps_async_applies_each_worker_gradient():
+    body = COMMON + """
+st = ParameterServerStrategy(mode="async")
+m, o = make(st, lr=5e-3)
+ref, ro = make(st, lr=5e-3)
+W = st.world_size
+co = ClusterCoordinator(st)
+for i in range(2 * W):
+    co.schedule(step_fn, args=(m, o, i))
+co.join()
+from pyspark_tf_gke_amd.nn import engine as E
+for rnd in range(2):
+    gs = []
+    for w in range(W):   # every worker of a round computed on the round-start values
+        ref.store.zero_grad()
+        out = E.run_forward(ref.ops, torch.from_numpy(X[rnd * W + w]), ref.ws, True)
+        d = ref._loss_grad(out, torch.from_numpy(Y[rnd * W + w]), torch.zeros(8))
+        E.run_backward(ref.ops, d, ref.ws)
+        gs.append(ref.store.flat_grad.clone())
+    for g in gs:         # ... and the PS applied them one after another, unaveraged
+        ref.store.flat_grad.copy_(g)
+        ro.apply(ref.store, gscale=1.0)
+diff = float((m.store.flat - ref.store.flat).abs().max())
+print("RESULT", json.dumps({"diff": diff, "it": o.iterations}), flush=True)
+"""
+    r = _launch(body, 2)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    res = _results(r.stdout)
+    assert len(res) == 2
+    for v in res.values():
+        assert v["diff"] < 1e-6 and v["it"] == 4, v
+
+
+RESUME_BODY = """
+import json, os, sys, numpy as np, torch
+from pyspark_tf_gke_amd.distribute import MultiWorkerMirroredStrategy
+from pyspark_tf_gke_amd.models import build_deep_model
+from pyspark_tf_gke_amd.utils.checkpoint import CheckpointCallback
+st = MultiWorkerMirroredStrategy(device="cpu")
+rng = np.random.default_rng(7)
+X = rng.normal(size=(2, 96, 3)).astype(np.float32); y = rng.integers(0, 5, (2, 96)).astype(np.int32)
+with st.scope():
+    m = build_deep_model(3, 5, device="cpu")
+cb = CheckpointCallback(os.environ["CKPT"], every=1, resume=True)
+m.fit(X[st.rank], y[st.rank], batch_size=16, epochs=4, verbose=0, callbacks=[cb])
+st.synchronize_master(m)
+if st.rank == 0:
+    np.save(os.environ["OUT"], m.store.flat.numpy())
+print("RESULT", json.dumps({"restart": os.environ.get("PTG_RESTART_COUNT"), "start": cb.start_epoch}), flush=True)
+"""
+
+
+def test_fault_restart_resume_matches_uninterrupted(tmp_path):
+    import numpy as np
+
+    clean = _launch(RESUME_BODY, 2, extra_env={"CKPT": str(tmp_path / "ck_clean"), "OUT": str(tmp_path / "clean.npy")})
+    assert clean.returncode == 0, clean.stdout[-2000:] + clean.stderr[-3000:]
+    # rank 1 dies at its 15th train step (epoch 3 of 6 steps per epoch); the launcher restarts the
+    # group, which resumes from the epoch-2 checkpoint
+    faulty = _launch(RESUME_BODY, 2, extra_env={"CKPT": str(tmp_path / "ck_fault"), "OUT": str(tmp_path / "fault.npy"),
+                                                "PTG_FAULT_RANK": "1", "PTG_FAULT_STEP": "15"},
+                     launcher_args=("--max-restarts", "1"))
+    assert faulty.returncode == 0, faulty.stdout[-2000:] + faulty.stderr[-3000:]
+    assert "injected failure on rank 1" in faulty.stdout + faulty.stderr and "restarting all ranks" in faulty.stderr
+    res = _results(faulty.stdout)
+    assert any(v["restart"] == "1" and v["start"] == 2 for v in res.values()), res
+    a, b = np.load(tmp_path / "clean.npy"), np.load(tmp_path / "fault.npy")
+    assert np.array_equal(a, b)
+
+
+def test_hang_detected_by_progress_counter():
+    body = """
+import os, time
+from pyspark_tf_gke_amd.parallel import comm
+from pyspark_tf_gke_amd.runtime import heartbeat
+comm.init()
+heartbeat.progress()
+if os.environ.get("PTG_RESTART_COUNT") == "0":
+    if comm.rank() == 1:
+        time.sleep(120)        # stuck: makes no progress
+    comm.barrier()             # rank 0 blocks in the collective; its heartbeat thread still runs
+heartbeat.progress()
+comm.barrier()
+print("RESULT {\\"ok\\": 1}", flush=True)
+"""
+    r = _launch(body, 2, launcher_args=("--hang-timeout", "4", "--startup-timeout", "60", "--max-restarts", "1"),
+                timeout=200)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    assert "made no progress" in r.stderr and "restarting all ranks" in r.stderr
+    assert len(_results(r.stdout)) == 2

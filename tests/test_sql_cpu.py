@@ -113,3 +113,25 @@ def test_row_and_describe(spark):
     d = {row["summary"]: row["v"] for row in df.describe().collect()}
     assert float(d["mean"]) == 2.0 and d["count"] == "2"
     _ = np
+
+
+def test_groupby_null_key_is_its_own_group():
+    """Nulls form one group outside the key domain: -2.0 (bit pattern 0xC000...) and -2**62 stay
+    ordinary keys (a sentinel key value collided with them)."""
+    from pyspark_tf_gke_amd.sql import SparkSession, functions as F
+
+    spark = SparkSession.builder.master("local[1]").getOrCreate()
+    df = spark.createDataFrame([(-2.0, 1), (-2.0, 2), (3.0, 5), (None, 7), (None, 1)], ["x", "y"])
+    got = {r["x"]: r["s"] for r in df.groupBy("x").agg(F.sum("y").alias("s")).collect()}
+    assert got == {-2.0: 3, 3.0: 5, None: 8}
+    df = spark.createDataFrame([(-2.0, 1), (-2.0, 2), (3.0, 5)], ["x", "y"])
+    got = {r["x"]: r["s"] for r in df.groupBy("x").agg(F.sum("y").alias("s")).collect()}
+    assert got == {-2.0: 3, 3.0: 5}
+    big = -(2 ** 62)
+    df = spark.createDataFrame([(big, 1), (big, 2), (5, 5), (None, 4)], ["k", "y"])
+    got = {r["k"]: r["c"] for r in df.groupBy("k").agg(F.count("*").alias("c")).collect()}
+    assert got == {big: 2, 5: 1, None: 1}
+    df = spark.createDataFrame([(1, None, 1.0), (1, "a", 2.0), (1, None, 3.0), (2, "a", 4.0)], ["a", "b", "v"])
+    got = {(r["a"], r["b"]): r["s"] for r in df.groupBy("a", "b").agg(F.sum("v").alias("s")).collect()}
+    assert got == {(1, None): 4.0, (1, "a"): 2.0, (2, "a"): 4.0}
+    assert df.agg(F.countDistinct("b").alias("d")).collect()[0]["d"] == 1
