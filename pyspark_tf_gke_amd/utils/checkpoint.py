@@ -62,7 +62,7 @@ def save_checkpoint(model, path: str, epoch: int, extra: dict | None = None) -> 
     if rank == 0:
         manifest = {"epoch": epoch, "step": opt.iterations if opt else 0, "world_size": comm.world_size(),
                     "sharded": sharded, "layout": "per-param", "time": time.time(),
-                    "torch_rng": torch.get_rng_state().tolist()[:16], **(extra or {})}
+                    **(extra or {})}
         with open(os.path.join(path, "manifest.json.tmp"), "w") as fh:
             json.dump(manifest, fh)
         os.replace(os.path.join(path, "manifest.json.tmp"), os.path.join(path, "manifest.json"))
@@ -111,6 +111,8 @@ def load_checkpoint(model, path: str) -> dict:
         opt.set_iterations(int(manifest["step"]))
     st.refresh_bf16()
     st.master_stale = False
+    if strat is not None and hasattr(strat, "on_state_loaded"):
+        strat.on_state_loaded(model)  # parameter server: re-pack the owned shards
     return manifest
 
 

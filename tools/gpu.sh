@@ -1,0 +1,88 @@
+#!/usr/bin/env bash
+# One parameterised driver for GPU-box work (run through gpurun from the repo root):
+#   gpurun --timeout 900 -- 'bash tools/gpu.sh tests bench prof'
+# Tasks run in the order given; every GPU step has its own time limit and the first failure
+# ends the script (no GPU step runs after a fault, abort or timeout).  Outputs go to gpurun_out/.
+#   tests            pytest -m gpu (one process, per-test timeout)
+#   tests:<expr>     pytest -m gpu -k <expr>
+#   smoke            __graft_entry__.smoke()
+#   bench            bench.py (defaults; BENCH_ARGS adds flags)
+#   bench:<wl>       bench.py --workload <wl> (BENCH_ARGS adds flags)
+#   prof[:<wl>]      rocprofv3 --kernel-trace --stats over a short bench run -> gpurun_out/prof_<wl>
+#   pmc[:<wl>]       two PMC passes (MFMA/LDS/VALU/wait counters; FETCH_SIZE) -> gpurun_out/pmc_<wl>_{a,b}
+#   ab               A/B: bench.py twice plain, twice with AB_ENV set (interleaved)
+#   py:<script>      timeout 300 python <script> (e.g. py:tools/gemm_bench.py)
+#   e2e              joint ETL->Parquet->train + MNIST + synthetic image train_tf_ps.py
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$PWD}
+cd /tmp && export TMPDIR=/tmp && cd "$R" && mkdir -p gpurun_out
+export PYTHONPATH=$R
+STEP_T=${STEP_T:-300}
+
+fail() { echo "FAILED: $1"; [ -f "$2" ] && tail -40 "$2"; exit 1; }
+
+for task in "$@"; do
+  name=${task%%:*}; arg=""; [ "$name" != "$task" ] && arg=${task#*:}
+  echo "== $task ($(date +%T))"
+  case $name in
+    tests)
+      log=gpurun_out/pytest_gpu${arg:+_$arg}.log
+      timeout -k 10 ${TESTS_T:-1100} python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread \
+        ${arg:+-k "$arg"} > "$log" 2>&1 || fail tests "$log"
+      tail -2 "$log" ;;
+    smoke)
+      timeout -k 10 $STEP_T python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 \
+        || fail smoke gpurun_out/smoke.log
+      tail -2 gpurun_out/smoke.log ;;
+    bench)
+      wl=${arg:-cnn_b1}
+      timeout -k 10 $STEP_T python bench.py --workload "$wl" $BENCH_ARGS > "gpurun_out/bench_$wl.json" \
+        2> "gpurun_out/bench_$wl.err" || fail bench "gpurun_out/bench_$wl.err"
+      cat "gpurun_out/bench_$wl.json" ;;
+    prof)
+      wl=${arg:-cnn_b1}
+      timeout -k 10 $STEP_T rocprofv3 --kernel-trace --stats --output-format csv -d "gpurun_out/prof_$wl" -o run -- \
+        python bench.py --workload "$wl" --steps ${PROF_STEPS:-10} --warmup 3 --groupby-extra 0 --extra-batches "" \
+        $BENCH_ARGS > "gpurun_out/prof_$wl.log" 2>&1 || fail prof "gpurun_out/prof_$wl.log"
+      grep metric "gpurun_out/prof_$wl.log" | cut -c1-200
+      python tools/prof_summary.py "gpurun_out/prof_$wl" > "gpurun_out/prof_${wl}_summary.txt" 2>&1 || true
+      head -40 "gpurun_out/prof_${wl}_summary.txt" ;;
+    pmc)
+      wl=${arg:-cnn_b1}
+      timeout -s KILL 150 rocprofv3 --kernel-trace --pmc SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS \
+        SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU SQ_INSTS_VMEM SQ_WAVE_CYCLES SQ_WAIT_ANY GRBM_GUI_ACTIVE --output-format csv \
+        -d "gpurun_out/pmc_${wl}_a" -o run -- python bench.py --workload "$wl" --steps 2 --warmup 1 --groupby-extra 0 \
+        --extra-batches "" $BENCH_ARGS > "gpurun_out/pmc_${wl}_a.log" 2>&1 || fail pmc_a "gpurun_out/pmc_${wl}_a.log"
+      timeout -s KILL 150 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d "gpurun_out/pmc_${wl}_b" \
+        -o run -- python bench.py --workload "$wl" --steps 2 --warmup 1 --groupby-extra 0 --extra-batches "" \
+        $BENCH_ARGS > "gpurun_out/pmc_${wl}_b.log" 2>&1 || fail pmc_b "gpurun_out/pmc_${wl}_b.log"
+      python tools/pmc_report.py "gpurun_out/pmc_${wl}_a" "gpurun_out/pmc_${wl}_b" > "gpurun_out/pmc_${wl}_report.txt" \
+        2>&1 || true
+      head -30 "gpurun_out/pmc_${wl}_report.txt" ;;
+    ab)
+      for i in 1 2; do
+        timeout -k 10 $STEP_T python bench.py --groupby-extra 0 --extra-batches "" $BENCH_ARGS > gpurun_out/ab_a$i.json \
+          2> gpurun_out/ab_a.err || fail ab_a gpurun_out/ab_a.err
+        echo "A $(cut -c1-160 gpurun_out/ab_a$i.json)"
+        timeout -k 10 $STEP_T env $AB_ENV python bench.py --groupby-extra 0 --extra-batches "" $BENCH_ARGS \
+          > gpurun_out/ab_b$i.json 2> gpurun_out/ab_b.err || fail ab_b gpurun_out/ab_b.err
+        echo "B $(cut -c1-160 gpurun_out/ab_b$i.json)"
+      done ;;
+    py)
+      out=gpurun_out/$(basename "$arg" .py).log
+      timeout -k 10 $STEP_T python $arg $PY_ARGS > "$out" 2>&1 || fail "py $arg" "$out"
+      tail -${PY_TAIL:-30} "$out" ;;
+    e2e)
+      timeout -k 10 $STEP_T python workloads/joint/etl_to_train.py --rows 20000000 --out /tmp/joint --epochs 2 \
+        --batch-size 8192 > gpurun_out/joint.log 2>&1 || fail joint gpurun_out/joint.log
+      tail -3 gpurun_out/joint.log
+      timeout -k 10 $STEP_T python workloads/raw-tf/train_mnist.py --epochs 3 --steps-per-epoch 50 --batch-size 256 \
+        --output-dir /tmp/mnist > gpurun_out/mnist.log 2>&1 || fail mnist gpurun_out/mnist.log
+      tail -3 gpurun_out/mnist.log
+      timeout -k 10 $STEP_T python workloads/raw-tf/train_tf_ps.py --data-is-images --synthetic 4096 --epochs 2 \
+        --batch-size 256 --output-dir /tmp/cnn > gpurun_out/train_images.log 2>&1 || fail images gpurun_out/train_images.log
+      tail -4 gpurun_out/train_images.log ;;
+    *) echo "unknown task $task"; exit 2 ;;
+  esac
+done
+echo "== done ($(date +%T))"
