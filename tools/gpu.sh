@@ -45,7 +45,7 @@ for task in "$@"; do
         python bench.py --workload "$wl" --steps ${PROF_STEPS:-10} --warmup 3 --groupby-extra 0 --extra-batches "" \
         $BENCH_ARGS > "gpurun_out/prof_$wl.log" 2>&1 || fail prof "gpurun_out/prof_$wl.log"
       grep metric "gpurun_out/prof_$wl.log" | cut -c1-200
-      python tools/prof_summary.py "gpurun_out/prof_$wl" > "gpurun_out/prof_${wl}_summary.txt" 2>&1 || true
+      python tools/prof_summary.py "gpurun_out/prof_$wl/run_kernel_stats.csv" $(( ${PROF_STEPS:-10} + 3 )) > "gpurun_out/prof_${wl}_summary.txt" 2>&1 || true
       head -40 "gpurun_out/prof_${wl}_summary.txt" ;;
     pmc)
       wl=${arg:-cnn_b1}
