@@ -440,104 +440,36 @@ __global__ __launch_bounds__(256) void hash_extract_k(const long long* __restric
 }
 
 // ---- radix-partitioned aggregation (high cardinality) -------------------------------------------
-// pass 1: partition histogram over P = 2^pbits partitions by the high hash bits
-__global__ __launch_bounds__(256) void part_hist_k(const long long* __restrict__ keys, long n, int pbits,
-                                                   unsigned int* __restrict__ counts) {
-  __shared__ unsigned int h[4096];
-  const int P = 1 << pbits;
-  for (int t = threadIdx.x; t < P; t += 256) h[t] = 0;
-  __syncthreads();
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
-    const unsigned p = (unsigned)(mix64((unsigned long long)keys[i]) >> (64 - pbits));
-    atomicAdd(&h[p], 1u);
-  }
-  __syncthreads();
-  for (int t = threadIdx.x; t < P; t += 256)
-    if (h[t]) atomicAdd(&counts[t], h[t]);
-}
-// pass 2: scatter rows (key + one value column as f64) into partition order
-__global__ __launch_bounds__(256) void part_scatter_k(const long long* __restrict__ keys, const void* __restrict__ val,
-                                                      int vtype, long n, int pbits,
-                                                      unsigned long long* __restrict__ cursor,
-                                                      long long* __restrict__ okeys, double* __restrict__ ovals,
-                                                      long rows_per_block) {
-  __shared__ unsigned int lc[4096];
-  __shared__ unsigned long long lbase[4096];
-  const int P = 1 << pbits;
-  const long r0 = (long)blockIdx.x * rows_per_block, r1 = min(n, r0 + rows_per_block);
-  for (int t = threadIdx.x; t < P; t += 256) lc[t] = 0;
-  __syncthreads();
-  for (long i = r0 + threadIdx.x; i < r1; i += 256)
-    atomicAdd(&lc[(unsigned)(mix64((unsigned long long)keys[i]) >> (64 - pbits))], 1u);
-  __syncthreads();
-  for (int t = threadIdx.x; t < P; t += 256) {
-    lbase[t] = lc[t] ? atomicAdd(&cursor[t], (unsigned long long)lc[t]) : 0ULL;
-    lc[t] = 0;
-  }
-  __syncthreads();
-  for (long i = r0 + threadIdx.x; i < r1; i += 256) {
-    const long long k = keys[i];
-    const unsigned p = (unsigned)(mix64((unsigned long long)k) >> (64 - pbits));
-    const unsigned off = atomicAdd(&lc[p], 1u);
-    const unsigned long long dst = lbase[p] + off;
-    bool ok = true;
-    okeys[dst] = k;
-    ovals[dst] = load_col(val, vtype, i, ok);
-  }
-}
-// Block-private partitioning (replaces the global-cursor scatter above for large inputs):
-// pass A counts each block's rows per partition into hist[p][block] (partition-major), an
-// exclusive scan over that array gives every (partition, block) pair its own contiguous output run,
-// and pass B scatters: a block's rows of partition p land in one run of ~rows_per_block/P rows
-// written by one CU, instead of single 8-byte stores spread over P global cursors (which leave
-// partially written lines in the L2s of all 8 XCDs).
-__global__ __launch_bounds__(256) void part_count_k(const long long* __restrict__ keys, long n, int pbits,
-                                                    long rows_per_block, unsigned int* __restrict__ hist, int nb) {
-  __shared__ unsigned int h[4096];
-  const int P = 1 << pbits;
-  for (int t = threadIdx.x; t < P; t += 256) h[t] = 0;
-  __syncthreads();
-  const long r0 = (long)blockIdx.x * rows_per_block, r1 = min(n, r0 + rows_per_block);
-  for (long i = r0 + threadIdx.x; i < r1; i += 256)
-    atomicAdd(&h[(unsigned)(mix64((unsigned long long)keys[i]) >> (64 - pbits))], 1u);
-  __syncthreads();
-  for (int t = threadIdx.x; t < P; t += 256) hist[(long)t * nb + blockIdx.x] = h[t];
-}
-__global__ __launch_bounds__(256) void part_scatter_runs_k(const long long* __restrict__ keys,
-                                                           const void* __restrict__ val, int vtype, long n, int pbits,
-                                                           long rows_per_block, const long long* __restrict__ offs,
-                                                           int nb, long long* __restrict__ okeys,
-                                                           double* __restrict__ ovals) {
-  __shared__ unsigned long long base[4096];
-  __shared__ unsigned int lc[4096];
-  const int P = 1 << pbits;
-  for (int t = threadIdx.x; t < P; t += 256) {
-    base[t] = (unsigned long long)offs[(long)t * nb + blockIdx.x];
-    lc[t] = 0;
-  }
-  __syncthreads();
-  const long r0 = (long)blockIdx.x * rows_per_block, r1 = min(n, r0 + rows_per_block);
-  for (long i = r0 + threadIdx.x; i < r1; i += 256) {
-    const long long k = keys[i];
-    const unsigned p = (unsigned)(mix64((unsigned long long)k) >> (64 - pbits));
-    bool ok = true;
-    const double v = load_col(val, vtype, i, ok);
-    const unsigned long long dst = base[p] + atomicAdd(&lc[p], 1u);
-    okeys[dst] = k;
-    ovals[dst] = v;
-  }
-}
-
-// Two-level LSD-free radix partitioning with LDS staging (the groupBy hot path at 1B rows).
-// Element-granular scatter is uncoalesced (cdna_hip_programming.md App. B "Scatter"), so each level
-// moves tiles of RT rows: a tile is counting-sorted by a 6-bit hash digit in LDS and then written
-// as 64 contiguous runs (~RT/64 rows = 512 B of keys per run).  Output offsets come from an
-// exclusive scan over per-tile digit counts laid out [segment][digit][tile]: one global scan gives
-// every (segment, digit, tile) its run.  Level 1 splits the input into 64 segments by hash bits
-// 58..63, level 2 splits each segment by bits 52..57 -> 4096 partitions of ~n/4096 rows and
-// ~keys/4096 distinct keys, small enough for one LDS hash table each (part_agg_k).
+// Recursive hash partitioning (the classic out-of-cache aggregation plan), LDS-staged:
+//   level l (l = 0, 1, ...) splits every segment by 6 more hash bits (mix64(key) >> (58 - 6l)):
+//   a tile of RT rows is counting-sorted by digit in LDS and written as 64 contiguous runs
+//   (element-granular scatter is uncoalesced, cdna_hip_programming.md App. B "Scatter"), run
+//   offsets come from one exclusive scan over per-tile digit counts laid out [segment][digit][tile].
+//   Rows carry their key and up to PAY_MAX value columns, converted to f64 on the first level with
+//   null -> NaN (aggregates skip NaN and null alike, as hash_agg_lds_k does).
+//   part_agg2_k then gives every partition one workgroup and one LDS open-addressing table; a
+//   partition whose distinct keys do not fit its table SPILLS (emits nothing, is listed in
+//   `spilled`) and the host re-partitions only the spilled segments one level deeper.  mix64 is a
+//   bijection, so partitions shrink to single keys after at most 64/6 levels: the recursion is
+//   exact at any cardinality, with no global overflow table and no lost rows.
 #define RT 2048
 #define RB 64
+#define PAY_MAX 4
+struct PayIn {  // value columns of a partitioning pass (first level: any type + validity)
+  const void* vals[PAY_MAX];
+  const uint8_t* valid[PAY_MAX];
+  int types[PAY_MAX];
+};
+struct PayOut {
+  double* vals[PAY_MAX];
+};
+PTG_DEV double load_pay(const PayIn& in, int j, long i) {
+  bool ok = true;
+  const double v = load_col(in.vals[j], in.types[j], i, ok);
+  if (in.valid[j]) ok = ok && in.valid[j][i];
+  return ok ? v : __builtin_nan("");
+}
+
 __global__ __launch_bounds__(256) void radix_count_k(const long long* __restrict__ keys,
                                                      const long long* __restrict__ tstart,
                                                      const int* __restrict__ trows,
@@ -567,18 +499,19 @@ __global__ __launch_bounds__(256) void radix_count_k(const long long* __restrict
   if (tid < RB) hist[thbase[b] + (long long)tid * thstride[b]] = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
 }
 
-__global__ __launch_bounds__(256) void radix_scatter_k(const long long* __restrict__ keys,
-                                                       const void* __restrict__ val, int vtype,
+template <int NV>
+__global__ __launch_bounds__(256) void radix_scatter_k(const long long* __restrict__ keys, PayIn pin,
                                                        const long long* __restrict__ tstart,
                                                        const int* __restrict__ trows,
                                                        const long long* __restrict__ thbase,
                                                        const long long* __restrict__ thstride, int shift,
                                                        const long long* __restrict__ offs, long n_out,
-                                                       long long* __restrict__ okeys, double* __restrict__ ovals) {
+                                                       long long* __restrict__ okeys, PayOut pout) {
   (void)n_out;
   constexpr int RPT = RT / 256;
+  constexpr int NVS = NV > 0 ? NV : 1;
   __shared__ long long sk[RT];
-  __shared__ double sv[RT];
+  __shared__ double sv[NVS][RT];
   __shared__ unsigned char sd[RT];
   __shared__ unsigned int cnt[RB];
   __shared__ unsigned int lstart[RB];
@@ -592,16 +525,16 @@ __global__ __launch_bounds__(256) void radix_scatter_k(const long long* __restri
   }
   __syncthreads();
   long long k[RPT];
-  double v[RPT];
+  double v[NVS][RPT];
   int d[RPT];
 #pragma unroll
   for (int j = 0; j < RPT; ++j) {
     const int i = tid + j * 256;
     d[j] = -1;
     if (i < nr) {
-      bool ok = true;
       k[j] = keys[s0 + i];
-      v[j] = load_col(val, vtype, s0 + i, ok);
+#pragma unroll
+      for (int q = 0; q < NV; ++q) v[q][j] = load_pay(pin, q, s0 + i);
       d[j] = (int)((mix64((unsigned long long)k[j]) >> shift) & (RB - 1));
       atomicAdd(&cnt[d[j]], 1u);
     }
@@ -624,7 +557,8 @@ __global__ __launch_bounds__(256) void radix_scatter_k(const long long* __restri
     if (d[j] < 0) continue;
     const unsigned pos = lstart[d[j]] + atomicAdd(&cnt[d[j]], 1u);
     sk[pos] = k[j];
-    sv[pos] = v[j];
+#pragma unroll
+    for (int q = 0; q < NV; ++q) sv[q][pos] = v[q][j];
     sd[pos] = (unsigned char)d[j];
   }
   __syncthreads();
@@ -632,62 +566,140 @@ __global__ __launch_bounds__(256) void radix_scatter_k(const long long* __restri
     const int dd = sd[i];
     const long long dst = PTG_CHECKED_IDX(goff[dd] + (i - (int)lstart[dd]), n_out);
     okeys[dst] = sk[i];
-    ovals[dst] = sv[i];
+#pragma unroll
+    for (int q = 0; q < NV; ++q) pout.vals[q][dst] = sv[q][i];
   }
 }
 
-// pass 3: one workgroup per partition segment aggregates in LDS (sum, count) — rows of a partition
-// never meet another partition's keys, so each partition's table is final: no merge needed.
-// PCAP = LDS table slots: 1024 for the 4096-partition path (~keys/4096 distinct keys per partition,
-// 244 at 1M keys: <25 % load, 20 KB LDS -> several blocks per CU), 4096 for coarser partitionings.
-template <int PCAP>
-__global__ __launch_bounds__(256) void part_agg_k(const long long* __restrict__ okeys, const double* __restrict__ ovals,
-                                                  const unsigned long long* __restrict__ pstart, int P,
-                                                  long long* __restrict__ out_keys, double* __restrict__ out_sum,
-                                                  double* __restrict__ out_cnt, unsigned long long* __restrict__ m_out,
-                                                  long long* __restrict__ gkeys, double* __restrict__ gtab, long gcap,
-                                                  int* __restrict__ overflow) {
-  __shared__ long long lk[PCAP];
-  __shared__ double ls[PCAP];
-  __shared__ unsigned int lcnt[PCAP];
-  auto insert = [&](long long key, double v) {
-    int h = (int)(mix64((unsigned long long)key) & (PCAP - 1));
-    for (int probe = 0; probe < 64; ++probe) {
-      const long long cur = lk[h];
-      if (cur == key) { atomicAdd(&ls[h], v); atomicAdd(&lcnt[h], 1u); return; }
-      if (cur == EMPTY_KEY) {
-        const long long prev = (long long)atomicCAS((unsigned long long*)&lk[h], (unsigned long long)EMPTY_KEY,
-                                                    (unsigned long long)key);
-        if (prev == EMPTY_KEY || prev == key) { atomicAdd(&ls[h], v); atomicAdd(&lcnt[h], 1u); return; }
-      }
-      h = (h + 1) & (PCAP - 1);
-    }
-    // partition exceeds the LDS table: global overflow table
-    const long gs = gtable_slot(gkeys, gcap, key);
-    if (gs < 0) { atomicAdd(overflow, 1); return; }
-    atomicAdd(&gtab[gs], 1.0);
-    atomicAdd(&gtab[gcap + gs], v);
-    atomicAdd(&gtab[2 * gcap + gs], 1.0);
-  };
+// Block-wide exclusive scan of one int per thread (256 threads); returns the total in *total.
+PTG_DEV int block_excl_scan256(int c, int* wsum, int* total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int incl = c;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += t;
+  }
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  int base = 0;
+  for (int q = 0; q < w; ++q) base += wsum[q];
+  *total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  return base + incl - c;
+}
+
+PTG_DEV void lds_min_f64(double* p, double v) {
+  unsigned long long* a = (unsigned long long*)p;
+  unsigned long long old = *a;
+  while (__longlong_as_double(old) > v) {
+    const unsigned long long prev = atomicCAS(a, old, (unsigned long long)__double_as_longlong(v));
+    if (prev == old) break;
+    old = prev;
+  }
+}
+PTG_DEV void lds_max_f64(double* p, double v) {
+  unsigned long long* a = (unsigned long long*)p;
+  unsigned long long old = *a;
+  while (__longlong_as_double(old) < v) {
+    const unsigned long long prev = atomicCAS(a, old, (unsigned long long)__double_as_longlong(v));
+    if (prev == old) break;
+    old = prev;
+  }
+}
+
+struct AggPay {
+  const double* vals[PAY_MAX];
+};
+
+// One workgroup per partition (grid-stride over partitions), LDS table of `pcap` slots (power of
+// two) laid out [keys i64][sum/min/max f64 per column][rows u32][cnt u32 per column] in dynamic
+// LDS.  Output (non-spilled partitions): keys + table rows [rows, (sum, cnt, min, max) per column]
+// in hash_extract_k's layout, one atomic per partition for the output base.
+__global__ __launch_bounds__(256) void part_agg2_k(const long long* __restrict__ okeys, AggPay pay, int nv,
+                                                   int minmax, const long long* __restrict__ pstart,
+                                                   const long long* __restrict__ pend, int P, int pcap,
+                                                   long long* __restrict__ out_keys, double* __restrict__ out_tab,
+                                                   long out_cap, unsigned long long* __restrict__ m_out,
+                                                   int* __restrict__ spilled, int* __restrict__ nspill) {
+  extern __shared__ __align__(16) unsigned char lds_raw[];
+  __shared__ volatile int sflag;
+  __shared__ int wsum[4];
+  __shared__ unsigned long long obase;
+  const int mask = pcap - 1;
+  const int nacc = minmax ? 3 : 1;  // f64 accumulators per column
+  long long* lk = (long long*)lds_raw;
+  double* lf = (double*)(lk + pcap);                       // [nv][nacc][pcap]
+  unsigned int* lrows = (unsigned int*)(lf + (long)nv * nacc * pcap);
+  unsigned int* lcnt = lrows + pcap;                        // [nv][pcap]
   for (int p = blockIdx.x; p < P; p += gridDim.x) {
-    for (int t = threadIdx.x; t < PCAP; t += 256) { lk[t] = EMPTY_KEY; ls[t] = 0; lcnt[t] = 0; }
-    __syncthreads();
-    const unsigned long long a = pstart[p], b = pstart[p + 1];
-    unsigned long long i = a + threadIdx.x;
-    for (; i + 3 * 256 < b; i += 4 * 256) {  // 4 rows in flight per thread
-      long long k4[4];
-      double v4[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) { k4[u] = okeys[i + u * 256]; v4[u] = ovals[i + u * 256]; }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) insert(k4[u], v4[u]);
+    for (int t = threadIdx.x; t < pcap; t += 256) {
+      lk[t] = EMPTY_KEY;
+      lrows[t] = 0;
+      for (int j = 0; j < nv; ++j) {
+        lf[(j * nacc) * pcap + t] = 0.0;
+        if (minmax) { lf[(j * nacc + 1) * pcap + t] = INFINITY; lf[(j * nacc + 2) * pcap + t] = -INFINITY; }
+        lcnt[j * pcap + t] = 0;
+      }
     }
-    for (; i < b; i += 256) insert(okeys[i], ovals[i]);
+    if (threadIdx.x == 0) sflag = 0;
     __syncthreads();
-    for (int t = threadIdx.x; t < PCAP; t += 256) {
-      if (lk[t] == EMPTY_KEY) continue;
-      const unsigned long long q = atomicAdd(m_out, 1ULL);
-      out_keys[q] = lk[t]; out_sum[q] = ls[t]; out_cnt[q] = (double)lcnt[t];
+    const long long a = pstart[p], b = pend[p];
+    for (long long i = a + threadIdx.x; i < b; i += 256) {
+      if (sflag) break;  // benign race: a spilled partition's remaining rows are re-partitioned
+      const long long key = okeys[i];
+      int h = (int)(mix64((unsigned long long)key) & (unsigned long long)mask);
+      int slot = -1;
+      for (int probe = 0; probe < 64; ++probe) {
+        const long long cur = lk[h];
+        if (cur == key) { slot = h; break; }
+        if (cur == EMPTY_KEY) {
+          const long long prev = (long long)atomicCAS((unsigned long long*)&lk[h], (unsigned long long)EMPTY_KEY,
+                                                      (unsigned long long)key);
+          if (prev == EMPTY_KEY || prev == key) { slot = h; break; }
+        }
+        h = (h + 1) & mask;
+      }
+      if (slot < 0) { sflag = 1; break; }
+      atomicAdd(&lrows[slot], 1u);
+      for (int j = 0; j < nv; ++j) {
+        const double v = pay.vals[j][i];
+        if (v != v) continue;  // null / NaN
+        atomicAdd(&lf[(j * nacc) * pcap + slot], v);
+        atomicAdd(&lcnt[j * pcap + slot], 1u);
+        if (minmax) { lds_min_f64(&lf[(j * nacc + 1) * pcap + slot], v); lds_max_f64(&lf[(j * nacc + 2) * pcap + slot], v); }
+      }
+    }
+    __syncthreads();
+    if (sflag) {
+      if (threadIdx.x == 0) spilled[atomicAdd(nspill, 1)] = p;
+      __syncthreads();
+      continue;
+    }
+    // compact the occupied slots: each thread owns pcap/256 consecutive slots
+    const int per = pcap >> 8;
+    const int s0 = threadIdx.x * per;
+    int c = 0;
+    for (int s = s0; s < s0 + per; ++s) c += lk[s] != EMPTY_KEY;
+    int total;
+    const int pre = block_excl_scan256(c, wsum, &total);
+    if (threadIdx.x == 0) obase = total ? atomicAdd(m_out, (unsigned long long)total) : 0ull;
+    __syncthreads();
+    long long q = (long long)obase + pre;
+    for (int s = s0; s < s0 + per; ++s) {
+      const long long key = lk[s];
+      if (key == EMPTY_KEY) continue;
+      if (q < out_cap) {
+        out_keys[q] = key;
+        out_tab[q] = (double)lrows[s];
+        for (int j = 0; j < nv; ++j) {
+          double* o = out_tab + out_cap * (1 + 4 * j);
+          o[q] = lf[(j * nacc) * pcap + s];
+          o[out_cap + q] = (double)lcnt[j * pcap + s];
+          o[2 * out_cap + q] = minmax ? lf[(j * nacc + 1) * pcap + s] : INFINITY;
+          o[3 * out_cap + q] = minmax ? lf[(j * nacc + 2) * pcap + s] : -INFINITY;
+        }
+      }
+      ++q;
     }
     __syncthreads();
   }
@@ -853,35 +865,8 @@ int ptg_hash_extract(const void* keys, const void* tab, long cap, int nv, void* 
   PTG_RETURN_LAUNCH();
 }
 
-// Partitioned sum/count aggregation of (key, val).  Workspace (device):
-//   counts u32[P], cursor u64[P], pstart u64[P+1] (host computes from counts), okeys i64[n], ovals f64[n]
-int ptg_part_hist(const void* keys, long n, int pbits, void* counts, hipStream_t s) {
-  if (pbits > 12) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(part_hist_k, dim3(grid_n(n)), dim3(256), 0, s, (const long long*)keys, n, pbits,
-                     (unsigned int*)counts);
-  PTG_RETURN_LAUNCH();
-}
-int ptg_part_scatter(const void* keys, const void* val, int vtype, long n, int pbits, void* cursor, void* okeys,
-                     void* ovals, hipStream_t s) {
-  long rpb = 16384;
-  const long nb = (n + rpb - 1) / rpb;
-  hipLaunchKernelGGL(part_scatter_k, dim3((unsigned)(nb < 1 ? 1 : nb)), dim3(256), 0, s, (const long long*)keys, val,
-                     vtype, n, pbits, (unsigned long long*)cursor, (long long*)okeys, (double*)ovals, rpb);
-  PTG_RETURN_LAUNCH();
-}
-int ptg_part_count(const void* keys, long n, int pbits, long rows_per_block, void* hist, int nb, hipStream_t s) {
-  if (pbits > 12) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(part_count_k, dim3(nb), dim3(256), 0, s, (const long long*)keys, n, pbits, rows_per_block,
-                     (unsigned int*)hist, nb);
-  PTG_RETURN_LAUNCH();
-}
-int ptg_part_scatter_runs(const void* keys, const void* val, int vtype, long n, int pbits, long rows_per_block,
-                          const void* offs, int nb, void* okeys, void* ovals, hipStream_t s) {
-  if (pbits > 12) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(part_scatter_runs_k, dim3(nb), dim3(256), 0, s, (const long long*)keys, val, vtype, n, pbits,
-                     rows_per_block, (const long long*)offs, nb, (long long*)okeys, (double*)ovals);
-  PTG_RETURN_LAUNCH();
-}
+// One radix level (see radix_count_k / radix_scatter_k): tiles described by tstart/trows, digit
+// counts at hist[thbase[t] + d*thstride[t]]; pin/pout: PayIn / PayOut structs (host-packed), nv <= 4.
 int ptg_radix_count(const void* keys, const void* tstart, const void* trows, const void* thbase,
                     const void* thstride, int ntiles, int shift, void* hist, hipStream_t s) {
   if (ntiles <= 0) return 0;
@@ -890,27 +875,49 @@ int ptg_radix_count(const void* keys, const void* tstart, const void* trows, con
                      (const long long*)thstride, shift, (unsigned int*)hist);
   PTG_RETURN_LAUNCH();
 }
-int ptg_radix_scatter(const void* keys, const void* val, int vtype, const void* tstart, const void* trows,
+int ptg_pay_desc_size() { return (int)sizeof(PayIn); }
+int ptg_radix_scatter(const void* keys, const void* pin_p, int nv, const void* tstart, const void* trows,
                       const void* thbase, const void* thstride, int ntiles, int shift, const void* offs, long n_out,
-                      void* okeys, void* ovals, hipStream_t s) {
+                      void* okeys, const void* pout_p, hipStream_t s) {
   if (ntiles <= 0) return 0;
-  hipLaunchKernelGGL(radix_scatter_k, dim3(ntiles), dim3(256), 0, s, (const long long*)keys, val, vtype,
-                     (const long long*)tstart, (const int*)trows, (const long long*)thbase,
-                     (const long long*)thstride, shift, (const long long*)offs, n_out, (long long*)okeys,
-                     (double*)ovals);
+  PayIn pin;
+  PayOut pout;
+  memcpy(&pin, pin_p, sizeof(PayIn));
+  memcpy(&pout, pout_p, sizeof(PayOut));
+#define PTG_SCATTER(NV)                                                                                      \
+  hipLaunchKernelGGL(radix_scatter_k<NV>, dim3(ntiles), dim3(256), 0, s, (const long long*)keys, pin,        \
+                     (const long long*)tstart, (const int*)trows, (const long long*)thbase,                  \
+                     (const long long*)thstride, shift, (const long long*)offs, n_out, (long long*)okeys, pout)
+  switch (nv) {
+    case 0: PTG_SCATTER(0); break;
+    case 1: PTG_SCATTER(1); break;
+    case 2: PTG_SCATTER(2); break;
+    case 3: PTG_SCATTER(3); break;
+    case 4: PTG_SCATTER(4); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+#undef PTG_SCATTER
   PTG_RETURN_LAUNCH();
 }
-int ptg_part_agg(const void* okeys, const void* ovals, const void* pstart, int P, void* out_keys, void* out_sum,
-                 void* out_cnt, void* m_out, void* gkeys, void* gtab, long gcap, void* overflow, hipStream_t s) {
-  int g = P < 2048 ? P : 2048;
-  if (P >= 4096)
-    hipLaunchKernelGGL(part_agg_k<1024>, dim3(g), dim3(256), 0, s, (const long long*)okeys, (const double*)ovals,
-                       (const unsigned long long*)pstart, P, (long long*)out_keys, (double*)out_sum, (double*)out_cnt,
-                       (unsigned long long*)m_out, (long long*)gkeys, (double*)gtab, gcap, (int*)overflow);
-  else
-    hipLaunchKernelGGL(part_agg_k<4096>, dim3(g), dim3(256), 0, s, (const long long*)okeys, (const double*)ovals,
-                       (const unsigned long long*)pstart, P, (long long*)out_keys, (double*)out_sum, (double*)out_cnt,
-                       (unsigned long long*)m_out, (long long*)gkeys, (double*)gtab, gcap, (int*)overflow);
+// vals: host array of nv f64 device pointers (payload columns in partition order)
+int ptg_part_agg2(const void* okeys, const void* const* vals, int nv, int minmax, const void* pstart, const void* pend,
+                  int P, int pcap, void* out_keys, void* out_tab, long out_cap, void* m_out, void* spilled,
+                  void* nspill, hipStream_t s) {
+  if (nv > PAY_MAX || pcap < 256 || (pcap & (pcap - 1)) || P <= 0) return (int)hipErrorInvalidValue;
+  // dynamic LDS for a table of pcap slots (ops/df.py _part_agg_lds mirrors this)
+  const long lds = (long)pcap * (8 + 4 + (long)nv * (4 + 8 * (minmax ? 3 : 1)));
+  if (lds > 150 * 1024) return (int)hipErrorInvalidValue;
+  AggPay pay;
+  for (int j = 0; j < PAY_MAX; ++j) pay.vals[j] = j < nv ? (const double*)vals[j] : nullptr;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)part_agg2_k, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+    attr_set = true;
+  }
+  const int g = P < 8192 ? P : 8192;
+  hipLaunchKernelGGL(part_agg2_k, dim3(g), dim3(256), (size_t)lds, s, (const long long*)okeys, pay, nv, minmax,
+                     (const long long*)pstart, (const long long*)pend, P, pcap, (long long*)out_keys,
+                     (double*)out_tab, out_cap, (unsigned long long*)m_out, (int*)spilled, (int*)nspill);
   PTG_RETURN_LAUNCH();
 }
 

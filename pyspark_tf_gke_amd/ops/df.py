@@ -176,19 +176,47 @@ def _extract(gkeys, gtab, cap, nv):
 
 
 RADIX_TILE = 2048  # rows per tile of radix_scatter_k (RT in df.hip)
+RADIX_BITS = 6  # digit bits per radix level (RB = 64 in df.hip)
+PAY_MAX = 4  # value columns carried through a partitioning pass (PAY_MAX in df.hip)
+_AGG_LDS_BUDGET = 64 * 1024  # part_agg2_k table bytes: keeps >= 2 workgroups resident per CU
 
 
-def _radix_level(keys, val, seg_start, seg_len, shift, buf, tag):
-    """One radix level over segments [seg_start, seg_start+seg_len): returns (okeys, ovals f64, offs)
-    where offs[(hb[s] + d*ntiles[s] + t)] is the output offset of tile t's digit-d run and
-    ``offs[-1] == n``, plus (hb, ntiles) per segment."""
+def _pay_in(cols) -> ctypes.Array:
+    """PayIn descriptor (df.hip) for a list of (tensor, valid u8 tensor or None)."""
+    cols = list(cols)
+    pad = PAY_MAX - len(cols)
+    b = struct.pack(f"{PAY_MAX}Q", *([c[0].data_ptr() for c in cols] + [0] * pad))
+    b += struct.pack(f"{PAY_MAX}Q", *([(c[1].data_ptr() if c[1] is not None else 0) for c in cols] + [0] * pad))
+    b += struct.pack(f"{PAY_MAX}i", *([TORCH_CT[c[0].dtype] for c in cols] + [0] * pad))
+    size = _native.hip_lib().ptg_pay_desc_size()
+    b += b"\0" * (size - len(b))
+    return ctypes.create_string_buffer(b, len(b))
+
+
+def _pay_out(tensors) -> ctypes.Array:
+    ts = list(tensors)
+    b = struct.pack(f"{PAY_MAX}Q", *([t.data_ptr() for t in ts] + [0] * (PAY_MAX - len(ts))))
+    return ctypes.create_string_buffer(b, len(b))
+
+
+def _radix_level(keys, pay_cols, seg_start, seg_len, shift, buf, tag):
+    """One radix level over segments [seg_start, seg_start+seg_len) of ``keys`` (+ payload columns,
+    written out as f64 with null -> NaN).  Rows are split by the 6 hash bits at ``shift``; the output
+    holds the segments' rows only (n_out = sum(seg_len)), segment-major then digit-major.
+    Returns (okeys, [ovals], new_start, new_end) of the nseg*64 sub-segments."""
     dev = keys.device
-    n = keys.numel()
     T = RADIX_TILE
     nseg = seg_start.numel()
     ntiles_s = (seg_len + T - 1) // T
     first = torch.cumsum(ntiles_s, 0) - ntiles_s
     total = int(ntiles_s.sum().item())
+    n_out = int(seg_len.sum().item())
+    nv = len(pay_cols)
+    okeys = buf(tag + "okeys", (max(n_out, 1),), torch.int64)[:n_out]
+    ovals = [buf(f"{tag}ov{j}", (max(n_out, 1),), torch.float64)[:n_out] for j in range(nv)]
+    if total == 0:
+        z = torch.zeros(nseg * 64, dtype=torch.int64, device=dev)
+        return okeys, ovals, z, z
     tile_seg = torch.repeat_interleave(torch.arange(nseg, device=dev), ntiles_s, output_size=total)
     tl = torch.arange(total, device=dev) - first[tile_seg]
     tstart = seg_start[tile_seg] + tl * T
@@ -202,72 +230,130 @@ def _radix_level(keys, val, seg_start, seg_len, shift, buf, tag):
     offs = buf(tag + "offs", (64 * total + 1,), torch.int64)
     torch.cumsum(hist, 0, dtype=torch.int64, out=offs[1:])
     offs[0] = 0
-    excl = offs[:-1]  # exclusive scan; offs[-1] = n is the sentinel for empty trailing segments
-    okeys = buf(tag + "okeys", (n,), torch.int64)
-    ovals = buf(tag + "ovals", (n,), torch.float64)
-    hip("ptg_radix_scatter", ptr(keys), ptr(val), TORCH_CT[val.dtype], ptr(tstart), ptr(trows), ptr(thbase),
-        ptr(thstride), total, shift, ptr(excl), n, ptr(okeys), ptr(ovals))
-    return okeys, ovals, offs, hb, ntiles_s
+    pin = _pay_in(pay_cols)
+    pout = _pay_out(ovals)
+    hip("ptg_radix_scatter", ptr(keys), ctypes.addressof(pin), nv, ptr(tstart), ptr(trows), ptr(thbase),
+        ptr(thstride), total, shift, ptr(offs[:-1]), n_out, ptr(okeys), ctypes.addressof(pout))
+    # sub-segment (s, d) starts at the run of its first tile; empty segments (no tiles) start where
+    # the next non-empty one does (offs[-1] = n_out is the sentinel)
+    idx = (hb.view(-1, 1) + torch.arange(64, device=dev).view(1, -1) * ntiles_s.view(-1, 1)).view(-1)
+    new_start = offs[idx]
+    new_end = torch.cat([new_start[1:], torch.full((1,), n_out, dtype=torch.int64, device=dev)])
+    return okeys, ovals, new_start, new_end
 
 
-def hash_agg_partitioned(keys: torch.Tensor, val: torch.Tensor, pbits: int = 9, ws: dict | None = None):
-    """High-cardinality sum/count aggregation: radix-partition by key hash, then one LDS table per
-    partition.  Returns (keys[m], sum[m], cnt[m]).  ``ws`` caches scratch buffers across calls."""
+def _part_agg_lds(pcap: int, nv: int, minmax: bool) -> int:
+    return pcap * (8 + 4 + nv * (4 + 8 * (3 if minmax else 1)))
+
+
+def estimate_distinct(keys: torch.Tensor, sample: int = 1 << 18) -> int:
+    """Distinct-key estimate from a strided sample: solves d = K (1 - exp(-m/K)) for K (uniform
+    key frequencies; skewed data is still handled exactly by the spill recursion)."""
+    n = keys.numel()
+    if n <= sample:
+        return int(hash_agg(keys, [], [], False)[0].numel())
+    s = keys[:: n // sample][:sample].contiguous()
+    d = int(hash_agg(s, [], [], False)[0].numel())
+    m = s.numel()
+    if d >= 0.999 * m:
+        return n
+    lo, hi = float(d), float(n)
+    for _ in range(60):
+        mid = math.sqrt(lo * hi)
+        if mid * (1.0 - math.exp(-m / mid)) < d:
+            lo = mid
+        else:
+            hi = mid
+    return int(min(n, max(d, hi)))
+
+
+def hash_agg_radix(keys: torch.Tensor, vals: list, valids: list, want_minmax: bool = False, ws: dict | None = None,
+                   est_keys: int | None = None):
+    """groupBy(key).agg over int64 keys by recursive radix partitioning (high cardinality, any
+    number of distinct keys).  Same result format as :func:`hash_agg`: (keys[m], rows[m],
+    [(sum, cnt, min, max)] per value column); at most PAY_MAX value columns per call."""
+    nv = len(vals)
+    if nv > PAY_MAX:
+        raise ValueError(f"hash_agg_radix: at most {PAY_MAX} value columns per call")
+    if not on_device(keys):
+        return hash_agg(keys, vals, valids, want_minmax)
     dev = keys.device
     n = keys.numel()
-    P = 1 << pbits
     ws = ws if ws is not None else {}
 
     def buf(name, shape, dtype):
         t = ws.get(name)
-        if t is None or t.numel() < int(np.prod(shape)) or t.dtype != dtype:
-            t = torch.empty(shape, dtype=dtype, device=dev)
+        numel = int(np.prod(shape))
+        if t is None or t.numel() < numel or t.dtype != dtype:
+            ws.pop(name, None)
+            t = torch.empty(numel, dtype=dtype, device=dev)
             ws[name] = t
-        return t[: int(np.prod(shape))].view(shape)
+        return t[:numel].view(shape)
 
-    if pbits == 12 and n >= (1 << 22):
-        # two 6-bit radix levels with LDS-staged, run-coalesced scatters (tiles of 4096 rows)
-        z = torch.zeros(1, dtype=torch.int64, device=dev)
-        k1, v1, offs1, hb1, nt1 = _radix_level(keys, val, z, torch.full((1,), n, dtype=torch.int64, device=dev),
-                                                58, buf, "l1")
-        seg_start = offs1[(hb1.view(-1, 1) + torch.arange(64, device=dev).view(1, -1) * nt1.view(-1, 1)).view(-1)]
-        seg_end = torch.cat([seg_start[1:], torch.full((1,), n, dtype=torch.int64, device=dev)])
-        okeys, ovals, offs2, hb2, nt2 = _radix_level(k1, v1, seg_start, seg_end - seg_start, 52, buf, "l2")
-        idx = (hb2.view(-1, 1) + torch.arange(64, device=dev).view(1, -1) * nt2.view(-1, 1)).view(-1)
-        pstart = buf("pstart", (P + 1,), torch.int64)
-        pstart[:P].copy_(offs2[idx])
-        pstart[P] = n
-    else:
-        # block-private partition runs: per-block histograms -> exclusive scan -> run scatter
-        rpb = 1 << 17 if n >= (1 << 26) else 1 << 14
-        nb = max(1, -(-n // rpb))
-        hist = buf("hist", (P * nb,), torch.int32)
-        hip("ptg_part_count", ptr(keys), n, pbits, rpb, ptr(hist), nb)
-        offs = buf("offs", (P * nb,), torch.int64)
-        torch.cumsum(hist, 0, dtype=torch.int64, out=offs)
-        offs.sub_(hist)
-        pstart = buf("pstart", (P + 1,), torch.int64)
-        pstart[:P].copy_(offs.view(P, nb)[:, 0])
-        pstart[P] = n
-        okeys = buf("okeys", (n,), torch.int64)
-        ovals = buf("ovals", (n,), torch.float64)
-        hip("ptg_part_scatter_runs", ptr(keys), ptr(val), TORCH_CT[val.dtype], n, pbits, rpb, ptr(offs), nb,
-            ptr(okeys), ptr(ovals))
-    cap_out = n if n < (1 << 26) else (1 << 26)
-    out_keys = buf("out_keys", (cap_out,), torch.int64)
-    out_sum = buf("out_sum", (cap_out,), torch.float64)
-    out_cnt = buf("out_cnt", (cap_out,), torch.float64)
-    m_out = buf("m_out", (1,), torch.int64)
-    m_out.zero_()
-    gcap = 1 << 16
-    gkeys = buf("gkeys", (gcap,), torch.int64)
-    gtab = buf("gtab", (5 * gcap,), torch.float64)
-    hip("ptg_hash_table_init", ptr(gkeys), ptr(gtab), gcap, 1)
-    overflow = buf("overflow", (1,), torch.int32)
-    overflow.zero_()
-    hip("ptg_part_agg", ptr(okeys), ptr(ovals), ptr(pstart), P, ptr(out_keys), ptr(out_sum), ptr(out_cnt), ptr(m_out),
-        ptr(gkeys), ptr(gtab), gcap, ptr(overflow))
-    return out_keys, out_sum, out_cnt, m_out, (gkeys, gtab, gcap), overflow
+    pay = []
+    for v, vd in zip(vals, valids):
+        v = v.view(torch.uint8) if v.dtype == torch.bool else v
+        if vd is not None and vd.dtype == torch.bool:
+            vd = vd.view(torch.uint8)
+        pay.append((v.contiguous(), vd))
+    K = est_keys if est_keys is not None else estimate_distinct(keys)
+    pcap_max = 256
+    while _part_agg_lds(pcap_max * 2, nv, want_minmax) <= _AGG_LDS_BUDGET and pcap_max < 4096:
+        pcap_max *= 2
+    levels = 1 if n < (1 << 20) else 2
+    while K / (64 ** levels) > pcap_max / 2 and levels < 4:
+        levels += 1
+    P = 64 ** levels
+    pcap = 256
+    while pcap < pcap_max and pcap < 4 * K / P:
+        pcap *= 2
+    seg_start = torch.zeros(1, dtype=torch.int64, device=dev)
+    seg_len = torch.full((1,), n, dtype=torch.int64, device=dev)
+    cur_keys, cur_pay = keys, pay
+    shift = 64 - RADIX_BITS
+    tags = ["a", "b"]
+    lvl = 0
+    for _ in range(levels):
+        cur_keys, ov, pstart, pend = _radix_level(cur_keys, cur_pay, seg_start, seg_len, shift, buf, tags[lvl % 2])
+        cur_pay = [(o, None) for o in ov]
+        seg_start, seg_len = pstart, pend - pstart
+        shift -= RADIX_BITS
+        lvl += 1
+    res_k, res_t = [], []
+    while True:
+        P = seg_start.numel()
+        cap = int(torch.clamp(seg_len, max=pcap).sum().item())
+        out_keys = torch.empty(max(cap, 1), dtype=torch.int64, device=dev)
+        out_tab = torch.empty((1 + 4 * nv) * max(cap, 1), dtype=torch.float64, device=dev)
+        m_out = torch.zeros(1, dtype=torch.int64, device=dev)
+        spilled = torch.empty(P, dtype=torch.int32, device=dev)
+        nspill = torch.zeros(1, dtype=torch.int32, device=dev)
+        vptrs = (ctypes.c_void_p * PAY_MAX)(*([c[0].data_ptr() for c in cur_pay] + [0] * (PAY_MAX - nv)))
+        pend = seg_start + seg_len
+        hip("ptg_part_agg2", ptr(cur_keys), ctypes.addressof(vptrs), nv, int(want_minmax), ptr(seg_start), ptr(pend),
+            P, pcap, ptr(out_keys), ptr(out_tab), max(cap, 1), ptr(m_out), ptr(spilled), ptr(nspill))
+        m = int(m_out.item())
+        if m > cap:
+            raise RuntimeError(f"hash_agg_radix: {m} groups exceed the output capacity {cap}")
+        res_k.append(out_keys[:m])
+        res_t.append(out_tab.view(1 + 4 * nv, max(cap, 1))[:, :m])
+        ns = int(nspill.item())
+        if ns == 0:
+            break
+        if shift < 16:
+            raise RuntimeError("hash_agg_radix: partition recursion did not converge")
+        sp = spilled[:ns].long()
+        # re-partition only the spilled partitions, one level deeper
+        cur_keys, ov, seg_start, pend2 = _radix_level(cur_keys, cur_pay, seg_start[sp], seg_len[sp], shift, buf,
+                                                      tags[lvl % 2])
+        cur_pay = [(o, None) for o in ov]
+        seg_len = pend2 - seg_start
+        shift -= RADIX_BITS
+        lvl += 1
+    ok = res_k[0] if len(res_k) == 1 else torch.cat(res_k)
+    ot = res_t[0] if len(res_t) == 1 else torch.cat(res_t, dim=1)
+    outs = [(ot[1 + 4 * j], ot[2 + 4 * j], ot[3 + 4 * j], ot[4 + 4 * j]) for j in range(nv)]
+    return ok, ot[0], outs
 
 
 def hash_partition(keys: torch.Tensor, P: int):

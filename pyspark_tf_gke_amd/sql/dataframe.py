@@ -926,33 +926,9 @@ class GroupedData:
         return df._new(t.take(idx))
 
 
-_PART_WS: dict = {}
-
-
-def _partitioned_agg(key: torch.Tensor, val):
-    n = key.numel()
-    v = val if val is not None else torch.zeros(1, dtype=torch.float64, device=key.device).expand(n)
-    if val is None:
-        v = torch.zeros(n, dtype=torch.float64, device=key.device)
-    pbits = 12 if n >= (1 << 28) else 10
-    ok, osum, ocnt, m, (gk, gt, gcap), overflow = D.hash_agg_partitioned(key, v, pbits=pbits, ws=_PART_WS)
-    m = int(m.item())
-    keys, sums, cnts = ok[:m], osum[:m], ocnt[:m]
-    # rows that overflowed their partition's LDS table went to the global table
-    ek, erows, eo = D._extract(gk, gt, gcap, 1)
-    if ek.numel():
-        keys = torch.cat([keys, ek])
-        sums = torch.cat([sums, eo[0][0]])
-        cnts = torch.cat([cnts, erows])
-        k2, r2, o2 = D.hash_agg(keys, [sums, cnts], [None, None], False)
-        keys, sums, cnts = k2, o2[0][0], o2[1][0]
-    rows = cnts
-    outs = [(sums, cnts, sums, sums)] if val is not None else []
-    return keys, rows, outs
-
-
-def _unused():
-    return Table
+_PART_WS: dict = {}  # scratch buffers of the radix-partitioned aggregation, reused across queries
+_RADIX_MIN_ROWS = 1 << 16
+_RADIX_MIN_KEYS = 4096
 
 
 def _num(cv: ColumnVector) -> torch.Tensor:
@@ -965,21 +941,24 @@ def _num(cv: ColumnVector) -> torch.Tensor:
 
 
 def _hash_agg_all(key, vals, valids, want_minmax):
-    """hash_agg with any number of value columns (chunks of 4 re-aligned by key order)."""
+    """Rank-local groupBy aggregate of any number of value columns.  Few distinct keys: LDS
+    tables + global table (hash_agg).  Many: recursive radix partitioning with one LDS table per
+    partition (hash_agg_radix; exact at any cardinality).  Value columns go 4 per pass, the passes
+    re-aligned by key order."""
     n = key.numel()
-    if (key.is_cuda and n >= (1 << 23) and len(vals) <= 1 and not want_minmax
-            and all(v is None for v in valids)):
-        # large inputs: estimate the cardinality on a prefix; high-cardinality keys take the
-        # radix-partitioned LDS aggregation (one LDS table per partition, no global atomics)
-        sk, _, _ = D.hash_agg(key[: 1 << 16], [], [], False)
-        if sk.numel() > (1 << 12):
-            return _partitioned_agg(key, vals[0] if vals else None)
+    fn = D.hash_agg
+    est = None
+    if key.is_cuda and n >= _RADIX_MIN_ROWS:
+        est = D.estimate_distinct(key)
+        if est > _RADIX_MIN_KEYS:
+            def fn(k, v, vd, mm):
+                return D.hash_agg_radix(k, v, vd, mm, ws=_PART_WS, est_keys=est)
     if len(vals) <= 4:
-        return D.hash_agg(key, vals, valids, want_minmax)
+        return fn(key, vals, valids, want_minmax)
     uk = rows = None
     outs = []
     for i in range(0, len(vals), 4):
-        k, r, o = D.hash_agg(key, vals[i:i + 4], valids[i:i + 4], want_minmax)
+        k, r, o = fn(key, vals[i:i + 4], valids[i:i + 4], want_minmax)
         order = torch.argsort(k)
         k, r = k[order], r[order]
         o = [tuple(x[order] for x in q) for q in o]

@@ -63,21 +63,95 @@ def test_hash_agg_matches_host(hip_built, nkeys):
     assert torch.allclose(og[0][3].cpu()[order], oh[0][3])
 
 
-@pytest.mark.parametrize("n,nkeys,pbits", [(4_000_000, 1_000_000, 9), (8_388_608, 1_000_000, 12),
-                                           (5_000_000, 3_000, 12)])
-def test_partitioned_agg(hip_built, n, nkeys, pbits):
-    """pbits=12 with n >= 2^22 takes the two-level LDS-staged radix partitioning; 3,000 keys leave
-    most of the 4,096 partitions (and some level-1 segments' tiles) empty."""
+def _sorted_agg(k, r, o):
+    order = torch.argsort(k.cpu())
+    return k.cpu()[order], r.cpu()[order], [tuple(x.cpu()[order] for x in q) for q in o]
+
+
+def _assert_agg_equal(got, want, minmax):
+    kg, rg, og = _sorted_agg(*got)
+    kh, rh, oh = _sorted_agg(*want)
+    assert torch.equal(kg, kh)
+    assert torch.equal(rg, rh)
+    for a, b in zip(og, oh):
+        assert torch.allclose(a[0], b[0], rtol=1e-9, atol=1e-9)  # sum
+        assert torch.equal(a[1], b[1])  # non-null count
+        if minmax:
+            assert torch.equal(a[2], b[2]) and torch.equal(a[3], b[3])
+
+
+@pytest.mark.parametrize("n,nkeys,nv,minmax", [(4_000_000, 1_000_000, 1, False), (8_388_608, 1_000_000, 1, False),
+                                               (5_000_000, 3_000, 1, False), (3_000_000, 200_000, 0, False),
+                                               (3_000_000, 200_000, 3, True), (700_000, 650_000, 4, True)])
+def test_radix_agg_matches_host(hip_built, n, nkeys, nv, minmax):
+    """Recursive radix aggregation vs the host path: value columns of mixed types with nulls and
+    NaNs, count-only (nv=0), min/max, and very sparse partitions (3,000 keys)."""
     k, v = D.fill_synthetic_kv(n, nkeys, "cuda")
-    ok, osum, ocnt, m, _, overflow = D.hash_agg_partitioned(k, v, pbits=pbits)
-    m = int(m.item())
-    assert int(overflow.item()) == 0
-    kh, rh, oh = D.hash_agg(k.cpu(), [v.cpu()], [None], False)
-    assert m == kh.numel()
-    order = torch.argsort(ok[:m].cpu())
-    assert torch.equal(ok[:m].cpu()[order], kh)
-    assert torch.allclose(osum[:m].cpu()[order], oh[0][0], rtol=1e-9)
-    assert torch.allclose(ocnt[:m].cpu()[order], rh)
+    g = torch.Generator().manual_seed(n + nv)
+    cols, valids = [], []
+    for j in range(nv):
+        if j == 0:
+            x = v.clone()
+        elif j == 1:
+            x = torch.randint(-1000, 1000, (n,), generator=g, dtype=torch.int32).cuda()
+        else:
+            x = torch.randn(n, generator=g).cuda()
+            x[::97] = math.nan
+        cols.append(x)
+        valids.append((torch.rand(n, generator=g) > 0.2).to(torch.uint8).cuda() if j % 2 == 1 else None)
+    got = D.hash_agg_radix(k, cols, valids, minmax)
+    want = D.hash_agg(k.cpu(), [c.cpu() for c in cols], [None if x is None else x.cpu() for x in valids], minmax)
+    _assert_agg_equal(got, want, minmax)
+
+
+@pytest.mark.parametrize("est", [1_000, 300_000])
+def test_radix_agg_spill_recursion(hip_built, est):
+    """An estimate far below the real 2M keys sizes the tables too small: partitions spill and are
+    re-partitioned one level deeper until every key is emitted exactly once (no lost rows)."""
+    k, v = D.fill_synthetic_kv(6_000_000, 2_000_000, "cuda")
+    got = D.hash_agg_radix(k, [v], [None], False, est_keys=est)
+    want = D.hash_agg(k.cpu(), [v.cpu()], [None], False)
+    _assert_agg_equal(got, want, False)
+
+
+def test_radix_agg_skewed_keys(hip_built):
+    """Heavy hitters plus a long tail: one partition holds most rows of a few keys."""
+    n = 4_000_000
+    g = torch.Generator().manual_seed(7)
+    k = torch.where(torch.rand(n, generator=g) < 0.6, torch.randint(0, 3, (n,), generator=g),
+                    torch.randint(0, 1 << 40, (n,), generator=g))
+    v = torch.rand(n, generator=g, dtype=torch.float64)
+    got = D.hash_agg_radix(k.cuda(), [v.cuda()], [None], True)
+    want = D.hash_agg(k, [v], [None], True)
+    _assert_agg_equal(got, want, True)
+
+
+@pytest.mark.parametrize("nkeys", [1_000, 1_000_000, 16_000_000, 128_000_000])
+def test_groupby_256m_rows_any_cardinality(spark_gpu, nkeys):
+    """DataFrame groupBy over 256M rows: sum(count) == n and sum(sum) == sum(values) at every
+    cardinality, the group count matches the keys present, and an 8M-row slice is exact vs the
+    host path."""
+    from pyspark_tf_gke_amd.sql import functions as F
+    from pyspark_tf_gke_amd.sql import types as T
+    from pyspark_tf_gke_amd.sql.dataframe import DataFrame
+    from pyspark_tf_gke_amd.sql.table import ColumnVector, Table
+
+    n = 256 * 1024 * 1024
+    k, v = D.fill_synthetic_kv(n, nkeys, "cuda", seed=nkeys)
+    df = DataFrame(Table({"key": ColumnVector(k, T.LongType()), "value": ColumnVector(v, T.DoubleType())}, n,
+                         k.device), spark_gpu)
+    out = df.groupBy("key").agg(F.sum("value").alias("s"), F.count("*").alias("c"))
+    c = out._t.column("c").data
+    ssum = out._t.column("s").data
+    assert int(c.sum().item()) == n
+    assert abs(float(ssum.sum().item()) - float(v.sum().item())) <= 1e-9 * n
+    present = int(torch.unique(k).numel())
+    assert out._t.num_rows == present
+    del out, c, ssum
+    m = 8 * 1024 * 1024
+    got = D.hash_agg_radix(k[:m].contiguous(), [v[:m].contiguous()], [None], True)
+    want = D.hash_agg(k[:m].cpu(), [v[:m].cpu()], [None], True)
+    _assert_agg_equal(got, want, True)
 
 
 def test_synthetic_kv_device_matches_host(hip_built):
