@@ -452,7 +452,10 @@ __global__ __launch_bounds__(256) void hash_extract_k(const long long* __restric
 //   `spilled`) and the host re-partitions only the spilled segments one level deeper.  mix64 is a
 //   bijection, so partitions shrink to single keys after at most 64/6 levels: the recursion is
 //   exact at any cardinality, with no global overflow table and no lost rows.
-#define RT 2048
+#ifndef PTG_RT
+#define PTG_RT 2048
+#endif
+#define RT PTG_RT  // max rows per tile; radix_scatter_k<NV> uses RT (NV <= 1) or RT/2 (LDS budget)
 #define RB 64
 #define PAY_MAX 4
 struct PayIn {  // value columns of a partitioning pass (first level: any type + validity)
@@ -508,11 +511,12 @@ __global__ __launch_bounds__(256) void radix_scatter_k(const long long* __restri
                                                        const long long* __restrict__ offs, long n_out,
                                                        long long* __restrict__ okeys, PayOut pout) {
   (void)n_out;
-  constexpr int RPT = RT / 256;
+  constexpr int RTT = NV <= 1 ? RT : RT / 2;  // tile rows (ops/df.py radix_tile mirrors this)
+  constexpr int RPT = RTT / 256;
   constexpr int NVS = NV > 0 ? NV : 1;
-  __shared__ long long sk[RT];
-  __shared__ double sv[NVS][RT];
-  __shared__ unsigned char sd[RT];
+  __shared__ long long sk[RTT];
+  __shared__ double sv[NVS][RTT];
+  __shared__ unsigned char sd[RTT];
   __shared__ unsigned int cnt[RB];
   __shared__ unsigned int lstart[RB];
   __shared__ long long goff[RB];
@@ -565,9 +569,15 @@ __global__ __launch_bounds__(256) void radix_scatter_k(const long long* __restri
   for (int i = tid; i < nr; i += 256) {  // consecutive rows of a digit run -> consecutive addresses
     const int dd = sd[i];
     const long long dst = PTG_CHECKED_IDX(goff[dd] + (i - (int)lstart[dd]), n_out);
+#if PTG_NT_STORE  // streamed once, re-read only by the next pass
+    __builtin_nontemporal_store(sk[i], &okeys[dst]);
+#pragma unroll
+    for (int q = 0; q < NV; ++q) __builtin_nontemporal_store(sv[q][i], &pout.vals[q][dst]);
+#else
     okeys[dst] = sk[i];
 #pragma unroll
     for (int q = 0; q < NV; ++q) pout.vals[q][dst] = sv[q][i];
+#endif
   }
 }
 
@@ -612,63 +622,91 @@ struct AggPay {
 };
 
 // One workgroup per partition (grid-stride over partitions), LDS table of `pcap` slots (power of
-// two) laid out [keys i64][sum/min/max f64 per column][rows u32][cnt u32 per column] in dynamic
+// two) laid out [keys i64][sum (, min, max) f64 per column][rows u32][cnt u32 per column] in dynamic
 // LDS.  Output (non-spilled partitions): keys + table rows [rows, (sum, cnt, min, max) per column]
-// in hash_extract_k's layout, one atomic per partition for the output base.
-__global__ __launch_bounds__(256) void part_agg2_k(const long long* __restrict__ okeys, AggPay pay, int nv,
-                                                   int minmax, const long long* __restrict__ pstart,
+// in hash_extract_k's layout, one atomic per partition for the output base.  Every thread keeps 4
+// rows' key + value loads in flight ahead of its LDS probes.
+template <int NV, bool MINMAX>
+__global__ __launch_bounds__(256) void part_agg2_k(const long long* __restrict__ okeys, AggPay pay,
+                                                   const long long* __restrict__ pstart,
                                                    const long long* __restrict__ pend, int P, int pcap,
                                                    long long* __restrict__ out_keys, double* __restrict__ out_tab,
                                                    long out_cap, unsigned long long* __restrict__ m_out,
                                                    int* __restrict__ spilled, int* __restrict__ nspill) {
+  constexpr int NACC = MINMAX ? 3 : 1;  // f64 accumulators per column
+  constexpr int NVS = NV > 0 ? NV : 1;
   extern __shared__ __align__(16) unsigned char lds_raw[];
   __shared__ volatile int sflag;
   __shared__ int wsum[4];
   __shared__ unsigned long long obase;
   const int mask = pcap - 1;
-  const int nacc = minmax ? 3 : 1;  // f64 accumulators per column
   long long* lk = (long long*)lds_raw;
-  double* lf = (double*)(lk + pcap);                       // [nv][nacc][pcap]
-  unsigned int* lrows = (unsigned int*)(lf + (long)nv * nacc * pcap);
-  unsigned int* lcnt = lrows + pcap;                        // [nv][pcap]
+  double* lf = (double*)(lk + pcap);                       // [NV][NACC][pcap]
+  unsigned int* lrows = (unsigned int*)(lf + (long)NV * NACC * pcap);
+  unsigned int* lcnt = lrows + pcap;                        // [NV][pcap]
+  auto insert = [&](long long key, const double* v) -> bool {
+    int h = (int)(mix64((unsigned long long)key) & (unsigned long long)mask);
+    int slot = -1;
+    for (int probe = 0; probe < 64; ++probe) {
+      const long long cur = lk[h];
+      if (cur == key) { slot = h; break; }
+      if (cur == EMPTY_KEY) {
+        const long long prev = (long long)atomicCAS((unsigned long long*)&lk[h], (unsigned long long)EMPTY_KEY,
+                                                    (unsigned long long)key);
+        if (prev == EMPTY_KEY || prev == key) { slot = h; break; }
+      }
+      h = (h + 1) & mask;
+    }
+    if (slot < 0) return false;
+    atomicAdd(&lrows[slot], 1u);
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      if (v[j] != v[j]) continue;  // null / NaN
+      atomicAdd(&lf[(j * NACC) * pcap + slot], v[j]);
+      atomicAdd(&lcnt[j * pcap + slot], 1u);
+      if (MINMAX) {
+        lds_min_f64(&lf[(j * NACC + 1) * pcap + slot], v[j]);
+        lds_max_f64(&lf[(j * NACC + 2) * pcap + slot], v[j]);
+      }
+    }
+    return true;
+  };
   for (int p = blockIdx.x; p < P; p += gridDim.x) {
     for (int t = threadIdx.x; t < pcap; t += 256) {
       lk[t] = EMPTY_KEY;
       lrows[t] = 0;
-      for (int j = 0; j < nv; ++j) {
-        lf[(j * nacc) * pcap + t] = 0.0;
-        if (minmax) { lf[(j * nacc + 1) * pcap + t] = INFINITY; lf[(j * nacc + 2) * pcap + t] = -INFINITY; }
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        lf[(j * NACC) * pcap + t] = 0.0;
+        if (MINMAX) { lf[(j * NACC + 1) * pcap + t] = INFINITY; lf[(j * NACC + 2) * pcap + t] = -INFINITY; }
         lcnt[j * pcap + t] = 0;
       }
     }
     if (threadIdx.x == 0) sflag = 0;
     __syncthreads();
     const long long a = pstart[p], b = pend[p];
-    for (long long i = a + threadIdx.x; i < b; i += 256) {
-      if (sflag) break;  // benign race: a spilled partition's remaining rows are re-partitioned
-      const long long key = okeys[i];
-      int h = (int)(mix64((unsigned long long)key) & (unsigned long long)mask);
-      int slot = -1;
-      for (int probe = 0; probe < 64; ++probe) {
-        const long long cur = lk[h];
-        if (cur == key) { slot = h; break; }
-        if (cur == EMPTY_KEY) {
-          const long long prev = (long long)atomicCAS((unsigned long long*)&lk[h], (unsigned long long)EMPTY_KEY,
-                                                      (unsigned long long)key);
-          if (prev == EMPTY_KEY || prev == key) { slot = h; break; }
-        }
-        h = (h + 1) & mask;
+    long long i = a + threadIdx.x;
+    bool ok = true;
+    for (; ok && i + 3 * 256 < b; i += 4 * 256) {
+      long long k4[4];
+      double v4[4][NVS];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        k4[u] = okeys[i + u * 256];
+#pragma unroll
+        for (int j = 0; j < NV; ++j) v4[u][j] = pay.vals[j][i + u * 256];
       }
-      if (slot < 0) { sflag = 1; break; }
-      atomicAdd(&lrows[slot], 1u);
-      for (int j = 0; j < nv; ++j) {
-        const double v = pay.vals[j][i];
-        if (v != v) continue;  // null / NaN
-        atomicAdd(&lf[(j * nacc) * pcap + slot], v);
-        atomicAdd(&lcnt[j * pcap + slot], 1u);
-        if (minmax) { lds_min_f64(&lf[(j * nacc + 1) * pcap + slot], v); lds_max_f64(&lf[(j * nacc + 2) * pcap + slot], v); }
-      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) ok = ok && insert(k4[u], v4[u]);
+      if (sflag) ok = false;  // benign race: a spilled partition's rows are re-partitioned anyway
     }
+    for (; ok && i < b; i += 256) {
+      double v1[NVS];
+#pragma unroll
+      for (int j = 0; j < NV; ++j) v1[j] = pay.vals[j][i];
+      ok = insert(okeys[i], v1);
+    }
+    if (!ok) sflag = 1;
     __syncthreads();
     if (sflag) {
       if (threadIdx.x == 0) spilled[atomicAdd(nspill, 1)] = p;
@@ -691,12 +729,13 @@ __global__ __launch_bounds__(256) void part_agg2_k(const long long* __restrict__
       if (q < out_cap) {
         out_keys[q] = key;
         out_tab[q] = (double)lrows[s];
-        for (int j = 0; j < nv; ++j) {
+#pragma unroll
+        for (int j = 0; j < NV; ++j) {
           double* o = out_tab + out_cap * (1 + 4 * j);
-          o[q] = lf[(j * nacc) * pcap + s];
+          o[q] = lf[(j * NACC) * pcap + s];
           o[out_cap + q] = (double)lcnt[j * pcap + s];
-          o[2 * out_cap + q] = minmax ? lf[(j * nacc + 1) * pcap + s] : INFINITY;
-          o[3 * out_cap + q] = minmax ? lf[(j * nacc + 2) * pcap + s] : -INFINITY;
+          o[2 * out_cap + q] = MINMAX ? lf[(j * NACC + 1) * pcap + s] : INFINITY;
+          o[3 * out_cap + q] = MINMAX ? lf[(j * NACC + 2) * pcap + s] : -INFINITY;
         }
       }
       ++q;
@@ -876,6 +915,7 @@ int ptg_radix_count(const void* keys, const void* tstart, const void* trows, con
   PTG_RETURN_LAUNCH();
 }
 int ptg_pay_desc_size() { return (int)sizeof(PayIn); }
+int ptg_radix_tile_rows() { return RT; }
 int ptg_radix_scatter(const void* keys, const void* pin_p, int nv, const void* tstart, const void* trows,
                       const void* thbase, const void* thstride, int ntiles, int shift, const void* offs, long n_out,
                       void* okeys, const void* pout_p, hipStream_t s) {
@@ -909,15 +949,27 @@ int ptg_part_agg2(const void* okeys, const void* const* vals, int nv, int minmax
   if (lds > 150 * 1024) return (int)hipErrorInvalidValue;
   AggPay pay;
   for (int j = 0; j < PAY_MAX; ++j) pay.vals[j] = j < nv ? (const double*)vals[j] : nullptr;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)part_agg2_k, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
-    attr_set = true;
-  }
   const int g = P < 8192 ? P : 8192;
-  hipLaunchKernelGGL(part_agg2_k, dim3(g), dim3(256), (size_t)lds, s, (const long long*)okeys, pay, nv, minmax,
-                     (const long long*)pstart, (const long long*)pend, P, pcap, (long long*)out_keys,
-                     (double*)out_tab, out_cap, (unsigned long long*)m_out, (int*)spilled, (int*)nspill);
+#define PTG_AGG(NV, MM)                                                                                     \
+  {                                                                                                         \
+    static bool attr = false;                                                                               \
+    if (!attr) {                                                                                            \
+      (void)hipFuncSetAttribute((const void*)part_agg2_k<NV, MM>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                150 * 1024);                                                                \
+      attr = true;                                                                                          \
+    }                                                                                                       \
+    hipLaunchKernelGGL((part_agg2_k<NV, MM>), dim3(g), dim3(256), (size_t)lds, s, (const long long*)okeys, pay, \
+                       (const long long*)pstart, (const long long*)pend, P, pcap, (long long*)out_keys,     \
+                       (double*)out_tab, out_cap, (unsigned long long*)m_out, (int*)spilled, (int*)nspill); \
+  }
+  if (minmax) {
+    switch (nv) { case 0: PTG_AGG(0, true) break; case 1: PTG_AGG(1, true) break; case 2: PTG_AGG(2, true) break;
+                  case 3: PTG_AGG(3, true) break; default: PTG_AGG(4, true) break; }
+  } else {
+    switch (nv) { case 0: PTG_AGG(0, false) break; case 1: PTG_AGG(1, false) break; case 2: PTG_AGG(2, false) break;
+                  case 3: PTG_AGG(3, false) break; default: PTG_AGG(4, false) break; }
+  }
+#undef PTG_AGG
   PTG_RETURN_LAUNCH();
 }
 

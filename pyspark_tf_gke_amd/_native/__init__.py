@@ -19,6 +19,8 @@ HERE = Path(__file__).resolve().parent
 # followed by a poll of the per-source-file check words, and a bad index raises with its line
 CHECKED = os.environ.get("PTG_CHECKED") == "1"
 HIP_LIB_PATH = HERE / ("libptg_hip_checked.so" if CHECKED else "libptg_hip.so")
+if os.environ.get("PTG_HIP_LIB"):  # A/B runs: an in-tree variant build (tools/build_variant.sh)
+    HIP_LIB_PATH = HERE / os.environ["PTG_HIP_LIB"]
 _CHECK_TUS = ("conv", "gemm", "nn_eltwise", "bn", "df", "ml")
 HOST_LIB_PATH = HERE / "libptg_host.so"
 

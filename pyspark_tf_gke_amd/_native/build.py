@@ -52,17 +52,21 @@ def _run(cmd: list[str]) -> None:
         raise RuntimeError(f"command failed ({r.returncode}): {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
 
 
-def build_hip(force: bool = False, jobs: int = 8, verbose: bool = True, checked: bool = False) -> Path:
+def build_hip(force: bool = False, jobs: int = 8, verbose: bool = True, checked: bool = False,
+              variant: str | None = None, defines: tuple = ()) -> Path:
     """``checked``: the bounds-checked variant - every PTG_CHECKED_IDX site verifies its
-    index, clamps it in range and reports the source line instead of faulting."""
+    index, clamps it in range and reports the source line instead of faulting.
+    ``variant``/``defines``: an A/B build ``libptg_hip_<variant>.so`` with extra -D macros, loaded by
+    setting ``PTG_HIP_LIB=libptg_hip_<variant>.so`` (not part of the default tree)."""
     srcs = sorted((CSRC / "kernels").glob("*.hip"))
     headers = sorted((CSRC / "kernels").glob("*.h"))
-    bdir = BUILD / "checked" if checked else BUILD
-    out_lib = HIP_LIB_CHECKED if checked else HIP_LIB
+    bdir = BUILD / ("checked" if checked else f"var_{variant}" if variant else "")
+    out_lib = HIP_LIB_CHECKED if checked else (HERE / f"libptg_hip_{variant}.so" if variant else HIP_LIB)
     bdir.mkdir(parents=True, exist_ok=True)
     hipcc = _hipcc()
     flags = ["--offload-arch=" + ARCH, "-O3", "-fPIC", "-std=c++17", "-munsafe-fp-atomics",
              "-Wno-unused-result", "-I", str(CSRC / "kernels")] + (["-DPTG_CHECKED"] if checked else [])
+    flags += [f"-D{d}" for d in defines]
     objs, todo = [], []
     for s in srcs:
         o = bdir / (s.stem + ".o")
@@ -121,8 +125,12 @@ def main(argv=None) -> int:
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=min(8, os.cpu_count() or 4))
     ap.add_argument("--host-only", action="store_true")
+    ap.add_argument("--variant", help="A/B build name (libptg_hip_<variant>.so)")
+    ap.add_argument("-D", dest="defines", action="append", default=[], help="extra macro for --variant")
     a = ap.parse_args(argv)
-    if a.host_only:
+    if a.variant:
+        build_hip(force=a.force, jobs=a.jobs, variant=a.variant, defines=tuple(a.defines))
+    elif a.host_only:
         build_host(force=a.force)
     else:
         build_all(force=a.force, jobs=a.jobs)

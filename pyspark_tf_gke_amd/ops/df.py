@@ -175,7 +175,10 @@ def _extract(gkeys, gtab, cap, nv):
     return ok, ot[0], outs
 
 
-RADIX_TILE = 2048  # rows per tile of radix_scatter_k (RT in df.hip)
+def radix_tile(nv: int) -> int:
+    """Tile rows of radix_scatter_k<nv> (RTT in df.hip: LDS holds a tile's keys + nv columns)."""
+    rt = _native.hip_lib().ptg_radix_tile_rows()
+    return rt if nv <= 1 else rt // 2
 RADIX_BITS = 6  # digit bits per radix level (RB = 64 in df.hip)
 PAY_MAX = 4  # value columns carried through a partitioning pass (PAY_MAX in df.hip)
 _AGG_LDS_BUDGET = 64 * 1024  # part_agg2_k table bytes: keeps >= 2 workgroups resident per CU
@@ -205,7 +208,7 @@ def _radix_level(keys, pay_cols, seg_start, seg_len, shift, buf, tag):
     holds the segments' rows only (n_out = sum(seg_len)), segment-major then digit-major.
     Returns (okeys, [ovals], new_start, new_end) of the nseg*64 sub-segments."""
     dev = keys.device
-    T = RADIX_TILE
+    T = radix_tile(len(pay_cols))
     nseg = seg_start.numel()
     ntiles_s = (seg_len + T - 1) // T
     first = torch.cumsum(ntiles_s, 0) - ntiles_s
@@ -246,7 +249,7 @@ def _part_agg_lds(pcap: int, nv: int, minmax: bool) -> int:
     return pcap * (8 + 4 + nv * (4 + 8 * (3 if minmax else 1)))
 
 
-def estimate_distinct(keys: torch.Tensor, sample: int = 1 << 18) -> int:
+def estimate_distinct(keys: torch.Tensor, sample: int = 1 << 16) -> int:
     """Distinct-key estimate from a strided sample: solves d = K (1 - exp(-m/K)) for K (uniform
     key frequencies; skewed data is still handled exactly by the spill recursion)."""
     n = keys.numel()

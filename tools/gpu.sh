@@ -11,6 +11,8 @@
 #   prof[:<wl>]      rocprofv3 --kernel-trace --stats over a short bench run -> gpurun_out/prof_<wl>
 #   pmc[:<wl>]       two PMC passes (MFMA/LDS/VALU/wait counters; FETCH_SIZE) -> gpurun_out/pmc_<wl>_{a,b}
 #   ab               A/B: bench.py twice plain, twice with AB_ENV set (interleaved)
+#   abvar:<name>     A/B: bench.py with the default library vs PTG_HIP_LIB=libptg_hip_<name>.so (built here by
+#                    python -m pyspark_tf_gke_amd._native.build --variant <name> -D MACRO=..), interleaved x2
 #   py:<script>      timeout 300 python <script> (e.g. py:tools/gemm_bench.py)
 #   e2e              joint ETL->Parquet->train + MNIST + synthetic image train_tf_ps.py
 set -o pipefail
@@ -67,6 +69,14 @@ for task in "$@"; do
         timeout -k 10 $STEP_T env $AB_ENV python bench.py --groupby-extra 0 --extra-batches "" $BENCH_ARGS \
           > gpurun_out/ab_b$i.json 2> gpurun_out/ab_b.err || fail ab_b gpurun_out/ab_b.err
         echo "B $(cut -c1-160 gpurun_out/ab_b$i.json)"
+      done ;;
+    abvar)
+      for i in 1 2; do
+        for lib in "" "libptg_hip_$arg.so"; do
+          PTG_HIP_LIB=$lib timeout -k 10 $STEP_T python bench.py --groupby-extra 0 --extra-batches "" $BENCH_ARGS \
+            > gpurun_out/abvar.json 2> gpurun_out/abvar.err || fail abvar gpurun_out/abvar.err
+          echo "${lib:-default} $(cut -c1-160 gpurun_out/abvar.json)"
+        done
       done ;;
     py)
       out=gpurun_out/$(basename "$arg" .py).log
