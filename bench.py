@@ -35,7 +35,7 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="cnn_b1", choices=["cnn_b1", "groupby", "mlp", "cnn_a1", "mnist", "resnet50"])
+    ap.add_argument("--workload", default="cnn_b1", choices=["cnn_b1", "groupby", "sort", "mlp", "cnn_a1", "mnist", "resnet50"])
     ap.add_argument("--batch-size", type=int, default=int(os.environ.get("PTG_BENCH_BATCH", "0")),
                     help="per-GPU batch (weak scaling); 0 = the workload default")
     ap.add_argument("--rows", type=int, default=1_000_000_000, help="groupby: rows per GPU")
@@ -219,6 +219,11 @@ def main():
     if args.workload == "groupby":
         res = bench_groupby(args, strategy, rank, world)
         dtype, data = "fp64", "synthetic (bigint keys = hash(row) % keys, double values), resident in HBM"
+    elif args.workload == "sort":
+        from pyspark_tf_gke_amd.sql import bench_groupby as bg
+
+        res = bg.run_sort(rows_per_gpu=args.rows, steps=args.steps, warmup=args.warmup, device=strategy.device)
+        dtype, data = "int64 keys / fp64 values", "synthetic (random full-range bigint keys, double values), resident in HBM"
     else:
         res = bench_train(args, strategy, rank, world)
         dtype = "bf16" if strategy.device.type == "cuda" else "fp32 (host reference path, no GPU)"

@@ -745,6 +745,201 @@ __global__ __launch_bounds__(256) void part_agg2_k(const long long* __restrict__
 }
 
 // ================================================================================================
+// Stable LSD radix sort of 64-bit keys with a 64-bit payload (DataFrame.orderBy / sort)
+//   sort_key_prep_k  column -> unsigned-orderable u64 (asc or desc; NaN above +inf, -0 == +0) and
+//                    the key range [min, max]: only the significant bits of (max - min) are sorted
+//   sort_count_k     per-tile 256-bin digit histograms, digit-major [digit][tile], so one
+//                    exclusive scan gives every (digit, tile) its output run in stable order
+//   sort_scatter_k   stable in-tile ranking (8-ballot match per wave, per-round wave prefix over
+//                    LDS), rows staged in LDS by digit, written out as 256 contiguous runs
+//   range_partition_k  destination rank = #splitters below the key (sample-based range shuffle)
+// ================================================================================================
+#ifndef PTG_ST
+#define PTG_ST 2048
+#endif
+#define ST PTG_ST        // rows per sort tile
+#define SB 256           // digit bins (8 bits per pass)
+#define SRPT (ST / 256)
+
+PTG_DEV unsigned long long orderable_key(const void* col, int type, long i, int desc) {
+  unsigned long long u;
+  switch (type) {
+    case CT_F32:
+    case CT_F64: {
+      double x = type == CT_F32 ? (double)((const float*)col)[i] : ((const double*)col)[i];
+      if (x != x) x = __builtin_nan("");
+      x = x + 0.0;  // -0 -> +0
+      const unsigned long long b = (unsigned long long)__double_as_longlong(x);
+      u = (b >> 63) ? ~b : (b | 0x8000000000000000ULL);
+      break;
+    }
+    case CT_I32: u = (unsigned long long)(long long)((const int*)col)[i] ^ 0x8000000000000000ULL; break;
+    case CT_U8: u = (unsigned long long)((const uint8_t*)col)[i]; break;
+    default: u = (unsigned long long)((const long long*)col)[i] ^ 0x8000000000000000ULL; break;
+  }
+  return desc ? ~u : u;
+}
+
+PTG_DEV unsigned long long wave_min_u64(unsigned long long v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) { const unsigned long long t = __shfl_xor(v, o, 64); v = t < v ? t : v; }
+  return v;
+}
+PTG_DEV unsigned long long wave_max_u64(unsigned long long v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) { const unsigned long long t = __shfl_xor(v, o, 64); v = t > v ? t : v; }
+  return v;
+}
+
+// range[0] = min, range[1] = max (initialised to ~0 / 0 by the host)
+__global__ __launch_bounds__(256) void sort_key_prep_k(const void* __restrict__ col, int type, long n, int desc,
+                                                       unsigned long long* __restrict__ out,
+                                                       unsigned long long* __restrict__ range) {
+  unsigned long long mn = ~0ULL, mx = 0ULL;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const unsigned long long u = orderable_key(col, type, i, desc);
+    out[i] = u;
+    mn = u < mn ? u : mn;
+    mx = u > mx ? u : mx;
+  }
+  mn = wave_min_u64(mn);
+  mx = wave_max_u64(mx);
+  if ((threadIdx.x & 63) == 0) {
+    atomicMin(&range[0], mn);
+    atomicMax(&range[1], mx);
+  }
+}
+
+__global__ __launch_bounds__(256) void sort_count_k(const unsigned long long* __restrict__ keys, long n,
+                                                    unsigned long long base, int shift, int ntiles,
+                                                    unsigned int* __restrict__ hist) {
+  __shared__ unsigned int h[4][SB];
+  const int tid = threadIdx.x, w = tid >> 6, b = blockIdx.x;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) h[q][tid] = 0;
+  const long s0 = (long)b * ST;
+  unsigned long long k[SRPT];
+#pragma unroll
+  for (int j = 0; j < SRPT; ++j) {
+    const long i = s0 + j * 256 + tid;
+    k[j] = i < n ? keys[i] : 0ULL;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < SRPT; ++j)
+    if (s0 + j * 256 + tid < n) atomicAdd(&h[w][(unsigned)((k[j] - base) >> shift) & (SB - 1)], 1u);
+  __syncthreads();
+  hist[(long)tid * ntiles + b] = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
+}
+
+// vals_in == nullptr: payload = row index (first pass of a fresh sort)
+__global__ __launch_bounds__(256) void sort_scatter_k(const unsigned long long* __restrict__ keys_in,
+                                                      const long long* __restrict__ vals_in, long n,
+                                                      unsigned long long base, int shift, int ntiles,
+                                                      const long long* __restrict__ offs,
+                                                      unsigned long long* __restrict__ keys_out,
+                                                      long long* __restrict__ vals_out) {
+  __shared__ unsigned long long sk[ST];
+  __shared__ long long sv[ST];
+  __shared__ unsigned char sd[ST];
+  __shared__ unsigned int wc[4][SB];
+  __shared__ unsigned int woff[4][SB];
+  __shared__ unsigned int lstart[SB];
+  __shared__ long long goff[SB];
+  __shared__ int wsum[4];
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, b = blockIdx.x;
+  const long s0 = (long)b * ST;
+  const int nr = (int)((n - s0) < ST ? (n - s0) : ST);
+  goff[tid] = offs[(long)tid * ntiles + b];
+  unsigned long long k[SRPT];
+  long long v[SRPT];
+  int d[SRPT], r[SRPT];
+#pragma unroll
+  for (int j = 0; j < SRPT; ++j) {
+    const int i = j * 256 + tid;
+    d[j] = -1;
+    if (i < nr) {
+      k[j] = keys_in[s0 + i];
+      v[j] = vals_in ? vals_in[s0 + i] : s0 + i;
+      d[j] = (int)((k[j] - base) >> shift) & (SB - 1);
+    }
+  }
+  const unsigned long long lt = (1ULL << lane) - 1ULL;
+  unsigned int running = 0;  // thread tid owns digit tid
+#pragma unroll
+  for (int j = 0; j < SRPT; ++j) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) wc[w][lane * 4 + q] = 0;
+    __syncthreads();
+    const bool valid = d[j] >= 0;
+    unsigned long long peers = __ballot(valid);
+#pragma unroll
+    for (int bit = 0; bit < 8; ++bit) {
+      const bool set = valid && ((d[j] >> bit) & 1);
+      const unsigned long long bb = __ballot(set);
+      peers &= set ? bb : ~bb;
+    }
+    const int rank_w = __popcll(peers & lt);
+    if (valid && rank_w == 0) wc[w][d[j]] = (unsigned)__popcll(peers);
+    __syncthreads();
+    {
+      const unsigned c0 = wc[0][tid], c1 = wc[1][tid], c2 = wc[2][tid], c3 = wc[3][tid];
+      woff[0][tid] = running;
+      woff[1][tid] = running + c0;
+      woff[2][tid] = running + c0 + c1;
+      woff[3][tid] = running + c0 + c1 + c2;
+      running += c0 + c1 + c2 + c3;
+    }
+    __syncthreads();
+    r[j] = valid ? (int)woff[w][d[j]] + rank_w : 0;
+  }
+  int total;
+  const int ls = block_excl_scan256((int)running, wsum, &total);
+  lstart[tid] = (unsigned)ls;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < SRPT; ++j) {
+    if (d[j] < 0) continue;
+    const int pos = (int)lstart[d[j]] + r[j];
+    sk[pos] = k[j];
+    sv[pos] = v[j];
+    sd[pos] = (unsigned char)d[j];
+  }
+  __syncthreads();
+  for (int i = tid; i < nr; i += 256) {
+    const int dd = sd[i];
+    const long long dst = PTG_CHECKED_IDX(goff[dd] + (i - (int)lstart[dd]), n);
+    keys_out[dst] = sk[i];
+    vals_out[dst] = sv[i];
+  }
+}
+
+// part[i] = number of splitters strictly below keys[i] (unsigned order); counts[dest] += 1
+__global__ __launch_bounds__(256) void range_partition_k(const unsigned long long* __restrict__ keys, long n,
+                                                         const unsigned long long* __restrict__ split, int nsplit,
+                                                         int* __restrict__ part,
+                                                         unsigned long long* __restrict__ counts) {
+  __shared__ unsigned long long sp[1024];
+  __shared__ unsigned int h[1025];
+  for (int t = threadIdx.x; t < nsplit; t += 256) sp[t] = split[t];
+  for (int t = threadIdx.x; t <= nsplit; t += 256) h[t] = 0;
+  __syncthreads();
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const unsigned long long k = keys[i];
+    int lo = 0, hi = nsplit;  // first splitter >= k
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (sp[mid] < k) lo = mid + 1; else hi = mid;
+    }
+    part[i] = lo;
+    atomicAdd(&h[lo], 1u);
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t <= nsplit; t += 256)
+    if (h[t]) atomicAdd(&counts[t], (unsigned long long)h[t]);
+}
+
+// ================================================================================================
 // histogram of int32 codes (StringIndexer fit); codes < 0 (null) counted in bin nbins
 // ================================================================================================
 __global__ __launch_bounds__(256) void histogram_k(const int* __restrict__ codes, long n, unsigned long long* __restrict__ out,
@@ -970,6 +1165,40 @@ int ptg_part_agg2(const void* okeys, const void* const* vals, int nv, int minmax
                   case 3: PTG_AGG(3, false) break; default: PTG_AGG(4, false) break; }
   }
 #undef PTG_AGG
+  PTG_RETURN_LAUNCH();
+}
+
+// sort: keys u64[n] out, range u64[2] (host-initialised {~0, 0})
+int ptg_sort_key_prep(const void* col, int type, long n, int desc, void* out, void* range, hipStream_t s) {
+  int g = grid_n(n);
+  if (g > 2048) g = 2048;
+  hipLaunchKernelGGL(sort_key_prep_k, dim3(g), dim3(256), 0, s, col, type, n, desc, (unsigned long long*)out,
+                     (unsigned long long*)range);
+  PTG_RETURN_LAUNCH();
+}
+int ptg_sort_tile_rows() { return ST; }
+// one LSD pass: hist u32[256*ntiles] (digit-major) -> offs i64[256*ntiles] (exclusive scan, host/torch)
+int ptg_sort_count(const void* keys, long n, long base, int shift, void* hist, hipStream_t s) {
+  const int ntiles = (int)((n + ST - 1) / ST);
+  if (ntiles <= 0) return 0;
+  hipLaunchKernelGGL(sort_count_k, dim3(ntiles), dim3(256), 0, s, (const unsigned long long*)keys, n,
+                     (unsigned long long)base, shift, ntiles, (unsigned int*)hist);
+  PTG_RETURN_LAUNCH();
+}
+int ptg_sort_scatter(const void* keys_in, const void* vals_in, long n, long base, int shift, const void* offs,
+                     void* keys_out, void* vals_out, hipStream_t s) {
+  const int ntiles = (int)((n + ST - 1) / ST);
+  if (ntiles <= 0) return 0;
+  hipLaunchKernelGGL(sort_scatter_k, dim3(ntiles), dim3(256), 0, s, (const unsigned long long*)keys_in,
+                     (const long long*)vals_in, n, (unsigned long long)base, shift, ntiles, (const long long*)offs,
+                     (unsigned long long*)keys_out, (long long*)vals_out);
+  PTG_RETURN_LAUNCH();
+}
+int ptg_range_partition(const void* keys, long n, const void* split, int nsplit, void* part, void* counts,
+                        hipStream_t s) {
+  if (nsplit > 1024 || nsplit < 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(range_partition_k, dim3(grid_n(n)), dim3(256), 0, s, (const unsigned long long*)keys, n,
+                     (const unsigned long long*)split, nsplit, (int*)part, (unsigned long long*)counts);
   PTG_RETURN_LAUNCH();
 }
 

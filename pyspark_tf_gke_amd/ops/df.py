@@ -359,6 +359,19 @@ def hash_agg_radix(keys: torch.Tensor, vals: list, valids: list, want_minmax: bo
     return ok, ot[0], outs
 
 
+def partition_perm(part: torch.Tensor, counts: torch.Tensor) -> torch.Tensor:
+    """Row indices grouped by destination partition (stable within a block of rows)."""
+    n = part.numel()
+    P = counts.numel()
+    if not on_device(part):
+        return torch.from_numpy(np.argsort(part.numpy(), kind="stable").astype(np.int64))
+    cursor = torch.zeros(P, dtype=torch.int64, device=part.device)
+    cursor[1:] = torch.cumsum(counts, 0)[:-1]
+    perm = torch.empty(n, dtype=torch.int64, device=part.device)
+    hip("ptg_partition_perm", ptr(part), n, P, ptr(cursor), ptr(perm))
+    return perm
+
+
 def hash_partition(keys: torch.Tensor, P: int):
     """-> (perm[n] int64 rows grouped by destination partition, counts[P] int64)."""
     n = keys.numel()
@@ -372,11 +385,120 @@ def hash_partition(keys: torch.Tensor, P: int):
     part = torch.empty(n, dtype=torch.int32, device=dev)
     counts = torch.zeros(P, dtype=torch.int64, device=dev)
     hip("ptg_hash_partition", ptr(keys), n, P, ptr(part), ptr(counts))
-    cursor = torch.zeros(P, dtype=torch.int64, device=dev)
-    cursor[1:] = torch.cumsum(counts, 0)[:-1]
-    perm = torch.empty(n, dtype=torch.int64, device=dev)
-    hip("ptg_partition_perm", ptr(part), n, P, ptr(cursor), ptr(perm))
-    return perm, counts
+    return partition_perm(part, counts), counts
+
+
+# ------------------------------------------------------------------------------------------------
+# sort (stable LSD radix over unsigned-orderable 64-bit keys)
+# ------------------------------------------------------------------------------------------------
+_U64 = (1 << 64) - 1
+_SIGN = np.uint64(1 << 63)
+
+
+def _signed(u: int) -> int:
+    return u - (1 << 64) if u >= (1 << 63) else u
+
+
+def _orderable_np(x: torch.Tensor, desc: bool) -> np.ndarray:
+    a = x.numpy()
+    if a.dtype.kind == "f":
+        f = a.astype(np.float64)
+        f = np.where(np.isnan(f), np.nan, f) + 0.0  # canonical NaN (sorts above +inf), -0 -> +0
+        b = f.view(np.uint64)
+        u = np.where((b >> np.uint64(63)) != 0, ~b, b | _SIGN)
+    elif a.dtype in (np.uint8, np.bool_):
+        u = a.astype(np.uint64)
+    else:
+        u = a.astype(np.int64).view(np.uint64) ^ _SIGN
+    return ~u if desc else u
+
+
+def sort_key(col: torch.Tensor, desc: bool = False):
+    """Column -> (int64 tensor holding unsigned-orderable u64 keys, lo, hi) with lo/hi the key range
+    as Python ints in [0, 2^64)."""
+    n = col.numel()
+    if not on_device(col):
+        u = _orderable_np(col.contiguous(), desc)
+        lo, hi = (int(u.min()), int(u.max())) if n else (0, 0)
+        return torch.from_numpy(u.view(np.int64).copy()), lo, hi
+    c = col.view(torch.uint8) if col.dtype == torch.bool else col.contiguous()
+    out = torch.empty(n, dtype=torch.int64, device=col.device)
+    rng = torch.tensor([-1, 0], dtype=torch.int64, device=col.device)
+    if n:
+        hip("ptg_sort_key_prep", ptr(c), TORCH_CT[c.dtype], n, int(desc), ptr(out), ptr(rng))
+    lo, hi = (x & _U64 for x in rng.cpu().tolist())
+    return out, (lo if n else 0), (hi if n else 0)
+
+
+def radix_sort_u64(keys: torch.Tensor, vals: torch.Tensor | None = None, lo: int = 0, hi: int = _U64):
+    """Stable sort of u64 keys (held in an int64 tensor) with an int64 payload (default: the row
+    index, i.e. the result payload is the sorting permutation).  Only the significant bits of
+    hi - lo are sorted: ceil(bits / 8) LSD passes of sort_count_k + sort_scatter_k."""
+    n = keys.numel()
+    if not on_device(keys):
+        u = keys.numpy().view(np.uint64)
+        order = np.argsort(u, kind="stable")
+        v = torch.from_numpy(order.astype(np.int64)) if vals is None else vals[torch.from_numpy(order)]
+        return keys[torch.from_numpy(order)], v
+    dev = keys.device
+    bits = (hi - lo).bit_length()
+    passes = (bits + 7) // 8
+    if n == 0 or passes == 0:
+        return keys, (torch.arange(n, dtype=torch.int64, device=dev) if vals is None else vals)
+    ntiles = -(-n // _native.hip_lib().ptg_sort_tile_rows())
+    hist = torch.empty(256 * ntiles, dtype=torch.int32, device=dev)
+    offs = torch.empty(256 * ntiles, dtype=torch.int64, device=dev)
+    ka, va = keys.contiguous(), (None if vals is None else vals.contiguous())
+    kb = torch.empty(n, dtype=torch.int64, device=dev)
+    vb = torch.empty(n, dtype=torch.int64, device=dev)
+    kc = vc = None
+    base = _signed(lo)
+    for p in range(passes):
+        shift = 8 * p
+        hip("ptg_sort_count", ptr(ka), n, base, shift, ptr(hist))
+        torch.cumsum(hist, 0, dtype=torch.int64, out=offs)
+        offs.sub_(hist)
+        hip("ptg_sort_scatter", ptr(ka), ptr(va), n, base, shift, ptr(offs), ptr(kb), ptr(vb))
+        if kc is None:  # third buffer pair so the caller's keys/vals are never overwritten
+            kc = torch.empty(n, dtype=torch.int64, device=dev)
+            vc = torch.empty(n, dtype=torch.int64, device=dev)
+            ka, va, kb, vb = kb, vb, kc, vc
+        else:
+            ka, va, kb, vb = kb, vb, ka, va
+    return ka, va
+
+
+def argsort_columns(cols) -> torch.Tensor | None:
+    """Stable multi-column argsort (Spark orderBy): ``cols`` = [(data, null mask or None, desc)] in
+    priority order; nulls first for ascending, last for descending (Spark's defaults).  LSD over
+    columns: the lowest-priority column is sorted first and every later pass is stable."""
+    perm = None
+    for data, null, desc in reversed(list(cols)):
+        src = data if perm is None else gather_rows(data, perm)
+        k, lo, hi = sort_key(src, desc)
+        _, perm = radix_sort_u64(k, perm, lo, hi)
+        if null is not None:
+            nl = gather_rows(null.to(torch.uint8).contiguous(), perm)
+            flag = nl.long() if desc else (1 - nl.long())  # key 0 sorts first
+            _, perm = radix_sort_u64(flag, perm, 0, 1)
+    return perm
+
+
+def range_partition(keys: torch.Tensor, splitters: torch.Tensor, P: int):
+    """-> (part int32[n], counts int64[P]): destination = number of splitters below the key
+    (unsigned order; equal keys always land together)."""
+    n = keys.numel()
+    ns = splitters.numel()
+    if not on_device(keys):
+        u = keys.numpy().view(np.uint64)
+        sp = splitters.numpy().view(np.uint64)
+        part = np.searchsorted(sp, u, side="left").astype(np.int32)
+        return torch.from_numpy(part), torch.from_numpy(np.bincount(part, minlength=P).astype(np.int64))
+    part = torch.empty(n, dtype=torch.int32, device=keys.device)
+    counts = torch.zeros(P, dtype=torch.int64, device=keys.device)
+    sp = splitters.to(keys.device).contiguous()
+    hip("ptg_range_partition", ptr(keys), n, ptr(sp), ns, ptr(part), ptr(counts))
+    return part, counts
 
 
 def _mix64_np(x: np.ndarray) -> np.ndarray:

@@ -158,6 +158,17 @@ def all_reduce_float(values, op=dist.ReduceOp.SUM) -> list:
     return [float(x) for x in t.cpu().tolist()]
 
 
+def all_gather_int(value: int) -> list:
+    """Every rank's int (one int64 all-gather) -> list in rank order."""
+    if not is_initialized() or dist.get_world_size() == 1:
+        return [int(value)]
+    dev = _ctl_device()
+    t = torch.tensor([int(value)], dtype=torch.int64, device=dev)
+    out = torch.empty(dist.get_world_size(), dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(out, t)
+    return [int(x) for x in out.cpu().tolist()]
+
+
 def all_reduce_tensor_(t: torch.Tensor, op=dist.ReduceOp.SUM) -> torch.Tensor:
     """In-place all-reduce of a tensor on whatever device it lives (staged through the control
     device when the backend cannot reach it, e.g. CPU tensors under RCCL)."""

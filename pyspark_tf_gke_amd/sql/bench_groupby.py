@@ -58,3 +58,47 @@ def run(total_rows: int = 1_000_000_000, num_keys: int = 1_000_000, steps: int =
             "config": {"model": "groupBy(key).agg(sum(value), count(*)) on (bigint key, double value)",
                        "rows_per_gpu": n, "global_rows": n * world, "distinct_keys": num_keys, "groups_out": groups,
                        "counts_check": ok, "parallelism": f"{world} executors (1 per GPU), RCCL all-to-all-v shuffle"}}
+
+
+def run_sort(rows_per_gpu: int = 1_000_000_000, steps: int = 3, warmup: int = 1, device=None,
+             key_range: int = (1 << 63) - 1) -> dict:
+    """``df.orderBy("key")`` over (bigint key, double value) rows resident in HBM: orderable-key
+    prep, stable LSD radix sort of the significant key bits (8 passes for full-range int64 keys),
+    row gather of both columns; world > 1 adds the sample-based range shuffle over RCCL.
+    rows/s = total rows sorted per second over all GPUs."""
+    from ..ops import df as D
+    from .dataframe import DataFrame
+    from .session import SparkSession
+    from .table import ColumnVector, Table
+    from . import types as T
+
+    world, rank = comm.world_size(), comm.rank()
+    n = rows_per_gpu
+    spark = SparkSession.builder.master("mi355x").getOrCreate()
+    dev = spark.device if device is None else torch.device(device)
+    keys, vals = D.fill_synthetic_kv(n, key_range, dev, offset=rank * n, seed=7)
+    df = DataFrame(Table({"key": ColumnVector(keys, T.LongType()), "value": ColumnVector(vals, T.DoubleType())}, n, dev),
+                   spark)
+    out = None
+    for _ in range(warmup):
+        out = df.orderBy("key")
+        del out
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    comm.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        out = df.orderBy("key")
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    comm.barrier()
+    dt = comm.all_reduce_max_scalar(time.perf_counter() - t0)
+    k = out._t.column("key").data
+    ok = bool((k[1:] >= k[:-1]).all().item()) if k.numel() > 1 else True
+    ok = bool(comm.all_reduce_int([int(not ok)])[0] == 0)
+    total = comm.all_reduce_int([out._t.num_rows])[0]
+    return {"metric": "rows/sec Spark orderBy (sort)", "value": round(n * world * steps / dt, 1), "unit": "rows/s",
+            "ms_per_step": round(dt / steps * 1e3, 3),
+            "config": {"model": "orderBy(key) on (bigint key, double value), full-range random int64 keys",
+                       "rows_per_gpu": n, "global_rows": n * world, "sorted_check": ok and total == n * world,
+                       "parallelism": f"{world} executors (1 per GPU), range shuffle over RCCL"}}

@@ -266,7 +266,7 @@ class DataFrame:
 
     def limit(self, num: int) -> "DataFrame":
         # global limit: ranks keep rows in rank order until `num` rows are taken
-        counts = comm.all_gather_object(self._t.num_rows)
+        counts = comm.all_gather_int(self._t.num_rows)
         before = sum(counts[: comm.rank()])
         keep = max(0, min(self._t.num_rows, num - before))
         return self._new(self._t.slice(0, keep))
@@ -304,18 +304,12 @@ class DataFrame:
 
     # ------------------------------------------------------------------ actions
     def count(self) -> int:
-        n = torch.tensor([self._t.num_rows], dtype=torch.int64)
-        if comm.world_size() > 1:
-            return int(sum(comm.all_gather_object(self._t.num_rows)))
-        return int(n.item())
+        return int(comm.all_reduce_int([self._t.num_rows])[0])
 
     def collect(self) -> list:
         names = self.columns
-        local = self._t.rows()
-        if comm.world_size() > 1:
-            parts = comm.all_gather_object(local)
-            local = [r for p in parts for r in p]
-        return [Row._make(names, r) for r in local]
+        t = _gather_table_all(self._t) if comm.world_size() > 1 else self._t
+        return [Row._make(names, r) for r in t.rows()]
 
     def take(self, num: int) -> list:
         return self.limit(num).collect()
@@ -393,8 +387,7 @@ class DataFrame:
             x = cv.data.double()
             ok = cv.valid_bool() & ~torch.isnan(x)
             dev2 = float(((x - (mean or 0.0)) ** 2)[ok].sum()) if c else 0.0
-            if comm.world_size() > 1:
-                dev2 = float(sum(comm.all_gather_object(dev2)))
+            dev2 = comm.all_reduce_float([dev2])[0]
             sd = math.sqrt(dev2 / (c - 1)) if c > 1 else None
             stats[n] = [str(int(c)), str(mean), str(sd), str(mn if c else None), str(mx if c else None)]
         rows = [["count"], ["mean"], ["stddev"], ["min"], ["max"]]
@@ -405,33 +398,42 @@ class DataFrame:
 
     # ------------------------------------------------------------------ misc
     def orderBy(self, *cols, ascending=True) -> "DataFrame":  # noqa: N802
+        """Global sort.  World > 1: sample-based range partitioning on the first sort column (one
+        tensor all-gather of samples, splitters picked on every rank identically), RCCL
+        all-to-all-v of the rows, then a stable multi-column LSD radix sort (sort_scatter_k) on
+        each rank; rank r holds the r-th key range, so rank-order concatenation is globally sorted."""
         if len(cols) == 1 and isinstance(cols[0], (list, tuple)):
             cols = tuple(cols[0])
-        t = self._t
-        if comm.world_size() > 1:
-            # global order: gather to rank 0 (sort results are small in the workloads), rank 0 sorts
-            t = _gather_table_to_rank0(t)
-        if t.num_rows == 0:
-            return self._new(t)
         asc = ascending if isinstance(ascending, (list, tuple)) else [ascending] * len(cols)
-        perm = torch.arange(t.num_rows, device=t.device)
-        for c, a in reversed(list(zip(cols, asc))):
+        specs = []
+        for c, a in zip(cols, asc):
             c = _to_col(c)
             if c.node[0] == "sort":
                 a = c.node[1]
                 c = Column(c.node[2])
-            _, cv = DataFrame(t, self.sparkSession)._eval(c)
-            key = cv.data.take(perm) if cv.data.dim() == 1 else cv.data[perm]
-            if isinstance(cv.dtype, T.StringType):
-                order = np.argsort(np.argsort(np.array(cv.dictionary or [], dtype=object)))
-                lut = torch.tensor(list(order) + [-1], dtype=torch.int64, device=t.device)
-                kk = key.long()
-                key = lut[torch.where(kk < 0, torch.full_like(kk, len(order)), kk)]
-            key = key.double() if key.dtype == torch.bool else key
-            idx = torch.argsort(key, stable=True, descending=not a)
-            perm = perm[idx]
-        return self._new(t.take(perm))
+            specs.append((c, bool(a)))
+        t = self._t
+        world = comm.world_size()
+        if world > 1:
+            from . import shuffle as SH
 
+            t = SH._unify_strings(t)
+            data0, null0 = _sort_operand(DataFrame(t, self.sparkSession)._eval(specs[0][0])[1])
+            k0, _, _ = D.sort_key(data0, desc=not specs[0][1])
+            splitters = _range_splitters(k0 if null0 is None else k0[~null0], world)
+            part, counts = D.range_partition(k0, splitters, world)
+            if null0 is not None and bool(null0.any()):
+                part = torch.where(null0, torch.full_like(part, 0 if specs[0][1] else world - 1), part)
+                counts = torch.bincount(part.long(), minlength=world).to(torch.int64)
+            t = SH.shuffle_table(t, D.partition_perm(part, counts), counts)
+        if t.num_rows == 0 or not specs:
+            return self._new(t)
+        df_t = DataFrame(t, self.sparkSession)
+        keys = []
+        for c, a in specs:
+            data, null = _sort_operand(df_t._eval(c)[1])
+            keys.append((data, null, not a))
+        return self._new(t.take(D.argsort_columns(keys)))
     sort = orderBy
 
     def distinct(self) -> "DataFrame":
@@ -459,6 +461,10 @@ class DataFrame:
         d = self._new(self._t)
         if cols and comm.world_size() > 1:
             d = self._new(_shuffle_by_key(self._t, _group_keys(self, [_to_col(c) for c in cols])[0]))
+        elif numPartitions and comm.world_size() > 1:
+            from .shuffle import round_robin_shuffle
+
+            d = self._new(round_robin_shuffle(self._t))
         if numPartitions:
             d._num_partitions = int(numPartitions)
         return d
@@ -609,10 +615,63 @@ def _global_stats(cv: ColumnVector):
     s, c, mn, mx, nul = D.reduce_stats(cv.data if cv.data.dtype != torch.bool else cv.data.to(torch.uint8),
                                        cv.valid_u8(), skip_nan=True)
     if comm.world_size() > 1:
-        parts = comm.all_gather_object((s, c, mn, mx, nul))
-        s = sum(p[0] for p in parts); c = sum(p[1] for p in parts)
-        mn = min(p[2] for p in parts); mx = max(p[3] for p in parts); nul = sum(p[4] for p in parts)
+        s, c, nul = comm.all_reduce_float([s, c, nul])
+        mx, neg_mn = comm.all_reduce_float([mx, -mn], op=torch.distributed.ReduceOp.MAX)
+        mn = -neg_mn
     return s, c, mn, mx, nul
+
+
+def _gather_table_all(t: Table) -> Table:
+    """Every rank's rows, in rank order, on every rank (collect): one tensor all-gather per column
+    (+ validity), string columns after a dictionary union."""
+    from .readwriter import unify_dictionary
+
+    cols = {}
+    for n, cv in t.columns.items():
+        if isinstance(cv.dtype, T.StringType):
+            cv = unify_dictionary(cv)
+        data = torch.cat(comm.all_gather_v(cv.data.contiguous()))
+        valid = None
+        if comm.all_reduce_int([int(cv.valid is not None)])[0]:
+            v = cv.valid_u8() if cv.valid is not None else torch.ones(len(cv), dtype=torch.uint8, device=cv.device)
+            valid = torch.cat(comm.all_gather_v(v.contiguous()))
+        cols[n] = ColumnVector(data, cv.dtype, valid, cv.dictionary)
+    return Table(cols, sum(comm.all_gather_int(t.num_rows)), t.device)
+
+
+def _sort_operand(cv: ColumnVector):
+    """Column -> (tensor sort_key can order, null mask or None).  Strings sort by the rank of their
+    dictionary entry (host sort of the distinct labels); NaN is a value (sorts above +inf)."""
+    d = cv.data
+    null = None
+    if isinstance(cv.dtype, T.StringType):
+        order = np.argsort(np.array(cv.dictionary or [], dtype=object), kind="stable")
+        rank = np.empty(len(order) + 1, dtype=np.int64)
+        rank[order] = np.arange(len(order))
+        rank[-1] = 0
+        lut = torch.from_numpy(rank).to(d.device)
+        codes = d.long()
+        null = codes < 0
+        d = D.gather_rows(lut, torch.where(null, torch.full_like(codes, len(order)), codes))
+    if cv.valid is not None:
+        inv = ~cv.valid.bool()
+        null = inv if null is None else (null | inv)
+    if null is not None and not bool(null.any()):
+        null = None
+    return d, null
+
+
+def _range_splitters(keys: torch.Tensor, world: int, per_rank: int = 4096) -> torch.Tensor:
+    """world-1 splitters (u64 bit patterns in int64) from a strided sample of every rank's keys."""
+    n = keys.numel()
+    step = max(1, n // per_rank)
+    sample = keys[::step][:per_rank].contiguous()
+    allk = torch.cat(comm.all_gather_v(sample)).cpu().numpy().view(np.uint64)
+    allk.sort()
+    if allk.size == 0:
+        return torch.zeros(world - 1, dtype=torch.int64)
+    pos = [min(allk.size - 1, (i * allk.size) // world) for i in range(1, world)]
+    return torch.from_numpy(allk[pos].view(np.int64).copy())
 
 
 # ------------------------------------------------------------------------------------------------
@@ -716,37 +775,10 @@ def _group_keys(df: "DataFrame", cols: list):
 
 
 def _shuffle_by_key(t: Table, key: torch.Tensor) -> Table:
-    """Hash-partition rows by key across ranks (RCCL all-to-all-v of every column)."""
-    world = comm.world_size()
-    perm, counts = D.hash_partition(key, world)
-    send = t.take(perm)
-    sc = [int(x) for x in counts.cpu().tolist()]
-    rc = None
-    cols = {}
-    for n, cv in send.columns.items():
-        data = comm.all_to_all_v(cv.data.contiguous(), sc, rc)
-        if rc is None:
-            rc = [int(x) for x in _recv_counts(sc)]
-        valid = comm.all_to_all_v(cv.valid_u8().contiguous(), sc, rc) if cv.valid is not None else None
-        cols[n] = ColumnVector(data, cv.dtype, valid, cv.dictionary)
-    nrows = sum(rc) if rc is not None else 0
-    return Table(cols, nrows, t.device)
+    """Hash-partition rows by key across ranks (bounded, chunked RCCL all-to-all-v; sql/shuffle.py)."""
+    from .shuffle import hash_shuffle
 
-
-def _recv_counts(send_counts):
-    parts = comm.all_gather_object(send_counts)
-    r = comm.rank()
-    return [p[r] for p in parts]
-
-
-def _gather_table_to_rank0(t: Table) -> Table:
-    parts = comm.all_gather_object({n: (c.data.cpu(), None if c.valid is None else c.valid.cpu(), c.dtype,
-                                        c.dictionary) for n, c in t.columns.items()})
-    if comm.rank() != 0:
-        return t.slice(0, 0)
-    tables = [Table({n: ColumnVector(v[0].to(t.device), v[2], None if v[1] is None else v[1].to(t.device), v[3])
-                     for n, v in p.items()}) for p in parts]
-    return Table.concat(tables)
+    return hash_shuffle(t, key)
 
 
 class GroupedData:
@@ -823,8 +855,7 @@ class GroupedData:
                     # Spark count(col) counts non-null values (NaN counts as a value)
                     x = cv.data
                     if x.dtype in (torch.float32, torch.float64):
-                        nn = int((cv.valid_bool()).sum())
-                        vals[label] = int(sum(comm.all_gather_object(nn))) if world > 1 else nn
+                        vals[label] = comm.all_reduce_int([int((cv.valid_bool()).sum())])[0]
                 elif fn == "sum":
                     vals[label] = s if c else None
                 elif fn == "avg":
@@ -837,9 +868,7 @@ class GroupedData:
                     mean = s / c if c else 0.0
                     x = cv.data.double()
                     ok = cv.valid_bool() & ~torch.isnan(x)
-                    d2 = float(((x - mean) ** 2)[ok].sum())
-                    if world > 1:
-                        d2 = float(sum(comm.all_gather_object(d2)))
+                    d2 = comm.all_reduce_float([float(((x - mean) ** 2)[ok].sum())])[0]
                     vals[label] = math.sqrt(d2 / (c - 1)) if c > 1 else None
                 else:
                     raise ValueError(f"unsupported aggregate {fn}")

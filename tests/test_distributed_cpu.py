@@ -205,3 +205,53 @@ def test_launcher_fails_fast_and_restarts():
     r2 = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=180, cwd=ROOT)
     assert r2.returncode == 0, r2.stderr
     assert len(_results(r2.stdout)) == 2
+
+
+def test_distributed_orderby_and_bounded_shuffle():
+    """2 gloo ranks: range-partitioned orderBy is globally sorted in rank order and equals the sort
+    of the union; a repartition under a 64 KB staging budget runs in several rounds, never stages
+    more than the budget per direction, and count/agg/describe/groupBy/orderBy on numeric columns
+    run without a single pickled collective."""
+    body = """
+    import json, numpy as np, torch
+    from pyspark_tf_gke_amd.parallel import comm
+    from pyspark_tf_gke_amd.sql import SparkSession
+    from pyspark_tf_gke_amd.sql import shuffle as SH
+    from pyspark_tf_gke_amd.sql.functions import col, sum as fsum, count
+    s = SparkSession.builder.master("spark://127.0.0.1:7077").config("spark.ptg.shuffle.buffer.gb", 64 / 2**20).getOrCreate()
+    r = comm.rank()
+    rng = np.random.default_rng(10 + r)
+    n = 20000 + 3000 * r
+    rows = [(int(rng.integers(-10**6, 10**6)), float(rng.normal()), r * 100000 + i) for i in range(n)]
+    df = s.createDataFrame(rows, ["a", "b", "id"], _local=True)
+    def boom(o):
+        raise AssertionError("pickled collective on a numeric data path")
+    orig = comm.all_gather_object
+    comm.all_gather_object = boom
+    total = df.count()
+    sums = df.agg(fsum("b")).collect()
+    d = df.describe("a")
+    g = df.groupBy("a").agg(count("*").alias("c"))
+    gc = g.agg(fsum("c")).collect()[0][0]
+    o = df.orderBy(col("a").desc(), "id")
+    local = [(x[0], x[2]) for x in o._t.rows()]
+    rep = df.repartition(4)
+    peak, rounds = SH.STATS["peak_staging_bytes"], SH.STATS["rounds"]
+    comm.all_gather_object = orig
+    d.collect()
+    print("RESULT", json.dumps({"total": total, "gc": gc, "local": local, "rep_n": rep._t.num_rows,
+                                "rep_total": rep.count(), "peak": peak, "rounds": rounds,
+                                "mine": [(x[0], x[2]) for x in rows]}), flush=True)
+    """
+    r = _run_ranks(body)
+    assert r.returncode == 0, r.stdout + r.stderr
+    res = _results(r.stdout)
+    allrows = res[0]["mine"] + res[1]["mine"]
+    want = sorted(allrows, key=lambda t: (-t[0], t[1]))
+    got = [tuple(x) for x in res[0]["local"] + res[1]["local"]]
+    assert got == [tuple(x) for x in want]
+    assert res[0]["local"] and res[1]["local"]  # both ranks hold a key range
+    for v in res.values():
+        assert v["total"] == len(allrows) and v["gc"] == len(allrows) and v["rep_total"] == len(allrows)
+        assert v["rounds"] > 1 and v["peak"] <= 2 * 64 * 1024
+    assert abs(res[0]["rep_n"] - res[1]["rep_n"]) <= 2

@@ -135,3 +135,61 @@ def test_groupby_null_key_is_its_own_group():
     got = {(r["a"], r["b"]): r["s"] for r in df.groupBy("a", "b").agg(F.sum("v").alias("s")).collect()}
     assert got == {(1, None): 4.0, (1, "a"): 2.0, (2, "a"): 4.0}
     assert df.agg(F.countDistinct("b").alias("d")).collect()[0]["d"] == 1
+
+
+def _py_sort_key(v, asc):
+    """Spark order of one value: nulls first (asc) / last (desc); NaN above every number."""
+    if v is None:
+        return (0,) if asc else (2,)
+    if isinstance(v, float) and math.isnan(v):
+        return (1, 1, 0.0)
+    return (1, 0, v)
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_orderby_matches_python_sort(spark, seed):
+    """Multi-column orderBy (radix sort path; host executor) vs Python's stable sort with Spark's
+    null/NaN ordering, ascending and descending."""
+    rng = np.random.default_rng(seed)
+    n = 3000
+    rows = []
+    for i in range(n):
+        x = None if rng.random() < 0.05 else int(rng.integers(-50, 50))
+        s = None if rng.random() < 0.05 else "k%02d" % rng.integers(0, 40)
+        f = None if rng.random() < 0.05 else (float("nan") if rng.random() < 0.03 else float(rng.normal()))
+        rows.append((x, s, f, i))
+    df = spark.createDataFrame(rows, ["x", "s", "f", "i"])
+    for spec in [(("x", True), ("f", False)), (("s", False), ("x", True)), (("f", True),), (("x", False), ("s", True), ("f", True))]:
+        got = [tuple(r)[3] for r in df.orderBy(*[col(c).asc() if a else col(c).desc() for c, a in spec]).collect()]
+        want = list(range(n))
+        for c, a in reversed(spec):
+            j = ["x", "s", "f"].index(c)
+            nulls = [r for r in want if rows[r][j] is None]
+            vals = [r for r in want if rows[r][j] is not None]
+            vals.sort(key=lambda r: _py_sort_key(rows[r][j], True), reverse=not a)
+            if not a:  # reverse=True breaks stability among equal keys: restore input order within ties
+                groups = {}
+                for r in vals:
+                    groups.setdefault(_py_sort_key(rows[r][j], True), []).append(r)
+                vals = [r for kk in sorted(groups, reverse=True) for r in sorted(groups[kk], key=want.index)]
+            want = (nulls + vals) if a else (vals + nulls)
+        assert got == want, spec
+
+
+def test_shuffle_budget_and_tensor_control_plane(spark):
+    """Single process: shuffles degenerate to a local take; count/describe/agg run without any
+    pickled collective (the multi-rank variant is in test_distributed_cpu)."""
+    from pyspark_tf_gke_amd.parallel import comm
+
+    calls = []
+    orig = comm.all_gather_object
+    comm.all_gather_object = lambda o: calls.append(o) or orig(o)
+    try:
+        df = spark.createDataFrame([(i % 7, float(i)) for i in range(100)], ["k", "v"])
+        assert df.count() == 100
+        df.describe("v").collect()
+        df.agg(fsum("v")).collect()
+        df.orderBy("v").limit(3).collect()
+    finally:
+        comm.all_gather_object = orig
+    assert calls == []
