@@ -755,7 +755,7 @@ __global__ __launch_bounds__(256) void part_agg2_k(const long long* __restrict__
 //   range_partition_k  destination rank = #splitters below the key (sample-based range shuffle)
 // ================================================================================================
 #ifndef PTG_ST
-#define PTG_ST 2048
+#define PTG_ST 4096
 #endif
 #define ST PTG_ST        // rows per sort tile
 #define SB 256           // digit bins (8 bits per pass)

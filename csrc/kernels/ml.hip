@@ -46,110 +46,267 @@ __global__ __launch_bounds__(256) void assemble_fill_k(AsmDesc d, long n, int D,
   }
 }
 
-// X [n][D] fp32, C [k][D] fp32 (k*D <= 8192), sums [k][D] f32 (zeroed), counts [k] f32, cost double[1]
-#define KM_MAX 8192
-__global__ __launch_bounds__(256) void kmeans_assign_k(const float* __restrict__ X, const float* __restrict__ C, long n,
-                                                       int D, int k, int* __restrict__ assign, float* __restrict__ sums,
-                                                       float* __restrict__ counts, double* __restrict__ cost,
-                                                       const float* __restrict__ weights, float* __restrict__ mind) {
-  __shared__ float sc[KM_MAX];
-  __shared__ float ss[KM_MAX];
-  __shared__ float scnt[256];
+// ------------------------------------------------------------------------------------------------
+// K-means Lloyd step on the matrix cores.  argmin_c ||x - c||^2 = argmin_c (||c||^2 - 2 x.c): the
+// x.c products of a 64-row tile against every center are exact-f32 MFMA (v_mfma_f32_16x16x4_f32,
+// bit-for-bit an fmaf chain, cdna_hip_programming.md 'FP32-input MFMA'): each wave owns 16 rows,
+// the 4 waves share each 16-center block (B operand read straight from L1/L2, k*D floats), two
+// independent accumulators hide the 40-cycle MFMA latency.  The 16 candidate distances of a row
+// live on 16 lanes and are min-reduced with xor shuffles (ties -> lower center, as the scalar
+// loop).  Per-cluster sums/counts accumulate in LDS when k*D fits, else with global atomics;
+// zero features (one-hot blocks) are skipped either way.  No k or k*D limit; D <= KM_DMAX.
+// `done` (device flag) turns every launch of a converged fit into a no-op, so the host can queue
+// several iterations without reading the convergence test back (ml/clustering.py).
+// ------------------------------------------------------------------------------------------------
+#define KM_ROWS 64
+#define KM_DMAX 576
+typedef float km_f4 __attribute__((ext_vector_type(4)));
+
+template <bool ACC_LDS>
+__global__ __launch_bounds__(256) void kmeans_mfma_k(const float* __restrict__ X, long n, int D, int DP,
+                                                     const float* __restrict__ C, const float* __restrict__ cn, int k,
+                                                     int* __restrict__ assign, float* __restrict__ mind,
+                                                     float* __restrict__ sums, float* __restrict__ counts,
+                                                     double* __restrict__ cost, const float* __restrict__ weights,
+                                                     const int* __restrict__ done) {
+  if (done && *done) return;
+  extern __shared__ __align__(16) float km_lds[];
+  const int S = DP + 1;  // odd row stride: the 16 rows of an A fragment hit 16 different banks
+  float* xs = km_lds;                   // [KM_ROWS][S]
+  float* sacc = xs + KM_ROWS * S;       // [k][D] (ACC_LDS)
+  float* scnt = sacc + (ACC_LDS ? (long)k * D : 0);  // [k] (ACC_LDS)
+  __shared__ int sarg[KM_ROWS];
+  __shared__ float sw[KM_ROWS];
   __shared__ float scost[4];
-  const int kd = k * D;
-  for (int t = threadIdx.x; t < kd; t += 256) { sc[t] = C[t]; ss[t] = 0.f; }
-  if (threadIdx.x < k) scnt[threadIdx.x] = 0.f;
-  __syncthreads();
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, g = l >> 4, c16 = l & 15;
+  if (ACC_LDS && sums) {
+    for (long t = tid; t < (long)k * D; t += 256) sacc[t] = 0.f;
+    for (int t = tid; t < k; t += 256) scnt[t] = 0.f;
+  }
   double mycost = 0.0;
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
-    const float* x = X + i * (long)D;
-    float best = INFINITY; int arg = 0;
-    for (int c = 0; c < k; ++c) {
-      const float* cc = sc + c * D;
-      float dist = 0.f;
-      for (int j = 0; j < D; ++j) { const float df = x[j] - cc[j]; dist = fmaf(df, df, dist); }
-      if (dist < best) { best = dist; arg = c; }
+  const long ntile = (n + KM_ROWS - 1) / KM_ROWS;
+  for (long tile = blockIdx.x; tile < ntile; tile += gridDim.x) {
+    const long r0 = tile * KM_ROWS;
+    __syncthreads();
+    for (int t = tid; t < KM_ROWS * DP; t += 256) {
+      const int r = t / DP, d = t - r * DP;
+      xs[r * S + d] = (r0 + r < n && d < D) ? X[(r0 + r) * D + d] : 0.f;
     }
-    const float w = weights ? weights[i] : 1.f;
-    if (assign) assign[i] = arg;
-    if (mind) mind[i] = best;
-    mycost += (double)best * w;
-    if (sums) {
-      atomicAdd(&scnt[arg], w);
-      for (int j = 0; j < D; ++j) {
-        const float v = x[j];
-        if (v != 0.f) atomicAdd(&ss[arg * D + j], v * w);
+    __syncthreads();
+    const float* xa = xs + (16 * w + c16) * S + g;
+    float best[4] = {INFINITY, INFINITY, INFINITY, INFINITY};
+    int arg[4] = {0, 0, 0, 0};
+    for (int cb = 0; cb < k; cb += 16) {
+      const int col = cb + c16;
+      const bool cv = col < k;
+      const float* cp = C + (long)(cv ? col : 0) * D + g;
+      km_f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+      for (int d0 = 0; d0 < DP; d0 += 8) {
+        const float b0 = (cv && d0 + g < D) ? cp[d0] : 0.f;
+        const float b1 = (cv && d0 + 4 + g < D) ? cp[d0 + 4] : 0.f;
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[d0], b0, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[d0 + 4], b1, acc1, 0, 0, 0);
+      }
+      const float cc = cv ? cn[col] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {  // C/D map: row 4g+i, column c16
+        float v = cv ? cc - 2.f * (acc0[i] + acc1[i]) : INFINITY;
+        int a = col;
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          const float ov = __shfl_xor(v, o, 64);
+          const int oa = __shfl_xor(a, o, 64);
+          if (ov < v || (ov == v && oa < a)) { v = ov; a = oa; }
+        }
+        if (v < best[i]) { best[i] = v; arg[i] = a; }
+      }
+    }
+    // lanes with c16 < 4 finish row 4g + c16 of this wave
+    if (c16 < 4) {
+      const int r = 16 * w + 4 * g + c16;
+      float bsel = best[0];
+      int asel = arg[0];
+#pragma unroll
+      for (int i = 1; i < 4; ++i)
+        if (c16 == i) { bsel = best[i]; asel = arg[i]; }
+      const long row = r0 + r;
+      float wt = 0.f;
+      if (row < n) {
+        float xn = 0.f;
+        for (int d = 0; d < D; ++d) xn = fmaf(xs[r * S + d], xs[r * S + d], xn);
+        const float dist = fmaxf(xn + bsel, 0.f);
+        wt = weights ? weights[row] : 1.f;
+        if (assign) assign[row] = asel;
+        if (mind) mind[row] = dist;
+        mycost += (double)dist * wt;
+      }
+      sarg[r] = asel;
+      sw[r] = wt;
+    }
+    __syncthreads();
+    if (sums) {  // each wave adds its 16 rows: lanes stride over the features (coalesced)
+      for (int rr = 0; rr < 16; ++rr) {
+        const int r = 16 * w + rr;
+        const float wt = sw[r];
+        if (wt == 0.f) continue;
+        const int a = sarg[r];
+        for (int d = l; d < D; d += 64) {
+          const float v = xs[r * S + d] * wt;
+          if (v != 0.f) {
+            if (ACC_LDS) atomicAdd(&sacc[a * D + d], v);
+            else atomicAdd(&sums[(long)a * D + d], v);
+          }
+        }
+        if (l == 0) {
+          if (ACC_LDS) atomicAdd(&scnt[a], wt);
+          else atomicAdd(&counts[a], wt);
+        }
       }
     }
   }
   const float c32 = block_sum256((float)mycost, scost);
-  __syncthreads();
-  if (threadIdx.x == 0 && cost) atomicAdd(cost, (double)c32);
-  if (sums) {
-    for (int t = threadIdx.x; t < kd; t += 256)
-      if (ss[t] != 0.f) atomicAdd(&sums[t], ss[t]);
-    if (threadIdx.x < k && scnt[threadIdx.x] != 0.f) atomicAdd(&counts[threadIdx.x], scnt[threadIdx.x]);
+  if (tid == 0 && cost) atomicAdd(cost, (double)c32);
+  if (ACC_LDS && sums) {
+    __syncthreads();
+    for (long t = tid; t < (long)k * D; t += 256)
+      if (sacc[t] != 0.f) atomicAdd(&sums[t], sacc[t]);
+    for (int t = tid; t < k; t += 256)
+      if (scnt[t] != 0.f) atomicAdd(&counts[t], scnt[t]);
   }
 }
 
-// new centers; moved[0] = max squared center shift (for Spark's tol convergence check)
-__global__ __launch_bounds__(256) void kmeans_update_k(const float* __restrict__ sums, const float* __restrict__ counts,
-                                                       float* __restrict__ C, int k, int D, float* __restrict__ moved) {
-  __shared__ float shift[256];
+// new centers + their squared norms; moved[0] = max squared center shift (Spark's tol test);
+// sums/counts are re-zeroed for the next iteration once read.
+__global__ __launch_bounds__(256) void kmeans_update_k(float* __restrict__ sums, float* __restrict__ counts,
+                                                       float* __restrict__ C, float* __restrict__ cn, int k, int D,
+                                                       float* __restrict__ moved, const int* __restrict__ done) {
+  if (done && *done) return;
+  __shared__ float sh[2][256];
   const int c = blockIdx.x;
-  float s2 = 0.f;
+  float s2 = 0.f, nn = 0.f;
   const float cnt = counts[c];
   for (int j = threadIdx.x; j < D; j += 256) {
-    const float old = C[c * D + j];
-    const float nw = cnt > 0.f ? sums[c * D + j] / cnt : old;
-    C[c * D + j] = nw;
+    const float old = C[(long)c * D + j];
+    const float nw = cnt > 0.f ? sums[(long)c * D + j] / cnt : old;
+    C[(long)c * D + j] = nw;
+    sums[(long)c * D + j] = 0.f;
     s2 += (nw - old) * (nw - old);
+    nn = fmaf(nw, nw, nn);
   }
-  shift[threadIdx.x] = s2;
+  sh[0][threadIdx.x] = s2;
+  sh[1][threadIdx.x] = nn;
   __syncthreads();
   for (int o = 128; o > 0; o >>= 1) {
-    if (threadIdx.x < o) shift[threadIdx.x] += shift[threadIdx.x + o];
+    if (threadIdx.x < o) { sh[0][threadIdx.x] += sh[0][threadIdx.x + o]; sh[1][threadIdx.x] += sh[1][threadIdx.x + o]; }
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    unsigned int* m = (unsigned int*)moved;  // non-negative floats order as unsigned ints
-    atomicMax(m, __float_as_uint(shift[0]));
+    atomicMax((unsigned int*)moved, __float_as_uint(sh[0][0]));  // non-negative floats order as uints
+    if (cn) cn[c] = sh[1][0];
+    counts[c] = 0.f;
   }
 }
 
-// per-point silhouette, summed: S [k][D] cluster sums, Q[k] sum of squared norms, cnt[k]
-__global__ __launch_bounds__(256) void silhouette_k(const float* __restrict__ X, const int* __restrict__ assign,
-                                                    const float* __restrict__ S, const float* __restrict__ Q,
-                                                    const float* __restrict__ cnt, long n, int D, int k,
-                                                    double* __restrict__ out) {
-  __shared__ float sS[KM_MAX];
-  __shared__ float sQ[256], sN[256];
+// convergence test on the device: state[0] = done, state[1] = iterations run
+__global__ void kmeans_check_k(float* __restrict__ moved, float tol2, int* __restrict__ state) {
+  if (threadIdx.x != 0 || blockIdx.x != 0 || state[0]) return;
+  state[1] += 1;
+  if (*moved <= tol2) state[0] = 1;
+  *moved = 0.f;
+}
+
+__global__ __launch_bounds__(256) void center_norms_k(const float* __restrict__ C, int k, int D, float* __restrict__ cn) {
+  for (int c = blockIdx.x * 256 + threadIdx.x; c < k; c += gridDim.x * 256) {
+    float nn = 0.f;
+    for (int j = 0; j < D; ++j) nn = fmaf(C[(long)c * D + j], C[(long)c * D + j], nn);
+    cn[c] = nn;
+  }
+}
+
+// Silhouette (Spark ClusteringEvaluator, squared Euclidean) summed over points, on the matrix cores:
+// sum_j ||x - x_j||^2 over cluster c = n_c ||x||^2 - 2 x.S_c + Q_c, so every point needs x.S_c for
+// all clusters — the same MFMA tile product as kmeans_mfma_k with the centers replaced by the
+// cluster sum vectors S.  a = own-cluster mean distance, b = min over the other non-empty clusters.
+__global__ __launch_bounds__(256) void silhouette_mfma_k(const float* __restrict__ X, const int* __restrict__ assign,
+                                                         const float* __restrict__ Sv, const float* __restrict__ Q,
+                                                         const float* __restrict__ cnt, long n, int D, int DP, int k,
+                                                         double* __restrict__ out) {
+  extern __shared__ __align__(16) float km_lds[];
+  const int S = DP + 1;
+  float* xs = km_lds;
+  __shared__ float sxn[KM_ROWS];
   __shared__ float scr[4];
-  for (int t = threadIdx.x; t < k * D; t += 256) sS[t] = S[t];
-  if (threadIdx.x < k) { sQ[threadIdx.x] = Q[threadIdx.x]; sN[threadIdx.x] = cnt[threadIdx.x]; }
-  __syncthreads();
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, g = l >> 4, c16 = l & 15;
   double acc = 0.0;
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
-    const float* x = X + i * (long)D;
-    float xn = 0.f;
-    for (int j = 0; j < D; ++j) xn = fmaf(x[j], x[j], xn);
-    const int own = assign[i];
-    float a = 0.f, b = INFINITY;
-    for (int c = 0; c < k; ++c) {
-      const float nc = sN[c];
-      if (nc <= 0.f) continue;
-      float dot = 0.f;
-      for (int j = 0; j < D; ++j) dot = fmaf(x[j], sS[c * D + j], dot);
-      const float total = nc * xn - 2.f * dot + sQ[c];  // sum_j ||x - x_j||^2 over cluster c
-      if (c == own) a = nc > 1.f ? total / (nc - 1.f) : 0.f;
-      else b = fminf(b, total / nc);
+  const long ntile = (n + KM_ROWS - 1) / KM_ROWS;
+  for (long tile = blockIdx.x; tile < ntile; tile += gridDim.x) {
+    const long r0 = tile * KM_ROWS;
+    __syncthreads();
+    for (int t = tid; t < KM_ROWS * DP; t += 256) {
+      const int r = t / DP, d = t - r * DP;
+      xs[r * S + d] = (r0 + r < n && d < D) ? X[(r0 + r) * D + d] : 0.f;
     }
-    float s = 0.f;
-    if (sN[own] > 1.f && b < INFINITY) {
-      const float m = fmaxf(a, b);
-      s = m > 0.f ? (b - a) / m : 0.f;
+    __syncthreads();
+    if (tid < KM_ROWS) {
+      float xn = 0.f;
+      for (int d = 0; d < D; ++d) xn = fmaf(xs[tid * S + d], xs[tid * S + d], xn);
+      sxn[tid] = xn;
     }
-    acc += s;
+    __syncthreads();
+    const float* xa = xs + (16 * w + c16) * S + g;
+    float xn[4], a_own[4], bmin[4];
+    int own[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = 16 * w + 4 * g + i;
+      xn[i] = sxn[r];
+      own[i] = r0 + r < n ? assign[r0 + r] : -1;
+      a_own[i] = 0.f;
+      bmin[i] = INFINITY;
+    }
+    for (int cb = 0; cb < k; cb += 16) {
+      const int col = cb + c16;
+      const bool cv = col < k;
+      const float* sp = Sv + (long)(cv ? col : 0) * D + g;
+      km_f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+      for (int d0 = 0; d0 < DP; d0 += 8) {
+        const float b0 = (cv && d0 + g < D) ? sp[d0] : 0.f;
+        const float b1 = (cv && d0 + 4 + g < D) ? sp[d0 + 4] : 0.f;
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[d0], b0, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[d0 + 4], b1, acc1, 0, 0, 0);
+      }
+      const float nc = cv ? cnt[col] : 0.f;
+      const float qc = cv ? Q[col] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float total = nc * xn[i] - 2.f * (acc0[i] + acc1[i]) + qc;
+        float v = INFINITY;
+        if (cv && nc > 0.f) {
+          if (col == own[i]) a_own[i] = nc > 1.f ? total / (nc - 1.f) : 0.f;
+          else v = total / nc;
+        }
+        // the own-cluster term lives on one lane: broadcast it with a max over the 16 lanes
+        float ao = (cv && col == own[i]) ? a_own[i] : -INFINITY;
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          v = fminf(v, __shfl_xor(v, o, 64));
+          ao = fmaxf(ao, __shfl_xor(ao, o, 64));
+        }
+        bmin[i] = fminf(bmin[i], v);
+        if (ao != -INFINITY) a_own[i] = ao;
+      }
+    }
+    if (c16 < 4) {
+      float a = a_own[0], b = bmin[0];
+      int o = own[0];
+#pragma unroll
+      for (int i = 1; i < 4; ++i)
+        if (c16 == i) { a = a_own[i]; b = bmin[i]; o = own[i]; }
+      if (o >= 0 && cnt[o] > 1.f && b < INFINITY) {
+        const float m = fmaxf(a, b);
+        acc += m > 0.f ? (double)((b - a) / m) : 0.0;
+      }
+    }
   }
   const float r = block_sum256((float)acc, scr);
   if (threadIdx.x == 0) atomicAdd(out, (double)r);
@@ -191,17 +348,51 @@ int ptg_assemble_features(const void* desc, long n, int D, void* out, hipStream_
   PTG_RETURN_LAUNCH();
 }
 
-int ptg_kmeans_assign_accum(const void* X, const void* C, long n, int D, int k, void* assign, void* sums, void* counts,
-                            void* cost, const void* weights, void* mind, hipStream_t s) {
-  if ((long)k * D > KM_MAX || k > 256) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(kmeans_assign_k, dim3(grid_m(n)), dim3(256), 0, s, (const float*)X, (const float*)C, n, D, k,
-                     (int*)assign, (float*)sums, (float*)counts, (double*)cost, (const float*)weights, (float*)mind);
+// cn: k squared center norms (ptg_center_norms); done: optional device flag (skip when set)
+int ptg_kmeans_assign_accum(const void* X, const void* C, const void* cn, long n, int D, int k, void* assign,
+                            void* sums, void* counts, void* cost, const void* weights, void* mind, const void* done,
+                            hipStream_t s) {
+  if (D > KM_DMAX || D <= 0 || k <= 0) return (int)hipErrorInvalidValue;
+  const int DP = (D + 7) / 8 * 8;
+  const long xs_bytes = (long)KM_ROWS * (DP + 1) * 4;
+  const long acc_bytes = ((long)k * D + k) * 4;
+  const bool acc_lds = sums != nullptr && xs_bytes + acc_bytes <= 150 * 1024;
+  const size_t lds = (size_t)(xs_bytes + (acc_lds ? acc_bytes : 0));
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)kmeans_mfma_k<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+    (void)hipFuncSetAttribute((const void*)kmeans_mfma_k<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+    attr = true;
+  }
+  long tiles = (n + KM_ROWS - 1) / KM_ROWS;
+  // LDS accumulation amortises its k*D flush over many tiles: fewer, longer-lived workgroups
+  const long cap = acc_lds ? 512 : 4096;
+  const int g = (int)(tiles < 1 ? 1 : (tiles > cap ? cap : tiles));
+  if (acc_lds)
+    hipLaunchKernelGGL(kmeans_mfma_k<true>, dim3(g), dim3(256), lds, s, (const float*)X, n, D, DP, (const float*)C,
+                       (const float*)cn, k, (int*)assign, (float*)mind, (float*)sums, (float*)counts, (double*)cost,
+                       (const float*)weights, (const int*)done);
+  else
+    hipLaunchKernelGGL(kmeans_mfma_k<false>, dim3(g), dim3(256), lds, s, (const float*)X, n, D, DP, (const float*)C,
+                       (const float*)cn, k, (int*)assign, (float*)mind, (float*)sums, (float*)counts, (double*)cost,
+                       (const float*)weights, (const int*)done);
   PTG_RETURN_LAUNCH();
 }
 
-int ptg_kmeans_update(const void* sums, const void* counts, void* C, int k, int D, void* moved, hipStream_t s) {
-  hipLaunchKernelGGL(kmeans_update_k, dim3(k), dim3(256), 0, s, (const float*)sums, (const float*)counts, (float*)C, k,
-                     D, (float*)moved);
+int ptg_center_norms(const void* C, int k, int D, void* cn, hipStream_t s) {
+  hipLaunchKernelGGL(center_norms_k, dim3((k + 255) / 256), dim3(256), 0, s, (const float*)C, k, D, (float*)cn);
+  PTG_RETURN_LAUNCH();
+}
+
+int ptg_kmeans_update(void* sums, void* counts, void* C, void* cn, int k, int D, void* moved, const void* done,
+                      hipStream_t s) {
+  hipLaunchKernelGGL(kmeans_update_k, dim3(k), dim3(256), 0, s, (float*)sums, (float*)counts, (float*)C, (float*)cn, k,
+                     D, (float*)moved, (const int*)done);
+  PTG_RETURN_LAUNCH();
+}
+
+int ptg_kmeans_check(void* moved, float tol2, void* state, hipStream_t s) {
+  hipLaunchKernelGGL(kmeans_check_k, dim3(1), dim3(64), 0, s, (float*)moved, tol2, (int*)state);
   PTG_RETURN_LAUNCH();
 }
 
@@ -213,9 +404,18 @@ int ptg_cluster_stats(const void* X, const void* assign, long n, int D, void* S,
 
 int ptg_silhouette(const void* X, const void* assign, const void* S, const void* Q, const void* cnt, long n, int D,
                    int k, void* out, hipStream_t s) {
-  if ((long)k * D > KM_MAX || k > 256) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(silhouette_k, dim3(grid_m(n)), dim3(256), 0, s, (const float*)X, (const int*)assign,
-                     (const float*)S, (const float*)Q, (const float*)cnt, n, D, k, (double*)out);
+  if (D > KM_DMAX || D <= 0 || k <= 0) return (int)hipErrorInvalidValue;
+  const int DP = (D + 7) / 8 * 8;
+  const size_t lds = (size_t)KM_ROWS * (DP + 1) * 4;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)silhouette_mfma_k, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+    attr = true;
+  }
+  long tiles = (n + KM_ROWS - 1) / KM_ROWS;
+  const int g = (int)(tiles < 1 ? 1 : (tiles > 4096 ? 4096 : tiles));
+  hipLaunchKernelGGL(silhouette_mfma_k, dim3(g), dim3(256), lds, s, (const float*)X, (const int*)assign,
+                     (const float*)S, (const float*)Q, (const float*)cnt, n, D, DP, k, (double*)out);
   PTG_RETURN_LAUNCH();
 }
 

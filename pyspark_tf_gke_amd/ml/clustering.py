@@ -2,10 +2,12 @@
 
 The feature matrix stays resident on the GPU for the whole fit (the reference re-runs its JDBC
 scan + pipeline every Lloyd iteration because nothing is cached).  Each iteration is
-ONE fused assign+accumulate kernel (centers in LDS, per-workgroup partial sums in LDS) plus a
-k x D center update; across ranks the (k*D + k) partial sums and the cost are all-reduced (the
-role of Spark's treeAggregate + broadcast, M6/M7).  Convergence follows Spark: stop when every
-center moved less than ``tol`` (squared distance <= tol^2) or after ``maxIter``.
+ONE fused assign+accumulate kernel (x.c products of 64-row tiles on the f32 matrix cores,
+per-workgroup partial sums in LDS) plus a k x D center update; across ranks the (k*D + k) partial
+sums are all-reduced as one tensor (the role of Spark's treeAggregate + broadcast, M6/M7).
+Convergence follows Spark (every center moved less than ``tol``, i.e. squared shift <= tol^2, or
+``maxIter``) and is tested ON THE DEVICE: a converged fit turns the remaining queued launches into
+no-ops, and the host reads the flag back once per batch of iterations, not once per iteration.
 
 Initialisation: ``k-means||`` (Spark's default, initSteps=2): uniform first center, then
 ``initSteps`` rounds sampling each point with probability min(1, 2k d^2(x)/cost), candidates
@@ -28,10 +30,13 @@ from .base import Estimator, MLReadable, MLWritable, Model, read_data, write_dat
 from .linalg import DenseVector
 
 
-def _allreduce_np(a: np.ndarray) -> np.ndarray:
-    if comm.world_size() == 1:
-        return a
-    return np.sum(comm.all_gather_object(a), axis=0)
+_ITER_BATCH = 4  # Lloyd iterations queued between two reads of the device convergence flag
+
+
+def _gather_rows_all(t: torch.Tensor, Dm: int) -> np.ndarray:
+    """Every rank's rows of a [m, Dm] float tensor, in rank order (one tensor all-gather)."""
+    parts = comm.all_gather_v(t.contiguous()) if comm.world_size() > 1 else [t]
+    return np.concatenate([p.cpu().numpy().reshape(-1, Dm) for p in parts]).astype(np.float32)
 
 
 class KMeans(Estimator, MLWritable, MLReadable):
@@ -55,26 +60,22 @@ class KMeans(Estimator, MLWritable, MLReadable):
         n, Dm = X.shape
         dev = X.device
         if self.getOrDefault("initMode") == "random":
-            loc = X[torch.from_numpy(rng.choice(n, size=min(k, n), replace=False)).to(dev)].cpu().numpy() if n else np.zeros((0, Dm))
-            allc = np.concatenate(comm.all_gather_object(loc)) if comm.world_size() > 1 else loc
+            loc = X[torch.from_numpy(rng.choice(n, size=min(k, n), replace=False)).to(dev)] if n else X[:0]
+            allc = _gather_rows_all(loc, Dm)
             return torch.from_numpy(allc[rng.choice(len(allc), size=k, replace=len(allc) < k)]).float().to(dev)
         # ---- k-means|| (distributed)
-        counts = comm.all_gather_object(n) if comm.world_size() > 1 else [n]
+        counts = comm.all_gather_int(n)
         total = sum(counts)
         first = int(rng.integers(total))
         owner = int(np.searchsorted(np.cumsum(counts), first, side="right"))
         local_first = first - int(sum(counts[:owner]))
-        c0 = X[local_first].cpu().numpy() if comm.rank() == owner else None
-        if comm.world_size() > 1:
-            c0 = next(c for c in comm.all_gather_object(c0) if c is not None)
-        cands = [np.asarray(c0, dtype=np.float32)]
+        c0 = X[local_first:local_first + 1] if comm.rank() == owner else X[:0]
+        cands = list(_gather_rows_all(c0, Dm))
         mind = torch.empty(n, dtype=torch.float32, device=dev)
         for step in range(int(self.getOrDefault("initSteps"))):
             C = torch.from_numpy(np.stack(cands)).float().to(dev)
-            if C.shape[0] * Dm > 8192:
-                C = C[: max(1, 8192 // Dm)]
             D.kmeans_assign_accum(X, C, mind=mind)
-            cost = float(_allreduce_np(np.array([float(mind.double().sum())]))[0])
+            cost = comm.all_reduce_float([float(mind.double().sum())])[0]
             if cost <= 0:
                 break
             g = torch.Generator(device="cpu")
@@ -82,27 +83,14 @@ class KMeans(Estimator, MLWritable, MLReadable):
             u = torch.rand(n, generator=g).to(dev)
             pick = (u < (2.0 * k * mind / cost)).to(torch.uint8)
             idx = D.compact(pick)
-            new = X[idx].cpu().numpy() if idx.numel() else np.zeros((0, Dm), np.float32)
-            if comm.world_size() > 1:
-                new = np.concatenate(comm.all_gather_object(new))
-            cands += list(new)
+            cands += list(_gather_rows_all(X[idx], Dm))
         C = np.stack(cands).astype(np.float32)
-        # weights: number of points closest to each candidate
-        w = np.zeros(len(C))
-        for s0 in range(0, len(C), max(1, 8192 // Dm)):
-            pass
+        # weights: number of points closest to each candidate (one fused assignment, any count)
         Ct = torch.from_numpy(C).to(dev)
         assign = torch.empty(n, dtype=torch.int32, device=dev)
-        chunk = max(1, min(256, 8192 // Dm))
-        best = torch.full((n,), math.inf, dtype=torch.float32, device=dev)
-        barg = torch.zeros(n, dtype=torch.int64, device=dev)
-        for s0 in range(0, len(C), chunk):
-            D.kmeans_assign_accum(X, Ct[s0:s0 + chunk].contiguous(), assign=assign, mind=mind)
-            better = mind < best
-            best = torch.where(better, mind, best)
-            barg = torch.where(better, assign.long() + s0, barg)
-        w = np.bincount(barg.cpu().numpy(), minlength=len(C)).astype(np.float64)
-        w = _allreduce_np(w)
+        D.kmeans_assign_accum(X, Ct, assign=assign)
+        w = torch.bincount(assign.long(), minlength=len(C)).double()
+        w = comm.all_reduce_tensor_(w).cpu().numpy()
         return torch.from_numpy(_weighted_kmeanspp(C.astype(np.float64), w, k, rng)).float().to(dev)
 
     def _fit(self, df: DataFrame):
@@ -119,26 +107,31 @@ class KMeans(Estimator, MLWritable, MLReadable):
         counts = torch.zeros(k, dtype=torch.float32, device=dev)
         cost = torch.zeros(1, dtype=torch.float64, device=dev)
         moved = torch.zeros(1, dtype=torch.float32, device=dev)
+        state = torch.zeros(2, dtype=torch.int32, device=dev)  # [done, iterations]
+        cn = D.center_norms(C)
         tol = float(self.getOrDefault("tol"))
         max_iter = int(self.getOrDefault("maxIter"))
-        it = 0
-        for it in range(1, max_iter + 1):
-            sums.zero_(); counts.zero_(); cost.zero_(); moved.zero_()
-            D.kmeans_assign_accum(X, C, sums=sums, counts=counts, cost=cost)
-            if comm.world_size() > 1:
-                buf = torch.cat([sums.view(-1), counts]).contiguous()
-                comm.all_reduce_(buf)
-                sums.copy_(buf[: k * Dm].view(k, Dm)); counts.copy_(buf[k * Dm:])
-            D.kmeans_update(sums, counts, C, moved)
-            if float(moved.item()) <= tol * tol:
+        launched = 0
+        while launched < max_iter:
+            for _ in range(min(_ITER_BATCH, max_iter - launched)):
+                D.kmeans_assign_accum(X, C, sums=sums, counts=counts, cn=cn, done=state)
+                if comm.world_size() > 1:
+                    # sums || counts all-reduced as one tensor (a converged fit reduces zeros: every
+                    # rank holds the same flag, so the collective sequence stays identical)
+                    buf = torch.cat([sums.view(-1), counts]).contiguous()
+                    comm.all_reduce_(buf)
+                    sums.copy_(buf[: k * Dm].view(k, Dm)); counts.copy_(buf[k * Dm:])
+                D.kmeans_update(sums, counts, C, moved, cn=cn, done=state)
+                D.kmeans_check(moved, tol * tol, state)
+                launched += 1
+            if int(state[0].item()):
                 break
+        it = int(state[1].item())
         assign = torch.empty(n, dtype=torch.int32, device=dev)
-        cost.zero_()
-        counts.zero_()
-        sums.zero_()
-        D.kmeans_assign_accum(X, C, assign=assign, sums=sums, counts=counts, cost=cost)
-        sizes = _allreduce_np(counts.cpu().numpy().astype(np.float64))
-        tcost = float(_allreduce_np(cost.cpu().numpy())[0])
+        sums.zero_(); counts.zero_(); cost.zero_()
+        D.kmeans_assign_accum(X, C, assign=assign, sums=sums, counts=counts, cost=cost, cn=cn)
+        sizes = comm.all_reduce_tensor_(counts.double()).cpu().numpy()
+        tcost = float(comm.all_reduce_tensor_(cost.clone()).item())
         model = KMeansModel(C.cpu().numpy().astype(np.float64))
         model._params.update(self._params)
         model.summary = KMeansSummary(k, it, tcost, [int(s) for s in sizes])
@@ -230,7 +223,7 @@ class KMeansModel(Model, MLWritable, MLReadable):
         C = torch.from_numpy(self._centers).float().to(X.device)
         cost = torch.zeros(1, dtype=torch.float64, device=X.device)
         D.kmeans_assign_accum(X, C, cost=cost)
-        return float(_allreduce_np(cost.cpu().numpy())[0])
+        return float(comm.all_reduce_tensor_(cost).item())
 
     def _save_impl(self, path):
         write_metadata(self, path)

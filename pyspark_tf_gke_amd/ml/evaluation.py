@@ -4,6 +4,8 @@ accumulated on the device and all-reduced, then each point's a/b terms are dot p
 the k cluster sums (one kernel), and the mean is reduced across ranks."""
 from __future__ import annotations
 
+import torch
+
 import numpy as np
 
 from ..ops import df as D
@@ -27,20 +29,16 @@ class ClusteringEvaluator(Params):
         X = t.column(self.getOrDefault("featuresCol")).data.float().contiguous()
         a = t.column(self.getOrDefault("predictionCol")).data.int().contiguous()
         k_loc = int(a.max().item()) + 1 if a.numel() else 0
-        k = max(comm.all_gather_object(k_loc)) if comm.world_size() > 1 else k_loc
+        k = comm.all_reduce_int([k_loc], op=torch.distributed.ReduceOp.MAX)[0]
         S, Q, cnt = D.silhouette_sum(X, a, k)
         if comm.world_size() > 1:
-            import torch
-
             buf = torch.cat([S.view(-1), Q, cnt]).contiguous()
             comm.all_reduce_(buf)
             kd = S.numel()
             S.copy_(buf[:kd].view_as(S)); Q.copy_(buf[kd:kd + k]); cnt.copy_(buf[kd + k:])
         total = D.silhouette_points(X, a, S, Q, cnt)
         n = X.shape[0]
-        if comm.world_size() > 1:
-            parts = comm.all_gather_object((total, n))
-            total, n = sum(p[0] for p in parts), sum(p[1] for p in parts)
+        total, n = comm.all_reduce_float([total, n])
         return float(total / n) if n else float("nan")
 
     def isLargerBetter(self) -> bool:  # noqa: N802

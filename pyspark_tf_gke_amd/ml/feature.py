@@ -29,8 +29,7 @@ from .base import Estimator, MLReadable, MLWritable, Model, Transformer, read_da
 def _all_reduce_counts(counts: torch.Tensor) -> torch.Tensor:
     if comm.world_size() == 1:
         return counts
-    parts = comm.all_gather_object(counts.cpu().numpy())
-    return torch.from_numpy(np.sum(parts, axis=0))
+    return comm.all_reduce_tensor_(counts.clone())
 
 
 class StringIndexer(Estimator, MLWritable, MLReadable):
@@ -147,8 +146,7 @@ class OneHotEncoder(Estimator, MLWritable, MLReadable):
             size = attr["num_vals"]
         else:
             _, c, _, mx, _ = D.reduce_stats(cv.data, cv.valid_u8())
-            if comm.world_size() > 1:
-                mx = max(comm.all_gather_object(mx))
+            mx = comm.all_reduce_float([mx], op=torch.distributed.ReduceOp.MAX)[0]
             size = int(mx) + 1 if c else 0
         m = OneHotEncoderModel(categorySizes=[size])
         m._params.update(self._params)

@@ -562,10 +562,27 @@ def assemble_features(segments, n: int, D: int, device):
     return out
 
 
-def kmeans_assign_accum(X, C, assign=None, sums=None, counts=None, cost=None, weights=None, mind=None):
+def center_norms(C: torch.Tensor) -> torch.Tensor:
+    k, Dm = C.shape
+    if not on_device(C):
+        return (C.double() ** 2).sum(1).float()
+    cn = torch.empty(k, dtype=torch.float32, device=C.device)
+    hip("ptg_center_norms", ptr(C), k, Dm, ptr(cn))
+    return cn
+
+
+KMEANS_DMAX = 576  # KM_DMAX in ml.hip (feature tile of 64 rows staged in LDS)
+
+
+def kmeans_assign_accum(X, C, assign=None, sums=None, counts=None, cost=None, weights=None, mind=None, cn=None,
+                        done=None):
+    """Fused k-means assignment: argmin_c ||x - c||^2 per row (-> assign, mind) and per-cluster
+    sums / counts / cost accumulation.  ``done``: device flag that makes the launch a no-op."""
     n, D = X.shape
     k = C.shape[0]
-    if not on_device(X):
+    if not on_device(X) or D > KMEANS_DMAX:
+        if on_device(X) and done is not None and int(done.item()):
+            return
         Xd, Cd = X.double(), C.double()
         d = (Xd * Xd).sum(1)[:, None] - 2 * Xd @ Cd.t() + (Cd * Cd).sum(1)[None, :]
         d = d.clamp_min(0)
@@ -574,25 +591,45 @@ def kmeans_assign_accum(X, C, assign=None, sums=None, counts=None, cost=None, we
             assign.copy_(arg.to(assign.dtype))
         if mind is not None:
             mind.copy_(best.to(mind.dtype))
-        w = torch.ones(n, dtype=torch.float64) if weights is None else weights.double()
+        w = torch.ones(n, dtype=torch.float64, device=X.device) if weights is None else weights.double()
         if sums is not None:
             sums.index_add_(0, arg, (X.double() * w[:, None]).to(sums.dtype))
             counts.index_add_(0, arg, w.to(counts.dtype))
         if cost is not None:
             cost += (best * w).sum().to(cost.dtype)
         return
-    hip("ptg_kmeans_assign_accum", ptr(X), ptr(C), n, D, k, ptr(assign), ptr(sums), ptr(counts), ptr(cost), ptr(weights),
-        ptr(mind))
+    if cn is None:
+        cn = center_norms(C)
+    hip("ptg_kmeans_assign_accum", ptr(X), ptr(C), ptr(cn), n, D, k, ptr(assign), ptr(sums), ptr(counts), ptr(cost),
+        ptr(weights), ptr(mind), ptr(done))
 
 
-def kmeans_update(sums, counts, C, moved):
+def kmeans_update(sums, counts, C, moved, cn=None, done=None):
+    """C = sums / counts (empty clusters keep their center); moved = max squared shift; sums and
+    counts are zeroed for the next iteration (device); cn = new squared center norms."""
     k, D = C.shape
     if not on_device(C):
         newc = torch.where(counts[:, None] > 0, sums / counts.clamp_min(1e-30)[:, None], C)
         moved.fill_(float(((newc - C) ** 2).sum(1).max()))
         C.copy_(newc)
+        if cn is not None:
+            cn.copy_(center_norms(C))
+        sums.zero_()
+        counts.zero_()
         return
-    hip("ptg_kmeans_update", ptr(sums), ptr(counts), ptr(C), k, D, ptr(moved))
+    hip("ptg_kmeans_update", ptr(sums), ptr(counts), ptr(C), ptr(cn), k, D, ptr(moved), ptr(done))
+
+
+def kmeans_check(moved, tol2: float, state):
+    """state[0] = done (moved <= tol2), state[1] += 1; moved reset — on the device, no readback."""
+    if not on_device(moved):
+        if not int(state[0]):
+            state[1] += 1
+            if float(moved[0]) <= tol2:
+                state[0] = 1
+        moved.zero_()
+        return
+    hip("ptg_kmeans_check", ptr(moved), float(tol2), ptr(state))
 
 
 def silhouette_sum(X, assign, k: int):
@@ -629,6 +666,8 @@ def silhouette_points(X, assign, S, Q, cnt) -> float:
         m = torch.maximum(a, b)
         s = torch.where((own_n > 1) & torch.isfinite(b) & (m > 0), (b - a) / m, torch.zeros_like(a))
         return float(s.sum())
+    if D > KMEANS_DMAX:
+        return silhouette_points(X.cpu(), assign.cpu(), S.cpu(), Q.cpu(), cnt.cpu())
     out = torch.zeros(1, dtype=torch.float64, device=X.device)
     hip("ptg_silhouette", ptr(X), ptr(assign), ptr(S), ptr(Q), ptr(cnt), n, D, k, ptr(out))
     return float(out.item())

@@ -256,3 +256,81 @@ def test_dataframe_orderby_gpu_vs_host(spark_gpu):
         return [tuple(r) for r in o.select("state_name", "value", "measure_name").collect()]
 
     assert run(spark_gpu) == _host(run)
+
+
+@pytest.mark.parametrize("n,k,Dm", [(20_000, 100, 153), (7_777, 5, 3), (30_000, 300, 300), (5_000, 40, 600)])
+def test_kmeans_mfma_assign_matches_host(hip_built, n, k, Dm):
+    """Fused MFMA assignment vs the fp64 host formula: same argmin wherever the best two centers
+    are not within f32 rounding, sums/counts/cost to f32 accuracy.  (300 x 300 exceeds the LDS
+    accumulator -> global-atomic path; D = 600 > KM_DMAX -> device fallback.)"""
+    g = torch.Generator().manual_seed(k)
+    X = torch.randn(n, Dm, generator=g)
+    X[:, : Dm // 3] = (X[:, : Dm // 3] > 1.0).float()  # one-hot-like sparse block (skipped zeros)
+    C = X[torch.randperm(n, generator=g)[:k]].clone() + 0.01 * torch.randn(k, Dm, generator=g)
+    out = {}
+    for dev in ("cuda", "cpu"):
+        Xd, Cd = X.to(dev), C.to(dev)
+        a = torch.empty(n, dtype=torch.int32, device=dev)
+        md = torch.empty(n, dtype=torch.float32, device=dev)
+        s = torch.zeros(k, Dm, dtype=torch.float32, device=dev)
+        c = torch.zeros(k, dtype=torch.float32, device=dev)
+        cost = torch.zeros(1, dtype=torch.float64, device=dev)
+        D.kmeans_assign_accum(Xd, Cd, assign=a, sums=s, counts=c, cost=cost, mind=md)
+        out[dev] = [t.cpu() for t in (a, md, s, c, cost)]
+    ag, mg, sg, cg, costg = out["cuda"]
+    ah, mh, sh, ch, costh = out["cpu"]
+    d = ((X.double()[:, None, :] - C.double()[None]) ** 2).sum(2) if n * k * Dm < 4e8 else None
+    if d is not None:
+        top2 = torch.topk(d, 2, dim=1, largest=False).values
+        clear = (top2[:, 1] - top2[:, 0]) > 1e-4 * top2[:, 1].clamp_min(1.0)
+        assert torch.equal(ag[clear], ah[clear])
+    assert (ag == ah).float().mean() > 0.999
+    assert torch.allclose(mg, mh, rtol=1e-4, atol=1e-3)
+    if bool((ag == ah).all()):
+        assert torch.equal(cg, ch)
+        assert torch.allclose(sg, sh, rtol=1e-4, atol=1e-3)
+    assert abs(float(costg) - float(costh)) <= 1e-5 * abs(float(costh))
+
+
+def test_kmeans_fit_k100_d153_vs_host_and_sklearn(spark_gpu):
+    """KMeans.fit with k=100 on 153-dim features (the reference's one-hot x5 + 3 numeric shape):
+    device convergence loop vs the host executor (same seed -> same random init), and one more
+    scikit-learn Lloyd step from our centers finds (almost) nothing left to improve."""
+    from sklearn.cluster import KMeans as SKM
+
+    from pyspark_tf_gke_amd.ml import KMeans
+    from pyspark_tf_gke_amd.sql.table import ColumnVector, Table
+    from pyspark_tf_gke_amd.sql import types as T
+    from pyspark_tf_gke_amd.sql.dataframe import DataFrame
+
+    g = torch.Generator().manual_seed(5)
+    n, Dm = 12_000, 153
+    codes = torch.randint(0, 30, (n,), generator=g)
+    X = torch.zeros(n, Dm)
+    for r in range(5):
+        X[torch.arange(n), r * 30 + codes] = 1.0
+    X[:, 150:] = torch.randn(n, 3, generator=g) * 3 + codes[:, None].float()
+
+    def fit(dev):
+        df = DataFrame(Table({"features": ColumnVector(X.to(dev), T.VectorUDT())}, n, dev), spark_gpu)
+        return KMeans(k=100, seed=3, maxIter=30, initMode="random").fit(df)
+
+    mg, mh = fit("cuda"), fit("cpu")
+    assert abs(mg.summary.trainingCost - mh.summary.trainingCost) <= 1e-3 * mh.summary.trainingCost
+    sk = SKM(n_clusters=100, init=np.asarray(mg.clusterCenters()), n_init=1, max_iter=1).fit(X.numpy().astype(np.float64))
+    assert mg.summary.trainingCost <= sk.inertia_ * 1.01
+    assert sum(mg.summary.clusterSizes) == n
+
+
+def test_silhouette_mfma_matches_host(hip_built):
+    n, k, Dm = 9_000, 37, 153
+    g = torch.Generator().manual_seed(1)
+    X = torch.randn(n, Dm, generator=g)
+    a = torch.randint(0, k, (n,), generator=g, dtype=torch.int32)
+    a[a == 7] = 8  # an empty cluster
+    Sg, Qg, cg = D.silhouette_sum(X.cuda(), a.cuda(), k)
+    Sh, Qh, ch = D.silhouette_sum(X, a, k)
+    assert torch.allclose(Sg.cpu(), Sh, atol=1e-2) and torch.equal(cg.cpu(), ch)
+    tg = D.silhouette_points(X.cuda(), a.cuda(), Sg, Qg, cg)
+    th = D.silhouette_points(X, a, Sh, Qh, ch)
+    assert abs(tg - th) <= 1e-3 * max(1.0, abs(th))
