@@ -52,6 +52,8 @@ def parse_args(argv: List[str]):
     p.add_argument("--chief-port", type=int, default=int(env("CHIEF_PORT", "2223")))
     # additions
     p.add_argument("--strategy", default=env("PTG_STRATEGY", "auto"), choices=["auto", "ps", "mirrored", "none"])
+    p.add_argument("--cache-decoded", action="store_true",
+                   help="keep decoded images in host RAM after the first epoch (Dataset.cache)")
     p.add_argument("--synthetic", type=int, default=int(env("PTG_SYNTHETIC", "0")),
                    help="generate N synthetic laser-spot images into --data-path first")
     head = p.add_mutually_exclusive_group()
@@ -260,8 +262,10 @@ def run_image_training(data_dir: str, output_dir: str, epochs: int, batch_size: 
         world = getattr(strategy, "world_size", 1) if strategy is not None else 1
         steps_per_epoch = max(1, train_count // batch_size // world)
         ictx = strategy.input_context() if strategy is not None and world > 1 else None
+        cache = bool(getattr(args, "cache_decoded", False))
         ds_train = make_image_dataset(data_dir, (img_height, img_width), batch_size, shuffle=True, input_context=ictx,
-                                      validation_split=val_split, subset="training", seed=seed, repeat=True)
+                                      validation_split=val_split, subset="training", seed=seed, repeat=True,
+                                      cache=cache)
         ds_val = make_image_dataset(data_dir, (img_height, img_width), batch_size, shuffle=False,
                                     validation_split=val_split, subset="validation", seed=seed, repeat=False)
         ctx = strategy.scope() if strategy is not None else _null()

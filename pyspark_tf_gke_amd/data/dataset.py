@@ -6,9 +6,10 @@ parallel on a thread pool, ``num_parallel_calls=AUTOTUNE``), ``filter``, ``shard
 ``batch`` (numpy stacking; ``drop_remainder``), ``unbatch``, ``repeat``, ``take``, ``skip``,
 ``prefetch`` (background thread), ``cache``, ``cardinality``, ``as_numpy_iterator``.
 
-Elements are tuples of numpy arrays (or a single array).  Batches stay on the host; the trainer
-uploads them with pinned, non-blocking copies (and raw uint8 images are resized/normalised on the
-GPU by the first conv op).
+Elements are tuples of numpy arrays (or a single array).  Batches stay on the host until the
+trainer's device feed (data/device_feed.py: pinned staging ring, H2D on a side stream, event
+handoff to the compute stream) moves them to HBM; raw uint8 images are resized / normalised on the
+GPU by the first conv op.
 
 Columnar fast path: a ``from_tensor_slices`` source followed only by ``shard`` / ``shuffle`` /
 ``batch`` / ``repeat`` / ``prefetch`` never iterates elements in Python: it builds index
@@ -405,6 +406,9 @@ class Dataset:
     def __iter__(self):
         return iter(self._gen_fn())
 
+    def apply(self, transformation_func) -> "Dataset":
+        return transformation_func(self)
+
     def as_numpy_iterator(self):
         return iter(self)
 
@@ -419,5 +423,12 @@ class Dataset:
 
 class experimental:  # noqa: N801
     AUTOTUNE = AUTOTUNE
+
+    @staticmethod
+    def prefetch_to_device(device, buffer_size=None):
+        from .device_feed import prefetch_to_device
+
+        return prefetch_to_device(device, buffer_size)
+
     INFINITE_CARDINALITY = INFINITE
     UNKNOWN_CARDINALITY = UNKNOWN

@@ -126,7 +126,7 @@ def _decode(path: str, h: int, w: int) -> np.ndarray:
 
 def make_image_dataset(data_dir: str, image_size, batch_size: int, shuffle: bool = True, input_context=None,
                        validation_split: float = 0.0, subset: Optional[str] = None, seed: int = 1337,
-                       repeat: bool = True) -> Dataset:
+                       repeat: bool = True, cache: bool = False) -> Dataset:
     img_h, img_w = int(image_size[0]), int(image_size[1])
     entries = [(p, x, y) for p, x, y in _label_entries(data_dir) if x is not None and y is not None]
     if not entries:
@@ -139,9 +139,11 @@ def make_image_dataset(data_dir: str, image_size, batch_size: int, shuffle: bool
     paths = [entries[i][0] for i in idx]
     targets = np.array([[entries[i][1], entries[i][2]] for i in idx], dtype=np.float32)
     ds = Dataset.zip((Dataset.from_tensor_slices(np.array(paths, dtype=object)), Dataset.from_tensor_slices(targets)))
-    ds = ds.map(lambda p, y: (_decode(str(p), img_h, img_w), y), num_parallel_calls=AUTOTUNE)
-    if input_context is not None:
+    if input_context is not None:  # shard before decoding: each worker decodes only its own files
         ds = ds.shard(input_context.num_input_pipelines, input_context.input_pipeline_id)
+    ds = ds.map(lambda p, y: (_decode(str(p), img_h, img_w), y), num_parallel_calls=AUTOTUNE)
+    if cache:  # decoded uint8 frames kept in host RAM after the first epoch (decode is the host bound)
+        ds = ds.cache()
     if shuffle:
         ds = ds.shuffle(min(3000, len(paths)), seed=seed)
     ds = ds.batch(batch_size)

@@ -33,6 +33,7 @@ from .params import ParamStore
 # Adam fused into the weight-gradient GEMM of big Dense layers on one replica (gemm.hip EpiAdam):
 # the 168 MB CNN-B1 Dense kernel gradient is never written or re-read.  PTG_FUSED_ADAM=0 disables.
 FUSED_ADAM = os.environ.get("PTG_FUSED_ADAM", "1") != "0"
+DEVICE_FEED = os.environ.get("PTG_DEVICE_FEED", "1") != "0"
 
 
 def default_device() -> torch.device:
@@ -409,11 +410,17 @@ class Sequential:
         return logs
 
     # ---------------------------------------------------------------- fit / evaluate / predict
-    @staticmethod
-    def _iter_batches(x, y, batch_size, shuffle, seed=None):
+    def _iter_batches(self, x, y, batch_size, shuffle, seed=None):
         from ..data.dataset import Dataset
 
         if isinstance(x, Dataset) or hasattr(x, "__iter__") and not isinstance(x, (np.ndarray, torch.Tensor)):
+            if (self.device.type == "cuda" and DEVICE_FEED and isinstance(x, Dataset)
+                    and getattr(x, "_plan", None) is None and not getattr(x, "_on_device", False)):
+                # host batches (decoded images, CSV rows): pinned ring + side-stream H2D, overlapped
+                # with the train step (data/device_feed.py)
+                from ..data.device_feed import DeviceFeeder
+
+                return DeviceFeeder(x, self.device)
             return iter(x)
         n = len(x)
         bs = batch_size or 32
@@ -464,9 +471,11 @@ class Sequential:
                 except StopIteration:
                     break
                 xb, yb = self._prep_batch(batch[0], batch[1])
+                self._last_batch = int(xb.shape[0])
                 self.train_step_fast(xb, yb, stats)
                 nsteps += 1
             logs = self._logs_from(stats)
+            dt_train = time.perf_counter() - t0  # the logs readback synchronised the device
             self._sync_master()  # every rank is here: the full fp32 master for callbacks / saving
             if validation_data is not None:
                 vlogs = self.evaluate(*(validation_data if isinstance(validation_data, tuple) else (validation_data,)),
@@ -480,7 +489,9 @@ class Sequential:
             if verbose and is_chief:
                 per = dt / max(nsteps, 1)
                 body = " - ".join(f"{k_}: {v_:.4f}" for k_, v_ in sorted(logs.items()))
-                print(f"{nsteps}/{nsteps} - {dt:.0f}s {per * 1e3:.0f}ms/step - {body}", flush=True)
+                bs = getattr(self, "_last_batch", 0)
+                rate = f" - {bs * nsteps / max(dt_train, 1e-9):.0f} samples/s (train)" if bs else ""
+                print(f"{nsteps}/{nsteps} - {dt:.0f}s {per * 1e3:.0f}ms/step{rate} - {body}", flush=True)
             for cb in callbacks:
                 if hasattr(cb, "on_epoch_end"):
                     cb.on_epoch_end(epoch, logs)

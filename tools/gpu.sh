@@ -89,9 +89,10 @@ for task in "$@"; do
       timeout -k 10 $STEP_T python workloads/raw-tf/train_mnist.py --epochs 3 --steps-per-epoch 50 --batch-size 256 \
         --output-dir /tmp/mnist > gpurun_out/mnist.log 2>&1 || fail mnist gpurun_out/mnist.log
       tail -3 gpurun_out/mnist.log
-      timeout -k 10 $STEP_T python workloads/raw-tf/train_tf_ps.py --data-is-images --synthetic 4096 --epochs 2 \
-        --batch-size 256 --output-dir /tmp/cnn > gpurun_out/train_images.log 2>&1 || fail images gpurun_out/train_images.log
-      tail -4 gpurun_out/train_images.log ;;
+      timeout -k 10 $STEP_T python workloads/raw-tf/train_tf_ps.py --data-is-images --synthetic ${E2E_IMAGES:-4096} \
+        --data-path /tmp/imgs --epochs 3 --batch-size 256 --cache-decoded --output-dir /tmp/cnn \
+        > gpurun_out/train_images.log 2>&1 || fail images gpurun_out/train_images.log
+      grep -E "Epoch|samples/s" gpurun_out/train_images.log | tail -6 ;;
     *) echo "unknown task $task"; exit 2 ;;
   esac
 done
