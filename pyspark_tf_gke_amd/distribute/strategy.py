@@ -270,8 +270,10 @@ class MultiWorkerMirroredStrategy(Strategy):
         self.sharded_update = bool(sharded_update) and self.world_size > 1
         self._works: list = []
         self._launched = 0
-        if self.world_size > 1 and self.device.type == "cuda" and os.environ.get("PTG_PERSIST_DYNAMIC") is None:
-            # reduce-scatter / all-gather kernels run beside the backward: work-queue conv kernels
+        if self.world_size > 1 and self.device.type == "cuda" and os.environ.get("PTG_PERSIST_DYNAMIC") == "1":
+            # opt-in: work-queue conv kernels (absorb CUs taken by the concurrent RCCL kernels).  The
+            # default stays the static-grid kernels, the faster ones in the only A/B measured so far
+            # (1 GPU, 119.5k vs 114.3k samples/s, README); re-measure on 8 GPUs before flipping it.
             from ..ops import nn as K
 
             K.set_persist_mode(True)

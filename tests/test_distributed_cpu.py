@@ -255,3 +255,14 @@ def test_distributed_orderby_and_bounded_shuffle():
         assert v["total"] == len(allrows) and v["gc"] == len(allrows) and v["rep_total"] == len(allrows)
         assert v["rounds"] > 1 and v["peak"] <= 2 * 64 * 1024
     assert abs(res[0]["rep_n"] - res[1]["rep_n"]) <= 2
+
+
+def test_rccl_check_script_gloo_rehearsal():
+    """tools/rccl_check.py (the >= 2-GPU RCCL test's body) on 2 gloo CPU ranks, so the multi-GPU
+    script is exercised every round even where no second GPU exists."""
+    cmd = [sys.executable, "-m", "pyspark_tf_gke_amd.runtime.launcher", "--nproc", "2", "--",
+           sys.executable, os.path.join(ROOT, "tools", "rccl_check.py")]
+    env = dict(os.environ, PYTHONPATH=ROOT, PTG_DEVICE="cpu", PTG_RCCL_ALLOW_GLOO="1", PTG_RCCL_ROWS="200000")
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert r.stdout.count('"ok": true') == 2, r.stdout[-2000:]
