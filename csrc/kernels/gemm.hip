@@ -24,7 +24,9 @@
 //     blockIdx.y indexes split-K slices (fp32 atomic epilogue).
 #include "common.h"
 
+#include <cstdlib>
 #include <type_traits>
+#include <utility>
 
 namespace ptg {
 
@@ -46,10 +48,13 @@ PTG_DEV U4 join(U2 a, U2 b) { U4 v; v.x = a.x; v.y = a.y; v.z = b.x; v.w = b.y; 
 template <int VEC>
 struct MatK {  // element(r,k) = p[r*ld + k]; ld % VEC == 0, K % 8 == 0 or zero-padded rows
   static constexpr bool K_CONTIG = true;
+  static constexpr bool DMA16 = VEC == 8;  // 8 consecutive k = one aligned 16-B chunk (off())
   const bf16_t* p; long ld; int R; int K; uint32_t bytes;
   struct Ctx { uint32_t row; };
   PTG_DEV Rsrc rsrc() const { return make_rsrc(p, bytes); }
   PTG_DEV Ctx ctx(int r) const { Ctx c; c.row = r < R ? (uint32_t)(r * ld) * 2u : OOB; return c; }
+  // byte offset of elements (r, k..k+7) for the LDS-DMA path (VEC == 8 only)
+  PTG_DEV uint32_t off(const Ctx& c, int k) const { return (k < K && c.row != OOB) ? c.row + 2u * k : OOB; }
   PTG_DEV U4 load(Rsrc rs, const Ctx& c, int k) const {
     const uint32_t off = k < K ? c.row + 2u * k : OOB;
     if constexpr (VEC == 8) {
@@ -76,6 +81,7 @@ struct MatMN {  // element(r,k) = p[k*ld + r]; R % 8 == 0, ld % 8 == 0
 template <int CVEC>
 struct ConvFwdA {
   static constexpr bool K_CONTIG = true;
+  static constexpr bool DMA16 = CVEC == 8;
   const bf16_t* x; int H, W, C, logC, OH, OW, KW, stride, pad, M, Kc; uint32_t bytes;
   FastDiv fKW, fOHW, fOW;  // set by init(): the per-load (kh, kw) and per-row pixel decodes without idiv
   ConvFwdA& init() {
@@ -102,6 +108,7 @@ struct ConvFwdA {
     const bool ok = (k < Kc) && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
     return ok ? c.img + (uint32_t)((ih * W + iw) * C + ci) * 2u : OOB;
   }
+  PTG_DEV uint32_t off(const Ctx& c, int k) const { return c.img == OOB ? OOB : at(c, k); }
   PTG_DEV U4 load(Rsrc rs, const Ctx& c, int k) const {
     if constexpr (CVEC == 8) return bload16(rs, at(c, k));
     else return join(bload8(rs, at(c, k)), bload8(rs, at(c, k + 4)));
@@ -559,6 +566,169 @@ __global__ __launch_bounds__(256) void gemm_kernel(LA la, LB lb, EPI epi, int M,
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// 256x256 tile, 8 waves (2 in M x 4 in N, 128x64 outputs = 8x4 MFMA fragments per wave), operands
+// staged by LDS-DMA (buffer_load ... lds, 16 B per lane: no VGPR round trip, the hardware range
+// check zero-fills padding / tails) into a two-stage ring (2 x 64 KiB): the DMA of K-tile t+1 is
+// in flight during the 64 MFMAs per wave of tile t (cdna_hip_programming.md "The 256^2 template";
+// 4x the MFMA work per barrier of the 128x128 kernel).  A DMA wave-instruction writes 1 KiB
+// lane-linearly = 8 rows x 8 16-B k-chunks, so the bank swizzle is applied on the SOURCE side:
+// lane l of a block fetches chunk (l&7) ^ ((row>>1)&7) and the fragment read un-XORs it — 16
+// consecutive rows of one k-chunk then hit 16 distinct 16-B bank slots (conflict-free ds_read_b128).
+// Both operands must be k-contiguous loaders with a 16-B off() (plain matrices, conv im2col).
+// ------------------------------------------------------------------------------------------
+template <class L, class = void> struct HasOff : std::false_type {};
+template <class L> struct HasOff<L, std::void_t<decltype(std::declval<L>().off(std::declval<typename L::Ctx>(), 0))>>
+    : std::integral_constant<bool, L::DMA16> {};
+
+typedef __attribute__((address_space(3))) void g256_lds_t;
+
+template <class LA, class LB, class EPI>
+__global__ __launch_bounds__(512) void gemm256_kernel(LA la, LB lb, EPI epi, int M, int N, int K, int kchunk) {
+  constexpr int TM = 256, TN = 256, WTM = 128, WTN = 64, FM = 8, FN = 4;
+  constexpr int OPB = TM * BK * 2;          // bytes of one operand tile (32 KiB)
+  constexpr int STB = 2 * OPB;              // stage bytes (A + B)
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * STB];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 2, wn = wid & 3;
+  const int tiles_n = (N + TN - 1) / TN;
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = t / tiles_n, tn = t - tm * tiles_n;
+  const int m0 = tm * TM, n0 = tn * TN;
+  const int kb = blockIdx.y * kchunk;
+  const int ke = min(K, kb + kchunk);
+  if (kb >= ke) return;
+  const int nk = (ke - kb + BK - 1) / BK;
+
+  // this lane's 4 DMA rows per operand: block b = wid*4 + j covers rows 8b..8b+7
+  typename LA::Ctx ca[4];
+  typename LB::Ctx cb[4];
+  int kcA[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int row = (wid * 4 + j) * 8 + (lane >> 3);
+    ca[j] = la.ctx(m0 + row);
+    cb[j] = lb.ctx(n0 + row);
+    kcA[j] = ((lane & 7) ^ ((row >> 1) & 7)) * 8;  // source-side swizzle
+  }
+  const Rsrc rsA = la.rsrc(), rsB = lb.rsrc();
+  auto dma = [&](int stage, int k0) {
+    unsigned char* base = smem + stage * STB;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int blk = wid * 4 + j;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (g256_lds_t*)(base + blk * 1024), 16,
+                                               la.off(ca[j], k0 + kcA[j]), 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (g256_lds_t*)(base + OPB + blk * 1024), 16,
+                                               lb.off(cb[j], k0 + kcA[j]), 0, 0, 0);
+    }
+  };
+  // fragment: rows row0..row0+15, k-chunk cbase + (lane>>4): one ds_read_b128
+  const int fr = lane & 15, fc = lane >> 4;
+  auto frag = [&](const unsigned char* img, int row0, int cbase) -> bf16x8_t {
+    const int r = row0 + fr;
+    const int pos = (cbase + fc) ^ ((r >> 1) & 7);
+    return __builtin_bit_cast(bf16x8_t, *(const U4*)(img + r * 128 + pos * 16));
+  };
+
+  f32x4_t acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  dma(0, kb);
+  __syncthreads();  // waits vmcnt(0): this wave's DMA landed; the barrier publishes every wave's
+  for (int it = 0; it < nk; ++it) {
+    const int cur = it & 1;
+    if (it + 1 < nk) dma(cur ^ 1, kb + (it + 1) * BK);  // stage cur^1 was last read in step it-1
+    const unsigned char* sA = smem + cur * STB;
+    const unsigned char* sB = sA + OPB;
+#pragma unroll
+    for (int kc = 0; kc < 8; kc += 4) {
+      bf16x8_t af[FM], bfr[FN];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bfr[j] = frag(sB, wn * WTN + j * 16, kc);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[i] = frag(sA, wm * WTM + i * 16, kc);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+
+  // C/D map of mfma_f32_16x16x32: col = lane&15, row = (lane>>4)*4 + r
+  if constexpr (!EPI::VEC) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm * WTM + i * 16 + (lane >> 4) * 4 + r;
+          const int n = n0 + wn * WTN + j * 16 + (lane & 15);
+          if (m < M && n < N) epi(m, n, acc[i][j][r]);
+        }
+    return;
+  } else {
+    // 4 passes of 64 rows through LDS: each thread then hands 8 consecutive columns to the epilogue
+    constexpr int CP = TN + 4;
+    float* cs = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int pass = 0; pass < 4; ++pass) {
+      if (wm == (pass >> 1)) {
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii) {
+          const int i = (pass & 1) * 4 + ii;
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              cs[(ii * 16 + (lane >> 4) * 4 + r) * CP + wn * WTN + j * 16 + (lane & 15)] = acc[i][j][r];
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int v0 = 0; v0 < 64 * TN / 8; v0 += 512) {
+        const int v = v0 + tid;
+        const int row = v / (TN / 8), c8 = v - row * (TN / 8);
+        const int m = m0 + pass * 64 + row, n = n0 + c8 * 8;
+        if (m < M && n < N) {
+          const float4 a = *(const float4*)(cs + row * CP + c8 * 8), b = *(const float4*)(cs + row * CP + c8 * 8 + 4);
+          float vals[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+          epi.vec8(m, n, vals, min(8, N - n));
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+template <class LA, class LB, class EPI>
+static int launch_gemm256(const LA& la, const LB& lb, const EPI& epi, int M, int N, int K, int splits, hipStream_t s) {
+  const int tiles = ptg_ceil_div(M, 256) * ptg_ceil_div(N, 256);
+  if (splits < 1) splits = 1;
+  int kchunk = ptg_ceil_div(ptg_ceil_div(K, splits), BK) * BK;
+  if (kchunk < BK) kchunk = BK;
+  splits = ptg_ceil_div(K, kchunk);
+  hipLaunchKernelGGL((gemm256_kernel<LA, LB, EPI>), dim3(tiles, splits), dim3(512), 0, s, la, lb, epi, M, N, K,
+                     kchunk);
+  PTG_RETURN_LAUNCH();
+}
+
+// PTG_GEMM256=0 (or ptg_gemm256_set(0)) disables the 256x256 LDS-DMA kernel (A/B runs)
+static int g_gemm256 = -1;
+static bool gemm256_enabled() {
+  if (g_gemm256 < 0) {
+    const char* e = getenv("PTG_GEMM256");
+    g_gemm256 = (e && e[0] == '1') ? 1 : 0;  // off until measured on the GPU (flip after A/B)
+  }
+  return g_gemm256 == 1;
+}
+
 template <int BM, int BN, int WM, int WN, class LA, class LB, class EPI>
 static int launch_gemm(const LA& la, const LB& lb, const EPI& epi, int M, int N, int K, int splits,
                        hipStream_t s) {
@@ -577,6 +747,12 @@ static int launch_gemm(const LA& la, const LB& lb, const EPI& epi, int M, int N,
 template <class LA, class LB, class EPI>
 static int dispatch_gemm(const LA& la, const LB& lb, const EPI& epi, int M, int N, int K, int splits,
                          hipStream_t s) {
+  if constexpr (HasOff<LA>::value && HasOff<LB>::value && EpiPre<EPI>::v == 0) {
+    // big problems: >= one 256x256 tile per CU and K deep enough to amortise the 2-stage ring
+    if (gemm256_enabled() && N >= 256 && M >= 256 && K >= 256 &&
+        (long)ptg_ceil_div(M, 256) * ptg_ceil_div(N, 256) * splits >= 200)
+      return launch_gemm256(la, lb, epi, M, N, K, splits, s);
+  }
   if (N <= 16) return launch_gemm<256, 16, 4, 1>(la, lb, epi, M, N, K, splits, s);
   if (N <= 32) return launch_gemm<256, 32, 4, 1>(la, lb, epi, M, N, K, splits, s);
   if (N <= 64) return launch_gemm<128, 64, 2, 2>(la, lb, epi, M, N, K, splits, s);
@@ -611,6 +787,11 @@ static bool is_pow2(int v) { return v > 0 && (v & (v - 1)) == 0; }
 using namespace ptg;
 
 extern "C" {
+
+int ptg_gemm256_set(int on) {
+  g_gemm256 = on ? 1 : 0;
+  return 0;
+}
 
 // Generic bf16 GEMM: C[M][N] = sum_k A(m,k) B(k,n).
 //   a_kcontig: A(m,k) = A[m*lda + k]  else A(m,k) = A[k*lda + m]
