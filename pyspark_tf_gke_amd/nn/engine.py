@@ -310,6 +310,36 @@ class DenseOp(Op):
         self._x, self._y = x, y
         return y
 
+    def forward_splitk_sums(self, x, ws):
+        """Big Dense forward that stops at the fp32 split-K sums (no bias / activation): the fused
+        regression head (head_mse_k) finishes the layer and re-zeroes the buffer for the next step."""
+        x = x.reshape(x.shape[0], -1)
+        B = x.shape[0]
+        N, Kd = self.dense.units, self.dense.fan_in
+        x = _bf16(x, ws, self.name + "/x16")
+        # zeroed when (re)allocated; afterwards the head kernel leaves it zero after every step
+        acc = ws.get(self.name + "/headacc", (B, N), torch.float32, x.device, zero=True)
+        tiles = -(-B // 128) * -(-N // 128)
+        splits = 1 if Kd < 4096 else max(1, min(16, 512 // max(tiles, 1), Kd // 1024))
+        K.gemm(B, N, Kd, x, Kd, 1, self.dense.kernel.bf16, Kd, 1, 3, acc, N, None, 0, splits)
+        self._x = x
+        return acc
+
+    def backward_dz(self, dz, ws):
+        """Big Dense backward from the pre-activation gradient dz (bias gradient already summed):
+        dX (unless first) then dW, or Adam fused into the dW GEMM."""
+        x = self._x
+        dx = None
+        if not self.first:
+            dx = ws.get(self.name + "/dx", x.shape, torch.bfloat16, x.device)
+            K.linear_dx(dz, self.dense.kernel.bf16, dx)
+        fused = self.fused_update
+        if fused is not None and dz.is_cuda:
+            fused.linear_dw(dz, x, self.dense.kernel)
+        else:
+            K.linear_dw(dz, x, self.dense.kernel.grad)
+        return dx
+
     def backward(self, dy, ws):
         x, y = self._x, self._y
         dev = y.device

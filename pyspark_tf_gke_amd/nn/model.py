@@ -34,6 +34,7 @@ from .params import ParamStore
 # the 168 MB CNN-B1 Dense kernel gradient is never written or re-read.  PTG_FUSED_ADAM=0 disables.
 FUSED_ADAM = os.environ.get("PTG_FUSED_ADAM", "1") != "0"
 DEVICE_FEED = os.environ.get("PTG_DEVICE_FEED", "1") != "0"
+FUSED_HEAD = os.environ.get("PTG_FUSED_HEAD", "1") != "0"
 
 
 def default_device() -> torch.device:
@@ -332,12 +333,48 @@ class Sequential:
             op.fused_update = ctx
         return ctx
 
+    def _head_fusable(self, xb, st) -> bool:
+        """[..., Dense(relu, big), Dense(N <= 4, linear)] + MSE on one GPU replica: the head runs as
+        one fused kernel (head_mse_k) instead of seven small ones."""
+        if not FUSED_HEAD or not xb.is_cuda or (st is not None and st.world_size != 1):
+            return False
+        ops = getattr(self, "ops", None) or []
+        if len(ops) < 3 or not isinstance(self.loss, LS.MeanSquaredError):
+            return False
+        d1, d2 = ops[-2], ops[-1]
+        return (isinstance(d1, E.DenseOp) and isinstance(d2, E.DenseOp) and d1.big and not d2.big
+                and d1.act == "relu" and d2.act in (None, "linear") and d1.dense.bias is not None
+                and d2.dense.bias is not None and d2.dense.units <= 4 and not d1.first
+                and d1.dense.units * (d2.dense.units + 1) * 4 <= 64 * 1024)
+
+    def _train_step_fused_head(self, xb, yb, stats, st) -> None:
+        d1, d2 = self.ops[-2], self.ops[-1]
+        x = E.run_forward(self.ops[:-2], xb, self.ws, True)
+        acc = d1.forward_splitk_sums(x, self.ws)
+        B, K1 = acc.shape
+        dz1 = self.ws.get(d1.name + "/dz", (B, K1), torch.bfloat16, acc.device)
+        K.head_mse(acc, d1.dense.bias.data, d2.dense.kernel.data, d2.dense.bias.data, yb.contiguous(), dz1,
+                   d2.dense.kernel.grad, d2.dense.bias.grad, d1.dense.bias.grad, stats)
+        fused = self._begin_fused_update(st)
+        try:
+            dx = d1.backward_dz(dz1, self.ws)
+            E.run_backward(self.ops[:-2], dx, self.ws)
+        finally:
+            for op in getattr(self, "_fusable_ops", []):
+                op.fused_update = None
+        if fused is not None:
+            self.optimizer.finish_fused(fused)
+        else:
+            self.optimizer.apply(self.store)
+
     def train_step(self, xb, yb, stats=None) -> None:
         _fault.maybe_fail()
         _heartbeat.progress()
         st = self._strategy()
         stats = self._stats_buf() if stats is None else stats
         self.store.zero_grad()
+        if self._head_fusable(xb, st):
+            return self._train_step_fused_head(xb, yb, stats, st)
         out = self._run_forward(xb, True)
         dpred = self._loss_grad(out, yb, stats)
         self.backward_and_update(dpred, st)

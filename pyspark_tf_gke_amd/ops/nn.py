@@ -298,6 +298,15 @@ def linear_dw_adam(dy, x, p, m, v, pbf, lr_t: float, b1: float, b2: float, eps: 
         float(lr_t), float(b1), float(b2), float(eps), float(gscale), ptr(lr_dev))
 
 
+def head_mse(acc, b1, w2, b2, tgt, dz1, dw2, db2, db1, stats, pred_out=None, gscale: float = 1.0):
+    """Fused Dense(relu) -> Dense(N2) -> MSE head on the Dense1 split-K sums ``acc`` [B, K1] (fp32,
+    re-zeroed): stats / dpred as mse_k, dz1 [B, K1] bf16, dw2 / db2 / db1 accumulated (GPU only)."""
+    B, K1 = acc.shape
+    N2 = w2.shape[0]
+    hip("ptg_head_mse", ptr(acc), ptr(b1), ptr(w2), ptr(b2), ptr(tgt), ptr(dz1), ptr(dw2), ptr(db2), ptr(db1),
+        ptr(stats), ptr(pred_out), B, K1, N2, float(gscale))
+
+
 def col_sum(g, out):
     """out[N] += sum over rows of g[M,N]."""
     if not on_device(g):

@@ -98,3 +98,27 @@ def test_device_feed_matches_plain_upload(hip_built):
     # bitwise deterministic run to run, so compare to fp32 reduction noise
     assert torch.allclose(params[0], params[1], rtol=1e-4, atol=1e-6)
     assert F.STATS["batches"] >= 32
+
+
+def test_fused_regression_head_matches_unfused(hip_built):
+    """CNN-B1 (flat) head as one head_mse_k launch vs the seven-kernel path: same losses / metrics
+    and parameters to bf16-activation tolerance after 3 steps (the fused head keeps the Dense(2048)
+    activation in fp32 where the unfused path rounds it to bf16)."""
+    from pyspark_tf_gke_amd.nn import model as M
+
+    g = torch.Generator().manual_seed(0)
+    X = torch.randint(0, 256, (3, 16, 64, 80, 3), generator=g, dtype=torch.uint8)
+    Y = torch.rand(3, 16, 2, generator=g) * 60
+    res = []
+    for fused in (True, False):
+        M.FUSED_HEAD = fused
+        torch.manual_seed(0)
+        m = build_cnn_model((64, 80, 3), flat=True, summary=False, device="cuda")
+        assert m._head_fusable(X[0].cuda(), None) == fused
+        logs = [m.train_on_batch(X[i], Y[i], return_dict=True) for i in range(3)]
+        res.append((logs, m.store.flat.detach().cpu().clone()))
+    M.FUSED_HEAD = True
+    for a, b in zip(res[0][0], res[1][0]):
+        for k in ("loss", "mae", "mse"):
+            assert abs(a[k] - b[k]) <= 2e-2 * max(1.0, abs(b[k])), (k, a, b)
+    assert torch.allclose(res[0][1], res[1][1], rtol=2e-2, atol=2e-3)
