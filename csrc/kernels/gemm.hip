@@ -578,8 +578,9 @@ __global__ __launch_bounds__(256) void gemm_kernel(LA la, LB lb, EPI epi, int M,
 // Both operands must be k-contiguous loaders with a 16-B off() (plain matrices, conv im2col).
 // ------------------------------------------------------------------------------------------
 template <class L, class = void> struct HasOff : std::false_type {};
-template <class L> struct HasOff<L, std::void_t<decltype(std::declval<L>().off(std::declval<typename L::Ctx>(), 0))>>
-    : std::integral_constant<bool, L::DMA16> {};
+// (detected from the DMA16 constant, not from off() itself: a __device__ member in an unevaluated
+// host-side expression resolves differently in the host and device compilation passes)
+template <class L> struct HasOff<L, std::void_t<decltype(L::DMA16)>> : std::integral_constant<bool, L::DMA16> {};
 
 typedef __attribute__((address_space(3))) void g256_lds_t;
 
@@ -612,17 +613,16 @@ __global__ __launch_bounds__(512) void gemm256_kernel(LA la, LB lb, EPI epi, int
     kcA[j] = ((lane & 7) ^ ((row >> 1) & 7)) * 8;  // source-side swizzle
   }
   const Rsrc rsA = la.rsrc(), rsB = lb.rsrc();
-  auto dma = [&](int stage, int k0) {
-    unsigned char* base = smem + stage * STB;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int blk = wid * 4 + j;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (g256_lds_t*)(base + blk * 1024), 16,
-                                               la.off(ca[j], k0 + kcA[j]), 0, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (g256_lds_t*)(base + OPB + blk * 1024), 16,
-                                               lb.off(cb[j], k0 + kcA[j]), 0, 0, 0);
-    }
-  };
+  // one K-tile of both operands: 4 LDS-DMA wave-instructions per operand per wave, written inline
+  // (a lambda or template helper around the device-only builtin breaks the host compilation pass
+  // and with it the kernel's host stub)
+#define G256_DMA(stage, k0)                                                                                  \
+  _Pragma("unroll") for (int j_ = 0; j_ < 4; ++j_) {                                                         \
+    unsigned char* b_ = smem + (stage) * STB + (wid * 4 + j_) * 1024;                                        \
+    const uint32_t oa_ = la.off(ca[j_], (k0) + kcA[j_]), ob_ = lb.off(cb[j_], (k0) + kcA[j_]);               \
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (g256_lds_t*)b_, 16, oa_, 0, 0, 0);                        \
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (g256_lds_t*)(b_ + OPB), 16, ob_, 0, 0, 0);                \
+  }
   // fragment: rows row0..row0+15, k-chunk cbase + (lane>>4): one ds_read_b128
   const int fr = lane & 15, fc = lane >> 4;
   auto frag = [&](const unsigned char* img, int row0, int cbase) -> bf16x8_t {
@@ -637,11 +637,13 @@ __global__ __launch_bounds__(512) void gemm256_kernel(LA la, LB lb, EPI epi, int
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  dma(0, kb);
+  { G256_DMA(0, kb) }
   __syncthreads();  // waits vmcnt(0): this wave's DMA landed; the barrier publishes every wave's
   for (int it = 0; it < nk; ++it) {
     const int cur = it & 1;
-    if (it + 1 < nk) dma(cur ^ 1, kb + (it + 1) * BK);  // stage cur^1 was last read in step it-1
+    if (it + 1 < nk) {  // stage cur^1 was last read in step it-1
+      G256_DMA(cur ^ 1, kb + (it + 1) * BK)
+    }
     const unsigned char* sA = smem + cur * STB;
     const unsigned char* sB = sA + OPB;
 #pragma unroll
@@ -660,6 +662,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(LA la, LB lb, EPI epi, int
     __syncthreads();
   }
 
+#undef G256_DMA
   // C/D map of mfma_f32_16x16x32: col = lane&15, row = (lane>>4)*4 + r
   if constexpr (!EPI::VEC) {
 #pragma unroll

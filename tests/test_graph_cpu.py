@@ -137,3 +137,19 @@ def test_saved_model_export_load(tmp_path):
         loaded = nn.saved_model.load(d, device="cpu")
         out = loaded.signatures["serving_default"](input_layer=x)["output_0"]
         np.testing.assert_allclose(out, m.predict(x), atol=1e-2)
+
+
+def test_native_libraries_link_completely():
+    """dlopen both HIP kernel libraries with immediate binding (no GPU needed): an unresolved
+    symbol (e.g. a kernel whose host stub was dropped) fails here on the CPU box, not at round end."""
+    import ctypes
+    import os
+
+    from pyspark_tf_gke_amd import _native
+
+    _native.ensure_built()
+    here = os.path.dirname(_native.__file__)
+    for name in ("libptg_hip.so", "libptg_hip_checked.so"):
+        path = os.path.join(here, name)
+        if os.path.exists(path):
+            ctypes.CDLL(path, mode=os.RTLD_NOW | os.RTLD_GLOBAL)
