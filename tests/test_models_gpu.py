@@ -101,9 +101,10 @@ def test_device_feed_matches_plain_upload(hip_built):
 
 
 def test_fused_regression_head_matches_unfused(hip_built):
-    """CNN-B1 (flat) head as one head_mse_k launch vs the seven-kernel path: same losses / metrics
-    and parameters to bf16-activation tolerance after 3 steps (the fused head keeps the Dense(2048)
-    activation in fp32 where the unfused path rounds it to bf16)."""
+    """CNN-B1 (flat) head as one head_mse_k launch vs the seven-kernel path over 3 steps: same
+    losses / metrics, and the parameter updates point the same way (Adam normalises each element's
+    step, so elements whose gradient is ~0 can move by +-lr either way: compare the update vectors'
+    cosine, not elementwise values)."""
     from pyspark_tf_gke_amd.nn import model as M
 
     g = torch.Generator().manual_seed(0)
@@ -114,11 +115,51 @@ def test_fused_regression_head_matches_unfused(hip_built):
         M.FUSED_HEAD = fused
         torch.manual_seed(0)
         m = build_cnn_model((64, 80, 3), flat=True, summary=False, device="cuda")
+        p0 = m.store.flat.detach().cpu().clone()
         assert m._head_fusable(X[0].cuda(), None) == fused
         logs = [m.train_on_batch(X[i], Y[i], return_dict=True) for i in range(3)]
-        res.append((logs, m.store.flat.detach().cpu().clone()))
+        res.append((logs, m.store.flat.detach().cpu() - p0))
     M.FUSED_HEAD = True
     for a, b in zip(res[0][0], res[1][0]):
         for k in ("loss", "mae", "mse"):
             assert abs(a[k] - b[k]) <= 2e-2 * max(1.0, abs(b[k])), (k, a, b)
-    assert torch.allclose(res[0][1], res[1][1], rtol=2e-2, atol=2e-3)
+    u, v = res[0][1], res[1][1]
+    cos = float((u * v).sum() / (u.norm() * v.norm()))
+    assert cos > 0.98, cos
+
+
+def test_head_mse_kernel_vs_fp32_reference(hip_built):
+    """head_mse_k against fp32 torch on the same split-K sums: dz1, dW2, db2, db1, stats, and the
+    accumulator left zeroed."""
+    from pyspark_tf_gke_amd.ops import nn as K
+
+    B, K1, N2 = 256, 2048, 2
+    g = torch.Generator().manual_seed(1)
+    acc = torch.randn(B, K1, generator=g)
+    b1 = torch.randn(K1, generator=g) * 0.1
+    w2 = torch.randn(N2, K1, generator=g) * 0.02
+    b2 = torch.randn(N2, generator=g)
+    t = torch.randn(B, N2, generator=g) * 3
+    h = torch.relu(acc + b1)
+    pred = h @ w2.t() + b2
+    d = pred - t
+    dp = 2 * d / (B * N2)
+    dz = (dp @ w2) * (h > 0)
+    dev = "cuda"
+    acc_d = acc.to(dev).contiguous()
+    dz1 = torch.empty(B, K1, device=dev, dtype=torch.bfloat16)
+    dw2 = torch.zeros(N2, K1, device=dev)
+    db2 = torch.zeros(N2, device=dev)
+    db1 = torch.zeros(K1, device=dev)
+    stats = torch.zeros(8, device=dev)
+    K.head_mse(acc_d, b1.to(dev), w2.to(dev), b2.to(dev), t.to(dev), dz1, dw2, db2, db1, stats)
+    torch.cuda.synchronize()
+    assert float(acc_d.abs().max()) == 0.0
+    assert torch.allclose(dz1.float().cpu(), dz, rtol=1e-2, atol=1e-6)
+    assert torch.allclose(dw2.cpu(), dp.t() @ h, rtol=1e-4, atol=1e-5)
+    assert torch.allclose(db2.cpu(), dp.sum(0), rtol=1e-4, atol=1e-6)
+    assert torch.allclose(db1.cpu(), dz.sum(0), rtol=1e-4, atol=1e-6)
+    st = stats.cpu()
+    assert abs(float(st[0]) - float((d * d).mean()) * B) <= 1e-4 * float((d * d).mean()) * B
+    assert abs(float(st[1]) - float(d.abs().sum())) <= 1e-4 * float(d.abs().sum())
+    assert float(st[3]) == B * N2 and float(st[4]) == B
