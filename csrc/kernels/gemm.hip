@@ -232,12 +232,13 @@ constexpr int BN_GROUPS = 64;  // BN_G in bn.hip
 struct EpiBf16Stats {
   static constexpr bool VEC = true;
   static constexpr bool STATS = true;
-  bf16_t* out; long ldc; float* part; int C;
-  PTG_DEV void operator()(int m, int n, float v) const { out[(long)m * ldc + n] = f2bf(v); }
-  // stores the 8 values and leaves their bf16-rounded form in v (the statistics see what is stored)
+  bf16_t* out; long ldc; float* part; int C; const float* bias;
+  PTG_DEV void operator()(int m, int n, float v) const { out[(long)m * ldc + n] = f2bf(v + (bias ? bias[n] : 0.f)); }
+  // stores the 8 values (+ bias) and leaves their bf16-rounded form in v (the statistics see what
+  // is stored)
   PTG_DEV void vec8(int m, int n, float* v, int cnt) const {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = j < cnt ? bf2f(f2bf(v[j])) : 0.f;
+    for (int j = 0; j < 8; ++j) v[j] = j < cnt ? bf2f(f2bf(v[j] + (bias ? bias[n + j] : 0.f))) : 0.f;
     bf16_store8(out + (long)m * ldc + n, v, cnt, false);
   }
 };
@@ -909,13 +910,13 @@ int ptg_gemm_bf16(int M, int N, int K, const void* A, long lda, int a_kcontig, c
 // bf16 GEMM with k-contiguous A and B (1x1 stride-1 convolution) whose epilogue also accumulates the
 // BatchNormalization statistics of its output into part [BN_GROUPS][2][N] (EpiBf16Stats).
 int ptg_gemm_bf16_bnstats(int M, int N, int K, const void* A, long lda, const void* B, long ldb, void* C, long ldc,
-                          float* part, hipStream_t s) {
+                          const float* bias, float* part, hipStream_t s) {
   if (M <= 0 || N <= 0 || K <= 0) return 0;
   if (lda % 8 || ldb % 8 || K % 8 || N % 8) return (int)hipErrorInvalidValue;
   if (!fits(matk_bytes(lda, M, K)) || !fits(matk_bytes(ldb, N, K))) return (int)hipErrorInvalidValue;
   MatK<8> la{(const bf16_t*)A, lda, M, K, (uint32_t)matk_bytes(lda, M, K)};
   MatK<8> lb{(const bf16_t*)B, ldb, N, K, (uint32_t)matk_bytes(ldb, N, K)};
-  return dispatch_gemm(la, lb, EpiBf16Stats{(bf16_t*)C, ldc, part, N}, M, N, K, 1, s);
+  return dispatch_gemm(la, lb, EpiBf16Stats{(bf16_t*)C, ldc, part, N, bias}, M, N, K, 1, s);
 }
 
 // Weight gradient with Adam fused into the epilogue (EpiAdam): G[M][N] = A^T-style product as in
@@ -933,7 +934,7 @@ int ptg_gemm_adam(int M, int N, int K, const void* A, long lda, int a_kcontig, c
 
 // Conv2D forward, NHWC bf16: z[n][oh][ow][co] = bias[co] + sum_{kh,kw,ci} x[..] w[co][kh][kw][ci]
 // w is [Cout][KH*KW*C] bf16. C must be a power of two >= 4.
-// bn_part (optional, C % 8 == 0, no bias/act): also accumulate the BatchNormalization statistics of z
+// bn_part (optional, C % 8 == 0, no act): also accumulate the BatchNormalization statistics of z
 int ptg_conv2d_fwd(const void* x, const void* w, const float* bias, void* z, int N, int H, int W, int C,
                    int Cout, int KH, int KW, int stride, int pad, int OH, int OW, int act, float* bn_part,
                    hipStream_t s) {
@@ -945,8 +946,8 @@ int ptg_conv2d_fwd(const void* x, const void* w, const float* bias, void* z, int
     ConvFwdA<8> la{(const bf16_t*)x, H, W, C, ilog2(C), OH, OW, KW, stride, pad, M, Kc};
     la.init();
     MatK<8> lb{(const bf16_t*)w, Kc, Cout, Kc, (uint32_t)matk_bytes(Kc, Cout, Kc)};
-    if (bn_part && !bias && !act && Cout % 8 == 0)
-      return dispatch_gemm(la, lb, EpiBf16Stats{(bf16_t*)z, Cout, bn_part, Cout}, M, Cout, Kc, 1, s);
+    if (bn_part && !act && Cout % 8 == 0)
+      return dispatch_gemm(la, lb, EpiBf16Stats{(bf16_t*)z, Cout, bn_part, Cout, bias}, M, Cout, Kc, 1, s);
     return dispatch_gemm(la, lb, epi, M, Cout, Kc, 1, s);
   } else {
     ConvFwdA<4> la{(const bf16_t*)x, H, W, C, ilog2(C), OH, OW, KW, stride, pad, M, Kc};

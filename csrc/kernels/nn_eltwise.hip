@@ -830,79 +830,132 @@ __global__ __launch_bounds__(256) void mse_k(const float* __restrict__ pred, con
 }
 
 // ----------------------------------------------------------------------------------------------
-// Fused regression head (CNN-B1's Dense(2048, relu) -> Dense(2) -> MSE, train_tf_ps.py:366-378),
-// one launch instead of bias_act / dense_small_fwd / mse / dense_small_dw / dense_small_dx /
-// col_sum / the split-K accumulator fill: every wave owns rows of the Dense1 split-K sums
-//   pass 1: h = relu(acc + b1) (fp32), pred = h.W2 + b2 -> MSE stats and dpred (as mse_k)
-//   pass 2: h again (L2-hot), dz1 = (dpred.W2) * [h > 0] -> bf16 for Dense1's dX / dW GEMMs,
-//           dW2 += dpred^T h and db1 += dz1 in LDS (one global atomic per element per workgroup),
-//           db2 += dpred; acc is re-zeroed for the next step's split-K atomics.
+// Fused regression head (CNN-B1's Dense(2048, relu) -> Dense(2) -> MSE, train_tf_ps.py:366-378):
+// two launches instead of bias_act / dense_small_fwd / mse / dense_small_dw / dense_small_dx /
+// col_sum / the split-K accumulator fill.
+//   head_row_k  one workgroup per sample row: h = relu(acc + b1) (fp32), pred = h.W2 + b2, the
+//               row's squared / absolute error and dpred (mse_k's formulas), then
+//               dz1 = (dpred.W2) * [h > 0] as bf16 for Dense1's dX / dW GEMMs
+//   head_col_k  one thread per hidden unit (x 4 row groups): dW2 += dpred^T h, db1 += sum dz1,
+//               re-zeroes acc for the next step's split-K atomics; workgroup (0, 0) also reduces the
+//               per-row errors into the metric stats and dpred into db2
 // ----------------------------------------------------------------------------------------------
-#define HEAD_ROWS 8
+#define HEAD_RG 4
 template <int N2>
-__global__ __launch_bounds__(256) void head_mse_k(float* __restrict__ acc, const float* __restrict__ b1,
+__global__ __launch_bounds__(256) void head_row_k(const float* __restrict__ acc, const float* __restrict__ b1,
                                                   const float* __restrict__ w2, const float* __restrict__ b2,
                                                   const float* __restrict__ tgt, bf16_t* __restrict__ dz1,
-                                                  float* __restrict__ dw2, float* __restrict__ db2,
-                                                  float* __restrict__ db1, float* __restrict__ stats,
+                                                  float* __restrict__ dpred, float* __restrict__ rowerr,
                                                   float* __restrict__ pred_out, int B, int K1, float gscale) {
-  extern __shared__ float hl[];  // [N2][K1] dW2 partials, then [K1] db1 partials
-  float* sdw = hl;
-  float* sdb = hl + N2 * K1;
-  for (int t = threadIdx.x; t < (N2 + 1) * K1; t += 256) hl[t] = 0.f;
+  __shared__ float red[4][N2];
+  __shared__ float sdp[N2];
+  const int m = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const float* arow = acc + (long)m * K1;
+  float dot[N2];
+#pragma unroll
+  for (int n = 0; n < N2; ++n) dot[n] = 0.f;
+  for (int k = tid; k < K1; k += 256) {
+    const float h = fmaxf(arow[k] + b1[k], 0.f);
+#pragma unroll
+    for (int n = 0; n < N2; ++n) dot[n] = fmaf(h, w2[(long)n * K1 + k], dot[n]);
+  }
+#pragma unroll
+  for (int n = 0; n < N2; ++n) {
+    const float v = wave_sum(dot[n]);
+    if (lane == 0) red[w][n] = v;
+  }
   __syncthreads();
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const float inv = 1.f / (float)(B * N2);
-  for (int rr = w; rr < HEAD_ROWS; rr += 4) {
-    const int m = blockIdx.x * HEAD_ROWS + rr;
-    if (m >= B) break;
-    float* arow = acc + (long)m * K1;
-    float dot[N2];
-#pragma unroll
-    for (int n = 0; n < N2; ++n) dot[n] = 0.f;
-    for (int k = lane; k < K1; k += 64) {
-      const float h = fmaxf(arow[k] + b1[k], 0.f);
-#pragma unroll
-      for (int n = 0; n < N2; ++n) dot[n] = fmaf(h, w2[(long)n * K1 + k], dot[n]);
-    }
-    float dp[N2];
+  if (tid == 0) {
+    const float inv = 1.f / (float)(B * N2);
     float se = 0.f, ae = 0.f;
 #pragma unroll
     for (int n = 0; n < N2; ++n) {
-      const float p = wave_sum(dot[n]) + b2[n];
+      const float p = red[0][n] + red[1][n] + red[2][n] + red[3][n] + b2[n];
       const float d = p - tgt[(long)m * N2 + n];
       se += d * d;
       ae += fabsf(d);
-      dp[n] = 2.f * d * inv * gscale;
-      if (pred_out && lane == 0) pred_out[(long)m * N2 + n] = p;
+      sdp[n] = 2.f * d * inv * gscale;
+      dpred[(long)m * N2 + n] = sdp[n];
+      if (pred_out) pred_out[(long)m * N2 + n] = p;
     }
-    if (lane == 0) {
-      atomicAdd(stats + 0, se * inv * (float)B);
-      atomicAdd(stats + 1, ae);
-      atomicAdd(stats + 2, se);
-      atomicAdd(stats + 3, (float)N2);
-      atomicAdd(stats + 4, 1.f);
-#pragma unroll
-      for (int n = 0; n < N2; ++n) atomicAdd(db2 + n, dp[n]);
-    }
-    for (int k = lane; k < K1; k += 64) {
-      const float h = fmaxf(arow[k] + b1[k], 0.f);
-      arow[k] = 0.f;
-      float g = 0.f;
-#pragma unroll
-      for (int n = 0; n < N2; ++n) g = fmaf(dp[n], w2[(long)n * K1 + k], g);
-      const float dz = h > 0.f ? g : 0.f;
-      dz1[(long)m * K1 + k] = f2bf(dz);
-      atomicAdd(&sdb[k], dz);
-#pragma unroll
-      for (int n = 0; n < N2; ++n) atomicAdd(&sdw[n * K1 + k], dp[n] * h);
-    }
+    rowerr[2 * m] = se;
+    rowerr[2 * m + 1] = ae;
   }
   __syncthreads();
-  for (int t = threadIdx.x; t < N2 * K1; t += 256)
-    if (sdw[t] != 0.f) atomicAdd(dw2 + t, sdw[t]);
-  for (int t = threadIdx.x; t < K1; t += 256)
-    if (sdb[t] != 0.f) atomicAdd(db1 + t, sdb[t]);
+  float dp[N2];
+#pragma unroll
+  for (int n = 0; n < N2; ++n) dp[n] = sdp[n];
+  for (int k = tid; k < K1; k += 256) {
+    const float h = fmaxf(arow[k] + b1[k], 0.f);
+    float g = 0.f;
+#pragma unroll
+    for (int n = 0; n < N2; ++n) g = fmaf(dp[n], w2[(long)n * K1 + k], g);
+    dz1[(long)m * K1 + k] = f2bf(h > 0.f ? g : 0.f);
+  }
+}
+
+template <int N2>
+__global__ __launch_bounds__(256) void head_col_k(float* __restrict__ acc, const float* __restrict__ b1,
+                                                  const float* __restrict__ w2, const float* __restrict__ dpred,
+                                                  const float* __restrict__ rowerr, float* __restrict__ dw2,
+                                                  float* __restrict__ db2, float* __restrict__ db1,
+                                                  float* __restrict__ stats, int B, int K1) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  const int rows = (B + HEAD_RG - 1) / HEAD_RG, m0 = blockIdx.y * rows, m1 = min(B, m0 + rows);
+  if (k < K1) {
+    const float bk = b1[k];
+    float wk[N2], sw[N2];
+#pragma unroll
+    for (int n = 0; n < N2; ++n) { wk[n] = w2[(long)n * K1 + k]; sw[n] = 0.f; }
+    float sb = 0.f;
+    for (int m = m0; m < m1; ++m) {
+      float* ap = acc + (long)m * K1 + k;
+      const float h = fmaxf(*ap + bk, 0.f);
+      *ap = 0.f;
+      float g = 0.f;
+#pragma unroll
+      for (int n = 0; n < N2; ++n) {
+        const float d = dpred[(long)m * N2 + n];
+        g = fmaf(d, wk[n], g);
+        sw[n] = fmaf(d, h, sw[n]);
+      }
+      sb += h > 0.f ? g : 0.f;
+    }
+#pragma unroll
+    for (int n = 0; n < N2; ++n) atomicAdd(dw2 + (long)n * K1 + k, sw[n]);
+    atomicAdd(db1 + k, sb);
+  }
+  if (blockIdx.x == 0 && blockIdx.y == 0) {
+    __shared__ float scr[4];
+    float se = 0.f, ae = 0.f, dsum[N2];
+#pragma unroll
+    for (int n = 0; n < N2; ++n) dsum[n] = 0.f;
+    for (int m = threadIdx.x; m < B; m += 256) {
+      se += rowerr[2 * m];
+      ae += rowerr[2 * m + 1];
+#pragma unroll
+      for (int n = 0; n < N2; ++n) dsum[n] += dpred[(long)m * N2 + n];
+    }
+    const float tse = block_sum256(se, scr);
+    __syncthreads();
+    const float tae = block_sum256(ae, scr);
+    float td[N2];
+#pragma unroll
+    for (int n = 0; n < N2; ++n) {
+      __syncthreads();
+      td[n] = block_sum256(dsum[n], scr);
+    }
+    if (threadIdx.x == 0) {
+      const float inv = 1.f / (float)(B * N2);
+      stats[0] += tse * inv * (float)B;
+      stats[1] += tae;
+      stats[2] += tse;
+      stats[3] += (float)(B * N2);
+      stats[4] += (float)B;
+#pragma unroll
+      for (int n = 0; n < N2; ++n) db2[n] += td[n];
+    }
+  }
 }
 
 // softmax + sparse categorical cross-entropy on logits (row per thread, C <= 64).
@@ -1271,16 +1324,20 @@ int ptg_prelu_bwd2(const void* da, const void* z, const float* alpha, void* dz, 
   PTG_RETURN_LAUNCH();
 }
 
-// fused Dense(relu) -> Dense(N2 <= 4, linear) -> MSE head (head_mse_k); acc is zeroed on exit
+// fused Dense(relu) -> Dense(N2 <= 4, linear) -> MSE head (head_row_k + head_col_k); acc is zeroed
+// on exit.  scratch: fp32 [B * (N2 + 2)] (dpred and per-row errors).
 int ptg_head_mse(void* acc, const float* b1, const float* w2, const float* b2, const float* tgt, void* dz1,
-                 float* dw2, float* db2, float* db1, float* stats, float* pred_out, int B, int K1, int N2,
-                 float gscale, hipStream_t s) {
-  const size_t lds = (size_t)(N2 + 1) * K1 * 4;
-  if (lds > 64 * 1024 || N2 < 1 || N2 > 4) return (int)hipErrorInvalidValue;
-  const dim3 grid((B + HEAD_ROWS - 1) / HEAD_ROWS);
-#define PTG_HEAD(NN)                                                                                        \
-  hipLaunchKernelGGL(head_mse_k<NN>, grid, dim3(256), lds, s, (float*)acc, b1, w2, b2, tgt, (bf16_t*)dz1, dw2, \
-                     db2, db1, stats, pred_out, B, K1, gscale)
+                 float* dw2, float* db2, float* db1, float* stats, float* pred_out, float* scratch, int B, int K1,
+                 int N2, float gscale, hipStream_t s) {
+  if (N2 < 1 || N2 > 4 || B <= 0 || K1 <= 0) return (int)hipErrorInvalidValue;
+  float* dpred = scratch;
+  float* rowerr = scratch + (long)B * N2;
+  const dim3 gc((K1 + 255) / 256, HEAD_RG);
+#define PTG_HEAD(NN)                                                                                          \
+  hipLaunchKernelGGL(head_row_k<NN>, dim3(B), dim3(256), 0, s, (const float*)acc, b1, w2, b2, tgt, (bf16_t*)dz1, \
+                     dpred, rowerr, pred_out, B, K1, gscale);                                                 \
+  hipLaunchKernelGGL(head_col_k<NN>, gc, dim3(256), 0, s, (float*)acc, b1, w2, dpred, rowerr, dw2, db2, db1,    \
+                     stats, B, K1)
   switch (N2) {
     case 1: PTG_HEAD(1); break;
     case 2: PTG_HEAD(2); break;

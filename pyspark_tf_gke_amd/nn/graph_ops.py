@@ -107,11 +107,11 @@ def conv_forward(x, w, bias, stride, pad, z, bn_part=None):
     if not K.on_device(x):
         K.conv2d_fwd(x, w, bias, stride, pad, z, None)
         return False
-    stats = bn_part is not None and BN_STATS_IN_EPILOGUE and bias is None and C % 8 == 0 and Co % 8 == 0
+    stats = bn_part is not None and BN_STATS_IN_EPILOGUE and C % 8 == 0 and Co % 8 == 0
     if KH == KW == 1 and stride == 1 and pad == 0:
         M = N * H * W
         if stats:
-            K.gemm_bnstats(M, Co, C, x, w, z, bn_part)
+            K.gemm_bnstats(M, Co, C, x, w, z, bn_part, bias)
             return True
         K.gemm(M, Co, C, x, C, 1, w, C, 1, 0, z, Co, bias, 0, 1)
         return False

@@ -344,8 +344,7 @@ class Sequential:
         d1, d2 = ops[-2], ops[-1]
         return (isinstance(d1, E.DenseOp) and isinstance(d2, E.DenseOp) and d1.big and not d2.big
                 and d1.act == "relu" and d2.act in (None, "linear") and d1.dense.bias is not None
-                and d2.dense.bias is not None and d2.dense.units <= 4 and not d1.first
-                and d1.dense.units * (d2.dense.units + 1) * 4 <= 64 * 1024)
+                and d2.dense.bias is not None and d2.dense.units <= 4 and not d1.first)
 
     def _train_step_fused_head(self, xb, yb, stats, st) -> None:
         d1, d2 = self.ops[-2], self.ops[-1]
@@ -353,8 +352,10 @@ class Sequential:
         acc = d1.forward_splitk_sums(x, self.ws)
         B, K1 = acc.shape
         dz1 = self.ws.get(d1.name + "/dz", (B, K1), torch.bfloat16, acc.device)
+        N2 = d2.dense.units
+        scratch = self.ws.get(d1.name + "/headscratch", (B * (N2 + 2),), torch.float32, acc.device)
         K.head_mse(acc, d1.dense.bias.data, d2.dense.kernel.data, d2.dense.bias.data, yb.contiguous(), dz1,
-                   d2.dense.kernel.grad, d2.dense.bias.grad, d1.dense.bias.grad, stats)
+                   d2.dense.kernel.grad, d2.dense.bias.grad, d1.dense.bias.grad, stats, scratch=scratch)
         fused = self._begin_fused_update(st)
         try:
             dx = d1.backward_dz(dz1, self.ws)

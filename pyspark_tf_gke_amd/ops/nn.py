@@ -32,7 +32,7 @@ def conv_out_size(h: int, k: int, stride: int, pad: int) -> int:
 # ----------------------------------------------------------------------------------------------
 def conv2d_fwd(x, w, bias, stride: int, pad: int, out, act: str | None = None, bn_part=None):
     """out[N,OH,OW,Cout] (bf16) = act(conv(x, w) + bias).  ``bn_part`` ([BN_G, 2, Cout] fp32, GPU,
-    C % 8 == 0, no bias/act): the GEMM epilogue also accumulates the BatchNormalization statistics of
+    C % 8 == 0, no act): the GEMM epilogue also accumulates the BatchNormalization statistics of
     ``out`` (returns True when it did, so the caller skips bn_stats)."""
     if not on_device(x):
         return ref.conv2d_fwd(x, w, bias, stride, pad, out, act)
@@ -43,16 +43,16 @@ def conv2d_fwd(x, w, bias, stride: int, pad: int, out, act: str | None = None, b
     assert tuple(out.shape) == (N, OH, OW, Cout), (out.shape, (N, OH, OW, Cout))
     need(x, torch.bfloat16, "conv2d_fwd.x"); need(w, torch.bfloat16, "conv2d_fwd.w")
     need(out, torch.bfloat16, "conv2d_fwd.out")
-    use_stats = bn_part is not None and C % 8 == 0 and bias is None and not ACT[act] and Cout % 8 == 0
+    use_stats = bn_part is not None and C % 8 == 0 and not ACT[act] and Cout % 8 == 0
     hip("ptg_conv2d_fwd", ptr(x), ptr(w), ptr(bias), ptr(out), N, H, W, C, Cout, KH, KW, stride, pad,
         OH, OW, ACT[act], ptr(bn_part) if use_stats else None)
     return use_stats if bn_part is not None else out
 
 
-def gemm_bnstats(M, N, K, a, b, c, part):
-    """c[M,N] bf16 = a[M,K] @ b[N,K]^T with the BatchNormalization statistics of c accumulated into
-    ``part`` [BN_G, 2, N] (1x1 stride-1 convolution + bn_stats in one kernel)."""
-    hip("ptg_gemm_bf16_bnstats", M, N, K, ptr(a), K, ptr(b), K, ptr(c), N, ptr(part))
+def gemm_bnstats(M, N, K, a, b, c, part, bias=None):
+    """c[M,N] bf16 = a[M,K] @ b[N,K]^T (+ bias) with the BatchNormalization statistics of c accumulated
+    into ``part`` [BN_G, 2, N] (1x1 stride-1 convolution + bn_stats in one kernel)."""
+    hip("ptg_gemm_bf16_bnstats", M, N, K, ptr(a), K, ptr(b), K, ptr(c), N, ptr(bias), ptr(part))
 
 
 def conv2d_dgrad(dz, w, pad: int, out, accumulate: bool = False):
@@ -307,13 +307,15 @@ def linear_dw_adam(dy, x, p, m, v, pbf, lr_t: float, b1: float, b2: float, eps: 
         float(lr_t), float(b1), float(b2), float(eps), float(gscale), ptr(lr_dev))
 
 
-def head_mse(acc, b1, w2, b2, tgt, dz1, dw2, db2, db1, stats, pred_out=None, gscale: float = 1.0):
+def head_mse(acc, b1, w2, b2, tgt, dz1, dw2, db2, db1, stats, pred_out=None, gscale: float = 1.0, scratch=None):
     """Fused Dense(relu) -> Dense(N2) -> MSE head on the Dense1 split-K sums ``acc`` [B, K1] (fp32,
     re-zeroed): stats / dpred as mse_k, dz1 [B, K1] bf16, dw2 / db2 / db1 accumulated (GPU only)."""
     B, K1 = acc.shape
     N2 = w2.shape[0]
+    if scratch is None or scratch.numel() < B * (N2 + 2):
+        scratch = torch.empty(B * (N2 + 2), dtype=torch.float32, device=acc.device)
     hip("ptg_head_mse", ptr(acc), ptr(b1), ptr(w2), ptr(b2), ptr(tgt), ptr(dz1), ptr(dw2), ptr(db2), ptr(db1),
-        ptr(stats), ptr(pred_out), B, K1, N2, float(gscale))
+        ptr(stats), ptr(pred_out), ptr(scratch), B, K1, N2, float(gscale))
 
 
 def col_sum(g, out):

@@ -551,15 +551,16 @@ def test_bn_statistics_in_gemm_epilogue(kind, M, N, KD):
     part = KB.part_buffer(N, DEV)
     if kind == "gemm":
         a, b = rnd(M, KD), rnd(N, KD)
+        bias = torch.randn(N)
         z = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
-        K.gemm_bnstats(M, N, KD, a.to(DEV), b.to(DEV), z, part)
-        ref = (a.float() @ b.float().t())
+        K.gemm_bnstats(M, N, KD, a.to(DEV), b.to(DEV), z, part, bias.to(DEV))
+        ref = (a.float() @ b.float().t()) + bias
         _close(z, ref, 2e-2, 2e-2, "gemm_bnstats z")
     else:
         B, H = M, 28
         x, w = rnd(B, H, H, KD), rnd(N, 3, 3, KD, scale=0.1)
         z = torch.empty(B, H, H, N, device=DEV, dtype=torch.bfloat16)
-        assert K.conv2d_fwd(x.to(DEV), w.to(DEV), None, 1, 1, z, None, bn_part=part) is True
+        assert K.conv2d_fwd(x.to(DEV), w.to(DEV), torch.randn(N).to(DEV), 1, 1, z, None, bn_part=part) is True
     zf = z.float().reshape(-1, N)
     s, q = part[:, 0, :].sum(0), part[:, 1, :].sum(0)
     assert torch.allclose(s, zf.sum(0), rtol=1e-3, atol=1e-2 * zf.shape[0] ** 0.5)
