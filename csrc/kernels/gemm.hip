@@ -224,53 +224,6 @@ struct EpiBf16 {  // out[m*ldc+n] = act(acc + bias[n]) (+ out if accum) as bf16 
     bf16_store8(out + (long)m * ldc + n, v, cnt, accum);
   }
 };
-// EpiBf16 + the training BatchNormalization statistics of the stored (bf16-rounded) outputs: the
-// kernel sums every stored value and its square per output channel and flushes one atomic per
-// (channel, sum) per workgroup into part[blockIdx % BN_GROUPS][0|1][N] — the layout bn_stats_k
-// writes, so bn_finalize_k consumes it unchanged and the separate statistics pass over z is gone.
-constexpr int BN_GROUPS = 64;  // BN_G in bn.hip
-struct EpiBf16Stats {
-  static constexpr bool VEC = true;
-  static constexpr bool STATS = true;
-  bf16_t* out; long ldc; float* part; int C; const float* bias;
-  PTG_DEV void operator()(int m, int n, float v) const { out[(long)m * ldc + n] = f2bf(v + (bias ? bias[n] : 0.f)); }
-  // stores the 8 values (+ bias) and leaves their bf16-rounded form in v (the statistics see what
-  // is stored)
-  PTG_DEV void vec8(int m, int n, float* v, int cnt) const {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = j < cnt ? bf2f(f2bf(v[j] + (bias ? bias[n + j] : 0.f))) : 0.f;
-    bf16_store8(out + (long)m * ldc + n, v, cnt, false);
-  }
-};
-template <class E, class = void> struct EpiStats { static constexpr bool v = false; };
-template <class E> struct EpiStats<E, std::void_t<decltype(E::STATS)>> { static constexpr bool v = E::STATS; };
-
-// per-thread [8] channel partials -> LDS -> one atomic per (channel, array) per workgroup.
-// Threads tid and tid + k*NG share the 8 channels of column group (tid % NG).
-template <int NT, int NG>
-PTG_DEV void flush_bn_stats(float* red, const float* s, const float* q, int n0, int N, float* part, int C) {
-  const int tid = threadIdx.x;
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < 8; ++j) { red[tid * 16 + j] = s[j]; red[tid * 16 + 8 + j] = q[j]; }
-  __syncthreads();
-  if (tid < NG) {
-    float as[8], aq[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) { as[j] = 0.f; aq[j] = 0.f; }
-    for (int r = tid; r < NT; r += NG) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) { as[j] += red[r * 16 + j]; aq[j] += red[r * 16 + 8 + j]; }
-    }
-    float* p = part + (long)(blockIdx.x % BN_GROUPS) * 2 * C;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int n = n0 + tid * 8 + j;
-      if (n < N) { atomicAdd(p + n, as[j]); atomicAdd(p + C + n, aq[j]); }
-    }
-  }
-}
-
 // Strided scatter (dgrad of a 1x1 stride-s conv): GEMM row m = output pixel (n, oh, ow) lands on
 // input pixel (n, oh*s, ow*s) of an [N][H][W][ldc] tensor; the other input pixels are untouched.
 struct EpiBf16Remap {
@@ -600,9 +553,6 @@ __global__ __launch_bounds__(256) void gemm_kernel(LA la, LB lb, EPI epi, int M,
     }
     return;
   }
-  float bs_s[8], bs_q[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) { bs_s[j] = 0.f; bs_q[j] = 0.f; }
 #pragma unroll
   for (int v0 = 0; v0 < NV; v0 += 256) {
     const int v = v0 + tid;
@@ -613,14 +563,6 @@ __global__ __launch_bounds__(256) void gemm_kernel(LA la, LB lb, EPI epi, int M,
     const float4 a = *(const float4*)(cs + row * CP + c8 * 8), b = *(const float4*)(cs + row * CP + c8 * 8 + 4);
     float vals[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
     epi.vec8(m, n, vals, min(8, N - n));
-    if constexpr (EpiStats<EPI>::v) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) { bs_s[j] += vals[j]; bs_q[j] = fmaf(vals[j], vals[j], bs_q[j]); }
-    }
-  }
-  if constexpr (EpiStats<EPI>::v) {
-    static_assert(NV % 256 == 0 && 256 % (BN / 8) == 0, "stats epilogue: whole 8-column groups per thread");
-    flush_bn_stats<256, BN / 8>(cs, bs_s, bs_q, n0, N, epi.part, epi.C);
   }
 }
 
@@ -738,9 +680,6 @@ __global__ __launch_bounds__(512) void gemm256_kernel(LA la, LB lb, EPI epi, int
     // 4 passes of 64 rows through LDS: each thread then hands 8 consecutive columns to the epilogue
     constexpr int CP = TN + 4;
     float* cs = reinterpret_cast<float*>(smem);
-    float bs_s[8], bs_q[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) { bs_s[j] = 0.f; bs_q[j] = 0.f; }
 #pragma unroll
     for (int pass = 0; pass < 4; ++pass) {
       if (wm == (pass >> 1)) {
@@ -764,15 +703,10 @@ __global__ __launch_bounds__(512) void gemm256_kernel(LA la, LB lb, EPI epi, int
           const float4 a = *(const float4*)(cs + row * CP + c8 * 8), b = *(const float4*)(cs + row * CP + c8 * 8 + 4);
           float vals[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
           epi.vec8(m, n, vals, min(8, N - n));
-          if constexpr (EpiStats<EPI>::v) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) { bs_s[j] += vals[j]; bs_q[j] = fmaf(vals[j], vals[j], bs_q[j]); }
-          }
         }
       }
       __syncthreads();
     }
-    if constexpr (EpiStats<EPI>::v) flush_bn_stats<512, TN / 8>(cs, bs_s, bs_q, n0, N, epi.part, epi.C);
   }
 }
 
@@ -907,18 +841,6 @@ int ptg_gemm_bf16(int M, int N, int K, const void* A, long lda, int a_kcontig, c
 #undef PTG_EPI_SWITCH
 }
 
-// bf16 GEMM with k-contiguous A and B (1x1 stride-1 convolution) whose epilogue also accumulates the
-// BatchNormalization statistics of its output into part [BN_GROUPS][2][N] (EpiBf16Stats).
-int ptg_gemm_bf16_bnstats(int M, int N, int K, const void* A, long lda, const void* B, long ldb, void* C, long ldc,
-                          const float* bias, float* part, hipStream_t s) {
-  if (M <= 0 || N <= 0 || K <= 0) return 0;
-  if (lda % 8 || ldb % 8 || K % 8 || N % 8) return (int)hipErrorInvalidValue;
-  if (!fits(matk_bytes(lda, M, K)) || !fits(matk_bytes(ldb, N, K))) return (int)hipErrorInvalidValue;
-  MatK<8> la{(const bf16_t*)A, lda, M, K, (uint32_t)matk_bytes(lda, M, K)};
-  MatK<8> lb{(const bf16_t*)B, ldb, N, K, (uint32_t)matk_bytes(ldb, N, K)};
-  return dispatch_gemm(la, lb, EpiBf16Stats{(bf16_t*)C, ldc, part, N, bias}, M, N, K, 1, s);
-}
-
 // Weight gradient with Adam fused into the epilogue (EpiAdam): G[M][N] = A^T-style product as in
 // ptg_gemm_bf16 (same operand conventions, no split-K), then p/m/v/pbf[m*ldc+n] updated in place.
 int ptg_gemm_adam(int M, int N, int K, const void* A, long lda, int a_kcontig, const void* B, long ldb,
@@ -934,9 +856,8 @@ int ptg_gemm_adam(int M, int N, int K, const void* A, long lda, int a_kcontig, c
 
 // Conv2D forward, NHWC bf16: z[n][oh][ow][co] = bias[co] + sum_{kh,kw,ci} x[..] w[co][kh][kw][ci]
 // w is [Cout][KH*KW*C] bf16. C must be a power of two >= 4.
-// bn_part (optional, C % 8 == 0, no act): also accumulate the BatchNormalization statistics of z
 int ptg_conv2d_fwd(const void* x, const void* w, const float* bias, void* z, int N, int H, int W, int C,
-                   int Cout, int KH, int KW, int stride, int pad, int OH, int OW, int act, float* bn_part,
+                   int Cout, int KH, int KW, int stride, int pad, int OH, int OW, int act,
                    hipStream_t s) {
   if (!is_pow2(C) || C < 4) return (int)hipErrorInvalidValue;
   const int M = N * OH * OW, Kc = KH * KW * C;
@@ -946,8 +867,6 @@ int ptg_conv2d_fwd(const void* x, const void* w, const float* bias, void* z, int
     ConvFwdA<8> la{(const bf16_t*)x, H, W, C, ilog2(C), OH, OW, KW, stride, pad, M, Kc};
     la.init();
     MatK<8> lb{(const bf16_t*)w, Kc, Cout, Kc, (uint32_t)matk_bytes(Kc, Cout, Kc)};
-    if (bn_part && !act && Cout % 8 == 0)
-      return dispatch_gemm(la, lb, EpiBf16Stats{(bf16_t*)z, Cout, bn_part, Cout, bias}, M, Cout, Kc, 1, s);
     return dispatch_gemm(la, lb, epi, M, Cout, Kc, 1, s);
   } else {
     ConvFwdA<4> la{(const bf16_t*)x, H, W, C, ilog2(C), OH, OW, KW, stride, pad, M, Kc};

@@ -96,33 +96,19 @@ class GraphOp:
 # with 4-64 channels; measured on ResNet-50's 3x3/64-channel layers (56x56, batch 128) the
 # implicit-GEMM path is faster, so graph ops use the halo kernels for 5x5 only.
 HALO_KS = (5,)
-BN_STATS_IN_EPILOGUE = __import__("os").environ.get("PTG_BN_EPI_STATS", "1") != "0"
-
-
-def conv_forward(x, w, bias, stride, pad, z, bn_part=None):
-    """Returns True when the BatchNormalization statistics of z were accumulated into ``bn_part``
-    by the conv GEMM's epilogue (the caller then skips the bn_stats pass)."""
+def conv_forward(x, w, bias, stride, pad, z):
     N, H, W, C = x.shape
     Co, KH, KW, _ = w.shape
     if not K.on_device(x):
-        K.conv2d_fwd(x, w, bias, stride, pad, z, None)
-        return False
-    stats = bn_part is not None and BN_STATS_IN_EPILOGUE and C % 8 == 0 and Co % 8 == 0
+        return K.conv2d_fwd(x, w, bias, stride, pad, z, None)
     if KH == KW == 1 and stride == 1 and pad == 0:
         M = N * H * W
-        if stats:
-            K.gemm_bnstats(M, Co, C, x, w, z, bn_part, bias)
-            return True
         K.gemm(M, Co, C, x, C, 1, w, C, 1, 0, z, Co, bias, 0, 1)
-        return False
+        return z
     same = pad == KH // 2 and KH == KW and stride == 1
     if KH in HALO_KS and K.halo_eligible(C, Co, KH, stride, same):
-        K.conv2d_fwd_fused(x, w, bias, pad, z)
-        return False
-    if stats:
-        return bool(K.conv2d_fwd(x, w, bias, stride, pad, z, None, bn_part=bn_part))
-    K.conv2d_fwd(x, w, bias, stride, pad, z, None)
-    return False
+        return K.conv2d_fwd_fused(x, w, bias, pad, z)
+    return K.conv2d_fwd(x, w, bias, stride, pad, z, None)
 
 
 def conv_wgrad(x, dz, stride, pad, dw):
@@ -175,14 +161,14 @@ class _BNState:
                 ws.get(self.name + "/bn_mean", (C,), f, dev), ws.get(self.name + "/bn_rstd", (C,), f, dev),
                 ws.get(self.name + "/bn_coef", (3, C), f, dev))
 
-    def forward(self, z, res, relu, y, ws, training, stats_done=False):
+    def forward(self, z, res, relu, y, ws, training):
         bn = self.bn
         C = z.shape[-1]
         M = z.numel() // C
         part, scale, shift, mean, rstd, _ = self.bufs(ws, C, z.device)
         g = bn.gamma.data if bn.gamma is not None else None
         b = bn.beta.data if bn.beta is not None else None
-        if training and not stats_done:
+        if training:
             KB.bn_stats(z, part)
         KB.bn_finalize(part, M, g, b, bn.epsilon, bn.momentum if training else -1.0, bn.moving_mean,
                        bn.moving_variance, scale, shift, mean, rstd, training)
@@ -243,10 +229,9 @@ class ConvBNOp:
         dev = x.device
         z = ws.get(self.name + "/z", (B, OH, OW, Co), torch.bfloat16, dev)
         b = self.conv.bias.data if self.conv.bias is not None else None
-        part = self.state.bufs(ws, Co, dev)[0] if training else None
-        done = conv_forward(x, self.conv.kernel.bf16, b, self.stride, self.pad, z, bn_part=part)
+        conv_forward(x, self.conv.kernel.bf16, b, self.stride, self.pad, z)
         y = ws.get(self.name + "/y", z.shape, torch.bfloat16, dev)
-        self.state.forward(z, res, self.relu, y, ws, training, stats_done=done)
+        self.state.forward(z, res, self.relu, y, ws, training)
         self._x, self._z, self._y = x, z, y
         return y
 

@@ -30,10 +30,8 @@ def conv_out_size(h: int, k: int, stride: int, pad: int) -> int:
 # ----------------------------------------------------------------------------------------------
 # Convolution (implicit GEMM on MFMA)
 # ----------------------------------------------------------------------------------------------
-def conv2d_fwd(x, w, bias, stride: int, pad: int, out, act: str | None = None, bn_part=None):
-    """out[N,OH,OW,Cout] (bf16) = act(conv(x, w) + bias).  ``bn_part`` ([BN_G, 2, Cout] fp32, GPU,
-    C % 8 == 0, no act): the GEMM epilogue also accumulates the BatchNormalization statistics of
-    ``out`` (returns True when it did, so the caller skips bn_stats)."""
+def conv2d_fwd(x, w, bias, stride: int, pad: int, out, act: str | None = None):
+    """out[N,OH,OW,Cout] (bf16) = act(conv(x, w) + bias)."""
     if not on_device(x):
         return ref.conv2d_fwd(x, w, bias, stride, pad, out, act)
     N, H, W, C = x.shape
@@ -43,16 +41,9 @@ def conv2d_fwd(x, w, bias, stride: int, pad: int, out, act: str | None = None, b
     assert tuple(out.shape) == (N, OH, OW, Cout), (out.shape, (N, OH, OW, Cout))
     need(x, torch.bfloat16, "conv2d_fwd.x"); need(w, torch.bfloat16, "conv2d_fwd.w")
     need(out, torch.bfloat16, "conv2d_fwd.out")
-    use_stats = bn_part is not None and C % 8 == 0 and not ACT[act] and Cout % 8 == 0
     hip("ptg_conv2d_fwd", ptr(x), ptr(w), ptr(bias), ptr(out), N, H, W, C, Cout, KH, KW, stride, pad,
-        OH, OW, ACT[act], ptr(bn_part) if use_stats else None)
-    return use_stats if bn_part is not None else out
-
-
-def gemm_bnstats(M, N, K, a, b, c, part, bias=None):
-    """c[M,N] bf16 = a[M,K] @ b[N,K]^T (+ bias) with the BatchNormalization statistics of c accumulated
-    into ``part`` [BN_G, 2, N] (1x1 stride-1 convolution + bn_stats in one kernel)."""
-    hip("ptg_gemm_bf16_bnstats", M, N, K, ptr(a), K, ptr(b), K, ptr(c), N, ptr(bias), ptr(part))
+        OH, OW, ACT[act])
+    return out
 
 
 def conv2d_dgrad(dz, w, pad: int, out, accumulate: bool = False):

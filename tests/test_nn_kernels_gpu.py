@@ -538,30 +538,3 @@ def test_conv_fwd_gemm256_resnet_layer():
     K.conv2d_fwd(x.to(DEV), w.to(DEV), b.to(DEV), 1, 1, out)
     ref = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), b, padding=1)
     _close(out, ref.permute(0, 2, 3, 1), 2e-2, 2e-2, "conv_fwd_256")
-
-
-@pytest.mark.parametrize("kind,M,N,KD", [("gemm", 4096, 256, 64), ("gemm", 1000, 64, 128), ("gemm", 50176, 256, 64),
-                                         ("conv3x3", 8, 64, 64), ("conv3x3", 32, 128, 128)])
-def test_bn_statistics_in_gemm_epilogue(kind, M, N, KD):
-    """Conv / 1x1 GEMM epilogue with the BatchNormalization statistics (EpiBf16Stats, both GEMM
-    kernels): the [BN_G, 2, C] partial sums total the per-channel sum and sum of squares of the
-    stored bf16 output (what bn_stats_k computes from it)."""
-    from pyspark_tf_gke_amd.ops import bn as KB
-
-    part = KB.part_buffer(N, DEV)
-    if kind == "gemm":
-        a, b = rnd(M, KD), rnd(N, KD)
-        bias = torch.randn(N)
-        z = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
-        K.gemm_bnstats(M, N, KD, a.to(DEV), b.to(DEV), z, part, bias.to(DEV))
-        ref = (a.float() @ b.float().t()) + bias
-        _close(z, ref, 2e-2, 2e-2, "gemm_bnstats z")
-    else:
-        B, H = M, 28
-        x, w = rnd(B, H, H, KD), rnd(N, 3, 3, KD, scale=0.1)
-        z = torch.empty(B, H, H, N, device=DEV, dtype=torch.bfloat16)
-        assert K.conv2d_fwd(x.to(DEV), w.to(DEV), torch.randn(N).to(DEV), 1, 1, z, None, bn_part=part) is True
-    zf = z.float().reshape(-1, N)
-    s, q = part[:, 0, :].sum(0), part[:, 1, :].sum(0)
-    assert torch.allclose(s, zf.sum(0), rtol=1e-3, atol=1e-2 * zf.shape[0] ** 0.5)
-    assert torch.allclose(q, (zf * zf).sum(0), rtol=1e-3, atol=1e-2 * zf.shape[0] ** 0.5)
