@@ -267,7 +267,8 @@ def run_image_training(data_dir: str, output_dir: str, epochs: int, batch_size: 
                                       validation_split=val_split, subset="training", seed=seed, repeat=True,
                                       cache=cache)
         ds_val = make_image_dataset(data_dir, (img_height, img_width), batch_size, shuffle=False,
-                                    validation_split=val_split, subset="validation", seed=seed, repeat=False)
+                                    validation_split=val_split, subset="validation", seed=seed, repeat=False,
+                                    cache=cache)
         ctx = strategy.scope() if strategy is not None else _null()
         with ctx:
             model = build_cnn_model(shape, num_outputs=2, flat=flat_layer, summary=True,

@@ -90,7 +90,7 @@ for task in "$@"; do
         --output-dir /tmp/mnist > gpurun_out/mnist.log 2>&1 || fail mnist gpurun_out/mnist.log
       tail -3 gpurun_out/mnist.log
       timeout -k 10 $STEP_T python workloads/raw-tf/train_tf_ps.py --data-is-images --synthetic ${E2E_IMAGES:-4096} \
-        --data-path /tmp/imgs --epochs 3 --batch-size 256 --cache-decoded --output-dir /tmp/cnn \
+        --data-path /tmp/imgs --epochs ${E2E_EPOCHS:-6} --batch-size 256 --cache-decoded --output-dir /tmp/cnn \
         > gpurun_out/train_images.log 2>&1 || fail images gpurun_out/train_images.log
       grep -E "Epoch|samples/s" gpurun_out/train_images.log | tail -6 ;;
     *) echo "unknown task $task"; exit 2 ;;
