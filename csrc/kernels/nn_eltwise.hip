@@ -77,127 +77,12 @@ PTG_DEV void bias_reduce_atomic(float db[8], int c8, int C8, float* sred, float*
               sred[threadIdx.x] + sred[256 + threadIdx.x] + sred[512 + threadIdx.x] + sred[768 + threadIdx.x]);
 }
 
-// Backward of prelu+pool. Grid: x over pooled (ph, pw, c8) vectors, y over batch chunks; samples
-// are processed two at a time so 10 independent 16-byte loads are in flight per lane.
-// dz is written for every element (zero where not the window's first argmax).
-// dalpha[h][w][c] += sum_n dA * min(z,0)  (dA = routed pooled gradient), dbias[c] += sum dz.
-__global__ __launch_bounds__(256) void prelu_pool_bwd_k(const bf16_t* __restrict__ dp,
-                                                        const bf16_t* __restrict__ z,
-                                                        const float* __restrict__ alpha,
-                                                        bf16_t* __restrict__ dz, float* __restrict__ dalpha,
-                                                        float* __restrict__ dbias, int N, int H, int W,
-                                                        int C, int nper) {
-  __shared__ float sred[4 * 256];
-  __shared__ float sda[256 * 32];
-  const int PH = H >> 1, PW = W >> 1, C8 = C >> 3;
-  const int npos = PH * PW * C8;
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  const int n0 = blockIdx.y * nper, n1 = min(N, n0 + nper);
-  float db[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  const bool active = i < npos;
-  const int c8 = active ? i % C8 : 0;
-  const int t = active ? i / C8 : 0;
-  const int pw = t % PW, ph = t / PW;
-  long zoff[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) zoff[q] = ((long)(2 * ph + (q >> 1)) * W + 2 * pw + (q & 1)) * C + c8 * 8;
-  const long HWC = (long)H * W * C, PHWC = (long)PH * PW * C;
-  const long poff = ((long)ph * PW + pw) * C + c8 * 8;
-  if (active) {
-    float da[4][8], av[4][8];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float4 a0 = *(const float4*)(alpha + zoff[q]), a1 = *(const float4*)(alpha + zoff[q] + 4);
-      av[q][0] = a0.x; av[q][1] = a0.y; av[q][2] = a0.z; av[q][3] = a0.w;
-      av[q][4] = a1.x; av[q][5] = a1.y; av[q][6] = a1.z; av[q][7] = a1.w;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) da[q][j] = 0.f;
-    }
-    const bool lastw = (W & 1) && pw == PW - 1, lasth = (H & 1) && ph == PH - 1;
-    for (int n = n0; n < n1; n += 2) {
-      const bool two = n + 1 < n1;
-      U4 graw[2], zraw[2][4];
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int nn = (u == 0 || two) ? n + u : n;
-        graw[u] = *(const U4*)(dp + nn * PHWC + poff);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) zraw[u][q] = *(const U4*)(z + nn * HWC + zoff[q]);
-      }
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        if (u == 1 && !two) break;
-        const long nb = (long)(n + u) * HWC;
-        float g[8], zv[4][8], y[4][8];
-        unpack8(graw[u], g);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          unpack8(zraw[u][q], zv[q]);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) y[q][j] = zv[q][j] > 0.f ? zv[q][j] : av[q][j] * zv[q][j];
-        }
-        int arg[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          int a = 0; float b = y[0][j];
-#pragma unroll
-          for (int q = 1; q < 4; ++q)
-            if (y[q][j] > b) { b = y[q][j]; a = q; }
-          arg[j] = a;
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          float o[8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float gq = (arg[j] == q) ? g[j] : 0.f;
-            const float zz = zv[q][j];
-            o[j] = zz > 0.f ? gq : gq * av[q][j];
-            da[q][j] += zz > 0.f ? 0.f : gq * zz;
-            db[j] += o[j];
-          }
-          *(U4*)(dz + nb + zoff[q]) = pack8(o);
-        }
-        // odd H/W (floor pooling): the last row/column belongs to no window -> zero gradient
-        if (lastw || lasth) {
-          const U4 zz = zero4();
-          bf16_t* d = dz + nb + c8 * 8;
-          if (lastw) {
-            *(U4*)(d + ((long)(2 * ph) * W + W - 1) * C) = zz;
-            *(U4*)(d + ((long)(2 * ph + 1) * W + W - 1) * C) = zz;
-          }
-          if (lasth) {
-            *(U4*)(d + ((long)(H - 1) * W + 2 * pw) * C) = zz;
-            *(U4*)(d + ((long)(H - 1) * W + 2 * pw + 1) * C) = zz;
-          }
-          if (lastw && lasth) *(U4*)(d + ((long)(H - 1) * W + W - 1) * C) = zz;
-        }
-      }
-    }
-    // stage in LDS ordered (qh, thread, qw, j) ~ global order, so each atomic wave-instruction
-    // below covers ~256 contiguous bytes instead of 64 scattered 32-byte runs
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) sda[(((q >> 1) * 256 + threadIdx.x) * 2 + (q & 1)) * 8 + j] = da[q][j];
-  }
-  __syncthreads();
-  for (int k = 0; k < 32; ++k) {
-    const int L = k * 256 + threadIdx.x;
-    const int j = L & 7, qw = (L >> 3) & 1, tt = (L >> 4) & 255, qh = L >> 12;
-    const int ii = blockIdx.x * 256 + tt;
-    if (ii >= npos) continue;
-    const int cc = ii % C8, tq = ii / C8, pww = tq % PW, phh = tq / PW;
-    atomicAdd(dalpha + ((long)(2 * phh + qh) * W + 2 * pww + qw) * C + cc * 8 + j, sda[L]);
-  }
-  bias_reduce_atomic(db, c8, C8, sred, dbias);
-}
-
 // Backward of prelu+pool, sample-parallel inside the block: 256 threads = 16 pooled positions x 16
 // sample groups, so a block owns its 16 positions over a whole batch chunk and reduces dalpha over
 // the sample groups in LDS.  Large layers run one chunk (dalpha += without atomics: no other block
 // touches those elements); small layers split the batch over a few chunks and add with atomics.
-// (prelu_pool_bwd_k adds every block's dalpha partial with fp32 atomics: ~17M per layer at batch 256.)
+// (the rejected per-block variant added every block's dalpha partial with fp32 atomics: ~17M per
+// layer at batch 256.)
 template <int CH>
 __global__ __launch_bounds__(256, 4) void prelu_pool_bwd_sg_k(const bf16_t* __restrict__ dp,
                                                            const bf16_t* __restrict__ z,
@@ -348,7 +233,7 @@ __global__ __launch_bounds__(256, 4) void prelu_pool_bwd_sg_k(const bf16_t* __re
 
 // Backward of prelu+pool from the sparse forward record (conv.hip EPI_POOLS): per pooled element the
 // argmax position q (uint8) and the z there (bf16).  dz is dense (zero off the argmax), dalpha and
-// dbias as in prelu_pool_bwd_k.  Reads dp + zsel + arg (2.5 B per pooled element) instead of the
+// dbias as in prelu_pool_bwd_sg_k.  Reads dp + zsel + arg (2.5 B per pooled element) instead of the
 // four z values of each window (8 B).
 __global__ __launch_bounds__(256) void prelu_pool_bwd_sparse_k(const bf16_t* __restrict__ dp,
                                                                const bf16_t* __restrict__ zs,
@@ -557,63 +442,10 @@ __global__ __launch_bounds__(256) void prelu_fwd_k(const bf16_t* __restrict__ z,
   }
 }
 
-// PReLU backward (no pool). Grid x over per-sample 8-vectors, y over batch chunks (two samples
-// in flight per iteration).
-__global__ __launch_bounds__(256) void prelu_bwd_k(const bf16_t* __restrict__ da,
-                                                   const bf16_t* __restrict__ z,
-                                                   const float* __restrict__ alpha,
-                                                   bf16_t* __restrict__ dz, float* __restrict__ dalpha,
-                                                   float* __restrict__ dbias, int N, int HWC, int C,
-                                                   int nper) {
-  __shared__ float sred[4 * 256];
-  __shared__ float sda[2048];
-  const int HWC8 = HWC >> 3;
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  const int n0 = blockIdx.y * nper, n1 = min(N, n0 + nper);
-  float db[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if (i < HWC8) {
-    const long e = (long)i * 8;
-    const float4 a0 = *(const float4*)(alpha + e), a1 = *(const float4*)(alpha + e + 4);
-    const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-    float dal[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int n = n0; n < n1; n += 2) {
-      const bool two = n + 1 < n1;
-      const long off0 = (long)n * HWC + e, off1 = two ? off0 + HWC : off0;
-      const U4 g0 = *(const U4*)(da + off0), z0 = *(const U4*)(z + off0);
-      const U4 g1 = *(const U4*)(da + off1), z1 = *(const U4*)(z + off1);
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        if (u == 1 && !two) break;
-        float g[8], zv[8], o[8];
-        unpack8(u ? g1 : g0, g);
-        unpack8(u ? z1 : z0, zv);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          o[j] = zv[j] > 0.f ? g[j] : g[j] * av[j];
-          dal[j] += zv[j] > 0.f ? 0.f : g[j] * zv[j];
-          db[j] += o[j];
-        }
-        *(U4*)(dz + (u ? off1 : off0)) = pack8(o);
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) sda[threadIdx.x * 8 + j] = dal[j];
-  }
-  __syncthreads();
-  // the block's 2048 dalpha values are contiguous: coalesced atomics
-  for (int k = 0; k < 8; ++k) {
-    const int L = k * 256 + threadIdx.x;
-    const long e = (long)blockIdx.x * 2048 + L;
-    if (e < HWC) atomicAdd(dalpha + e, sda[L]);
-  }
-  // channel group of this thread: i % (C/8) (== tid % (C/8) when C/8 is a power of two)
-  bias_reduce_atomic(db, i % (C >> 3), C >> 3, sred, dbias);
-}
-
 // PReLU backward, sample-parallel (the prelu_pool_bwd_sg_k layout without the pool): a block owns
 // 16 8-element positions over a batch chunk split into 16 sample groups and reduces dalpha over the
 // groups in LDS - one dalpha add per element and chunk instead of one fp32 atomic per element and
-// sample pair (prelu_bwd_k: 2.6M contended atomics for CNN-B1's last conv layer at batch 256).
+// sample pair (the rejected per-pair variant: 2.6M contended atomics for CNN-B1's last conv layer at batch 256).
 __global__ __launch_bounds__(256) void prelu_bwd_sg_k(const bf16_t* __restrict__ da, const bf16_t* __restrict__ z,
                                                       const float* __restrict__ alpha, bf16_t* __restrict__ dz,
                                                       float* __restrict__ dalpha, float* __restrict__ dbias, int N,
@@ -1068,11 +900,6 @@ __global__ __launch_bounds__(256) void cast_f32_bf16_k(const float* __restrict__
                                                        long n) {
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) y[i] = f2bf(x[i]);
 }
-__global__ __launch_bounds__(256) void cast_bf16_f32_k(const bf16_t* __restrict__ x, float* __restrict__ y,
-                                                       long n) {
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) y[i] = bf2f(x[i]);
-}
-
 // Bilinear resize (tf.image.resize: half-pixel centres, no antialias) of uint8 NHWC (3 ch) images,
 // scaled by 1/255, written as 4-channel NHWC bf16 (4th channel 0 = MFMA-friendly padding).
 __global__ __launch_bounds__(256) void resize_norm_k(const uint8_t* __restrict__ in, bf16_t* __restrict__ out,
@@ -1220,22 +1047,6 @@ int ptg_prelu_pool_fwd(const void* z, const float* alpha, void* p, int N, int H,
   PTG_RETURN_LAUNCH();
 }
 
-int ptg_prelu_pool_bwd(const void* dp, const void* z, const float* alpha, void* dz, float* dalpha,
-                       float* dbias, int N, int H, int W, int C, int nper, hipStream_t s) {
-  if (C % 8 || C > 256 || H < 2 || W < 2) return (int)hipErrorInvalidValue;
-  const int npos = (H / 2) * (W / 2) * (C / 8);
-  if (nper <= 0) {
-    const int bx = (npos + 255) / 256;
-    int chunks = (2048 + bx - 1) / bx;
-    if (chunks > N) chunks = N;
-    nper = (N + chunks - 1) / chunks;
-  }
-  dim3 grid((npos + 255) / 256, (N + nper - 1) / nper);
-  hipLaunchKernelGGL(prelu_pool_bwd_k, grid, dim3(256), 0, s, (const bf16_t*)dp, (const bf16_t*)z, alpha,
-                     (bf16_t*)dz, dalpha, dbias, N, H, W, C, nper);
-  PTG_RETURN_LAUNCH();
-}
-
 int ptg_prelu_pool_bwd2(const void* dp, const void* z, const float* alpha, void* dz, float* dalpha,
                         float* dbias, int N, int H, int W, int C, int nper, hipStream_t s) {
   if (C % 8 || C > 256 || H < 2 || W < 2 || !ptg_fits_2g((long)N * H * W * C * 2)) return (int)hipErrorInvalidValue;
@@ -1290,22 +1101,6 @@ int ptg_prelu_fwd(const void* z, const float* alpha, void* a, int N, int HWC, hi
   const long total8 = (long)N * HWC / 8;
   hipLaunchKernelGGL(prelu_fwd_k, dim3(grid_for(total8)), dim3(256), 0, s, (const bf16_t*)z, alpha,
                      (bf16_t*)a, total8, HWC / 8);
-  PTG_RETURN_LAUNCH();
-}
-
-int ptg_prelu_bwd(const void* da, const void* z, const float* alpha, void* dz, float* dalpha,
-                  float* dbias, int N, int HWC, int C, int nper, hipStream_t s) {
-  if (HWC % 8 || C % 8 || C > 256) return (int)hipErrorInvalidValue;
-  const int nvec = HWC / 8;
-  if (nper <= 0) {
-    const int bx = (nvec + 255) / 256;
-    int chunks = (2048 + bx - 1) / bx;
-    if (chunks > N) chunks = N;
-    nper = (N + chunks - 1) / chunks;
-  }
-  dim3 grid((nvec + 255) / 256, (N + nper - 1) / nper);
-  hipLaunchKernelGGL(prelu_bwd_k, grid, dim3(256), 0, s, (const bf16_t*)da, (const bf16_t*)z, alpha,
-                     (bf16_t*)dz, dalpha, dbias, N, HWC, C, nper);
   PTG_RETURN_LAUNCH();
 }
 
@@ -1472,10 +1267,6 @@ int ptg_sgd(float* p, const float* g, float* vel, void* pbf, long n, float lr, f
 
 int ptg_cast_f32_bf16(const float* x, void* y, long n, hipStream_t s) {
   hipLaunchKernelGGL(cast_f32_bf16_k, dim3(grid_for(n)), dim3(256), 0, s, x, (bf16_t*)y, n);
-  PTG_RETURN_LAUNCH();
-}
-int ptg_cast_bf16_f32(const void* x, float* y, long n, hipStream_t s) {
-  hipLaunchKernelGGL(cast_bf16_f32_k, dim3(grid_for(n)), dim3(256), 0, s, (const bf16_t*)x, y, n);
   PTG_RETURN_LAUNCH();
 }
 int ptg_resize_norm(const void* in_u8, void* out, int N, int Hin, int Win, int H, int W, hipStream_t s) {

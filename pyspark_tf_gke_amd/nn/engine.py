@@ -30,10 +30,8 @@ from . import layers as L
 _HOST_FP32 = [os.environ.get("PTG_HOST_FP32") == "1"]
 
 # Sparse PReLU+pool record (conv.hip EPI_POOLS: z at the argmax + argmax index instead of the full
-# z).  Opt-in: on CNN-B1 (batch 256, MI355X) it moves 0.8 GB less per step but its longer epilogue
-# makes the latency-bound layer-1/2 forward kernels slower than the backward saves (98.1k vs 99.2k
-# samples/s measured), so the dense record stays the default.
-SPARSE_POOL = os.environ.get("PTG_SPARSE_POOL", "0") == "1"
+# z) for layers 2-4 as well was measured and rejected (README): its longer epilogue makes those
+# latency-bound forward kernels slower than the backward saves.
 # The FIRST conv layer (no data gradient) keeps its whole backward sparse: forward writes the record,
 # prelu_pool_bwd_sel turns it into dZ's record (dZ at the argmax) and the weight gradient expands it in
 # LDS, so the full-resolution z and dZ (335 MB each for CNN-B1 at batch 256) never exist.  Measured
@@ -146,7 +144,7 @@ class ConvOp(Op):
         halo_ok = self._halo()[0] and not (self.pool is not None and (OH % 2 or OW % 2))
         self._sel = halo_ok and self.pool is not None and x.is_cuda and self.first and SPARSE_FIRST \
             and self.conv.kernel_size[0] == 5
-        if halo_ok and self.pool is not None and x.is_cuda and (SPARSE_POOL or self._sel):
+        if halo_ok and self.pool is not None and x.is_cuda and self._sel:
             # sparse pool record: pooled output + z at the argmax + argmax position (no full z)
             self._x, self._sparse = x, True
             return self._forward_pool_sparse(x, b, ws, B, OH, OW, Co, dev)

@@ -18,7 +18,6 @@ from ._util import hip, need, on_device, ptr
 
 # prelu+pool backward kernel: "sg" = sample-parallel blocks with an in-LDS dalpha reduction
 # (prelu_pool_bwd_sg_k), "chunk" = position-parallel blocks adding dalpha partials with atomics
-PPBWD_KERNEL = os.environ.get("PTG_PPBWD", "sg")
 
 ACT = {None: 0, "linear": 0, "none": 0, "relu": 1, "softmax": 2}
 
@@ -373,7 +372,7 @@ def prelu_pool_bwd(dp, z, alpha, dz_out, dalpha, dbias, nper: int = 0):
     if not on_device(z):
         return ref.prelu_pool_bwd(dp, z, alpha, dz_out, dalpha, dbias)
     N, H, W, C = z.shape
-    hip("ptg_prelu_pool_bwd2" if PPBWD_KERNEL == "sg" else "ptg_prelu_pool_bwd", ptr(dp), ptr(z), ptr(alpha), ptr(dz_out), ptr(dalpha), ptr(dbias), N, H, W, C, nper)
+    hip("ptg_prelu_pool_bwd2", ptr(dp), ptr(z), ptr(alpha), ptr(dz_out), ptr(dalpha), ptr(dbias), N, H, W, C, nper)
     return dz_out
 
 
@@ -416,7 +415,7 @@ def prelu_bwd(da, z, alpha, dz_out, dalpha, dbias, nper: int = 0):
         return ref.prelu_bwd(da, z, alpha, dz_out, dalpha, dbias)
     N = z.shape[0]
     C = z.shape[-1]
-    hip("ptg_prelu_bwd2" if PPBWD_KERNEL == "sg" else "ptg_prelu_bwd", ptr(da), ptr(z), ptr(alpha), ptr(dz_out),
+    hip("ptg_prelu_bwd2", ptr(da), ptr(z), ptr(alpha), ptr(dz_out),
         ptr(dalpha), ptr(dbias), N, z[0].numel(), C, nper)
     return dz_out
 

@@ -332,9 +332,7 @@ def test_conv_halo_dgrad(N, H, W, C, Co, KS):
                                           (24, 7, 10, 14, 3), (8, 9, 7, 9, 4), (32, 5, 6, 6, 2),
                                           (8, 40, 6, 10, 0), (16, 130, 4, 4, 0), (8, 67, 7, 9, 0),
                                           (64, 9, 32, 40, 0), (256, 5, 4, 6, 2), (16, 33, 18, 22, 0)])
-@pytest.mark.parametrize("kernel", ["sg", "chunk"])
-def test_prelu_pool_fwd_bwd(C, N, H, W, nper, kernel, monkeypatch):
-    monkeypatch.setattr(K, "PPBWD_KERNEL", kernel)
+def test_prelu_pool_fwd_bwd(C, N, H, W, nper):
     z = rnd(N, H, W, C)
     alpha = torch.randn(H, W, C) * 0.3
     alpha[0, 0, :] = 0.0  # exercise ties of zeros

@@ -58,11 +58,8 @@ def main():
         da = torch.zeros_like(al)
         db = torch.zeros(Co, device=dev)
         if pool:
-            for var in ("chunk", "sg"):
-                def f(dp=dp, z=z, al=al, dz=dz, da=da, db=db, var=var):
-                    ops.PPBWD_KERNEL = var
-                    ops.prelu_pool_bwd(dp, z, al, dz, da, db)
-                ops_[f"ppbwd{li}_{var}"] = (f, dp.numel() * 2 + z.numel() * 4)
+            ops_[f"ppbwd{li}"] = (lambda dp=dp, z=z, al=al, dz=dz, da=da, db=db: ops.prelu_pool_bwd(dp, z, al, dz, da, db),
+                                  dp.numel() * 2 + z.numel() * 4)
         else:
             ops_[f"pbwd{li}"] = (lambda dp=dp, z=z, al=al, dz=dz, da=da, db=db: ops.prelu_bwd(dp, z, al, dz, da, db),
                                  dp.numel() * 2 + z.numel() * 4)
