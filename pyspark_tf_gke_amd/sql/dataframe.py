@@ -2,8 +2,10 @@
 (k_means.py, spark_workload_to_cloud_k8s.py, spark_installation_check.py, google_health_SQL.py).
 
 Execution model: SPMD, one rank per GPU = one Spark executor.  Each rank holds its partition as a
-device-resident :class:`~.table.Table`; transformations run immediately on that partition with
-the HIP kernels (expression VM, compaction, hash aggregation) and keep their result resident
+device-resident :class:`~.table.Table`.  Narrow transformations (filter, withColumn) are lazy: they
+accumulate into a pending stage that is optimised (predicate pushdown, filter fusion) and run as
+one retried task when the table is first needed (sql/plan.py); everything else runs on the
+partition with the HIP kernels (expression VM, compaction, hash aggregation) and keeps its result resident
 (the reference re-reads its JDBC source on every action because nothing is cached, SURVEY §3.3;
 here nothing needs re-reading).  Actions combine ranks with RCCL (count/agg all-reduce, groupBy
 partial-aggregate -> hash shuffle -> final aggregate) and gather small results to the driver view
@@ -72,10 +74,41 @@ def _to_col(c) -> Column:
 
 
 class DataFrame:
-    def __init__(self, table: Table, session, replicated: bool = False):
-        self._t = table
+    def __init__(self, table: Table, session, replicated: bool = False, pending: list | None = None):
+        self._src = table
+        self._pending = list(pending or [])
+        self._mat = None if self._pending else table
         self.sparkSession = session
         self._num_partitions = session.default_parallelism if session is not None else 1
+
+    @property
+    def _t(self) -> Table:
+        """The materialised partition; runs the pending narrow stage (sql/plan.py) on first use."""
+        if self._mat is None:
+            from . import plan as P
+
+            self._mat = P.run_task(self._src, self._pending, self.sparkSession)
+        return self._mat
+
+    def _lazy(self, op) -> "DataFrame":
+        from . import plan as P
+
+        names = {n.lower() for n in self._src.names} | {o[1].lower() for o in self._pending if o[0] == "with"}
+        node = op[1].node if op[0] == "filter" else op[2].node
+        missing = P.referenced_columns(node) - names
+        if missing:
+            raise KeyError(f"Column '{sorted(missing)[0]}' does not exist. Available: {', '.join(sorted(names))}")
+        base = self if self._mat is None else None
+        d = DataFrame(self._src if base is not None else self._mat, self.sparkSession,
+                      pending=(self._pending if base is not None else []) + [op])
+        d._num_partitions = self._num_partitions
+        return d
+
+    def explain(self, extended: bool = False) -> None:
+        from . import plan as P
+
+        if comm.rank() == 0:
+            print(P.describe(self._pending if self._mat is None else []), flush=True)
 
     # ------------------------------------------------------------------ schema
     @property
@@ -217,8 +250,9 @@ class DataFrame:
 
     # ------------------------------------------------------------------ transformations
     def filter(self, condition) -> "DataFrame":
-        idx = D.compact(self._mask(condition))
-        return self._new(self._t.take(idx))
+        if isinstance(condition, str):
+            condition = _parse_sql_predicate(condition)
+        return self._lazy(("filter", condition))
 
     where = filter
 
@@ -247,8 +281,12 @@ class DataFrame:
         return self.select(*[col(e) for e in exprs])
 
     def withColumn(self, colName: str, c: Column) -> "DataFrame":  # noqa: N802, N803
-        _, cv = self._eval(c, colName)
-        return self._new(self._t.with_column(colName, cv))
+        base = C.strip_alias(c.node)
+        if base[0] in ("split", "explode", "agg", "strmap", "strlen") or (base[0] == "lit" and isinstance(base[1], str)) \
+                or (base[0] == "bin" and base[1] == "coalesce") or base[0] == "col":
+            _, cv = self._eval(c, colName)  # dictionary-string / pass-through columns: eager
+            return self._new(self._t.with_column(colName, cv))
+        return self._lazy(("with", colName, c))
 
     def withColumnRenamed(self, existing: str, new: str) -> "DataFrame":  # noqa: N802
         cols = {}
@@ -475,6 +513,8 @@ class DataFrame:
         return d
 
     def cache(self):
+        """Materialise now (runs the pending narrow stage once) and keep the result resident."""
+        _ = self._t
         return self
 
     persist = cache

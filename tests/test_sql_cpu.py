@@ -193,3 +193,41 @@ def test_shuffle_budget_and_tensor_control_plane(spark):
     finally:
         comm.all_gather_object = orig
     assert calls == []
+
+
+def test_lazy_stage_pushdown_fusion_and_retry(spark, capsys):
+    """filter/withColumn chains run as one optimised narrow stage: filters on source columns are
+    pushed ahead of the projections and fused into one predicate (one VM pass, one compaction, one
+    gather); results equal the step-by-step evaluation; a failing task attempt is retried
+    (spark.task.maxFailures) and explain() shows the plan."""
+    from pyspark_tf_gke_amd.sql import plan as P
+
+    rows = [(i, float(i) * 0.5 if i % 7 else None, "s%d" % (i % 5)) for i in range(1000)]
+    df = spark.createDataFrame(rows, ["a", "b", "s"])
+    q = (df.filter(col("a") > 10)
+         .withColumn("c", col("a") * 2)
+         .filter(col("b").isNotNull())
+         .withColumn("d", when(col("c") > 100, col("c")).otherwise(lit(0)))
+         .filter(col("d") > 0)
+         .filter(col("a") < 900))
+    q.explain()
+    out = capsys.readouterr().out
+    assert "pushed down" in out and "a > 10" in out.replace("(", "").replace(")", "") or "Filter" in out
+    before = dict(P.STATS)
+    got = sorted((r["a"], r["c"], r["d"]) for r in q.collect())
+    # 3 source filters fused into 1 pass + 2 projections + 1 post filter = 4 VM passes, 2 gathers
+    assert P.STATS["vm_passes"] - before["vm_passes"] == 4
+    assert P.STATS["gathers"] - before["gathers"] == 2
+    want = sorted((i, 2 * i, 2 * i) for i in range(1000) if 10 < i < 900 and i % 7 and 2 * i > 100)
+    assert got == want
+    # injected task failures are retried; beyond maxFailures the job fails
+    P._FAULTS["left"] = 2
+    r0 = P.STATS["retries"]
+    assert df.filter(col("a") < 5).count() == 5
+    assert P.STATS["retries"] - r0 == 2
+    P._FAULTS["left"] = 10
+    with pytest.raises(P.TaskFailure):
+        df.filter(col("a") < 5).count()
+    P._FAULTS["left"] = 0
+    with pytest.raises(KeyError):
+        df.filter(col("nope") > 1)
