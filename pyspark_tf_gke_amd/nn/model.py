@@ -334,9 +334,12 @@ class Sequential:
         return ctx
 
     def _head_fusable(self, xb, st) -> bool:
-        """[..., Dense(relu, big), Dense(N <= 4, linear)] + MSE on one GPU replica: the head runs as
-        one fused kernel (head_mse_k) instead of seven small ones."""
-        if not FUSED_HEAD or not xb.is_cuda or (st is not None and st.world_size != 1):
+        """[..., Dense(relu, big), Dense(N <= 4, linear)] + MSE on the GPU: the head runs as two fused
+        kernels (head_row_k + head_col_k) instead of seven small ones, on one replica or under a
+        data-parallel strategy (its gradient hooks fire for the two Dense ops as usual)."""
+        if not FUSED_HEAD or not xb.is_cuda:
+            return False
+        if st is not None and st.world_size != 1 and not hasattr(st, "on_op_grads_ready"):
             return False
         ops = getattr(self, "ops", None) or []
         if len(ops) < 3 or not isinstance(self.loss, LS.MeanSquaredError):
@@ -348,7 +351,11 @@ class Sequential:
 
     def _train_step_fused_head(self, xb, yb, stats, st) -> None:
         d1, d2 = self.ops[-2], self.ops[-1]
-        x = E.run_forward(self.ops[:-2], xb, self.ws, True)
+        pre = self._pre_op_hook()
+        x = E.run_forward(self.ops[:-2], xb, self.ws, True, pre_op=pre)
+        if pre is not None:  # sharded update: the two Dense ops' parameter all-gathers
+            pre(d1)
+            pre(d2)
         acc = d1.forward_splitk_sums(x, self.ws)
         B, K1 = acc.shape
         dz1 = self.ws.get(d1.name + "/dz", (B, K1), torch.bfloat16, acc.device)
@@ -356,15 +363,24 @@ class Sequential:
         scratch = self.ws.get(d1.name + "/headscratch", (B * (N2 + 2),), torch.float32, acc.device)
         K.head_mse(acc, d1.dense.bias.data, d2.dense.kernel.data, d2.dense.bias.data, yb.contiguous(), dz1,
                    d2.dense.kernel.grad, d2.dense.bias.grad, d1.dense.bias.grad, stats, scratch=scratch)
+        hook = st.on_op_grads_ready if st is not None else None
         fused = self._begin_fused_update(st)
         try:
+            if hook is not None:
+                hook(self, d2)  # Dense2 weights/bias and Dense1 bias gradients exist now
             dx = d1.backward_dz(dz1, self.ws)
-            E.run_backward(self.ops[:-2], dx, self.ws)
+            if hook is not None:
+                hook(self, d1)
+            E.run_backward(self.ops[:-2], dx, self.ws,
+                           on_op_done=(lambda op: hook(self, op)) if hook is not None else None)
         finally:
             for op in getattr(self, "_fusable_ops", []):
                 op.fused_update = None
         if fused is not None:
             self.optimizer.finish_fused(fused)
+        elif st is not None:
+            st.finish_gradients(self)
+            st.apply_update(self)
         else:
             self.optimizer.apply(self.store)
 
