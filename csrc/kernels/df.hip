@@ -453,7 +453,7 @@ __global__ __launch_bounds__(256) void hash_extract_k(const long long* __restric
 //   bijection, so partitions shrink to single keys after at most 64/6 levels: the recursion is
 //   exact at any cardinality, with no global overflow table and no lost rows.
 #ifndef PTG_RT
-#define PTG_RT 2048
+#define PTG_RT 4096
 #endif
 #define RT PTG_RT  // max rows per tile; radix_scatter_k<NV> uses RT (NV <= 1) or RT/2 (LDS budget)
 #define RB 64
@@ -502,8 +502,13 @@ __global__ __launch_bounds__(256) void radix_count_k(const long long* __restrict
   if (tid < RB) hist[thbase[b] + (long long)tid * thstride[b]] = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
 }
 
-template <int NV>
-__global__ __launch_bounds__(256) void radix_scatter_k(const long long* __restrict__ keys, PayIn pin,
+#ifndef PTG_SCATTER_NT
+#define PTG_SCATTER_NT 512
+#endif
+// NT threads per tile-workgroup (each holds RPT rows in registers): 512 threads keep the same
+// waves per CU as two 256-thread tiles while each tile (and so each digit run) is twice as long.
+template <int NV, int NT = PTG_SCATTER_NT>
+__global__ __launch_bounds__(NT) void radix_scatter_k(const long long* __restrict__ keys, PayIn pin,
                                                        const long long* __restrict__ tstart,
                                                        const int* __restrict__ trows,
                                                        const long long* __restrict__ thbase,
@@ -512,7 +517,8 @@ __global__ __launch_bounds__(256) void radix_scatter_k(const long long* __restri
                                                        long long* __restrict__ okeys, PayOut pout) {
   (void)n_out;
   constexpr int RTT = NV <= 1 ? RT : RT / 2;  // tile rows (ops/df.py radix_tile mirrors this)
-  constexpr int RPT = RTT / 256;
+  constexpr int RPT = RTT / NT;
+  static_assert(RPT >= 1 && RTT % NT == 0, "tile rows must be a multiple of the thread count");
   constexpr int NVS = NV > 0 ? NV : 1;
   __shared__ long long sk[RTT];
   __shared__ double sv[NVS][RTT];
@@ -533,7 +539,7 @@ __global__ __launch_bounds__(256) void radix_scatter_k(const long long* __restri
   int d[RPT];
 #pragma unroll
   for (int j = 0; j < RPT; ++j) {
-    const int i = tid + j * 256;
+    const int i = tid + j * NT;
     d[j] = -1;
     if (i < nr) {
       k[j] = keys[s0 + i];
@@ -566,7 +572,7 @@ __global__ __launch_bounds__(256) void radix_scatter_k(const long long* __restri
     sd[pos] = (unsigned char)d[j];
   }
   __syncthreads();
-  for (int i = tid; i < nr; i += 256) {  // consecutive rows of a digit run -> consecutive addresses
+  for (int i = tid; i < nr; i += NT) {  // consecutive rows of a digit run -> consecutive addresses
     const int dd = sd[i];
     const long long dst = PTG_CHECKED_IDX(goff[dd] + (i - (int)lstart[dd]), n_out);
 #if PTG_NT_STORE  // streamed once, re-read only by the next pass
@@ -1120,7 +1126,7 @@ int ptg_radix_scatter(const void* keys, const void* pin_p, int nv, const void* t
   memcpy(&pin, pin_p, sizeof(PayIn));
   memcpy(&pout, pout_p, sizeof(PayOut));
 #define PTG_SCATTER(NV)                                                                                      \
-  hipLaunchKernelGGL(radix_scatter_k<NV>, dim3(ntiles), dim3(256), 0, s, (const long long*)keys, pin,        \
+  hipLaunchKernelGGL(radix_scatter_k<NV>, dim3(ntiles), dim3(PTG_SCATTER_NT), 0, s, (const long long*)keys, pin, \
                      (const long long*)tstart, (const int*)trows, (const long long*)thbase,                  \
                      (const long long*)thstride, shift, (const long long*)offs, n_out, (long long*)okeys, pout)
   switch (nv) {
