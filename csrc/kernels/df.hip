@@ -473,13 +473,25 @@ PTG_DEV double load_pay(const PayIn& in, int j, long i) {
   return ok ? v : __builtin_nan("");
 }
 
-__global__ __launch_bounds__(256) void radix_count_k(const long long* __restrict__ keys,
+// Keys travel as i64, or — when the first level finds max - min < 2^32 - 1 — as u32 offsets from
+// kbase = min (12 instead of 16 bytes per row through every later pass; the 1B-row / 1M-key
+// groupBy moves 21 % fewer bytes).  Digits always hash the ORIGINAL key, mix64(kbase + offset),
+// so the partitioning does not depend on the storage width.
+template <class KT>
+PTG_DEV unsigned long long orig_key(KT k, long long kbase) {
+  if constexpr (sizeof(KT) == 4) return (unsigned long long)(kbase + (long long)(unsigned int)k);
+  else return (unsigned long long)k;
+}
+
+// range (level 1 only, optional): per-tile [min, max] of the i64 keys, [ntiles][2]
+template <class KT>
+__global__ __launch_bounds__(256) void radix_count_k(const KT* __restrict__ keys, long long kbase,
                                                      const long long* __restrict__ tstart,
                                                      const int* __restrict__ trows,
                                                      const long long* __restrict__ thbase,
                                                      const long long* __restrict__ thstride, int shift,
-                                                     unsigned int* __restrict__ hist) {
-  // All RT/256 keys of a thread are loaded before the first LDS atomic (8 independent 8-B loads in
+                                                     unsigned int* __restrict__ hist, long long* __restrict__ range) {
+  // All RT/256 keys of a thread are loaded before the first LDS atomic (independent loads in
   // flight instead of a load->atomic chain per row), and each wave counts into its own 64-bin
   // histogram so the 4 waves never contend on a bin; trows <= RT by construction (_radix_level).
   constexpr int RPT = RT / 256;
@@ -492,7 +504,32 @@ __global__ __launch_bounds__(256) void radix_count_k(const long long* __restrict
 #pragma unroll
   for (int j = 0; j < RPT; ++j) {
     const int i = tid + j * 256;
-    k[j] = i < nr ? (unsigned long long)keys[s0 + i] : 0ull;
+    k[j] = i < nr ? orig_key<KT>(keys[s0 + i], kbase) : 0ull;
+  }
+  if (range) {  // per-tile [min, max] (no contended global atomics): the host reduces the tile pairs
+    __shared__ long long rmn[4], rmx[4];
+    long long mn = 0x7fffffffffffffffLL, mx = (long long)0x8000000000000000ULL;
+#pragma unroll
+    for (int j = 0; j < RPT; ++j)
+      if (tid + j * 256 < nr) {
+        const long long v = (long long)k[j];
+        mn = v < mn ? v : mn;
+        mx = v > mx ? v : mx;
+      }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const long long a = __shfl_xor(mn, o, 64), c = __shfl_xor(mx, o, 64);
+      mn = a < mn ? a : mn;
+      mx = c > mx ? c : mx;
+    }
+    if ((tid & 63) == 0) { rmn[w] = mn; rmx[w] = mx; }
+    __syncthreads();
+    if (tid == 0) {
+      long long a = rmn[0], c = rmx[0];
+      for (int q = 1; q < 4; ++q) { a = rmn[q] < a ? rmn[q] : a; c = rmx[q] > c ? rmx[q] : c; }
+      range[2 * b] = a;
+      range[2 * b + 1] = c;
+    }
   }
   __syncthreads();
 #pragma unroll
@@ -507,20 +544,20 @@ __global__ __launch_bounds__(256) void radix_count_k(const long long* __restrict
 #endif
 // NT threads per tile-workgroup (each holds RPT rows in registers): 512 threads keep the same
 // waves per CU as two 256-thread tiles while each tile (and so each digit run) is twice as long.
-template <int NV, int NT = PTG_SCATTER_NT>
-__global__ __launch_bounds__(NT) void radix_scatter_k(const long long* __restrict__ keys, PayIn pin,
+template <int NV, class KIN, class KOUT, int NT = PTG_SCATTER_NT>
+__global__ __launch_bounds__(NT) void radix_scatter_k(const KIN* __restrict__ keys, long long kbase_in, PayIn pin,
                                                        const long long* __restrict__ tstart,
                                                        const int* __restrict__ trows,
                                                        const long long* __restrict__ thbase,
                                                        const long long* __restrict__ thstride, int shift,
                                                        const long long* __restrict__ offs, long n_out,
-                                                       long long* __restrict__ okeys, PayOut pout) {
+                                                       KOUT* __restrict__ okeys, long long kbase_out, PayOut pout) {
   (void)n_out;
   constexpr int RTT = NV <= 1 ? RT : RT / 2;  // tile rows (ops/df.py radix_tile mirrors this)
   constexpr int RPT = RTT / NT;
   static_assert(RPT >= 1 && RTT % NT == 0, "tile rows must be a multiple of the thread count");
   constexpr int NVS = NV > 0 ? NV : 1;
-  __shared__ long long sk[RTT];
+  __shared__ KOUT sk[RTT];
   __shared__ double sv[NVS][RTT];
   __shared__ unsigned char sd[RTT];
   __shared__ unsigned int cnt[RB];
@@ -534,7 +571,7 @@ __global__ __launch_bounds__(NT) void radix_scatter_k(const long long* __restric
     goff[tid] = offs[thbase[b] + (long long)tid * thstride[b]];
   }
   __syncthreads();
-  long long k[RPT];
+  unsigned long long k[RPT];
   double v[NVS][RPT];
   int d[RPT];
 #pragma unroll
@@ -542,10 +579,10 @@ __global__ __launch_bounds__(NT) void radix_scatter_k(const long long* __restric
     const int i = tid + j * NT;
     d[j] = -1;
     if (i < nr) {
-      k[j] = keys[s0 + i];
+      k[j] = orig_key<KIN>(keys[s0 + i], kbase_in);
 #pragma unroll
       for (int q = 0; q < NV; ++q) v[q][j] = load_pay(pin, q, s0 + i);
-      d[j] = (int)((mix64((unsigned long long)k[j]) >> shift) & (RB - 1));
+      d[j] = (int)((mix64(k[j]) >> shift) & (RB - 1));
       atomicAdd(&cnt[d[j]], 1u);
     }
   }
@@ -566,7 +603,8 @@ __global__ __launch_bounds__(NT) void radix_scatter_k(const long long* __restric
   for (int j = 0; j < RPT; ++j) {
     if (d[j] < 0) continue;
     const unsigned pos = lstart[d[j]] + atomicAdd(&cnt[d[j]], 1u);
-    sk[pos] = k[j];
+    if constexpr (sizeof(KOUT) == 4) sk[pos] = (KOUT)(unsigned int)((long long)k[j] - kbase_out);
+    else sk[pos] = (KOUT)k[j];
 #pragma unroll
     for (int q = 0; q < NV; ++q) sv[q][pos] = v[q][j];
     sd[pos] = (unsigned char)d[j];
@@ -632,8 +670,8 @@ struct AggPay {
 // LDS.  Output (non-spilled partitions): keys + table rows [rows, (sum, cnt, min, max) per column]
 // in hash_extract_k's layout, one atomic per partition for the output base.  Every thread keeps 4
 // rows' key + value loads in flight ahead of its LDS probes.
-template <int NV, bool MINMAX>
-__global__ __launch_bounds__(256) void part_agg2_k(const long long* __restrict__ okeys, AggPay pay,
+template <int NV, bool MINMAX, class KT>
+__global__ __launch_bounds__(256) void part_agg2_k(const KT* __restrict__ okeys, long long kbase, AggPay pay,
                                                    const long long* __restrict__ pstart,
                                                    const long long* __restrict__ pend, int P, int pcap,
                                                    long long* __restrict__ out_keys, double* __restrict__ out_tab,
@@ -698,7 +736,7 @@ __global__ __launch_bounds__(256) void part_agg2_k(const long long* __restrict__
       double v4[4][NVS];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        k4[u] = okeys[i + u * 256];
+        k4[u] = (long long)orig_key<KT>(okeys[i + u * 256], kbase);
 #pragma unroll
         for (int j = 0; j < NV; ++j) v4[u][j] = pay.vals[j][i + u * 256];
       }
@@ -710,7 +748,7 @@ __global__ __launch_bounds__(256) void part_agg2_k(const long long* __restrict__
       double v1[NVS];
 #pragma unroll
       for (int j = 0; j < NV; ++j) v1[j] = pay.vals[j][i];
-      ok = insert(okeys[i], v1);
+      ok = insert((long long)orig_key<KT>(okeys[i], kbase), v1);
     }
     if (!ok) sflag = 1;
     __syncthreads();
@@ -1107,28 +1145,44 @@ int ptg_hash_extract(const void* keys, const void* tab, long cap, int nv, void* 
 
 // One radix level (see radix_count_k / radix_scatter_k): tiles described by tstart/trows, digit
 // counts at hist[thbase[t] + d*thstride[t]]; pin/pout: PayIn / PayOut structs (host-packed), nv <= 4.
-int ptg_radix_count(const void* keys, const void* tstart, const void* trows, const void* thbase,
-                    const void* thstride, int ntiles, int shift, void* hist, hipStream_t s) {
+// key32: keys are u32 offsets from kbase (else i64); range: optional per-tile [min, max] (i64 keys only)
+int ptg_radix_count(const void* keys, int key32, long kbase, const void* tstart, const void* trows,
+                    const void* thbase, const void* thstride, int ntiles, int shift, void* hist, void* range,
+                    hipStream_t s) {
   if (ntiles <= 0) return 0;
-  hipLaunchKernelGGL(radix_count_k, dim3(ntiles), dim3(256), 0, s, (const long long*)keys,
-                     (const long long*)tstart, (const int*)trows, (const long long*)thbase,
-                     (const long long*)thstride, shift, (unsigned int*)hist);
+  if (key32)
+    hipLaunchKernelGGL(radix_count_k<unsigned int>, dim3(ntiles), dim3(256), 0, s, (const unsigned int*)keys,
+                       (long long)kbase, (const long long*)tstart, (const int*)trows, (const long long*)thbase,
+                       (const long long*)thstride, shift, (unsigned int*)hist, (long long*)nullptr);
+  else
+    hipLaunchKernelGGL(radix_count_k<long long>, dim3(ntiles), dim3(256), 0, s, (const long long*)keys,
+                       (long long)kbase, (const long long*)tstart, (const int*)trows, (const long long*)thbase,
+                       (const long long*)thstride, shift, (unsigned int*)hist, (long long*)range);
   PTG_RETURN_LAUNCH();
 }
 int ptg_pay_desc_size() { return (int)sizeof(PayIn); }
 int ptg_radix_tile_rows() { return RT; }
-int ptg_radix_scatter(const void* keys, const void* pin_p, int nv, const void* tstart, const void* trows,
-                      const void* thbase, const void* thstride, int ntiles, int shift, const void* offs, long n_out,
-                      void* okeys, const void* pout_p, hipStream_t s) {
+// in32 / out32: input / output keys as u32 offsets from kbase_in / kbase_out (else i64); the
+// (i64 -> u32) and (u32 -> u32) forms are the compressed-key levels
+int ptg_radix_scatter(const void* keys, int in32, long kbase_in, const void* pin_p, int nv, const void* tstart,
+                      const void* trows, const void* thbase, const void* thstride, int ntiles, int shift,
+                      const void* offs, long n_out, void* okeys, int out32, long kbase_out, const void* pout_p,
+                      hipStream_t s) {
   if (ntiles <= 0) return 0;
+  if (in32 && !out32) return (int)hipErrorInvalidValue;
   PayIn pin;
   PayOut pout;
   memcpy(&pin, pin_p, sizeof(PayIn));
   memcpy(&pout, pout_p, sizeof(PayOut));
+#define PTG_SCATTER3(NV, KI, KO)                                                                             \
+  hipLaunchKernelGGL((radix_scatter_k<NV, KI, KO>), dim3(ntiles), dim3(PTG_SCATTER_NT), 0, s, (const KI*)keys, \
+                     (long long)kbase_in, pin, (const long long*)tstart, (const int*)trows,                   \
+                     (const long long*)thbase, (const long long*)thstride, shift, (const long long*)offs, n_out, \
+                     (KO*)okeys, (long long)kbase_out, pout)
 #define PTG_SCATTER(NV)                                                                                      \
-  hipLaunchKernelGGL(radix_scatter_k<NV>, dim3(ntiles), dim3(PTG_SCATTER_NT), 0, s, (const long long*)keys, pin, \
-                     (const long long*)tstart, (const int*)trows, (const long long*)thbase,                  \
-                     (const long long*)thstride, shift, (const long long*)offs, n_out, (long long*)okeys, pout)
+  if (!out32) PTG_SCATTER3(NV, long long, long long);                                                        \
+  else if (!in32) PTG_SCATTER3(NV, long long, unsigned int);                                                 \
+  else PTG_SCATTER3(NV, unsigned int, unsigned int)
   switch (nv) {
     case 0: PTG_SCATTER(0); break;
     case 1: PTG_SCATTER(1); break;
@@ -1138,10 +1192,12 @@ int ptg_radix_scatter(const void* keys, const void* pin_p, int nv, const void* t
     default: return (int)hipErrorInvalidValue;
   }
 #undef PTG_SCATTER
+#undef PTG_SCATTER3
   PTG_RETURN_LAUNCH();
 }
 // vals: host array of nv f64 device pointers (payload columns in partition order)
-int ptg_part_agg2(const void* okeys, const void* const* vals, int nv, int minmax, const void* pstart, const void* pend,
+int ptg_part_agg2(const void* okeys, int key32, long kbase, const void* const* vals, int nv, int minmax,
+                  const void* pstart, const void* pend,
                   int P, int pcap, void* out_keys, void* out_tab, long out_cap, void* m_out, void* spilled,
                   void* nspill, hipStream_t s) {
   if (nv > PAY_MAX || pcap < 256 || (pcap & (pcap - 1)) || P <= 0) return (int)hipErrorInvalidValue;
@@ -1151,15 +1207,18 @@ int ptg_part_agg2(const void* okeys, const void* const* vals, int nv, int minmax
   AggPay pay;
   for (int j = 0; j < PAY_MAX; ++j) pay.vals[j] = j < nv ? (const double*)vals[j] : nullptr;
   const int g = P < 8192 ? P : 8192;
-#define PTG_AGG(NV, MM)                                                                                     \
+#define PTG_AGG(NV, MM) \
+  if (key32) { PTG_AGGK(NV, MM, unsigned int) } else { PTG_AGGK(NV, MM, long long) }
+#define PTG_AGGK(NV, MM, KT)                                                                                \
   {                                                                                                         \
     static bool attr = false;                                                                               \
     if (!attr) {                                                                                            \
-      (void)hipFuncSetAttribute((const void*)part_agg2_k<NV, MM>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+      (void)hipFuncSetAttribute((const void*)part_agg2_k<NV, MM, KT>, hipFuncAttributeMaxDynamicSharedMemorySize, \
                                 150 * 1024);                                                                \
       attr = true;                                                                                          \
     }                                                                                                       \
-    hipLaunchKernelGGL((part_agg2_k<NV, MM>), dim3(g), dim3(256), (size_t)lds, s, (const long long*)okeys, pay, \
+    hipLaunchKernelGGL((part_agg2_k<NV, MM, KT>), dim3(g), dim3(256), (size_t)lds, s, (const KT*)okeys,         \
+                       (long long)kbase, pay,                                                              \
                        (const long long*)pstart, (const long long*)pend, P, pcap, (long long*)out_keys,     \
                        (double*)out_tab, out_cap, (unsigned long long*)m_out, (int*)spilled, (int*)nspill); \
   }
@@ -1171,6 +1230,7 @@ int ptg_part_agg2(const void* okeys, const void* const* vals, int nv, int minmax
                   case 3: PTG_AGG(3, false) break; default: PTG_AGG(4, false) break; }
   }
 #undef PTG_AGG
+#undef PTG_AGGK
   PTG_RETURN_LAUNCH();
 }
 

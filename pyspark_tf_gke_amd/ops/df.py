@@ -202,11 +202,14 @@ def _pay_out(tensors) -> ctypes.Array:
     return ctypes.create_string_buffer(b, len(b))
 
 
-def _radix_level(keys, pay_cols, seg_start, seg_len, shift, buf, tag):
+def _radix_level(keys, kbase, pay_cols, seg_start, seg_len, shift, buf, tag, compress=False):
     """One radix level over segments [seg_start, seg_start+seg_len) of ``keys`` (+ payload columns,
     written out as f64 with null -> NaN).  Rows are split by the 6 hash bits at ``shift``; the output
     holds the segments' rows only (n_out = sum(seg_len)), segment-major then digit-major.
-    Returns (okeys, [ovals], new_start, new_end) of the nseg*64 sub-segments."""
+    ``keys`` are int64, or int32 bit patterns of u32 offsets from ``kbase``; ``compress`` (first
+    level): the count pass also finds the key range and, when max - min < 2^32 - 1, the scatter
+    writes u32 offsets from min (12 instead of 16 bytes per row through every later pass).
+    Returns (okeys, kbase_out, [ovals], new_start, new_end) of the nseg*64 sub-segments."""
     dev = keys.device
     T = radix_tile(len(pay_cols))
     nseg = seg_start.numel()
@@ -215,11 +218,11 @@ def _radix_level(keys, pay_cols, seg_start, seg_len, shift, buf, tag):
     total = int(ntiles_s.sum().item())
     n_out = int(seg_len.sum().item())
     nv = len(pay_cols)
-    okeys = buf(tag + "okeys", (max(n_out, 1),), torch.int64)[:n_out]
+    in32 = keys.dtype == torch.int32
     ovals = [buf(f"{tag}ov{j}", (max(n_out, 1),), torch.float64)[:n_out] for j in range(nv)]
     if total == 0:
         z = torch.zeros(nseg * 64, dtype=torch.int64, device=dev)
-        return okeys, ovals, z, z
+        return keys[:0], kbase, ovals, z, z
     tile_seg = torch.repeat_interleave(torch.arange(nseg, device=dev), ntiles_s, output_size=total)
     tl = torch.arange(total, device=dev) - first[tile_seg]
     tstart = seg_start[tile_seg] + tl * T
@@ -229,20 +232,30 @@ def _radix_level(keys, pay_cols, seg_start, seg_len, shift, buf, tag):
     thbase = hb[tile_seg] + tl
     thstride = ntiles_s[tile_seg]
     hist = buf(tag + "hist", (64 * total,), torch.int32)
-    hip("ptg_radix_count", ptr(keys), ptr(tstart), ptr(trows), ptr(thbase), ptr(thstride), total, shift, ptr(hist))
+    rng = buf(tag + "rng", (total, 2), torch.int64) if (compress and not in32) else None
+    hip("ptg_radix_count", ptr(keys), int(in32), int(kbase), ptr(tstart), ptr(trows), ptr(thbase), ptr(thstride),
+        total, shift, ptr(hist), ptr(rng))
     offs = buf(tag + "offs", (64 * total + 1,), torch.int64)
     torch.cumsum(hist, 0, dtype=torch.int64, out=offs[1:])
     offs[0] = 0
+    out32, kbase_out = in32, kbase
+    if rng is not None:
+        lo, hi = (int(x) for x in torch.stack([rng[:, 0].min(), rng[:, 1].max()]).tolist())
+        if hi - lo < (1 << 32) - 1:
+            out32, kbase_out = True, lo
+    okeys = buf(tag + ("okeys32" if out32 else "okeys"), (max(n_out, 1),),
+                torch.int32 if out32 else torch.int64)[:n_out]
     pin = _pay_in(pay_cols)
     pout = _pay_out(ovals)
-    hip("ptg_radix_scatter", ptr(keys), ctypes.addressof(pin), nv, ptr(tstart), ptr(trows), ptr(thbase),
-        ptr(thstride), total, shift, ptr(offs[:-1]), n_out, ptr(okeys), ctypes.addressof(pout))
+    hip("ptg_radix_scatter", ptr(keys), int(in32), int(kbase), ctypes.addressof(pin), nv, ptr(tstart), ptr(trows),
+        ptr(thbase), ptr(thstride), total, shift, ptr(offs[:-1]), n_out, ptr(okeys), int(out32), int(kbase_out),
+        ctypes.addressof(pout))
     # sub-segment (s, d) starts at the run of its first tile; empty segments (no tiles) start where
     # the next non-empty one does (offs[-1] = n_out is the sentinel)
     idx = (hb.view(-1, 1) + torch.arange(64, device=dev).view(1, -1) * ntiles_s.view(-1, 1)).view(-1)
     new_start = offs[idx]
     new_end = torch.cat([new_start[1:], torch.full((1,), n_out, dtype=torch.int64, device=dev)])
-    return okeys, ovals, new_start, new_end
+    return okeys, kbase_out, ovals, new_start, new_end
 
 
 def _part_agg_lds(pcap: int, nv: int, minmax: bool) -> int:
@@ -312,12 +325,13 @@ def hash_agg_radix(keys: torch.Tensor, vals: list, valids: list, want_minmax: bo
         pcap *= 2
     seg_start = torch.zeros(1, dtype=torch.int64, device=dev)
     seg_len = torch.full((1,), n, dtype=torch.int64, device=dev)
-    cur_keys, cur_pay = keys, pay
+    cur_keys, cur_pay, kbase = keys.contiguous(), pay, 0
     shift = 64 - RADIX_BITS
     tags = ["a", "b"]
     lvl = 0
     for _ in range(levels):
-        cur_keys, ov, pstart, pend = _radix_level(cur_keys, cur_pay, seg_start, seg_len, shift, buf, tags[lvl % 2])
+        cur_keys, kbase, ov, pstart, pend = _radix_level(cur_keys, kbase, cur_pay, seg_start, seg_len, shift, buf,
+                                                         tags[lvl % 2], compress=(lvl == 0))
         cur_pay = [(o, None) for o in ov]
         seg_start, seg_len = pstart, pend - pstart
         shift -= RADIX_BITS
@@ -333,8 +347,9 @@ def hash_agg_radix(keys: torch.Tensor, vals: list, valids: list, want_minmax: bo
         nspill = torch.zeros(1, dtype=torch.int32, device=dev)
         vptrs = (ctypes.c_void_p * PAY_MAX)(*([c[0].data_ptr() for c in cur_pay] + [0] * (PAY_MAX - nv)))
         pend = seg_start + seg_len
-        hip("ptg_part_agg2", ptr(cur_keys), ctypes.addressof(vptrs), nv, int(want_minmax), ptr(seg_start), ptr(pend),
-            P, pcap, ptr(out_keys), ptr(out_tab), max(cap, 1), ptr(m_out), ptr(spilled), ptr(nspill))
+        hip("ptg_part_agg2", ptr(cur_keys), int(cur_keys.dtype == torch.int32), int(kbase), ctypes.addressof(vptrs), nv,
+            int(want_minmax), ptr(seg_start), ptr(pend), P, pcap, ptr(out_keys), ptr(out_tab), max(cap, 1), ptr(m_out),
+            ptr(spilled), ptr(nspill))
         m = int(m_out.item())
         if m > cap:
             raise RuntimeError(f"hash_agg_radix: {m} groups exceed the output capacity {cap}")
@@ -347,8 +362,8 @@ def hash_agg_radix(keys: torch.Tensor, vals: list, valids: list, want_minmax: bo
             raise RuntimeError("hash_agg_radix: partition recursion did not converge")
         sp = spilled[:ns].long()
         # re-partition only the spilled partitions, one level deeper
-        cur_keys, ov, seg_start, pend2 = _radix_level(cur_keys, cur_pay, seg_start[sp], seg_len[sp], shift, buf,
-                                                      tags[lvl % 2])
+        cur_keys, kbase, ov, seg_start, pend2 = _radix_level(cur_keys, kbase, cur_pay, seg_start[sp], seg_len[sp],
+                                                             shift, buf, tags[lvl % 2])
         cur_pay = [(o, None) for o in ov]
         seg_len = pend2 - seg_start
         shift -= RADIX_BITS

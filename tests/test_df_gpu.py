@@ -334,3 +334,18 @@ def test_silhouette_mfma_matches_host(hip_built):
     tg = D.silhouette_points(X.cuda(), a.cuda(), Sg, Qg, cg)
     th = D.silhouette_points(X, a, Sh, Qh, ch)
     assert abs(tg - th) <= 1e-3 * max(1.0, abs(th))
+
+
+@pytest.mark.parametrize("lo,span", [(-3_000_000_000, 4_000_000_000), (1 << 40, (1 << 32) - 2), (-(1 << 62), 1 << 62)])
+def test_radix_agg_key_compression_ranges(hip_built, lo, span):
+    """u32-offset key compression (key range < 2^32 - 1, including negative and offset ranges) and the
+    i64 fallback (a 2^62 range) give the same groups as the host path."""
+    n = 3_000_000
+    g = torch.Generator().manual_seed(span % 1000)
+    base = torch.randint(0, 300_000, (n,), generator=g, dtype=torch.int64)
+    k = lo + (base * (span // 300_000)) % span
+    k[:2] = torch.tensor([lo, lo + span - 1])  # both ends of the range
+    v = torch.rand(n, generator=g, dtype=torch.float64)
+    got = D.hash_agg_radix(k.cuda(), [v.cuda()], [None], True)
+    want = D.hash_agg(k, [v], [None], True)
+    _assert_agg_equal(got, want, True)
