@@ -55,13 +55,17 @@ def save_checkpoint(model, path: str, epoch: int, extra: dict | None = None) -> 
                 if getattr(l, "moving_mean", None) is not None:
                     tensors[f"bn/{l.name}/moving_mean"] = l.moving_mean.detach().cpu().contiguous()
                     tensors[f"bn/{l.name}/moving_variance"] = l.moving_variance.detach().cpu().contiguous()
+            tensors["rng/cpu"] = torch.get_rng_state().contiguous()
+            if torch.cuda.is_available() and st.flat.device.type == "cuda":
+                tensors["rng/cuda"] = torch.cuda.get_rng_state(st.flat.device).contiguous()
         tmp = os.path.join(path, f"shard-{rank:05d}.safetensors.tmp")
         save_file(tensors, tmp, metadata={"lo": str(lo), "hi": str(hi)})
         os.replace(tmp, os.path.join(path, f"shard-{rank:05d}.safetensors"))
     comm.barrier()
     if rank == 0:
         manifest = {"epoch": epoch, "step": opt.iterations if opt else 0, "world_size": comm.world_size(),
-                    "sharded": sharded, "layout": "per-param", "time": time.time(),
+                    "sharded": sharded, "layout": "ps-flat" if sharded else "per-param",
+                    "total": int(st.total), "time": time.time(),
                     **(extra or {})}
         with open(os.path.join(path, "manifest.json.tmp"), "w") as fh:
             json.dump(manifest, fh)
@@ -76,9 +80,16 @@ def load_checkpoint(model, path: str) -> dict:
     with open(os.path.join(path, "manifest.json")) as fh:
         manifest = json.load(fh)
     strat = getattr(model, "strategy", None)
+    st = model.store
+    if manifest["sharded"] and (int(manifest.get("total", -1)) != int(st.total)
+                                or int(manifest["world_size"]) != comm.world_size()
+                                or not _ps_sharded(model)):
+        # flat [lo:hi] optimizer slices only mean something in the layout that wrote them
+        raise ValueError(f"checkpoint {path}: parameter-server optimizer shards were written for "
+                         f"world {manifest['world_size']} / flat size {manifest.get('total')}; this model "
+                         f"has world {comm.world_size()} / flat size {st.total} (load it with the same layout)")
     if strat is not None and hasattr(strat, "wait_parameters"):
         strat.wait_parameters(model)  # no parameter gather still in flight may land on the loaded values
-    st = model.store
     opt = model.optimizer
     if opt is not None:
         opt.build(st)
@@ -98,6 +109,10 @@ def load_checkpoint(model, path: str) -> dict:
             if getattr(l, "moving_mean", None) is not None and f"bn/{l.name}/moving_mean" in keys:
                 l.moving_mean.copy_(f.get_tensor(f"bn/{l.name}/moving_mean").to(l.moving_mean.device))
                 l.moving_variance.copy_(f.get_tensor(f"bn/{l.name}/moving_variance").to(l.moving_variance.device))
+        if "rng/cpu" in keys:
+            torch.set_rng_state(f.get_tensor("rng/cpu"))
+        if "rng/cuda" in keys and st.flat.device.type == "cuda":
+            torch.cuda.set_rng_state(f.get_tensor("rng/cuda"), st.flat.device)
     if manifest["sharded"] and opt is not None:
         for r in range(manifest["world_size"]):
             fn = os.path.join(path, f"shard-{r:05d}.safetensors")
