@@ -22,6 +22,7 @@ import torch
 
 from ..ops import nn as K
 from . import layers as L
+from . import streams as S
 
 
 # Host-path debug precision: with PTG_HOST_FP32=1 (or ``host_fp32(True)``) CPU models keep their
@@ -257,10 +258,11 @@ class ConvOp(Op):
             dz = dy
             K.col_sum(dz.reshape(-1, dz.shape[-1]), bias_g)
         halo_fwd, halo_dgrad = self._halo()
+        g = self.conv.kernel.grad
         if halo_fwd:
-            K.conv2d_wgrad_halo(x, dz, self.pad, self.conv.kernel.grad, zeroed=True)
+            S.launch(lambda: K.conv2d_wgrad_halo(x, dz, self.pad, g, zeroed=True), dev)
         else:
-            K.conv2d_wgrad(x, dz, self.stride, self.pad, self.conv.kernel.grad, accumulate=True)
+            S.launch(lambda: K.conv2d_wgrad(x, dz, self.stride, self.pad, g, accumulate=True), dev)
         if self.first:
             return None
         if self.stride != 1:
@@ -335,7 +337,8 @@ class DenseOp(Op):
         if fused is not None and dz.is_cuda:
             fused.linear_dw(dz, x, self.dense.kernel)
         else:
-            K.linear_dw(dz, x, self.dense.kernel.grad)
+            g = self.dense.kernel.grad
+            S.launch(lambda: K.linear_dw(dz, x, g), dz.device)
         return dx
 
     def backward(self, dy, ws):
@@ -359,7 +362,8 @@ class DenseOp(Op):
             if fused is not None and dz.is_cuda:
                 fused.linear_dw(dz, x, self.dense.kernel)  # Adam in the wgrad epilogue
             else:
-                K.linear_dw(dz, x, self.dense.kernel.grad)
+                g = self.dense.kernel.grad
+                S.launch(lambda: K.linear_dw(dz, x, g), dev)
             return dx
         # skinny path (fp32 math)
         if self.act == "relu" and not self.grad_masked_by_next:

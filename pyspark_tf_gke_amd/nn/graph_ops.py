@@ -27,6 +27,7 @@ from ..ops import bn as KB
 from ..ops import nn as K
 from . import engine as E
 from . import layers as L
+from . import streams as S
 
 
 def _bf16(x, ws, key):
@@ -242,7 +243,8 @@ class ConvBNOp:
         dz = ws.get(self.name + "/dz", z.shape, torch.bfloat16, dev)
         dres = ws.get(self.name + "/dres", z.shape, torch.bfloat16, dev) if self.residual else None
         self.state.backward(dy, y, z, self.relu, dz, dres, ws)
-        conv_wgrad(x, dz, self.stride, self.pad, self.conv.kernel.grad)
+        g = self.conv.kernel.grad
+        S.launch(lambda: conv_wgrad(x, dz, self.stride, self.pad, g), dev)
         dx = None
         if not self.first:
             ex = existing[0]

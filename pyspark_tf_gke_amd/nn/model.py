@@ -24,6 +24,7 @@ from ..ops import nn as K
 from ..runtime import fault as _fault
 from ..runtime import heartbeat as _heartbeat
 from . import engine as E
+from . import streams as S
 from . import layers as L
 from . import losses as LS
 from . import metrics as MT
@@ -300,14 +301,16 @@ class Sequential:
             # one local replica: big Dense layers apply Adam in their weight-gradient epilogue,
             # the rest of the flat store gets the usual fused Adam pass afterwards
             try:
-                self._run_backward(dpred)
+                with S.active(S.for_step(self.store, st)):
+                    self._run_backward(dpred)
             finally:
                 for op in self._fusable_ops:
                     op.fused_update = None
             self.optimizer.finish_fused(fused)
             return
         hook = st.on_op_grads_ready if st is not None else None
-        self._run_backward(dpred, on_op_done=(lambda op: hook(self, op)) if hook else None)
+        with S.active(S.for_step(self.store, st)):  # joined before the gradient sync / update
+            self._run_backward(dpred, on_op_done=(lambda op: hook(self, op)) if hook else None)
         if st is not None:
             st.finish_gradients(self)
             st.apply_update(self)
@@ -366,13 +369,14 @@ class Sequential:
         hook = st.on_op_grads_ready if st is not None else None
         fused = self._begin_fused_update(st)
         try:
-            if hook is not None:
-                hook(self, d2)  # Dense2 weights/bias and Dense1 bias gradients exist now
-            dx = d1.backward_dz(dz1, self.ws)
-            if hook is not None:
-                hook(self, d1)
-            E.run_backward(self.ops[:-2], dx, self.ws,
-                           on_op_done=(lambda op: hook(self, op)) if hook is not None else None)
+            with S.active(S.for_step(self.store, st)):
+                if hook is not None:
+                    hook(self, d2)  # Dense2 weights/bias and Dense1 bias gradients exist now
+                dx = d1.backward_dz(dz1, self.ws)
+                if hook is not None:
+                    hook(self, d1)
+                E.run_backward(self.ops[:-2], dx, self.ws,
+                               on_op_done=(lambda op: hook(self, op)) if hook is not None else None)
         finally:
             for op in getattr(self, "_fusable_ops", []):
                 op.fused_update = None

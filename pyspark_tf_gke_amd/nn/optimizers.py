@@ -13,6 +13,7 @@ import math
 import torch
 
 from ..ops import nn as K
+from . import streams as S
 
 
 class Optimizer:
@@ -131,9 +132,11 @@ class FusedAdamStep:
         o, n = param.offset, param.numel
         st, opt = self.store, self.opt
         shp = param.grad.shape
-        K.linear_dw_adam(dz, x, st.flat[o:o + n].view(shp), opt.m[o:o + n].view(shp), opt.v[o:o + n].view(shp),
-                         st.flat_bf16[o:o + n].view(shp), opt.lr_t(self.step), opt.beta_1, opt.beta_2, opt.epsilon,
-                         1.0, lr_dev=self.lr_dev)
+        lr_t = opt.lr_t(self.step)
+        # a weight-gradient producer: overlaps the rest of the backward on the side stream (streams.py)
+        S.launch(lambda: K.linear_dw_adam(dz, x, st.flat[o:o + n].view(shp), opt.m[o:o + n].view(shp),
+                                          opt.v[o:o + n].view(shp), st.flat_bf16[o:o + n].view(shp), lr_t,
+                                          opt.beta_1, opt.beta_2, opt.epsilon, 1.0, lr_dev=self.lr_dev), dz.device)
         self.done.append((o, o + n))
 
 
