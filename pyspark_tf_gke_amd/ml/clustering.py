@@ -119,7 +119,7 @@ class KMeans(Estimator, MLWritable, MLReadable):
                     # sums || counts all-reduced as one tensor (a converged fit reduces zeros: every
                     # rank holds the same flag, so the collective sequence stays identical)
                     buf = torch.cat([sums.view(-1), counts]).contiguous()
-                    comm.all_reduce_(buf)
+                    comm.all_reduce_tensor_(buf)  # one-shot IPC kernel under PTG_IPC_ALLREDUCE=1
                     sums.copy_(buf[: k * Dm].view(k, Dm)); counts.copy_(buf[k * Dm:])
                 D.kmeans_update(sums, counts, C, moved, cn=cn, done=state)
                 D.kmeans_check(moved, tol * tol, state)

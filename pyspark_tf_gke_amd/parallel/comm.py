@@ -174,6 +174,12 @@ def all_reduce_tensor_(t: torch.Tensor, op=dist.ReduceOp.SUM) -> torch.Tensor:
     device when the backend cannot reach it, e.g. CPU tensors under RCCL)."""
     if not is_initialized() or dist.get_world_size() == 1:
         return t
+    if op == dist.ReduceOp.SUM and t.is_cuda:
+        from . import ipc
+
+        fast = ipc.get(t.device)  # PTG_IPC_ALLREDUCE=1: one-shot kernel over peer-mapped HBM
+        if fast is not None and fast.fits(t):
+            return fast.all_reduce_(t)
     dev = _ctl_device()
     if t.device == dev or (dev.type == "cuda" and t.is_cuda):
         dist.all_reduce(t, op=op)

@@ -1,0 +1,79 @@
+"""One-shot IPC all-reduce (csrc/kernels/comm.hip, parallel/ipc.py) against the exact sum.
+
+On the 1-GPU box two ranks share cuda:0 (gloo process group for the handle exchange; HIP IPC opens
+another process's allocation on the same device just as on a peer): the kernel's slot / epoch-flag
+protocol, the cross-process visibility and the bounded wait are all exercised.  On an 8-GPU node the
+same code maps the peers over xGMI."""
+import json
+import os
+import subprocess
+import sys
+import textwrap
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+BODY = """
+import json, torch
+from pyspark_tf_gke_amd.parallel import comm, ipc
+comm.init(backend="gloo", device_type="cuda")
+r, w = comm.rank(), comm.world_size()
+dev = torch.device("cuda", torch.cuda.current_device())
+ar = ipc.IpcAllReduce(dev, cap_bytes=1 << 20, spin_limit=50_000_000)
+cases = [(1, torch.float32), (100, torch.float32), (15453, torch.float32), (70000, torch.float64),
+         (5000, torch.int64), (262144, torch.float32), (3, torch.float64)] * 3
+
+
+def make(it, rank, n, dt):
+    g = torch.Generator().manual_seed(1000 * it + rank)
+    if dt == torch.int64:
+        return torch.randint(-1000, 1000, (n,), generator=g)
+    return (torch.randn(n, generator=g, dtype=torch.float64) * 100).to(dt)
+
+
+worst, exact = 0.0, True
+for it, (n, dt) in enumerate(cases):
+    x = make(it, r, n, dt).to(dev)
+    ar.all_reduce_(x)
+    parts = [make(it, q, n, dt).to(torch.int64 if dt == torch.int64 else torch.float64) for q in range(w)]
+    ref = sum(parts)
+    mag = sum(p.abs() for p in parts)
+    got = x.cpu()
+    if dt == torch.int64:
+        exact = exact and bool(torch.equal(got, ref))
+    else:
+        # fp32 sums round once per add: scale by the magnitudes added, not by the (cancelling) result
+        err = float(((got.double() - ref).abs() / (mag + 1e-30)).max())
+        worst = max(worst, err)
+torch.cuda.synchronize()
+ar.check()
+# in-flight reuse: many back-to-back calls without host syncs in between
+y = torch.ones(4096, device=dev)
+for _ in range(50):
+    ar.all_reduce_(y)
+    y.div_(w)
+torch.cuda.synchronize()
+ar.check()
+ones = bool(torch.allclose(y.cpu(), torch.ones(4096)))
+ar.close()
+print("RESULT", json.dumps({"worst": worst, "exact": exact, "ones": ones, "epochs": ar.epoch}), flush=True)
+"""
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
+@pytest.mark.parametrize("nproc", [2, 3])
+def test_ipc_allreduce_matches_sum(nproc):
+    env = dict(os.environ)
+    env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    cmd = [sys.executable, "-m", "pyspark_tf_gke_amd.runtime.launcher", "--nproc", str(nproc), "--",
+           sys.executable, "-c", textwrap.dedent(BODY)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=180, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    res = [json.loads(line.split("RESULT ", 1)[1]) for line in r.stdout.splitlines() if "RESULT " in line]
+    assert len(res) == nproc, r.stdout[-2000:]
+    for v in res:
+        assert v["exact"] and v["ones"] and v["worst"] < 1e-6, v
+        assert v["epochs"] == 21 + 50, v
