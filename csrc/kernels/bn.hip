@@ -28,21 +28,23 @@ namespace {
 
 constexpr int BN_G = 64;
 
-// Rows per block: ~1024 blocks for big tensors, but at least 16 rows per thread (memory-level
-// parallelism) and at least 64 rows per block, so the 2*C partial-sum atomics a block flushes stay
-// small next to the 2*C*rows bytes it reads (C = 2048 layers have only a few thousand rows).
-inline int bn_rows_per_block(long M, int rpi) {
-  long r = (M + 1023) / 1024;
-  if (r < 16L * rpi) r = 16L * rpi;
-  if (r < 64) r = 64;
-  r = (r + rpi - 1) / rpi * rpi;
-  return (int)r;
+// Channel slices: a workgroup reduces BN_CS channels (8 threads x 8 channels) over 32 rows at a time,
+// and grid.y walks the C / BN_CS slices.  With whole-C rows per workgroup, the C = 1024 / 2048 layers
+// (a few thousand rows) ran ~100-400 workgroups of 1 row per pass: too few bytes in flight for HBM
+// (0.7-2 TB/s measured).  Rows per workgroup: ~1024 workgroups in total, at least 8 rows per thread
+// so the 2*BN_CS partial-sum atomics a workgroup flushes stay small next to the bytes it reads.
+constexpr int BN_CS = 64;
+inline int bn_slice(int C) { return (C <= BN_CS || C % BN_CS) ? C : BN_CS; }
+inline int bn_rows_per_block(long M, int rpi, int slices) {
+  long per_thread = (M * slices + 1024L * rpi - 1) / (1024L * rpi);
+  if (per_thread < 8) per_thread = 8;
+  return (int)(per_thread * rpi);
 }
 
 // Shared LDS reduction of per-thread [8] partials over the `rpi` row slots of each channel slot,
 // then one atomic per (channel, array) into the block's partial group.
 PTG_DEV void bn_flush(float (*red)[256][8], const float* s, const float* q, int tid, int cpt, int rpi,
-                      float* part, int C) {
+                      float* part, int C, int cbase) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) { red[0][tid][j] = s[j]; red[1][tid][j] = q[j]; }
   __syncthreads();
@@ -54,7 +56,7 @@ PTG_DEV void bn_flush(float (*red)[256][8], const float* s, const float* q, int 
 #pragma unroll
       for (int j = 0; j < 8; ++j) { as[j] += red[0][r * cpt + tid][j]; aq[j] += red[1][r * cpt + tid][j]; }
     }
-    float* p = part + (long)(blockIdx.x % BN_G) * 2 * C;
+    float* p = part + (long)(blockIdx.x % BN_G) * 2 * C + cbase;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       atomicAdd(p + tid * 8 + j, as[j]);
@@ -88,11 +90,12 @@ PTG_DEV void bn_part_sums(float* part, int C, int c, double& s, double& q) {
 
 }  // namespace
 
-__global__ __launch_bounds__(256) void bn_stats_k(const bf16_t* __restrict__ z, long M, int C, int rpb,
+__global__ __launch_bounds__(256) void bn_stats_k(const bf16_t* __restrict__ z, long M, int C, int rpb, int cs,
                                                   float* __restrict__ part) {
   __shared__ float red[2][256][8];
-  const int tid = threadIdx.x, cpt = C >> 3, rpi = 256 / cpt;
+  const int tid = threadIdx.x, cpt = cs >> 3, rpi = 256 / cpt, cbase = blockIdx.y * cs;
   const int slot = tid % cpt, rsub = tid / cpt;
+  z += cbase;
   float s[8], q[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) { s[j] = 0.f; q[j] = 0.f; }
@@ -118,7 +121,7 @@ __global__ __launch_bounds__(256) void bn_stats_k(const bf16_t* __restrict__ z, 
       for (int j = 0; j < 8; ++j) { s[j] += f[j]; q[j] = fmaf(f[j], f[j], q[j]); }
     }
   }
-  bn_flush(red, s, q, tid, cpt, rpi, part, C);
+  bn_flush(red, s, q, tid, cpt, rpi, part, C, cbase);
 }
 
 __global__ __launch_bounds__(256) void bn_finalize_k(float* __restrict__ part, int C, long M,
@@ -182,18 +185,21 @@ __global__ __launch_bounds__(256) void bn_apply_k(const bf16_t* __restrict__ z, 
 // fmaf(z, scale, shift) > 0 - exactly the forward's pre-activation when no residual was added, so
 // the y tensor is not read at all (a third less traffic for those BatchNormalizations).
 __global__ __launch_bounds__(256) void bn_bwd_reduce_k(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
-                                                       const bf16_t* __restrict__ z, long M, int C, int rpb,
+                                                       const bf16_t* __restrict__ z, long M, int C, int rpb, int cs,
                                                        int relu, float* __restrict__ part,
                                                        const float* __restrict__ scale, const float* __restrict__ shift) {
   __shared__ float red[2][256][8];
-  const int tid = threadIdx.x, cpt = C >> 3, rpi = 256 / cpt;
+  const int tid = threadIdx.x, cpt = cs >> 3, rpi = 256 / cpt, cbase = blockIdx.y * cs;
   const int slot = tid % cpt, rsub = tid / cpt;
+  dy += cbase;
+  z += cbase;
+  if (y) y += cbase;
   float s[8], q[8], sc[8], sh[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) { s[j] = 0.f; q[j] = 0.f; sc[j] = 0.f; sh[j] = 0.f; }
   if (relu == 2) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { sc[j] = scale[slot * 8 + j]; sh[j] = shift[slot * 8 + j]; }
+    for (int j = 0; j < 8; ++j) { sc[j] = scale[cbase + slot * 8 + j]; sh[j] = shift[cbase + slot * 8 + j]; }
   }
   const long r0 = (long)blockIdx.x * rpb, r1 = min(M, r0 + rpb);
   auto acc_row = [&](const U4& vd, const U4& vz, const U4& vy) {
@@ -232,7 +238,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_k(const bf16_t* __restrict_
       acc_row(vd, *(const U4*)(z + off), relu == 1 ? *(const U4*)(y + off) : vd);
     }
   }
-  bn_flush(red, s, q, tid, cpt, rpi, part, C);
+  bn_flush(red, s, q, tid, cpt, rpi, part, C, cbase);
 }
 
 // dz = gamma*rstd*(g - mean(g) - xhat*mean(g*xhat)) = a*g + c1*z + c0.
@@ -411,10 +417,10 @@ extern "C" {
 // part: fp32 [BN_G][2][C], zero on entry (the finalize kernels re-zero it after reading).  C % 8 == 0 and C <= 2048.
 int ptg_bn_stats(const void* z, long M, int C, float* part, hipStream_t s) {
   if (C % 8 || C > 2048 || M <= 0) return (int)hipErrorInvalidValue;
-  const int rpi = 256 / (C / 8);
-  const int rpb = bn_rows_per_block(M, rpi);
-  const int grid = ptg_ceil_div(M, rpb);
-  hipLaunchKernelGGL(bn_stats_k, dim3(grid), dim3(256), 0, s, (const bf16_t*)z, M, C, rpb, part);
+  const int cs = bn_slice(C), rpi = 256 / (cs / 8);
+  const int rpb = bn_rows_per_block(M, rpi, C / cs);
+  hipLaunchKernelGGL(bn_stats_k, dim3(ptg_ceil_div(M, rpb), C / cs), dim3(256), 0, s, (const bf16_t*)z, M, C, rpb,
+                     cs, part);
   PTG_RETURN_LAUNCH();
 }
 
@@ -439,10 +445,10 @@ int ptg_bn_bwd_reduce(const void* dy, const void* y, const void* z, long M, int 
                       const float* scale, const float* shift, hipStream_t s) {
   if (relu == 2 && (!scale || !shift)) return (int)hipErrorInvalidValue;
   if (C % 8 || C > 2048 || M <= 0) return (int)hipErrorInvalidValue;
-  const int rpi = 256 / (C / 8);
-  const int rpb = bn_rows_per_block(M, rpi);
-  hipLaunchKernelGGL(bn_bwd_reduce_k, dim3(ptg_ceil_div(M, rpb)), dim3(256), 0, s, (const bf16_t*)dy,
-                     (const bf16_t*)y, (const bf16_t*)z, M, C, rpb, relu, part, scale, shift);
+  const int cs = bn_slice(C), rpi = 256 / (cs / 8);
+  const int rpb = bn_rows_per_block(M, rpi, C / cs);
+  hipLaunchKernelGGL(bn_bwd_reduce_k, dim3(ptg_ceil_div(M, rpb), C / cs), dim3(256), 0, s, (const bf16_t*)dy,
+                     (const bf16_t*)y, (const bf16_t*)z, M, C, rpb, cs, relu, part, scale, shift);
   PTG_RETURN_LAUNCH();
 }
 

@@ -22,7 +22,7 @@ def _lib(hip_built):
     return hip_built
 
 
-@pytest.mark.parametrize("M,C", [(4096, 64), (1000, 256), (392, 2048), (50176, 128)])
+@pytest.mark.parametrize("M,C", [(4096, 64), (1000, 256), (392, 2048), (50176, 128), (6272, 2048), (25088, 512), (300, 96), (100000, 256)])
 def test_bn_forward_backward(M, C):
     torch.manual_seed(0)
     z = (torch.randn(M, C) * 2 + 0.5).to(torch.bfloat16)
@@ -56,7 +56,7 @@ def test_bn_forward_backward(M, C):
         assert _rel(out[DEV][k], out["cpu"][k]) < 2e-2, k
 
 
-@pytest.mark.parametrize("M,C", [(4096, 64), (1000, 256), (392, 2048)])
+@pytest.mark.parametrize("M,C", [(4096, 64), (1000, 256), (392, 2048), (6272, 1024), (300, 96)])
 def test_bn_backward_mask_from_z(M, C):
     """BN without a residual: the ReLU mask recomputed from z (y not read) == the mask from y."""
     torch.manual_seed(5)
