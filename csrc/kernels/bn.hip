@@ -65,31 +65,27 @@ PTG_DEV void bn_flush(float (*red)[256][8], const float* s, const float* q, int 
   }
 }
 
-// Totals over the BN_G partial groups of channel c, read and re-zeroed (the buffer is reused).  The
-// finalize kernels give each channel 8 adjacent lanes (lane gl sums groups gl, gl+8, ...; xor-shuffle
-// over the 8): 16 loads + 16 stores in flight per lane instead of 128 + 128 dependent-on-vmcnt ones
-// per thread (8-12 us per launch measured with one lane per channel, 106 launches per ResNet-50 step).
-PTG_DEV void bn_part_sums(float* part, int C, int c, int gl, bool valid, double& s, double& q) {
-  constexpr int K = BN_G / 8;
-  float a[K], b[K];
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    const float* p = part + (long)(gl + 8 * k) * 2 * C;
-    a[k] = valid ? p[c] : 0.f;
-    b[k] = valid ? p[C + c] : 0.f;
-  }
+// Totals over the BN_G partial groups of channel c, read and re-zeroed (the buffer is reused).  All
+// 2*BN_G loads are issued before any store: the finalize kernels are one or a few workgroups, so
+// their time is the number of dependent memory round trips (stores interleaved with the loads
+// serialised every load (possible aliasing); 8 batches of 8 groups still measured ~9 us per launch,
+// 106 launches per ResNet-50 step).
+PTG_DEV void bn_part_sums(float* part, int C, int c, double& s, double& q) {
   s = 0.0; q = 0.0;
+  float a[BN_G], b[BN_G];
 #pragma unroll
-  for (int k = 0; k < K; ++k) { s += a[k]; q += b[k]; }
-  if (valid) {
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      float* p = part + (long)(gl + 8 * k) * 2 * C;
-      p[c] = 0.f; p[C + c] = 0.f;
-    }
+  for (int g = 0; g < BN_G; ++g) {
+    const float* p = part + (long)g * 2 * C;
+    a[g] = p[c];
+    b[g] = p[C + c];
   }
 #pragma unroll
-  for (int o = 1; o < 8; o <<= 1) { s += __shfl_xor(s, o, 64); q += __shfl_xor(q, o, 64); }
+  for (int g = 0; g < BN_G; ++g) { s += a[g]; q += b[g]; }
+#pragma unroll
+  for (int g = 0; g < BN_G; ++g) {
+    float* p = part + (long)g * 2 * C;
+    p[c] = 0.f; p[C + c] = 0.f;
+  }
 }
 
 }  // namespace
@@ -135,15 +131,15 @@ __global__ __launch_bounds__(256) void bn_finalize_k(float* __restrict__ part, i
                                                      float* __restrict__ scale, float* __restrict__ shift,
                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                                      int training) {
-  const int c = blockIdx.x * 32 + (threadIdx.x >> 3), gl = threadIdx.x & 7;
-  const bool valid = c < C;
-  double s = 0.0, q = 0.0;
-  if (training) bn_part_sums(part, C, c, gl, valid, s, q);  // all 64 lanes of the wave shuffle
-  if (!valid || gl) return;
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  // every per-channel operand is loaded up front, in the same round trip as the partial sums
   const float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
   const float mm0 = mmean ? mmean[c] : 0.f, mv0 = mmean ? mvar[c] : 0.f;
   float mean, var;
   if (training) {
+    double s, q;
+    bn_part_sums(part, C, c, s, q);
     const double invM = 1.0 / (double)M;
     const double m = s * invM;
     double v = q * invM - m * m;
@@ -253,13 +249,12 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_k(float* __restrict__ par
                                                          const float* __restrict__ rstd,
                                                          float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                          float* __restrict__ coef) {
-  const int c = blockIdx.x * 32 + (threadIdx.x >> 3), gl = threadIdx.x & 7;
-  const bool valid = c < C;
-  double sg, sgz;
-  bn_part_sums(part, C, c, gl, valid, sg, sgz);
-  if (!valid || gl) return;
-  const float m = mean[c], rs = rstd[c], gm = gamma ? gamma[c] : 1.f;
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  const float m = mean[c], rs = rstd[c], gm = gamma ? gamma[c] : 1.f;  // loaded with the partials
   const float dg0 = dgamma ? dgamma[c] : 0.f, db0 = dbeta ? dbeta[c] : 0.f;
+  double sg, sgz;
+  bn_part_sums(part, C, c, sg, sgz);
   const float db = (float)sg;
   const float dg = (float)((sgz - (double)m * sg) * rs);
   if (dgamma) dgamma[c] = dg0 + dg;
@@ -432,7 +427,7 @@ int ptg_bn_stats(const void* z, long M, int C, float* part, hipStream_t s) {
 int ptg_bn_finalize(float* part, int C, long M, const float* gamma, const float* beta, float eps,
                     float momentum, float* mmean, float* mvar, float* scale, float* shift, float* mean_out,
                     float* rstd_out, int training, hipStream_t s) {
-  hipLaunchKernelGGL(bn_finalize_k, dim3(ptg_ceil_div(C, 32)), dim3(256), 0, s, part, C, M, gamma, beta, eps,
+  hipLaunchKernelGGL(bn_finalize_k, dim3(ptg_ceil_div(C, 256)), dim3(256), 0, s, part, C, M, gamma, beta, eps,
                      momentum, mmean, mvar, scale, shift, mean_out, rstd_out, training);
   PTG_RETURN_LAUNCH();
 }
@@ -459,7 +454,7 @@ int ptg_bn_bwd_reduce(const void* dy, const void* y, const void* z, long M, int 
 
 int ptg_bn_bwd_finalize(float* part, int C, long M, const float* gamma, const float* mean, const float* rstd,
                         float* dgamma, float* dbeta, float* coef, hipStream_t s) {
-  hipLaunchKernelGGL(bn_bwd_finalize_k, dim3(ptg_ceil_div(C, 32)), dim3(256), 0, s, part, C, M, gamma, mean, rstd,
+  hipLaunchKernelGGL(bn_bwd_finalize_k, dim3(ptg_ceil_div(C, 256)), dim3(256), 0, s, part, C, M, gamma, mean, rstd,
                      dgamma, dbeta, coef);
   PTG_RETURN_LAUNCH();
 }
