@@ -259,6 +259,8 @@ class MultiWorkerMirroredStrategy(Strategy):
     this moves (w-1)/w * (4 + 2) bytes per bf16-forward parameter instead of the all-reduce's
     (w-1)/w * 8 over xGMI.  Without it: bucketed fp32 all-reduce launched during backward."""
 
+    side_stream_ok = True  # gradient collectives go through streams.launch (see _rs / _launch)
+
     def __init__(self, cluster_resolver=None, communication_options=None, bucket_mb: float | None = None,
                  device=None, sharded_update: bool | None = None):
         super().__init__(device)
@@ -285,10 +287,13 @@ class MultiWorkerMirroredStrategy(Strategy):
 
     # ---- replicated update: bucketed all-reduce
     def _launch(self, model, hi: int) -> None:
+        from ..nn import streams as S
+
         g = model.store.flat_grad
         while self._launched < hi:
             end = min(hi, self._launched + 4 * self.bucket_elems)
-            self._works.append(comm.all_reduce_(g[self._launched:end], async_op=True))
+            seg = g[self._launched:end]
+            self._works.append(S.launch(lambda: comm.all_reduce_(seg, async_op=True), seg.device))
             self._launched = end
 
     # ---- sharded update
@@ -296,7 +301,12 @@ class MultiWorkerMirroredStrategy(Strategy):
         st = model.store
         if b.gshard is None or b.gshard.device != st.flat_grad.device:
             b.gshard = torch.empty(b.shi - b.slo, dtype=torch.float32, device=st.flat_grad.device)
-        plan.rs_works.append(comm.reduce_scatter_flat(b.gshard, st.flat_grad[b.lo:b.hi], async_op=True))
+        # through the step's side stream (nn/streams.py): after this bucket's side-stream wgrads and
+        # everything the compute stream queued so far, without making the compute stream wait
+        from ..nn import streams as S
+
+        g = st.flat_grad[b.lo:b.hi]
+        plan.rs_works.append(S.launch(lambda: comm.reduce_scatter_flat(b.gshard, g, async_op=True), g.device))
         plan.launched[b.idx] = True
 
     def _wait_gather(self, model, plan, b) -> None:

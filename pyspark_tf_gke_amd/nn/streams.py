@@ -41,9 +41,10 @@ class SideStream:
         side = _stream(dev)
         side.wait_stream(torch.cuda.current_stream(side.device))
         with torch.cuda.stream(side):
-            fn()
+            out = fn()
         if side not in self._forks:
             self._forks.append(side)
+        return out
 
     def join(self) -> None:
         for side in self._forks:
@@ -52,11 +53,13 @@ class SideStream:
 
 
 def for_step(store, strategy) -> SideStream | None:
-    """A SideStream for this training step, or None (CPU, disabled, or a data-parallel strategy
-    whose per-op gradient hooks read the gradients as soon as each op's backward returns)."""
+    """A SideStream for this training step, or None (CPU, disabled, or a strategy that did not opt
+    in).  Data-parallel strategies launch their per-bucket gradient collectives through
+    :func:`launch` too, so a collective is ordered after the side-stream wgrads of its bucket without
+    making the step's stream wait for them."""
     if not ENABLED or not store.flat.is_cuda:
         return None
-    if strategy is not None and strategy.world_size != 1:
+    if strategy is not None and strategy.world_size != 1 and not getattr(strategy, "side_stream_ok", False):
         return None
     return SideStream()
 
@@ -69,13 +72,13 @@ def current() -> SideStream | None:
     return _CUR[0]
 
 
-def launch(fn, dev) -> None:
-    """Weight-gradient launch: forked onto the side stream when a step has one, else inline."""
+def launch(fn, dev):
+    """Weight-gradient (or gradient-collective) launch: forked onto the side stream when a step has
+    one, else inline.  Returns ``fn()``'s result (e.g. an async collective's work handle)."""
     side = _CUR[0]
     if side is not None and torch.device(dev).type == "cuda":
-        side.fork(fn, dev)
-    else:
-        fn()
+        return side.fork(fn, dev)
+    return fn()
 
 
 class active:
