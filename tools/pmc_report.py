@@ -1,7 +1,7 @@
 #!/usr/bin/env python
 """Per-kernel MFMA / LDS / memory report from the three PMC passes of tools/gpu_pmc_evidence.sh.
 
-usage: python tools/pmc_report.py <dir_a> <dir_b> <dir_c> [steps]
+usage: python tools/pmc_report.py <dir_a> <dir_b> [<dir_c>] [steps]   (dir_c: a WRITE_SIZE pass)
 
   MFMA util   SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs * 1024 SIMDs)  (busy fraction of
               every SIMD's matrix core over the kernel; GUI_ACTIVE reads high on sub-0.3 ms
@@ -36,10 +36,14 @@ def short(n):
 
 
 def main():
-    da, db, dc = sys.argv[1:4]
-    steps = float(sys.argv[4]) if len(sys.argv) > 4 else 1.0
+    args = sys.argv[1:]
+    dirs = [a for a in args if os.path.isdir(a)]
+    rest = [a for a in args if not os.path.isdir(a)]
+    da, db = dirs[0], dirs[1]
+    dc = dirs[2] if len(dirs) > 2 else None
+    steps = float(rest[0]) if rest else 1.0
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
-    for d in (da, db, dc):
+    for d in [x for x in (da, db, dc) if x]:
         per, dur, name = load(d)
         for k, cs in per.items():
             a = agg[short(name[k])]
