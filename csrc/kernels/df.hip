@@ -876,15 +876,17 @@ __global__ __launch_bounds__(256) void sort_count_k(const unsigned long long* __
   hist[(long)tid * ntiles + b] = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
 }
 
-// vals_in == nullptr: payload = row index (first pass of a fresh sort)
+// vals_in == nullptr: payload = row index (first pass of a fresh sort).  VT = unsigned int when the
+// row count fits 32 bits: 12 instead of 16 bytes per row read and written by every pass.
+template <typename VT>
 __global__ __launch_bounds__(256) void sort_scatter_k(const unsigned long long* __restrict__ keys_in,
-                                                      const long long* __restrict__ vals_in, long n,
+                                                      const VT* __restrict__ vals_in, long n,
                                                       unsigned long long base, int shift, int ntiles,
                                                       const long long* __restrict__ offs,
                                                       unsigned long long* __restrict__ keys_out,
-                                                      long long* __restrict__ vals_out) {
+                                                      VT* __restrict__ vals_out) {
   __shared__ unsigned long long sk[ST];
-  __shared__ long long sv[ST];
+  __shared__ VT sv[ST];
   __shared__ unsigned char sd[ST];
   __shared__ unsigned int wc[4][SB];
   __shared__ unsigned int woff[4][SB];
@@ -896,7 +898,7 @@ __global__ __launch_bounds__(256) void sort_scatter_k(const unsigned long long* 
   const int nr = (int)((n - s0) < ST ? (n - s0) : ST);
   goff[tid] = offs[(long)tid * ntiles + b];
   unsigned long long k[SRPT];
-  long long v[SRPT];
+  VT v[SRPT];
   int d[SRPT], r[SRPT];
 #pragma unroll
   for (int j = 0; j < SRPT; ++j) {
@@ -904,7 +906,7 @@ __global__ __launch_bounds__(256) void sort_scatter_k(const unsigned long long* 
     d[j] = -1;
     if (i < nr) {
       k[j] = keys_in[s0 + i];
-      v[j] = vals_in ? vals_in[s0 + i] : s0 + i;
+      v[j] = vals_in ? vals_in[s0 + i] : (VT)(s0 + i);
       d[j] = (int)((k[j] - base) >> shift) & (SB - 1);
     }
   }
@@ -1251,13 +1253,20 @@ int ptg_sort_count(const void* keys, long n, long base, int shift, void* hist, h
                      (unsigned long long)base, shift, ntiles, (unsigned int*)hist);
   PTG_RETURN_LAUNCH();
 }
+// v32: payload is u32 (requires n <= 2^32) instead of i64
 int ptg_sort_scatter(const void* keys_in, const void* vals_in, long n, long base, int shift, const void* offs,
-                     void* keys_out, void* vals_out, hipStream_t s) {
+                     void* keys_out, void* vals_out, int v32, hipStream_t s) {
   const int ntiles = (int)((n + ST - 1) / ST);
   if (ntiles <= 0) return 0;
-  hipLaunchKernelGGL(sort_scatter_k, dim3(ntiles), dim3(256), 0, s, (const unsigned long long*)keys_in,
-                     (const long long*)vals_in, n, (unsigned long long)base, shift, ntiles, (const long long*)offs,
-                     (unsigned long long*)keys_out, (long long*)vals_out);
+  if (v32 && n > 4294967296L) return (int)hipErrorInvalidValue;
+  if (v32)
+    hipLaunchKernelGGL(sort_scatter_k<unsigned int>, dim3(ntiles), dim3(256), 0, s, (const unsigned long long*)keys_in,
+                       (const unsigned int*)vals_in, n, (unsigned long long)base, shift, ntiles, (const long long*)offs,
+                       (unsigned long long*)keys_out, (unsigned int*)vals_out);
+  else
+    hipLaunchKernelGGL(sort_scatter_k<long long>, dim3(ntiles), dim3(256), 0, s, (const unsigned long long*)keys_in,
+                       (const long long*)vals_in, n, (unsigned long long)base, shift, ntiles, (const long long*)offs,
+                       (unsigned long long*)keys_out, (long long*)vals_out);
   PTG_RETURN_LAUNCH();
 }
 int ptg_range_partition(const void* keys, long n, const void* split, int nsplit, void* part, void* counts,

@@ -232,6 +232,19 @@ def test_radix_sort_matches_stable_host_sort(hip_built, n, kind, desc):
     assert torch.equal(sk.cpu(), kh[torch.from_numpy(want)])
 
 
+def test_radix_sort_wide_payload(hip_built):
+    """An arbitrary int64 payload (not row ids) keeps the 64-bit scatter path: values above 2^32
+    come back intact, in stable key order."""
+    n = 300_001
+    g = torch.Generator().manual_seed(5)
+    k = torch.randint(0, 1 << 20, (n,), generator=g, dtype=torch.int64)
+    pay = torch.randint(-(1 << 62), 1 << 62, (n,), generator=g, dtype=torch.int64)
+    sk, sv = D.radix_sort_u64(k.cuda(), pay.cuda(), 0, (1 << 20) - 1)
+    order = np.argsort(k.numpy(), kind="stable")
+    assert torch.equal(sk.cpu(), k[torch.from_numpy(order)])
+    assert torch.equal(sv.cpu(), pay[torch.from_numpy(order)])
+
+
 def test_argsort_columns_gpu_vs_host(hip_built):
     """Multi-column orderBy permutation (asc/desc, nulls first/last) on the GPU equals the host."""
     n = 500_000
