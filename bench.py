@@ -105,6 +105,17 @@ def _build(workload, B, dev, seed, rank, world):
     return model, meta, xs, ys
 
 
+def _input_note(workload: str) -> str:
+    if workload == "mlp":
+        return "fp32 features resident in HBM"
+    if workload == "mnist":
+        return "fp32 28x28x1 images in [0, 1) resident in HBM"
+    if workload == "cnn_b1":
+        return ("in the timed step: uint8 NHWC images resident in HBM, read by the first conv's forward and "
+                "weight-gradient kernels themselves (/255 + channel pad in registers, no packed copy)")
+    return "in the timed step: uint8 NHWC images resident in HBM -> /255, channel-padded bf16 (pack_u8rgb4_k)"
+
+
 def _time_steps(model, xs, ys, steps, warmup):
     from pyspark_tf_gke_amd.parallel import comm
 
@@ -174,9 +185,7 @@ def bench_train(args, strategy, rank, world):
                       "parallelism": f"dp{world}" + (" (MultiWorkerMirroredStrategy, RCCL reduce-scatter/all-gather)"
                                                      if world > 1 else ""),
                       "optimizer": opt, "final_loss": round(logs["loss"], 6),
-                      "input_pipeline": ("in the timed step: uint8 NHWC images resident in HBM -> /255, "
-                                         "channel-padded bf16 (pack_u8rgb4_k)") if args.workload != "mlp"
-                      else "fp32 features resident in HBM"}}
+                      "input_pipeline": _input_note(args.workload)}}
     probe = _comm_probe(model, strategy)
     if probe is not None:
         res["comm"] = probe

@@ -123,6 +123,27 @@ template <> PTG_DEV vu2_t bload_vt<vu2_t>(Rsrc r, uint32_t off) {
 }
 
 // dpp row_shl:n - lane l receives lane l+n of its 16-lane row (others keep their own value)
+// The 6 bytes of an RGB pixel pair at byte offset o (o even) as two ALIGNED dword loads covering
+// [o & ~3, +8); sh = 8 * (o & 3) selects them.  The rsrc size is rounded up to 4 bytes, so the last
+// pair's window stays in range (the caching allocator's 512-byte rounding backs the 2 extra bytes).
+struct U8Pair { uint32_t w0, w1, sh; };
+PTG_DEV U8Pair u8pair_load(Rsrc r, uint32_t o, bool ok) {
+  const uint32_t a = o & ~3u;
+  return U8Pair{bload4(r, ok ? a : PTG_OOB), bload4(r, ok ? a + 4u : PTG_OOB), (o & 3u) * 8u};
+}
+PTG_DEV U4 u8pair_to_bf16x8(const U8Pair& p) {
+  constexpr float s = 1.f / 255.f;
+  const unsigned long long v = (((unsigned long long)p.w1 << 32) | p.w0) >> p.sh;
+  auto c = [&](int i) { return (float)((uint32_t)(v >> (8 * i)) & 255u) * s; };
+  U4 o;
+  o.x = pack_bf(c(0), c(1));
+  o.y = pack_bf(c(2), 0.f);
+  o.z = pack_bf(c(3), c(4));
+  o.w = pack_bf(c(5), 0.f);
+  return o;
+}
+PTG_DEV uint32_t u8_rsrc_bytes(long n_bytes) { return (uint32_t)((n_bytes + 3) & ~3L); }
+
 template <int NSH>
 PTG_DEV float row_shl(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), 0x100 | NSH, 0xF, 0xF, false));
@@ -591,7 +612,9 @@ PTG_DEV s16x4_t tr_read(const bf16_t* p) {
 // = dZ at each window's argmax, argq = the argmax position q = 2*dh + dw; dZ is zero elsewhere in
 // the window): each thread loads 4 channels of one pooled pixel (8 + 4 bytes instead of the 32
 // bytes of the dense 2x2 window) and expands them into the same dense LDS dZ tile.
-template <int C, int KS, int TW, int TH, int MF, int NB, bool RING, bool SPARSE = false>
+// U8 (C == 4 only): x is uint8 [N][H][W][3]; each halo pixel is three byte loads, converted to the
+// 4-channel bf16 pixel (/255, zero 4th channel) in registers before the LDS store.
+template <int C, int KS, int TW, int TH, int MF, int NB, bool RING, bool SPARSE = false, bool U8 = false>
 __global__ __launch_bounds__(256) void conv_wgrad_strip_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dz,
                                                           float* __restrict__ dw, int N, int H, int W, int Cout, int pad,
                                                           int tiles_h, int tiles_w, int nslices,
@@ -610,7 +633,9 @@ __global__ __launch_bounds__(256) void conv_wgrad_strip_k(const bf16_t* __restri
   constexpr int DPITCH = MF * 16 + 4;     // dZ tile pixel pitch (bf16): 8-byte aligned, bank-shifted
   constexpr int HALO_ELEMS = NROWS * ROWE;
   constexpr int DZ_ELEMS = M * DPITCH;
-  constexpr int PFN = (HR * HC * VPP + 255) / 256;
+  static_assert(!U8 || HC % 2 == 0, "uint8 halo rows are loaded as pixel pairs");
+  // U8: one slot = a pixel PAIR (16 bytes of bf16 in LDS); otherwise one 16-/8-byte vector
+  constexpr int PFN = U8 ? (HR * (HC / 2) + 255) / 256 : (HR * HC * VPP + 255) / 256;
   constexpr int DV = (SPARSE ? M / 4 : M) * MF * 4;  // 8-byte dZ vectors per tile (upper bound: Cout <= MF*16)
   constexpr int PFD = (DV + 255) / 256;
   static_assert(!SPARSE || (TH % 2 == 0 && TW % 2 == 0), "sparse dZ needs whole 2x2 windows per tile");
@@ -644,18 +669,26 @@ __global__ __launch_bounds__(256) void conv_wgrad_strip_k(const bf16_t* __restri
 #pragma unroll
   for (int k = 0; k < PFN; ++k) {
     const int idx = tid + k * 256;
-    const int pix = idx / VPP, vv = idx - pix * VPP;
-    pr_r[k] = pix / HC;
-    pr_c[k] = pix - pr_r[k] * HC;
-    pr_l[k] = pr_c[k] * PIX + vv * VE;
+    if constexpr (U8) {
+      pr_r[k] = idx / (HC / 2);
+      pr_c[k] = 2 * (idx - pr_r[k] * (HC / 2));
+      pr_l[k] = pr_c[k] * PIX;
+    } else {
+      const int pix = idx / VPP, vv = idx - pix * VPP;
+      pr_r[k] = pix / HC;
+      pr_c[k] = pix - pr_r[k] * HC;
+      pr_l[k] = pr_c[k] * PIX + vv * VE;
+    }
   }
-  VT pf[PFN];
+  static_assert(!U8 || (C == 4 && PIX == 4), "uint8 input is the 3-channel image (C padded to 4, unpadded pixels)");
+  VT pf[U8 ? 1 : PFN];
+  U8Pair pu[U8 ? PFN : 1];
   U2 pd[PFD];
   uint32_t pq[SPARSE ? PFD : 1];
   const int CV = Cout / 4;
   const int PH = H >> 1, PW = W >> 1;
   // buffer loads: halo padding, pixels past the image and unused slots read as 0 (PTG_OOB)
-  const Rsrc xr = make_rsrc(x, (uint32_t)((long)N * H * W * C * 2));
+  const Rsrc xr = make_rsrc(x, U8 ? u8_rsrc_bytes((long)N * H * W * 3) : (uint32_t)((long)N * H * W * C * 2));
   const Rsrc dr = make_rsrc(dz, (uint32_t)(SPARSE ? (long)N * PH * PW * Cout * 2 : (long)N * H * W * Cout * 2));
   const Rsrc qr = make_rsrc(argq, SPARSE ? (uint32_t)((long)N * PH * PW * Cout) : 0u);
   auto load_tile = [&](int s_, int th_, int nrows, int ih_first) {
@@ -665,7 +698,11 @@ __global__ __launch_bounds__(256) void conv_wgrad_strip_k(const bf16_t* __restri
     for (int k = 0; k < PFN; ++k) {
       const int ih = ih_first + pr_r[k], iw = ow0 - pad + pr_c[k];
       const bool ok = pr_r[k] < nrows && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
-      pf[k] = bload_vt<VT>(xr, ok ? img + (uint32_t)((ih * W + iw) * C + (pr_l[k] - pr_c[k] * PIX)) * 2u : PTG_OOB);
+      if constexpr (U8) {  // iw even, W even: both pixels of the pair are in the row or both are padding
+        pu[k] = u8pair_load(xr, (uint32_t)((n * H + ih) * W + iw) * 3u, ok && pr_r[k] < HR);
+      } else {
+        pf[k] = bload_vt<VT>(xr, ok ? img + (uint32_t)((ih * W + iw) * C + (pr_l[k] - pr_c[k] * PIX)) * 2u : PTG_OOB);
+      }
     }
 #pragma unroll
     for (int k = 0; k < PFD; ++k) {
@@ -692,8 +729,14 @@ __global__ __launch_bounds__(256) void conv_wgrad_strip_k(const bf16_t* __restri
         int slot = slot_first + pr_r[k];
         if constexpr (RING) slot = slot >= HR ? slot - HR : slot;
         bf16_t* dst = smem + slot * ROWE + pr_l[k];
-        *(VT*)dst = pf[k];
-        if constexpr (RING) *(VT*)(dst + HR * ROWE) = pf[k];
+        if constexpr (U8) {
+          const U4 v = u8pair_to_bf16x8(pu[k]);
+          *(U4*)dst = v;
+          if constexpr (RING) *(U4*)(dst + HR * ROWE) = v;
+        } else {
+          *(VT*)dst = pf[k];
+          if constexpr (RING) *(VT*)(dst + HR * ROWE) = pf[k];
+        }
       }
     }
 #pragma unroll
@@ -821,7 +864,11 @@ __global__ __launch_bounds__(256) void conv_wgrad_strip_k(const bf16_t* __restri
 // SPARSE: the sparse pool record (EPI_POOLS) instead of the full-resolution z: `z` receives, per
 // pooled element, the z of the window's argmax ([N][H/2][W/2][8]) and `argout` its position
 // q = 2*dh + dw (first maximum in q order wins, as in the dense backward).
-template <int KS, bool SPARSE>
+// U8: x is the raw decoded image batch, uint8 [N][H][W][3]: a pixel pair is three 2-byte buffer
+// loads (6 bytes instead of 16), and the /255 + zero 4th channel of pack_u8rgb4_k happens in
+// registers before the LDS store (same rounding), so no packed bf16 copy of the input is written.
+
+template <int KS, bool SPARSE, bool U8 = false>
 __global__ __launch_bounds__(256, 5) void conv1_pair_pool_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
                                                          const float* __restrict__ bias, const float* __restrict__ alpha,
                                                          bf16_t* __restrict__ z, bf16_t* __restrict__ pooled,
@@ -874,14 +921,19 @@ __global__ __launch_bounds__(256, 5) void conv1_pair_pool_k(const bf16_t* __rest
     pr_c[p] = idx - pr_r[p] * HP;
   }
   U4 pf[PFN];
-  const Rsrc xr = make_rsrc(x, (uint32_t)((long)N * H * W * C * 2));
+  U8Pair pu[U8 ? PFN : 1];
+  const Rsrc xr = make_rsrc(x, U8 ? u8_rsrc_bytes((long)N * H * W * 3) : (uint32_t)((long)N * H * W * C * 2));
   auto load_rows = [&](int n, int iw0, int ih_first, int nrows) {  // padding reads 0 (PTG_OOB)
-    const uint32_t img = (uint32_t)(n * H * W * C) * 2u;
 #pragma unroll
     for (int p = 0; p < PFN; ++p) {
       const int ih = ih_first + pr_r[p], iw = iw0 + 2 * pr_c[p];
       const bool ok = pr_r[p] < nrows && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
-      pf[p] = bload16(xr, ok ? img + (uint32_t)((ih * W + iw) * C) * 2u : PTG_OOB);
+      if constexpr (U8) {  // iw is even and W is even: the pair's second pixel is in the row too
+        pu[p] = u8pair_load(xr, (uint32_t)((n * H + ih) * W + iw) * 3u, ok);
+      } else {
+        const uint32_t img = (uint32_t)(n * H * W * C) * 2u;
+        pf[p] = bload16(xr, ok ? img + (uint32_t)((ih * W + iw) * C) * 2u : PTG_OOB);
+      }
     }
   };
   auto store_rows = [&](int nrows, int slot_first) {
@@ -891,8 +943,10 @@ __global__ __launch_bounds__(256, 5) void conv1_pair_pool_k(const bf16_t* __rest
         int slot = slot_first + pr_r[p];
         slot = slot >= HR ? slot - HR : slot;
         bf16_t* dst = smem + slot * ROWE + pr_c[p] * 8;
-        *(U4*)dst = pf[p];
-        *(U4*)(dst + HR * ROWE) = pf[p];
+        U4 v = pf[p];
+        if constexpr (U8) v = u8pair_to_bf16x8(pu[p]);
+        *(U4*)dst = v;
+        *(U4*)(dst + HR * ROWE) = v;
       }
     }
   };
@@ -1285,6 +1339,43 @@ int ptg_conv2d_wgrad_halo_sparse(const void* x, const void* dzsel, const void* a
   if (MF == 1) return wgrad_by_cin<5, 1, true>(x, dzsel, dw, N, H, W, C, Cout, pad, s, argq);
   if (MF == 2) return wgrad_by_cin<5, 2, true>(x, dzsel, dw, N, H, W, C, Cout, pad, s, argq);
   return wgrad_by_cin<5, 4, true>(x, dzsel, dw, N, H, W, C, Cout, pad, s, argq);
+}
+
+// First layer straight from the raw uint8 [N][H][W][3] image batch (no packed bf16 copy): the
+// 5x5 Cout=8 conv + bias + PReLU + 2x2 max-pool with the sparse pool record (epi 3 of
+// ptg_conv2d_fwd_halo), and its weight gradient from the sparse dZ record.  H, W even, pad 2.
+int ptg_conv1_pool_sparse_u8(const void* x_u8, const void* w, const float* bias, const float* alpha, void* zsel,
+                             void* pooled, void* arg, int N, int H, int W, hipStream_t s) {
+  if ((H & 1) || (W & 1) || !ptg_fits_2g((long)N * H * W * 3)) return (int)hipErrorInvalidValue;
+  const auto kern = conv1_pair_pool_k<5, true, true>;
+  static const int resident = ptg_resident_blocks((const void*)kern);
+  const int th = (H + 3) / 4, tw = (W + 63) / 64;
+  const long tiles = (long)N * th * tw;
+  const int grid = (int)std::min<long>(tiles, (long)resident * persist_oversub());
+  int* wq = persist_dynamic() ? work_queue(1, s) : nullptr;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, s, (const bf16_t*)x_u8, (const bf16_t*)w, bias, alpha,
+                     (bf16_t*)zsel, (bf16_t*)pooled, (uint8_t*)arg, N, H, W, 2, th, tw, wq, wq_chunk(tiles, grid));
+  PTG_RETURN_LAUNCH();
+}
+
+int ptg_conv1_wgrad_sparse_u8(const void* x_u8, const void* dzsel, const void* argq, float* dw, int N, int H, int W,
+                              int Cout, hipStream_t s) {
+  if (Cout != 8 || (H & 1) || (W & 1) || !ptg_fits_2g((long)N * H * W * 3)) return (int)hipErrorInvalidValue;
+  constexpr int C = 4, KS = 5, TW = 64, TH = 4, MF = 1;
+  constexpr bool RING = TH < 2 * (KS - 1);
+  constexpr int KF = KS * KS * C;
+  constexpr int NB = KF > 512 ? 4 : 2;
+  const auto kern = conv_wgrad_strip_k<C, KS, TW, TH, MF, NB, RING, true, true>;
+  static const int resident = ptg_resident_blocks((const void*)kern);
+  const int th = (H + TH - 1) / TH, tw = (W + TW - 1) / TW;
+  const long tiles = (long)N * tw * th;
+  const int nslices = (KF + 64 * NB - 1) / (64 * NB);
+  int chunks = (resident * persist_oversub() + nslices - 1) / nslices;
+  if (chunks > tiles) chunks = (int)tiles;
+  int* wq = persist_dynamic() ? work_queue(nslices, s) : nullptr;
+  hipLaunchKernelGGL(kern, dim3(chunks * nslices), dim3(256), 0, s, (const bf16_t*)x_u8, (const bf16_t*)dzsel, dw, N,
+                     H, W, Cout, 2, th, tw, nslices, (const uint8_t*)argq, wq, wq_chunk(tiles, chunks));
+  PTG_RETURN_LAUNCH();
 }
 
 // dynamic: 1 = persistent conv kernels claim tile chunks from a work queue, 0 = static ranges,

@@ -38,6 +38,11 @@ _HOST_FP32 = [os.environ.get("PTG_HOST_FP32") == "1"]
 # LDS, so the full-resolution z and dZ (335 MB each for CNN-B1 at batch 256) never exist.  Measured
 # on CNN-B1 b256: 118.6k vs 116.6k samples/s with the dense first-layer record.
 SPARSE_FIRST = os.environ.get("PTG_SPARSE_FIRST", "1") == "1"
+# That first layer reads the raw uint8 [N,H,W,3] image batch itself (conv.hip U8 loaders: /255 and
+# the zero 4th channel applied in registers) in both its forward and its weight gradient, so the
+# packed bf16 copy of the input (pack_u8rgb4_k: 3 B read + 8 B written per pixel, 8 B read twice
+# more) is never made.  PTG_RAW_U8_INPUT=0 restores the pack.
+RAW_U8 = os.environ.get("PTG_RAW_U8_INPUT", "1") != "0"
 
 
 def host_fp32(enabled: bool | None = None) -> bool:
@@ -135,7 +140,24 @@ class ConvOp(Op):
         t.fill_(value)
         return t
 
+    def _raw_u8_ok(self, x) -> bool:
+        """Raw uint8 images straight into the sparse first-layer kernels (same size, no resize)."""
+        OH, OW, Co = self.conv.out_shape
+        return (RAW_U8 and SPARSE_FIRST and self.first and x.is_cuda and x.dtype == torch.uint8 and x.dim() == 4
+                and x.shape[-1] == 3 and self.conv.cin_p == 4 and tuple(x.shape[1:3]) == tuple(self.conv.in_shape[:2])
+                and self.conv.kernel_size == (5, 5) and self.stride == 1 and self.pad == 2 and Co == 8
+                and self.pool is not None and OH % 2 == 0 and OW % 2 == 0 and self.conv.activation != "relu"
+                and self._halo()[0])
+
     def forward(self, x, ws, training):
+        if self._raw_u8_ok(x):
+            x = x.contiguous()
+            B = x.shape[0]
+            OH, OW, Co = self.conv.out_shape
+            b = self.conv.bias.data if self.conv.bias is not None else None
+            self._sel = True
+            self._x, self._sparse = x, True
+            return self._forward_pool_sparse(x, b, ws, B, OH, OW, Co, x.device)
         x = self._prep_input(x, ws)
         B = x.shape[0]
         OH, OW, Co = self.conv.out_shape

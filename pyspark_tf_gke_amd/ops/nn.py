@@ -133,6 +133,14 @@ def conv2d_fwd_fused(x, w, bias, pad: int, z_out, alpha=None, aux_out=None, epi=
         return z_out
     N, H, W, C = x.shape
     Cout, KS, _, Cw = w.shape
+    if x.dtype == torch.uint8:  # raw [N,H,W,3] images: the first-layer kernel packs them itself
+        if not (epi == "pools" and C == 3 and Cw == 4 and KS == 5 and Cout == 8 and pad == 2):
+            raise ValueError("conv2d_fwd_fused: uint8 input only for the 5x5 -> 8 sparse-pool first layer")
+        assert tuple(z_out.shape) == (N, H // 2, W // 2, Cout) and tuple(arg_out.shape) == tuple(z_out.shape)
+        need(w, torch.bfloat16, "conv1_u8.w")
+        hip("ptg_conv1_pool_sparse_u8", ptr(x), ptr(w), ptr(bias), ptr(alpha), ptr(z_out), ptr(aux_out), ptr(arg_out),
+            N, H, W)
+        return aux_out
     if epi == "pools":
         assert tuple(z_out.shape) == (N, H // 2, W // 2, Cout) and arg_out is not None
         assert arg_out.dtype == torch.uint8 and tuple(arg_out.shape) == tuple(z_out.shape)
@@ -169,6 +177,15 @@ def conv2d_wgrad_halo_sparse(x, dzsel, arg, pad: int, out, zeroed: bool = False)
         dz = ref.expand_pool_record(dzsel, arg, (N, H, W, Cout)).to(dzsel.dtype)
         return ref.conv2d_wgrad(x, dz, 1, pad, out, zeroed)
     assert tuple(dzsel.shape) == (N, H // 2, W // 2, Cout) and tuple(arg.shape) == tuple(dzsel.shape)
+    if x.dtype == torch.uint8:  # raw [N,H,W,3] images (first layer, see conv2d_fwd_fused)
+        if not (C == 3 and KS == 5 and Cout == 8 and pad == 2 and out.shape[-1] == 4):
+            raise ValueError("conv2d_wgrad_halo_sparse: uint8 input only for the 5x5 -> 8 first layer")
+        need(dzsel, torch.bfloat16, "wgrad_u8.dzsel"); need(arg, torch.uint8, "wgrad_u8.arg")
+        need(out, torch.float32, "wgrad_u8.out")
+        if not zeroed:
+            out.zero_()
+        hip("ptg_conv1_wgrad_sparse_u8", ptr(x), ptr(dzsel), ptr(arg), ptr(out), N, H, W, Cout)
+        return out
     need(x, torch.bfloat16, "wgrad_sparse.x"); need(dzsel, torch.bfloat16, "wgrad_sparse.dzsel")
     need(arg, torch.uint8, "wgrad_sparse.arg"); need(out, torch.float32, "wgrad_sparse.out")
     if not zeroed:

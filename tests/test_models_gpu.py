@@ -163,3 +163,31 @@ def test_head_mse_kernel_vs_fp32_reference(hip_built):
     assert abs(float(st[0]) - float((d * d).mean()) * B) <= 1e-4 * float((d * d).mean()) * B
     assert abs(float(st[1]) - float(d.abs().sum())) <= 1e-4 * float(d.abs().sum())
     assert float(st[3]) == B * N2 and float(st[4]) == B
+
+
+def test_raw_uint8_first_layer_matches_packed_input(hip_built):
+    """The first conv layer reading the raw uint8 [N,H,W,3] batch itself (U8 loaders of
+    conv1_pair_pool_k / conv_wgrad_strip_k) == the packed-bf16 path: identical forward (same /255
+    rounding), same first-layer weight gradient up to atomic-order noise, same losses.  W = 80 leaves
+    a partial 64-pixel tile; H = 62 a partial 4-row tile."""
+    from pyspark_tf_gke_amd.nn import engine as E
+
+    g = torch.Generator().manual_seed(1)
+    X = torch.randint(0, 256, (3, 16, 62, 80, 3), generator=g, dtype=torch.uint8)
+    Y = torch.rand(3, 16, 2, generator=g) * 60
+    res = []
+    for raw in (True, False):
+        E.RAW_U8 = raw
+        torch.manual_seed(0)
+        m = build_cnn_model((62, 80, 3), flat=True, summary=False, device="cuda")
+        pred = m.predict(X[0].cuda()) if hasattr(m, "predict") else None
+        first = m.ops[0]
+        m.store.zero_grad()
+        logs = [m.train_on_batch(X[i], Y[i], return_dict=True) for i in range(3)]
+        assert first._raw_u8_ok(X[0].cuda()) == raw
+        res.append((torch.as_tensor(pred).float().cpu(), logs, first.conv.kernel.data.detach().cpu().clone()))
+    E.RAW_U8 = True
+    assert torch.equal(res[0][0], res[1][0])
+    for a, b in zip(res[0][1], res[1][1]):
+        assert abs(a["loss"] - b["loss"]) <= 1e-3 * max(1.0, abs(b["loss"])), (a, b)
+    assert torch.allclose(res[0][2], res[1][2], rtol=1e-3, atol=1e-5)
