@@ -277,12 +277,22 @@ def linear_fwd(x, w, bias, act, out, workspace=None, splits: int = 0):
     return out
 
 
+# A plain GEMM with nothing to fuse goes to the vendor library when it measured faster: the big
+# Dense layer's dX (M = batch 256, N = 20480, K = 2048) is 34 us in hipBLASLt vs 45 us in gemm_kernel
+# (tools/dense_gemm_bench.py).  PTG_BLASLT_DX=0 keeps it on gemm_kernel.
+BLASLT_DX = os.environ.get("PTG_BLASLT_DX", "1") != "0"
+
+
 def linear_dx(dy, w, out):
     """out[M,K] bf16 = dy[M,N] @ w[N,K]."""
     if not on_device(dy):
         return ref.linear_dx(dy, w, out)
     M, N = dy.shape
     K = w.shape[1]
+    if BLASLT_DX and dy.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and out.dtype == torch.bfloat16 \
+            and M <= 512 and K >= 8192:
+        torch.matmul(dy, w, out=out)
+        return out
     gemm(M, K, N, dy, N, 1, w, K, 0, 0, out, K)
     return out
 

@@ -53,12 +53,20 @@ def test_gemm_splitk_atomic_and_bias_relu():
     _close(out, ref, 2e-2, 2e-2, "linear_fwd")
 
 
-def test_linear_dx_dw():
-    M, N, Kd = 128, 2048, 20480 // 8
+@pytest.mark.parametrize("blaslt", [False, True])
+def test_linear_dx_dw(blaslt):
+    """dX on gemm_kernel and, for the CNN-B1 shape class (M <= 512, K >= 8192), on hipBLASLt."""
+    M, N, Kd = (128, 2048, 20480 // 8) if not blaslt else (256, 2048, 20480)
     dy, w, x = rnd(M, N), rnd(N, Kd), rnd(M, Kd)
     dx = torch.empty(M, Kd, device=DEV, dtype=torch.bfloat16)
     K.linear_dx(dy.to(DEV), w.to(DEV), dx)
     _close(dx, dy.float() @ w.float(), 2e-2, 2e-2, "dx")
+    if blaslt:
+        K.BLASLT_DX = False  # the same shape on gemm_kernel agrees too
+        dx2 = torch.empty_like(dx)
+        K.linear_dx(dy.to(DEV), w.to(DEV), dx2)
+        K.BLASLT_DX = True
+        _close(dx2, dy.float() @ w.float(), 2e-2, 2e-2, "dx gemm_kernel")
     dw = torch.empty(N, Kd, device=DEV)
     K.linear_dw(dy.to(DEV), x.to(DEV), dw)
     _close(dw, dy.float().t() @ x.float(), 1e-3, 1e-3, "dw")

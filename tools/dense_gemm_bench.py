@@ -44,7 +44,7 @@ def main():
     p, m, v = torch.randn(N, Kd, device=dev), torch.zeros(N, Kd, device=dev), torch.zeros(N, Kd, device=dev)
     pb = torch.empty(N, Kd, device=dev, dtype=torch.bfloat16)
     res = {}
-    for s in (0, 1, 2, 4, 8, 16, 20):
+    for s in (0, 1, 4, 8, 16, 20, 25, 32, 40):
         res[f"fwd_splits{s}"] = timeit(lambda: K.linear_fwd(x, w, b, "relu", y, workspace=wsp, splits=s))
     res["dx"] = timeit(lambda: K.linear_dx(dy, w, dx))
     res["dw"] = timeit(lambda: K.linear_dw(dy, x, g))
