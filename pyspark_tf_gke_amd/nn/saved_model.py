@@ -3,16 +3,18 @@ reference itself only writes ``.keras`` files, train_tf_ps.py:675-676, :810-811)
 
 Layout written by :func:`save` (mirrors a TF SavedModel directory)::
 
+    <dir>/saved_model.pb                SavedModel proto: tags + serving_default SignatureDef (nn/tf_proto.py)
     <dir>/saved_model.json              graph (Keras layer configs + connectivity) and signatures
     <dir>/fingerprint.json              content hash of graph + variables
     <dir>/variables/variables.safetensors   every variable in Keras layout, keyed <layer>/<i>
     <dir>/variables/variables.index.json    name -> shape / dtype
     <dir>/assets/                           extra files (e.g. label_map.json)
 
-What is NOT reproduced: TF's protobuf encodings (``saved_model.pb`` MetaGraphDef/GraphDef and the
-TensorBundle ``variables.index``/``data`` shards) — TensorFlow and its proto schemas are not available
-here, so the graph is stored as the same Keras-config JSON the ``.keras`` zip uses and the tensors as
-safetensors.  :func:`load` restores a model whose ``signatures["serving_default"]`` runs inference on
+``saved_model.pb`` is a real protobuf ``SavedModel`` (wire-encoded by ``nn/tf_proto.py`` with TF's field
+numbers) holding the ``serve`` tag set and the ``serving_default`` signature, so TF tooling can read the
+serving contract.  What is NOT reproduced: the GraphDef body and the TensorBundle
+``variables.index``/``data`` shards — TensorFlow and its proto schemas are not available here, so the
+graph is stored as the same Keras-config JSON the ``.keras`` zip uses and the tensors as safetensors.  :func:`load` restores a model whose ``signatures["serving_default"]`` runs inference on
 the MI355X kernels, like ``tf.saved_model.load(...).signatures["serving_default"]``.
 """
 from __future__ import annotations
@@ -81,6 +83,12 @@ def save(model, export_dir: str, signatures=None, assets: dict | None = None) ->
             "signatures": {"serving_default": {"inputs": [in_name], "outputs": [out_name],
                                                "input_shape": [None, *model.input_shape],
                                                "output_shape": [None, *model.output_shape]}}}
+    from . import tf_proto
+
+    sig = tf_proto.signature_def({in_name: (f"serving_default_{in_name}:0", [None, *model.input_shape])},
+                                 {out_name: ("StatefulPartitionedCall:0", [None, *model.output_shape])})
+    with open(os.path.join(tmp, "saved_model.pb"), "wb") as fh:
+        fh.write(tf_proto.saved_model({"serving_default": sig}))
     body = json.dumps(meta, sort_keys=True).encode()
     with open(os.path.join(tmp, "saved_model.json"), "wb") as fh:
         fh.write(json.dumps(meta, indent=1).encode())
@@ -106,6 +114,18 @@ def load(export_dir: str, device=None) -> LoadedModel:
 
     with open(os.path.join(export_dir, "saved_model.json")) as fh:
         meta = json.load(fh)
+    pb = os.path.join(export_dir, "saved_model.pb")
+    if os.path.exists(pb):  # the proto's serving contract must agree with the JSON graph
+        from . import tf_proto
+
+        with open(pb, "rb") as fh:
+            proto = tf_proto.read(fh.read())
+        sd = meta["signatures"]["serving_default"]
+        got = proto["meta_graphs"][0]["signature_def"]["serving_default"]
+        if (got["inputs"][sd["inputs"][0]]["shape"] != sd["input_shape"]
+                or got["outputs"][sd["outputs"][0]]["shape"] != sd["output_shape"]):
+            raise ValueError(f"{pb}: serving_default signature disagrees with saved_model.json")
+        meta["saved_model_pb"] = proto
     g = meta["graph"]
     if g["class_name"] == "Functional":
         from .functional import model_from_config

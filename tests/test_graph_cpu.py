@@ -131,12 +131,83 @@ def test_saved_model_export_load(tmp_path):
                   np.random.rand(3, 32, 40, 3).astype(np.float32))):
         d = str(tmp_path / m.name)
         m.export(d, assets={"label_map.json": {"0": "a"}})
-        for f in ("saved_model.json", "fingerprint.json", "variables/variables.safetensors",
+        for f in ("saved_model.pb", "saved_model.json", "fingerprint.json", "variables/variables.safetensors",
                   "variables/variables.index.json", "assets/label_map.json"):
             assert os.path.exists(os.path.join(d, f)), f
         loaded = nn.saved_model.load(d, device="cpu")
         out = loaded.signatures["serving_default"](input_layer=x)["output_0"]
         np.testing.assert_allclose(out, m.predict(x), atol=1e-2)
+        sig = loaded.meta["saved_model_pb"]["meta_graphs"][0]["signature_def"]["serving_default"]
+        assert sig["inputs"]["input_layer"]["shape"] == [None, *x.shape[1:]]
+
+
+def _tf_saved_model_classes():
+    """SavedModel / MetaGraphDef / SignatureDef / TensorInfo message classes built by google.protobuf
+    from a descriptor with TensorFlow's field numbers (saved_model.proto, meta_graph.proto,
+    tensor_shape.proto): an encoder-independent parser for saved_model.pb."""
+    from google.protobuf import descriptor_pb2, descriptor_pool, message_factory
+
+    F = descriptor_pb2.FieldDescriptorProto
+    fd = descriptor_pb2.FileDescriptorProto(name="ptg_tf_subset.proto", package="tfsub", syntax="proto3")
+
+    def msg(name, fields, nested=()):
+        m = fd.message_type.add(name=name)
+        for n in nested:
+            m.nested_type.add().CopyFrom(n)
+        for num, fname, ftype, label, tname in fields:
+            f = m.field.add(name=fname, number=num, type=ftype, label=label)
+            if tname:
+                f.type_name = tname
+        return m
+
+    def entry(name, vtype):
+        e = descriptor_pb2.DescriptorProto(name=name)
+        e.options.map_entry = True
+        e.field.add(name="key", number=1, type=F.TYPE_STRING, label=F.LABEL_OPTIONAL)
+        e.field.add(name="value", number=2, type=F.TYPE_MESSAGE, label=F.LABEL_OPTIONAL, type_name=vtype)
+        return e
+
+    O, R = F.LABEL_OPTIONAL, F.LABEL_REPEATED
+    dim = descriptor_pb2.DescriptorProto(name="Dim")
+    dim.field.add(name="size", number=1, type=F.TYPE_INT64, label=O)
+    msg("TensorShapeProto", [(2, "dim", F.TYPE_MESSAGE, R, ".tfsub.TensorShapeProto.Dim")], [dim])
+    msg("TensorInfo", [(1, "name", F.TYPE_STRING, O, None), (2, "dtype", F.TYPE_INT32, O, None),
+                       (3, "tensor_shape", F.TYPE_MESSAGE, O, ".tfsub.TensorShapeProto")])
+    msg("SignatureDef", [(1, "inputs", F.TYPE_MESSAGE, R, ".tfsub.SignatureDef.InputsEntry"),
+                         (2, "outputs", F.TYPE_MESSAGE, R, ".tfsub.SignatureDef.OutputsEntry"),
+                         (3, "method_name", F.TYPE_STRING, O, None)],
+        [entry("InputsEntry", ".tfsub.TensorInfo"), entry("OutputsEntry", ".tfsub.TensorInfo")])
+    msg("MetaInfoDef", [(1, "meta_graph_version", F.TYPE_STRING, O, None), (4, "tags", F.TYPE_STRING, R, None),
+                        (5, "tensorflow_version", F.TYPE_STRING, O, None)])
+    msg("MetaGraphDef", [(1, "meta_info_def", F.TYPE_MESSAGE, O, ".tfsub.MetaInfoDef"),
+                         (5, "signature_def", F.TYPE_MESSAGE, R, ".tfsub.MetaGraphDef.SignatureDefEntry")],
+        [entry("SignatureDefEntry", ".tfsub.SignatureDef")])
+    msg("SavedModel", [(1, "saved_model_schema_version", F.TYPE_INT64, O, None),
+                       (2, "meta_graphs", F.TYPE_MESSAGE, R, ".tfsub.MetaGraphDef")])
+    pool = descriptor_pool.DescriptorPool()
+    pool.Add(fd)
+    return message_factory.GetMessageClass(pool.FindMessageTypeByName("tfsub.SavedModel"))
+
+
+def test_saved_model_pb_parses_with_protobuf(tmp_path):
+    from pyspark_tf_gke_amd.models import build_cnn_model
+
+    m = build_cnn_model((32, 40, 3), flat=True, summary=False, device="cpu")
+    d = str(tmp_path / "sm")
+    m.export(d)
+    SavedModel = _tf_saved_model_classes()
+    sm = SavedModel()
+    with open(os.path.join(d, "saved_model.pb"), "rb") as fh:
+        sm.ParseFromString(fh.read())
+    assert sm.saved_model_schema_version == 1 and len(sm.meta_graphs) == 1
+    mg = sm.meta_graphs[0]
+    assert list(mg.meta_info_def.tags) == ["serve"]
+    sig = mg.signature_def["serving_default"]
+    assert sig.method_name == "tensorflow/serving/predict"
+    ti = sig.inputs["input_layer"]
+    assert ti.dtype == 1 and ti.name == "serving_default_input_layer:0"
+    assert [d.size for d in ti.tensor_shape.dim] == [-1, 32, 40, 3]
+    assert [d.size for d in sig.outputs["output_0"].tensor_shape.dim] == [-1, 2]
 
 
 def test_native_libraries_link_completely():
