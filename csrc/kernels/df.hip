@@ -473,6 +473,25 @@ PTG_DEV double load_pay(const PayIn& in, int j, long i) {
   return ok ? v : __builtin_nan("");
 }
 
+// XCD-aware tile order for the scatter passes: the dispatcher deals consecutive workgroups round-
+// robin to the 8 XCDs, each with its own L2.  A digit's runs from consecutive tiles are adjacent in
+// the output, so a short run (16-32 rows at 256 bins) shares its first / last cache line with the
+// neighbouring tiles' runs; mapping workgroup b to tile xcd_tile(b) gives every XCD a contiguous
+// range of tiles, so those partial lines are completed in ONE L2 instead of being written partially
+// from several (cdna_hip_programming.md: XCD-aware blockIdx mapping).  A bijection on [0, ntiles).
+#ifndef PTG_XCD_TILES
+#define PTG_XCD_TILES 1
+#endif
+PTG_DEV int xcd_tile(int b, int ntiles) {
+#if PTG_XCD_TILES
+  const int q = ntiles >> 3, r = ntiles & 7, x = b & 7, i = b >> 3;
+  return x < r ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
+#else
+  (void)ntiles;
+  return b;
+#endif
+}
+
 // Keys travel as i64, or — when the first level finds max - min < 2^32 - 1 — as u32 offsets from
 // kbase = min (12 instead of 16 bytes per row through every later pass; the 1B-row / 1M-key
 // groupBy moves 21 % fewer bytes).  Digits always hash the ORIGINAL key, mix64(kbase + offset),
@@ -563,7 +582,7 @@ __global__ __launch_bounds__(NT) void radix_scatter_k(const KIN* __restrict__ ke
   __shared__ unsigned int cnt[RB];
   __shared__ unsigned int lstart[RB];
   __shared__ long long goff[RB];
-  const int tid = threadIdx.x, b = blockIdx.x;
+  const int tid = threadIdx.x, b = xcd_tile(blockIdx.x, gridDim.x);
   const long long s0 = tstart[b];
   const int nr = trows[b];
   if (tid < RB) {
@@ -788,6 +807,202 @@ __global__ __launch_bounds__(256) void part_agg2_k(const KT* __restrict__ okeys,
   }
 }
 
+
+// ---- dense small-range integer keys: one range level + direct-indexed LDS aggregation -----------
+// When a groupBy key column spans R = max - min + 1 <= 2^20 values (ids, codes, bucketed keys), a
+// partition by the top 8 bits of (key - lo) holds a contiguous window of W = 2^sh <= 4096 keys, so
+// its aggregate table is a direct-indexed LDS array: no stored keys, no probing, no spill, and ONE
+// partitioning pass instead of the two hash levels above (the 1B-row / 1M-key groupBy: count +
+// scatter + aggregate, ~12 of its 21 ms were the second level).
+//   range_count_k    per-tile 256-bin digit counts, digit-major [digit][tile], and per-tile [min, max]
+//                    (the host checks that every key fell inside the sample-guessed window)
+//   range_scatter_k  rows staged in LDS by digit, written as 256 contiguous runs; keys leave as u32
+//                    offsets (key - lo), values as f64 (null -> NaN)
+//   range_agg_k      (chunk, partition) workgroups: rows u32 / per-column sum f64 + count u32 over the
+//                    partition's W-key window in LDS, written out as one dense partial table per chunk
+//                    (plain coalesced stores, no atomics; the host sums the chunks: deterministic)
+#define RGB 256
+PTG_DEV int range_digit(long long k, long long lo, int sh) {
+  long long d = (k - lo) >> sh;
+  return d < 0 ? 0 : (d > RGB - 1 ? RGB - 1 : (int)d);  // out-of-window keys are detected via range
+}
+
+__global__ __launch_bounds__(256) void range_count_k(const long long* __restrict__ keys, long n, long long lo, int sh,
+                                                     int T, int ntiles, unsigned int* __restrict__ hist,
+                                                     long long* __restrict__ range) {
+  constexpr int RPT = RT / 256;
+  __shared__ unsigned int h[4][RGB];
+  __shared__ long long rmn[4], rmx[4];
+  const int tid = threadIdx.x, b = blockIdx.x, w = tid >> 6;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) h[q][tid] = 0;
+  const long s0 = (long)b * T;
+  const int nr = (int)min((long)T, n - s0);
+  long long k[RPT];
+#pragma unroll
+  for (int j = 0; j < RPT; ++j) {
+    const int i = tid + j * 256;
+    k[j] = i < nr ? keys[s0 + i] : 0;
+  }
+  long long mn = 0x7fffffffffffffffLL, mx = (long long)0x8000000000000000ULL;
+#pragma unroll
+  for (int j = 0; j < RPT; ++j)
+    if (tid + j * 256 < nr) { mn = k[j] < mn ? k[j] : mn; mx = k[j] > mx ? k[j] : mx; }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const long long a = __shfl_xor(mn, o, 64), c = __shfl_xor(mx, o, 64);
+    mn = a < mn ? a : mn;
+    mx = c > mx ? c : mx;
+  }
+  if ((tid & 63) == 0) { rmn[w] = mn; rmx[w] = mx; }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < RPT; ++j)
+    if (tid + j * 256 < nr) atomicAdd(&h[w][range_digit(k[j], lo, sh)], 1u);
+  __syncthreads();
+  hist[(long)tid * ntiles + b] = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
+  if (tid == 0) {
+    long long a = rmn[0], c = rmx[0];
+    for (int q = 1; q < 4; ++q) { a = rmn[q] < a ? rmn[q] : a; c = rmx[q] > c ? rmx[q] : c; }
+    range[2 * b] = a;
+    range[2 * b + 1] = c;
+  }
+}
+
+template <int NV, int RTT, int NT = 512>
+__global__ __launch_bounds__(NT) void range_scatter_k(const long long* __restrict__ keys, PayIn pin, long n,
+                                                       long long lo, int sh, int ntiles,
+                                                       const long long* __restrict__ offs,
+                                                       unsigned int* __restrict__ okeys, PayOut pout) {
+  constexpr int RPT = RTT / NT;
+  static_assert(RPT >= 1 && RTT % NT == 0, "tile rows must be a multiple of the thread count");
+  constexpr int NVS = NV > 0 ? NV : 1;
+  __shared__ unsigned int sk[RTT];
+  __shared__ double sv[NVS][RTT];
+  __shared__ unsigned char sd[RTT];
+  __shared__ unsigned int cnt[RGB];
+  __shared__ unsigned int lstart[RGB];
+  __shared__ long long goff[RGB];
+  const int tid = threadIdx.x, b = xcd_tile(blockIdx.x, ntiles);
+  const long s0 = (long)b * RTT;
+  const int nr = (int)min((long)RTT, n - s0);
+  for (int d = tid; d < RGB; d += NT) {
+    cnt[d] = 0;
+    goff[d] = offs[(long)d * ntiles + b];
+  }
+  __syncthreads();
+  long long k[RPT];
+  double v[NVS][RPT];
+  int d[RPT];
+#pragma unroll
+  for (int j = 0; j < RPT; ++j) {
+    const int i = tid + j * NT;
+    d[j] = -1;
+    if (i < nr) {
+      k[j] = keys[s0 + i];
+#pragma unroll
+      for (int q = 0; q < NV; ++q) v[q][j] = load_pay(pin, q, s0 + i);
+      d[j] = range_digit(k[j], lo, sh);
+      atomicAdd(&cnt[d[j]], 1u);
+    }
+  }
+  __syncthreads();
+  if (tid < 64) {  // exclusive scan of the 256 digit counts in one wave, 4 per lane
+    unsigned c4[4], sum = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) { c4[q] = cnt[4 * tid + q]; sum += c4[q]; }
+    unsigned incl = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned t = __shfl_up(incl, o, 64);
+      if (tid >= o) incl += t;
+    }
+    unsigned run = incl - sum;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) { lstart[4 * tid + q] = run; run += c4[q]; cnt[4 * tid + q] = 0; }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < RPT; ++j) {
+    if (d[j] < 0) continue;
+    const unsigned pos = lstart[d[j]] + atomicAdd(&cnt[d[j]], 1u);
+    sk[pos] = (unsigned int)(k[j] - lo);
+#pragma unroll
+    for (int q = 0; q < NV; ++q) sv[q][pos] = v[q][j];
+    sd[pos] = (unsigned char)d[j];
+  }
+  __syncthreads();
+  for (int i = tid; i < nr; i += NT) {  // consecutive rows of a digit run -> consecutive addresses
+    const int dd = sd[i];
+    const long long dst = PTG_CHECKED_IDX(goff[dd] + (i - (int)lstart[dd]), n);
+    okeys[dst] = sk[i];
+#pragma unroll
+    for (int q = 0; q < NV; ++q) pout.vals[q][dst] = sv[q][i];
+  }
+}
+
+// grid (chunks, 256): partition p = blockIdx.y holds rows [offs[p*ntiles], offs[(p+1)*ntiles]) whose
+// keys (u32 offsets from lo) lie in [p*W, (p+1)*W).  Output per chunk c (Rw = 256*W entries):
+// prow[c][0][Rw] rows, prow[c][1+j][Rw] non-null count of column j, psum[c][j][Rw] sums.
+template <int NV>
+__global__ __launch_bounds__(256) void range_agg_k(const unsigned int* __restrict__ okeys, AggPay pay,
+                                                   const long long* __restrict__ offs, int ntiles, int sh,
+                                                   unsigned int* __restrict__ prow, double* __restrict__ psum) {
+  constexpr int NVS = NV > 0 ? NV : 1;
+  extern __shared__ __align__(16) unsigned char lds_raw[];
+  const int W = 1 << sh, p = blockIdx.y, c = blockIdx.x, C = gridDim.x;
+  double* lsum = (double*)lds_raw;                          // [NV][W]
+  unsigned int* lrow = (unsigned int*)(lsum + (long)NV * W); // [1 + NV][W]
+  for (int t = threadIdx.x; t < W; t += 256) {
+    lrow[t] = 0;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) { lsum[j * W + t] = 0.0; lrow[(1 + j) * W + t] = 0; }
+  }
+  __syncthreads();
+  const long long a0 = offs[(long)p * ntiles], b0 = offs[(long)(p + 1) * ntiles], len = b0 - a0;
+  const long long a = a0 + len * c / C, b = a0 + len * (c + 1) / C;
+  const unsigned int wbase = (unsigned int)p << sh, wmask = (unsigned int)W - 1;
+  auto add = [&](unsigned int key, const double* v) {
+    const unsigned int i = (key - wbase) & wmask;
+    atomicAdd(&lrow[i], 1u);
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      if (v[j] != v[j]) continue;  // null / NaN
+      atomicAdd(&lsum[j * W + i], v[j]);
+      atomicAdd(&lrow[(1 + j) * W + i], 1u);
+    }
+  };
+  long long i = a + threadIdx.x;
+  for (; i + 3 * 256 < b; i += 4 * 256) {  // 4 rows' loads in flight ahead of the LDS atomics
+    unsigned int k4[4];
+    double v4[4][NVS];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      k4[u] = okeys[i + u * 256];
+#pragma unroll
+      for (int j = 0; j < NV; ++j) v4[u][j] = pay.vals[j][i + u * 256];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) add(k4[u], v4[u]);
+  }
+  for (; i < b; i += 256) {
+    double v1[NVS];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) v1[j] = pay.vals[j][i];
+    add(okeys[i], v1);
+  }
+  __syncthreads();
+  const long Rw = (long)RGB * W, o = (long)p * W;
+  for (int t = threadIdx.x; t < W; t += 256) {
+    prow[((long)c * (1 + NV)) * Rw + o + t] = lrow[t];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      prow[((long)c * (1 + NV) + 1 + j) * Rw + o + t] = lrow[(1 + j) * W + t];
+      psum[((long)c * NV + j) * Rw + o + t] = lsum[j * W + t];
+    }
+  }
+}
+
 // ================================================================================================
 // Stable LSD radix sort of 64-bit keys with a 64-bit payload (DataFrame.orderBy / sort)
 //   sort_key_prep_k  column -> unsigned-orderable u64 (asc or desc; NaN above +inf, -0 == +0) and
@@ -893,7 +1108,7 @@ __global__ __launch_bounds__(256) void sort_scatter_k(const unsigned long long* 
   __shared__ unsigned int lstart[SB];
   __shared__ long long goff[SB];
   __shared__ int wsum[4];
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, b = blockIdx.x;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, b = xcd_tile(blockIdx.x, ntiles);
   const long s0 = (long)b * ST;
   const int nr = (int)((n - s0) < ST ? (n - s0) : ST);
   goff[tid] = offs[(long)tid * ntiles + b];
@@ -1233,6 +1448,60 @@ int ptg_part_agg2(const void* okeys, int key32, long kbase, const void* const* v
   }
 #undef PTG_AGG
 #undef PTG_AGGK
+  PTG_RETURN_LAUNCH();
+}
+
+// dense small-range groupBy (range_count_k / range_scatter_k / range_agg_k).  Tiles are
+// ptg_range_tile_rows(nv) rows; hist u32[256*ntiles] digit-major, range i64[ntiles][2];
+// offs i64[256*ntiles + 1] = exclusive scan of hist with offs[last] = n.  sh <= 12, nv <= 2.
+int ptg_range_tile_rows(int nv) { return nv <= 1 ? RT : RT / 2; }
+int ptg_range_count(const void* keys, long n, long lo, int sh, int T, int ntiles, void* hist, void* range,
+                    hipStream_t s) {
+  if (ntiles <= 0 || T > RT || sh < 0 || sh > 12) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(range_count_k, dim3(ntiles), dim3(256), 0, s, (const long long*)keys, n, (long long)lo, sh, T,
+                     ntiles, (unsigned int*)hist, (long long*)range);
+  PTG_RETURN_LAUNCH();
+}
+int ptg_range_scatter(const void* keys, const void* pin_p, int nv, long n, long lo, int sh, int ntiles,
+                      const void* offs, void* okeys, const void* pout_p, hipStream_t s) {
+  if (ntiles <= 0 || sh < 0 || sh > 12) return (int)hipErrorInvalidValue;
+  PayIn pin;
+  PayOut pout;
+  memcpy(&pin, pin_p, sizeof(PayIn));
+  memcpy(&pout, pout_p, sizeof(PayOut));
+#define PTG_RSC(NV, TR)                                                                                       \
+  hipLaunchKernelGGL((range_scatter_k<NV, TR>), dim3(ntiles), dim3(512), 0, s, (const long long*)keys, pin, n,   \
+                     (long long)lo, sh, ntiles, (const long long*)offs, (unsigned int*)okeys, pout)
+  switch (nv) {
+    case 0: PTG_RSC(0, RT); break;
+    case 1: PTG_RSC(1, RT); break;
+    case 2: PTG_RSC(2, RT / 2); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+#undef PTG_RSC
+  PTG_RETURN_LAUNCH();
+}
+// vals: host array of nv f64 device pointers (scattered payload); prow u32[chunks][1+nv][256<<sh],
+// psum f64[chunks][nv][256<<sh]
+int ptg_range_agg(const void* okeys, const void* const* vals, int nv, const void* offs, int ntiles, int sh,
+                  int chunks, void* prow, void* psum, hipStream_t s) {
+  if (nv < 0 || nv > 2 || sh < 0 || sh > 12 || chunks <= 0) return (int)hipErrorInvalidValue;
+  const size_t lds = ((size_t)1 << sh) * (4 + (size_t)nv * 12);
+  AggPay pay;
+  for (int j = 0; j < PAY_MAX; ++j) pay.vals[j] = j < nv ? (const double*)vals[j] : nullptr;
+#define PTG_RAG(NV)                                                                                           \
+  {                                                                                                           \
+    static bool attr = false;                                                                                 \
+    if (!attr) {                                                                                              \
+      (void)hipFuncSetAttribute((const void*)range_agg_k<NV>, hipFuncAttributeMaxDynamicSharedMemorySize,     \
+                                150 * 1024);                                                                  \
+      attr = true;                                                                                            \
+    }                                                                                                         \
+    hipLaunchKernelGGL((range_agg_k<NV>), dim3(chunks, RGB), dim3(256), lds, s, (const unsigned int*)okeys, pay, \
+                       (const long long*)offs, ntiles, sh, (unsigned int*)prow, (double*)psum);              \
+  }
+  switch (nv) { case 0: PTG_RAG(0) break; case 1: PTG_RAG(1) break; default: PTG_RAG(2) break; }
+#undef PTG_RAG
   PTG_RETURN_LAUNCH();
 }
 

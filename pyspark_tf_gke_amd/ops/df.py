@@ -7,6 +7,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 import struct
 
 import numpy as np
@@ -283,6 +284,73 @@ def estimate_distinct(keys: torch.Tensor, sample: int = 1 << 16) -> int:
     return int(min(n, max(d, hi)))
 
 
+RANGE_MAX_SPAN = 1 << 20  # dense-key path: keys within a window of 256 partitions x <= 4096 keys
+RANGE_MIN_ROWS = 1 << 22  # below this the sample/plan overhead is not worth a second code path
+
+
+def _range_window(lo: int, hi: int):
+    """(window base, sh): a window of 256 << sh >= hi - lo + 1 keys (sh <= 12) centred on [lo, hi],
+    so keys a sample missed just past its ends still fall inside; None if the span is too wide."""
+    span = hi - lo + 1
+    sh = 0
+    while (RADIX_RANGE_BINS << sh) < span:
+        sh += 1
+    return None if sh > 12 else (lo - ((RADIX_RANGE_BINS << sh) - span) // 2, sh)
+
+
+RADIX_RANGE_BINS = 256
+
+
+def hash_agg_range(keys: torch.Tensor, pay: list, buf, nv: int, sample_lohi: tuple[int, int]):
+    """groupBy(key).agg for int64 keys spanning at most 2^20 values (csrc/kernels/df.hip range_*_k):
+    one range-partitioning pass by the top 8 bits of (key - lo) and a direct-indexed LDS aggregation
+    per (partition, chunk), instead of the two hash levels of :func:`hash_agg_radix`.  ``sample_lohi``
+    guesses the window from a sample; the count pass returns the exact [min, max] and a key outside
+    the guess re-plans the window (or returns None: the caller takes the hash path).  Same result
+    format as :func:`hash_agg` (min/max columns are +-inf: the caller only routes sum/count/avg here)."""
+    dev = keys.device
+    n = keys.numel()
+    lib = _native.hip_lib()
+    T = int(lib.ptg_range_tile_rows(nv))
+    ntiles = (n + T - 1) // T
+    win = _range_window(*sample_lohi)
+    if win is None:
+        return None
+    hist = buf("rhist", (256 * ntiles,), torch.int32)
+    rng = buf("rrng", (ntiles, 2), torch.int64)
+    for attempt in range(2):
+        lo, sh = win
+        hip("ptg_range_count", ptr(keys), n, int(lo), sh, T, ntiles, ptr(hist), ptr(rng))
+        mn, mx = (int(x) for x in torch.stack([rng[:, 0].min(), rng[:, 1].max()]).tolist())
+        if mn >= lo and mx < lo + (256 << sh):
+            break
+        win = _range_window(mn, mx) if attempt == 0 else None
+        if win is None:
+            return None
+    offs = buf("roffs", (256 * ntiles + 1,), torch.int64)
+    torch.cumsum(hist, 0, dtype=torch.int64, out=offs[1:])
+    offs[0] = 0
+    okeys = buf("aokeys32", (max(n, 1),), torch.int32)[:n]
+    ovals = [buf(f"aov{j}", (max(n, 1),), torch.float64)[:n] for j in range(nv)]
+    pin, pout = _pay_in(pay), _pay_out(ovals)
+    hip("ptg_range_scatter", ptr(keys), ctypes.addressof(pin), nv, n, int(lo), sh, ntiles, ptr(offs), ptr(okeys),
+        ctypes.addressof(pout))
+    Rw = 256 << sh
+    chunks = max(1, min(16, 2048 // 256, (n // 256) // (1 << 16) or 1))
+    prow = buf("rprow", (chunks, 1 + nv, Rw), torch.int32)
+    psum = buf("rpsum", (chunks, max(nv, 1), Rw), torch.float64)
+    vptrs = (ctypes.c_void_p * PAY_MAX)(*([o.data_ptr() for o in ovals] + [0] * (PAY_MAX - nv)))
+    hip("ptg_range_agg", ptr(okeys), ctypes.addressof(vptrs), nv, ptr(offs), ntiles, sh, chunks, ptr(prow), ptr(psum))
+    cnts = prow.to(torch.int64).sum(0) if chunks > 1 else prow[0].to(torch.int64)  # [1 + nv][Rw]
+    sums = psum.sum(0) if chunks > 1 else psum[0]
+    idx = torch.nonzero(cnts[0] > 0).view(-1)
+    out_keys = idx + lo
+    rows = cnts[0][idx].to(torch.float64)
+    inf = torch.full((idx.numel(),), math.inf, dtype=torch.float64, device=dev)
+    outs = [(sums[j][idx], cnts[1 + j][idx].to(torch.float64), inf, -inf) for j in range(nv)]
+    return out_keys, rows, outs
+
+
 def hash_agg_radix(keys: torch.Tensor, vals: list, valids: list, want_minmax: bool = False, ws: dict | None = None,
                    est_keys: int | None = None):
     """groupBy(key).agg over int64 keys by recursive radix partitioning (high cardinality, any
@@ -312,6 +380,14 @@ def hash_agg_radix(keys: torch.Tensor, vals: list, valids: list, want_minmax: bo
         if vd is not None and vd.dtype == torch.bool:
             vd = vd.view(torch.uint8)
         pay.append((v.contiguous(), vd))
+    if (nv <= 2 and not want_minmax and keys.dtype == torch.int64 and n >= RANGE_MIN_ROWS
+            and os.environ.get("PTG_GROUPBY_RANGE", "1") != "0"):
+        smp = keys[:: max(1, n // 65536)]
+        slo, shi = (int(x) for x in torch.stack([smp.min(), smp.max()]).tolist())
+        if shi - slo < RANGE_MAX_SPAN:
+            r = hash_agg_range(keys.contiguous(), pay, buf, nv, (slo, shi))
+            if r is not None:
+                return r
     K = est_keys if est_keys is not None else estimate_distinct(keys)
     pcap_max = 256
     while _part_agg_lds(pcap_max * 2, nv, want_minmax) <= _AGG_LDS_BUDGET and pcap_max < 4096:

@@ -104,6 +104,46 @@ def test_radix_agg_matches_host(hip_built, n, nkeys, nv, minmax):
     _assert_agg_equal(got, want, minmax)
 
 
+@pytest.mark.parametrize("lo,span,nv", [(0, 1_000_000, 1), (-5_000_000_000, 1 << 20, 2), (123, 4_000, 0),
+                                         (7, 300_000, 2)])
+def test_range_agg_matches_host(hip_built, lo, span, nv):
+    """Dense small-range keys take the one-level range partition + direct-indexed LDS aggregation
+    (range_*_k): sums / non-null counts with NaN values and a validity mask, count-only, negative
+    keys, and a span of exactly 2^20 whose extremes the sample misses (the window is re-planned
+    from the count pass's exact range).  Checked against the host path."""
+    n = 6_000_000
+    g = torch.Generator().manual_seed(span + nv)
+    k = torch.randint(0, span, (n,), generator=g) + lo
+    k[17], k[n - 5] = lo, lo + span - 1
+    cols, valids = [], []
+    for j in range(nv):
+        if j == 0:
+            x = torch.rand(n, generator=g, dtype=torch.float64)
+            x[::101] = math.nan
+            vd = None
+        else:
+            x = torch.randint(-1000, 1000, (n,), generator=g, dtype=torch.int32)
+            vd = (torch.rand(n, generator=g) > 0.3).to(torch.uint8)
+        cols.append(x)
+        valids.append(vd)
+    ws = {}
+    got = D.hash_agg_radix(k.cuda(), [c.cuda() for c in cols], [None if x is None else x.cuda() for x in valids],
+                           False, ws=ws)
+    assert "rprow" in ws, "range path not taken"
+    want = D.hash_agg(k, cols, valids, False)
+    _assert_agg_equal(got, want, False)
+
+
+def test_range_agg_off_switch_same_result(hip_built, monkeypatch):
+    k, v = D.fill_synthetic_kv(5_000_000, 50_000, "cuda")
+    a = D.hash_agg_radix(k, [v], [None], False)
+    monkeypatch.setenv("PTG_GROUPBY_RANGE", "0")
+    ws = {}
+    b = D.hash_agg_radix(k, [v], [None], False, ws=ws)
+    assert "rprow" not in ws
+    _assert_agg_equal(a, b, False)
+
+
 @pytest.mark.parametrize("est", [1_000, 300_000])
 def test_radix_agg_spill_recursion(hip_built, est):
     """An estimate far below the real 2M keys sizes the tables too small: partitions spill and are
