@@ -231,3 +231,18 @@ def test_lazy_stage_pushdown_fusion_and_retry(spark, capsys):
     P._FAULTS["left"] = 0
     with pytest.raises(KeyError):
         df.filter(col("nope") > 1)
+
+
+def test_range_window_plan():
+    """Window planning of the dense-key groupBy path (ops/df.py): 256 << sh keys, centred on the
+    sampled range so keys just past the sample's ends still fall inside; spans above 2^20 refuse."""
+    from pyspark_tf_gke_amd.ops import df as D
+
+    for lo, hi in ((0, 999_999), (15, 999_985), (-5_000_000_000, -5_000_000_000 + (1 << 20) - 1), (7, 7), (3, 300)):
+        base, sh = D._range_window(lo, hi)
+        assert sh <= 12 and (256 << sh) >= hi - lo + 1
+        assert sh == 0 or (256 << (sh - 1)) < hi - lo + 1  # smallest window that fits
+        assert base <= lo and hi < base + (256 << sh)
+    base, sh = D._range_window(15, 999_985)  # a 64K-key sample of keys 0..999,999
+    assert base <= 0 and 999_999 < base + (256 << sh)
+    assert D._range_window(0, 1 << 20) is None
