@@ -822,6 +822,10 @@ __global__ __launch_bounds__(256) void part_agg2_k(const KT* __restrict__ okeys,
 //                    partition's W-key window in LDS, written out as one dense partial table per chunk
 //                    (plain coalesced stores, no atomics; the host sums the chunks: deterministic)
 #define RGB 256
+#ifndef PTG_RGT
+#define PTG_RGT 4096  // range tile rows (nv <= 1; nv = 2 uses half); 8192: 62.7 vs 73.4G rows/s (1 workgroup per CU)
+#endif
+#define RGT PTG_RGT
 PTG_DEV int range_digit(long long k, long long lo, int sh) {
   long long d = (k - lo) >> sh;
   return d < 0 ? 0 : (d > RGB - 1 ? RGB - 1 : (int)d);  // out-of-window keys are detected via range
@@ -830,7 +834,7 @@ PTG_DEV int range_digit(long long k, long long lo, int sh) {
 __global__ __launch_bounds__(256) void range_count_k(const long long* __restrict__ keys, long n, long long lo, int sh,
                                                      int T, int ntiles, unsigned int* __restrict__ hist,
                                                      long long* __restrict__ range) {
-  constexpr int RPT = RT / 256;
+  constexpr int RPT = RGT / 256;
   __shared__ unsigned int h[4][RGB];
   __shared__ long long rmn[4], rmx[4];
   const int tid = threadIdx.x, b = blockIdx.x, w = tid >> 6;
@@ -1454,10 +1458,10 @@ int ptg_part_agg2(const void* okeys, int key32, long kbase, const void* const* v
 // dense small-range groupBy (range_count_k / range_scatter_k / range_agg_k).  Tiles are
 // ptg_range_tile_rows(nv) rows; hist u32[256*ntiles] digit-major, range i64[ntiles][2];
 // offs i64[256*ntiles + 1] = exclusive scan of hist with offs[last] = n.  sh <= 12, nv <= 2.
-int ptg_range_tile_rows(int nv) { return nv <= 1 ? RT : RT / 2; }
+int ptg_range_tile_rows(int nv) { return nv <= 1 ? RGT : RGT / 2; }
 int ptg_range_count(const void* keys, long n, long lo, int sh, int T, int ntiles, void* hist, void* range,
                     hipStream_t s) {
-  if (ntiles <= 0 || T > RT || sh < 0 || sh > 12) return (int)hipErrorInvalidValue;
+  if (ntiles <= 0 || T > RGT || sh < 0 || sh > 12) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(range_count_k, dim3(ntiles), dim3(256), 0, s, (const long long*)keys, n, (long long)lo, sh, T,
                      ntiles, (unsigned int*)hist, (long long*)range);
   PTG_RETURN_LAUNCH();
@@ -1473,9 +1477,9 @@ int ptg_range_scatter(const void* keys, const void* pin_p, int nv, long n, long 
   hipLaunchKernelGGL((range_scatter_k<NV, TR>), dim3(ntiles), dim3(512), 0, s, (const long long*)keys, pin, n,   \
                      (long long)lo, sh, ntiles, (const long long*)offs, (unsigned int*)okeys, pout)
   switch (nv) {
-    case 0: PTG_RSC(0, RT); break;
-    case 1: PTG_RSC(1, RT); break;
-    case 2: PTG_RSC(2, RT / 2); break;
+    case 0: PTG_RSC(0, RGT); break;
+    case 1: PTG_RSC(1, RGT); break;
+    case 2: PTG_RSC(2, RGT / 2); break;
     default: return (int)hipErrorInvalidValue;
   }
 #undef PTG_RSC

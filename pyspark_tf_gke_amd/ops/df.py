@@ -336,7 +336,7 @@ def hash_agg_range(keys: torch.Tensor, pay: list, buf, nv: int, sample_lohi: tup
     hip("ptg_range_scatter", ptr(keys), ctypes.addressof(pin), nv, n, int(lo), sh, ntiles, ptr(offs), ptr(okeys),
         ctypes.addressof(pout))
     Rw = 256 << sh
-    chunks = max(1, min(16, 2048 // 256, (n // 256) // (1 << 16) or 1))
+    chunks = max(1, min(int(os.environ.get("PTG_RANGE_CHUNKS", "8")), (n // 256) // (1 << 16) or 1))
     prow = buf("rprow", (chunks, 1 + nv, Rw), torch.int32)
     psum = buf("rpsum", (chunks, max(nv, 1), Rw), torch.float64)
     vptrs = (ctypes.c_void_p * PAY_MAX)(*([o.data_ptr() for o in ovals] + [0] * (PAY_MAX - nv)))
