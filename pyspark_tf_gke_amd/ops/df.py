@@ -521,6 +521,13 @@ def sort_key(col: torch.Tensor, desc: bool = False):
     return out, (lo if n else 0), (hi if n else 0)
 
 
+def decode_sort_key(sk: torch.Tensor, dtype, desc: bool) -> torch.Tensor:
+    """Inverse of :func:`sort_key` for integer columns: orderable u64 bit patterns -> values."""
+    u = ~sk if desc else sk
+    x = u ^ torch.iinfo(torch.int64).min  # flip the sign bit back
+    return x if dtype == torch.int64 else x.to(dtype)
+
+
 def radix_sort_u64(keys: torch.Tensor, vals: torch.Tensor | None = None, lo: int = 0, hi: int = _U64,
                    row_payload: bool = False):
     """Stable sort of u64 keys (held in an int64 tensor) with an int64 payload (default: the row

@@ -466,6 +466,18 @@ class DataFrame:
             t = SH.shuffle_table(t, D.partition_perm(part, counts), counts)
         if t.num_rows == 0 or not specs:
             return self._new(t)
+        if len(specs) == 1 and specs[0][0].node[0] == "col":
+            # one null-free integer sort column: the radix sort's own output keys ARE the sorted
+            # column (decoded from the orderable form), so only the other columns are gathered
+            name = t.resolve(specs[0][0].node[1])
+            cv = t.column(name)
+            if cv.valid is None and cv.data.dtype in (torch.int64, torch.int32) and not isinstance(cv.dtype, T.StringType):
+                k, lo, hi = D.sort_key(cv.data, desc=not specs[0][1])
+                sk, perm = D.radix_sort_u64(k, None, lo, hi, row_payload=True)
+                cols = {n: (ColumnVector(D.decode_sort_key(sk, cv.data.dtype, not specs[0][1]), cv.dtype, None,
+                                         cv.dictionary) if n == name else c.take(perm))
+                        for n, c in t.columns.items()}
+                return self._new(Table(cols, t.num_rows, t.device))
         df_t = DataFrame(t, self.sparkSession)
         keys = []
         for c, a in specs:

@@ -285,6 +285,36 @@ def test_radix_sort_wide_payload(hip_built):
     assert torch.equal(sv.cpu(), pay[torch.from_numpy(order)])
 
 
+@pytest.mark.parametrize("dtype,asc", [(torch.int64, True), (torch.int64, False), (torch.int32, True)])
+def test_orderby_integer_key_output_keys(spark_gpu, dtype, asc):
+    """Single null-free integer sort column: the sorted key column is decoded from the radix
+    sort's own output keys (not gathered); the result equals a stable host sort, ties included."""
+    from pyspark_tf_gke_amd.sql import types as T
+    from pyspark_tf_gke_amd.sql.dataframe import DataFrame
+    from pyspark_tf_gke_amd.sql.table import ColumnVector, Table
+
+    n = 1_000_000
+    g = torch.Generator().manual_seed(11)
+    info = torch.iinfo(dtype)
+    k = torch.randint(info.min, info.max, (n,), generator=g, dtype=dtype)
+    k[1::2] = k[0::2]  # ties (n is even)
+    k[5], k[6] = info.min, info.max
+    v = torch.rand(n, generator=g, dtype=torch.float64)
+    lt = T.LongType() if dtype == torch.int64 else T.IntegerType()
+    df = DataFrame(Table({"key": ColumnVector(k.cuda(), lt), "value": ColumnVector(v.cuda(), T.DoubleType())}, n,
+                         torch.device("cuda")), spark_gpu)
+    out = df.orderBy("key", ascending=asc)
+    kk = k.numpy()
+    if asc:
+        order = np.argsort(kk, kind="stable")
+    else:  # descending keys, ties in input order
+        order = (n - 1) - np.argsort(kk[::-1], kind="stable")[::-1]
+    order = torch.as_tensor(np.ascontiguousarray(order, dtype=np.int64))
+    assert out._t.column("key").data.dtype == dtype
+    assert torch.equal(out._t.column("key").data.cpu(), k[order])
+    assert torch.equal(out._t.column("value").data.cpu(), v[order])
+
+
 def test_argsort_columns_gpu_vs_host(hip_built):
     """Multi-column orderBy permutation (asc/desc, nulls first/last) on the GPU equals the host."""
     n = 500_000
