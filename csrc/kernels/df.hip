@@ -1116,12 +1116,19 @@ __global__ __launch_bounds__(256) void sort_scatter_k(const unsigned long long* 
   const long s0 = (long)b * ST;
   const int nr = (int)((n - s0) < ST ? (n - s0) : ST);
   goff[tid] = offs[(long)tid * ntiles + b];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) wc[q][tid] = 0;
+  // Wave-contiguous rows: wave w owns tile rows [w*ST/4, (w+1)*ST/4), 64 consecutive rows per round
+  // (coalesced loads), so the stable order inside the tile is (wave, round, lane).  Ranks come from
+  // a wave-private running count per digit (wc[w]): no block barrier per round, only the one
+  // cross-wave prefix per digit after the last round (the round-interleaved form needed 2 block
+  // barriers per round to keep the order).
   unsigned long long k[SRPT];
   VT v[SRPT];
   int d[SRPT], r[SRPT];
 #pragma unroll
   for (int j = 0; j < SRPT; ++j) {
-    const int i = j * 256 + tid;
+    const int i = w * (ST / 4) + j * 64 + lane;
     d[j] = -1;
     if (i < nr) {
       k[j] = keys_in[s0 + i];
@@ -1129,13 +1136,10 @@ __global__ __launch_bounds__(256) void sort_scatter_k(const unsigned long long* 
       d[j] = (int)((k[j] - base) >> shift) & (SB - 1);
     }
   }
+  __syncthreads();  // wc zeroed by every wave before any wave counts into it
   const unsigned long long lt = (1ULL << lane) - 1ULL;
-  unsigned int running = 0;  // thread tid owns digit tid
 #pragma unroll
   for (int j = 0; j < SRPT; ++j) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) wc[w][lane * 4 + q] = 0;
-    __syncthreads();
     const bool valid = d[j] >= 0;
     unsigned long long peers = __ballot(valid);
 #pragma unroll
@@ -1145,18 +1149,21 @@ __global__ __launch_bounds__(256) void sort_scatter_k(const unsigned long long* 
       peers &= set ? bb : ~bb;
     }
     const int rank_w = __popcll(peers & lt);
-    if (valid && rank_w == 0) wc[w][d[j]] = (unsigned)__popcll(peers);
-    __syncthreads();
-    {
-      const unsigned c0 = wc[0][tid], c1 = wc[1][tid], c2 = wc[2][tid], c3 = wc[3][tid];
-      woff[0][tid] = running;
-      woff[1][tid] = running + c0;
-      woff[2][tid] = running + c0 + c1;
-      woff[3][tid] = running + c0 + c1 + c2;
-      running += c0 + c1 + c2 + c3;
-    }
-    __syncthreads();
-    r[j] = valid ? (int)woff[w][d[j]] + rank_w : 0;
+    const unsigned old = valid ? wc[w][d[j]] : 0u;  // every lane reads before the leader writes
+    __builtin_amdgcn_wave_barrier();
+    if (valid && rank_w == 0) wc[w][d[j]] = old + (unsigned)__popcll(peers);
+    __builtin_amdgcn_wave_barrier();
+    r[j] = (int)old + rank_w;
+  }
+  __syncthreads();
+  unsigned int running;
+  {  // thread tid owns digit tid: per-wave offsets inside the digit's run, and the tile total
+    const unsigned c0 = wc[0][tid], c1 = wc[1][tid], c2 = wc[2][tid], c3 = wc[3][tid];
+    woff[0][tid] = 0;
+    woff[1][tid] = c0;
+    woff[2][tid] = c0 + c1;
+    woff[3][tid] = c0 + c1 + c2;
+    running = c0 + c1 + c2 + c3;
   }
   int total;
   const int ls = block_excl_scan256((int)running, wsum, &total);
@@ -1165,7 +1172,7 @@ __global__ __launch_bounds__(256) void sort_scatter_k(const unsigned long long* 
 #pragma unroll
   for (int j = 0; j < SRPT; ++j) {
     if (d[j] < 0) continue;
-    const int pos = (int)lstart[d[j]] + r[j];
+    const int pos = (int)lstart[d[j]] + (int)woff[w][d[j]] + r[j];
     sk[pos] = k[j];
     sv[pos] = v[j];
     sd[pos] = (unsigned char)d[j];
