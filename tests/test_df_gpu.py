@@ -144,6 +144,28 @@ def test_range_agg_off_switch_same_result(hip_built, monkeypatch):
     _assert_agg_equal(a, b, False)
 
 
+def test_repeat_runs_agree(hip_built):
+    """Deterministic-mode check: the same groupBy / sort twice.  Keys and counts are
+    exact and identical (range path, hash radix path, LDS hash path); f64 sums differ at most by the
+    order of LDS atomic adds; the stable radix sort is bitwise identical."""
+    k, v = D.fill_synthetic_kv(6_000_000, 700_000, "cuda", seed=5)
+    for env in ("1", "0"):
+        os.environ["PTG_GROUPBY_RANGE"] = env
+        try:
+            runs = [_sorted_agg(*D.hash_agg_radix(k, [v], [None], False)) for _ in range(2)]
+        finally:
+            os.environ.pop("PTG_GROUPBY_RANGE", None)
+        (k1, r1, o1), (k2, r2, o2) = runs
+        assert torch.equal(k1, k2) and torch.equal(r1, r2) and torch.equal(o1[0][1], o2[0][1])
+        assert torch.allclose(o1[0][0], o2[0][0], rtol=1e-12, atol=1e-12)
+    small = [_sorted_agg(*D.hash_agg(k[:1_000_000] % 1000, [v[:1_000_000]], [None], False)) for _ in range(2)]
+    assert torch.equal(small[0][0], small[1][0]) and torch.equal(small[0][1], small[1][1])
+    sk, lo, hi = D.sort_key(k, False)
+    a = D.radix_sort_u64(sk, None, lo, hi, row_payload=True)
+    b = D.radix_sort_u64(sk, None, lo, hi, row_payload=True)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+
+
 @pytest.mark.parametrize("est", [1_000, 300_000])
 def test_radix_agg_spill_recursion(hip_built, est):
     """An estimate far below the real 2M keys sizes the tables too small: partitions spill and are
