@@ -816,8 +816,9 @@ __global__ __launch_bounds__(256) void part_agg2_k(const KT* __restrict__ okeys,
 // scatter + aggregate, ~12 of its 21 ms were the second level).
 //   range_count_k    per-tile 256-bin digit counts, digit-major [digit][tile], and per-tile [min, max]
 //                    (the host checks that every key fell inside the sample-guessed window)
-//   range_scatter_k  rows staged in LDS by digit, written as 256 contiguous runs; keys leave as u32
-//                    offsets (key - lo), values as f64 (null -> NaN)
+//   range_scatter_k  rows staged in LDS by digit, written as 256 contiguous runs; a key leaves as its
+//                    u16 index inside its partition's window ((key - lo) & (W - 1): the partition
+//                    is implied by the run), values as f64 (null -> NaN)
 //   range_agg_k      (chunk, partition) workgroups: rows u32 / per-column sum f64 + count u32 over the
 //                    partition's W-key window in LDS, written out as one dense partial table per chunk
 //                    (plain coalesced stores, no global atomics; the host sums the chunks in a fixed order)
@@ -877,11 +878,11 @@ template <int NV, int RTT, int NT = 512>
 __global__ __launch_bounds__(NT) void range_scatter_k(const long long* __restrict__ keys, PayIn pin, long n,
                                                        long long lo, int sh, int ntiles,
                                                        const long long* __restrict__ offs,
-                                                       unsigned int* __restrict__ okeys, PayOut pout) {
+                                                       unsigned short* __restrict__ okeys, PayOut pout) {
   constexpr int RPT = RTT / NT;
   static_assert(RPT >= 1 && RTT % NT == 0, "tile rows must be a multiple of the thread count");
   constexpr int NVS = NV > 0 ? NV : 1;
-  __shared__ unsigned int sk[RTT];
+  __shared__ unsigned short sk[RTT];
   __shared__ double sv[NVS][RTT];
   __shared__ unsigned char sd[RTT];
   __shared__ unsigned int cnt[RGB];
@@ -930,7 +931,7 @@ __global__ __launch_bounds__(NT) void range_scatter_k(const long long* __restric
   for (int j = 0; j < RPT; ++j) {
     if (d[j] < 0) continue;
     const unsigned pos = lstart[d[j]] + atomicAdd(&cnt[d[j]], 1u);
-    sk[pos] = (unsigned int)(k[j] - lo);
+    sk[pos] = (unsigned short)((unsigned long long)(k[j] - lo) & ((1u << sh) - 1u));
 #pragma unroll
     for (int q = 0; q < NV; ++q) sv[q][pos] = v[q][j];
     sd[pos] = (unsigned char)d[j];
@@ -945,11 +946,11 @@ __global__ __launch_bounds__(NT) void range_scatter_k(const long long* __restric
   }
 }
 
-// grid (chunks, 256): partition p = blockIdx.y holds rows [offs[p*ntiles], offs[(p+1)*ntiles]) whose
-// keys (u32 offsets from lo) lie in [p*W, (p+1)*W).  Output per chunk c (Rw = 256*W entries):
+// grid (chunks, 256): partition p = blockIdx.y holds rows [offs[p*ntiles], offs[(p+1)*ntiles]), keys
+// lo + p*W + okeys[i] (u16 window indices).  Output per chunk c (Rw = 256*W entries):
 // prow[c][0][Rw] rows, prow[c][1+j][Rw] non-null count of column j, psum[c][j][Rw] sums.
 template <int NV>
-__global__ __launch_bounds__(256) void range_agg_k(const unsigned int* __restrict__ okeys, AggPay pay,
+__global__ __launch_bounds__(256) void range_agg_k(const unsigned short* __restrict__ okeys, AggPay pay,
                                                    const long long* __restrict__ offs, int ntiles, int sh,
                                                    unsigned int* __restrict__ prow, double* __restrict__ psum) {
   constexpr int NVS = NV > 0 ? NV : 1;
@@ -965,9 +966,7 @@ __global__ __launch_bounds__(256) void range_agg_k(const unsigned int* __restric
   __syncthreads();
   const long long a0 = offs[(long)p * ntiles], b0 = offs[(long)(p + 1) * ntiles], len = b0 - a0;
   const long long a = a0 + len * c / C, b = a0 + len * (c + 1) / C;
-  const unsigned int wbase = (unsigned int)p << sh, wmask = (unsigned int)W - 1;
-  auto add = [&](unsigned int key, const double* v) {
-    const unsigned int i = (key - wbase) & wmask;
+  auto add = [&](unsigned int i, const double* v) {  // i: index inside the window
     atomicAdd(&lrow[i], 1u);
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
@@ -1482,7 +1481,7 @@ int ptg_range_scatter(const void* keys, const void* pin_p, int nv, long n, long 
   memcpy(&pout, pout_p, sizeof(PayOut));
 #define PTG_RSC(NV, TR)                                                                                       \
   hipLaunchKernelGGL((range_scatter_k<NV, TR>), dim3(ntiles), dim3(512), 0, s, (const long long*)keys, pin, n,   \
-                     (long long)lo, sh, ntiles, (const long long*)offs, (unsigned int*)okeys, pout)
+                     (long long)lo, sh, ntiles, (const long long*)offs, (unsigned short*)okeys, pout)
   switch (nv) {
     case 0: PTG_RSC(0, RGT); break;
     case 1: PTG_RSC(1, RGT); break;
@@ -1508,7 +1507,7 @@ int ptg_range_agg(const void* okeys, const void* const* vals, int nv, const void
                                 150 * 1024);                                                                  \
       attr = true;                                                                                            \
     }                                                                                                         \
-    hipLaunchKernelGGL((range_agg_k<NV>), dim3(chunks, RGB), dim3(256), lds, s, (const unsigned int*)okeys, pay, \
+    hipLaunchKernelGGL((range_agg_k<NV>), dim3(chunks, RGB), dim3(256), lds, s, (const unsigned short*)okeys, pay, \
                        (const long long*)offs, ntiles, sh, (unsigned int*)prow, (double*)psum);              \
   }
   switch (nv) { case 0: PTG_RAG(0) break; case 1: PTG_RAG(1) break; default: PTG_RAG(2) break; }

@@ -330,7 +330,7 @@ def hash_agg_range(keys: torch.Tensor, pay: list, buf, nv: int, sample_lohi: tup
     offs = buf("roffs", (256 * ntiles + 1,), torch.int64)
     torch.cumsum(hist, 0, dtype=torch.int64, out=offs[1:])
     offs[0] = 0
-    okeys = buf("aokeys32", (max(n, 1),), torch.int32)[:n]
+    okeys = buf("rokeys16", (max(n, 1),), torch.int16)[:n]  # u16 index inside the partition's window
     ovals = [buf(f"aov{j}", (max(n, 1),), torch.float64)[:n] for j in range(nv)]
     pin, pout = _pay_in(pay), _pay_out(ovals)
     hip("ptg_range_scatter", ptr(keys), ctypes.addressof(pin), nv, n, int(lo), sh, ntiles, ptr(offs), ptr(okeys),
