@@ -948,20 +948,28 @@ __global__ __launch_bounds__(NT) void range_scatter_k(const long long* __restric
 
 // grid (chunks, 256): partition p = blockIdx.y holds rows [offs[p*ntiles], offs[(p+1)*ntiles]), keys
 // lo + p*W + okeys[i] (u16 window indices).  Output per chunk c (Rw = 256*W entries):
-// prow[c][0][Rw] rows, prow[c][1+j][Rw] non-null count of column j, psum[c][j][Rw] sums.
-template <int NV>
+// prow[c][0][Rw] rows, prow[c][1+j][Rw] non-null count of column j, psum[c][j][Rw] sums and, with
+// MINMAX, pmm[c][2j][Rw] / pmm[c][2j+1][Rw] min / max (+-inf where a key has no non-null value).
+// LDS: W * (4 + NV * (12 + (MINMAX ? 16 : 0))) bytes (ops/df.py picks W to fit).
+template <int NV, bool MINMAX>
 __global__ __launch_bounds__(256) void range_agg_k(const unsigned short* __restrict__ okeys, AggPay pay,
                                                    const long long* __restrict__ offs, int ntiles, int sh,
-                                                   unsigned int* __restrict__ prow, double* __restrict__ psum) {
+                                                   unsigned int* __restrict__ prow, double* __restrict__ psum,
+                                                   double* __restrict__ pmm) {
   constexpr int NVS = NV > 0 ? NV : 1;
   extern __shared__ __align__(16) unsigned char lds_raw[];
   const int W = 1 << sh, p = blockIdx.y, c = blockIdx.x, C = gridDim.x;
-  double* lsum = (double*)lds_raw;                          // [NV][W]
-  unsigned int* lrow = (unsigned int*)(lsum + (long)NV * W); // [1 + NV][W]
+  double* lsum = (double*)lds_raw;                                    // [NV][W]
+  double* lmm = lsum + (long)NV * W;                                  // [NV][2][W] (MINMAX)
+  unsigned int* lrow = (unsigned int*)(lmm + (MINMAX ? 2L * NV * W : 0L)); // [1 + NV][W]
   for (int t = threadIdx.x; t < W; t += 256) {
     lrow[t] = 0;
 #pragma unroll
-    for (int j = 0; j < NV; ++j) { lsum[j * W + t] = 0.0; lrow[(1 + j) * W + t] = 0; }
+    for (int j = 0; j < NV; ++j) {
+      lsum[j * W + t] = 0.0;
+      lrow[(1 + j) * W + t] = 0;
+      if (MINMAX) { lmm[(2 * j) * W + t] = INFINITY; lmm[(2 * j + 1) * W + t] = -INFINITY; }
+    }
   }
   __syncthreads();
   const long long a0 = offs[(long)p * ntiles], b0 = offs[(long)(p + 1) * ntiles], len = b0 - a0;
@@ -973,6 +981,10 @@ __global__ __launch_bounds__(256) void range_agg_k(const unsigned short* __restr
       if (v[j] != v[j]) continue;  // null / NaN
       atomicAdd(&lsum[j * W + i], v[j]);
       atomicAdd(&lrow[(1 + j) * W + i], 1u);
+      if (MINMAX) {
+        lds_min_f64(&lmm[(2 * j) * W + i], v[j]);
+        lds_max_f64(&lmm[(2 * j + 1) * W + i], v[j]);
+      }
     }
   };
   long long i = a + threadIdx.x;
@@ -1002,6 +1014,10 @@ __global__ __launch_bounds__(256) void range_agg_k(const unsigned short* __restr
     for (int j = 0; j < NV; ++j) {
       prow[((long)c * (1 + NV) + 1 + j) * Rw + o + t] = lrow[(1 + j) * W + t];
       psum[((long)c * NV + j) * Rw + o + t] = lsum[j * W + t];
+      if (MINMAX) {
+        pmm[((long)c * 2 * NV + 2 * j) * Rw + o + t] = lmm[(2 * j) * W + t];
+        pmm[((long)c * 2 * NV + 2 * j + 1) * Rw + o + t] = lmm[(2 * j + 1) * W + t];
+      }
     }
   }
 }
@@ -1463,8 +1479,8 @@ int ptg_part_agg2(const void* okeys, int key32, long kbase, const void* const* v
 
 // dense small-range groupBy (range_count_k / range_scatter_k / range_agg_k).  Tiles are
 // ptg_range_tile_rows(nv) rows; hist u32[256*ntiles] digit-major, range i64[ntiles][2];
-// offs i64[256*ntiles + 1] = exclusive scan of hist with offs[last] = n.  sh <= 12, nv <= 2.
-int ptg_range_tile_rows(int nv) { return nv <= 1 ? RGT : RGT / 2; }
+// offs i64[256*ntiles + 1] = exclusive scan of hist with offs[last] = n.  sh <= 12, nv <= 4.
+int ptg_range_tile_rows(int nv) { return nv <= 1 ? RGT : (nv == 2 ? RGT / 2 : RGT / 4); }
 int ptg_range_count(const void* keys, long n, long lo, int sh, int T, int ntiles, void* hist, void* range,
                     hipStream_t s) {
   if (ntiles <= 0 || T > RGT || sh < 0 || sh > 12) return (int)hipErrorInvalidValue;
@@ -1486,35 +1502,43 @@ int ptg_range_scatter(const void* keys, const void* pin_p, int nv, long n, long 
     case 0: PTG_RSC(0, RGT); break;
     case 1: PTG_RSC(1, RGT); break;
     case 2: PTG_RSC(2, RGT / 2); break;
+    case 3: PTG_RSC(3, RGT / 4); break;
+    case 4: PTG_RSC(4, RGT / 4); break;
     default: return (int)hipErrorInvalidValue;
   }
 #undef PTG_RSC
   PTG_RETURN_LAUNCH();
 }
 // vals: host array of nv f64 device pointers (scattered payload); prow u32[chunks][1+nv][256<<sh],
-// psum f64[chunks][nv][256<<sh]
-int ptg_range_agg(const void* okeys, const void* const* vals, int nv, const void* offs, int ntiles, int sh,
-                  int chunks, void* prow, void* psum, hipStream_t s) {
-  if (nv < 0 || nv > 2 || sh < 0 || sh > 12 || chunks <= 0) return (int)hipErrorInvalidValue;
-  const size_t lds = ((size_t)1 << sh) * (4 + (size_t)nv * 12);
+// psum f64[chunks][nv][256<<sh], pmm f64[chunks][2*nv][256<<sh] (minmax only)
+int ptg_range_agg(const void* okeys, const void* const* vals, int nv, int minmax, const void* offs, int ntiles,
+                  int sh, int chunks, void* prow, void* psum, void* pmm, hipStream_t s) {
+  if (nv < 0 || nv > PAY_MAX || sh < 0 || sh > 12 || chunks <= 0 || (minmax && !pmm)) return (int)hipErrorInvalidValue;
+  const size_t lds = ((size_t)1 << sh) * (4 + (size_t)nv * (12 + (minmax ? 16 : 0)));
+  if (lds > 150 * 1024) return (int)hipErrorInvalidValue;
   AggPay pay;
   for (int j = 0; j < PAY_MAX; ++j) pay.vals[j] = j < nv ? (const double*)vals[j] : nullptr;
-#define PTG_RAG(NV)                                                                                           \
+#define PTG_RAG(NV, MM)                                                                                       \
   {                                                                                                           \
     static bool attr = false;                                                                                 \
     if (!attr) {                                                                                              \
-      (void)hipFuncSetAttribute((const void*)range_agg_k<NV>, hipFuncAttributeMaxDynamicSharedMemorySize,     \
+      (void)hipFuncSetAttribute((const void*)range_agg_k<NV, MM>, hipFuncAttributeMaxDynamicSharedMemorySize, \
                                 150 * 1024);                                                                  \
       attr = true;                                                                                            \
     }                                                                                                         \
-    hipLaunchKernelGGL((range_agg_k<NV>), dim3(chunks, RGB), dim3(256), lds, s, (const unsigned short*)okeys, pay, \
-                       (const long long*)offs, ntiles, sh, (unsigned int*)prow, (double*)psum);              \
+    hipLaunchKernelGGL((range_agg_k<NV, MM>), dim3(chunks, RGB), dim3(256), lds, s, (const unsigned short*)okeys, \
+                       pay, (const long long*)offs, ntiles, sh, (unsigned int*)prow, (double*)psum, (double*)pmm); \
   }
-  switch (nv) { case 0: PTG_RAG(0) break; case 1: PTG_RAG(1) break; default: PTG_RAG(2) break; }
+  if (minmax) {
+    switch (nv) { case 0: PTG_RAG(0, true) break; case 1: PTG_RAG(1, true) break; case 2: PTG_RAG(2, true) break;
+                  case 3: PTG_RAG(3, true) break; default: PTG_RAG(4, true) break; }
+  } else {
+    switch (nv) { case 0: PTG_RAG(0, false) break; case 1: PTG_RAG(1, false) break; case 2: PTG_RAG(2, false) break;
+                  case 3: PTG_RAG(3, false) break; default: PTG_RAG(4, false) break; }
+  }
 #undef PTG_RAG
   PTG_RETURN_LAUNCH();
 }
-
 // sort: keys u64[n] out, range u64[2] (host-initialised {~0, 0})
 int ptg_sort_key_prep(const void* col, int type, long n, int desc, void* out, void* range, hipStream_t s) {
   int g = grid_n(n);

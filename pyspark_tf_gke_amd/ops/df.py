@@ -284,36 +284,48 @@ def estimate_distinct(keys: torch.Tensor, sample: int = 1 << 16) -> int:
     return int(min(n, max(d, hi)))
 
 
-RANGE_MAX_SPAN = 1 << 20  # dense-key path: keys within a window of 256 partitions x <= 4096 keys
+RANGE_MAX_SPAN = 1 << 20  # dense-key path: keys within 256 partitions x <= 4096 keys (fewer with more columns)
 RANGE_MIN_ROWS = 1 << 22  # below this the sample/plan overhead is not worth a second code path
 
 
-def _range_window(lo: int, hi: int):
-    """(window base, sh): a window of 256 << sh >= hi - lo + 1 keys (sh <= 12) centred on [lo, hi],
+def _range_sh_max(nv: int, minmax: bool) -> int:
+    """Widest partition window (log2, <= 12 = 4096 keys) whose direct-indexed LDS table fits range_agg_k's
+    150 KB: 4 B of row count + per column 12 B (sum, count) and 16 B more with min/max per key."""
+    per = 4 + nv * (12 + (16 if minmax else 0))
+    sh = 12
+    while sh > 0 and (per << sh) > 150 * 1024:
+        sh -= 1
+    return sh
+
+
+def _range_window(lo: int, hi: int, sh_max: int = 12):
+    """(window base, sh): a window of 256 << sh >= hi - lo + 1 keys (sh <= sh_max) centred on [lo, hi],
     so keys a sample missed just past its ends still fall inside; None if the span is too wide."""
     span = hi - lo + 1
     sh = 0
     while (RADIX_RANGE_BINS << sh) < span:
         sh += 1
-    return None if sh > 12 else (lo - ((RADIX_RANGE_BINS << sh) - span) // 2, sh)
+    return None if sh > sh_max else (lo - ((RADIX_RANGE_BINS << sh) - span) // 2, sh)
 
 
 RADIX_RANGE_BINS = 256
 
 
-def hash_agg_range(keys: torch.Tensor, pay: list, buf, nv: int, sample_lohi: tuple[int, int]):
+def hash_agg_range(keys: torch.Tensor, pay: list, buf, nv: int, sample_lohi: tuple[int, int],
+                   minmax: bool = False):
     """groupBy(key).agg for int64 keys spanning at most 2^20 values (csrc/kernels/df.hip range_*_k):
     one range-partitioning pass by the top 8 bits of (key - lo) and a direct-indexed LDS aggregation
     per (partition, chunk), instead of the two hash levels of :func:`hash_agg_radix`.  ``sample_lohi``
     guesses the window from a sample; the count pass returns the exact [min, max] and a key outside
     the guess re-plans the window (or returns None: the caller takes the hash path).  Same result
-    format as :func:`hash_agg` (min/max columns are +-inf: the caller only routes sum/count/avg here)."""
+    format as :func:`hash_agg` (min/max are +-inf unless ``minmax``)."""
     dev = keys.device
     n = keys.numel()
     lib = _native.hip_lib()
     T = int(lib.ptg_range_tile_rows(nv))
     ntiles = (n + T - 1) // T
-    win = _range_window(*sample_lohi)
+    sh_max = _range_sh_max(nv, minmax)
+    win = _range_window(*sample_lohi, sh_max)
     if win is None:
         return None
     hist = buf("rhist", (256 * ntiles,), torch.int32)
@@ -324,7 +336,7 @@ def hash_agg_range(keys: torch.Tensor, pay: list, buf, nv: int, sample_lohi: tup
         mn, mx = (int(x) for x in torch.stack([rng[:, 0].min(), rng[:, 1].max()]).tolist())
         if mn >= lo and mx < lo + (256 << sh):
             break
-        win = _range_window(mn, mx) if attempt == 0 else None
+        win = _range_window(mn, mx, sh_max) if attempt == 0 else None
         if win is None:
             return None
     offs = buf("roffs", (256 * ntiles + 1,), torch.int64)
@@ -339,15 +351,22 @@ def hash_agg_range(keys: torch.Tensor, pay: list, buf, nv: int, sample_lohi: tup
     chunks = max(1, min(int(os.environ.get("PTG_RANGE_CHUNKS", "8")), (n // 256) // (1 << 16) or 1))
     prow = buf("rprow", (chunks, 1 + nv, Rw), torch.int32)
     psum = buf("rpsum", (chunks, max(nv, 1), Rw), torch.float64)
+    pmm = buf("rpmm", (chunks, 2 * max(nv, 1), Rw), torch.float64) if minmax else None
     vptrs = (ctypes.c_void_p * PAY_MAX)(*([o.data_ptr() for o in ovals] + [0] * (PAY_MAX - nv)))
-    hip("ptg_range_agg", ptr(okeys), ctypes.addressof(vptrs), nv, ptr(offs), ntiles, sh, chunks, ptr(prow), ptr(psum))
+    hip("ptg_range_agg", ptr(okeys), ctypes.addressof(vptrs), nv, int(minmax), ptr(offs), ntiles, sh, chunks,
+        ptr(prow), ptr(psum), ptr(pmm) if minmax else None)
     cnts = prow.to(torch.int64).sum(0) if chunks > 1 else prow[0].to(torch.int64)  # [1 + nv][Rw]
     sums = psum.sum(0) if chunks > 1 else psum[0]
     idx = torch.nonzero(cnts[0] > 0).view(-1)
     out_keys = idx + lo
     rows = cnts[0][idx].to(torch.float64)
-    inf = torch.full((idx.numel(),), math.inf, dtype=torch.float64, device=dev)
-    outs = [(sums[j][idx], cnts[1 + j][idx].to(torch.float64), inf, -inf) for j in range(nv)]
+    if minmax:
+        mins = pmm[:, 0::2].amin(0) if chunks > 1 else pmm[0, 0::2]
+        maxs = pmm[:, 1::2].amax(0) if chunks > 1 else pmm[0, 1::2]
+        outs = [(sums[j][idx], cnts[1 + j][idx].to(torch.float64), mins[j][idx], maxs[j][idx]) for j in range(nv)]
+    else:
+        inf = torch.full((idx.numel(),), math.inf, dtype=torch.float64, device=dev)
+        outs = [(sums[j][idx], cnts[1 + j][idx].to(torch.float64), inf, -inf) for j in range(nv)]
     return out_keys, rows, outs
 
 
@@ -380,12 +399,11 @@ def hash_agg_radix(keys: torch.Tensor, vals: list, valids: list, want_minmax: bo
         if vd is not None and vd.dtype == torch.bool:
             vd = vd.view(torch.uint8)
         pay.append((v.contiguous(), vd))
-    if (nv <= 2 and not want_minmax and keys.dtype == torch.int64 and n >= RANGE_MIN_ROWS
-            and os.environ.get("PTG_GROUPBY_RANGE", "1") != "0"):
+    if keys.dtype == torch.int64 and n >= RANGE_MIN_ROWS and os.environ.get("PTG_GROUPBY_RANGE", "1") != "0":
         smp = keys[:: max(1, n // 65536)]
         slo, shi = (int(x) for x in torch.stack([smp.min(), smp.max()]).tolist())
-        if shi - slo < RANGE_MAX_SPAN:
-            r = hash_agg_range(keys.contiguous(), pay, buf, nv, (slo, shi))
+        if shi - slo < (RADIX_RANGE_BINS << _range_sh_max(nv, want_minmax)):
+            r = hash_agg_range(keys.contiguous(), pay, buf, nv, (slo, shi), want_minmax)
             if r is not None:
                 return r
     K = est_keys if est_keys is not None else estimate_distinct(keys)

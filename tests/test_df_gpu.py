@@ -104,13 +104,15 @@ def test_radix_agg_matches_host(hip_built, n, nkeys, nv, minmax):
     _assert_agg_equal(got, want, minmax)
 
 
-@pytest.mark.parametrize("lo,span,nv", [(0, 1_000_000, 1), (-5_000_000_000, 1 << 20, 2), (123, 4_000, 0),
-                                         (7, 300_000, 2)])
-def test_range_agg_matches_host(hip_built, lo, span, nv):
+@pytest.mark.parametrize("lo,span,nv,minmax", [(0, 1_000_000, 1, False), (-5_000_000_000, 1 << 20, 2, False),
+                                                (123, 4_000, 0, False), (7, 300_000, 2, False),
+                                                (0, 1_000_000, 1, True), (11, 200_000, 4, True),
+                                                (-7, 500_000, 3, False)])
+def test_range_agg_matches_host(hip_built, lo, span, nv, minmax):
     """Dense small-range keys take the one-level range partition + direct-indexed LDS aggregation
-    (range_*_k): sums / non-null counts with NaN values and a validity mask, count-only, negative
-    keys, and a span of exactly 2^20 whose extremes the sample misses (the window is re-planned
-    from the count pass's exact range).  Checked against the host path."""
+    (range_*_k): sums / non-null counts / min / max with NaN values and validity masks, 0-4 value
+    columns, negative keys, and a span of exactly 2^20 whose extremes the sample misses (the window
+    is re-planned from the count pass's exact range).  Checked against the host path."""
     n = 6_000_000
     g = torch.Generator().manual_seed(span + nv)
     k = torch.randint(0, span, (n,), generator=g) + lo
@@ -128,10 +130,10 @@ def test_range_agg_matches_host(hip_built, lo, span, nv):
         valids.append(vd)
     ws = {}
     got = D.hash_agg_radix(k.cuda(), [c.cuda() for c in cols], [None if x is None else x.cuda() for x in valids],
-                           False, ws=ws)
+                           minmax, ws=ws)
     assert "rprow" in ws, "range path not taken"
-    want = D.hash_agg(k, cols, valids, False)
-    _assert_agg_equal(got, want, False)
+    want = D.hash_agg(k, cols, valids, minmax)
+    _assert_agg_equal(got, want, minmax)
 
 
 def test_range_agg_off_switch_same_result(hip_built, monkeypatch):
