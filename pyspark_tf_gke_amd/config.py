@@ -1,0 +1,145 @@
+"""Typed runtime configuration: one registry for every framework knob.
+
+The reference mixes argparse-with-env-defaults (train_tf_ps.py:822-840), raw env vars
+(spark_session.py:44-50, k_means.py:57,186) and Spark ``--conf`` / builder ``.config()`` keys.  The
+user-facing names of those stay where they are (the CLIs keep the reference's flags and env names).
+Everything this framework adds is declared here once, with its type, default, env var and
+``spark.ptg.*`` conf key, and resolved with a fixed precedence:
+
+    CLI override (:func:`set_cli`)  >  environment variable  >  Spark conf (the active session's
+    ``.config()`` / ``spark-submit --conf``, :func:`register_conf`; ``PTG_SPARK_CONF`` JSON)  >  default
+
+``python -m pyspark_tf_gke_amd.config`` prints the table with the value each knob resolves to.
+Knobs read at import time (the ``nn`` step switches) see the CLI, the environment and
+``PTG_SPARK_CONF``; session confs set later apply to knobs read at call time (groupBy, shuffle).
+"""
+from __future__ import annotations
+
+import json
+import os
+from dataclasses import dataclass
+from typing import Any
+
+_FALSE = ("0", "false", "no", "off", "")
+
+
+@dataclass(frozen=True)
+class Knob:
+    name: str
+    type: type
+    default: Any
+    env: str | None
+    conf: str | None
+    doc: str
+
+    def parse(self, raw: Any) -> Any:
+        if self.type is bool:
+            return raw if isinstance(raw, bool) else str(raw).strip().lower() not in _FALSE
+        if raw is None or (isinstance(raw, str) and raw == "" and self.type is not str):
+            return self.default
+        return self.type(raw)
+
+
+_K = [
+    # data engine
+    Knob("groupby_range", bool, True, "PTG_GROUPBY_RANGE", "spark.ptg.groupby.range",
+         "dense small-range integer keys take the one-pass range partition + direct LDS aggregation"),
+    Knob("groupby_range_chunks", int, 8, "PTG_RANGE_CHUNKS", "spark.ptg.groupby.rangeChunks",
+         "row chunks per range partition in the range aggregation (workgroups = 256 x chunks)"),
+    Knob("shuffle_buffer_gb", float, 64.0, "PTG_SHUFFLE_BUFFER_GB", "spark.ptg.shuffle.buffer.gb",
+         "HBM staging budget of one all-to-all-v shuffle round"),
+    Knob("device", str, "", "PTG_DEVICE", "spark.ptg.device", "executor device: cuda / cpu (default: cuda if present)"),
+    Knob("jdbc_root", str, "", "PTG_JDBC_ROOT", None, "directory of the SQLite files behind jdbc: URLs"),
+    Knob("fault_task", int, 0, "PTG_FAULT_TASK", None, "fault injection: fail this many stage-task attempts"),
+    # training step
+    Knob("fused_adam", bool, True, "PTG_FUSED_ADAM", None, "Adam inside the big Dense weight-gradient GEMM epilogue (1 GPU)"),
+    Knob("fused_head", bool, True, "PTG_FUSED_HEAD", None, "CNN-B1 Dense(relu)->Dense->MSE head as two kernels"),
+    Knob("device_feed", bool, True, "PTG_DEVICE_FEED", None, "fit(): pinned ring + side-stream H2D for host datasets"),
+    Knob("side_stream", bool, True, "PTG_SIDE_STREAM", None, "weight gradients on a side HIP stream (1 replica)"),
+    Knob("raw_u8_input", bool, True, "PTG_RAW_U8_INPUT", None, "first conv reads the uint8 image batch directly"),
+    Knob("sparse_first", bool, True, "PTG_SPARSE_FIRST", None, "first conv layer keeps a sparse pool record"),
+    Knob("blaslt_dx", bool, True, "PTG_BLASLT_DX", None, "big-Dense dX through hipBLASLt where measured faster"),
+    Knob("hip_graph", bool, False, "PTG_HIP_GRAPH", None, "capture the training step in a HIP graph (jit_compile)"),
+    Knob("host_fp32", bool, False, "PTG_HOST_FP32", None, "CPU tensors: fp32 reference path everywhere"),
+    Knob("seed", int, 1337, "PTG_SEED", None, "weight-initialisation seed when none is given"),
+    # distribution
+    Knob("dist_backend", str, "", "PTG_DIST_BACKEND", None, "torch.distributed backend override (default nccl=RCCL / gloo)"),
+    Knob("pg_timeout_s", float, 600.0, "PTG_PG_TIMEOUT", None, "process-group collective timeout (hang -> error -> restart)"),
+    Knob("bucket_mb", float, 64.0, "PTG_BUCKET_MB", None, "MWMS gradient bucket size"),
+    Knob("sharded_update", bool, True, "PTG_SHARDED_UPDATE", None, "MWMS: reduce-scatter + sharded optimizer + all-gather"),
+    Knob("persist_dynamic", bool, False, "PTG_PERSIST_DYNAMIC", None, "persistent conv kernels in work-queue mode for N > 1"),
+    Knob("ps_mode", str, "sync", "PTG_PS_MODE", None, "ParameterServerStrategy: sync or async"),
+    Knob("ipc_allreduce", bool, False, "PTG_IPC_ALLREDUCE", None, "one-shot IPC all-reduce for small messages"),
+    Knob("fault_rank", str, "", "PTG_FAULT_RANK", None, "fault injection: rank to kill"),
+    Knob("fault_step", int, 1, "PTG_FAULT_STEP", None, "fault injection: step at which fault_rank dies"),
+    Knob("heartbeat_dir", str, "", "PTG_HEARTBEAT_DIR", None, "progress heartbeat files for the launcher's hang detector"),
+    # native code / observability
+    Knob("checked", bool, False, "PTG_CHECKED", None, "load the bounds-checked kernel library"),
+    Knob("hip_lib", str, "", "PTG_HIP_LIB", None, "in-tree kernel library variant to load (A/B runs)"),
+    Knob("roctx", bool, True, "PTG_ROCTX", None, "roctx ranges around steps"),
+    Knob("metrics_jsonl", str, "", "PTG_METRICS_JSONL", None, "per-step metrics JSONL path"),
+    Knob("log_all_ranks", bool, False, "PTG_LOG_ALL_RANKS", None, "INFO logs from every rank, not only rank 0"),
+]
+KNOBS: dict[str, Knob] = {k.name: k for k in _K}
+
+_cli: dict[str, Any] = {}
+_confs: list[dict] = []
+
+
+def set_cli(name: str, value: Any) -> None:
+    """A command-line value: highest precedence."""
+    _cli[KNOBS[name].name] = value
+
+
+def register_conf(conf: dict | None) -> None:
+    """Spark conf of the active session (``SparkSession.builder.config`` / ``spark.conf.set``, read
+    live); ``None`` when the session stops."""
+    _confs[:] = [conf] if conf is not None else []
+
+
+def _submitted_conf() -> dict:
+    raw = os.environ.get("PTG_SPARK_CONF")
+    try:
+        return json.loads(raw) if raw else {}
+    except ValueError:
+        return {}
+
+
+def source(name: str) -> str:
+    k = KNOBS[name]
+    if k.name in _cli:
+        return "cli"
+    if k.env and os.environ.get(k.env) is not None:
+        return "env"
+    if k.conf and (any(k.conf in c for c in _confs) or k.conf in _submitted_conf()):
+        return "conf"
+    return "default"
+
+
+def get(name: str) -> Any:
+    k = KNOBS[name]
+    if k.name in _cli:
+        return k.parse(_cli[k.name])
+    if k.env:
+        raw = os.environ.get(k.env)
+        if raw is not None:
+            return k.parse(raw)
+    if k.conf:
+        for c in reversed(_confs):
+            if k.conf in c:
+                return k.parse(c[k.conf])
+        sub = _submitted_conf()
+        if k.conf in sub:
+            return k.parse(sub[k.conf])
+    return k.default
+
+
+def describe() -> list[dict]:
+    return [{"name": k.name, "type": k.type.__name__, "value": get(k.name), "source": source(k.name),
+             "env": k.env, "conf": k.conf, "default": k.default, "doc": k.doc} for k in _K]
+
+
+if __name__ == "__main__":
+    for r in describe():
+        print(f"{r['name']:22s} {r['type']:5s} {str(r['value']):10s} [{r['source']:7s}] "
+              f"env={r['env'] or '-'} conf={r['conf'] or '-'}  {r['doc']}")

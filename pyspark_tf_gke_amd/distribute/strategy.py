@@ -24,6 +24,7 @@ import torch
 
 from ..parallel import comm
 from .cluster import ClusterSpec, InputContext, MinSizePartitioner, TFConfigClusterResolver
+from .. import config
 
 _STACK: list = []
 
@@ -265,14 +266,14 @@ class MultiWorkerMirroredStrategy(Strategy):
                  device=None, sharded_update: bool | None = None):
         super().__init__(device)
         self.cluster_resolver = cluster_resolver or TFConfigClusterResolver()
-        mb = bucket_mb if bucket_mb is not None else float(os.environ.get("PTG_BUCKET_MB", "64"))
+        mb = bucket_mb if bucket_mb is not None else float(config.get("bucket_mb"))
         self.bucket_elems = max(1, int(mb * (1 << 20) / 4))
         if sharded_update is None:
-            sharded_update = os.environ.get("PTG_SHARDED_UPDATE", "1") != "0"
+            sharded_update = config.get("sharded_update")
         self.sharded_update = bool(sharded_update) and self.world_size > 1
         self._works: list = []
         self._launched = 0
-        if self.world_size > 1 and self.device.type == "cuda" and os.environ.get("PTG_PERSIST_DYNAMIC") == "1":
+        if self.world_size > 1 and self.device.type == "cuda" and config.get("persist_dynamic"):
             # opt-in: work-queue conv kernels (absorb CUs taken by the concurrent RCCL kernels).  The
             # default stays the static-grid kernels, the faster ones in the only A/B measured so far
             # (1 GPU, 119.5k vs 114.3k samples/s, README); re-measure on 8 GPUs before flipping it.
@@ -545,7 +546,7 @@ class ParameterServerStrategy(Strategy):
         self.num_workers = max(self.cluster_spec.num_tasks("worker"), self.world_size)
         self.num_ps = self.cluster_spec.num_tasks("ps") or self.world_size
         self.variable_partitioner = variable_partitioner or MinSizePartitioner(256 << 10, max(self.num_ps, 1))
-        self.mode = (mode or os.environ.get("PTG_PS_MODE", "sync")).lower()
+        self.mode = (mode or config.get("ps_mode")).lower()
         if self.mode not in ("sync", "async"):
             raise ValueError(f"ParameterServerStrategy mode must be 'sync' or 'async', not {self.mode!r}")
 

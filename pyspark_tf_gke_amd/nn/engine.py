@@ -23,12 +23,13 @@ import torch
 from ..ops import nn as K
 from . import layers as L
 from . import streams as S
+from .. import config
 
 
 # Host-path debug precision: with PTG_HOST_FP32=1 (or ``host_fp32(True)``) CPU models keep their
 # "bf16" activations and compute-weight mirror in fp32, so the CPU engine can be checked against
 # an fp32 autograd oracle exactly (the GPU path is always bf16).
-_HOST_FP32 = [os.environ.get("PTG_HOST_FP32") == "1"]
+_HOST_FP32 = [config.get("host_fp32")]
 
 # Sparse PReLU+pool record (conv.hip EPI_POOLS: z at the argmax + argmax index instead of the full
 # z) for layers 2-4 as well was measured and rejected (README): its longer epilogue makes those
@@ -37,12 +38,12 @@ _HOST_FP32 = [os.environ.get("PTG_HOST_FP32") == "1"]
 # prelu_pool_bwd_sel turns it into dZ's record (dZ at the argmax) and the weight gradient expands it in
 # LDS, so the full-resolution z and dZ (335 MB each for CNN-B1 at batch 256) never exist.  Measured
 # on CNN-B1 b256: 118.6k vs 116.6k samples/s with the dense first-layer record.
-SPARSE_FIRST = os.environ.get("PTG_SPARSE_FIRST", "1") == "1"
+SPARSE_FIRST = config.get("sparse_first")
 # That first layer reads the raw uint8 [N,H,W,3] image batch itself (conv.hip U8 loaders: /255 and
 # the zero 4th channel applied in registers) in both its forward and its weight gradient, so the
 # packed bf16 copy of the input (pack_u8rgb4_k: 3 B read + 8 B written per pixel, 8 B read twice
 # more) is never made.  PTG_RAW_U8_INPUT=0 restores the pack.
-RAW_U8 = os.environ.get("PTG_RAW_U8_INPUT", "1") != "0"
+RAW_U8 = config.get("raw_u8_input")
 
 
 def host_fp32(enabled: bool | None = None) -> bool:

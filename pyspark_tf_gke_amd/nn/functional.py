@@ -29,6 +29,7 @@ from . import graph_ops as G
 from . import layers as L
 from .model import Sequential
 from .params import ParamStore
+from .. import config
 
 
 class KerasTensor:
@@ -266,7 +267,7 @@ class Model(Sequential):
             shapes[id(t)] = t.layer.build(ins[0] if len(ins) == 1 else tuple(ins), self.store)
         self.output_shape = shapes[id(self._out)]
         if seed is None:
-            seed = int(os.environ.get("PTG_SEED", "1337"))
+            seed = config.get("seed")
         self.store.finalize(self.device, seed=seed)
         for l in self.layers:
             if isinstance(l, L.BatchNormalization):

@@ -30,12 +30,13 @@ from . import losses as LS
 from . import metrics as MT
 from . import optimizers as OPT
 from .params import ParamStore
+from .. import config
 
 # Adam fused into the weight-gradient GEMM of big Dense layers on one replica (gemm.hip EpiAdam):
 # the 168 MB CNN-B1 Dense kernel gradient is never written or re-read.  PTG_FUSED_ADAM=0 disables.
-FUSED_ADAM = os.environ.get("PTG_FUSED_ADAM", "1") != "0"
-DEVICE_FEED = os.environ.get("PTG_DEVICE_FEED", "1") != "0"
-FUSED_HEAD = os.environ.get("PTG_FUSED_HEAD", "1") != "0"
+FUSED_ADAM = config.get("fused_adam")
+DEVICE_FEED = config.get("device_feed")
+FUSED_HEAD = config.get("fused_head")
 
 
 def default_device() -> torch.device:
@@ -120,7 +121,7 @@ class Sequential:
             shape = l.build(shape, self.store)
         self.output_shape = shape
         if seed is None:
-            seed = int(os.environ.get("PTG_SEED", "1337"))
+            seed = config.get("seed")
         self.store.finalize(self.device, seed=seed)
         self.ops = E.lower(self._layers)
         self.store.update_zero_ranges()
@@ -164,7 +165,7 @@ class Sequential:
         (single-GPU training; multi-rank strategies stay eager because their collectives are
         launched from host hooks)."""
         if jit_compile is None:
-            jit_compile = os.environ.get("PTG_HIP_GRAPH", "0") == "1"
+            jit_compile = config.get("hip_graph")
         self.jit_compile = bool(jit_compile)
         self._graphs = {}
         self._graph_warm = {}

@@ -16,8 +16,9 @@ from __future__ import annotations
 import os
 
 import torch
+from .. import config
 
-ENABLED = os.environ.get("PTG_SIDE_STREAM", "1") != "0"
+ENABLED = config.get("side_stream")
 _STREAMS: dict = {}
 
 

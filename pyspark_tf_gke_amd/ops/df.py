@@ -13,7 +13,7 @@ import struct
 import numpy as np
 import torch
 
-from .. import _native
+from .. import _native, config
 from ._util import hip, on_device, ptr
 
 CT_F32, CT_F64, CT_I32, CT_I64, CT_U8, CT_CODE = range(6)
@@ -348,7 +348,7 @@ def hash_agg_range(keys: torch.Tensor, pay: list, buf, nv: int, sample_lohi: tup
     hip("ptg_range_scatter", ptr(keys), ctypes.addressof(pin), nv, n, int(lo), sh, ntiles, ptr(offs), ptr(okeys),
         ctypes.addressof(pout))
     Rw = 256 << sh
-    chunks = max(1, min(int(os.environ.get("PTG_RANGE_CHUNKS", "8")), (n // 256) // (1 << 16) or 1))
+    chunks = max(1, min(int(config.get("groupby_range_chunks")), (n // 256) // (1 << 16) or 1))
     prow = buf("rprow", (chunks, 1 + nv, Rw), torch.int32)
     psum = buf("rpsum", (chunks, max(nv, 1), Rw), torch.float64)
     pmm = buf("rpmm", (chunks, 2 * max(nv, 1), Rw), torch.float64) if minmax else None
@@ -399,7 +399,7 @@ def hash_agg_radix(keys: torch.Tensor, vals: list, valids: list, want_minmax: bo
         if vd is not None and vd.dtype == torch.bool:
             vd = vd.view(torch.uint8)
         pay.append((v.contiguous(), vd))
-    if keys.dtype == torch.int64 and n >= RANGE_MIN_ROWS and os.environ.get("PTG_GROUPBY_RANGE", "1") != "0":
+    if keys.dtype == torch.int64 and n >= RANGE_MIN_ROWS and config.get("groupby_range"):
         smp = keys[:: max(1, n // 65536)]
         slo, shi = (int(x) for x in torch.stack([smp.min(), smp.max()]).tolist())
         if shi - slo < (RADIX_RANGE_BINS << _range_sh_max(nv, want_minmax)):

@@ -15,6 +15,7 @@ import torch
 
 from . import reference as ref
 from ._util import hip, need, on_device, ptr
+from .. import config
 
 # prelu+pool backward kernel: "sg" = sample-parallel blocks with an in-LDS dalpha reduction
 # (prelu_pool_bwd_sg_k), "chunk" = position-parallel blocks adding dalpha partials with atomics
@@ -280,7 +281,7 @@ def linear_fwd(x, w, bias, act, out, workspace=None, splits: int = 0):
 # A plain GEMM with nothing to fuse goes to the vendor library when it measured faster: the big
 # Dense layer's dX (M = batch 256, N = 20480, K = 2048) is 34 us in hipBLASLt vs 45 us in gemm_kernel
 # (tools/dense_gemm_bench.py).  PTG_BLASLT_DX=0 keeps it on gemm_kernel.
-BLASLT_DX = os.environ.get("PTG_BLASLT_DX", "1") != "0"
+BLASLT_DX = config.get("blaslt_dx")
 
 
 def linear_dx(dy, w, out):

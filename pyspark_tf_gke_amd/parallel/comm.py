@@ -16,6 +16,7 @@ import os
 
 import torch
 import torch.distributed as dist
+from .. import config
 
 
 def env_rank() -> tuple[int, int, int]:
@@ -35,7 +36,7 @@ def init(backend: str | None = None, device_type: str | None = None, timeout_s: 
     collective: a rank whose peer died or hung gets an error (gloo) or is aborted by the RCCL
     watchdog instead of blocking forever, exits non-zero, and the launcher restarts the group."""
     if timeout_s is None:
-        timeout_s = int(float(os.environ.get("PTG_PG_TIMEOUT", "600")))
+        timeout_s = int(config.get("pg_timeout_s"))
     rank, local, world = env_rank()
     if is_initialized():
         return dist.get_rank(), dist.get_world_size()
@@ -46,7 +47,7 @@ def init(backend: str | None = None, device_type: str | None = None, timeout_s: 
     if backend is None:
         # PTG_DIST_BACKEND=gloo: host-staged collectives even for GPU tensors (lets several ranks share
         # one GPU, e.g. a multi-rank rehearsal on a 1-GPU box; RCCL refuses duplicate devices)
-        backend = os.environ.get("PTG_DIST_BACKEND") or ("nccl" if device_type == "cuda" else "gloo")
+        backend = config.get("dist_backend") or ("nccl" if device_type == "cuda" else "gloo")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29500")
     kw = {}

@@ -25,8 +25,9 @@ import torch
 import torch.distributed as dist
 
 from .. import _native
+from .. import config
 
-ENABLED = os.environ.get("PTG_IPC_ALLREDUCE", "0") == "1"
+ENABLED = config.get("ipc_allreduce")
 DEFAULT_CAP = 1 << 20
 _DT = {torch.float32: 0, torch.float64: 1, torch.int64: 2}
 _INSTANCES: dict = {}

@@ -119,6 +119,9 @@ class SparkSession:
                     return SparkSession._active
                 master = self._master or os.environ.get("SPARK_MASTER") or self._conf.get("spark.master") or "local[*]"
                 s = SparkSession(self._app, master, self._conf)
+                from .. import config
+
+                config.register_conf(s.conf._conf)  # spark.ptg.* knobs (pyspark_tf_gke_amd/config.py)
                 SparkSession._active = s
                 return s
 
@@ -254,6 +257,9 @@ class SparkSession:
         with SparkSession._lock:
             if SparkSession._active is self:
                 SparkSession._active = None
+                from .. import config
+
+                config.register_conf(None)
         comm.barrier()
 
     def __enter__(self):

@@ -21,6 +21,7 @@ from ..ops import df as D
 from ..parallel import comm
 from . import types as T
 from .table import ColumnVector, Table
+from .. import config
 
 DEFAULT_BUDGET_GB = 64.0  # deploy/node.yaml spark.ptg.shuffle.buffer.gb
 STATS: dict = {"peak_staging_bytes": 0, "rounds": 0, "count_exchanges": 0}
@@ -30,9 +31,9 @@ def budget_bytes() -> int:
     from .session import SparkSession
 
     s = SparkSession.getActiveSession()
-    gb = DEFAULT_BUDGET_GB
-    if s is not None:
-        gb = float(s.conf.get("spark.ptg.shuffle.buffer.gb", gb))
+    gb = float(config.get("shuffle_buffer_gb"))  # env / submitted conf / default
+    if s is not None and config.source("shuffle_buffer_gb") not in ("cli", "env"):
+        gb = float(s.conf.get("spark.ptg.shuffle.buffer.gb", gb))  # the active session's conf
     return max(1, int(gb * (1 << 30)))
 
 

@@ -246,3 +246,32 @@ def test_range_window_plan():
     base, sh = D._range_window(15, 999_985)  # a 64K-key sample of keys 0..999,999
     assert base <= 0 and 999_999 < base + (256 << sh)
     assert D._range_window(0, 1 << 20) is None
+
+
+def test_config_precedence(monkeypatch):
+    """Typed knob registry: CLI > env > active session conf > default; the stopped
+    session's conf no longer applies; bool parsing of env strings."""
+    from pyspark_tf_gke_amd import config
+    from pyspark_tf_gke_amd.sql import SparkSession
+
+    monkeypatch.delenv("PTG_RANGE_CHUNKS", raising=False)
+    monkeypatch.delenv("PTG_SPARK_CONF", raising=False)
+    assert config.get("groupby_range_chunks") == 8 and config.source("groupby_range_chunks") == "default"
+    s = SparkSession.builder.master("local[1]").config("spark.ptg.groupby.rangeChunks", "4").getOrCreate()
+    try:
+        assert config.get("groupby_range_chunks") == 4 and config.source("groupby_range_chunks") == "conf"
+        s.conf.set("spark.ptg.groupby.rangeChunks", 2)  # live
+        assert config.get("groupby_range_chunks") == 2
+        monkeypatch.setenv("PTG_RANGE_CHUNKS", "16")
+        assert config.get("groupby_range_chunks") == 16 and config.source("groupby_range_chunks") == "env"
+        config.set_cli("groupby_range_chunks", 3)
+        assert config.get("groupby_range_chunks") == 3 and config.source("groupby_range_chunks") == "cli"
+    finally:
+        config._cli.pop("groupby_range_chunks", None)
+        s.stop()
+    monkeypatch.delenv("PTG_RANGE_CHUNKS")
+    assert config.get("groupby_range_chunks") == 8
+    for raw, want in (("0", False), ("false", False), ("1", True), ("yes", True)):
+        monkeypatch.setenv("PTG_GROUPBY_RANGE", raw)
+        assert config.get("groupby_range") is want
+    assert {r["name"] for r in config.describe()} >= {"fused_adam", "shuffle_buffer_gb", "pg_timeout_s"}
