@@ -125,6 +125,42 @@ def _pow2(x: int) -> int:
     return 1 << max(4, int(math.ceil(math.log2(max(x, 1)))))
 
 
+def _small_range_agg(keys, vals, valids):
+    """Keys spanning < ~4K values (small_range_agg_k): the whole range is one direct-indexed LDS
+    table per workgroup, one pass over the rows; None when the span is wider."""
+    n = keys.numel()
+    nv = len(vals)
+    smp = keys[:: max(1, n // 65536)]
+    wmax = (150 * 1024) // (4 + 12 * nv)
+    if int(smp.max().item()) - int(smp.min().item()) >= wmax:
+        return None
+    lo_t, hi_t = torch.aminmax(keys)
+    lo, hi = int(lo_t.item()), int(hi_t.item())
+    W = hi - lo + 1
+    if W > wmax:
+        return None
+    pay = []
+    for v, vd in zip(vals, valids):
+        v = v.view(torch.uint8) if v.dtype == torch.bool else v.contiguous()
+        if vd is not None and vd.dtype == torch.bool:
+            vd = vd.view(torch.uint8)
+        pay.append((v, vd))
+    G = 1024
+    rpb = -(-n // G)
+    G = -(-n // rpb)
+    prow = torch.empty((G, 1 + nv, W), dtype=torch.int32, device=keys.device)
+    psum = torch.empty((G, max(nv, 1), W), dtype=torch.float64, device=keys.device)
+    pin = _pay_in(pay)
+    hip("ptg_small_range_agg", ptr(keys.contiguous()), n, lo, W, ctypes.addressof(pin), nv, rpb, G, ptr(prow),
+        ptr(psum))
+    cnts = prow.to(torch.int64).sum(0)
+    sums = psum.sum(0)
+    idx = torch.nonzero(cnts[0] > 0).view(-1)
+    inf = torch.full((idx.numel(),), math.inf, dtype=torch.float64, device=keys.device)
+    outs = [(sums[j][idx], cnts[1 + j][idx].to(torch.float64), inf, -inf) for j in range(nv)]
+    return idx + lo, cnts[0][idx].to(torch.float64), outs
+
+
 def hash_agg(keys: torch.Tensor, vals: list, valids: list, want_minmax: bool = False, cap_hint: int | None = None):
     """groupBy(key).agg over int64 keys.  Returns (keys[m], rows[m], [(sum, cnt, min, max)] per value column)
     as tensors on the keys' device."""
@@ -145,6 +181,11 @@ def hash_agg(keys: torch.Tensor, vals: list, valids: list, want_minmax: bool = F
             mx = torch.full((m,), -math.inf, dtype=torch.float64).scatter_reduce_(0, inv, torch.where(ok, x, torch.full_like(x, -math.inf)), "amax")
             outs.append((s, c, mn, mx))
         return uk, rows, outs
+    if (not want_minmax and keys.dtype == torch.int64 and n >= RANGE_MIN_ROWS and nv <= PAY_MAX
+            and config.get("groupby_range")):
+        r = _small_range_agg(keys, vals, valids)
+        if r is not None:
+            return r
     dev = keys.device
     cap = _pow2(2 * (cap_hint if cap_hint else min(n, 1 << 22)) + 16)
     gkeys = torch.empty(cap, dtype=torch.int64, device=dev)

@@ -136,6 +136,29 @@ def test_range_agg_matches_host(hip_built, lo, span, nv, minmax):
     _assert_agg_equal(got, want, minmax)
 
 
+@pytest.mark.parametrize("lo,span,nv", [(0, 1000, 1), (-70, 3000, 2), (5_000_000_000, 17, 0), (3, 2000, 4)])
+def test_small_range_agg_matches_host(hip_built, lo, span, nv):
+    """Key spans of a few thousand values skip partitioning (small_range_agg_k: one direct-indexed
+    LDS table per workgroup over the whole range); NaN values and validity masks, vs the host path."""
+    n = 5_000_000
+    g = torch.Generator().manual_seed(span + nv)
+    k = torch.randint(0, span, (n,), generator=g) + lo
+    cols, valids = [], []
+    for j in range(nv):
+        if j % 2 == 0:
+            x = torch.randn(n, generator=g, dtype=torch.float64)
+            x[::89] = math.nan
+            vd = None
+        else:
+            x = torch.randint(-500, 500, (n,), generator=g, dtype=torch.int32)
+            vd = (torch.rand(n, generator=g) > 0.25).to(torch.uint8)
+        cols.append(x)
+        valids.append(vd)
+    got = D.hash_agg(k.cuda(), [c.cuda() for c in cols], [None if x is None else x.cuda() for x in valids], False)
+    want = D.hash_agg(k, cols, valids, False)
+    _assert_agg_equal(got, want, False)
+
+
 def test_range_agg_off_switch_same_result(hip_built, monkeypatch):
     k, v = D.fill_synthetic_kv(5_000_000, 50_000, "cuda")
     a = D.hash_agg_radix(k, [v], [None], False)
