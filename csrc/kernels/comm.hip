@@ -5,7 +5,7 @@
 // GPU maps every other GPU's memory directly (7 point-to-point links), so a small message is
 // reduced in ONE kernel: each rank copies its input into its own registered buffer, tells every peer
 // "block b of my data is ready" by storing the call's epoch into that peer's flag slot, waits until
-// all peers have done the same for block b, then reads block b from all world buffers over the links
+// all peers have reached at least the same call for block b, then reads block b from all world buffers over the links
 // and sums it locally.  One launch, one flag round trip, world-1 link reads per element.
 //
 // Registered buffer of each rank (hipMalloc'd once, exported with hipIpcGetMemHandle, opened by the
@@ -15,8 +15,10 @@
 //   [.. + cap, + 2*cap)        data slot 1
 // Call k writes slot k&1.  Passing call k-1's flag wait means every peer has started its call k-1
 // kernel, so (one stream per rank) its call k-2 kernel — the last reader of slot k&1 — has finished:
-// two slots and one flag round trip per call are enough, and epochs strictly increase, so a stale
-// flag never matches.
+// two slots and one flag round trip per call are enough.  Epochs strictly increase and a wait passes on
+// a flag at or past its own epoch (wrap-safe compare): a peer that has already finished call k and
+// signalled call k+1 overwrote the k signal with k+1, which still releases the call-k waiter, and it
+// cannot get to call k+2 (the next writer of this call's slot) before this rank signals k+1.
 //
 // Memory ordering: data is written with plain stores, then made visible at system scope
 // (__threadfence_system) before the signalling store-release; the waiting side uses system-scope
@@ -60,7 +62,9 @@ __global__ __launch_bounds__(256) void ipc_allreduce_k(const T* in, T* out, long
   if (tid < world) {
     const uint32_t* f = (const uint32_t*)peers.base[rank] + b * IPC_MAXW + tid;
     long long it = 0;
-    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
+    // at-or-past, wrap-safe: a fast peer may already have signalled call epoch+1 into this slot
+    // (it passed its call-epoch wait, so it has read nothing of ours that we are about to reuse)
+    while ((int)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
       if (++it > spin_limit) {
         atomicOr(err, 1);
         break;

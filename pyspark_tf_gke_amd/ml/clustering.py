@@ -126,6 +126,7 @@ class KMeans(Estimator, MLWritable, MLReadable):
                 launched += 1
             if int(state[0].item()):
                 break
+        comm.check_fast_paths()  # a timed-out one-shot all-reduce would have summed stale slots
         it = int(state[1].item())
         assign = torch.empty(n, dtype=torch.int32, device=dev)
         sums.zero_(); counts.zero_(); cost.zero_()

@@ -304,7 +304,11 @@ def _part_agg_lds(pcap: int, nv: int, minmax: bool) -> int:
     return pcap * (8 + 4 + nv * (4 + 8 * (3 if minmax else 1)))
 
 
-def estimate_distinct(keys: torch.Tensor, sample: int = 1 << 16) -> int:
+ESTIMATE_SAMPLE = 1 << 16
+ESTIMATE_SAMPLE_MAX = 1 << 20  # the widened sample stays a few MB: never a full-size hash_agg
+
+
+def estimate_distinct(keys: torch.Tensor, sample: int = ESTIMATE_SAMPLE) -> int:
     """Distinct-key estimate from a strided sample: solves d = K (1 - exp(-m/K)) for K (uniform
     key frequencies; skewed data is still handled exactly by the spill recursion)."""
     n = keys.numel()
@@ -313,10 +317,11 @@ def estimate_distinct(keys: torch.Tensor, sample: int = 1 << 16) -> int:
     s = keys[:: n // sample][:sample].contiguous()
     d = int(hash_agg(s, [], [], False)[0].numel())
     m = s.numel()
-    if d >= 0.999 * m and n >= 16 * sample:
-        # a saturated sample says only "many more keys than the sample": look again 16x wider
-        # before concluding every row is distinct (1B rows / 128M keys planned 4 radix levels and
-        # 16.7M tiny partitions from K = n: 202 ms in part_agg2_k)
+    if d >= 0.999 * m and n >= 16 * sample and sample * 16 <= ESTIMATE_SAMPLE_MAX:
+        # a saturated sample says only "many more keys than the sample": look again 16x wider, ONCE
+        # (64K -> 1M rows), before concluding every row is distinct (1B rows / 128M keys planned 4
+        # radix levels and 16.7M tiny partitions from K = n: 202 ms in part_agg2_k).  Still
+        # saturated at 1M rows means >~ 1e9 keys: K = n and hash_agg_radix's spill recursion copes.
         return estimate_distinct(keys, sample * 16)
     if d >= 0.999 * m:
         return n

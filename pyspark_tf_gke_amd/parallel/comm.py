@@ -191,6 +191,16 @@ def all_reduce_tensor_(t: torch.Tensor, op=dist.ReduceOp.SUM) -> torch.Tensor:
     return t
 
 
+def check_fast_paths() -> None:
+    """Fail loudly if a one-shot IPC all-reduce issued so far timed out (its error word is only read
+    every few calls, so a consumer calls this before it trusts the reduced values)."""
+    if not is_initialized() or dist.get_world_size() == 1:
+        return
+    from . import ipc
+
+    ipc.check_all()
+
+
 def all_gather_v(t: torch.Tensor) -> list:
     """Variable-length all-gather along dim 0 -> list of per-rank tensors (on ``t``'s device).
     One int64 all-gather of the lengths, then one all_gather_into_tensor of the padded rows."""

@@ -11,7 +11,8 @@ Setup is collective: each rank hipMallocs a registered buffer (2 data slots of `
 flag region), exports it with hipIpcGetMemHandle, all-gathers the 64-byte handles as a uint8 tensor
 and opens the peers' buffers.  Ranks must share a node (LOCAL_WORLD_SIZE == WORLD_SIZE) and issue
 their calls in the same order on one stream each.  A flag wait that exceeds its poll budget marks an
-error word instead of hanging; :meth:`check` (and every ``check_every``-th call) raises on it.
+error word instead of hanging; :meth:`check` (and every ``check_every``-th call) raises on it, and
+consumers call :func:`check_all` (via ``comm.check_fast_paths``) before they read a result.
 
 Off by default: ``PTG_IPC_ALLREDUCE=1`` routes :func:`comm.all_reduce_tensor_` calls on CUDA tensors
 of up to ``cap_bytes`` (fp32 / fp64 / int64, SUM) through it; RCCL handles everything else.
@@ -124,6 +125,14 @@ class IpcAllReduce:
             lib.ptg_ipc_close(ctypes.c_void_p(p))
         lib.ptg_ipc_free(ctypes.c_void_p(self._own))
         self._own = None
+
+
+def check_all() -> None:
+    """Raise if any live instance's flag wait timed out.  Call before reading results that went
+    through the one-shot path (the per-call check runs only every ``check_every`` calls)."""
+    for inst in list(_INSTANCES.values()):
+        if getattr(inst, "_own", None) is not None:
+            inst.check()
 
 
 def get(device=None) -> IpcAllReduce | None:

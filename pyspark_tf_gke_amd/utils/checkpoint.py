@@ -1,9 +1,9 @@
 """Checkpoint / resume.  The reference only saves the final ``model.keras``; here a
 checkpoint holds the fp32 parameters (per parameter name), the optimizer state (Adam moments / SGD velocity) and
-step, the BatchNormalization moving statistics, the epoch, and the RNG
-state, written atomically with safetensors + a JSON manifest.  Parameters/moments are identical
-on every rank for mirrored training (rank 0 writes), while the sharded parameter-server strategy
-writes one shard file per rank (its slice of the optimizer state) plus the gathered parameters.
+step, the BatchNormalization moving statistics, the epoch, and every rank's RNG state, written
+atomically with safetensors + a JSON manifest.  Parameters/moments are stored once, per parameter
+name, in the full layout (rank 0 writes them after the strategy gathered any sharded state); each
+rank writes its own RNG file.
 """
 from __future__ import annotations
 
@@ -16,16 +16,18 @@ import torch
 from ..parallel import comm
 
 
-def _ps_sharded(model) -> bool:
-    st = getattr(model, "strategy", None)
-    return st is not None and hasattr(st, "shard_range") and comm.world_size() > 1
+def _rng_file(path: str, rank: int) -> str:
+    return os.path.join(path, f"rng-{rank:05d}.safetensors")
 
 
 def save_checkpoint(model, path: str, epoch: int, extra: dict | None = None) -> str:
-    """Collective (every rank calls it).  Parameters and mirrored optimizer state are stored per
-    parameter name (``param/<name>``, ``opt_<slot>/<name>``), so a checkpoint loads into any
-    flat-buffer layout (1 GPU, or N GPUs with the sharded data-parallel update's re-laid-out store).
-    The parameter-server strategy keeps its per-rank flat optimizer shards (``opt_<slot>`` + lo/hi)."""
+    """Collective (every rank calls it).  Parameters and optimizer state are stored per parameter
+    name (``param/<name>``, ``opt_<slot>/<name>``) by rank 0, so a checkpoint loads into any
+    flat-buffer layout (1 GPU, N GPUs with the sharded data-parallel update's re-laid-out store, or
+    the parameter-server placement): strategies that shard the state (MWMS sharded update, PS owners)
+    first gather it into the full layout (``synchronize_state``).  Every rank writes its own RNG
+    state (``rng-<rank>.safetensors``) and restores its own on load, so data-parallel ranks keep
+    distinct random streams across a resume."""
     from safetensors.torch import save_file
 
     os.makedirs(path, exist_ok=True)
@@ -33,39 +35,34 @@ def save_checkpoint(model, path: str, epoch: int, extra: dict | None = None) -> 
     st = model.store
     strat = getattr(model, "strategy", None)
     if strat is not None and hasattr(strat, "synchronize_state"):
-        strat.synchronize_state(model)  # sharded update: full fp32 master + optimizer moments
+        strat.synchronize_state(model)  # sharded update / PS owners: full fp32 master + optimizer moments
     rank = comm.rank()
-    tensors = {}
-    sharded = _ps_sharded(model)
-    if rank == 0 or sharded:
-        lo, hi = model.strategy.shard_range(model) if sharded else (0, st.total)
+    rng = {"rng/cpu": torch.get_rng_state().contiguous()}
+    if torch.cuda.is_available() and st.flat.device.type == "cuda":
+        rng["rng/cuda"] = torch.cuda.get_rng_state(st.flat.device).contiguous()
+    save_file(rng, _rng_file(path, rank) + ".tmp")
+    os.replace(_rng_file(path, rank) + ".tmp", _rng_file(path, rank))
+    if rank == 0:
+        tensors = {}
         if opt is not None:
             for k, t in opt.state_tensors().items():
                 if t is None:
                     continue
-                if sharded:
-                    tensors["opt_" + k] = t[lo:hi].detach().cpu().contiguous()
-                elif rank == 0:
-                    for p in st.params:
-                        tensors[f"opt_{k}/{p.name}"] = t[p.offset:p.offset + p.numel].detach().cpu().contiguous()
-        if rank == 0:
-            for p in st.params:
-                tensors["param/" + p.name] = p.data.detach().reshape(-1).cpu().contiguous()
-            for l in model.layers:  # non-trainable BatchNormalization state
-                if getattr(l, "moving_mean", None) is not None:
-                    tensors[f"bn/{l.name}/moving_mean"] = l.moving_mean.detach().cpu().contiguous()
-                    tensors[f"bn/{l.name}/moving_variance"] = l.moving_variance.detach().cpu().contiguous()
-            tensors["rng/cpu"] = torch.get_rng_state().contiguous()
-            if torch.cuda.is_available() and st.flat.device.type == "cuda":
-                tensors["rng/cuda"] = torch.cuda.get_rng_state(st.flat.device).contiguous()
-        tmp = os.path.join(path, f"shard-{rank:05d}.safetensors.tmp")
-        save_file(tensors, tmp, metadata={"lo": str(lo), "hi": str(hi)})
-        os.replace(tmp, os.path.join(path, f"shard-{rank:05d}.safetensors"))
+                for p in st.params:
+                    tensors[f"opt_{k}/{p.name}"] = t[p.offset:p.offset + p.numel].detach().cpu().contiguous()
+        for p in st.params:
+            tensors["param/" + p.name] = p.data.detach().reshape(-1).cpu().contiguous()
+        for l in model.layers:  # non-trainable BatchNormalization state
+            if getattr(l, "moving_mean", None) is not None:
+                tensors[f"bn/{l.name}/moving_mean"] = l.moving_mean.detach().cpu().contiguous()
+                tensors[f"bn/{l.name}/moving_variance"] = l.moving_variance.detach().cpu().contiguous()
+        tmp = os.path.join(path, "shard-00000.safetensors.tmp")
+        save_file(tensors, tmp)
+        os.replace(tmp, os.path.join(path, "shard-00000.safetensors"))
     comm.barrier()
     if rank == 0:
         manifest = {"epoch": epoch, "step": opt.iterations if opt else 0, "world_size": comm.world_size(),
-                    "sharded": sharded, "layout": "ps-flat" if sharded else "per-param",
-                    "total": int(st.total), "time": time.time(),
+                    "sharded": False, "layout": "per-param", "total": int(st.total), "time": time.time(),
                     **(extra or {})}
         with open(os.path.join(path, "manifest.json.tmp"), "w") as fh:
             json.dump(manifest, fh)
@@ -79,15 +76,13 @@ def load_checkpoint(model, path: str) -> dict:
 
     with open(os.path.join(path, "manifest.json")) as fh:
         manifest = json.load(fh)
+    if manifest.get("sharded") or manifest.get("layout", "per-param") != "per-param":
+        # round-1/2 parameter-server checkpoints stored flat [lo:hi] optimizer slices per rank; every
+        # checkpoint is now written per parameter name
+        raise ValueError(f"checkpoint {path}: layout {manifest.get('layout')!r} (flat per-rank optimizer "
+                         "shards) is no longer readable; checkpoints are stored per parameter name")
     strat = getattr(model, "strategy", None)
     st = model.store
-    if manifest["sharded"] and (int(manifest.get("total", -1)) != int(st.total)
-                                or int(manifest["world_size"]) != comm.world_size()
-                                or not _ps_sharded(model)):
-        # flat [lo:hi] optimizer slices only mean something in the layout that wrote them
-        raise ValueError(f"checkpoint {path}: parameter-server optimizer shards were written for "
-                         f"world {manifest['world_size']} / flat size {manifest.get('total')}; this model "
-                         f"has world {comm.world_size()} / flat size {st.total} (load it with the same layout)")
     if strat is not None and hasattr(strat, "wait_parameters"):
         strat.wait_parameters(model)  # no parameter gather still in flight may land on the loaded values
     opt = model.optimizer
@@ -101,27 +96,23 @@ def load_checkpoint(model, path: str) -> dict:
             if key not in keys:
                 raise KeyError(f"checkpoint {path} has no parameter {p.name!r}")
             p.data.copy_(f.get_tensor(key).to(st.flat.device).view(p.shape))
-            if not manifest["sharded"]:
-                for k, t in state.items():
-                    if t is not None and f"opt_{k}/{p.name}" in keys:
-                        t[p.offset:p.offset + p.numel].copy_(f.get_tensor(f"opt_{k}/{p.name}").to(t.device))
+            for k, t in state.items():
+                if t is not None and f"opt_{k}/{p.name}" in keys:
+                    t[p.offset:p.offset + p.numel].copy_(f.get_tensor(f"opt_{k}/{p.name}").to(t.device))
         for l in model.layers:
             if getattr(l, "moving_mean", None) is not None and f"bn/{l.name}/moving_mean" in keys:
                 l.moving_mean.copy_(f.get_tensor(f"bn/{l.name}/moving_mean").to(l.moving_mean.device))
                 l.moving_variance.copy_(f.get_tensor(f"bn/{l.name}/moving_variance").to(l.moving_variance.device))
-        if "rng/cpu" in keys:
-            torch.set_rng_state(f.get_tensor("rng/cpu"))
-        if "rng/cuda" in keys and st.flat.device.type == "cuda":
-            torch.cuda.set_rng_state(f.get_tensor("rng/cuda"), st.flat.device)
-    if manifest["sharded"] and opt is not None:
-        for r in range(manifest["world_size"]):
-            fn = os.path.join(path, f"shard-{r:05d}.safetensors")
-            with safe_open(fn, "pt") as f:
-                md = f.metadata()
-                lo, hi = int(md["lo"]), int(md["hi"])
-                for k, t in state.items():
-                    if t is not None and "opt_" + k in f.keys():
-                        t[lo:hi].copy_(f.get_tensor("opt_" + k).to(t.device))
+        legacy_rng = {k: f.get_tensor(k) for k in ("rng/cpu", "rng/cuda") if k in keys}
+    rank = comm.rank()
+    rng = legacy_rng
+    if os.path.exists(_rng_file(path, rank)):
+        with safe_open(_rng_file(path, rank), "pt") as f:
+            rng = {k: f.get_tensor(k) for k in f.keys()}
+    if "rng/cpu" in rng:
+        torch.set_rng_state(rng["rng/cpu"])
+    if "rng/cuda" in rng and st.flat.device.type == "cuda":
+        torch.cuda.set_rng_state(rng["rng/cuda"], st.flat.device)
     if opt is not None:
         opt.set_iterations(int(manifest["step"]))
     st.refresh_bf16()

@@ -1,5 +1,5 @@
-"""Single-process checkpoint details: RNG state round-trips, and parameter-server flat optimizer shards
-refuse to load into a layout they were not written for (a silent scramble otherwise)."""
+"""Checkpoint details: RNG state round-trips per rank, and the retired flat per-rank optimizer-shard
+layout is refused with a clear error instead of loading scrambled."""
 import json
 import os
 
@@ -39,5 +39,41 @@ def test_ps_flat_shards_refuse_other_layout(tmp_path):
     man.update(sharded=True, layout="ps-flat", world_size=2)
     with open(mf, "w") as fh:
         json.dump(man, fh)
-    with pytest.raises(ValueError, match="parameter-server optimizer shards"):
+    with pytest.raises(ValueError, match="no longer readable"):
         C.load_checkpoint(_model(), d)
+
+
+def test_each_rank_restores_its_own_rng(tmp_path):
+    """Two gloo ranks seed different RNG streams, checkpoint, scramble, resume: each gets its own
+    stream back (rank 0's state used to be restored on every rank)."""
+    import subprocess
+    import sys
+    import textwrap
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    body = f"""
+    import json, torch
+    from pyspark_tf_gke_amd.distribute import MultiWorkerMirroredStrategy
+    from pyspark_tf_gke_amd.models import build_deep_model
+    from pyspark_tf_gke_amd.utils import checkpoint as C
+    st = MultiWorkerMirroredStrategy()
+    with st.scope():
+        m = build_deep_model(3, 5, device="cpu")
+    torch.manual_seed(100 + st.rank)
+    C.save_checkpoint(m, {str(tmp_path / "ck")!r}, 0)
+    want = torch.rand(3).tolist()
+    torch.manual_seed(7)
+    C.load_checkpoint(m, {str(tmp_path / "ck")!r})
+    print("RESULT", json.dumps({{"rank": st.rank, "want": want, "got": torch.rand(3).tolist()}}), flush=True)
+    """
+    env = dict(os.environ, PYTHONPATH=root, PTG_DEVICE="cpu", PTG_HOST_FP32="1")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, "-m", "pyspark_tf_gke_amd.runtime.launcher", "--nproc", "2", "--",
+                        sys.executable, "-c", textwrap.dedent(body)], env=env, capture_output=True, text=True,
+                       timeout=240, cwd=root)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    res = [json.loads(l.split("RESULT ", 1)[1]) for l in r.stdout.splitlines() if "RESULT " in l]
+    assert len(res) == 2
+    for v in res:
+        assert v["got"] == v["want"], v
+    assert res[0]["want"] != res[1]["want"]

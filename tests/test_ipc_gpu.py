@@ -57,8 +57,38 @@ for _ in range(50):
 torch.cuda.synchronize()
 ar.check()
 ones = bool(torch.allclose(y.cpu(), torch.ones(4096)))
+# a deliberately slow rank: the last rank sleeps on the host before every call, so the fast ranks
+# run ahead into the next call and overwrite their flag slots with epoch+1 while it still waits on
+# epoch (the at-or-past flag compare must release it)
+import time
+z = torch.full((20000,), float(r + 1), device=dev)
+want = float(sum(q + 1 for q in range(w)))
+slow_ok = True
+for i in range(20):
+    if r == w - 1:
+        torch.cuda.synchronize()
+        time.sleep(0.004)
+    z.fill_(float(r + 1))
+    ar.all_reduce_(z)
+    slow_ok = slow_ok and bool((z == want).all().item())
+torch.cuda.synchronize()
+ar.check()
 ar.close()
-print("RESULT", json.dumps({"worst": worst, "exact": exact, "ones": ones, "epochs": ar.epoch}), flush=True)
+# a peer that never arrives: rank 0 issues one call alone on a fresh instance with a tiny poll budget;
+# the kernel must drain and check() must raise instead of returning stale sums
+lone = ipc.IpcAllReduce(dev, cap_bytes=1 << 16, spin_limit=2000)
+raised = None
+if r == 0:
+    lone.all_reduce_(torch.ones(64, device=dev))
+    torch.cuda.synchronize()
+    try:
+        lone.check()
+        raised = False
+    except RuntimeError:
+        raised = True
+lone.close()
+print("RESULT", json.dumps({"worst": worst, "exact": exact, "ones": ones, "epochs": ar.epoch,
+                            "slow_ok": slow_ok, "raised": raised}), flush=True)
 """
 
 
@@ -76,4 +106,6 @@ def test_ipc_allreduce_matches_sum(nproc):
     assert len(res) == nproc, r.stdout[-2000:]
     for v in res:
         assert v["exact"] and v["ones"] and v["worst"] < 1e-6, v
-        assert v["epochs"] == 21 + 50, v
+        assert v["epochs"] == 21 + 50 + 20, v
+        assert v["slow_ok"], v
+    assert res[0]["raised"] is True or any(v["raised"] is True for v in res), res

@@ -275,3 +275,29 @@ def test_config_precedence(monkeypatch):
         monkeypatch.setenv("PTG_GROUPBY_RANGE", raw)
         assert config.get("groupby_range") is want
     assert {r["name"] for r in config.describe()} >= {"fused_adam", "shuffle_buffer_gb", "pg_timeout_s"}
+
+
+def test_distinct_estimate_widens_at_most_to_the_cap(monkeypatch):
+    """All-unique keys saturate every sample: the estimate widens once (bounded sample), then
+    returns n instead of hashing ever larger samples (64K -> 1M -> 16M -> 256M)."""
+    import torch
+
+    from pyspark_tf_gke_amd.ops import df as D
+
+    seen = []
+    real = D.hash_agg
+
+    def spy(keys, *a, **kw):
+        seen.append(keys.numel())
+        return real(keys, *a, **kw)
+
+    monkeypatch.setattr(D, "hash_agg", spy)
+    monkeypatch.setattr(D, "ESTIMATE_SAMPLE_MAX", 1 << 14)
+    keys = torch.arange(1 << 20, dtype=torch.int64) * 7919
+    assert D.estimate_distinct(keys, sample=1 << 10) == keys.numel()
+    assert max(seen) <= 1 << 14 and len(seen) == 2, seen
+    # a genuinely small key set is still estimated from the first sample
+    seen.clear()
+    small = torch.randint(0, 300, (1 << 20,), generator=torch.Generator().manual_seed(0))
+    assert 250 <= D.estimate_distinct(small, sample=1 << 10) <= 400
+    assert len(seen) == 1
