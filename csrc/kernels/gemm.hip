@@ -746,10 +746,35 @@ static int launch_gemm(const LA& la, const LB& lb, const EPI& epi, int M, int N,
   PTG_RETURN_LAUNCH();
 }
 
+// Skinny-M, wide-N GEMMs (the Dense layers' dX: M = batch <= 256, N = 20480, K = 2048): one 256-row
+// tile covers all of M, so every column panel of B is streamed from HBM exactly once (the 128x128
+// tiling read the 84 MB weight twice), and BN is picked so the grid is ~one workgroup per CU
+// (N = 20480: 256 x 80 tiles = 256 workgroups).  PTG_SKINNY_BN=0 disables it, =64/80 forces a width.
+static int g_skinny_bn = -2;
+int skinny_bn_choice(int M, int N) {
+  if (g_skinny_bn == -2) {
+    const char* e = getenv("PTG_SKINNY_BN");
+    g_skinny_bn = e ? atoi(e) : -1;
+  }
+  if (g_skinny_bn == 0 || M <= 128 || M > 256) return 0;
+  if (g_skinny_bn > 0) return g_skinny_bn;
+  const int cands[2] = {80, 64};
+  for (int bn : cands)
+    if (N % bn == 0 && N / bn >= 192 && N / bn <= 320) return bn;
+  return N >= 64 * 192 ? 64 : 0;
+}
+
 // Tile-shape choice. N is the narrow dimension for convolutions (output channels).
 template <class LA, class LB, class EPI>
 static int dispatch_gemm(const LA& la, const LB& lb, const EPI& epi, int M, int N, int K, int splits,
                          hipStream_t s) {
+  if (splits == 1 && N >= 4096) {
+    switch (skinny_bn_choice(M, N)) {
+      case 64: return launch_gemm<256, 64, 4, 1>(la, lb, epi, M, N, K, 1, s);
+      case 80: return launch_gemm<256, 80, 4, 1>(la, lb, epi, M, N, K, 1, s);
+      default: break;
+    }
+  }
   if constexpr (HasOff<LA>::value && HasOff<LB>::value && EpiPre<EPI>::v == 0) {
     // big problems: >= one 256x256 tile per CU and K deep enough to amortise the 2-stage ring
     if (gemm256_enabled() && N >= 256 && M >= 256 && K >= 256 &&
@@ -793,6 +818,12 @@ extern "C" {
 
 int ptg_gemm256_set(int on) {
   g_gemm256 = on ? 1 : 0;
+  return 0;
+}
+
+// A/B switch for the skinny-M tiles: 0 = off, -1 = automatic, 64 / 80 = forced tile width
+int ptg_gemm_skinny_set(int bn) {
+  g_skinny_bn = bn;
   return 0;
 }
 

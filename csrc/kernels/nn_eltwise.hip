@@ -846,14 +846,18 @@ __global__ void adam_step_k(float* st, float lr, float b1, float b2) {
   }
 }
 
-__global__ __launch_bounds__(256) void adam_k(float* __restrict__ p, const float* __restrict__ g,
+// clear: the gradient is consumed here, so store zeros back (4 B/parameter, no separate fill pass
+// before the next backward: the store skips its per-step zero_grad after a clearing update)
+__global__ __launch_bounds__(256) void adam_k(float* __restrict__ p, float* __restrict__ g,
                                               float* __restrict__ m, float* __restrict__ v,
                                               bf16_t* __restrict__ pbf, long n4, float lr_t, float b1,
-                                              float b2, float eps, float gscale, const float* __restrict__ lr_dev) {
+                                              float b2, float eps, float gscale, const float* __restrict__ lr_dev,
+                                              int clear) {
   if (lr_dev) lr_t = lr_dev[1];
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
     float4 pp = ((float4*)p)[i];
     const float4 gg = ((const float4*)g)[i];
+    if (clear) ((float4*)g)[i] = float4{0.f, 0.f, 0.f, 0.f};
     float4 mm = ((float4*)m)[i], vv = ((float4*)v)[i];
     float* P = &pp.x; const float* G = &gg.x; float* Mm = &mm.x; float* V = &vv.x;
 #pragma unroll
@@ -873,12 +877,13 @@ __global__ __launch_bounds__(256) void adam_k(float* __restrict__ p, const float
 
 // Fused flat SGD (+momentum, optional Nesterov), Keras convention:
 //   v = momentum*v - lr*g ; p += v            (nesterov: p += momentum*v - lr*g)
-__global__ __launch_bounds__(256) void sgd_k(float* __restrict__ p, const float* __restrict__ g,
+__global__ __launch_bounds__(256) void sgd_k(float* __restrict__ p, float* __restrict__ g,
                                              float* __restrict__ vel, bf16_t* __restrict__ pbf, long n4, float lr,
-                                             float momentum, int nesterov, float gscale) {
+                                             float momentum, int nesterov, float gscale, int clear) {
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
     float4 pp = ((float4*)p)[i];
     const float4 gg = ((const float4*)g)[i];
+    if (clear) ((float4*)g)[i] = float4{0.f, 0.f, 0.f, 0.f};
     float4 vv = vel ? ((float4*)vel)[i] : float4{0.f, 0.f, 0.f, 0.f};
     float* P = &pp.x; const float* G = &gg.x; float* V = &vv.x;
 #pragma unroll
@@ -1242,12 +1247,12 @@ int ptg_softmax_xent(const float* logits, const int* labels, float* dlogits, flo
   PTG_RETURN_LAUNCH();
 }
 
-int ptg_adam(float* p, const float* g, float* m, float* v, void* pbf, long n, float lr_t, float b1, float b2,
-             float eps, float gscale, const float* lr_dev, hipStream_t s) {
+int ptg_adam(float* p, float* g, float* m, float* v, void* pbf, long n, float lr_t, float b1, float b2,
+             float eps, float gscale, const float* lr_dev, int clear, hipStream_t s) {
   if (n % 4) return (int)hipErrorInvalidValue;
   const long n4 = n / 4;
   hipLaunchKernelGGL(adam_k, dim3(grid_for(n4)), dim3(256), 0, s, p, g, m, v, (bf16_t*)pbf, n4, lr_t, b1, b2,
-                     eps, gscale, lr_dev);
+                     eps, gscale, lr_dev, clear);
   PTG_RETURN_LAUNCH();
 }
 
@@ -1256,12 +1261,12 @@ int ptg_adam_step(float* st, float lr, float b1, float b2, hipStream_t s) {
   PTG_RETURN_LAUNCH();
 }
 
-int ptg_sgd(float* p, const float* g, float* vel, void* pbf, long n, float lr, float momentum, int nesterov,
-            float gscale, hipStream_t s) {
+int ptg_sgd(float* p, float* g, float* vel, void* pbf, long n, float lr, float momentum, int nesterov,
+            float gscale, int clear, hipStream_t s) {
   if (n % 4) return (int)hipErrorInvalidValue;
   const long n4 = n / 4;
   hipLaunchKernelGGL(sgd_k, dim3(grid_for(n4)), dim3(256), 0, s, p, g, vel, (bf16_t*)pbf, n4, lr, momentum,
-                     nesterov, gscale);
+                     nesterov, gscale, clear);
   PTG_RETURN_LAUNCH();
 }
 

@@ -80,7 +80,9 @@ class Adam(Optimizer):
         if hi > lo:
             sl = slice(lo, hi)
             K.adam(store.flat[sl], store.flat_grad[sl], self.m[sl], self.v[sl], store.flat_bf16[sl],
-                   self.lr_t(step), self.beta_1, self.beta_2, self.epsilon, gscale, lr_dev=ds)
+                   self.lr_t(step), self.beta_1, self.beta_2, self.epsilon, gscale, lr_dev=ds, clear_grad=True)
+        if lo == 0 and hi >= store.total:
+            store.grad_clean = True  # the update consumed and zeroed every gradient
         if advance:
             self.iterations = step
 
@@ -110,6 +112,8 @@ class Adam(Optimizer):
             if a > lo:
                 self.apply(ctx.store, lo=lo, hi=a, advance=False)
             lo = max(lo, b)
+        # the gaps were cleared by their updates; the fused producers' ranges were never written
+        ctx.store.grad_clean = True
         self.iterations = ctx.step
 
     def get_config(self):
@@ -160,7 +164,9 @@ class SGD(Optimizer):
         if hi > lo:
             sl = slice(lo, hi)
             K.sgd(store.flat[sl], store.flat_grad[sl], self.velocity[sl] if self.velocity is not None else None,
-                  store.flat_bf16[sl], self.learning_rate, self.momentum, self.nesterov, gscale)
+                  store.flat_bf16[sl], self.learning_rate, self.momentum, self.nesterov, gscale, clear_grad=True)
+        if lo == 0 and hi >= store.total:
+            store.grad_clean = True
         if advance:
             self.iterations += 1
 

@@ -159,6 +159,12 @@ class ParamStore:
             p.bf16 = self.flat_bf16[sl].view(p.shape)
 
     def zero_grad(self) -> None:
+        """Zero every accumulated gradient before a backward.  Skipped when the last optimizer
+        update consumed the whole gradient buffer and stored zeros back (``grad_clean``, set by the
+        clearing Adam/SGD kernels): the per-step fill pass then disappears from the step."""
+        if getattr(self, "grad_clean", False):
+            self.grad_clean = False
+            return
         for lo, hi in self._zero_ranges:
             self.flat_grad[lo:hi].zero_()
 

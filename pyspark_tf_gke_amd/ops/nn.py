@@ -278,9 +278,9 @@ def linear_fwd(x, w, bias, act, out, workspace=None, splits: int = 0):
     return out
 
 
-# A plain GEMM with nothing to fuse goes to the vendor library when it measured faster: the big
-# Dense layer's dX (M = batch 256, N = 20480, K = 2048) is 34 us in hipBLASLt vs 45 us in gemm_kernel
-# (tools/dense_gemm_bench.py).  PTG_BLASLT_DX=0 keeps it on gemm_kernel.
+# The big Dense layer's dX (M = batch 256, N = 20480, K = 2048) runs on gemm_kernel's skinny-M tiles
+# (256 x 80: the 84 MB weight streamed once, one workgroup per CU); PTG_BLASLT_DX=1 routes it to
+# hipBLASLt for A/B runs only (tools/dense_gemm_bench.py).
 BLASLT_DX = config.get("blaslt_dx")
 
 
@@ -482,15 +482,20 @@ def softmax_xent(logits, labels, dlogits, stats, gscale: float = 1.0):
     hip("ptg_softmax_xent", ptr(logits), ptr(labels), ptr(dlogits), ptr(stats), B, C, float(gscale))
 
 
-def adam(p, g, m, v, pbf, lr_t: float, b1: float, b2: float, eps: float, gscale: float = 1.0, lr_dev=None):
+def adam(p, g, m, v, pbf, lr_t: float, b1: float, b2: float, eps: float, gscale: float = 1.0, lr_dev=None,
+         clear_grad: bool = False):
     """Fused Adam; with ``lr_dev`` (the device step state of :func:`adam_step`) the step size is read
-    on the device, so the launch can be captured once into a HIP graph and replayed every step."""
+    on the device, so the launch can be captured once into a HIP graph and replayed every step.
+    ``clear_grad``: store zeros into ``g`` after reading it (replaces the next step's zero fill)."""
     if not on_device(p):
         if lr_dev is not None:
             lr_t = float(lr_dev[1])
-        return ref.adam(p, g, m, v, pbf, lr_t, b1, b2, eps, gscale)
+        ref.adam(p, g, m, v, pbf, lr_t, b1, b2, eps, gscale)
+        if clear_grad:
+            g.zero_()
+        return
     hip("ptg_adam", ptr(p), ptr(g), ptr(m), ptr(v), ptr(pbf), p.numel(), float(lr_t), float(b1), float(b2),
-        float(eps), float(gscale), ptr(lr_dev))
+        float(eps), float(gscale), ptr(lr_dev), int(clear_grad))
 
 
 def adam_step(state, lr: float, b1: float, b2: float):
@@ -504,8 +509,9 @@ def adam_step(state, lr: float, b1: float, b2: float):
     return state
 
 
-def sgd(p, g, vel, pbf, lr: float, momentum: float, nesterov: bool, gscale: float = 1.0):
-    """Keras SGD: v = momentum*v - lr*g; p += v (Nesterov: p += momentum*v - lr*g); refreshes pbf."""
+def sgd(p, g, vel, pbf, lr: float, momentum: float, nesterov: bool, gscale: float = 1.0, clear_grad: bool = False):
+    """Keras SGD: v = momentum*v - lr*g; p += v (Nesterov: p += momentum*v - lr*g); refreshes pbf.
+    ``clear_grad`` as in :func:`adam`."""
     if not on_device(p):
         gg = g * gscale
         if vel is not None:
@@ -515,9 +521,11 @@ def sgd(p, g, vel, pbf, lr: float, momentum: float, nesterov: bool, gscale: floa
             p.sub_(lr * gg)
         if pbf is not None:
             pbf.copy_(p.to(pbf.dtype))
+        if clear_grad:
+            g.zero_()
         return
     hip("ptg_sgd", ptr(p), ptr(g), ptr(vel), ptr(pbf), p.numel(), float(lr), float(momentum), int(nesterov),
-        float(gscale))
+        float(gscale), int(clear_grad))
 
 
 def cast_f32_bf16(x, out):

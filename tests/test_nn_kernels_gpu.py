@@ -53,23 +53,42 @@ def test_gemm_splitk_atomic_and_bias_relu():
     _close(out, ref, 2e-2, 2e-2, "linear_fwd")
 
 
-@pytest.mark.parametrize("blaslt", [False, True])
-def test_linear_dx_dw(blaslt):
-    """dX on gemm_kernel and, for the CNN-B1 shape class (M <= 512, K >= 8192), on hipBLASLt."""
-    M, N, Kd = (128, 2048, 20480 // 8) if not blaslt else (256, 2048, 20480)
+@pytest.mark.parametrize("M,N,Kd,bn", [(128, 2048, 20480 // 8, -1), (256, 2048, 20480, -1), (256, 2048, 20480, 64),
+                                       (200, 512, 64 * 200, -1), (256, 2048, 20480, 0)])
+def test_linear_dx_dw(M, N, Kd, bn):
+    """dX on gemm_kernel: the CNN-B1 shape (M = 256, K = 20480) on the skinny-M 256x80 tiles (bn -1),
+    forced 256x64 tiles, a ragged M with 256x64, and the 128x128 tiling (bn 0); never hipBLASLt."""
+    from pyspark_tf_gke_amd import _native
+
     dy, w, x = rnd(M, N), rnd(N, Kd), rnd(M, Kd)
     dx = torch.empty(M, Kd, device=DEV, dtype=torch.bfloat16)
-    K.linear_dx(dy.to(DEV), w.to(DEV), dx)
+    assert not K.BLASLT_DX
+    _native.hip_lib().ptg_gemm_skinny_set(bn)
+    try:
+        K.linear_dx(dy.to(DEV), w.to(DEV), dx)
+    finally:
+        _native.hip_lib().ptg_gemm_skinny_set(-1)
     _close(dx, dy.float() @ w.float(), 2e-2, 2e-2, "dx")
-    if blaslt:
-        K.BLASLT_DX = False  # the same shape on gemm_kernel agrees too
-        dx2 = torch.empty_like(dx)
-        K.linear_dx(dy.to(DEV), w.to(DEV), dx2)
-        K.BLASLT_DX = True
-        _close(dx2, dy.float() @ w.float(), 2e-2, 2e-2, "dx gemm_kernel")
     dw = torch.empty(N, Kd, device=DEV)
     K.linear_dw(dy.to(DEV), x.to(DEV), dw)
     _close(dw, dy.float().t() @ x.float(), 1e-3, 1e-3, "dw")
+
+
+def test_adam_sgd_clear_grad():
+    """clear_grad: same update, and the gradient buffer holds zeros afterwards."""
+    n = 8192
+    p, g, m, v = torch.randn(n), torch.randn(n), torch.randn(n).abs() * 0.1, torch.rand(n) * 0.1
+    P, G, Mm, V = (t.clone().to(DEV) for t in (p, g, m, v))
+    K.adam(P, G, Mm, V, None, 1e-3, 0.9, 0.999, 1e-7, 1.0, clear_grad=True)
+    R.adam(p, g, m, v, None, 1e-3, 0.9, 0.999, 1e-7, 1.0)
+    _close(P, p, 1e-6, 1e-6, "adam_p")
+    assert not G.any()
+    p, g, vel = torch.randn(n), torch.randn(n), torch.randn(n)
+    P, G, VE = p.clone().to(DEV), g.clone().to(DEV), vel.clone().to(DEV)
+    K.sgd(P, G, VE, None, 0.1, 0.9, False, 1.0, clear_grad=True)
+    vel = 0.9 * vel - 0.1 * g
+    _close(P, p + vel, 1e-6, 1e-6, "sgd_p")
+    assert not G.any()
 
 
 CONV_CASES = [(2, 16, 20, 4, 8, 5), (2, 16, 20, 8, 16, 5), (2, 12, 10, 16, 32, 5), (3, 8, 10, 32, 64, 5),

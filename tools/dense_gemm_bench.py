@@ -46,13 +46,24 @@ def main():
     res = {}
     for s in (0, 1, 4, 8, 16, 20, 25, 32, 40):
         res[f"fwd_splits{s}"] = timeit(lambda: K.linear_fwd(x, w, b, "relu", y, workspace=wsp, splits=s))
+    from pyspark_tf_gke_amd import _native
+
+    lib = _native.hip_lib()
+    K.BLASLT_DX = False
+    for bn in (-1, 0, 64, 80):
+        lib.ptg_gemm_skinny_set(bn)
+        res[f"dx_skinny{bn}"] = timeit(lambda: K.linear_dx(dy, w, dx))
+        if bn == -1:
+            ref = torch.matmul(dy.float(), w.float())
+            res["dx_maxrel"] = float(((dx.float() - ref).abs().max() / ref.abs().max()).item())
+    lib.ptg_gemm_skinny_set(-1)
     res["dx"] = timeit(lambda: K.linear_dx(dy, w, dx))
     res["dw"] = timeit(lambda: K.linear_dw(dy, x, g))
     res["dw_adam"] = timeit(lambda: K.linear_dw_adam(dy, x, p, m, v, pb, 1e-3, 0.9, 0.999, 1e-7))
     res["torch_fwd"] = timeit(lambda: torch.matmul(x, w.t()))
     res["torch_dx"] = timeit(lambda: torch.matmul(dy, w))
     res["torch_dw"] = timeit(lambda: torch.matmul(dy.t(), x))
-    print(json.dumps({k: round(v_, 1) for k, v_ in res.items()}))
+    print(json.dumps({k: (round(v_, 1) if v_ > 0.01 else v_) for k, v_ in res.items()}))
 
 
 if __name__ == "__main__":
