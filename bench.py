@@ -47,6 +47,10 @@ def parse(argv=None):
                          "report it under extra.groupby (1B rows per GPU)")
     ap.add_argument("--extra-batches", default=os.environ.get("PTG_BENCH_EXTRA_BATCHES", "32,64"),
                     help="cnn_b1: also time these per-GPU batches (the reference's 32 and 64) into extra")
+    ap.add_argument("--sim-world", type=int, default=int(os.environ.get("PTG_BENCH_SIM_WORLD", "8")),
+                    help="cnn_b1 on 1 GPU: also time rank 0's kernel sequence of an N-rank sharded data-parallel "
+                         "step (PTG_SIM_WORLD: collectives replaced by local kernels of the same HBM bytes) into "
+                         "extra.sim_world<N>; 0 = off")
     ap.add_argument("--seed", type=int, default=1234)
     return ap.parse_args(argv)
 
@@ -245,6 +249,24 @@ def main():
                 r2 = bench_train(a2, strategy, rank, world)
                 extra[f"batch{b}"] = {"value": r2["value"], "unit": "samples/s", "ms_per_step": r2["ms_per_step"],
                                       "per_gpu_batch": b, "global_batch": b * world}
+        if args.workload == "cnn_b1" and args.sim_world > 1 and world == 1 and torch.cuda.is_available():
+            # the N>1 compute path on one GPU: dW into flat_grad, per-bucket reduce-scatter stand-in,
+            # shard Adam, all-gather stand-in + bf16 re-cast (MultiWorkerMirroredStrategy sim mode)
+            from pyspark_tf_gke_amd import config as _cfg
+
+            _cfg.set_cli("sim_world", args.sim_world)
+            try:
+                sst = MultiWorkerMirroredStrategy()
+                a2 = argparse.Namespace(**vars(args))
+                r2 = bench_train(a2, sst, rank, world)
+                extra[f"sim_world{args.sim_world}"] = {
+                    "ms_per_step": r2["ms_per_step"], "value": r2["value"], "unit": "samples/s",
+                    "per_gpu_batch": r2["config"]["per_gpu_batch"],
+                    "vs_n1_step": round(r2["ms_per_step"] / res["ms_per_step"], 4),
+                    "note": "rank 0's kernels of a dp%d sharded step on 1 GPU, collectives replaced by local "
+                            "kernels moving the same local bytes (no xGMI time)" % args.sim_world}
+            finally:
+                _cfg._cli.pop("sim_world", None)
         if args.workload == "cnn_b1" and args.groupby_extra and torch.cuda.is_available():
             # second half of BASELINE.json's metric ("rows/sec Spark groupBy + samples/sec TF CNN
             # train"); timed separately, after the CNN steps, so it cannot perturb them

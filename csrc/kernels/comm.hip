@@ -80,9 +80,139 @@ __global__ __launch_bounds__(256) void ipc_allreduce_k(const T* in, T* out, long
   }
 }
 
+// ---- collective stand-ins of the simulated-world mode (distribute/strategy.py, PTG_SIM_WORLD=N):
+// one rank runs rank 0's kernel sequence of an N-rank sharded update with its collectives replaced
+// by local kernels that move the same local HBM bytes.  Reduce-scatter: read every chunk of the
+// bucket (a ring sends N-1 of them), write the owned shard = own_scale * chunk 0 (+ w_peer * the other
+// chunks, 0 for "N ranks with identical data": their chunk-0 partials equal ours).
+__global__ __launch_bounds__(256) void sim_rs_k(const float4* __restrict__ g, float4* __restrict__ out, long cnt4,
+                                                int nchunks, float own_scale, float w_peer) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < cnt4; i += (long)gridDim.x * 256) {
+    float4 a = g[i], p = float4{0.f, 0.f, 0.f, 0.f};
+    for (int r = 1; r < nchunks; ++r) {
+      const float4 b = g[(long)r * cnt4 + i];
+      p.x += b.x; p.y += b.y; p.z += b.z; p.w += b.w;
+    }
+    out[i] = float4{own_scale * a.x + w_peer * p.x, own_scale * a.y + w_peer * p.y, own_scale * a.z + w_peer * p.z,
+                    own_scale * a.w + w_peer * p.w};
+  }
+}
+
+// All-gather: the N-1 peer chunks of a bucket land in local HBM; here they are rewritten in place
+// (read + write of (N-1)/N of the bucket: the received bytes, plus a read the real gather does not do)
+__global__ __launch_bounds__(256) void sim_ag_k(uint4* __restrict__ buf, long lo4, long hi4, uint32_t mask) {
+  for (long i = lo4 + blockIdx.x * 256L + threadIdx.x; i < hi4; i += (long)gridDim.x * 256) {
+    uint4 v = buf[i];
+    v.x ^= mask; v.y ^= mask; v.z ^= mask; v.w ^= mask;
+    buf[i] = v;
+  }
+}
+
+// ---- parameter-server piece copies (distribute/strategy.py _PSPlan): a model's variables are cut
+// into pieces placed on PS owners; push / pull move every piece between the flat parameter store and
+// the owners' packed segments.  ONE launch moves all pieces of a step (the pieces are pre-split into
+// chunks of <= 64K elements on the host, one workgroup per chunk), converting fp32 <-> bf16 on the
+// way; a base may be a peer's IPC-mapped window (reads / writes over xGMI).
+struct PieceBases {
+  char* base[IPC_MAXW];
+};
+
+// sys: the source is memory another agent writes (a peer's window, or this rank's window written by
+// peers): element loads are system-scope, so no line a cache kept from an earlier read is returned
+// (hipMalloc memory is coarse-grained; only the scope of the access makes a peer's write visible)
+template <typename T>
+PTG_DEV T ld_sys(const T* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// table: 5 longs per chunk = src base index, src element offset, dst base index, dst element offset, n
+template <bool SYS>
+__global__ __launch_bounds__(256) void piece_copy_k(PieceBases src, int src_bf, PieceBases dst, int dst_bf,
+                                                    const long* __restrict__ table, int nchunks) {
+  for (int c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    const long* e = table + 5L * c;
+    const char* sb = src.base[e[0]];
+    char* db = dst.base[e[2]];
+    const long so = e[1], dof = e[3], n = e[4];
+    if (src_bf == dst_bf && !src_bf) {
+      const uint32_t* sp = (const uint32_t*)sb + so;
+      for (long i = threadIdx.x; i < n; i += 256) ((uint32_t*)db)[dof + i] = SYS ? ld_sys(sp + i) : sp[i];
+    } else if (src_bf == dst_bf) {
+      const uint16_t* sp = (const uint16_t*)sb + so;
+      for (long i = threadIdx.x; i < n; i += 256) ((uint16_t*)db)[dof + i] = SYS ? ld_sys(sp + i) : sp[i];
+    } else if (src_bf) {  // bf16 -> fp32
+      const uint16_t* sp = (const uint16_t*)sb + so;
+      for (long i = threadIdx.x; i < n; i += 256) {
+        const uint16_t u = SYS ? ld_sys(sp + i) : sp[i];
+        ((float*)db)[dof + i] = __uint_as_float((uint32_t)u << 16);
+      }
+    } else {  // fp32 -> bf16
+      const uint32_t* sp = (const uint32_t*)sb + so;
+      for (long i = threadIdx.x; i < n; i += 256) {
+        const uint32_t u = SYS ? ld_sys(sp + i) : sp[i];
+        ((uint16_t*)db)[dof + i] = (uint16_t)f2bf(__uint_as_float(u));
+      }
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+// srcs / dsts: host arrays of up to 16 base addresses; table: device array of 5 * nchunks longs
+int ptg_piece_copy(const void* srcs, int nsrc, int src_bf16, const void* dsts, int ndst, int dst_bf16,
+                   const long* table, int nchunks, int sys, hipStream_t stream) {
+  if (nsrc < 1 || nsrc > IPC_MAXW || ndst < 1 || ndst > IPC_MAXW || nchunks < 0) return (int)hipErrorInvalidValue;
+  if (nchunks == 0) return 0;
+  PieceBases sb, db;
+  const unsigned long long* sp = (const unsigned long long*)srcs;
+  const unsigned long long* dp = (const unsigned long long*)dsts;
+  for (int i = 0; i < IPC_MAXW; ++i) {
+    sb.base[i] = i < nsrc ? (char*)sp[i] : nullptr;
+    db.base[i] = i < ndst ? (char*)dp[i] : nullptr;
+  }
+  const int grid = nchunks < 4096 ? nchunks : 4096;
+  if (sys)
+    hipLaunchKernelGGL(piece_copy_k<true>, dim3(grid), dim3(256), 0, stream, sb, src_bf16, db, dst_bf16, table, nchunks);
+  else
+    hipLaunchKernelGGL(piece_copy_k<false>, dim3(grid), dim3(256), 0, stream, sb, src_bf16, db, dst_bf16, table, nchunks);
+  PTG_RETURN_LAUNCH();
+}
+
+// export a pointer inside a device allocation (e.g. a torch tensor): IPC handle of its allocation +
+// the byte offset of the pointer in it (peers open the handle and add the offset)
+int ptg_ipc_export(void* ptr, void* out_handle, long* out_offset) {
+  void* base = nullptr;
+  size_t size = 0;
+  hipError_t e = hipMemGetAddressRange(&base, &size, ptr);
+  if (e != hipSuccess) return (int)e;
+  e = hipIpcGetMemHandle((hipIpcMemHandle_t*)out_handle, base);
+  if (e != hipSuccess) return (int)e;
+  *out_offset = (long)((char*)ptr - (char*)base);
+  return 0;
+}
+
+int ptg_sim_reduce_scatter(const float* g, float* out, long cnt, int nchunks, float own_scale, float w_peer,
+                           hipStream_t stream) {
+  if (cnt % 4 || nchunks < 1) return (int)hipErrorInvalidValue;
+  const long cnt4 = cnt / 4;
+  if (cnt4 == 0) return 0;
+  const int grid = (int)min(2048L, (cnt4 + 255) / 256);
+  hipLaunchKernelGGL(sim_rs_k, dim3(grid), dim3(256), 0, stream, (const float4*)g, (float4*)out, cnt4, nchunks,
+                     own_scale, w_peer);
+  PTG_RETURN_LAUNCH();
+}
+
+// buf: the bucket's first byte; bytes [lo, hi) (16-B multiples) are the peer chunks
+int ptg_sim_all_gather(void* buf, long lo, long hi, hipStream_t stream) {
+  if (lo % 16 || hi % 16 || hi < lo) return (int)hipErrorInvalidValue;
+  const long lo4 = lo / 16, hi4 = hi / 16;
+  if (hi4 == lo4) return 0;
+  const int grid = (int)min(2048L, (hi4 - lo4 + 255) / 256);
+  hipLaunchKernelGGL(sim_ag_k, dim3(grid), dim3(256), 0, stream, (uint4*)buf, lo4, hi4, 0u);
+  PTG_RETURN_LAUNCH();
+}
 
 // layout constants for the host side (parallel/ipc.py): flag region bytes, max ranks
 int ptg_ipc_flag_bytes() { return (int)IPC_FLAG_BYTES; }

@@ -369,7 +369,10 @@ struct LdsImg {
   static constexpr int ELEMS = L::K_CONTIG ? R * LD : BK * LD;
 };
 
-template <int BM, int BN, int WM, int WN, class LA, class LB, class EPI>
+// PF: how many K-steps ahead the global loads run (register slots; 1 = the next step only).  With one
+// 4-wave workgroup per CU (256-row skinny tiles) one K-step of MFMAs is shorter than an HBM round
+// trip, so those tiles load 2 steps ahead.
+template <int BM, int BN, int WM, int WN, class LA, class LB, class EPI, int PF = 1>
 __global__ __launch_bounds__(256) void gemm_kernel(LA la, LB lb, EPI epi, int M, int N, int K,
                                                    int kchunk) {
   constexpr int WTM = BM / WM, WTN = BN / WN, FM = WTM / 16, FN = WTN / 16;
@@ -421,25 +424,28 @@ __global__ __launch_bounds__(256) void gemm_kernel(LA la, LB lb, EPI epi, int M,
     }
   }
 
-  U4 ra[AI], rb[BI];
+  static_assert(PF >= 1 && PF <= 3, "register prefetch depth");
+  U4 ra[PF][AI], rb[PF][BI];
   const Rsrc rsA = la.rsrc(), rsB = lb.rsrc();
   // slots past the tile (AV or BV not a multiple of 256) exist only in the last unrolled slot
   constexpr bool AFULL = AV % 256 == 0, BFULL = BV % 256 == 0;
-  auto gload = [&](int k0) {
+  auto gload = [&](auto slot, int k0) {
+    constexpr int sl = decltype(slot)::value;
 #pragma unroll
-    for (int i = 0; i < AI; ++i) ra[i] = la.load(rsA, ca[i], k0 + akk[i]);
+    for (int i = 0; i < AI; ++i) ra[sl][i] = la.load(rsA, ca[i], k0 + akk[i]);
 #pragma unroll
-    for (int i = 0; i < BI; ++i) rb[i] = lb.load(rsB, cb[i], k0 + bkk[i]);
+    for (int i = 0; i < BI; ++i) rb[sl][i] = lb.load(rsB, cb[i], k0 + bkk[i]);
   };
-  auto sstore = [&](int stage) {
+  auto sstore = [&](auto slot, int stage) {
+    constexpr int sl = decltype(slot)::value;
     bf16_t* sA = smem + stage * STAGE;
     bf16_t* sB = sA + IA::ELEMS;
 #pragma unroll
     for (int i = 0; i < AI; ++i)
-      if (AFULL || aon[i]) *(U4*)(sA + aoff[i]) = ra[i];
+      if (AFULL || aon[i]) *(U4*)(sA + aoff[i]) = ra[sl][i];
 #pragma unroll
     for (int i = 0; i < BI; ++i)
-      if (BFULL || bon[i]) *(U4*)(sB + boff[i]) = rb[i];
+      if (BFULL || bon[i]) *(U4*)(sB + boff[i]) = rb[sl][i];
   };
   // fragment (16 rows x 32 k at k-offset kk) of an LDS image; rows start at `row0`
   const int g = lane >> 4, li = lane & 15, q = li >> 2, p4 = (li & 3) * 4;
@@ -467,12 +473,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(LA la, LB lb, EPI epi, int M,
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  gload(kb);
-  sstore(0);
-  __syncthreads();
-  for (int it = 0; it < nk; ++it) {
-    const int cur = it & 1;
-    if (it + 1 < nk) gload(kb + (it + 1) * BK);
+  auto compute = [&](int cur) {
     const bf16_t* sA = smem + cur * STAGE;
     const bf16_t* sB = sA + IA::ELEMS;
 #pragma unroll
@@ -494,9 +495,32 @@ __global__ __launch_bounds__(256) void gemm_kernel(LA la, LB lb, EPI epi, int M,
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    // the other stage was last read in step it-1, which ended with a barrier
-    if (it + 1 < nk) sstore(cur ^ 1);
-    __syncthreads();
+  };
+  // K-step t's tile sits in register slot t % PF from its load (PF steps ahead) until it is written to
+  // LDS stage t & 1 at the end of step t-1; step t then refills slot t % PF with tile t + PF.
+  gload(std::integral_constant<int, 0>{}, kb);
+  sstore(std::integral_constant<int, 0>{}, 0);
+  if constexpr (PF >= 2) { if (1 < nk) gload(std::integral_constant<int, 1>{}, kb + BK); }
+  if constexpr (PF >= 3) { if (2 < nk) gload(std::integral_constant<int, 2>{}, kb + 2 * BK); }
+  __syncthreads();
+  for (int it = 0; it < nk; it += PF) {
+    auto step = [&](auto u) {
+      constexpr int U = decltype(u)::value;
+      const int t = it + U;
+      if (t >= nk) return;
+      if constexpr (PF == 1) {
+        if (t + 1 < nk) gload(std::integral_constant<int, 0>{}, kb + (t + 1) * BK);
+      } else {
+        if (t + PF < nk) gload(std::integral_constant<int, U>{}, kb + (t + PF) * BK);
+      }
+      compute(t & 1);
+      // the other stage was last read in step t-1, which ended with a barrier
+      if (t + 1 < nk) sstore(std::integral_constant<int, (U + 1) % PF>{}, (t + 1) & 1);
+      __syncthreads();
+    };
+    step(std::integral_constant<int, 0>{});
+    if constexpr (PF >= 2) step(std::integral_constant<int, 1>{});
+    if constexpr (PF >= 3) step(std::integral_constant<int, 2>{});
   }
 
   // C/D map of mfma_f32_16x16x32: col = lane&15, row = (lane>>4)*4 + r
@@ -732,7 +756,7 @@ static bool gemm256_enabled() {
   return g_gemm256 == 1;
 }
 
-template <int BM, int BN, int WM, int WN, class LA, class LB, class EPI>
+template <int BM, int BN, int WM, int WN, class LA, class LB, class EPI, int PF = 1>
 static int launch_gemm(const LA& la, const LB& lb, const EPI& epi, int M, int N, int K, int splits,
                        hipStream_t s) {
   const int tiles = ptg_ceil_div(M, BM) * ptg_ceil_div(N, BN);
@@ -741,7 +765,7 @@ static int launch_gemm(const LA& la, const LB& lb, const EPI& epi, int M, int N,
   if (kchunk < BK) kchunk = BK;
   splits = ptg_ceil_div(K, kchunk);
   dim3 grid(tiles, splits);
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, LA, LB, EPI>), grid, dim3(256), 0, s, la, lb, epi, M,
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, LA, LB, EPI, PF>), grid, dim3(256), 0, s, la, lb, epi, M,
                      N, K, kchunk);
   PTG_RETURN_LAUNCH();
 }
@@ -770,8 +794,10 @@ static int dispatch_gemm(const LA& la, const LB& lb, const EPI& epi, int M, int 
                          hipStream_t s) {
   if (splits == 1 && N >= 4096) {
     switch (skinny_bn_choice(M, N)) {
-      case 64: return launch_gemm<256, 64, 4, 1>(la, lb, epi, M, N, K, 1, s);
-      case 80: return launch_gemm<256, 80, 4, 1>(la, lb, epi, M, N, K, 1, s);
+      case 64: return launch_gemm<256, 64, 4, 1, LA, LB, EPI, 2>(la, lb, epi, M, N, K, 1, s);
+      case 80: return launch_gemm<256, 80, 4, 1, LA, LB, EPI, 2>(la, lb, epi, M, N, K, 1, s);
+      case 81: return launch_gemm<256, 80, 4, 1, LA, LB, EPI, 3>(la, lb, epi, M, N, K, 1, s);
+      case 82: return launch_gemm<256, 80, 4, 1, LA, LB, EPI, 1>(la, lb, epi, M, N, K, 1, s);
       default: break;
     }
   }

@@ -67,6 +67,10 @@ _K = [
     Knob("pg_timeout_s", float, 600.0, "PTG_PG_TIMEOUT", None, "process-group collective timeout (hang -> error -> restart)"),
     Knob("bucket_mb", float, 64.0, "PTG_BUCKET_MB", None, "MWMS gradient bucket size"),
     Knob("sharded_update", bool, True, "PTG_SHARDED_UPDATE", None, "MWMS: reduce-scatter + sharded optimizer + all-gather"),
+    Knob("sim_world", int, 0, "PTG_SIM_WORLD", None,
+         "1-rank MWMS runs rank 0's kernel sequence of an N-rank sharded update (collectives -> local kernels)"),
+    Knob("sim_exact", bool, False, "PTG_SIM_EXACT", None,
+         "sim_world: also apply the peers' shard updates (exact numerics of N identical-data ranks, N x the Adam work)"),
     Knob("persist_dynamic", bool, False, "PTG_PERSIST_DYNAMIC", None, "persistent conv kernels in work-queue mode for N > 1"),
     Knob("ps_mode", str, "sync", "PTG_PS_MODE", None, "ParameterServerStrategy: sync or async"),
     Knob("ipc_allreduce", bool, False, "PTG_IPC_ALLREDUCE", None, "one-shot IPC all-reduce for small messages"),

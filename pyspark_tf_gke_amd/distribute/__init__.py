@@ -3,7 +3,8 @@ from .cluster import (ClusterSpec, InputContext, MinSizePartitioner, Server, Sim
                       TFConfigClusterResolver, build_cluster_def, make_tf_config, validate_chief_addr)
 from .coordinator import ClusterCoordinator, RemoteValue  # noqa: F401
 from .strategy import (MirroredStrategy, MultiWorkerMirroredStrategy, OneDeviceStrategy,  # noqa: F401
-                       ParameterServerStrategy, Strategy, current_strategy)
+                       Strategy, current_strategy)
+from .ps import ParameterServerStrategy  # noqa: F401
 
 
 class cluster_resolver:  # noqa: N801 - namespace like tf.distribute.cluster_resolver

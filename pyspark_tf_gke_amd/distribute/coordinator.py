@@ -1,32 +1,42 @@
 """``ClusterCoordinator``: the reference's schedule/join driver (train_tf_ps.py:612-614, :634-647,
 :734-736, :755-769) on SPMD ranks.
 
-Every rank runs the same driver script.  ``schedule(fn, args)`` queues a closure and returns a
-:class:`RemoteValue`; ``join()`` executes the queue in rounds of ``world_size`` closures, closure i
-of a round running on rank ``i % world`` (so ``steps_per_epoch`` scheduled steps are spread over the
-workers, each worker consuming its own per-worker dataset iterator).  ``join()`` is the epoch
-barrier of the reference.
+Every rank runs the same driver script, so every rank holds the same closure queue;
+``schedule(fn, args)`` queues a closure and returns a :class:`RemoteValue`; ``join()`` is the epoch
+barrier of the reference.  A closure runs on exactly one rank, with that rank's per-worker dataset
+iterator (``create_per_worker_dataset``), and its scalar result is visible on every rank.
 
-A round is a transaction:
+Asynchronous parameter server (``ParameterServerStrategy(mode="async")``, N > 1): closures are
+handed to whichever worker is idle - each rank draws the next closure index from a counter in the
+TCP store until the queue is exhausted - and a closure's ``apply_gradients`` pushes straight to the
+PS owners (one-sided, ps.py) without any collective, so a slow worker simply runs fewer closures
+(TF's ``ClusterCoordinator.schedule`` dispatch).  A closure that raises is re-run by the worker that
+is idle at that moment - the one that just failed it - up to ``max_retries`` times.  Results travel
+through the store.
+
+Synchronous strategies (sync PS, MWMS): ``join()`` runs the queue in rounds of ``world_size``
+closures, closure i of a round on rank ``i % world``; a round is a transaction:
   1. every rank runs its closure (if any) with the strategy in *deferred* mode: gradient pushes and
      optimizer updates inside the closure (``optimizer.apply_gradients``, ``model.train_step``) are
      recorded, not executed, so a closure that raises leaves no collective half-issued;
   2. the ranks exchange one small status tensor (all-reduce, no pickles): per rank ok / no closure /
      failed, plus which (model, optimizer) the update belongs to;
-  3. if some closure failed and may be retried, EVERY rank discards the round's gradients and the
-     whole round is queued again with the same closure-to-rank assignment (TF's coordinator
-     re-schedules failed closures; re-running the round keeps every rank's step sequence
-     identical, and a deterministic closure reproduces the fault-free result bit for bit);
-     a closure that exhausted ``max_retries`` is dropped with its error recorded on every rank;
-  4. otherwise the round is committed collectively: the strategy pushes the contributors'
-     gradients (ranks without a closure push nothing and the average is over the contributors;
-     nobody contributing means no optimizer step).
+  3. if some closure failed and may be retried, ONLY the failed closures run again, on the ranks
+     that failed them, with their partial gradients discarded; the ranks whose closures succeeded
+     keep their pending gradients and results (their iterators are not advanced twice, their forward
+     side effects are not repeated); a closure that exhausted ``max_retries`` is dropped with its
+     error recorded on every rank;
+  4. then the round is committed collectively: the strategy pushes the contributors' gradients
+     (ranks without a closure push nothing and the average is over the contributors; nobody
+     contributing means no optimizer step).
 
 Closures must not call collectives themselves (every rank would have to reach them).
 """
 from __future__ import annotations
 
 from ..parallel import comm
+
+_COORDINATORS = [0]
 
 
 def _encode_value(v) -> tuple[int, float]:
@@ -56,11 +66,26 @@ class RemoteValue:
         self._done = False
         self._error = None
         self._local = False
+        self._remote_key = None  # async dispatch: where the executing rank published the result
 
     def _set(self, v, local=True):
         self._value, self._done, self._local = v, True, local
 
+    def _resolve(self):
+        if self._done or self._error is not None or self._remote_key is None:
+            return
+        from .ps import _store
+
+        msg = _store().get(self._remote_key).decode()
+        kind, _, rest = msg.partition(":")
+        if kind == "E":
+            self._error = RuntimeError(rest)
+        else:
+            vt, _, x = rest.partition(":")
+            self._set(_decode_value(int(vt), float(x)), local=False)
+
     def fetch(self):
+        self._resolve()
         if self._error is not None:
             raise self._error
         return self._value
@@ -95,6 +120,9 @@ class ClusterCoordinator:
         self.max_retries = max_retries
         self.closures_run = 0
         self.retries = 0
+        _COORDINATORS[0] += 1
+        self._cid = _COORDINATORS[0]  # same on every rank: coordinators are created in the same order
+        self._gen = 0
 
     def create_per_worker_dataset(self, dataset_fn):
         ctx = self.strategy.input_context()
@@ -107,6 +135,56 @@ class ClusterCoordinator:
         return rv
 
     def join(self) -> None:
+        if getattr(self.strategy, "is_async", False):
+            self._join_async()
+        else:
+            self._join_rounds()
+
+    # ---- asynchronous dispatch ------------------------------------------------------------------
+    def _join_async(self) -> None:
+        from ..runtime import heartbeat
+        from .ps import _store
+
+        st = self.strategy
+        store = _store()
+        self._gen += 1
+        pre = f"ptg/coord/{st._token if getattr(st, '_token', None) else 'x'}/{self._cid}/{self._gen}"
+        queue, self._queue = self._queue, []
+        n = len(queue)
+        while True:
+            i = store.add(pre + "/next", 1) - 1  # the next closure goes to whichever worker asks first
+            if i >= n:
+                break
+            fn, args, kwargs, rv, tries = queue[i]
+            while True:
+                try:
+                    value = fn(*args, **kwargs)
+                except StopIteration as e:
+                    rv._error = e
+                    store.set(f"{pre}/rv/{i}", f"E:StopIteration on worker {st.rank}")
+                    break
+                except Exception as e:  # noqa: BLE001 - rescheduled on the (now idle) worker
+                    if tries >= self.max_retries:
+                        rv._error = e
+                        store.set(f"{pre}/rv/{i}", f"E:closure failed on worker {st.rank} after {tries + 1} attempts: {e!r}"[:2000])
+                        break
+                    tries += 1
+                    self.retries += 1
+                    continue
+                rv._set(value)
+                vt, x = _encode_value(value)
+                store.set(f"{pre}/rv/{i}", f"V:{vt}:{x!r}")
+                self.closures_run += 1
+                break
+            heartbeat.progress()
+        st.wait_all_applied()  # collective: every push applied, every rank pulled the final values
+        for i, (_, _, _, rv, _) in enumerate(queue):
+            if not rv._done and rv._error is None:
+                rv._remote_key = f"{pre}/rv/{i}"  # ran elsewhere: resolved on fetch()
+        comm.barrier()
+
+    # ---- transactional rounds (sync) ---------------------------------------------------------------
+    def _join_rounds(self) -> None:
         import torch
 
         from ..runtime import heartbeat
@@ -117,55 +195,52 @@ class ClusterCoordinator:
             batch = self._queue[:world]
             rest = self._queue[world:]
             mine = batch[rank] if rank < len(batch) else None
-            status, err = 0, None  # 0 = no closure / StopIteration, 1 = gradient pending, 2 = failed
+            tries = mine[4] if mine is not None else 0
+            # 0 = no closure / StopIteration, 1 = gradient pending, 2 = failed (retry), 3 = ran, no
+            # update, 4 = failed for good (dropped)
+            status, err, value = None, None, None
             st.begin_round()
-            try:
-                if mine is not None:
-                    fn, args, kwargs, rv, tries = mine
-                    try:
-                        value = fn(*args, **kwargs)
-                        status = 1
-                    except StopIteration as e:
-                        err = e
-                    except Exception as e:  # noqa: BLE001 - reported to every rank below
-                        status, err = 2, e
-            finally:
-                st.end_round_local()
-            mi, oi = st.pending_ids() if status == 1 else (-1, -1)
-            if status == 1 and mi < 0:
-                status = 3  # ran fine but produced no update (e.g. an evaluation closure)
-            vtype, vnum = _encode_value(value) if status == 1 or status == 3 else (0, 0.0)
-            vec = torch.zeros(4 * world, dtype=torch.int64)
-            vec[4 * rank: 4 * rank + 4] = torch.tensor([status, mi + 1, oi + 1, vtype])
-            vec = torch.tensor(comm.all_reduce_int(vec.tolist()), dtype=torch.int64).view(world, 4)
+            while True:
+                if status is None or status == 2:
+                    status, err, value = self._run_mine(st, mine)
+                    if status == 2 and tries >= self.max_retries:
+                        status = 4
+                        st.abort_round()  # dropped: its partial gradient goes nowhere
+                mi, oi = st.pending_ids() if status == 1 else (-1, -1)
+                if status == 1 and mi < 0:
+                    status = 3  # ran fine but produced no update (e.g. an evaluation closure)
+                vtype, vnum = _encode_value(value) if status in (1, 3) else (0, 0.0)
+                vec = torch.zeros(4 * world, dtype=torch.int64)
+                vec[4 * rank: 4 * rank + 4] = torch.tensor([status, mi + 1, oi + 1, vtype])
+                vec = torch.tensor(comm.all_reduce_int(vec.tolist()), dtype=torch.int64).view(world, 4)
+                statuses = vec[:, 0].tolist()
+                failed = [r for r, s_ in enumerate(statuses) if s_ == 2]
+                if not failed:
+                    break
+                # only the failed closures run again; the others keep their pending gradients
+                self.retries += len(failed)
+                if status == 2:
+                    st.abort_round()  # this rank's partial gradient of the failed attempt
+                    tries += 1
+                    st.begin_round_retry()
             fvec = [0.0] * world
             fvec[rank] = vnum
             fvec = comm.all_reduce_float(fvec) if any(vec[:, 3].tolist()) else fvec
-            statuses = vec[:, 0].tolist()
-            failed = [r for r, s_ in enumerate(statuses) if s_ == 2]
-            if failed:
-                st.abort_round()
-                requeue = []
-                for r, item in enumerate(batch):
-                    fn, args, kwargs, rv, tries = item
-                    if r in failed:
-                        if tries >= self.max_retries:
-                            rv._error = err if r == rank else RuntimeError(
-                                f"closure failed on worker {r} after {tries + 1} attempts")
-                            rv._done = True
-                            continue
-                        tries += 1
-                    requeue.append((fn, args, kwargs, rv, tries))
-                self.retries += sum(1 for r in failed if r < len(batch))
-                self._queue = requeue + rest
-                continue
-            if mine is not None:
-                rv = mine[3]
-                if status in (1, 3):
-                    rv._set(value)
-                    self.closures_run += 1
-                elif err is not None:
-                    rv._error = err
+            for r, item in enumerate(batch):
+                rv_ = item[3]
+                if r == rank:
+                    if status in (1, 3):
+                        rv_._set(value)
+                        self.closures_run += 1
+                    elif err is not None:
+                        rv_._error = err
+                elif statuses[r] == 4:
+                    rv_._error = RuntimeError(f"closure failed on worker {r} after {self.max_retries + 1} attempts")
+                elif statuses[r] in (1, 3):
+                    # executed on another rank: scalar results travel in the status exchange
+                    rv_._set(_decode_value(int(vec[r, 3]), fvec[r]), local=False)
+                elif statuses[r] == 0:
+                    rv_._set(None, local=False)
             contributed = [s_ == 1 for s_ in statuses]
             ids = [(int(m) - 1, int(o) - 1) for m, o in vec[:, 1:3].tolist() if m > 0]
             if ids:
@@ -175,14 +250,24 @@ class ClusterCoordinator:
                 model = st.models[mi]
                 opt = st.optimizers[oi] if oi < len(st.optimizers) else model.optimizer
                 st.commit_round(model, opt, contributed)
-            for r, item in enumerate(batch):
-                rv_ = item[3]
-                if not rv_._done and rv_._error is None:
-                    # executed on another rank: scalar results travel in the status exchange
-                    rv_._set(_decode_value(int(vec[r, 3]), fvec[r]), local=False)
+            else:
+                st.abort_round()
             self._queue = rest
             heartbeat.progress()
         comm.barrier()
+
+    def _run_mine(self, st, mine):
+        if mine is None:
+            return 0, None, None
+        fn, args, kwargs, _, _ = mine
+        try:
+            return 1, None, fn(*args, **kwargs)
+        except StopIteration as e:
+            return 0, e, None
+        except Exception as e:  # noqa: BLE001 - reported to every rank
+            return 2, e, None
+        finally:
+            st.end_round_local()
 
     def done(self) -> bool:
         return not self._queue

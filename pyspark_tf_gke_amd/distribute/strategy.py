@@ -6,12 +6,10 @@
   in backward-completion order), so the large Dense/last-layer gradients travel over xGMI while
   the convolution backward is still running.  Gradient averaging (1/world) is folded into the
   fused Adam kernel.
-* :class:`ParameterServerStrategy` (the reference's strategy, train_tf_ps.py:440-511): variables
-  are sharded across the GPUs that act as PS shards; each step reduce-scatters the flat gradient
-  to the shard owners, every rank applies Adam to the shard it owns, and the updated parameters
-  are all-gathered back ("pull" = all-gather, "push + apply" = reduce-scatter + sharded Adam; M1/M2
-  of SURVEY §2.2.c).  Combined with :class:`~.coordinator.ClusterCoordinator` for the
-  ``schedule()/join()`` driver API.
+* :class:`~.ps.ParameterServerStrategy` (the reference's strategy, train_tf_ps.py:440-511), in
+  ps.py: variables sharded over the ranks acting as PS tasks, sync (collective push/pull) or async
+  (one-sided windows + owner service threads) - with :class:`~.coordinator.ClusterCoordinator` for
+  the ``schedule()/join()`` driver API.
 * :class:`OneDeviceStrategy` / :class:`MirroredStrategy` for single-process use.
 """
 from __future__ import annotations
@@ -52,6 +50,12 @@ class Strategy:
 
     @property
     def num_replicas_in_sync(self) -> int:
+        return self.world_size
+
+    @property
+    def dp_degree(self) -> int:
+        """Data-parallel degree the step's kernel sequence is built for (the world size, or the
+        simulated world of MultiWorkerMirroredStrategy's PTG_SIM_WORLD mode on one rank)."""
         return self.world_size
 
     @property
@@ -124,6 +128,11 @@ class Strategy:
     def end_round_local(self) -> None:
         self._in_round = False
 
+    def begin_round_retry(self) -> None:
+        """A failed closure runs again inside the same round (its rank's pending update was aborted)."""
+        self._in_round = True
+        self._pending = None
+
     def in_round(self) -> bool:
         return getattr(self, "_in_round", False)
 
@@ -144,9 +153,13 @@ class Strategy:
         return self.models.index(model), self.optimizers.index(opt)
 
     def abort_round(self) -> None:
+        """Discard this rank's gradients of the round (a failed closure may have stopped anywhere in
+        its backward, before or after its deferred update was recorded)."""
         pend = getattr(self, "_pending", None)
-        if pend is not None:
-            pend[0].store.flat_grad.zero_()
+        models = list(self.models) + ([pend[0]] if pend is not None and pend[0] not in self.models else [])
+        for m in models:
+            m.store.flat_grad.zero_()
+            m.store.grad_clean = True
         self._pending = None
 
     def commit_round(self, model, optimizer, contributed: list) -> None:
@@ -268,9 +281,24 @@ class MultiWorkerMirroredStrategy(Strategy):
         self.cluster_resolver = cluster_resolver or TFConfigClusterResolver()
         mb = bucket_mb if bucket_mb is not None else float(config.get("bucket_mb"))
         self.bucket_elems = max(1, int(mb * (1 << 20) / 4))
+        # simulated world (PTG_SIM_WORLD=N on ONE rank): build the shard plan of an N-rank job and run
+        # rank 0's exact kernel sequence of the sharded update - weight gradients into flat_grad, per-
+        # bucket reduce-scatter, shard optimizer, all-gather + bf16 re-cast - with each collective
+        # replaced by a local kernel moving the same local HBM bytes (ops.nn.sim_reduce_scatter /
+        # sim_all_gather).  The peers are N-1 ranks with identical data: the reduced shard is N x ours.
+        # PTG_SIM_EXACT=1 also applies the peers' shard updates, so parameters equal a real N-rank run
+        # with identical per-rank batches (at N x the optimizer work); without it the peers' chunks keep
+        # their values (cost model only).
+        self.sim_world = 0
+        self.sim_exact = False
+        if self.world_size == 1 and int(config.get("sim_world")) > 1:
+            self.sim_world = int(config.get("sim_world"))
+            self.sim_exact = bool(config.get("sim_exact"))
         if sharded_update is None:
             sharded_update = config.get("sharded_update")
-        self.sharded_update = bool(sharded_update) and self.world_size > 1
+        self.sharded_update = bool(sharded_update) and self.dp_degree > 1
+        if self.sim_world and not self.sharded_update:
+            raise ValueError("PTG_SIM_WORLD simulates the sharded update only (PTG_SHARDED_UPDATE=1)")
         self._works: list = []
         self._launched = 0
         if self.world_size > 1 and self.device.type == "cuda" and config.get("persist_dynamic"):
@@ -281,9 +309,13 @@ class MultiWorkerMirroredStrategy(Strategy):
 
             K.set_persist_mode(True)
 
+    @property
+    def dp_degree(self) -> int:
+        return self.sim_world or self.world_size
+
     def register_model(self, model) -> None:
         if self.sharded_update:
-            model._shard_plan = _ShardPlan(model, self.world_size, self.rank, self.bucket_elems)
+            model._shard_plan = _ShardPlan(model, self.dp_degree, self.rank, self.bucket_elems)
         super().register_model(model)
 
     # ---- replicated update: bucketed all-reduce
@@ -307,7 +339,13 @@ class MultiWorkerMirroredStrategy(Strategy):
         from ..nn import streams as S
 
         g = st.flat_grad[b.lo:b.hi]
-        plan.rs_works.append(S.launch(lambda: comm.reduce_scatter_flat(b.gshard, g, async_op=True), g.device))
+        if self.sim_world:
+            from ..ops import nn as K
+
+            n = self.sim_world
+            S.launch(lambda: K.sim_reduce_scatter(g, b.gshard, n, float(n), 0.0), g.device)
+        else:
+            plan.rs_works.append(S.launch(lambda: comm.reduce_scatter_flat(b.gshard, g, async_op=True), g.device))
         plan.launched[b.idx] = True
 
     def _wait_gather(self, model, plan, b) -> None:
@@ -347,6 +385,9 @@ class MultiWorkerMirroredStrategy(Strategy):
         if plan is None or not getattr(st, "master_stale", False):
             return
         self.wait_parameters(model)
+        if self.sim_world:  # no peers to gather from (exact mode keeps every chunk's master current)
+            st.master_stale = False
+            return
         for b in plan.buckets:
             if not b.fp32:
                 comm.all_gather_flat(st.flat[b.lo:b.hi], st.flat[b.slo:b.shi].clone())
@@ -359,7 +400,7 @@ class MultiWorkerMirroredStrategy(Strategy):
             return
         self.synchronize_master(model)
         opt = model.optimizer
-        if opt is None:
+        if opt is None or self.sim_world:
             return
         for t in opt.state_tensors().values():
             if t is None or t.numel() != model.store.total:
@@ -369,7 +410,7 @@ class MultiWorkerMirroredStrategy(Strategy):
 
     # ---- engine hooks
     def on_op_grads_ready(self, model, op) -> None:
-        if self.world_size == 1 or not op.params or self.in_round():
+        if self.dp_degree == 1 or not op.params or self.in_round():
             return
         plan = getattr(model, "_shard_plan", None)
         if plan is not None:
@@ -389,7 +430,7 @@ class MultiWorkerMirroredStrategy(Strategy):
             self._launch(model, hi)
 
     def finish_gradients(self, model) -> None:
-        if self.world_size == 1 or self.in_round():
+        if self.dp_degree == 1 or self.in_round():
             return
         plan = getattr(model, "_shard_plan", None)
         if plan is not None:
@@ -416,7 +457,7 @@ class MultiWorkerMirroredStrategy(Strategy):
             return
         opt = optimizer or model.optimizer
         plan = getattr(model, "_shard_plan", None)
-        gs = self._commit_scale / self.world_size
+        gs = self._commit_scale / self.dp_degree
         if plan is None:
             opt.apply(model.store, gscale=gs)
             return
@@ -424,6 +465,10 @@ class MultiWorkerMirroredStrategy(Strategy):
         self.wait_parameters(model)  # (no-op in steady state: the forward waited for every bucket)
         for b in plan.buckets:
             opt.apply_shard(st, b.gshard, b.slo, b.shi, gscale=gs, advance=False)
+        if self.sim_world:
+            self._sim_peers_update(model, plan, opt, gs)
+            opt.iterations += 1
+            return
         opt.iterations += 1
         for b in plan.buckets:
             buf = st.flat if b.fp32 else st.flat_bf16
@@ -431,242 +476,36 @@ class MultiWorkerMirroredStrategy(Strategy):
             plan.ag_works[b.idx] = (comm.all_gather_flat(buf[b.lo:b.hi], src, async_op=True), src)
         st.master_stale = any(not b.fp32 for b in plan.buckets)
 
+    def _sim_peers_update(self, model, plan, opt, gs) -> None:
+        """Simulated world: the all-gather of every bucket.  Exact mode computes what each identical
+        peer applied to its own chunk (N x our gradient chunk, the same optimizer step); otherwise the
+        peers' chunks are rewritten in place (the bytes the gather writes, values unchanged).  fp32
+        buckets are re-cast to bf16 before their forward use, as after a real gather."""
+        from ..ops import nn as K
+
+        st = model.store
+        n = self.sim_world
+        for b in plan.buckets:
+            cnt = b.shi - b.slo
+            if self.sim_exact:
+                for r in range(1, n):
+                    lo = b.lo + r * cnt
+                    tmp = torch.empty(cnt, dtype=torch.float32, device=st.flat_grad.device)
+                    K.sim_reduce_scatter(st.flat_grad[lo:lo + cnt], tmp, 1, float(n), 0.0)
+                    opt.apply_shard(st, tmp, lo, lo + cnt, gscale=gs, advance=False)
+            else:
+                buf = st.flat if b.fp32 else st.flat_bf16
+                K.sim_all_gather(buf[b.lo:b.hi], cnt)
+            plan.ag_works[b.idx] = (None, None)
+        st.master_stale = False
+
 
 MirroredStrategy = MultiWorkerMirroredStrategy
 
 
-class _Piece:
-    __slots__ = ("param", "lo", "n", "owner", "xlo", "task")
+def __getattr__(name):  # ParameterServerStrategy lives in ps.py (it builds on Strategy above)
+    if name == "ParameterServerStrategy":
+        from .ps import ParameterServerStrategy
 
-    def __init__(self, param, lo, n, owner, task):
-        self.param, self.lo, self.n, self.owner, self.task = param, lo, n, owner, task
-        self.xlo = -1
-
-
-class _PSPlan:
-    """Variable placement of one model: every parameter is cut by the partitioner along axis 0
-    (whole rows per shard, TF's MinSizePartitioner rule) and shard i of the running count goes to
-    PS task ``i % num_ps`` (TF's round-robin variable placement); PS task t lives on rank
-    ``t % world``.  An owner's shards are packed into its segment of an exchange buffer of
-    ``world * seg`` elements, so "push" is ONE reduce-scatter (sync) or one send per owner (async)
-    and "pull" is ONE all-gather, whatever the placement.  The owner keeps its shards' fp32 values
-    and optimizer moments in packed form: the variables live on the PS."""
-
-    def __init__(self, model, partitioner, num_ps: int, world: int, rank: int):
-        from ..nn.params import ALIGN
-
-        st = model.store
-        self.pieces: list[_Piece] = []
-        task = 0
-        for p in sorted(st.params, key=lambda q: q.order):  # variable creation order
-            k = partitioner.num_shards(p.shape, 4) if partitioner is not None else 1
-            rows = p.shape[0] if p.shape else 1
-            row_elems = p.numel // max(rows, 1)
-            k = max(1, min(k, rows))
-            base, rem = divmod(rows, k)
-            r0 = 0
-            for j in range(k):
-                nr = base + (1 if j < rem else 0)
-                t = task % num_ps
-                self.pieces.append(_Piece(p, p.offset + r0 * row_elems, nr * row_elems, t % world, t))
-                r0 += nr
-                task += 1
-        per_owner = [0] * world
-        for pc in self.pieces:
-            pc.xlo = per_owner[pc.owner]
-            per_owner[pc.owner] += pc.n
-        self.owner_elems = per_owner
-        self.seg = max(ALIGN, int(math.ceil(max(per_owner) / ALIGN) * ALIGN))
-        for pc in self.pieces:
-            pc.xlo += pc.owner * self.seg
-        self.world, self.rank = world, rank
-        self.mine = [pc for pc in self.pieces if pc.owner == rank]
-        dev = st.flat.device
-        self.xbuf = torch.zeros(world * self.seg, dtype=torch.float32, device=dev)  # exchange buffer
-        self.gshard = torch.zeros(self.seg, dtype=torch.float32, device=dev)
-        self.master = torch.zeros(self.seg, dtype=torch.float32, device=dev)  # owned values
-        self.master_bf = torch.zeros(self.seg, dtype=st.flat_bf16.dtype, device=dev)
-        self.slots: dict[str, torch.Tensor] = {}  # packed optimizer moments of the owned shards
-        self.pack_params(st)
-
-    def placement(self) -> list:
-        """[(param name, row range, ps task, owner rank)] — the variable-to-PS map."""
-        out = []
-        for pc in self.pieces:
-            rows = pc.param.shape[0] if pc.param.shape else 1
-            re = pc.param.numel // max(rows, 1)
-            r0 = (pc.lo - pc.param.offset) // max(re, 1)
-            out.append((pc.param.name, (r0, r0 + pc.n // max(re, 1)), pc.task, pc.owner))
-        return out
-
-    def pack(self, src: torch.Tensor, dst: torch.Tensor, only_mine: bool = False) -> None:
-        for pc in (self.mine if only_mine else self.pieces):
-            x0 = pc.xlo - (self.rank * self.seg if only_mine else 0)
-            dst[x0:x0 + pc.n].copy_(src[pc.lo:pc.lo + pc.n])
-
-    def unpack(self, src: torch.Tensor, dst: torch.Tensor) -> None:
-        for pc in self.pieces:
-            dst[pc.lo:pc.lo + pc.n].copy_(src[pc.xlo:pc.xlo + pc.n])
-
-    def pack_params(self, st) -> None:
-        self.pack(st.flat, self.master, only_mine=True)
-
-    def slot(self, name: str) -> torch.Tensor:
-        t = self.slots.get(name)
-        if t is None:
-            t = self.slots[name] = torch.zeros(self.seg, dtype=torch.float32, device=self.master.device)
-        return t
-
-
-class ParameterServerStrategy(Strategy):
-    """The reference's strategy (train_tf_ps.py:440-511) on GPU ranks: every rank is a worker and
-    hosts PS tasks.  Variables are placed per shard by ``variable_partitioner`` (default
-    ``MinSizePartitioner(256 KiB, max_shards=#ps)``, :505-507) round-robin over the PS tasks; PS
-    task t lives on rank ``t % world`` (``num_ps`` from the cluster spec, or one per rank).
-
-    ``mode="sync"`` (default): a step pushes gradients with one reduce-scatter of the packed
-    exchange buffer (owners receive the sum), owners apply the optimizer to the shards they host
-    with the gradient averaged over the workers that contributed, and every worker pulls the new
-    values with one all-gather (M1/M2 of SURVEY §2.2.c).
-
-    ``mode="async"`` (TF's asynchronous PS semantics): each worker's gradient is sent point-to-point
-    to the owner of every shard (``batch_isend_irecv``; RCCL runs it on its own stream) and the
-    owner applies it as its own optimizer step, in worker order, without averaging; workers pull the
-    values after all pushes of the round were applied, so a worker's gradient is up to
-    ``workers - 1`` updates stale, as under TF's asynchronous PS with that many concurrent workers.
-
-    Under :class:`~.coordinator.ClusterCoordinator` the push/apply is committed per round after the
-    ranks agree who contributed: no zero-gradient pushes, no optimizer step when nobody did."""
-
-    def __init__(self, cluster_resolver=None, variable_partitioner=None, device=None, mode: str | None = None):
-        super().__init__(device)
-        self.cluster_resolver = cluster_resolver or TFConfigClusterResolver()
-        spec = self.cluster_resolver.cluster_spec() if hasattr(self.cluster_resolver, "cluster_spec") else ClusterSpec({})
-        self.cluster_spec = ClusterSpec(spec)
-        self.num_workers = max(self.cluster_spec.num_tasks("worker"), self.world_size)
-        self.num_ps = self.cluster_spec.num_tasks("ps") or self.world_size
-        self.variable_partitioner = variable_partitioner or MinSizePartitioner(256 << 10, max(self.num_ps, 1))
-        self.mode = (mode or config.get("ps_mode")).lower()
-        if self.mode not in ("sync", "async"):
-            raise ValueError(f"ParameterServerStrategy mode must be 'sync' or 'async', not {self.mode!r}")
-
-    def register_model(self, model) -> None:
-        super().register_model(model)  # broadcast rank 0's initial values first
-        model._ps_plan = _PSPlan(model, self.variable_partitioner, self.num_ps, self.world_size, self.rank)
-
-    def placement(self, model) -> list:
-        return model._ps_plan.placement()
-
-    # ---- optimizer on the owned (packed) shards
-    def _apply_owned(self, model, opt, grad: torch.Tensor, gscale: float) -> None:
-        from ..nn import optimizers as OPT
-        from ..ops import nn as K
-
-        plan = model._ps_plan
-        n = plan.seg
-        if isinstance(opt, OPT.Adam):
-            step = opt.iterations + 1
-            K.adam(plan.master[:n], grad[:n], plan.slot("m"), plan.slot("v"), plan.master_bf[:n], opt.lr_t(step),
-                   opt.beta_1, opt.beta_2, opt.epsilon, gscale)
-        elif isinstance(opt, OPT.SGD):
-            vel = plan.slot("velocity") if opt.momentum > 0 else None
-            K.sgd(plan.master[:n], grad[:n], vel, plan.master_bf[:n], opt.learning_rate, opt.momentum, opt.nesterov,
-                  gscale)
-        else:
-            raise TypeError(f"unsupported optimizer {type(opt).__name__}")
-        opt.iterations += 1
-
-    def _pull(self, model) -> None:
-        from ..ops import nn as K
-
-        plan = model._ps_plan
-        st = model.store
-        comm.all_gather_flat(plan.xbuf, plan.master)
-        plan.unpack(plan.xbuf, st.flat)
-        K.cast_f32_bf16(st.flat, st.flat_bf16)
-
-    def _push_apply(self, model, opt, contributed: list) -> None:
-        plan = model._ps_plan
-        st = model.store
-        n_ok = sum(bool(c) for c in contributed)
-        if n_ok == 0:
-            return
-        if self.world_size == 1:
-            opt.apply(st)
-            return
-        if self.mode == "sync":
-            if contributed[self.rank]:
-                plan.pack(st.flat_grad, plan.xbuf)
-            else:
-                plan.xbuf.zero_()
-            comm.reduce_scatter_flat(plan.gshard, plan.xbuf)
-            self._apply_owned(model, opt, plan.gshard, 1.0 / n_ok)
-        else:
-            import torch.distributed as dist
-
-            if contributed[self.rank]:
-                plan.pack(st.flat_grad, plan.xbuf)
-            ops, recv = [], {}
-            for w in range(self.world_size):
-                if w == self.rank or not contributed[w]:
-                    continue
-                recv[w] = torch.empty(plan.seg, dtype=torch.float32, device=plan.xbuf.device)
-                ops.append(dist.P2POp(dist.irecv, recv[w], w))
-            if contributed[self.rank]:
-                for r in range(self.world_size):
-                    if r != self.rank:
-                        ops.append(dist.P2POp(dist.isend, plan.xbuf[r * plan.seg:(r + 1) * plan.seg], r))
-            if ops:
-                for req in dist.batch_isend_irecv(ops):
-                    req.wait()
-            for w in range(self.world_size):  # apply each worker's push as its own step, in order
-                if not contributed[w]:
-                    continue
-                g = plan.xbuf[self.rank * plan.seg:(self.rank + 1) * plan.seg] if w == self.rank else recv[w]
-                self._apply_owned(model, opt, g, 1.0)
-        self._pull(model)
-
-    # ---- engine hooks
-    def finish_gradients(self, model) -> None:
-        pass  # the push happens in apply_update (after the whole backward)
-
-    def apply_update(self, model, optimizer=None) -> None:
-        if self.in_round():
-            self._defer(model, optimizer)
-            return
-        self._push_apply(model, optimizer or model.optimizer, [True] * self.world_size)
-
-    def commit_round(self, model, optimizer, contributed: list) -> None:
-        self._push_apply(model, optimizer or model.optimizer, contributed)
-        self._pending = None
-
-    # ---- checkpoint support: the canonical optimizer state is per parameter (full layout)
-    def synchronize_state(self, model) -> None:
-        """Collective: unpack every owner's moments into the optimizer's full-layout slots (and the
-        values into the store) on every rank, so checkpoints are stored per parameter name."""
-        plan = getattr(model, "_ps_plan", None)
-        opt = model.optimizer
-        if plan is None or self.world_size == 1:
-            return
-        self._pull(model)
-        if opt is None:
-            return
-        opt.build(model.store)
-        for name, full in opt.state_tensors().items():
-            if full is None or full.numel() != model.store.total:
-                continue
-            comm.all_gather_flat(plan.xbuf, plan.slot(name))
-            plan.unpack(plan.xbuf, full)
-
-    def on_state_loaded(self, model) -> None:
-        """After a checkpoint load into the full layout: re-pack the owned shards."""
-        plan = getattr(model, "_ps_plan", None)
-        if plan is None:
-            return
-        plan.pack_params(model.store)
-        opt = model.optimizer
-        if opt is None:
-            return
-        for name, full in opt.state_tensors().items():
-            if full is not None and full.numel() == model.store.total:
-                plan.pack(full, plan.slot(name), only_mine=True)
+        return ParameterServerStrategy
+    raise AttributeError(name)

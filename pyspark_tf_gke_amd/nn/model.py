@@ -323,7 +323,7 @@ class Sequential:
         one replica (no gradient collective between backward and update), GPU, PTG_FUSED_ADAM != 0."""
         if not FUSED_ADAM or not isinstance(self.optimizer, OPT.Adam) or not self.store.flat.is_cuda:
             return None
-        if st is not None and st.world_size != 1:
+        if st is not None and st.dp_degree != 1:
             return None
         all_ops = getattr(self, "ops", None) or []
         if getattr(self, "_fusable_key", None) is not all_ops:
@@ -406,7 +406,7 @@ class Sequential:
         if not getattr(self, "jit_compile", False) or not xb.is_cuda:
             return False
         st = self._strategy()
-        return st is None or st.world_size == 1
+        return st is None or st.dp_degree == 1
 
     def train_step_fast(self, xb, yb, stats=None) -> None:
         """One training step; replays a captured HIP graph when ``jit_compile`` is on (same batch

@@ -60,7 +60,7 @@ def for_step(store, strategy) -> SideStream | None:
     making the step's stream wait for them."""
     if not ENABLED or not store.flat.is_cuda:
         return None
-    if strategy is not None and strategy.world_size != 1 and not getattr(strategy, "side_stream_ok", False):
+    if strategy is not None and strategy.dp_degree != 1 and not getattr(strategy, "side_stream_ok", False):
         return None
     return SideStream()
 

@@ -528,6 +528,27 @@ def sgd(p, g, vel, pbf, lr: float, momentum: float, nesterov: bool, gscale: floa
         float(gscale), int(clear_grad))
 
 
+def sim_reduce_scatter(g, out, nchunks: int, own_scale: float, w_peer: float):
+    """Simulated-world reduce-scatter (see distribute/strategy.py): out = own_scale * chunk 0 of ``g``
+    + w_peer * (chunks 1..n-1), every chunk read (the local bytes of a ring reduce-scatter)."""
+    cnt = out.numel()
+    if not on_device(g):
+        ch = g[: nchunks * cnt].view(nchunks, cnt)
+        out.copy_(own_scale * ch[0] + (w_peer * ch[1:].sum(0) if nchunks > 1 else 0.0))
+        return out
+    hip("ptg_sim_reduce_scatter", ptr(g), ptr(out), cnt, int(nchunks), float(own_scale), float(w_peer))
+    return out
+
+
+def sim_all_gather(bucket, cnt: int):
+    """Simulated-world all-gather: rewrite the peer chunks [cnt, numel) of ``bucket`` in place."""
+    if not on_device(bucket):
+        return bucket
+    es = bucket.element_size()
+    hip("ptg_sim_all_gather", ptr(bucket), cnt * es, bucket.numel() * es)
+    return bucket
+
+
 def cast_f32_bf16(x, out):
     if not on_device(x):
         # host mode: the "bf16" mirror may be fp32 (PTG_HOST_FP32, possibly aliasing ``x``)

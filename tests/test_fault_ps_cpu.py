@@ -104,8 +104,9 @@ print("RESULT", json.dumps({"same": same, "retries": co2.retries, "it_ok": o_ok.
 
 
 def test_coordinator_exhausted_retries_and_partial_rounds():
-    """A closure failing more than max_retries is dropped (error on every rank); a round with one
-    closure on two ranks averages over that one worker; no optimizer step without contributors."""
+    """A closure failing more than max_retries is dropped (error on every rank) while the round's
+    successful closure is committed without being re-run; a round with one closure on two ranks
+    averages over that one worker; no optimizer step without contributors."""
     body = COMMON + """
 st = ParameterServerStrategy()
 m, o = make(st)
@@ -120,18 +121,22 @@ for rv in rvs:
         rv.fetch(); errs.append(None)
     except RuntimeError as e:
         errs.append("failed")
-# emulate: round 1 = {0, 1}: closure 1 dropped after 2 attempts -> round re-run as {0, 2}?
-# requeue keeps order: [0, 2] form the next round (rank 0 runs 0, rank 1 runs 2): mean of both.
+# round 1 = {rank 0: closure 0, rank 1: closure 1}: closure 1 fails twice (1 retry) and is dropped;
+# rank 0's pending gradient is kept (not recomputed) and committed alone; round 2 = {rank 0: closure 2}
 from pyspark_tf_gke_amd.nn import engine as E
 def grad(model, i):
+    model.store.grad_clean = False
     model.store.zero_grad()
     out = E.run_forward(model.ops, torch.from_numpy(X[i]), model.ws, True)
     d = model._loss_grad(out, torch.from_numpy(Y[i]), torch.zeros(8))
     E.run_backward(model.ops, d, model.ws)
     return model.store.flat_grad.clone()
-g0, g2 = grad(ref, 0), grad(ref, 2)
-ref.store.flat_grad.copy_(g0 + g2)
-ro.apply(ref.store, gscale=0.5)
+g0 = grad(ref, 0)
+ref.store.flat_grad.copy_(g0)
+ro.apply(ref.store, gscale=1.0)
+g2 = grad(ref, 2)
+ref.store.flat_grad.copy_(g2)
+ro.apply(ref.store, gscale=1.0)
 diff = float((m.store.flat - ref.store.flat).abs().max())
 # a 3-closure queue on 2 ranks with no failures: last round has one contributor
 m2, o2 = make(st)
@@ -154,7 +159,7 @@ print("RESULT", json.dumps({"errs": errs, "diff": diff, "it": o.iterations, "dif
     assert len(res) == 2
     for v in res.values():
         assert v["errs"] == [None, "failed", None], v
-        assert v["it"] == 1 and v["diff"] < 1e-6, v
+        assert v["it"] == 2 and v["diff"] < 1e-6, v
         assert v["it2"] == 2 and v["diff2"] < 1e-6, v
 
 
@@ -219,37 +224,131 @@ print("RESULT", json.dumps({"owners": sorted({p[3] for p in st.placement(m)}), "
     assert res[0]["owners"] == [0] and res[0]["sum"] == res[1]["sum"]
 
 
-def test_ps_async_applies_each_worker_gradient():
+def test_ps_async_single_active_worker_is_sequential_adam():
+    """Async PS: rank 1 arrives late, so rank 0 draws every closure; each push is applied by the
+    owners (both ranks' service threads) before apply_gradients returns and the next closure pulls,
+    so the result is exactly 8 sequential Adam steps."""
     body = COMMON + """
-st = ParameterServerStrategy(mode="async")
+import time
+st = ParameterServerStrategy(mode="async", variable_partitioner=MinSizePartitioner(min_shard_bytes=256, max_shards=4))
 m, o = make(st, lr=5e-3)
 ref, ro = make(st, lr=5e-3)
-W = st.world_size
 co = ClusterCoordinator(st)
-for i in range(2 * W):
+for i in range(8):
     co.schedule(step_fn, args=(m, o, i))
+if st.rank == 1:
+    time.sleep(1.5)
 co.join()
+st.synchronize_master(m)
 from pyspark_tf_gke_amd.nn import engine as E
-for rnd in range(2):
-    gs = []
-    for w in range(W):   # every worker of a round computed on the round-start values
-        ref.store.zero_grad()
-        out = E.run_forward(ref.ops, torch.from_numpy(X[rnd * W + w]), ref.ws, True)
-        d = ref._loss_grad(out, torch.from_numpy(Y[rnd * W + w]), torch.zeros(8))
-        E.run_backward(ref.ops, d, ref.ws)
-        gs.append(ref.store.flat_grad.clone())
-    for g in gs:         # ... and the PS applied them one after another, unaveraged
-        ref.store.flat_grad.copy_(g)
-        ro.apply(ref.store, gscale=1.0)
+for i in range(8):
+    ref.store.grad_clean = False
+    ref.store.zero_grad()
+    out = E.run_forward(ref.ops, torch.from_numpy(X[i]), ref.ws, True)
+    d = ref._loss_grad(out, torch.from_numpy(Y[i]), torch.zeros(8))
+    E.run_backward(ref.ops, d, ref.ws)
+    ro.apply(ref.store, gscale=1.0)
 diff = float((m.store.flat - ref.store.flat).abs().max())
-print("RESULT", json.dumps({"diff": diff, "it": o.iterations}), flush=True)
+owners = sorted({p[3] for p in st.placement(m)})
+print("RESULT", json.dumps({"diff": diff, "it": o.iterations, "ran": co.closures_run, "owners": owners}), flush=True)
+st.shutdown()
 """
     r = _launch(body, 2)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     res = _results(r.stdout)
     assert len(res) == 2
+    assert res[0]["ran"] == 8 and res[1]["ran"] == 0 and res[0]["owners"] == [0, 1], res
     for v in res.values():
-        assert v["diff"] < 1e-6 and v["it"] == 4, v
+        assert v["diff"] < 1e-6 and v["it"] == 8, v
+
+
+SLOW_BODY = COMMON + """
+import time
+mode = os.environ["PS_MODE"]
+st = ParameterServerStrategy(mode=mode)
+m, o = make(st, lr=1e-3)
+co = ClusterCoordinator(st)
+def slow_step(i):
+    if st.rank == 2:
+        time.sleep(0.1)        # the straggler: 100 ms per step
+    return step_fn(m, o, i % 16)
+comm_t = torch.zeros(1)
+from pyspark_tf_gke_amd.parallel import comm
+comm.barrier()
+t0 = time.time()
+for i in range(30):
+    co.schedule(slow_step, args=(i,))
+co.join()
+dt = time.time() - t0
+print("RESULT", json.dumps({"dt": dt, "ran": co.closures_run, "it": o.iterations}), flush=True)
+if mode == "async":
+    st.shutdown()
+"""
+
+
+def test_ps_async_slow_worker_does_not_stall_the_others():
+    """3 ranks, one sleeping 100 ms per step: the async coordinator hands the closures to the idle
+    workers, so the job ends in about the straggler's few steps, not in 10 lock-step rounds of
+    100 ms as the sync rounds do; every closure runs exactly once."""
+    ra = _launch(SLOW_BODY, 3, extra_env={"PS_MODE": "async"})
+    assert ra.returncode == 0, ra.stdout[-3000:] + ra.stderr[-3000:]
+    a = _results(ra.stdout)
+    rs = _launch(SLOW_BODY, 3, extra_env={"PS_MODE": "sync"})
+    assert rs.returncode == 0, rs.stdout[-3000:] + rs.stderr[-3000:]
+    s = _results(rs.stdout)
+    assert sum(v["ran"] for v in a.values()) == 30 and all(v["it"] == 30 for v in a.values()), a
+    assert a[2]["ran"] <= 4 < min(a[0]["ran"], a[1]["ran"]), a
+    dt_async, dt_sync = max(v["dt"] for v in a.values()), max(v["dt"] for v in s.values())
+    assert dt_sync >= 1.0, s
+    assert dt_async < 0.6 * dt_sync, (dt_async, dt_sync)
+
+
+def test_coordinator_retry_with_per_worker_iterators():
+    """The reference's closure (train_tf_ps.py:616-631,642): ``next(per_worker_iterator)`` inside the
+    scheduled step.  A closure that fails on rank 1 before drawing its batch is re-run there alone:
+    the other ranks' closures are neither re-run nor their iterators advanced twice, so the result is
+    bit-identical to the fault-free run and every rank consumed the same batches."""
+    body = COMMON + """
+from pyspark_tf_gke_amd.data.dataset import Dataset
+XA = torch.from_numpy(rng.normal(size=(96, 3)).astype(np.float32))
+YA = torch.from_numpy(rng.integers(0, 4, size=(96,)).astype(np.int32))
+def run(fail_calls):
+    st = ParameterServerStrategy()
+    m, o = make(st)
+    co = ClusterCoordinator(st, max_retries=2)
+    ds = co.create_per_worker_dataset(
+        lambda ctx: Dataset.from_tensor_slices((XA, YA)).shard(ctx.num_input_pipelines, ctx.input_pipeline_id).batch(8).repeat())
+    it = iter(ds)
+    calls, drawn = [0], []
+    def per_worker_train_step(iterator):
+        calls[0] += 1
+        if st.rank == 1 and calls[0] in fail_calls:
+            raise RuntimeError("injected worker failure")
+        x, y = next(iterator)
+        drawn.append(float(x.sum()))
+        with GradientTape() as tape:
+            loss = loss_fn(y, m(x, training=True))
+        o.apply_gradients(zip(tape.gradient(loss, m.trainable_variables), m.trainable_variables))
+        return 1
+    for epoch in range(2):
+        for _ in range(5):
+            co.schedule(per_worker_train_step, args=(it,))
+        co.join()
+    return flat(m), drawn, co.retries, calls[0], o.iterations
+a, da, _, ca, ia = run(set())
+b, db, rb, cb, ib = run({2, 4})
+print("RESULT", json.dumps({"same": bool(torch.equal(a, b)), "drawn_same": da == db, "retries": rb,
+                            "calls": [ca, cb], "it": [ia, ib]}), flush=True)
+"""
+    r = _launch(body, 3)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    res = _results(r.stdout)
+    assert len(res) == 3
+    for rank, v in res.items():
+        assert v["same"] and v["drawn_same"], v
+        assert v["retries"] == 2 and v["it"] == [4, 4], v
+        extra = 2 if rank == 1 else 0  # only the failed closures ran twice
+        assert v["calls"][1] == v["calls"][0] + extra, v
 
 
 RESUME_BODY = """

@@ -50,7 +50,7 @@ def main():
 
     lib = _native.hip_lib()
     K.BLASLT_DX = False
-    for bn in (-1, 0, 64, 80):
+    for bn in (-1, 0, 64, 80, 81, 82):
         lib.ptg_gemm_skinny_set(bn)
         res[f"dx_skinny{bn}"] = timeit(lambda: K.linear_dx(dy, w, dx))
         if bn == -1:
