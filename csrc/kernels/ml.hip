@@ -54,7 +54,8 @@ __global__ __launch_bounds__(256) void assemble_fill_k(AsmDesc d, long n, int D,
 // independent accumulators hide the 40-cycle MFMA latency.  The 16 candidate distances of a row
 // live on 16 lanes and are min-reduced with xor shuffles (ties -> lower center, as the scalar
 // loop).  Per-cluster sums/counts accumulate in LDS when k*D fits, else with global atomics;
-// zero features (one-hot blocks) are skipped either way.  No k or k*D limit; D <= KM_DMAX.
+// zero features (one-hot blocks) are skipped either way.  No k or k*D limit; D > KM_DMAX takes the
+// chunked variant below.
 // `done` (device flag) turns every launch of a converged fit into a no-op, so the host can queue
 // several iterations without reading the convergence test back (ml/clustering.py).
 // ------------------------------------------------------------------------------------------------
@@ -329,6 +330,220 @@ __global__ __launch_bounds__(256) void cluster_stats_k(const float* __restrict__
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// D > KM_DMAX (e.g. MEASURE_NAME_WEIGHT = 20 -> D = 623 in k_means.py:56-64, or wide assembled
+// vectors): the same exact-f32 MFMA assignment with the feature dimension tiled through LDS in
+// KM_DT-wide chunks.  Loop order per 64-row tile: for every 16-center block, the X tile is staged
+// chunk by chunk (from L2) and the x.c partial products accumulate in the two MFMA accumulators
+// across chunks, so the argmin sees complete dot products; ||x||^2 is accumulated during the first
+// block's pass.  Cluster sums take one more chunked pass with device atomics (k*D is large here).
+// ------------------------------------------------------------------------------------------------
+#define KM_DT 512
+
+PTG_DEV void km_stage_chunk(float* xs, int S, const float* __restrict__ X, long n, int D, long r0, int d0, int DPc,
+                            int dc) {
+  for (int t = threadIdx.x; t < KM_ROWS * DPc; t += 256) {
+    const int r = t / DPc, d = t - r * DPc;
+    xs[r * S + d] = (r0 + r < n && d < dc) ? X[(r0 + r) * D + d0 + d] : 0.f;
+  }
+}
+
+__global__ __launch_bounds__(256) void kmeans_chunk_k(const float* __restrict__ X, long n, int D,
+                                                      const float* __restrict__ C, const float* __restrict__ cn, int k,
+                                                      int* __restrict__ assign, float* __restrict__ mind,
+                                                      float* __restrict__ sums, float* __restrict__ counts,
+                                                      double* __restrict__ cost, const float* __restrict__ weights,
+                                                      const int* __restrict__ done) {
+  if (done && *done) return;
+  constexpr int S = KM_DT + 1;
+  __shared__ __align__(16) float xs[KM_ROWS * S];
+  __shared__ float sxn[KM_ROWS];
+  __shared__ int sarg[KM_ROWS];
+  __shared__ float sw[KM_ROWS];
+  __shared__ float scost[4];
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, g = l >> 4, c16 = l & 15;
+  double mycost = 0.0;
+  const long ntile = (n + KM_ROWS - 1) / KM_ROWS;
+  for (long tile = blockIdx.x; tile < ntile; tile += gridDim.x) {
+    const long r0 = tile * KM_ROWS;
+    if (tid < KM_ROWS) sxn[tid] = 0.f;
+    float best[4] = {INFINITY, INFINITY, INFINITY, INFINITY};
+    int arg[4] = {0, 0, 0, 0};
+    const float* xa = xs + (16 * w + c16) * S + g;
+    for (int cb = 0; cb < k; cb += 16) {
+      const int col = cb + c16;
+      const bool cv = col < k;
+      km_f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+      for (int d0 = 0; d0 < D; d0 += KM_DT) {
+        const int dc = min(KM_DT, D - d0), DPc = (dc + 7) / 8 * 8;
+        __syncthreads();
+        km_stage_chunk(xs, S, X, n, D, r0, d0, DPc, dc);
+        __syncthreads();
+        if (cb == 0 && tid < KM_ROWS) {
+          float xn = sxn[tid];
+          for (int d = 0; d < dc; ++d) xn = fmaf(xs[tid * S + d], xs[tid * S + d], xn);
+          sxn[tid] = xn;
+        }
+        const float* cp = C + (long)(cv ? col : 0) * D + d0 + g;
+        for (int e = 0; e < DPc; e += 8) {
+          const float b0 = (cv && e + g < dc) ? cp[e] : 0.f;
+          const float b1 = (cv && e + 4 + g < dc) ? cp[e + 4] : 0.f;
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[e], b0, acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[e + 4], b1, acc1, 0, 0, 0);
+        }
+      }
+      const float cc = cv ? cn[col] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float v = cv ? cc - 2.f * (acc0[i] + acc1[i]) : INFINITY;
+        int a = col;
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          const float ov = __shfl_xor(v, o, 64);
+          const int oa = __shfl_xor(a, o, 64);
+          if (ov < v || (ov == v && oa < a)) { v = ov; a = oa; }
+        }
+        if (v < best[i]) { best[i] = v; arg[i] = a; }
+      }
+    }
+    __syncthreads();  // sxn complete
+    if (c16 < 4) {
+      const int r = 16 * w + 4 * g + c16;
+      float bsel = best[0];
+      int asel = arg[0];
+#pragma unroll
+      for (int i = 1; i < 4; ++i)
+        if (c16 == i) { bsel = best[i]; asel = arg[i]; }
+      const long row = r0 + r;
+      float wt = 0.f;
+      if (row < n) {
+        const float dist = fmaxf(sxn[r] + bsel, 0.f);
+        wt = weights ? weights[row] : 1.f;
+        if (assign) assign[row] = asel;
+        if (mind) mind[row] = dist;
+        mycost += (double)dist * wt;
+      }
+      sarg[r] = asel;
+      sw[r] = wt;
+    }
+    if (sums) {
+      for (int d0 = 0; d0 < D; d0 += KM_DT) {
+        const int dc = min(KM_DT, D - d0), DPc = (dc + 7) / 8 * 8;
+        __syncthreads();
+        km_stage_chunk(xs, S, X, n, D, r0, d0, DPc, dc);
+        __syncthreads();
+        for (int rr = 0; rr < 16; ++rr) {
+          const int r = 16 * w + rr;
+          const float wt = sw[r];
+          if (wt == 0.f) continue;
+          const int a = sarg[r];
+          for (int d = l; d < dc; d += 64) {
+            const float v = xs[r * S + d] * wt;
+            if (v != 0.f) atomicAdd(&sums[(long)a * D + d0 + d], v);
+          }
+          if (l == 0 && d0 == 0) atomicAdd(&counts[a], wt);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  const float c32 = block_sum256((float)mycost, scost);
+  if (tid == 0 && cost) atomicAdd(cost, (double)c32);
+}
+
+__global__ __launch_bounds__(256) void silhouette_chunk_k(const float* __restrict__ X, const int* __restrict__ assign,
+                                                          const float* __restrict__ Sv, const float* __restrict__ Q,
+                                                          const float* __restrict__ cnt, long n, int D, int k,
+                                                          double* __restrict__ out) {
+  constexpr int S = KM_DT + 1;
+  __shared__ __align__(16) float xs[KM_ROWS * S];
+  __shared__ float sxn[KM_ROWS];
+  __shared__ float scr[4];
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, g = l >> 4, c16 = l & 15;
+  double acc = 0.0;
+  const long ntile = (n + KM_ROWS - 1) / KM_ROWS;
+  for (long tile = blockIdx.x; tile < ntile; tile += gridDim.x) {
+    const long r0 = tile * KM_ROWS;
+    if (tid < KM_ROWS) sxn[tid] = 0.f;
+    const float* xa = xs + (16 * w + c16) * S + g;
+    float a_own[4], bmin[4];
+    int own[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = 16 * w + 4 * g + i;
+      own[i] = r0 + r < n ? assign[r0 + r] : -1;
+      a_own[i] = 0.f;
+      bmin[i] = INFINITY;
+    }
+    // pass 0 computes ||x||^2 only (the distances need it for every center block)
+    for (int d0 = 0; d0 < D; d0 += KM_DT) {
+      const int dc = min(KM_DT, D - d0), DPc = (dc + 7) / 8 * 8;
+      __syncthreads();
+      km_stage_chunk(xs, S, X, n, D, r0, d0, DPc, dc);
+      __syncthreads();
+      if (tid < KM_ROWS) {
+        float xn = sxn[tid];
+        for (int d = 0; d < dc; ++d) xn = fmaf(xs[tid * S + d], xs[tid * S + d], xn);
+        sxn[tid] = xn;
+      }
+    }
+    __syncthreads();
+    float xn[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) xn[i] = sxn[16 * w + 4 * g + i];
+    for (int cb = 0; cb < k; cb += 16) {
+      const int col = cb + c16;
+      const bool cv = col < k;
+      km_f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+      for (int d0 = 0; d0 < D; d0 += KM_DT) {
+        const int dc = min(KM_DT, D - d0), DPc = (dc + 7) / 8 * 8;
+        __syncthreads();
+        km_stage_chunk(xs, S, X, n, D, r0, d0, DPc, dc);
+        __syncthreads();
+        const float* sp = Sv + (long)(cv ? col : 0) * D + d0 + g;
+        for (int e = 0; e < DPc; e += 8) {
+          const float b0 = (cv && e + g < dc) ? sp[e] : 0.f;
+          const float b1 = (cv && e + 4 + g < dc) ? sp[e + 4] : 0.f;
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[e], b0, acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[e + 4], b1, acc1, 0, 0, 0);
+        }
+      }
+      const float nc = cv ? cnt[col] : 0.f;
+      const float qc = cv ? Q[col] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float total = nc * xn[i] - 2.f * (acc0[i] + acc1[i]) + qc;
+        float v = INFINITY;
+        if (cv && nc > 0.f) {
+          if (col == own[i]) a_own[i] = nc > 1.f ? total / (nc - 1.f) : 0.f;
+          else v = total / nc;
+        }
+        float ao = (cv && col == own[i]) ? a_own[i] : -INFINITY;
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          v = fminf(v, __shfl_xor(v, o, 64));
+          ao = fmaxf(ao, __shfl_xor(ao, o, 64));
+        }
+        bmin[i] = fminf(bmin[i], v);
+        if (ao != -INFINITY) a_own[i] = ao;
+      }
+    }
+    if (c16 < 4) {
+      float a = a_own[0], b = bmin[0];
+      int o = own[0];
+#pragma unroll
+      for (int i = 1; i < 4; ++i)
+        if (c16 == i) { a = a_own[i]; b = bmin[i]; o = own[i]; }
+      if (o >= 0 && cnt[o] > 1.f && b < INFINITY) {
+        const float m = fmaxf(a, b);
+        acc += m > 0.f ? (double)((b - a) / m) : 0.0;
+      }
+    }
+  }
+  const float r = block_sum256((float)acc, scr);
+  if (threadIdx.x == 0) atomicAdd(out, (double)r);
+}
+
 static inline int grid_m(long n) {
   long g = (n + 255) / 256;
   if (g < 1) g = 1;
@@ -352,7 +567,15 @@ int ptg_assemble_features(const void* desc, long n, int D, void* out, hipStream_
 int ptg_kmeans_assign_accum(const void* X, const void* C, const void* cn, long n, int D, int k, void* assign,
                             void* sums, void* counts, void* cost, const void* weights, void* mind, const void* done,
                             hipStream_t s) {
-  if (D > KM_DMAX || D <= 0 || k <= 0) return (int)hipErrorInvalidValue;
+  if (D <= 0 || k <= 0) return (int)hipErrorInvalidValue;
+  if (D > KM_DMAX) {  // feature dimension tiled through LDS
+    const long tiles = (n + KM_ROWS - 1) / KM_ROWS;
+    const int g = (int)(tiles < 1 ? 1 : (tiles > 4096 ? 4096 : tiles));
+    hipLaunchKernelGGL(kmeans_chunk_k, dim3(g), dim3(256), 0, s, (const float*)X, n, D, (const float*)C,
+                       (const float*)cn, k, (int*)assign, (float*)mind, (float*)sums, (float*)counts, (double*)cost,
+                       (const float*)weights, (const int*)done);
+    PTG_RETURN_LAUNCH();
+  }
   const int DP = (D + 7) / 8 * 8;
   const long xs_bytes = (long)KM_ROWS * (DP + 1) * 4;
   const long acc_bytes = ((long)k * D + k) * 4;
@@ -404,7 +627,14 @@ int ptg_cluster_stats(const void* X, const void* assign, long n, int D, void* S,
 
 int ptg_silhouette(const void* X, const void* assign, const void* S, const void* Q, const void* cnt, long n, int D,
                    int k, void* out, hipStream_t s) {
-  if (D > KM_DMAX || D <= 0 || k <= 0) return (int)hipErrorInvalidValue;
+  if (D <= 0 || k <= 0) return (int)hipErrorInvalidValue;
+  if (D > KM_DMAX) {
+    const long tiles = (n + KM_ROWS - 1) / KM_ROWS;
+    const int g = (int)(tiles < 1 ? 1 : (tiles > 4096 ? 4096 : tiles));
+    hipLaunchKernelGGL(silhouette_chunk_k, dim3(g), dim3(256), 0, s, (const float*)X, (const int*)assign,
+                       (const float*)S, (const float*)Q, (const float*)cnt, n, D, k, (double*)out);
+    PTG_RETURN_LAUNCH();
+  }
   const int DP = (D + 7) / 8 * 8;
   const size_t lds = (size_t)KM_ROWS * (DP + 1) * 4;
   static bool attr = false;

@@ -746,7 +746,7 @@ def center_norms(C: torch.Tensor) -> torch.Tensor:
     return cn
 
 
-KMEANS_DMAX = 576  # KM_DMAX in ml.hip (feature tile of 64 rows staged in LDS)
+KMEANS_DMAX = 576  # KM_DMAX in ml.hip: above it the kernels tile the feature dimension through LDS
 
 
 def kmeans_assign_accum(X, C, assign=None, sums=None, counts=None, cost=None, weights=None, mind=None, cn=None,
@@ -755,8 +755,8 @@ def kmeans_assign_accum(X, C, assign=None, sums=None, counts=None, cost=None, we
     sums / counts / cost accumulation.  ``done``: device flag that makes the launch a no-op."""
     n, D = X.shape
     k = C.shape[0]
-    if not on_device(X) or D > KMEANS_DMAX:
-        if on_device(X) and done is not None and int(done.item()):
+    if not on_device(X):
+        if done is not None and int(done.reshape(-1)[0]):
             return
         Xd, Cd = X.double(), C.double()
         d = (Xd * Xd).sum(1)[:, None] - 2 * Xd @ Cd.t() + (Cd * Cd).sum(1)[None, :]
@@ -841,8 +841,6 @@ def silhouette_points(X, assign, S, Q, cnt) -> float:
         m = torch.maximum(a, b)
         s = torch.where((own_n > 1) & torch.isfinite(b) & (m > 0), (b - a) / m, torch.zeros_like(a))
         return float(s.sum())
-    if D > KMEANS_DMAX:
-        return silhouette_points(X.cpu(), assign.cpu(), S.cpu(), Q.cpu(), cnt.cpu())
     out = torch.zeros(1, dtype=torch.float64, device=X.device)
     hip("ptg_silhouette", ptr(X), ptr(assign), ptr(S), ptr(Q), ptr(cnt), n, D, k, ptr(out))
     return float(out.item())

@@ -90,12 +90,25 @@ class DataFrame:
             self._mat = P.run_task(self._src, self._pending, self.sparkSession)
         return self._mat
 
+    def _visible_names(self) -> list:
+        """Column names after the pending stage, without running it."""
+        if self._mat is not None:
+            return list(self._mat.names)
+        names = list(self._src.names)
+        for o in self._pending:
+            if o[0] == "with":
+                if o[1].lower() not in {n.lower() for n in names}:
+                    names.append(o[1])
+            elif o[0] == "select":
+                names = [n for n, _ in o[1]]
+        return names
+
     def _lazy(self, op) -> "DataFrame":
         from . import plan as P
 
-        names = {n.lower() for n in self._src.names} | {o[1].lower() for o in self._pending if o[0] == "with"}
-        node = op[1].node if op[0] == "filter" else op[2].node
-        missing = P.referenced_columns(node) - names
+        names = {n.lower() for n in self._visible_names()}
+        nodes = [op[1].node] if op[0] == "filter" else [c.node for _, c in op[1]] if op[0] == "select" else [op[2].node]
+        missing = set().union(*[P.referenced_columns(nd) for nd in nodes]) - names
         if missing:
             raise KeyError(f"Column '{sorted(missing)[0]}' does not exist. Available: {', '.join(sorted(names))}")
         base = self if self._mat is None else None
@@ -108,12 +121,14 @@ class DataFrame:
         from . import plan as P
 
         if comm.rank() == 0:
-            print(P.describe(self._pending if self._mat is None else []), flush=True)
+            text = getattr(self, "_plan_text", None)  # an aggregation computed by a fused scan
+            print(text if text and self._mat is not None else P.describe(self._pending if self._mat is None else []),
+                  flush=True)
 
     # ------------------------------------------------------------------ schema
     @property
     def columns(self):
-        return self._t.names
+        return self._visible_names()
 
     @property
     def schema(self) -> T.StructType:
@@ -271,6 +286,13 @@ class DataFrame:
                 return self._explode(base, name)
             if base[0] == "agg":
                 return self.agg(*cs)
+        if self._mat is None:
+            from . import plan as P
+
+            named = [(expr_name(c.node), c) for c in cs]
+            if all(P._inlinable(c.node) for _, c in named):
+                # projection of a pending stage: stays lazy (fused into the next task / aggregation)
+                return self._lazy(("select", named))
         out = {}
         for c in cs:
             name, cv = self._eval(c)
@@ -505,24 +527,74 @@ class DataFrame:
         return self._new(Table.concat([self._t, other._t.select(self.columns)]))
 
     def repartition(self, numPartitions=None, *cols) -> "DataFrame":  # noqa: N803
+        """``numPartitions`` partitions in total (default: spark.sql.shuffle.partitions with key
+        columns, else the current count), partition p living on rank p % world as a contiguous row
+        range of that rank's table (``_part_sizes``).  With columns: hash partitioning of the key
+        (partition = hash % n) through the bucketed shuffle, one exchange round per partition round;
+        without: rows spread round-robin over the ranks, then cut into that rank's share of equal
+        contiguous partitions.  Each partition is a task of partition-wise operations (one file per
+        partition on write)."""
+        from .shuffle import bucket_exchange, round_robin_shuffle, shuffle_partitions
+
         if isinstance(numPartitions, (str, Column)):
             cols = (numPartitions,) + cols
             numPartitions = None
-        d = self._new(self._t)
-        if cols and comm.world_size() > 1:
-            d = self._new(_shuffle_by_key(self._t, _group_keys(self, [_to_col(c) for c in cols])[0]))
-        elif numPartitions and comm.world_size() > 1:
-            from .shuffle import round_robin_shuffle
-
-            d = self._new(round_robin_shuffle(self._t))
-        if numPartitions:
-            d._num_partitions = int(numPartitions)
+        world, rank = comm.world_size(), comm.rank()
+        n = int(numPartitions) if numPartitions else (shuffle_partitions() if cols else self._num_partitions)
+        n = max(1, n)
+        t = self._t
+        if cols:
+            key = _group_keys(self, [_to_col(c) for c in cols])[0]
+            if world > 1:
+                pieces, sizes = [], []
+                for _, pt in bucket_exchange(t, key, n, coalesce=False):
+                    pieces.append(pt)
+                    sizes.append(pt.num_rows)
+                table = Table.concat(pieces) if pieces else t.take(torch.zeros(0, dtype=torch.int64, device=t.device))
+            else:
+                perm, counts = D.hash_partition(key, n)
+                table = t.take(perm)
+                sizes = [int(x) for x in counts.cpu().tolist()]
+        else:
+            table = round_robin_shuffle(t) if world > 1 else t
+            mine = len(range(rank, n, world))
+            sizes = [table.num_rows * (i + 1) // mine - table.num_rows * i // mine for i in range(mine)]
+        d = self._new(table)
+        d._num_partitions = n
+        d._part_sizes = sizes
         return d
 
     def coalesce(self, numPartitions: int) -> "DataFrame":  # noqa: N803
+        """Fewer partitions without a shuffle: adjacent local partitions are merged."""
         d = self._new(self._t)
-        d._num_partitions = min(self._num_partitions, int(numPartitions))
+        n = max(1, min(self._num_partitions, int(numPartitions)))
+        d._num_partitions = n
+        sizes = self.local_partition_sizes()
+        mine = max(1, len(range(comm.rank(), n, comm.world_size())))
+        if len(sizes) > mine:
+            step = len(sizes) / mine
+            d._part_sizes = [sum(sizes[int(i * step):int((i + 1) * step)]) for i in range(mine)]
+        else:
+            d._part_sizes = sizes
         return d
+
+    def local_partition_sizes(self) -> list:
+        """Row counts of this rank's partitions (contiguous ranges of its table, in order)."""
+        sizes = getattr(self, "_part_sizes", None)
+        n_rows = self._t.num_rows
+        if sizes is not None and sum(sizes) == n_rows:
+            return list(sizes)
+        mine = max(1, len(range(comm.rank(), max(1, self._num_partitions), comm.world_size())))
+        return [n_rows * (i + 1) // mine - n_rows * i // mine for i in range(mine)]
+
+    def local_partitions(self) -> list:
+        """This rank's partitions as Tables (views by row range, no copy of the data)."""
+        t = self._t
+        out, lo = [], 0
+        for sz in self.local_partition_sizes():
+            out.append(t.slice(lo, lo + sz))
+            lo += sz
+        return out
 
     def cache(self):
         """Materialise now (runs the pending narrow stage once) and keep the result resident."""
@@ -882,8 +954,118 @@ class GroupedData:
 
     def agg(self, *exprs) -> DataFrame:
         df = self.df
-        t = df._t
         aggs = self._aggs_from(exprs)
+        if df._mat is None and df._pending:
+            from . import plan as P
+
+            exprs_ok = all(P._inlinable(c.node) for c in self.cols) and all(
+                src is None or P._inlinable(src.node) for _, fn, src in aggs) and all(
+                fn not in ("first",) for _, fn, _ in aggs)
+            if exprs_ok and P.fusable(df._pending):
+                return self._agg_fused(aggs)
+        return self._agg_table(df, aggs)
+
+    def _agg_fused(self, aggs) -> DataFrame:
+        """The aggregation consumes the pending stage in one fused scan (sql/plan.py): projections
+        inlined, one predicate mask; a global aggregate reduces under the mask, a grouped one
+        compacts once and gathers only the source columns its expressions read."""
+        from . import plan as P
+
+        df = self.df
+        src = df._src
+        inl = P.Inlined(df._pending)
+        P.STATS["fused_aggs"] += 1
+        base = DataFrame(src, df.sparkSession)
+        mask = None
+        if inl.cond is not None:
+            mask = base._mask(Column(inl.cond))
+            P.STATS["vm_passes"] += 1
+        text = P.describe_fused_agg(df._pending, self.cols, aggs)
+        if not self.cols:
+            out = self._agg_global(aggs, lambda c: base._eval(Column(inl.expr(c.node)), expr_name(c.node)), mask,
+                                   src)
+            out._plan_text = text
+            return out
+        # grouped: compact once, gather only the source columns the key / value expressions read
+        nodes = [inl.expr(c.node) for c in self.cols] + [inl.expr(s.node) for _, _, s in aggs if s is not None]
+        leaves = set()
+        for nd in nodes:
+            leaves |= C.referenced_columns(nd)
+        keep = [n for n in src.names if n in leaves or n.lower() in {x.lower() for x in leaves}]
+        pruned = src.select(keep)
+        if mask is not None:
+            pruned = pruned.take(D.compact(mask))
+            P.STATS["compactions"] += 1
+            P.STATS["gathers"] += 1
+        pdf = DataFrame(pruned, df.sparkSession)
+        pdf._num_partitions = df._num_partitions
+        keys = [Column(("alias", expr_name(c.node), inl.expr(c.node))) for c in self.cols]
+        aggs2 = [(label, fn, None if s is None else Column(inl.expr(s.node))) for label, fn, s in aggs]
+        out = GroupedData(pdf, keys)._agg_table(pdf, aggs2)
+        out._plan_text = text
+        return out
+
+    def _agg_global(self, aggs, evalf, mask, t) -> DataFrame:
+        """Global aggregates of value columns ``evalf(src)`` restricted to the rows of ``mask``."""
+        df = self.df
+        sess = df.sparkSession
+        world = comm.world_size()
+        vals = {}
+
+        def masked(cv):
+            if mask is None:
+                return cv
+            v = cv.valid_u8() if cv.valid is not None else None
+            m = mask if v is None else (mask & v)
+            return ColumnVector(cv.data, cv.dtype, m, cv.dictionary)
+
+        nrows = None
+        for label, fn, src in aggs:
+            if src is None:
+                if nrows is None:
+                    local = int(mask.sum()) if mask is not None else t.num_rows
+                    nrows = comm.all_reduce_int([local])[0]
+                vals[label] = nrows
+                continue
+            _, cv = evalf(src)
+            cv = masked(cv)
+            if fn == "count_distinct":
+                k, null = _key_of(cv)
+                ok = cv.valid_bool() if null is None else (cv.valid_bool() & ~null)
+                loc = torch.unique(k[ok])
+                vals[label] = int(comm.all_gather_unique(loc).numel()) if world > 1 else int(loc.numel())
+                continue
+            s_, c, mn, mx, nul = _global_stats(cv)
+            if fn == "count":
+                vals[label] = comm.all_reduce_int([int(cv.valid_bool().sum())])[0]
+            elif fn == "sum":
+                vals[label] = s_ if c else None
+            elif fn == "avg":
+                vals[label] = s_ / c if c else None
+            elif fn == "min":
+                vals[label] = mn if c else None
+            elif fn == "max":
+                vals[label] = mx if c else None
+            elif fn == "stddev":
+                mean = s_ / c if c else 0.0
+                x = cv.data.double()
+                ok = cv.valid_bool() & ~torch.isnan(x)
+                d2 = comm.all_reduce_float([float(((x - mean) ** 2)[ok].sum())])[0]
+                vals[label] = math.sqrt(d2 / (c - 1)) if c > 1 else None
+            else:
+                raise ValueError(f"unsupported aggregate {fn}")
+        data = [tuple(vals.values())] if comm.rank() == 0 else []
+        schema = []
+        for (label, fn, src), v in zip(aggs, vals.values()):
+            dt = T.LongType() if fn in ("count", "count_distinct") else T.DoubleType()
+            if fn in ("min", "max", "sum") and src is not None:
+                st = evalf(src)[1].dtype
+                dt = st if fn != "sum" or isinstance(st, (T.DoubleType, T.FloatType)) else T.LongType()
+            schema.append(T.StructField(label, dt))
+        return sess.createDataFrame(data, T.StructType(schema), _local=True)
+
+    def _agg_table(self, df, aggs) -> DataFrame:
+        t = df._t
         sess = df.sparkSession
         world = comm.world_size()
         if not self.cols:  # global aggregation -> one row on rank 0
@@ -947,23 +1129,37 @@ class GroupedData:
         vvalid = [cv.valid_u8() for cv in value_cols]
         ukeys, rows, outs = _hash_agg_all(key, vdata, vvalid, need_minmax)
         if world > 1:
-            # shuffle partials to the key owner (RCCL all-to-all-v) and merge them
+            # shuffle the partials to the key owners in spark.sql.shuffle.partitions hash buckets, one
+            # reduce partition per round (RCCL all-to-all-v), and merge each received bucket as its
+            # own reduce task: staging per round ~ 1/buckets of the partials
+            from .shuffle import bucket_exchange, shuffle_partitions
+
             part_cols = {"__k": ColumnVector(ukeys, T.LongType()), "__rows": ColumnVector(rows, T.DoubleType())}
             for j, (s, c, mn, mx) in enumerate(outs):
                 part_cols[f"__s{j}"] = ColumnVector(s, T.DoubleType())
                 part_cols[f"__c{j}"] = ColumnVector(c, T.DoubleType())
                 part_cols[f"__mn{j}"] = ColumnVector(mn, T.DoubleType())
                 part_cols[f"__mx{j}"] = ColumnVector(mx, T.DoubleType())
-            pt = _shuffle_by_key(Table(part_cols, ukeys.numel(), t.device), ukeys)
-            k2 = pt.column("__k").data
-            vals2 = [pt.column("__rows").data]
-            for j in range(len(outs)):
-                vals2 += [pt.column(f"__s{j}").data, pt.column(f"__c{j}").data, pt.column(f"__mn{j}").data,
-                          pt.column(f"__mx{j}").data]
-            uk2, _, o2 = _hash_agg_all(k2, vals2, [None] * len(vals2), need_minmax)
-            ukeys = uk2
-            rows = o2[0][0]
-            outs = [(o2[1 + 4 * j][0], o2[2 + 4 * j][0], o2[3 + 4 * j][2], o2[4 + 4 * j][3]) for j in range(len(outs))]
+            ks, rs, os_ = [], [], []
+            for _, pt in bucket_exchange(Table(part_cols, ukeys.numel(), t.device), ukeys, shuffle_partitions()):
+                if pt.num_rows == 0:
+                    continue
+                k2 = pt.column("__k").data
+                vals2 = [pt.column("__rows").data]
+                for j in range(len(outs)):
+                    vals2 += [pt.column(f"__s{j}").data, pt.column(f"__c{j}").data, pt.column(f"__mn{j}").data,
+                              pt.column(f"__mx{j}").data]
+                uk2, _, o2 = _hash_agg_all(k2, vals2, [None] * len(vals2), need_minmax)
+                ks.append(uk2)
+                rs.append(o2[0][0])
+                os_.append([(o2[1 + 4 * j][0], o2[2 + 4 * j][0], o2[3 + 4 * j][2], o2[4 + 4 * j][3])
+                            for j in range(len(outs))])
+            if ks:
+                ukeys, rows = torch.cat(ks), torch.cat(rs)
+                outs = [tuple(torch.cat([o[j][q] for o in os_]) for q in range(4)) for j in range(len(outs))]
+            else:
+                ukeys, rows = ukeys[:0], rows[:0]
+                outs = [tuple(x[:0] for x in o) for o in outs]
         cols = dict(decode(ukeys))
         j = 0
         for label, fn, src in aggs:

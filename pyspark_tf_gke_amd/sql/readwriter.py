@@ -14,7 +14,8 @@
   all-rows-in-partition-0 skew).  Without a database file, ``dbtable`` resolves to an
   exported CSV/Parquet file (``url`` = ``file:<dir>`` or option ``path``).
 * Parquet (pyarrow for the file format only), text, JSON lines.
-* Writer: one ``part-<rank>-<uuid>.parquet`` / ``.csv`` per rank + ``_SUCCESS``; modes
+* Writer: one ``part-<partition>-<uuid>.parquet`` / ``.csv`` per non-empty partition (a write task;
+  partition p lives on rank p % world) + ``_SUCCESS``; modes
   overwrite / append / error / ignore.
 """
 from __future__ import annotations
@@ -487,6 +488,18 @@ class DataFrameWriter:
     def save(self, path=None):
         return getattr(self, self._fmt)(path or self._opts.get("path"))
 
+    def _tasks(self):
+        """(global partition index, Table) of this rank's non-empty partitions - one write task and
+        one output file per partition, as Spark writes them (partition p lives on rank p % world).
+        A rank whose partitions are all empty writes one empty file when it is rank 0 (the schema)."""
+        df = self._df
+        world, rank = comm.world_size(), comm.rank()
+        parts = df.local_partitions()
+        out = [(rank + i * world, t) for i, t in enumerate(parts) if t.num_rows]
+        if not out and rank == 0:
+            out = [(0, df._t)]
+        return out
+
     def parquet(self, path, mode=None, compression="snappy"):
         import pyarrow.parquet as pq
 
@@ -494,9 +507,9 @@ class DataFrameWriter:
             self._mode = mode
         if not self._prepare(path):
             return
-        at = table_to_arrow(self._df._t)
-        pq.write_table(at, os.path.join(path, f"part-{comm.rank():05d}-{uuid.uuid4().hex[:12]}.{compression}.parquet"),
-                       compression=compression)
+        for p, t in self._tasks():
+            pq.write_table(table_to_arrow(t), os.path.join(path, f"part-{p:05d}-{uuid.uuid4().hex[:12]}.{compression}.parquet"),
+                           compression=compression)
         self._finish(path)
 
     def csv(self, path, mode=None, header=None):
@@ -507,12 +520,13 @@ class DataFrameWriter:
         hdr = DataFrameReader._truthy(header if header is not None else self._opts.get("header", False))
         import csv as pycsv
 
-        with open(os.path.join(path, f"part-{comm.rank():05d}-{uuid.uuid4().hex[:12]}.csv"), "w", newline="") as fh:
-            w = pycsv.writer(fh)
-            if hdr:
-                w.writerow(self._df.columns)
-            for row in self._df._t.rows():
-                w.writerow(["" if v is None else v for v in row])
+        for p, t in self._tasks():
+            with open(os.path.join(path, f"part-{p:05d}-{uuid.uuid4().hex[:12]}.csv"), "w", newline="") as fh:
+                w = pycsv.writer(fh)
+                if hdr:
+                    w.writerow(self._df.columns)
+                for row in t.rows():
+                    w.writerow(["" if v is None else v for v in row])
         self._finish(path)
 
     def json(self, path, mode=None):
@@ -521,8 +535,9 @@ class DataFrameWriter:
         if not self._prepare(path):
             return
         names = self._df.columns
-        with open(os.path.join(path, f"part-{comm.rank():05d}-{uuid.uuid4().hex[:12]}.json"), "w") as fh:
-            for row in self._df._t.rows():
-                fh.write(json.dumps({k: (list(map(float, v)) if hasattr(v, "toArray") else v)
-                                     for k, v in zip(names, row)}) + "\n")
+        for p, t in self._tasks():
+            with open(os.path.join(path, f"part-{p:05d}-{uuid.uuid4().hex[:12]}.json"), "w") as fh:
+                for row in t.rows():
+                    fh.write(json.dumps({k: (list(map(float, v)) if hasattr(v, "toArray") else v)
+                                         for k, v in zip(names, row)}) + "\n")
         self._finish(path)

@@ -7,7 +7,11 @@ these blocks over the pod network, spark_session.py:80-83 sizes their memory).
   whole table), in as many rounds as the staging budget requires — ``spark.ptg.shuffle.buffer.gb``
   (deploy/node.yaml) bounds the bytes staged per direction per round, and every rank runs the same
   number of rounds (one all-reduce MAX of the round count);
-* received chunks land directly in their final place of the output columns.
+* received chunks land directly in their final place of the output columns;
+* ``spark.sql.shuffle.partitions`` (spark_installation_check.py:16) is the number of hash buckets of
+  a keyed shuffle (:func:`bucket_exchange`): bucket b belongs to rank b % world and the exchange
+  runs one reduce partition per round (round r moves bucket r * world + d to rank d), so each round
+  stages ~1/buckets of the data and the consumer runs one reduce task per received bucket.
 
 :data:`STATS` records the peak staging of the last shuffle (tests assert it stays under budget).
 """
@@ -24,7 +28,7 @@ from .table import ColumnVector, Table
 from .. import config
 
 DEFAULT_BUDGET_GB = 64.0  # deploy/node.yaml spark.ptg.shuffle.buffer.gb
-STATS: dict = {"peak_staging_bytes": 0, "rounds": 0, "count_exchanges": 0}
+STATS: dict = {"peak_staging_bytes": 0, "rounds": 0, "count_exchanges": 0, "buckets": 0, "reduce_tasks": 0}
 
 
 def budget_bytes() -> int:
@@ -126,3 +130,88 @@ def round_robin_shuffle(t: Table, budget: int | None = None) -> Table:
     counts = torch.bincount(part.long(), minlength=world).to(torch.int64)
     perm = D.partition_perm(part, counts)
     return shuffle_table(t, perm, counts, budget)
+
+
+def shuffle_partitions(default: int = 200) -> int:
+    """``spark.sql.shuffle.partitions`` of the active session (Spark's default 200)."""
+    from .session import SparkSession
+
+    sess = SparkSession.getActiveSession()
+    try:
+        return max(1, int(getattr(sess, "shuffle_partitions", default) if sess is not None else default))
+    except (TypeError, ValueError):
+        return default
+
+
+def _aqe_advisory_bytes() -> int:
+    """Adaptive coalescing of small shuffle partitions (Spark 3's ``spark.sql.adaptive.enabled``,
+    default on, ``spark.sql.adaptive.advisoryPartitionSizeInBytes`` default 64 MB): 0 = off."""
+    from .session import SparkSession
+
+    sess = SparkSession.getActiveSession()
+    conf = sess.conf if sess is not None else None
+    get = (lambda k, d: conf.get(k, d)) if conf is not None else (lambda k, d: d)
+    if str(get("spark.sql.adaptive.enabled", "true")).lower() in ("false", "0", "no"):
+        return 0
+    if str(get("spark.sql.adaptive.coalescePartitions.enabled", "true")).lower() in ("false", "0", "no"):
+        return 0
+    raw = str(get("spark.sql.adaptive.advisoryPartitionSizeInBytes", str(64 << 20))).strip().lower()
+    mult = {"k": 1 << 10, "kb": 1 << 10, "m": 1 << 20, "mb": 1 << 20, "g": 1 << 30, "gb": 1 << 30}
+    for suf in ("kb", "mb", "gb", "k", "m", "g"):
+        if raw.endswith(suf):
+            return int(float(raw[: -len(suf)]) * mult[suf])
+    return int(float(raw))
+
+
+def bucket_exchange(t: Table, key: torch.Tensor, nbuckets: int, budget: int | None = None, coalesce: bool = True):
+    """Keyed shuffle in ``nbuckets`` hash buckets: bucket b belongs to rank b % world; yields
+    ``(buckets, rows of those buckets from every rank)`` per reduce task of this rank, in bucket
+    order.  A reduce round moves bucket-round rr (buckets rr * world + d to rank d); with adaptive
+    coalescing on, consecutive bucket-rounds are merged until a round holds the advisory partition
+    size (one reduce task then reads several buckets, as Spark's coalesced shuffle partitions do).
+    Collective: every rank iterates the generator to the end."""
+    world, rank = comm.world_size(), comm.rank()
+    perm, counts = D.hash_partition(key, nbuckets)
+    ch = [int(x) for x in counts.cpu().tolist()]
+    starts = [0] * nbuckets
+    for b in range(1, nbuckets):
+        starts[b] = starts[b - 1] + ch[b - 1]
+    nrr = -(-nbuckets // world)
+    row_bytes = sum(_row_bytes(cv) for cv in t.columns.values()) or 1
+    advisory = _aqe_advisory_bytes() if coalesce else 0
+    if advisory > 0 and nrr > 1:
+        glob = comm.all_reduce_int(ch)  # global rows per bucket (one collective, tensors)
+        per_rr = [sum(glob[rr * world + d] for d in range(world) if rr * world + d < nbuckets) * row_bytes
+                  for rr in range(nrr)]
+        groups, cur, acc = [], [], 0
+        for rr in range(nrr):
+            cur.append(rr)
+            acc += per_rr[rr]
+            if acc >= advisory:
+                groups.append(cur)
+                cur, acc = [], 0
+        if cur:
+            groups.append(cur)
+    else:
+        groups = [[rr] for rr in range(nrr)]
+    peak = 0
+    for g in groups:
+        sel, sc = [], []
+        for d in range(world):
+            n_d = 0
+            for rr in g:
+                b = rr * world + d
+                if b < nbuckets and ch[b]:
+                    sel.append(perm[starts[b]: starts[b] + ch[b]])
+                    n_d += ch[b]
+            sc.append(n_d)
+        idx = torch.cat(sel) if sel else perm[:0]
+        out = shuffle_table(t, idx, torch.tensor(sc, dtype=torch.int64), budget)
+        peak = max(peak, STATS["peak_staging_bytes"])
+        STATS["reduce_tasks"] += 1
+        mine = [rr * world + rank for rr in g if rr * world + rank < nbuckets]
+        if mine:
+            yield mine, out
+    STATS["peak_staging_bytes"] = peak
+    STATS["buckets"] = nbuckets
+    STATS["rounds"] = len(groups)

@@ -388,11 +388,14 @@ def test_dataframe_orderby_gpu_vs_host(spark_gpu):
     assert run(spark_gpu) == _host(run)
 
 
-@pytest.mark.parametrize("n,k,Dm", [(20_000, 100, 153), (7_777, 5, 3), (30_000, 300, 300), (5_000, 40, 600)])
+@pytest.mark.parametrize("n,k,Dm", [(20_000, 100, 153), (7_777, 5, 3), (30_000, 300, 300), (5_000, 40, 600),
+                                    (6_000, 25, 623), (4_000, 25, 2048), (3_000, 7, 1031)])
 def test_kmeans_mfma_assign_matches_host(hip_built, n, k, Dm):
     """Fused MFMA assignment vs the fp64 host formula: same argmin wherever the best two centers
     are not within f32 rounding, sums/counts/cost to f32 accuracy.  (300 x 300 exceeds the LDS
-    accumulator -> global-atomic path; D = 600 > KM_DMAX -> device fallback.)"""
+    accumulator -> global-atomic path; D > KM_DMAX = 576 -> the feature dimension tiled through
+    LDS in 512-wide chunks: D = 623 is k_means.py with MEASURE_NAME_WEIGHT = 20, 1031 a ragged
+    last chunk.)"""
     g = torch.Generator().manual_seed(k)
     X = torch.randn(n, Dm, generator=g)
     X[:, : Dm // 3] = (X[:, : Dm // 3] > 1.0).float()  # one-hot-like sparse block (skipped zeros)
@@ -452,8 +455,9 @@ def test_kmeans_fit_k100_d153_vs_host_and_sklearn(spark_gpu):
     assert sum(mg.summary.clusterSizes) == n
 
 
-def test_silhouette_mfma_matches_host(hip_built):
-    n, k, Dm = 9_000, 37, 153
+@pytest.mark.parametrize("n,k,Dm", [(9_000, 37, 153), (5_000, 25, 623), (3_000, 9, 2048)])
+def test_silhouette_mfma_matches_host(hip_built, n, k, Dm):
+    """Silhouette sum on the matrix cores (D-chunked above 576 features) vs the fp64 host formula."""
     g = torch.Generator().manual_seed(1)
     X = torch.randn(n, Dm, generator=g)
     a = torch.randint(0, k, (n,), generator=g, dtype=torch.int32)
@@ -464,6 +468,42 @@ def test_silhouette_mfma_matches_host(hip_built):
     tg = D.silhouette_points(X.cuda(), a.cuda(), Sg, Qg, cg)
     th = D.silhouette_points(X, a, Sh, Qh, ch)
     assert abs(tg - th) <= 1e-3 * max(1.0, abs(th))
+
+
+@pytest.mark.parametrize("weight", [20, 66])
+def test_kmeans_fit_wide_features_vs_host_and_sklearn(spark_gpu, weight):
+    """k_means.py's feature weighting (k_means.py:56-64): the 31-wide one-hot repeated
+    MEASURE_NAME_WEIGHT times + 3 numeric columns -> D = 623 (weight 20) / 2049 (weight 66), on the
+    HIP path end to end (no host fallback above 576 features): cost vs the host executor, and a
+    scikit-learn Lloyd step from our centers finds (almost) nothing to improve."""
+    from sklearn.cluster import KMeans as SKM
+
+    from pyspark_tf_gke_amd.ml import ClusteringEvaluator, KMeans
+    from pyspark_tf_gke_amd.sql import types as T
+    from pyspark_tf_gke_amd.sql.dataframe import DataFrame
+    from pyspark_tf_gke_amd.sql.table import ColumnVector, Table
+
+    g = torch.Generator().manual_seed(7)
+    n, V = 6_000, 31
+    Dm = V * weight + 3
+    codes = torch.randint(0, 30, (n,), generator=g)
+    X = torch.zeros(n, Dm)
+    for r in range(weight):
+        X[torch.arange(n), r * V + codes] = 1.0
+    X[:, -3:] = torch.randn(n, 3, generator=g) * 3 + codes[:, None].float()
+
+    def fit(dev):
+        df = DataFrame(Table({"features": ColumnVector(X.to(dev), T.VectorUDT())}, n, dev), spark_gpu)
+        m = KMeans(k=25, seed=1, maxIter=20, initMode="random").fit(df)
+        sil = ClusteringEvaluator().evaluate(m.transform(df))
+        return m, sil
+
+    (mg, sg), (mh, sh) = fit("cuda"), fit("cpu")
+    assert abs(mg.summary.trainingCost - mh.summary.trainingCost) <= 1e-3 * mh.summary.trainingCost
+    assert abs(sg - sh) <= 2e-3
+    sk = SKM(n_clusters=25, init=np.asarray(mg.clusterCenters()), n_init=1, max_iter=1).fit(X.numpy().astype(np.float64))
+    assert mg.summary.trainingCost <= sk.inertia_ * 1.01
+    assert sum(mg.summary.clusterSizes) == n
 
 
 @pytest.mark.parametrize("lo,span", [(-3_000_000_000, 4_000_000_000), (1 << 40, (1 << 32) - 2), (-(1 << 62), 1 << 62)])

@@ -327,3 +327,53 @@ def torch_load(path):
     import torch
 
     return torch.load(str(path), weights_only=True)
+
+
+SHUFFLE_PARTS_BODY = """
+import json, torch
+from pyspark_tf_gke_amd.sql import SparkSession
+from pyspark_tf_gke_amd.sql.functions import col, count, sum as fsum
+from pyspark_tf_gke_amd.sql import shuffle as SH
+from pyspark_tf_gke_amd.parallel import comm
+out = {}
+for parts in (2, 64):
+    spark = (SparkSession.builder.master("spark://127.0.0.1:7077").config("spark.sql.shuffle.partitions", str(parts))
+             .config("spark.sql.adaptive.enabled", "false").getOrCreate())
+    r = comm.rank()
+    rows = [((i * 7919 + r) % 5000, float(i % 97), i % 11) for i in range(20000)]
+    df = spark.createDataFrame(rows, ["k", "v", "w"])
+    t0 = dict(SH.STATS)
+    g = df.groupBy("k").agg(fsum("v").alias("s"), count("*").alias("n"))
+    res = sorted((int(a), float(b), int(c)) for a, b, c in g.collect())
+    out[parts] = {"res": res, "peak": SH.STATS["peak_staging_bytes"], "buckets": SH.STATS["buckets"],
+                  "rounds": SH.STATS["rounds"], "tasks": SH.STATS["reduce_tasks"] - t0["reduce_tasks"],
+                  "rp": len(df.repartition(6, "k").local_partition_sizes())}
+    spark.stop()
+# AQE on (default): the 64 small buckets coalesce into few reduce rounds
+spark = (SparkSession.builder.master("spark://127.0.0.1:7077").config("spark.sql.shuffle.partitions", "64")
+         .config("spark.sql.adaptive.enabled", "true").getOrCreate())
+rows = [((i * 7919 + comm.rank()) % 5000, float(i % 97), i % 11) for i in range(20000)]
+spark.createDataFrame(rows, ["k", "v", "w"]).groupBy("k").agg(fsum("v")).collect()
+aqe_rounds = SH.STATS["rounds"]
+print("RESULT", json.dumps({"same": out[2]["res"] == out[64]["res"], "n": len(out[2]["res"]),
+                            "peak2": out[2]["peak"], "peak64": out[64]["peak"], "b": [out[2]["buckets"], out[64]["buckets"]],
+                            "rounds": [out[2]["rounds"], out[64]["rounds"]], "aqe_rounds": aqe_rounds,
+                            "rp": out[2]["rp"]}), flush=True)
+"""
+
+
+def test_shuffle_partitions_bucket_the_groupby_exchange():
+    """spark.sql.shuffle.partitions = number of hash buckets of the groupBy exchange, one reduce
+    round per bucket pair: 2 vs 64 give identical results, the 64-bucket run stages far less per
+    round; with adaptive execution on, small buckets coalesce into fewer rounds; repartition(6, k)
+    leaves 3 partitions on each of the 2 ranks."""
+    r = _run_ranks(SHUFFLE_PARTS_BODY, nproc=2, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    res = _results(r.stdout)
+    assert len(res) == 2
+    for v in res.values():
+        assert v["same"] and v["n"] == 5000, v
+        assert v["b"] == [2, 64] and v["rounds"] == [1, 32], v
+        assert v["peak64"] * 8 < v["peak2"], v
+        assert v["aqe_rounds"] < 32, v
+        assert v["rp"] == 3, v

@@ -18,8 +18,9 @@ def test_joint_single_rank(tmp_path, handoff):
                     master="local[2]", verbose=False)
     assert 5500 < rep["rows_after_etl"] <= 6000  # ~2% null values filtered
     files = [f for f in os.listdir(os.path.join(out, "etl.parquet")) if f.endswith(".parquet")]
-    assert len(files) == 1 and os.path.exists(os.path.join(out, "etl.parquet", "_SUCCESS"))
-    t = pq.read_table(os.path.join(out, "etl.parquet", files[0]))
+    # local[2]: spark.default.parallelism = 2 partitions -> one write task and one file each
+    assert len(files) == 2 and os.path.exists(os.path.join(out, "etl.parquet", "_SUCCESS"))
+    t = pq.read_table(os.path.join(out, "etl.parquet"))
     assert t.column_names == ["f0", "f1", "f2", "label"] and t.num_rows == rep["rows_after_etl"]
     f0 = t.column("f0").to_numpy()
     assert abs(f0.mean()) < 0.05 and abs(f0.std() - 1) < 0.05  # standardised

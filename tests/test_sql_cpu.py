@@ -301,3 +301,123 @@ def test_distinct_estimate_widens_at_most_to_the_cap(monkeypatch):
     small = torch.randint(0, 300, (1 << 20,), generator=torch.Generator().manual_seed(0))
     assert 250 <= D.estimate_distinct(small, sample=1 << 10) <= 400
     assert len(seen) == 1
+
+
+def test_kmeans_chain_is_one_fused_scan(spark, capsys):
+    """k_means.py:23-51 on health.csv: filter(measure_name not null) -> per column
+    select(c).filter(~isnan & not null).agg(avg) -> withColumn(when(...)) imputation.  Every
+    avg runs as ONE fused scan of the source (projections inlined, one predicate pass, masked
+    reduction: no compaction or row gather), explain() shows it, and the numbers equal the
+    materialise-everything evaluation."""
+    from pyspark_tf_gke_amd.sql import plan as P
+
+    src = spark.read.csv(HEALTH, header=True, inferSchema=True).cache()
+    df = src.filter(col("measure_name").isNotNull())
+    means, ref = {}, {}
+    before = dict(P.STATS)
+    for c in ["value", "lower_ci", "upper_ci"]:
+        q = df.select(c).filter(~isnan(col(c)) & col(c).isNotNull()).agg({c: "avg"})
+        means[c] = q.collect()[0][0]
+        df = df.withColumn(c, when(col(c).isNull() | isnan(col(c)), means[c]).otherwise(col(c)))
+    q.explain()
+    out = capsys.readouterr().out
+    assert "one fused scan" in out and "masked reduction" in out and "measure_name IS NOT NULL" in out, out
+    assert P.STATS["fused_aggs"] - before["fused_aggs"] == 3
+    assert P.STATS["compactions"] - before["compactions"] == 0 and P.STATS["gathers"] - before["gathers"] == 0
+    assert P.STATS["tasks"] - before["tasks"] == 0  # nothing materialised
+    # reference: pandas on the same rows
+    pdf = pd.read_csv(HEALTH)
+    pdf = pdf[pdf["measure_name"].notna()]
+    for c in ["value", "lower_ci", "upper_ci"]:
+        ref[c] = float(pdf[c].dropna().mean())
+        pdf[c] = pdf[c].fillna(ref[c])
+        assert abs(means[c] - ref[c]) <= 1e-9 * max(1.0, abs(ref[c])), (c, means[c], ref[c])
+    # the imputed frame is still a pending stage: its aggregate inlines the CASE WHEN imputation
+    fin = df.agg(avg("upper_ci"))
+    fin.explain()
+    assert "CASE WHEN" in capsys.readouterr().out
+    got = fin.collect()[0][0]
+    assert abs(got - float(pdf["upper_ci"].mean())) < 1e-9 * max(1.0, abs(got))
+
+
+def test_grouped_agg_over_pending_stage_prunes_columns(spark, capsys):
+    """filter -> withColumn -> groupBy.agg: one predicate pass, one compaction, and a gather of only
+    the source columns the key / value expressions read (pruned), equal to the materialised path."""
+    from pyspark_tf_gke_amd.sql import plan as P
+
+    rows = [(i % 13, float(i), "x" * (i % 3), i * 2) for i in range(5000)]
+    df = spark.createDataFrame(rows, ["k", "v", "s", "w"])
+    before = dict(P.STATS)
+    q = (df.filter(col("v") > 100).withColumn("v2", col("v") * 2 + col("k"))
+         .filter(col("w") % 3 != 0).groupBy("k").agg(fsum("v2").alias("t"), count("*").alias("n")))
+    got = sorted(tuple(r) for r in q.collect())
+    assert P.STATS["fused_aggs"] - before["fused_aggs"] == 1 and P.STATS["compactions"] - before["compactions"] == 1
+    assert P.STATS["tasks"] - before["tasks"] == 0
+    q.explain()
+    out = capsys.readouterr().out
+    assert "pruned: k, v" in out and "w" not in out.split("pruned:")[1].split("]")[0].split(", ")
+    pdf = pd.DataFrame(rows, columns=["k", "v", "s", "w"])
+    pdf = pdf[(pdf.v > 100) & (pdf.w % 3 != 0)]
+    pdf["v2"] = pdf.v * 2 + pdf.k
+    want = sorted((int(k), float(g.v2.sum()), int(len(g))) for k, g in pdf.groupby("k"))
+    assert [(a, pytest.approx(b), c) for a, b, c in want] == got
+
+
+def test_stage_retry_on_genuine_runtime_error_and_oom_replan(spark, monkeypatch):
+    """A RuntimeError raised inside a narrow stage (as a failed HIP launch would) is retried; an
+    out-of-memory attempt re-plans the stage over 2 row chunks; the results are unchanged."""
+    from pyspark_tf_gke_amd.ops import df as D
+    from pyspark_tf_gke_amd.sql import plan as P
+
+    df = spark.createDataFrame([(i, float(i % 17)) for i in range(4000)], ["a", "b"])
+    q = df.filter(col("b") > 3).withColumn("c", col("a") + col("b"))
+    want = sorted((r["a"], r["c"]) for r in q.cache().collect())
+    real = D.compact
+    state = {"n": 1}
+
+    def flaky(mask):
+        if state["n"] > 0:
+            state["n"] -= 1
+            raise RuntimeError("native kernel ptg_compact failed: hipError_t=719")
+        return real(mask)
+
+    monkeypatch.setattr(D, "compact", flaky)
+    r0 = P.STATS["retries"]
+    q2 = df.filter(col("b") > 3).withColumn("c", col("a") + col("b"))
+    assert sorted((r["a"], r["c"]) for r in q2.collect()) == want
+    assert P.STATS["retries"] - r0 == 1 and state["n"] == 0
+    monkeypatch.setattr(D, "compact", real)
+    # out of memory: re-planned in chunks
+    p0, c0 = P.STATS["replans"], P.STATS["chunks"]
+    P._FAULTS["oom"] = 1
+    q3 = df.filter(col("b") > 3).withColumn("c", col("a") + col("b"))
+    assert sorted((r["a"], r["c"]) for r in q3.collect()) == want
+    assert P.STATS["replans"] - p0 == 1 and P.STATS["chunks"] - c0 == 2
+    # a programming error is not retried
+    with pytest.raises(KeyError):
+        df.filter(col("zz") > 1)
+
+
+def test_repartition_makes_local_partitions_and_write_tasks(spark, tmp_path):
+    """repartition(n, col) on one executor: n hash partitions as contiguous row ranges, every key in
+    exactly one partition; write() runs one task / file per non-empty partition; coalesce merges
+    adjacent partitions without moving rows."""
+    import pyarrow.parquet as pq
+
+    df = spark.createDataFrame([(i % 50, float(i)) for i in range(3000)], ["k", "v"])
+    r = df.repartition(8, "k")
+    sizes = r.local_partition_sizes()
+    assert len(sizes) == 8 and sum(sizes) == 3000 and r.rdd.getNumPartitions() == 8
+    seen = {}
+    for p, t in enumerate(r.local_partitions()):
+        for k in set(int(x) for x in t.column("k").data.tolist()):
+            assert seen.setdefault(k, p) == p
+    assert len(seen) == 50
+    out = str(tmp_path / "parts")
+    r.write.parquet(out)
+    files = [f for f in os.listdir(out) if f.endswith(".parquet")]
+    assert len(files) == sum(1 for s in sizes if s)
+    assert pq.read_table(out).num_rows == 3000
+    c = r.coalesce(2)
+    assert len(c.local_partition_sizes()) == 2 and sum(c.local_partition_sizes()) == 3000
+    assert len(df.repartition(5).local_partition_sizes()) == 5
