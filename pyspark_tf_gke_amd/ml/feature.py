@@ -49,6 +49,11 @@ class StringIndexer(Estimator, MLWritable, MLReadable):
             from ..sql.table import column_from_python
 
             cv = column_from_python(vals, T.StringType(), cv.device)
+        # ranks hold their own dictionaries: unify them (tensor control plane) before codes are
+        # counted and the per-code histogram is all-reduced
+        from ..sql.readwriter import unify_dictionary
+
+        cv = unify_dictionary(cv)
         nd = len(cv.dictionary or [])
         counts = _all_reduce_counts(D.histogram(cv.data, nd).cpu())[:nd].numpy()
         labels = list(cv.dictionary or [])

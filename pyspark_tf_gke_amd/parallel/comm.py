@@ -228,6 +228,65 @@ def all_gather_unique(t: torch.Tensor) -> torch.Tensor:
     return torch.unique(torch.cat(parts))
 
 
+def all_gather_bytes(blobs: list) -> list:
+    """Every rank's list of byte strings, in rank order: one all_gather_v of the int64 lengths and
+    one of the concatenated uint8 payload (tensors only, nothing pickled)."""
+    if not is_initialized() or dist.get_world_size() == 1:
+        return [list(blobs)]
+    lens = torch.tensor([len(b) for b in blobs], dtype=torch.int64)
+    raw = b"".join(blobs)
+    data = torch.frombuffer(bytearray(raw), dtype=torch.uint8) if raw else torch.zeros(0, dtype=torch.uint8)
+    all_lens = all_gather_v(lens.to(_ctl_device()))
+    all_data = all_gather_v(data.to(_ctl_device()))
+    out = []
+    for ln, dt in zip(all_lens, all_data):
+        buf = dt.cpu().numpy().tobytes()
+        parts, o = [], 0
+        for n in ln.cpu().tolist():
+            parts.append(buf[o:o + n])
+            o += n
+        out.append(parts)
+    return out
+
+
+def _str_hash64(s: str) -> int:
+    import hashlib
+
+    return int.from_bytes(hashlib.blake2b(s.encode("utf-8"), digest_size=8).digest(), "little", signed=True)
+
+
+def union_strings(strings: list) -> list:
+    """Union of every rank's string list, first occurrence in rank order (identical on every rank).
+    Tensor control plane: one all_gather_v of 64-bit string hashes decides which rank first holds
+    each distinct string, then only those strings' UTF-8 bytes travel (all_gather_bytes)."""
+    strings = list(strings)
+    if not is_initialized() or dist.get_world_size() == 1:
+        seen, out = set(), []
+        for x in strings:
+            if x not in seen:
+                seen.add(x)
+                out.append(x)
+        return out
+    rank = dist.get_rank()
+    h = torch.tensor([_str_hash64(x) for x in strings], dtype=torch.int64)
+    per_rank = [t.cpu().tolist() for t in all_gather_v(h.to(_ctl_device()))]
+    seen: set = set()
+    first: list = []  # (rank, index) of every first occurrence, in merge order
+    for r, hs in enumerate(per_rank):
+        for i, x in enumerate(hs):
+            if x not in seen:
+                seen.add(x)
+                first.append((r, i))
+    mine = [strings[i].encode("utf-8") for r, i in first if r == rank]
+    got = all_gather_bytes(mine)
+    cursor = [0] * len(got)
+    out = []
+    for r, _ in first:
+        out.append(got[r][cursor[r]].decode("utf-8"))
+        cursor[r] += 1
+    return out
+
+
 def all_gather_object(obj):
     if not is_initialized() or dist.get_world_size() == 1:
         return [obj]

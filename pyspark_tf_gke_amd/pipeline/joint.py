@@ -102,7 +102,7 @@ def run_joint(rows_per_executor: int = 1_000_000, out_dir: str = "./joint-out", 
     _sync(dev)
     comm.barrier()
     etl_s = comm.all_reduce_max_scalar(time.perf_counter() - t0)
-    n_total = int(sum(comm.all_gather_object(int(n_local)))) if world > 1 else int(n_local)
+    n_total = int(comm.all_reduce_int([int(n_local)])[0]) if world > 1 else int(n_local)
     pq_bytes = sum(os.path.getsize(os.path.join(pq_path, f)) for f in os.listdir(pq_path) if f.endswith(".parquet"))
 
     # ---- 3. train
@@ -116,7 +116,7 @@ def run_joint(rows_per_executor: int = 1_000_000, out_dir: str = "./joint-out", 
     x, y = _to_device_tensors(train_df, strategy.device)
     n_train = x.shape[0]
     steps = max(1, n_train // batch_size)
-    steps = int(min(comm.all_gather_object(steps))) if world > 1 else steps  # lock-step collectives
+    steps = int(min(comm.all_gather_int(steps))) if world > 1 else steps  # lock-step collectives
     ds_train = Dataset.from_tensor_slices((x, y)).shuffle(n_train, seed=seed + rank).batch(
         batch_size, drop_remainder=True).repeat().prefetch(1)
     with strategy.scope():

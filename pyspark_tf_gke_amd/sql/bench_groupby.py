@@ -51,7 +51,7 @@ def run(total_rows: int = 1_000_000_000, num_keys: int = 1_000_000, steps: int =
     groups = out.count()
     total_c = int(out._t.column("c").data.sum().item())
     if world > 1:
-        total_c = int(sum(comm.all_gather_object(total_c)))
+        total_c = int(comm.all_reduce_int([total_c])[0])
     ok = total_c == n * world
     return {"metric": "rows/sec Spark groupBy-aggregate", "value": round(n * world * steps / dt, 1), "unit": "rows/s",
             "ms_per_step": round(dt / steps * 1e3, 3),

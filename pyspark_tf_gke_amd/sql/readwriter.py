@@ -42,13 +42,8 @@ def unify_dictionary(cv: ColumnVector) -> ColumnVector:
     local codes — required before codes can be compared, shuffled or grouped across ranks."""
     if comm.world_size() == 1 or not isinstance(cv.dtype, T.StringType):
         return cv
-    dicts = comm.all_gather_object(cv.dictionary or [])
-    merged, idx = [], {}
-    for d in dicts:
-        for s in d:
-            if s not in idx:
-                idx[s] = len(merged)
-                merged.append(s)
+    merged = comm.union_strings(cv.dictionary or [])  # tensor collectives: hashes, then new strings' bytes
+    idx = {s: i for i, s in enumerate(merged)}
     lut = torch.tensor([idx[s] for s in (cv.dictionary or [])] + [-1], dtype=torch.int32, device=cv.device)
     codes = cv.data.long()
     codes = torch.where(codes < 0, torch.full_like(codes, len(cv.dictionary or [])), codes)
@@ -111,7 +106,8 @@ def _parse_csv_bytes(buf: bytes, header: bool, infer: bool, sep: str, device, sc
         lib.ptgh_csv_infer(cbuf, p(fs), p(fl), p(fq), m, Cn, j, ctypes.byref(tcode))
         types.append(tcode.value)
     if infer and comm.world_size() > 1 and not isinstance(schema, T.StructType):
-        allt = comm.all_gather_object(types)
+        allt = [row.tolist() for row in comm.all_gather_v(torch.tensor([types], dtype=torch.int64))[0:]]
+        allt = [r[0] for r in allt]
         merged = []
         for j in range(Cn):
             ts = [t[j] for t in allt if t[j] != 5]

@@ -217,9 +217,11 @@ class SparkSession:
                 # infer over the global data so every rank agrees on the type
                 dt = infer_python_type(vals)
                 if comm.world_size() > 1 and not _local:
-                    kinds = comm.all_gather_object(type(dt).__name__)
-                    if len(set(kinds)) > 1:
-                        dt = T.DoubleType() if set(kinds) <= {"LongType", "DoubleType"} else T.StringType()
+                    names_ = ["BooleanType", "IntegerType", "LongType", "DoubleType", "StringType"]
+                    code = names_.index(type(dt).__name__) if type(dt).__name__ in names_ else len(names_)
+                    kinds = {names_[c] if c < len(names_) else "other" for c in comm.all_gather_int(code)}
+                    if len(kinds) > 1:
+                        dt = T.DoubleType() if kinds <= {"LongType", "DoubleType"} else T.StringType()
             cols[nm] = column_from_python(vals, dt, self.device)
         return DataFrame(Table(cols, len(rows), self.device), self)
 

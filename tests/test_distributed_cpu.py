@@ -377,3 +377,54 @@ def test_shuffle_partitions_bucket_the_groupby_exchange():
         assert v["peak64"] * 8 < v["peak2"], v
         assert v["aqe_rounds"] < 32, v
         assert v["rp"] == 3, v
+
+
+NO_PICKLE_BODY = """
+import json, os, torch
+import torch.distributed as dist
+from pyspark_tf_gke_amd.parallel import comm
+
+def _refuse(*a, **k):
+    raise AssertionError("pickled collective on a data path")
+
+dist.all_gather_object = _refuse
+dist.broadcast_object_list = _refuse
+comm.all_gather_object = _refuse
+from pyspark_tf_gke_amd.sql import SparkSession
+from pyspark_tf_gke_amd.sql.functions import col, explode, split
+from pyspark_tf_gke_amd.ml import StringIndexer
+spark = SparkSession.builder.master("spark://127.0.0.1:7077").getOrCreate()
+r = comm.rank()
+text = os.environ["WC_TEXT"]
+words = spark.read.text(text).select(explode(split(col("value"), r"\\s+")).alias("word")).filter(col("word") != "")
+wc = {w: c for w, c in ((row.word, row["count"]) for row in words.groupBy("word").count().collect())}
+# rank-specific strings: dictionaries differ per rank and must be unified without pickles
+df = spark.createDataFrame([("only%d" % r if i % 5 == 0 else "w%d" % (i % 7), float(i)) for i in range(40)],
+                           ["s", "v"], _local=True)
+idx = StringIndexer(inputCol="s", outputCol="si").fit(df)
+labels = idx.labels
+got = sorted((row.s, float(row.v)) for row in df.collect())
+from pyspark_tf_gke_amd.pipeline import run_joint
+rep = run_joint(rows_per_executor=3000, out_dir=os.environ["JOINT_OUT"], epochs=1, batch_size=256,
+                master="spark://127.0.0.1:7077", verbose=False)
+print("RESULT", json.dumps({"wc": wc, "labels": labels, "n": len(got), "rows": rep["rows_after_etl"],
+                            "only": sorted(s for s, _ in got if s.startswith("only"))[:1]}), flush=True)
+"""
+
+
+def test_control_plane_never_pickles(tmp_path):
+    """With every pickled collective made to raise, 2 ranks still run wordcount (string groupBy
+    across ranks), StringIndexer over rank-specific dictionaries, a string collect and the joint
+    ETL -> Parquet -> train pipeline: strings travel as hashes + UTF-8 bytes in tensors."""
+    p = tmp_path / "t.txt"
+    p.write_text("a b a\nc a b\n\nd\n" * 3)
+    r = _run_ranks(NO_PICKLE_BODY, nproc=2, timeout=600,
+                   extra_env={"WC_TEXT": str(p), "JOINT_OUT": str(tmp_path / "joint")})
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    res = _results(r.stdout)
+    assert len(res) == 2
+    for v in res.values():
+        assert v["wc"] == {"a": 9, "b": 6, "c": 3, "d": 3}, v
+        assert v["labels"][:1] != [] and "only0" in v["labels"] and "only1" in v["labels"], v
+        assert v["n"] == 80 and v["rows"] > 5000, v
+    assert res[0]["labels"] == res[1]["labels"]
