@@ -279,8 +279,18 @@ def main():
                                    rank, world)
                 extra["groupby"] = {"metric": gb["metric"], "value": gb["value"], "unit": gb["unit"],
                                     "ms_per_step": gb["ms_per_step"], "rows_per_gpu": gb["config"]["rows_per_gpu"],
-                                    "distinct_keys": gb["config"]["distinct_keys"],
+                                    "distinct_keys": gb["config"]["distinct_keys"], "keys": gb["config"]["keys"],
                                     "counts_check": gb["config"]["counts_check"], "dtype": "fp64"}
+                from pyspark_tf_gke_amd.sql import bench_groupby as bg
+
+                gc.collect()
+                torch.cuda.empty_cache()
+                gs = bg.run(rows_per_gpu=args.rows, num_keys=args.keys, steps=3, warmup=1, device=strategy.device,
+                            sparse=True)
+                extra["groupby_sparse"] = {"value": gs["value"], "unit": gs["unit"], "ms_per_step": gs["ms_per_step"],
+                                           "distinct_keys": gs["config"]["distinct_keys"], "keys": gs["config"]["keys"],
+                                           "groups_out": gs["config"]["groups_out"],
+                                           "counts_check": gs["config"]["counts_check"], "dtype": "fp64"}
             except Exception as e:  # noqa: BLE001 - never lose the headline line
                 extra["groupby"] = {"error": repr(e)[:300]}
     out = {"metric": res["metric"], "value": res["value"], "unit": res["unit"], "n_gpus": world,

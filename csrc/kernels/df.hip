@@ -1365,11 +1365,14 @@ __global__ __launch_bounds__(256) void partition_perm_k(const int* __restrict__ 
 // ================================================================================================
 // synthetic (key, value) generator: key = hash(seed, row) % num_keys, value uniform [0,1)
 // ================================================================================================
+// sparse: the dense key k in [0, num_keys) is replaced by mix64(k + 1) (a bijection): the same
+// number of distinct keys spread over the whole int64 range (the general hash path, not the range one)
 __global__ __launch_bounds__(256) void fill_kv_k(long long* __restrict__ keys, double* __restrict__ vals, long n,
-                                                 long offset, long num_keys, unsigned long long seed) {
+                                                 long offset, long num_keys, unsigned long long seed, int sparse) {
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
     const unsigned long long h = mix64((unsigned long long)(i + offset) * 0x9E3779B97F4A7C15ULL + seed);
-    keys[i] = (long long)(h % (unsigned long long)num_keys);
+    const unsigned long long k = h % (unsigned long long)num_keys;
+    keys[i] = (long long)(sparse ? mix64(k + 1ULL) : k);
     vals[i] = (double)(mix64(h ^ 0x632BE59BD9B4E019ULL) >> 11) * (1.0 / 9007199254740992.0);
   }
 }
@@ -1529,6 +1532,8 @@ int ptg_part_agg2(const void* okeys, int key32, long kbase, const void* const* v
   AggPay pay;
   for (int j = 0; j < PAY_MAX; ++j) pay.vals[j] = j < nv ? (const double*)vals[j] : nullptr;
   const int g = P < 8192 ? P : 8192;
+  (void)hipMemsetAsync(m_out, 0, 8, s);  // output / spill counters start at zero (no host fill)
+  (void)hipMemsetAsync(nspill, 0, 4, s);
 #define PTG_AGG(NV, MM) \
   if (key32) { PTG_AGGK(NV, MM, unsigned int) } else { PTG_AGGK(NV, MM, long long) }
 #define PTG_AGGK(NV, MM, KT)                                                                                \
@@ -1703,9 +1708,10 @@ int ptg_partition_perm(const void* part, long n, int P, void* cursor, void* perm
   PTG_RETURN_LAUNCH();
 }
 
-int ptg_fill_synthetic_kv(void* keys, void* vals, long n, long offset, long num_keys, long seed, hipStream_t s) {
+int ptg_fill_synthetic_kv(void* keys, void* vals, long n, long offset, long num_keys, long seed, int sparse,
+                          hipStream_t s) {
   hipLaunchKernelGGL(fill_kv_k, dim3(grid_n(n)), dim3(256), 0, s, (long long*)keys, (double*)vals, n, offset, num_keys,
-                     (unsigned long long)seed);
+                     (unsigned long long)seed, sparse);
   PTG_RETURN_LAUNCH();
 }
 

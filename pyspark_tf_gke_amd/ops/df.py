@@ -84,6 +84,12 @@ def gather_rows(t: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
         return out
     row_bytes = t[0].numel() * t.element_size() if t.dim() > 0 and t.shape[0] > 0 else t.element_size()
     src = t.contiguous()
+    if row_bytes in (4, 8) and idx.dtype in (torch.int64, torch.int32) and not _native.CHECKED:
+        # one row per thread, 4 in flight (dfutil.hip gather_fixed_k); int32 indices are u32 row ids
+        hip("ptg_gather_fixed", ptr(src), ptr(idx), int(idx.dtype == torch.int32), m, row_bytes, ptr(out))
+        return out
+    if idx.dtype != torch.int64:
+        idx = idx.to(torch.int64)
     hip("ptg_gather_rows", ptr(src), ptr(idx), m, row_bytes, t.shape[0] if t.dim() > 0 else 1, ptr(out))
     return out
 
@@ -119,6 +125,72 @@ def histogram(codes: torch.Tensor, nbins: int) -> torch.Tensor:
 
 
 # ------------------------------------------------------------------------------------------------
+# small device utilities (csrc/kernels/dfutil.hip): the groupBy / sort paths launch only our kernels
+# ------------------------------------------------------------------------------------------------
+def scan_excl(x: torch.Tensor, out: torch.Tensor | None = None, total: torch.Tensor | None = None) -> torch.Tensor:
+    """Exclusive prefix sum of an int32 / int64 vector into int64 ``out``; ``total`` (1-element
+    int64 view, anywhere) receives the sum."""
+    n = x.numel()
+    if out is None:
+        out = torch.empty(max(n, 1), dtype=torch.int64, device=x.device)[:n]
+    if not on_device(x):
+        cs = torch.cumsum(x.to(torch.int64), 0)
+        out[:n] = cs - x.to(torch.int64)
+        if total is not None:
+            total.fill_(int(cs[-1]) if n else 0)
+        return out
+    ws = torch.empty(max(1, int(_native.hip_lib().ptg_scan_ws_elems(n))), dtype=torch.int64, device=x.device)
+    hip("ptg_scan_excl", ptr(x), int(x.dtype == torch.int64), n, ptr(out), ptr(total), ptr(ws))
+    return out
+
+
+def minmax_i64(x: torch.Tensor, n: int | None = None, stride: int = 1, off_min: int = 0, off_max: int = 0):
+    """(min over x[i*stride + off_min], max over x[i*stride + off_max]) as Python ints; ``x`` a
+    contiguous int64 buffer (a strided sample of a column, or the [tiles, 2] range table)."""
+    n = (x.numel() + stride - 1) // stride if n is None else n
+    if not on_device(x):
+        flat = x.reshape(-1)
+        return int(flat[off_min::stride][:n].min()), int(flat[off_max::stride][:n].max())
+    out = torch.empty(2, dtype=torch.int64, device=x.device)
+    hip("ptg_minmax_i64", ptr(x), n, stride, off_min, off_max, ptr(out))
+    lo, hi = out.tolist()
+    return int(lo), int(hi)
+
+
+def strided_sample(keys: torch.Tensor, stride: int, m: int) -> torch.Tensor:
+    """keys[::stride][:m] as a contiguous int64 tensor."""
+    if not on_device(keys):
+        return keys[::stride][:m].contiguous()
+    out = torch.empty(max(m, 1), dtype=torch.int64, device=keys.device)[:m]
+    hip("ptg_strided_copy_i64", ptr(keys), stride, m, ptr(out))
+    return out
+
+
+def _dense_extract(prow, psum, pmm, C: int, nv: int, W: int, lo: int, dev):
+    """Sum the C per-chunk partial tables of a direct-indexed aggregation and compact the occupied
+    keys (dense_count_k / dense_write_k): -> (keys, rows, [(sum, cnt, min, max)] per column)."""
+    nb = max(1, -(-W // 4096))
+    bcount = torch.empty(nb, dtype=torch.int32, device=dev)
+    boff = torch.empty(nb, dtype=torch.int64, device=dev)
+    total = torch.empty(1, dtype=torch.int64, device=dev)
+    hip("ptg_dense_extract", ptr(prow), ptr(psum), ptr(pmm), C, nv, W, int(lo), ptr(bcount), ptr(boff), ptr(total),
+        None, 1)
+    m = int(total.item())
+    keys = torch.empty(max(m, 1), dtype=torch.int64, device=dev)[:m]
+    cols = torch.empty((1 + 4 * max(nv, 1), max(m, 1)), dtype=torch.float64, device=dev)[:, :m]
+    rows = cols[0]
+    outs = [(cols[1 + 4 * j], cols[2 + 4 * j], cols[3 + 4 * j], cols[4 + 4 * j]) for j in range(nv)]
+    ptrs = [keys.data_ptr(), rows.data_ptr()]
+    for q in range(4):  # sum, cnt, min, max
+        ptrs += [outs[j][q].data_ptr() if j < nv else 0 for j in range(4)]
+    arr = (ctypes.c_uint64 * 18)(*ptrs)
+    if m:
+        hip("ptg_dense_extract", ptr(prow), ptr(psum), ptr(pmm), C, nv, W, int(lo), ptr(bcount), ptr(boff),
+            ptr(total), ctypes.addressof(arr), 2)
+    return keys, rows, outs
+
+
+# ------------------------------------------------------------------------------------------------
 # hash aggregation
 # ------------------------------------------------------------------------------------------------
 def _pow2(x: int) -> int:
@@ -130,12 +202,13 @@ def _small_range_agg(keys, vals, valids):
     table per workgroup, one pass over the rows; None when the span is wider."""
     n = keys.numel()
     nv = len(vals)
-    smp = keys[:: max(1, n // 65536)]
+    keys = keys.contiguous()
     wmax = (150 * 1024) // (4 + 12 * nv)
-    if int(smp.max().item()) - int(smp.min().item()) >= wmax:
+    st = max(1, n // 65536)
+    slo, shi = minmax_i64(keys, n=(n + st - 1) // st, stride=st)
+    if shi - slo >= wmax:
         return None
-    lo_t, hi_t = torch.aminmax(keys)
-    lo, hi = int(lo_t.item()), int(hi_t.item())
+    lo, hi = minmax_i64(keys)
     W = hi - lo + 1
     if W > wmax:
         return None
@@ -151,14 +224,9 @@ def _small_range_agg(keys, vals, valids):
     prow = torch.empty((G, 1 + nv, W), dtype=torch.int32, device=keys.device)
     psum = torch.empty((G, max(nv, 1), W), dtype=torch.float64, device=keys.device)
     pin = _pay_in(pay)
-    hip("ptg_small_range_agg", ptr(keys.contiguous()), n, lo, W, ctypes.addressof(pin), nv, rpb, G, ptr(prow),
+    hip("ptg_small_range_agg", ptr(keys), n, lo, W, ctypes.addressof(pin), nv, rpb, G, ptr(prow),
         ptr(psum))
-    cnts = prow.to(torch.int64).sum(0)
-    sums = psum.sum(0)
-    idx = torch.nonzero(cnts[0] > 0).view(-1)
-    inf = torch.full((idx.numel(),), math.inf, dtype=torch.float64, device=keys.device)
-    outs = [(sums[j][idx], cnts[1 + j][idx].to(torch.float64), inf, -inf) for j in range(nv)]
-    return idx + lo, cnts[0][idx].to(torch.float64), outs
+    return _dense_extract(prow, psum, None, G, nv, W, lo, keys.device)
 
 
 def hash_agg(keys: torch.Tensor, vals: list, valids: list, want_minmax: bool = False, cap_hint: int | None = None):
@@ -255,34 +323,37 @@ def _radix_level(keys, kbase, pay_cols, seg_start, seg_len, shift, buf, tag, com
     dev = keys.device
     T = radix_tile(len(pay_cols))
     nseg = seg_start.numel()
-    ntiles_s = (seg_len + T - 1) // T
-    first = torch.cumsum(ntiles_s, 0) - ntiles_s
-    total = int(ntiles_s.sum().item())
-    n_out = int(seg_len.sum().item())
+    # tile plan on the device (dfutil.hip): tiles per segment, their exclusive prefix, and the
+    # per-tile start / rows / histogram base and stride; one readback of (tiles, rows)
+    ntiles_s = buf(tag + "nts", (nseg,), torch.int64)
+    hip("ptg_radix_plan", ptr(seg_start), ptr(seg_len), nseg, T, ptr(ntiles_s), None, 0, None, None, None, None, 0)
+    first = buf(tag + "first", (nseg,), torch.int64)
+    tot2 = buf(tag + "tot2", (2,), torch.int64)
+    scan_excl(ntiles_s, out=first, total=tot2[0:1])
+    lens_scan = buf(tag + "lscan", (nseg,), torch.int64)
+    scan_excl(seg_len, out=lens_scan, total=tot2[1:2])
+    total, n_out = (int(x) for x in tot2.tolist())
     nv = len(pay_cols)
     in32 = keys.dtype == torch.int32
     ovals = [buf(f"{tag}ov{j}", (max(n_out, 1),), torch.float64)[:n_out] for j in range(nv)]
     if total == 0:
         z = torch.zeros(nseg * 64, dtype=torch.int64, device=dev)
-        return keys[:0], kbase, ovals, z, z
-    tile_seg = torch.repeat_interleave(torch.arange(nseg, device=dev), ntiles_s, output_size=total)
-    tl = torch.arange(total, device=dev) - first[tile_seg]
-    tstart = seg_start[tile_seg] + tl * T
-    seg_end = seg_start + seg_len
-    trows = torch.minimum(torch.full_like(tstart, T), seg_end[tile_seg] - tstart).to(torch.int32)
-    hb = 64 * first
-    thbase = hb[tile_seg] + tl
-    thstride = ntiles_s[tile_seg]
+        return keys[:0], kbase, ovals, z, z, z
+    tstart = buf(tag + "tst", (total,), torch.int64)
+    trows = buf(tag + "trw", (total,), torch.int32)
+    thbase = buf(tag + "thb", (total,), torch.int64)
+    thstride = buf(tag + "ths", (total,), torch.int64)
+    hip("ptg_radix_plan", ptr(seg_start), ptr(seg_len), nseg, T, ptr(ntiles_s), ptr(first), total, ptr(tstart),
+        ptr(trows), ptr(thbase), ptr(thstride), 1)
     hist = buf(tag + "hist", (64 * total,), torch.int32)
     rng = buf(tag + "rng", (total, 2), torch.int64) if (compress and not in32) else None
     hip("ptg_radix_count", ptr(keys), int(in32), int(kbase), ptr(tstart), ptr(trows), ptr(thbase), ptr(thstride),
         total, shift, ptr(hist), ptr(rng))
     offs = buf(tag + "offs", (64 * total + 1,), torch.int64)
-    torch.cumsum(hist, 0, dtype=torch.int64, out=offs[1:])
-    offs[0] = 0
+    scan_excl(hist, out=offs[:-1], total=offs[-1:])
     out32, kbase_out = in32, kbase
     if rng is not None:
-        lo, hi = (int(x) for x in torch.stack([rng[:, 0].min(), rng[:, 1].max()]).tolist())
+        lo, hi = minmax_i64(rng, n=total, stride=2, off_min=0, off_max=1)
         if hi - lo < (1 << 32) - 1:
             out32, kbase_out = True, lo
     okeys = buf(tag + ("okeys32" if out32 else "okeys"), (max(n_out, 1),),
@@ -294,10 +365,12 @@ def _radix_level(keys, kbase, pay_cols, seg_start, seg_len, shift, buf, tag, com
         ctypes.addressof(pout))
     # sub-segment (s, d) starts at the run of its first tile; empty segments (no tiles) start where
     # the next non-empty one does (offs[-1] = n_out is the sentinel)
-    idx = (hb.view(-1, 1) + torch.arange(64, device=dev).view(1, -1) * ntiles_s.view(-1, 1)).view(-1)
-    new_start = offs[idx]
-    new_end = torch.cat([new_start[1:], torch.full((1,), n_out, dtype=torch.int64, device=dev)])
-    return okeys, kbase_out, ovals, new_start, new_end
+    new_start = buf(tag + "nst", (nseg * 64,), torch.int64)
+    new_end = buf(tag + "nen", (nseg * 64,), torch.int64)
+    new_len = buf(tag + "nln", (nseg * 64,), torch.int64)
+    hip("ptg_radix_bounds", ptr(offs), ptr(first), ptr(ntiles_s), nseg, n_out, ptr(new_start), ptr(new_end),
+        ptr(new_len))
+    return okeys, kbase_out, ovals, new_start, new_end, new_len
 
 
 def _part_agg_lds(pcap: int, nv: int, minmax: bool) -> int:
@@ -314,7 +387,7 @@ def estimate_distinct(keys: torch.Tensor, sample: int = ESTIMATE_SAMPLE) -> int:
     n = keys.numel()
     if n <= sample:
         return int(hash_agg(keys, [], [], False)[0].numel())
-    s = keys[:: n // sample][:sample].contiguous()
+    s = strided_sample(keys.contiguous(), n // sample, sample)
     d = int(hash_agg(s, [], [], False)[0].numel())
     m = s.numel()
     if d >= 0.999 * m and n >= 16 * sample and sample * 16 <= ESTIMATE_SAMPLE_MAX:
@@ -384,15 +457,14 @@ def hash_agg_range(keys: torch.Tensor, pay: list, buf, nv: int, sample_lohi: tup
     for attempt in range(2):
         lo, sh = win
         hip("ptg_range_count", ptr(keys), n, int(lo), sh, T, ntiles, ptr(hist), ptr(rng))
-        mn, mx = (int(x) for x in torch.stack([rng[:, 0].min(), rng[:, 1].max()]).tolist())
+        mn, mx = minmax_i64(rng, n=ntiles, stride=2, off_min=0, off_max=1)
         if mn >= lo and mx < lo + (256 << sh):
             break
         win = _range_window(mn, mx, sh_max) if attempt == 0 else None
         if win is None:
             return None
     offs = buf("roffs", (256 * ntiles + 1,), torch.int64)
-    torch.cumsum(hist, 0, dtype=torch.int64, out=offs[1:])
-    offs[0] = 0
+    scan_excl(hist, out=offs[:-1], total=offs[-1:])
     okeys = buf("rokeys16", (max(n, 1),), torch.int16)[:n]  # u16 index inside the partition's window
     ovals = [buf(f"aov{j}", (max(n, 1),), torch.float64)[:n] for j in range(nv)]
     pin, pout = _pay_in(pay), _pay_out(ovals)
@@ -406,19 +478,7 @@ def hash_agg_range(keys: torch.Tensor, pay: list, buf, nv: int, sample_lohi: tup
     vptrs = (ctypes.c_void_p * PAY_MAX)(*([o.data_ptr() for o in ovals] + [0] * (PAY_MAX - nv)))
     hip("ptg_range_agg", ptr(okeys), ctypes.addressof(vptrs), nv, int(minmax), ptr(offs), ntiles, sh, chunks,
         ptr(prow), ptr(psum), ptr(pmm) if minmax else None)
-    cnts = prow.to(torch.int64).sum(0) if chunks > 1 else prow[0].to(torch.int64)  # [1 + nv][Rw]
-    sums = psum.sum(0) if chunks > 1 else psum[0]
-    idx = torch.nonzero(cnts[0] > 0).view(-1)
-    out_keys = idx + lo
-    rows = cnts[0][idx].to(torch.float64)
-    if minmax:
-        mins = pmm[:, 0::2].amin(0) if chunks > 1 else pmm[0, 0::2]
-        maxs = pmm[:, 1::2].amax(0) if chunks > 1 else pmm[0, 1::2]
-        outs = [(sums[j][idx], cnts[1 + j][idx].to(torch.float64), mins[j][idx], maxs[j][idx]) for j in range(nv)]
-    else:
-        inf = torch.full((idx.numel(),), math.inf, dtype=torch.float64, device=dev)
-        outs = [(sums[j][idx], cnts[1 + j][idx].to(torch.float64), inf, -inf) for j in range(nv)]
-    return out_keys, rows, outs
+    return _dense_extract(prow, psum, pmm if minmax else None, chunks, nv, Rw, lo, dev)
 
 
 def hash_agg_radix(keys: torch.Tensor, vals: list, valids: list, want_minmax: bool = False, ws: dict | None = None,
@@ -451,8 +511,8 @@ def hash_agg_radix(keys: torch.Tensor, vals: list, valids: list, want_minmax: bo
             vd = vd.view(torch.uint8)
         pay.append((v.contiguous(), vd))
     if keys.dtype == torch.int64 and n >= RANGE_MIN_ROWS and config.get("groupby_range"):
-        smp = keys[:: max(1, n // 65536)]
-        slo, shi = (int(x) for x in torch.stack([smp.min(), smp.max()]).tolist())
+        st_ = max(1, n // 65536)
+        slo, shi = minmax_i64(keys.contiguous(), n=(n + st_ - 1) // st_, stride=st_)
         if shi - slo < (RADIX_RANGE_BINS << _range_sh_max(nv, want_minmax)):
             r = hash_agg_range(keys.contiguous(), pay, buf, nv, (slo, shi), want_minmax)
             if r is not None:
@@ -468,30 +528,31 @@ def hash_agg_radix(keys: torch.Tensor, vals: list, valids: list, want_minmax: bo
     pcap = 256
     while pcap < pcap_max and pcap < 4 * K / P:
         pcap *= 2
-    seg_start = torch.zeros(1, dtype=torch.int64, device=dev)
-    seg_len = torch.full((1,), n, dtype=torch.int64, device=dev)
+    seg_start = torch.tensor([0], dtype=torch.int64).to(dev)  # host -> device copies, no fill kernels
+    seg_len = torch.tensor([n], dtype=torch.int64).to(dev)
     cur_keys, cur_pay, kbase = keys.contiguous(), pay, 0
     shift = 64 - RADIX_BITS
     tags = ["a", "b"]
     lvl = 0
+    pend = None
     for _ in range(levels):
-        cur_keys, kbase, ov, pstart, pend = _radix_level(cur_keys, kbase, cur_pay, seg_start, seg_len, shift, buf,
-                                                         tags[lvl % 2], compress=(lvl == 0))
+        cur_keys, kbase, ov, seg_start, pend, seg_len = _radix_level(cur_keys, kbase, cur_pay, seg_start, seg_len,
+                                                                     shift, buf, tags[lvl % 2], compress=(lvl == 0))
         cur_pay = [(o, None) for o in ov]
-        seg_start, seg_len = pstart, pend - pstart
         shift -= RADIX_BITS
         lvl += 1
     res_k, res_t = [], []
+    capbuf = torch.empty(1, dtype=torch.int64, device=dev)
     while True:
         P = seg_start.numel()
-        cap = int(torch.clamp(seg_len, max=pcap).sum().item())
+        hip("ptg_sum_clamp_i64", ptr(seg_len), P, pcap, ptr(capbuf))
+        cap = int(capbuf.item())
         out_keys = torch.empty(max(cap, 1), dtype=torch.int64, device=dev)
         out_tab = torch.empty((1 + 4 * nv) * max(cap, 1), dtype=torch.float64, device=dev)
-        m_out = torch.zeros(1, dtype=torch.int64, device=dev)
+        m_out = torch.empty(1, dtype=torch.int64, device=dev)  # zeroed by ptg_part_agg2
         spilled = torch.empty(P, dtype=torch.int32, device=dev)
-        nspill = torch.zeros(1, dtype=torch.int32, device=dev)
+        nspill = torch.empty(1, dtype=torch.int32, device=dev)
         vptrs = (ctypes.c_void_p * PAY_MAX)(*([c[0].data_ptr() for c in cur_pay] + [0] * (PAY_MAX - nv)))
-        pend = seg_start + seg_len
         hip("ptg_part_agg2", ptr(cur_keys), int(cur_keys.dtype == torch.int32), int(kbase), ctypes.addressof(vptrs), nv,
             int(want_minmax), ptr(seg_start), ptr(pend), P, pcap, ptr(out_keys), ptr(out_tab), max(cap, 1), ptr(m_out),
             ptr(spilled), ptr(nspill))
@@ -507,10 +568,9 @@ def hash_agg_radix(keys: torch.Tensor, vals: list, valids: list, want_minmax: bo
             raise RuntimeError("hash_agg_radix: partition recursion did not converge")
         sp = spilled[:ns].long()
         # re-partition only the spilled partitions, one level deeper
-        cur_keys, kbase, ov, seg_start, pend2 = _radix_level(cur_keys, kbase, cur_pay, seg_start[sp], seg_len[sp],
-                                                             shift, buf, tags[lvl % 2])
+        cur_keys, kbase, ov, seg_start, pend, seg_len = _radix_level(
+            cur_keys, kbase, cur_pay, seg_start[sp].contiguous(), seg_len[sp].contiguous(), shift, buf, tags[lvl % 2])
         cur_pay = [(o, None) for o in ov]
-        seg_len = pend2 - seg_start
         shift -= RADIX_BITS
         lvl += 1
     ok = res_k[0] if len(res_k) == 1 else torch.cat(res_k)
@@ -525,8 +585,7 @@ def partition_perm(part: torch.Tensor, counts: torch.Tensor) -> torch.Tensor:
     P = counts.numel()
     if not on_device(part):
         return torch.from_numpy(np.argsort(part.numpy(), kind="stable").astype(np.int64))
-    cursor = torch.zeros(P, dtype=torch.int64, device=part.device)
-    cursor[1:] = torch.cumsum(counts, 0)[:-1]
+    cursor = scan_excl(counts.contiguous())
     perm = torch.empty(n, dtype=torch.int64, device=part.device)
     hip("ptg_partition_perm", ptr(part), n, P, ptr(cursor), ptr(perm))
     return perm
@@ -629,8 +688,7 @@ def radix_sort_u64(keys: torch.Tensor, vals: torch.Tensor | None = None, lo: int
     for p in range(passes):
         shift = 8 * p
         hip("ptg_sort_count", ptr(ka), n, base, shift, ptr(hist))
-        torch.cumsum(hist, 0, dtype=torch.int64, out=offs)
-        offs.sub_(hist)
+        scan_excl(hist, out=offs)
         hip("ptg_sort_scatter", ptr(ka), ptr(va), n, base, shift, ptr(offs), ptr(kb), ptr(vb), int(v32))
         if kc is None:  # third buffer pair so the caller's keys/vals are never overwritten
             kc = torch.empty(n, dtype=torch.int64, device=dev)
@@ -638,8 +696,9 @@ def radix_sort_u64(keys: torch.Tensor, vals: torch.Tensor | None = None, lo: int
             ka, va, kb, vb = kb, vb, kc, vc
         else:
             ka, va, kb, vb = kb, vb, ka, va
-    if v32:
-        va = va.to(torch.int64) & 0xFFFFFFFF  # u32 row ids (n may reach 2^32)
+    if v32:  # u32 row ids (n may reach 2^32) widened to int64 in one pass
+        hip("ptg_widen_u32", ptr(va), n, ptr(kb))  # kb: our spare int64 buffer (never the caller's keys)
+        va = kb
     return ka, va
 
 
@@ -687,18 +746,23 @@ def _mix64_np(x: np.ndarray) -> np.ndarray:
     return x
 
 
-def fill_synthetic_kv(n: int, num_keys: int, device, offset: int = 0, seed: int = 42):
+def fill_synthetic_kv(n: int, num_keys: int, device, offset: int = 0, seed: int = 42, sparse: bool = False):
+    """(key, value) rows: key = hash(row) % num_keys (``sparse``: that dense key mixed over the whole
+    int64 range, same number of distinct keys), value uniform in [0, 1)."""
     keys = torch.empty(n, dtype=torch.int64, device=device)
     vals = torch.empty(n, dtype=torch.float64, device=device)
     if torch.device(device).type != "cuda":
         i = np.arange(offset, offset + n, dtype=np.uint64)
         with np.errstate(over="ignore"):
             h = _mix64_np(i * np.uint64(0x9E3779B97F4A7C15) + np.uint64(seed))
-            keys.copy_(torch.from_numpy((h % np.uint64(num_keys)).astype(np.int64)))
+            k = h % np.uint64(num_keys)
+            if sparse:
+                k = _mix64_np(k + np.uint64(1))
+            keys.copy_(torch.from_numpy(k.view(np.int64) if sparse else k.astype(np.int64)))
             v = (_mix64_np(h ^ np.uint64(0x632BE59BD9B4E019)) >> np.uint64(11)).astype(np.float64) / 9007199254740992.0
         vals.copy_(torch.from_numpy(v))
         return keys, vals
-    hip("ptg_fill_synthetic_kv", ptr(keys), ptr(vals), n, offset, num_keys, seed)
+    hip("ptg_fill_synthetic_kv", ptr(keys), ptr(vals), n, offset, num_keys, seed, int(sparse))
     return keys, vals
 
 

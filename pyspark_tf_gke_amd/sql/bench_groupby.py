@@ -16,7 +16,9 @@ from ..parallel import comm
 
 
 def run(total_rows: int = 1_000_000_000, num_keys: int = 1_000_000, steps: int = 5, warmup: int = 1, device=None,
-        rows_per_gpu: int | None = None) -> dict:
+        rows_per_gpu: int | None = None, sparse: bool = False) -> dict:
+    """``sparse``: the same number of distinct keys spread over the whole int64 range (the general
+    hash-partitioned path), instead of the dense [0, num_keys) range."""
     from ..ops import df as D
     from . import functions as F
     from .dataframe import DataFrame
@@ -28,7 +30,7 @@ def run(total_rows: int = 1_000_000_000, num_keys: int = 1_000_000, steps: int =
     n = rows_per_gpu or total_rows
     spark = SparkSession.builder.master("mi355x").getOrCreate()
     dev = spark.device if device is None else torch.device(device)
-    keys, vals = D.fill_synthetic_kv(n, num_keys, dev, offset=rank * n, seed=42)
+    keys, vals = D.fill_synthetic_kv(n, num_keys, dev, offset=rank * n, seed=42, sparse=sparse)
     df = DataFrame(Table({"key": ColumnVector(keys, T.LongType()), "value": ColumnVector(vals, T.DoubleType())}, n, dev),
                    spark)
 
@@ -57,6 +59,7 @@ def run(total_rows: int = 1_000_000_000, num_keys: int = 1_000_000, steps: int =
             "ms_per_step": round(dt / steps * 1e3, 3),
             "config": {"model": "groupBy(key).agg(sum(value), count(*)) on (bigint key, double value)",
                        "rows_per_gpu": n, "global_rows": n * world, "distinct_keys": num_keys, "groups_out": groups,
+                       "keys": "sparse (spread over int64)" if sparse else "dense [0, distinct_keys)",
                        "counts_check": ok, "parallelism": f"{world} executors (1 per GPU), RCCL all-to-all-v shuffle"}}
 
 

@@ -519,3 +519,48 @@ def test_radix_agg_key_compression_ranges(hip_built, lo, span):
     got = D.hash_agg_radix(k.cuda(), [v.cuda()], [None], True)
     want = D.hash_agg(k, [v], [None], True)
     _assert_agg_equal(got, want, True)
+
+
+@pytest.mark.parametrize("n", [0, 1, 4095, 4096, 4097, 1 << 20, 5_000_003])
+def test_scan_minmax_sample_gather_kernels(hip_built, n):
+    """dfutil.hip: exclusive scans (int32 / int64, total slot), int64 min/max over strided views,
+    strided sampling and the fixed-row gathers (int64 / u32 indices) vs torch on the host."""
+    g = torch.Generator().manual_seed(n)
+    x32 = torch.randint(0, 1000, (n,), generator=g, dtype=torch.int32)
+    x64 = torch.randint(-(1 << 40), 1 << 40, (n,), generator=g, dtype=torch.int64)
+    for x in (x32, x64):
+        out = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+        D.scan_excl(x.cuda(), out=out[:n], total=out[n:])
+        cs = torch.cumsum(x.long(), 0)
+        want = torch.cat([torch.zeros(1, dtype=torch.int64), cs])
+        assert torch.equal(out.cpu(), want)
+    if n:
+        assert D.minmax_i64(x64.cuda()) == (int(x64.min()), int(x64.max()))
+        pairs = x64[: (n // 2) * 2].view(-1, 2)
+        if pairs.numel():
+            assert D.minmax_i64(pairs.cuda().contiguous(), n=pairs.shape[0], stride=2, off_min=0, off_max=1) == (
+                int(pairs[:, 0].min()), int(pairs[:, 1].max()))
+        st = max(1, n // 1000)
+        m = (n + st - 1) // st
+        assert torch.equal(D.strided_sample(x64.cuda(), st, m).cpu(), x64[::st][:m])
+        idx = torch.randint(0, n, (n,), generator=g)
+        vals = torch.randn(n, generator=g, dtype=torch.float64)
+        assert torch.equal(D.gather_rows(vals.cuda(), idx.cuda()).cpu(), vals[idx])
+        assert torch.equal(D.gather_rows(x32.cuda(), idx.to(torch.int32).cuda()).cpu(), x32[idx])
+
+
+def test_groupby_sparse_keys_hash_path_vs_host(hip_built):
+    """1M distinct keys spread over the int64 range (bench extra.groupby_sparse): the sparse fill
+    equals its host twin, and the radix-partitioned hash aggregation matches the host groupBy."""
+    n, nk = 4_000_000, 1_000_000
+    kc, vc = D.fill_synthetic_kv(n, nk, "cpu", sparse=True)
+    kg, vg = D.fill_synthetic_kv(n, nk, "cuda", sparse=True)
+    assert torch.equal(kg.cpu(), kc) and torch.equal(vg.cpu(), vc)
+    assert int(kc.max()) - int(kc.min()) > (1 << 60)
+    uk, rows, outs = D.hash_agg_radix(kg, [vg], [None], False)
+    order = torch.argsort(uk.cpu())
+    hk, hrows, houts = D.hash_agg(kc, [vc], [None], False)
+    horder = torch.argsort(hk)
+    assert torch.equal(uk.cpu()[order], hk[horder])
+    assert torch.equal(rows.cpu()[order], hrows[horder])
+    assert torch.allclose(outs[0][0].cpu()[order], houts[0][0][horder], rtol=1e-9, atol=1e-9)
