@@ -20,11 +20,9 @@
 //                     chunk of tiles kept in registers, one fp32 atomic per output per workgroup.
 //   conv_flip_k       W'[ci][kh][kw][co] = W[co][KS-1-kh][KS-1-kw][ci] (dgrad weights), bf16.
 #include "common.h"
+#include "conv_common.h"
 
 #include <algorithm>
-
-typedef __attribute__((ext_vector_type(4))) short s16x4_t;
-typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
 
 namespace ptgc {
 
@@ -123,27 +121,6 @@ template <> PTG_DEV vu2_t bload_vt<vu2_t>(Rsrc r, uint32_t off) {
 }
 
 // dpp row_shl:n - lane l receives lane l+n of its 16-lane row (others keep their own value)
-// The 6 bytes of an RGB pixel pair at byte offset o (o even) as two ALIGNED dword loads covering
-// [o & ~3, +8); sh = 8 * (o & 3) selects them.  The rsrc size is rounded up to 4 bytes, so the last
-// pair's window stays in range (the caching allocator's 512-byte rounding backs the 2 extra bytes).
-struct U8Pair { uint32_t w0, w1, sh; };
-PTG_DEV U8Pair u8pair_load(Rsrc r, uint32_t o, bool ok) {
-  const uint32_t a = o & ~3u;
-  return U8Pair{bload4(r, ok ? a : PTG_OOB), bload4(r, ok ? a + 4u : PTG_OOB), (o & 3u) * 8u};
-}
-PTG_DEV U4 u8pair_to_bf16x8(const U8Pair& p) {
-  constexpr float s = 1.f / 255.f;
-  const unsigned long long v = (((unsigned long long)p.w1 << 32) | p.w0) >> p.sh;
-  auto c = [&](int i) { return (float)((uint32_t)(v >> (8 * i)) & 255u) * s; };
-  U4 o;
-  o.x = pack_bf(c(0), c(1));
-  o.y = pack_bf(c(2), 0.f);
-  o.z = pack_bf(c(3), c(4));
-  o.w = pack_bf(c(5), 0.f);
-  return o;
-}
-PTG_DEV uint32_t u8_rsrc_bytes(long n_bytes) { return (uint32_t)((n_bytes + 3) & ~3L); }
-
 template <int NSH>
 PTG_DEV float row_shl(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), 0x100 | NSH, 0xF, 0xF, false));
@@ -597,11 +574,6 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
 // ================================================================================================
 // weight gradient
 // ================================================================================================
-// ds_read_b64_tr_b16: lane 4q+p of each 16-lane group supplies the address of row q, 4 columns;
-// lane i of the group receives column i of the 4 rows (row q in element q).
-PTG_DEV s16x4_t tr_read(const bf16_t* p) {
-  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(p));
-}
 
 // Persistent: a workgroup owns one 64*NB-wide kflat slice and a contiguous strip-major range of
 // tiles; the next tile's halo rows (RING: only the TH new ones) and dZ tile are prefetched into

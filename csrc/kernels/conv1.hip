@@ -1,0 +1,431 @@
+// First conv layer of the reference CNN (train_tf_ps.py:351-353: Conv2D(8, 5x5, 'same') on the
+// 3-channel image, PReLU, MaxPooling2D) as two position-major kernels with nothing but the pooled
+// output in between:
+//
+//   conv1_fwd_pm_k   pooled = maxpool2x2(prelu(conv(x) + bias, alpha))       (writes 2 B/pooled elt)
+//   conv1_bwd_pm_k   recomputes z, the PReLU and the window argmax from x in registers, turns the
+//                    pooled gradient dp into dZ (non-zero only at each window's argmax), and in the
+//                    same pass accumulates dW (MFMA over the tile's pixels), dalpha and dbias.
+//
+// The previous pipeline (conv.hip conv1_pair_pool_k EPI_POOLS -> prelu_pool_bwd_sel_k ->
+// conv_wgrad_strip_k SPARSE) wrote a z-at-argmax + argmax record in the forward (126 MB at batch
+// 256, 256x320), read it back and wrote/read a dZ record in between (210 MB more): three kernels
+// and ~0.6 GB of traffic for a layer whose math is 25 GFLOP.  Recomputing the 5x5x4 -> 8 conv in
+// the backward costs 8 MFMAs per wave and tile, far less than moving those records.
+//
+// Work decomposition (both kernels): a workgroup owns one 64x4-pixel output tile POSITION and a
+// contiguous chunk of samples, and walks the samples.  Per-position operands (alpha, and in the
+// backward the dalpha partial sums) stay in registers for the whole chunk; the next sample's halo
+// (and pooled gradient) is prefetched into registers while this sample computes, into a second LDS
+// halo buffer.  Items are laid out th-fastest and handed to XCDs in contiguous ranges (xcd_remap),
+// so the two tiles sharing halo rows run at the same pace on the same L2.
+//
+// MFMA layout of the conv (shared with conv1_pair_pool_k): A rows 0-7 = the 8 filters, rows 8-15 the
+// same filters shifted one column right (they fit the spare kw' = 5 column of the KWP = 6 padded K),
+// B columns = 16 even pixels, so one v_mfma_f32_16x16x32_bf16 yields all 8 channels of 32 pixels;
+// lane (px, g) ends with pixel 2*px + (g >> 1), channels 4*(g & 1) .. +3; the horizontal pool
+// partner is lane ^ 32, the vertical one the wave's other fragment.
+//
+// The weight gradient is the conv_wgrad_strip_k GEMM (M = Cout, N = (kh, kw, ci) = 100, K = the
+// tile's 256 pixels) with both operands read by ds_read_b64_tr_b16: dZ from a [pixel][co] LDS tile,
+// x from the same halo buffer the recompute used.
+#include "common.h"
+#include "conv_common.h"
+
+namespace ptgc1 {
+using namespace ptgc;
+
+constexpr int KS = 5, C = 4, TW = 64, TH = 4, KWP = KS + 1, PAD = 2, COUT = 8;
+constexpr int HR = TH + KS - 1;                 // halo rows
+constexpr int HC = TW + KWP - 1;                // halo columns
+constexpr int HP = (HC + 1) / 2;                // 16-byte pixel pairs per halo row
+constexpr int ROWE = HP * 8;                    // halo row pitch (elements)
+constexpr int HBUF = HR * ROWE;                 // one halo buffer (elements)
+constexpr int KROW = KWP * C, KTOT = KS * KROW, KSTEPS = (KTOT + 31) / 32;
+constexpr int PFN = (HR * HP + 255) / 256;      // halo pair slots per thread
+constexpr int MPIX = TH * TW;                   // pixels per tile (K of the weight-gradient GEMM)
+constexpr int DPITCH = 20;                      // dZ tile pixel pitch (bf16): 16 MFMA rows + bank shift
+constexpr int KF = KS * KS * C;                 // weight-gradient columns (kh, kw, ci)
+constexpr int NB = 2;                           // 16-column B fragments per wave (4 waves x 32 >= KF)
+constexpr int ZSLOT = 2 * HBUF;                 // 8 zero elements: reads of K past KTOT / KF
+static_assert(4 * NB * 16 >= KF, "weight-gradient columns");
+
+struct Item { int oh0, ow0, n0, n1; };
+
+// item = chunk-major, position th-fastest; xcd_remap gives every XCD a contiguous item range
+PTG_DEV Item work_item(int N, int tiles_h, int tiles_w, int nchunks) {
+  const int npos = tiles_h * tiles_w;
+  const int item = xcd_remap(blockIdx.x, gridDim.x);
+  const int chunk = item / npos, pos = item - chunk * npos;
+  const int twi = pos / tiles_h, thi = pos - twi * tiles_h;
+  Item it;
+  it.oh0 = thi * TH;
+  it.ow0 = twi * TW;
+  it.n0 = (int)((long)N * chunk / nchunks);
+  it.n1 = (int)((long)N * (chunk + 1) / nchunks);
+  return it;
+}
+
+// A operand: row px = filter (px & 7), shifted one column right when px >= 8
+PTG_DEV void load_wreg(const bf16_t* __restrict__ w, int px, int g, bf16x8_t* wreg) {
+  const int co = px & 7, sh = px >> 3;
+#pragma unroll
+  for (int ks = 0; ks < KSTEPS; ++ks) {
+    const int kf = ks * 32 + 8 * g;
+    U4 v = zero4();
+    if (kf < KTOT) {
+      const int kh = kf / KROW, kw = (kf - kh * KROW) / C;  // kw even
+      const bf16_t* wp = w + ((long)co * KS + kh) * KS * C;
+      const int a = kw - sh, b = kw + 1 - sh;
+      if (a >= 0 && a < KS) { const U2 t = *(const U2*)(wp + a * C); v.x = t.x; v.y = t.y; }
+      if (b >= 0 && b < KS) { const U2 t = *(const U2*)(wp + b * C); v.z = t.x; v.w = t.y; }
+    }
+    wreg[ks] = __builtin_bit_cast(bf16x8_t, v);
+  }
+}
+
+// One sample's halo: HR rows x HP pixel pairs, zero outside the image (buffer-load range check).
+template <bool U8>
+struct Halo {
+  U4 pf[U8 ? 1 : PFN];
+  U8Pair pu[U8 ? PFN : 1];
+  // slot p of this thread: halo row idx / HP, pair idx % HP with idx = tid + 256 p (recomputed at
+  // each use: cheaper than 2 * PFN live registers across the sample loop)
+  PTG_DEV void load(const Rsrc& xr, int n, int H, int W, int oh0, int ow0) {
+#pragma unroll
+    for (int p = 0; p < PFN; ++p) {
+      const int idx = (int)threadIdx.x + p * 256, r = idx / HP, c = idx - r * HP;
+      const int ih = oh0 - PAD + r, iw = ow0 - PAD + 2 * c;
+      const bool ok = r < HR && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+      if constexpr (U8) {  // iw even, W even: the pair's second pixel is in the row too
+        pu[p] = u8pair_load(xr, (uint32_t)((n * H + ih) * W + iw) * 3u, ok);
+      } else {
+        pf[p] = bload16(xr, ok ? (uint32_t)(((n * H + ih) * W + iw) * C) * 2u : PTG_OOB);
+      }
+    }
+  }
+  PTG_DEV void store(bf16_t* buf) const {
+#pragma unroll
+    for (int p = 0; p < PFN; ++p) {
+      const int idx = (int)threadIdx.x + p * 256, r = idx / HP, c = idx - r * HP;
+      if (r < HR) {
+        U4 v;
+        if constexpr (U8) v = u8pair_to_bf16x8(pu[p]);
+        else v = pf[p];
+        *(U4*)(buf + r * ROWE + c * 8) = v;
+      }
+    }
+  }
+};
+
+template <bool U8>
+PTG_DEV Rsrc x_rsrc(const void* x, int N, int H, int W) {
+  return make_rsrc(x, U8 ? u8_rsrc_bytes((long)N * H * W * 3) : (uint32_t)((long)N * H * W * C * 2));
+}
+
+// z (fp32 accumulators, 2 row fragments x 4 channels) of this wave's 32 x 2 pixels from halo `hb`
+PTG_DEV void conv_tile(const bf16_t* hb, const bf16_t* smem, const bf16x8_t* wreg, int rp, int hf, int px, int g,
+                       f32x4_t* acc) {
+  acc[0] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  acc[1] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < KSTEPS; ++ks) {
+    const int kf = ks * 32 + 8 * g;
+    const int kh = kf / KROW, kw = (kf - kh * KROW) / C;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const bf16_t* src = kf < KTOT ? hb + (2 * rp + i + kh) * ROWE + (hf * 32 + 2 * px + kw) * C : smem + ZSLOT;
+      const bf16x8_t xf = *(const bf16x8_t*)src;
+      acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wreg[ks], xf, acc[i], 0, 0, 0);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// forward: pooled output only
+// ------------------------------------------------------------------------------------------------
+template <bool U8>
+__global__ __launch_bounds__(256) void conv1_fwd_pm_k(const void* __restrict__ x, const bf16_t* __restrict__ w,
+                                                      const float* __restrict__ bias, const float* __restrict__ alpha,
+                                                      bf16_t* __restrict__ pooled, int N, int H, int W, int tiles_h,
+                                                      int tiles_w, int nchunks) {
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * HBUF + 8];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int px = lane & 15, g = lane >> 4, hf = wid & 1, rp = wid >> 1;
+  if (tid < 8) smem[ZSLOT + tid] = 0;
+  const Item it = work_item(N, tiles_h, tiles_w, nchunks);
+  if (it.n0 >= it.n1) return;  // whole workgroup
+  bf16x8_t wreg[KSTEPS];
+  load_wreg(w, px, g, wreg);
+  const int cc = 4 * (g & 1);
+  float bv[4] = {0.f, 0.f, 0.f, 0.f};
+  if (bias) { const float4 b4 = *(const float4*)(bias + cc); bv[0] = b4.x; bv[1] = b4.y; bv[2] = b4.z; bv[3] = b4.w; }
+  const int ow = it.ow0 + hf * 32 + 2 * px + (g >> 1);
+  float al[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int oh = it.oh0 + 2 * rp + i;
+    const float4 a = (oh < H && ow < W) ? *(const float4*)(alpha + ((long)oh * W + ow) * COUT + cc)
+                                        : make_float4(0.f, 0.f, 0.f, 0.f);
+    al[i][0] = a.x; al[i][1] = a.y; al[i][2] = a.z; al[i][3] = a.w;
+  }
+  const int PH = H >> 1, PW = W >> 1;
+  const int ph = (it.oh0 >> 1) + rp, pw = (it.ow0 >> 1) + hf * 16 + px;
+  const bool store_lane = g < 2 && ph < PH && pw < PW;
+  const Rsrc xr = x_rsrc<U8>(x, N, H, W);
+  Halo<U8> hl;
+  hl.load(xr, it.n0, H, W, it.oh0, it.ow0);
+  hl.store(smem);
+  __syncthreads();
+  for (int n = it.n0; n < it.n1; ++n) {
+    const int b = (n - it.n0) & 1;
+    const bool has_next = n + 1 < it.n1;
+    if (has_next) hl.load(xr, n + 1, H, W, it.oh0, it.ow0);
+    f32x4_t acc[2];
+    conv_tile(smem + b * HBUF, smem, wreg, rp, hf, px, g, acc);
+    float pm[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float y[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const float zr = bf2f(f2bf(acc[i][r] + bv[r]));  // PReLU of the bf16-rounded z (as the backward)
+        y[i] = zr > 0.f ? zr : al[i][r] * zr;
+      }
+      const float v = fmaxf(y[0], y[1]);
+      pm[r] = fmaxf(v, __shfl_xor(v, 32, 64));
+    }
+    if (store_lane)
+      *(U2*)(pooled + (((long)n * PH + ph) * PW + pw) * COUT + cc) = U2{pack_bf(pm[0], pm[1]), pack_bf(pm[2], pm[3])};
+    if (has_next) hl.store(smem + (b ^ 1) * HBUF);  // buffer b^1 was last read before the previous barrier
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// backward: recompute + PReLU/pool backward + weight gradient, one pass
+// ------------------------------------------------------------------------------------------------
+template <bool U8>
+__global__ __launch_bounds__(256, 4) void conv1_bwd_pm_k(const void* __restrict__ x, const bf16_t* __restrict__ w,
+                                                      const float* __restrict__ bias, const float* __restrict__ alpha,
+                                                      const bf16_t* __restrict__ dp, float* __restrict__ dw,
+                                                      float* __restrict__ dalpha, float* __restrict__ dbias, int N,
+                                                      int H, int W, int tiles_h, int tiles_w, int nchunks) {
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * HBUF + 8 + MPIX * DPITCH + 8];
+  __shared__ float sdb[4][COUT];
+  bf16_t* const ds = smem + 2 * HBUF + 8;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int px = lane & 15, g = lane >> 4, hf = wid & 1, rp = wid >> 1;
+  if (tid < 8) smem[ZSLOT + tid] = 0;
+  for (int i = tid; i < (MPIX * DPITCH + 8) / 8; i += 256) *(U4*)(ds + 8 * i) = zero4();  // MFMA rows 8-15: 0
+  const Item it = work_item(N, tiles_h, tiles_w, nchunks);
+  if (it.n0 >= it.n1) return;  // whole workgroup
+  bf16x8_t wreg[KSTEPS];
+  load_wreg(w, px, g, wreg);
+  const int cc = 4 * (g & 1), dwo = g >> 1;
+  // the 8 biases stay wave-uniform (scalar registers); each lane selects its 4 per sample
+  float b8[COUT];
+#pragma unroll
+  for (int c = 0; c < COUT; ++c) b8[c] = bias ? __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(bias[c]))) : 0.f;
+  const int ow = it.ow0 + hf * 32 + 2 * px + dwo;
+  float al[2][4], da[2][4], db[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int oh = it.oh0 + 2 * rp + i;
+    const float4 a = (oh < H && ow < W) ? *(const float4*)(alpha + ((long)oh * W + ow) * COUT + cc)
+                                        : make_float4(0.f, 0.f, 0.f, 0.f);
+    al[i][0] = a.x; al[i][1] = a.y; al[i][2] = a.z; al[i][3] = a.w;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) da[i][r] = 0.f;
+  }
+  const int PH = H >> 1, PW = W >> 1;
+  const int ph = (it.oh0 >> 1) + rp, pw = (it.ow0 >> 1) + hf * 16 + px;
+  const bool pin = ph < PH && pw < PW;
+  const Rsrc xr = x_rsrc<U8>(x, N, H, W);
+  const Rsrc dr = make_rsrc(dp, (uint32_t)((long)N * PH * PW * COUT * 2));
+  auto dp_off = [&](int n) { return pin ? (uint32_t)((((n * PH + ph) * PW + pw) * COUT + cc) * 2) : PTG_OOB; };
+  const int li = lane & 15;
+  f32x4_t wacc[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) wacc[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  // this lane's two dZ pixels in the tile (row 2*rp + i, column hf*32 + 2*px + dwo)
+  const int m_lane = (2 * rp) * TW + hf * 32 + 2 * px + dwo;
+
+  Halo<U8> hl;
+  hl.load(xr, it.n0, H, W, it.oh0, it.ow0);
+  U2 dpr = bload8(dr, dp_off(it.n0));
+  hl.store(smem);
+  __syncthreads();
+  for (int n = it.n0; n < it.n1; ++n) {
+    const int b = (n - it.n0) & 1;
+    const bf16_t* hb = smem + b * HBUF;
+    const bool has_next = n + 1 < it.n1;
+    const U2 dcur = dpr;
+    // lane-derived LDS offsets are recomputed per sample from an opaque copy of the lane id:
+    // hoisted out of the sample loop they would pin ~50 address registers and spill
+    int ol = lane;
+    asm volatile("" : "+v"(ol));
+    const int opx = ol & 15, og = ol >> 4, oq = (ol & 15) >> 2, op = ol & 3;
+    if (has_next) {
+      hl.load(xr, n + 1, H, W, it.oh0, it.ow0);
+      dpr = bload8(dr, dp_off(n + 1));
+    }
+    f32x4_t acc[2];
+    conv_tile(hb, smem, wreg, rp, hf, opx, og, acc);
+    const float gv[4] = {lo_bf(dcur.x), hi_bf(dcur.x), lo_bf(dcur.y), hi_bf(dcur.y)};
+    float dz[2][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float zr[2], y[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        zr[i] = bf2f(f2bf(acc[i][r] + ((og & 1) ? b8[4 + r] : b8[r])));
+        y[i] = zr[i] > 0.f ? zr[i] : al[i][r] * zr[i];
+      }
+      // window (dh, dw) in q = 2*dh + dw order; this lane holds dw = dwo, the partner lane ^ 32 the other
+      const float p0 = __shfl_xor(y[0], 32, 64), p1 = __shfl_xor(y[1], 32, 64);
+      const float yq[4] = {dwo ? p0 : y[0], dwo ? y[0] : p0, dwo ? p1 : y[1], dwo ? y[1] : p1};
+      float best = yq[0];
+      int a = 0;
+#pragma unroll
+      for (int qq = 1; qq < 4; ++qq)
+        if (yq[qq] > best) { best = yq[qq]; a = qq; }  // first maximum wins (as the forward record)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const bool hit = a == 2 * i + dwo;
+        const bool pos = zr[i] > 0.f;
+        const float gq = hit ? gv[r] : 0.f;
+        dz[i][r] = pos ? gq : gq * al[i][r];
+        da[i][r] += pos ? 0.f : gq * zr[i];
+        db[r] += dz[i][r];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      *(U2*)(ds + (m_lane + i * TW) * DPITCH + cc) = U2{pack_bf(dz[i][0], dz[i][1]), pack_bf(dz[i][2], dz[i][3])};
+    __syncthreads();  // dZ tile complete
+#pragma unroll 2
+    for (int k0 = 0; k0 < MPIX; k0 += 32) {
+      const int m0 = k0 + 8 * og + oq, m1 = m0 + 4;
+      const s16x4_t alo = tr_read(ds + m0 * DPITCH + 4 * op);
+      const s16x4_t ahi = tr_read(ds + m1 * DPITCH + 4 * op);
+      U2 ua = __builtin_bit_cast(U2, alo), ub = __builtin_bit_cast(U2, ahi);
+      const bf16x8_t af = __builtin_bit_cast(bf16x8_t, U4{ua.x, ua.y, ub.x, ub.y});
+      const int h0 = (m0 / TW) * ROWE + (m0 % TW) * C, h1 = (m1 / TW) * ROWE + (m1 % TW) * C;
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        // B column (kflat) base of this lane: (kh, kw) of kf = (wid*NB + j)*16 + 4*op, ci = 0..3
+        const int kf = (wid * NB + j) * 16 + 4 * op;
+        const int kh = kf / (KS * C), kw = (kf - kh * KS * C) / C;
+        const bool bv_ok = kf < KF;
+        const bf16_t* s0 = bv_ok ? hb + h0 + kh * ROWE + kw * C : smem + ZSLOT;
+        const bf16_t* s1 = bv_ok ? hb + h1 + kh * ROWE + kw * C : smem + ZSLOT;
+        const s16x4_t blo = tr_read(s0), bhi = tr_read(s1);
+        ua = __builtin_bit_cast(U2, blo);
+        ub = __builtin_bit_cast(U2, bhi);
+        const bf16x8_t bfr = __builtin_bit_cast(bf16x8_t, U4{ua.x, ua.y, ub.x, ub.y});
+        wacc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, wacc[j], 0, 0, 0);
+      }
+    }
+    if (has_next) hl.store(smem + (b ^ 1) * HBUF);
+    __syncthreads();  // next halo visible; this dZ tile fully read before it is rewritten
+  }
+  // flush: dW rows co = g*4 + r (< 8), columns kf = (wid*NB + j)*16 + li
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int kf = (wid * NB + j) * 16 + li;
+    if (kf < KF && g < 2) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) atomicAdd(dw + (g * 4 + r) * KF + kf, wacc[j][r]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int oh = it.oh0 + 2 * rp + i;
+    if (oh < H && ow < W) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (da[i][r] != 0.f) atomicAdd(dalpha + ((long)oh * W + ow) * COUT + cc + r, da[i][r]);
+    }
+  }
+  // dbias: sum over the 16 px lanes and the two pixel halves (lane ^ 32), then over the waves
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float v = db[r];
+    v += __shfl_xor(v, 1, 64);
+    v += __shfl_xor(v, 2, 64);
+    v += __shfl_xor(v, 4, 64);
+    v += __shfl_xor(v, 8, 64);
+    v += __shfl_xor(v, 32, 64);
+    db[r] = v;
+  }
+  if (px == 0 && g < 2) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sdb[wid][cc + r] = db[r];
+  }
+  __syncthreads();
+  if (tid < COUT) atomicAdd(dbias + tid, sdb[0][tid] + sdb[1][tid] + sdb[2][tid] + sdb[3][tid]);
+}
+
+// sample chunks per tile position: as many work items as fit the device at once (one wave of
+// workgroups, no tail), or PTG_CONV1_*_PER_CU workgroups per CU when set
+static int conv1_chunks(int N, long npos, const void* kern, const char* env) {
+  long slots = ptg_resident_blocks(kern);
+  if (const char* e = getenv(env)) {
+    static int cus = 0;
+    if (!cus) {
+      int dev = 0;
+      hipGetDevice(&dev);
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      if (cus <= 0) cus = 256;
+    }
+    if (atoi(e) > 0) slots = (long)cus * atoi(e);
+  }
+  long c = slots / npos;
+  if (c > N) c = N;
+  return (int)(c < 1 ? 1 : c);
+}
+
+}  // namespace ptgc1
+
+using namespace ptgc1;
+
+extern "C" {
+
+// pooled [N][H/2][W/2][8] = maxpool2x2(prelu(conv5x5(x) + bias, alpha)); x is the raw uint8
+// [N][H][W][3] image batch (u8 = 1) or bf16 [N][H][W][4]; w bf16 [8][5][5][4]; alpha fp32 [H][W][8].
+int ptg_conv1_fwd_pm(const void* x, int u8, const void* w, const float* bias, const float* alpha, void* pooled, int N,
+                     int H, int W, hipStream_t s) {
+  if ((H & 1) || (W & 1) || N <= 0 || !ptg_fits_2g((long)N * H * W * (u8 ? 3 : 8)) ||
+      !ptg_fits_2g((long)N * H * W * 4))
+    return (int)hipErrorInvalidValue;
+  const int th = (H + TH - 1) / TH, tw = (W + TW - 1) / TW;
+  const auto kern = u8 ? conv1_fwd_pm_k<true> : conv1_fwd_pm_k<false>;
+  const int nch = conv1_chunks(N, (long)th * tw, (const void*)kern, "PTG_CONV1_FWD_PER_CU");
+  const long items = (long)th * tw * nch;
+  if (items > 0x7fffffff) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(kern, dim3((unsigned)items), dim3(256), 0, s, x, (const bf16_t*)w, bias, alpha, (bf16_t*)pooled,
+                     N, H, W, th, tw, nch);
+  PTG_RETURN_LAUNCH();
+}
+
+// Backward of ptg_conv1_fwd_pm from the pooled gradient dp [N][H/2][W/2][8] (bf16): accumulates
+// (atomically, onto zeroed buffers) dw fp32 [8][5][5][4], dalpha fp32 [H][W][8], dbias fp32 [8].
+int ptg_conv1_bwd_pm(const void* x, int u8, const void* w, const float* bias, const float* alpha, const void* dp,
+                     float* dw, float* dalpha, float* dbias, int N, int H, int W, hipStream_t s) {
+  if ((H & 1) || (W & 1) || N <= 0 || !ptg_fits_2g((long)N * H * W * (u8 ? 3 : 8)) ||
+      !ptg_fits_2g((long)N * H * W * 4))
+    return (int)hipErrorInvalidValue;
+  const int th = (H + TH - 1) / TH, tw = (W + TW - 1) / TW;
+  const auto kern = u8 ? conv1_bwd_pm_k<true> : conv1_bwd_pm_k<false>;
+  const int nch = conv1_chunks(N, (long)th * tw, (const void*)kern, "PTG_CONV1_BWD_PER_CU");
+  const long items = (long)th * tw * nch;
+  if (items > 0x7fffffff) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(kern, dim3((unsigned)items), dim3(256), 0, s, x, (const bf16_t*)w, bias, alpha,
+                     (const bf16_t*)dp, dw, dalpha, dbias, N, H, W, th, tw, nch);
+  PTG_RETURN_LAUNCH();
+}
+
+}  // extern "C"
+
+PTG_CHECK_STATUS(conv1)

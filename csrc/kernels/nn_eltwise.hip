@@ -516,11 +516,13 @@ __global__ __launch_bounds__(256) void prelu_bwd_sg_k(const bf16_t* __restrict__
 }
 
 // out_bf16[m][n] = act(acc[m][n] + bias[n])   (split-K GEMM finishing pass)
-__global__ __launch_bounds__(256) void bias_act_k(const float* __restrict__ acc,
+// clear: zero the accumulator after reading it, so the next split-K GEMM into it needs no fill
+__global__ __launch_bounds__(256) void bias_act_k(float* __restrict__ acc,
                                                   const float* __restrict__ bias, bf16_t* __restrict__ out,
-                                                  float* __restrict__ out32, long total, int N, int act) {
+                                                  float* __restrict__ out32, long total, int N, int act, int clear) {
   for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
     float v = acc[i] + (bias ? bias[i % N] : 0.f);
+    if (clear) acc[i] = 0.f;
     if (act == 1) v = fmaxf(v, 0.f);
     if (out) out[i] = f2bf(v);
     if (out32) out32[i] = v;
@@ -1148,11 +1150,11 @@ int ptg_head_mse(void* acc, const float* b1, const float* w2, const float* b2, c
   PTG_RETURN_LAUNCH();
 }
 
-int ptg_bias_act(const float* acc, const float* bias, void* out_bf16, float* out32, long M, int N, int act,
+int ptg_bias_act(float* acc, const float* bias, void* out_bf16, float* out32, long M, int N, int act, int clear,
                  hipStream_t s) {
   const long total = M * N;
   hipLaunchKernelGGL(bias_act_k, dim3(grid_for(total)), dim3(256), 0, s, acc, bias, (bf16_t*)out_bf16, out32,
-                     total, N, act);
+                     total, N, act, clear);
   PTG_RETURN_LAUNCH();
 }
 

@@ -44,6 +44,12 @@ SPARSE_FIRST = config.get("sparse_first")
 # packed bf16 copy of the input (pack_u8rgb4_k: 3 B read + 8 B written per pixel, 8 B read twice
 # more) is never made.  PTG_RAW_U8_INPUT=0 restores the pack.
 RAW_U8 = config.get("raw_u8_input")
+# With CONV1_FUSED (default) that first layer runs as two position-major kernels instead
+# (conv1.hip): the forward writes only the pooled output, and ONE backward kernel recomputes z, the
+# PReLU and the pool argmax from x and accumulates dW, dalpha and dbias from the pooled gradient -
+# no record, no dZ, no separate prelu/pool backward.  PTG_CONV1_FUSED=0 restores the sparse-record
+# pipeline above for A/B.
+CONV1_FUSED = config.get("conv1_fused")
 
 
 def host_fp32(enabled: bool | None = None) -> bool:
@@ -150,7 +156,26 @@ class ConvOp(Op):
                 and self.pool is not None and OH % 2 == 0 and OW % 2 == 0 and self.conv.activation != "relu"
                 and self._halo()[0])
 
+    def _fused1_ok(self, x) -> bool:
+        """First layer served by conv1.hip (5x5, 3(+pad) -> 8, pad 2, PReLU/ReLU/identity + 2x2 pool)."""
+        OH, OW, Co = self.conv.out_shape
+        if not (CONV1_FUSED and self.first and x.is_cuda and x.dim() == 4 and self.pool is not None
+                and self.conv.cin_p == 4 and self.conv.kernel_size == (5, 5) and self.stride == 1
+                and self.pad == 2 and Co == 8 and OH % 2 == 0 and OW % 2 == 0 and self._halo()[0]):
+            return False
+        if x.dtype == torch.uint8:  # raw images: only at the layer's own size (no resize pass)
+            return RAW_U8 and x.shape[-1] == 3 and tuple(x.shape[1:3]) == tuple(self.conv.in_shape[:2])
+        return True
+
     def forward(self, x, ws, training):
+        self._fused1 = False
+        if self._fused1_ok(x):
+            x = x.contiguous() if x.dtype == torch.uint8 else self._prep_input(x, ws)
+            OH, OW, Co = self.conv.out_shape
+            p = ws.get(self.name + "/p", (x.shape[0], OH // 2, OW // 2, Co), torch.bfloat16, x.device)
+            b = self.conv.bias.data if self.conv.bias is not None else None
+            self._fused1, self._x, self._sel, self._sparse = True, x, False, False
+            return K.conv1_fwd_pm(x, self.conv.kernel.bf16, b, self._pool_alpha(ws, x.device), p)
         if self._raw_u8_ok(x):
             x = x.contiguous()
             B = x.shape[0]
@@ -229,6 +254,18 @@ class ConvOp(Op):
         K.conv2d_wgrad_halo_sparse(x, dzs, self._arg, self.pad, self.conv.kernel.grad, zeroed=True)
         return None
 
+    def _backward_fused1(self, x, dy, ws, dev):
+        """First layer, conv1.hip: one kernel from the pooled gradient to dW / dalpha / dbias."""
+        OH, OW, Co = self.conv.out_shape
+        bias_g = self.conv.bias.grad if self.conv.bias is not None else \
+            ws.get(self.name + "/nobias", (Co,), torch.float32, dev)
+        dalpha = self.prelu.alpha.grad if self.prelu is not None else \
+            ws.get(self.name + "/dalpha_dummy", (OH, OW, Co), torch.float32, dev)
+        b = self.conv.bias.data if self.conv.bias is not None else None
+        K.conv1_bwd_pm(x, self.conv.kernel.bf16, b, self._pool_alpha(ws, dev), dy, self.conv.kernel.grad, dalpha,
+                       bias_g)
+        return None
+
     def _forward_halo(self, x, z, b, ws, B, OH, OW, Co, dev):
         """One kernel: conv + bias, and the PReLU/ReLU (+ 2x2 max-pool) epilogue fused in."""
         w = self.conv.kernel.bf16
@@ -252,6 +289,8 @@ class ConvOp(Op):
         x = self._x
         dev = x.device
         dy = _bf16(dy, ws, self.name + "/dy16")
+        if getattr(self, "_fused1", False):
+            return self._backward_fused1(x, dy, ws, dev)
         if getattr(self, "_sel", False):
             return self._backward_sel(x, dy, ws, dev)
         zshape = self._zshape if self._sparse else self._z.shape
@@ -325,8 +364,9 @@ class DenseOp(Op):
         if self.big:
             x = _bf16(x, ws, self.name + "/x16")
             y = ws.get(self.name + "/y", (B, N), torch.bfloat16, dev)
-            wsp = ws.get(self.name + "/splitk", (B * N,), torch.float32, dev)
-            K.linear_fwd(x, self.dense.kernel.bf16, b, act, y, workspace=wsp)
+            # created zeroed and cleared again by the bias/activation pass after each use
+            wsp = ws.get(self.name + "/splitk", (B * N,), torch.float32, dev, zero=True)
+            K.linear_fwd(x, self.dense.kernel.bf16, b, act, y, workspace=wsp, workspace_zeroed=True)
         else:
             y = ws.get(self.name + "/y", (B, N), torch.float32, dev)
             K.dense_small_fwd(x, self.dense.kernel.data, b, act, y)

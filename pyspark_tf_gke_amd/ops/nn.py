@@ -195,6 +195,57 @@ def conv2d_wgrad_halo_sparse(x, dzsel, arg, pad: int, out, zeroed: bool = False)
     return out
 
 
+def _conv1_check(x, w, alpha, N, H, W):
+    if x.dtype == torch.uint8:
+        assert x.shape[-1] == 3, "conv1: uint8 input is the [N,H,W,3] image batch"
+    else:
+        need(x, torch.bfloat16, "conv1.x")
+        assert x.shape[-1] == 4, "conv1: bf16 input is the channel-padded [N,H,W,4] batch"
+    assert x.is_contiguous(), "conv1: x must be contiguous"
+    need(w, torch.bfloat16, "conv1.w")
+    assert tuple(w.shape) == (8, 5, 5, 4), w.shape
+    need(alpha, torch.float32, "conv1.alpha")
+    assert tuple(alpha.shape) == (H, W, 8), alpha.shape
+    if H % 2 or W % 2:
+        raise ValueError("conv1: H and W must be even (2x2 pool)")
+
+
+def conv1_fwd_pm(x, w, bias, alpha, pooled):
+    """First conv layer of the reference CNN in one kernel (conv1.hip conv1_fwd_pm_k): pooled =
+    maxpool2x2(prelu(conv5x5(x, w, pad 2) + bias, alpha)), nothing else written.  x is the raw
+    uint8 [N,H,W,3] image batch (/255 in registers) or bf16 [N,H,W,4]; w bf16 [8,5,5,4]."""
+    if not on_device(x):
+        return ref.conv1_fwd_pm(x, w, bias, alpha, pooled)
+    N, H, W, _ = x.shape
+    _conv1_check(x, w, alpha, N, H, W)
+    need(pooled, torch.bfloat16, "conv1.pooled")
+    assert tuple(pooled.shape) == (N, H // 2, W // 2, 8), pooled.shape
+    if bias is not None:
+        need(bias, torch.float32, "conv1.bias")
+    hip("ptg_conv1_fwd_pm", ptr(x), int(x.dtype == torch.uint8), ptr(w), ptr(bias), ptr(alpha), ptr(pooled), N, H, W)
+    return pooled
+
+
+def conv1_bwd_pm(x, w, bias, alpha, dp, dw, dalpha, dbias):
+    """Backward of :func:`conv1_fwd_pm` in one kernel (conv1.hip conv1_bwd_pm_k): z, the PReLU and
+    the pool argmax are recomputed from x; dw [8,5,5,4], dalpha [H,W,8] and dbias [8] (fp32)
+    accumulate atomically (the caller provides them zeroed or holding the sum so far)."""
+    if not on_device(x):
+        return ref.conv1_bwd_pm(x, w, bias, alpha, dp, dw, dalpha, dbias)
+    N, H, W, _ = x.shape
+    _conv1_check(x, w, alpha, N, H, W)
+    need(dp, torch.bfloat16, "conv1.dp")
+    assert tuple(dp.shape) == (N, H // 2, W // 2, 8), dp.shape
+    need(dw, torch.float32, "conv1.dw"); need(dalpha, torch.float32, "conv1.dalpha")
+    need(dbias, torch.float32, "conv1.dbias")
+    assert tuple(dw.shape) == (8, 5, 5, 4) and tuple(dalpha.shape) == (H, W, 8) and dbias.numel() == 8
+    if bias is not None:
+        need(bias, torch.float32, "conv1.bias")
+    hip("ptg_conv1_bwd_pm", ptr(x), int(x.dtype == torch.uint8), ptr(w), ptr(bias), ptr(alpha), ptr(dp), ptr(dw),
+        ptr(dalpha), ptr(dbias), N, H, W)
+    return dw
+
+
 def set_persist_mode(dynamic: bool | None) -> None:
     """Persistent conv kernels: True = claim tile chunks from a work queue (robust when another
     stream's kernels, e.g. RCCL collectives overlapping the backward, hold CUs), False = static
@@ -256,9 +307,11 @@ def gemm(M, N, K, a, lda, a_kcontig, b, ldb, b_kcontig, epi, c, ldc, bias=None, 
         ptr(bias), act, splits)
 
 
-def linear_fwd(x, w, bias, act, out, workspace=None, splits: int = 0):
+def linear_fwd(x, w, bias, act, out, workspace=None, splits: int = 0, workspace_zeroed: bool = False):
     """out[M,N] bf16 = act(x[M,K] @ w[N,K]^T + bias). Split-K with an fp32 workspace when the
-    output tile grid alone cannot fill the 256 CUs (e.g. M=batch, K=20480)."""
+    output tile grid alone cannot fill the 256 CUs (e.g. M=batch, K=20480).  ``workspace_zeroed``:
+    the workspace holds zeros (a persistent buffer created zeroed): the split-K partial sums land on
+    it directly and the bias/activation pass clears it again for the next call (no fill kernel)."""
     if not on_device(x):
         return ref.linear_fwd(x, w, bias, act, out)
     M, K = x.shape
@@ -269,10 +322,12 @@ def linear_fwd(x, w, bias, act, out, workspace=None, splits: int = 0):
     if splits > 1:
         if workspace is None or workspace.numel() < M * N:
             workspace = torch.empty(M * N, device=x.device, dtype=torch.float32)
+            workspace_zeroed = False
         ws = workspace[: M * N]
-        ws.zero_()
+        if not workspace_zeroed:
+            ws.zero_()
         gemm(M, N, K, x, K, 1, w, K, 1, 3, ws, N, None, 0, splits)
-        hip("ptg_bias_act", ptr(ws), ptr(bias), ptr(out), None, M, N, ACT[act])
+        hip("ptg_bias_act", ptr(ws), ptr(bias), ptr(out), None, M, N, ACT[act], int(workspace_zeroed))
     else:
         gemm(M, N, K, x, K, 1, w, K, 1, 0, out, N, bias, ACT[act], 1)
     return out
@@ -349,7 +404,7 @@ def bias_act(acc, bias, act, out_bf16=None, out32=None):
     if not on_device(acc):
         return ref.bias_act(acc, bias, act, out_bf16, out32)
     M, N = acc.shape
-    hip("ptg_bias_act", ptr(acc), ptr(bias), ptr(out_bf16), ptr(out32), M, N, ACT[act])
+    hip("ptg_bias_act", ptr(acc), ptr(bias), ptr(out_bf16), ptr(out32), M, N, ACT[act], 0)
 
 
 def dense_small_fwd(x, w, b, act, out, out_bf16=None):

@@ -195,6 +195,44 @@ def prelu_pool_bwd_sel(dp, zsel, arg, alpha, dzsel_out, dalpha, dbias):
     return dzsel_out
 
 
+def conv1_input(x):
+    """The first-layer kernels' view of their input: uint8 [N,H,W,3] images -> /255, bf16-rounded,
+    zero 4th channel; bf16 [N,H,W,4] as is."""
+    if x.dtype == torch.uint8:
+        xf = (x.float() * (1.0 / 255.0)).to(torch.bfloat16).float()
+        return torch.cat([xf, torch.zeros_like(xf[..., :1])], dim=-1)
+    return _f(x)
+
+
+def _conv1_z(x, w, bias):
+    """bf16-rounded z = conv5x5(x) + bias of the first layer (fp32 math)."""
+    xn = conv1_input(x).permute(0, 3, 1, 2)
+    z = F.conv2d(xn, _f(w).permute(0, 3, 1, 2), None if bias is None else _f(bias), padding=2)
+    return z.permute(0, 2, 3, 1).to(torch.bfloat16).float()
+
+
+def conv1_fwd_pm(x, w, bias, alpha, pooled):
+    """pooled = maxpool2x2(prelu(conv5x5(x) + bias, alpha)) (conv1.hip conv1_fwd_pm_k)."""
+    return prelu_pool_fwd(_conv1_z(x, w, bias), alpha, pooled)
+
+
+def conv1_bwd_pm(x, w, bias, alpha, dp, dw, dalpha, dbias):
+    """Backward of conv1_fwd_pm from the pooled gradient: dw, dalpha, dbias accumulate."""
+    z = _conv1_z(x, w, bias)
+    N, H, W, C = z.shape
+    zsel = torch.empty((N, H // 2, W // 2, C))
+    arg = torch.empty((N, H // 2, W // 2, C), dtype=torch.uint8)
+    prelu_pool_fwd_sparse(z, alpha, torch.empty_like(zsel), zsel, arg)
+    dzs = torch.empty_like(zsel)
+    prelu_pool_bwd_sel(dp, zsel, arg, alpha, dzs, dalpha, dbias)
+    dz = expand_pool_record(dzs.to(torch.bfloat16), arg, (N, H, W, C))
+    xin = conv1_input(x)
+    g = torch.nn.grad.conv2d_weight(xin.permute(0, 3, 1, 2), (C, xin.shape[-1], 5, 5), dz.permute(0, 3, 1, 2),
+                                    padding=2)
+    dw.add_(g.permute(0, 2, 3, 1))
+    return dw
+
+
 def prelu_fwd(z, alpha, out):
     out.copy_(_prelu(_f(z), _f(alpha)).to(out.dtype))
     return out

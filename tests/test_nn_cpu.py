@@ -110,3 +110,36 @@ def test_odd_spatial_pooling_floor():
     x = torch.rand(2, 36, 44, 3)
     y = torch.rand(2, 2)
     assert np.isfinite(m.train_on_batch(x, y, return_dict=True)["loss"])
+
+
+def test_conv1_reference_matches_autograd():
+    """The fp32 oracle of the fused first-layer kernels (ops/reference.py conv1_fwd_pm / conv1_bwd_pm,
+    which the conv1.hip GPU tests compare against) equals autograd through
+    conv -> bias -> PReLU -> 2x2 max-pool on the same bf16-rounded z."""
+    from pyspark_tf_gke_amd.ops import reference as R
+
+    torch.manual_seed(0)
+    N, H, W = 2, 8, 12
+    x = torch.randint(0, 256, (N, H, W, 3), dtype=torch.uint8)
+    w = (torch.randn(8, 5, 5, 4) * 0.2).to(torch.bfloat16)
+    b, alpha = torch.randn(8) * 0.1, torch.rand(H, W, 8) * 0.5
+    dp = torch.randn(N, H // 2, W // 2, 8).to(torch.bfloat16)
+    p = torch.empty(N, H // 2, W // 2, 8)
+    R.conv1_fwd_pm(x, w, b, alpha, p)
+    dw, da, db = torch.zeros(8, 5, 5, 4), torch.zeros(H, W, 8), torch.zeros(8)
+    R.conv1_bwd_pm(x, w, b, alpha, dp, dw, da, db)
+
+    xin = R.conv1_input(x).permute(0, 3, 1, 2)
+    wf = w.float().detach().requires_grad_(True)
+    bf = b.clone().requires_grad_(True)
+    af = alpha.clone().requires_grad_(True)
+    z = torch.nn.functional.conv2d(xin, wf.permute(0, 3, 1, 2), bf, padding=2).permute(0, 2, 3, 1)
+    z = z + (z.to(torch.bfloat16).float() - z).detach()  # the kernels' bf16 rounding, straight-through
+    y = torch.where(z > 0, z, af * z)
+    pool = torch.nn.functional.max_pool2d(y.permute(0, 3, 1, 2), 2, 2).permute(0, 2, 3, 1)
+    pool.backward(dp.float())
+    assert torch.allclose(p, pool.detach(), atol=1e-6)
+    # dZ is bf16 in the kernels (and their oracle): 2^-8 relative per term of dW / dbias
+    assert torch.allclose(dw, wf.grad, rtol=1e-2, atol=1e-2)
+    assert torch.allclose(db, bf.grad, rtol=1e-2, atol=1e-2)
+    assert torch.allclose(da, af.grad, rtol=1e-3, atol=1e-3)

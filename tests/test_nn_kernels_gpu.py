@@ -279,6 +279,7 @@ def test_first_layer_sparse_chain_matches_dense(monkeypatch):
     x = torch.rand(4, 64, 80, 3)
     y = torch.rand(4, 2) * 50
     grads = {}
+    monkeypatch.setattr(E, "CONV1_FUSED", False)
     for mode in (False, True):
         monkeypatch.setattr(E, "SPARSE_FIRST", mode)
         m = build_cnn_model((64, 80, 3), flat=True, summary=False, device=DEV)
@@ -292,6 +293,93 @@ def test_first_layer_sparse_chain_matches_dense(monkeypatch):
         grads[mode] = {p.name: p.grad.detach().float().cpu().clone() for p in m.store.params}
     for name, g in grads[False].items():
         _close(grads[True][name], g, 2e-2, 1e-3, "sel_grad_" + name)
+
+
+def _conv1_inputs(N, H, W, u8):
+    if u8:
+        x = torch.randint(0, 256, (N, H, W, 3), dtype=torch.uint8)
+    else:
+        x = torch.cat([rnd(N, H, W, 3), torch.zeros(N, H, W, 1, dtype=torch.bfloat16)], -1)
+    w = rnd(8, 5, 5, 4, scale=0.2)
+    w[..., 3] = 0
+    b = torch.randn(8) * 0.1
+    alpha = torch.rand(H, W, 8) * 0.5
+    dp = rnd(N, H // 2, W // 2, 8, scale=0.1)
+    return x, w, b, alpha, dp
+
+
+@pytest.mark.parametrize("N,H,W,u8", [(3, 12, 140, True), (2, 14, 64, False), (5, 20, 70, False),
+                                      (7, 256, 320, True)])
+def test_conv1_fused_vs_reference(N, H, W, u8):
+    """conv1.hip: pooled output and dW / dalpha / dbias of the recomputing backward vs the fp32
+    reference (z rounded to bf16 as the kernels do)."""
+    x, w, b, alpha, dp = _conv1_inputs(N, H, W, u8)
+    p = torch.empty(N, H // 2, W // 2, 8, dtype=torch.bfloat16, device=DEV)
+    K.conv1_fwd_pm(x.to(DEV), w.to(DEV), b.to(DEV), alpha.to(DEV), p)
+    pr = torch.empty(N, H // 2, W // 2, 8)
+    R.conv1_fwd_pm(x, w, b, alpha, pr)
+    _close(p, pr, 2e-2, 2e-2, "conv1_pooled")
+    dw = torch.full((8, 5, 5, 4), 1.5, device=DEV)  # accumulates onto what is there
+    da = torch.full((H, W, 8), 0.25, device=DEV)
+    db = torch.full((8,), -1.0, device=DEV)
+    K.conv1_bwd_pm(x.to(DEV), w.to(DEV), b.to(DEV), alpha.to(DEV), dp.to(DEV), dw, da, db)
+    dwr, dar, dbr = torch.full((8, 5, 5, 4), 1.5), torch.full((H, W, 8), 0.25), torch.full((8,), -1.0)
+    R.conv1_bwd_pm(x, w, b, alpha, dp, dwr, dar, dbr)
+    _close(dw, dwr, 2e-2, 1e-2, "conv1_dw")
+    _close(db, dbr, 2e-2, 1e-2, "conv1_db")
+    # an argmax flip from a 1-ulp z difference moves one element's gradient: compare in the mean
+    assert (da.cpu() - dar).abs().mean().item() < 1e-3, "conv1_dalpha"
+
+
+@pytest.mark.parametrize("N,H,W,u8", [(4, 12, 140, True), (3, 16, 80, False), (16, 256, 320, True)])
+def test_conv1_fused_matches_sparse_record_pipeline(N, H, W, u8):
+    """Same MFMA math for z in both pipelines, so the argmax agrees exactly: the fused kernels must
+    reproduce the sparse-record pipeline (forward record -> sel backward -> sparse wgrad) up to
+    summation order."""
+    x, w, b, alpha, dp = _conv1_inputs(N, H, W, u8)
+    xd, wd, bd, ad, dpd = x.to(DEV), w.to(DEV), b.to(DEV), alpha.to(DEV), dp.to(DEV)
+    shp = (N, H // 2, W // 2, 8)
+    p1 = torch.empty(shp, dtype=torch.bfloat16, device=DEV)
+    K.conv1_fwd_pm(xd, wd, bd, ad, p1)
+    p0 = torch.empty(shp, dtype=torch.bfloat16, device=DEV)
+    zs = torch.empty(shp, dtype=torch.bfloat16, device=DEV)
+    arg = torch.empty(shp, dtype=torch.uint8, device=DEV)
+    K.conv2d_fwd_fused(xd, wd, bd, 2, zs, ad, p0, "pools", arg)
+    assert torch.equal(p1.cpu(), p0.cpu()), "pooled outputs differ"
+    dw1, da1, db1 = torch.zeros(8, 5, 5, 4, device=DEV), torch.zeros(H, W, 8, device=DEV), torch.zeros(8, device=DEV)
+    K.conv1_bwd_pm(xd, wd, bd, ad, dpd, dw1, da1, db1)
+    dw0, da0, db0 = torch.zeros(8, 5, 5, 4, device=DEV), torch.zeros(H, W, 8, device=DEV), torch.zeros(8, device=DEV)
+    dzs = torch.empty(shp, dtype=torch.bfloat16, device=DEV)
+    K.prelu_pool_bwd_sel(dpd, zs, arg, ad, dzs, da0, db0)
+    K.conv2d_wgrad_halo_sparse(xd, dzs, arg, 2, dw0, zeroed=True)
+    _close(dw1, dw0, 1e-3, 1e-4, "fused_dw")
+    _close(da1, da0, 1e-4, 1e-5, "fused_dalpha")
+    _close(db1, db0, 1e-3, 1e-4, "fused_dbias")
+
+
+def test_first_layer_fused_model_grads(monkeypatch):
+    """CNN first layer inside the model: conv1.hip path == sparse-record path (weights, bias, alpha
+    gradients of every layer), with raw uint8 images."""
+    from pyspark_tf_gke_amd.models import build_cnn_model
+    from pyspark_tf_gke_amd.nn import engine as E
+
+    torch.manual_seed(4)
+    x = torch.randint(0, 256, (4, 64, 80, 3), dtype=torch.uint8)
+    y = torch.rand(4, 2) * 50
+    grads = {}
+    for mode in (False, True):
+        monkeypatch.setattr(E, "CONV1_FUSED", mode)
+        m = build_cnn_model((64, 80, 3), flat=True, summary=False, device=DEV)
+        xb, yb = m._prep_batch(x, y)
+        m.store.zero_grad()
+        out = m._run_forward(xb, True)
+        d = m._loss_grad(out, yb, m._stats_buf())
+        m._run_backward(d)
+        torch.cuda.synchronize()
+        assert m.ops[0]._fused1 == mode
+        grads[mode] = {p.name: p.grad.detach().float().cpu().clone() for p in m.store.params}
+    for name, g in grads[False].items():
+        _close(grads[True][name], g, 1e-2, 1e-4, "fused1_grad_" + name)
 
 
 @pytest.mark.parametrize("N,H,W,C,Co,epi", [(16, 256, 320, 4, 8, "pools"), (32, 128, 160, 8, 16, "pool"),
