@@ -28,6 +28,7 @@ from ..ops import nn as K
 from . import engine as E
 from . import layers as L
 from . import streams as S
+from .. import config
 
 
 def _bf16(x, ws, key):
@@ -97,26 +98,62 @@ class GraphOp:
 # with 4-64 channels; measured on ResNet-50's 3x3/64-channel layers (56x56, batch 128) the
 # implicit-GEMM path is faster, so graph ops use the halo kernels for 5x5 only.
 HALO_KS = (5,)
-def conv_forward(x, w, bias, stride, pad, z):
+# BatchNormalization fusion (PTG_BN_FUSE, default on): every ConvBNOp's batch statistics come out of
+# its conv GEMM's epilogue (no bn_stats pass over z), and a Conv -> BN -> ReLU whose only consumer is
+# another ConvBNOp leaves its BN + ReLU to that consumer's operand loaders (forward A operand and
+# weight-gradient B operand read the stored z and apply relu(z*scale + shift) in registers), so its
+# apply pass and its y tensor disappear (gemm.hip BnLoad / EpiBf16 stats).
+BN_FUSE = config.get("bn_fuse")
+
+
+def _pow2(v):
+    return v > 0 and (v & (v - 1)) == 0
+
+
+def bn_input_ok(conv: L.Conv2D, pad: int) -> bool:
+    """A conv that can apply its producer's BN + ReLU in its loaders (implicit-GEMM / 1x1 GEMM path)."""
+    C, KH = conv.cin_p, conv.kernel_size[0]
+    same = pad == KH // 2 and conv.kernel_size[0] == conv.kernel_size[1] and conv.strides[0] == 1
+    halo = KH in HALO_KS and K.halo_eligible(C, conv.out_shape[-1], KH, conv.strides[0], same)
+    return C % 8 == 0 and _pow2(C) and not halo and conv.out_shape[-1] % 8 == 0
+
+
+def conv_forward(x, w, bias, stride, pad, z, in_bn=None, stats=None) -> bool:
+    """z = conv(x) (+ bias).  ``in_bn``: (scale, shift) of the producer's BN + ReLU to apply to x on
+    load; ``stats``: [64,2,Cout] partial sums for this op's BN, filled by the conv epilogue when it
+    can.  Returns True when ``stats`` were produced."""
     N, H, W, C = x.shape
     Co, KH, KW, _ = w.shape
+    if in_bn is not None or stats is not None:
+        same = pad == KH // 2 and KH == KW and stride == 1
+        halo = KH in HALO_KS and K.halo_eligible(C, Co, KH, stride, same)
+        if not halo and _pow2(C) and C >= 4 and (in_bn is None or C % 8 == 0) and Co % 8 == 0:
+            K.conv_bn_fwd(x, w, bias, stride, pad, z, in_bn, stats)
+            return stats is not None
+        if in_bn is not None:
+            raise RuntimeError("conv_forward: BN-on-load input for a conv outside the implicit-GEMM path")
     if not K.on_device(x):
-        return K.conv2d_fwd(x, w, bias, stride, pad, z, None)
+        K.conv2d_fwd(x, w, bias, stride, pad, z, None)
+        return False
     if KH == KW == 1 and stride == 1 and pad == 0:
         M = N * H * W
         K.gemm(M, Co, C, x, C, 1, w, C, 1, 0, z, Co, bias, 0, 1)
-        return z
+        return False
     same = pad == KH // 2 and KH == KW and stride == 1
     if KH in HALO_KS and K.halo_eligible(C, Co, KH, stride, same):
-        return K.conv2d_fwd_fused(x, w, bias, pad, z)
-    return K.conv2d_fwd(x, w, bias, stride, pad, z, None)
+        K.conv2d_fwd_fused(x, w, bias, pad, z)
+        return False
+    K.conv2d_fwd(x, w, bias, stride, pad, z, None)
+    return False
 
 
-def conv_wgrad(x, dz, stride, pad, dw):
-    """dw (fp32, already zeroed by the store) += d(conv)/dw."""
+def conv_wgrad(x, dz, stride, pad, dw, in_bn=None):
+    """dw (fp32, already zeroed by the store) += d(conv)/dw; ``in_bn`` as in :func:`conv_forward`."""
     N, H, W, C = x.shape
     _, OH, OW, Co = dz.shape
     _, KH, KW, _ = dw.shape
+    if in_bn is not None:
+        return K.conv_bn_wgrad(x, dz, stride, pad, dw, in_bn)
     if not K.on_device(x):
         return K.conv2d_wgrad(x, dz, stride, pad, dw, accumulate=True)
     if KH == KW == 1 and stride == 1 and pad == 0:
@@ -162,19 +199,23 @@ class _BNState:
                 ws.get(self.name + "/bn_mean", (C,), f, dev), ws.get(self.name + "/bn_rstd", (C,), f, dev),
                 ws.get(self.name + "/bn_coef", (3, C), f, dev))
 
-    def forward(self, z, res, relu, y, ws, training):
+    def forward(self, z, res, relu, y, ws, training, stats_done=False, apply=True):
+        """Statistics (unless the conv epilogue produced them), finalize, and - unless the consumer
+        applies it on load - the apply pass into y."""
         bn = self.bn
         C = z.shape[-1]
         M = z.numel() // C
         part, scale, shift, mean, rstd, _ = self.bufs(ws, C, z.device)
         g = bn.gamma.data if bn.gamma is not None else None
         b = bn.beta.data if bn.beta is not None else None
-        if training:
+        if training and not stats_done:
             KB.bn_stats(z, part)
         KB.bn_finalize(part, M, g, b, bn.epsilon, bn.momentum if training else -1.0, bn.moving_mean,
                        bn.moving_variance, scale, shift, mean, rstd, training)
         if not K.on_device(z) and training:
             part.zero_()
+        if not apply:
+            return z
         return KB.bn_apply(z, scale, shift, res, relu, y)
 
     def backward(self, dy, y, z, relu, dz, dres, ws):
@@ -206,6 +247,10 @@ class ConvBNOp:
         self.pad = conv.pad_amount() + extra_pad
         self.name = conv.name
         self.state = _BNState(bn, conv.name)
+        # set by the graph lowering (functional._fuse_bn_links): defer = our BN + ReLU is applied by
+        # our single consumer's loaders; in_bn_op = the producer whose BN + ReLU we apply on load
+        self.defer = False
+        self.in_bn_op = None
         if conv.activation not in ("linear", None):
             raise NotImplementedError("Conv2D(activation=...) followed by BatchNormalization")
 
@@ -220,8 +265,16 @@ class ConvBNOp:
         xi[..., : x.shape[-1]] = x
         return xi
 
+    def _in_bn(self, ws, dev):
+        """(scale, shift) of the producer's BN when its apply is folded into our loads."""
+        p = self.in_bn_op
+        if p is None:
+            return None
+        _, scale, shift, _, _, _ = p.state.bufs(ws, p.conv.out_shape[-1], dev)
+        return scale, shift
+
     def forward(self, xs, ws, training):
-        x = self._prep_input(xs[0], ws)
+        x = xs[0] if self.in_bn_op is not None else self._prep_input(xs[0], ws)
         res = xs[1] if self.residual else None
         if res is not None:
             res = _bf16(res, ws, self.name + "/res16")
@@ -230,10 +283,17 @@ class ConvBNOp:
         dev = x.device
         z = ws.get(self.name + "/z", (B, OH, OW, Co), torch.bfloat16, dev)
         b = self.conv.bias.data if self.conv.bias is not None else None
-        conv_forward(x, self.conv.kernel.bf16, b, self.stride, self.pad, z)
+        in_bn = self._in_bn(ws, dev)
+        part = self.state.bufs(ws, Co, dev)[0] if (training and BN_FUSE) else None
+        stats_done = conv_forward(x, self.conv.kernel.bf16, b, self.stride, self.pad, z, in_bn, part)
+        self._x, self._z, self._in_bn_t = x, z, in_bn
+        if self.defer:
+            self.state.forward(z, None, self.relu, None, ws, training, stats_done, apply=False)
+            self._y = None
+            return z  # the consumer applies relu(z*scale + shift) itself
         y = ws.get(self.name + "/y", z.shape, torch.bfloat16, dev)
-        self.state.forward(z, res, self.relu, y, ws, training)
-        self._x, self._z, self._y = x, z, y
+        self.state.forward(z, res, self.relu, y, ws, training, stats_done)
+        self._y = y
         return y
 
     def backward(self, dy, ws, existing):
@@ -244,7 +304,8 @@ class ConvBNOp:
         dres = ws.get(self.name + "/dres", z.shape, torch.bfloat16, dev) if self.residual else None
         self.state.backward(dy, y, z, self.relu, dz, dres, ws)
         g = self.conv.kernel.grad
-        S.launch(lambda: conv_wgrad(x, dz, self.stride, self.pad, g), dev)
+        in_bn = self._in_bn_t
+        S.launch(lambda: conv_wgrad(x, dz, self.stride, self.pad, g, in_bn), dev)
         dx = None
         if not self.first:
             ex = existing[0]
