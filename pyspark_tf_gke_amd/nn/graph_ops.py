@@ -98,12 +98,13 @@ class GraphOp:
 # with 4-64 channels; measured on ResNet-50's 3x3/64-channel layers (56x56, batch 128) the
 # implicit-GEMM path is faster, so graph ops use the halo kernels for 5x5 only.
 HALO_KS = (5,)
-# BatchNormalization fusion (PTG_BN_FUSE, default on): every ConvBNOp's batch statistics come out of
-# its conv GEMM's epilogue (no bn_stats pass over z), and a Conv -> BN -> ReLU whose only consumer is
+# BatchNormalization fusion: every ConvBNOp's batch statistics come out of its conv GEMM's epilogue
+# (PTG_BN_EPI_STATS; no bn_stats pass over z), and (PTG_BN_FUSE) a Conv -> BN -> ReLU whose only consumer is
 # another ConvBNOp leaves its BN + ReLU to that consumer's operand loaders (forward A operand and
 # weight-gradient B operand read the stored z and apply relu(z*scale + shift) in registers), so its
 # apply pass and its y tensor disappear (gemm.hip BnLoad / EpiBf16 stats).
 BN_FUSE = config.get("bn_fuse")
+BN_EPI_STATS = config.get("bn_epi_stats")
 
 
 def _pow2(v):
@@ -284,7 +285,7 @@ class ConvBNOp:
         z = ws.get(self.name + "/z", (B, OH, OW, Co), torch.bfloat16, dev)
         b = self.conv.bias.data if self.conv.bias is not None else None
         in_bn = self._in_bn(ws, dev)
-        part = self.state.bufs(ws, Co, dev)[0] if (training and BN_FUSE) else None
+        part = self.state.bufs(ws, Co, dev)[0] if (training and BN_EPI_STATS) else None
         stats_done = conv_forward(x, self.conv.kernel.bf16, b, self.stride, self.pad, z, in_bn, part)
         self._x, self._z, self._in_bn_t = x, z, in_bn
         if self.defer:

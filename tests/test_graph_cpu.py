@@ -77,6 +77,7 @@ def test_bn_fusion_defers_bottleneck_links(fp32_host, monkeypatch):
     grads = {}
     for fuse in (False, True):
         monkeypatch.setattr(G, "BN_FUSE", fuse)
+        monkeypatch.setattr(G, "BN_EPI_STATS", fuse)
         torch.manual_seed(1)
         m = ResNet((2, 1), input_shape=(32, 32, 3), classes=10, width=8, device="cpu")
         m.compile(optimizer=nn.optimizers.SGD(0.0), loss="sparse_categorical_crossentropy")

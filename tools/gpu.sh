@@ -11,6 +11,7 @@
 #   prof[:<wl>]      rocprofv3 --kernel-trace --stats over a short bench run -> gpurun_out/prof_<wl>
 #   pmc[:<wl>]       two PMC passes (MFMA/LDS/VALU/wait counters; FETCH_SIZE) -> gpurun_out/pmc_<wl>_{a,b}
 #   ab               A/B: bench.py twice plain, twice with AB_ENV set (interleaved)
+#   abm[:<wl>]       multi-way A/B: bench.py under each env set of ABM_ENVS ("X=1;Y=0"), plus defaults, x2
 #   abvar:<name>     A/B: bench.py with the default library vs PTG_HIP_LIB=libptg_hip_<name>.so (built here by
 #                    python -m pyspark_tf_gke_amd._native.build --variant <name> -D MACRO=..), interleaved x2
 #   py:<script>      timeout 300 python <script> (e.g. py:tools/gemm_bench.py)
@@ -69,6 +70,17 @@ for task in "$@"; do
         timeout -k 10 $STEP_T env $AB_ENV python bench.py --groupby-extra 0 --extra-batches "" --sim-world 0 $BENCH_ARGS \
           > gpurun_out/ab_b$i.json 2> gpurun_out/ab_b.err || fail ab_b gpurun_out/ab_b.err
         echo "B $(cut -c1-160 gpurun_out/ab_b$i.json)"
+      done ;;
+    abm)
+      # multi-way interleaved A/B: ABM_ENVS="A=1 B=2;C=0;" (';'-separated env sets, empty = defaults)
+      wl=${arg:-cnn_b1}
+      IFS=';' read -ra sets <<< "${ABM_ENVS:-}"
+      for i in 1 2; do
+        for e in "${sets[@]}" ""; do
+          timeout -k 10 $STEP_T env $e python bench.py --workload "$wl" --groupby-extra 0 --extra-batches "" --sim-world 0 \
+            $BENCH_ARGS > gpurun_out/abm.json 2> gpurun_out/abm.err || fail abm gpurun_out/abm.err
+          echo "[${e:-default}] $(cut -c1-150 gpurun_out/abm.json)"
+        done
       done ;;
     abvar)
       for i in 1 2; do
