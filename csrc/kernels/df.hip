@@ -832,7 +832,7 @@ __global__ __launch_bounds__(256) void part_agg2_k(const KT* __restrict__ okeys,
 // its aggregate table is a direct-indexed LDS array: no stored keys, no probing, no spill, and ONE
 // partitioning pass instead of the two hash levels above (the 1B-row / 1M-key groupBy: count +
 // scatter + aggregate, ~12 of its 21 ms were the second level).
-//   range_count_k    per-tile 256-bin digit counts, digit-major [digit][tile], and per-tile [min, max]
+//   range_count_k    per-tile 256-bin digit counts, tile-major [tile][digit], and per-tile [min, max]
 //                    (the host checks that every key fell inside the sample-guessed window)
 //   range_scatter_k  rows staged in LDS by digit, written as 256 contiguous runs; a key leaves as its
 //                    u16 index inside its partition's window ((key - lo) & (W - 1): the partition
@@ -883,7 +883,8 @@ __global__ __launch_bounds__(256) void range_count_k(const long long* __restrict
   for (int j = 0; j < RPT; ++j)
     if (tid + j * 256 < nr) atomicAdd(&h[w][range_digit(k[j], lo, sh)], 1u);
   __syncthreads();
-  hist[(long)tid * ntiles + b] = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
+  hist[(long)b * RGB + tid] = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
+  (void)ntiles;
   if (tid == 0) {
     long long a = rmn[0], c = rmx[0];
     for (int q = 1; q < 4; ++q) { a = rmn[q] < a ? rmn[q] : a; c = rmx[q] > c ? rmx[q] : c; }
@@ -911,7 +912,7 @@ __global__ __launch_bounds__(NT) void range_scatter_k(const long long* __restric
   const int nr = (int)min((long)RTT, n - s0);
   for (int d = tid; d < RGB; d += NT) {
     cnt[d] = 0;
-    goff[d] = offs[(long)d * ntiles + b];
+    goff[d] = offs[(long)b * RGB + d];  // tile-major offsets (ptg_digit_offsets)
   }
   __syncthreads();
   long long k[RPT];
@@ -964,7 +965,8 @@ __global__ __launch_bounds__(NT) void range_scatter_k(const long long* __restric
   }
 }
 
-// grid (chunks, 256): partition p = blockIdx.y holds rows [offs[p*ntiles], offs[(p+1)*ntiles]), keys
+// grid (chunks, 256): partition p = blockIdx.y holds rows [offs[p], offs[p+1]) (tile 0's row of the
+// tile-major offsets; offs[256*ntiles] = n closes the last partition), keys
 // lo + p*W + okeys[i] (u16 window indices).  Output per chunk c (Rw = 256*W entries):
 // prow[c][0][Rw] rows, prow[c][1+j][Rw] non-null count of column j, psum[c][j][Rw] sums and, with
 // MINMAX, pmm[c][2j][Rw] / pmm[c][2j+1][Rw] min / max (+-inf where a key has no non-null value).
@@ -990,7 +992,7 @@ __global__ __launch_bounds__(256) void range_agg_k(const unsigned short* __restr
     }
   }
   __syncthreads();
-  const long long a0 = offs[(long)p * ntiles], b0 = offs[(long)(p + 1) * ntiles], len = b0 - a0;
+  const long long a0 = offs[p], b0 = p + 1 < RGB ? offs[p + 1] : offs[(long)RGB * ntiles], len = b0 - a0;
   const long long a = a0 + len * c / C, b = a0 + len * (c + 1) / C;
   auto add = [&](unsigned int i, const double* v) {  // i: index inside the window
     atomicAdd(&lrow[i], 1u);
@@ -1105,8 +1107,9 @@ __global__ __launch_bounds__(256) void small_range_agg_k(const long long* __rest
 // Stable LSD radix sort of 64-bit keys with a 64-bit payload (DataFrame.orderBy / sort)
 //   sort_key_prep_k  column -> unsigned-orderable u64 (asc or desc; NaN above +inf, -0 == +0) and
 //                    the key range [min, max]: only the significant bits of (max - min) are sorted
-//   sort_count_k     per-tile 256-bin digit histograms, digit-major [digit][tile], so one
-//                    exclusive scan gives every (digit, tile) its output run in stable order
+//   sort_count_k     per-tile 256-bin digit histograms, tile-major [tile][digit] (one coalesced
+//                    1 KB row per tile); dfutil.hip ptg_digit_offsets turns them into every
+//                    (tile, digit)'s output run in stable (digit-major) order, also tile-major
 //   sort_scatter_k   stable in-tile ranking (8-ballot match per wave, per-round wave prefix over
 //                    LDS), rows staged in LDS by digit, written out as 256 contiguous runs
 //   range_partition_k  destination rank = #splitters below the key (sample-based range shuffle)
@@ -1186,7 +1189,8 @@ __global__ __launch_bounds__(256) void sort_count_k(const unsigned long long* __
   for (int j = 0; j < SRPT; ++j)
     if (s0 + j * 256 + tid < n) atomicAdd(&h[w][(unsigned)((k[j] - base) >> shift) & (SB - 1)], 1u);
   __syncthreads();
-  hist[(long)tid * ntiles + b] = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
+  hist[(long)b * SB + tid] = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
+  (void)ntiles;
 }
 
 // vals_in == nullptr: payload = row index (first pass of a fresh sort).  VT = unsigned int when the
@@ -1209,7 +1213,7 @@ __global__ __launch_bounds__(256) void sort_scatter_k(const unsigned long long* 
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, b = xcd_tile(blockIdx.x, ntiles);
   const long s0 = (long)b * ST;
   const int nr = (int)((n - s0) < ST ? (n - s0) : ST);
-  goff[tid] = offs[(long)tid * ntiles + b];
+  goff[tid] = offs[(long)b * SB + tid];  // tile-major: one coalesced 2 KB row
 #pragma unroll
   for (int q = 0; q < 4; ++q) wc[q][tid] = 0;
   // Wave-contiguous rows: wave w owns tile rows [w*ST/4, (w+1)*ST/4), 64 consecutive rows per round

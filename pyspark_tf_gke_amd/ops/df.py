@@ -464,7 +464,7 @@ def hash_agg_range(keys: torch.Tensor, pay: list, buf, nv: int, sample_lohi: tup
         if win is None:
             return None
     offs = buf("roffs", (256 * ntiles + 1,), torch.int64)
-    scan_excl(hist, out=offs[:-1], total=offs[-1:])
+    digit_offsets(hist, ntiles, offs, buf)
     okeys = buf("rokeys16", (max(n, 1),), torch.int16)[:n]  # u16 index inside the partition's window
     ovals = [buf(f"aov{j}", (max(n, 1),), torch.float64)[:n] for j in range(nv)]
     pin, pout = _pay_in(pay), _pay_out(ovals)
@@ -656,6 +656,23 @@ def decode_sort_key(sk: torch.Tensor, dtype, desc: bool) -> torch.Tensor:
     return x if dtype == torch.int64 else x.to(dtype)
 
 
+DIGIT_OFFS_TPC = 64  # tiles per column-scan chunk (ptg_digit_offsets)
+
+
+def digit_offsets(hist: torch.Tensor, ntiles: int, offs: torch.Tensor, buf) -> torch.Tensor:
+    """offs[t*256 + d] (int64, tile-major) = the stable output position of tile t's digit-d run, i.e.
+    the digit-major exclusive scan of the tile-major [ntiles][256] counts ``hist``; offs[256*ntiles]
+    = total.  ``buf(name, shape, dtype)`` supplies workspace."""
+    tpc = DIGIT_OFFS_TPC
+    nch = -(-ntiles // tpc)
+    csum = buf("do_csum", (256 * nch,), torch.int64)
+    cbase = buf("do_cbase", (256 * nch,), torch.int64)
+    hip("ptg_digit_offsets", 0, ptr(hist), ntiles, tpc, ptr(csum), nch, None)
+    scan_excl(csum, out=cbase, total=offs[256 * ntiles: 256 * ntiles + 1])
+    hip("ptg_digit_offsets", 1, ptr(hist), ntiles, tpc, ptr(cbase), nch, ptr(offs))
+    return offs
+
+
 def radix_sort_u64(keys: torch.Tensor, vals: torch.Tensor | None = None, lo: int = 0, hi: int = _U64,
                    row_payload: bool = False):
     """Stable sort of u64 keys (held in an int64 tensor) with an int64 payload (default: the row
@@ -675,7 +692,14 @@ def radix_sort_u64(keys: torch.Tensor, vals: torch.Tensor | None = None, lo: int
         return keys, (torch.arange(n, dtype=torch.int64, device=dev) if vals is None else vals)
     ntiles = -(-n // _native.hip_lib().ptg_sort_tile_rows())
     hist = torch.empty(256 * ntiles, dtype=torch.int32, device=dev)
-    offs = torch.empty(256 * ntiles, dtype=torch.int64, device=dev)
+    offs = torch.empty(256 * ntiles + 1, dtype=torch.int64, device=dev)
+    dws: dict = {}
+
+    def dbuf(name, shape, dtype):
+        t = dws.get(name)
+        if t is None:
+            t = dws[name] = torch.empty(int(np.prod(shape)), dtype=dtype, device=dev)
+        return t.view(shape)
     # row-index payloads travel as u32 when the rows fit 32 bits (12 instead of 16 B per row per pass)
     v32 = n <= (1 << 32) and (vals is None or row_payload)
     vdt = torch.int32 if v32 else torch.int64
@@ -688,7 +712,7 @@ def radix_sort_u64(keys: torch.Tensor, vals: torch.Tensor | None = None, lo: int
     for p in range(passes):
         shift = 8 * p
         hip("ptg_sort_count", ptr(ka), n, base, shift, ptr(hist))
-        scan_excl(hist, out=offs)
+        digit_offsets(hist, ntiles, offs, dbuf)
         hip("ptg_sort_scatter", ptr(ka), ptr(va), n, base, shift, ptr(offs), ptr(kb), ptr(vb), int(v32))
         if kc is None:  # third buffer pair so the caller's keys/vals are never overwritten
             kc = torch.empty(n, dtype=torch.int64, device=dev)

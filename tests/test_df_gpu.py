@@ -564,3 +564,28 @@ def test_groupby_sparse_keys_hash_path_vs_host(hip_built):
     assert torch.equal(uk.cpu()[order], hk[horder])
     assert torch.equal(rows.cpu()[order], hrows[horder])
     assert torch.allclose(outs[0][0].cpu()[order], houts[0][0][horder], rtol=1e-9, atol=1e-9)
+
+
+@pytest.mark.parametrize("ntiles", [1, 63, 64, 65, 1000, 5003])
+def test_digit_offsets_tile_major(ntiles):
+    """dfutil.hip ptg_digit_offsets: the digit-major exclusive scan of tile-major [ntiles][256] counts,
+    written tile-major, with the total after the last row."""
+    from pyspark_tf_gke_amd.ops import df as D
+
+    torch.manual_seed(ntiles)
+    hist = torch.randint(0, 5000, (ntiles, 256), dtype=torch.int32)
+    ref = torch.cumsum(hist.t().reshape(-1).long(), 0) - hist.t().reshape(-1).long()  # digit-major
+    ref = ref.view(256, ntiles).t().reshape(-1)
+    ws = {}
+
+    def buf(name, shape, dtype):
+        t = ws.get(name)
+        if t is None:
+            t = ws[name] = torch.empty(int(np.prod(shape)), dtype=dtype, device="cuda")
+        return t.view(shape)
+
+    offs = torch.full((256 * ntiles + 1,), -7, dtype=torch.int64, device="cuda")
+    D.digit_offsets(hist.reshape(-1).cuda(), ntiles, offs, buf)
+    out = offs.cpu()
+    assert torch.equal(out[:-1], ref)
+    assert int(out[-1]) == int(hist.long().sum())
