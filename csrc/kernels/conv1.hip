@@ -367,8 +367,336 @@ __global__ __launch_bounds__(256, 4) void conv1_bwd_pm_k(const void* __restrict_
   if (tid < COUT) atomicAdd(dbias + tid, sdb[0][tid] + sdb[1][tid] + sdb[2][tid] + sdb[3][tid]);
 }
 
+// ================================================================================================
+// Wave-independent variants (default): each of the block's 4 waves owns its 32x2-pixel quarter of
+// the tile (hf = columns, rp = row pair) with a PRIVATE LDS halo (6 rows x 36 pixels, double
+// buffered) and dZ tile, and walks the chunk's samples on its own - no block barrier inside the
+// sample loop.  The block-synchronised loop above stalled every sample on the slowest wave's
+// halo load (measured 474 us for the b256 backward, 114 us forward): with independent waves the
+// 16 waves of a CU keep their loads in flight while others compute.  Waves rp = 0 / 1 re-read 4 of
+// their 6 halo rows from L2.
+// ================================================================================================
+constexpr int WTW = 32, WHR = 2 + KS - 1;         // wave tile: 32 x 2 pixels, 6 halo rows
+constexpr int WHP = (2 * 15 + (KWP - 2) + 2) / 2;  // pixel pairs per halo row (36 pixels)
+constexpr int WROWE = WHP * 8;                     // wave halo row pitch (elements)
+constexpr int WHB = WHR * WROWE;                   // one wave halo buffer
+constexpr int WPIX = 2 * WTW;                      // dZ pixels per wave (K of its weight-gradient GEMM)
+constexpr int WDZ = WPIX * DPITCH;
+constexpr int WREG = 2 * WHB + WDZ;                // LDS elements per wave
+constexpr int WZS = 4 * WREG;                      // zero slot
+constexpr int WPF = (WHR * WHP + 63) / 64;         // halo pair slots per lane
+constexpr int WNB = (KF + 15) / 16;                // 16-column B fragments of the wave's dW
+static_assert(WREG % 8 == 0 && WHP == 18, "wave halo layout");
+
+PTG_DEV void wave_lds_sync() {  // this wave's LDS stores visible to its other lanes
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <bool U8>
+struct WaveHalo {
+  U4 pf[U8 ? 1 : WPF];
+  U8Pair pu[U8 ? WPF : 1];
+  PTG_DEV void load(const Rsrc& xr, int n, int H, int W, int ih0, int iw0, int lane) {
+#pragma unroll
+    for (int p = 0; p < WPF; ++p) {
+      const int idx = lane + p * 64, r = idx / WHP, c = idx - r * WHP;
+      const int ih = ih0 + r, iw = iw0 + 2 * c;
+      const bool ok = r < WHR && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+      if constexpr (U8) pu[p] = u8pair_load(xr, (uint32_t)((n * H + ih) * W + iw) * 3u, ok);
+      else pf[p] = bload16(xr, ok ? (uint32_t)(((n * H + ih) * W + iw) * C) * 2u : PTG_OOB);
+    }
+  }
+  PTG_DEV void store(bf16_t* buf, int lane) const {
+#pragma unroll
+    for (int p = 0; p < WPF; ++p) {
+      const int idx = lane + p * 64, r = idx / WHP, c = idx - r * WHP;
+      if (r < WHR) {
+        U4 v;
+        if constexpr (U8) v = u8pair_to_bf16x8(pu[p]);
+        else v = pf[p];
+        *(U4*)(buf + r * WROWE + c * 8) = v;
+      }
+    }
+  }
+};
+
+// z accumulators of the wave's 32 x 2 pixels from its halo `hb` (rows i + kh, columns 2*px + kw)
+PTG_DEV void conv_tile_w(const bf16_t* hb, const bf16_t* zs, const bf16x8_t* wreg, int px, int g, f32x4_t* acc) {
+  acc[0] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  acc[1] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < KSTEPS; ++ks) {
+    const int kf = ks * 32 + 8 * g;
+    const int kh = kf / KROW, kw = (kf - kh * KROW) / C;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const bf16_t* src = kf < KTOT ? hb + (i + kh) * WROWE + (2 * px + kw) * C : zs;
+      acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wreg[ks], *(const bf16x8_t*)src, acc[i], 0, 0, 0);
+    }
+  }
+}
+
+template <bool U8>
+__global__ __launch_bounds__(256) void conv1_fwd_wv_k(const void* __restrict__ x, const bf16_t* __restrict__ w,
+                                                      const float* __restrict__ bias, const float* __restrict__ alpha,
+                                                      bf16_t* __restrict__ pooled, int N, int H, int W, int tiles_h,
+                                                      int tiles_w, int nchunks) {
+  __shared__ __attribute__((aligned(16))) bf16_t smem[WZS + 8];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int px = lane & 15, g = lane >> 4, hf = wid & 1, rp = wid >> 1;
+  if (tid < 8) smem[WZS + tid] = 0;
+  __syncthreads();  // zero slot visible (the only block barrier)
+  const Item it = work_item(N, tiles_h, tiles_w, nchunks);
+  if (it.n0 >= it.n1) return;
+  bf16_t* const wr = smem + wid * WREG;
+  bf16x8_t wreg[KSTEPS];
+  load_wreg(w, px, g, wreg);
+  const int cc = 4 * (g & 1), dwo = g >> 1;
+  float b8[COUT];
+#pragma unroll
+  for (int c = 0; c < COUT; ++c) b8[c] = bias ? __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(bias[c]))) : 0.f;
+  const int ow = it.ow0 + hf * WTW + 2 * px + dwo;
+  float al[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int oh = it.oh0 + 2 * rp + i;
+    const float4 a = (oh < H && ow < W) ? *(const float4*)(alpha + ((long)oh * W + ow) * COUT + cc)
+                                        : make_float4(0.f, 0.f, 0.f, 0.f);
+    al[i][0] = a.x; al[i][1] = a.y; al[i][2] = a.z; al[i][3] = a.w;
+  }
+  const int PH = H >> 1, PW = W >> 1;
+  const int ph = (it.oh0 >> 1) + rp, pw = (it.ow0 >> 1) + hf * 16 + px;
+  const bool store_lane = g < 2 && ph < PH && pw < PW;
+  const int ih0 = it.oh0 + 2 * rp - PAD, iw0 = it.ow0 + hf * WTW - PAD;
+  const Rsrc xr = x_rsrc<U8>(x, N, H, W);
+  WaveHalo<U8> hl;
+  hl.load(xr, it.n0, H, W, ih0, iw0, lane);
+  hl.store(wr, lane);
+  wave_lds_sync();
+  for (int n = it.n0; n < it.n1; ++n) {
+    const int b = (n - it.n0) & 1;
+    const bool has_next = n + 1 < it.n1;
+    if (has_next) hl.load(xr, n + 1, H, W, ih0, iw0, lane);
+    f32x4_t acc[2];
+    conv_tile_w(wr + b * WHB, smem + WZS, wreg, px, g, acc);
+    float pm[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float y[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const float zr = bf2f(f2bf(acc[i][r] + ((g & 1) ? b8[4 + r] : b8[r])));
+        y[i] = zr > 0.f ? zr : al[i][r] * zr;
+      }
+      const float v = fmaxf(y[0], y[1]);
+      pm[r] = fmaxf(v, __shfl_xor(v, 32, 64));
+    }
+    if (store_lane)
+      *(U2*)(pooled + (((long)n * PH + ph) * PW + pw) * COUT + cc) = U2{pack_bf(pm[0], pm[1]), pack_bf(pm[2], pm[3])};
+    if (has_next) {
+      hl.store(wr + (b ^ 1) * WHB, lane);
+      wave_lds_sync();
+    }
+  }
+}
+
+template <bool U8>
+__global__ __launch_bounds__(256, 4) void conv1_bwd_wv_k(const void* __restrict__ x, const bf16_t* __restrict__ w,
+                                                         const float* __restrict__ bias, const float* __restrict__ alpha,
+                                                         const bf16_t* __restrict__ dp, float* __restrict__ dw,
+                                                         float* __restrict__ dalpha, float* __restrict__ dbias, int N,
+                                                         int H, int W, int tiles_h, int tiles_w, int nchunks) {
+  __shared__ __attribute__((aligned(16))) bf16_t smem[WZS + 8];
+  __shared__ float sdb[4][COUT];
+  __shared__ float4 sda[4][2][64];  // dalpha partial sums: [wave][pixel row i][lane]
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int px = lane & 15, g = lane >> 4, hf = wid & 1, rp = wid >> 1;
+  if (tid < 8) smem[WZS + tid] = 0;
+  bf16_t* const wr = smem + wid * WREG;
+  bf16_t* const ds = wr + 2 * WHB;
+  for (int i = lane; i < WDZ / 8; i += 64) *(U4*)(ds + 8 * i) = zero4();  // MFMA rows 8-15 read 0
+  __syncthreads();
+  const Item it = work_item(N, tiles_h, tiles_w, nchunks);
+  if (it.n0 >= it.n1) return;
+  bf16x8_t wreg[KSTEPS];
+  load_wreg(w, px, g, wreg);
+  const int cc = 4 * (g & 1), dwo = g >> 1;
+  float b8[COUT];
+#pragma unroll
+  for (int c = 0; c < COUT; ++c) b8[c] = bias ? __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(bias[c]))) : 0.f;
+  const int ow = it.ow0 + hf * WTW + 2 * px + dwo;
+  float db[4] = {0.f, 0.f, 0.f, 0.f};
+  // dalpha partial sums live in LDS (lane-private slots), not in 8 registers across the loop
+  sda[wid][0][lane] = sda[wid][1][lane] = make_float4(0.f, 0.f, 0.f, 0.f);
+  // alpha of this lane's 2 x 4 (pixel, channel) elements: re-read per sample (an L1 / L2 hit)
+  // rather than held in 8 registers across the loop
+  const bool ain0 = it.oh0 + 2 * rp < H && ow < W, ain1 = it.oh0 + 2 * rp + 1 < H && ow < W;
+  const long aoff = ((long)(it.oh0 + 2 * rp) * W + ow) * COUT + cc;
+  const int PH = H >> 1, PW = W >> 1;
+  const int ph = (it.oh0 >> 1) + rp, pw = (it.ow0 >> 1) + hf * 16 + px;
+  const bool pin = ph < PH && pw < PW;
+  const int ih0 = it.oh0 + 2 * rp - PAD, iw0 = it.ow0 + hf * WTW - PAD;
+  const Rsrc xr = x_rsrc<U8>(x, N, H, W);
+  const Rsrc dr = make_rsrc(dp, (uint32_t)((long)N * PH * PW * COUT * 2));
+  auto dp_off = [&](int n) { return pin ? (uint32_t)((((n * PH + ph) * PW + pw) * COUT + cc) * 2) : PTG_OOB; };
+  f32x4_t wacc[WNB];
+#pragma unroll
+  for (int j = 0; j < WNB; ++j) wacc[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int li = lane & 15;
+
+  WaveHalo<U8> hl;
+  hl.load(xr, it.n0, H, W, ih0, iw0, lane);
+  U2 dpr = bload8(dr, dp_off(it.n0));
+  hl.store(wr, lane);
+  wave_lds_sync();
+  for (int n = it.n0; n < it.n1; ++n) {
+    const int b = (n - it.n0) & 1;
+    const bf16_t* hb = wr + b * WHB;
+    const bool has_next = n + 1 < it.n1;
+    const U2 dcur = dpr;
+    if (has_next) {
+      hl.load(xr, n + 1, H, W, ih0, iw0, lane);
+      dpr = bload8(dr, dp_off(n + 1));
+    }
+    // lane-derived offsets from an opaque lane id (hoisted out of the loop they would spill)
+    int ol = lane;
+    asm volatile("" : "+v"(ol));
+    const int opx = ol & 15, og = ol >> 4, oq = (ol & 15) >> 2, op = ol & 3;
+    f32x4_t acc[2];
+    conv_tile_w(hb, smem + WZS, wreg, opx, og, acc);
+    const float gv[4] = {lo_bf(dcur.x), hi_bf(dcur.x), lo_bf(dcur.y), hi_bf(dcur.y)};
+    float al[2][4];
+    {
+      const long ao = aoff + (ol - lane);  // == aoff: keeps the loads inside the loop
+      const float4 a0 = ain0 ? *(const float4*)(alpha + ao) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 a1 = ain1 ? *(const float4*)(alpha + ao + (long)W * COUT) : make_float4(0.f, 0.f, 0.f, 0.f);
+      al[0][0] = a0.x; al[0][1] = a0.y; al[0][2] = a0.z; al[0][3] = a0.w;
+      al[1][0] = a1.x; al[1][1] = a1.y; al[1][2] = a1.z; al[1][3] = a1.w;
+    }
+    float dz[2][4], da[2][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float zr[2], y[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        zr[i] = bf2f(f2bf(acc[i][r] + ((og & 1) ? b8[4 + r] : b8[r])));
+        y[i] = zr[i] > 0.f ? zr[i] : al[i][r] * zr[i];
+      }
+      const float p0 = __shfl_xor(y[0], 32, 64), p1 = __shfl_xor(y[1], 32, 64);
+      const float yq[4] = {dwo ? p0 : y[0], dwo ? y[0] : p0, dwo ? p1 : y[1], dwo ? y[1] : p1};
+      float best = yq[0];
+      int a = 0;
+#pragma unroll
+      for (int qq = 1; qq < 4; ++qq)
+        if (yq[qq] > best) { best = yq[qq]; a = qq; }  // first maximum wins (as the forward)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const bool hit = a == 2 * i + dwo;
+        const bool pos = zr[i] > 0.f;
+        const float gq = hit ? gv[r] : 0.f;
+        dz[i][r] = pos ? gq : gq * al[i][r];
+        da[i][r] = pos ? 0.f : gq * zr[i];
+        db[r] += dz[i][r];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      float4 t = sda[wid][i][lane];
+      t.x += da[i][0]; t.y += da[i][1]; t.z += da[i][2]; t.w += da[i][3];
+      sda[wid][i][lane] = t;
+    }
+    const int m_lane = 2 * opx + (og >> 1);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      *(U2*)(ds + (m_lane + i * WTW) * DPITCH + 4 * (og & 1)) =
+          U2{pack_bf(dz[i][0], dz[i][1]), pack_bf(dz[i][2], dz[i][3])};
+    wave_lds_sync();
+    // dW[co][kf] += sum over the wave's 64 pixels of dZ[pix][co] * x[pix + (kh, kw)][ci]
+#pragma unroll 1
+    for (int k0 = 0; k0 < WPIX; k0 += 32) {
+      const int m0 = k0 + 8 * og + oq, m1 = m0 + 4;
+      const s16x4_t alo = tr_read(ds + m0 * DPITCH + 4 * op);
+      const s16x4_t ahi = tr_read(ds + m1 * DPITCH + 4 * op);
+      U2 ua = __builtin_bit_cast(U2, alo), ub = __builtin_bit_cast(U2, ahi);
+      const bf16x8_t af = __builtin_bit_cast(bf16x8_t, U4{ua.x, ua.y, ub.x, ub.y});
+      const int h0 = (m0 / WTW) * WROWE + (m0 % WTW) * C, h1 = (m1 / WTW) * WROWE + (m1 % WTW) * C;
+#pragma unroll
+      for (int j = 0; j < WNB; ++j) {
+        const int kf = j * 16 + 4 * op;
+        const int kh = kf / (KS * C), kw = (kf - kh * KS * C) / C;
+        const bool ok = kf < KF;
+        const bf16_t* s0 = ok ? hb + h0 + kh * WROWE + kw * C : smem + WZS;
+        const bf16_t* s1 = ok ? hb + h1 + kh * WROWE + kw * C : smem + WZS;
+        const s16x4_t blo = tr_read(s0), bhi = tr_read(s1);
+        ua = __builtin_bit_cast(U2, blo);
+        ub = __builtin_bit_cast(U2, bhi);
+        wacc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, __builtin_bit_cast(bf16x8_t, U4{ua.x, ua.y, ub.x, ub.y}),
+                                                          wacc[j], 0, 0, 0);
+      }
+    }
+    if (has_next) hl.store(wr + (b ^ 1) * WHB, lane);
+    wave_lds_sync();  // next halo visible; this dZ tile read before it is rewritten
+  }
+  // dalpha: every (pixel, channel) of the tile belongs to exactly one lane
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int oh = it.oh0 + 2 * rp + i;
+    const float4 t = sda[wid][i][lane];
+    const float dv[4] = {t.x, t.y, t.z, t.w};
+    if (oh < H && ow < W) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (dv[r] != 0.f) atomicAdd(dalpha + ((long)oh * W + ow) * COUT + cc + r, dv[r]);
+    }
+  }
+  // dbias: lanes sharing a channel group, then the waves
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float v = db[r];
+    v += __shfl_xor(v, 1, 64);
+    v += __shfl_xor(v, 2, 64);
+    v += __shfl_xor(v, 4, 64);
+    v += __shfl_xor(v, 8, 64);
+    v += __shfl_xor(v, 32, 64);
+    db[r] = v;
+  }
+  if (px == 0 && g < 2) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sdb[wid][cc + r] = db[r];
+  }
+  // dW: the 4 waves' partial tiles summed in LDS (the halo area is free now), one atomic per output
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(smem);  // [4][COUT * KF] floats = 12.8 KB < the wave regions
+  if (g < 2) {
+#pragma unroll
+    for (int j = 0; j < WNB; ++j) {
+      const int kf = j * 16 + li;
+      if (kf < KF) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[wid * COUT * KF + (g * 4 + r) * KF + kf] = wacc[j][r];
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < COUT * KF; i += 256)
+    atomicAdd(dw + i, red[i] + red[COUT * KF + i] + red[2 * COUT * KF + i] + red[3 * COUT * KF + i]);
+  if (tid < COUT) atomicAdd(dbias + tid, sdb[0][tid] + sdb[1][tid] + sdb[2][tid] + sdb[3][tid]);
+}
+static_assert(4 * COUT * KF * 4 <= WZS * 2, "dW reduction scratch fits the wave regions");
+
 // sample chunks per tile position: as many work items as fit the device at once (one wave of
 // workgroups, no tail), or PTG_CONV1_*_PER_CU workgroups per CU when set
+// PTG_CONV1_WAVE=0: the block-synchronised sample loop (A/B)
+static bool conv1_wave() {
+  static const bool on = [] {
+    const char* e = getenv("PTG_CONV1_WAVE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 static int conv1_chunks(int N, long npos, const void* kern, const char* env) {
   long slots = ptg_resident_blocks(kern);
   if (const char* e = getenv(env)) {
@@ -400,7 +728,8 @@ int ptg_conv1_fwd_pm(const void* x, int u8, const void* w, const float* bias, co
       !ptg_fits_2g((long)N * H * W * 4))
     return (int)hipErrorInvalidValue;
   const int th = (H + TH - 1) / TH, tw = (W + TW - 1) / TW;
-  const auto kern = u8 ? conv1_fwd_pm_k<true> : conv1_fwd_pm_k<false>;
+  const auto kern = conv1_wave() ? (u8 ? conv1_fwd_wv_k<true> : conv1_fwd_wv_k<false>)
+                                  : (u8 ? conv1_fwd_pm_k<true> : conv1_fwd_pm_k<false>);
   const int nch = conv1_chunks(N, (long)th * tw, (const void*)kern, "PTG_CONV1_FWD_PER_CU");
   const long items = (long)th * tw * nch;
   if (items > 0x7fffffff) return (int)hipErrorInvalidValue;
@@ -417,7 +746,8 @@ int ptg_conv1_bwd_pm(const void* x, int u8, const void* w, const float* bias, co
       !ptg_fits_2g((long)N * H * W * 4))
     return (int)hipErrorInvalidValue;
   const int th = (H + TH - 1) / TH, tw = (W + TW - 1) / TW;
-  const auto kern = u8 ? conv1_bwd_pm_k<true> : conv1_bwd_pm_k<false>;
+  const auto kern = conv1_wave() ? (u8 ? conv1_bwd_wv_k<true> : conv1_bwd_wv_k<false>)
+                                  : (u8 ? conv1_bwd_pm_k<true> : conv1_bwd_pm_k<false>);
   const int nch = conv1_chunks(N, (long)th * tw, (const void*)kern, "PTG_CONV1_BWD_PER_CU");
   const long items = (long)th * tw * nch;
   if (items > 0x7fffffff) return (int)hipErrorInvalidValue;

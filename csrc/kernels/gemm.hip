@@ -432,27 +432,42 @@ PTG_DEV void stats_acc8(const float* v, int cnt, float* s, float* q) {
     q[j] = fmaf(r, r, q[j]);
   }
 }
-// Block reduction of the per-thread sums into the tile's TN columns (LDS float atomics: thread tid
-// always owns column group tid % (TN/8) in the epilogue loops), then 2 * TN global atomics into
-// partial group tm % EPI_BN_G.  `scratch` (>= 2*TN floats) is the epilogue's LDS staging area.
+// Block reduction of the per-thread sums into the tile's TN columns: thread tid always owns column
+// group tid % (TN/8) in the epilogue loops, so the lanes of a wave that share a group are reduced
+// with xor shuffles, each wave writes its TN partial sums to LDS (no LDS atomics: 16-way contended
+// ds_add_f32 made this flush cost more than the bn_stats pass it replaces), and TN threads add the
+// waves' rows into partial group tm % EPI_BN_G with 2 * TN global atomics.  `scratch` (>= 2 * TN *
+// NT/64 floats) is the epilogue's LDS staging area.
 template <int TN, int NT>
-PTG_DEV void stats_flush(float* stats, int N, int tm, int n0, const float* s, const float* q, float* scratch) {
-  __syncthreads();  // every thread is done reading the staged C tile
-  const int tid = threadIdx.x;
-  for (int i = tid; i < 2 * TN; i += NT) scratch[i] = 0.f;
-  __syncthreads();
-  const int c8 = tid % (TN / 8);
+PTG_DEV void stats_flush(float* stats, int N, int tm, int n0, float* s, float* q, float* scratch) {
+  constexpr int G = TN / 8, NW = NT / 64;
+  static_assert(G <= 64, "column groups per wave");
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    atomicAdd(scratch + c8 * 8 + j, s[j]);
-    atomicAdd(scratch + TN + c8 * 8 + j, q[j]);
+  for (int o = G; o < 64; o <<= 1) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      s[j] += __shfl_xor(s[j], o, 64);
+      q[j] += __shfl_xor(q[j], o, 64);
+    }
+  }
+  __syncthreads();  // every thread is done reading the staged C tile
+  if (lane < G) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      scratch[(w * 2) * TN + lane * 8 + j] = s[j];
+      scratch[(w * 2 + 1) * TN + lane * 8 + j] = q[j];
+    }
   }
   __syncthreads();
   float* g = stats + (long)(tm % EPI_BN_G) * 2 * N;
   for (int i = tid; i < TN; i += NT) {
     if (n0 + i < N) {
-      atomicAdd(g + n0 + i, scratch[i]);
-      atomicAdd(g + N + n0 + i, scratch[TN + i]);
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < NW; ++ww) { a += scratch[(ww * 2) * TN + i]; b += scratch[(ww * 2 + 1) * TN + i]; }
+      atomicAdd(g + n0 + i, a);
+      atomicAdd(g + N + n0 + i, b);
     }
   }
 }
