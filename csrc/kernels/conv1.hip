@@ -223,10 +223,11 @@ __global__ __launch_bounds__(256, 4) void conv1_bwd_pm_k(const void* __restrict_
   bf16x8_t wreg[KSTEPS];
   load_wreg(w, px, g, wreg);
   const int cc = 4 * (g & 1), dwo = g >> 1;
-  // the 8 biases stay wave-uniform (scalar registers); each lane selects its 4 per sample
-  float b8[COUT];
-#pragma unroll
-  for (int c = 0; c < COUT; ++c) b8[c] = bias ? __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(bias[c]))) : 0.f;
+  // the 8 biases in LDS, read per sample (a register array indexed by a lane-dependent select
+  // is lowered to scratch memory)
+  __shared__ float4 sbias[2];
+  if (tid < 2) sbias[tid] = bias ? *(const float4*)(bias + 4 * tid) : make_float4(0.f, 0.f, 0.f, 0.f);
+  __syncthreads();
   const int ow = it.ow0 + hf * 32 + 2 * px + dwo;
   float al[2][4], da[2][4], db[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -273,13 +274,15 @@ __global__ __launch_bounds__(256, 4) void conv1_bwd_pm_k(const void* __restrict_
     f32x4_t acc[2];
     conv_tile(hb, smem, wreg, rp, hf, opx, og, acc);
     const float gv[4] = {lo_bf(dcur.x), hi_bf(dcur.x), lo_bf(dcur.y), hi_bf(dcur.y)};
+    const float4 bq = sbias[og & 1];
+    const float bsel[4] = {bq.x, bq.y, bq.z, bq.w};
     float dz[2][4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       float zr[2], y[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        zr[i] = bf2f(f2bf(acc[i][r] + ((og & 1) ? b8[4 + r] : b8[r])));
+        zr[i] = bf2f(f2bf(acc[i][r] + bsel[r]));
         y[i] = zr[i] > 0.f ? zr[i] : al[i][r] * zr[i];
       }
       // window (dh, dw) in q = 2*dh + dw order; this lane holds dw = dwo, the partner lane ^ 32 the other
@@ -454,9 +457,8 @@ __global__ __launch_bounds__(256) void conv1_fwd_wv_k(const void* __restrict__ x
   bf16x8_t wreg[KSTEPS];
   load_wreg(w, px, g, wreg);
   const int cc = 4 * (g & 1), dwo = g >> 1;
-  float b8[COUT];
-#pragma unroll
-  for (int c = 0; c < COUT; ++c) b8[c] = bias ? __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(bias[c]))) : 0.f;
+  float bv[4] = {0.f, 0.f, 0.f, 0.f};
+  if (bias) { const float4 b4 = *(const float4*)(bias + cc); bv[0] = b4.x; bv[1] = b4.y; bv[2] = b4.z; bv[3] = b4.w; }
   const int ow = it.ow0 + hf * WTW + 2 * px + dwo;
   float al[2][4];
 #pragma unroll
@@ -487,7 +489,7 @@ __global__ __launch_bounds__(256) void conv1_fwd_wv_k(const void* __restrict__ x
       float y[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const float zr = bf2f(f2bf(acc[i][r] + ((g & 1) ? b8[4 + r] : b8[r])));
+        const float zr = bf2f(f2bf(acc[i][r] + bv[r]));
         y[i] = zr > 0.f ? zr : al[i][r] * zr;
       }
       const float v = fmaxf(y[0], y[1]);
@@ -523,9 +525,11 @@ __global__ __launch_bounds__(256, 4) void conv1_bwd_wv_k(const void* __restrict_
   bf16x8_t wreg[KSTEPS];
   load_wreg(w, px, g, wreg);
   const int cc = 4 * (g & 1), dwo = g >> 1;
-  float b8[COUT];
-#pragma unroll
-  for (int c = 0; c < COUT; ++c) b8[c] = bias ? __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(bias[c]))) : 0.f;
+  // the 8 biases in LDS, read per sample (a register array indexed by a lane-dependent select
+  // is lowered to scratch memory)
+  __shared__ float4 sbias[2];
+  if (tid < 2) sbias[tid] = bias ? *(const float4*)(bias + 4 * tid) : make_float4(0.f, 0.f, 0.f, 0.f);
+  __syncthreads();
   const int ow = it.ow0 + hf * WTW + 2 * px + dwo;
   float db[4] = {0.f, 0.f, 0.f, 0.f};
   // dalpha partial sums live in LDS (lane-private slots), not in 8 registers across the loop
@@ -567,6 +571,8 @@ __global__ __launch_bounds__(256, 4) void conv1_bwd_wv_k(const void* __restrict_
     f32x4_t acc[2];
     conv_tile_w(hb, smem + WZS, wreg, opx, og, acc);
     const float gv[4] = {lo_bf(dcur.x), hi_bf(dcur.x), lo_bf(dcur.y), hi_bf(dcur.y)};
+    const float4 bq = sbias[og & 1];
+    const float bsel[4] = {bq.x, bq.y, bq.z, bq.w};
     float al[2][4];
     {
       const long ao = aoff + (ol - lane);  // == aoff: keeps the loads inside the loop
@@ -581,7 +587,7 @@ __global__ __launch_bounds__(256, 4) void conv1_bwd_wv_k(const void* __restrict_
       float zr[2], y[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        zr[i] = bf2f(f2bf(acc[i][r] + ((og & 1) ? b8[4 + r] : b8[r])));
+        zr[i] = bf2f(f2bf(acc[i][r] + bsel[r]));
         y[i] = zr[i] > 0.f ? zr[i] : al[i][r] * zr[i];
       }
       const float p0 = __shfl_xor(y[0], 32, 64), p1 = __shfl_xor(y[1], 32, 64);
