@@ -83,6 +83,15 @@ PTG_DEV void bias_reduce_atomic(float db[8], int c8, int C8, float* sred, float*
 // touches those elements); small layers split the batch over a few chunks and add with atomics.
 // (the rejected per-block variant added every block's dalpha partial with fp32 atomics: ~17M per
 // layer at batch 256.)
+// dword w of a 2- or 4-dword vector (w a compile-time constant after unrolling): keeps the vectors
+// in registers - indexing them through a uint32_t* put them in scratch memory
+PTG_DEV uint32_t vword(const U2& v, int w) { return w == 0 ? v.x : v.y; }
+PTG_DEV uint32_t vword(const U4& v, int w) { return w == 0 ? v.x : w == 1 ? v.y : w == 2 ? v.z : v.w; }
+PTG_DEV void vset(U2& v, int w, uint32_t x) { if (w == 0) v.x = x; else v.y = x; }
+PTG_DEV void vset(U4& v, int w, uint32_t x) {
+  if (w == 0) v.x = x; else if (w == 1) v.y = x; else if (w == 2) v.z = x; else v.w = x;
+}
+
 template <int CH>
 __global__ __launch_bounds__(256, 4) void prelu_pool_bwd_sg_k(const bf16_t* __restrict__ dp,
                                                            const bf16_t* __restrict__ z,
@@ -105,9 +114,10 @@ __global__ __launch_bounds__(256, 4) void prelu_pool_bwd_sg_k(const bf16_t* __re
   const int cg = active ? i % CG : 0;
   const int t = active ? i / CG : 0;
   const int pw = t % PW, ph = t / PW;
-  uint32_t zoff[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) zoff[q] = (uint32_t)(((2 * ph + (q >> 1)) * W + 2 * pw + (q & 1)) * C + cg * CH);
+  // window position q = 2*dh + dw sits at zbase + dh*W*C + dw*C (the row/column steps are uniform,
+  // so only zbase lives in a vector register)
+  const uint32_t zbase = (uint32_t)((2 * ph * W + 2 * pw) * C + cg * CH), rowC = (uint32_t)(W * C);
+  auto zoff = [&](int q) { return zbase + (uint32_t)(q >> 1) * rowC + (uint32_t)(q & 1) * (uint32_t)C; };
   const uint32_t HWC = (uint32_t)(H * W * C), PHWC = (uint32_t)(PH * PW * C);
   const uint32_t poff = (uint32_t)((ph * PW + pw) * C + cg * CH);
   float da[4][CH], db[CH];
@@ -127,7 +137,7 @@ __global__ __launch_bounds__(256, 4) void prelu_pool_bwd_sg_k(const bf16_t* __re
     for (int q = 0; q < 4; ++q)
 #pragma unroll
       for (int j = 0; j < CH; j += 4) {
-        const float4 a4 = *(const float4*)(alpha + zoff[q] + j);
+        const float4 a4 = *(const float4*)(alpha + zoff(q) + j);
         av[q][j] = a4.x; av[q][j + 1] = a4.y; av[q][j + 2] = a4.z; av[q][j + 3] = a4.w;
       }
     const bool lastw = (W & 1) && pw == PW - 1, lasth = (H & 1) && ph == PH - 1;
@@ -137,25 +147,25 @@ __global__ __launch_bounds__(256, 4) void prelu_pool_bwd_sg_k(const bf16_t* __re
     auto ld = [&](int nn, V& gq, V* zq) {
       gq = bload(dpr, ((uint32_t)nn * PHWC + poff) * 2u);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) zq[q] = bload(zr, ((uint32_t)nn * HWC + zoff[q]) * 2u);
+      for (int q = 0; q < 4; ++q) zq[q] = bload(zr, ((uint32_t)nn * HWC + zoff(q)) * 2u);
     };
     if (n0 + sg < n1) ld(n0 + sg, gc, zc);
     for (int n = n0 + sg; n < n1; n += SG) {
       V gn, zn[4];
       ld(min(n + SG, n1 - 1), gn, zn);
-      const uint32_t* gw = (const uint32_t*)&gc;
       uint32_t ow[4][CH / 2];
 #pragma unroll
       for (int w = 0; w < CH / 2; ++w) {
         float ov[2][4];
+        const uint32_t gww = vword(gc, w);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const int jj = 2 * w + h;
-          const float gj = h ? hi_bf(gw[w]) : lo_bf(gw[w]);
+          const float gj = h ? hi_bf(gww) : lo_bf(gww);
           float zq[4], yq[4];
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            const uint32_t word = ((const uint32_t*)&zc[q])[w];
+            const uint32_t word = vword(zc[q], w);
             zq[q] = h ? hi_bf(word) : lo_bf(word);
             yq[q] = zq[q] > 0.f ? zq[q] : av[q][jj] * zq[q];
           }
@@ -181,8 +191,8 @@ __global__ __launch_bounds__(256, 4) void prelu_pool_bwd_sg_k(const bf16_t* __re
       for (int q = 0; q < 4; ++q) {
         V o;
 #pragma unroll
-        for (int w = 0; w < CH / 2; ++w) ((uint32_t*)&o)[w] = ow[q][w];
-        *(V*)(dz + nb + zoff[q]) = o;
+        for (int w = 0; w < CH / 2; ++w) vset(o, w, ow[q][w]);
+        *(V*)(dz + nb + zoff(q)) = o;
       }
       gc = gn;
 #pragma unroll
@@ -190,7 +200,7 @@ __global__ __launch_bounds__(256, 4) void prelu_pool_bwd_sg_k(const bf16_t* __re
       if (lastw || lasth) {  // odd H / W: the row / column outside every window gets zero gradient
         V zz;
 #pragma unroll
-        for (int w = 0; w < CH / 2; ++w) ((uint32_t*)&zz)[w] = 0u;
+        for (int w = 0; w < CH / 2; ++w) vset(zz, w, 0u);
         bf16_t* d = dz + nb + cg * CH;
         if (lastw) {
           *(V*)(d + ((long)(2 * ph) * W + W - 1) * C) = zz;
