@@ -692,6 +692,308 @@ __global__ __launch_bounds__(256, 4) void conv1_bwd_wv_k(const void* __restrict_
 }
 static_assert(4 * COUT * KF * 4 <= WZS * 2, "dW reduction scratch fits the wave regions");
 
+// ================================================================================================
+// Record pipeline (default): the forward keeps, per pooled element, z at the window's argmax (bf16)
+// and the argmax q = 2*dh + dw (uint8) - 3 bytes next to the pooled output's 2 - and the backward
+// turns (dp, zsel, q) into dZ directly: no conv recompute, and the PReLU/pool backward math runs
+// once per POOLED element instead of once per pixel with an argmax search.  The recomputing backward
+// above was VALU-bound (PMC: ~73% of VALU issue, 20 VALU instructions per MFMA).
+// u8 images enter the MFMA as exact bf16 integers 0..255 (v_cvt_f32_ubyteN + the float's top half),
+// the 1/255 is applied to the fp32 accumulators (forward) and to the weight gradient (backward).
+// ================================================================================================
+PTG_DEV U4 u8pair_to_bf16x8_int(const U8Pair& p) {
+  const unsigned long long v = (((unsigned long long)p.w1 << 32) | p.w0) >> p.sh;
+  const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+  auto f = [](uint32_t w, int b) { return __float_as_uint((float)((w >> (8 * b)) & 255u)); };
+  U4 o;
+  o.x = (f(lo, 0) >> 16) | (f(lo, 1) & 0xffff0000u);
+  o.y = f(lo, 2) >> 16;
+  o.z = (f(lo, 3) >> 16) | (f(hi, 0) & 0xffff0000u);
+  o.w = f(hi, 1) >> 16;
+  return o;
+}
+
+// One sample's wave halo with the per-slot offsets precomputed (the bounds do not depend on the
+// sample): goff = byte offset of the pixel pair inside one image (~0u: padding), loff = LDS element
+// offset (~0u: slot past the halo).
+template <bool U8>
+struct WaveHaloR {
+  uint32_t goff[WPF], loff[WPF];
+  U4 pf[U8 ? 1 : WPF];
+  U8Pair pu[U8 ? WPF : 1];
+  PTG_DEV void init(int H, int W, int ih0, int iw0, int lane) {
+#pragma unroll
+    for (int p = 0; p < WPF; ++p) {
+      const int idx = lane + p * 64, r = idx / WHP, c = idx - r * WHP;
+      const int ih = ih0 + r, iw = iw0 + 2 * c;
+      const bool ok = r < WHR && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+      goff[p] = ok ? (uint32_t)(ih * W + iw) * (U8 ? 3u : 8u) : ~0u;
+      loff[p] = r < WHR ? (uint32_t)(r * WROWE + c * 8) : ~0u;
+    }
+  }
+  PTG_DEV void load(const Rsrc& xr, uint32_t img_bytes, int n) {
+    const uint32_t base = (uint32_t)n * img_bytes;
+#pragma unroll
+    for (int p = 0; p < WPF; ++p) {
+      const bool ok = goff[p] != ~0u;
+      if constexpr (U8) pu[p] = u8pair_load(xr, base + goff[p], ok);
+      else pf[p] = bload16(xr, ok ? base + goff[p] : PTG_OOB);
+    }
+  }
+  PTG_DEV void store(bf16_t* buf) const {
+#pragma unroll
+    for (int p = 0; p < WPF; ++p) {
+      if (loff[p] != ~0u) {
+        U4 v;
+        if constexpr (U8) v = u8pair_to_bf16x8_int(pu[p]);
+        else v = pf[p];
+        *(U4*)(buf + loff[p]) = v;
+      }
+    }
+  }
+};
+
+template <bool U8>
+__global__ __launch_bounds__(256) void conv1_fwd_rec_k(const void* __restrict__ x, const bf16_t* __restrict__ w,
+                                                       const float* __restrict__ bias, const float* __restrict__ alpha,
+                                                       bf16_t* __restrict__ pooled, bf16_t* __restrict__ zsel,
+                                                       uint8_t* __restrict__ argq, int N, int H, int W, int tiles_h,
+                                                       int tiles_w, int nchunks) {
+  __shared__ __attribute__((aligned(16))) bf16_t smem[WZS + 8];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int px = lane & 15, g = lane >> 4, hf = wid & 1, rp = wid >> 1;
+  if (tid < 8) smem[WZS + tid] = 0;
+  __syncthreads();
+  const Item it = work_item(N, tiles_h, tiles_w, nchunks);
+  if (it.n0 >= it.n1) return;
+  bf16_t* const wr = smem + wid * WREG;
+  bf16x8_t wreg[KSTEPS];
+  load_wreg(w, px, g, wreg);
+  const int cc = 4 * (g & 1), dwo = g >> 1;
+  constexpr float XS = U8 ? 1.f / 255.f : 1.f;  // integer pixels: z = acc / 255 + bias
+  float bv[4] = {0.f, 0.f, 0.f, 0.f};
+  if (bias) { const float4 b4 = *(const float4*)(bias + cc); bv[0] = b4.x; bv[1] = b4.y; bv[2] = b4.z; bv[3] = b4.w; }
+  const int ow = it.ow0 + hf * WTW + 2 * px + dwo;
+  float al[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int oh = it.oh0 + 2 * rp + i;
+    const float4 a = (oh < H && ow < W) ? *(const float4*)(alpha + ((long)oh * W + ow) * COUT + cc)
+                                        : make_float4(0.f, 0.f, 0.f, 0.f);
+    al[i][0] = a.x; al[i][1] = a.y; al[i][2] = a.z; al[i][3] = a.w;
+  }
+  const int PH = H >> 1, PW = W >> 1;
+  const int ph = (it.oh0 >> 1) + rp, pw = (it.ow0 >> 1) + hf * 16 + px;
+  const bool store_lane = g < 2 && ph < PH && pw < PW;
+  const long pstep = (long)PH * PW * COUT, pbase = ((long)ph * PW + pw) * COUT + cc;
+  const Rsrc xr = x_rsrc<U8>(x, N, H, W);
+  const uint32_t img_bytes = (uint32_t)(H * W) * (U8 ? 3u : 8u);
+  WaveHaloR<U8> hl;
+  hl.init(H, W, it.oh0 + 2 * rp - PAD, it.ow0 + hf * WTW - PAD, lane);
+  hl.load(xr, img_bytes, it.n0);
+  hl.store(wr);
+  wave_lds_sync();
+  for (int n = it.n0; n < it.n1; ++n) {
+    const int b = (n - it.n0) & 1;
+    const bool has_next = n + 1 < it.n1;
+    if (has_next) hl.load(xr, img_bytes, n + 1);
+    f32x4_t acc[2];
+    conv_tile_w(wr + b * WHB, smem + WZS, wreg, px, g, acc);
+    float pm[4], zs[4];
+    uint32_t qs = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float y[2], zr[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        zr[i] = bf2f(f2bf(fmaf(acc[i][r], XS, bv[r])));
+        y[i] = zr[i] > 0.f ? zr[i] : al[i][r] * zr[i];
+      }
+      // window (dh, dw) in q = 2*dh + dw order; this lane holds dw = dwo, the partner lane ^ 32 the other
+      const float py0 = __shfl_xor(y[0], 32, 64), py1 = __shfl_xor(y[1], 32, 64);
+      const float pz0 = __shfl_xor(zr[0], 32, 64), pz1 = __shfl_xor(zr[1], 32, 64);
+      const float yq[4] = {dwo ? py0 : y[0], dwo ? y[0] : py0, dwo ? py1 : y[1], dwo ? y[1] : py1};
+      const float zq[4] = {dwo ? pz0 : zr[0], dwo ? zr[0] : pz0, dwo ? pz1 : zr[1], dwo ? zr[1] : pz1};
+      float bm = yq[0], bz = zq[0];
+      uint32_t a = 0;
+#pragma unroll
+      for (int q = 1; q < 4; ++q)
+        if (yq[q] > bm) { bm = yq[q]; bz = zq[q]; a = q; }  // first maximum in q order
+      pm[r] = bm;
+      zs[r] = bz;
+      qs |= a << (8 * r);
+    }
+    if (store_lane) {
+      const long po = (long)n * pstep + pbase;
+      *(U2*)(pooled + po) = U2{pack_bf(pm[0], pm[1]), pack_bf(pm[2], pm[3])};
+      *(U2*)(zsel + po) = U2{pack_bf(zs[0], zs[1]), pack_bf(zs[2], zs[3])};
+      *(uint32_t*)(argq + po) = qs;
+    }
+    if (has_next) {
+      hl.store(wr + (b ^ 1) * WHB);
+      wave_lds_sync();
+    }
+  }
+}
+
+template <bool U8>
+__global__ __launch_bounds__(256) void conv1_bwd_rec_k(const void* __restrict__ x, const float* __restrict__ alpha,
+                                                       const bf16_t* __restrict__ dp, const bf16_t* __restrict__ zsel,
+                                                       const uint8_t* __restrict__ argq, float* __restrict__ dw,
+                                                       float* __restrict__ dalpha, float* __restrict__ dbias, int N,
+                                                       int H, int W, int tiles_h, int tiles_w, int nchunks) {
+  __shared__ __attribute__((aligned(16))) bf16_t smem[WZS + 8];
+  __shared__ float2 sda[4][4][64];  // dalpha partials: [wave][window position q][lane] (2 channels)
+  __shared__ float sdb[4][COUT];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int hf = wid & 1, rp = wid >> 1;
+  const int g = lane >> 4, li = lane & 15;
+  // record lane: pooled column pc of the wave's 16, channels 2*c2, 2*c2 + 1
+  const int pc = lane & 15, c2 = lane >> 4;
+  if (tid < 8) smem[WZS + tid] = 0;
+  bf16_t* const wr = smem + wid * WREG;
+  bf16_t* const ds = wr + 2 * WHB;
+  for (int i = lane; i < WDZ / 8; i += 64) *(U4*)(ds + 8 * i) = zero4();  // MFMA rows 8-15 read 0
+#pragma unroll
+  for (int q = 0; q < 4; ++q) sda[wid][q][lane] = make_float2(0.f, 0.f);
+  __syncthreads();
+  const Item it = work_item(N, tiles_h, tiles_w, nchunks);
+  if (it.n0 >= it.n1) return;
+  const int PH = H >> 1, PW = W >> 1;
+  const int ph = (it.oh0 >> 1) + rp, pw = (it.ow0 >> 1) + hf * 16 + pc;
+  const bool pin = ph < PH && pw < PW;
+  // alpha of the lane's 2 channels at the 4 window pixels
+  float2 al[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int oh = 2 * ph + (q >> 1), ow = 2 * pw + (q & 1);
+    al[q] = pin ? *(const float2*)(alpha + ((long)oh * W + ow) * COUT + 2 * c2) : make_float2(0.f, 0.f);
+  }
+  const Rsrc xr = x_rsrc<U8>(x, N, H, W);
+  const uint32_t img_bytes = (uint32_t)(H * W) * (U8 ? 3u : 8u);
+  const uint32_t rec_elems = (uint32_t)(N * PH * PW * COUT);
+  const Rsrc dr = make_rsrc(dp, rec_elems * 2u), zr_ = make_rsrc(zsel, rec_elems * 2u), qr = make_rsrc(argq, rec_elems);
+  const uint32_t roff = (uint32_t)((ph * PW + pw) * COUT + 2 * c2), rstep = (uint32_t)(PH * PW * COUT);
+  auto rec_load = [&](int n, uint32_t& gw, uint32_t& zw, uint32_t& qw) {
+    const uint32_t o = pin ? (uint32_t)n * rstep + roff : PTG_OOB / 2;  // element index (PTG_OOB/2 * 2 = OOB bytes)
+    gw = bload4(dr, pin ? 2u * o : PTG_OOB);
+    zw = bload4(zr_, pin ? 2u * o : PTG_OOB);
+    qw = __builtin_amdgcn_raw_buffer_load_b16(qr, pin ? o : PTG_OOB, 0, 0);
+  };
+  f32x4_t wacc[WNB];
+#pragma unroll
+  for (int j = 0; j < WNB; ++j) wacc[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float db[2] = {0.f, 0.f};
+  WaveHaloR<U8> hl;
+  hl.init(H, W, it.oh0 + 2 * rp - PAD, it.ow0 + hf * WTW - PAD, lane);
+  hl.load(xr, img_bytes, it.n0);
+  uint32_t gn, zn, qn;
+  rec_load(it.n0, gn, zn, qn);
+  hl.store(wr);
+  wave_lds_sync();
+  for (int n = it.n0; n < it.n1; ++n) {
+    const int b = (n - it.n0) & 1;
+    const bf16_t* hb = wr + b * WHB;
+    const bool has_next = n + 1 < it.n1;
+    const uint32_t gw = gn, zw = zn, qw = qn;
+    if (has_next) {
+      hl.load(xr, img_bytes, n + 1);
+      rec_load(n + 1, gn, zn, qn);
+    }
+    // dZ at each window's argmax for the lane's 2 channels, zero at the other 3 pixels
+    uint32_t dzw[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int ch = 0; ch < 2; ++ch) {
+      const float gv = ch ? hi_bf(gw) : lo_bf(gw);
+      const float zv = ch ? hi_bf(zw) : lo_bf(zw);
+      const int q = (qw >> (8 * ch)) & 3;
+      const float a = q == 0 ? (ch ? al[0].y : al[0].x) : q == 1 ? (ch ? al[1].y : al[1].x)
+                    : q == 2 ? (ch ? al[2].y : al[2].x) : (ch ? al[3].y : al[3].x);
+      const bool pos = zv > 0.f;
+      const float d = pos ? gv : gv * a;
+      db[ch] += d;
+      if (!pos && gv != 0.f) {  // dalpha at the argmax pixel (lane-private LDS slot)
+        float2* sp = &sda[wid][q][lane];
+        if (ch) sp->y += gv * zv; else sp->x += gv * zv;
+      }
+      const uint32_t dbits = (uint32_t)f2bf(d) << (16 * ch);
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) dzw[qq] |= q == qq ? dbits : 0u;
+    }
+    // pixel (dh, dw) of pooled column pc is wave pixel m = dh*32 + 2*pc + dw
+    int ol = lane;
+    asm volatile("" : "+v"(ol));
+    const int opc = ol & 15, oc2 = ol >> 4;
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq)
+      *(uint32_t*)(ds + ((qq >> 1) * WTW + 2 * opc + (qq & 1)) * DPITCH + 2 * oc2) = dzw[qq];
+    wave_lds_sync();
+    const int og = ol >> 4, oq = (ol & 15) >> 2, op = ol & 3;
+#pragma unroll 1
+    for (int k0 = 0; k0 < WPIX; k0 += 32) {
+      const int m0 = k0 + 8 * og + oq, m1 = m0 + 4;
+      const s16x4_t alo = tr_read(ds + m0 * DPITCH + 4 * op);
+      const s16x4_t ahi = tr_read(ds + m1 * DPITCH + 4 * op);
+      U2 ua = __builtin_bit_cast(U2, alo), ub = __builtin_bit_cast(U2, ahi);
+      const bf16x8_t af = __builtin_bit_cast(bf16x8_t, U4{ua.x, ua.y, ub.x, ub.y});
+      const int h0 = (m0 / WTW) * WROWE + (m0 % WTW) * C, h1 = (m1 / WTW) * WROWE + (m1 % WTW) * C;
+#pragma unroll
+      for (int j = 0; j < WNB; ++j) {
+        const int kf = j * 16 + 4 * op;
+        const int kh = kf / (KS * C), kw = (kf - kh * KS * C) / C;
+        const bool ok = kf < KF;
+        const bf16_t* s0 = ok ? hb + h0 + kh * WROWE + kw * C : smem + WZS;
+        const bf16_t* s1 = ok ? hb + h1 + kh * WROWE + kw * C : smem + WZS;
+        const s16x4_t blo = tr_read(s0), bhi = tr_read(s1);
+        ua = __builtin_bit_cast(U2, blo);
+        ub = __builtin_bit_cast(U2, bhi);
+        wacc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, __builtin_bit_cast(bf16x8_t, U4{ua.x, ua.y, ub.x, ub.y}),
+                                                          wacc[j], 0, 0, 0);
+      }
+    }
+    if (has_next) hl.store(wr + (b ^ 1) * WHB);
+    wave_lds_sync();  // next halo visible; this dZ tile read before it is rewritten
+  }
+  // dalpha (each (pixel, channel) of the tile belongs to exactly one lane and window position)
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float2 t = sda[wid][q][lane];
+    const long o = ((long)(2 * ph + (q >> 1)) * W + 2 * pw + (q & 1)) * COUT + 2 * c2;
+    if (pin) {
+      if (t.x != 0.f) atomicAdd(dalpha + o, t.x);
+      if (t.y != 0.f) atomicAdd(dalpha + o + 1, t.y);
+    }
+  }
+  // dbias: the 16 pooled columns of a channel pair, then the waves
+#pragma unroll
+  for (int ch = 0; ch < 2; ++ch) {
+    float v = db[ch];
+    v += __shfl_xor(v, 1, 64);
+    v += __shfl_xor(v, 2, 64);
+    v += __shfl_xor(v, 4, 64);
+    v += __shfl_xor(v, 8, 64);
+    db[ch] = v;
+  }
+  if (pc == 0) { sdb[wid][2 * c2] = db[0]; sdb[wid][2 * c2 + 1] = db[1]; }
+  __syncthreads();
+  constexpr float XS = U8 ? 1.f / 255.f : 1.f;  // integer pixels in the halo: dW = sum / 255
+  float* red = reinterpret_cast<float*>(smem);
+  if (g < 2) {
+#pragma unroll
+    for (int j = 0; j < WNB; ++j) {
+      const int kf = j * 16 + li;
+      if (kf < KF) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[wid * COUT * KF + (g * 4 + r) * KF + kf] = wacc[j][r];
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < COUT * KF; i += 256)
+    atomicAdd(dw + i, XS * (red[i] + red[COUT * KF + i] + red[2 * COUT * KF + i] + red[3 * COUT * KF + i]));
+  if (tid < COUT) atomicAdd(dbias + tid, sdb[0][tid] + sdb[1][tid] + sdb[2][tid] + sdb[3][tid]);
+}
+
 // sample chunks per tile position: as many work items as fit the device at once (one wave of
 // workgroups, no tail), or PTG_CONV1_*_PER_CU workgroups per CU when set
 // PTG_CONV1_WAVE=0: the block-synchronised sample loop (A/B)
@@ -759,6 +1061,38 @@ int ptg_conv1_bwd_pm(const void* x, int u8, const void* w, const float* bias, co
   if (items > 0x7fffffff) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(kern, dim3((unsigned)items), dim3(256), 0, s, x, (const bf16_t*)w, bias, alpha,
                      (const bf16_t*)dp, dw, dalpha, dbias, N, H, W, th, tw, nch);
+  PTG_RETURN_LAUNCH();
+}
+
+// Record pipeline: forward writes pooled, zsel (bf16 z at each window's argmax) and argq (uint8
+// argmax q = 2*dh + dw), all [N][H/2][W/2][8]; the backward reads them with x and the pooled gradient.
+int ptg_conv1_fwd_rec(const void* x, int u8, const void* w, const float* bias, const float* alpha, void* pooled,
+                      void* zsel, void* argq, int N, int H, int W, hipStream_t s) {
+  if ((H & 1) || (W & 1) || N <= 0 || !ptg_fits_2g((long)N * H * W * (u8 ? 3 : 8)) ||
+      !ptg_fits_2g((long)N * H * W * 4))
+    return (int)hipErrorInvalidValue;
+  const int th = (H + TH - 1) / TH, tw = (W + TW - 1) / TW;
+  const auto kern = u8 ? conv1_fwd_rec_k<true> : conv1_fwd_rec_k<false>;
+  const int nch = conv1_chunks(N, (long)th * tw, (const void*)kern, "PTG_CONV1_FWD_PER_CU");
+  const long items = (long)th * tw * nch;
+  if (items > 0x7fffffff) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(kern, dim3((unsigned)items), dim3(256), 0, s, x, (const bf16_t*)w, bias, alpha, (bf16_t*)pooled,
+                     (bf16_t*)zsel, (uint8_t*)argq, N, H, W, th, tw, nch);
+  PTG_RETURN_LAUNCH();
+}
+
+int ptg_conv1_bwd_rec(const void* x, int u8, const float* alpha, const void* dp, const void* zsel, const void* argq,
+                      float* dw, float* dalpha, float* dbias, int N, int H, int W, hipStream_t s) {
+  if ((H & 1) || (W & 1) || N <= 0 || !ptg_fits_2g((long)N * H * W * (u8 ? 3 : 8)) ||
+      !ptg_fits_2g((long)N * H * W * 4))
+    return (int)hipErrorInvalidValue;
+  const int th = (H + TH - 1) / TH, tw = (W + TW - 1) / TW;
+  const auto kern = u8 ? conv1_bwd_rec_k<true> : conv1_bwd_rec_k<false>;
+  const int nch = conv1_chunks(N, (long)th * tw, (const void*)kern, "PTG_CONV1_BWD_PER_CU");
+  const long items = (long)th * tw * nch;
+  if (items > 0x7fffffff) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(kern, dim3((unsigned)items), dim3(256), 0, s, x, alpha, (const bf16_t*)dp, (const bf16_t*)zsel,
+                     (const uint8_t*)argq, dw, dalpha, dbias, N, H, W, th, tw, nch);
   PTG_RETURN_LAUNCH();
 }
 

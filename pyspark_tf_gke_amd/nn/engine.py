@@ -50,6 +50,10 @@ RAW_U8 = config.get("raw_u8_input")
 # no record, no dZ, no separate prelu/pool backward.  PTG_CONV1_FUSED=0 restores the sparse-record
 # pipeline above for A/B.
 CONV1_FUSED = config.get("conv1_fused")
+# ... and by default (CONV1_REC) its forward keeps the pool record (z at each window's argmax + the
+# argmax: 3 bytes per pooled element) so the backward kernel needs no conv recompute and no argmax
+# search; PTG_CONV1_REC=0 runs the recomputing backward.
+CONV1_REC = config.get("conv1_rec")
 
 
 def host_fp32(enabled: bool | None = None) -> bool:
@@ -175,6 +179,13 @@ class ConvOp(Op):
             p = ws.get(self.name + "/p", (x.shape[0], OH // 2, OW // 2, Co), torch.bfloat16, x.device)
             b = self.conv.bias.data if self.conv.bias is not None else None
             self._fused1, self._x, self._sel, self._sparse = True, x, False, False
+            if CONV1_REC:
+                shp = (x.shape[0], OH // 2, OW // 2, Co)
+                self._zs = ws.get(self.name + "/zsel", shp, torch.bfloat16, x.device)
+                self._arg = ws.get(self.name + "/arg", shp, torch.uint8, x.device)
+                return K.conv1_fwd_rec(x, self.conv.kernel.bf16, b, self._pool_alpha(ws, x.device), p, self._zs,
+                                       self._arg)
+            self._zs = self._arg = None
             return K.conv1_fwd_pm(x, self.conv.kernel.bf16, b, self._pool_alpha(ws, x.device), p)
         if self._raw_u8_ok(x):
             x = x.contiguous()
@@ -261,6 +272,9 @@ class ConvOp(Op):
             ws.get(self.name + "/nobias", (Co,), torch.float32, dev)
         dalpha = self.prelu.alpha.grad if self.prelu is not None else \
             ws.get(self.name + "/dalpha_dummy", (OH, OW, Co), torch.float32, dev)
+        if getattr(self, "_zs", None) is not None:
+            K.conv1_bwd_rec(x, self._pool_alpha(ws, dev), dy, self._zs, self._arg, self.conv.kernel.grad, dalpha, bias_g)
+            return None
         b = self.conv.bias.data if self.conv.bias is not None else None
         K.conv1_bwd_pm(x, self.conv.kernel.bf16, b, self._pool_alpha(ws, dev), dy, self.conv.kernel.grad, dalpha,
                        bias_g)

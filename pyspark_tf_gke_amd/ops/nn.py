@@ -279,6 +279,50 @@ def conv1_fwd_pm(x, w, bias, alpha, pooled):
     return pooled
 
 
+def conv1_fwd_rec(x, w, bias, alpha, pooled, zsel, argq):
+    """First conv layer forward keeping the pool record (conv1.hip conv1_fwd_rec_k): pooled =
+    maxpool2x2(prelu(conv5x5(x) + bias, alpha)), zsel = z at each 2x2 window's argmax (bf16) and
+    argq = the argmax q = 2*dh + dw (uint8), all [N,H/2,W/2,8].  uint8 images enter the MFMA as
+    exact integers with the 1/255 applied to the accumulators."""
+    if not on_device(x):
+        return ref.conv1_fwd_rec(x, w, bias, alpha, pooled, zsel, argq)
+    N, H, W, _ = x.shape
+    _conv1_check(x, w, alpha, N, H, W)
+    shp = (N, H // 2, W // 2, 8)
+    need(pooled, torch.bfloat16, "conv1.pooled"); need(zsel, torch.bfloat16, "conv1.zsel"); need(argq, torch.uint8, "conv1.argq")
+    assert tuple(pooled.shape) == shp and tuple(zsel.shape) == shp and tuple(argq.shape) == shp
+    if bias is not None:
+        need(bias, torch.float32, "conv1.bias")
+    hip("ptg_conv1_fwd_rec", ptr(x), int(x.dtype == torch.uint8), ptr(w), ptr(bias), ptr(alpha), ptr(pooled), ptr(zsel),
+        ptr(argq), N, H, W)
+    return pooled
+
+
+def conv1_bwd_rec(x, alpha, dp, zsel, argq, dw, dalpha, dbias):
+    """Backward of :func:`conv1_fwd_rec` from its record (conv1.hip conv1_bwd_rec_k): dZ at each
+    window's argmax from (dp, zsel, argq, alpha), then dw [8,5,5,4], dalpha [H,W,8], dbias [8]
+    (fp32, accumulated atomically into what the buffers hold)."""
+    if not on_device(x):
+        return ref.conv1_bwd_rec(x, alpha, dp, zsel, argq, dw, dalpha, dbias)
+    N, H, W, _ = x.shape
+    if x.dtype == torch.uint8:
+        assert x.shape[-1] == 3
+    else:
+        need(x, torch.bfloat16, "conv1.x")
+        assert x.shape[-1] == 4
+    shp = (N, H // 2, W // 2, 8)
+    for t, nm in ((dp, "dp"), (zsel, "zsel")):
+        need(t, torch.bfloat16, "conv1." + nm)
+        assert tuple(t.shape) == shp, (nm, t.shape)
+    need(argq, torch.uint8, "conv1.argq"); need(alpha, torch.float32, "conv1.alpha")
+    need(dw, torch.float32, "conv1.dw"); need(dalpha, torch.float32, "conv1.dalpha"); need(dbias, torch.float32, "conv1.dbias")
+    assert tuple(argq.shape) == shp and tuple(alpha.shape) == (H, W, 8) and tuple(dalpha.shape) == (H, W, 8)
+    assert tuple(dw.shape) == (8, 5, 5, 4) and dbias.numel() == 8
+    hip("ptg_conv1_bwd_rec", ptr(x), int(x.dtype == torch.uint8), ptr(alpha), ptr(dp), ptr(zsel), ptr(argq), ptr(dw),
+        ptr(dalpha), ptr(dbias), N, H, W)
+    return dw
+
+
 def conv1_bwd_pm(x, w, bias, alpha, dp, dw, dalpha, dbias):
     """Backward of :func:`conv1_fwd_pm` in one kernel (conv1.hip conv1_bwd_pm_k): z, the PReLU and
     the pool argmax are recomputed from x; dw [8,5,5,4], dalpha [H,W,8] and dbias [8] (fp32)

@@ -216,6 +216,24 @@ def conv1_fwd_pm(x, w, bias, alpha, pooled):
     return prelu_pool_fwd(_conv1_z(x, w, bias), alpha, pooled)
 
 
+def conv1_fwd_rec(x, w, bias, alpha, pooled, zsel, argq):
+    """pooled + the pool record (z at each window's argmax, argmax q) (conv1.hip conv1_fwd_rec_k)."""
+    return prelu_pool_fwd_sparse(_conv1_z(x, w, bias), alpha, pooled, zsel, argq)
+
+
+def conv1_bwd_rec(x, alpha, dp, zsel, argq, dw, dalpha, dbias):
+    """Backward of conv1_fwd_rec from its record: dw, dalpha, dbias accumulate."""
+    N, PH, PW, C = zsel.shape
+    dzs = torch.empty((N, PH, PW, C))
+    prelu_pool_bwd_sel(dp, zsel, argq, alpha, dzs, dalpha, dbias)
+    dz = expand_pool_record(dzs.to(torch.bfloat16), argq, (N, 2 * PH, 2 * PW, C))
+    xin = conv1_input(x)
+    g = torch.nn.grad.conv2d_weight(xin.permute(0, 3, 1, 2), (C, xin.shape[-1], 5, 5), dz.permute(0, 3, 1, 2),
+                                    padding=2)
+    dw.add_(g.permute(0, 2, 3, 1))
+    return dw
+
+
 def conv1_bwd_pm(x, w, bias, alpha, dp, dw, dalpha, dbias):
     """Backward of conv1_fwd_pm from the pooled gradient: dw, dalpha, dbias accumulate."""
     z = _conv1_z(x, w, bias)
