@@ -296,14 +296,27 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
   // consecutive tiles of a workgroup share one output position and the per-element PReLU alphas
   // (for CNN-B1 layer 2 16 KB per tile, more than its halo) stay in registers across samples
   constexpr bool SMAJ = !RING && EPI != EPI_Z;
-  auto decode = [&](int tt, int& s_, int& th_) {
+  // tile t -> (sample n, column strip twi, row tile th); divisions only for a range's first tile,
+  // then the next tile is stepped incrementally (each runtime 32-bit division is ~40 scalar and
+  // vector instructions, and the tile loop did six of them per tile)
+  auto decode = [&](int tt, int& n_, int& twi_, int& th_) {
     if constexpr (SMAJ) {
-      const int nn = tt % N, pos = tt / N;
-      th_ = pos % tiles_h;
-      s_ = nn * tiles_w + pos / tiles_h;
+      const int pos = tt / N;
+      n_ = tt - pos * N;
+      twi_ = pos / tiles_h;
+      th_ = pos - twi_ * tiles_h;
     } else {
-      s_ = tt / tiles_h;
+      const int s_ = tt / tiles_h;
       th_ = tt - s_ * tiles_h;
+      n_ = s_ / tiles_w;
+      twi_ = s_ - n_ * tiles_w;
+    }
+  };
+  auto step = [&](int& n_, int& twi_, int& th_) {
+    if constexpr (SMAJ) {  // sample fastest, then row tile, then column strip
+      if (++n_ == N) { n_ = 0; if (++th_ == tiles_h) { th_ = 0; ++twi_; } }
+    } else {               // row tile fastest (down a strip), then strip, then sample
+      if (++th_ == tiles_h) { th_ = 0; if (++twi_ == tiles_w) { twi_ = 0; ++n_; } }
     }
   };
   float4 al[EPI != EPI_Z ? FM : 1][NF];
@@ -321,36 +334,31 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
     t1 = (int)(T * (bid + 1) / nblk);
   }
   if (t0 >= t1) break;
-  int s, th;
-  decode(t0, s, th);
+  int n, twi, th;
+  decode(t0, n, twi, th);
   int apos = -1;  // output position whose alphas are in al (SMAJ)
   {  // first tile: synchronous fill of its HR rows
-    const int n = s / tiles_w, ow0 = (s - n * tiles_w) * TW;
-    load_rows(n, ow0 - pad, th * TH - pad, HR);
+    load_rows(n, twi * TW - pad, th * TH - pad, HR);
     store_rows(HR, RING ? (th * TH) % HR : 0);
   }
   __syncthreads();
 
   const int PH = H >> 1, PW = W >> 1;
   for (int t = t0; t < t1; ++t) {
-    const int n = s / tiles_w, ow0 = (s - n * tiles_w) * TW, oh0 = th * TH;
+    const int ow0 = twi * TW, oh0 = th * TH;
     // next tile of the range and the rows it needs that are not resident
-    int s2 = s, th2 = th + 1;
-    if constexpr (SMAJ) {
-      decode(t + 1, s2, th2);
-    } else if (th2 >= tiles_h) {
-      s2 = s + 1; th2 = 0;
-    }
+    int n2 = n, twi2 = twi, th2 = th;
+    step(n2, twi2, th2);
     const bool has_next = t + 1 < t1;
-    const bool same_strip = !SMAJ && s2 == s;
-    const int n2 = s2 / tiles_w, ow02 = (s2 - n2 * tiles_w) * TW;
+    const bool same_strip = !SMAJ && n2 == n && twi2 == twi;
+    const int ow02 = twi2 * TW;
     const int nrows2 = (RING && same_strip) ? TH : HR;
     const int ih2 = (RING && same_strip) ? th2 * TH - pad + HR - TH : th2 * TH - pad;
     const int slot2 = !RING ? 0 : same_strip ? (th2 * TH + HR - TH) % HR : (th2 * TH) % HR;
     if (has_next) load_rows(n2, ow02 - pad, ih2, nrows2);
 
     // alpha for this lane's (pixel, 4 channels) of every fragment, needed after the MFMAs
-    const int pos = SMAJ ? t / N : t;
+    const int pos = twi * tiles_h + th;
     if constexpr (EPI != EPI_Z) {
       if (pos != apos) {
         apos = pos;
@@ -565,7 +573,8 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
     }
     if (!has_next) break;
     __syncthreads();  // next tile's halo rows visible
-    s = s2;
+    n = n2;
+    twi = twi2;
     th = th2;
   }
   }  // work rounds
@@ -663,8 +672,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_strip_k(const bf16_t* __restri
   const Rsrc xr = make_rsrc(x, U8 ? u8_rsrc_bytes((long)N * H * W * 3) : (uint32_t)((long)N * H * W * C * 2));
   const Rsrc dr = make_rsrc(dz, (uint32_t)(SPARSE ? (long)N * PH * PW * Cout * 2 : (long)N * H * W * Cout * 2));
   const Rsrc qr = make_rsrc(argq, SPARSE ? (uint32_t)((long)N * PH * PW * Cout) : 0u);
-  auto load_tile = [&](int s_, int th_, int nrows, int ih_first) {
-    const int n = s_ / tiles_w, ow0 = (s_ - n * tiles_w) * TW, oh0 = th_ * TH;
+  auto load_tile = [&](int n, int twi_, int th_, int nrows, int ih_first) {
+    const int ow0 = twi_ * TW, oh0 = th_ * TH;
     const uint32_t img = (uint32_t)(n * H * W * C) * 2u;
 #pragma unroll
     for (int k = 0; k < PFN; ++k) {
@@ -752,19 +761,26 @@ __global__ __launch_bounds__(256) void conv_wgrad_strip_k(const bf16_t* __restri
     t1 = (int)(T * (chunk + 1) / nchunks);
   }
   if (t0 >= t1) break;
-  int s = t0 / tiles_h, th = t0 - s * tiles_h;
-  load_tile(s, th, HR, th * TH - pad);
+  // (sample, column strip, row tile) of t0; later tiles are stepped without divisions
+  int th, twi, n;
+  {
+    const int s = t0 / tiles_h;
+    th = t0 - s * tiles_h;
+    n = s / tiles_w;
+    twi = s - n * tiles_w;
+  }
+  load_tile(n, twi, th, HR, th * TH - pad);
   store_tile(HR, RING ? (th * TH) % HR : 0);
   __syncthreads();
   for (int t = t0; t < t1; ++t) {
-    int s2 = s, th2 = th + 1;
-    if (th2 >= tiles_h) { s2 = s + 1; th2 = 0; }
+    int n2 = n, twi2 = twi, th2 = th + 1;
+    if (th2 >= tiles_h) { th2 = 0; if (++twi2 == tiles_w) { twi2 = 0; ++n2; } }
     const bool has_next = t + 1 < t1;
-    const bool same_strip = s2 == s;
+    const bool same_strip = th2 != 0;
     const int nrows2 = (RING && same_strip) ? TH : HR;
     const int ih2 = (RING && same_strip) ? th2 * TH - pad + HR - TH : th2 * TH - pad;
     const int slot2 = !RING ? 0 : same_strip ? (th2 * TH + HR - TH) % HR : (th2 * TH) % HR;
-    if (has_next) load_tile(s2, th2, nrows2, ih2);
+    if (has_next) load_tile(n2, twi2, th2, nrows2, ih2);
 
     const int wrow = RING ? (th * TH) % HR : 0;
 #pragma unroll 2
@@ -800,7 +816,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_strip_k(const bf16_t* __restri
     __syncthreads();  // all reads of this tile done
     store_tile(nrows2, slot2);
     __syncthreads();
-    s = s2;
+    n = n2;
+    twi = twi2;
     th = th2;
   }
   }  // work rounds
