@@ -417,7 +417,8 @@ def test_first_layer_fused_model_grads(monkeypatch, u8):
             _close(g1, g, 1e-2, 1e-4, "fused1_grad_" + name)
             continue
         cos = float(torch.dot(g1.flatten(), g.flatten()) / (g1.norm() * g.norm() + 1e-20))
-        assert cos > (0.9 if name.startswith("conv2d/") else 0.99), ("fused1_grad_" + name, cos)
+        first = name.startswith(("conv2d/", "p_re_lu/"))  # the first layer itself (argmax flips)
+        assert cos > (0.9 if first else 0.99), ("fused1_grad_" + name, cos)
 
 
 @pytest.mark.parametrize("N,H,W,C,Co,epi", [(16, 256, 320, 4, 8, "pools"), (32, 128, 160, 8, 16, "pool"),
