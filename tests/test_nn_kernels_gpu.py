@@ -417,8 +417,10 @@ def test_first_layer_fused_model_grads(monkeypatch, u8):
             _close(g1, g, 1e-2, 1e-4, "fused1_grad_" + name)
             continue
         cos = float(torch.dot(g1.flatten(), g.flatten()) / (g1.norm() * g.norm() + 1e-20))
-        first = name.startswith(("conv2d/", "p_re_lu/"))  # the first layer itself (argmax flips)
-        assert cos > (0.9 if first else 0.99), ("fused1_grad_" + name, cos)
+        # the first layer's own parameters and the per-element PReLU alphas downstream (their gradient
+        # follows each pool window's argmax) move the most
+        sensitive = name.startswith("conv2d/") or "alpha" in name
+        assert cos > (0.9 if sensitive else 0.99), ("fused1_grad_" + name, cos)
 
 
 @pytest.mark.parametrize("N,H,W,C,Co,epi", [(16, 256, 320, 4, 8, "pools"), (32, 128, 160, 8, 16, "pool"),
