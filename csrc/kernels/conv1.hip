@@ -713,6 +713,28 @@ PTG_DEV U4 u8pair_to_bf16x8_int(const U8Pair& p) {
   return o;
 }
 
+// Per-lane B-fragment offsets of the conv MFMA (sample-invariant, computed once): k-step ks reads
+// halo element (i + kh) * WROWE + (2*px + kw) * C; past KTOT the A fragment is zero, so any finite
+// halo element will do (offset 0) and no zero-slot select is needed per read.
+PTG_DEV void conv_boffs(int px, int g, int* boff) {
+#pragma unroll
+  for (int ks = 0; ks < KSTEPS; ++ks) {
+    const int kf = ks * 32 + 8 * g;
+    const int kh = kf / KROW, kw = (kf - kh * KROW) / C;
+    boff[ks] = kf < KTOT ? kh * WROWE + (2 * px + kw) * C : 0;
+  }
+}
+PTG_DEV void conv_tile_r(const bf16_t* hb, const int* boff, const bf16x8_t* wreg, f32x4_t* acc) {
+  acc[0] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  acc[1] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < KSTEPS; ++ks) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wreg[ks], *(const bf16x8_t*)(hb + boff[ks] + i * WROWE), acc[i], 0, 0, 0);
+  }
+}
+
 // One sample's wave halo with the per-slot offsets precomputed (the bounds do not depend on the
 // sample): goff = byte offset of the pixel pair inside one image (~0u: padding), loff = LDS element
 // offset (~0u: slot past the halo).
@@ -788,6 +810,8 @@ __global__ __launch_bounds__(256) void conv1_fwd_rec_k(const void* __restrict__ 
   const long pstep = (long)PH * PW * COUT, pbase = ((long)ph * PW + pw) * COUT + cc;
   const Rsrc xr = x_rsrc<U8>(x, N, H, W);
   const uint32_t img_bytes = (uint32_t)(H * W) * (U8 ? 3u : 8u);
+  int boff[KSTEPS];
+  conv_boffs(px, g, boff);
   WaveHaloR<U8> hl;
   hl.init(H, W, it.oh0 + 2 * rp - PAD, it.ow0 + hf * WTW - PAD, lane);
   hl.load(xr, img_bytes, it.n0);
@@ -798,7 +822,7 @@ __global__ __launch_bounds__(256) void conv1_fwd_rec_k(const void* __restrict__ 
     const bool has_next = n + 1 < it.n1;
     if (has_next) hl.load(xr, img_bytes, n + 1);
     f32x4_t acc[2];
-    conv_tile_w(wr + b * WHB, smem + WZS, wreg, px, g, acc);
+    conv_tile_r(wr + b * WHB, boff, wreg, acc);
     float pm[4], zs[4];
     uint32_t qs = 0;
 #pragma unroll
@@ -809,11 +833,12 @@ __global__ __launch_bounds__(256) void conv1_fwd_rec_k(const void* __restrict__ 
         zr[i] = bf2f(f2bf(fmaf(acc[i][r], XS, bv[r])));
         y[i] = zr[i] > 0.f ? zr[i] : al[i][r] * zr[i];
       }
-      // window (dh, dw) in q = 2*dh + dw order; this lane holds dw = dwo, the partner lane ^ 32 the other
+      // window (dh, dw) in q = 2*dh + dw order: only the dw = 0 lanes (g < 2) store, so the window is
+      // assembled in their order (own pixel = dw 0, lane ^ 32 = dw 1); the dw = 1 lanes' result is unused
       const float py0 = __shfl_xor(y[0], 32, 64), py1 = __shfl_xor(y[1], 32, 64);
       const float pz0 = __shfl_xor(zr[0], 32, 64), pz1 = __shfl_xor(zr[1], 32, 64);
-      const float yq[4] = {dwo ? py0 : y[0], dwo ? y[0] : py0, dwo ? py1 : y[1], dwo ? y[1] : py1};
-      const float zq[4] = {dwo ? pz0 : zr[0], dwo ? zr[0] : pz0, dwo ? pz1 : zr[1], dwo ? zr[1] : pz1};
+      const float yq[4] = {y[0], py0, y[1], py1};
+      const float zq[4] = {zr[0], pz0, zr[1], pz1};
       float bm = yq[0], bz = zq[0];
       uint32_t a = 0;
 #pragma unroll
@@ -837,7 +862,7 @@ __global__ __launch_bounds__(256) void conv1_fwd_rec_k(const void* __restrict__ 
 }
 
 template <bool U8>
-__global__ __launch_bounds__(256) void conv1_bwd_rec_k(const void* __restrict__ x, const float* __restrict__ alpha,
+__global__ __launch_bounds__(256, 4) void conv1_bwd_rec_k(const void* __restrict__ x, const float* __restrict__ alpha,
                                                        const bf16_t* __restrict__ dp, const bf16_t* __restrict__ zsel,
                                                        const uint8_t* __restrict__ argq, float* __restrict__ dw,
                                                        float* __restrict__ dalpha, float* __restrict__ dbias, int N,
@@ -884,6 +909,25 @@ __global__ __launch_bounds__(256) void conv1_bwd_rec_k(const void* __restrict__ 
 #pragma unroll
   for (int j = 0; j < WNB; ++j) wacc[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   float db[2] = {0.f, 0.f};
+  // weight-gradient operand offsets (sample-invariant): the A (dZ) rows of the lane's two pixels per
+  // k-step, the halo pixel of those rows, and the B column base (kh, kw) of each 16-column fragment
+  // (columns past KF read any finite halo element: their outputs are never flushed)
+  const int q4 = (lane & 15) >> 2, p4 = lane & 3;
+  int aoff[2][2], hoff[2][2], bcol[WNB];
+#pragma unroll
+  for (int k = 0; k < 2; ++k)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int m = k * 32 + 8 * g + q4 + 4 * h;
+      aoff[k][h] = m * DPITCH + 4 * p4;
+      hoff[k][h] = (m / WTW) * WROWE + (m % WTW) * C;
+    }
+#pragma unroll
+  for (int jj = 0; jj < WNB; ++jj) {
+    const int kf = jj * 16 + 4 * p4;
+    const int kh = kf / (KS * C), kw = (kf - kh * KS * C) / C;
+    bcol[jj] = kf < KF ? kh * WROWE + kw * C : 0;
+  }
   WaveHaloR<U8> hl;
   hl.init(H, W, it.oh0 + 2 * rp - PAD, it.ow0 + hf * WTW - PAD, lane);
   hl.load(xr, img_bytes, it.n0);
@@ -921,34 +965,25 @@ __global__ __launch_bounds__(256) void conv1_bwd_rec_k(const void* __restrict__ 
       for (int qq = 0; qq < 4; ++qq) dzw[qq] |= q == qq ? dbits : 0u;
     }
     // pixel (dh, dw) of pooled column pc is wave pixel m = dh*32 + 2*pc + dw
-    int ol = lane;
-    asm volatile("" : "+v"(ol));
-    const int opc = ol & 15, oc2 = ol >> 4;
 #pragma unroll
     for (int qq = 0; qq < 4; ++qq)
-      *(uint32_t*)(ds + ((qq >> 1) * WTW + 2 * opc + (qq & 1)) * DPITCH + 2 * oc2) = dzw[qq];
+      *(uint32_t*)(ds + ((qq >> 1) * WTW + 2 * pc + (qq & 1)) * DPITCH + 2 * c2) = dzw[qq];
     wave_lds_sync();
-    const int og = ol >> 4, oq = (ol & 15) >> 2, op = ol & 3;
-#pragma unroll 1
-    for (int k0 = 0; k0 < WPIX; k0 += 32) {
-      const int m0 = k0 + 8 * og + oq, m1 = m0 + 4;
-      const s16x4_t alo = tr_read(ds + m0 * DPITCH + 4 * op);
-      const s16x4_t ahi = tr_read(ds + m1 * DPITCH + 4 * op);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const s16x4_t alo = tr_read(ds + aoff[k][0]);
+      const s16x4_t ahi = tr_read(ds + aoff[k][1]);
       U2 ua = __builtin_bit_cast(U2, alo), ub = __builtin_bit_cast(U2, ahi);
       const bf16x8_t af = __builtin_bit_cast(bf16x8_t, U4{ua.x, ua.y, ub.x, ub.y});
-      const int h0 = (m0 / WTW) * WROWE + (m0 % WTW) * C, h1 = (m1 / WTW) * WROWE + (m1 % WTW) * C;
+      const bf16_t* h0 = hb + hoff[k][0];
+      const bf16_t* h1 = hb + hoff[k][1];
 #pragma unroll
-      for (int j = 0; j < WNB; ++j) {
-        const int kf = j * 16 + 4 * op;
-        const int kh = kf / (KS * C), kw = (kf - kh * KS * C) / C;
-        const bool ok = kf < KF;
-        const bf16_t* s0 = ok ? hb + h0 + kh * WROWE + kw * C : smem + WZS;
-        const bf16_t* s1 = ok ? hb + h1 + kh * WROWE + kw * C : smem + WZS;
-        const s16x4_t blo = tr_read(s0), bhi = tr_read(s1);
+      for (int jj = 0; jj < WNB; ++jj) {
+        const s16x4_t blo = tr_read(h0 + bcol[jj]), bhi = tr_read(h1 + bcol[jj]);
         ua = __builtin_bit_cast(U2, blo);
         ub = __builtin_bit_cast(U2, bhi);
-        wacc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, __builtin_bit_cast(bf16x8_t, U4{ua.x, ua.y, ub.x, ub.y}),
-                                                          wacc[j], 0, 0, 0);
+        wacc[jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, __builtin_bit_cast(bf16x8_t, U4{ua.x, ua.y, ub.x, ub.y}),
+                                                           wacc[jj], 0, 0, 0);
       }
     }
     if (has_next) hl.store(wr + (b ^ 1) * WHB);
