@@ -121,6 +121,7 @@ def _input_note(workload: str) -> str:
 
 
 def _time_steps(model, xs, ys, steps, warmup):
+    from pyspark_tf_gke_amd.ops import nn as K
     from pyspark_tf_gke_amd.parallel import comm
 
     stats = model._stats_buf()
@@ -129,7 +130,7 @@ def _time_steps(model, xs, ys, steps, warmup):
     _sync()
     comm.barrier()
     _sync()
-    stats.zero_()
+    K.fill_(stats, 0.0)
     t0 = time.perf_counter()
     for i in range(steps):
         model.train_step_fast(xs[i % 2], ys[i % 2], stats)

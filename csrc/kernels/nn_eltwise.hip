@@ -1282,6 +1282,23 @@ int ptg_sgd(float* p, float* g, float* vel, void* pbf, long n, float lr, float m
   PTG_RETURN_LAUNCH();
 }
 
+// p[0 .. nwords) = value (32-bit words): the runtime's buffer fills (zeroed workspaces, optimizer
+// state, gradient buffers) without a framework fill kernel
+__global__ __launch_bounds__(256) void fill_u32_k(uint32_t* __restrict__ p, long n4, long nwords, uint32_t value) {
+  const U4 v = U4{value, value, value, value};
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) *(U4*)(p + 4 * i) = v;
+  const long tail = nwords - 4 * n4;  // < 4 words
+  if (blockIdx.x == 0 && threadIdx.x < tail) p[4 * n4 + threadIdx.x] = value;
+}
+
+int ptg_fill_u32(void* p, long nwords, unsigned int value, hipStream_t s) {
+  if (nwords <= 0) return 0;
+  if (((uintptr_t)p & 15) != 0) return (int)hipErrorInvalidValue;
+  const long n4 = nwords / 4;
+  hipLaunchKernelGGL(fill_u32_k, dim3(grid_for(n4 > 0 ? n4 : 1)), dim3(256), 0, s, (uint32_t*)p, n4, nwords, value);
+  PTG_RETURN_LAUNCH();
+}
+
 int ptg_cast_f32_bf16(const float* x, void* y, long n, hipStream_t s) {
   hipLaunchKernelGGL(cast_f32_bf16_k, dim3(grid_for(n)), dim3(256), 0, s, x, (bf16_t*)y, n);
   PTG_RETURN_LAUNCH();

@@ -72,7 +72,7 @@ class Workspace:
             dtype = torch.float32
         t = self.bufs.get(key)
         if t is None or tuple(t.shape) != shape or t.dtype != dtype or t.device != torch.device(device):
-            t = (torch.zeros if zero else torch.empty)(shape, dtype=dtype, device=device)
+            t = K.zeros(shape, dtype, device) if zero else torch.empty(shape, dtype=dtype, device=device)
             self.bufs[key] = t
         return t
 

@@ -254,10 +254,10 @@ class Sequential:
     def _stats_buf(self, which="train"):
         if which == "train":
             if self._stats is None or self._stats.device != self.device:
-                self._stats = torch.zeros(8, dtype=torch.float32, device=self.device)
+                self._stats = K.zeros(8, torch.float32, self.device)
             return self._stats
         if self._eval_stats is None or self._eval_stats.device != self.device:
-            self._eval_stats = torch.zeros(8, dtype=torch.float32, device=self.device)
+            self._eval_stats = K.zeros(8, torch.float32, self.device)
         return self._eval_stats
 
     # ---------------------------------------------------------------- forward / loss / step
@@ -439,7 +439,7 @@ class Sequential:
     def train_on_batch(self, x, y, return_dict: bool = False):
         xb, yb = self._prep_batch(x, y)
         stats = self._stats_buf()
-        stats.zero_()
+        K.fill_(stats, 0.0)
         self.train_step(xb, yb, stats)
         self._sync_master()
         logs = self._logs_from(stats)
@@ -519,7 +519,7 @@ class Sequential:
         for epoch in range(initial_epoch, epochs):
             if verbose and is_chief:
                 print(f"Epoch {epoch + 1}/{epochs}", flush=True)
-            stats.zero_()
+            K.fill_(stats, 0.0)
             t0 = time.perf_counter()
             it = persistent_it if persistent_it is not None else self._iter_batches(x, y, batch_size, shuffle,
                                                                                    seed=epoch)
@@ -565,7 +565,7 @@ class Sequential:
     def evaluate(self, x=None, y=None, batch_size=None, steps=None, verbose="auto", return_dict=False,
                  _prefix=""):
         stats = self._stats_buf("eval")
-        stats.zero_()
+        K.fill_(stats, 0.0)
         it = self._iter_batches(x, y, batch_size, False)
         n = 0
         while steps is None or n < steps:

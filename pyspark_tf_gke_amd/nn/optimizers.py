@@ -56,8 +56,8 @@ class Adam(Optimizer):
 
     def build(self, store) -> None:
         if self.m is None or self.m.numel() != store.total or self.m.device != store.flat.device:
-            self.m = torch.zeros(store.total, dtype=torch.float32, device=store.flat.device)
-            self.v = torch.zeros(store.total, dtype=torch.float32, device=store.flat.device)
+            self.m = K.zeros(store.total, torch.float32, store.flat.device)
+            self.v = K.zeros(store.total, torch.float32, store.flat.device)
             self.dev_state = None
 
     def use_device_step(self, store) -> None:
@@ -156,7 +156,7 @@ class SGD(Optimizer):
     def build(self, store) -> None:
         if self.momentum > 0 and (self.velocity is None or self.velocity.numel() != store.total
                                   or self.velocity.device != store.flat.device):
-            self.velocity = torch.zeros(store.total, dtype=torch.float32, device=store.flat.device)
+            self.velocity = K.zeros(store.total, torch.float32, store.flat.device)
 
     def apply(self, store, gscale: float = 1.0, lo: int = 0, hi: int | None = None, advance: bool = True) -> None:
         self.build(store)

@@ -96,7 +96,9 @@ class ParamStore:
         for p in self.params:
             flat_host[p.offset:p.offset + p.numel] = host_vals[p.name].reshape(-1)
         self.flat = torch.from_numpy(flat_host).to(self.device)
-        self.flat_grad = torch.zeros(self.total, dtype=torch.float32, device=self.device)
+        from ..ops import nn as K
+
+        self.flat_grad = K.zeros(self.total, torch.float32, self.device)
         from .engine import host_fp32
 
         mirror = torch.float32 if (host_fp32() and self.device.type == "cpu") else torch.bfloat16
@@ -138,14 +140,16 @@ class ParamStore:
             off = int(math.ceil(off / align) * align)
             ranges.append((lo, off))
         total = max(off, ALIGN)
-        flat = torch.zeros(total, dtype=self.flat.dtype, device=self.flat.device)
-        mirror = torch.zeros(total, dtype=self.flat_bf16.dtype, device=self.flat.device)
+        from ..ops import nn as K
+
+        flat = K.zeros(total, self.flat.dtype, self.flat.device)
+        mirror = K.zeros(total, self.flat_bf16.dtype, self.flat.device)
         for p in self.params:
             o, n = old[id(p)]
             flat[p.offset:p.offset + n] = self.flat[o:o + n]
             mirror[p.offset:p.offset + n] = self.flat_bf16[o:o + n]
         self.flat, self.flat_bf16 = flat, mirror
-        self.flat_grad = torch.zeros(total, dtype=torch.float32, device=flat.device)
+        self.flat_grad = K.zeros(total, torch.float32, flat.device)
         self.total = total
         self._bind_views()
         self.update_zero_ranges()
@@ -165,11 +169,18 @@ class ParamStore:
         if getattr(self, "grad_clean", False):
             self.grad_clean = False
             return
+        from ..ops import nn as K
+
         for lo, hi in self._zero_ranges:
-            self.flat_grad[lo:hi].zero_()
+            K.fill_(self.flat_grad[lo:hi], 0.0)
 
     def refresh_bf16(self) -> None:
-        self.flat_bf16.copy_(self.flat.to(self.flat_bf16.dtype))
+        from ..ops import nn as K
+
+        if self.flat.is_cuda and self.flat_bf16.dtype == torch.bfloat16:
+            K.cast_f32_bf16(self.flat, self.flat_bf16)
+        else:
+            self.flat_bf16.copy_(self.flat.to(self.flat_bf16.dtype))
 
     def by_name(self, name: str) -> Param:
         for p in self.params:

@@ -11,6 +11,7 @@ from __future__ import annotations
 import math
 import os
 
+import numpy as np
 import torch
 
 from . import reference as ref
@@ -699,6 +700,29 @@ def sim_all_gather(bucket, cnt: int):
     es = bucket.element_size()
     hip("ptg_sim_all_gather", ptr(bucket), cnt * es, bucket.numel() * es)
     return bucket
+
+
+def fill_(t: torch.Tensor, value: float = 0.0) -> torch.Tensor:
+    """t[:] = value with the HIP fill kernel (GPU, 4-byte elements or zero fills of 16-byte aligned
+    buffers whose size is a multiple of 4 bytes); torch's fill elsewhere."""
+    nbytes = t.numel() * t.element_size()
+    if not on_device(t) or not t.is_contiguous() or nbytes % 4 or t.data_ptr() % 16 or \
+            (value != 0.0 and t.element_size() != 4):
+        return t.fill_(value)
+    if t.dtype == torch.float32:
+        word = int(np.float32(value).view(np.uint32))
+    elif value == 0.0:
+        word = 0
+    else:
+        word = int(np.int32(int(value)).view(np.uint32))
+    hip("ptg_fill_u32", ptr(t), nbytes // 4, word)
+    return t
+
+
+def zeros(shape, dtype=torch.float32, device=None) -> torch.Tensor:
+    """torch.zeros without the framework fill kernel on the GPU."""
+    t = torch.empty(shape, dtype=dtype, device=device)
+    return fill_(t, 0.0)
 
 
 def cast_f32_bf16(x, out):
