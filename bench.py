@@ -125,15 +125,19 @@ def _time_steps(model, xs, ys, steps, warmup):
     from pyspark_tf_gke_amd.parallel import comm
 
     stats = model._stats_buf()
-    for i in range(warmup):
-        model.train_step_fast(xs[i % 2], ys[i % 2], stats)
+    # overlapped_steps: a step's big Dense dW+Adam may overlap the next step's conv forward; each
+    # step still launches all of its own kernels, and the scope waits for them before it closes
+    with model.overlapped_steps():
+        for i in range(warmup):
+            model.train_step_fast(xs[i % 2], ys[i % 2], stats)
     _sync()
     comm.barrier()
     _sync()
     K.fill_(stats, 0.0)
     t0 = time.perf_counter()
-    for i in range(steps):
-        model.train_step_fast(xs[i % 2], ys[i % 2], stats)
+    with model.overlapped_steps():
+        for i in range(steps):
+            model.train_step_fast(xs[i % 2], ys[i % 2], stats)
     _sync()
     comm.barrier()
     _sync()

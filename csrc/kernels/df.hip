@@ -1103,6 +1103,331 @@ __global__ __launch_bounds__(256) void small_range_agg_k(const long long* __rest
   }
 }
 
+// ---- sparse keys at mid cardinality: ONE 512-way hash partition + LDS hash tables --------------
+// The recursive radix path needs two 64-way levels for ~1M distinct keys (count + scatter twice:
+// ~96 B moved per row with one f64 column).  Partitioned 512 ways by the top 9 bits of mix64(key),
+// a partition holds K/512 keys (~2K at 1M groups), which fit one LDS hash table, so the data is
+// counted, scattered and aggregated once (~56 B per row):
+//   hash9_count_k    per-tile 512-bin histograms, tile-major [tile][512] (ptg_digit_offsets_b)
+//   hash9_scatter_k  rows staged in LDS by digit, written as 512 contiguous runs (i64 key, f64
+//                    values, null -> NaN); XCD-aware tile order as the other scatter passes
+//   hash9_agg_k      (chunk, partition) workgroups of 1024 threads: an LDS hash table over the
+//                    chunk's rows, occupied slots compacted into the (partition, chunk) region of a
+//                    partial table (no global atomics on data)
+//   hash9_merge_k    one workgroup per partition folds its chunks' partials into one table and
+//                    appends the groups to the output in hash_extract_k's layout
+// A table that overflows (far more keys than the estimate) sets the error word; the host then takes
+// the recursive path, so a bad estimate costs time, never correctness.
+#define H9B 512
+#define H9T 4096  // tile rows for nv <= 1 (nv == 2: 2048, the LDS staging budget)
+PTG_DEV int h9_digit(long long k) { return (int)(mix64((unsigned long long)k) >> (64 - 9)); }
+
+__global__ __launch_bounds__(256) void hash9_count_k(const long long* __restrict__ keys, long n, int T,
+                                                     unsigned int* __restrict__ hist) {
+  constexpr int RPT = H9T / 256;
+  __shared__ unsigned int h[4][H9B];
+  const int tid = threadIdx.x, b = blockIdx.x, w = tid >> 6;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) { h[q][tid] = 0; h[q][tid + 256] = 0; }
+  const long s0 = (long)b * T;
+  const int nr = (int)min((long)T, n - s0);
+  long long k[RPT];
+#pragma unroll
+  for (int j = 0; j < RPT; ++j) {
+    const int i = tid + j * 256;
+    k[j] = i < nr ? keys[s0 + i] : 0;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < RPT; ++j)
+    if (tid + j * 256 < nr) atomicAdd(&h[w][h9_digit(k[j])], 1u);
+  __syncthreads();
+  for (int d = tid; d < H9B; d += 256) hist[(long)b * H9B + d] = h[0][d] + h[1][d] + h[2][d] + h[3][d];
+}
+
+template <int NV, int RTT, int NT = 512>
+__global__ __launch_bounds__(NT) void hash9_scatter_k(const long long* __restrict__ keys, PayIn pin, long n,
+                                                      int ntiles, const long long* __restrict__ offs,
+                                                      long long* __restrict__ okeys, PayOut pout) {
+  constexpr int RPT = RTT / NT;
+  static_assert(RPT >= 1 && RTT % NT == 0, "tile rows must be a multiple of the thread count");
+  constexpr int NVS = NV > 0 ? NV : 1;
+  __shared__ long long sk[RTT];
+  __shared__ double sv[NVS][NV > 0 ? RTT : 1];
+  __shared__ unsigned short sd[RTT];
+  __shared__ unsigned int cnt[H9B];
+  __shared__ unsigned int lstart[H9B];
+  __shared__ long long goff[H9B];
+  const int tid = threadIdx.x, b = xcd_tile(blockIdx.x, ntiles);
+  const long s0 = (long)b * RTT;
+  const int nr = (int)min((long)RTT, n - s0);
+  for (int d = tid; d < H9B; d += NT) {
+    cnt[d] = 0;
+    goff[d] = offs[(long)b * H9B + d];
+  }
+  __syncthreads();
+  long long k[RPT];
+  double v[NVS][RPT];
+  int d[RPT];
+#pragma unroll
+  for (int j = 0; j < RPT; ++j) {
+    const int i = tid + j * NT;
+    d[j] = -1;
+    if (i < nr) {
+      k[j] = keys[s0 + i];
+#pragma unroll
+      for (int q = 0; q < NV; ++q) v[q][j] = load_pay(pin, q, s0 + i);
+      d[j] = h9_digit(k[j]);
+      atomicAdd(&cnt[d[j]], 1u);
+    }
+  }
+  __syncthreads();
+  if (tid < 64) {  // exclusive scan of the 512 digit counts in one wave, 8 per lane
+    unsigned c8[8], sum = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) { c8[q] = cnt[8 * tid + q]; sum += c8[q]; }
+    unsigned incl = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned t = __shfl_up(incl, o, 64);
+      if (tid >= o) incl += t;
+    }
+    unsigned run = incl - sum;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) { lstart[8 * tid + q] = run; run += c8[q]; cnt[8 * tid + q] = 0; }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < RPT; ++j) {
+    if (d[j] < 0) continue;
+    const unsigned pos = lstart[d[j]] + atomicAdd(&cnt[d[j]], 1u);
+    sk[pos] = k[j];
+#pragma unroll
+    for (int q = 0; q < NV; ++q) sv[q][pos] = v[q][j];
+    sd[pos] = (unsigned short)d[j];
+  }
+  __syncthreads();
+  for (int i = tid; i < nr; i += NT) {  // consecutive rows of a digit run -> consecutive addresses
+    const int dd = sd[i];
+    const long long dst = PTG_CHECKED_IDX(goff[dd] + (i - (int)lstart[dd]), n);
+    okeys[dst] = sk[i];
+#pragma unroll
+    for (int q = 0; q < NV; ++q) pout.vals[q][dst] = sv[q][i];
+  }
+}
+
+// LDS hash table of TS slots (power of two, >= 1024): [keys i64][sum f64 per column][rows u32][cnt u32
+// per column]; rows/sum/cnt added with LDS atomics.  Returns false when no slot was found in
+// H9_PROBES probes (the table is too full: the host falls back).
+#define H9_PROBES 256
+template <int NV>
+struct H9Table {
+  long long* lk;
+  double* lsum;
+  unsigned int* lrow;
+  unsigned int* lcnt;
+  int TS;
+  PTG_DEV H9Table(unsigned char* raw, int ts) : TS(ts) {
+    lk = (long long*)raw;
+    lsum = (double*)(lk + ts);
+    lrow = (unsigned int*)(lsum + (long)NV * ts);
+    lcnt = lrow + ts;
+  }
+  PTG_DEV void clear(int tid, int nt) {
+    for (int t = tid; t < TS; t += nt) {
+      lk[t] = EMPTY_KEY;
+      lrow[t] = 0;
+#pragma unroll
+      for (int j = 0; j < NV; ++j) { lsum[j * TS + t] = 0.0; lcnt[j * TS + t] = 0; }
+    }
+  }
+  PTG_DEV int slot(long long key) {
+    const int mask = TS - 1;
+    int h = (int)(mix64((unsigned long long)key) & (unsigned long long)mask);
+    for (int probe = 0; probe < H9_PROBES; ++probe) {
+      const long long cur = lk[h];
+      if (cur == key) return h;
+      if (cur == EMPTY_KEY) {
+        const long long prev = (long long)atomicCAS((unsigned long long*)&lk[h], (unsigned long long)EMPTY_KEY,
+                                                    (unsigned long long)key);
+        if (prev == EMPTY_KEY || prev == key) return h;
+      }
+      h = (h + 1) & mask;
+    }
+    return -1;
+  }
+};
+
+// Block-wide exclusive scan over 1024 threads (16 waves); *total = the sum.
+PTG_DEV int block_excl_scan1024(int c, int* wsum, int* total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int incl = c;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += t;
+  }
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  int base = 0, tot = 0;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int x = wsum[q];
+    base += q < w ? x : 0;
+    tot += x;
+  }
+  *total = tot;
+  return base + incl - c;
+}
+
+// grid (chunks, 512): partition p = blockIdx.y holds rows [offs[p], offs[p+1]) of the scattered
+// arrays (offs tile-major, offs[512*ntiles] = n); chunk c its c-th slice.  Partial region
+// (p, c) = entries [(p*C + c)*TS, +pn[p*C + c]) of pkeys / prow / psum[j] / pcnt[j] (R = 512*C*TS each).
+template <int NV>
+__global__ __launch_bounds__(1024) void hash9_agg_k(const long long* __restrict__ okeys, AggPay pay,
+                                                    const long long* __restrict__ offs, int ntiles, int TS,
+                                                    long long* __restrict__ pkeys, unsigned int* __restrict__ prow,
+                                                    double* __restrict__ psum, unsigned int* __restrict__ pcnt,
+                                                    int* __restrict__ pn, unsigned long long* __restrict__ state) {
+  constexpr int NVS = NV > 0 ? NV : 1;
+  extern __shared__ __align__(16) unsigned char lds_raw[];
+  __shared__ int wsum[16];
+  __shared__ int sfail;
+  const int p = blockIdx.y, c = blockIdx.x, C = gridDim.x, tid = threadIdx.x;
+  H9Table<NV> tb(lds_raw, TS);
+  tb.clear(tid, 1024);
+  if (tid == 0) sfail = 0;
+  __syncthreads();
+  const long long a0 = offs[p], b0 = p + 1 < H9B ? offs[p + 1] : offs[(long)H9B * ntiles], len = b0 - a0;
+  const long long a = a0 + len * c / C, b = a0 + len * (c + 1) / C;
+  bool ok = true;
+  auto add = [&](long long key, const double* v) {
+    const int sl = tb.slot(key);
+    if (sl < 0) { ok = false; return; }
+    atomicAdd(&tb.lrow[sl], 1u);
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      if (v[j] != v[j]) continue;  // null / NaN
+      atomicAdd(&tb.lsum[j * TS + sl], v[j]);
+      atomicAdd(&tb.lcnt[j * TS + sl], 1u);
+    }
+  };
+  long long i = a + tid;
+  for (; i + 3 * 1024 < b; i += 4 * 1024) {  // 4 rows' loads in flight ahead of the LDS probes
+    long long k4[4];
+    double v4[4][NVS];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      k4[u] = okeys[i + u * 1024];
+#pragma unroll
+      for (int j = 0; j < NV; ++j) v4[u][j] = pay.vals[j][i + u * 1024];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) add(k4[u], v4[u]);
+  }
+  for (; i < b; i += 1024) {
+    double v1[NVS];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) v1[j] = pay.vals[j][i];
+    add(okeys[i], v1);
+  }
+  if (!ok) sfail = 1;
+  __syncthreads();
+  if (sfail) {
+    if (tid == 0) { atomicOr(&state[1], 1ull); pn[p * C + c] = 0; }
+    return;
+  }
+  // compact the occupied slots into the region: each thread owns TS/1024 consecutive slots
+  const int per = TS >> 10, s0 = tid * per;
+  int cn = 0;
+  for (int t = s0; t < s0 + per; ++t) cn += tb.lk[t] != EMPTY_KEY;
+  int total;
+  int q = block_excl_scan1024(cn, wsum, &total);
+  const long R = (long)H9B * C * TS, base = ((long)p * C + c) * TS;
+  for (int t = s0; t < s0 + per; ++t) {
+    const long long key = tb.lk[t];
+    if (key == EMPTY_KEY) continue;
+    pkeys[base + q] = key;
+    prow[base + q] = tb.lrow[t];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      psum[j * R + base + q] = tb.lsum[j * TS + t];
+      pcnt[j * R + base + q] = tb.lcnt[j * TS + t];
+    }
+    ++q;
+  }
+  if (tid == 0) pn[p * C + c] = total;
+}
+
+// grid 512: partition p folds its C partial regions into one LDS table, then appends its groups at
+// state[0] (atomic base) to out_keys / out_tab ([1 + 4*NV][out_cap]: rows, then per column sum,
+// non-null count, min, max as f64; min / max are +-inf: this path serves sum / count / avg).
+template <int NV>
+__global__ __launch_bounds__(1024) void hash9_merge_k(const long long* __restrict__ pkeys,
+                                                      const unsigned int* __restrict__ prow,
+                                                      const double* __restrict__ psum,
+                                                      const unsigned int* __restrict__ pcnt,
+                                                      const int* __restrict__ pn, int C, int TS,
+                                                      long long* __restrict__ out_keys, double* __restrict__ out_tab,
+                                                      long out_cap, unsigned long long* __restrict__ state) {
+  extern __shared__ __align__(16) unsigned char lds_raw[];
+  __shared__ int wsum[16];
+  __shared__ int sfail;
+  __shared__ unsigned long long obase;
+  const int p = blockIdx.x, tid = threadIdx.x;
+  H9Table<NV> tb(lds_raw, TS);
+  tb.clear(tid, 1024);
+  if (tid == 0) sfail = 0;
+  __syncthreads();
+  const long R = (long)H9B * C * TS;
+  bool ok = true;
+  for (int c = 0; c < C; ++c) {
+    const long base = ((long)p * C + c) * TS;
+    const int m = pn[p * C + c];
+    for (int i = tid; i < m; i += 1024) {
+      const int sl = tb.slot(pkeys[base + i]);
+      if (sl < 0) { ok = false; continue; }
+      atomicAdd(&tb.lrow[sl], prow[base + i]);
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        atomicAdd(&tb.lsum[j * TS + sl], psum[j * R + base + i]);
+        atomicAdd(&tb.lcnt[j * TS + sl], pcnt[j * R + base + i]);
+      }
+    }
+  }
+  if (!ok) sfail = 1;
+  __syncthreads();
+  if (sfail) {
+    if (tid == 0) atomicOr(&state[1], 1ull);
+    return;
+  }
+  const int per = TS >> 10, s0 = tid * per;
+  int cn = 0;
+  for (int t = s0; t < s0 + per; ++t) cn += tb.lk[t] != EMPTY_KEY;
+  int total;
+  const int pre = block_excl_scan1024(cn, wsum, &total);
+  if (tid == 0) obase = total ? atomicAdd(&state[0], (unsigned long long)total) : 0ull;
+  __syncthreads();
+  long long q = (long long)obase + pre;
+  for (int t = s0; t < s0 + per; ++t) {
+    const long long key = tb.lk[t];
+    if (key == EMPTY_KEY) continue;
+    if (q < out_cap) {
+      out_keys[q] = key;
+      out_tab[q] = (double)tb.lrow[t];
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        double* o = out_tab + out_cap * (1 + 4 * j);
+        o[q] = tb.lsum[j * TS + t];
+        o[out_cap + q] = (double)tb.lcnt[j * TS + t];
+        o[2 * out_cap + q] = INFINITY;
+        o[3 * out_cap + q] = -INFINITY;
+      }
+    }
+    ++q;
+  }
+}
+
 // ================================================================================================
 // Stable LSD radix sort of 64-bit keys with a 64-bit payload (DataFrame.orderBy / sort)
 //   sort_key_prep_k  column -> unsigned-orderable u64 (asc or desc; NaN above +inf, -0 == +0) and
@@ -1719,6 +2044,83 @@ int ptg_fill_synthetic_kv(void* keys, void* vals, long n, long offset, long num_
   PTG_RETURN_LAUNCH();
 }
 
+
+// sparse-key mid-cardinality groupBy (hash9_*_k).  Tiles: ptg_hash9_tile_rows(nv) rows, nv <= 2;
+// hist u32[512*ntiles] tile-major; offs i64[512*ntiles + 1] from ptg_digit_offsets_b(bins = 512).
+int ptg_hash9_tile_rows(int nv) { return nv <= 1 ? H9T : H9T / 2; }
+int ptg_hash9_count(const void* keys, long n, int T, int ntiles, void* hist, hipStream_t s) {
+  if (ntiles <= 0 || T > H9T || T <= 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(hash9_count_k, dim3(ntiles), dim3(256), 0, s, (const long long*)keys, n, T, (unsigned int*)hist);
+  PTG_RETURN_LAUNCH();
+}
+int ptg_hash9_scatter(const void* keys, const void* pin_p, int nv, long n, int ntiles, const void* offs, void* okeys,
+                      const void* pout_p, hipStream_t s) {
+  if (ntiles <= 0) return (int)hipErrorInvalidValue;
+  PayIn pin;
+  PayOut pout;
+  memcpy(&pin, pin_p, sizeof(PayIn));
+  memcpy(&pout, pout_p, sizeof(PayOut));
+#define PTG_H9S(NV, TR)                                                                                        \
+  hipLaunchKernelGGL((hash9_scatter_k<NV, TR>), dim3(ntiles), dim3(512), 0, s, (const long long*)keys, pin, n,  \
+                     ntiles, (const long long*)offs, (long long*)okeys, pout)
+  switch (nv) {
+    case 0: PTG_H9S(0, H9T); break;
+    case 1: PTG_H9S(1, H9T); break;
+    case 2: PTG_H9S(2, H9T / 2); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+#undef PTG_H9S
+  PTG_RETURN_LAUNCH();
+}
+static size_t h9_lds(int nv, int TS) { return (size_t)TS * (12 + 12 * (size_t)nv); }
+// vals: host array of nv f64 device pointers (the scattered payload).  state u64[2] = {groups, error}:
+// zeroed here; pkeys i64 / prow u32 / psum f64[nv] / pcnt u32[nv] regions of R = 512*chunks*TS
+// entries, pn i32[512*chunks].
+int ptg_hash9_agg(const void* okeys, const void* const* vals, int nv, const void* offs, int ntiles, int TS, int chunks,
+                  void* pkeys, void* prow, void* psum, void* pcnt, void* pn, void* state, hipStream_t s) {
+  if (nv < 0 || nv > 2 || chunks <= 0 || TS < 1024 || (TS & (TS - 1)) || h9_lds(nv, TS) > 150 * 1024)
+    return (int)hipErrorInvalidValue;
+  (void)hipMemsetAsync(state, 0, 16, s);
+  AggPay pay;
+  for (int j = 0; j < PAY_MAX; ++j) pay.vals[j] = j < nv ? (const double*)vals[j] : nullptr;
+#define PTG_H9A(NV)                                                                                            \
+  {                                                                                                            \
+    static bool attr = false;                                                                                  \
+    if (!attr) {                                                                                               \
+      (void)hipFuncSetAttribute((const void*)hash9_agg_k<NV>, hipFuncAttributeMaxDynamicSharedMemorySize,      \
+                                150 * 1024);                                                                   \
+      attr = true;                                                                                             \
+    }                                                                                                          \
+    hipLaunchKernelGGL((hash9_agg_k<NV>), dim3(chunks, H9B), dim3(1024), h9_lds(NV, TS), s,                    \
+                       (const long long*)okeys, pay, (const long long*)offs, ntiles, TS, (long long*)pkeys,    \
+                       (unsigned int*)prow, (double*)psum, (unsigned int*)pcnt, (int*)pn,                      \
+                       (unsigned long long*)state);                                                            \
+  }
+  switch (nv) { case 0: PTG_H9A(0) break; case 1: PTG_H9A(1) break; default: PTG_H9A(2) break; }
+#undef PTG_H9A
+  PTG_RETURN_LAUNCH();
+}
+int ptg_hash9_merge(const void* pkeys, const void* prow, const void* psum, const void* pcnt, const void* pn, int nv,
+                    int TS, int chunks, void* out_keys, void* out_tab, long out_cap, void* state, hipStream_t s) {
+  if (nv < 0 || nv > 2 || chunks <= 0 || TS < 1024 || (TS & (TS - 1)) || h9_lds(nv, TS) > 150 * 1024)
+    return (int)hipErrorInvalidValue;
+#define PTG_H9M(NV)                                                                                            \
+  {                                                                                                            \
+    static bool attr = false;                                                                                  \
+    if (!attr) {                                                                                               \
+      (void)hipFuncSetAttribute((const void*)hash9_merge_k<NV>, hipFuncAttributeMaxDynamicSharedMemorySize,    \
+                                150 * 1024);                                                                   \
+      attr = true;                                                                                             \
+    }                                                                                                          \
+    hipLaunchKernelGGL((hash9_merge_k<NV>), dim3(H9B), dim3(1024), h9_lds(NV, TS), s, (const long long*)pkeys, \
+                       (const unsigned int*)prow, (const double*)psum, (const unsigned int*)pcnt,              \
+                       (const int*)pn, chunks, TS, (long long*)out_keys, (double*)out_tab, out_cap,            \
+                       (unsigned long long*)state);                                                            \
+  }
+  switch (nv) { case 0: PTG_H9M(0) break; case 1: PTG_H9M(1) break; default: PTG_H9M(2) break; }
+#undef PTG_H9M
+  PTG_RETURN_LAUNCH();
+}
 }  // extern "C"
 
 PTG_CHECK_STATUS(df)

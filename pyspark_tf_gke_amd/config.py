@@ -46,6 +46,10 @@ _K = [
          "dense small-range integer keys take the one-pass range partition + direct LDS aggregation"),
     Knob("groupby_range_chunks", int, 8, "PTG_RANGE_CHUNKS", "spark.ptg.groupby.rangeChunks",
          "row chunks per range partition in the range aggregation (workgroups = 256 x chunks)"),
+    Knob("groupby_hash9", bool, True, "PTG_GROUPBY_HASH9", "spark.ptg.groupby.hash9",
+         "sparse keys at ~64K..1.3M groups: one 512-way hash partition + LDS hash tables (sum/count/avg, <= 2 columns)"),
+    Knob("groupby_h9_chunks", int, 4, "PTG_H9_CHUNKS", "spark.ptg.groupby.h9Chunks",
+         "row chunks per partition in the 512-way hash aggregation (workgroups = 512 x chunks)"),
     Knob("shuffle_buffer_gb", float, 64.0, "PTG_SHUFFLE_BUFFER_GB", "spark.ptg.shuffle.buffer.gb",
          "HBM staging budget of one all-to-all-v shuffle round"),
     Knob("device", str, "", "PTG_DEVICE", "spark.ptg.device", "executor device: cuda / cpu (default: cuda if present)"),
@@ -53,6 +57,9 @@ _K = [
     Knob("fault_task", int, 0, "PTG_FAULT_TASK", None, "fault injection: fail this many stage-task attempts"),
     # training step
     Knob("fused_adam", bool, True, "PTG_FUSED_ADAM", None, "Adam inside the big Dense weight-gradient GEMM epilogue (1 GPU)"),
+    Knob("defer_dense_update", bool, True, "PTG_DEFER_DENSE_UPDATE", None,
+         "inside fit()/bench step loops: the big Dense dW+Adam GEMM runs under the next step's conv forward "
+         "instead of under this step's backward (waited for before the layer that overwrites its input)"),
     Knob("fused_head", bool, True, "PTG_FUSED_HEAD", None, "CNN-B1 Dense(relu)->Dense->MSE head as two kernels"),
     Knob("device_feed", bool, True, "PTG_DEVICE_FEED", None, "fit(): pinned ring + side-stream H2D for host datasets"),
     Knob("side_stream", bool, True, "PTG_SIDE_STREAM", None, "weight gradients on a side HIP stream (1 replica)"),

@@ -481,6 +481,75 @@ def hash_agg_range(keys: torch.Tensor, pay: list, buf, nv: int, sample_lohi: tup
     return _dense_extract(prow, psum, pmm if minmax else None, chunks, nv, Rw, lo, dev)
 
 
+H9_BINS = 512
+H9_MIN_KEYS = 1 << 16  # below this the recursive path needs one 64-way level: the same passes
+
+
+def _h9_table_slots(est_keys: int, nv: int) -> int | None:
+    """LDS hash-table slots per partition of hash9_agg_k / hash9_merge_k: a power of two >= 1024
+    holding the expected keys of the fullest of the 512 partitions (mean + ~7%) at load <= 0.7, within
+    the 150 KB LDS budget (12 + 12 nv bytes per slot); None when no such table fits."""
+    need = est_keys / H9_BINS * 1.15 / 0.7
+    ts = 1024
+    while ts < need:
+        ts *= 2
+    return ts if ts * (12 + 12 * nv) <= 150 * 1024 else None
+
+
+def hash_agg_h9(keys: torch.Tensor, pay: list, buf, nv: int, est_keys: int):
+    """groupBy(key).agg (sum / count / avg, nv <= 2 columns) for int64 keys of mid cardinality
+    (~64K..1.3M groups) in ONE partitioning pass (csrc/kernels/df.hip hash9_*_k): 512 partitions by the
+    top 9 bits of mix64(key), each aggregated into an LDS hash table by chunks and the chunks folded by
+    a per-partition merge.  Same result format as :func:`hash_agg` (min / max are +-inf).  Returns None
+    when a table overflowed (estimate far too low): the caller then takes :func:`hash_agg_radix`'s
+    recursive levels."""
+    ts = _h9_table_slots(est_keys, nv)
+    if ts is None or nv > 2:
+        return None
+    dev = keys.device
+    n = keys.numel()
+    lib = _native.hip_lib()
+    T = int(lib.ptg_hash9_tile_rows(nv))
+    ntiles = (n + T - 1) // T
+    hist = buf("h9hist", (H9_BINS * ntiles,), torch.int32)
+    hip("ptg_hash9_count", ptr(keys), n, T, ntiles, ptr(hist))
+    offs = buf("h9offs", (H9_BINS * ntiles + 1,), torch.int64)
+    tpc = DIGIT_OFFS_TPC
+    nch = -(-ntiles // tpc)
+    csum = buf("h9_csum", (H9_BINS * nch,), torch.int64)
+    cbase = buf("h9_cbase", (H9_BINS * nch,), torch.int64)
+    hip("ptg_digit_offsets_b", 0, ptr(hist), ntiles, tpc, ptr(csum), nch, None, H9_BINS)
+    scan_excl(csum, out=cbase, total=offs[H9_BINS * ntiles:])
+    hip("ptg_digit_offsets_b", 1, ptr(hist), ntiles, tpc, ptr(cbase), nch, ptr(offs), H9_BINS)
+    okeys = buf("h9okeys", (max(n, 1),), torch.int64)[:n]
+    ovals = [buf(f"h9ov{j}", (max(n, 1),), torch.float64)[:n] for j in range(nv)]
+    pin, pout = _pay_in(pay), _pay_out(ovals)
+    hip("ptg_hash9_scatter", ptr(keys), ctypes.addressof(pin), nv, n, ntiles, ptr(offs), ptr(okeys),
+        ctypes.addressof(pout))
+    C = max(1, int(config.get("groupby_h9_chunks")))
+    R = H9_BINS * C * ts
+    pkeys = buf("h9pk", (R,), torch.int64)
+    prow = buf("h9pr", (R,), torch.int32)
+    psum = buf("h9ps", (max(nv, 1) * R,), torch.float64)
+    pcnt = buf("h9pc", (max(nv, 1) * R,), torch.int32)
+    pn = buf("h9pn", (H9_BINS * C,), torch.int32)
+    state = buf("h9st", (2,), torch.int64)
+    vptrs = (ctypes.c_void_p * PAY_MAX)(*([o.data_ptr() for o in ovals] + [0] * (PAY_MAX - nv)))
+    hip("ptg_hash9_agg", ptr(okeys), ctypes.addressof(vptrs), nv, ptr(offs), ntiles, ts, C, ptr(pkeys), ptr(prow),
+        ptr(psum), ptr(pcnt), ptr(pn), ptr(state))
+    cap = H9_BINS * ts
+    out_keys = torch.empty(cap, dtype=torch.int64, device=dev)
+    out_tab = torch.empty((1 + 4 * nv) * cap, dtype=torch.float64, device=dev)
+    hip("ptg_hash9_merge", ptr(pkeys), ptr(prow), ptr(psum), ptr(pcnt), ptr(pn), nv, ts, C, ptr(out_keys),
+        ptr(out_tab), cap, ptr(state))
+    m, err = (int(x) for x in state.tolist())
+    if err:
+        return None
+    ot = out_tab.view(1 + 4 * nv, cap)[:, :m]
+    outs = [(ot[1 + 4 * j], ot[2 + 4 * j], ot[3 + 4 * j], ot[4 + 4 * j]) for j in range(nv)]
+    return out_keys[:m], ot[0], outs
+
+
 def hash_agg_radix(keys: torch.Tensor, vals: list, valids: list, want_minmax: bool = False, ws: dict | None = None,
                    est_keys: int | None = None):
     """groupBy(key).agg over int64 keys by recursive radix partitioning (high cardinality, any
@@ -518,6 +587,11 @@ def hash_agg_radix(keys: torch.Tensor, vals: list, valids: list, want_minmax: bo
             if r is not None:
                 return r
     K = est_keys if est_keys is not None else estimate_distinct(keys)
+    if (keys.dtype == torch.int64 and n >= RANGE_MIN_ROWS and nv <= 2 and not want_minmax and K >= H9_MIN_KEYS
+            and config.get("groupby_hash9")):
+        r = hash_agg_h9(keys.contiguous(), pay, buf, nv, K)
+        if r is not None:
+            return r
     pcap_max = 256
     while _part_agg_lds(pcap_max * 2, nv, want_minmax) <= _AGG_LDS_BUDGET and pcap_max < 4096:
         pcap_max *= 2

@@ -592,3 +592,73 @@ def test_digit_offsets_tile_major(ntiles):
     out = offs.cpu()
     assert torch.equal(out[:-1], ref)
     assert int(out[-1]) == int(hist.long().sum())
+
+
+def _h9_buf():
+    ws = {}
+
+    def buf(name, shape, dtype):
+        numel = int(np.prod(shape))
+        t = ws.get(name)
+        if t is None or t.numel() < numel or t.dtype != dtype:
+            t = ws[name] = torch.empty(numel, dtype=dtype, device="cuda")
+        return t[:numel].view(shape)
+    return buf
+
+
+@pytest.mark.parametrize("n,nkeys,nv", [(8_388_608, 1_000_000, 1), (6_000_000, 120_000, 2), (5_000_000, 400_000, 0),
+                                        (4_500_000, 1_200_000, 1)])
+def test_hash9_agg_matches_host(hip_built, n, nkeys, nv):
+    """One-level 512-way hash partition + chunked LDS hash tables + per-partition merge (df.hip
+    hash9_*_k) vs the host groupBy: sparse int64 keys, f64 and int32 columns with nulls / NaN."""
+    k, v = D.fill_synthetic_kv(n, nkeys, "cuda", sparse=True)
+    g = torch.Generator().manual_seed(n + nv)
+    cols, valids = [], []
+    for j in range(nv):
+        x = v.clone() if j == 0 else torch.randint(-1000, 1000, (n,), generator=g, dtype=torch.int32).cuda()
+        if j == 0:
+            x[::101] = math.nan
+        cols.append(x)
+        valids.append((torch.rand(n, generator=g) > 0.2).to(torch.uint8).cuda() if j == 1 else None)
+    pay = [(c.contiguous(), vd) for c, vd in zip(cols, valids)]
+    got = D.hash_agg_h9(k, pay, _h9_buf(), nv, nkeys)
+    assert got is not None
+    want = D.hash_agg(k.cpu(), [c.cpu() for c in cols], [None if x is None else x.cpu() for x in valids], False)
+    _assert_agg_equal(got, want, False)
+    # and through the planner (sampled distinct-key estimate)
+    _assert_agg_equal(D.hash_agg_radix(k, cols, valids, False), want, False)
+
+
+def test_hash9_overflow_falls_back(hip_built):
+    """An estimate 40x too low sizes the LDS tables far too small: the kernels flag the overflow,
+    hash_agg_h9 returns None and the planner's recursive path still gives the exact result."""
+    n, nk = 4_500_000, 1_000_000
+    k, v = D.fill_synthetic_kv(n, nk, "cuda", sparse=True)
+    assert D.hash_agg_h9(k, [(v, None)], _h9_buf(), 1, nk // 40) is None
+    got = D.hash_agg_radix(k, [v], [None], False, est_keys=nk // 40)
+    want = D.hash_agg(k.cpu(), [v.cpu()], [None], False)
+    _assert_agg_equal(got, want, False)
+
+
+@pytest.mark.parametrize("ntiles", [1, 65, 3001])
+def test_digit_offsets_512_bins(ntiles):
+    """ptg_digit_offsets_b with 512 digits (the hash9 partition) = digit-major exclusive scan."""
+    from pyspark_tf_gke_amd.ops._util import hip, ptr
+
+    torch.manual_seed(ntiles)
+    B = 512
+    hist = torch.randint(0, 3000, (ntiles, B), dtype=torch.int32)
+    ref = torch.cumsum(hist.t().reshape(-1).long(), 0) - hist.t().reshape(-1).long()
+    ref = ref.view(B, ntiles).t().reshape(-1)
+    tpc = D.DIGIT_OFFS_TPC
+    nch = -(-ntiles // tpc)
+    hg = hist.reshape(-1).cuda()
+    csum = torch.empty(B * nch, dtype=torch.int64, device="cuda")
+    cbase = torch.empty_like(csum)
+    offs = torch.full((B * ntiles + 1,), -7, dtype=torch.int64, device="cuda")
+    hip("ptg_digit_offsets_b", 0, ptr(hg), ntiles, tpc, ptr(csum), nch, None, B)
+    D.scan_excl(csum, out=cbase, total=offs[B * ntiles:])
+    hip("ptg_digit_offsets_b", 1, ptr(hg), ntiles, tpc, ptr(cbase), nch, ptr(offs), B)
+    out = offs.cpu()
+    assert torch.equal(out[:-1], ref)
+    assert int(out[-1]) == int(hist.long().sum())

@@ -199,3 +199,45 @@ def test_raw_uint8_first_layer_matches_packed_input(hip_built):
         assert torch.allclose(res[0][2], res[1][2], rtol=1e-3, atol=1e-5)
     else:  # Adam moves a weight by ~lr per step whatever the gradient's size: 3 steps of 1e-3 at most
         assert (res[0][2] - res[1][2]).abs().max().item() <= 6.5e-3
+
+
+def test_deferred_dense_update_is_bit_identical(hip_built):
+    """overlapped_steps(): the Dense dW+Adam GEMM of step t runs under step t+1's conv forward on the
+    side stream.  Same kernels, same inputs, same order per parameter -> the same weights, Adam
+    moments and per-step losses as the undeferred loop."""
+    from pyspark_tf_gke_amd.nn import model as M
+
+    torch.manual_seed(0)
+    xs = [torch.randint(0, 256, (16, 64, 80, 3), dtype=torch.uint8, device="cuda") for _ in range(2)]
+    ys = [torch.rand(16, 2, device="cuda") * 60 for _ in range(2)]
+
+    def run(defer):
+        torch.manual_seed(1)
+        m = build_cnn_model((64, 80, 3), flat=True, summary=False, device="cuda")
+        st = m._stats_buf()
+        losses = []
+        old = M.DEFER_DENSE
+        M.DEFER_DENSE = defer
+        try:
+            with m.overlapped_steps():
+                for i in range(6):
+                    st.zero_()
+                    m.train_step_fast(xs[i % 2], ys[i % 2], st)
+                    if defer:
+                        assert m._deferred_ev is not None  # the Dense update really was deferred
+                    losses.append(m._logs_from(st)["loss"])
+        finally:
+            M.DEFER_DENSE = old
+        assert m._deferred_ev is None
+        torch.cuda.synchronize()
+        return m, losses
+
+    m0, l0 = run(False)
+    m1, l1 = run(True)
+    # (not bit-exact: the conv weight gradients add workgroup partials with fp32 atomics in run order)
+    np.testing.assert_allclose(l1, l0, rtol=2e-3)
+    assert torch.allclose(m0.store.flat, m1.store.flat, rtol=1e-3, atol=2e-5)
+    assert torch.allclose(m0.optimizer.m, m1.optimizer.m, rtol=1e-2, atol=1e-5)
+    # the deferred Dense kernel itself saw the same inputs: its update equals the undeferred one's
+    d0, d1 = m0.ops[-2].dense.kernel, m1.ops[-2].dense.kernel
+    assert torch.allclose(d0.data, d1.data, rtol=1e-3, atol=2e-5)
