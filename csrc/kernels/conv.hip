@@ -1113,15 +1113,28 @@ static bool persist_dynamic() {
   }
   return g_persist_dynamic == 1;
 }
-// queue counters (one per channel group / weight slice), zeroed once; every launch leaves them at 0
+// queue counters (one per channel group / weight slice), zeroed once; every launch leaves them at 0.
+// One counter block PER STREAM: kernels of one stream run in order, but a dgrad on the step's stream
+// and a wgrad on the side stream run at the same time and must never draw from the same counter
+// (each would skip the chunks the other claimed).  Up to 16 streams; beyond that -> static ranges.
 static int* work_queue(int slots, hipStream_t s) {
-  (void)s;
+  constexpr int NSTREAM = 16, SLOTS = 64;
   static int* buf = nullptr;
+  static hipStream_t owner[NSTREAM];
+  static int used = 0;
   if (!buf) {
-    if (hipMalloc(&buf, 64 * sizeof(int)) != hipSuccess || hipMemset(buf, 0, 64 * sizeof(int)) != hipSuccess)
+    if (hipMalloc(&buf, NSTREAM * SLOTS * sizeof(int)) != hipSuccess ||
+        hipMemset(buf, 0, NSTREAM * SLOTS * sizeof(int)) != hipSuccess) {
       buf = nullptr;
+      return nullptr;
+    }
   }
-  return (buf && slots <= 64) ? buf : nullptr;
+  if (slots > SLOTS) return nullptr;
+  for (int i = 0; i < used; ++i)
+    if (owner[i] == s) return buf + i * SLOTS;
+  if (used == NSTREAM) return nullptr;
+  owner[used] = s;
+  return buf + (used++) * SLOTS;
 }
 // tiles per claimed chunk: ~4 chunks per workgroup, at least 4 tiles (each chunk restarts the halo;
 // 8 per workgroup cost 14% on CNN-B1 with the claim not yet prefetched)

@@ -57,9 +57,9 @@ _K = [
     Knob("fault_task", int, 0, "PTG_FAULT_TASK", None, "fault injection: fail this many stage-task attempts"),
     # training step
     Knob("fused_adam", bool, True, "PTG_FUSED_ADAM", None, "Adam inside the big Dense weight-gradient GEMM epilogue (1 GPU)"),
-    Knob("defer_dense_update", bool, True, "PTG_DEFER_DENSE_UPDATE", None,
+    Knob("defer_dense_update", bool, False, "PTG_DEFER_DENSE_UPDATE", None,
          "inside fit()/bench step loops: the big Dense dW+Adam GEMM runs under the next step's conv forward "
-         "instead of under this step's backward (waited for before the layer that overwrites its input)"),
+         "instead of under this step's backward (A/B on CNN-B1 b256: 1.70-1.71 vs 1.65-1.66 ms, so off)"),
     Knob("fused_head", bool, True, "PTG_FUSED_HEAD", None, "CNN-B1 Dense(relu)->Dense->MSE head as two kernels"),
     Knob("device_feed", bool, True, "PTG_DEVICE_FEED", None, "fit(): pinned ring + side-stream H2D for host datasets"),
     Knob("side_stream", bool, True, "PTG_SIDE_STREAM", None, "weight gradients on a side HIP stream (1 replica)"),

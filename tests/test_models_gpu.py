@@ -201,7 +201,22 @@ def test_raw_uint8_first_layer_matches_packed_input(hip_built):
         assert (res[0][2] - res[1][2]).abs().max().item() <= 6.5e-3
 
 
-def test_deferred_dense_update_is_bit_identical(hip_built):
+def _same_training(m0, m1, init, l0, l1):
+    """Two runs of the same steps agree: per-step losses, and the parameters up to the run-order noise
+    of the fp32-atomic weight-gradient sums (Adam turns noise-level gradients of tiny parameters into
+    full-size steps, so the check is on the whole update: |p1 - p0| <= 5% of |p0 - init|; a skipped
+    or misplaced update differs by its whole size)."""
+    np.testing.assert_allclose(l1, l0, rtol=2e-3)
+    d = (m1.store.flat - m0.store.flat).norm().item()
+    u = (m0.store.flat - init).norm().item()
+    assert u > 0 and d <= 0.05 * u, (d, u)
+    for p0, p1 in zip(m0.ops[-2].dense.params, m1.ops[-2].dense.params):
+        dd = (p1.data - p0.data).norm().item()
+        assert dd <= 0.05 * max((p0.data - init[p0.offset:p0.offset + p0.numel].view(p0.data.shape)).norm().item(),
+                                1e-12), (p0.name, dd)
+
+
+def test_deferred_dense_update_same_training(hip_built):
     """overlapped_steps(): the Dense dW+Adam GEMM of step t runs under step t+1's conv forward on the
     side stream.  Same kernels, same inputs, same order per parameter -> the same weights, Adam
     moments and per-step losses as the undeferred loop."""
@@ -214,6 +229,7 @@ def test_deferred_dense_update_is_bit_identical(hip_built):
     def run(defer):
         torch.manual_seed(1)
         m = build_cnn_model((64, 80, 3), flat=True, summary=False, device="cuda")
+        init = m.store.flat.clone()
         st = m._stats_buf()
         losses = []
         old = M.DEFER_DENSE
@@ -230,14 +246,42 @@ def test_deferred_dense_update_is_bit_identical(hip_built):
             M.DEFER_DENSE = old
         assert m._deferred_ev is None
         torch.cuda.synchronize()
-        return m, losses
+        return m, losses, init
 
-    m0, l0 = run(False)
-    m1, l1 = run(True)
-    # (not bit-exact: the conv weight gradients add workgroup partials with fp32 atomics in run order)
-    np.testing.assert_allclose(l1, l0, rtol=2e-3)
-    assert torch.allclose(m0.store.flat, m1.store.flat, rtol=1e-3, atol=2e-5)
-    assert torch.allclose(m0.optimizer.m, m1.optimizer.m, rtol=1e-2, atol=1e-5)
-    # the deferred Dense kernel itself saw the same inputs: its update equals the undeferred one's
-    d0, d1 = m0.ops[-2].dense.kernel, m1.ops[-2].dense.kernel
-    assert torch.allclose(d0.data, d1.data, rtol=1e-3, atol=2e-5)
+    m0, l0, init = run(False)
+    m1, l1, _ = run(True)
+    _same_training(m0, m1, init, l0, l1)
+
+
+def test_persistent_work_queue_mode_matches_static(hip_built):
+    """Work-queue mode of the persistent conv kernels (tile chunks claimed from per-stream counters)
+    computes the same training step as static per-workgroup ranges, with the side-stream weight
+    gradients running concurrently with the dgrad chain (a shared counter would make each kernel skip
+    the chunks the other claimed)."""
+    from pyspark_tf_gke_amd.ops import nn as K
+
+    torch.manual_seed(0)
+    xs = [torch.randint(0, 256, (64, 128, 160, 3), dtype=torch.uint8, device="cuda") for _ in range(2)]
+    ys = [torch.rand(64, 2, device="cuda") * 100 for _ in range(2)]
+
+    def run(dynamic):
+        K.set_persist_mode(dynamic)
+        try:
+            torch.manual_seed(1)
+            m = build_cnn_model((128, 160, 3), flat=True, summary=False, device="cuda")
+            init = m.store.flat.clone()
+            st = m._stats_buf()
+            losses = []
+            with m.overlapped_steps():
+                for i in range(5):
+                    st.zero_()
+                    m.train_step_fast(xs[i % 2], ys[i % 2], st)
+                    losses.append(m._logs_from(st)["loss"])
+            torch.cuda.synchronize()
+            return m, losses, init
+        finally:
+            K.set_persist_mode(None)
+
+    m0, l0, init = run(False)
+    m1, l1, _ = run(True)
+    _same_training(m0, m1, init, l0, l1)

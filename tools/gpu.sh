@@ -79,7 +79,7 @@ for task in "$@"; do
         for e in "${sets[@]}" ""; do
           timeout -k 10 $STEP_T env $e python bench.py --workload "$wl" --groupby-extra 0 --extra-batches "" --sim-world 0 \
             $BENCH_ARGS > gpurun_out/abm.json 2> gpurun_out/abm.err || fail abm gpurun_out/abm.err
-          echo "[${e:-default}] $(cut -c1-150 gpurun_out/abm.json)"
+          echo "[${e:-default}] $(python -c "import json; d = json.load(open('gpurun_out/abm.json')); print(d['value'], d['ms_per_step'], 'final_loss', d['config'].get('final_loss'))")"
         done
       done ;;
     abvar)
