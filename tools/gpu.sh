@@ -90,6 +90,22 @@ for task in "$@"; do
           echo "${lib:-default} $(cut -c1-160 gpurun_out/abvar.json)"
         done
       done ;;
+    profpy)
+      # profpy:<script>: rocprofv3 kernel stats of one python script (PY_ARGS, PROF_TAG, PROF_DIV = divisor)
+      tag=$(basename "$arg" .py)${PROF_TAG:+_$PROF_TAG}
+      timeout -k 10 $STEP_T rocprofv3 --kernel-trace --stats --output-format csv -d "gpurun_out/prof_$tag" -o run -- \
+        python $arg $PY_ARGS > "gpurun_out/prof_$tag.log" 2>&1 || fail "profpy $arg" "gpurun_out/prof_$tag.log"
+      grep -v "^\[" "gpurun_out/prof_$tag.log" | tail -3 | cut -c1-250
+      python tools/prof_summary.py "gpurun_out/prof_$tag/run_kernel_stats.csv" ${PROF_DIV:-1} \
+        > "gpurun_out/prof_${tag}_summary.txt" 2>&1 || true
+      head -${PROF_HEAD:-16} "gpurun_out/prof_${tag}_summary.txt" | cut -c1-200 ;;
+    joint2)
+      # Spark ETL -> Parquet -> train with 2 executors/workers sharing the GPU (gloo: RCCL refuses two
+      # ranks on one device)
+      PTG_DIST_BACKEND=gloo timeout -k 10 $STEP_T python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+        --master-addr 127.0.0.1 --master-port 29641 workloads/joint/etl_to_train.py --rows ${JOINT_ROWS:-5000000} \
+        --out /tmp/joint2 --epochs 2 --batch-size 8192 > gpurun_out/joint2.log 2>&1 || fail joint2 gpurun_out/joint2.log
+      tail -4 gpurun_out/joint2.log | cut -c1-300 ;;
     py)
       out=gpurun_out/$(basename "$arg" .py).log
       timeout -k 10 $STEP_T python $arg $PY_ARGS > "$out" 2>&1 || fail "py $arg" "$out"
