@@ -92,7 +92,9 @@ PTG_DEV void vset(U4& v, int w, uint32_t x) {
   if (w == 0) v.x = x; else if (w == 1) v.y = x; else if (w == 2) v.z = x; else v.w = x;
 }
 
-template <int CH>
+// STORE = false: dalpha / dbias only (dz already produced by the dgrad epilogue of the layer above,
+// conv.hip EPI_PPB): the same loads and arithmetic, no dz stores.
+template <int CH, bool STORE = true>
 __global__ __launch_bounds__(256, 4) void prelu_pool_bwd_sg_k(const bf16_t* __restrict__ dp,
                                                            const bf16_t* __restrict__ z,
                                                            const float* __restrict__ alpha,
@@ -187,17 +189,21 @@ __global__ __launch_bounds__(256, 4) void prelu_pool_bwd_sg_k(const bf16_t* __re
         for (int q = 0; q < 4; ++q) ow[q][w] = pack_bf(ov[0][q], ov[1][q]);
       }
       const long nb = (long)n * HWC;
+      if constexpr (STORE) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        V o;
+        for (int q = 0; q < 4; ++q) {
+          V o;
 #pragma unroll
-        for (int w = 0; w < CH / 2; ++w) vset(o, w, ow[q][w]);
-        *(V*)(dz + nb + zoff(q)) = o;
+          for (int w = 0; w < CH / 2; ++w) vset(o, w, ow[q][w]);
+          *(V*)(dz + nb + zoff(q)) = o;
+        }
+      } else {
+        (void)ow;
       }
       gc = gn;
 #pragma unroll
       for (int q = 0; q < 4; ++q) zc[q] = zn[q];
-      if (lastw || lasth) {  // odd H / W: the row / column outside every window gets zero gradient
+      if (STORE && (lastw || lasth)) {  // odd H / W: the row / column outside every window gets zero gradient
         V zz;
 #pragma unroll
         for (int w = 0; w < CH / 2; ++w) vset(zz, w, 0u);
@@ -1075,8 +1081,12 @@ int ptg_prelu_pool_bwd2(const void* dp, const void* z, const float* alpha, void*
     nper = (N + chunks - 1) / chunks;
   }
   dim3 grid(bx, (N + nper - 1) / nper);
-  hipLaunchKernelGGL(prelu_pool_bwd_sg_k<4>, grid, dim3(256), 0, s, (const bf16_t*)dp, (const bf16_t*)z, alpha,
-                     (bf16_t*)dz, dalpha, dbias, N, H, W, C, nper);
+  if (dz)
+    hipLaunchKernelGGL(prelu_pool_bwd_sg_k<4>, grid, dim3(256), 0, s, (const bf16_t*)dp, (const bf16_t*)z, alpha,
+                       (bf16_t*)dz, dalpha, dbias, N, H, W, C, nper);
+  else  // dalpha / dbias only (dz == nullptr)
+    hipLaunchKernelGGL((prelu_pool_bwd_sg_k<4, false>), grid, dim3(256), 0, s, (const bf16_t*)dp, (const bf16_t*)z,
+                       alpha, (bf16_t*)nullptr, dalpha, dbias, N, H, W, C, nper);
   PTG_RETURN_LAUNCH();
 }
 

@@ -54,6 +54,11 @@ CONV1_FUSED = config.get("conv1_fused")
 # argmax: 3 bytes per pooled element) so the backward kernel needs no conv recompute and no argmax
 # search; PTG_CONV1_REC=0 runs the recomputing backward.
 CONV1_REC = config.get("conv1_rec")
+# PPB_DGRAD: a 5x5 conv over >= 32 channels whose input is the pooled output of a Conv + PReLU +
+# MaxPool block runs its dgrad with the EPI_PPB epilogue (conv.hip): besides dA it writes the
+# block's dZ, so the block's backward skips its PReLU/pool backward on the step's stream (that
+# kernel still runs, on the side stream and without stores, for dalpha / dbias, ahead of the wgrad).
+PPB_DGRAD = config.get("ppb_dgrad")
 
 
 def host_fp32(enabled: bool | None = None) -> bool:
@@ -253,6 +258,25 @@ class ConvOp(Op):
             return None
         return self.conv.kernel.bf16, self._wflip_buf(ws, self.conv.kernel.bf16.device)
 
+    def _ppb_block(self, dz):
+        """The Conv + PReLU + MaxPool op below this one when this op's dgrad can also produce that
+        block's dZ (EPI_PPB), else None."""
+        blk = getattr(self, "below", None)
+        if not (PPB_DGRAD and dz.is_cuda and isinstance(blk, ConvOp) and blk.prelu is not None
+                and blk.pool is not None and self.conv.kernel_size == (5, 5) and self.conv.out_shape[-1] >= 32
+                and self.conv.out_shape[-1] in (32, 64)):
+            return None
+        if getattr(blk, "_fused1", False) or getattr(blk, "_sel", False) or getattr(blk, "_sparse", True):
+            return None
+        z = getattr(blk, "_z", None)
+        N, H, W, _ = self._x.shape
+        cin = self.conv.cin_p
+        if z is None or tuple(z.shape) != (N, 2 * H, 2 * W, cin) or z.dtype != torch.bfloat16:
+            return None
+        if tuple(blk.prelu.alpha.data.shape) != tuple(z.shape[1:]) or cin % 8 or cin > 64:
+            return None
+        return blk
+
     def _backward_sel(self, x, dy, ws, dev):
         """First layer: sparse record -> dZ record -> weight gradient (no dense z / dZ, no dgrad)."""
         C = self._zshape[-1]
@@ -312,7 +336,15 @@ class ConvOp(Op):
         bias_g = self.conv.bias.grad if self.conv.bias is not None else \
             ws.get(self.name + "/nobias", (zshape[-1],), torch.float32, dev)
         z = self._z if not self._sparse else None
-        if self._sparse:
+        pre = getattr(self, "_dz_pre", None)
+        self._dz_pre = None
+        if pre is not None:
+            # dZ came from the dgrad epilogue of the op above (EPI_PPB); dalpha / dbias from the pooled
+            # gradient on the side stream, ordered before this layer's wgrad there
+            dz = pre
+            alpha_g = self.prelu.alpha.grad
+            S.launch(lambda: K.prelu_pool_bwd(dy, z, self.prelu.alpha.data, None, alpha_g, bias_g), dev)
+        elif self._sparse:
             if self.prelu is not None:
                 dalpha = self.prelu.alpha.grad
             else:
@@ -344,7 +376,14 @@ class ConvOp(Op):
         if self.stride != 1:
             raise NotImplementedError("dgrad for strided convolutions")
         dx = ws.get(self.name + "/dx", x.shape, torch.bfloat16, dev)
-        if halo_dgrad:
+        blk = self._ppb_block(dz) if halo_dgrad and self.pad == 2 else None
+        if blk is not None:
+            wf = self._wflip_buf(ws, dev)
+            dzb = ws.get(blk.name + "/dz", blk._z.shape, torch.bfloat16, dev)
+            K.conv2d_dgrad_halo_ppb(dz, self.conv.kernel.bf16, self.pad, dx, wf, blk._z, blk.prelu.alpha.data, dzb,
+                                    flipped=getattr(self, "_wf_ready", False))
+            blk._dz_pre = dzb
+        elif halo_dgrad:
             wf = self._wflip_buf(ws, dev)
             K.conv2d_dgrad_halo(dz, self.conv.kernel.bf16, self.pad, dx, wf,
                                 flipped=getattr(self, "_wf_ready", False))
@@ -583,6 +622,8 @@ def lower(layers: list) -> list:
             raise NotImplementedError(type(l).__name__)
     if ops:
         ops[0].first = True
+    for k in range(1, len(ops)):
+        ops[k].below = ops[k - 1]
     # ReLU-mask hand-off: a skinny Dense applies the previous relu-Dense's mask in its dX
     for k in range(1, len(ops)):
         cur, prev = ops[k], ops[k - 1]

@@ -113,7 +113,7 @@ def halo_eligible(C: int, Cout: int, KS: int, stride: int, same: bool) -> bool:
     return same and stride == 1 and KS in (3, 5) and C in HALO_C and Cout % 8 == 0 and Cout <= 64
 
 
-EPI = {None: 0, "pool": 1, "prelu": 2, "pools": 3}
+EPI = {None: 0, "pool": 1, "prelu": 2, "pools": 3, "ppb": 4}
 
 
 def conv2d_fwd_fused(x, w, bias, pad: int, z_out, alpha=None, aux_out=None, epi=None, arg_out=None):
@@ -397,6 +397,27 @@ def conv2d_dgrad_halo(dz, w, pad: int, out, wflip_buf, flipped: bool = False):
     return conv2d_fwd_fused(dz, wflip_buf, None, KS - 1 - pad, out)
 
 
+def conv2d_dgrad_halo_ppb(dz, w, pad: int, out, wflip_buf, z_blk, alpha_blk, dz_blk_out, flipped: bool = False):
+    """conv2d_dgrad_halo whose epilogue also back-propagates through the MaxPool(2x2) + PReLU of the
+    block below (conv.hip EPI_PPB): ``out`` = dA (the block's pooled gradient, [N,H,W,Cin]) and
+    ``dz_blk_out`` = dZ of the block ([N,2H,2W,Cin]) from its forward ``z_blk`` and per-element
+    ``alpha_blk`` ([2H,2W,Cin] fp32) - what prelu_pool_bwd(out, z_blk, alpha_blk, ...) writes as dz.
+    GPU only; 5x5 filters over >= 32 input channels."""
+    if not flipped:
+        conv_flip_weights(w, wflip_buf)
+    KS = w.shape[1]
+    N, H, W, C = dz.shape
+    Cout = wflip_buf.shape[0]
+    assert tuple(out.shape) == (N, H, W, Cout)
+    assert tuple(z_blk.shape) == (N, 2 * H, 2 * W, Cout) and tuple(dz_blk_out.shape) == tuple(z_blk.shape)
+    assert tuple(alpha_blk.shape) == (2 * H, 2 * W, Cout) and alpha_blk.dtype == torch.float32
+    for t, nm in ((dz, "dz"), (wflip_buf, "wflip"), (z_blk, "z_blk"), (dz_blk_out, "dz_blk")):
+        need(t, torch.bfloat16, "conv_ppb." + nm)
+    hip("ptg_conv2d_fwd_halo", ptr(dz), ptr(wflip_buf), None, ptr(alpha_blk.contiguous()), ptr(out), ptr(dz_blk_out),
+        ptr(z_blk), N, H, W, C, Cout, KS, KS - 1 - pad, EPI["ppb"])
+    return out
+
+
 # ----------------------------------------------------------------------------------------------
 # Dense (MFMA GEMM)
 # ----------------------------------------------------------------------------------------------
@@ -549,7 +570,7 @@ def prelu_pool_fwd(z, alpha, out):
 
 def prelu_pool_bwd(dp, z, alpha, dz_out, dalpha, dbias, nper: int = 0):
     """dz_out = d/dz of maxpool2x2(prelu(z)); dalpha, dbias accumulate (fp32).  ``nper``: samples
-    per workgroup (0 = auto)."""
+    per workgroup (0 = auto).  ``dz_out`` None: dalpha / dbias only (dz made by an EPI_PPB dgrad)."""
     if not on_device(z):
         return ref.prelu_pool_bwd(dp, z, alpha, dz_out, dalpha, dbias)
     N, H, W, C = z.shape

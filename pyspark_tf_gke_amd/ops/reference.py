@@ -129,7 +129,8 @@ def prelu_pool_bwd(dp, z, alpha, dz_out, dalpha, dbias):
     af = _f(alpha).detach().requires_grad_(True)
     p = F.max_pool2d(_prelu(zf, af).permute(0, 3, 1, 2), 2, 2).permute(0, 2, 3, 1)
     p.backward(_f(dp))
-    dz_out.copy_(zf.grad.to(dz_out.dtype))
+    if dz_out is not None:
+        dz_out.copy_(zf.grad.to(dz_out.dtype))
     dalpha.add_(af.grad)
     dbias.add_(zf.grad.sum((0, 1, 2)))
     return dz_out
