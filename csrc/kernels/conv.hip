@@ -303,7 +303,7 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
   // SMAJ (no halo ring, PReLU epilogue): tiles are ordered position-major, sample-minor, so the
   // consecutive tiles of a workgroup share one output position and the per-element PReLU alphas
   // (for CNN-B1 layer 2 16 KB per tile, more than its halo) stay in registers across samples
-  constexpr bool SMAJ = !RING && EPI != EPI_Z;
+  constexpr bool SMAJ = !RING && EPI != EPI_Z && EPI != EPI_PPB;
   // tile t -> (sample n, column strip twi, row tile th); divisions only for a range's first tile,
   // then the next tile is stepped incrementally (each runtime 32-bit division is ~40 scalar and
   // vector instructions, and the tile loop did six of them per tile)
@@ -328,7 +328,6 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
     }
   };
   float4 al[(EPI != EPI_Z && EPI != EPI_PPB) ? FM : 1][NF];
-  float4 alq[EPI == EPI_PPB ? FM : 1][NF][EPI == EPI_PPB ? 4 : 1];  // EPI_PPB: alpha at the 4 window pixels
   const bf16_t* __restrict__ zin = reinterpret_cast<const bf16_t*>(argout);  // EPI_PPB only
   __shared__ int s_wq;
   for (int round = 0;; ++round) {
@@ -369,22 +368,7 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
 
     // alpha for this lane's (pixel, 4 channels) of every fragment, needed after the MFMAs
     const int pos = twi * tiles_h + th;
-    if constexpr (EPI == EPI_PPB) {
-      if (pos != apos) {
-        apos = pos;
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int j = 0; j < NF; ++j) {
-            const int oh = oh0 + f_r[i], ow = ow0 + f_c[i], co0 = cb + j * 16 + g * 4;
-            const bool ok = co0 < Cout && oh < H && ow < W;
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-              alq[i][j][q] = ok ? *(const float4*)(alpha + ((long)(2 * oh + (q >> 1)) * (2 * W) + 2 * ow + (q & 1)) * Cout + co0)
-                                : make_float4(0.f, 0.f, 0.f, 0.f);
-          }
-      }
-    } else if constexpr (EPI != EPI_Z) {
+    if constexpr (EPI != EPI_Z && EPI != EPI_PPB) {
       if (pos != apos) {
         apos = pos;
 #pragma unroll
@@ -567,10 +551,17 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
         if constexpr (EPI == EPI_PPB) {
           if (in) {
             // zr = this pooled element's gradient (bf16-rounded, as prelu_pool_bwd_sg_k reads it)
+            // alpha of the 4 window pixels straight from L2 (shared by every sample; caching it in
+            // registers across a position-major tile order cost occupancy)
             const long W2 = 2L * W, zb = (((long)n * 2 * H + 2 * oh) * W2 + 2 * ow) * Cout + co0;
+            const long ab = ((long)(2 * oh) * W2 + 2 * ow) * Cout + co0;
             U2 zq[4];
+            float4 aq[4];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) zq[q] = *(const U2*)(zin + zb + ((q >> 1) * W2 + (q & 1)) * Cout);
+            for (int q = 0; q < 4; ++q) {
+              zq[q] = *(const U2*)(zin + zb + ((q >> 1) * W2 + (q & 1)) * Cout);
+              aq[q] = *(const float4*)(alpha + ab + ((q >> 1) * W2 + (q & 1)) * Cout);
+            }
             float ov[4][4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -579,7 +570,7 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
               for (int q = 0; q < 4; ++q) {
                 const uint32_t word = (r >> 1) ? zq[q].y : zq[q].x;
                 zv[q] = (r & 1) ? hi_bf(word) : lo_bf(word);
-                av[q] = r == 0 ? alq[i][j][q].x : r == 1 ? alq[i][j][q].y : r == 2 ? alq[i][j][q].z : alq[i][j][q].w;
+                av[q] = r == 0 ? aq[q].x : r == 1 ? aq[q].y : r == 2 ? aq[q].z : aq[q].w;
                 yv[q] = zv[q] > 0.f ? zv[q] : av[q] * zv[q];
               }
               int am = 0;

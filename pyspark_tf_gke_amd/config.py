@@ -67,9 +67,9 @@ _K = [
     Knob("sparse_first", bool, True, "PTG_SPARSE_FIRST", None, "first conv layer keeps a sparse pool record"),
     Knob("bn_fuse", bool, False, "PTG_BN_FUSE", None, "ResNet: the BN+ReLU of conv->conv links applied in the next conv's operand loaders (A/B: 8.04k vs 8.75k img/s)"),
     Knob("bn_epi_stats", bool, True, "PTG_BN_EPI_STATS", None, "ResNet: BN batch statistics from the conv GEMM epilogue (A/B: 9.00k vs 8.78k img/s with the shuffle flush)"),
-    Knob("ppb_dgrad", bool, True, "PTG_PPB_DGRAD", None,
+    Knob("ppb_dgrad", bool, False, "PTG_PPB_DGRAD", None,
          "CNN-B1 layers 3-5: the dgrad epilogue also writes the pooled block's dZ (conv.hip EPI_PPB); the "
-         "PReLU/pool backward moves to the side stream for dalpha/dbias only"),
+         "PReLU/pool backward moves to the side stream for dalpha/dbias only (A/B: 1.80-1.88 vs 1.65 ms, off)"),
     Knob("conv1_rec", bool, True, "PTG_CONV1_REC", None, "first conv layer (conv1.hip): forward keeps the pool record, backward needs no recompute (0: recompute z in the backward)"),
     Knob("conv1_fused", bool, True, "PTG_CONV1_FUSED", None, "first conv layer: pooled-only forward + one recomputing backward kernel (conv1.hip)"),
     Knob("blaslt_dx", bool, False, "PTG_BLASLT_DX", None, "A/B only: big-Dense dX through hipBLASLt instead of the skinny-M MFMA GEMM"),
