@@ -273,10 +273,28 @@ PTG_DEV void bf16_store8(bf16_t* p, float* v, int cnt, bool accum) {
 // into partial group (tile row % BN_G), the layout bn_finalize_k reads; the separate bn_stats pass
 // over z disappears.
 constexpr int EPI_BN_G = 64;  // == bn.hip BN_G
+// Backward form (bz != nullptr, with stats): the GEMM is the data gradient feeding a Conv -> BN -> ReLU
+// block whose forward z is bz ([M][ldc] bf16): each output is first masked by that block's ReLU,
+// g = (z*bsc + bsh > 0) ? v : 0 (no mask when bsc is null), stored as g, and the statistics are the
+// BN backward's sums - sum g and sum g*z per column, bn_bwd_reduce_k's partial layout - so that
+// reduction pass over dy and z disappears (graph_ops.ConvBNOp.bwd_bn_op).
 struct EpiBf16 {  // out[m*ldc+n] = act(acc + bias[n]) (+ out if accum) as bf16 (optionally also fp32)
   static constexpr bool VEC = true;
   static constexpr bool STATS = true;
   bf16_t* out; long ldc; const float* bias; int act; float* out32; int accum; float* stats = nullptr;
+  const bf16_t* bz = nullptr; const float* bsc = nullptr; const float* bsh = nullptr;
+  // backward form: mask v in place with the block's ReLU and return its z values in zz
+  PTG_DEV void bwd_prep(int m, int n, float* v, int cnt, float* zz) const {
+    const bf16_t* zp = bz + (long)m * ldc + n;
+    if (cnt == 8 && al16(zp)) {
+      unpack8(*(const U4*)zp, zz);
+    } else {
+      for (int j = 0; j < 8; ++j) zz[j] = j < cnt ? bf2f(zp[j]) : 0.f;
+    }
+    if (bsc) {
+      for (int j = 0; j < cnt; ++j) v[j] = fmaf(zz[j], bsc[n + j], bsh[n + j]) > 0.f ? v[j] : 0.f;
+    }
+  }
   PTG_DEV void operator()(int m, int n, float v) const {
     if (bias) v += bias[n];
     if (act == ACT_RELU) v = fmaxf(v, 0.f);
@@ -423,6 +441,15 @@ struct EpiAtomic {  // split-K: out[m*ldc+n] += acc  (device-scope fp32 atomic, 
 template <class E, class = void> struct EpiStats { static constexpr bool v = false; };
 template <class E> struct EpiStats<E, std::void_t<decltype(E::STATS)>> { static constexpr bool v = E::STATS; };
 
+// backward form: sums of the stored (bf16-rounded, masked) gradient g and of g*z
+PTG_DEV void stats_acc8_bwd(const float* v, const float* zz, int cnt, float* s, float* q) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float r = j < cnt ? bf2f(f2bf(v[j])) : 0.f;
+    s[j] += r;
+    q[j] = fmaf(r, zz[j], q[j]);
+  }
+}
 // per-thread column sums of the stored (bf16-rounded) values
 PTG_DEV void stats_acc8(const float* v, int cnt, float* s, float* q) {
 #pragma unroll
@@ -718,6 +745,15 @@ __global__ __launch_bounds__(256) void gemm_kernel(LA la, LB lb, EPI epi, int M,
     if (m >= M || n >= N) continue;
     const float4 a = *(const float4*)(cs + row * CP + c8 * 8), b = *(const float4*)(cs + row * CP + c8 * 8 + 4);
     float vals[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    if constexpr (EpiStats<EPI>::v) {
+      if (epi.stats && epi.bz) {
+        float zz[8];
+        epi.bwd_prep(m, n, vals, min(8, N - n), zz);
+        epi.vec8(m, n, vals, min(8, N - n));
+        stats_acc8_bwd(vals, zz, min(8, N - n), st_s, st_q);
+        continue;
+      }
+    }
     epi.vec8(m, n, vals, min(8, N - n));
     if constexpr (EpiStats<EPI>::v) {
       if (epi.stats) stats_acc8(vals, min(8, N - n), st_s, st_q);
@@ -871,9 +907,21 @@ __global__ __launch_bounds__(512) void gemm256_kernel(LA la, LB lb, EPI epi, int
         if (m < M && n < N) {
           const float4 a = *(const float4*)(cs + row * CP + c8 * 8), b = *(const float4*)(cs + row * CP + c8 * 8 + 4);
           float vals[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-          epi.vec8(m, n, vals, min(8, N - n));
+          bool done = false;
           if constexpr (EpiStats<EPI>::v) {
-            if (epi.stats) stats_acc8(vals, min(8, N - n), st_s, st_q);
+            if (epi.stats && epi.bz) {
+              float zz[8];
+              epi.bwd_prep(m, n, vals, min(8, N - n), zz);
+              epi.vec8(m, n, vals, min(8, N - n));
+              stats_acc8_bwd(vals, zz, min(8, N - n), st_s, st_q);
+              done = true;
+            }
+          }
+          if (!done) {
+            epi.vec8(m, n, vals, min(8, N - n));
+            if constexpr (EpiStats<EPI>::v) {
+              if (epi.stats) stats_acc8(vals, min(8, N - n), st_s, st_q);
+            }
           }
         }
       }
@@ -1097,6 +1145,34 @@ int ptg_conv2d_dgrad(const void* dz, const void* w, void* dx, int N, int H, int 
   lb.init();
   EpiBf16 epi{(bf16_t*)dx, Cin, nullptr, ACT_NONE, nullptr, accum};
   return dispatch_gemm(la, lb, epi, M, Cin, Kc2, 1, s);
+}
+
+// Data gradients feeding a Conv -> BN -> ReLU block (EpiBf16 backward form): dx = g (masked by the
+// block's ReLU via bsc / bsh, may be null), and stats ([64][2][Cin] fp32, accumulated into) += the
+// block's BN backward sums over (g, g*bz).  Stride 1, no accumulation, Cin < 4096.
+int ptg_conv2d_dgrad_bnstats(const void* dz, const void* w, void* dx, int N, int H, int W, int Cin, int Cout, int KH,
+                             int KW, int pad, float* stats, const void* bz, const float* bsc, const float* bsh,
+                             hipStream_t s) {
+  if (!is_pow2(Cout) || Cout < 8 || Cin % 8 || Cin >= 4096 || !stats || !bz) return (int)hipErrorInvalidValue;
+  const int M = N * H * W, Kc2 = KH * KW * Cout;
+  if (!fits((long)M * Cout * 2) || !fits((long)Kc2 * Cin * 2) || !fits((long)M * Cin * 2))
+    return (int)hipErrorInvalidValue;
+  ConvFwdA<8> la{(const bf16_t*)dz, H, W, Cout, ilog2(Cout), H, W, KW, 1, KH - 1 - pad, M, Kc2};
+  ConvDgradB lb{(const bf16_t*)w, Cin, Cout, ilog2(Cout), KH, KW, Kc2};
+  la.init();
+  lb.init();
+  EpiBf16 epi{(bf16_t*)dx, Cin, nullptr, ACT_NONE, nullptr, 0, stats, (const bf16_t*)bz, bsc, bsh};
+  return dispatch_gemm(la, lb, epi, M, Cin, Kc2, 1, s);
+}
+int ptg_conv1x1_dgrad_bnstats(const void* dz, const void* w, void* dx, int N, int H, int W, int Cin, int Cout,
+                              float* stats, const void* bz, const float* bsc, const float* bsh, hipStream_t s) {
+  if (Cin % 8 || Cout % 8 || Cin >= 4096 || !stats || !bz) return (int)hipErrorInvalidValue;
+  const int M = N * H * W;
+  if (!fits((long)M * Cout * 2) || !fits((long)M * Cin * 2)) return (int)hipErrorInvalidValue;
+  MatK<8> la{(const bf16_t*)dz, Cout, M, Cout, (uint32_t)matk_bytes(Cout, M, Cout)};
+  MatMN lb{(const bf16_t*)w, Cin, Cin, Cout, (uint32_t)matmn_bytes(Cin, Cin, Cout)};
+  EpiBf16 epi{(bf16_t*)dx, Cin, nullptr, ACT_NONE, nullptr, 0, stats, (const bf16_t*)bz, bsc, bsh};
+  return dispatch_gemm(la, lb, epi, M, Cin, Cout, 1, s);
 }
 
 // Data gradient of a 1x1 convolution with stride s (pad 0): dx[n][oh*s][ow*s][ci] (+)= sum_co

@@ -218,6 +218,7 @@ def _lower(nodes: list, input_idx: int) -> list:
         ops.append(G.Adapter(inner(layer), [src(ins[0])], k))
     if G.BN_FUSE:
         _fuse_bn_links(ops)
+    _bn_bwd_links(ops)
     # dense relu-mask hand-off as in the Sequential engine
     for a, b in zip(ops, ops[1:]):
         ia, ib = getattr(a, "inner", None), getattr(b, "inner", None)
@@ -249,6 +250,26 @@ def _fuse_bn_links(ops) -> None:
             continue
         pa.defer = True
         b.op.in_bn_op = pa
+
+
+def _bn_bwd_links(ops) -> None:
+    """Conv -> BN -> ReLU (no residual) feeding exactly one ConvBNOp: that consumer's dgrad epilogue
+    computes the producer's BN backward sums (graph_ops.BN_BWD_EPI)."""
+    uses: dict = {}
+    for op in ops:
+        for i in op.inputs:
+            uses.setdefault(i, []).append(op)
+    for a in ops:
+        pa = getattr(a, "op", None)
+        if not isinstance(pa, G.ConvBNOp) or not pa.relu or pa.residual:
+            continue
+        cons = uses.get(a.output, [])
+        if len(cons) != 1 or not isinstance(getattr(cons[0], "op", None), G.ConvBNOp):
+            continue
+        b = cons[0]
+        if b.inputs[0] != a.output or a.output in b.inputs[1:]:
+            continue
+        b.op.bwd_bn_op = pa
 
 
 class Model(Sequential):

@@ -105,6 +105,11 @@ HALO_KS = (5,)
 # apply pass and its y tensor disappear (gemm.hip BnLoad / EpiBf16 stats).
 BN_FUSE = config.get("bn_fuse")
 BN_EPI_STATS = config.get("bn_epi_stats")
+# Backward: a Conv -> BN -> ReLU block whose output feeds exactly one ConvBNOp gets its BN backward
+# sums (sum g, sum g*z) from the epilogue of that consumer's dgrad GEMM, which also applies the ReLU
+# mask to the gradient it stores (gemm.hip EpiBf16 backward form): the bn_bwd_reduce pass over dy and
+# z disappears.  PTG_BN_BWD_EPI_STATS=0 keeps the separate reduction.
+BN_BWD_EPI = config.get("bn_bwd_epi_stats")
 
 
 def _pow2(v):
@@ -219,14 +224,15 @@ class _BNState:
             return z
         return KB.bn_apply(z, scale, shift, res, relu, y)
 
-    def backward(self, dy, y, z, relu, dz, dres, ws):
+    def backward(self, dy, y, z, relu, dz, dres, ws, stats_done=False):
         bn = self.bn
         C = z.shape[-1]
         M = z.numel() // C
         part, scale, shift, mean, rstd, coef = self.bufs(ws, C, z.device)
         # no residual was added before the ReLU: its mask is z*scale+shift > 0, y need not be read
         sc, sh = (scale, shift) if (relu and dres is None) else (None, None)
-        KB.bn_bwd_reduce(dy, y, z, relu, part, sc, sh)
+        if not stats_done:  # else: the producing dgrad's epilogue summed (g, g*z) into part already
+            KB.bn_bwd_reduce(dy, y, z, relu, part, sc, sh)
         KB.bn_bwd_finalize(part, M, bn.gamma.data if bn.gamma is not None else None, mean, rstd,
                            bn.gamma.grad if bn.gamma is not None else None,
                            bn.beta.grad if bn.beta is not None else None, coef)
@@ -252,6 +258,10 @@ class ConvBNOp:
         # our single consumer's loaders; in_bn_op = the producer whose BN + ReLU we apply on load
         self.defer = False
         self.in_bn_op = None
+        # the Conv -> BN -> ReLU producer whose BN backward sums our dgrad epilogue computes (set by
+        # functional._bn_bwd_links); _bwd_stats_done marks a step in which it did
+        self.bwd_bn_op = None
+        self._bwd_stats_done = False
         if conv.activation not in ("linear", None):
             raise NotImplementedError("Conv2D(activation=...) followed by BatchNormalization")
 
@@ -303,7 +313,8 @@ class ConvBNOp:
         dy = _bf16(dy, ws, self.name + "/dy16")
         dz = ws.get(self.name + "/dz", z.shape, torch.bfloat16, dev)
         dres = ws.get(self.name + "/dres", z.shape, torch.bfloat16, dev) if self.residual else None
-        self.state.backward(dy, y, z, self.relu, dz, dres, ws)
+        done, self._bwd_stats_done = self._bwd_stats_done, False
+        self.state.backward(dy, y, z, self.relu, dz, dres, ws, stats_done=done)
         g = self.conv.kernel.grad
         in_bn = self._in_bn_t
         S.launch(lambda: conv_wgrad(x, dz, self.stride, self.pad, g, in_bn), dev)
@@ -315,6 +326,14 @@ class ConvBNOp:
                 dx = ex
             else:
                 dx = ws.get(self.name + "/dx", x.shape, torch.bfloat16, dev)
+                p = self.bwd_bn_op
+                if (p is not None and BN_BWD_EPI and self.stride == 1 and ex is None and p.relu and not p.residual
+                        and getattr(p, "_z", None) is not None and tuple(p._z.shape) == tuple(x.shape)):
+                    pc = p.conv.out_shape[-1]
+                    part, scale, shift = p.state.bufs(ws, pc, dev)[:3]
+                    if K.conv_dgrad_bnstats(dz, self.conv.kernel.bf16, self.pad, dx, part, p._z, scale, shift):
+                        p._bwd_stats_done = True
+                        return [dx] + ([dres] if self.residual else [])
                 conv_dgrad(dz, self.conv.kernel.bf16, self.stride, self.pad, dx, False, ws, self.name)
         return [dx] + ([dres] if self.residual else [])
 

@@ -64,6 +64,35 @@ def conv2d_dgrad(dz, w, pad: int, out, accumulate: bool = False):
     return out
 
 
+def conv_dgrad_bnstats(dz, w, pad: int, out, part, z_blk, scale=None, shift=None) -> bool:
+    """Stride-1 data gradient whose output feeds a Conv -> BN (-> ReLU) block (gemm.hip EpiBf16
+    backward form): ``out`` = the gradient masked by the block's ReLU (relu(z_blk*scale + shift) > 0;
+    no mask when ``scale`` is None) and ``part`` ([64, 2, Cin] fp32, accumulated into) += the block's BN
+    backward sums (sum g, sum g*z_blk), i.e. what bn_bwd_reduce would compute.  Returns False (nothing
+    launched) when the shape is not served by the fused GEMM paths."""
+    if not on_device(dz):
+        return False
+    N, H, W, Cout = dz.shape
+    Cw, KH, KW, Cin = w.shape
+    if (tuple(out.shape) != (N, H, W, Cin) or tuple(z_blk.shape) != tuple(out.shape) or Cin % 8 or Cin >= 4096
+            or Cw != Cout or part.dtype != torch.float32):
+        return False
+    for t in (dz, out, z_blk):
+        if t.dtype != torch.bfloat16 or not t.is_contiguous():
+            return False
+    sc, sh = (ptr(scale), ptr(shift)) if scale is not None else (None, None)
+    if KH == KW == 1 and pad == 0:
+        if Cout % 8:
+            return False
+        hip("ptg_conv1x1_dgrad_bnstats", ptr(dz), ptr(w), ptr(out), N, H, W, Cin, Cout, ptr(part), ptr(z_blk), sc, sh)
+        return True
+    if Cout < 8 or Cout & (Cout - 1):
+        return False
+    hip("ptg_conv2d_dgrad_bnstats", ptr(dz), ptr(w), ptr(out), N, H, W, Cin, Cout, KH, KW, pad, ptr(part),
+        ptr(z_blk), sc, sh)
+    return True
+
+
 def conv1x1_dgrad(dz, w, stride: int, out, accumulate: bool = False):
     """out[N,H,W,Cin] (+)= d/dx of a 1x1 convolution with stride ``stride`` (pad 0).  With
     stride > 1 and accumulate=False the off-lattice pixels are zeroed here."""

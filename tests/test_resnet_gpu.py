@@ -266,3 +266,46 @@ def test_resnet_bn_fusion_matches_unfused(monkeypatch):
         g1 = res[True][1][name]
         cos = float(torch.dot(g1.flatten(), g0.flatten()) / (g1.norm() * g0.norm() + 1e-20))
         assert cos > 0.99 and _rel(g1, g0) < 0.15, (name, cos, _rel(g1, g0))
+
+
+def test_resnet_bn_backward_epilogue_sums_match_reduce(monkeypatch):
+    """Small ResNet: the BN backward sums of every Conv -> BN -> ReLU -> Conv link come from the
+    consumer's dgrad epilogue (gemm.hip EpiBf16 backward form; no bn_bwd_reduce for that BN) and
+    give the separate-reduction plan's loss and gradients."""
+    from pyspark_tf_gke_amd.models.resnet import ResNet
+    from pyspark_tf_gke_amd.nn import graph_ops as G
+
+    x = torch.rand(16, 64, 64, 3)
+    y = torch.randint(0, 10, (16,))
+    res = {}
+    calls = {}
+    real = KB.bn_bwd_reduce
+
+    def counting(*a, **k):
+        calls[cur] = calls.get(cur, 0) + 1
+        return real(*a, **k)
+
+    monkeypatch.setattr(KB, "bn_bwd_reduce", counting)
+    for cur in (False, True):
+        monkeypatch.setattr(G, "BN_BWD_EPI", cur)
+        torch.manual_seed(0)
+        m = ResNet((2, 1), input_shape=(64, 64, 3), classes=10, width=16, device=DEV)
+        m.compile(optimizer=nn.optimizers.SGD(0.0), loss="sparse_categorical_crossentropy")
+        links = sum(1 for op in m.ops if getattr(getattr(op, "op", None), "bwd_bn_op", None) is not None)
+        assert links >= 6  # two per bottleneck (1x1 -> 3x3 -> 1x1), three bottlenecks
+        stats = m._stats_buf()
+        stats.zero_()
+        m.store.zero_grad()
+        xb, yb = m._prep_batch(x, y)
+        out = m._run_forward(xb, True)
+        m._run_backward(m._loss_grad(out, yb, stats))
+        torch.cuda.synchronize()
+        res[cur] = (m._logs_from(stats)["loss"], {p.name: p.grad.detach().float().cpu().clone() for p in m.store.params})
+    assert calls[False] - calls[True] == links  # one bn_bwd_reduce pass fewer per link
+    assert abs(res[True][0] - res[False][0]) < 1e-3 * max(1.0, abs(res[False][0]))
+    for name, g0 in res[False][1].items():
+        if name.endswith("_conv/bias"):  # ~0 in exact arithmetic (a per-channel shift before BN)
+            continue
+        g1 = res[True][1][name]
+        cos = float(torch.dot(g1.flatten(), g0.flatten()) / (g1.norm() * g0.norm() + 1e-20))
+        assert cos > 0.99 and _rel(g1, g0) < 0.1, (name, cos, _rel(g1, g0))
