@@ -338,19 +338,26 @@ PTG_DEV void gtable_add(double* tab, long cap, long slot, double rows, const dou
 }
 
 // LDS-first aggregation: each workgroup aggregates a contiguous chunk of rows into an LDS table
-// (LCAP slots), overflowing rows go straight to the global table; the LDS table is flushed with
-// one global update per distinct key per workgroup.  Low/moderate cardinality => global atomics
-// drop by the per-chunk reuse factor.
-#define LCAP 1024
+// (lcap slots, a power of two sized by the host to ~2x the expected keys: at 1K sparse keys the old
+// fixed 1024-slot table ran at load ~1, its probe chains hit the limit and rows spilled to global
+// atomics - 41.6 ms per 1B rows), overflowing rows go straight to the global table; the LDS table is
+// flushed with one global update per distinct key per workgroup.  Low/moderate cardinality =>
+// global atomics drop by the per-chunk reuse factor.  Dynamic LDS: keys i64[lcap], sums
+// f64[nv][lcap], rows u32[lcap], non-null counts u32[nv][lcap] (rows_per_block < 2^32).
 __global__ __launch_bounds__(256) void hash_agg_lds_k(const long long* __restrict__ keys, long n, AggIn in,
                                                       long long* __restrict__ gkeys, double* __restrict__ gtab,
-                                                      long gcap, long rows_per_block, int* __restrict__ overflow) {
-  __shared__ long long lk[LCAP];
-  __shared__ double lrows[LCAP];
-  __shared__ double lacc[AGG_MAXV][2][LCAP];  // sum, cnt (min/max go global-direct)
-  for (int t = threadIdx.x; t < LCAP; t += 256) {
+                                                      long gcap, long rows_per_block, int* __restrict__ overflow,
+                                                      int lcap) {
+  extern __shared__ __align__(16) unsigned char lds_raw[];
+  const int nvl = in.nv;
+  long long* lk = (long long*)lds_raw;
+  double* lsum = (double*)(lk + lcap);                    // [nv][lcap]
+  unsigned int* lrows = (unsigned int*)(lsum + (long)nvl * lcap);
+  unsigned int* lcnt = lrows + lcap;                      // [nv][lcap]
+  const int lmask = lcap - 1;
+  for (int t = threadIdx.x; t < lcap; t += 256) {
     lk[t] = EMPTY_KEY; lrows[t] = 0;
-    for (int j = 0; j < AGG_MAXV; ++j) { lacc[j][0][t] = 0; lacc[j][1][t] = 0; }
+    for (int j = 0; j < nvl; ++j) { lsum[j * lcap + t] = 0.0; lcnt[j * lcap + t] = 0; }
   }
   __syncthreads();
   const long r0 = (long)blockIdx.x * rows_per_block, r1 = min(n, r0 + rows_per_block);
@@ -366,7 +373,7 @@ __global__ __launch_bounds__(256) void hash_agg_lds_k(const long long* __restric
     }
   };
   auto add_row = [&](long long key, const double* s, const double* c) {
-    int h = (int)(mix64((unsigned long long)key) & (LCAP - 1));
+    int h = (int)(mix64((unsigned long long)key) & (unsigned long long)lmask);
     int slot = -1;
     for (int probe = 0; probe < 32; ++probe) {
       const long long cur = lk[h];
@@ -376,12 +383,12 @@ __global__ __launch_bounds__(256) void hash_agg_lds_k(const long long* __restric
                                                     (unsigned long long)key);
         if (prev == EMPTY_KEY || prev == key) { slot = h; break; }
       }
-      h = (h + 1) & (LCAP - 1);
+      h = (h + 1) & lmask;
     }
     if (slot >= 0) {
-      atomicAdd(&lrows[slot], 1.0);
-      for (int j = 0; j < in.nv; ++j) {
-        if (c[j] > 0) { atomicAdd(&lacc[j][0][slot], s[j]); atomicAdd(&lacc[j][1][slot], 1.0); }
+      atomicAdd(&lrows[slot], 1u);
+      for (int j = 0; j < nvl; ++j) {
+        if (c[j] > 0) { atomicAdd(&lsum[j * lcap + slot], s[j]); atomicAdd(&lcnt[j * lcap + slot], 1u); }
       }
     }
     if (slot < 0 || need_minmax) {
@@ -417,15 +424,18 @@ __global__ __launch_bounds__(256) void hash_agg_lds_k(const long long* __restric
     add_row(key, s1, c1);
   }
   __syncthreads();
-  for (int t = threadIdx.x; t < LCAP; t += 256) {
+  for (int t = threadIdx.x; t < lcap; t += 256) {
     const long long key = lk[t];
     if (key == EMPTY_KEY) continue;
     const long gs = gtable_slot(gkeys, gcap, key);
     if (gs < 0) { atomicAdd(overflow, 1); continue; }
-    atomicAdd(&gtab[gs], lrows[t]);
-    for (int j = 0; j < in.nv; ++j) {
+    atomicAdd(&gtab[gs], (double)lrows[t]);
+    for (int j = 0; j < nvl; ++j) {
       double* base = gtab + gcap * (1 + 4 * j);
-      if (lacc[j][1][t] > 0) { atomicAdd(&base[gs], lacc[j][0][t]); atomicAdd(&base[gcap + gs], lacc[j][1][t]); }
+      if (lcnt[j * lcap + t] > 0) {
+        atomicAdd(&base[gs], lsum[j * lcap + t]);
+        atomicAdd(&base[gcap + gs], (double)lcnt[j * lcap + t]);
+      }
     }
   }
 }
@@ -1770,9 +1780,19 @@ int ptg_hash_table_init(void* keys, void* tab, long cap, int nv, hipStream_t s) 
 }
 
 // vals/valids/types: host arrays of nv entries (device pointers inside)
+// est_keys: expected distinct keys (sizes the per-workgroup LDS table: ~2x, 1024..budget slots)
 int ptg_hash_agg(const void* keys, long n, const void* const* vals, const void* const* valids, const int* types,
-                 int nv, int minmax, void* gkeys, void* gtab, long gcap, void* overflow, hipStream_t s) {
-  if (nv > AGG_MAXV) return (int)hipErrorInvalidValue;
+                 int nv, int minmax, void* gkeys, void* gtab, long gcap, void* overflow, long est_keys,
+                 hipStream_t s) {
+  if (nv > AGG_MAXV || nv < 0) return (int)hipErrorInvalidValue;
+  const size_t per_slot = 12 + 12 * (size_t)nv;
+  int lcap = 1024;
+  while ((long)lcap < 2 * est_keys && (size_t)lcap * 2 * per_slot <= 64 * 1024) lcap *= 2;  // >= 2 workgroups/CU
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)hash_agg_lds_k, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+    attr = true;
+  }
   AggIn in;
   for (int j = 0; j < AGG_MAXV; ++j) {
     in.vals[j] = j < nv ? vals[j] : nullptr;
@@ -1785,8 +1805,8 @@ int ptg_hash_agg(const void* keys, long n, const void* const* vals, const void* 
   long nb = (n + rpb - 1) / rpb;
   if (nb < 512) { rpb = (n + 511) / 512; if (rpb < 256) rpb = 256; nb = (n + rpb - 1) / rpb; }
   if (nb < 1) nb = 1;
-  hipLaunchKernelGGL(hash_agg_lds_k, dim3((unsigned)nb), dim3(256), 0, s, (const long long*)keys, n, in,
-                     (long long*)gkeys, (double*)gtab, gcap, rpb, (int*)overflow);
+  hipLaunchKernelGGL(hash_agg_lds_k, dim3((unsigned)nb), dim3(256), (size_t)lcap * per_slot, s,
+                     (const long long*)keys, n, in, (long long*)gkeys, (double*)gtab, gcap, rpb, (int*)overflow, lcap);
   PTG_RETURN_LAUNCH();
 }
 

@@ -229,9 +229,11 @@ def _small_range_agg(keys, vals, valids):
     return _dense_extract(prow, psum, None, G, nv, W, lo, keys.device)
 
 
-def hash_agg(keys: torch.Tensor, vals: list, valids: list, want_minmax: bool = False, cap_hint: int | None = None):
+def hash_agg(keys: torch.Tensor, vals: list, valids: list, want_minmax: bool = False, cap_hint: int | None = None,
+             est_keys: int | None = None):
     """groupBy(key).agg over int64 keys.  Returns (keys[m], rows[m], [(sum, cnt, min, max)] per value column)
-    as tensors on the keys' device."""
+    as tensors on the keys' device.  ``est_keys`` (expected distinct keys) sizes the per-workgroup LDS
+    tables of hash_agg_lds_k."""
     nv = len(vals)
     n = keys.numel()
     if not on_device(keys):
@@ -264,10 +266,10 @@ def hash_agg(keys: torch.Tensor, vals: list, valids: list, want_minmax: bool = F
     vvals = (ctypes.c_void_p * 4)(*[(vd.data_ptr() if vd is not None else 0) for vd in valids])
     types = (ctypes.c_int * 4)(*[TORCH_CT[v.dtype] for v in vals])
     hip("ptg_hash_agg", ptr(keys), n, ctypes.addressof(vptrs), ctypes.addressof(vvals), ctypes.addressof(types), nv,
-        int(want_minmax), ptr(gkeys), ptr(gtab), cap, ptr(overflow))
+        int(want_minmax), ptr(gkeys), ptr(gtab), cap, ptr(overflow), int(est_keys or cap_hint or 512))
     if int(overflow.item()):
         # table too small for the key cardinality: retry with a larger table
-        return hash_agg(keys, vals, valids, want_minmax, cap_hint=cap * 2)
+        return hash_agg(keys, vals, valids, want_minmax, cap_hint=cap * 2, est_keys=est_keys)
     return _extract(gkeys, gtab, cap, nv)
 
 

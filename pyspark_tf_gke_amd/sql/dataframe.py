@@ -1230,6 +1230,9 @@ def _hash_agg_all(key, vals, valids, want_minmax):
         if est > _RADIX_MIN_KEYS:
             def fn(k, v, vd, mm):
                 return D.hash_agg_radix(k, v, vd, mm, ws=_PART_WS, est_keys=est)
+        else:
+            def fn(k, v, vd, mm):
+                return D.hash_agg(k, v, vd, mm, est_keys=est)
     if len(vals) <= 4:
         return fn(key, vals, valids, want_minmax)
     uk = rows = None
