@@ -736,6 +736,43 @@ __global__ __launch_bounds__(256) void gemm_kernel(LA la, LB lb, EPI epi, int M,
   float st_s[8], st_q[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) { st_s[j] = 0.f; st_q[j] = 0.f; }
+  if constexpr (EpiStats<EPI>::v && NV % 256 == 0 && 256 % (BN / 8) == 0) {
+    if (epi.stats && epi.bz) {
+      // backward BN form: every z vector of this thread's NV/256 output groups is loaded up front
+      // (independent 16-B loads in flight instead of one exposed load per group), and the block's
+      // ReLU coefficients once (this thread's column group is fixed), then mask, store, sum
+      constexpr int NIT = NV / 256;
+      const int c8 = tid % (BN / 8), n = n0 + c8 * 8;
+      U4 zv[NIT];
+#pragma unroll
+      for (int u = 0; u < NIT; ++u) {
+        const int m = m0 + (u * 256 + tid) / (BN / 8);
+        zv[u] = (m < M && n + 8 <= N) ? *(const U4*)(epi.bz + (long)m * epi.ldc + n) : zero4();
+      }
+      float sc[8], sh[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { sc[j] = 0.f; sh[j] = 1.f; }
+      if (epi.bsc && n + 8 <= N) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { sc[j] = epi.bsc[n + j]; sh[j] = epi.bsh[n + j]; }
+      }
+#pragma unroll
+      for (int u = 0; u < NIT; ++u) {
+        const int row = (u * 256 + tid) / (BN / 8), m = m0 + row;
+        if (m >= M || n >= N) continue;
+        const float4 a = *(const float4*)(cs + row * CP + c8 * 8), b = *(const float4*)(cs + row * CP + c8 * 8 + 4);
+        float vals[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        float zz[8];
+        unpack8(zv[u], zz);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) vals[j] = fmaf(zz[j], sc[j], sh[j]) > 0.f ? vals[j] : 0.f;
+        epi.vec8(m, n, vals, min(8, N - n));
+        stats_acc8_bwd(vals, zz, min(8, N - n), st_s, st_q);
+      }
+      stats_flush<BN, 256>(epi.stats, N, tm, n0, st_s, st_q, cs);
+      return;
+    }
+  }
 #pragma unroll
   for (int v0 = 0; v0 < NV; v0 += 256) {
     const int v = v0 + tid;
