@@ -60,6 +60,8 @@ _K = [
     Knob("defer_dense_update", bool, False, "PTG_DEFER_DENSE_UPDATE", None,
          "inside fit()/bench step loops: the big Dense dW+Adam GEMM runs under the next step's conv forward "
          "instead of under this step's backward (A/B on CNN-B1 b256: 1.70-1.71 vs 1.65-1.66 ms, so off)"),
+    Knob("dense_adam_after", int, 0, "PTG_DENSE_ADAM_AFTER", None,
+         "CNN-B1: fork the Dense dW+Adam GEMM after the k-th conv op's backward (0 = right after the Dense dX)"),
     Knob("fused_head", bool, True, "PTG_FUSED_HEAD", None, "CNN-B1 Dense(relu)->Dense->MSE head as two kernels"),
     Knob("device_feed", bool, True, "PTG_DEVICE_FEED", None, "fit(): pinned ring + side-stream H2D for host datasets"),
     Knob("side_stream", bool, True, "PTG_SIDE_STREAM", None, "weight gradients on a side HIP stream (1 replica)"),

@@ -45,6 +45,9 @@ FUSED_HEAD = config.get("fused_head")
 # that overwrites the GEMM's input (and so before the Dense forward reads the updated weights):
 # the same arithmetic in the same order, only the overlap partner changes.
 DEFER_DENSE = config.get("defer_dense_update")
+# Within the backward: the big Dense dW+Adam GEMM is forked onto the side stream after the backward
+# of the k-th conv op from the top (0 = as soon as its inputs exist, right after the Dense dX)
+DENSE_ADAM_AFTER = config.get("dense_adam_after")
 
 
 def default_device() -> torch.device:
@@ -392,7 +395,9 @@ class Sequential:
         K.head_mse(acc, d1.dense.bias.data, d2.dense.kernel.data, d2.dense.bias.data, yb.contiguous(), dz1,
                    d2.dense.kernel.grad, d2.dense.bias.grad, d1.dense.bias.grad, stats, scratch=scratch)
         hook = st.on_op_grads_ready if st is not None else None
-        fused = self._begin_fused_update(st, defer=self._defer_active(acc))
+        defer = self._defer_active(acc)
+        late = 0 if defer else DENSE_ADAM_AFTER
+        fused = self._begin_fused_update(st, defer=defer or (late > 0 and acc.is_cuda))
         try:
             with S.active(S.for_step(self.store, st)):
                 if hook is not None:
@@ -400,8 +405,23 @@ class Sequential:
                 dx = d1.backward_dz(dz1, self.ws)
                 if hook is not None:
                     hook(self, d1)
-                E.run_backward(self.ops[:-2], dx, self.ws,
-                               on_op_done=(lambda op: hook(self, op)) if hook is not None else None)
+                done_ops = [0]
+
+                def on_done(op):
+                    if hook is not None:
+                        hook(self, op)
+                    if fused is not None and late > 0 and fused.deferred and isinstance(op, E.ConvOp):
+                        done_ops[0] += 1
+                        if done_ops[0] == late:  # fork the Dense dW+Adam GEMM under the lower layers
+                            for fn in fused.deferred:
+                                S.launch(fn, acc.device)
+                            fused.deferred.clear()
+
+                E.run_backward(self.ops[:-2], dx, self.ws, on_op_done=on_done)
+                if fused is not None and late > 0 and fused.deferred:  # fewer conv ops than `late`
+                    for fn in fused.deferred:
+                        S.launch(fn, acc.device)
+                    fused.deferred.clear()
         finally:
             for op in getattr(self, "_fusable_ops", []):
                 op.fused_update = None
