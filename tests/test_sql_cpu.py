@@ -421,3 +421,17 @@ def test_repartition_makes_local_partitions_and_write_tasks(spark, tmp_path):
     c = r.coalesce(2)
     assert len(c.local_partition_sizes()) == 2 and sum(c.local_partition_sizes()) == 3000
     assert len(df.repartition(5).local_partition_sizes()) == 5
+
+
+def test_hash9_table_sizing():
+    """Planner side of the 512-way hash groupBy (ops/df.py): the LDS table holds the fullest of the
+    512 partitions at load <= 0.7 within 150 KB, and declines key counts it cannot hold."""
+    from pyspark_tf_gke_amd.ops import df as D
+
+    assert D._h9_table_slots(1_000_000, 1) == 4096          # ~1953 keys / partition -> 4096 slots
+    assert D._h9_table_slots(65_536, 1) == 1024              # minimum table
+    assert D._h9_table_slots(1_000_000, 2) == 4096           # 36 B/slot -> 144 KB
+    assert D._h9_table_slots(2_000_000, 1) is None           # 8192 x 24 B > 150 KB
+    for k, nv in ((70_000, 0), (300_000, 1), (900_000, 2)):
+        ts = D._h9_table_slots(k, nv)
+        assert ts & (ts - 1) == 0 and k / D.H9_BINS * 1.15 <= 0.7 * ts and ts * (12 + 12 * nv) <= 150 * 1024
