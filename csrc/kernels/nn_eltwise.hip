@@ -462,6 +462,7 @@ __global__ __launch_bounds__(256) void prelu_fwd_k(const bf16_t* __restrict__ z,
 // 16 8-element positions over a batch chunk split into 16 sample groups and reduces dalpha over the
 // groups in LDS - one dalpha add per element and chunk instead of one fp32 atomic per element and
 // sample pair (the rejected per-pair variant: 2.6M contended atomics for CNN-B1's last conv layer at batch 256).
+template <bool STORE = true>  // false: dalpha / dbias only (dz made by the Dense dX epilogue, gemm.hip out2)
 __global__ __launch_bounds__(256) void prelu_bwd_sg_k(const bf16_t* __restrict__ da, const bf16_t* __restrict__ z,
                                                       const float* __restrict__ alpha, bf16_t* __restrict__ dz,
                                                       float* __restrict__ dalpha, float* __restrict__ dbias, int N,
@@ -503,7 +504,7 @@ __global__ __launch_bounds__(256) void prelu_bwd_sg_k(const bf16_t* __restrict__
           dal[j] += pos ? 0.f : g[j] * zv[j];
           db[j] += o[j];
         }
-        *(U4*)(dz + (long)(n + u * SG) * HWC + e) = pack8(o);
+        if constexpr (STORE) *(U4*)(dz + (long)(n + u * SG) * HWC + e) = pack8(o);
       }
     }
   }
@@ -1141,8 +1142,12 @@ int ptg_prelu_bwd2(const void* da, const void* z, const float* alpha, void* dz, 
     nper = (N + chunks - 1) / chunks;
   }
   dim3 grid(bx, (N + nper - 1) / nper);
-  hipLaunchKernelGGL(prelu_bwd_sg_k, grid, dim3(256), 0, s, (const bf16_t*)da, (const bf16_t*)z, alpha,
-                     (bf16_t*)dz, dalpha, dbias, N, HWC, C, nper);
+  if (dz)
+    hipLaunchKernelGGL(prelu_bwd_sg_k<true>, grid, dim3(256), 0, s, (const bf16_t*)da, (const bf16_t*)z, alpha,
+                       (bf16_t*)dz, dalpha, dbias, N, HWC, C, nper);
+  else  // dalpha / dbias only
+    hipLaunchKernelGGL(prelu_bwd_sg_k<false>, grid, dim3(256), 0, s, (const bf16_t*)da, (const bf16_t*)z, alpha,
+                       (bf16_t*)nullptr, dalpha, dbias, N, HWC, C, nper);
   PTG_RETURN_LAUNCH();
 }
 

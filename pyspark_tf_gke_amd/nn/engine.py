@@ -59,6 +59,9 @@ CONV1_REC = config.get("conv1_rec")
 # block's dZ, so the block's backward skips its PReLU/pool backward on the step's stream (that
 # kernel still runs, on the side stream and without stores, for dalpha / dbias, ahead of the wgrad).
 PPB_DGRAD = config.get("ppb_dgrad")
+# DENSE_PRELU_DX: a big Dense fed (through Flatten) by a Conv + PReLU block (CNN-B1's last conv) writes
+# that block's dZ in its dX epilogue; the block's prelu_bwd then runs store-less on the side stream
+DENSE_PRELU_DX = config.get("dense_prelu_dx")
 
 
 def host_fp32(enabled: bool | None = None) -> bool:
@@ -343,7 +346,10 @@ class ConvOp(Op):
             # gradient on the side stream, ordered before this layer's wgrad there
             dz = pre
             alpha_g = self.prelu.alpha.grad
-            S.launch(lambda: K.prelu_pool_bwd(dy, z, self.prelu.alpha.data, None, alpha_g, bias_g), dev)
+            if self.pool is not None:
+                S.launch(lambda: K.prelu_pool_bwd(dy, z, self.prelu.alpha.data, None, alpha_g, bias_g), dev)
+            else:
+                S.launch(lambda: K.prelu_bwd(dy, z, self.prelu.alpha.data, None, alpha_g, bias_g), dev)
         elif self._sparse:
             if self.prelu is not None:
                 dalpha = self.prelu.alpha.grad
@@ -441,12 +447,37 @@ class DenseOp(Op):
         self._x = x
         return acc
 
+    def _prelu_block(self, dz):
+        """The Conv + PReLU (no pool) op feeding this Dense through Flatten, when the dX epilogue can
+        write its dZ (DENSE_PRELU_DX), else None."""
+        fl = getattr(self, "below", None)
+        blk = getattr(fl, "below", None)
+        if not (DENSE_PRELU_DX and dz.is_cuda and self.big and isinstance(fl, FlattenOp) and isinstance(blk, ConvOp)
+                and blk.prelu is not None and blk.pool is None and not blk.first):
+            return None
+        if getattr(blk, "_fused1", False) or getattr(blk, "_sel", False) or getattr(blk, "_sparse", True):
+            return None
+        z = getattr(blk, "_z", None)
+        B = self._x.shape[0]
+        if (z is None or z.dtype != torch.bfloat16 or z.shape[0] != B or z[0].numel() != self.dense.fan_in
+                or tuple(blk.prelu.alpha.data.shape) != tuple(z.shape[1:])):
+            return None
+        return blk
+
     def backward_dz(self, dz, ws):
         """Big Dense backward from the pre-activation gradient dz (bias gradient already summed):
         dX (unless first) then dW, or Adam fused into the dW GEMM."""
         x = self._x
         dx = None
-        if not self.first:
+        blk = None if self.first else self._prelu_block(dz)
+        if blk is not None:
+            dx = ws.get(self.name + "/dx", x.shape, torch.bfloat16, x.device)
+            dzb = ws.get(blk.name + "/dz", blk._z.shape, torch.bfloat16, x.device)
+            B = x.shape[0]
+            K.linear_dx_prelu(dz, self.dense.kernel.bf16, dx, dzb.view(B, -1), blk._z.view(B, -1),
+                              blk.prelu.alpha.data.view(-1))
+            blk._dz_pre = dzb
+        elif not self.first:
             dx = ws.get(self.name + "/dx", x.shape, torch.bfloat16, x.device)
             K.linear_dx(dz, self.dense.kernel.bf16, dx)
         fused = self.fused_update

@@ -501,6 +501,20 @@ def linear_dx(dy, w, out):
     return out
 
 
+def linear_dx_prelu(dy, w, out, out_dz, z, alpha):
+    """linear_dx plus out_dz = out * prelu'(z) with per-column ``alpha`` (gemm.hip EpiBf16 out2): the
+    Dense dX hands the PReLU conv block below it (through Flatten) its dZ.  GPU only; ``z`` / ``out_dz``
+    [M, K] bf16 views of the block's z / dz, ``alpha`` [K] fp32."""
+    M, N = dy.shape
+    K = w.shape[1]
+    assert tuple(out.shape) == (M, K) and tuple(out_dz.shape) == (M, K) and tuple(z.shape) == (M, K)
+    assert alpha.numel() == K and alpha.dtype == torch.float32
+    for t, nm in ((dy, "dy"), (w, "w"), (out, "out"), (out_dz, "out_dz"), (z, "z")):
+        need(t, torch.bfloat16, "linear_dx_prelu." + nm)
+    hip("ptg_linear_dx_prelu", M, N, K, ptr(dy), ptr(w), ptr(out), ptr(out_dz), ptr(z), ptr(alpha.contiguous()))
+    return out
+
+
 def linear_dw(dy, x, out, accumulate: bool = False):
     """out[N,K] fp32 (+)= dy[M,N]^T @ x[M,K]."""
     if not on_device(dy):
@@ -646,6 +660,7 @@ def prelu_bwd(da, z, alpha, dz_out, dalpha, dbias, nper: int = 0):
         return ref.prelu_bwd(da, z, alpha, dz_out, dalpha, dbias)
     N = z.shape[0]
     C = z.shape[-1]
+    # dz_out None: dalpha / dbias only (dz made by linear_dx_prelu)
     hip("ptg_prelu_bwd2", ptr(da), ptr(z), ptr(alpha), ptr(dz_out),
         ptr(dalpha), ptr(dbias), N, z[0].numel(), C, nper)
     return dz_out

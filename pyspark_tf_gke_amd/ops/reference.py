@@ -260,7 +260,8 @@ def prelu_fwd(z, alpha, out):
 def prelu_bwd(da, z, alpha, dz_out, dalpha, dbias):
     zf, af, g = _f(z), _f(alpha), _f(da)
     dz = torch.where(zf > 0, g, g * af)
-    dz_out.copy_(dz.to(dz_out.dtype))
+    if dz_out is not None:
+        dz_out.copy_(dz.to(dz_out.dtype))
     dalpha.add_(torch.where(zf > 0, torch.zeros_like(g), g * zf).sum(0))
     dbias.add_(dz.reshape(-1, dz.shape[-1]).sum(0))
     return dz_out

@@ -773,3 +773,74 @@ def test_ppb_dgrad_model_step_matches_two_kernel_path(hip_built):
     d = (m1.store.flat - m0.store.flat).norm().item()
     u = (m0.store.flat - init).norm().item()
     assert d <= 0.05 * u, (d, u)
+
+
+def test_linear_dx_prelu_matches_two_kernels(hip_built):
+    """gemm.hip EpiBf16 out2: the Dense dX also writes the PReLU block's dZ; equal bit for bit to
+    linear_dx + prelu_bwd_sg_k, and the store-less prelu_bwd gives the same dalpha / dbias."""
+    torch.manual_seed(3)
+    B, N, Kd, C = 64, 256, 16 * 20 * 64, 64
+    dy = (torch.randn(B, N) * 0.1).to(torch.bfloat16).cuda()
+    w = (torch.randn(N, Kd) * 0.02).to(torch.bfloat16).cuda()
+    z = torch.randn(B, 16, 20, C).to(torch.bfloat16).cuda()
+    alpha = (torch.rand(16, 20, C) * 0.5 - 0.1).cuda()
+    da_ref = torch.empty(B, Kd, dtype=torch.bfloat16, device="cuda")
+    K.linear_dx(dy, w, da_ref)
+    dz_ref = torch.empty_like(z)
+    dal_ref = torch.zeros_like(alpha)
+    db_ref = torch.zeros(C, device="cuda")
+    K.prelu_bwd(da_ref.view(B, 16, 20, C), z, alpha, dz_ref, dal_ref, db_ref)
+    da = torch.empty_like(da_ref)
+    dz = torch.full_like(z, 5.0)
+    K.linear_dx_prelu(dy, w, da, dz.view(B, -1), z.view(B, -1), alpha.view(-1))
+    torch.cuda.synchronize()
+    assert torch.equal(da, da_ref) and torch.equal(dz, dz_ref)
+    dal, db = torch.zeros_like(dal_ref), torch.zeros_like(db_ref)
+    K.prelu_bwd(da.view(B, 16, 20, C), z, alpha, None, dal, db)
+    assert torch.allclose(dal, dal_ref, rtol=1e-5, atol=1e-6) and torch.allclose(db, db_ref, rtol=1e-5, atol=1e-5)
+
+
+def test_dense_prelu_dx_model_step_matches(hip_built):
+    """CNN-B1-shaped model with DENSE_PRELU_DX: conv5's dZ comes from the Dense dX epilogue (one
+    call per step) and training matches the separate prelu_bwd path."""
+    from pyspark_tf_gke_amd.models import build_cnn_model
+    from pyspark_tf_gke_amd.nn import engine as E
+
+    torch.manual_seed(0)
+    xs = [torch.randint(0, 256, (32, 128, 160, 3), dtype=torch.uint8, device="cuda") for _ in range(2)]
+    ys = [torch.rand(32, 2, device="cuda") * 100 for _ in range(2)]
+    calls = [0]
+    real = E.K.linear_dx_prelu
+
+    def counting(*a, **k):
+        calls[0] += 1
+        return real(*a, **k)
+
+    def run(on):
+        old = E.DENSE_PRELU_DX
+        E.DENSE_PRELU_DX = on
+        E.K.linear_dx_prelu = counting
+        try:
+            torch.manual_seed(1)
+            m = build_cnn_model((128, 160, 3), flat=True, summary=False, device="cuda")
+            init = m.store.flat.clone()
+            st = m._stats_buf()
+            losses = []
+            for i in range(5):
+                st.zero_()
+                m.train_step_fast(xs[i % 2], ys[i % 2], st)
+                losses.append(m._logs_from(st)["loss"])
+            torch.cuda.synchronize()
+            return m, losses, init
+        finally:
+            E.DENSE_PRELU_DX = old
+            E.K.linear_dx_prelu = real
+
+    m0, l0, init = run(False)
+    assert calls[0] == 0
+    m1, l1, _ = run(True)
+    assert calls[0] == 5
+    np.testing.assert_allclose(l1, l0, rtol=2e-3)
+    d = (m1.store.flat - m0.store.flat).norm().item()
+    u = (m0.store.flat - init).norm().item()
+    assert d <= 0.05 * u, (d, u)
