@@ -71,8 +71,9 @@ _K = [
     Knob("bn_bwd_epi_stats", bool, True, "PTG_BN_BWD_EPI_STATS", None,
          "ResNet: the BN backward sums of a Conv->BN->ReLU block come from the epilogue of the dgrad that produces its gradient (no bn_bwd_reduce pass)"),
     Knob("bn_epi_stats", bool, True, "PTG_BN_EPI_STATS", None, "ResNet: BN batch statistics from the conv GEMM epilogue (A/B: 9.00k vs 8.78k img/s with the shuffle flush)"),
-    Knob("dense_prelu_dx", bool, True, "PTG_DENSE_PRELU_DX", None,
-         "CNN-B1: the Dense dX epilogue also writes the PReLU conv block's dZ (prelu_bwd runs store-less on the side stream)"),
+    Knob("dense_prelu_dx", bool, False, "PTG_DENSE_PRELU_DX", None,
+         "CNN-B1: the Dense dX epilogue also writes the PReLU conv block's dZ (prelu_bwd runs store-less on the side stream; "
+         "A/B 1.72 vs 1.70 ms: the conv5 dgrad then meets the Adam GEMM and the side-stream reduction, off)"),
     Knob("ppb_dgrad", bool, False, "PTG_PPB_DGRAD", None,
          "CNN-B1 layers 3-5: the dgrad epilogue also writes the pooled block's dZ (conv.hip EPI_PPB); the "
          "PReLU/pool backward moves to the side stream for dalpha/dbias only (A/B: 1.80-1.88 vs 1.65 ms, off)"),
