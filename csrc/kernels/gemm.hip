@@ -941,8 +941,33 @@ __global__ __launch_bounds__(512) void gemm256_kernel(LA la, LB lb, EPI epi, int
     float st_s[8], st_q[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) { st_s[j] = 0.f; st_q[j] = 0.f; }
+    // backward BN form (EpiBf16 bz): this thread's column group is fixed (512 % (TN/8) == 0), so its
+    // ReLU coefficients load once, and each pass's 4 z vectors are issued together before the pass
+    constexpr int G256 = 64 * TN / 8 / 512;
+    bool bwd = false;
+    float bsc8[8], bsh8[8];
+    const int bc8 = tid % (TN / 8), bn8 = n0 + bc8 * 8;
+    if constexpr (EpiStats<EPI>::v) {
+      bwd = epi.stats && epi.bz;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { bsc8[j] = 0.f; bsh8[j] = 1.f; }
+      if (bwd && epi.bsc && bn8 + 8 <= N) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { bsc8[j] = epi.bsc[bn8 + j]; bsh8[j] = epi.bsh[bn8 + j]; }
+      }
+    }
 #pragma unroll
     for (int pass = 0; pass < 4; ++pass) {
+      U4 zv[G256];
+      if constexpr (EpiStats<EPI>::v) {
+        if (bwd) {
+#pragma unroll
+          for (int u = 0; u < G256; ++u) {
+            const int m = m0 + pass * 64 + (u * 512 + tid) / (TN / 8);
+            zv[u] = (m < M && bn8 + 8 <= N) ? *(const U4*)(epi.bz + (long)m * epi.ldc + bn8) : zero4();
+          }
+        }
+      }
       if (wm == (pass >> 1)) {
 #pragma unroll
         for (int ii = 0; ii < 4; ++ii) {
@@ -965,9 +990,11 @@ __global__ __launch_bounds__(512) void gemm256_kernel(LA la, LB lb, EPI epi, int
           float vals[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
           bool done = false;
           if constexpr (EpiStats<EPI>::v) {
-            if (epi.stats && epi.bz) {
+            if (bwd) {
               float zz[8];
-              epi.bwd_prep(m, n, vals, min(8, N - n), zz);
+              unpack8(zv[v0 / 512], zz);
+#pragma unroll
+              for (int j = 0; j < 8; ++j) vals[j] = fmaf(zz[j], bsc8[j], bsh8[j]) > 0.f ? vals[j] : 0.f;
               epi.vec8(m, n, vals, min(8, N - n));
               stats_acc8_bwd(vals, zz, min(8, N - n), st_s, st_q);
               done = true;

@@ -309,3 +309,32 @@ def test_resnet_bn_backward_epilogue_sums_match_reduce(monkeypatch):
         g1 = res[True][1][name]
         cos = float(torch.dot(g1.flatten(), g0.flatten()) / (g1.norm() * g0.norm() + 1e-20))
         assert cos > 0.99 and _rel(g1, g0) < 0.1, (name, cos, _rel(g1, g0))
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout,KS", [(64, 28, 28, 512, 256, 1), (8, 28, 28, 128, 64, 1), (8, 14, 14, 64, 64, 3)])
+def test_dgrad_bnstats_matches_reduce(N, H, W, Cin, Cout, KS):
+    """gemm.hip EpiBf16 backward form on both GEMM kernels (the first shape takes the 256x256 LDS-DMA
+    kernel): the masked data gradient equals conv dgrad + ReLU mask, and the partial sums equal
+    bn_bwd_reduce's over the same (dy, z)."""
+    torch.manual_seed(N + Cin)
+    dz = (torch.randn(N, H, W, Cout) * 0.3).to(torch.bfloat16).cuda()
+    w = (torch.randn(Cout, KS, KS, Cin) * 0.05).to(torch.bfloat16).cuda()
+    zb = torch.randn(N, H, W, Cin).to(torch.bfloat16).cuda()
+    sc, sh = _bn_pair(Cin)
+    dx_ref = torch.empty(N, H, W, Cin, dtype=torch.bfloat16, device=DEV)
+    if KS == 1:
+        K.conv1x1_dgrad(dz, w, 1, dx_ref)
+    else:
+        K.conv2d_dgrad(dz, w, KS // 2, dx_ref)
+    part_ref = KB.part_buffer(Cin, DEV)
+    KB.bn_bwd_reduce(dx_ref, None, zb, True, part_ref, sc, sh)
+    dx = torch.empty_like(dx_ref)
+    part = KB.part_buffer(Cin, DEV)
+    assert K.conv_dgrad_bnstats(dz, w, KS // 2, dx, part, zb, sc, sh)
+    torch.cuda.synchronize()
+    mask = (zb.float() * sc + sh) > 0
+    want = torch.where(mask, dx_ref, torch.zeros_like(dx_ref))
+    bad = int((dx != want).sum())  # (fma vs mul+add can flip a mask bit exactly at 0)
+    assert bad <= max(2, dx.numel() // 1_000_000), bad
+    s_ref, s = part_ref.sum(0), part.sum(0)
+    assert torch.allclose(s, s_ref, rtol=1e-3, atol=1e-2 * float(s_ref.abs().max()) / 100 + 1e-3)
