@@ -57,6 +57,35 @@ print(json.dumps({"path": "fit (train_step_fast)", "ms_per_step": round(fit_ms, 
                   "samples_per_s": round(a.batch / fit_ms * 1e3, 1), "batch": a.batch}), flush=True)
 del m
 
+# ---- the same GradientTape step without a strategy / coordinator: splits the PS path's overhead
+# into the tape step itself (separate loss, unfused optimizer launch) and the PS dispatch
+torch.manual_seed(1)
+mt_ = build_cnn_model((H, W, 3), flat=True, summary=False, device=dev)
+opt_ = nn.optimizers.Adam(learning_rate=1e-4)
+lo_ = nn.losses.MeanSquaredError()
+
+
+def tape_step(xb, yb):
+    with nn.GradientTape() as tape:
+        p = mt_(xb, training=True)
+        lv = lo_(yb, p)
+    gr = tape.gradient(lv, mt_.trainable_variables)
+    opt_.apply_gradients(zip(gr, mt_.trainable_variables))
+
+
+for i in range(3):
+    tape_step(xs[i % 2], ys[i % 2])
+sync()
+t0 = time.perf_counter()
+for i in range(a.steps):
+    tape_step(xs[i % 2], ys[i % 2])
+sync()
+tape_ms = (time.perf_counter() - t0) / a.steps * 1e3
+print(json.dumps({"path": "GradientTape loop, no strategy", "ms_per_step": round(tape_ms, 4),
+                  "samples_per_s": round(a.batch / tape_ms * 1e3, 1), "batch": a.batch,
+                  "vs_fit": round(tape_ms / fit_ms, 3)}), flush=True)
+del mt_, opt_
+
 # ---- ParameterServerStrategy + ClusterCoordinator (the reference's loop)
 strategy = make_parameter_server_strategy(1, 1)
 with strategy.scope():
