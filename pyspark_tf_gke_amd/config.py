@@ -65,6 +65,8 @@ _K = [
     Knob("fused_head", bool, True, "PTG_FUSED_HEAD", None, "CNN-B1 Dense(relu)->Dense->MSE head as two kernels"),
     Knob("device_feed", bool, True, "PTG_DEVICE_FEED", None, "fit(): pinned ring + side-stream H2D for host datasets"),
     Knob("side_stream", bool, True, "PTG_SIDE_STREAM", None, "weight gradients on a side HIP stream (1 replica)"),
+    Knob("tape_overlap", bool, True, "PTG_TAPE_OVERLAP", None,
+         "GradientTape loops: big Dense Adam on an aux stream overlapping the rest of the backward"),
     Knob("raw_u8_input", bool, True, "PTG_RAW_U8_INPUT", None, "first conv reads the uint8 image batch directly"),
     Knob("sparse_first", bool, True, "PTG_SPARSE_FIRST", None, "first conv layer keeps a sparse pool record"),
     Knob("bn_fuse", bool, False, "PTG_BN_FUSE", None, "ResNet: the BN+ReLU of conv->conv links applied in the next conv's operand loaders (A/B: 8.04k vs 8.75k img/s)"),

@@ -209,7 +209,11 @@ class ClusterCoordinator:
                 mi, oi = st.pending_ids() if status == 1 else (-1, -1)
                 if status == 1 and mi < 0:
                     status = 3  # ran fine but produced no update (e.g. an evaluation closure)
-                vtype, vnum = _encode_value(value) if status in (1, 3) else (0, 0.0)
+                # a tensor result is shared through the status exchange only when another rank
+                # needs it: encoding reads it on the host, which drained the stream every closure
+                # (one worker: 2.08 -> see profiles/r3_tape_overlap_ps_vs_fit.txt)
+                share = status in (1, 3) and (world > 1 or not isinstance(value, torch.Tensor))
+                vtype, vnum = _encode_value(value) if share else (0, 0.0)
                 vec = torch.zeros(4 * world, dtype=torch.int64)
                 vec[4 * rank: 4 * rank + 4] = torch.tensor([status, mi + 1, oi + 1, vtype])
                 vec = torch.tensor(comm.all_reduce_int(vec.tolist()), dtype=torch.int64).view(world, 4)

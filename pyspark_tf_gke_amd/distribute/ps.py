@@ -550,7 +550,7 @@ class ParameterServerStrategy(Strategy):
             return
         opt = optimizer or model.optimizer
         if self.world_size == 1:
-            opt.apply(model.store)
+            self._apply_local(model, opt)
         elif self.is_async:
             self._push_async(model, opt)
         else:
@@ -562,10 +562,24 @@ class ParameterServerStrategy(Strategy):
             self._pending = None
             return
         if self.world_size == 1:
-            opt.apply(model.store, gscale=1.0)
+            self._apply_local(model, opt)
         else:
             self._push_apply_sync(model, opt, contributed)
         self._pending = None
+
+    @staticmethod
+    def _apply_local(model, opt) -> None:
+        """One worker: the update is local.  After a GradientTape step whose gradients went straight
+        to apply_gradients, the big Dense ranges update on an aux stream as soon as their dW is
+        ready (nn/tape.py _apply_overlapped); otherwise one flat pass."""
+        ready = getattr(model, "_tape_overlap", None)
+        model._tape_overlap = None
+        if ready:
+            from ..nn.tape import _apply_overlapped
+
+            _apply_overlapped(opt, model.store, ready)
+        else:
+            opt.apply(model.store)
 
     # ---- full-precision state (saving, checkpoints) -------------------------------------------------
     def _gather_full(self, model, src_local: torch.Tensor, src_window, dst: torch.Tensor) -> None:

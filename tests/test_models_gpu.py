@@ -285,3 +285,99 @@ def test_persistent_work_queue_mode_matches_static(hip_built):
     m0, l0, init = run(False)
     m1, l1, _ = run(True)
     _same_training(m0, m1, init, l0, l1)
+
+
+def test_tape_loop_overlapped_adam_same_training(hip_built):
+    """The reference's GradientTape loop (train_tf_ps.py:616-631): with the side-stream backward
+    and the big Dense Adam on an auxiliary stream waiting only for its dW (tape.py), the weights,
+    moments and losses match the serial tape loop (PTG_TAPE_OVERLAP=0) up to run-order noise."""
+    from pyspark_tf_gke_amd import nn
+    from pyspark_tf_gke_amd.nn import tape as T
+
+    torch.manual_seed(0)
+    xs = [torch.randint(0, 256, (16, 64, 80, 3), dtype=torch.uint8, device="cuda") for _ in range(2)]
+    ys = [torch.rand(16, 2, device="cuda") * 60 for _ in range(2)]
+
+    def run(overlap):
+        torch.manual_seed(1)
+        m = build_cnn_model((64, 80, 3), flat=True, summary=False, device="cuda")
+        init = m.store.flat.clone()
+        opt = nn.optimizers.Adam(learning_rate=1e-3)
+        lo = nn.losses.MeanSquaredError()
+        losses, used = [], []
+        old = T.OVERLAP
+        T.OVERLAP = overlap
+        try:
+            for i in range(6):
+                with nn.GradientTape() as tape:
+                    p = m(xs[i % 2], training=True)
+                    lv = lo(ys[i % 2], p)
+                g = tape.gradient(lv, m.trainable_variables)
+                used.append(bool(m._tape_ready) and T._overlap_ok(opt, list(zip(g, m.trainable_variables))))
+                opt.apply_gradients(zip(g, m.trainable_variables))
+                losses.append(float(lv))
+        finally:
+            T.OVERLAP = old
+        torch.cuda.synchronize()
+        assert opt.iterations == 6 and m.store.grad_clean
+        return m, losses, init, used
+
+    m0, l0, init, u0 = run(False)
+    m1, l1, _, u1 = run(True)
+    assert not any(u0) and all(u1), (u0, u1)  # the overlapped path really ran
+    _same_training(m0, m1, init, l0, l1)
+
+
+def test_ps_one_worker_tape_overlap_same_training(hip_built):
+    """The reference's primary loop (ParameterServerStrategy + ClusterCoordinator.schedule of the
+    GradientTape closure, train_tf_ps.py:612-645) with one worker: the round-commit update takes the
+    overlapped Dense Adam (ps.py _apply_local) and trains exactly like the serial update."""
+    from pyspark_tf_gke_amd import distribute as ds
+    from pyspark_tf_gke_amd import nn
+    from pyspark_tf_gke_amd.cli.train import make_parameter_server_strategy
+    from pyspark_tf_gke_amd.nn import tape as T
+
+    torch.manual_seed(0)
+    xs = [torch.randint(0, 256, (16, 64, 80, 3), dtype=torch.uint8, device="cuda") for _ in range(2)]
+    ys = [torch.rand(16, 2, device="cuda") * 60 for _ in range(2)]
+
+    def run(overlap):
+        strategy = make_parameter_server_strategy(1, 1)
+        with strategy.scope():
+            torch.manual_seed(1)
+            m = build_cnn_model((64, 80, 3), flat=True, summary=False, device="cuda")
+            opt = nn.optimizers.Adam(learning_rate=1e-3)
+            lo = nn.losses.MeanSquaredError()
+        init = m.store.flat.clone()
+        coord = ds.ClusterCoordinator(strategy)
+        losses, used = [], []
+
+        def step_fn(i):
+            with nn.GradientTape() as tape:
+                p = m(xs[i % 2], training=True)
+                lv = lo(ys[i % 2], p)
+            g = tape.gradient(lv, m.trainable_variables)
+            opt.apply_gradients(zip(g, m.trainable_variables))
+            return lv
+
+        old, orig = T.OVERLAP, T._apply_overlapped
+
+        def counted(*a):
+            used.append(1)
+            return orig(*a)
+
+        T.OVERLAP, T._apply_overlapped = overlap, counted
+        try:
+            for i in range(6):
+                r = coord.schedule(lambda i=i: strategy.run(step_fn, args=(i,)))
+                coord.join()
+                losses.append(float(r.fetch()))
+        finally:
+            T.OVERLAP, T._apply_overlapped = old, orig
+        torch.cuda.synchronize()
+        assert opt.iterations == 6 and len(used) == (6 if overlap else 0), used
+        return m, losses, init
+
+    m0, l0, init = run(False)
+    m1, l1, _ = run(True)
+    _same_training(m0, m1, init, l0, l1)
