@@ -96,6 +96,9 @@ _K = [
          "sim_world: also apply the peers' shard updates (exact numerics of N identical-data ranks, N x the Adam work)"),
     Knob("persist_dynamic", bool, False, "PTG_PERSIST_DYNAMIC", None, "persistent conv kernels in work-queue mode for N > 1"),
     Knob("ps_mode", str, "sync", "PTG_PS_MODE", None, "ParameterServerStrategy: sync or async"),
+    Knob("coord_dead_s", float, 60.0, "PTG_COORD_DEAD_S", None,
+         "async ClusterCoordinator: a worker whose liveness beat is this old has its drawn-but-unfinished "
+         "closures re-queued for the others"),
     Knob("ipc_allreduce", bool, False, "PTG_IPC_ALLREDUCE", None, "one-shot IPC all-reduce for small messages"),
     Knob("fault_rank", str, "", "PTG_FAULT_RANK", None, "fault injection: rank to kill"),
     Knob("fault_step", int, 1, "PTG_FAULT_STEP", None, "fault injection: step at which fault_rank dies"),

@@ -10,9 +10,10 @@ Asynchronous parameter server (``ParameterServerStrategy(mode="async")``, N > 1)
 handed to whichever worker is idle - each rank draws the next closure index from a counter in the
 TCP store until the queue is exhausted - and a closure's ``apply_gradients`` pushes straight to the
 PS owners (one-sided, ps.py) without any collective, so a slow worker simply runs fewer closures
-(TF's ``ClusterCoordinator.schedule`` dispatch).  A closure that raises is re-run by the worker that
-is idle at that moment - the one that just failed it - up to ``max_retries`` times.  Results travel
-through the store.
+(TF's ``ClusterCoordinator.schedule`` dispatch).  A closure that raises before its push goes back to
+a shared retry queue for a DIFFERENT idle worker, up to ``max_retries`` times; the closures of a
+worker whose process stops beating are re-queued for the others.  Results travel through the
+store.
 
 Synchronous strategies (sync PS, MWMS): ``join()`` runs the queue in rounds of ``world_size``
 closures, closure i of a round on rank ``i % world``; a round is a transaction:
@@ -142,6 +143,18 @@ class ClusterCoordinator:
 
     # ---- asynchronous dispatch ------------------------------------------------------------------
     def _join_async(self) -> None:
+        """Closures go to whichever worker asks first (a store counter).  A closure that raises
+        before its gradient push goes back to a shared retry queue with the failing worker excluded,
+        so a different idle worker runs it (TF's ClusterCoordinator reschedules a failed closure on
+        another worker, train_tf_ps.py:612,642-645); a worker excluded by every rank may take it
+        again.  A closure that fails after its push (the update is already applied) or after
+        ``max_retries`` retries is recorded as failed.  Closures drawn by a worker whose liveness
+        beat stops (its process died) are re-queued for the others.  Every outcome is published in
+        the store, so each rank's RemoteValue resolves to it."""
+        import threading
+        import time
+
+        from .. import config
         from ..runtime import heartbeat
         from .ps import _store
 
@@ -151,37 +164,118 @@ class ClusterCoordinator:
         pre = f"ptg/coord/{st._token if getattr(st, '_token', None) else 'x'}/{self._cid}/{self._gen}"
         queue, self._queue = self._queue, []
         n = len(queue)
-        while True:
-            i = store.add(pre + "/next", 1) - 1  # the next closure goes to whichever worker asks first
-            if i >= n:
-                break
-            fn, args, kwargs, rv, tries = queue[i]
+        world, rank = st.world_size, st.rank
+        every = (1 << world) - 1
+        dead_s = float(config.get("coord_dead_s"))
+        stop = threading.Event()
+
+        def beat():  # liveness (not progress): stops only when this process does
+            bs = _store()
+            while not stop.is_set():
+                bs.set(f"{pre}/hb/{rank}", repr(time.time()))
+                stop.wait(min(1.0, dead_s / 4))
+
+        store.set(f"{pre}/hb/{rank}", repr(time.time()))  # nobody reads this rank as dead before its thread runs
+        hb = threading.Thread(target=beat, daemon=True, name="ptg-coord-beat")
+        hb.start()
+
+        def finalize(i, msg) -> bool:
+            # exactly one outcome per closure (a re-queued closure of a worker presumed dead may
+            # still complete there)
+            if store.add(f"{pre}/fin/{i}", 1) != 1:
+                return False
+            store.set(f"{pre}/rv/{i}", msg)
+            store.add(pre + "/nfin", 1)
+            return True
+
+        def requeue(i, tries, excl):
+            j = store.add(pre + "/rq/alloc", 1) - 1
+            store.set(f"{pre}/rq/{j}", f"{i}:{tries}:{excl}")
+
+        cursor, fresh_done, last_scan = 0, False, time.time()
+        try:
             while True:
+                job = None
+                nq = store.add(pre + "/rq/alloc", 0)
+                while job is None and cursor < nq:
+                    store.wait([f"{pre}/rq/{cursor}"])
+                    i, tries, excl = (int(x) for x in store.get(f"{pre}/rq/{cursor}").decode().split(":"))
+                    j, cursor = cursor, cursor + 1
+                    if excl & (1 << rank) and excl != every:
+                        continue  # a worker that failed it leaves it to the others
+                    if store.add(f"{pre}/rq/{j}/claim", 1) == 1:
+                        job = (i, tries, excl & every if excl != every else 0)
+                if job is None and not fresh_done:
+                    i = store.add(pre + "/next", 1) - 1
+                    if i < n:
+                        job = (i, 0, 0)
+                    else:
+                        fresh_done = True
+                if job is None:
+                    if store.add(pre + "/nfin", 0) >= n:
+                        break
+                    if time.time() - last_scan > min(1.0, dead_s / 4):
+                        last_scan = time.time()
+                        self._rescue_dead(store, pre, n, world, rank, dead_s, requeue)
+                    time.sleep(0.002)
+                    continue
+                i, tries, excl = job
+                store.set(f"{pre}/own/{i}", str(rank))
+                fn, args, kwargs, rv, _ = queue[i]
+                st._closure_pushed = False
                 try:
                     value = fn(*args, **kwargs)
                 except StopIteration as e:
-                    rv._error = e
-                    store.set(f"{pre}/rv/{i}", f"E:StopIteration on worker {st.rank}")
-                    break
-                except Exception as e:  # noqa: BLE001 - rescheduled on the (now idle) worker
-                    if tries >= self.max_retries:
+                    if finalize(i, f"E:StopIteration on worker {rank}"):
                         rv._error = e
-                        store.set(f"{pre}/rv/{i}", f"E:closure failed on worker {st.rank} after {tries + 1} attempts: {e!r}"[:2000])
-                        break
-                    tries += 1
-                    self.retries += 1
-                    continue
-                rv._set(value)
-                vt, x = _encode_value(value)
-                store.set(f"{pre}/rv/{i}", f"V:{vt}:{x!r}")
-                self.closures_run += 1
-                break
-            heartbeat.progress()
+                except Exception as e:  # noqa: BLE001 - rescheduled on another idle worker
+                    if getattr(st, "_closure_pushed", False) or tries >= self.max_retries:
+                        why = "after its gradient push" if getattr(st, "_closure_pushed", False) else \
+                            f"after {tries + 1} attempts"
+                        msg = f"closure failed on worker {rank} {why}: {e!r}"[:2000]
+                        if finalize(i, "E:" + msg):
+                            rv._error = RuntimeError(msg)
+                            rv._error.__cause__ = e
+                    else:
+                        self.retries += 1
+                        requeue(i, tries + 1, excl | (1 << rank))
+                else:
+                    vt, x = _encode_value(value)
+                    if finalize(i, f"V:{vt}:{x!r}"):
+                        rv._set(value)
+                        self.closures_run += 1
+                heartbeat.progress()
+        finally:
+            stop.set()
+            hb.join(timeout=5)
         st.wait_all_applied()  # collective: every push applied, every rank pulled the final values
         for i, (_, _, _, rv, _) in enumerate(queue):
             if not rv._done and rv._error is None:
                 rv._remote_key = f"{pre}/rv/{i}"  # ran elsewhere: resolved on fetch()
         comm.barrier()
+
+    @staticmethod
+    def _rescue_dead(store, pre, n, world, rank, dead_s, requeue) -> None:
+        """Re-queue the unfinished closures of workers whose liveness beat is older than dead_s."""
+        import time
+
+        now = time.time()
+        dead = []
+        for r in range(world):
+            if r == rank:
+                continue
+            key = f"{pre}/hb/{r}"
+            if store.check([key]) and now - float(store.get(key).decode()) > dead_s:
+                dead.append(r)
+        if not dead:
+            return
+        for i in range(n):
+            own = f"{pre}/own/{i}"
+            if not store.check([own]) or store.check([f"{pre}/rv/{i}"]):
+                continue
+            r = int(store.get(own).decode())
+            if r in dead and store.add(f"{pre}/rescue/{i}/{r}", 1) == 1:
+                requeue(i, 0, 1 << r)
 
     # ---- transactional rounds (sync) ---------------------------------------------------------------
     def _join_rounds(self) -> None:

@@ -48,6 +48,7 @@ from .strategy import Strategy
 
 _CHUNK = 1 << 16  # elements per device-table chunk (one workgroup each)
 NSLOT = 4  # gradient inbox slots per owner (pushes in flight to one owner)
+_MAX_WINDOWS = 16  # base addresses one ptg_piece_copy launch takes (comm.hip IPC_MAXW)
 
 
 _TLS = threading.local()
@@ -103,8 +104,11 @@ class _PieceTable:
         from .. import _native
         from ..ops._util import stream_handle
 
+        if len(srcs) > _MAX_WINDOWS or len(dsts) > _MAX_WINDOWS:
+            raise ValueError(f"ptg_piece_copy takes at most {_MAX_WINDOWS} base addresses per side")
+
         def bases(xs):
-            arr = (ctypes.c_uint64 * 16)()
+            arr = (ctypes.c_uint64 * _MAX_WINDOWS)()
             for i, x in enumerate(xs):
                 arr[i] = x if isinstance(x, int) else x.data_ptr()
             return arr
@@ -121,7 +125,7 @@ class _PSPlan:
     [seg_b, seg); the owner keeps its shards' fp32 values (``master``), their bf16 copy
     (``master_bf``) and optimizer moments in that layout: the variables live on the PS."""
 
-    def __init__(self, model, partitioner, num_ps: int, world: int, rank: int):
+    def __init__(self, model, partitioner, num_ps: int, world: int, rank: int, windows: bool = False):
         from ..nn.params import ALIGN
 
         st = model.store
@@ -159,11 +163,20 @@ class _PSPlan:
         dev = st.flat.device
         self.device = dev
         T = lambda rows: _PieceTable(rows, dev)  # noqa: E731
-        # push: fp32 gradient pieces -> owner segments; pulls: owner segments -> flat store
-        self.t_push = T([(0, pc.lo, pc.owner, pc.xlo, pc.n) for pc in self.pieces])
-        self.t_pull_b = T([(pc.owner, pc.xlo, 0, pc.lo, pc.n) for pc in self.pieces if pc.bf])
-        self.t_pull_f = T([(pc.owner, pc.xlo - self.seg_b, 0, pc.lo, pc.n) for pc in self.pieces if not pc.bf])
-        self.t_pull_all = T([(pc.owner, pc.xlo, 0, pc.lo, pc.n) for pc in self.pieces])
+        # push: fp32 gradient pieces -> owner segments; pulls: owner segments -> flat store.
+        # windows (async): one base address per owner (its IPC / shm window, <= 16 of them);
+        # otherwise the owners' segments are consecutive slices of ONE collective buffer, so every
+        # row names base 0 at the owner's slice offset and the world size is not capped.
+        self.windows = windows
+
+        def own(pc, size, off):  # (base index, element offset) of a piece in an owner layout
+            return (pc.owner, off) if windows else (0, pc.owner * size + off)
+
+        self.t_push = T([(0, pc.lo) + own(pc, self.seg, pc.xlo) + (pc.n,) for pc in self.pieces])
+        self.t_pull_b = T([own(pc, self.seg_b, pc.xlo) + (0, pc.lo, pc.n) for pc in self.pieces if pc.bf])
+        self.t_pull_f = T([own(pc, self.seg_f, pc.xlo - self.seg_b) + (0, pc.lo, pc.n)
+                           for pc in self.pieces if not pc.bf])
+        self.t_pull_all = T([own(pc, self.seg, pc.xlo) + (0, pc.lo, pc.n) for pc in self.pieces])
         self.t_own = T([(0, pc.lo, 0, pc.xlo, pc.n) for pc in self.mine])
         self.xbuf = None  # sync push buffer (world * seg fp32), allocated on first use
         self.gshard = torch.zeros(self.seg, dtype=torch.float32, device=dev)
@@ -331,6 +344,9 @@ class _OwnerService(threading.Thread):
         super().__init__(daemon=True, name=f"ptg-ps-owner-{prefix}")
         self.st, self.model, self.plan, self.win, self.prefix = strategy, model, plan, win, prefix
         self.applied = 0
+        # optimizer steps applied before this service's first push (a restored checkpoint): Adam's
+        # bias correction continues from there (on_state_loaded sets it)
+        self.step_offset = 0
         self.last_opt = None
         self.stop_flag = False
         self.error: BaseException | None = None
@@ -361,7 +377,8 @@ class _OwnerService(threading.Thread):
                     # the inbox slot is written by peers: read it with system-scope loads
                     self._one.copy([self.win.inbox(rank, t % NSLOT)], False, [self.grad], False, sys=True)
                     master = self.win.vals(rank)
-                    _apply_packed(opt, master, self.grad, self.plan.slot, self.win.vals_bf(rank), t + 1, gscale)
+                    _apply_packed(opt, master, self.grad, self.plan.slot, self.win.vals_bf(rank),
+                                  self.step_offset + t + 1, gscale)
                 if stream is not None:
                     stream.synchronize()
                 self.applied = t + 1
@@ -405,7 +422,11 @@ class ParameterServerStrategy(Strategy):
 
     def register_model(self, model) -> None:
         super().register_model(model)  # broadcast rank 0's initial values first
-        plan = model._ps_plan = _PSPlan(model, self.variable_partitioner, self.num_ps, self.world_size, self.rank)
+        if self.is_async and self.world_size > _MAX_WINDOWS:
+            raise ValueError(f"asynchronous ParameterServerStrategy maps every rank's window into one copy kernel: "
+                             f"at most {_MAX_WINDOWS} ranks (world size {self.world_size}); use mode='sync'")
+        plan = model._ps_plan = _PSPlan(model, self.variable_partitioner, self.num_ps, self.world_size, self.rank,
+                                        windows=self.is_async)
         if self.is_async:
             if self._token is None:  # one job-unique token for the store keys and shm files
                 store = _store()
@@ -440,13 +461,11 @@ class ParameterServerStrategy(Strategy):
             if plan.seg_b:
                 xb = torch.empty(self.world_size * plan.seg_b, dtype=plan.master_bf.dtype, device=plan.device)
                 comm.all_gather_flat(xb, plan.master_bf[:plan.seg_b].contiguous())
-                plan.t_pull_b.copy([xb[r * plan.seg_b:(r + 1) * plan.seg_b] for r in range(self.world_size)], True,
-                                   [st.flat_bf16], True)
+                plan.t_pull_b.copy([xb], True, [st.flat_bf16], True)
             if plan.seg_f:
                 xf = torch.empty(self.world_size * plan.seg_f, dtype=torch.float32, device=plan.device)
                 comm.all_gather_flat(xf, plan.master[plan.seg_b:plan.seg_b + plan.seg_f].contiguous())
-                plan.t_pull_f.copy([xf[r * plan.seg_f:(r + 1) * plan.seg_f] for r in range(self.world_size)], False,
-                                   [st.flat], False)
+                plan.t_pull_f.copy([xf], False, [st.flat], False)
         st.master_stale = plan.seg_b > 0 and st.flat_bf16.data_ptr() != st.flat.data_ptr()
 
     def _push_apply_sync(self, model, opt, contributed: list) -> None:
@@ -456,7 +475,7 @@ class ParameterServerStrategy(Strategy):
         if plan.xbuf is None:
             plan.xbuf = torch.zeros(self.world_size * plan.seg, dtype=torch.float32, device=plan.device)
         if contributed[self.rank]:
-            plan.t_push.copy([st.flat_grad], False, plan.segs(plan.xbuf), False)
+            plan.t_push.copy([st.flat_grad], False, [plan.xbuf], False)
         else:
             plan.xbuf.zero_()
         comm.reduce_scatter_flat(plan.gshard, plan.xbuf)
@@ -474,6 +493,16 @@ class ParameterServerStrategy(Strategy):
         svc = plan.service
         if svc.error is not None:
             raise RuntimeError("parameter-server service thread failed") from svc.error
+        # the owners name the optimizer by its index in strategy.optimizers, which is the same on
+        # every rank only for optimizers created under strategy.scope(); the model's compiled
+        # optimizer is addressed as "" (every owner has its own copy of that model)
+        if any(o is opt for o in self.optimizers):
+            oi = str(next(i for i, o in enumerate(self.optimizers) if o is opt))
+        elif opt is model.optimizer:
+            oi = ""
+        else:
+            raise RuntimeError("asynchronous ParameterServerStrategy: create the optimizer under strategy.scope() "
+                               "(or compile it into the model) so every parameter server knows it")
         owners = [r for r in range(self.world_size) if plan.owner_elems[r] > 0]
         tick = {}
         for r in owners:
@@ -487,11 +516,9 @@ class ParameterServerStrategy(Strategy):
         plan.t_push.copy([st.flat_grad], False, dsts, False)
         if st.flat_grad.is_cuda:
             torch.cuda.current_stream(st.flat_grad.device).synchronize()
-        if opt not in self.optimizers:
-            self.optimizers.append(opt)
-        oi = self.optimizers.index(opt)
         for r, t in tick.items():
             store.set(f"{plan.prefix}/{r}/ready/{t}", f"{float(self._commit_scale)!r}|{oi}")
+        self._closure_pushed = True  # from here on the update is applied whatever the closure does next
         store.wait([f"{plan.prefix}/{r}/done/{t}" for r, t in tick.items()])
         opt.iterations += 1
         self._pull(model)
@@ -513,7 +540,8 @@ class ParameterServerStrategy(Strategy):
                 self._pull(model)
                 # the host step counter of the optimizer that pushed = the updates the owners applied
                 # (every push goes to every owner: each owner's count is the job's step count)
-                n_applied = comm.all_reduce_int([model._ps_plan.service.applied], op=dist.ReduceOp.MAX)[0]
+                svc = model._ps_plan.service
+                n_applied = comm.all_reduce_int([svc.step_offset + svc.applied], op=dist.ReduceOp.MAX)[0]
                 for opt in {id(o): o for o in [model.optimizer, model._ps_plan.service.last_opt] if o}.values():
                     if opt is model._ps_plan.service.last_opt or opt.iterations:
                         opt.iterations = max(opt.iterations, n_applied)
@@ -589,7 +617,7 @@ class ParameterServerStrategy(Strategy):
         else:
             xb = torch.empty(self.world_size * plan.seg, dtype=torch.float32, device=plan.device)
             comm.all_gather_flat(xb, src_local.contiguous())
-            plan.t_pull_all.copy(plan.segs(xb), False, [dst], False)
+            plan.t_pull_all.copy([xb], False, [dst], False)
 
     def synchronize_master(self, model) -> None:
         """Collective: the full fp32 values on every rank (after bf16 pulls only the fp32 pieces are)."""
@@ -620,7 +648,10 @@ class ParameterServerStrategy(Strategy):
                 continue
             xb = torch.empty(self.world_size * plan.seg, dtype=torch.float32, device=plan.device)
             comm.all_gather_flat(xb, plan.slot(name))
-            plan.t_pull_all.copy(plan.segs(xb), False, [full], False)
+            if plan.windows:
+                plan.t_pull_all.copy(plan.segs(xb), False, [full], False)
+            else:
+                plan.t_pull_all.copy([xb], False, [full], False)
 
     def on_state_loaded(self, model) -> None:
         """After a checkpoint load into the full layout: re-pack the owned shards."""
@@ -633,6 +664,8 @@ class ParameterServerStrategy(Strategy):
         opt = model.optimizer
         if opt is None:
             return
+        if plan.window is not None:
+            plan.service.step_offset = opt.iterations - plan.service.applied
         for name, full in opt.state_tensors().items():
             if full is not None and full.numel() == model.store.total:
                 plan.t_own.copy([full], False, [plan.slot(name)], False)

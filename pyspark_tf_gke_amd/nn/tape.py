@@ -153,6 +153,12 @@ def _apply_overlapped(optimizer, store, ready) -> None:
     # stream).  The gradients of those ranges are cleared by the update, so code that reads them
     # between gradient() and apply_gradients() must turn this off (PTG_TAPE_OVERLAP=0).
     step = optimizer.iterations + 1
+    # a fresh optimizer allocates and zero-fills its moments HERE, on the step's stream; the aux
+    # stream must not read them before that fill (it otherwise never waits for the step's stream)
+    before = optimizer.m
+    optimizer.build(store)
+    if optimizer.m is not before:
+        aux.wait_stream(cur)
     with torch.cuda.stream(aux):
         for lo, hi, ev in ready:
             aux.wait_event(ev)
