@@ -285,7 +285,9 @@ def main():
                 extra["groupby"] = {"metric": gb["metric"], "value": gb["value"], "unit": gb["unit"],
                                     "ms_per_step": gb["ms_per_step"], "rows_per_gpu": gb["config"]["rows_per_gpu"],
                                     "distinct_keys": gb["config"]["distinct_keys"], "keys": gb["config"]["keys"],
-                                    "counts_check": gb["config"]["counts_check"], "dtype": "fp64"}
+                                    "counts_check": gb["config"]["counts_check"],
+                                    "sums_check": gb["config"]["sums_check"],
+                                    "groups_check": gb["config"]["groups_check"], "dtype": "fp64"}
                 from pyspark_tf_gke_amd.sql import bench_groupby as bg
 
                 gc.collect()
@@ -295,7 +297,9 @@ def main():
                 extra["groupby_sparse"] = {"value": gs["value"], "unit": gs["unit"], "ms_per_step": gs["ms_per_step"],
                                            "distinct_keys": gs["config"]["distinct_keys"], "keys": gs["config"]["keys"],
                                            "groups_out": gs["config"]["groups_out"],
-                                           "counts_check": gs["config"]["counts_check"], "dtype": "fp64"}
+                                           "counts_check": gs["config"]["counts_check"],
+                                           "sums_check": gs["config"]["sums_check"],
+                                           "groups_check": gs["config"]["groups_check"], "dtype": "fp64"}
             except Exception as e:  # noqa: BLE001 - never lose the headline line
                 extra["groupby"] = {"error": repr(e)[:300]}
     out = {"metric": res["metric"], "value": res["value"], "unit": res["unit"], "n_gpus": world,

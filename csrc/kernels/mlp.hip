@@ -1,0 +1,269 @@
+// Whole training step of a small MLP in ONE launch: the reference's CSV classifier
+// (train_tf_ps.py:328-343, Input(3) -> Dense16 relu -> Dense32 relu -> Dense64 relu -> Dense(C)
+// softmax, Adam, SparseCategoricalCrossentropy; 3,695 parameters) at the batch sizes the reference
+// trains it with (32, train_tf_ps.py:831; 64, run_tf_training_from_bastion.sh:17).
+//
+// At those sizes the step is launch- and barrier-bound, not FLOP-bound (~1.4 MFLOP at batch 64),
+// so one 512-thread workgroup keeps everything in LDS:
+//   * every layer's weights and bias (fp32, read once from the flat master store), with odd row
+//     strides so threads of one wave that read different rows hit different banks;
+//   * every layer's activation for the batch (kept for the backward) and two ping-pong gradient
+//     buffers.
+// Per step: forward (thread per output element), fused softmax + cross-entropy (or MSE) producing
+// dlogits, then per layer from the top ONE phase that computes dX for the layer below (with the
+// ReLU mask) from the pre-update LDS weights AND each parameter's gradient followed immediately
+// by its Adam update straight into the flat master / m / v / bf16 copy in HBM (no gradient buffer
+// is written).  After the last layer the updated weights are re-read into LDS by the threads that
+// wrote them.  ``steps`` > 1 runs consecutive batches of a device-resident dataset in the same
+// launch (Keras' steps_per_execution): each step is still a full forward / backward / Adam step.
+// Metric sums are kept in registers and added to `stats` once (the layouts of softmax_xent_k /
+// mse_k).
+#include "common.h"
+
+namespace ptgm {
+
+constexpr int MAXL = 6;
+constexpr int NT = 512;
+
+struct MlpDesc {
+  int L, B, steps, loss;        // loss 0: softmax + sparse categorical cross-entropy, 1: MSE
+  int d[MAXL + 1];              // d[0] input features, d[l + 1] units of layer l
+  int act[MAXL];                // hidden activation of layer l: 0 linear, 1 relu (last: from loss)
+  long woff[MAXL], boff[MAXL];  // element offsets of W_l ([d[l+1]][d[l]]) and b_l in the flat store
+  int lw[MAXL], lb[MAXL];       // LDS float offsets of W_l (row stride ws[l]) and b_l
+  int ws[MAXL];                 // LDS row stride of W_l (odd)
+  int la[MAXL + 1], as[MAXL + 1];  // LDS offset / row stride (odd) of activation l
+  int lg0, lg1, gs;             // the two gradient buffers (row stride gs, odd) and red scratch
+  int lred;
+  float lr, b1, b2, eps;
+  int t0;                       // optimizer steps taken before this launch
+};
+
+PTG_DEV float sum_block(float v, float* red) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float r = 0.f;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) r += red[i];
+  return r;
+}
+
+__global__ __launch_bounds__(NT) void mlp_train_k(const float* __restrict__ x, const void* __restrict__ y,
+                                                  float* __restrict__ p, float* __restrict__ m,
+                                                  float* __restrict__ v, bf16_t* __restrict__ pbf,
+                                                  float* __restrict__ stats, const MlpDesc D) {
+  extern __shared__ __align__(16) float sm[];
+  const int tid = threadIdx.x;
+  const int L = D.L, B = D.B;
+  // weights + biases -> LDS
+  for (int l = 0; l < L; ++l) {
+    const int K = D.d[l], N = D.d[l + 1], S = D.ws[l];
+    for (int i = tid; i < N * K; i += NT) sm[D.lw[l] + (i / K) * S + i % K] = p[D.woff[l] + i];
+    for (int n = tid; n < N; n += NT) sm[D.lb[l] + n] = D.boff[l] >= 0 ? p[D.boff[l] + n] : 0.f;
+  }
+  float s_loss = 0.f, s_a = 0.f, s_b = 0.f;
+  const int C = D.d[L];
+  for (int st = 0; st < D.steps; ++st) {
+    // ---- input batch
+    const int K0 = D.d[0];
+    const float* xs = x + (long)st * B * K0;
+    for (int i = tid; i < B * K0; i += NT) sm[D.la[0] + (i / K0) * D.as[0] + i % K0] = xs[i];
+    __syncthreads();
+    // ---- forward: thread per output element
+    for (int l = 0; l < L; ++l) {
+      const int K = D.d[l], N = D.d[l + 1], S = D.ws[l], SA = D.as[l], SO = D.as[l + 1];
+      const float* A = sm + D.la[l];
+      const float* W = sm + D.lw[l];
+      float* O = sm + D.la[l + 1];
+      const bool relu = l < L - 1 && D.act[l] == 1;
+      for (int i = tid; i < B * N; i += NT) {
+        const int r = i / N, n = i - r * N;
+        const float* a = A + r * SA;
+        const float* w = W + n * S;
+        float acc = sm[D.lb[l] + n];
+        for (int k = 0; k < K; ++k) acc = fmaf(a[k], w[k], acc);
+        O[r * SO + n] = relu ? fmaxf(acc, 0.f) : acc;
+      }
+      __syncthreads();
+    }
+    // ---- loss: dlogits into gradient buffer 0
+    float* G = sm + D.lg0;
+    const float* Z = sm + D.la[L];
+    const int SZ = D.as[L];
+    if (D.loss == 0) {
+      const int* lab = (const int*)y + (long)st * B;
+      const float scale = 1.f / (float)B;
+      for (int r = tid; r < B; r += NT) {
+        const float* z = Z + r * SZ;
+        float mx = z[0];
+        int am = 0;
+        for (int c = 1; c < C; ++c)
+          if (z[c] > mx) { mx = z[c]; am = c; }
+        float s = 0.f;
+        for (int c = 0; c < C; ++c) s += __expf(z[c] - mx);
+        const float inv = 1.f / s;
+        const int t = lab[r];
+        for (int c = 0; c < C; ++c) G[r * D.gs + c] = (__expf(z[c] - mx) * inv - (c == t ? 1.f : 0.f)) * scale;
+        const float pl = fminf(fmaxf(__expf(z[t] - mx) * inv, 1e-7f), 1.f - 1e-7f);
+        s_loss += -__logf(pl);
+        s_a += am == t ? 1.f : 0.f;
+      }
+    } else {
+      const float* tg = (const float*)y + (long)st * B * C;
+      const float inv = 1.f / (float)(B * C);
+      for (int i = tid; i < B * C; i += NT) {
+        const int r = i / C, c = i - r * C;
+        const float d = Z[r * SZ + c] - tg[i];
+        G[r * D.gs + c] = 2.f * d * inv;
+        s_loss += d * d * inv * (float)B;
+        s_a += fabsf(d);
+        s_b += d * d;
+      }
+    }
+    __syncthreads();
+    // ---- backward: per layer one phase (dX below + gradient + Adam), one barrier
+    const float t = (float)(D.t0 + st + 1);
+    const float lr_t = D.lr * sqrtf(1.f - powf(D.b2, t)) / (1.f - powf(D.b1, t));
+    int cur = D.lg0, nxt = D.lg1;
+    for (int l = L - 1; l >= 0; --l) {
+      const int K = D.d[l], N = D.d[l + 1], S = D.ws[l], SA = D.as[l];
+      const float* Gc = sm + cur;
+      const float* A = sm + D.la[l];
+      const float* W = sm + D.lw[l];
+      if (l > 0) {
+        const bool mask = D.act[l - 1] == 1;
+        float* Gn = sm + nxt;
+        for (int i = tid; i < B * K; i += NT) {
+          const int r = i / K, k = i - r * K;
+          const float* g = Gc + r * D.gs;
+          float s = 0.f;
+          for (int n = 0; n < N; ++n) s = fmaf(g[n], W[n * S + k], s);
+          if (mask && !(A[r * SA + k] > 0.f)) s = 0.f;
+          Gn[r * D.gs + k] = s;
+        }
+      }
+      const int nb = D.boff[l] >= 0 ? N : 0;
+      for (int i = tid; i < N * K + nb; i += NT) {
+        float g = 0.f;
+        long idx;
+        if (i < N * K) {
+          const int n = i / K, k = i - n * K;
+          for (int r = 0; r < B; ++r) g = fmaf(Gc[r * D.gs + n], A[r * SA + k], g);
+          idx = D.woff[l] + i;
+        } else {
+          const int n = i - N * K;
+          for (int r = 0; r < B; ++r) g += Gc[r * D.gs + n];
+          idx = D.boff[l] + n;
+        }
+        const float mm = D.b1 * m[idx] + (1.f - D.b1) * g;
+        const float vv = D.b2 * v[idx] + (1.f - D.b2) * g * g;
+        const float pp = p[idx] - lr_t * mm / (sqrtf(vv) + D.eps);
+        m[idx] = mm;
+        v[idx] = vv;
+        p[idx] = pp;
+        if (pbf) pbf[idx] = f2bf(pp);
+      }
+      __syncthreads();
+      const int tmp = cur; cur = nxt; nxt = tmp;
+    }
+    // ---- updated weights back into LDS (each thread re-reads exactly what it wrote)
+    if (st + 1 < D.steps) {
+      for (int l = 0; l < L; ++l) {
+        const int K = D.d[l], N = D.d[l + 1], S = D.ws[l];
+        const int nb = D.boff[l] >= 0 ? N : 0;
+        for (int i = tid; i < N * K + nb; i += NT) {
+          if (i < N * K) sm[D.lw[l] + (i / K) * S + i % K] = p[D.woff[l] + i];
+          else sm[D.lb[l] + (i - N * K)] = p[D.boff[l] + (i - N * K)];
+        }
+      }
+      // (the next step's input barrier orders these writes before any forward read)
+    }
+  }
+  float* red = sm + D.lred;
+  const float tl = sum_block(s_loss, red);
+  const float ta = sum_block(s_a, red);
+  const float tb = sum_block(s_b, red);
+  if (tid == 0) {
+    const float nb = (float)(B * D.steps);
+    if (D.loss == 0) {
+      stats[0] += tl;
+      stats[1] += ta;
+      stats[4] += nb;
+    } else {
+      stats[0] += tl;
+      stats[1] += ta;
+      stats[2] += tb;
+      stats[3] += nb * (float)C;
+      stats[4] += nb;
+    }
+  }
+}
+
+}  // namespace ptgm
+
+static int odd(int n) { return n | 1; }
+
+// LDS bytes of the fused step (0: shape not supported).  hdesc (host, int64):
+// [d0 .. dL][act0 .. act_{L-1}][woff0 .. woff_{L-1}][boff0 .. boff_{L-1}]
+static long mlp_plan(const long* hdesc, int L, int B, ptgm::MlpDesc* D) {
+  if (L < 1 || L > ptgm::MAXL || B < 1) return 0;
+  D->L = L; D->B = B;
+  int dmax = 0;
+  for (int i = 0; i <= L; ++i) {
+    D->d[i] = (int)hdesc[i];
+    if (D->d[i] < 1 || D->d[i] > 1024) return 0;
+    if (i > 0) dmax = dmax > D->d[i] ? dmax : D->d[i];
+  }
+  int off = 0;
+  for (int l = 0; l < L; ++l) {
+    D->act[l] = (int)hdesc[L + 1 + l];
+    D->woff[l] = hdesc[2 * L + 1 + l];
+    D->boff[l] = hdesc[3 * L + 1 + l];
+    D->ws[l] = odd(D->d[l]);
+    D->lw[l] = off; off += D->d[l + 1] * D->ws[l];
+    D->lb[l] = off; off += D->d[l + 1];
+  }
+  for (int l = 0; l <= L; ++l) {
+    D->as[l] = odd(D->d[l]);
+    D->la[l] = off; off += B * D->as[l];
+  }
+  D->gs = odd(dmax);
+  D->lg0 = off; off += B * D->gs;
+  D->lg1 = off; off += B * D->gs;
+  D->lred = off; off += 16;
+  return (long)off * 4;
+}
+
+extern "C" {
+
+// Bytes of LDS the fused step needs for this shape (the Python side checks it against the
+// 160 KiB per CU before choosing the fused path); 0 = unsupported.
+int ptg_mlp_lds_bytes(const long* hdesc, int L, int B, long* out) {
+  ptgm::MlpDesc D;
+  *out = mlp_plan(hdesc, L, B, &D);
+  return 0;
+}
+
+int ptg_mlp_train(const void* x, const void* y, float* p, float* m, float* v, void* pbf, float* stats,
+                  const long* hdesc, int L, int B, int steps, int loss, float lr, float b1, float b2, float eps,
+                  int t0, hipStream_t s) {
+  ptgm::MlpDesc D;
+  const long bytes = mlp_plan(hdesc, L, B, &D);
+  if (bytes <= 0 || bytes > 160 * 1024 || steps < 1 || (loss != 0 && loss != 1)) return (int)hipErrorInvalidValue;
+  D.steps = steps; D.loss = loss;
+  D.lr = lr; D.b1 = b1; D.b2 = b2; D.eps = eps; D.t0 = t0;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)ptgm::mlp_train_k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    attr = true;
+  }
+  hipLaunchKernelGGL(ptgm::mlp_train_k, dim3(1), dim3(ptgm::NT), (size_t)bytes, s, (const float*)x, y, p, m, v,
+                     (bf16_t*)pbf, stats, D);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

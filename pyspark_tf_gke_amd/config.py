@@ -62,6 +62,8 @@ _K = [
          "instead of under this step's backward (A/B on CNN-B1 b256: 1.70-1.71 vs 1.65-1.66 ms, so off)"),
     Knob("dense_adam_after", int, 0, "PTG_DENSE_ADAM_AFTER", None,
          "CNN-B1: fork the Dense dW+Adam GEMM after the k-th conv op's backward (0 = right after the Dense dX)"),
+    Knob("mlp_fused", bool, True, "PTG_MLP_FUSED", None,
+         "a model that is only a small Dense stack (the CSV MLP) runs each training step as ONE kernel (mlp.hip)"),
     Knob("fused_head", bool, True, "PTG_FUSED_HEAD", None, "CNN-B1 Dense(relu)->Dense->MSE head as two kernels"),
     Knob("device_feed", bool, True, "PTG_DEVICE_FEED", None, "fit(): pinned ring + side-stream H2D for host datasets"),
     Knob("side_stream", bool, True, "PTG_SIDE_STREAM", None, "weight gradients on a side HIP stream (1 replica)"),
@@ -87,6 +89,11 @@ _K = [
     Knob("seed", int, 1337, "PTG_SEED", None, "weight-initialisation seed when none is given"),
     # distribution
     Knob("dist_backend", str, "", "PTG_DIST_BACKEND", None, "torch.distributed backend override (default nccl=RCCL / gloo)"),
+    Knob("force_pg", bool, False, "PTG_FORCE_PG", None,
+         "create the process group even for one rank (a 1-rank RCCL group: the collective code paths run for real)"),
+    Knob("shard_world1", bool, False, "PTG_SHARD_WORLD1", None,
+         "MWMS on one rank with a process group: build the sharded update anyway (RCCL reduce-scatter / all-gather "
+         "of one rank through the side streams; a test of the N>1 path on one GPU)"),
     Knob("pg_timeout_s", float, 600.0, "PTG_PG_TIMEOUT", None, "process-group collective timeout (hang -> error -> restart)"),
     Knob("bucket_mb", float, 64.0, "PTG_BUCKET_MB", None, "MWMS gradient bucket size"),
     Knob("sharded_update", bool, True, "PTG_SHARDED_UPDATE", None, "MWMS: reduce-scatter + sharded optimizer + all-gather"),

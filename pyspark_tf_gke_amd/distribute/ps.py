@@ -356,6 +356,8 @@ class _OwnerService(threading.Thread):
     def run(self):  # noqa: D401 - thread body
         store = _store()
         rank = self.plan.rank
+        if self.plan.device.type == "cuda":
+            torch.cuda.set_device(self.plan.device)  # a new thread starts on device 0
         stream = torch.cuda.Stream(self.plan.device) if self.plan.device.type == "cuda" else None
         try:
             while not self.stop_flag:

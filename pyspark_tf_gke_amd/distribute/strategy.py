@@ -296,7 +296,11 @@ class MultiWorkerMirroredStrategy(Strategy):
             self.sim_exact = bool(config.get("sim_exact"))
         if sharded_update is None:
             sharded_update = config.get("sharded_update")
-        self.sharded_update = bool(sharded_update) and self.dp_degree > 1
+        # PTG_SHARD_WORLD1 (with PTG_FORCE_PG): a 1-rank process group still takes the sharded path, so
+        # the RCCL reduce-scatter / all-gather calls of an N-rank step run for real on one GPU
+        force1 = self.world_size == 1 and not self.sim_world and comm.is_initialized() and bool(
+            config.get("shard_world1"))
+        self.sharded_update = bool(sharded_update) and (self.dp_degree > 1 or force1)
         if self.sim_world and not self.sharded_update:
             raise ValueError("PTG_SIM_WORLD simulates the sharded update only (PTG_SHARDED_UPDATE=1)")
         self._works: list = []
@@ -410,7 +414,7 @@ class MultiWorkerMirroredStrategy(Strategy):
 
     # ---- engine hooks
     def on_op_grads_ready(self, model, op) -> None:
-        if self.dp_degree == 1 or not op.params or self.in_round():
+        if (self.dp_degree == 1 and not self.sharded_update) or not op.params or self.in_round():
             return
         plan = getattr(model, "_shard_plan", None)
         if plan is not None:
@@ -430,7 +434,7 @@ class MultiWorkerMirroredStrategy(Strategy):
             self._launch(model, hi)
 
     def finish_gradients(self, model) -> None:
-        if self.dp_degree == 1 or self.in_round():
+        if (self.dp_degree == 1 and not self.sharded_update) or self.in_round():
             return
         plan = getattr(model, "_shard_plan", None)
         if plan is not None:

@@ -48,6 +48,9 @@ DEFER_DENSE = config.get("defer_dense_update")
 # Within the backward: the big Dense dW+Adam GEMM is forked onto the side stream after the backward
 # of the k-th conv op from the top (0 = as soon as its inputs exist, right after the Dense dX)
 DENSE_ADAM_AFTER = config.get("dense_adam_after")
+# A model that is only a small Dense stack (the reference's CSV MLP) trains one whole step per launch
+# (mlp.hip): forward, loss, backward and Adam in one workgroup, everything in LDS.
+MLP_FUSED = config.get("mlp_fused")
 
 
 def default_device() -> torch.device:
@@ -337,7 +340,7 @@ class Sequential:
         one replica (no gradient collective between backward and update), GPU, PTG_FUSED_ADAM != 0."""
         if not FUSED_ADAM or not isinstance(self.optimizer, OPT.Adam) or not self.store.flat.is_cuda:
             return None
-        if st is not None and st.dp_degree != 1:
+        if st is not None and (st.dp_degree != 1 or getattr(st, "sharded_update", False)):
             return None
         all_ops = getattr(self, "ops", None) or []
         if getattr(self, "_fusable_key", None) is not all_ops:
@@ -475,11 +478,84 @@ class Sequential:
             torch.cuda.current_stream(self.device).wait_event(ev)
             self._deferred_ev = None
 
+    # ---------------------------------------------------------------- fused small-MLP step
+    def _mlp_plan(self, st):
+        """(dims, acts, woffs, boffs, loss kind) when the whole model is a small Dense stack that the
+        one-launch training step (mlp.hip) covers, else None.  Cached per (ops, loss)."""
+        key = (id(self.ops), id(self.loss), id(self.optimizer))
+        if getattr(self, "_mlp_key", None) != key:
+            self._mlp_key = key
+            self._mlp_cached = self._build_mlp_plan()
+        plan = self._mlp_cached
+        if plan is None:
+            return None
+        if st is not None and (st.world_size != 1 or st.dp_degree != 1 or getattr(st, "sharded_update", False)
+                               or st.in_round() or hasattr(st, "variable_partitioner")):
+            return None
+        return plan
+
+    def _build_mlp_plan(self):
+        if not MLP_FUSED or not self.ops or self.device is None or self.device.type != "cuda":
+            return None
+        opt = self.optimizer
+        if type(opt) is not OPT.Adam or getattr(opt, "dev_state", None) is not None:
+            return None
+        if not all(isinstance(op, E.DenseOp) for op in self.ops) or len(self.ops) > 6:
+            return None
+        last = self.ops[-1]
+        if isinstance(self.loss, LS.SparseCategoricalCrossentropy) and last.act == "softmax" and last.logits_only:
+            kind = 0
+        elif isinstance(self.loss, LS.MeanSquaredError) and last.act in (None, "linear"):
+            kind = 1
+        else:
+            return None
+        acts = []
+        for op in self.ops[:-1]:
+            if op.act not in (None, "linear", "relu"):
+                return None
+            acts.append(1 if op.act == "relu" else 0)
+        acts.append(0)
+        dims = [self.ops[0].dense.fan_in] + [op.dense.units for op in self.ops]
+        woffs = [op.dense.kernel.offset for op in self.ops]
+        boffs = [op.dense.bias.offset if op.dense.bias is not None else -1 for op in self.ops]
+        if max(w + dims[l + 1] * dims[l] for l, w in enumerate(woffs)) > self.store.total:
+            return None
+        return dims, acts, woffs, boffs, kind, K.mlp_desc(dims, acts, woffs, boffs)
+
+    def _mlp_fusable(self, xb, yb, st):
+        if xb.dtype != torch.float32 or not xb.is_cuda or xb.dim() != 2:
+            return None
+        plan = self._mlp_plan(st)
+        if plan is None or xb.shape[1] != plan[0][0]:
+            return None
+        B = xb.shape[0]
+        ok = getattr(self, "_mlp_lds_ok", None)
+        if ok is None:
+            ok = self._mlp_lds_ok = {}
+        if B not in ok:
+            ok[B] = 0 < K.mlp_lds_bytes(plan[0], B) <= 160 * 1024
+        return plan if ok[B] else None
+
+    def _train_step_mlp(self, xb, yb, stats, plan, steps: int = 1) -> None:
+        dims, acts, woffs, boffs, kind, desc = plan
+        opt, store = self.optimizer, self.store
+        opt.build(store)
+        if not getattr(store, "grad_clean", False):
+            store.zero_grad()  # (the fused step writes no gradient; leave the buffer clean)
+        y = yb.view(-1).contiguous() if kind == 0 else yb.contiguous()
+        K.mlp_train(xb.contiguous(), y, store.flat, opt.m, opt.v, store.flat_bf16, stats, dims, acts, woffs, boffs,
+                    steps, kind, opt.learning_rate, opt.beta_1, opt.beta_2, opt.epsilon, opt.iterations, desc=desc)
+        opt.iterations += steps
+        store.grad_clean = True
+
     def train_step(self, xb, yb, stats=None) -> None:
         _fault.maybe_fail()
         _heartbeat.progress()
         st = self._strategy()
         stats = self._stats_buf() if stats is None else stats
+        plan = self._mlp_fusable(xb, yb, st)
+        if plan is not None:
+            return self._train_step_mlp(xb, yb, stats, plan)
         if self._head_fusable(xb, st):
             self.store.zero_grad()
             return self._train_step_fused_head(xb, yb, stats, st)

@@ -1008,3 +1008,131 @@ def silhouette_points(X, assign, S, Q, cnt) -> float:
     out = torch.zeros(1, dtype=torch.float64, device=X.device)
     hip("ptg_silhouette", ptr(X), ptr(assign), ptr(S), ptr(Q), ptr(cnt), n, D, k, ptr(out))
     return float(out.item())
+
+
+# ------------------------------------------------------------------------------------------------
+# group keys of any column types (csrc/kernels/dfkey.hip): exact multi-column / nullable keys
+# ------------------------------------------------------------------------------------------------
+KT_CODE = 5  # dictionary codes (int32, < 0 = null)
+KMAX = 8
+
+
+class _PackDesc(ctypes.Structure):
+    _fields_ = [("ncols", ctypes.c_int), ("u", ctypes.c_void_p * KMAX), ("ok", ctypes.c_void_p * KMAX),
+                ("lut", ctypes.c_void_p * KMAX), ("nlut", ctypes.c_long * KMAX), ("lo", ctypes.c_uint64 * KMAX),
+                ("nullcode", ctypes.c_uint64 * KMAX), ("shift", ctypes.c_int * KMAX), ("bits", ctypes.c_int * KMAX),
+                ("type", ctypes.c_int * KMAX)]
+
+
+class _UnpackOut(ctypes.Structure):
+    _fields_ = [("data", ctypes.c_void_p * KMAX), ("valid", ctypes.c_void_p * KMAX)]
+
+
+AMAX = 16
+
+
+class _FinDesc(ctypes.Structure):
+    _fields_ = [("nout", ctypes.c_int), ("fn", ctypes.c_int * AMAX), ("type", ctypes.c_int * AMAX),
+                ("s", ctypes.c_void_p * AMAX), ("c", ctypes.c_void_p * AMAX), ("mn", ctypes.c_void_p * AMAX),
+                ("mx", ctypes.c_void_p * AMAX), ("out", ctypes.c_void_p * AMAX), ("valid", ctypes.c_void_p * AMAX)]
+
+
+def _check_struct_sizes() -> None:
+    lib = _native.hip_lib()
+    for name, st in (("ptg_key_desc_size", _PackDesc), ("ptg_unpack_out_size", _UnpackOut),
+                     ("ptg_fin_desc_size", _FinDesc)):
+        if getattr(lib, name)() != ctypes.sizeof(st):
+            raise RuntimeError(f"{name}: host struct layout {ctypes.sizeof(st)} != device {getattr(lib, name)()}")
+
+
+_STRUCTS_OK = [False]
+
+
+def key_prep(data: torch.Tensor, kt: int, valid: torch.Tensor | None, need_ok: bool, stats: torch.Tensor):
+    """One column -> (orderable u64 keys in an int64 tensor, per-row valid flags u8 or None); its
+    (min, max, null count) go into ``stats`` (3 int64 on the device, u64 bit patterns)."""
+    if not _STRUCTS_OK[0]:
+        _check_struct_sizes()
+        _STRUCTS_OK[0] = True
+    n = data.numel()
+    d = data.view(torch.uint8) if data.dtype == torch.bool else data.contiguous()
+    v = None if valid is None else (valid.view(torch.uint8) if valid.dtype == torch.bool else valid.contiguous())
+    u = torch.empty(n, dtype=torch.int64, device=data.device)
+    ok = torch.empty(n, dtype=torch.uint8, device=data.device) if need_ok else None
+    hip("ptg_key_prep", ptr(d), kt, ptr(v), n, ptr(u), ptr(ok), ptr(stats))
+    return u, ok
+
+
+def key_pack(cols, n: int, device) -> torch.Tensor:
+    """``cols``: dicts with u, ok, lut (sorted distinct u or None), lo, nullcode, shift, bits, type."""
+    D_ = _PackDesc()
+    D_.ncols = len(cols)
+    for j, c in enumerate(cols):
+        D_.u[j] = c["u"].data_ptr()
+        D_.ok[j] = c["ok"].data_ptr() if c["ok"] is not None else None
+        D_.lut[j] = c["lut"].data_ptr() if c["lut"] is not None else None
+        D_.nlut[j] = c["lut"].numel() if c["lut"] is not None else 0
+        D_.lo[j], D_.nullcode[j] = c["lo"], c["nullcode"]
+        D_.shift[j], D_.bits[j], D_.type[j] = c["shift"], c["bits"], c["type"]
+    out = torch.empty(n, dtype=torch.int64, device=device)
+    hip("ptg_key_pack", ctypes.addressof(D_), n, ptr(out))
+    return out, D_
+
+
+def key_unpack(keys: torch.Tensor, desc, outs: list) -> None:
+    """``outs``: per column (data tensor of the column's type, valid u8 tensor or None)."""
+    O = _UnpackOut()
+    for j, (d, v) in enumerate(outs):
+        O.data[j] = d.data_ptr()
+        O.valid[j] = v.data_ptr() if v is not None else None
+    hip("ptg_key_unpack", ptr(keys), keys.numel(), ctypes.addressof(desc), ctypes.addressof(O))
+
+
+AF = {"rows": 0, "count": 1, "sum_int": 2, "sum": 3, "avg": 4, "min": 5, "max": 6}
+
+
+def agg_finalize(rows: torch.Tensor, specs: list) -> None:
+    """``specs``: (fn name, output KT type, s, c, mn, mx, out tensor, valid u8 tensor or None)."""
+    for i in range(0, len(specs), AMAX):
+        F = _FinDesc()
+        part = specs[i:i + AMAX]
+        F.nout = len(part)
+        for j, (fn, kt, s, c, mn, mx, out, valid) in enumerate(part):
+            F.fn[j], F.type[j] = AF[fn], kt
+            F.s[j], F.c[j], F.mn[j], F.mx[j] = ptr(s), ptr(c), ptr(mn), ptr(mx)
+            F.out[j], F.valid[j] = out.data_ptr(), ptr(valid)
+        hip("ptg_agg_finalize", ptr(rows), rows.numel(), ctypes.addressof(F))
+
+
+def iota_f64(n: int, device) -> torch.Tensor:
+    out = torch.empty(n, dtype=torch.float64, device=device)
+    hip("ptg_iota_f64", ptr(out), n)
+    return out
+
+
+def f64_to_i64(x: torch.Tensor) -> torch.Tensor:
+    out = torch.empty(x.numel(), dtype=torch.int64, device=x.device)
+    hip("ptg_f64_to_i64", ptr(x.contiguous()), ptr(out), x.numel())
+    return out
+
+
+def unique_sorted_u64(u: torch.Tensor) -> torch.Tensor:
+    """Sorted distinct values of orderable u64 keys (int64 storage): hash aggregation without value
+    columns, then the LSD radix sort of the distinct keys."""
+    n = u.numel()
+    if n == 0:
+        return u
+    uk = hash_agg(u, [], [], est_keys=estimate_distinct(u) if n >= 65536 else None)[0]
+    sk, _ = radix_sort_u64(uk, None, 0, _U64)
+    return sk
+
+
+def rr_part(n: int, rank: int, world: int, device) -> torch.Tensor:
+    part = torch.empty(n, dtype=torch.int32, device=device)
+    hip("ptg_rr_part", n, rank, world, ptr(part))
+    return part
+
+
+def part_override(part: torch.Tensor, flag: torch.Tensor, value: int) -> None:
+    f = flag.view(torch.uint8) if flag.dtype == torch.bool else flag.contiguous()
+    hip("ptg_part_override", ptr(part), ptr(f), part.numel(), int(value))

@@ -716,6 +716,56 @@ def adam(p, g, m, v, pbf, lr_t: float, b1: float, b2: float, eps: float, gscale:
         float(eps), float(gscale), ptr(lr_dev), int(clear_grad))
 
 
+def _mlp_desc(dims, acts, woffs, boffs):
+    import ctypes
+
+    vals = list(dims) + list(acts) + list(woffs) + list(boffs)
+    return (ctypes.c_long * len(vals))(*[int(v) for v in vals])
+
+
+def mlp_lds_bytes(dims, B: int) -> int:
+    """LDS bytes the fused MLP step (mlp.hip) needs for these layer widths at batch B (0: no)."""
+    import ctypes
+
+    from .. import _native
+
+    L = len(dims) - 1
+    desc = _mlp_desc(dims, [0] * L, [0] * L, [0] * L)
+    out = ctypes.c_long(0)
+    _native.check(_native.hip_lib().ptg_mlp_lds_bytes(ctypes.addressof(desc), L, B, ctypes.byref(out)),
+                  "ptg_mlp_lds_bytes")
+    return int(out.value)
+
+
+def mlp_desc(dims, acts, woffs, boffs):
+    """The host descriptor of a fused MLP step (build once per model, pass as ``desc=``)."""
+    return _mlp_desc(dims, acts, woffs, boffs)
+
+
+def mlp_train(x, y, flat, m, v, flat_bf16, stats, dims, acts, woffs, boffs, steps: int, loss_kind: int,
+              lr: float, b1: float, b2: float, eps: float, t0: int, desc=None):
+    """``steps`` full training steps of a small MLP (Dense stack) in ONE launch (mlp.hip): x holds
+    steps x B rows (fp32), y the labels (int32, loss_kind 0 = softmax + sparse categorical
+    cross-entropy) or targets (fp32, loss_kind 1 = MSE); the Adam update goes straight into the
+    flat master store, its moments and the bf16 copy; metric sums into ``stats``."""
+    if not on_device(flat):
+        return ref.mlp_train(x, y, flat, m, v, flat_bf16, stats, dims, acts, woffs, boffs, steps, loss_kind, lr,
+                             b1, b2, eps, t0)
+    import ctypes
+
+    L = len(dims) - 1
+    B = x.shape[0] // steps
+    need(x, torch.float32, "mlp_train.x")
+    need(y, torch.int32 if loss_kind == 0 else torch.float32, "mlp_train.y")
+    assert x.numel() == steps * B * dims[0] and y.shape[0] == steps * B, (x.shape, y.shape, steps, dims)
+    if desc is None:  # (a cached descriptor was checked against the store when it was built)
+        assert max(woffs[l] + dims[l + 1] * dims[l] for l in range(L)) <= flat.numel()
+        desc = _mlp_desc(dims, acts, woffs, boffs)
+    pbf = flat_bf16 if flat_bf16 is not None and flat_bf16.data_ptr() != flat.data_ptr() else None
+    hip("ptg_mlp_train", x.data_ptr(), y.data_ptr(), flat.data_ptr(), m.data_ptr(), v.data_ptr(), ptr(pbf),
+        stats.data_ptr(), ctypes.addressof(desc), L, B, steps, loss_kind, lr, b1, b2, eps, t0)
+
+
 def adam_step(state, lr: float, b1: float, b2: float):
     """state[0] += 1; state[1] = bias-corrected step size (on the device)."""
     if not on_device(state):

@@ -318,3 +318,47 @@ def resize_norm(images_u8, out, H, W):
     out.zero_()
     out[..., :3] = y.permute(0, 2, 3, 1).to(out.dtype)
     return out
+
+
+def mlp_train(x, y, flat, m, v, flat_bf16, stats, dims, acts, woffs, boffs, steps, loss_kind, lr, b1, b2, eps, t0):
+    """fp32 oracle of mlp.hip's fused step (forward, softmax-xent / MSE, backward, Adam per step)."""
+    import math
+
+    L = len(dims) - 1
+    B = x.shape[0] // steps
+    for s in range(steps):
+        xs = _f(x[s * B:(s + 1) * B]).reshape(B, dims[0])
+        Ws = [flat[woffs[l]:woffs[l] + dims[l + 1] * dims[l]].view(dims[l + 1], dims[l]) for l in range(L)]
+        bs = [flat[boffs[l]:boffs[l] + dims[l + 1]] if boffs[l] >= 0 else None for l in range(L)]
+        a = [xs]
+        for l in range(L):
+            z = a[-1] @ Ws[l].t()
+            if bs[l] is not None:
+                z = z + bs[l]
+            if l < L - 1 and acts[l] == 1:
+                z = torch.relu(z)
+            a.append(z)
+        g = torch.empty_like(a[-1])
+        if loss_kind == 0:
+            softmax_xent(a[-1], y[s * B:(s + 1) * B], g, stats)
+        else:
+            mse(a[-1], y[s * B:(s + 1) * B].reshape(B, -1), g, stats)
+        t = t0 + s + 1
+        lr_t = lr * math.sqrt(1.0 - b2 ** t) / (1.0 - b1 ** t)
+        grads = []
+        for l in range(L - 1, -1, -1):
+            gw = g.t() @ a[l]
+            gb = g.sum(0)
+            if l > 0:
+                g = g @ Ws[l]
+                if acts[l - 1] == 1:
+                    g = g * (a[l] > 0).float()
+            grads.append((l, gw, gb))
+        for l, gw, gb in grads:
+            sl = slice(woffs[l], woffs[l] + gw.numel())
+            adam(flat[sl], gw.reshape(-1), m[sl], v[sl], None, lr_t, b1, b2, eps)
+            if boffs[l] >= 0:
+                sb = slice(boffs[l], boffs[l] + gb.numel())
+                adam(flat[sb], gb, m[sb], v[sb], None, lr_t, b1, b2, eps)
+    if flat_bf16 is not None and flat_bf16.data_ptr() != flat.data_ptr():
+        flat_bf16.copy_(flat.to(flat_bf16.dtype))

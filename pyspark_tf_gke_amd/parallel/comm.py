@@ -40,7 +40,7 @@ def init(backend: str | None = None, device_type: str | None = None, timeout_s: 
     rank, local, world = env_rank()
     if is_initialized():
         return dist.get_rank(), dist.get_world_size()
-    if world <= 1:
+    if world <= 1 and not config.get("force_pg"):
         return 0, 1
     if device_type is None:
         device_type = "cuda" if torch.cuda.is_available() else "cpu"
@@ -225,7 +225,15 @@ def all_gather_v(t: torch.Tensor) -> list:
 def all_gather_unique(t: torch.Tensor) -> torch.Tensor:
     """Sorted union of the per-rank distinct values of a 1-D tensor."""
     parts = all_gather_v(t)
-    return torch.unique(torch.cat(parts))
+    allv = torch.cat(parts)
+    if allv.is_cuda and allv.dtype == torch.int64:
+        from ..ops import df as D
+
+        # our kernels: sign-flipped orderable keys, distinct by hash aggregation, radix-sorted
+        stats = torch.empty(3, dtype=torch.int64, device=allv.device)
+        u, _ = D.key_prep(allv, D.TORCH_CT[torch.int64], None, False, stats)
+        return D.decode_sort_key(D.unique_sorted_u64(u), torch.int64, False)
+    return torch.unique(allv)
 
 
 def all_gather_bytes(blobs: list) -> list:

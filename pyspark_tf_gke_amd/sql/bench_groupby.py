@@ -55,12 +55,24 @@ def run(total_rows: int = 1_000_000_000, num_keys: int = 1_000_000, steps: int =
     if world > 1:
         total_c = int(comm.all_reduce_int([total_c])[0])
     ok = total_c == n * world
+    # value checksums against the input columns (reduced by a different kernel, in another order):
+    # sum over the groups of sum(value) == sum of every value; for dense keys also
+    # sum over the groups of key * count == sum of every key; and with >= 50 rows per key the
+    # number of groups is the number of distinct keys (P(a key is never drawn) ~ e^-50)
+    s_out = float(out._t.column("s").data.double().sum().item())
+    s_in = D.reduce_stats(vals, None, skip_nan=False)[0]
+    kw_out = 0.0 if sparse else float((out._t.column("key").data.double() * out._t.column("c").data.double()).sum().item())
+    kw_in = 0.0 if sparse else D.reduce_stats(keys, None, skip_nan=False)[0]
+    s_out, s_in, kw_out, kw_in = comm.all_reduce_float([s_out, s_in, kw_out, kw_in])
+    sums_ok = abs(s_out - s_in) <= 1e-9 * max(1.0, abs(s_in)) and abs(kw_out - kw_in) <= 1e-12 * max(1.0, abs(kw_in))
+    groups_ok = groups == num_keys if n * world >= 50 * num_keys else None
     return {"metric": "rows/sec Spark groupBy-aggregate", "value": round(n * world * steps / dt, 1), "unit": "rows/s",
             "ms_per_step": round(dt / steps * 1e3, 3),
             "config": {"model": "groupBy(key).agg(sum(value), count(*)) on (bigint key, double value)",
                        "rows_per_gpu": n, "global_rows": n * world, "distinct_keys": num_keys, "groups_out": groups,
                        "keys": "sparse (spread over int64)" if sparse else "dense [0, distinct_keys)",
-                       "counts_check": ok, "parallelism": f"{world} executors (1 per GPU), RCCL all-to-all-v shuffle"}}
+                       "counts_check": ok, "sums_check": bool(sums_ok), "groups_check": groups_ok,
+                       "parallelism": f"{world} executors (1 per GPU), RCCL all-to-all-v shuffle"}}
 
 
 def run_sort(rows_per_gpu: int = 1_000_000_000, steps: int = 3, warmup: int = 1, device=None,

@@ -18,6 +18,7 @@ import re
 
 import numpy as np
 import torch
+import torch.distributed as dist
 
 from ..ops import df as D
 from ..parallel import comm
@@ -483,8 +484,12 @@ class DataFrame:
             splitters = _range_splitters(k0 if null0 is None else k0[~null0], world)
             part, counts = D.range_partition(k0, splitters, world)
             if null0 is not None and bool(null0.any()):
-                part = torch.where(null0, torch.full_like(part, 0 if specs[0][1] else world - 1), part)
-                counts = torch.bincount(part.long(), minlength=world).to(torch.int64)
+                if part.is_cuda:
+                    D.part_override(part, null0, 0 if specs[0][1] else world - 1)
+                    counts = D.histogram(part, world)[:world]
+                else:
+                    part = torch.where(null0, torch.full_like(part, 0 if specs[0][1] else world - 1), part)
+                    counts = torch.bincount(part.long(), minlength=world).to(torch.int64)
             t = SH.shuffle_table(t, D.partition_perm(part, counts), counts)
         if t.num_rows == 0 or not specs:
             return self._new(t)
@@ -843,16 +848,115 @@ def _decode_key(k: torch.Tensor, src: ColumnVector, null: torch.Tensor | None = 
     return ColumnVector(v.to(src.data.dtype), src.dtype, valid)
 
 
+def _count_distinct(cv: ColumnVector) -> int:
+    """countDistinct of one column (nulls ignored, NaN a value) across ranks.  GPU: orderable keys
+    (key_prep), the valid rows compacted, distinct keys by hash aggregation without value columns,
+    the ranks' distinct sets merged the same way - only our kernels."""
+    world = comm.world_size()
+    if cv.data.is_cuda:
+        kt = _kt_of(cv)
+        stats = torch.empty(3, dtype=torch.int64, device=cv.data.device)
+        u, ok = D.key_prep(cv.data, kt, cv.valid, cv.valid is not None or kt == D.KT_CODE, stats)
+        if ok is not None:
+            u = D.gather_rows(u, D.compact(ok))
+        uk = D.hash_agg(u, [], [], est_keys=D.estimate_distinct(u) if u.numel() >= 65536 else None)[0]
+        if world > 1:
+            uk = D.hash_agg(torch.cat(comm.all_gather_v(uk)), [], [])[0]
+        return int(uk.numel())
+    k, null = _key_of(cv)
+    ok = cv.valid_bool() if null is None else (cv.valid_bool() & ~null)
+    loc = torch.unique(k[ok])
+    return int(comm.all_gather_unique(loc).numel()) if world > 1 else int(loc.numel())
+
+
 def _any_rank(flag: bool) -> bool:
     if comm.world_size() == 1:
         return flag
     return bool(comm.all_reduce_int([int(flag)])[0])
 
 
+def _kt_of(cv: ColumnVector) -> int:
+    if isinstance(cv.dtype, T.StringType):
+        return D.KT_CODE
+    return D.TORCH_CT[cv.data.dtype]
+
+
+def _group_keys_device(srcs: list):
+    """Device path of :func:`_group_keys` (csrc/kernels/dfkey.hip): every key column becomes an
+    orderable u64 key + valid flag + (min, max, nulls) in one kernel; the ranks agree on the ranges
+    (three small all-reduces); each column gets a bit field of the combined int64 key holding
+    (key - min), or its rank among the sorted distinct keys when the ranges do not fit 63 bits
+    together, plus one code for null.  Exact (no hashing), and decoding the result groups is one
+    kernel.  Returns None when even rank coding cannot fit (then the host-dictionary path runs)."""
+    n = srcs[0][1].data.shape[0]
+    dev = srcs[0][1].data.device
+    nc = len(srcs)
+    stats = torch.empty(3 * nc, dtype=torch.int64, device=dev)
+    cols = []
+    for j, (name, cv) in enumerate(srcs):
+        kt = _kt_of(cv)
+        maybe_null = cv.valid is not None or kt == D.KT_CODE
+        u, ok = D.key_prep(cv.data, kt, cv.valid, maybe_null, stats[3 * j:3 * j + 3])
+        cols.append({"name": name, "cv": cv, "u": u, "ok": ok, "lut": None, "type": kt})
+    st = [x & ((1 << 64) - 1) for x in stats.cpu().tolist()]  # u64 bit patterns
+    world = comm.world_size()
+    if world > 1:  # orderable u64 -> signed order for the int64 collectives
+        sg = lambda x: x - (1 << 63)  # noqa: E731
+        mins = comm.all_reduce_int([sg(st[3 * j]) for j in range(nc)], op=dist.ReduceOp.MIN)
+        maxs = comm.all_reduce_int([sg(st[3 * j + 1]) for j in range(nc)], op=dist.ReduceOp.MAX)
+        nulls = comm.all_reduce_int([st[3 * j + 2] for j in range(nc)])
+        for j in range(nc):
+            st[3 * j], st[3 * j + 1], st[3 * j + 2] = mins[j] + (1 << 63), maxs[j] + (1 << 63), nulls[j]
+    for j, c in enumerate(cols):
+        lo, hi, nn = st[3 * j], st[3 * j + 1], st[3 * j + 2]
+        empty = lo > hi  # every row null (or no rows)
+        c["lo"] = 0 if empty else lo
+        c["nvals"] = 0 if empty else hi - lo + 1
+        c["has_null"] = nn > 0
+        if not c["has_null"]:
+            c["ok"] = None
+    def bits_of(c):
+        return max(1, (c["nvals"] + int(c["has_null"]) - 1).bit_length())
+    # columns whose value range is too wide for the 63-bit budget switch to rank coding, widest first
+    while sum(bits_of(c) for c in cols) > 63:
+        wide = [c for c in cols if c["lut"] is None and c["nvals"] > 1]
+        if not wide:
+            return None
+        c = max(wide, key=lambda q: q["nvals"])
+        u = c["u"] if c["ok"] is None else D.gather_rows(c["u"], D.compact(c["ok"]))
+        lut = D.unique_sorted_u64(u)
+        if world > 1:
+            lut = D.unique_sorted_u64(torch.cat(comm.all_gather_v(lut)))
+        c["lut"], c["lo"], c["nvals"] = lut, 0, int(lut.numel())
+    shift = 0
+    for c in cols:
+        c["bits"] = bits_of(c)
+        c["shift"] = shift
+        c["nullcode"] = c["nvals"]
+        shift += c["bits"]
+    key, desc = D.key_pack(cols, n, dev)
+
+    def decode(kk):
+        m = kk.numel()
+        outs, res = [], {}
+        for c in cols:
+            cv = c["cv"]
+            data = torch.empty(m, dtype=torch.int32 if c["type"] == D.KT_CODE else cv.data.dtype, device=dev)
+            valid = torch.empty(m, dtype=torch.uint8, device=dev) if c["has_null"] else None
+            outs.append((data.view(torch.uint8) if data.dtype == torch.bool else data, valid))
+            res[c["name"]] = ColumnVector(data, cv.dtype, valid, cv.dictionary)
+        if m:
+            D.key_unpack(kk.contiguous(), desc, outs)
+        return res
+
+    return key, decode
+
+
 def _group_keys(df: "DataFrame", cols: list):
-    """-> (int64 combined key per row, decode(keys) -> {name: ColumnVector}).  A single non-null
-    column is its own key; otherwise (several columns, or nulls) every column is mapped to a dense
-    code over the global set of its distinct values (+1 code for null), and the codes are combined
+    """-> (int64 combined key per row, decode(keys) -> {name: ColumnVector}).  A single null-free
+    int64 column is its own key.  On the GPU every other case packs the columns into one exact key
+    on the device (:func:`_group_keys_device`); on the host every column is mapped to a dense code
+    over the global set of its distinct values (+1 code for null), and the codes are combined
     mixed-radix (exact, no hash collisions)."""
     srcs = []
     for c in cols:
@@ -860,6 +964,14 @@ def _group_keys(df: "DataFrame", cols: list):
         srcs.append((name, cv))
     if not srcs:
         return torch.zeros(df._t.num_rows, dtype=torch.int64, device=df._t.device), lambda kk: {}
+    cv0 = srcs[0][1]
+    if cv0.data.is_cuda:
+        plain = (len(srcs) == 1 and cv0.data.dtype == torch.int64 and not isinstance(cv0.dtype, T.StringType)
+                 and not _any_rank(cv0.valid is not None))
+        if not plain:
+            r = _group_keys_device(srcs) if len(srcs) <= D.KMAX else None
+            if r is not None:
+                return r
     keyed = [(name, cv) + _key_of(cv) for name, cv in srcs]
     if len(keyed) == 1 and not _any_rank(keyed[0][3] is not None):
         name, cv, k, _ = keyed[0]
@@ -1030,10 +1142,7 @@ class GroupedData:
             _, cv = evalf(src)
             cv = masked(cv)
             if fn == "count_distinct":
-                k, null = _key_of(cv)
-                ok = cv.valid_bool() if null is None else (cv.valid_bool() & ~null)
-                loc = torch.unique(k[ok])
-                vals[label] = int(comm.all_gather_unique(loc).numel()) if world > 1 else int(loc.numel())
+                vals[label] = _count_distinct(cv)
                 continue
             s_, c, mn, mx, nul = _global_stats(cv)
             if fn == "count":
@@ -1076,9 +1185,7 @@ class GroupedData:
                     continue
                 _, cv = df._eval(src)
                 if fn == "count_distinct":
-                    k, null = _key_of(cv)
-                    loc = torch.unique(k if null is None else k[~null])
-                    vals[label] = int(comm.all_gather_unique(loc).numel()) if world > 1 else int(loc.numel())
+                    vals[label] = _count_distinct(cv)
                     continue
                 if fn == "first":
                     vals[label] = df.select(src).first()[0] if df.count() else None
@@ -1161,6 +1268,8 @@ class GroupedData:
                 ukeys, rows = ukeys[:0], rows[:0]
                 outs = [tuple(x[:0] for x in o) for o in outs]
         cols = dict(decode(ukeys))
+        if ukeys.is_cuda:
+            return df._new(Table(self._finalize_device(cols, aggs, value_cols, rows, outs), ukeys.numel(), t.device))
         j = 0
         for label, fn, src in aggs:
             if src is None:
@@ -1189,6 +1298,53 @@ class GroupedData:
                 raise ValueError(f"unsupported grouped aggregate {fn}")
         return df._new(Table(cols, ukeys.numel(), t.device))
 
+    @staticmethod
+    def _finalize_device(cols, aggs, value_cols, rows, outs) -> dict:
+        """Result columns of a keyed aggregation in one kernel (dfkey.hip agg_finalize_k): counts,
+        integral sums and min / max keep their integer types, null where a group had no value."""
+        m = rows.numel()
+        dev = rows.device
+        specs = []
+        j = 0
+        for label, fn, src in aggs:
+            if src is None:
+                out = torch.empty(m, dtype=torch.int64, device=dev)
+                specs.append(("rows", 3, None, None, None, None, out, None))
+                cols[label] = ColumnVector(out, T.LongType())
+                continue
+            s_, c_, mn, mx = outs[j]
+            srct = value_cols[j].dtype
+            j += 1
+            integral = isinstance(srct, (T.IntegerType, T.LongType, T.BooleanType))
+            valid = torch.empty(m, dtype=torch.uint8, device=dev)
+            if fn == "count":
+                out = torch.empty(m, dtype=torch.int64, device=dev)
+                specs.append(("count", 3, s_, c_, mn, mx, out, None))
+                cols[label] = ColumnVector(out, T.LongType())
+            elif fn == "sum":
+                out = torch.empty(m, dtype=torch.int64 if integral else torch.float64, device=dev)
+                specs.append(("sum_int" if integral else "sum", 3 if integral else 1, s_, c_, mn, mx, out, valid))
+                cols[label] = ColumnVector(out, T.LongType() if integral else T.DoubleType(), valid)
+            elif fn == "avg":
+                out = torch.empty(m, dtype=torch.float64, device=dev)
+                specs.append(("avg", 1, s_, c_, mn, mx, out, valid))
+                cols[label] = ColumnVector(out, T.DoubleType(), valid)
+            elif fn in ("min", "max"):
+                if isinstance(srct, (T.IntegerType, T.LongType)):
+                    tdt = _TORCH_OF[type(srct)]
+                    out = torch.empty(m, dtype=tdt, device=dev)
+                    specs.append((fn, D.TORCH_CT[tdt], s_, c_, mn, mx, out, valid))
+                    cols[label] = ColumnVector(out, srct, valid)
+                else:
+                    out = torch.empty(m, dtype=torch.float64, device=dev)
+                    specs.append((fn, 1, s_, c_, mn, mx, out, valid))
+                    cols[label] = ColumnVector(out, T.DoubleType(), valid)
+            else:
+                raise ValueError(f"unsupported grouped aggregate {fn}")
+        if m and specs:
+            D.agg_finalize(rows, specs)
+        return cols
+
     def _first_rows(self) -> DataFrame:
         df = self.df
         t = df._t
@@ -1197,6 +1353,14 @@ class GroupedData:
             t = _shuffle_by_key(t, key)
             df = df._new(t)
             key, _ = _group_keys(df, self.cols)
+        if key.is_cuda:
+            # first row of every group: min row id per key (hash aggregation), ids sorted by our
+            # radix sort, rows gathered - dropDuplicates keeps the input order of the survivors
+            ridx = D.iota_f64(t.num_rows, t.device)
+            _, _, rep = _hash_agg_all(key, [ridx], [None], True)
+            ids = D.f64_to_i64(rep[0][2])
+            idx, _ = D.radix_sort_u64(ids, None, 0, max(t.num_rows - 1, 0))
+            return df._new(t.take(idx))
         ridx = torch.arange(t.num_rows, dtype=torch.float64, device=t.device)
         _, _, rep = _hash_agg_all(key, [ridx], [None], True)
         idx = torch.sort(rep[0][2].long()).values
@@ -1239,9 +1403,15 @@ def _hash_agg_all(key, vals, valids, want_minmax):
     outs = []
     for i in range(0, len(vals), 4):
         k, r, o = fn(key, vals[i:i + 4], valids[i:i + 4], want_minmax)
-        order = torch.argsort(k)
-        k, r = k[order], r[order]
-        o = [tuple(x[order] for x in q) for q in o]
+        # every pass yields the same key set: one radix sort each (any consistent order aligns them)
+        if k.is_cuda:
+            k, order = D.radix_sort_u64(k, None, 0, D._U64, row_payload=True)
+            r = D.gather_rows(r, order)
+            o = [tuple(D.gather_rows(x, order) for x in q) for q in o]
+        else:
+            order = torch.argsort(k)
+            k, r = k[order], r[order]
+            o = [tuple(x[order] for x in q) for q in o]
         if uk is None:
             uk, rows = k, r
         outs += o

@@ -125,9 +125,14 @@ def round_robin_shuffle(t: Table, budget: int | None = None) -> Table:
     """repartition(n) without columns: spread this rank's rows evenly over all ranks."""
     world = comm.world_size()
     n = t.num_rows
-    part = (torch.arange(n, dtype=torch.int64, device=t.device) + comm.rank()) % world
-    part = part.to(torch.int32)
-    counts = torch.bincount(part.long(), minlength=world).to(torch.int64)
+    rank = comm.rank()
+    # row i -> (i + rank) % world; the counts follow in closed form (no histogram pass)
+    counts = torch.tensor([(n - ((p - rank) % world) + world - 1) // world for p in range(world)], dtype=torch.int64)
+    if t.device.type == "cuda":
+        part = D.rr_part(n, rank, world, t.device)
+        counts = counts.to(t.device)
+    else:
+        part = ((torch.arange(n, dtype=torch.int64) + rank) % world).to(torch.int32)
     perm = D.partition_perm(part, counts)
     return shuffle_table(t, perm, counts, budget)
 

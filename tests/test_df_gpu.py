@@ -662,3 +662,92 @@ def test_digit_offsets_512_bins(ntiles):
     out = offs.cpu()
     assert torch.equal(out[:-1], ref)
     assert int(out[-1]) == int(hist.long().sum())
+
+
+# ---- multi-column / nullable group keys on our kernels (dfkey.hip) vs pandas -----------------------
+def _pd_health():
+    import pandas as pd
+
+    return pd.read_csv(HEALTH)
+
+
+def test_groupby_two_nullable_keys_vs_pandas(spark_gpu):
+    """groupBy(measure_name, subpopulation) on health.csv: `subpopulation` has 1,508 empty values
+    (null in Spark), so the key is a 2-column nullable tuple packed into one exact int64 key."""
+    from pyspark_tf_gke_amd.sql.functions import avg, count, max as fmax, min as fmin, sum as fsum
+
+    df = spark_gpu.read.csv(HEALTH, header=True, inferSchema=True)
+    g = df.groupBy("measure_name", "subpopulation").agg(
+        count("*").alias("n"), count("value").alias("nv"), avg("value").alias("m"), fsum("value").alias("s"),
+        fmin("value").alias("lo"), fmax("upper_ci").alias("hi"))
+    got = {(r["measure_name"], r["subpopulation"]): (r["n"], r["nv"], r["m"], r["s"], r["lo"], r["hi"])
+           for r in g.collect()}
+    p = _pd_health()
+    ref = {}
+    for (mn, sp), grp in p.groupby(["measure_name", "subpopulation"], dropna=False):
+        sp = None if isinstance(sp, float) and math.isnan(sp) else sp
+        v = grp["value"].dropna()
+        ref[(mn, sp)] = (len(grp), len(v), v.mean() if len(v) else None, v.sum() if len(v) else None,
+                         v.min() if len(v) else None, grp["upper_ci"].max())
+    assert set(got) == set(ref)
+    assert any(k[1] is None for k in got)  # the null group exists
+    for k, (n, nv, m, s, lo, hi) in ref.items():
+        g_ = got[k]
+        assert g_[0] == n and g_[1] == nv, (k, g_, ref[k])
+        for a, b in zip(g_[2:], (m, s, lo, hi)):
+            assert (a is None and (b is None or b != b)) or math.isclose(a, b, rel_tol=1e-9, abs_tol=1e-9), (k, g_, ref[k])
+
+
+def test_groupby_three_keys_wide_ranges_vs_host(spark_gpu):
+    """Three key columns whose value ranges cannot share 63 bits (two full-range int64 columns):
+    the widest switch to rank coding (sorted distinct keys, binary search in the pack kernel)."""
+    from pyspark_tf_gke_amd.sql.functions import count, sum as fsum
+    from pyspark_tf_gke_amd.sql.session import SparkSession
+
+    rng = np.random.default_rng(3)
+    n = 50_000
+    a = rng.integers(-(1 << 62), 1 << 62, 40)[rng.integers(0, 40, n)]
+    b = rng.integers(-(1 << 62), 1 << 62, 30)[rng.integers(0, 30, n)]
+    c = rng.integers(0, 5, n)
+    v = rng.normal(size=n)
+    rows = [(int(x), int(y), int(z), float(w)) for x, y, z, w in zip(a, b, c, v)]
+
+    def run(spark):
+        df = spark.createDataFrame(rows, ["a", "b", "c", "v"])
+        out = df.groupBy("a", "b", "c").agg(count("*").alias("n"), fsum("v").alias("s")).collect()
+        return sorted((r["a"], r["b"], r["c"], r["n"], round(r["s"], 9)) for r in out)
+
+    assert run(spark_gpu) == _host(run)
+
+
+def test_count_distinct_and_drop_duplicates_vs_pandas(spark_gpu):
+    from pyspark_tf_gke_amd.sql.functions import countDistinct
+
+    df = spark_gpu.read.csv(HEALTH, header=True, inferSchema=True)
+    p = _pd_health()
+    got = df.agg(countDistinct("subpopulation").alias("a"), countDistinct("value").alias("b"),
+                 countDistinct("state_name").alias("c")).collect()[0]
+    assert got["a"] == p["subpopulation"].nunique() and got["c"] == p["state_name"].nunique()
+    assert got["b"] == p["value"].nunique()
+    dd = df.dropDuplicates(["measure_name", "subpopulation"]).collect()
+    ref = p.drop_duplicates(["measure_name", "subpopulation"])
+    assert len(dd) == len(ref)
+    # the surviving rows are the first occurrences, in input order
+    assert [r["edition"] for r in dd] == ref["edition"].tolist()
+    assert [r["measure_name"] for r in dd] == ref["measure_name"].tolist()
+    assert df.select("measure_name", "subpopulation").distinct().count() == len(ref)
+
+
+def test_groupby_more_than_four_value_columns(spark_gpu):
+    from pyspark_tf_gke_amd.sql.functions import avg, max as fmax, sum as fsum
+
+    df = spark_gpu.read.csv(HEALTH, header=True, inferSchema=True)
+    g = df.groupBy("state_name").agg(fsum("value").alias("s1"), avg("lower_ci").alias("a2"), fmax("upper_ci").alias("m3"),
+                                     fsum("lower_ci").alias("s4"), avg("value").alias("a5"), fmax("value").alias("m6"))
+    got = {r["state_name"]: r for r in g.collect()}
+    p = _pd_health()
+    for st, grp in p.groupby("state_name"):
+        r = got[st]
+        for name, ref in (("s1", grp["value"].sum()), ("a2", grp["lower_ci"].mean()), ("m3", grp["upper_ci"].max()),
+                          ("s4", grp["lower_ci"].sum()), ("a5", grp["value"].mean()), ("m6", grp["value"].max())):
+            assert math.isclose(r[name], ref, rel_tol=1e-9, abs_tol=1e-9), (st, name, r[name], ref)

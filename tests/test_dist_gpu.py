@@ -1,0 +1,304 @@
+"""The reference's distributed training modes on the GPU box (train_tf_ps.py:505-510, 612-645,
+734-765), with ranks sharing the one MI355X the way ``tests/test_ipc_gpu.py`` does (gloo process
+group for control; HIP IPC maps another process's allocation on the same device exactly as it maps a
+peer GPU's over xGMI):
+
+* asynchronous ParameterServerStrategy: HIP-IPC windows, gradient pushes into the owners' inbox
+  slots and pulls by ``ptg_piece_copy`` with system-scope loads, each owner's service thread applying
+  Adam on its own HIP stream while its main thread runs closures;
+* a straggler under async dispatch, and failed closures rescheduled on other workers;
+* synchronous PS with 3 ranks on device, including coordinator retries of ``next(iterator)``
+  closures (bit-identical to the fault-free run);
+* a 1-rank RCCL process group running MultiWorkerMirroredStrategy's sharded update for real:
+  ``reduce_scatter_tensor`` / ``all_gather_into_tensor`` with ``async_op=True`` issued from the
+  side stream (nn/streams.py) must give the replicated update's parameters;
+* a GradientTape loop whose first ``apply_gradients`` builds a fresh Adam on the overlap path.
+"""
+import json
+import os
+import subprocess
+import sys
+import textwrap
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _launch(body: str, nproc: int, extra_env=None, timeout=240):
+    env = dict(os.environ)
+    env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    env["PTG_DIST_BACKEND"] = "gloo"  # RCCL refuses two ranks on one device
+    env.pop("WORLD_SIZE", None)
+    env.update(extra_env or {})
+    cmd = [sys.executable, "-m", "pyspark_tf_gke_amd.runtime.launcher", "--nproc", str(nproc), "--",
+           sys.executable, "-c", textwrap.dedent(body)]
+    return subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout, cwd=ROOT)
+
+
+def _results(out: str):
+    res = {}
+    for line in out.splitlines():
+        if "RESULT " in line:
+            rank = int(line.split("]")[0].replace("[rank", ""))
+            res[rank] = json.loads(line.split("RESULT ", 1)[1])
+    return res
+
+
+COMMON = """
+import json, os, time, torch, numpy as np
+from pyspark_tf_gke_amd import nn
+from pyspark_tf_gke_amd.distribute import ParameterServerStrategy, ClusterCoordinator
+from pyspark_tf_gke_amd.distribute.cluster import MinSizePartitioner
+from pyspark_tf_gke_amd.models import build_deep_model
+from pyspark_tf_gke_amd.nn.tape import GradientTape
+from pyspark_tf_gke_amd.nn import engine as E
+rng = np.random.default_rng(0)
+DEV = torch.device("cuda", torch.cuda.current_device())
+X = torch.from_numpy(rng.normal(size=(16, 64, 3)).astype(np.float32)).to(DEV)
+Y = torch.from_numpy(rng.integers(0, 4, size=(16, 64)).astype(np.int32)).to(DEV)
+loss_fn = nn.losses.SparseCategoricalCrossentropy()
+
+def make(st, lr=1e-2):
+    with st.scope():
+        m = build_deep_model(3, 4)
+        opt = nn.optimizers.Adam(lr)
+    return m, opt
+
+def step_fn(m, opt, i):
+    with GradientTape() as tape:
+        out = m(X[i], training=True)
+        loss = loss_fn(Y[i], out)
+    grads = tape.gradient(loss, m.trainable_variables)
+    opt.apply_gradients(zip(grads, m.trainable_variables))
+    return 1
+
+def ref_steps(ref, ro, idx):
+    for i in idx:
+        ref.store.grad_clean = False
+        ref.store.zero_grad()
+        out = E.run_forward(ref.ops, X[i], ref.ws, True)
+        d = ref._loss_grad(out, Y[i], torch.zeros(8, device=DEV))
+        E.run_backward(ref.ops, d, ref.ws)
+        ro.apply(ref.store, gscale=1.0)
+    torch.cuda.synchronize()
+"""
+
+
+def test_async_ps_on_gpu_is_sequential_adam(hip_built):
+    """Rank 1 arrives late, so rank 0 draws every closure.  Both ranks own shards (4-way partitioned
+    variables): every push goes one-sided into both owners' HIP-IPC inbox slots, both service
+    threads apply it on their own streams, and the next closure pulls both owners' bf16 values with
+    system-scope loads - so 8 closures equal 8 sequential Adam steps of the same kernels."""
+    body = COMMON + """
+st = ParameterServerStrategy(mode="async", variable_partitioner=MinSizePartitioner(min_shard_bytes=256, max_shards=4))
+m, o = make(st, lr=5e-3)
+ref, ro = make(st, lr=5e-3)
+co = ClusterCoordinator(st)
+for i in range(8):
+    co.schedule(step_fn, args=(m, o, i))
+if st.rank == 1:
+    time.sleep(2.0)
+co.join()
+st.synchronize_master(m)
+ref_steps(ref, ro, range(8))
+diff = float((m.store.flat - ref.store.flat).abs().max())
+scale = float(ref.store.flat.abs().max())
+owners = sorted({p[3] for p in st.placement(m)})
+print("RESULT", json.dumps({"diff": diff, "scale": scale, "it": o.iterations, "ran": co.closures_run,
+                            "owners": owners, "cuda": m.store.flat.is_cuda}), flush=True)
+st.shutdown()
+"""
+    r = _launch(body, 2)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    res = _results(r.stdout)
+    assert len(res) == 2, r.stdout[-2000:]
+    assert res[0]["ran"] == 8 and res[1]["ran"] == 0 and res[0]["owners"] == [0, 1], res
+    for v in res.values():
+        assert v["cuda"] and v["it"] == 8, v
+        assert v["diff"] <= 1e-5 * max(1.0, v["scale"]), v
+
+
+def test_async_ps_on_gpu_straggler_and_rescheduled_failures(hip_built):
+    """3 ranks on the GPU: rank 2 sleeps 100 ms per closure and rank 1 fails every third closure it
+    draws (before the push).  The failures go to the other workers, the straggler runs few closures,
+    every closure updates the model exactly once and every result is visible on every rank."""
+    body = COMMON + """
+st = ParameterServerStrategy(mode="async")
+m, o = make(st, lr=1e-3)
+co = ClusterCoordinator(st, max_retries=2)
+calls = [0]
+def closure(i):
+    calls[0] += 1
+    if st.rank == 2:
+        time.sleep(0.1)
+    if st.rank == 1 and calls[0] % 3 == 0:
+        raise RuntimeError("injected failure on worker 1")
+    step_fn(m, o, i % 16)
+    return i
+from pyspark_tf_gke_amd.parallel import comm
+comm.barrier()
+t0 = time.time()
+rvs = [co.schedule(closure, args=(i,)) for i in range(30)]
+co.join()
+dt = time.time() - t0
+st.synchronize_master(m)
+finite = bool(torch.isfinite(m.store.flat).all())
+print("RESULT", json.dumps({"dt": dt, "ran": co.closures_run, "it": o.iterations, "retries": co.retries,
+                            "vals": [rv.fetch() for rv in rvs], "finite": finite,
+                            "sum": float(m.store.flat.double().sum())}), flush=True)
+st.shutdown()
+"""
+    r = _launch(body, 3)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    res = _results(r.stdout)
+    assert len(res) == 3, r.stdout[-2000:]
+    assert sum(v["ran"] for v in res.values()) == 30, res
+    assert res[2]["ran"] < min(res[0]["ran"], res[1]["ran"]), res
+    assert res[1]["retries"] >= 1, res
+    for v in res.values():
+        assert v["vals"] == list(range(30)) and v["it"] == 30 and v["finite"], v
+    assert len({round(v["sum"], 6) for v in res.values()}) == 1, res  # same final parameters everywhere
+
+
+def test_sync_ps_three_ranks_on_gpu_retry_bit_identical(hip_built):
+    """Sync PS on device with 3 ranks (packed reduce-scatter push, bf16 + fp32 all-gather pulls,
+    owner Adam on packed shards): the reference's ``next(iterator)`` closures, with rank 1 failing
+    two of its calls, give bit-identical parameters to the fault-free run, and only the failed
+    closures ran twice."""
+    body = COMMON + """
+from pyspark_tf_gke_amd.data.dataset import Dataset
+XA = torch.from_numpy(rng.normal(size=(192, 3)).astype(np.float32))
+YA = torch.from_numpy(rng.integers(0, 4, size=(192,)).astype(np.int32))
+def run(fail_calls):
+    st = ParameterServerStrategy(variable_partitioner=MinSizePartitioner(min_shard_bytes=256, max_shards=3))
+    m, o = make(st)
+    co = ClusterCoordinator(st, max_retries=2)
+    ds = co.create_per_worker_dataset(
+        lambda ctx: Dataset.from_tensor_slices((XA, YA)).shard(ctx.num_input_pipelines, ctx.input_pipeline_id).batch(16).repeat())
+    it = iter(ds)
+    calls = [0]
+    def per_worker_train_step(iterator):
+        calls[0] += 1
+        if st.rank == 1 and calls[0] in fail_calls:
+            raise RuntimeError("injected worker failure")
+        x, y = next(iterator)
+        with GradientTape() as tape:
+            loss = loss_fn(y.to(DEV), m(x.to(DEV), training=True))
+        o.apply_gradients(zip(tape.gradient(loss, m.trainable_variables), m.trainable_variables))
+        return 1
+    for epoch in range(2):
+        for _ in range(6):
+            co.schedule(per_worker_train_step, args=(it,))
+        co.join()
+    st.synchronize_master(m)
+    return m.store.flat.clone(), co.retries, calls[0], o.iterations, m.store.flat.is_cuda
+a, _, ca, ia, cuda = run(set())
+b, rb, cb, ib, _ = run({2, 4})
+print("RESULT", json.dumps({"same": bool(torch.equal(a, b)), "retries": rb, "calls": [ca, cb], "it": [ia, ib],
+                            "cuda": cuda}), flush=True)
+"""
+    r = _launch(body, 3)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    res = _results(r.stdout)
+    assert len(res) == 3, r.stdout[-2000:]
+    for rank, v in res.items():
+        assert v["cuda"] and v["same"], v
+        assert v["retries"] == 2 and v["it"] == [4, 4], v
+        assert v["calls"][1] == v["calls"][0] + (2 if rank == 1 else 0), v
+
+
+RCCL_BODY = """
+import json, torch
+from pyspark_tf_gke_amd.distribute import MultiWorkerMirroredStrategy
+from pyspark_tf_gke_amd.models import build_cnn_model
+from pyspark_tf_gke_amd.parallel import comm
+import torch.distributed as dist
+st_s = MultiWorkerMirroredStrategy(sharded_update=True, bucket_mb=1.0)
+st_p = MultiWorkerMirroredStrategy(sharded_update=False)
+dev = st_s.device
+g = torch.Generator().manual_seed(11)
+X = torch.rand(4, 16, 64, 80, 3, generator=g)
+Y = torch.rand(4, 16, 2, generator=g) * 60
+models = {}
+for name, st in (("sharded", st_s), ("plain", st_p)):
+    with st.scope():
+        models[name] = build_cnn_model((64, 80, 3), flat=True, summary=False, device=dev)
+ms, mp = models["sharded"], models["plain"]
+calls = {"rs": 0, "ag": 0}
+orig_rs, orig_ag = comm.reduce_scatter_flat, comm.all_gather_flat
+def rs(*a, **k):
+    calls["rs"] += 1
+    assert k.get("async_op"), "bucket reduce-scatter must be asynchronous"
+    return orig_rs(*a, **k)
+def ag(*a, **k):
+    calls["ag"] += 1
+    return orig_ag(*a, **k)
+comm.reduce_scatter_flat, comm.all_gather_flat = rs, ag
+for i in range(4):
+    for m in (ms, mp):
+        xb, yb = m._prep_batch(X[i], Y[i])
+        stats = m._stats_buf()
+        stats.zero_()
+        m.train_step_fast(xb, yb, stats)
+st_s.synchronize_master(ms)
+torch.cuda.synchronize()
+diff = max(float((p.data - mp.store.by_name(p.name).data).abs().max()) for p in ms.store.params)
+scale = max(float(p.data.abs().max()) for p in mp.store.params)
+print("RESULT", json.dumps({"backend": dist.get_backend(), "world": dist.get_world_size(), "sharded": st_s.sharded_update,
+                            "buckets": len(ms._shard_plan.buckets), "calls": calls, "diff": diff, "scale": scale}),
+      flush=True)
+"""
+
+
+def test_single_rank_rccl_sharded_update_matches_replicated(hip_built):
+    """A real 1-rank RCCL group (PTG_FORCE_PG, backend nccl): the sharded update's per-bucket
+    reduce-scatters (async, from the side stream) and bf16 / fp32 all-gathers run as RCCL kernels,
+    and four CNN steps give the replicated update's parameters."""
+    env = dict(os.environ)
+    env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    env.update({"PTG_FORCE_PG": "1", "PTG_SHARD_WORLD1": "1", "RANK": "0", "WORLD_SIZE": "1", "LOCAL_RANK": "0",
+                "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": "29653"})
+    env.pop("PTG_DIST_BACKEND", None)
+    r = subprocess.run([sys.executable, "-c", textwrap.dedent(RCCL_BODY)], env=env, capture_output=True, text=True,
+                       timeout=240, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    v = [json.loads(line.split("RESULT ", 1)[1]) for line in r.stdout.splitlines() if "RESULT " in line][0]
+    assert v["backend"] == "nccl" and v["world"] == 1 and v["sharded"] and v["buckets"] > 2, v
+    assert v["calls"]["rs"] >= 4 * v["buckets"] and v["calls"]["ag"] >= 4 * v["buckets"], v
+    assert v["diff"] <= 1e-4 * max(1.0, v["scale"]), v
+
+
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
+def test_tape_overlap_with_fresh_adam_matches_serial(hip_built):
+    """the first apply_gradients of a fresh Adam on the overlap path builds the moments on
+    the step's stream before the aux stream reads them.  CNN-B1-shaped model (big Dense on the aux
+    stream) vs the same loop with the overlap off."""
+    from pyspark_tf_gke_amd import nn
+    from pyspark_tf_gke_amd.models import build_cnn_model
+    from pyspark_tf_gke_amd.nn import tape as T
+
+    g = torch.Generator().manual_seed(5)
+    X = (torch.rand(3, 16, 64, 80, 3, generator=g)).cuda()
+    Y = (torch.rand(3, 16, 2, generator=g) * 60).cuda()
+    flats = []
+    for overlap in (True, False):
+        T.OVERLAP = overlap
+        try:
+            torch.manual_seed(3)
+            m = build_cnn_model((64, 80, 3), flat=True, summary=False, device="cuda")
+            opt = nn.optimizers.Adam(1e-3)  # unbuilt: its first apply allocates m / v
+            loss_fn = nn.losses.MeanSquaredError()
+            for i in range(3):
+                with T.GradientTape() as tape:
+                    loss = loss_fn(Y[i], m(X[i], training=True))
+                opt.apply_gradients(zip(tape.gradient(loss, m.trainable_variables), m.trainable_variables))
+            torch.cuda.synchronize()
+            flats.append(m.store.flat.clone())
+        finally:
+            T.OVERLAP = True
+    a, b = flats
+    assert torch.isfinite(a).all()
+    assert float((a - b).abs().max()) <= 1e-4 * max(1.0, float(b.abs().max()))

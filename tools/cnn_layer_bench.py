@@ -71,6 +71,11 @@ def main():
             wf = torch.empty((C, 5, 5, Co), device=dev, dtype=torch.bfloat16)
             ops_[f"dgrad{li}"] = (lambda dz=dz, w=w, dx=dx, wf=wf: ops.conv2d_dgrad_halo(dz, w, 2, dx, wf),
                                   dz.numel() * 2 + dx.numel() * 2)
+            # the implicit-GEMM path of gemm.hip for the same dgrad / forward (A/B reference)
+            ops_[f"dgradG{li}"] = (lambda dz=dz, w=w, dx=dx: ops.conv2d_dgrad(dz, w, 2, dx),
+                                   dz.numel() * 2 + dx.numel() * 2)
+            ops_[f"fwdG{li}"] = (lambda x=x, w=w, b=b, z=z: ops.conv2d_fwd(x, w, b, 1, 2, z),
+                                 x.numel() * 2 + z.numel() * 2)
         for name, (fn, nbytes) in ops_.items():
             if only and name not in only:
                 continue

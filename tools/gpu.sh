@@ -106,6 +106,11 @@ for task in "$@"; do
         --master-addr 127.0.0.1 --master-port 29641 workloads/joint/etl_to_train.py --rows ${JOINT_ROWS:-5000000} \
         --out /tmp/joint2 --epochs 2 --batch-size 8192 > gpurun_out/joint2.log 2>&1 || fail joint2 gpurun_out/joint2.log
       tail -4 gpurun_out/joint2.log | cut -c1-300 ;;
+    psmodes)
+      # psmodes[:<nproc>]: the reference's PS loop, sync vs async, N ranks sharing the GPU (gloo control)
+      PTG_DIST_BACKEND=gloo timeout -k 10 $STEP_T python -m pyspark_tf_gke_amd.runtime.launcher --nproc ${arg:-2} -- \
+        python tools/ps_modes_bench.py $PY_ARGS > gpurun_out/psmodes_${arg:-2}.log 2>&1 || fail psmodes gpurun_out/psmodes_${arg:-2}.log
+      grep '"mode"' gpurun_out/psmodes_${arg:-2}.log | cut -c1-400 ;;
     py)
       out=gpurun_out/$(basename "$arg" .py).log
       timeout -k 10 $STEP_T python $arg $PY_ARGS > "$out" 2>&1 || fail "py $arg" "$out"
