@@ -65,19 +65,45 @@ __global__ void key_stats_init_k(unsigned long long* st) {
   if (threadIdx.x == 0) { st[0] = ~0ULL; st[1] = 0ULL; st[2] = 0ULL; }
 }
 
-// stats: [min, max, nulls] over the column (min / max over non-null rows)
-__global__ __launch_bounds__(256) void key_prep_k(const void* __restrict__ col, int type,
+// The hash tables of df.hip reserve INT64_MIN as their empty key, and the orderable form maps int 0
+// and +0.0 there.  Keys that feed a hash aggregation use the RAW canonical form instead: the int64
+// value, the dictionary code, or the canonical double's bits (NaN canonical, -0 -> +0, so the bits
+// are never INT64_MIN); mode 2 turns raw canonical keys of the column's type into the orderable form.
+PTG_DEV unsigned long long raw_of_orderable(unsigned long long u, int type) {
+  switch (type) {
+    case KT_F32:
+    case KT_F64: return (u >> 63) ? (u & ~SIGN) : ~u;
+    case KT_CODE:
+    case KT_U8: return u;
+    default: return u ^ SIGN;
+  }
+}
+PTG_DEV unsigned long long orderable_of_raw(unsigned long long r, int type) {
+  switch (type) {
+    case KT_F32:
+    case KT_F64: return (r >> 63) ? ~r : (r | SIGN);
+    case KT_CODE:
+    case KT_U8: return r;
+    default: return r ^ SIGN;
+  }
+}
+
+// mode 0: orderable keys; 1: raw canonical keys; 2: `col` holds raw canonical int64 keys of `type`,
+// out = their orderable form.  stats: [min, max, nulls] of the orderable keys (mode 0)
+__global__ __launch_bounds__(256) void key_prep_k(const void* __restrict__ col, int type, int mode,
                                                   const uint8_t* __restrict__ valid, long n,
                                                   unsigned long long* __restrict__ out, uint8_t* __restrict__ oks,
                                                   unsigned long long* __restrict__ st) {
   unsigned long long mn = ~0ULL, mx = 0ULL, nn = 0ULL;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
-    bool null;
-    unsigned long long u = okey(col, type, i, null);
+    bool null = false;
+    unsigned long long u;
+    if (mode == 2) u = orderable_of_raw(((const unsigned long long*)col)[i], type);
+    else u = okey(col, type, i, null);
     if (valid && !valid[i]) null = true;
     if (null) { u = 0ULL; ++nn; }
     else { mn = u < mn ? u : mn; mx = u > mx ? u : mx; }
-    out[i] = u;
+    out[i] = (mode == 1 && !null) ? raw_of_orderable(u, type) : u;
     if (oks) oks[i] = null ? 0 : 1;
   }
   __shared__ unsigned long long s[3][4];
@@ -242,11 +268,12 @@ int ptg_key_desc_size() { return (int)sizeof(ptgk::PackDesc); }
 int ptg_unpack_out_size() { return (int)sizeof(ptgk::UnpackOut); }
 int ptg_fin_desc_size() { return (int)sizeof(ptgk::FinDesc); }
 
-int ptg_key_prep(const void* col, int type, const void* valid, long n, void* out, void* oks, void* stats,
+int ptg_key_prep(const void* col, int type, int mode, const void* valid, long n, void* out, void* oks, void* stats,
                  hipStream_t s) {
+  if (mode < 0 || mode > 2) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(ptgk::key_stats_init_k, dim3(1), dim3(64), 0, s, (unsigned long long*)stats);
   if (n > 0)
-    hipLaunchKernelGGL(ptgk::key_prep_k, dim3(ptgk::grid_for_n(n)), dim3(256), 0, s, col, type, (const uint8_t*)valid, n,
+    hipLaunchKernelGGL(ptgk::key_prep_k, dim3(ptgk::grid_for_n(n)), dim3(256), 0, s, col, type, mode, (const uint8_t*)valid, n,
                        (unsigned long long*)out, (uint8_t*)oks, (unsigned long long*)stats);
   PTG_RETURN_LAUNCH();
 }

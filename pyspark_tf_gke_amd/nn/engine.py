@@ -59,6 +59,8 @@ CONV1_REC = config.get("conv1_rec")
 # block's dZ, so the block's backward skips its PReLU/pool backward on the step's stream (that
 # kernel still runs, on the side stream and without stores, for dalpha / dbias, ahead of the wgrad).
 PPB_DGRAD = config.get("ppb_dgrad")
+# PReLU + 2x2 max-pool backward in the row-pair layout (ppb.hip): coalesced 16-byte z / dz accesses
+PPB_ROWS = config.get("ppb_rows")
 # DENSE_PRELU_DX: a big Dense fed (through Flatten) by a Conv + PReLU block (CNN-B1's last conv) writes
 # that block's dZ in its dX epilogue; the block's prelu_bwd then runs store-less on the side stream
 DENSE_PRELU_DX = config.get("dense_prelu_dx")
@@ -357,7 +359,17 @@ class ConvOp(Op):
                 dalpha = ws.get(self.name + "/dalpha_dummy", zshape[1:], torch.float32, dev)
             K.prelu_pool_bwd_sparse(dy, self._zs, self._arg, self._pool_alpha(ws, dev), dz, dalpha, bias_g)
         elif self.prelu is not None and self.pool is not None:
-            K.prelu_pool_bwd(dy, z, self.prelu.alpha.data, dz, self.prelu.alpha.grad, bias_g)
+            N_, H_, W_, C_ = z.shape
+            if PPB_ROWS and z.is_cuda and H_ % 2 == 0 and W_ % 2 == 0 and C_ in (8, 16, 32, 64):
+                # row-pair kernel (ppb.hip) + dalpha partials reduced by a second launch
+                key = (N_, H_, W_, C_)
+                if getattr(self, "_ppb_key", None) != key:
+                    self._ppb_key = key
+                    self._ppb_nf = K.ppb_rows_ws_floats(N_, H_, W_, C_, K.ppb_rows_chunks(N_, H_, W_, C_))
+                wsb = ws.get(self.name + "/ppbws", (self._ppb_nf,), torch.float32, dev)
+                K.prelu_pool_bwd_rows(dy, z, self.prelu.alpha.data, dz, self.prelu.alpha.grad, bias_g, ws=wsb)
+            else:
+                K.prelu_pool_bwd(dy, z, self.prelu.alpha.data, dz, self.prelu.alpha.grad, bias_g)
         elif self.prelu is not None:
             K.prelu_bwd(dy, z, self.prelu.alpha.data, dz, self.prelu.alpha.grad, bias_g)
         elif self.pool is not None:

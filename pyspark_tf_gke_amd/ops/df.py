@@ -1048,9 +1048,16 @@ def _check_struct_sizes() -> None:
 _STRUCTS_OK = [False]
 
 
-def key_prep(data: torch.Tensor, kt: int, valid: torch.Tensor | None, need_ok: bool, stats: torch.Tensor):
+KEY_ORDERABLE, KEY_RAW, KEY_RAW_TO_ORDERABLE = 0, 1, 2
+
+
+def key_prep(data: torch.Tensor, kt: int, valid: torch.Tensor | None, need_ok: bool, stats: torch.Tensor,
+             mode: int = KEY_ORDERABLE):
     """One column -> (orderable u64 keys in an int64 tensor, per-row valid flags u8 or None); its
-    (min, max, null count) go into ``stats`` (3 int64 on the device, u64 bit patterns)."""
+    (min, max, null count) go into ``stats`` (3 int64 on the device, u64 bit patterns).
+    ``mode`` KEY_RAW: raw canonical keys instead (what hash aggregation takes: never the tables'
+    INT64_MIN empty marker except for that int64 value itself); KEY_RAW_TO_ORDERABLE: ``data`` holds
+    raw canonical int64 keys of type ``kt``, converted to the orderable form."""
     if not _STRUCTS_OK[0]:
         _check_struct_sizes()
         _STRUCTS_OK[0] = True
@@ -1059,7 +1066,7 @@ def key_prep(data: torch.Tensor, kt: int, valid: torch.Tensor | None, need_ok: b
     v = None if valid is None else (valid.view(torch.uint8) if valid.dtype == torch.bool else valid.contiguous())
     u = torch.empty(n, dtype=torch.int64, device=data.device)
     ok = torch.empty(n, dtype=torch.uint8, device=data.device) if need_ok else None
-    hip("ptg_key_prep", ptr(d), kt, ptr(v), n, ptr(u), ptr(ok), ptr(stats))
+    hip("ptg_key_prep", ptr(d), kt, int(mode), ptr(v), n, ptr(u), ptr(ok), ptr(stats))
     return u, ok
 
 
@@ -1116,14 +1123,20 @@ def f64_to_i64(x: torch.Tensor) -> torch.Tensor:
     return out
 
 
-def unique_sorted_u64(u: torch.Tensor) -> torch.Tensor:
-    """Sorted distinct values of orderable u64 keys (int64 storage): hash aggregation without value
-    columns, then the LSD radix sort of the distinct keys."""
-    n = u.numel()
-    if n == 0:
-        return u
-    uk = hash_agg(u, [], [], est_keys=estimate_distinct(u) if n >= 65536 else None)[0]
-    sk, _ = radix_sort_u64(uk, None, 0, _U64)
+def distinct_raw(raw: torch.Tensor) -> torch.Tensor:
+    """Distinct raw canonical keys (unordered): hash aggregation without value columns."""
+    if raw.numel() == 0:
+        return raw
+    return hash_agg(raw, [], [], est_keys=estimate_distinct(raw) if raw.numel() >= 65536 else None)[0]
+
+
+def sorted_orderable(raw: torch.Tensor, kt: int) -> torch.Tensor:
+    """Raw canonical keys of type ``kt`` -> their orderable forms, radix-sorted."""
+    if raw.numel() == 0:
+        return raw
+    st = torch.empty(3, dtype=torch.int64, device=raw.device)
+    u, _ = key_prep(raw, kt, None, False, st, mode=KEY_RAW_TO_ORDERABLE)
+    sk, _ = radix_sort_u64(u, None, 0, _U64)
     return sk
 
 

@@ -621,6 +621,39 @@ def prelu_pool_bwd(dp, z, alpha, dz_out, dalpha, dbias, nper: int = 0):
     return dz_out
 
 
+def ppb_rows_chunks(N: int, H: int, W: int, C: int) -> int:
+    """Sample chunks of the row-pair PReLU+pool backward: ~1280 workgroups in all."""
+    bx = -(-((H // 2) * W * (C // 8)) // 256)
+    return max(1, min(N, -(-1280 // bx)))
+
+
+def ppb_rows_ws_floats(N: int, H: int, W: int, C: int, nchunks: int) -> int:
+    import ctypes
+
+    from .. import _native
+
+    out = ctypes.c_long(0)
+    _native.check(_native.hip_lib().ptg_ppb_rows_ws_floats(N, H, W, C, nchunks, ctypes.byref(out)),
+                  "ptg_ppb_rows_ws_floats")
+    return int(out.value)
+
+
+def prelu_pool_bwd_rows(dp, z, alpha, dz_out, dalpha, dbias, ws=None, nchunks: int = 0):
+    """prelu_pool_bwd with the row-pair kernel (ppb.hip): coalesced 16-byte z / dz accesses, the
+    window partner by lane swizzle, dalpha through per-sample-chunk partials (``ws``, fp32, at
+    least ``ppb_rows_ws_floats`` elements) reduced by a second kernel.  Same dz bits."""
+    if not on_device(z):
+        return ref.prelu_pool_bwd(dp, z, alpha, dz_out, dalpha, dbias)
+    N, H, W, C = z.shape
+    nchunks = nchunks or ppb_rows_chunks(N, H, W, C)
+    need_f = ppb_rows_ws_floats(N, H, W, C, nchunks)
+    if ws is None or ws.numel() < need_f:
+        ws = torch.empty(need_f, dtype=torch.float32, device=z.device)
+    hip("ptg_prelu_pool_bwd_rows", ptr(dp), ptr(z), ptr(alpha), ptr(dz_out), ptr(dalpha), ptr(dbias), N, H, W, C,
+        nchunks, ptr(ws))
+    return ws
+
+
 def prelu_pool_bwd_sparse(dp, zsel, arg, alpha, dz_out, dalpha, dbias, nper: int = 0):
     """Backward of maxpool2x2(prelu(z)) from the sparse forward record (zsel, arg)."""
     if not on_device(dp):

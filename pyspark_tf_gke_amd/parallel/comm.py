@@ -229,10 +229,9 @@ def all_gather_unique(t: torch.Tensor) -> torch.Tensor:
     if allv.is_cuda and allv.dtype == torch.int64:
         from ..ops import df as D
 
-        # our kernels: sign-flipped orderable keys, distinct by hash aggregation, radix-sorted
-        stats = torch.empty(3, dtype=torch.int64, device=allv.device)
-        u, _ = D.key_prep(allv, D.TORCH_CT[torch.int64], None, False, stats)
-        return D.decode_sort_key(D.unique_sorted_u64(u), torch.int64, False)
+        # our kernels: distinct by hash aggregation, orderable form radix-sorted, decoded back
+        kt = D.TORCH_CT[torch.int64]
+        return D.decode_sort_key(D.sorted_orderable(D.distinct_raw(allv), kt), torch.int64, False)
     return torch.unique(allv)
 
 

@@ -856,12 +856,12 @@ def _count_distinct(cv: ColumnVector) -> int:
     if cv.data.is_cuda:
         kt = _kt_of(cv)
         stats = torch.empty(3, dtype=torch.int64, device=cv.data.device)
-        u, ok = D.key_prep(cv.data, kt, cv.valid, cv.valid is not None or kt == D.KT_CODE, stats)
+        u, ok = D.key_prep(cv.data, kt, cv.valid, cv.valid is not None or kt == D.KT_CODE, stats, mode=D.KEY_RAW)
         if ok is not None:
             u = D.gather_rows(u, D.compact(ok))
-        uk = D.hash_agg(u, [], [], est_keys=D.estimate_distinct(u) if u.numel() >= 65536 else None)[0]
+        uk = D.distinct_raw(u)
         if world > 1:
-            uk = D.hash_agg(torch.cat(comm.all_gather_v(uk)), [], [])[0]
+            uk = D.distinct_raw(torch.cat(comm.all_gather_v(uk)))
         return int(uk.numel())
     k, null = _key_of(cv)
     ok = cv.valid_bool() if null is None else (cv.valid_bool() & ~null)
@@ -923,10 +923,16 @@ def _group_keys_device(srcs: list):
         if not wide:
             return None
         c = max(wide, key=lambda q: q["nvals"])
-        u = c["u"] if c["ok"] is None else D.gather_rows(c["u"], D.compact(c["ok"]))
-        lut = D.unique_sorted_u64(u)
+        # distinct keys by hash aggregation over the RAW canonical keys (the orderable form of 0 is
+        # the hash tables' empty marker), then orderable + radix-sorted for the pack kernel's search
+        st1 = torch.empty(3, dtype=torch.int64, device=dev)
+        raw, _ = D.key_prep(c["cv"].data, c["type"], c["cv"].valid, False, st1, mode=D.KEY_RAW)
+        if c["ok"] is not None:
+            raw = D.gather_rows(raw, D.compact(c["ok"]))
+        raw = D.distinct_raw(raw)
         if world > 1:
-            lut = D.unique_sorted_u64(torch.cat(comm.all_gather_v(lut)))
+            raw = D.distinct_raw(torch.cat(comm.all_gather_v(raw)))
+        lut = D.sorted_orderable(raw, c["type"])
         c["lut"], c["lo"], c["nvals"] = lut, 0, int(lut.numel())
     shift = 0
     for c in cols:
