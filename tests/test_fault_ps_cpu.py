@@ -491,6 +491,11 @@ if st.rank != 2:
     C.comm.barrier = lambda: None
 co.join()
 print("RESULT", json.dumps({"vals": [rv.fetch() for rv in rvs], "ran": co.closures_run}), flush=True)
+# rank 0 hosts the TCP store: it leaves only after rank 1 has read its results
+from pyspark_tf_gke_amd.distribute.ps import _store
+_store().set(f"test/done/{st.rank}", "1")
+if st.rank == 0:
+    _store().wait(["test/done/1"])
 os._exit(0)
 """
     r = _launch(body, 3, extra_env={"PTG_COORD_DEAD_S": "2"})
