@@ -81,6 +81,9 @@ _K = [
     Knob("ppb_dgrad", bool, False, "PTG_PPB_DGRAD", None,
          "CNN-B1 layers 3-5: the dgrad epilogue also writes the pooled block's dZ (conv.hip EPI_PPB); the "
          "PReLU/pool backward moves to the side stream for dalpha/dbias only (A/B: 1.80-1.88 vs 1.65 ms, off)"),
+    Knob("conv32", bool, False, "PTG_CONV32", None,
+         "5x5 convs with C, Cout in 16..64 (CNN-B1 layers 3-5 and their data gradients): the 32x32x16-MFMA "
+         "implicit GEMM of conv32.hip instead of the halo strip kernels"),
     Knob("ppb_rows", bool, False, "PTG_PPB_ROWS", None,
          "CNN-B1 layers 2-4: PReLU + max-pool backward in the row-pair layout (ppb.hip, dalpha via chunk partials)"),
     Knob("conv1_rec", bool, True, "PTG_CONV1_REC", None, "first conv layer (conv1.hip): forward keeps the pool record, backward needs no recompute (0: recompute z in the backward)"),

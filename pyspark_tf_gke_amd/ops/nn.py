@@ -180,8 +180,54 @@ def conv2d_fwd_fused(x, w, bias, pad: int, z_out, alpha=None, aux_out=None, epi=
         assert tuple(z_out.shape) == (N, H, W, Cout)
     assert Cw == C
     need(x, torch.bfloat16, "conv_halo.x"); need(w, torch.bfloat16, "conv_halo.w")
+    if CONV32 and epi in (None, "pool", "prelu") and KS == 5 and pad == 2 and _conv32_ok(H, W, C, Cout, epi):
+        # channel-rich 5x5 layers (and data gradients): the 32x32x16-MFMA implicit GEMM (conv32.hip)
+        return conv32(x, w, bias, z_out, alpha, aux_out, epi)
     hip("ptg_conv2d_fwd_halo", ptr(x), ptr(w), ptr(bias), ptr(alpha), ptr(z_out), ptr(aux_out), ptr(arg_out), N, H, W,
         C, Cout, KS, pad, EPI[epi])
+    return z_out
+
+
+EPI32 = {None: 0, "z": 0, "pool": 1, "prelu": 2}
+CONV32 = config.get("conv32")
+_C32_OK: dict = {}
+
+
+def _conv32_ok(H, W, C, Cout, epi) -> bool:
+    key = (H, W, C, Cout, epi)
+    v = _C32_OK.get(key)
+    if v is None:
+        v = _C32_OK[key] = conv32_supported(H, W, C, Cout, 5, 2, epi)
+    return v
+
+
+def conv32_supported(H: int, W: int, C: int, Cout: int, KS: int, pad: int, epi=None) -> bool:
+    """The 32x32x16-MFMA implicit-GEMM conv (conv32.hip) covers this 5x5 'same' shape."""
+    from .. import _native
+
+    return bool(_native.hip_lib().ptg_conv32_supported(H, W, C, Cout, KS, pad, EPI32[epi]))
+
+
+def conv32(x, w, bias, z_out, alpha=None, aux_out=None, epi=None):
+    """z = conv5x5(x, w) + bias (stride 1, pad 2) on the 32x32x16 MFMA kernel (conv32.hip);
+    epi "pool": aux = maxpool2x2(prelu(z, alpha)); "prelu": aux = prelu(z, alpha).  For a data
+    gradient pass dz as x and the flipped filter [Cin][5][5][Cout] as w."""
+    if not on_device(x):
+        ref.conv2d_fwd(x, w, bias, 1, 2, z_out, None)
+        if epi == "pool":
+            ref.prelu_pool_fwd(z_out, alpha, aux_out)
+        elif epi == "prelu":
+            ref.prelu_fwd(z_out, alpha, aux_out)
+        return z_out
+    N, H, W, C = x.shape
+    Cout = w.shape[0]
+    assert tuple(w.shape) == (Cout, 5, 5, C) and tuple(z_out.shape) == (N, H, W, Cout), (x.shape, w.shape, z_out.shape)
+    need(x, torch.bfloat16, "conv32.x"); need(w, torch.bfloat16, "conv32.w"); need(z_out, torch.bfloat16, "conv32.z")
+    if epi == "pool":
+        assert aux_out is not None and tuple(aux_out.shape) == (N, H // 2, W // 2, Cout)
+    elif epi == "prelu":
+        assert aux_out is not None and tuple(aux_out.shape) == (N, H, W, Cout)
+    hip("ptg_conv32", ptr(x), ptr(w), ptr(bias), ptr(alpha), ptr(z_out), ptr(aux_out), N, H, W, C, Cout, EPI32[epi])
     return z_out
 
 

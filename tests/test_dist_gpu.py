@@ -185,9 +185,14 @@ def run(fail_calls):
         if st.rank == 1 and calls[0] in fail_calls:
             raise RuntimeError("injected worker failure")
         x, y = next(iterator)
-        with GradientTape() as tape:
-            loss = loss_fn(y.to(DEV), m(x.to(DEV), training=True))
-        o.apply_gradients(zip(tape.gradient(loss, m.trainable_variables), m.trainable_variables))
+        try:
+            with GradientTape() as tape:
+                loss = loss_fn(y, m(x, training=True))
+            o.apply_gradients(zip(tape.gradient(loss, m.trainable_variables), m.trainable_variables))
+        except Exception:
+            import traceback, sys
+            traceback.print_exc(file=sys.stderr)
+            raise
         return 1
     for epoch in range(2):
         for _ in range(6):

@@ -89,6 +89,12 @@ def main():
             wf = torch.empty((C, 5, 5, Co), device=dev, dtype=torch.bfloat16)
             ops_[f"dgrad{li}"] = (lambda dz=dz, w=w, dx=dx, wf=wf: ops.conv2d_dgrad_halo(dz, w, 2, dx, wf),
                                   dz.numel() * 2 + dx.numel() * 2)
+            if ops.conv32_supported(H, W, Co, C, 5, 2, None):  # conv32.hip data gradient (flipped filters)
+                ops_[f"dgrad32_{li}"] = (lambda dz=dz, wf=wf, dx=dx: ops.conv32(dz, wf, None, dx),
+                                         dz.numel() * 2 + dx.numel() * 2)
+            if ops.conv32_supported(H, W, C, Co, 5, 2, epi):
+                ops_[f"fwd32_{li}"] = (lambda x=x, w=w, b=b, z=z, al=al, aux=aux, epi=epi: ops.conv32(
+                    x, w, b, z, al, aux, epi), x.numel() * 2 + z.numel() * 2 + aux.numel() * 2)
             # the implicit-GEMM path of gemm.hip for the same dgrad / forward (A/B reference)
             ops_[f"dgradG{li}"] = (lambda dz=dz, w=w, dx=dx: ops.conv2d_dgrad(dz, w, 2, dx),
                                    dz.numel() * 2 + dx.numel() * 2)
