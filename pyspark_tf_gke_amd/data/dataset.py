@@ -112,7 +112,28 @@ class _ColPlan:
         chunks = [c[rng.permutation(len(c))] for c in chunks]
         return np.concatenate([chunks[i] for i in rng.permutation(len(chunks))]) if chunks else base
 
+    def on_device(self, dev) -> "_ColPlan":
+        """The same plan over copies of the columns resident on ``dev`` (uploaded once): batches are
+        then gathered on the device, no per-step host gather or host->device copy."""
+        import torch
+
+        arrs = [a if (self._is_torch(a) and a.device == dev) else torch.as_tensor(np.ascontiguousarray(_np(a))).to(dev)
+                for a in self.arrays]
+        p = _ColPlan(arrs, self.kind, self.keys)
+        p.ops = list(self.ops)
+        return p
+
     def __iter__(self):
+        return self.iter_groups(1)
+
+    def iter_groups(self, group: int = 1, with_count: bool = False):
+        """Batches as the plan defines them; ``group`` > 1 yields up to ``group`` consecutive FULL
+        batches as one gather (``with_count``: (batch, number of batches)); a partial batch always
+        comes alone.  Same order and contents as ``group`` = 1."""
+        for b, k in self._iter(max(1, int(group))):
+            yield (b, k) if with_count else b
+
+    def _iter(self, group):
         dev = self._device()
         if dev is not None:
             import torch
@@ -142,16 +163,19 @@ class _ColPlan:
         if batch is None:
             for order in epoch_orders():
                 for i in order:
-                    yield self._pack([a[int(i)] for a in self.arrays])
+                    yield self._pack([a[int(i)] for a in self.arrays]), 1
             return
         bs, drop = batch[1], batch[2]
         if batch_before_repeat:
             for order in epoch_orders():
-                for st in range(0, len(order), bs):
-                    sel = order[st:st + bs]
+                st = 0
+                while st < len(order):
+                    k = max(1, min(group, (len(order) - st) // bs))
+                    sel = order[st:st + k * bs]
                     if drop and len(sel) < bs:
                         break
-                    yield self._gather(sel)
+                    yield self._gather(sel), (k if len(sel) == k * bs else 1)
+                    st += len(sel)
             return
         pending = None
         for order in epoch_orders():
@@ -164,10 +188,11 @@ class _ColPlan:
             else:
                 pending = np.concatenate([pending, order])
             while len(pending) >= bs:
-                yield self._gather(pending[:bs])
-                pending = pending[bs:]
+                k = max(1, min(group, len(pending) // bs))
+                yield self._gather(pending[:k * bs]), k
+                pending = pending[k * bs:]
         if pending is not None and len(pending) and not drop:
-            yield self._gather(pending)
+            yield self._gather(pending), 1
 
 
 def _keep(a):

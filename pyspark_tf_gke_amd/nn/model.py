@@ -175,7 +175,7 @@ class Sequential:
         self.store.refresh_bf16()
 
     # ---------------------------------------------------------------- compile
-    def compile(self, optimizer="adam", loss=None, metrics=None, jit_compile=None) -> None:
+    def compile(self, optimizer="adam", loss=None, metrics=None, jit_compile=None, steps_per_execution: int = 1) -> None:
         """``jit_compile=True`` (or env PTG_HIP_GRAPH=1) captures the whole training step - forward,
         loss, backward, optimizer - into one HIP graph after two eager warm-up steps and replays it
         (single-GPU training; multi-rank strategies stay eager because their collectives are
@@ -183,6 +183,9 @@ class Sequential:
         if jit_compile is None:
             jit_compile = config.get("hip_graph")
         self.jit_compile = bool(jit_compile)
+        # Keras' steps_per_execution: batches run per device launch where the step allows it (the
+        # fused small-MLP step: fit() hands it this many consecutive batches of a column dataset)
+        self.steps_per_execution = max(1, int(steps_per_execution))
         self._graphs = {}
         self._graph_warm = {}
         self.optimizer = OPT.get(optimizer)
@@ -522,6 +525,36 @@ class Sequential:
             return None
         return dims, acts, woffs, boffs, kind, K.mlp_desc(dims, acts, woffs, boffs)
 
+    def _mlp_fit_plan(self, x, y, st):
+        """(iterator factory over (batch group, batches), MLP plan) when fit() can feed the fused
+        MLP step groups of batches from a device-resident column dataset, else None."""
+        from ..data.dataset import Dataset
+
+        if self.device is None or self.device.type != "cuda" or getattr(self, "jit_compile", False):
+            return None
+        plan = self._mlp_plan(st)
+        if plan is None:
+            return None
+        if isinstance(x, Dataset):
+            cp = getattr(x, "_plan", None)
+            if cp is None or "batch" not in cp.names():
+                return None
+        elif isinstance(x, (np.ndarray, torch.Tensor)) and y is not None:
+            return None  # array inputs keep the per-batch path (its shuffle order is _iter_batches')
+        else:
+            return None
+        if sum(int(np.prod(getattr(a, "shape", (0,)))) * 4 for a in cp.arrays) > (1 << 30):
+            return None  # large datasets stay host-resident
+        dev_plans = getattr(self, "_dev_plans", None)
+        if dev_plans is None:
+            dev_plans = self._dev_plans = {}
+        key = id(cp)
+        dp = dev_plans.get(key)
+        if dp is None or dp[0] is not cp:
+            dp = dev_plans[key] = (cp, cp.on_device(self.device))
+        group = self.steps_per_execution if getattr(self, "steps_per_execution", 1) > 1 else 64
+        return (lambda: dp[1].iter_groups(group, with_count=True)), plan
+
     def _mlp_fusable(self, xb, yb, st):
         if xb.dtype != torch.float32 or not xb.is_cuda or xb.dim() != 2:
             return None
@@ -679,19 +712,52 @@ class Sequential:
                 cb.on_train_begin()
             initial_epoch = max(initial_epoch, int(getattr(cb, "start_epoch", 0) or 0))
         persistent_it = None
+        # the fused small-MLP step (mlp.hip) over a column dataset: the columns go to the device once
+        # and fit() takes groups of consecutive full batches per launch (no per-batch callbacks exist,
+        # so this changes nothing but the launch count; steps_per_execution sets the group size)
+        mlp_group = self._mlp_fit_plan(x, y, st)
         if steps_per_epoch is not None:
-            persistent_it = self._iter_batches(x, y, batch_size, shuffle)
+            persistent_it = mlp_group[0]() if mlp_group else self._iter_batches(x, y, batch_size, shuffle)
+        stash = None
         stats = self._stats_buf()
         for epoch in range(initial_epoch, epochs):
             if verbose and is_chief:
                 print(f"Epoch {epoch + 1}/{epochs}", flush=True)
             K.fill_(stats, 0.0)
             t0 = time.perf_counter()
-            it = persistent_it if persistent_it is not None else self._iter_batches(x, y, batch_size, shuffle,
-                                                                                   seed=epoch)
+            if persistent_it is not None:
+                it = persistent_it
+            elif mlp_group:
+                it = mlp_group[0]()
+            else:
+                it = self._iter_batches(x, y, batch_size, shuffle, seed=epoch)
             nsteps = 0
             with self.overlapped_steps():
                 while steps_per_epoch is None or nsteps < steps_per_epoch:
+                    if mlp_group:
+                        if stash is not None:
+                            (xb, yb, k), stash = stash, None
+                        else:
+                            try:
+                                batch, k = next(it)
+                            except StopIteration:
+                                break
+                            xb, yb = self._prep_batch(batch[0], batch[1])
+                        if steps_per_epoch is not None and nsteps + k > steps_per_epoch:
+                            k1 = steps_per_epoch - nsteps  # the rest of the group opens the next epoch
+                            B = xb.shape[0] // k
+                            stash = (xb[k1 * B:], yb[k1 * B:], k - k1)
+                            xb, yb, k = xb[:k1 * B], yb[:k1 * B], k1
+                        B = xb.shape[0] // k
+                        self._last_batch = int(B)
+                        if self._mlp_fusable(xb[:B], yb[:B], st) is not None:
+                            _heartbeat.progress(k)
+                            self._train_step_mlp(xb, yb, stats, mlp_group[1], steps=k)
+                        else:
+                            for j in range(k):
+                                self.train_step_fast(xb[j * B:(j + 1) * B], yb[j * B:(j + 1) * B], stats)
+                        nsteps += k
+                        continue
                     try:
                         batch = next(it)
                     except StopIteration:

@@ -107,3 +107,38 @@ def test_mlp_fit_uses_fused_step(hip_built, monkeypatch):
     h = m.fit(x.numpy(), y.numpy(), batch_size=64, epochs=2, verbose=0)
     assert len(calls) >= 2 * 20 and all(v == v for v in h.history["loss"])
     assert h.history["loss"][-1] < h.history["loss"][0] + 1e-3
+
+
+@pytest.mark.gpu
+@gpu
+def test_mlp_fit_dataset_grouped_launches_match_per_batch_engine(hip_built, monkeypatch):
+    """The reference's local MLP fit (cli/train.py: from_tensor_slices -> shuffle(3000) -> batch -> repeat,
+    steps_per_epoch): columns uploaded once, groups of full batches per fused launch (with a group
+    split across the epoch boundary) == the layer-by-layer engine step per batch."""
+    from pyspark_tf_gke_amd.data import Dataset
+    from pyspark_tf_gke_amd.nn import model as M
+
+    g = torch.Generator().manual_seed(4)
+    X = torch.randn(1000, 3, generator=g).numpy()
+    y = torch.randint(0, 15, (1000,), generator=g).to(torch.int32).numpy()
+
+    def run(fused):
+        monkeypatch.setattr(M, "MLP_FUSED", fused)
+        torch.manual_seed(5)
+        m = build_deep_model(3, 15, device="cuda")
+        m.compile(optimizer=nn.optimizers.Adam(1e-3), loss=nn.losses.SparseCategoricalCrossentropy(),
+                  metrics=["accuracy"], steps_per_execution=5)
+        ds = Dataset.from_tensor_slices((X, y)).shuffle(300, seed=1).batch(32).repeat().prefetch(1)
+        calls = []
+        orig = K.mlp_train
+        monkeypatch.setattr(K, "mlp_train", lambda *a, **k: (calls.append(a[11]), orig(*a, **k))[1])
+        h = m.fit(ds, epochs=3, steps_per_epoch=13, verbose=0)
+        monkeypatch.setattr(K, "mlp_train", orig)
+        torch.cuda.synchronize()
+        return m.store.flat.clone(), h.history["loss"], calls, m.optimizer.iterations
+
+    fa, la, ca, ia = run(True)
+    fb, lb, cb, ib = run(False)
+    assert ia == ib == 39 and not cb and sum(ca) == 39 and max(ca) == 5, (ia, ib, ca)
+    assert torch.allclose(fa, fb, rtol=1e-3, atol=1e-5), float((fa - fb).abs().max())
+    assert all(abs(a - b) <= 1e-3 * max(1.0, abs(b)) for a, b in zip(la, lb)), (la, lb)
