@@ -607,7 +607,7 @@ class ParameterServerStrategy(Strategy):
         if ready:
             from ..nn.tape import _apply_overlapped
 
-            _apply_overlapped(opt, model.store, ready)
+            _apply_overlapped(opt, model.store, ready, model)
         else:
             opt.apply(model.store)
 

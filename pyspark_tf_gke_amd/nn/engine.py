@@ -493,7 +493,7 @@ class DenseOp(Op):
             dx = ws.get(self.name + "/dx", x.shape, torch.bfloat16, x.device)
             K.linear_dx(dz, self.dense.kernel.bf16, dx)
         fused = self.fused_update
-        if fused is not None and dz.is_cuda:
+        if fused is not None and (dz.is_cuda or getattr(fused, "cpu_ok", False)):
             fused.linear_dw(dz, x, self.dense.kernel)
         else:
             g = self.dense.kernel.grad
@@ -518,7 +518,7 @@ class DenseOp(Op):
                 # before the weight update below: dX reads this step's (pre-update) bf16 weights
                 dx = ws.get(self.name + "/dx", x.shape, torch.bfloat16, dev)
                 K.linear_dx(dz, self.dense.kernel.bf16, dx)
-            if fused is not None and dz.is_cuda:
+            if fused is not None and (dz.is_cuda or getattr(fused, "cpu_ok", False)):
                 fused.linear_dw(dz, x, self.dense.kernel)  # Adam in the wgrad epilogue
             else:
                 g = self.dense.kernel.grad

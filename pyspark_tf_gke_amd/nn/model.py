@@ -205,6 +205,10 @@ class Sequential:
 
     # ---------------------------------------------------------------- execution plan hooks
     def _run_forward(self, xb, training: bool):
+        if getattr(self, "_lazy_dw", None):
+            from .tape import flush_lazy
+
+            flush_lazy(self)  # a deferred tape dW still reads this workspace
         return E.run_forward(self.ops, xb, self.ws, training, pre_op=self._pre_op_hook())
 
     def _pre_op_hook(self):

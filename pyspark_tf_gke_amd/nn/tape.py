@@ -13,6 +13,12 @@ The same code runs here.  The tape does not trace Python ops: it records the mod
 ``gradient()`` runs the fused loss kernel + fused backward into the flat gradient buffer.
 ``apply_gradients`` then performs the active strategy's collective (all-reduce / reduce-scatter)
 and the single fused Adam launch.
+
+One local replica (no strategy, or a one-worker parameter server) defers each big Dense layer's
+weight-gradient GEMM: ``gradient()`` hands back a :class:`_LazyGrad` for that kernel, which computes
+the gradient the moment anything reads it.  When it reaches ``apply_gradients`` untouched, the
+update runs Adam inside that GEMM's epilogue (``ops.nn.linear_dw_adam``, as fit() does) on an
+auxiliary stream, so the [2048, 20480] fp32 gradient is never written nor read back.
 """
 from __future__ import annotations
 
@@ -22,10 +28,112 @@ from .. import config
 
 _TAPES: list = []
 OVERLAP = config.get("tape_overlap")
+LAZY_DW = config.get("tape_lazy_dw")
 
 
 def _active_tape():
     return _TAPES[-1] if _TAPES else None
+
+
+_META = {"shape", "dtype", "device", "is_cuda", "ndim", "size", "dim", "numel", "layout", "requires_grad",
+         "is_floating_point", "element_size", "__len__"}
+
+
+def _func_name(func) -> str:
+    n = getattr(func, "__name__", "")
+    if n == "__get__":  # a property getter: the descriptor carries the name
+        n = getattr(getattr(func, "__self__", None), "__name__", "")
+    return n
+
+
+class _LazyGrad(torch.Tensor):
+    """The gradient of a big Dense kernel whose GEMM has not run yet.  It aliases the parameter's
+    gradient buffer; any torch operation on it (metadata queries aside) first computes the gradient
+    into that buffer, so user code sees an ordinary tensor."""
+
+    @classmethod
+    def __torch_function__(cls, func, types, args=(), kwargs=None):
+        kwargs = kwargs or {}
+        if _func_name(func) not in _META:
+            _materialize_in(args)
+            _materialize_in(kwargs.values())
+        with torch._C.DisableTorchFunctionSubclass():
+            return func(*args, **kwargs)
+
+
+def _materialize_in(xs) -> None:
+    for a in xs:
+        if isinstance(a, _LazyGrad):
+            lz = getattr(a, "_lz", None)
+            if lz is not None:
+                lz.materialize()
+        elif isinstance(a, (list, tuple)):
+            _materialize_in(a)
+        elif isinstance(a, dict):
+            _materialize_in(a.values())
+
+
+def _event(dev):
+    if dev.type != "cuda":
+        return None
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(dev))
+    return ev
+
+
+class _LazyDW:
+    """One deferred Dense weight gradient dW = dz^T @ x: the bf16 operands stay in the model's
+    workspace until ``materialize()`` (the plain GEMM into the gradient buffer) or ``fused_adam()``
+    (Adam in the GEMM epilogue) consumes them; the model flushes pending ones before its next
+    forward rewrites that workspace."""
+
+    def __init__(self, dz, x, param):
+        self.dz, self.x, self.param = dz, x, param
+        self.pending = True
+        self.ev = _event(dz.device)  # after dz, x are final (and this layer's dX has read the weights)
+        self.view = None
+
+    def materialize(self) -> None:
+        if not self.pending:
+            return
+        self.pending = False
+        from ..ops import nn as K
+
+        K.linear_dw(self.dz, self.x, self.param.grad)
+        self.ev = _event(self.dz.device)
+
+    def fused_adam(self, opt, store, step: int) -> None:
+        from ..ops import nn as K
+
+        self.pending = False
+        p = self.param
+        o, n = p.offset, p.numel
+        shp = p.grad.shape
+        K.linear_dw_adam(self.dz, self.x, store.flat[o:o + n].view(shp), opt.m[o:o + n].view(shp),
+                         opt.v[o:o + n].view(shp), store.flat_bf16[o:o + n].view(shp), opt.lr_t(step),
+                         opt.beta_1, opt.beta_2, opt.epsilon, 1.0)
+
+
+class _DeferDW:
+    """Stands in for fit()'s FusedAdamStep during a tape backward (DenseOp.backward calls
+    ``linear_dw``): it records the GEMM's operands instead of launching it."""
+
+    cpu_ok = True
+
+    def __init__(self):
+        self.items: list = []
+
+    def linear_dw(self, dz, x, param) -> None:
+        self.items.append(_LazyDW(dz, x, param))
+
+
+def flush_lazy(model) -> None:
+    """Compute every deferred weight gradient of ``model`` (on the current stream)."""
+    lz = getattr(model, "_lazy_dw", None)
+    if lz:
+        model._lazy_dw = None
+        for d in lz:
+            d.materialize()
 
 
 class GradientTape:
@@ -59,6 +167,7 @@ class GradientTape:
         m = self.model
         if m is None or self.loss_obj is None:
             raise RuntimeError("GradientTape.gradient: no model forward / loss recorded")
+        flush_lazy(m)
         out = self.out
         last = m._last_op()
         if isinstance(self.loss_obj, LS.SparseCategoricalCrossentropy) and isinstance(last, E.DenseOp) \
@@ -85,22 +194,40 @@ class GradientTape:
         st = getattr(m, "strategy", None) or current_strategy()
         side = S.for_step(m.store, st)
         ready: list = []
+        local = st is None or getattr(st, "world_size", 2) == 1
+        # one local replica (no strategy, or a one-worker parameter server): defer the big Dense dW
+        defer = _DeferDW() if (OVERLAP and LAZY_DW and local) else None
+        big = [op for op in m.ops if isinstance(op, E.DenseOp) and op.big] if defer is not None else []
+        for op in big:
+            op.fused_update = defer
 
         def dense_done(op):
             # a big Dense layer's dW has just been forked onto the side stream: an event there lets
             # apply_gradients start that layer's Adam while the conv backward below still runs
-            if side is not None and isinstance(op, E.DenseOp) and op.big:
+            if side is not None and defer is None and isinstance(op, E.DenseOp) and op.big:
                 p = op.dense.kernel
                 ev = torch.cuda.Event()
                 ev.record(S._stream(p.grad.device))
-                ready.append((p.offset, p.offset + p.numel, ev))
+                ready.append((p.offset, p.offset + p.numel, ev, None))
 
-        with S.active(side):
-            m._run_backward(dpred, on_op_done=dense_done)
-        # one local replica (no strategy, or a one-worker parameter server) can overlap its update
-        m._tape_ready = ready if st is None or getattr(st, "world_size", 2) == 1 else None
+        try:
+            with S.active(side):
+                m._run_backward(dpred, on_op_done=dense_done)
+        finally:
+            for op in big:
+                op.fused_update = None
+        grads = {}
+        if defer is not None and defer.items:
+            m._lazy_dw = defer.items
+            for d in defer.items:
+                p = d.param
+                d.view = p.grad.as_subclass(_LazyGrad)
+                d.view._lz = d
+                grads[id(p)] = d.view
+                ready.append((p.offset, p.offset + p.numel, None, d))
+        m._tape_ready = ready if local else None
         m._pending_grads = True
-        return [v.param.grad for v in sources]
+        return [grads.get(id(v.param), v.param.grad) for v in sources]
 
 
 def apply_gradients(optimizer, grads_and_vars) -> None:
@@ -113,14 +240,17 @@ def apply_gradients(optimizer, grads_and_vars) -> None:
     st = getattr(model, "strategy", None) or current_strategy()
     ready = getattr(model, "_tape_ready", None)
     model._tape_ready = None
+    ok = bool(ready) and _overlap_ok(optimizer, gv, ready)
+    if not ok:
+        flush_lazy(model)  # the update below reads every gradient from the flat buffer
     if st is not None:
         # a one-worker ParameterServerStrategy applies the update itself (possibly at round commit)
         # and takes the overlapped form from here (ps.py _apply_local)
-        model._tape_overlap = ready if ready and _overlap_ok(optimizer, gv) else None
+        model._tape_overlap = ready if ok else None
         st.finish_gradients(model)
         st.apply_update(model, optimizer)
-    elif ready and _overlap_ok(optimizer, gv):
-        _apply_overlapped(optimizer, model.store, ready)
+    elif ok:
+        _apply_overlapped(optimizer, model.store, ready, model)
     else:
         optimizer.apply(model.store)
     model._pending_grads = False
@@ -129,20 +259,42 @@ def apply_gradients(optimizer, grads_and_vars) -> None:
 _AUX: dict = {}
 
 
-def _overlap_ok(optimizer, gv) -> bool:
+def _overlap_ok(optimizer, gv, ready) -> bool:
     """The gradients handed in are the tape's own buffers, untouched (no clipping / scaling in
-    between), and the optimizer is plain flat Adam with a host-side step counter."""
+    between: a deferred Dense gradient that something has read counts as touched), and the
+    optimizer is plain flat Adam with a host-side step counter."""
     from .optimizers import Adam
 
-    return (OVERLAP and type(optimizer) is Adam and getattr(optimizer, "dev_state", None) is None
-            and all(getattr(v, "param", None) is not None and g is v.param.grad for g, v in gv))
+    if not (OVERLAP and type(optimizer) is Adam and getattr(optimizer, "dev_state", None) is None):
+        return False
+    lazy = {id(r[3].param): r[3] for r in ready if r[3] is not None}
+    for g, v in gv:
+        p = getattr(v, "param", None)
+        if p is None:
+            return False
+        d = lazy.get(id(p))
+        if d is None:
+            if g is not p.grad:
+                return False
+        elif g is not d.view or not d.pending:
+            return False
+    return True
 
 
-def _apply_overlapped(optimizer, store, ready) -> None:
+def _apply_overlapped(optimizer, store, ready, model=None) -> None:
     """Adam over the big Dense ranges on an auxiliary stream, each waiting only for its layer's dW
     (so the HBM-bound update overlaps the rest of the backward), then the remaining gaps on the
     step's stream, which joins the auxiliary stream before returning."""
     dev = store.flat.device
+    step = optimizer.iterations + 1
+    if dev.type != "cuda":  # CPU: the same update, in order
+        optimizer.build(store)
+        _update_ranges(optimizer, store, ready, step)
+        if model is not None:
+            model._lazy_dw = None
+        store.grad_clean = True
+        optimizer.iterations = step
+        return
     aux = _AUX.get(dev)
     if aux is None:
         aux = _AUX[dev] = torch.cuda.Stream(device=dev)
@@ -152,7 +304,6 @@ def _apply_overlapped(optimizer, store, ready) -> None:
     # read the bf16 weights before the dW fork; the previous update was joined into the step's
     # stream).  The gradients of those ranges are cleared by the update, so code that reads them
     # between gradient() and apply_gradients() must turn this off (PTG_TAPE_OVERLAP=0).
-    step = optimizer.iterations + 1
     # a fresh optimizer allocates and zero-fills its moments HERE, on the step's stream; the aux
     # stream must not read them before that fill (it otherwise never waits for the step's stream)
     before = optimizer.m
@@ -160,14 +311,35 @@ def _apply_overlapped(optimizer, store, ready) -> None:
     if optimizer.m is not before:
         aux.wait_stream(cur)
     with torch.cuda.stream(aux):
-        for lo, hi, ev in ready:
-            aux.wait_event(ev)
-            optimizer.apply(store, lo=lo, hi=hi, advance=False)
+        for lo, hi, ev, lazy in ready:
+            ev = lazy.ev if lazy is not None else ev
+            if ev is not None:
+                aux.wait_event(ev)
+            _update_range(optimizer, store, lo, hi, lazy, step)
+    _update_gaps(optimizer, store, ready)
+    cur.wait_stream(aux)
+    if model is not None:
+        model._lazy_dw = None
+    store.grad_clean = True
+    optimizer.iterations = step
+
+
+def _update_range(optimizer, store, lo, hi, lazy, step) -> None:
+    if lazy is not None and lazy.pending:
+        lazy.fused_adam(optimizer, store, step)  # dW never stored: Adam in the GEMM epilogue
+    else:
+        optimizer.apply(store, lo=lo, hi=hi, advance=False)
+
+
+def _update_gaps(optimizer, store, ready) -> None:
     lo = 0
     for a, b in sorted((r[0], r[1]) for r in ready) + [(store.total, store.total)]:
         if a > lo:
             optimizer.apply(store, lo=lo, hi=a, advance=False)
         lo = max(lo, b)
-    cur.wait_stream(aux)
-    store.grad_clean = True
-    optimizer.iterations = step
+
+
+def _update_ranges(optimizer, store, ready, step) -> None:
+    for lo, hi, _, lazy in ready:
+        _update_range(optimizer, store, lo, hi, lazy, step)
+    _update_gaps(optimizer, store, ready)

@@ -143,3 +143,74 @@ def test_conv1_reference_matches_autograd():
     assert torch.allclose(dw, wf.grad, rtol=1e-2, atol=1e-2)
     assert torch.allclose(db, bf.grad, rtol=1e-2, atol=1e-2)
     assert torch.allclose(da, af.grad, rtol=1e-3, atol=1e-3)
+
+
+def _tape_step(m, opt, x, y, touch=None):
+    loss_obj = nn.losses.MeanSquaredError()
+    with nn.GradientTape() as tape:
+        pred = m(x, training=True)
+        loss = loss_obj(y, pred)
+    grads = tape.gradient(loss, m.trainable_variables)
+    if touch is not None:
+        touch(grads)
+    opt.apply_gradients(zip(grads, m.trainable_variables))
+    return grads
+
+
+def test_tape_lazy_dense_dw_matches_train_on_batch():
+    """A CNN-B1-shaped tape loop (flat head, big Dense): the deferred Dense dW fused with Adam at
+    apply_gradients (nn/tape.py _LazyDW) gives the train_on_batch weights."""
+    from pyspark_tf_gke_amd.nn import tape as T
+
+    torch.manual_seed(0)
+    x = torch.rand(4, 32, 40, 3)
+    y = torch.rand(4, 2)
+    m1 = build_cnn_model((32, 40, 3), flat=True, summary=False, device="cpu")
+    m2 = build_cnn_model((32, 40, 3), flat=True, summary=False, device="cpu")
+    m2.set_weights(m1.get_weights())
+    m2.compile(optimizer=nn.optimizers.Adam(1e-3), loss="mse")
+    opt = nn.optimizers.Adam(1e-3)
+    lazies = []
+    for _ in range(3):
+        grads = _tape_step(m1, opt, x, y, touch=lambda g: lazies.extend(t for t in g if isinstance(t, T._LazyGrad)))
+        m2.train_on_batch(x, y)
+    assert lazies, "the big Dense kernel gradient should be deferred"
+    assert all(not t._lz.pending for t in lazies)
+    assert m1._lazy_dw is None
+    assert torch.allclose(m1.store.flat, m2.store.flat, atol=1e-5)
+
+
+def test_tape_lazy_dense_dw_materializes_on_read():
+    """Reading a deferred gradient computes it (the plain update path then runs), and a gradient()
+    followed by another forward without apply_gradients flushes it before the workspace is reused."""
+    from pyspark_tf_gke_amd.nn import tape as T
+
+    torch.manual_seed(1)
+    x = torch.rand(4, 32, 40, 3)
+    y = torch.rand(4, 2)
+    m1 = build_cnn_model((32, 40, 3), flat=True, summary=False, device="cpu")
+    m2 = build_cnn_model((32, 40, 3), flat=True, summary=False, device="cpu")
+    m2.set_weights(m1.get_weights())
+    o1, o2 = nn.optimizers.Adam(1e-3), nn.optimizers.Adam(1e-3)
+    seen = {}
+
+    def norms(grads):
+        seen["n"] = [float(torch.linalg.vector_norm(g)) for g in grads]
+
+    saved = T.LAZY_DW
+    try:
+        _tape_step(m1, o1, x, y, touch=norms)
+        T.LAZY_DW = False
+        _tape_step(m2, o2, x, y, touch=lambda g: seen.setdefault("ref", [float(torch.linalg.vector_norm(t)) for t in g]))
+    finally:
+        T.LAZY_DW = saved
+    assert np.allclose(seen["n"], seen["ref"], rtol=1e-5)
+    assert torch.allclose(m1.store.flat, m2.store.flat, atol=1e-6)
+    # gradient() then a forward: the pending dW is computed first
+    with nn.GradientTape() as tape:
+        loss = nn.losses.MeanSquaredError()(y, m1(x, training=True))
+    g = tape.gradient(loss, m1.trainable_variables)
+    lz = [t for t in g if isinstance(t, T._LazyGrad)]
+    assert lz and lz[0]._lz.pending
+    m1(x)
+    assert not lz[0]._lz.pending and float(torch.linalg.vector_norm(lz[0])) > 0
