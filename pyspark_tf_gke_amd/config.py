@@ -69,6 +69,8 @@ _K = [
     Knob("side_stream", bool, True, "PTG_SIDE_STREAM", None, "weight gradients on a side HIP stream (1 replica)"),
     Knob("tape_overlap", bool, True, "PTG_TAPE_OVERLAP", None,
          "GradientTape loops: big Dense Adam on an aux stream overlapping the rest of the backward"),
+    Knob("tape_fused_head", bool, True, "PTG_TAPE_FUSED_HEAD", None,
+         "GradientTape loops: an MSE loss on a [Dense(relu), Dense(<=4)] tail runs the fused head kernels"),
     Knob("tape_lazy_dw", bool, True, "PTG_TAPE_LAZY_DW", None,
          "GradientTape loops: big Dense dW deferred to apply_gradients and fused with Adam (computed on first read)"),
     Knob("raw_u8_input", bool, True, "PTG_RAW_U8_INPUT", None, "first conv reads the uint8 image batch directly"),

@@ -453,6 +453,10 @@ class DenseOp(Op):
         x = _bf16(x, ws, self.name + "/x16")
         # zeroed when (re)allocated; afterwards the head kernel leaves it zero after every step
         acc = ws.get(self.name + "/headacc", (B, N), torch.float32, x.device, zero=True)
+        if not x.is_cuda:
+            acc.add_(x.float() @ self.dense.kernel.bf16.float().t())
+            self._x = x
+            return acc
         tiles = -(-B // 128) * -(-N // 128)
         splits = 1 if Kd < 4096 else max(1, min(16, 512 // max(tiles, 1), Kd // 1024))
         K.gemm(B, N, Kd, x, Kd, 1, self.dense.kernel.bf16, Kd, 1, 3, acc, N, None, 0, splits)

@@ -289,10 +289,14 @@ class Sequential:
             self.build()
         self.wait_deferred()
         xb = self._to_device(x, self._x_dtype(x))
-        out = self._run_forward(xb, training)
         from .tape import _active_tape
 
         tape = _active_tape()
+        if tape is not None and training and self._tape_head_ok():
+            out = self._tape_head_forward(xb)
+            tape.record_forward(self, out)
+            return out
+        out = self._run_forward(xb, training)
         if tape is not None:
             tape.record_forward(self, out)
         if isinstance(self._last_op(), E.DenseOp) and self._last_op().logits_only:
@@ -369,13 +373,39 @@ class Sequential:
             return False
         if st is not None and st.world_size != 1 and not hasattr(st, "on_op_grads_ready"):
             return False
+        return isinstance(self.loss, LS.MeanSquaredError) and self._head_ops_ok()
+
+    def _head_ops_ok(self) -> bool:
         ops = getattr(self, "ops", None) or []
-        if len(ops) < 3 or not isinstance(self.loss, LS.MeanSquaredError):
+        if len(ops) < 3:
             return False
         d1, d2 = ops[-2], ops[-1]
         return (isinstance(d1, E.DenseOp) and isinstance(d2, E.DenseOp) and d1.big and not d2.big
                 and d1.act == "relu" and d2.act in (None, "linear") and d1.dense.bias is not None
                 and d2.dense.bias is not None and d2.dense.units <= 4 and not d1.first)
+
+    def _tape_head_ok(self) -> bool:
+        """A GradientTape forward on one local replica whose tail the fused head covers (the loss is
+        only known when the loss object is called: nn/tape.py _HeadPred)."""
+        from . import tape as T
+
+        if not (T.TAPE_HEAD and FUSED_HEAD and self._head_ops_ok()):
+            return False
+        st = self._strategy()
+        return st is None or getattr(st, "world_size", 2) == 1
+
+    def _tape_head_forward(self, xb):
+        from .tape import _HeadPred, _HeadState, flush_lazy
+
+        if getattr(self, "_lazy_dw", None):
+            flush_lazy(self)
+        d1, d2 = self.ops[-2], self.ops[-1]
+        x = E.run_forward(self.ops[:-2], xb, self.ws, True, pre_op=self._pre_op_hook())
+        acc = d1.forward_splitk_sums(x, self.ws)
+        pred = self.ws.get(d2.name + "/tapepred", (acc.shape[0], d2.dense.units), torch.float32, acc.device)
+        out = pred.as_subclass(_HeadPred)
+        out._lz = _HeadState(self, acc, pred)
+        return out
 
     def _train_step_fused_head(self, xb, yb, stats, st) -> None:
         d1, d2 = self.ops[-2], self.ops[-1]

@@ -14,7 +14,10 @@ The same code runs here.  The tape does not trace Python ops: it records the mod
 ``apply_gradients`` then performs the active strategy's collective (all-reduce / reduce-scatter)
 and the single fused Adam launch.
 
-One local replica (no strategy, or a one-worker parameter server) defers each big Dense layer's
+On one local replica (no strategy, or a one-worker parameter server) a model ending in
+[Dense(relu, big), Dense(N <= 4)] returns its prediction from the tape forward as a deferred tensor
+held at the big layer's split-K sums; an MSE loss object called on it runs fit()'s two-kernel fused
+head instead of the seven-kernel tail + loss + loss gradient.  The same replica defers each big Dense layer's
 weight-gradient GEMM: ``gradient()`` hands back a :class:`_LazyGrad` for that kernel, which computes
 the gradient the moment anything reads it.  When it reaches ``apply_gradients`` untouched, the
 update runs Adam inside that GEMM's epilogue (``ops.nn.linear_dw_adam``, as fit() does) on an
@@ -29,6 +32,7 @@ from .. import config
 _TAPES: list = []
 OVERLAP = config.get("tape_overlap")
 LAZY_DW = config.get("tape_lazy_dw")
+TAPE_HEAD = config.get("tape_fused_head")
 
 
 def _active_tape():
@@ -46,10 +50,10 @@ def _func_name(func) -> str:
     return n
 
 
-class _LazyGrad(torch.Tensor):
-    """The gradient of a big Dense kernel whose GEMM has not run yet.  It aliases the parameter's
-    gradient buffer; any torch operation on it (metadata queries aside) first computes the gradient
-    into that buffer, so user code sees an ordinary tensor."""
+class _Deferred(torch.Tensor):
+    """A tensor whose contents a deferred kernel still has to produce (``_lz.materialize()``).  It
+    aliases the buffer that kernel writes; any torch operation on it (metadata queries aside)
+    first runs the kernel, so user code sees an ordinary tensor."""
 
     @classmethod
     def __torch_function__(cls, func, types, args=(), kwargs=None):
@@ -61,9 +65,74 @@ class _LazyGrad(torch.Tensor):
             return func(*args, **kwargs)
 
 
+class _LazyGrad(_Deferred):
+    """The gradient of a big Dense kernel whose GEMM has not run yet (``_lz``: a :class:`_LazyDW`)."""
+
+
+class _HeadPred(_Deferred):
+    """The prediction of a [..., Dense(relu, big), Dense(N <= 4)] tail under a tape, held at the
+    big layer's split-K sums (``_lz``: a :class:`_HeadState`): an MSE loss object called on it runs
+    fit()'s fused head (forward, loss, head backward in two launches); anything else runs the
+    plain tail first."""
+
+
+class _HeadState:
+    def __init__(self, model, acc, pred):
+        self.model, self.acc, self.pred = model, acc, pred
+        self.state = "pending"  # -> "plain" (unfused tail ran) or "fused" (head_mse ran for the loss)
+        self.dz1 = None
+        self.loss_obj = None
+
+    def materialize(self) -> None:
+        """The unfused tail: Dense1 bias + ReLU from the split-K sums (re-zeroing them), Dense2."""
+        if self.state != "pending":
+            return
+        from ..ops import nn as K
+
+        self.state = "plain"
+        m = self.model
+        d1, d2 = m.ops[-2], m.ops[-1]
+        B, N1 = self.acc.shape
+        y1 = m.ws.get(d1.name + "/y", (B, N1), torch.bfloat16, self.acc.device)
+        K.bias_act(self.acc, d1.dense.bias.data, "relu", out_bf16=y1, clear=True)
+        d1._y = y1
+        if d2.mask_for_prev:
+            d2._prev_y = y1
+        y2 = d2.forward(y1, m.ws, True)
+        self.pred.copy_(y2)
+
+    def fused_loss(self, loss_obj, y_true):
+        """The loss value of an MSE loss object, computed by fit()'s fused head kernels, which also
+        leave dz1 (Dense1's pre-activation gradient) and the Dense2 / Dense1-bias gradients."""
+        from ..ops import nn as K
+
+        m = self.model
+        d1, d2 = m.ops[-2], m.ops[-1]
+        B, K1 = self.acc.shape
+        N2 = d2.dense.units
+        yb = y_true.float()
+        if yb.dim() == 1:
+            yb = yb.view(-1, 1)
+        if tuple(yb.shape) != (B, N2):
+            return None
+        yb = yb.contiguous()
+        flush_lazy(m)
+        m.store.zero_grad()  # the head accumulates the Dense2 and Dense1-bias gradients
+        dev = self.acc.device
+        dz1 = m.ws.get(d1.name + "/dz", (B, K1), torch.bfloat16, dev)
+        scratch = m.ws.get(d1.name + "/headscratch", (B * (N2 + 2),), torch.float32, dev)
+        stats = m.ws.get("__tape_head_stats", (8,), torch.float32, dev)
+        stats.zero_()
+        K.head_mse(self.acc, d1.dense.bias.data, d2.dense.kernel.data, d2.dense.bias.data, yb, dz1,
+                   d2.dense.kernel.grad, d2.dense.bias.grad, d1.dense.bias.grad, stats, pred_out=self.pred,
+                   scratch=scratch)
+        self.state, self.dz1, self.loss_obj = "fused", dz1, loss_obj
+        return stats[2] / float(B * N2)
+
+
 def _materialize_in(xs) -> None:
     for a in xs:
-        if isinstance(a, _LazyGrad):
+        if isinstance(a, _Deferred):
             lz = getattr(a, "_lz", None)
             if lz is not None:
                 lz.materialize()
@@ -173,21 +242,24 @@ class GradientTape:
         if isinstance(self.loss_obj, LS.SparseCategoricalCrossentropy) and isinstance(last, E.DenseOp) \
                 and last.act == "softmax" and not last.logits_only:
             raise RuntimeError("compile() the model with the loss (or build with from_logits) before a tape loop")
-        stats = torch.zeros(8, dtype=torch.float32, device=out.device)
-        saved_loss = m.loss
-        m.loss = self.loss_obj
-        try:
-            yb = self.y_true
-            if isinstance(self.loss_obj, LS.SparseCategoricalCrossentropy):
-                yb = yb.to(torch.int32).view(-1).contiguous()
-            else:
-                yb = yb.float().contiguous()
-                if yb.dim() == 1:
-                    yb = yb.view(-1, 1)
-            m.store.zero_grad()
-            dpred = m._loss_grad(out, yb, stats)
-        finally:
-            m.loss = saved_loss
+        hd = getattr(out, "_lz", None) if isinstance(out, _HeadPred) else None
+        head = hd is not None and hd.state == "fused" and hd.loss_obj is self.loss_obj
+        if not head:
+            stats = torch.zeros(8, dtype=torch.float32, device=out.device)
+            saved_loss = m.loss
+            m.loss = self.loss_obj
+            try:
+                yb = self.y_true
+                if isinstance(self.loss_obj, LS.SparseCategoricalCrossentropy):
+                    yb = yb.to(torch.int32).view(-1).contiguous()
+                else:
+                    yb = yb.float().contiguous()
+                    if yb.dim() == 1:
+                        yb = yb.view(-1, 1)
+                m.store.zero_grad()
+                dpred = m._loss_grad(out, yb, stats)
+            finally:
+                m.loss = saved_loss
         # the same side-stream overlap as fit()'s step (streams.py): every wgrad forks off the dgrad
         # chain and the step's stream joins it before returning, so the gradients handed back are
         # stream-ordered complete, exactly as with the serial backward
@@ -212,7 +284,13 @@ class GradientTape:
 
         try:
             with S.active(side):
-                m._run_backward(dpred, on_op_done=dense_done)
+                if head:  # the head kernels already produced dz1 and the head's own gradients
+                    d1 = m.ops[-2]
+                    dx = d1.backward_dz(hd.dz1, m.ws)
+                    dense_done(d1)
+                    E.run_backward(m.ops[:-2], dx, m.ws, on_op_done=dense_done)
+                else:
+                    m._run_backward(dpred, on_op_done=dense_done)
         finally:
             for op in big:
                 op.fused_update = None

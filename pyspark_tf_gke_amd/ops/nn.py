@@ -591,6 +591,8 @@ def linear_dw_adam(dy, x, p, m, v, pbf, lr_t: float, b1: float, b2: float, eps: 
 def head_mse(acc, b1, w2, b2, tgt, dz1, dw2, db2, db1, stats, pred_out=None, gscale: float = 1.0, scratch=None):
     """Fused Dense(relu) -> Dense(N2) -> MSE head on the Dense1 split-K sums ``acc`` [B, K1] (fp32,
     re-zeroed): stats / dpred as mse_k, dz1 [B, K1] bf16, dw2 / db2 / db1 accumulated (GPU only)."""
+    if not on_device(acc):
+        return ref.head_mse(acc, b1, w2, b2, tgt, dz1, dw2, db2, db1, stats, pred_out, gscale)
     B, K1 = acc.shape
     N2 = w2.shape[0]
     if scratch is None or scratch.numel() < B * (N2 + 2):
@@ -608,11 +610,15 @@ def col_sum(g, out):
     return out
 
 
-def bias_act(acc, bias, act, out_bf16=None, out32=None):
+def bias_act(acc, bias, act, out_bf16=None, out32=None, clear: bool = False):
+    """act(acc + bias) into out_bf16 / out32; ``clear`` re-zeroes acc (a split-K accumulator)."""
     if not on_device(acc):
-        return ref.bias_act(acc, bias, act, out_bf16, out32)
+        ref.bias_act(acc, bias, act, out_bf16, out32)
+        if clear:
+            acc.zero_()
+        return
     M, N = acc.shape
-    hip("ptg_bias_act", ptr(acc), ptr(bias), ptr(out_bf16), ptr(out32), M, N, ACT[act], 0)
+    hip("ptg_bias_act", ptr(acc), ptr(bias), ptr(out_bf16), ptr(out32), M, N, ACT[act], int(clear))
 
 
 def dense_small_fwd(x, w, b, act, out, out_bf16=None):

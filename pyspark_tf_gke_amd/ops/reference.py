@@ -291,6 +291,22 @@ def mse(pred, y, dpred, stats, gscale=1.0):
     stats[4] += B
 
 
+def head_mse(acc, b1, w2, b2, tgt, dz1, dw2, db2, db1, stats, pred_out=None, gscale=1.0):
+    """Dense(relu) -> Dense(N2) -> MSE on the Dense1 split-K sums (head_row_k / head_col_k)."""
+    h = torch.relu(_f(acc) + _f(b1))
+    pred = h @ _f(w2).t() + _f(b2)
+    B, N2 = pred.shape
+    dp = torch.empty_like(pred)
+    mse(pred, tgt, dp, stats, gscale)
+    dz1.copy_(((dp @ _f(w2)) * (h > 0)).to(dz1.dtype))
+    dw2.add_(dp.t() @ h)
+    db2.add_(dp.sum(0))
+    db1.add_(_f(dz1).sum(0))
+    if pred_out is not None:
+        pred_out.copy_(pred)
+    acc.zero_()
+
+
 def softmax_xent(logits, labels, dlogits, stats, gscale=1.0):
     lg = _f(logits)
     B, C = lg.shape

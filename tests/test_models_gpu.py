@@ -313,7 +313,7 @@ def test_tape_loop_overlapped_adam_same_training(hip_built):
                     p = m(xs[i % 2], training=True)
                     lv = lo(ys[i % 2], p)
                 g = tape.gradient(lv, m.trainable_variables)
-                used.append(bool(m._tape_ready) and T._overlap_ok(opt, list(zip(g, m.trainable_variables))))
+                used.append(bool(m._tape_ready) and T._overlap_ok(opt, list(zip(g, m.trainable_variables)), m._tape_ready))
                 opt.apply_gradients(zip(g, m.trainable_variables))
                 losses.append(float(lv))
         finally:
@@ -326,6 +326,46 @@ def test_tape_loop_overlapped_adam_same_training(hip_built):
     m1, l1, _, u1 = run(True)
     assert not any(u0) and all(u1), (u0, u1)  # the overlapped path really ran
     _same_training(m0, m1, init, l0, l1)
+
+
+def test_tape_fused_head_lazy_dw_matches_fit(hip_built):
+    """The tape loop on CNN-B1 (flat) takes fit()'s fused head (MSE on the _HeadPred) and the big
+    Dense dW fused with Adam at apply_gradients (_LazyDW): same training as train_step_fast, and
+    both deferred paths really ran."""
+    from pyspark_tf_gke_amd import nn
+    from pyspark_tf_gke_amd.nn import tape as T
+
+    torch.manual_seed(0)
+    xs = [torch.randint(0, 256, (16, 64, 80, 3), dtype=torch.uint8, device="cuda") for _ in range(2)]
+    ys = [torch.rand(16, 2, device="cuda") * 60 for _ in range(2)]
+    torch.manual_seed(1)
+    mf = build_cnn_model((64, 80, 3), flat=True, summary=False, device="cuda")
+    init = mf.store.flat.clone()
+    st = mf._stats_buf()
+    lf = []
+    for i in range(6):
+        st.zero_()
+        mf.train_step_fast(xs[i % 2], ys[i % 2], st)
+        lf.append(float(st[0] / st[4]))
+    torch.manual_seed(1)
+    mt = build_cnn_model((64, 80, 3), flat=True, summary=False, device="cuda")
+    assert torch.equal(mt.store.flat, init)
+    opt = nn.optimizers.Adam(learning_rate=1e-3)
+    lo = nn.losses.MeanSquaredError()
+    lt, kinds = [], []
+    for i in range(6):
+        with nn.GradientTape() as tape:
+            p = mt(xs[i % 2], training=True)
+            lv = lo(ys[i % 2], p)
+        g = tape.gradient(lv, mt.trainable_variables)
+        kinds.append((isinstance(p, T._HeadPred) and p._lz.state == "fused",
+                      any(isinstance(t, T._LazyGrad) and t._lz.pending for t in g)))
+        opt.apply_gradients(zip(g, mt.trainable_variables))
+        lt.append(float(lv))
+    torch.cuda.synchronize()
+    assert all(a and b for a, b in kinds), kinds
+    assert mt._lazy_dw is None and opt.iterations == 6
+    _same_training(mf, mt, init, lf, lt)
 
 
 def test_ps_one_worker_tape_overlap_same_training(hip_built):

@@ -171,9 +171,14 @@ def test_tape_lazy_dense_dw_matches_train_on_batch():
     m2.compile(optimizer=nn.optimizers.Adam(1e-3), loss="mse")
     opt = nn.optimizers.Adam(1e-3)
     lazies = []
-    for _ in range(3):
-        grads = _tape_step(m1, opt, x, y, touch=lambda g: lazies.extend(t for t in g if isinstance(t, T._LazyGrad)))
-        m2.train_on_batch(x, y)
+    saved = T.TAPE_HEAD
+    T.TAPE_HEAD = False  # the same unfused tail as train_on_batch on the CPU: bitwise-equal inputs to Adam
+    try:
+        for _ in range(3):
+            _tape_step(m1, opt, x, y, touch=lambda g: lazies.extend(t for t in g if isinstance(t, T._LazyGrad)))
+            m2.train_on_batch(x, y)
+    finally:
+        T.TAPE_HEAD = saved
     assert lazies, "the big Dense kernel gradient should be deferred"
     assert all(not t._lz.pending for t in lazies)
     assert m1._lazy_dw is None
@@ -214,3 +219,62 @@ def test_tape_lazy_dense_dw_materializes_on_read():
     assert lz and lz[0]._lz.pending
     m1(x)
     assert not lz[0]._lz.pending and float(torch.linalg.vector_norm(lz[0])) > 0
+
+
+def test_tape_fused_head_matches_unfused_tail():
+    """Under a tape, MSE on the CNN-B1 tail runs the fused head (nn/tape.py _HeadPred): same loss,
+    predictions and gradients as the unfused tail + loss + loss-gradient path (bf16 rounding aside)."""
+    from pyspark_tf_gke_amd.nn import tape as T
+
+    torch.manual_seed(0)
+    x = torch.rand(4, 32, 40, 3)
+    y = torch.rand(4, 2)
+    m = build_cnn_model((32, 40, 3), flat=True, summary=False, device="cpu")
+    res = {}
+    saved = T.TAPE_HEAD
+    try:
+        for head in (True, False):
+            T.TAPE_HEAD = head
+            with nn.GradientTape() as tape:
+                p = m(x, training=True)
+                loss = nn.losses.MeanSquaredError()(y, p)
+            if head:
+                assert isinstance(p, T._HeadPred) and p._lz.state == "fused"
+            g = tape.gradient(loss, m.trainable_variables)
+            res[head] = ([t.float().clone() for t in g], float(loss), p.float().clone())
+    finally:
+        T.TAPE_HEAD = saved
+    assert abs(res[True][1] - res[False][1]) <= 1e-4 * abs(res[False][1])
+    assert torch.allclose(res[True][2], res[False][2], atol=1e-4)
+    for a, b in zip(res[True][0], res[False][0]):
+        assert float((a - b).abs().max()) <= 1e-2 * max(float(b.abs().max()), 1e-3)
+
+
+def test_tape_head_pred_read_first_runs_plain_tail():
+    """A prediction read before the loss (a metric on it) runs the plain tail; the loss then takes
+    the ordinary path and the training matches the unfused run."""
+    from pyspark_tf_gke_amd.nn import tape as T
+
+    torch.manual_seed(2)
+    x = torch.rand(4, 32, 40, 3)
+    y = torch.rand(4, 2)
+    m1 = build_cnn_model((32, 40, 3), flat=True, summary=False, device="cpu")
+    m2 = build_cnn_model((32, 40, 3), flat=True, summary=False, device="cpu")
+    m2.set_weights(m1.get_weights())
+    o1, o2 = nn.optimizers.Adam(1e-3), nn.optimizers.Adam(1e-3)
+    mae = nn.metrics.MeanAbsoluteError()
+    for m, o in ((m1, o1), (m2, o2)):
+        saved = T.TAPE_HEAD
+        T.TAPE_HEAD = m is m1
+        try:
+            with nn.GradientTape() as tape:
+                p = m(x, training=True)
+                mae.update_state(y, p)
+                loss = nn.losses.MeanSquaredError()(y, p)
+            if m is m1:
+                assert p._lz.state == "plain"
+            g = tape.gradient(loss, m.trainable_variables)
+            o.apply_gradients(zip(g, m.trainable_variables))
+        finally:
+            T.TAPE_HEAD = saved
+    assert torch.equal(m1.store.flat, m2.store.flat)
