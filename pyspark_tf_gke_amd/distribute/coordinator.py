@@ -285,6 +285,9 @@ class ClusterCoordinator:
 
         st = self.strategy
         world, rank = st.world_size, st.rank
+        if world == 1:
+            self._join_local()
+            return
         while self._queue:
             batch = self._queue[:world]
             rest = self._queue[world:]
@@ -353,6 +356,47 @@ class ClusterCoordinator:
             self._queue = rest
             heartbeat.progress()
         comm.barrier()
+
+    def _join_local(self) -> None:
+        """One worker: the same transactional rounds (retry, drop after max_retries, commit) with no
+        status exchange and no per-round host tensors."""
+        from ..runtime import heartbeat
+
+        st = self.strategy
+        while self._queue:
+            q, self._queue = self._queue, []
+            for k, item in enumerate(q):
+                tries = item[4]
+                st.begin_round()
+                while True:
+                    status, err, value = self._run_mine(st, item)
+                    if status != 2:
+                        break
+                    st.abort_round()  # the failed attempt's partial gradient
+                    if tries >= self.max_retries:
+                        status = 4
+                        break
+                    self.retries += 1
+                    tries += 1
+                    st.begin_round_retry()
+                mi, oi = st.pending_ids() if status == 1 else (-1, -1)
+                rv = item[3]
+                if status in (1, 3):
+                    rv._set(value)
+                    self.closures_run += 1
+                elif err is not None:
+                    rv._error = err
+                if status == 1 and mi >= 0:
+                    model = st.models[mi]
+                    opt = st.optimizers[oi] if oi < len(st.optimizers) else model.optimizer
+                    try:
+                        st.commit_round(model, opt, [True])
+                    except BaseException:
+                        self._queue = list(q[k + 1:]) + self._queue
+                        raise
+                elif status != 4:
+                    st.abort_round()
+                heartbeat.progress()
 
     def _run_mine(self, st, mine):
         if mine is None:

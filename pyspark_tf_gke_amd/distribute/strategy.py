@@ -158,6 +158,8 @@ class Strategy:
         pend = getattr(self, "_pending", None)
         models = list(self.models) + ([pend[0]] if pend is not None and pend[0] not in self.models else [])
         for m in models:
+            m._lazy_dw = None  # deferred tape weight gradients of the aborted attempt (nn/tape.py)
+            m._tape_overlap = None
             m.store.flat_grad.zero_()
             m.store.grad_clean = True
         self._pending = None

@@ -505,3 +505,46 @@ os._exit(0)
     for v in res.values():
         assert v["vals"] == [i + 100 for i in range(6)], v
     assert res[0]["ran"] + res[1]["ran"] == 6, res
+
+
+def test_coordinator_one_worker_rounds():
+    """One worker (the reference's smallest PS cluster): the local round loop (coordinator.py
+    _join_local) retries a failing closure bit-identically, drops one that keeps failing (no
+    optimizer step, error on its RemoteValue), passes StopIteration through and returns values."""
+    body = COMMON + """
+st = ParameterServerStrategy()
+assert st.world_size == 1
+m_ok, o_ok = make(st)
+m_ft, o_ft = make(st)
+co = ClusterCoordinator(st)
+for i in range(6):
+    co.schedule(step_fn, args=(m_ok, o_ok, i))
+co.join()
+fail = {2: 1, 4: 5, "ranks": (0,)}   # closure 2 fails once, closure 4 always
+co2 = ClusterCoordinator(st, max_retries=2)
+rvs = [co2.schedule(step_fn, args=(m_ft, o_ft, i, fail, st.rank)) for i in range(6)]
+def stop():
+    raise StopIteration
+rs = co2.schedule(stop)
+co2.join()
+errs = []
+for rv in rvs + [rs]:
+    try:
+        errs.append(rv.fetch())
+    except BaseException as e:
+        errs.append(type(e).__name__)
+m_ref, o_ref = make(st)
+co3 = ClusterCoordinator(st)
+for i in (0, 1, 2, 3, 5):
+    co3.schedule(step_fn, args=(m_ref, o_ref, i))
+co3.join()
+print("RESULT", json.dumps({"retries": co2.retries, "it_ok": o_ok.iterations, "it_ft": o_ft.iterations,
+                            "vals": errs, "same_as_skip4": bool(torch.equal(flat(m_ref), flat(m_ft))),
+                            "ran": co2.closures_run}), flush=True)
+"""
+    r = _launch(body, 1)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    v = _results(r.stdout)[0]
+    assert v["retries"] == 3 and v["it_ok"] == 6 and v["it_ft"] == 5, v
+    assert v["vals"] == [1, 1, 1, 1, "RuntimeError", 1, "StopIteration"], v
+    assert v["same_as_skip4"] and v["ran"] == 5, v
