@@ -20,8 +20,10 @@ each.  Workers never hold a current fp32 copy of the bf16 pieces between steps
 ``mode="async"`` (TF's asynchronous PS): no collective per step.  Each rank exposes a one-sided
 *window* - [owned fp32 values][owned bf16 values][NSLOT gradient inbox slots] - in HBM exported
 with HIP IPC (peers map it over xGMI; on CPU ranks a shared-memory file).  A worker's push claims a
-ticket per owner from the TCP store, writes its gradient pieces straight into the owners' inbox
-slots (one kernel for all owners), publishes the tickets and waits until the owners applied them
+ticket per owner (an atomic fetch-add in a /dev/shm control block, :class:`_Mailbox`, signalled
+with shared futexes by csrc/host/shmsync.cpp instead of TCP-store round trips), writes its gradient
+pieces straight into the owners' inbox slots (one kernel for all owners), publishes the tickets and
+waits until the owners applied them
 (``apply_gradients`` returns after the PS update, as in TF); each owner runs a service thread that
 applies every push as its own optimizer step, in ticket order, on its own HIP stream - while its
 main thread is busy with its own closure.  Pulls read the owners' bf16 / fp32 values directly from
@@ -34,6 +36,7 @@ from __future__ import annotations
 import ctypes
 import datetime
 import math
+import mmap
 import os
 import threading
 import uuid
@@ -336,6 +339,87 @@ class _PSWindow:
         self._files = []
 
 
+class _Mailbox:
+    """Push signalling of one async-PS model between the ranks of a node: per owner one 64-byte line
+    each for the ticket counter, the applied counter and a stop word, then NSLOT slot lines
+    (sequence, optimizer index, gradient scale).  Rank 0 creates the /dev/shm file, every rank maps
+    it; the atomics and futex waits are csrc/host/shmsync.cpp."""
+
+    LINE = 64
+    PER = 3 + NSLOT
+
+    def __init__(self, path: str, world: int, rank: int):
+        from .. import _native
+
+        self.lib = _native.host_lib()
+        self.path, self.world, self.owner_file = path, world, rank == 0
+        size = world * self.PER * self.LINE
+        if rank == 0:
+            with open(path, "wb") as fh:
+                fh.truncate(size)
+        comm.barrier()
+        fd = os.open(path, os.O_RDWR)
+        try:
+            self.mm = mmap.mmap(fd, size)
+        finally:
+            os.close(fd)
+        self._anchor = ctypes.c_char.from_buffer(self.mm)
+        self.base = ctypes.addressof(self._anchor)
+        self.timeout_s = float(config.get("pg_timeout_s"))
+
+    def _line(self, r: int, k: int) -> ctypes.c_void_p:
+        return ctypes.c_void_p(self.base + (r * self.PER + k) * self.LINE)
+
+    def ticket(self, r: int) -> int:
+        old = ctypes.c_int()
+        self.lib.ptgh_shm_add(self._line(r, 0), 1, ctypes.byref(old))
+        return old.value
+
+    def tickets_issued(self, r: int) -> int:
+        v = ctypes.c_int()
+        self.lib.ptgh_shm_load(self._line(r, 0), ctypes.byref(v))
+        return v.value
+
+    def wait_applied(self, r: int, n: int, alive=None) -> None:
+        """Block until owner r applied n pushes; ``alive()`` raises if this rank's own service died."""
+        waited = 0.0
+        while self.lib.ptgh_shm_wait_ge(self._line(r, 1), int(n), 1_000_000):
+            waited += 1.0
+            if alive is not None:
+                alive()
+            if waited >= self.timeout_s:
+                raise RuntimeError(f"parameter server {r} did not apply push {n - 1} within {self.timeout_s:.0f} s")
+
+    def set_applied(self, r: int, n: int) -> None:
+        self.lib.ptgh_shm_store(self._line(r, 1), int(n))
+
+    def publish(self, r: int, t: int, gscale: float, oi: int) -> None:
+        self.lib.ptgh_mbox_publish(self._line(r, 3 + t % NSLOT), t + 1, float(gscale), int(oi))
+
+    def take(self, r: int, t: int, timeout_us: int):
+        """(gscale, optimizer index) of push t to owner r, or None on timeout."""
+        g, oi = ctypes.c_double(), ctypes.c_int()
+        if self.lib.ptgh_mbox_take(self._line(r, 3 + t % NSLOT), t + 1, int(timeout_us), ctypes.byref(g),
+                                   ctypes.byref(oi)):
+            return None
+        return g.value, oi.value
+
+    def wake(self, r: int, t: int) -> None:
+        self.lib.ptgh_shm_wake(self._line(r, 3 + t % NSLOT))
+
+    def close(self) -> None:
+        if self.mm is None:
+            return
+        del self._anchor
+        self.mm.close()
+        self.mm = None
+        if self.owner_file:
+            try:
+                os.unlink(self.path)
+            except OSError:
+                pass
+
+
 class _OwnerService(threading.Thread):
     """Applies the pushes addressed to this rank's shards, one optimizer step each, in ticket order,
     on its own stream, while the rank's main thread runs closures (async mode)."""
@@ -354,25 +438,19 @@ class _OwnerService(threading.Thread):
         self._one = _PieceTable([(0, 0, 0, 0, plan.seg)], plan.device)
 
     def run(self):  # noqa: D401 - thread body
-        store = _store()
         rank = self.plan.rank
+        mbox = self.plan.mbox
         if self.plan.device.type == "cuda":
             torch.cuda.set_device(self.plan.device)  # a new thread starts on device 0
         stream = torch.cuda.Stream(self.plan.device) if self.plan.device.type == "cuda" else None
         try:
             while not self.stop_flag:
-                key = f"{self.prefix}/{rank}/ready/{self.applied}"
-                try:
-                    store.wait([key], datetime.timedelta(seconds=2))
-                except Exception:  # noqa: BLE001 - timeout: look at the stop flag, wait again
+                got = mbox.take(rank, self.applied, 500_000)
+                if got is None:  # timeout: look at the stop flag, wait again
                     continue
-                msg = store.get(key).decode()
-                if msg == "STOP":
-                    break
-                gs, _, oi = msg.partition("|")
-                gscale = float(gs)
+                gscale, oi = got
                 t = self.applied
-                opt = self.st.optimizers[int(oi)] if oi else self.model.optimizer
+                opt = self.st.optimizers[oi] if oi >= 0 else self.model.optimizer
                 self.last_opt = opt
                 ctx = torch.cuda.stream(stream) if stream is not None else _nullctx()
                 with ctx:
@@ -384,7 +462,7 @@ class _OwnerService(threading.Thread):
                 if stream is not None:
                     stream.synchronize()
                 self.applied = t + 1
-                store.set(f"{self.prefix}/{rank}/done/{t}", "1")
+                mbox.set_applied(rank, t + 1)
         except BaseException as e:  # noqa: BLE001 - surfaced to the main thread on its next push
             self.error = e
 
@@ -440,6 +518,7 @@ class ParameterServerStrategy(Strategy):
             plan.window = _PSWindow(plan, prefix)
             plan.window.publish_values(plan.master, plan.master_bf)
             plan.prefix = prefix
+            plan.mbox = _Mailbox("/dev/shm/" + prefix.replace("/", "_") + "_ctl", self.world_size, self.rank)
             plan.tickets = [0] * self.world_size
             svc = _OwnerService(self, model, plan, plan.window, prefix)
             plan.service = svc
@@ -491,7 +570,6 @@ class ParameterServerStrategy(Strategy):
         ``apply_gradients`` on PS variables returns after the PS update); then pull."""
         plan = model._ps_plan
         st = model.store
-        store = _store()
         svc = plan.service
         if svc.error is not None:
             raise RuntimeError("parameter-server service thread failed") from svc.error
@@ -499,18 +577,19 @@ class ParameterServerStrategy(Strategy):
         # every rank only for optimizers created under strategy.scope(); the model's compiled
         # optimizer is addressed as "" (every owner has its own copy of that model)
         if any(o is opt for o in self.optimizers):
-            oi = str(next(i for i, o in enumerate(self.optimizers) if o is opt))
+            oi = next(i for i, o in enumerate(self.optimizers) if o is opt)
         elif opt is model.optimizer:
-            oi = ""
+            oi = -1
         else:
             raise RuntimeError("asynchronous ParameterServerStrategy: create the optimizer under strategy.scope() "
                                "(or compile it into the model) so every parameter server knows it")
         owners = [r for r in range(self.world_size) if plan.owner_elems[r] > 0]
+        mbox = plan.mbox
         tick = {}
         for r in owners:
-            t = store.add(f"{plan.prefix}/{r}/tickets", 1) - 1
+            t = mbox.ticket(r)
             if t >= NSLOT:  # the slot's previous push must have been consumed
-                store.wait([f"{plan.prefix}/{r}/done/{t - NSLOT}"])
+                mbox.wait_applied(r, t - NSLOT + 1, self._check_service(svc))
             tick[r] = t
         win = plan.window
         dsts = [win.inbox(r, tick[r] % NSLOT) if r in tick else win.inbox(self.rank, 0)
@@ -519,23 +598,30 @@ class ParameterServerStrategy(Strategy):
         if st.flat_grad.is_cuda:
             torch.cuda.current_stream(st.flat_grad.device).synchronize()
         for r, t in tick.items():
-            store.set(f"{plan.prefix}/{r}/ready/{t}", f"{float(self._commit_scale)!r}|{oi}")
+            mbox.publish(r, t, self._commit_scale, oi)
         self._closure_pushed = True  # from here on the update is applied whatever the closure does next
-        store.wait([f"{plan.prefix}/{r}/done/{t}" for r, t in tick.items()])
+        for r, t in tick.items():
+            mbox.wait_applied(r, t + 1, self._check_service(svc))
         opt.iterations += 1
         self._pull(model)
+
+    @staticmethod
+    def _check_service(svc):
+        def alive():
+            if svc.error is not None:
+                raise RuntimeError("parameter-server service thread failed") from svc.error
+        return alive
 
     def wait_all_applied(self) -> None:
         """Collective: every push issued so far has been applied by its owner (end of ``join``)."""
         comm.barrier()
-        store = _store()
         for model in self.models:
             plan = getattr(model, "_ps_plan", None)
             if plan is None or plan.window is None:
                 continue
-            n = store.add(f"{plan.prefix}/{self.rank}/tickets", 0)
+            n = plan.mbox.tickets_issued(self.rank)
             if n:
-                store.wait([f"{plan.prefix}/{self.rank}/done/{n - 1}"])
+                plan.mbox.wait_applied(self.rank, n, self._check_service(plan.service))
         comm.barrier()
         for model in self.models:
             if getattr(model, "_ps_plan", None) is not None and model._ps_plan.window is not None:
@@ -552,14 +638,13 @@ class ParameterServerStrategy(Strategy):
         """Stop the owner threads and unmap the windows (collective)."""
         if not self._services:
             return
-        store = _store()
         comm.barrier()
         for model in self.models:
             plan = getattr(model, "_ps_plan", None)
             if plan is None or plan.window is None:
                 continue
             plan.service.stop_flag = True
-            store.set(f"{plan.prefix}/{self.rank}/ready/{plan.service.applied}", "STOP")
+            plan.mbox.wake(self.rank, plan.service.applied)
         for svc in self._services:
             svc.join(timeout=10)
         comm.barrier()
@@ -568,6 +653,7 @@ class ParameterServerStrategy(Strategy):
             if plan is not None and plan.window is not None:
                 plan.window.close()
                 plan.window = None
+                plan.mbox.close()
         self._services = []
 
     # ---- engine hooks -----------------------------------------------------------------------------
