@@ -88,6 +88,8 @@ _K = [
     Knob("conv32", bool, False, "PTG_CONV32", None,
          "5x5 convs with C, Cout in 16..64 (CNN-B1 layers 3-5 and their data gradients): the 32x32x16-MFMA "
          "implicit GEMM of conv32.hip instead of the halo strip kernels"),
+    Knob("conv32_min_ch", int, 32, "PTG_CONV32_MINCH", None,
+         "conv32 only where min(C, Cout) >= this (layer bench: it wins on CNN-B1 layers 4-5, loses the 32->16 dgrad)"),
     Knob("ppb_rows", bool, False, "PTG_PPB_ROWS", None,
          "CNN-B1 layers 2-4: PReLU + max-pool backward in the row-pair layout (ppb.hip, dalpha via chunk partials)"),
     Knob("conv1_rec", bool, True, "PTG_CONV1_REC", None, "first conv layer (conv1.hip): forward keeps the pool record, backward needs no recompute (0: recompute z in the backward)"),

@@ -190,6 +190,7 @@ def conv2d_fwd_fused(x, w, bias, pad: int, z_out, alpha=None, aux_out=None, epi=
 
 EPI32 = {None: 0, "z": 0, "pool": 1, "prelu": 2}
 CONV32 = config.get("conv32")
+CONV32_MINCH = config.get("conv32_min_ch")
 _C32_OK: dict = {}
 
 
@@ -197,7 +198,7 @@ def _conv32_ok(H, W, C, Cout, epi) -> bool:
     key = (H, W, C, Cout, epi)
     v = _C32_OK.get(key)
     if v is None:
-        v = _C32_OK[key] = conv32_supported(H, W, C, Cout, 5, 2, epi)
+        v = _C32_OK[key] = min(C, Cout) >= CONV32_MINCH and conv32_supported(H, W, C, Cout, 5, 2, epi)
     return v
 
 
