@@ -9,12 +9,12 @@
 //     strides so threads of one wave that read different rows hit different banks;
 //   * every layer's activation for the batch (kept for the backward) and two ping-pong gradient
 //     buffers.
-// Per step: forward (thread per output element), fused softmax + cross-entropy (or MSE) producing
-// dlogits, then per layer from the top ONE phase that computes dX for the layer below (with the
-// ReLU mask) from the pre-update LDS weights AND each parameter's gradient followed immediately
-// by its Adam update straight into the flat master / m / v / bf16 copy in HBM (no gradient buffer
-// is written).  After the last layer the updated weights are re-read into LDS by the threads that
-// wrote them.  ``steps`` > 1 runs consecutive batches of a device-resident dataset in the same
+// Per step: forward, fused softmax + cross-entropy (or MSE) producing dlogits, then per layer from
+// the top ONE phase that computes dX for the layer below (with the ReLU mask) from the pre-update
+// LDS weights AND each parameter's gradient followed immediately by its Adam update straight into
+// the flat master / m / v / bf16 copy in HBM and into the second LDS weight copy (no gradient
+// buffer is written; the copies swap roles every step).  Every matrix product is a register-tiled
+// LDS GEMM (tile_gemm: up to 4 x 4 outputs per thread).  ``steps`` > 1 runs consecutive batches of a device-resident dataset in the same
 // launch (Keras' steps_per_execution): each step is still a full forward / backward / Adam step.
 // Metric sums are kept in registers and added to `stats` once (the layouts of softmax_xent_k /
 // mse_k).
@@ -30,7 +30,8 @@ struct MlpDesc {
   int d[MAXL + 1];              // d[0] input features, d[l + 1] units of layer l
   int act[MAXL];                // hidden activation of layer l: 0 linear, 1 relu (last: from loss)
   long woff[MAXL], boff[MAXL];  // element offsets of W_l ([d[l+1]][d[l]]) and b_l in the flat store
-  int lw[MAXL], lb[MAXL];       // LDS float offsets of W_l (row stride ws[l]) and b_l
+  int lw[MAXL], lb[MAXL];       // LDS float offsets of W_l (row stride ws[l]) and b_l, copy 0
+  int wtot;                     // floats of one weight copy (copy 1 starts there)
   int ws[MAXL];                 // LDS row stride of W_l (odd)
   int la[MAXL + 1], as[MAXL + 1];  // LDS offset / row stride (odd) of activation l
   int lg0, lg1, gs;             // the two gradient buffers (row stride gs, odd) and red scratch
@@ -51,6 +52,57 @@ PTG_DEV float sum_block(float v, float* red) {
   return r;
 }
 
+// out(i, j) = sum_k P[i*pi + k*pk] * Q[j*qj + k*qk] for i < M, j < N, all operands in LDS.  Each
+// thread owns a TM x TN register tile: TM + TN LDS reads feed TM*TN independent FMA chains (the
+// step is latency-bound on one CU, so the ILP is what matters).  Out-of-range rows / columns read
+// the last valid one and are dropped at the epilogue.
+template <int TM, int TN, class Epi>
+PTG_DEV void tile_gemm(int M, int N, int K, const float* P, int pi, int pk, const float* Q, int qj, int qk,
+                       Epi epi) {
+  const int tm = (M + TM - 1) / TM, tn = (N + TN - 1) / TN;
+  for (int t = threadIdx.x; t < tm * tn; t += NT) {
+    const int i0 = (t / tn) * TM, j0 = (t - (t / tn) * tn) * TN;
+    const float* pr[TM];
+    const float* qr[TN];
+#pragma unroll
+    for (int a = 0; a < TM; ++a) pr[a] = P + min(i0 + a, M - 1) * pi;
+#pragma unroll
+    for (int b = 0; b < TN; ++b) qr[b] = Q + min(j0 + b, N - 1) * qj;
+    float acc[TM][TN];
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b) acc[a][b] = 0.f;
+    for (int k = 0; k < K; ++k) {
+      float av[TM], bv[TN];
+#pragma unroll
+      for (int a = 0; a < TM; ++a) av[a] = pr[a][k * pk];
+#pragma unroll
+      for (int b = 0; b < TN; ++b) bv[b] = qr[b][k * qk];
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b) acc[a][b] = fmaf(av[a], bv[b], acc[a][b]);
+    }
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b)
+        if (i0 + a < M && j0 + b < N) epi(i0 + a, j0 + b, acc[a][b]);
+  }
+}
+
+// the largest register tile that still gives every thread at least one tile
+template <class Epi>
+PTG_DEV void gemm(int M, int N, int K, const float* P, int pi, int pk, const float* Q, int qj, int qk, Epi epi) {
+  const int outs = M * N;
+  if (outs >= 16 * NT) tile_gemm<4, 4>(M, N, K, P, pi, pk, Q, qj, qk, epi);
+  else if (outs >= 8 * NT) tile_gemm<2, 4>(M, N, K, P, pi, pk, Q, qj, qk, epi);
+  else if (outs >= 4 * NT) tile_gemm<2, 2>(M, N, K, P, pi, pk, Q, qj, qk, epi);
+  else if (outs >= 2 * NT) tile_gemm<1, 2>(M, N, K, P, pi, pk, Q, qj, qk, epi);
+  else tile_gemm<1, 1>(M, N, K, P, pi, pk, Q, qj, qk, epi);
+}
+
 __global__ __launch_bounds__(NT) void mlp_train_k(const float* __restrict__ x, const void* __restrict__ y,
                                                   float* __restrict__ p, float* __restrict__ m,
                                                   float* __restrict__ v, bf16_t* __restrict__ pbf,
@@ -58,35 +110,35 @@ __global__ __launch_bounds__(NT) void mlp_train_k(const float* __restrict__ x, c
   extern __shared__ __align__(16) float sm[];
   const int tid = threadIdx.x;
   const int L = D.L, B = D.B;
-  // weights + biases -> LDS
+  // weights + biases -> LDS (copy 0; the Adam epilogues write the updated values into the other copy)
   for (int l = 0; l < L; ++l) {
     const int K = D.d[l], N = D.d[l + 1], S = D.ws[l];
     for (int i = tid; i < N * K; i += NT) sm[D.lw[l] + (i / K) * S + i % K] = p[D.woff[l] + i];
-    for (int n = tid; n < N; n += NT) sm[D.lb[l] + n] = D.boff[l] >= 0 ? p[D.boff[l] + n] : 0.f;
+    for (int n = tid; n < N; n += NT) {
+      sm[D.lb[l] + n] = D.boff[l] >= 0 ? p[D.boff[l] + n] : 0.f;
+      if (D.boff[l] < 0) sm[D.wtot + D.lb[l] + n] = 0.f;  // a bias-less layer's zeros in both copies
+    }
   }
   float s_loss = 0.f, s_a = 0.f, s_b = 0.f;
   const int C = D.d[L];
+  int wcur = 0;  // float offset of the current weight copy
   for (int st = 0; st < D.steps; ++st) {
+    const int wnxt = D.wtot - wcur;
     // ---- input batch
     const int K0 = D.d[0];
     const float* xs = x + (long)st * B * K0;
     for (int i = tid; i < B * K0; i += NT) sm[D.la[0] + (i / K0) * D.as[0] + i % K0] = xs[i];
     __syncthreads();
-    // ---- forward: thread per output element
+    // ---- forward: O[r][n] = act(b[n] + A[r] . W[n])
     for (int l = 0; l < L; ++l) {
-      const int K = D.d[l], N = D.d[l + 1], S = D.ws[l], SA = D.as[l], SO = D.as[l + 1];
-      const float* A = sm + D.la[l];
-      const float* W = sm + D.lw[l];
+      const int K = D.d[l], N = D.d[l + 1], SO = D.as[l + 1];
+      const float* bias = sm + wcur + D.lb[l];
       float* O = sm + D.la[l + 1];
       const bool relu = l < L - 1 && D.act[l] == 1;
-      for (int i = tid; i < B * N; i += NT) {
-        const int r = i / N, n = i - r * N;
-        const float* a = A + r * SA;
-        const float* w = W + n * S;
-        float acc = sm[D.lb[l] + n];
-        for (int k = 0; k < K; ++k) acc = fmaf(a[k], w[k], acc);
+      gemm(B, N, K, sm + D.la[l], D.as[l], 1, sm + wcur + D.lw[l], D.ws[l], 1, [&](int r, int n, float acc) {
+        acc += bias[n];
         O[r * SO + n] = relu ? fmaxf(acc, 0.f) : acc;
-      }
+      });
       __syncthreads();
     }
     // ---- loss: dlogits into gradient buffer 0
@@ -124,63 +176,60 @@ __global__ __launch_bounds__(NT) void mlp_train_k(const float* __restrict__ x, c
       }
     }
     __syncthreads();
-    // ---- backward: per layer one phase (dX below + gradient + Adam), one barrier
+    // ---- backward: per layer one phase (dX below from the current weights + each gradient's Adam
+    // update into HBM and into the next weight copy), one barrier
     const float t = (float)(D.t0 + st + 1);
     const float lr_t = D.lr * sqrtf(1.f - powf(D.b2, t)) / (1.f - powf(D.b1, t));
+    const float b1 = D.b1, b2 = D.b2, eps = D.eps;
     int cur = D.lg0, nxt = D.lg1;
     for (int l = L - 1; l >= 0; --l) {
       const int K = D.d[l], N = D.d[l + 1], S = D.ws[l], SA = D.as[l];
       const float* Gc = sm + cur;
       const float* A = sm + D.la[l];
-      const float* W = sm + D.lw[l];
       if (l > 0) {
         const bool mask = D.act[l - 1] == 1;
         float* Gn = sm + nxt;
-        for (int i = tid; i < B * K; i += NT) {
-          const int r = i / K, k = i - r * K;
-          const float* g = Gc + r * D.gs;
-          float s = 0.f;
-          for (int n = 0; n < N; ++n) s = fmaf(g[n], W[n * S + k], s);
+        const int gs = D.gs;
+        // Gn[r][k] = (G[r] . W[:, k]) * relu'(A[r][k])
+        gemm(B, K, N, Gc, gs, 1, sm + wcur + D.lw[l], 1, S, [&](int r, int k, float s) {
           if (mask && !(A[r * SA + k] > 0.f)) s = 0.f;
-          Gn[r * D.gs + k] = s;
-        }
+          Gn[r * gs + k] = s;
+        });
       }
-      const int nb = D.boff[l] >= 0 ? N : 0;
-      for (int i = tid; i < N * K + nb; i += NT) {
-        float g = 0.f;
-        long idx;
-        if (i < N * K) {
-          const int n = i / K, k = i - n * K;
-          for (int r = 0; r < B; ++r) g = fmaf(Gc[r * D.gs + n], A[r * SA + k], g);
-          idx = D.woff[l] + i;
-        } else {
-          const int n = i - N * K;
-          for (int r = 0; r < B; ++r) g += Gc[r * D.gs + n];
-          idx = D.boff[l] + n;
-        }
-        const float mm = D.b1 * m[idx] + (1.f - D.b1) * g;
-        const float vv = D.b2 * v[idx] + (1.f - D.b2) * g * g;
-        const float pp = p[idx] - lr_t * mm / (sqrtf(vv) + D.eps);
+      // dW[n][k] = sum_r G[r][n] A[r][k], Adam straight from the register
+      float* Wn = sm + wnxt + D.lw[l];
+      const long wo = D.woff[l];
+      gemm(N, K, B, Gc, 1, D.gs, A, 1, SA, [&](int n, int k, float g) {
+        const long idx = wo + (long)n * K + k;
+        const float mm = b1 * m[idx] + (1.f - b1) * g;
+        const float vv = b2 * v[idx] + (1.f - b2) * g * g;
+        const float pp = p[idx] - lr_t * mm / (sqrtf(vv) + eps);
         m[idx] = mm;
         v[idx] = vv;
         p[idx] = pp;
         if (pbf) pbf[idx] = f2bf(pp);
+        Wn[n * S + k] = pp;
+      });
+      if (D.boff[l] >= 0) {
+        float* bn = sm + wnxt + D.lb[l];
+        for (int n = tid; n < N; n += NT) {
+          float g = 0.f;
+          for (int r = 0; r < B; ++r) g += Gc[r * D.gs + n];
+          const long idx = D.boff[l] + n;
+          const float mm = b1 * m[idx] + (1.f - b1) * g;
+          const float vv = b2 * v[idx] + (1.f - b2) * g * g;
+          const float pp = p[idx] - lr_t * mm / (sqrtf(vv) + eps);
+          m[idx] = mm;
+          v[idx] = vv;
+          p[idx] = pp;
+          if (pbf) pbf[idx] = f2bf(pp);
+          bn[n] = pp;
+        }
       }
       __syncthreads();
       const int tmp = cur; cur = nxt; nxt = tmp;
     }
-    // ---- updated weights back into LDS (each thread re-reads exactly what it wrote)
-    if (st + 1 < D.steps) {
-      for (int l = 0; l < L; ++l) {
-        const int K = D.d[l], N = D.d[l + 1], S = D.ws[l];
-        const int nb = D.boff[l] >= 0 ? N : 0;
-        for (int i = tid; i < N * K + nb; i += NT) {
-          if (i < N * K) sm[D.lw[l] + (i / K) * S + i % K] = p[D.woff[l] + i];
-          else sm[D.lb[l] + (i - N * K)] = p[D.boff[l] + (i - N * K)];
-        }
-      }
-      // (the next step's input barrier orders these writes before any forward read)
-    }
+    wcur = wnxt;  // (the next step's input barrier orders the new copy before any forward read)
   }
   float* red = sm + D.lred;
   const float tl = sum_block(s_loss, red);
@@ -226,6 +275,8 @@ static long mlp_plan(const long* hdesc, int L, int B, ptgm::MlpDesc* D) {
     D->lw[l] = off; off += D->d[l + 1] * D->ws[l];
     D->lb[l] = off; off += D->d[l + 1];
   }
+  D->wtot = off;
+  off *= 2;  // two weight copies: a step reads one while its Adam epilogues write the other
   for (int l = 0; l <= L; ++l) {
     D->as[l] = odd(D->d[l]);
     D->la[l] = off; off += B * D->as[l];
