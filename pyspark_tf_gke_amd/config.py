@@ -67,6 +67,9 @@ _K = [
     Knob("fused_head", bool, True, "PTG_FUSED_HEAD", None, "CNN-B1 Dense(relu)->Dense->MSE head as two kernels"),
     Knob("device_feed", bool, True, "PTG_DEVICE_FEED", None, "fit(): pinned ring + side-stream H2D for host datasets"),
     Knob("side_stream", bool, True, "PTG_SIDE_STREAM", None, "weight gradients on a side HIP stream (1 replica)"),
+    Knob("side_cu_quarters", int, 4, "PTG_SIDE_CU_QUARTERS", None,
+         "side stream confined to 1-3 quarters of the CUs (4 = all): its wgrad / Dense dW+Adam kernels then "
+         "never take CUs from the step's dgrad chain"),
     Knob("tape_overlap", bool, True, "PTG_TAPE_OVERLAP", None,
          "GradientTape loops: big Dense Adam on an aux stream overlapping the rest of the backward"),
     Knob("tape_fused_head", bool, True, "PTG_TAPE_FUSED_HEAD", None,

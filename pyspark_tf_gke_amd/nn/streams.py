@@ -19,6 +19,7 @@ import torch
 from .. import config
 
 ENABLED = config.get("side_stream")
+SIDE_CU_QUARTERS = config.get("side_cu_quarters")
 _STREAMS: dict = {}
 
 
@@ -26,8 +27,25 @@ def _stream(dev) -> "torch.cuda.Stream":
     dev = torch.device(dev)
     s = _STREAMS.get(dev)
     if s is None:
-        s = _STREAMS[dev] = torch.cuda.Stream(device=dev)
+        s = _STREAMS[dev] = _new_side_stream(dev)
     return s
+
+
+def _new_side_stream(dev):
+    """The side stream; PTG_SIDE_CU_QUARTERS < 4 confines it to that many quarters of the CUs
+    (csrc/kernels/comm.hip ptg_stream_cumask_create), so its kernels never occupy the CUs the
+    step's own chain runs on."""
+    q = int(SIDE_CU_QUARTERS)
+    if q >= 4:
+        return torch.cuda.Stream(device=dev)
+    import ctypes
+
+    from .. import _native
+
+    with torch.cuda.device(dev):
+        h = ctypes.c_void_p()
+        _native.check(_native.hip_lib().ptg_stream_cumask_create(q, ctypes.byref(h)), "ptg_stream_cumask_create")
+        return torch.cuda.ExternalStream(h.value, device=dev)
 
 
 class SideStream:
