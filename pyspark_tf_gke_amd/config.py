@@ -50,6 +50,9 @@ _K = [
          "sparse keys at ~64K..1.3M groups: one 512-way hash partition + LDS hash tables (sum/count/avg, <= 2 columns)"),
     Knob("groupby_h9_chunks", int, 4, "PTG_H9_CHUNKS", "spark.ptg.groupby.h9Chunks",
          "row chunks per partition in the 512-way hash aggregation (workgroups = 512 x chunks)"),
+    Knob("sort_onesweep", bool, True, "PTG_SORT_ONESWEEP", "spark.ptg.sort.onesweep",
+         "radix sort passes without a count pass: every pass's digit histogram from one read, tile offsets by "
+         "decoupled look-back (onesweep)"),
     Knob("shuffle_buffer_gb", float, 64.0, "PTG_SHUFFLE_BUFFER_GB", "spark.ptg.shuffle.buffer.gb",
          "HBM staging budget of one all-to-all-v shuffle round"),
     Knob("device", str, "", "PTG_DEVICE", "spark.ptg.device", "executor device: cuda / cpu (default: cuda if present)"),
