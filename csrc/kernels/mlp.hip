@@ -103,13 +103,17 @@ PTG_DEV void gemm(int M, int N, int K, const float* P, int pi, int pk, const flo
   else tile_gemm<1, 1>(M, N, K, P, pi, pk, Q, qj, qk, epi);
 }
 
+// tstep (nullable): the optimizer step counter on the device (read for Adam's bias correction and
+// advanced by `steps` at the end), so a cached launch needs no per-step host argument
 __global__ __launch_bounds__(NT) void mlp_train_k(const float* __restrict__ x, const void* __restrict__ y,
                                                   float* __restrict__ p, float* __restrict__ m,
                                                   float* __restrict__ v, bf16_t* __restrict__ pbf,
-                                                  float* __restrict__ stats, const MlpDesc D) {
+                                                  float* __restrict__ stats, float* __restrict__ tstep,
+                                                  const MlpDesc D) {
   extern __shared__ __align__(16) float sm[];
   const int tid = threadIdx.x;
   const int L = D.L, B = D.B;
+  const int t0 = tstep ? (int)tstep[0] : D.t0;
   // weights + biases -> LDS (copy 0; the Adam epilogues write the updated values into the other copy)
   for (int l = 0; l < L; ++l) {
     const int K = D.d[l], N = D.d[l + 1], S = D.ws[l];
@@ -178,7 +182,7 @@ __global__ __launch_bounds__(NT) void mlp_train_k(const float* __restrict__ x, c
     __syncthreads();
     // ---- backward: per layer one phase (dX below from the current weights + each gradient's Adam
     // update into HBM and into the next weight copy), one barrier
-    const float t = (float)(D.t0 + st + 1);
+    const float t = (float)(t0 + st + 1);
     const float lr_t = D.lr * sqrtf(1.f - powf(D.b2, t)) / (1.f - powf(D.b1, t));
     const float b1 = D.b1, b2 = D.b2, eps = D.eps;
     int cur = D.lg0, nxt = D.lg1;
@@ -236,6 +240,7 @@ __global__ __launch_bounds__(NT) void mlp_train_k(const float* __restrict__ x, c
   const float ta = sum_block(s_a, red);
   const float tb = sum_block(s_b, red);
   if (tid == 0) {
+    if (tstep) tstep[0] = (float)(t0 + D.steps);  // every thread read it before the barriers above
     const float nb = (float)(B * D.steps);
     if (D.loss == 0) {
       stats[0] += tl;
@@ -313,8 +318,49 @@ int ptg_mlp_train(const void* x, const void* y, float* p, float* m, float* v, vo
     attr = true;
   }
   hipLaunchKernelGGL(ptgm::mlp_train_k, dim3(1), dim3(ptgm::NT), (size_t)bytes, s, (const float*)x, y, p, m, v,
-                     (bf16_t*)pbf, stats, D);
+                     (bf16_t*)pbf, stats, (float*)nullptr, D);
   return (int)hipGetLastError();
+}
+
+// Cached launch state of one model's fused step (ops/nn.py MlpStep): every pointer, the LDS plan and
+// the hyper-parameters are fixed at creation; a step passes only the batch and the stream, and the
+// step counter lives on the device (tstep), so the per-step host cost is one short call.
+struct MlpCtx {
+  ptgm::MlpDesc D;
+  long bytes;
+  float *p, *m, *v, *stats, *tstep;
+  bf16_t* pbf;
+};
+
+int ptg_mlp_ctx_create(float* p, float* m, float* v, void* pbf, float* stats, float* tstep, const long* hdesc, int L,
+                       int B, int loss, float lr, float b1, float b2, float eps, void** out) {
+  MlpCtx* c = new MlpCtx();
+  c->bytes = mlp_plan(hdesc, L, B, &c->D);
+  if (c->bytes <= 0 || c->bytes > 160 * 1024 || (loss != 0 && loss != 1) || !tstep) {
+    delete c;
+    return (int)hipErrorInvalidValue;
+  }
+  c->D.loss = loss; c->D.steps = 1;
+  c->D.lr = lr; c->D.b1 = b1; c->D.b2 = b2; c->D.eps = eps; c->D.t0 = 0;
+  c->p = p; c->m = m; c->v = v; c->pbf = (bf16_t*)pbf; c->stats = stats; c->tstep = tstep;
+  (void)hipFuncSetAttribute((const void*)ptgm::mlp_train_k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  *out = c;
+  return 0;
+}
+
+int ptg_mlp_ctx_run(void* ctx, const void* x, const void* y, int steps, hipStream_t s) {
+  MlpCtx* c = (MlpCtx*)ctx;
+  if (!c || steps < 1) return (int)hipErrorInvalidValue;
+  ptgm::MlpDesc D = c->D;
+  D.steps = steps;
+  hipLaunchKernelGGL(ptgm::mlp_train_k, dim3(1), dim3(ptgm::NT), (size_t)c->bytes, s, (const float*)x, y, c->p, c->m,
+                     c->v, c->pbf, c->stats, c->tstep, D);
+  return (int)hipGetLastError();
+}
+
+int ptg_mlp_ctx_free(void* ctx) {
+  delete (MlpCtx*)ctx;
+  return 0;
 }
 
 }  // extern "C"

@@ -610,8 +610,22 @@ class Sequential:
         if not getattr(store, "grad_clean", False):
             store.zero_grad()  # (the fused step writes no gradient; leave the buffer clean)
         y = yb.view(-1).contiguous() if kind == 0 else yb.contiguous()
-        K.mlp_train(xb.contiguous(), y, store.flat, opt.m, opt.v, store.flat_bf16, stats, dims, acts, woffs, boffs,
-                    steps, kind, opt.learning_rate, opt.beta_1, opt.beta_2, opt.epsilon, opt.iterations, desc=desc)
+        x = xb.contiguous()
+        if x.is_cuda and x.dtype == torch.float32 and y.dtype == (torch.int32 if kind == 0 else torch.float32):
+            B = x.shape[0] // steps
+            key = (id(plan), B, store.flat.data_ptr(), opt.m.data_ptr(), opt.v.data_ptr(), stats.data_ptr(),
+                   opt.learning_rate, opt.beta_1, opt.beta_2, opt.epsilon)
+            ms = self._mlp_steps.get(key) if hasattr(self, "_mlp_steps") else None
+            if ms is None:
+                if not hasattr(self, "_mlp_steps") or len(self._mlp_steps) > 8:
+                    self._mlp_steps = {}
+                ms = self._mlp_steps[key] = K.MlpStep(store.flat, opt.m, opt.v, store.flat_bf16, stats, dims, acts,
+                                                      woffs, boffs, B, kind, opt.learning_rate, opt.beta_1,
+                                                      opt.beta_2, opt.epsilon, opt.iterations, desc=desc)
+            ms.run(x, y, steps, opt.iterations)
+        else:
+            K.mlp_train(x, y, store.flat, opt.m, opt.v, store.flat_bf16, stats, dims, acts, woffs, boffs, steps, kind,
+                        opt.learning_rate, opt.beta_1, opt.beta_2, opt.epsilon, opt.iterations, desc=desc)
         opt.iterations += steps
         store.grad_clean = True
 

@@ -852,6 +852,49 @@ def mlp_train(x, y, flat, m, v, flat_bf16, stats, dims, acts, woffs, boffs, step
         stats.data_ptr(), ctypes.addressof(desc), L, B, steps, loss_kind, lr, b1, b2, eps, t0)
 
 
+class MlpStep:
+    """A cached launch of :func:`mlp_train` for one model, batch size and optimizer state (mlp.hip
+    ``ptg_mlp_ctx_*``): pointers, LDS plan and hyper-parameters are bound once, the Adam step counter
+    lives on the device, and a step is one short native call with the batch pointers."""
+
+    def __init__(self, flat, m, v, flat_bf16, stats, dims, acts, woffs, boffs, B: int, loss_kind: int, lr: float,
+                 b1: float, b2: float, eps: float, t0: int, desc=None):
+        import ctypes
+
+        from .. import _native
+
+        self.lib = _native.hip_lib()
+        L = len(dims) - 1
+        desc = desc if desc is not None else _mlp_desc(dims, acts, woffs, boffs)
+        pbf = flat_bf16 if flat_bf16 is not None and flat_bf16.data_ptr() != flat.data_ptr() else None
+        self.tstep = torch.full((1,), float(t0), dtype=torch.float32, device=flat.device)
+        h = ctypes.c_void_p()
+        _native.check(self.lib.ptg_mlp_ctx_create(flat.data_ptr(), m.data_ptr(), v.data_ptr(), ptr(pbf),
+                                                  stats.data_ptr(), self.tstep.data_ptr(), ctypes.addressof(desc), L,
+                                                  B, loss_kind, lr, b1, b2, eps, ctypes.byref(h)), "ptg_mlp_ctx_create")
+        self.h = h.value
+        self._keep = (flat, m, v, pbf, stats, desc)
+        self.t = int(t0)
+        self.B, self.in_dim, self.kind = B, int(dims[0]), loss_kind
+
+    def run(self, x, y, steps: int, t0: int) -> None:
+        """``steps`` fused steps on x (steps*B rows, fp32) / y; ``t0`` = optimizer steps so far."""
+        if t0 != self.t:  # the host counter moved (set_iterations, a checkpoint): resync the device one
+            self.tstep.fill_(float(t0))
+        rc = self.lib.ptg_mlp_ctx_run(self.h, x.data_ptr(), y.data_ptr(), steps, torch.cuda.current_stream().cuda_stream)
+        if rc:
+            raise RuntimeError(f"native kernel ptg_mlp_ctx_run failed: hipError_t={rc}")
+        self.t = t0 + steps
+
+    def __del__(self):
+        h, self.h = getattr(self, "h", None), None
+        if h:
+            try:
+                self.lib.ptg_mlp_ctx_free(h)
+            except Exception:  # noqa: BLE001 - interpreter shutdown
+                pass
+
+
 def adam_step(state, lr: float, b1: float, b2: float):
     """state[0] += 1; state[1] = bias-corrected step size (on the device)."""
     if not on_device(state):
