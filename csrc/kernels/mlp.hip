@@ -10,14 +10,14 @@
 //   * every layer's activation for the batch (kept for the backward) and two ping-pong gradient
 //     buffers.
 // Per step: forward, fused softmax + cross-entropy (or MSE) producing dlogits, then per layer from
-// the top ONE phase that computes dX for the layer below (with the ReLU mask) from the pre-update
-// LDS weights AND each parameter's gradient followed immediately by its Adam update straight into
-// the flat master / m / v / bf16 copy in HBM and into the second LDS weight copy (no gradient
-// buffer is written; the copies swap roles every step).  Every matrix product is a register-tiled
-// LDS GEMM (tile_gemm: up to 4 x 4 outputs per thread).  ``steps`` > 1 runs consecutive batches of a device-resident dataset in the same
-// launch (Keras' steps_per_execution): each step is still a full forward / backward / Adam step.
-// Metric sums are kept in registers and added to `stats` once (the layouts of softmax_xent_k /
-// mse_k).
+// the top: dX for the layer below (with the ReLU mask) from the pre-update LDS weights, a barrier,
+// then each parameter's gradient followed immediately by its Adam update straight into the flat
+// master / m / v / bf16 copy in HBM and into the LDS weights in place (no gradient buffer is
+// written).  Every matrix product is a register-tiled LDS GEMM (tile_gemm: up to 4 x 4 outputs per
+// thread, so a few LDS reads feed many independent FMA chains).  ``steps`` > 1 runs consecutive
+// batches of a device-resident dataset in the same launch (Keras' steps_per_execution): each step
+// is still a full forward / backward / Adam step.  Metric sums are kept in registers and added to
+// `stats` once (the layouts of softmax_xent_k / mse_k).
 #include "common.h"
 
 namespace ptgm {
@@ -30,8 +30,7 @@ struct MlpDesc {
   int d[MAXL + 1];              // d[0] input features, d[l + 1] units of layer l
   int act[MAXL];                // hidden activation of layer l: 0 linear, 1 relu (last: from loss)
   long woff[MAXL], boff[MAXL];  // element offsets of W_l ([d[l+1]][d[l]]) and b_l in the flat store
-  int lw[MAXL], lb[MAXL];       // LDS float offsets of W_l (row stride ws[l]) and b_l, copy 0
-  int wtot;                     // floats of one weight copy (copy 1 starts there)
+  int lw[MAXL], lb[MAXL];       // LDS float offsets of W_l (row stride ws[l]) and b_l
   int ws[MAXL];                 // LDS row stride of W_l (odd)
   int la[MAXL + 1], as[MAXL + 1];  // LDS offset / row stride (odd) of activation l
   int lg0, lg1, gs;             // the two gradient buffers (row stride gs, odd) and red scratch
@@ -114,20 +113,16 @@ __global__ __launch_bounds__(NT) void mlp_train_k(const float* __restrict__ x, c
   const int tid = threadIdx.x;
   const int L = D.L, B = D.B;
   const int t0 = tstep ? (int)tstep[0] : D.t0;
-  // weights + biases -> LDS (copy 0; the Adam epilogues write the updated values into the other copy)
+  // weights + biases -> LDS (the Adam epilogues keep them current in place)
   for (int l = 0; l < L; ++l) {
     const int K = D.d[l], N = D.d[l + 1], S = D.ws[l];
     for (int i = tid; i < N * K; i += NT) sm[D.lw[l] + (i / K) * S + i % K] = p[D.woff[l] + i];
-    for (int n = tid; n < N; n += NT) {
-      sm[D.lb[l] + n] = D.boff[l] >= 0 ? p[D.boff[l] + n] : 0.f;
-      if (D.boff[l] < 0) sm[D.wtot + D.lb[l] + n] = 0.f;  // a bias-less layer's zeros in both copies
-    }
+    for (int n = tid; n < N; n += NT) sm[D.lb[l] + n] = D.boff[l] >= 0 ? p[D.boff[l] + n] : 0.f;
   }
   float s_loss = 0.f, s_a = 0.f, s_b = 0.f;
   const int C = D.d[L];
-  int wcur = 0;  // float offset of the current weight copy
+  const int wcur = 0;
   for (int st = 0; st < D.steps; ++st) {
-    const int wnxt = D.wtot - wcur;
     // ---- input batch
     const int K0 = D.d[0];
     const float* xs = x + (long)st * B * K0;
@@ -180,8 +175,8 @@ __global__ __launch_bounds__(NT) void mlp_train_k(const float* __restrict__ x, c
       }
     }
     __syncthreads();
-    // ---- backward: per layer one phase (dX below from the current weights + each gradient's Adam
-    // update into HBM and into the next weight copy), one barrier
+    // ---- backward, per layer: dX for the layer below from the pre-update LDS weights, a barrier,
+    // then each weight gradient with its Adam update into HBM and into the LDS weights in place
     const float t = (float)(t0 + st + 1);
     const float lr_t = D.lr * sqrtf(1.f - powf(D.b2, t)) / (1.f - powf(D.b1, t));
     const float b1 = D.b1, b2 = D.b2, eps = D.eps;
@@ -199,9 +194,10 @@ __global__ __launch_bounds__(NT) void mlp_train_k(const float* __restrict__ x, c
           if (mask && !(A[r * SA + k] > 0.f)) s = 0.f;
           Gn[r * gs + k] = s;
         });
+        __syncthreads();  // every dX read of W_l before the in-place update below
       }
       // dW[n][k] = sum_r G[r][n] A[r][k], Adam straight from the register
-      float* Wn = sm + wnxt + D.lw[l];
+      float* Wn = sm + D.lw[l];
       const long wo = D.woff[l];
       gemm(N, K, B, Gc, 1, D.gs, A, 1, SA, [&](int n, int k, float g) {
         const long idx = wo + (long)n * K + k;
@@ -215,7 +211,7 @@ __global__ __launch_bounds__(NT) void mlp_train_k(const float* __restrict__ x, c
         Wn[n * S + k] = pp;
       });
       if (D.boff[l] >= 0) {
-        float* bn = sm + wnxt + D.lb[l];
+        float* bn = sm + D.lb[l];
         for (int n = tid; n < N; n += NT) {
           float g = 0.f;
           for (int r = 0; r < B; ++r) g += Gc[r * D.gs + n];
@@ -233,7 +229,6 @@ __global__ __launch_bounds__(NT) void mlp_train_k(const float* __restrict__ x, c
       __syncthreads();
       const int tmp = cur; cur = nxt; nxt = tmp;
     }
-    wcur = wnxt;  // (the next step's input barrier orders the new copy before any forward read)
   }
   float* red = sm + D.lred;
   const float tl = sum_block(s_loss, red);
@@ -280,8 +275,6 @@ static long mlp_plan(const long* hdesc, int L, int B, ptgm::MlpDesc* D) {
     D->lw[l] = off; off += D->d[l + 1] * D->ws[l];
     D->lb[l] = off; off += D->d[l + 1];
   }
-  D->wtot = off;
-  off *= 2;  // two weight copies: a step reads one while its Adam epilogues write the other
   for (int l = 0; l <= L; ++l) {
     D->as[l] = odd(D->d[l]);
     D->la[l] = off; off += B * D->as[l];
