@@ -38,7 +38,7 @@ class Strategy:
         if device is not None:
             self.device = torch.device(device)
         elif torch.cuda.is_available():
-            self.device = torch.device("cuda", local % max(torch.cuda.device_count(), 1))
+            self.device = torch.device("cuda", comm.device_index())
             torch.cuda.set_device(self.device)
         else:
             self.device = torch.device("cpu")

@@ -26,6 +26,12 @@ def env_rank() -> tuple[int, int, int]:
     return rank, local, world
 
 
+def device_index() -> int:
+    """This rank's GPU: LOCAL_RANK, or the launcher's PTG_DEVICE_ORDINAL after an executor was lost."""
+    rank, local, _ = env_rank()
+    return int(os.environ.get("PTG_DEVICE_ORDINAL", local)) % max(torch.cuda.device_count(), 1)
+
+
 def is_initialized() -> bool:
     return dist.is_available() and dist.is_initialized()
 
@@ -52,7 +58,7 @@ def init(backend: str | None = None, device_type: str | None = None, timeout_s: 
     os.environ.setdefault("MASTER_PORT", "29500")
     kw = {}
     if device_type == "cuda":
-        dev = local % max(torch.cuda.device_count(), 1)
+        dev = device_index()
         torch.cuda.set_device(dev)
         if backend == "nccl":
             kw["device_id"] = torch.device("cuda", dev)

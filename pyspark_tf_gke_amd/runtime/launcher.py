@@ -10,6 +10,11 @@ Failure detection / elastic recovery:
     treated as hung (before its first step the limit is ``startup_timeout``);
   * ``max_restarts`` relaunches the whole group (applications resume from their checkpoint, e.g.
     ``train --checkpoint-every 1 --resume``);
+  * ``min_nprocs`` (executor loss, Spark standalone's lost-executor handling): instead of relaunching
+    the failed rank, the group restarts WITHOUT it on the remaining devices (``PTG_DEVICE_ORDINAL``
+    keeps every survivor on its own GPU).  Sources are split by (rank, world) at read time, so the
+    lost executor's partitions are re-assigned to the survivors and recomputed from their lineage
+    (the source read + the narrow / wide stages after it) - down to ``min_nprocs`` executors;
   * fault injection for tests: ``PTG_FAULT_RANK`` / ``PTG_FAULT_STEP`` (:mod:`.fault`).
 """
 from __future__ import annotations
@@ -50,13 +55,15 @@ def _die_with_parent():
         pass
 
 
-def _spawn(cmd, nprocs, master_addr, master_port, env_extra, hb_dir, prefix):
+def _spawn(cmd, nprocs, master_addr, master_port, env_extra, hb_dir, prefix, devices=None):
     procs, pumps = [], []
     for r in range(nprocs):
         env = dict(os.environ)
         env.update(env_extra or {})
         env.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(nprocs), "LOCAL_WORLD_SIZE": str(nprocs),
                     "MASTER_ADDR": master_addr, "MASTER_PORT": str(master_port), "PTG_HEARTBEAT_DIR": hb_dir})
+        if devices is not None:
+            env["PTG_DEVICE_ORDINAL"] = str(devices[r])
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         if prefix:
             p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, start_new_session=True,
@@ -91,15 +98,22 @@ def _terminate(procs, grace: float = 10.0):
 
 def launch(cmd: list, nprocs: int, master_addr: str = "127.0.0.1", master_port: int | None = None,
            env_extra: dict | None = None, max_restarts: int = 0, hang_timeout: float = 0.0, prefix_output: bool = True,
-           poll: float = 0.2, startup_timeout: float | None = None) -> int:
-    """Run ``cmd`` on ``nprocs`` ranks; return 0 or the first failing rank's exit code."""
+           poll: float = 0.2, startup_timeout: float | None = None, min_nprocs: int = 0) -> int:
+    """Run ``cmd`` on ``nprocs`` ranks; return 0 or the first failing rank's exit code.
+    ``min_nprocs`` > 0: a failed rank's executor is dropped and the group restarts on the survivors
+    (while at least ``min_nprocs`` remain) instead of relaunching it."""
     attempt = 0
+    devices = list(range(nprocs))
+    lost: list = []
     while True:
         port = master_port or free_port(master_addr)
         hb_dir = tempfile.mkdtemp(prefix="ptg_hb_")
         env = dict(env_extra or {})
         env["PTG_RESTART_COUNT"] = str(attempt)
-        procs, pumps = _spawn(cmd, nprocs, master_addr, port, env, hb_dir, prefix_output)
+        if lost:
+            env["PTG_LOST_EXECUTORS"] = ",".join(str(d) for d in lost)
+        procs, pumps = _spawn(cmd, nprocs, master_addr, port, env, hb_dir, prefix_output,
+                              devices if min_nprocs > 0 else None)
         rc, failed = 0, None
         try:
             while True:
@@ -130,6 +144,12 @@ def launch(cmd: list, nprocs: int, master_addr: str = "127.0.0.1", master_port: 
         if rc == 0 or attempt >= max_restarts:
             return rc
         attempt += 1
+        if min_nprocs > 0 and failed is not None and nprocs - 1 >= min_nprocs:
+            lost.append(devices.pop(failed))
+            nprocs -= 1
+            sys.stderr.write(f"[launcher] executor {lost[-1]} lost: its partitions are re-planned onto the {nprocs} "
+                             f"remaining executors (attempt {attempt}/{max_restarts})\n")
+            continue
         sys.stderr.write(f"[launcher] restarting all ranks (attempt {attempt}/{max_restarts})\n")
 
 
@@ -143,6 +163,8 @@ def main(argv=None) -> int:
     ap.add_argument("--max-restarts", type=int, default=0)
     ap.add_argument("--hang-timeout", type=float, default=0.0)
     ap.add_argument("--startup-timeout", type=float, default=None)
+    ap.add_argument("--min-nproc", type=int, default=0,
+                    help="on a rank failure drop its executor and restart on the survivors (down to this many)")
     ap.add_argument("cmd", nargs=argparse.REMAINDER)
     a = ap.parse_args(argv)
     cmd = a.cmd[1:] if a.cmd and a.cmd[0] == "--" else a.cmd
@@ -150,7 +172,7 @@ def main(argv=None) -> int:
         ap.error("missing command")
     n = a.nproc or _gpu_count() or 1
     return launch(cmd, n, a.master_addr, a.master_port or None, max_restarts=a.max_restarts,
-                  hang_timeout=a.hang_timeout, startup_timeout=a.startup_timeout)
+                  hang_timeout=a.hang_timeout, startup_timeout=a.startup_timeout, min_nprocs=a.min_nproc)
 
 
 def _gpu_count() -> int:

@@ -151,7 +151,7 @@ class SparkSession:
             if want:
                 self.device = torch.device(want)
             elif torch.cuda.is_available():
-                self.device = torch.device("cuda", local % max(1, torch.cuda.device_count()))
+                self.device = torch.device("cuda", comm.device_index())
                 torch.cuda.set_device(self.device)
             else:
                 self.device = torch.device("cpu")
