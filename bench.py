@@ -47,6 +47,9 @@ def parse(argv=None):
                          "report it under extra.groupby (1B rows per GPU)")
     ap.add_argument("--extra-batches", default=os.environ.get("PTG_BENCH_EXTRA_BATCHES", "32,64"),
                     help="cnn_b1: also time these per-GPU batches (the reference's 32 and 64) into extra")
+    ap.add_argument("--mlp-batches", default=os.environ.get("PTG_BENCH_MLP_BATCHES", "32,64"),
+                    help="cnn_b1: also time the reference's CSV-MLP step (train_tf_ps.py build_deep_model) at these "
+                         "batches into extra.mlp_b<B> (the fused one-launch step)")
     ap.add_argument("--sim-world", type=int, default=int(os.environ.get("PTG_BENCH_SIM_WORLD", "8")),
                     help="cnn_b1 on 1 GPU: also time rank 0's kernel sequence of an N-rank sharded data-parallel "
                          "step (PTG_SIM_WORLD: collectives replaced by local kernels of the same HBM bytes) into "
@@ -262,6 +265,14 @@ def main():
                 r2 = bench_train(a2, strategy, rank, world)
                 extra[f"batch{b}"] = {"value": r2["value"], "unit": "samples/s", "ms_per_step": r2["ms_per_step"],
                                       "per_gpu_batch": b, "global_batch": b * world}
+        if args.workload == "cnn_b1" and args.mlp_batches:
+            for b in [int(x) for x in args.mlp_batches.split(",") if x.strip()]:
+                a2 = argparse.Namespace(**{**vars(args), "batch_size": b, "workload": "mlp", "steps": 200,
+                                           "warmup": 20})
+                r2 = bench_train(a2, strategy, rank, world)
+                extra[f"mlp_b{b}"] = {"value": r2["value"], "unit": "samples/s", "ms_per_step": r2["ms_per_step"],
+                                      "per_gpu_batch": b, "global_batch": b * world,
+                                      "model": "CSV-MLP 3->16->32->64->15 (train_tf_ps.py:328-343), Adam, fp32"}
         if args.workload == "cnn_b1" and args.sim_world > 1 and world == 1 and torch.cuda.is_available():
             # the N>1 compute path on one GPU: dW into flat_grad, per-bucket reduce-scatter stand-in,
             # shard Adam, all-gather stand-in + bf16 re-cast (MultiWorkerMirroredStrategy sim mode)
