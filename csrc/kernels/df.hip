@@ -903,15 +903,15 @@ __global__ __launch_bounds__(256) void range_count_k(const long long* __restrict
   }
 }
 
-template <int NV, int RTT, int NT = 512>
+template <int NV, int RTT, int NT = 512, class OK = unsigned short>
 __global__ __launch_bounds__(NT) void range_scatter_k(const long long* __restrict__ keys, PayIn pin, long n,
                                                        long long lo, int sh, int ntiles,
                                                        const long long* __restrict__ offs,
-                                                       unsigned short* __restrict__ okeys, PayOut pout) {
+                                                       OK* __restrict__ okeys, PayOut pout) {
   constexpr int RPT = RTT / NT;
   static_assert(RPT >= 1 && RTT % NT == 0, "tile rows must be a multiple of the thread count");
   constexpr int NVS = NV > 0 ? NV : 1;
-  __shared__ unsigned short sk[RTT];
+  __shared__ OK sk[RTT];
   __shared__ double sv[NVS][RTT];
   __shared__ unsigned char sd[RTT];
   __shared__ unsigned int cnt[RGB];
@@ -960,7 +960,7 @@ __global__ __launch_bounds__(NT) void range_scatter_k(const long long* __restric
   for (int j = 0; j < RPT; ++j) {
     if (d[j] < 0) continue;
     const unsigned pos = lstart[d[j]] + atomicAdd(&cnt[d[j]], 1u);
-    sk[pos] = (unsigned short)((unsigned long long)(k[j] - lo) & ((1u << sh) - 1u));
+    sk[pos] = (OK)((unsigned long long)(k[j] - lo) & ((1ull << sh) - 1ull));
 #pragma unroll
     for (int q = 0; q < NV; ++q) sv[q][pos] = v[q][j];
     sd[pos] = (unsigned char)d[j];
@@ -981,14 +981,16 @@ __global__ __launch_bounds__(NT) void range_scatter_k(const long long* __restric
 // prow[c][0][Rw] rows, prow[c][1+j][Rw] non-null count of column j, psum[c][j][Rw] sums and, with
 // MINMAX, pmm[c][2j][Rw] / pmm[c][2j+1][Rw] min / max (+-inf where a key has no non-null value).
 // LDS: W * (4 + NV * (12 + (MINMAX ? 16 : 0))) bytes (ops/df.py picks W to fit).
-template <int NV, bool MINMAX>
-__global__ __launch_bounds__(256) void range_agg_k(const unsigned short* __restrict__ okeys, AggPay pay,
-                                                   const long long* __restrict__ offs, int ntiles, int sh,
-                                                   unsigned int* __restrict__ prow, double* __restrict__ psum,
-                                                   double* __restrict__ pmm) {
+// One (partition, chunk) of a direct-indexed LDS aggregation: rows [a0, b0) of okeys (window
+// indices < W = 2^sh) / pay, split C ways; the partition's dense partial table starts at column o of
+// prow[c][1+NV][Rw] / psum[c][NV][Rw] (/ pmm[c][2NV][Rw] with MINMAX).
+template <int NV, bool MINMAX, class OK>
+PTG_DEV void range_agg_part(const OK* __restrict__ okeys, const AggPay& pay, long long a0, long long b0, int c, int C,
+                            int sh, long Rw, long o, unsigned int* __restrict__ prow, double* __restrict__ psum,
+                            double* __restrict__ pmm) {
   constexpr int NVS = NV > 0 ? NV : 1;
   extern __shared__ __align__(16) unsigned char lds_raw[];
-  const int W = 1 << sh, p = blockIdx.y, c = blockIdx.x, C = gridDim.x;
+  const int W = 1 << sh;
   double* lsum = (double*)lds_raw;                                    // [NV][W]
   double* lmm = lsum + (long)NV * W;                                  // [NV][2][W] (MINMAX)
   unsigned int* lrow = (unsigned int*)(lmm + (MINMAX ? 2L * NV * W : 0L)); // [1 + NV][W]
@@ -1002,7 +1004,7 @@ __global__ __launch_bounds__(256) void range_agg_k(const unsigned short* __restr
     }
   }
   __syncthreads();
-  const long long a0 = offs[p], b0 = p + 1 < RGB ? offs[p + 1] : offs[(long)RGB * ntiles], len = b0 - a0;
+  const long long len = b0 - a0;
   const long long a = a0 + len * c / C, b = a0 + len * (c + 1) / C;
   auto add = [&](unsigned int i, const double* v) {  // i: index inside the window
     atomicAdd(&lrow[i], 1u);
@@ -1037,7 +1039,6 @@ __global__ __launch_bounds__(256) void range_agg_k(const unsigned short* __restr
     add(okeys[i], v1);
   }
   __syncthreads();
-  const long Rw = (long)RGB * W, o = (long)p * W;
   for (int t = threadIdx.x; t < W; t += 256) {
     prow[((long)c * (1 + NV)) * Rw + o + t] = lrow[t];
 #pragma unroll
@@ -1050,6 +1051,145 @@ __global__ __launch_bounds__(256) void range_agg_k(const unsigned short* __restr
       }
     }
   }
+}
+
+// grid (chunks, 256): partition p = blockIdx.y holds rows [offs[p], offs[p+1]) (tile 0's row of the
+// tile-major offsets; offs[256*ntiles] = n closes the last partition), keys
+// lo + p*W + okeys[i] (u16 window indices).  Output per chunk c (Rw = 256*W entries):
+// prow[c][0][Rw] rows, prow[c][1+j][Rw] non-null count of column j, psum[c][j][Rw] sums and, with
+// MINMAX, pmm[c][2j][Rw] / pmm[c][2j+1][Rw] min / max (+-inf where a key has no non-null value).
+// LDS: W * (4 + NV * (12 + (MINMAX ? 16 : 0))) bytes (ops/df.py picks W to fit).
+template <int NV, bool MINMAX>
+__global__ __launch_bounds__(256) void range_agg_k(const unsigned short* __restrict__ okeys, AggPay pay,
+                                                   const long long* __restrict__ offs, int ntiles, int sh,
+                                                   unsigned int* __restrict__ prow, double* __restrict__ psum,
+                                                   double* __restrict__ pmm) {
+  const int p = blockIdx.y;
+  const long long a0 = offs[p], b0 = p + 1 < RGB ? offs[p + 1] : offs[(long)RGB * ntiles];
+  range_agg_part<NV, MINMAX>(okeys, pay, a0, b0, (int)blockIdx.x, (int)gridDim.x, sh, (long)RGB << sh,
+                             (long)p << sh, prow, psum, pmm);
+}
+
+// ---- dense key spans up to 2^28 (ids, dates x ids, ...): two 256-way range levels -----------------
+// Level 1 (range_count_k + range_scatter_k<.., u32>): 256 coarse partitions of 2^(sh2+8) keys, keys
+// leave as u32 offsets inside their coarse window.  Level 2 (range2_count_k / range2_scatter_k):
+// every coarse partition is tiled on its own (ptg_seg_plan with 256 bins: histograms digit-major
+// per segment, so ONE exclusive scan of all of them gives every (coarse, fine, tile) run its output
+// position) and split 256 ways by off >> sh2; keys leave as u16 offsets inside 2^sh2-key fine windows.
+// range2_agg_k: one workgroup (x chunks) per fine partition, the same direct-indexed LDS table as
+// range_agg_k.  ~70 B of traffic per row, against ~100 for three hash radix levels + LDS hash tables.
+template <int RTT>
+__global__ __launch_bounds__(256) void range2_count_k(const unsigned int* __restrict__ okeys,
+                                                      const long long* __restrict__ tstart,
+                                                      const int* __restrict__ trows,
+                                                      const long long* __restrict__ thbase,
+                                                      const long long* __restrict__ thstride, int sh2,
+                                                      unsigned int* __restrict__ hist) {
+  constexpr int RPT = RTT / 256;
+  __shared__ unsigned int h[4][RGB];
+  const int tid = threadIdx.x, b = blockIdx.x, w = tid >> 6;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) h[q][tid] = 0;
+  const long long s0 = tstart[b];
+  const int nr = trows[b];
+  unsigned int k[RPT];
+#pragma unroll
+  for (int j = 0; j < RPT; ++j) {
+    const int i = tid + j * 256;
+    k[j] = i < nr ? okeys[s0 + i] : 0u;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < RPT; ++j)
+    if (tid + j * 256 < nr) atomicAdd(&h[w][(k[j] >> sh2) & (RGB - 1)], 1u);
+  __syncthreads();
+  hist[thbase[b] + (long long)tid * thstride[b]] = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
+}
+
+template <int NV, int RTT, int NT = 512>
+__global__ __launch_bounds__(NT) void range2_scatter_k(const unsigned int* __restrict__ keys, AggPay pin,
+                                                       const long long* __restrict__ tstart,
+                                                       const int* __restrict__ trows,
+                                                       const long long* __restrict__ thbase,
+                                                       const long long* __restrict__ thstride, int sh2,
+                                                       const long long* __restrict__ offs, long n,
+                                                       unsigned short* __restrict__ okeys, PayOut pout) {
+  constexpr int RPT = RTT / NT;
+  static_assert(RPT >= 1 && RTT % NT == 0, "tile rows must be a multiple of the thread count");
+  constexpr int NVS = NV > 0 ? NV : 1;
+  __shared__ unsigned short sk[RTT];
+  __shared__ double sv[NVS][RTT];
+  __shared__ unsigned char sd[RTT];
+  __shared__ unsigned int cnt[RGB];
+  __shared__ unsigned int lstart[RGB];
+  __shared__ long long goff[RGB];
+  const int tid = threadIdx.x, b = xcd_tile(blockIdx.x, gridDim.x);
+  const long long s0 = tstart[b];
+  const int nr = trows[b];
+  for (int d = tid; d < RGB; d += NT) {
+    cnt[d] = 0;
+    goff[d] = offs[thbase[b] + (long long)d * thstride[b]];
+  }
+  __syncthreads();
+  unsigned int k[RPT];
+  double v[NVS][RPT];
+  int d[RPT];
+#pragma unroll
+  for (int j = 0; j < RPT; ++j) {
+    const int i = tid + j * NT;
+    d[j] = -1;
+    if (i < nr) {
+      k[j] = keys[s0 + i];
+#pragma unroll
+      for (int q = 0; q < NV; ++q) v[q][j] = pin.vals[q][s0 + i];
+      d[j] = (int)((k[j] >> sh2) & (RGB - 1));
+      atomicAdd(&cnt[d[j]], 1u);
+    }
+  }
+  __syncthreads();
+  if (tid < 64) {  // exclusive scan of the 256 digit counts in one wave, 4 per lane
+    unsigned c4[4], sum = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) { c4[q] = cnt[4 * tid + q]; sum += c4[q]; }
+    unsigned incl = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned t = __shfl_up(incl, o, 64);
+      if (tid >= o) incl += t;
+    }
+    unsigned run = incl - sum;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) { lstart[4 * tid + q] = run; run += c4[q]; cnt[4 * tid + q] = 0; }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < RPT; ++j) {
+    if (d[j] < 0) continue;
+    const unsigned pos = lstart[d[j]] + atomicAdd(&cnt[d[j]], 1u);
+    sk[pos] = (unsigned short)(k[j] & ((1u << sh2) - 1u));
+#pragma unroll
+    for (int q = 0; q < NV; ++q) sv[q][pos] = v[q][j];
+    sd[pos] = (unsigned char)d[j];
+  }
+  __syncthreads();
+  for (int i = tid; i < nr; i += NT) {
+    const int dd = sd[i];
+    const long long dst = PTG_CHECKED_IDX(goff[dd] + (i - (int)lstart[dd]), n);
+    okeys[dst] = sk[i];
+#pragma unroll
+    for (int q = 0; q < NV; ++q) pout.vals[q][dst] = sv[q][i];
+  }
+}
+
+// one workgroup per (fine partition p, chunk c): blockIdx.x = p * C + c; fine partition p holds rows
+// [fstart[p], fend[p]) and keys lo + (p << sh2) + okeys[i]
+template <int NV>
+__global__ __launch_bounds__(256) void range2_agg_k(const unsigned short* __restrict__ okeys, AggPay pay,
+                                                    const long long* __restrict__ fstart,
+                                                    const long long* __restrict__ fend, int C, int sh2, long Rw,
+                                                    unsigned int* __restrict__ prow, double* __restrict__ psum) {
+  const int p = blockIdx.x / C, c = blockIdx.x - p * C;
+  range_agg_part<NV, false>(okeys, pay, fstart[p], fend[p], c, C, sh2, Rw, (long)p << sh2, prow, psum, nullptr);
 }
 
 // ---- tiny key ranges (max - min < ~4K): no partitioning at all ---------------------------------
@@ -2021,6 +2161,86 @@ int ptg_range_scatter(const void* keys, const void* pin_p, int nv, long n, long 
     default: return (int)hipErrorInvalidValue;
   }
 #undef PTG_RSC
+  PTG_RETURN_LAUNCH();
+}
+// coarse level of the two-level dense range groupBy: keys leave as u32 offsets inside 2^sh windows
+int ptg_range_scatter32(const void* keys, const void* pin_p, int nv, long n, long lo, int sh, int ntiles,
+                        const void* offs, void* okeys, const void* pout_p, hipStream_t s) {
+  if (ntiles <= 0 || sh < 0 || sh > 24) return (int)hipErrorInvalidValue;
+  PayIn pin;
+  PayOut pout;
+  memcpy(&pin, pin_p, sizeof(PayIn));
+  memcpy(&pout, pout_p, sizeof(PayOut));
+#define PTG_RSC(NV, TR)                                                                                       \
+  hipLaunchKernelGGL((range_scatter_k<NV, TR, 512, unsigned int>), dim3(ntiles), dim3(512), 0, s,             \
+                     (const long long*)keys, pin, n, (long long)lo, sh, ntiles, (const long long*)offs,       \
+                     (unsigned int*)okeys, pout)
+  switch (nv) {
+    case 0: PTG_RSC(0, RGT); break;
+    case 1: PTG_RSC(1, RGT); break;
+    case 2: PTG_RSC(2, RGT / 2); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+#undef PTG_RSC
+  PTG_RETURN_LAUNCH();
+}
+// fine level: tiles from ptg_seg_plan(.., 256 bins) over the coarse partitions; T = ptg_range_tile_rows(nv)
+int ptg_range2_count(const void* okeys, const void* tstart, const void* trows, const void* thbase,
+                     const void* thstride, int ntiles, int nv, int sh2, void* hist, hipStream_t s) {
+  if (ntiles <= 0) return 0;
+  if (sh2 < 0 || sh2 > 12) return (int)hipErrorInvalidValue;
+#define PTG_R2C(TR)                                                                                            \
+  hipLaunchKernelGGL(range2_count_k<TR>, dim3(ntiles), dim3(256), 0, s, (const unsigned int*)okeys,            \
+                     (const long long*)tstart, (const int*)trows, (const long long*)thbase,                    \
+                     (const long long*)thstride, sh2, (unsigned int*)hist)
+  if (nv <= 1) PTG_R2C(RGT); else PTG_R2C(RGT / 2);
+#undef PTG_R2C
+  PTG_RETURN_LAUNCH();
+}
+int ptg_range2_scatter(const void* okeys32, const void* const* vals, int nv, const void* tstart, const void* trows,
+                       const void* thbase, const void* thstride, int ntiles, int sh2, const void* offs, long n,
+                       void* okeys16, const void* pout_p, hipStream_t s) {
+  if (ntiles <= 0) return 0;
+  if (sh2 < 0 || sh2 > 12 || nv < 0 || nv > 2) return (int)hipErrorInvalidValue;
+  AggPay pin;
+  for (int j = 0; j < PAY_MAX; ++j) pin.vals[j] = j < nv ? (const double*)vals[j] : nullptr;
+  PayOut pout;
+  memcpy(&pout, pout_p, sizeof(PayOut));
+#define PTG_R2S(NV, TR)                                                                                        \
+  hipLaunchKernelGGL((range2_scatter_k<NV, TR>), dim3(ntiles), dim3(512), 0, s, (const unsigned int*)okeys32,  \
+                     pin, (const long long*)tstart, (const int*)trows, (const long long*)thbase,               \
+                     (const long long*)thstride, sh2, (const long long*)offs, n, (unsigned short*)okeys16, pout)
+  switch (nv) {
+    case 0: PTG_R2S(0, RGT); break;
+    case 1: PTG_R2S(1, RGT); break;
+    default: PTG_R2S(2, RGT / 2); break;
+  }
+#undef PTG_R2S
+  PTG_RETURN_LAUNCH();
+}
+// nfine fine partitions x chunks workgroups; prow u32[chunks][1+nv][nfine<<sh2], psum f64[chunks][nv][nfine<<sh2]
+int ptg_range2_agg(const void* okeys16, const void* const* vals, int nv, const void* fstart, const void* fend,
+                   int nfine, int chunks, int sh2, void* prow, void* psum, hipStream_t s) {
+  if (nv < 0 || nv > 2 || sh2 < 0 || sh2 > 12 || chunks <= 0 || nfine <= 0) return (int)hipErrorInvalidValue;
+  const size_t lds = ((size_t)1 << sh2) * (4 + (size_t)nv * 12);
+  if (lds > 150 * 1024) return (int)hipErrorInvalidValue;
+  AggPay pay;
+  for (int j = 0; j < PAY_MAX; ++j) pay.vals[j] = j < nv ? (const double*)vals[j] : nullptr;
+  const long Rw = (long)nfine << sh2;
+#define PTG_R2A(NV)                                                                                            \
+  {                                                                                                            \
+    static bool attr = false;                                                                                  \
+    if (!attr) {                                                                                               \
+      (void)hipFuncSetAttribute((const void*)range2_agg_k<NV>, hipFuncAttributeMaxDynamicSharedMemorySize,     \
+                                150 * 1024);                                                                   \
+      attr = true;                                                                                             \
+    }                                                                                                          \
+    hipLaunchKernelGGL(range2_agg_k<NV>, dim3((unsigned)nfine * chunks), dim3(256), lds, s,                    \
+                       (const unsigned short*)okeys16, pay, (const long long*)fstart, (const long long*)fend,  \
+                       chunks, sh2, Rw, (unsigned int*)prow, (double*)psum);                                   \
+  }
+  switch (nv) { case 0: PTG_R2A(0) break; case 1: PTG_R2A(1) break; default: PTG_R2A(2) break; }
+#undef PTG_R2A
   PTG_RETURN_LAUNCH();
 }
 // vals: host array of nv f64 device pointers (scattered payload); prow u32[chunks][1+nv][256<<sh],

@@ -203,7 +203,8 @@ __global__ __launch_bounds__(256) void radix_tiles_k(const long long* __restrict
                                                      const long long* __restrict__ ntiles,
                                                      const long long* __restrict__ first, int nseg, long long total,
                                                      long long T, long long* __restrict__ tstart, int* __restrict__ trows,
-                                                     long long* __restrict__ thbase, long long* __restrict__ thstride) {
+                                                     long long* __restrict__ thbase, long long* __restrict__ thstride,
+                                                     int bins) {
   for (long long t = blockIdx.x * 256L + threadIdx.x; t < total; t += (long long)gridDim.x * 256) {
     int lo = 0, hi = nseg - 1;  // last segment with first[s] <= t (and at least one tile)
     while (lo < hi) {
@@ -216,25 +217,25 @@ __global__ __launch_bounds__(256) void radix_tiles_k(const long long* __restrict
     const long long st = seg_start[s] + tl * T;
     tstart[t] = st;
     trows[t] = (int)min(T, seg_start[s] + seg_len[s] - st);
-    thbase[t] = 64 * first[s] + tl;
+    thbase[t] = (long long)bins * first[s] + tl;
     thstride[t] = ntiles[s];
   }
 }
 
-// sub-segment (s, d) starts at offs[64 first[s] + d ntiles[s]]; ends where the next one starts
+// sub-segment (s, d) starts at offs[bins first[s] + d ntiles[s]]; ends where the next one starts
 __global__ __launch_bounds__(256) void radix_bounds_k(const long long* __restrict__ offs,
                                                       const long long* __restrict__ first,
                                                       const long long* __restrict__ ntiles, int nseg, long long n_out,
                                                       long long* __restrict__ new_start, long long* __restrict__ new_end,
-                                                      long long* __restrict__ new_len) {
-  const long total = (long)nseg * 64;
+                                                      long long* __restrict__ new_len, int bins) {
+  const long total = (long)nseg * bins;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    const int s = (int)(i >> 6), d = (int)(i & 63);
-    new_start[i] = offs[64 * first[s] + d * ntiles[s]];
+    const int s = (int)(i / bins), d = (int)(i - (long)s * bins);
+    new_start[i] = offs[(long long)bins * first[s] + d * ntiles[s]];
     long long e = n_out;
     if (i + 1 < total) {
-      const int s2 = (int)((i + 1) >> 6), d2 = (int)((i + 1) & 63);
-      e = offs[64 * first[s2] + d2 * ntiles[s2]];
+      const int s2 = (int)((i + 1) / bins), d2 = (int)((i + 1) - (long)s2 * bins);
+      e = offs[(long long)bins * first[s2] + d2 * ntiles[s2]];
     }
     new_end[i] = e;
     new_len[i] = e - new_start[i];
@@ -412,8 +413,9 @@ int ptg_dense_extract(const void* prow, const void* psum, const void* pmm, int C
 
 // radix level planning.  step 0: ntiles[s] = ceil(seg_len[s] / T); the caller then scans ntiles ->
 // first (+ total) and seg_len -> n_out.  step 1: per-tile arrays for `total` tiles.
-int ptg_radix_plan(const void* seg_start, const void* seg_len, int nseg, long T, void* ntiles, const void* first,
-                   long total, void* tstart, void* trows, void* thbase, void* thstride, int step, hipStream_t s) {
+static int seg_plan(const void* seg_start, const void* seg_len, int nseg, long T, void* ntiles, const void* first,
+                    long total, void* tstart, void* trows, void* thbase, void* thstride, int step, int bins,
+                    hipStream_t s) {
   if (step == 0) {
     if (nseg > 0)
       hipLaunchKernelGGL(radix_ntiles_k, dim3(grid_for(nseg)), dim3(256), 0, s, (const long long*)seg_len, nseg,
@@ -422,18 +424,36 @@ int ptg_radix_plan(const void* seg_start, const void* seg_len, int nseg, long T,
     hipLaunchKernelGGL(radix_tiles_k, dim3(grid_for(total)), dim3(256), 0, s, (const long long*)seg_start,
                        (const long long*)seg_len, (const long long*)ntiles, (const long long*)first, nseg,
                        (long long)total, (long long)T, (long long*)tstart, (int*)trows, (long long*)thbase,
-                       (long long*)thstride);
+                       (long long*)thstride, bins);
   }
   PTG_RETURN_LAUNCH();
 }
+int ptg_radix_plan(const void* seg_start, const void* seg_len, int nseg, long T, void* ntiles, const void* first,
+                   long total, void* tstart, void* trows, void* thbase, void* thstride, int step, hipStream_t s) {
+  return seg_plan(seg_start, seg_len, nseg, T, ntiles, first, total, tstart, trows, thbase, thstride, step, 64, s);
+}
+// the same tile plan for `bins`-way segmented passes (the 256-way level of the dense range groupBy)
+int ptg_seg_plan(const void* seg_start, const void* seg_len, int nseg, long T, void* ntiles, const void* first,
+                 long total, void* tstart, void* trows, void* thbase, void* thstride, int step, int bins,
+                 hipStream_t s) {
+  return seg_plan(seg_start, seg_len, nseg, T, ntiles, first, total, tstart, trows, thbase, thstride, step, bins, s);
+}
 
+static int seg_bounds(const void* offs, const void* first, const void* ntiles, int nseg, long n_out, void* new_start,
+                      void* new_end, void* new_len, int bins, hipStream_t s) {
+  if (nseg > 0)
+    hipLaunchKernelGGL(radix_bounds_k, dim3(grid_for((long)nseg * bins)), dim3(256), 0, s, (const long long*)offs,
+                       (const long long*)first, (const long long*)ntiles, nseg, (long long)n_out,
+                       (long long*)new_start, (long long*)new_end, (long long*)new_len, bins);
+  PTG_RETURN_LAUNCH();
+}
 int ptg_radix_bounds(const void* offs, const void* first, const void* ntiles, int nseg, long n_out, void* new_start,
                      void* new_end, void* new_len, hipStream_t s) {
-  if (nseg > 0)
-    hipLaunchKernelGGL(radix_bounds_k, dim3(grid_for((long)nseg * 64)), dim3(256), 0, s, (const long long*)offs,
-                       (const long long*)first, (const long long*)ntiles, nseg, (long long)n_out,
-                       (long long*)new_start, (long long*)new_end, (long long*)new_len);
-  PTG_RETURN_LAUNCH();
+  return seg_bounds(offs, first, ntiles, nseg, n_out, new_start, new_end, new_len, 64, s);
+}
+int ptg_seg_bounds(const void* offs, const void* first, const void* ntiles, int nseg, long n_out, void* new_start,
+                   void* new_end, void* new_len, int bins, hipStream_t s) {
+  return seg_bounds(offs, first, ntiles, nseg, n_out, new_start, new_end, new_len, bins, s);
 }
 
 int ptg_sum_clamp_i64(const void* x, long n, long cap, void* out, hipStream_t s) {

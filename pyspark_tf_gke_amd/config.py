@@ -44,6 +44,8 @@ _K = [
     # data engine
     Knob("groupby_range", bool, True, "PTG_GROUPBY_RANGE", "spark.ptg.groupby.range",
          "dense small-range integer keys take the one-pass range partition + direct LDS aggregation"),
+    Knob("groupby_range2", bool, True, "PTG_GROUPBY_RANGE2", "spark.ptg.groupby.range2",
+         "dense integer keys spanning 2^20..2^28 values: two 256-way range partitioning passes + direct LDS aggregation"),
     Knob("groupby_range_chunks", int, 8, "PTG_RANGE_CHUNKS", "spark.ptg.groupby.rangeChunks",
          "row chunks per range partition in the range aggregation (workgroups = 256 x chunks)"),
     Knob("groupby_hash9", bool, True, "PTG_GROUPBY_HASH9", "spark.ptg.groupby.hash9",

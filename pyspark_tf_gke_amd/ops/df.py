@@ -483,6 +483,87 @@ def hash_agg_range(keys: torch.Tensor, pay: list, buf, nv: int, sample_lohi: tup
     return _dense_extract(prow, psum, pmm if minmax else None, chunks, nv, Rw, lo, dev)
 
 
+RANGE2_MAX_SPAN = 1 << 28  # two 256-way range levels x 4096-key LDS windows
+
+
+def hash_agg_range2(keys: torch.Tensor, pay: list, buf, nv: int, sample_lohi: tuple[int, int]):
+    """groupBy(key).agg (sum / count / avg, nv <= 2, no min/max) for int64 keys spanning 2^20 .. 2^28
+    values (csrc/kernels/df.hip range2_*): a coarse 256-way range pass (u32 window offsets), a fine
+    256-way pass inside every coarse partition (u16 offsets) and a direct-indexed LDS aggregation per
+    fine partition - two partitioning passes and no hashing, where the hash path needs three radix
+    levels and LDS hash tables.  None when the keys do not fit (the caller falls back)."""
+    if nv > 2:
+        return None
+    dev = keys.device
+    n = keys.numel()
+    lib = _native.hip_lib()
+    sh2_max = min(12, _range_sh_max(nv, False))
+    win = _range_window(*sample_lohi, sh2_max + 8)
+    if win is None or win[1] < 8:
+        return None
+    T = int(lib.ptg_range_tile_rows(nv))
+    ntiles = (n + T - 1) // T
+    hist = buf("rhist", (256 * ntiles,), torch.int32)
+    rng = buf("rrng", (ntiles, 2), torch.int64)
+    for attempt in range(2):
+        lo, sh1 = win
+        hip("ptg_range_count", ptr(keys), n, int(lo), sh1, T, ntiles, ptr(hist), ptr(rng))
+        mn, mx = minmax_i64(rng, n=ntiles, stride=2, off_min=0, off_max=1)
+        if mn >= lo and mx < lo + (256 << sh1):
+            break
+        win = _range_window(mn, mx, sh2_max + 8) if attempt == 0 else None
+        if win is None or win[1] < 8:
+            return None
+    sh2 = sh1 - 8
+    offs = buf("roffs", (256 * ntiles + 1,), torch.int64)
+    digit_offsets(hist, ntiles, offs, buf)
+    ok32 = buf("r2ok32", (max(n, 1),), torch.int32)[:n]
+    ov1 = [buf(f"r2ov1_{j}", (max(n, 1),), torch.float64)[:n] for j in range(nv)]
+    pin, pout = _pay_in(pay), _pay_out(ov1)
+    hip("ptg_range_scatter32", ptr(keys), ctypes.addressof(pin), nv, n, int(lo), sh1, ntiles, ptr(offs), ptr(ok32),
+        ctypes.addressof(pout))
+    # coarse partition c = rows [offs[c], offs[c+1]) (tile 0's row of the tile-major offsets)
+    seg_start = offs[:256]
+    bounds = torch.cat([offs[:256], offs[256 * ntiles:256 * ntiles + 1]])
+    seg_len = bounds[1:] - bounds[:-1]
+    nts = buf("r2nts", (256,), torch.int64)
+    hip("ptg_seg_plan", ptr(seg_start), ptr(seg_len), 256, T, ptr(nts), None, 0, None, None, None, None, 0, 256)
+    first = buf("r2first", (256,), torch.int64)
+    tot = buf("r2tot", (1,), torch.int64)
+    scan_excl(nts, out=first, total=tot)
+    total = int(tot.item())
+    tstart = buf("r2tst", (total,), torch.int64)
+    trows = buf("r2trw", (total,), torch.int32)
+    thbase = buf("r2thb", (total,), torch.int64)
+    thstride = buf("r2ths", (total,), torch.int64)
+    hip("ptg_seg_plan", ptr(seg_start), ptr(seg_len), 256, T, ptr(nts), ptr(first), total, ptr(tstart), ptr(trows),
+        ptr(thbase), ptr(thstride), 1, 256)
+    hist2 = buf("r2hist", (256 * total,), torch.int32)
+    hip("ptg_range2_count", ptr(ok32), ptr(tstart), ptr(trows), ptr(thbase), ptr(thstride), total, nv, sh2,
+        ptr(hist2))
+    offs2 = buf("r2offs", (256 * total + 1,), torch.int64)
+    scan_excl(hist2, out=offs2[:-1], total=offs2[-1:])
+    ok16 = buf("rokeys16", (max(n, 1),), torch.int16)[:n]
+    ov2 = [buf(f"aov{j}", (max(n, 1),), torch.float64)[:n] for j in range(nv)]
+    vin = (ctypes.c_void_p * PAY_MAX)(*([o.data_ptr() for o in ov1] + [0] * (PAY_MAX - nv)))
+    pout2 = _pay_out(ov2)
+    hip("ptg_range2_scatter", ptr(ok32), ctypes.addressof(vin), nv, ptr(tstart), ptr(trows), ptr(thbase),
+        ptr(thstride), total, sh2, ptr(offs2), n, ptr(ok16), ctypes.addressof(pout2))
+    nfine = 256 * 256
+    fstart = buf("r2fst", (nfine,), torch.int64)
+    fend = buf("r2fen", (nfine,), torch.int64)
+    flen = buf("r2fln", (nfine,), torch.int64)
+    hip("ptg_seg_bounds", ptr(offs2), ptr(first), ptr(nts), 256, n, ptr(fstart), ptr(fend), ptr(flen), 256)
+    Rw = nfine << sh2
+    chunks = 1
+    prow = buf("r2prow", (chunks, 1 + nv, Rw), torch.int32)
+    psum = buf("r2psum", (chunks, max(nv, 1), Rw), torch.float64)
+    vptrs = (ctypes.c_void_p * PAY_MAX)(*([o.data_ptr() for o in ov2] + [0] * (PAY_MAX - nv)))
+    hip("ptg_range2_agg", ptr(ok16), ctypes.addressof(vptrs), nv, ptr(fstart), ptr(fend), nfine, chunks, sh2,
+        ptr(prow), ptr(psum))
+    return _dense_extract(prow, psum, None, chunks, nv, Rw, lo, dev)
+
+
 H9_BINS = 512
 H9_MIN_KEYS = 1 << 16  # below this the recursive path needs one 64-way level: the same passes
 
@@ -586,6 +667,12 @@ def hash_agg_radix(keys: torch.Tensor, vals: list, valids: list, want_minmax: bo
         slo, shi = minmax_i64(keys.contiguous(), n=(n + st_ - 1) // st_, stride=st_)
         if shi - slo < (RADIX_RANGE_BINS << _range_sh_max(nv, want_minmax)):
             r = hash_agg_range(keys.contiguous(), pay, buf, nv, (slo, shi), want_minmax)
+            if r is not None:
+                return r
+        elif (not want_minmax and nv <= 2 and shi - slo < RANGE2_MAX_SPAN // 2 and config.get("groupby_range2")
+              and (shi - slo) < 4 * n):
+            # a dense wide span (a sample covering it densely: at least ~1 row per 4 keys)
+            r = hash_agg_range2(keys.contiguous(), pay, buf, nv, (slo, shi))
             if r is not None:
                 return r
     K = est_keys if est_keys is not None else estimate_distinct(keys)

@@ -136,6 +136,36 @@ def test_range_agg_matches_host(hip_built, lo, span, nv, minmax):
     _assert_agg_equal(got, want, minmax)
 
 
+@pytest.mark.parametrize("lo,span,nv", [(0, 1 << 21, 1), (-3_000_000_000, 5_000_000, 2), (77, 20_000_000, 0),
+                                         (5, 9_000_000, 1)])
+def test_range2_agg_matches_host(hip_built, lo, span, nv):
+    """Dense keys spanning 2^20..2^28 values take the two-level range path (range2_*: coarse 256-way
+    pass with u32 window offsets, fine 256-way pass per coarse partition, direct-indexed LDS
+    aggregation per fine window): sums / non-null counts with NaNs and validity masks, 0-2 value
+    columns, negative keys, sparse coverage (20M keys over 6M rows).  Checked against the host path."""
+    n = 6_000_000
+    g = torch.Generator().manual_seed(span + nv + 1)
+    k = torch.randint(0, span, (n,), generator=g) + lo
+    k[3], k[n - 9] = lo, lo + span - 1
+    cols, valids = [], []
+    for j in range(nv):
+        if j == 0:
+            x = torch.rand(n, generator=g, dtype=torch.float64)
+            x[::89] = math.nan
+            vd = None
+        else:
+            x = torch.randint(-1000, 1000, (n,), generator=g, dtype=torch.int32)
+            vd = (torch.rand(n, generator=g) > 0.3).to(torch.uint8)
+        cols.append(x)
+        valids.append(vd)
+    ws = {}
+    got = D.hash_agg_radix(k.cuda(), [c.cuda() for c in cols], [None if x is None else x.cuda() for x in valids],
+                           False, ws=ws)
+    assert "r2prow" in ws, "two-level range path not taken"
+    want = D.hash_agg(k, cols, valids, False)
+    _assert_agg_equal(got, want, False)
+
+
 @pytest.mark.parametrize("lo,span,nv", [(0, 1000, 1), (-70, 3000, 2), (5_000_000_000, 17, 0), (3, 2000, 4)])
 def test_small_range_agg_matches_host(hip_built, lo, span, nv):
     """Key spans of a few thousand values skip partitioning (small_range_agg_k: one direct-indexed
