@@ -132,10 +132,12 @@ def test_mlp_fit_dataset_grouped_launches_match_per_batch_engine(hip_built, monk
                   metrics=["accuracy"], steps_per_execution=5)
         ds = Dataset.from_tensor_slices((X, y)).shuffle(300, seed=1).batch(32).repeat().prefetch(1)
         calls = []
-        orig = K.mlp_train
+        orig, orig_run = K.mlp_train, K.MlpStep.run
         monkeypatch.setattr(K, "mlp_train", lambda *a, **k: (calls.append(a[11]), orig(*a, **k))[1])
+        monkeypatch.setattr(K.MlpStep, "run", lambda self, *a, **k: (calls.append(a[2]), orig_run(self, *a, **k))[1])
         h = m.fit(ds, epochs=3, steps_per_epoch=13, verbose=0)
         monkeypatch.setattr(K, "mlp_train", orig)
+        monkeypatch.setattr(K.MlpStep, "run", orig_run)
         torch.cuda.synchronize()
         return m.store.flat.clone(), h.history["loss"], calls, m.optimizer.iterations
 
