@@ -339,6 +339,9 @@ class Model(Sequential):
         last = self.ops[-1]
         return getattr(last, "inner", last)
 
+    def _tape_head_ok(self) -> bool:
+        return False  # the deferred-prediction head (nn/tape.py) follows the Sequential plan only
+
     def first_op(self):
         first = self.ops[0]
         return getattr(first, "op", getattr(first, "inner", first))
