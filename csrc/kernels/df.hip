@@ -2137,7 +2137,7 @@ int ptg_part_agg2(const void* okeys, int key32, long kbase, const void* const* v
 int ptg_range_tile_rows(int nv) { return nv <= 1 ? RGT : (nv == 2 ? RGT / 2 : RGT / 4); }
 int ptg_range_count(const void* keys, long n, long lo, int sh, int T, int ntiles, void* hist, void* range,
                     hipStream_t s) {
-  if (ntiles <= 0 || T > RGT || sh < 0 || sh > 12) return (int)hipErrorInvalidValue;
+  if (ntiles <= 0 || T > RGT || sh < 0 || sh > 24) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(range_count_k, dim3(ntiles), dim3(256), 0, s, (const long long*)keys, n, (long long)lo, sh, T,
                      ntiles, (unsigned int*)hist, (long long*)range);
   PTG_RETURN_LAUNCH();

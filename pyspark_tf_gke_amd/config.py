@@ -52,9 +52,10 @@ _K = [
          "sparse keys at ~64K..1.3M groups: one 512-way hash partition + LDS hash tables (sum/count/avg, <= 2 columns)"),
     Knob("groupby_h9_chunks", int, 4, "PTG_H9_CHUNKS", "spark.ptg.groupby.h9Chunks",
          "row chunks per partition in the 512-way hash aggregation (workgroups = 512 x chunks)"),
-    Knob("sort_onesweep", bool, True, "PTG_SORT_ONESWEEP", "spark.ptg.sort.onesweep",
+    Knob("sort_onesweep", bool, False, "PTG_SORT_ONESWEEP", "spark.ptg.sort.onesweep",
          "radix sort passes without a count pass: every pass's digit histogram from one read, tile offsets by "
-         "decoupled look-back (onesweep)"),
+         "decoupled look-back (onesweep; 1B rows: 157.6 vs 134.0 ms for count + scatter, the cross-XCD "
+         "coherent look-back polls cost more than the saved key read, so off)"),
     Knob("shuffle_buffer_gb", float, 64.0, "PTG_SHUFFLE_BUFFER_GB", "spark.ptg.shuffle.buffer.gb",
          "HBM staging budget of one all-to-all-v shuffle round"),
     Knob("device", str, "", "PTG_DEVICE", "spark.ptg.device", "executor device: cuda / cpu (default: cuda if present)"),
@@ -93,16 +94,19 @@ _K = [
     Knob("ppb_dgrad", bool, False, "PTG_PPB_DGRAD", None,
          "CNN-B1 layers 3-5: the dgrad epilogue also writes the pooled block's dZ (conv.hip EPI_PPB); the "
          "PReLU/pool backward moves to the side stream for dalpha/dbias only (A/B: 1.80-1.88 vs 1.65 ms, off)"),
-    Knob("conv32", bool, False, "PTG_CONV32", None,
-         "5x5 convs with C, Cout in 16..64 (CNN-B1 layers 3-5 and their data gradients): the 32x32x16-MFMA "
-         "implicit GEMM of conv32.hip instead of the halo strip kernels"),
+    Knob("conv32", bool, True, "PTG_CONV32", None,
+         "5x5 convs with C, Cout in 16..64 (CNN-B1 layers 4-5 and their data gradients, see conv32_min_ch): the "
+         "32x32x16-MFMA implicit GEMM of conv32.hip instead of the halo strip kernels (b256 A/B: 1.652/1.649 vs "
+         "1.657/1.650 ms; on layer 3 as well: 1.80 ms)"),
     Knob("conv32_min_ch", int, 32, "PTG_CONV32_MINCH", None,
          "conv32 only where min(C, Cout) >= this (layer bench: it wins on CNN-B1 layers 4-5, loses the 32->16 dgrad)"),
     Knob("ppb_rows", bool, False, "PTG_PPB_ROWS", None,
          "CNN-B1 layers 2-4: PReLU + max-pool backward in the row-pair layout (ppb.hip, dalpha via chunk partials)"),
     Knob("conv1_rec", bool, True, "PTG_CONV1_REC", None, "first conv layer (conv1.hip): forward keeps the pool record, backward needs no recompute (0: recompute z in the backward)"),
     Knob("conv1_fused", bool, True, "PTG_CONV1_FUSED", None, "first conv layer: pooled-only forward + one recomputing backward kernel (conv1.hip)"),
-    Knob("blaslt_dx", bool, False, "PTG_BLASLT_DX", None, "A/B only: big-Dense dX through hipBLASLt instead of the skinny-M MFMA GEMM"),
+    Knob("blaslt_dx", bool, True, "PTG_BLASLT_DX", None,
+         "big-Dense dX (a plain GEMM) through hipBLASLt instead of the skinny-M MFMA GEMM "
+         "(CNN-B1 b256 A/B: 1.642/1.629 vs 1.657/1.650 ms)"),
     Knob("hip_graph", bool, False, "PTG_HIP_GRAPH", None, "capture the training step in a HIP graph (jit_compile)"),
     Knob("host_fp32", bool, False, "PTG_HOST_FP32", None, "CPU tensors: fp32 reference path everywhere"),
     Knob("seed", int, 1337, "PTG_SEED", None, "weight-initialisation seed when none is given"),
