@@ -104,6 +104,87 @@ PTG_DEV void gemm(int M, int N, int K, const float* P, int pi, int pk, const flo
 
 // tstep (nullable): the optimizer step counter on the device (read for Adam's bias correction and
 // advanced by `steps` at the end), so a cached launch needs no per-step host argument
+struct AdamArgs {
+  float* p;
+  float* m;
+  float* v;
+  bf16_t* pbf;
+  float lr_t, b1, b2, eps;
+};
+
+PTG_DEV float adam_update(const AdamArgs& o, long idx, float g, float p0, float m0, float v0) {
+  const float mm = o.b1 * m0 + (1.f - o.b1) * g;
+  const float vv = o.b2 * v0 + (1.f - o.b2) * g * g;
+  const float pp = p0 - o.lr_t * mm / (sqrtf(vv) + o.eps);
+  o.m[idx] = mm;
+  o.v[idx] = vv;
+  o.p[idx] = pp;
+  if (o.pbf) o.pbf[idx] = f2bf(pp);
+  return pp;
+}
+
+// dW[i][j] = sum_k P[i*pi + k*pk] Q[j*qj + k*qk] (i < M output units, j < N inputs) with Adam on
+// element wo + i*N + j: the thread's p / m / v are loaded BEFORE its GEMM loop, so the HBM latency
+// hides under the FMAs instead of following each output; the updated weight also goes to LDS W.
+template <int TM, int TN>
+PTG_DEV void dw_adam_tile(int M, int N, int K, const float* P, int pi, int pk, const float* Q, int qj, int qk,
+                          const AdamArgs& o, long wo, float* Wl, int S) {
+  const int tm = (M + TM - 1) / TM, tn = (N + TN - 1) / TN;
+  for (int t = threadIdx.x; t < tm * tn; t += NT) {
+    const int i0 = (t / tn) * TM, j0 = (t - (t / tn) * tn) * TN;
+    float p0[TM][TN], m0[TM][TN], v0[TM][TN];
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        const long idx = wo + (long)min(i0 + a, M - 1) * N + min(j0 + b, N - 1);
+        p0[a][b] = o.p[idx];
+        m0[a][b] = o.m[idx];
+        v0[a][b] = o.v[idx];
+      }
+    const float* pr[TM];
+    const float* qr[TN];
+#pragma unroll
+    for (int a = 0; a < TM; ++a) pr[a] = P + min(i0 + a, M - 1) * pi;
+#pragma unroll
+    for (int b = 0; b < TN; ++b) qr[b] = Q + min(j0 + b, N - 1) * qj;
+    float acc[TM][TN];
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b) acc[a][b] = 0.f;
+    for (int k = 0; k < K; ++k) {
+      float av[TM], bv[TN];
+#pragma unroll
+      for (int a = 0; a < TM; ++a) av[a] = pr[a][k * pk];
+#pragma unroll
+      for (int b = 0; b < TN; ++b) bv[b] = qr[b][k * qk];
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b) acc[a][b] = fmaf(av[a], bv[b], acc[a][b]);
+    }
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b)
+        if (i0 + a < M && j0 + b < N) {
+          const int i = i0 + a, j = j0 + b;
+          Wl[i * S + j] = adam_update(o, wo + (long)i * N + j, acc[a][b], p0[a][b], m0[a][b], v0[a][b]);
+        }
+  }
+}
+
+PTG_DEV void dw_adam(int M, int N, int K, const float* P, int pi, int pk, const float* Q, int qj, int qk,
+                     const AdamArgs& o, long wo, float* Wl, int S) {
+  const int outs = M * N;
+  if (outs >= 16 * NT) dw_adam_tile<4, 4>(M, N, K, P, pi, pk, Q, qj, qk, o, wo, Wl, S);
+  else if (outs >= 8 * NT) dw_adam_tile<2, 4>(M, N, K, P, pi, pk, Q, qj, qk, o, wo, Wl, S);
+  else if (outs >= 4 * NT) dw_adam_tile<2, 2>(M, N, K, P, pi, pk, Q, qj, qk, o, wo, Wl, S);
+  else if (outs >= 2 * NT) dw_adam_tile<1, 2>(M, N, K, P, pi, pk, Q, qj, qk, o, wo, Wl, S);
+  else dw_adam_tile<1, 1>(M, N, K, P, pi, pk, Q, qj, qk, o, wo, Wl, S);
+}
+
 __global__ __launch_bounds__(NT) void mlp_train_k(const float* __restrict__ x, const void* __restrict__ y,
                                                   float* __restrict__ p, float* __restrict__ m,
                                                   float* __restrict__ v, bf16_t* __restrict__ pbf,
@@ -179,7 +260,7 @@ __global__ __launch_bounds__(NT) void mlp_train_k(const float* __restrict__ x, c
     // then each weight gradient with its Adam update into HBM and into the LDS weights in place
     const float t = (float)(t0 + st + 1);
     const float lr_t = D.lr * sqrtf(1.f - powf(D.b2, t)) / (1.f - powf(D.b1, t));
-    const float b1 = D.b1, b2 = D.b2, eps = D.eps;
+    const AdamArgs ad{p, m, v, pbf, lr_t, D.b1, D.b2, D.eps};
     int cur = D.lg0, nxt = D.lg1;
     for (int l = L - 1; l >= 0; --l) {
       const int K = D.d[l], N = D.d[l + 1], S = D.ws[l], SA = D.as[l];
@@ -196,34 +277,32 @@ __global__ __launch_bounds__(NT) void mlp_train_k(const float* __restrict__ x, c
         });
         __syncthreads();  // every dX read of W_l before the in-place update below
       }
+      // bias gradients of this layer: their p / m / v loads are issued first (consumed after the dW GEMM)
+      const bool hasb = D.boff[l] >= 0;
+      const int bn0 = tid, bn1 = tid + NT;
+      float bp[2] = {0.f, 0.f}, bm[2] = {0.f, 0.f}, bvv[2] = {0.f, 0.f};
+      if (hasb) {
+        if (bn0 < N) { const long q = D.boff[l] + bn0; bp[0] = p[q]; bm[0] = m[q]; bvv[0] = v[q]; }
+        if (bn1 < N) { const long q = D.boff[l] + bn1; bp[1] = p[q]; bm[1] = m[q]; bvv[1] = v[q]; }
+      }
       // dW[n][k] = sum_r G[r][n] A[r][k], Adam straight from the register
-      float* Wn = sm + D.lw[l];
-      const long wo = D.woff[l];
-      gemm(N, K, B, Gc, 1, D.gs, A, 1, SA, [&](int n, int k, float g) {
-        const long idx = wo + (long)n * K + k;
-        const float mm = b1 * m[idx] + (1.f - b1) * g;
-        const float vv = b2 * v[idx] + (1.f - b2) * g * g;
-        const float pp = p[idx] - lr_t * mm / (sqrtf(vv) + eps);
-        m[idx] = mm;
-        v[idx] = vv;
-        p[idx] = pp;
-        if (pbf) pbf[idx] = f2bf(pp);
-        Wn[n * S + k] = pp;
-      });
-      if (D.boff[l] >= 0) {
-        float* bn = sm + D.lb[l];
-        for (int n = tid; n < N; n += NT) {
+      dw_adam(N, K, B, Gc, 1, D.gs, A, 1, SA, ad, D.woff[l], sm + D.lw[l], S);
+      if (hasb) {
+        float* bnl = sm + D.lb[l];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int n = u ? bn1 : bn0;
+          if (n < N) {
+            float g = 0.f;
+            for (int r = 0; r < B; ++r) g += Gc[r * D.gs + n];
+            bnl[n] = adam_update(ad, D.boff[l] + n, g, bp[u], bm[u], bvv[u]);
+          }
+        }
+        for (int n = tid + 2 * NT; n < N; n += NT) {  // (layers wider than 2 x NT units)
           float g = 0.f;
           for (int r = 0; r < B; ++r) g += Gc[r * D.gs + n];
-          const long idx = D.boff[l] + n;
-          const float mm = b1 * m[idx] + (1.f - b1) * g;
-          const float vv = b2 * v[idx] + (1.f - b2) * g * g;
-          const float pp = p[idx] - lr_t * mm / (sqrtf(vv) + eps);
-          m[idx] = mm;
-          v[idx] = vv;
-          p[idx] = pp;
-          if (pbf) pbf[idx] = f2bf(pp);
-          bn[n] = pp;
+          const long q = D.boff[l] + n;
+          bnl[n] = adam_update(ad, q, g, p[q], m[q], v[q]);
         }
       }
       __syncthreads();
