@@ -385,8 +385,12 @@ int ptg_dense_extract(const void* prow, const void* psum, const void* pmm, int C
                       void* bcount, void* boff, void* total, const void* outs, int pass, hipStream_t s) {
   if (nv < 0 || nv > 4 || C < 1) return (int)hipErrorInvalidValue;
   const int nb = (int)((W + SC_TILE - 1) / SC_TILE);
-  if (nb > SC_TILE) return (int)hipErrorInvalidValue;  // block counts are scanned by one workgroup tile
   if (nb == 0) return (int)hipMemsetAsync(total, 0, 8, s);
+  if (pass == 0) {  // block counts only (the caller scans them: any W)
+    hipLaunchKernelGGL(dense_count_k, dim3(nb), dim3(256), 0, s, (const int*)prow, C, nv, W, (int*)bcount);
+    PTG_RETURN_LAUNCH();
+  }
+  if (pass == 1 && nb > SC_TILE) return (int)hipErrorInvalidValue;  // one workgroup tile scans the block counts
   if (pass == 1) {
     hipLaunchKernelGGL(dense_count_k, dim3(nb), dim3(256), 0, s, (const int*)prow, C, nv, W, (int*)bcount);
     hipLaunchKernelGGL(scan_reduce_k<int>, dim3(1), dim3(256), 0, s, (const int*)bcount, (long)nb, (long long*)total);

@@ -173,8 +173,13 @@ def _dense_extract(prow, psum, pmm, C: int, nv: int, W: int, lo: int, dev):
     bcount = torch.empty(nb, dtype=torch.int32, device=dev)
     boff = torch.empty(nb, dtype=torch.int64, device=dev)
     total = torch.empty(1, dtype=torch.int64, device=dev)
-    hip("ptg_dense_extract", ptr(prow), ptr(psum), ptr(pmm), C, nv, W, int(lo), ptr(bcount), ptr(boff), ptr(total),
-        None, 1)
+    if nb <= 4096:
+        hip("ptg_dense_extract", ptr(prow), ptr(psum), ptr(pmm), C, nv, W, int(lo), ptr(bcount), ptr(boff),
+            ptr(total), None, 1)
+    else:  # windows beyond 2^24 keys (the two-level range path): block counts scanned by scan_excl
+        hip("ptg_dense_extract", ptr(prow), ptr(psum), ptr(pmm), C, nv, W, int(lo), ptr(bcount), ptr(boff),
+            ptr(total), None, 0)
+        scan_excl(bcount, out=boff, total=total)
     m = int(total.item())
     keys = torch.empty(max(m, 1), dtype=torch.int64, device=dev)[:m]
     cols = torch.empty((1 + 4 * max(nv, 1), max(m, 1)), dtype=torch.float64, device=dev)[:, :m]
