@@ -56,14 +56,15 @@ def test_gemm_splitk_atomic_and_bias_relu():
 
 @pytest.mark.parametrize("M,N,Kd,bn", [(128, 2048, 20480 // 8, -1), (256, 2048, 20480, -1), (256, 2048, 20480, 64),
                                        (200, 512, 64 * 200, -1), (256, 2048, 20480, 0)])
-def test_linear_dx_dw(M, N, Kd, bn):
+def test_linear_dx_dw(M, N, Kd, bn, monkeypatch):
     """dX on gemm_kernel: the CNN-B1 shape (M = 256, K = 20480) on the skinny-M 256x80 tiles (bn -1),
-    forced 256x64 tiles, a ragged M with 256x64, and the 128x128 tiling (bn 0); never hipBLASLt."""
+    forced 256x64 tiles, a ragged M with 256x64, and the 128x128 tiling (bn 0); the hipBLASLt route
+    (the default for this plain GEMM) is switched off so our kernel is the one checked."""
     from pyspark_tf_gke_amd import _native
 
+    monkeypatch.setattr(K, "BLASLT_DX", False)
     dy, w, x = rnd(M, N), rnd(N, Kd), rnd(M, Kd)
     dx = torch.empty(M, Kd, device=DEV, dtype=torch.bfloat16)
-    assert not K.BLASLT_DX
     _native.hip_lib().ptg_gemm_skinny_set(bn)
     try:
         K.linear_dx(dy.to(DEV), w.to(DEV), dx)

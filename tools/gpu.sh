@@ -30,7 +30,7 @@ for task in "$@"; do
   case $name in
     tests)
       log=gpurun_out/pytest_gpu${arg:+_$arg}.log
-      timeout -k 10 ${TESTS_T:-1100} python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread \
+      timeout -k 10 ${TESTS_T:-1100} python -u -m pytest tests -m gpu ${TESTS_X--x} -q --timeout 240 --timeout-method thread \
         ${arg:+-k "$arg"} > "$log" 2>&1 || fail tests "$log"
       tail -2 "$log" ;;
     smoke)
