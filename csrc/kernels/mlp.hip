@@ -72,7 +72,8 @@ PTG_DEV void tile_gemm(int M, int N, int K, const float* P, int pi, int pk, cons
     for (int a = 0; a < TM; ++a)
 #pragma unroll
       for (int b = 0; b < TN; ++b) acc[a][b] = 0.f;
-    for (int k = 0; k < K; ++k) {
+#pragma unroll 8
+    for (int k = 0; k < K; ++k) {  // unrolled: several k's LDS loads in flight at once
       float av[TM], bv[TN];
 #pragma unroll
       for (int a = 0; a < TM; ++a) av[a] = pr[a][k * pk];
@@ -153,7 +154,8 @@ PTG_DEV void dw_adam_tile(int M, int N, int K, const float* P, int pi, int pk, c
     for (int a = 0; a < TM; ++a)
 #pragma unroll
       for (int b = 0; b < TN; ++b) acc[a][b] = 0.f;
-    for (int k = 0; k < K; ++k) {
+#pragma unroll 8
+    for (int k = 0; k < K; ++k) {  // unrolled: several k's LDS loads in flight at once
       float av[TM], bv[TN];
 #pragma unroll
       for (int a = 0; a < TM; ++a) av[a] = pr[a][k * pk];

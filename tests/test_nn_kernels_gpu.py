@@ -697,11 +697,13 @@ def test_conv_fwd_gemm256_resnet_layer():
 
 
 @pytest.mark.parametrize("N,H,W,Cin,Co", [(3, 16, 20, 32, 64), (2, 8, 10, 64, 64), (4, 32, 40, 16, 32)])
-def test_dgrad_ppb_epilogue_matches_two_kernels(hip_built, N, H, W, Cin, Co):
+def test_dgrad_ppb_epilogue_matches_two_kernels(hip_built, N, H, W, Cin, Co, monkeypatch):
     """conv.hip EPI_PPB: one dgrad launch writes dA and the pooled block's dZ; both equal the dgrad
-    kernel + prelu_pool_bwd_sg_k pair bit for bit, and the store-less prelu_pool_bwd gives the same
-    dalpha / dbias as the storing one."""
+    kernel + prelu_pool_bwd_sg_k pair bit for bit (the halo strip dgrad on both sides: conv32 is
+    switched off), and the store-less prelu_pool_bwd gives the same dalpha / dbias as the storing one."""
     from pyspark_tf_gke_amd.ops import nn as K
+
+    monkeypatch.setattr(K, "CONV32", False)
 
     torch.manual_seed(N * H + Cin)
     dz = (torch.randn(N, H, W, Co) * 0.5).to(torch.bfloat16).cuda()          # this layer's dZ
@@ -776,9 +778,11 @@ def test_ppb_dgrad_model_step_matches_two_kernel_path(hip_built):
     assert d <= 0.05 * u, (d, u)
 
 
-def test_linear_dx_prelu_matches_two_kernels(hip_built):
+def test_linear_dx_prelu_matches_two_kernels(hip_built, monkeypatch):
     """gemm.hip EpiBf16 out2: the Dense dX also writes the PReLU block's dZ; equal bit for bit to
-    linear_dx + prelu_bwd_sg_k, and the store-less prelu_bwd gives the same dalpha / dbias."""
+    linear_dx (our GEMM, not the hipBLASLt route) + prelu_bwd_sg_k, and the store-less prelu_bwd
+    gives the same dalpha / dbias."""
+    monkeypatch.setattr(K, "BLASLT_DX", False)
     torch.manual_seed(3)
     B, N, Kd, C = 64, 256, 16 * 20 * 64, 64
     dy = (torch.randn(B, N) * 0.1).to(torch.bfloat16).cuda()
