@@ -1269,7 +1269,10 @@ __global__ __launch_bounds__(256) void small_range_agg_k(const long long* __rest
 // A table that overflows (far more keys than the estimate) sets the error word; the host then takes
 // the recursive path, so a bad estimate costs time, never correctness.
 #define H9B 512
-#define H9T 4096  // tile rows for nv <= 1 (nv == 2: 2048, the LDS staging budget)
+#ifndef PTG_H9T
+#define PTG_H9T 4096
+#endif
+#define H9T PTG_H9T  // tile rows for nv <= 1 (nv == 2: half, the LDS staging budget)
 PTG_DEV int h9_digit(long long k) { return (int)(mix64((unsigned long long)k) >> (64 - 9)); }
 
 __global__ __launch_bounds__(256) void hash9_count_k(const long long* __restrict__ keys, long n, int T,
