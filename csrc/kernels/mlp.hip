@@ -23,7 +23,10 @@
 namespace ptgm {
 
 constexpr int MAXL = 6;
-constexpr int NT = 512;
+#ifndef PTG_MLP_NT
+#define PTG_MLP_NT 512
+#endif
+constexpr int NT = PTG_MLP_NT;  // threads of the one workgroup (A/B builds: 256 / 1024)
 
 struct MlpDesc {
   int L, B, steps, loss;        // loss 0: softmax + sparse categorical cross-entropy, 1: MSE
