@@ -23,6 +23,7 @@ for nk in [int(x) for x in a.keys.split(",")]:
         r = bg.run(rows_per_gpu=a.rows, num_keys=nk, steps=a.steps, warmup=1, sparse=sparse)
         print(json.dumps({"keys": nk, "kind": "sparse" if sparse else "dense", "G_rows_per_s": round(r["value"] / 1e9, 2),
                           "ms": r["ms_per_step"], "groups_out": r["config"].get("groups_out"),
-                          "counts_check": r["config"].get("counts_check")}), flush=True)
+                          "counts_check": r["config"].get("counts_check"), "sums_check": r["config"].get("sums_check"),
+                          "groups_check": r["config"].get("groups_check")}), flush=True)
         gc.collect()
         torch.cuda.empty_cache()
