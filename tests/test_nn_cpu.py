@@ -278,3 +278,45 @@ def test_tape_head_pred_read_first_runs_plain_tail():
         finally:
             T.TAPE_HEAD = saved
     assert torch.equal(m1.store.flat, m2.store.flat)
+
+
+def test_ps_one_worker_tape_lazy_path_matches_plain_loop():
+    """The reference's primary loop with one worker (ParameterServerStrategy + ClusterCoordinator
+    scheduling the GradientTape closure) on the CNN-B1 shape: the deferred Dense dW, the fused
+    head and the round commit (ps.py _apply_local -> tape._apply_overlapped) train exactly like
+    a plain tape loop."""
+    from pyspark_tf_gke_amd import distribute as ds
+    from pyspark_tf_gke_amd.cli.train import make_parameter_server_strategy
+    from pyspark_tf_gke_amd.nn import tape as T
+
+    torch.manual_seed(4)
+    xs = [torch.rand(4, 32, 40, 3) for _ in range(2)]
+    ys = [torch.rand(4, 2) for _ in range(2)]
+    m0 = build_cnn_model((32, 40, 3), flat=True, summary=False, device="cpu")
+    init = m0.get_weights()
+    o0 = nn.optimizers.Adam(1e-3)
+    for i in range(4):
+        _tape_step(m0, o0, xs[i % 2], ys[i % 2])
+    strategy = make_parameter_server_strategy(1, 1)
+    with strategy.scope():
+        m1 = build_cnn_model((32, 40, 3), flat=True, summary=False, device="cpu")
+        o1 = nn.optimizers.Adam(1e-3)
+        lo = nn.losses.MeanSquaredError()
+    m1.set_weights(init)
+    coord = ds.ClusterCoordinator(strategy)
+    seen = []
+
+    def step_fn(i):
+        with nn.GradientTape() as tape:
+            p = m1(xs[i % 2], training=True)
+            lv = lo(ys[i % 2], p)
+        g = tape.gradient(lv, m1.trainable_variables)
+        seen.append(any(isinstance(t, T._LazyGrad) for t in g))
+        o1.apply_gradients(zip(g, m1.trainable_variables))
+        return lv
+
+    for i in range(4):
+        coord.schedule(lambda i=i: strategy.run(step_fn, args=(i,)))
+    coord.join()
+    assert all(seen) and o1.iterations == 4
+    assert torch.allclose(m0.store.flat, m1.store.flat, atol=1e-6)
