@@ -457,6 +457,15 @@ class DenseOp(Op):
             acc.add_(x.float() @ self.dense.kernel.bf16.float().t())
             self._x = x
             return acc
+        if BLASLT_DENSE_FWD[0]:
+            # a plain bf16 GEMM with fp32 output: hipBLASLt (the head kernel re-zeroes acc afterwards,
+            # harmless here since the GEMM overwrites it)
+            try:
+                torch.mm(x, self.dense.kernel.bf16.t(), out_dtype=torch.float32, out=acc)
+                self._x = x
+                return acc
+            except (TypeError, RuntimeError):
+                BLASLT_DENSE_FWD[0] = False
         tiles = -(-B // 128) * -(-N // 128)
         splits = 1 if Kd < 4096 else max(1, min(16, 512 // max(tiles, 1), Kd // 1024))
         K.gemm(B, N, Kd, x, Kd, 1, self.dense.kernel.bf16, Kd, 1, 3, acc, N, None, 0, splits)
@@ -545,6 +554,11 @@ class DenseOp(Op):
         dx = ws.get(self.name + "/dx", x.shape, out_dtype, dev)
         K.dense_small_dx(dz, self.dense.kernel.data, mask, dx)
         return dx
+
+
+# CNN-B1 Dense forward before the fused head (split-K sums in fp32): hipBLASLt with fp32 output
+# instead of our split-K atomic GEMM (A/B option, PTG_BLASLT_DENSE_FWD=1)
+BLASLT_DENSE_FWD = [config.get("blaslt_dense_fwd")]
 
 
 class FlattenOp(Op):
