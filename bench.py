@@ -265,7 +265,7 @@ def main():
                 r2 = bench_train(a2, strategy, rank, world)
                 extra[f"batch{b}"] = {"value": r2["value"], "unit": "samples/s", "ms_per_step": r2["ms_per_step"],
                                       "per_gpu_batch": b, "global_batch": b * world}
-        if args.workload == "cnn_b1" and args.mlp_batches:
+        if args.workload == "cnn_b1" and args.mlp_batches and world == 1:
             for b in [int(x) for x in args.mlp_batches.split(",") if x.strip()]:
                 a2 = argparse.Namespace(**{**vars(args), "batch_size": b, "workload": "mlp", "steps": 200,
                                            "warmup": 20})
