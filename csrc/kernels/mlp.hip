@@ -33,7 +33,8 @@ struct MlpDesc {
   int d[MAXL + 1];              // d[0] input features, d[l + 1] units of layer l
   int act[MAXL];                // hidden activation of layer l: 0 linear, 1 relu (last: from loss)
   long woff[MAXL], boff[MAXL];  // element offsets of W_l ([d[l+1]][d[l]]) and b_l in the flat store
-  int lw[MAXL], lb[MAXL];       // LDS float offsets of W_l (row stride ws[l]) and b_l
+  int lw[MAXL], lb[MAXL];       // LDS float offsets of W_l (row stride ws[l]) and b_l (copy 0)
+  int wtot, dbl;                // floats of one weight copy; dbl: a second copy follows (LDS permitting)
   int ws[MAXL];                 // LDS row stride of W_l (odd)
   int la[MAXL + 1], as[MAXL + 1];  // LDS offset / row stride (odd) of activation l
   int lg0, lg1, gs;             // the two gradient buffers (row stride gs, odd) and red scratch
@@ -203,12 +204,18 @@ __global__ __launch_bounds__(NT) void mlp_train_k(const float* __restrict__ x, c
   for (int l = 0; l < L; ++l) {
     const int K = D.d[l], N = D.d[l + 1], S = D.ws[l];
     for (int i = tid; i < N * K; i += NT) sm[D.lw[l] + (i / K) * S + i % K] = p[D.woff[l] + i];
-    for (int n = tid; n < N; n += NT) sm[D.lb[l] + n] = D.boff[l] >= 0 ? p[D.boff[l] + n] : 0.f;
+    for (int n = tid; n < N; n += NT) {
+      sm[D.lb[l] + n] = D.boff[l] >= 0 ? p[D.boff[l] + n] : 0.f;
+      if (D.dbl && D.boff[l] < 0) sm[D.wtot + D.lb[l] + n] = 0.f;  // bias-less: zeros in both copies
+    }
   }
   float s_loss = 0.f, s_a = 0.f, s_b = 0.f;
   const int C = D.d[L];
-  const int wcur = 0;
+  // with two weight copies a step reads one and its Adam epilogues write the other, so a layer's dX
+  // and its weight update share one phase; otherwise the update is in place after a barrier
+  int wcur = 0;
   for (int st = 0; st < D.steps; ++st) {
+    const int wnxt = D.dbl ? D.wtot - wcur : wcur;
     // ---- input batch
     const int K0 = D.d[0];
     const float* xs = x + (long)st * B * K0;
@@ -280,7 +287,7 @@ __global__ __launch_bounds__(NT) void mlp_train_k(const float* __restrict__ x, c
           if (mask && !(A[r * SA + k] > 0.f)) s = 0.f;
           Gn[r * gs + k] = s;
         });
-        __syncthreads();  // every dX read of W_l before the in-place update below
+        if (!D.dbl) __syncthreads();  // every dX read of W_l before the in-place update below
       }
       // bias gradients of this layer: their p / m / v loads are issued first (consumed after the dW GEMM)
       const bool hasb = D.boff[l] >= 0;
@@ -291,9 +298,9 @@ __global__ __launch_bounds__(NT) void mlp_train_k(const float* __restrict__ x, c
         if (bn1 < N) { const long q = D.boff[l] + bn1; bp[1] = p[q]; bm[1] = m[q]; bvv[1] = v[q]; }
       }
       // dW[n][k] = sum_r G[r][n] A[r][k], Adam straight from the register
-      dw_adam(N, K, B, Gc, 1, D.gs, A, 1, SA, ad, D.woff[l], sm + D.lw[l], S);
+      dw_adam(N, K, B, Gc, 1, D.gs, A, 1, SA, ad, D.woff[l], sm + wnxt + D.lw[l], S);
       if (hasb) {
-        float* bnl = sm + D.lb[l];
+        float* bnl = sm + wnxt + D.lb[l];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
           const int n = u ? bn1 : bn0;
@@ -313,6 +320,7 @@ __global__ __launch_bounds__(NT) void mlp_train_k(const float* __restrict__ x, c
       __syncthreads();
       const int tmp = cur; cur = nxt; nxt = tmp;
     }
+    wcur = wnxt;  // (the next step's input barrier orders the new copy before any forward read)
   }
   float* red = sm + D.lred;
   const float tl = sum_block(s_loss, red);
@@ -367,6 +375,13 @@ static long mlp_plan(const long* hdesc, int L, int B, ptgm::MlpDesc* D) {
   D->lg0 = off; off += B * D->gs;
   D->lg1 = off; off += B * D->gs;
   D->lred = off; off += 16;
+  D->wtot = D->la[0];
+  D->dbl = (long)(off + D->wtot) * 4 <= 160 * 1024;
+  if (D->dbl) {  // the second weight copy goes right after the first: shift everything behind it
+    for (int l = 0; l <= L; ++l) D->la[l] += D->wtot;
+    D->lg0 += D->wtot; D->lg1 += D->wtot; D->lred += D->wtot;
+    off += D->wtot;
+  }
   return (long)off * 4;
 }
 
