@@ -1372,3 +1372,69 @@ int ptg_gap_bwd(const float* dy, void* out, int N, int HW, int C, hipStream_t s)
 }  // extern "C"
 
 PTG_CHECK_STATUS(nn_eltwise)
+
+// ----------------------------------------------------------------------------------------------
+// Streaming metric update in ONE launch (nn/metrics.py): state f64[2] = (total, count) += (the
+// batch's sum, `count`).  kind 0 Mean(values), 1 MeanAbsoluteError, 2 MeanSquaredError (yp - yt
+// elementwise, n elements), 3 SparseCategoricalAccuracy (yp [n][C] scores, yt [n] labels).  The
+// Keras metric objects of the reference's custom loops (train_tf_ps.py:608-609,627-628) update every
+// step; as torch ops each update was 4-7 small launches.  Types: 0 f32, 1 f64, 2 bf16, 3 i32, 4 i64.
+// ----------------------------------------------------------------------------------------------
+PTG_DEV double metric_ld(const void* p, int t, long i) {
+  switch (t) {
+    case 0: return (double)((const float*)p)[i];
+    case 1: return ((const double*)p)[i];
+    case 2: return (double)bf2f(((const bf16_t*)p)[i]);
+    case 3: return (double)((const int*)p)[i];
+    default: return (double)((const long long*)p)[i];
+  }
+}
+
+__global__ __launch_bounds__(256) void metric_update_k(int kind, const void* __restrict__ yp, int tp,
+                                                       const void* __restrict__ yt, int tt, long n, int C,
+                                                       double count, double* __restrict__ state) {
+  __shared__ double red[4];
+  double s = 0.0;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    if (kind == 0) {
+      s += metric_ld(yp, tp, i);
+    } else if (kind == 3) {
+      double best = metric_ld(yp, tp, i * C);
+      int am = 0;
+      for (int c = 1; c < C; ++c) {
+        const double v = metric_ld(yp, tp, i * C + c);
+        if (v > best) { best = v; am = c; }
+      }
+      s += (long long)metric_ld(yt, tt, i) == (long long)am ? 1.0 : 0.0;
+    } else {
+      const double d = metric_ld(yp, tp, i) - metric_ld(yt, tt, i);
+      s += kind == 1 ? fabs(d) : d * d;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double t = red[0] + red[1] + red[2] + red[3];
+    if (gridDim.x == 1) {
+      state[0] += t;
+      state[1] += count;
+    } else {
+      atomicAdd(state, t);
+      if (blockIdx.x == 0) atomicAdd(state + 1, count);
+    }
+  }
+}
+
+extern "C" {
+int ptg_metric_update(int kind, const void* yp, int tp, const void* yt, int tt, long n, int C, double count,
+                      void* state, hipStream_t s) {
+  if (kind < 0 || kind > 3 || (kind == 3 && C < 1) || n < 0) return (int)hipErrorInvalidValue;
+  long work = kind == 3 ? n * (long)C : n;
+  int g = (int)((work + 8191) / 8192);
+  g = g < 1 ? 1 : (g > 1024 ? 1024 : g);
+  hipLaunchKernelGGL(metric_update_k, dim3(g), dim3(256), 0, s, kind, yp, tp, yt, tt, n, C, count, (double*)state);
+  return (int)hipGetLastError();
+}
+}  // extern "C"

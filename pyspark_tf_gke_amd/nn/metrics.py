@@ -9,24 +9,50 @@ from __future__ import annotations
 import torch
 
 
+_MT = {torch.float32: 0, torch.float64: 1, torch.bfloat16: 2, torch.int32: 3, torch.int64: 4}
+
+
 class Metric:
     def __init__(self, name: str):
         from ..distribute import current_strategy
 
         self.name = name
+        self._state = None  # f64[2] = (total, count) on the data's device
         self._total = None
         self._count = None
         self._strategy = current_strategy()  # metrics created under strategy.scope() stay bound to it
 
     def _ensure(self, device):
-        if self._total is None or self._total.device != torch.device(device):
-            self._total = torch.zeros((), dtype=torch.float64, device=device)
-            self._count = torch.zeros((), dtype=torch.float64, device=device)
+        if self._state is None or self._state.device != torch.device(device):
+            self._state = torch.zeros(2, dtype=torch.float64, device=device)
+            self._total, self._count = self._state[0], self._state[1]
+
+    def _fused(self, kind: int, yp, yt=None, C: int = 0) -> bool:
+        """One-launch update on the GPU (nn_eltwise.hip metric_update_k); False: use the torch ops."""
+        if not (isinstance(yp, torch.Tensor) and yp.is_cuda and yp.dtype in _MT and yp.is_contiguous()):
+            return False
+        if yt is not None:
+            if not (isinstance(yt, torch.Tensor) and yt.is_cuda and yt.dtype in _MT and yt.is_contiguous()):
+                return False
+            n = yt.numel() if kind == 3 else yp.numel()
+            if (kind == 3 and yp.numel() != n * C) or (kind != 3 and yt.numel() != n):
+                return False
+        else:
+            n = yp.numel()
+        from ..ops._util import hip
+        from .tape import _Deferred
+
+        for t in (yp, yt):  # a deferred prediction (nn/tape.py) is computed before the kernel reads it
+            if isinstance(t, _Deferred) and getattr(t, "_lz", None) is not None:
+                t._lz.materialize()
+        self._ensure(yp.device)
+        hip("ptg_metric_update", kind, yp.data_ptr(), _MT[yp.dtype], yt.data_ptr() if yt is not None else None,
+            _MT[yt.dtype] if yt is not None else 0, n, C, float(n), self._state.data_ptr())
+        return True
 
     def reset_state(self):
-        if self._total is not None:
-            self._total.zero_()
-            self._count.zero_()
+        if self._state is not None:
+            self._state.zero_()
 
     def _add(self, total, count, device):
         self._ensure(device)
@@ -38,7 +64,7 @@ class Metric:
             self._ensure("cpu" if self._strategy is None else self._strategy.device)
         from ..distribute import current_strategy
 
-        t = torch.stack([self._total, self._count])
+        t = self._state.clone()
         st = self._strategy or current_strategy()
         if st is not None:
             t = st.all_reduce_sum(t)
@@ -51,6 +77,8 @@ class Mean(Metric):
         super().__init__(name)
 
     def update_state(self, values, sample_weight=None):
+        if sample_weight is None and self._fused(0, values):
+            return
         v = torch.as_tensor(values)
         self._add(v.double().sum(), float(v.numel()), v.device)
 
@@ -60,6 +88,8 @@ class MeanAbsoluteError(Metric):
         super().__init__(name)
 
     def update_state(self, y_true, y_pred, sample_weight=None):
+        if sample_weight is None and self._fused(1, y_pred, y_true):
+            return
         yp = torch.as_tensor(y_pred)
         yt = torch.as_tensor(y_true, device=yp.device)
         d = (yp.double() - yt.double()).abs()
@@ -71,6 +101,8 @@ class MeanSquaredError(Metric):
         super().__init__(name)
 
     def update_state(self, y_true, y_pred, sample_weight=None):
+        if sample_weight is None and self._fused(2, y_pred, y_true):
+            return
         yp = torch.as_tensor(y_pred)
         yt = torch.as_tensor(y_true, device=yp.device)
         d = yp.double() - yt.double()
@@ -82,6 +114,9 @@ class SparseCategoricalAccuracy(Metric):
         super().__init__(name)
 
     def update_state(self, y_true, y_pred, sample_weight=None):
+        if (sample_weight is None and isinstance(y_pred, torch.Tensor) and y_pred.dim() == 2
+                and self._fused(3, y_pred, y_true, y_pred.shape[-1])):
+            return
         yp = torch.as_tensor(y_pred)
         yt = torch.as_tensor(y_true, device=yp.device)
         c = (yp.argmax(-1) == yt.long().view(-1)).double()

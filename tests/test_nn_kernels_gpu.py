@@ -849,3 +849,36 @@ def test_dense_prelu_dx_model_step_matches(hip_built):
     d = (m1.store.flat - m0.store.flat).norm().item()
     u = (m0.store.flat - init).norm().item()
     assert d <= 0.05 * u, (d, u)
+
+
+@pytest.mark.parametrize("n", [64, 300_000])
+def test_metric_update_kernel_matches_torch(n):
+    """nn/metrics.py one-launch updates (metric_update_k) == the fp64 torch formulas: Mean of a
+    loss scalar / vector, MAE and MSE over fp32 and bf16 predictions, sparse categorical accuracy;
+    n = 300K takes the multi-workgroup atomic form."""
+    from pyspark_tf_gke_amd.nn import metrics as MT
+
+    g = torch.Generator().manual_seed(n)
+    yp = torch.randn(n, 2, generator=g)
+    yt = torch.randn(n, 2, generator=g)
+    logits = torch.randn(n, 15, generator=g)
+    lab = torch.randint(0, 15, (n,), generator=g, dtype=torch.int32)
+    for dt in (torch.float32, torch.bfloat16):
+        p, t = yp.to(dt), yt.to(dt)
+        m1, m2 = MT.MeanAbsoluteError(), MT.MeanSquaredError()
+        for _ in range(2):
+            m1.update_state(t.cuda(), p.cuda())
+            m2.update_state(t.cuda(), p.cuda())
+        d = p.double() - t.double()
+        assert abs(float(m1.result()) - float(d.abs().mean())) <= 1e-5 * max(1.0, float(d.abs().mean()))
+        assert abs(float(m2.result()) - float((d * d).mean())) <= 1e-5 * max(1.0, float((d * d).mean()))
+        assert float(m1._state[1]) == 2 * p.numel()
+    mean = MT.Mean()
+    mean.update_state(torch.tensor(2.5, device="cuda"))
+    mean.update_state(yp[:, 0].cuda())
+    want = (2.5 + float(yp[:, 0].double().sum())) / (n + 1)
+    assert abs(float(mean.result()) - want) <= 1e-5 * max(1.0, abs(want))
+    acc = MT.SparseCategoricalAccuracy()
+    acc.update_state(lab.cuda(), logits.cuda())
+    want = float((logits.argmax(-1) == lab.long()).double().mean())
+    assert abs(float(acc.result()) - want) <= 1e-9
