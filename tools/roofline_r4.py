@@ -59,6 +59,12 @@ def classify(name, ppb_seen):
         if E in (1, 2):
             return {8: "L2 fwd", 16: "L3 fwd", 32: "L4 fwd", 64: "L5 fwd"}.get(C)
         return {16: "L2 dgrad", 32: "L3 dgrad", 64: "L4 dgrad" if NF == 2 else "L5 dgrad"}.get(C)
+    m = re.search(r"conv32_k<(\d+), (\d+), (\d+)", name)
+    if m:
+        C, CO, E = int(m.group(1)), int(m.group(2)), int(m.group(3))
+        if E in (1, 2):
+            return {16: "L3 fwd", 32: "L4 fwd", 64: "L5 fwd"}.get(C)
+        return {(32, 16): "L3 dgrad", (64, 32): "L4 dgrad", (64, 64): "L5 dgrad"}.get((C, CO))
     m = re.search(r"conv_wgrad_strip_k<(\d+),", name)
     if m:
         return {8: "L2 wgrad", 16: "L3 wgrad", 32: "L4 wgrad", 64: "L5 wgrad"}.get(int(m.group(1)))
