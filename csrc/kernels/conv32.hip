@@ -28,6 +28,16 @@
 namespace ptgm32 {
 
 constexpr int NW = 5, NT = NW * 64, PX = 320, KS = 5, PAD = 2;
+// PTG_C32_WLDS=1: the filter taps are staged in LDS once per workgroup, one (kh, kw) slice of
+// [CO][C] at a time (double-buffered, the next slice's global loads in flight while this one
+// computes), instead of every wave fetching its weight fragments from L2 each k-step (5x the L2
+// traffic of the taps: ~1 MB per 320-pixel tile at C = CO = 64).
+#ifndef PTG_C32_WLDS
+#define PTG_C32_WLDS 0
+#endif
+constexpr bool WLDS = PTG_C32_WLDS != 0;
+template <int C, int CO>
+constexpr int wslice_elems() { return CO * (C + 8); }  // one (kh, kw) slice, row pitch C + 8
 enum { EPI_Z = 0, EPI_POOL = 1, EPI_PRELU = 2 };
 
 template <int C, int CO, int EPI>
@@ -69,6 +79,69 @@ __global__ __launch_bounds__(NT) void conv32_k(const bf16_t* __restrict__ x, con
     const int pr = p / W, pc = p - pr * W;
     hbase[b] = (pr * HC + pc) * CP + 8 * h;
   }
+  f32x16_t acc[NCO][2];
+#pragma unroll
+  for (int j = 0; j < NCO; ++j)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[j][b][i] = 0.f;
+  if constexpr (WLDS) {
+    // ---- taps from LDS: slice khw = W[0..CO)[kh][kw][0..C) at lds + halo_elems + (khw & 1) * WSL ----
+    constexpr int WP = C + 8, WSL = wslice_elems<C, CO>(), WV = CO * C / 8;  // 16-byte vectors per slice
+    constexpr int WPT = (WV + NT - 1) / NT;
+    bf16_t* wbuf = lds + HR * HC * CP;
+    U4 wreg[WPT];
+    auto wfetch = [&](int khw) {  // this thread's part of slice khw into registers (zeros past Cout)
+#pragma unroll
+      for (int q = 0; q < WPT; ++q) {
+        const int t = tid + q * NT;
+        U4 v = zero4();
+        if (t < WV) {
+          const int co = t / (C / 8), cv = t - co * (C / 8);
+          if (co < Cout) v = *(const U4*)(w + ((long)co * KS * KS + khw) * C + cv * 8);
+        }
+        wreg[q] = v;
+      }
+    };
+    auto wstore = [&](int khw) {
+      bf16_t* dst = wbuf + (khw & 1) * WSL;
+#pragma unroll
+      for (int q = 0; q < WPT; ++q) {
+        const int t = tid + q * NT;
+        if (t < WV) {
+          const int co = t / (C / 8), cv = t - co * (C / 8);
+          *(U4*)(dst + co * WP + cv * 8) = wreg[q];
+        }
+      }
+    };
+    wfetch(0);
+    wstore(0);
+    __syncthreads();  // halo + slice 0 staged
+    for (int khw = 0; khw < KS * KS; ++khw) {
+      if (khw + 1 < KS * KS) wfetch(khw + 1);  // global loads in flight under this slice's MFMAs
+      const int kh = khw / KS, kw = khw - kh * KS;
+      const bf16_t* ws = wbuf + (khw & 1) * WSL;
+#pragma unroll
+      for (int cb = 0; cb < CB; ++cb) {
+        const int koff = (kh * HC + kw) * CP + cb * 16;
+        bf16x8_t wa[NCO];
+#pragma unroll
+        for (int j = 0; j < NCO; ++j) wa[j] = *(const bf16x8_t*)(ws + (32 * j + r) * WP + cb * 16 + 8 * h);
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const bf16x8_t xb = *(const bf16x8_t*)(lds + hbase[b] + koff);
+#pragma unroll
+          for (int j = 0; j < NCO; ++j)
+            acc[j][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[j], xb, acc[j][b], 0, 0, 0);
+        }
+      }
+      if (khw + 1 < KS * KS) {
+        wstore(khw + 1);  // the other buffer: last read in iteration khw - 1, before the barrier below
+        __syncthreads();
+      }
+    }
+  } else {
   // weight fragments: W[co][kh][kw][C], lane (co = r (+32), k = 8h..8h+7 of the 16-channel block)
   const bf16_t* wl[NCO];
 #pragma unroll
@@ -89,13 +162,6 @@ __global__ __launch_bounds__(NT) void conv32_k(const bf16_t* __restrict__ x, con
   for (int s = 0; s < PF; ++s)
 #pragma unroll
     for (int j = 0; j < NCO; ++j) wq[s][j] = wload(s, j);
-  f32x16_t acc[NCO][2];
-#pragma unroll
-  for (int j = 0; j < NCO; ++j)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) acc[j][b][i] = 0.f;
   __syncthreads();
   // ---- K loop: (kh, kw, 16-channel block) ----
 #pragma unroll PF
@@ -117,6 +183,7 @@ __global__ __launch_bounds__(NT) void conv32_k(const bf16_t* __restrict__ x, con
 #pragma unroll
       for (int j = 0; j < NCO; ++j) acc[j][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[j], xb, acc[j][b], 0, 0, 0);
     }
+  }
   }
   __syncthreads();  // halo reads done: the buffer becomes the epilogue staging tile
   // ---- stage bf16(acc + bias) as [pixel][channel] ----
@@ -198,7 +265,7 @@ static int launch(const void* x, const void* w, const float* bias, const float* 
                   int W, int Cout, hipStream_t s) {
   const int TR = PX / W;
   constexpr int CP = C + 8, SP = CO + 8;
-  const long halo = (long)(TR + KS - 1) * (W + KS - 1) * CP * 2;
+  const long halo = (long)(TR + KS - 1) * (W + KS - 1) * CP * 2 + (WLDS ? 2L * wslice_elems<C, CO>() * 2 : 0L);
   const long stage = (long)PX * SP * 2;
   const long bytes = halo > stage ? halo : stage;
   if (bytes > 160 * 1024) return (int)hipErrorInvalidValue;
