@@ -180,7 +180,8 @@ def conv2d_fwd_fused(x, w, bias, pad: int, z_out, alpha=None, aux_out=None, epi=
         assert tuple(z_out.shape) == (N, H, W, Cout)
     assert Cw == C
     need(x, torch.bfloat16, "conv_halo.x"); need(w, torch.bfloat16, "conv_halo.w")
-    if CONV32 and epi in (None, "pool", "prelu") and KS == 5 and pad == 2 and _conv32_ok(H, W, C, Cout, epi):
+    if (CONV32 and epi in (None, "pool", "prelu") and KS == 5 and pad == 2 and _conv32_ok(H, W, C, Cout, epi)
+            and W > 0 and N * (H // max(1, 320 // W)) >= CONV32_MIN_WG):
         # channel-rich 5x5 layers (and data gradients): the 32x32x16-MFMA implicit GEMM (conv32.hip)
         return conv32(x, w, bias, z_out, alpha, aux_out, epi)
     hip("ptg_conv2d_fwd_halo", ptr(x), ptr(w), ptr(bias), ptr(alpha), ptr(z_out), ptr(aux_out), ptr(arg_out), N, H, W,
@@ -191,6 +192,9 @@ def conv2d_fwd_fused(x, w, bias, pad: int, z_out, alpha=None, aux_out=None, epi=
 EPI32 = {None: 0, "z": 0, "pool": 1, "prelu": 2}
 CONV32 = config.get("conv32")
 CONV32_MINCH = config.get("conv32_min_ch")
+# conv32 runs one workgroup per 320-pixel tile (N * H / (320 / W) of them): below one per CU (CNN-B1
+# layer 5 at batch < 256) the persistent strip kernels fill the GPU better (b32: 91 vs ~12 us)
+CONV32_MIN_WG = config.get("conv32_min_wg")
 _C32_OK: dict = {}
 
 
