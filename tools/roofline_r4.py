@@ -98,6 +98,7 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--step", type=int, default=-2)
+    ap.add_argument("--serial", action="store_true", help="label: the trace is of a serialized run (PTG_SIDE_STREAM=0)")
     a = ap.parse_args()
     rows = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r["Start_Timestamp"]))
     starts = [i for i, r in enumerate(rows) if "conv1_fwd" in r["Kernel_Name"]]
@@ -106,7 +107,8 @@ def main():
     table = ops(a.batch)
     t0 = int(ks[0]["Start_Timestamp"])
     t1 = max(int(r["End_Timestamp"]) for r in ks)
-    print(f"CNN-B1 b{a.batch}: {len(ks)} kernels in one step, first start -> last end {(t1 - t0) / 1e3:.1f} us")
+    print(f"CNN-B1 b{a.batch} ({'serialized, one stream' if a.serial else 'overlapped, two streams'}): {len(ks)} kernels in "
+          f"one step, first start -> last end {(t1 - t0) / 1e3:.1f} us")
     print(f"{'op':40s} {'us':>7s} {'GFLOP':>7s} {'MB':>8s} {'TF/s':>7s} {'TB/s':>6s} {'bound':>7s} {'%roof':>6s} "
           f"{'floor us':>8s}")
     acc = {}
