@@ -76,6 +76,8 @@ _K = [
     Knob("side_cu_quarters", int, 4, "PTG_SIDE_CU_QUARTERS", None,
          "side stream confined to 1-3 quarters of the CUs (4 = all): its wgrad / Dense dW+Adam kernels then "
          "never take CUs from the step's dgrad chain"),
+    Knob("heavy_cu_quarters", int, 4, "PTG_HEAVY_CU_QUARTERS", None,
+         "the Dense dW+Adam GEMM on its own stream confined to 1-3 quarters of the CUs (4 = on the side stream)"),
     Knob("tape_overlap", bool, True, "PTG_TAPE_OVERLAP", None,
          "GradientTape loops: big Dense Adam on an aux stream overlapping the rest of the backward"),
     Knob("tape_fused_head", bool, True, "PTG_TAPE_FUSED_HEAD", None,

@@ -148,7 +148,7 @@ class FusedAdamStep:
         if self.defer:
             self.deferred.append(fn)
         else:
-            S.launch(fn, dz.device)
+            S.launch(fn, dz.device, heavy=True)
         self.done.append((o, o + n))
 
 
