@@ -146,3 +146,38 @@ def test_mlp_fit_dataset_grouped_launches_match_per_batch_engine(hip_built, monk
     assert ia == ib == 39 and not cb and sum(ca) == 39 and max(ca) == 5, (ia, ib, ca)
     assert torch.allclose(fa, fb, rtol=1e-3, atol=1e-5), float((fa - fb).abs().max())
     assert all(abs(a - b) <= 1e-3 * max(1.0, abs(b)) for a, b in zip(la, lb)), (la, lb)
+
+
+@pytest.mark.gpu
+@gpu
+@pytest.mark.parametrize("B", [32, 128])
+def test_mlp_cached_launch_matches_direct_launch(hip_built, B):
+    """MlpStep (bound pointers, device-side Adam step counter) == ptg_mlp_train with the host
+    counter, bit for bit, over 3 cached launches of 2 steps each (the counter advances on the
+    device) and a resync after the host counter moves."""
+    torch.manual_seed(3)
+    m = build_deep_model(3, 15, device="cuda")
+    dims, acts, wo, bo = _plan(m)
+    x, y = _data(B, 2, 15)
+    xd, yd = x.cuda(), y.cuda()
+    flat0 = m.store.flat.clone()
+    outs = []
+    for cached in (True, False):
+        p = flat0.clone()
+        mm, vv = torch.zeros_like(p), torch.zeros_like(p)
+        pbf = torch.zeros_like(p, dtype=torch.bfloat16)
+        st = torch.zeros(8, device="cuda")
+        t = 0
+        ms = K.MlpStep(p, mm, vv, pbf, st, dims, acts, wo, bo, B, 0, 1e-3, 0.9, 0.999, 1e-7, 0) if cached else None
+        for rep in range(4):
+            if rep == 3:
+                t += 5  # the host counter moved (e.g. set_iterations): the device counter resyncs
+            if cached:
+                ms.run(xd, yd, 2, t)
+            else:
+                K.mlp_train(xd, yd, p, mm, vv, pbf, st, dims, acts, wo, bo, 2, 0, 1e-3, 0.9, 0.999, 1e-7, t)
+            t += 2
+        torch.cuda.synchronize()
+        outs.append((p.cpu(), mm.cpu(), vv.cpu(), st.cpu()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
