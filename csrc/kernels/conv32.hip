@@ -31,16 +31,18 @@ constexpr int NW = 5, NT = NW * 64, PX = 320, KS = 5, PAD = 2;
 // PTG_C32_WLDS=1: the filter taps are staged in LDS once per workgroup, one (kh, kw) slice of
 // [CO][C] at a time (double-buffered, the next slice's global loads in flight while this one
 // computes), instead of every wave fetching its weight fragments from L2 each k-step (5x the L2
-// traffic of the taps: ~1 MB per 320-pixel tile at C = CO = 64).
+// traffic of the taps: ~1 MB per 320-pixel tile at C = CO = 64).  On by default since round 4 for
+// the big slices (see launch()): CNN-B1 b256 1.650 -> 1.601 ms per step (profiles/r4_ab_conv32_wlds.txt);
+// =0 for the A/B.
 #ifndef PTG_C32_WLDS
-#define PTG_C32_WLDS 0
+#define PTG_C32_WLDS 1
 #endif
 constexpr bool WLDS = PTG_C32_WLDS != 0;
 template <int C, int CO>
 constexpr int wslice_elems() { return CO * (C + 8); }  // one (kh, kw) slice, row pitch C + 8
 enum { EPI_Z = 0, EPI_POOL = 1, EPI_PRELU = 2 };
 
-template <int C, int CO, int EPI>
+template <int C, int CO, int EPI, bool WL>
 __global__ __launch_bounds__(NT) void conv32_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
                                                const float* __restrict__ bias, const float* __restrict__ alpha,
                                                bf16_t* __restrict__ z, bf16_t* __restrict__ aux, int H, int W,
@@ -86,7 +88,7 @@ __global__ __launch_bounds__(NT) void conv32_k(const bf16_t* __restrict__ x, con
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[j][b][i] = 0.f;
-  if constexpr (WLDS) {
+  if constexpr (WL) {
     // ---- taps from LDS: slice khw = W[0..CO)[kh][kw][0..C) at lds + halo_elems + (khw & 1) * WSL ----
     constexpr int WP = C + 8, WSL = wslice_elems<C, CO>(), WV = CO * C / 8;  // 16-byte vectors per slice
     constexpr int WPT = (WV + NT - 1) / NT;
@@ -260,23 +262,35 @@ __global__ __launch_bounds__(NT) void conv32_k(const bf16_t* __restrict__ x, con
   }
 }
 
+template <int C, int CO, int EPI, bool WL>
+static int launch_k(const void* x, const void* w, const float* bias, const float* alpha, void* z, void* aux, int N,
+                    int H, int W, int Cout, long bytes, hipStream_t s) {
+  const int TR = PX / W;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)conv32_k<C, CO, EPI, WL>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    attr = true;
+  }
+  hipLaunchKernelGGL((conv32_k<C, CO, EPI, WL>), dim3(N * (H / TR)), dim3(NT), (size_t)bytes, s, (const bf16_t*)x,
+                     (const bf16_t*)w, bias, alpha, (bf16_t*)z, (bf16_t*)aux, H, W, TR, Cout);
+  return (int)hipGetLastError();
+}
+
+// The LDS-staged taps pay where a (kh, kw) slice is big (C * CO >= 2048: L4 / L5 of CNN-B1, fwd 69 ->
+// 61 and 40 -> 30 us, dgrad 74 -> 68 and 36 -> 26 us); with smaller slices the L2 fragment loads are
+// cheap and the extra LDS / barriers lost (fwd 64 -> 72, dgrads 92 -> 98 and 175 -> 208 us).
 template <int C, int CO, int EPI>
 static int launch(const void* x, const void* w, const float* bias, const float* alpha, void* z, void* aux, int N, int H,
                   int W, int Cout, hipStream_t s) {
+  constexpr bool wl = WLDS && C * CO >= 2048;
   const int TR = PX / W;
   constexpr int CP = C + 8, SP = CO + 8;
-  const long halo = (long)(TR + KS - 1) * (W + KS - 1) * CP * 2 + (WLDS ? 2L * wslice_elems<C, CO>() * 2 : 0L);
+  const long halo = (long)(TR + KS - 1) * (W + KS - 1) * CP * 2 + (wl ? 2L * wslice_elems<C, CO>() * 2 : 0L);
   const long stage = (long)PX * SP * 2;
   const long bytes = halo > stage ? halo : stage;
   if (bytes > 160 * 1024) return (int)hipErrorInvalidValue;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)conv32_k<C, CO, EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr = true;
-  }
-  hipLaunchKernelGGL((conv32_k<C, CO, EPI>), dim3(N * (H / TR)), dim3(NT), (size_t)bytes, s, (const bf16_t*)x,
-                     (const bf16_t*)w, bias, alpha, (bf16_t*)z, (bf16_t*)aux, H, W, TR, Cout);
-  return (int)hipGetLastError();
+  return launch_k<C, CO, EPI, wl>(x, w, bias, alpha, z, aux, N, H, W, Cout, bytes, s);
 }
 
 template <int C, int EPI>
