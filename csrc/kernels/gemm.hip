@@ -547,6 +547,26 @@ struct LdsImg {
 // PF: how many K-steps ahead the global loads run (register slots; 1 = the next step only).  With one
 // 4-wave workgroup per CU (256-row skinny tiles) one K-step of MFMAs is shorter than an HBM round
 // trip, so those tiles load 2 steps ahead.
+// Work item of a split-K GEMM workgroup.  kchunk > 0: tile = XCD-remapped blockIdx.x (tiles sharing
+// a panel share an L2), split = blockIdx.y.  kchunk < 0 (split-major, the host's choice when there
+// are >= 8 splits): every XCD takes whole K-splits - all tiles of a split run on one XCD, so both
+// operands' K-range panels of that split are fetched into its L2 once and shared by every tile
+// (the Dense forward, M = 256, N = 2048, 16 splits: the tile mapping fetched each weight panel on two
+// XCDs and each activation panel on all eight).  Workgroups go to XCDs round-robin by linear id.
+PTG_DEV void split_xcd_map(int& t, int& split, int& kchunk) {
+  if (kchunk > 0) {
+    t = xcd_remap(blockIdx.x, gridDim.x);
+    split = blockIdx.y;
+    return;
+  }
+  kchunk = -kchunk;
+  const int tiles = gridDim.x, total = tiles * gridDim.y;
+  const int lin = blockIdx.y * tiles + blockIdx.x;
+  const int item = (lin % 8) * (total / 8) + lin / 8;  // host guarantees total % 8 == 0
+  split = item / tiles;
+  t = item - split * tiles;
+}
+
 template <int BM, int BN, int WM, int WN, class LA, class LB, class EPI, int PF = 1>
 __global__ __launch_bounds__(256) void gemm_kernel(LA la, LB lb, EPI epi, int M, int N, int K,
                                                    int kchunk) {
@@ -564,10 +584,11 @@ __global__ __launch_bounds__(256) void gemm_kernel(LA la, LB lb, EPI epi, int M,
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
   const int tiles_n = (N + BN - 1) / BN;
-  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  int t, split;
+  split_xcd_map(t, split, kchunk);
   const int tm = t / tiles_n, tn = t - tm * tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int kb = blockIdx.y * kchunk;
+  const int kb = split * kchunk;
   const int ke = min(K, kb + kchunk);
   if (kb >= ke) return;
   const int nk = (ke - kb + BK - 1) / BK;
@@ -1038,6 +1059,16 @@ static bool gemm256_enabled() {
   return g_gemm256 == 1;
 }
 
+// PTG_GEMM_SPLIT_XCD=1: split-major XCD mapping for split-K launches (split_xcd_map)
+static int g_split_xcd = -1;
+static bool split_xcd_on() {
+  if (g_split_xcd < 0) {
+    const char* e = getenv("PTG_GEMM_SPLIT_XCD");
+    g_split_xcd = e && e[0] == '1';
+  }
+  return g_split_xcd == 1;
+}
+
 template <int BM, int BN, int WM, int WN, class LA, class LB, class EPI, int PF = 1>
 static int launch_gemm(const LA& la, const LB& lb, const EPI& epi, int M, int N, int K, int splits,
                        hipStream_t s) {
@@ -1047,6 +1078,7 @@ static int launch_gemm(const LA& la, const LB& lb, const EPI& epi, int M, int N,
   if (kchunk < BK) kchunk = BK;
   splits = ptg_ceil_div(K, kchunk);
   dim3 grid(tiles, splits);
+  if (split_xcd_on() && splits >= 8 && ((long)tiles * splits) % 8 == 0) kchunk = -kchunk;  // split-major
   hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, LA, LB, EPI, PF>), grid, dim3(256), 0, s, la, lb, epi, M,
                      N, K, kchunk);
   PTG_RETURN_LAUNCH();
@@ -1123,6 +1155,12 @@ static bool is_pow2(int v) { return v > 0 && (v & (v - 1)) == 0; }
 using namespace ptg;
 
 extern "C" {
+
+// PTG_GEMM_SPLIT_XCD at run time (tests / A/B): 1 split-major split-K mapping, 0 the tile mapping
+int ptg_gemm_set_split_xcd(int on) {
+  ptg::g_split_xcd = on ? 1 : 0;
+  return 0;
+}
 
 int ptg_gemm256_set(int on) {
   g_gemm256 = on ? 1 : 0;

@@ -685,6 +685,29 @@ def test_gemm256_lds_dma(M, N, KD, epi):
     _close(outs[0], outs[1], 1e-2, 1e-2, "256 vs 128 kernel")
 
 
+@pytest.mark.parametrize("M,N,KD,splits", [(256, 2048, 20480, 16), (200, 1000, 9000, 8), (64, 640, 4096, 12)])
+def test_gemm_split_major_xcd_mapping(M, N, KD, splits):
+    """Split-K GEMM (fp32 atomic epilogue) with the split-major XCD mapping (ptg_gemm_set_split_xcd)
+    == the tile mapping and the fp32 reference: every (tile, split) item is covered exactly once,
+    including grids whose tile count is not a multiple of 8 (then the tile mapping is kept)."""
+    from pyspark_tf_gke_amd import _native
+
+    a, b = rnd(M, KD), rnd(N, KD)
+    ref = a.float() @ b.float().t()
+    outs = []
+    try:
+        for on in (1, 0):
+            _native.hip_lib().ptg_gemm_set_split_xcd(on)
+            c = torch.zeros(M, N, device=DEV, dtype=torch.float32)
+            K.gemm(M, N, KD, a.to(DEV), KD, 1, b.to(DEV), KD, 1, 3, c, N, None, 0, splits)
+            torch.cuda.synchronize()
+            _close(c, ref, 1e-3, 1e-3, f"split-K on={on}")
+            outs.append(c.cpu())
+    finally:
+        _native.hip_lib().ptg_gemm_set_split_xcd(0)
+    _close(outs[0], outs[1], 1e-4, 1e-4, "split-major vs tile mapping")
+
+
 def test_conv_fwd_gemm256_resnet_layer():
     """A ResNet-50 stage-1 3x3 conv at batch 32 (M = 100352 output pixels, 392 tiles) through the
     LDS-DMA kernel's im2col loader vs the fp32 reference."""
