@@ -41,7 +41,7 @@ struct MlpDesc {
   int la[MAXL + 1], as[MAXL + 1];  // LDS offset / row stride (odd) of activation l
   int lg0, lg1, gs;             // the two gradient buffers (row stride gs, odd) and red scratch
   int lred;
-  int res;                      // 1: Adam m / v resident in LDS for the whole launch (written back at the end)
+  int res;                      // 1 (PTG_MLP_RESIDENT=1): Adam m / v resident in LDS for the launch, written back at the end
   int lm, R;                    // LDS offset of the resident m (v follows R floats later), R = parameter count
   int rw[MAXL], rb[MAXL];       // offset of layer l's weight / bias moments inside the resident block
   int lg;                       // lanes per row of the softmax loss (16 / 32 / 64; 0: one thread per row)
@@ -533,7 +533,9 @@ static long mlp_plan(const long* hdesc, int L, int B, ptgm::MlpDesc* D) {
   }
   D->R = R;
   const char* e = getenv("PTG_MLP_RESIDENT");
-  const bool res_ok = !wide && !(e && e[0] == '0');
+  // opt-in: measured 35.3 vs 32.2 us per single-step launch and 26.5 vs 26.7 us per step in 8-step
+  // launches (the per-layer moment loads were already hidden behind the dW GEMMs)
+  const bool res_ok = !wide && e && e[0] == '1';
   const long cap = 160 * 1024 / 4;
   // LDS priority: resident moments (no HBM access inside a step), then the second weight copy
   D->res = res_ok && off + 2L * R <= cap;
