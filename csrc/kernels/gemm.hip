@@ -1059,12 +1059,14 @@ static bool gemm256_enabled() {
   return g_gemm256 == 1;
 }
 
-// PTG_GEMM_SPLIT_XCD=1: split-major XCD mapping for split-K launches (split_xcd_map)
+// split-major XCD mapping for split-K launches with >= 8 splits (split_xcd_map); PTG_GEMM_SPLIT_XCD=0
+// keeps the tile mapping.  Measured: ResNet-50 b128 8.83k -> 8.88k img/s, CNN-B1 b256 within noise
+// (profiles/r4_ab_gemm_split_xcd.txt)
 static int g_split_xcd = -1;
 static bool split_xcd_on() {
   if (g_split_xcd < 0) {
     const char* e = getenv("PTG_GEMM_SPLIT_XCD");
-    g_split_xcd = e && e[0] == '1';
+    g_split_xcd = !(e && e[0] == '0');
   }
   return g_split_xcd == 1;
 }

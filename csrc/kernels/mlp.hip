@@ -41,9 +41,6 @@ struct MlpDesc {
   int la[MAXL + 1], as[MAXL + 1];  // LDS offset / row stride (odd) of activation l
   int lg0, lg1, gs;             // the two gradient buffers (row stride gs, odd) and red scratch
   int lred;
-  int res;                      // 1 (PTG_MLP_RESIDENT=1): Adam m / v resident in LDS for the launch, written back at the end
-  int lm, R;                    // LDS offset of the resident m (v follows R floats later), R = parameter count
-  int rw[MAXL], rb[MAXL];       // offset of layer l's weight / bias moments inside the resident block
   int lg;                       // lanes per row of the softmax loss (16 / 32 / 64; 0: one thread per row)
   float lr, b1, b2, eps;
   int t0;                       // optimizer steps taken before this launch
@@ -123,17 +120,10 @@ struct AdamArgs {
   float lr_t, b1, b2, eps;
 };
 
-PTG_DEV float adam_math(const AdamArgs& o, float g, float p0, float& m0, float& v0) {
+PTG_DEV float adam_update(const AdamArgs& o, long idx, float g, float p0, float m0, float v0) {
   const float mm = o.b1 * m0 + (1.f - o.b1) * g;
   const float vv = o.b2 * v0 + (1.f - o.b2) * g * g;
-  m0 = mm;
-  v0 = vv;
-  return p0 - o.lr_t * mm / (sqrtf(vv) + o.eps);
-}
-
-PTG_DEV float adam_update(const AdamArgs& o, long idx, float g, float p0, float m0, float v0) {
-  float mm = m0, vv = v0;
-  const float pp = adam_math(o, g, p0, mm, vv);
+  const float pp = p0 - o.lr_t * mm / (sqrtf(vv) + o.eps);
   o.m[idx] = mm;
   o.v[idx] = vv;
   o.p[idx] = pp;
@@ -141,20 +131,12 @@ PTG_DEV float adam_update(const AdamArgs& o, long idx, float g, float p0, float 
   return pp;
 }
 
-// LDS-resident optimizer state (MlpDesc::res): the current weights are the LDS copy being read, m / v
-// live in LDS for the whole launch, so a step's Adam epilogues touch no HBM at all
-struct ResState {
-  const float* Wc;  // current LDS weights of the layer (row stride S)
-  float* lm;        // m of the layer's weights ([M][N], dense); v at lm + R
-  int R;
-};
-
 // dW[i][j] = sum_k P[i*pi + k*pk] Q[j*qj + k*qk] (i < M output units, j < N inputs) with Adam on
 // element wo + i*N + j: the thread's p / m / v are loaded BEFORE its GEMM loop, so the HBM latency
 // hides under the FMAs instead of following each output; the updated weight also goes to LDS W.
-template <int TM, int TN, bool RES>
+template <int TM, int TN>
 PTG_DEV void dw_adam_tile(int M, int N, int K, const float* P, int pi, int pk, const float* Q, int qj, int qk,
-                          const AdamArgs& o, long wo, float* Wl, int S, const ResState& rs) {
+                          const AdamArgs& o, long wo, float* Wl, int S) {
   const int tm = (M + TM - 1) / TM, tn = (N + TN - 1) / TN;
   for (int t = threadIdx.x; t < tm * tn; t += NT) {
     const int i0 = (t / tn) * TM, j0 = (t - (t / tn) * tn) * TN;
@@ -163,17 +145,10 @@ PTG_DEV void dw_adam_tile(int M, int N, int K, const float* P, int pi, int pk, c
     for (int a = 0; a < TM; ++a)
 #pragma unroll
       for (int b = 0; b < TN; ++b) {
-        const int ci = min(i0 + a, M - 1), cj = min(j0 + b, N - 1);
-        if (RES) {
-          p0[a][b] = rs.Wc[ci * S + cj];
-          m0[a][b] = rs.lm[ci * N + cj];
-          v0[a][b] = rs.lm[rs.R + ci * N + cj];
-        } else {
-          const long idx = wo + (long)ci * N + cj;
-          p0[a][b] = o.p[idx];
-          m0[a][b] = o.m[idx];
-          v0[a][b] = o.v[idx];
-        }
+        const long idx = wo + (long)min(i0 + a, M - 1) * N + min(j0 + b, N - 1);
+        p0[a][b] = o.p[idx];
+        m0[a][b] = o.m[idx];
+        v0[a][b] = o.v[idx];
       }
     const float* pr[TM];
     const float* qr[TN];
@@ -204,27 +179,19 @@ PTG_DEV void dw_adam_tile(int M, int N, int K, const float* P, int pi, int pk, c
       for (int b = 0; b < TN; ++b)
         if (i0 + a < M && j0 + b < N) {
           const int i = i0 + a, j = j0 + b;
-          if (RES) {
-            float mm = m0[a][b], vv = v0[a][b];
-            Wl[i * S + j] = adam_math(o, acc[a][b], p0[a][b], mm, vv);
-            rs.lm[i * N + j] = mm;
-            rs.lm[rs.R + i * N + j] = vv;
-          } else {
-            Wl[i * S + j] = adam_update(o, wo + (long)i * N + j, acc[a][b], p0[a][b], m0[a][b], v0[a][b]);
-          }
+          Wl[i * S + j] = adam_update(o, wo + (long)i * N + j, acc[a][b], p0[a][b], m0[a][b], v0[a][b]);
         }
   }
 }
 
-template <bool RES>
 PTG_DEV void dw_adam(int M, int N, int K, const float* P, int pi, int pk, const float* Q, int qj, int qk,
-                     const AdamArgs& o, long wo, float* Wl, int S, const ResState& rs) {
+                     const AdamArgs& o, long wo, float* Wl, int S) {
   const int outs = M * N;
-  if (outs >= 16 * NT) dw_adam_tile<4, 4, RES>(M, N, K, P, pi, pk, Q, qj, qk, o, wo, Wl, S, rs);
-  else if (outs >= 8 * NT) dw_adam_tile<2, 4, RES>(M, N, K, P, pi, pk, Q, qj, qk, o, wo, Wl, S, rs);
-  else if (outs >= 4 * NT) dw_adam_tile<2, 2, RES>(M, N, K, P, pi, pk, Q, qj, qk, o, wo, Wl, S, rs);
-  else if (outs >= 2 * NT) dw_adam_tile<1, 2, RES>(M, N, K, P, pi, pk, Q, qj, qk, o, wo, Wl, S, rs);
-  else dw_adam_tile<1, 1, RES>(M, N, K, P, pi, pk, Q, qj, qk, o, wo, Wl, S, rs);
+  if (outs >= 16 * NT) dw_adam_tile<4, 4>(M, N, K, P, pi, pk, Q, qj, qk, o, wo, Wl, S);
+  else if (outs >= 8 * NT) dw_adam_tile<2, 4>(M, N, K, P, pi, pk, Q, qj, qk, o, wo, Wl, S);
+  else if (outs >= 4 * NT) dw_adam_tile<2, 2>(M, N, K, P, pi, pk, Q, qj, qk, o, wo, Wl, S);
+  else if (outs >= 2 * NT) dw_adam_tile<1, 2>(M, N, K, P, pi, pk, Q, qj, qk, o, wo, Wl, S);
+  else dw_adam_tile<1, 1>(M, N, K, P, pi, pk, Q, qj, qk, o, wo, Wl, S);
 }
 
 // max / first-argmax / sum over the `g` lanes of a row group (g = 16 / 32 / 64, aligned in the wave)
@@ -248,55 +215,27 @@ __global__ __launch_bounds__(NT) void mlp_train_k(const float* __restrict__ x, c
   extern __shared__ __align__(16) float sm[];
   const int tid = threadIdx.x;
   const int L = D.L, B = D.B;
-  const int C = D.d[L];
-  const int K0 = D.d[0];
-  // the batch of a step is loaded into registers one step ahead (first slot of every thread; larger
-  // batches read the rest directly), the labels / targets in the loss phase's own layout
-  const int lrow = D.lg ? tid / D.lg : tid;  // the row whose label this thread uses in the loss
-  auto fetch = [&](int st, float& xv, int& lv, float& tv) {
-    const int bk = B * K0;
-    xv = tid < bk ? x[(long)st * bk + tid] : 0.f;
-    if (D.loss == 0) lv = lrow < B ? ((const int*)y)[(long)st * B + lrow] : 0;
-    else tv = tid < B * C ? ((const float*)y)[(long)st * B * C + tid] : 0.f;
-  };
-  float xv = 0.f, tv = 0.f;
-  int lv = 0;
-  fetch(0, xv, lv, tv);
   const int t0 = tstep ? (int)tstep[0] : D.t0;
-  // weights + biases -> LDS (the Adam epilogues keep them current in place), and with D.res the
-  // Adam moments too
+  // weights + biases -> LDS (the Adam epilogues keep them current in place)
   for (int l = 0; l < L; ++l) {
     const int K = D.d[l], N = D.d[l + 1], S = D.ws[l];
-    for (int i = tid; i < N * K; i += NT) {
-      sm[D.lw[l] + (i / K) * S + i % K] = p[D.woff[l] + i];
-      if (D.res) {
-        sm[D.lm + D.rw[l] + i] = m[D.woff[l] + i];
-        sm[D.lm + D.R + D.rw[l] + i] = v[D.woff[l] + i];
-      }
-    }
+    for (int i = tid; i < N * K; i += NT) sm[D.lw[l] + (i / K) * S + i % K] = p[D.woff[l] + i];
     for (int n = tid; n < N; n += NT) {
       sm[D.lb[l] + n] = D.boff[l] >= 0 ? p[D.boff[l] + n] : 0.f;
       if (D.dbl && D.boff[l] < 0) sm[D.wtot + D.lb[l] + n] = 0.f;  // bias-less: zeros in both copies
-      if (D.res && D.boff[l] >= 0) {
-        sm[D.lm + D.rb[l] + n] = m[D.boff[l] + n];
-        sm[D.lm + D.R + D.rb[l] + n] = v[D.boff[l] + n];
-      }
     }
   }
   float s_loss = 0.f, s_a = 0.f, s_b = 0.f;
+  const int C = D.d[L];
   // with two weight copies a step reads one and its Adam epilogues write the other, so a layer's dX
   // and its weight update share one phase; otherwise the update is in place after a barrier
   int wcur = 0;
   for (int st = 0; st < D.steps; ++st) {
     const int wnxt = D.dbl ? D.wtot - wcur : wcur;
     // ---- input batch
-    const int bk = B * K0;
-    const float* xs = x + (long)st * bk;
-    if (tid < bk) sm[D.la[0] + (tid / K0) * D.as[0] + tid % K0] = xv;
-    for (int i = tid + NT; i < bk; i += NT) sm[D.la[0] + (i / K0) * D.as[0] + i % K0] = xs[i];
-    const int lab_t = lv;
-    const float tg_t = tv;
-    if (st + 1 < D.steps) fetch(st + 1, xv, lv, tv);  // lands while this step computes
+    const int K0 = D.d[0];
+    const float* xs = x + (long)st * B * K0;
+    for (int i = tid; i < B * K0; i += NT) sm[D.la[0] + (i / K0) * D.as[0] + i % K0] = xs[i];
     __syncthreads();
     // ---- forward: O[r][n] = act(b[n] + A[r] . W[n])
     for (int l = 0; l < L; ++l) {
@@ -322,6 +261,7 @@ __global__ __launch_bounds__(NT) void mlp_train_k(const float* __restrict__ x, c
       for (int r0 = 0; r0 < B; r0 += rpp) {  // uniform trip count: every lane joins the shuffles
         const int r = r0 + tid / g;
         const bool ok = r < B;
+        const int t = ok ? lab[r] : 0;  // (issued first: its latency hides under the reductions)
         const float* z = Z + (ok ? r : 0) * SZ;
         const float zc = c < C ? z[c] : -__builtin_inff();
         float mx = zc;
@@ -329,7 +269,6 @@ __global__ __launch_bounds__(NT) void mlp_train_k(const float* __restrict__ x, c
         group_max_arg(mx, am, g);
         const float e = c < C ? __expf(zc - mx) : 0.f;
         const float inv = 1.f / group_sum(e, g);
-        const int t = r0 == 0 ? lab_t : (ok ? lab[r] : 0);
         if (ok && c < C) {
           G[r * D.gs + c] = (e * inv - (c == t ? 1.f : 0.f)) * scale;
           if (c == t) {
@@ -350,7 +289,7 @@ __global__ __launch_bounds__(NT) void mlp_train_k(const float* __restrict__ x, c
         float s = 0.f;
         for (int c = 0; c < C; ++c) s += __expf(z[c] - mx);
         const float inv = 1.f / s;
-        const int t = r == tid ? lab_t : lab[r];
+        const int t = lab[r];
         for (int c = 0; c < C; ++c) G[r * D.gs + c] = (__expf(z[c] - mx) * inv - (c == t ? 1.f : 0.f)) * scale;
         const float pl = fminf(fmaxf(__expf(z[t] - mx) * inv, 1e-7f), 1.f - 1e-7f);
         s_loss += -__logf(pl);
@@ -361,7 +300,7 @@ __global__ __launch_bounds__(NT) void mlp_train_k(const float* __restrict__ x, c
       const float inv = 1.f / (float)(B * C);
       for (int i = tid; i < B * C; i += NT) {
         const int r = i / C, c = i - r * C;
-        const float d = Z[r * SZ + c] - (i == tid ? tg_t : tg[i]);
+        const float d = Z[r * SZ + c] - tg[i];
         G[r * D.gs + c] = 2.f * d * inv;
         s_loss += d * d * inv * (float)B;
         s_a += fabsf(d);
@@ -370,8 +309,7 @@ __global__ __launch_bounds__(NT) void mlp_train_k(const float* __restrict__ x, c
     }
     __syncthreads();
     // ---- backward, per layer: dX for the layer below from the pre-update LDS weights, a barrier,
-    // then each weight gradient with its Adam update (into HBM, or the LDS-resident state) and into
-    // the LDS weights
+    // then each weight gradient with its Adam update into HBM and into the LDS weights in place
     const float t = (float)(t0 + st + 1);
     const float lr_t = D.lr * sqrtf(1.f - powf(D.b2, t)) / (1.f - powf(D.b1, t));
     const AdamArgs ad{p, m, v, pbf, lr_t, D.b1, D.b2, D.eps};
@@ -394,27 +332,13 @@ __global__ __launch_bounds__(NT) void mlp_train_k(const float* __restrict__ x, c
       // bias gradients of this layer: their p / m / v loads are issued first (consumed after the dW GEMM)
       const bool hasb = D.boff[l] >= 0;
       const int bn0 = tid, bn1 = tid + NT;
-      const float* bcur = sm + wcur + D.lb[l];
-      float* bmr = sm + D.lm + D.rb[l];
       float bp[2] = {0.f, 0.f}, bm[2] = {0.f, 0.f}, bvv[2] = {0.f, 0.f};
       if (hasb) {
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const int n = u ? bn1 : bn0;
-          if (n < N) {
-            if (D.res) { bp[u] = bcur[n]; bm[u] = bmr[n]; bvv[u] = bmr[D.R + n]; }
-            else { const long q = D.boff[l] + n; bp[u] = p[q]; bm[u] = m[q]; bvv[u] = v[q]; }
-          }
-        }
+        if (bn0 < N) { const long q = D.boff[l] + bn0; bp[0] = p[q]; bm[0] = m[q]; bvv[0] = v[q]; }
+        if (bn1 < N) { const long q = D.boff[l] + bn1; bp[1] = p[q]; bm[1] = m[q]; bvv[1] = v[q]; }
       }
       // dW[n][k] = sum_r G[r][n] A[r][k], Adam straight from the register
-      if (D.res) {
-        const ResState rs{sm + wcur + D.lw[l], sm + D.lm + D.rw[l], D.R};
-        dw_adam<true>(N, K, B, Gc, 1, D.gs, A, 1, SA, ad, D.woff[l], sm + wnxt + D.lw[l], S, rs);
-      } else {
-        const ResState rs{nullptr, nullptr, 0};
-        dw_adam<false>(N, K, B, Gc, 1, D.gs, A, 1, SA, ad, D.woff[l], sm + wnxt + D.lw[l], S, rs);
-      }
+      dw_adam(N, K, B, Gc, 1, D.gs, A, 1, SA, ad, D.woff[l], sm + wnxt + D.lw[l], S);
       if (hasb) {
         float* bnl = sm + wnxt + D.lb[l];
 #pragma unroll
@@ -423,17 +347,10 @@ __global__ __launch_bounds__(NT) void mlp_train_k(const float* __restrict__ x, c
           if (n < N) {
             float g = 0.f;
             for (int r = 0; r < B; ++r) g += Gc[r * D.gs + n];
-            if (D.res) {
-              float mm = bm[u], vv = bvv[u];
-              bnl[n] = adam_math(ad, g, bp[u], mm, vv);
-              bmr[n] = mm;
-              bmr[D.R + n] = vv;
-            } else {
-              bnl[n] = adam_update(ad, D.boff[l] + n, g, bp[u], bm[u], bvv[u]);
-            }
+            bnl[n] = adam_update(ad, D.boff[l] + n, g, bp[u], bm[u], bvv[u]);
           }
         }
-        for (int n = tid + 2 * NT; n < N; n += NT) {  // (layers wider than 2 x NT units; never with D.res)
+        for (int n = tid + 2 * NT; n < N; n += NT) {  // (layers wider than 2 x NT units)
           float g = 0.f;
           for (int r = 0; r < B; ++r) g += Gc[r * D.gs + n];
           const long q = D.boff[l] + n;
@@ -444,30 +361,6 @@ __global__ __launch_bounds__(NT) void mlp_train_k(const float* __restrict__ x, c
       const int tmp = cur; cur = nxt; nxt = tmp;
     }
     wcur = wnxt;  // (the next step's input barrier orders the new copy before any forward read)
-  }
-  if (D.res) {
-    // write the launch's final weights (master + bf16 copy) and moments back, coalesced
-    for (int l = 0; l < L; ++l) {
-      const int K = D.d[l], N = D.d[l + 1], S = D.ws[l];
-      for (int i = tid; i < N * K; i += NT) {
-        const float w = sm[wcur + D.lw[l] + (i / K) * S + i % K];
-        const long q = D.woff[l] + i;
-        p[q] = w;
-        if (pbf) pbf[q] = f2bf(w);
-        m[q] = sm[D.lm + D.rw[l] + i];
-        v[q] = sm[D.lm + D.R + D.rw[l] + i];
-      }
-      if (D.boff[l] >= 0) {
-        for (int n = tid; n < N; n += NT) {
-          const float w = sm[wcur + D.lb[l] + n];
-          const long q = D.boff[l] + n;
-          p[q] = w;
-          if (pbf) pbf[q] = f2bf(w);
-          m[q] = sm[D.lm + D.rb[l] + n];
-          v[q] = sm[D.lm + D.R + D.rb[l] + n];
-        }
-      }
-    }
   }
   float* red = sm + D.lred;
   const float tl = sum_block(s_loss, red);
@@ -523,28 +416,10 @@ static long mlp_plan(const long* hdesc, int L, int B, ptgm::MlpDesc* D) {
   D->lg1 = off; off += B * D->gs;
   D->lred = off; off += 16;
   D->wtot = D->la[0];
-  // resident Adam moments: every layer's weights (dense [N][K]) then biases, m then v
-  int R = 0;
-  bool wide = false;
-  for (int l = 0; l < L; ++l) {
-    D->rw[l] = R; R += D->d[l + 1] * D->d[l];
-    D->rb[l] = R; R += D->d[l + 1];
-    wide |= D->d[l + 1] > 2 * ptgm::NT;
-  }
-  D->R = R;
-  const char* e = getenv("PTG_MLP_RESIDENT");
-  // opt-in: measured 35.3 vs 32.2 us per single-step launch and 26.5 vs 26.7 us per step in 8-step
-  // launches (the per-layer moment loads were already hidden behind the dW GEMMs)
-  const bool res_ok = !wide && e && e[0] == '1';
-  const long cap = 160 * 1024 / 4;
-  // LDS priority: resident moments (no HBM access inside a step), then the second weight copy
-  D->res = res_ok && off + 2L * R <= cap;
-  D->dbl = off + 2L * R * D->res + D->wtot <= cap;
-  D->lm = off;  // (used only with res)
-  if (D->res) off += 2 * R;
+  D->dbl = (long)(off + D->wtot) * 4 <= 160 * 1024;
   if (D->dbl) {  // the second weight copy goes right after the first: shift everything behind it
     for (int l = 0; l <= L; ++l) D->la[l] += D->wtot;
-    D->lg0 += D->wtot; D->lg1 += D->wtot; D->lred += D->wtot; D->lm += D->wtot;
+    D->lg0 += D->wtot; D->lg1 += D->wtot; D->lred += D->wtot;
     off += D->wtot;
   }
   // softmax loss with one row per lane group (PTG_MLP_LOSS_LANES=0: one thread per row)

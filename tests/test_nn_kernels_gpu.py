@@ -704,7 +704,7 @@ def test_gemm_split_major_xcd_mapping(M, N, KD, splits):
             _close(c, ref, 1e-3, 1e-3, f"split-K on={on}")
             outs.append(c.cpu())
     finally:
-        _native.hip_lib().ptg_gemm_set_split_xcd(0)
+        _native.hip_lib().ptg_gemm_set_split_xcd(1)  # the default
     _close(outs[0], outs[1], 1e-4, 1e-4, "split-major vs tile mapping")
 
 
