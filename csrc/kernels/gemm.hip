@@ -24,6 +24,10 @@
 //     blockIdx.y indexes split-K slices (fp32 atomic epilogue).
 #include "common.h"
 
+#ifndef PTG_ADAM_NT
+#define PTG_ADAM_NT 0
+#endif
+
 #include <cstdlib>
 #include <type_traits>
 #include <utility>
@@ -413,12 +417,33 @@ struct EpiAdam {
     p[i] = pp; mo[i] = mm; ve[i] = vv;
     pbf[i] = f2bf(pp);
   }
+#if PTG_ADAM_NT
+  // streaming hints: the 1.1 GB of CNN-B1's Dense state is touched once per step (A/B build)
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+  PTG_DEV static float4 ld4(const float* a) {
+    const f4v v = __builtin_nontemporal_load((const f4v*)a);
+    return make_float4(v.x, v.y, v.z, v.w);
+  }
+  PTG_DEV static void st4(float* a, float4 v) {
+    const f4v w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, (f4v*)a);
+  }
+  PTG_DEV static void st16(bf16_t* a, U4 v) {
+    const u4v w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, (u4v*)a);
+  }
+#else
+  PTG_DEV static float4 ld4(const float* a) { return *(const float4*)a; }
+  PTG_DEV static void st4(float* a, float4 v) { *(float4*)a = v; }
+  PTG_DEV static void st16(bf16_t* a, U4 v) { *(U4*)a = v; }
+#endif
   PTG_DEV void preload(int m, int n, int cnt, Pre& r) const {
     const long i = (long)m * ldc + n;
     if (!fast(i, cnt)) return;
-    r.P[0] = *(const float4*)(p + i); r.P[1] = *(const float4*)(p + i + 4);
-    r.Mm[0] = *(const float4*)(mo + i); r.Mm[1] = *(const float4*)(mo + i + 4);
-    r.V[0] = *(const float4*)(ve + i); r.V[1] = *(const float4*)(ve + i + 4);
+    r.P[0] = ld4(p + i); r.P[1] = ld4(p + i + 4);
+    r.Mm[0] = ld4(mo + i); r.Mm[1] = ld4(mo + i + 4);
+    r.V[0] = ld4(ve + i); r.V[1] = ld4(ve + i + 4);
   }
   PTG_DEV void vec8_pre(int m, int n, float* v, int cnt, Pre& r) const {
     const long i = (long)m * ldc + n;
@@ -434,10 +459,10 @@ struct EpiAdam {
 #pragma unroll
       for (int j = 0; j < 4; ++j) { upd(pp[j], mm[j], vv[j], v[4 * h + j], l); o[4 * h + j] = pp[j]; }
     }
-    *(float4*)(p + i) = r.P[0]; *(float4*)(p + i + 4) = r.P[1];
-    *(float4*)(mo + i) = r.Mm[0]; *(float4*)(mo + i + 4) = r.Mm[1];
-    *(float4*)(ve + i) = r.V[0]; *(float4*)(ve + i + 4) = r.V[1];
-    *(U4*)(pbf + i) = pack8(o);
+    st4(p + i, r.P[0]); st4(p + i + 4, r.P[1]);
+    st4(mo + i, r.Mm[0]); st4(mo + i + 4, r.Mm[1]);
+    st4(ve + i, r.V[0]); st4(ve + i + 4, r.V[1]);
+    st16(pbf + i, pack8(o));
   }
   PTG_DEV void vec8(int m, int n, float* v, int cnt) const {
     Pre r;
