@@ -24,8 +24,10 @@
 //     blockIdx.y indexes split-K slices (fp32 atomic epilogue).
 #include "common.h"
 
+// nontemporal loads/stores of the fused Adam epilogue (on: CNN-B1 b256 1.608 -> 1.600 ms,
+// profiles/r4_ab_adam_nt.txt); -DPTG_ADAM_NT=0 for the A/B
 #ifndef PTG_ADAM_NT
-#define PTG_ADAM_NT 0
+#define PTG_ADAM_NT 1
 #endif
 
 #include <cstdlib>
@@ -418,7 +420,7 @@ struct EpiAdam {
     pbf[i] = f2bf(pp);
   }
 #if PTG_ADAM_NT
-  // streaming hints: the 1.1 GB of CNN-B1's Dense state is touched once per step (A/B build)
+  // streaming hints: the 1.1 GB of CNN-B1's Dense state is touched once per step
   typedef float f4v __attribute__((ext_vector_type(4)));
   typedef uint32_t u4v __attribute__((ext_vector_type(4)));
   PTG_DEV static float4 ld4(const float* a) {
