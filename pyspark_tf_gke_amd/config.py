@@ -111,6 +111,8 @@ _K = [
     Knob("blaslt_dense_fwd", bool, False, "PTG_BLASLT_DENSE_FWD", None,
          "A/B: the big Dense forward that feeds the fused regression head through hipBLASLt (bf16 in, fp32 out) "
          "instead of the split-K atomic MFMA GEMM"),
+    Knob("dense_fwd_splits", int, 0, "PTG_DENSE_FWD_SPLITS", None,
+         "K-splits of the big Dense forward's atomic MFMA GEMM (0: the default rule, <= 16 and ~512 workgroups)"),
     Knob("blaslt_dx", bool, True, "PTG_BLASLT_DX", None,
          "big-Dense dX (a plain GEMM) through hipBLASLt instead of the skinny-M MFMA GEMM "
          "(CNN-B1 b256 A/B: 1.642/1.629 vs 1.657/1.650 ms)"),

@@ -468,6 +468,8 @@ class DenseOp(Op):
                 BLASLT_DENSE_FWD[0] = False
         tiles = -(-B // 128) * -(-N // 128)
         splits = 1 if Kd < 4096 else max(1, min(16, 512 // max(tiles, 1), Kd // 1024))
+        if DENSE_FWD_SPLITS > 0:
+            splits = min(int(DENSE_FWD_SPLITS), max(1, Kd // 64))
         K.gemm(B, N, Kd, x, Kd, 1, self.dense.kernel.bf16, Kd, 1, 3, acc, N, None, 0, splits)
         self._x = x
         return acc
@@ -559,6 +561,7 @@ class DenseOp(Op):
 # CNN-B1 Dense forward before the fused head (split-K sums in fp32): hipBLASLt with fp32 output
 # instead of our split-K atomic GEMM (A/B option, PTG_BLASLT_DENSE_FWD=1)
 BLASLT_DENSE_FWD = [config.get("blaslt_dense_fwd")]
+DENSE_FWD_SPLITS = config.get("dense_fwd_splits")
 
 
 class FlattenOp(Op):
