@@ -467,7 +467,9 @@ class DenseOp(Op):
             except (TypeError, RuntimeError):
                 BLASLT_DENSE_FWD[0] = False
         tiles = -(-B // 128) * -(-N // 128)
-        splits = 1 if Kd < 4096 else max(1, min(16, 512 // max(tiles, 1), Kd // 1024))
+        # ~512 workgroups, <= 32 splits of >= 640 (CNN-B1 b32: 32 splits 0.645/0.657 vs 16 splits
+        # 0.660/0.667 ms; b256 keeps 16 - 8/12 within noise, 4/6/20/32 slower: r4_ab_dense_fwd_splits.txt)
+        splits = 1 if Kd < 4096 else max(1, min(32, 512 // max(tiles, 1), Kd // 640))
         if DENSE_FWD_SPLITS > 0:
             splits = min(int(DENSE_FWD_SPLITS), max(1, Kd // 64))
         K.gemm(B, N, Kd, x, Kd, 1, self.dense.kernel.bf16, Kd, 1, 3, acc, N, None, 0, splits)
