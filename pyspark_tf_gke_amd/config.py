@@ -102,8 +102,9 @@ _K = [
          "1.657/1.650 ms; on layer 3 as well: 1.80 ms)"),
     Knob("conv32_min_ch", int, 32, "PTG_CONV32_MINCH", None,
          "conv32 only where min(C, Cout) >= this (layer bench: it wins on CNN-B1 layers 4-5, loses the 32->16 dgrad)"),
-    Knob("conv32_min_wg", int, 256, "PTG_CONV32_MINWG", None,
-         "conv32 only when its grid (N x H / rows-per-tile workgroups) has at least this many workgroups"),
+    Knob("conv32_min_wg", int, 128, "PTG_CONV32_MINWG", None,
+         "conv32 only when its grid (N x H / rows-per-tile workgroups) has at least this many workgroups "
+         "(128 since the LDS-staged taps: CNN-B1 b32 0.646/0.638 vs 0.655/0.655 ms at 256)"),
     Knob("ppb_rows", bool, False, "PTG_PPB_ROWS", None,
          "CNN-B1 layers 2-4: PReLU + max-pool backward in the row-pair layout (ppb.hip, dalpha via chunk partials)"),
     Knob("conv1_rec", bool, True, "PTG_CONV1_REC", None, "first conv layer (conv1.hip): forward keeps the pool record, backward needs no recompute (0: recompute z in the backward)"),
