@@ -52,6 +52,10 @@ def parse_args(argv: List[str]):
     p.add_argument("--chief-port", type=int, default=int(env("CHIEF_PORT", "2223")))
     # additions
     p.add_argument("--strategy", default=env("PTG_STRATEGY", "auto"), choices=["auto", "ps", "mirrored", "none"])
+    p.add_argument("--ps-mode", default=env("PTG_PS_MODE", "sync"), choices=["sync", "async"],
+                   help="ParameterServerStrategy update mode: 'async' is TF's (workers push gradients that the "
+                        "owning ranks apply as they arrive, train_tf_ps.py:505-510); 'sync' commits one "
+                        "update per coordinator round")
     p.add_argument("--cache-decoded", action="store_true",
                    help="keep decoded images in host RAM after the first epoch (Dataset.cache)")
     p.add_argument("--synthetic", type=int, default=int(env("PTG_SYNTHETIC", "0")),
@@ -74,7 +78,7 @@ def _is_chief() -> bool:
 
 
 def make_parameter_server_strategy(worker_replicas: int, ps_replicas: int, port: int = 2222, worker_addrs=None,
-                                   ps_addrs=None, chief_addr=None, chief_port: int = 2223):
+                                   ps_addrs=None, chief_addr=None, chief_port: int = 2223, mode: str | None = None):
     """Same contract as train_tf_ps.py:440-511: print the ClusterSpec, validate the chief IPv4, export
     TF_CONFIG (task=chief), build the resolver/partitioner/strategy."""
     from .. import distribute as ds
@@ -89,7 +93,7 @@ def make_parameter_server_strategy(worker_replicas: int, ps_replicas: int, port:
             print("TF_CONFIG set:", os.environ["TF_CONFIG"], flush=True)
     resolver = ds.SimpleClusterResolver(ds.ClusterSpec(cluster), rpc_layer="grpc")
     part = ds.MinSizePartitioner(min_shard_bytes=256 << 10, max_shards=max(ps_replicas, 1))
-    return ds.ParameterServerStrategy(cluster_resolver=resolver, variable_partitioner=part)
+    return ds.ParameterServerStrategy(cluster_resolver=resolver, variable_partitioner=part, mode=mode)
 
 
 def _strategy_for(args, use_ps: bool):
@@ -102,7 +106,8 @@ def _strategy_for(args, use_ps: bool):
         wa = [s.strip() for s in args.worker_addrs.split(",") if s.strip()] or None
         pa = [s.strip() for s in args.ps_addrs.split(",") if s.strip()] or None
         return "ps", make_parameter_server_strategy(args.worker_replicas, args.ps_replicas, args.port, wa, pa,
-                                                    args.chief_addr or None, args.chief_port)
+                                                    args.chief_addr or None, args.chief_port,
+                                                    mode=getattr(args, "ps_mode", None))
     if mode == "mirrored":
         return "mirrored", ds.MultiWorkerMirroredStrategy()
     return "none", None
@@ -121,7 +126,7 @@ def _save_artifacts(model, history: dict, output_dir: str) -> None:
 def _ps_loop(model, strategy, per_worker_fn, steps_per_epoch, epochs, loss_obj, optimizer, metrics, fmt):
     """The reference's coordinator loop: schedule steps_per_epoch closures, join() per epoch."""
     from .. import distribute as ds
-    from ..nn import GradientTape
+    from ..nn import GradientTape, add_n
 
     coordinator = ds.ClusterCoordinator(strategy)
     it = iter(coordinator.create_per_worker_dataset(per_worker_fn))
@@ -131,6 +136,8 @@ def _ps_loop(model, strategy, per_worker_fn, steps_per_epoch, epochs, loss_obj, 
         with GradientTape() as tape:
             preds = model(features, training=True)
             loss = loss_obj(labels, preds)
+            # Add possible regularization losses (train_tf_ps.py:624)
+            loss += add_n(model.losses) if model.losses else 0.0
         grads = tape.gradient(loss, model.trainable_variables)
         optimizer.apply_gradients(zip(grads, model.trainable_variables))
         for m in metrics[1:]:

@@ -189,10 +189,16 @@ class ClusterCoordinator:
             return True
 
         def requeue(i, tries, excl):
+            # the owner mark says "queued" from now on, so a dead-worker scan cannot queue it twice
+            store.set(f"{pre}/own/{i}", "q")
             j = store.add(pre + "/rq/alloc", 1) - 1
             store.set(f"{pre}/rq/{j}", f"{i}:{tries}:{excl}")
 
-        cursor, fresh_done, last_scan = 0, False, time.time()
+        dead_mask = [0]  # ranks found dead by this rank's scans
+        seen_nfin = [-1]
+        skipped: list = []  # retry entries this rank was excluded from (claimable once the others die)
+        deadline_s = float(config.get("pg_timeout_s"))
+        cursor, fresh_done, last_scan, last_progress = 0, False, time.time(), time.time()
         try:
             while True:
                 job = None
@@ -201,8 +207,9 @@ class ClusterCoordinator:
                     store.wait([f"{pre}/rq/{cursor}"])
                     i, tries, excl = (int(x) for x in store.get(f"{pre}/rq/{cursor}").decode().split(":"))
                     j, cursor = cursor, cursor + 1
-                    if excl & (1 << rank) and excl != every:
-                        continue  # a worker that failed it leaves it to the others
+                    if excl & (1 << rank) and (excl | dead_mask[0]) != every:
+                        skipped.append((j, i, tries, excl))
+                        continue  # a worker that failed it leaves it to the others (while one is alive)
                     if store.add(f"{pre}/rq/{j}/claim", 1) == 1:
                         job = (i, tries, excl & every if excl != every else 0)
                 if job is None and not fresh_done:
@@ -212,13 +219,28 @@ class ClusterCoordinator:
                     else:
                         fresh_done = True
                 if job is None:
-                    if store.add(pre + "/nfin", 0) >= n:
+                    nfin = store.add(pre + "/nfin", 0)
+                    if nfin >= n:
                         break
-                    if time.time() - last_scan > min(1.0, dead_s / 4):
-                        last_scan = time.time()
-                        self._rescue_dead(store, pre, n, world, rank, dead_s, requeue)
-                    time.sleep(0.002)
-                    continue
+                    now = time.time()
+                    if now - last_scan > min(1.0, dead_s / 4):
+                        last_scan = now
+                        dead_mask[0] |= self._rescue_dead(store, pre, n, world, rank, dead_s, requeue)
+                        if nfin != seen_nfin[0]:
+                            seen_nfin[0], last_progress = nfin, now
+                        elif now - last_progress > deadline_s:
+                            raise RuntimeError(f"ClusterCoordinator.join: no closure finished for {deadline_s:.0f} s "
+                                               f"({nfin}/{n} done; PTG_PG_TIMEOUT)")
+                    for k, (j, i, tries, excl) in enumerate(skipped):
+                        if (excl | dead_mask[0]) == every:
+                            del skipped[k]
+                            if store.add(f"{pre}/rq/{j}/claim", 1) == 1:
+                                job = (i, tries, 0)
+                            break
+                    if job is None:
+                        time.sleep(0.002)
+                        continue
+                last_progress = time.time()
                 i, tries, excl = job
                 store.set(f"{pre}/own/{i}", str(rank))
                 fn, args, kwargs, rv, _ = queue[i]
@@ -268,14 +290,18 @@ class ClusterCoordinator:
             if store.check([key]) and now - float(store.get(key).decode()) > dead_s:
                 dead.append(r)
         if not dead:
-            return
+            return 0
         for i in range(n):
             own = f"{pre}/own/{i}"
             if not store.check([own]) or store.check([f"{pre}/rv/{i}"]):
                 continue
-            r = int(store.get(own).decode())
+            o = store.get(own).decode()
+            if not o.isdigit():
+                continue  # already back in the retry queue (its failed attempt re-queued it)
+            r = int(o)
             if r in dead and store.add(f"{pre}/rescue/{i}/{r}", 1) == 1:
                 requeue(i, 0, 1 << r)
+        return sum(1 << r for r in dead)
 
     # ---- transactional rounds (sync) ---------------------------------------------------------------
     def _join_rounds(self) -> None:

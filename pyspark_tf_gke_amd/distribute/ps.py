@@ -505,6 +505,11 @@ class ParameterServerStrategy(Strategy):
         if self.is_async and self.world_size > _MAX_WINDOWS:
             raise ValueError(f"asynchronous ParameterServerStrategy maps every rank's window into one copy kernel: "
                              f"at most {_MAX_WINDOWS} ranks (world size {self.world_size}); use mode='sync'")
+        lws = os.environ.get("LOCAL_WORLD_SIZE")
+        if self.is_async and lws is not None and int(lws) != self.world_size:
+            raise ValueError("asynchronous ParameterServerStrategy signals gradient pushes through a /dev/shm "
+                             "control block and maps its peers' windows by HIP IPC: every rank must run on one node "
+                             f"(LOCAL_WORLD_SIZE {lws} != WORLD_SIZE {self.world_size}); use mode='sync' across nodes")
         plan = model._ps_plan = _PSPlan(model, self.variable_partitioner, self.num_ps, self.world_size, self.rank,
                                         windows=self.is_async)
         if self.is_async:

@@ -160,6 +160,8 @@ class Strategy:
         for m in models:
             m._lazy_dw = None  # deferred tape weight gradients of the aborted attempt (nn/tape.py)
             m._tape_overlap = None
+            if hasattr(m, "_drop_pending_head"):
+                m._drop_pending_head()  # a closure that failed between its forward and its loss
             m.store.flat_grad.zero_()
             m.store.grad_clean = True
         self._pending = None

@@ -5,4 +5,4 @@ from .layers import (Activation, Add, BatchNormalization, Conv2D, Dense, Flatten
                      GlobalAveragePooling2D, Input, MaxPooling2D, PReLU, ReLU, ZeroPadding2D)
 from .functional import Model  # noqa: F401
 from .model import Sequential, load_model  # noqa: F401
-from .tape import GradientTape  # noqa: F401
+from .tape import GradientTape, add_n  # noqa: F401

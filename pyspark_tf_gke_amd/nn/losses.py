@@ -25,10 +25,14 @@ class Loss:
         hd = getattr(y_pred, "_lz", None) if isinstance(y_pred, _HeadPred) else None
         if hd is not None and hd.state == "pending" and self.kind == "mse" and tape is not None and tape.out is y_pred:
             val = hd.fused_loss(self, y_true)  # fit()'s fused regression head (nn/tape.py)
+        fused = val is not None
         if val is None:
             val = self.compute(y_true, y_pred)
         if tape is not None:
-            tape.record_loss(self, y_true, y_pred, val)
+            # a differentiable scalar: tape.gradient() accepts it and linear combinations of it
+            val = tape.record_loss(self, y_true, y_pred, val)
+            if fused:
+                hd.record = val._terms[0][0]
         return val
 
     def compute(self, y_true, y_pred):

@@ -301,6 +301,8 @@ class Sequential:
             tape.record_forward(self, out)
         if isinstance(self._last_op(), E.DenseOp) and self._last_op().logits_only:
             out = torch.softmax(out.float(), -1)
+            if tape is not None:
+                tape.ret = out  # the probabilities handed to the caller stand for this forward too
         return out
 
     def _loss_grad(self, out, yb, stats, gscale=1.0):
@@ -399,15 +401,25 @@ class Sequential:
 
         if getattr(self, "_lazy_dw", None):
             flush_lazy(self)
+        self._drop_pending_head()
         d1, d2 = self.ops[-2], self.ops[-1]
         x = E.run_forward(self.ops[:-2], xb, self.ws, True, pre_op=self._pre_op_hook())
         acc = d1.forward_splitk_sums(x, self.ws)
         pred = self.ws.get(d2.name + "/tapepred", (acc.shape[0], d2.dense.units), torch.float32, acc.device)
         out = pred.as_subclass(_HeadPred)
-        out._lz = _HeadState(self, acc, pred)
+        out._lz = self._head_state = _HeadState(self, acc, pred)
         return out
 
+    def _drop_pending_head(self) -> None:
+        """A tape prediction still held at the split-K sums (its loss never ran) is abandoned: clear
+        the sums so the next big-Dense forward does not add onto them."""
+        prev = getattr(self, "_head_state", None)
+        if prev is not None:
+            prev.discard()
+            self._head_state = None
+
     def _train_step_fused_head(self, xb, yb, stats, st) -> None:
+        self._drop_pending_head()
         d1, d2 = self.ops[-2], self.ops[-1]
         pre = self._pre_op_hook()
         if self._deferred_ev is not None:
@@ -799,6 +811,8 @@ class Sequential:
                         B = xb.shape[0] // k
                         self._last_batch = int(B)
                         if self._mlp_fusable(xb[:B], yb[:B], st) is not None:
+                            for _ in range(k):  # fault injection counts every step of the group
+                                _fault.maybe_fail()
                             _heartbeat.progress(k)
                             self._train_step_mlp(xb, yb, stats, mlp_group[1], steps=k)
                         else:

@@ -69,6 +69,129 @@ class _LazyGrad(_Deferred):
     """The gradient of a big Dense kernel whose GEMM has not run yet (``_lz``: a :class:`_LazyDW`)."""
 
 
+# ---------------------------------------------------------------------------------------------
+# Differentiable targets.  The tape does not trace arbitrary torch code; what it can differentiate
+# is a LINEAR combination of the loss values it recorded (train_tf_ps.py:620-625 builds
+# ``loss = loss_obj(labels, preds); loss += tf.add_n(model.losses) if model.losses else 0.0``).
+# A loss object called under a tape returns a _TapeLoss: the scalar value plus its terms
+# ((record, coefficient), ...).  +, -, unary -, * and / by a constant, add_n and sum keep the
+# terms; any other operation returns a plain tensor, which gradient() refuses.
+# ---------------------------------------------------------------------------------------------
+class _LossRecord:
+    """One loss-object call under a tape: its gradient is d(loss_obj(y_true, y_pred)) / d(params)."""
+
+    def __init__(self, tape, loss_obj, y_true, y_pred):
+        self.tape, self.loss_obj, self.y_true, self.y_pred = tape, loss_obj, y_true, y_pred
+
+
+_ADD = {"add", "__add__", "__radd__", "__iadd__", "add_"}
+_SUB = {"sub", "__sub__", "__isub__", "sub_", "subtract"}
+_RSUB = {"__rsub__", "rsub"}
+_MUL = {"mul", "__mul__", "__rmul__", "__imul__", "mul_", "multiply"}
+_DIV = {"div", "__truediv__", "__itruediv__", "div_", "true_divide", "divide"}
+_NEG = {"neg", "__neg__", "negative"}
+_SAME = {"float", "to", "clone", "contiguous", "reshape", "view", "squeeze", "unsqueeze", "sum", "mean",
+         "__pos__", "positive"}
+
+
+def _terms(x):
+    """Terms of a tape loss, () for a constant (a number or a tensor the tape does not track)."""
+    return getattr(x, "_terms", ()) if isinstance(x, _TapeLoss) else ()
+
+
+def _const(x) -> float | None:
+    if isinstance(x, _TapeLoss):
+        return None
+    if isinstance(x, (int, float)):
+        return float(x)
+    if isinstance(x, torch.Tensor) and x.numel() == 1:
+        return float(x)
+    return None
+
+
+def _scaled(ts, c: float):
+    return tuple((r, k * c) for r, k in ts)
+
+
+def _lin_terms(name: str, args, kwargs):
+    """The terms of func(*args) for a linear func of tape losses and constants, or None."""
+    a = args[0] if args else None
+    b = args[1] if len(args) > 1 else kwargs.get("other")
+    alpha = kwargs.get("alpha", 1)
+    if name in _SAME:
+        return _terms(a)
+    if name in _NEG:
+        return _scaled(_terms(a), -1.0)
+    if name in _ADD:
+        return _terms(a) + _scaled(_terms(b), float(alpha))
+    if name in _SUB:
+        return _terms(a) + _scaled(_terms(b), -float(alpha))
+    if name in _RSUB:  # b - a
+        return _terms(b) + _scaled(_terms(a), -1.0)
+    if name in _MUL:
+        ta, tb = _terms(a), _terms(b)
+        if ta and tb:
+            return None  # loss * loss is not linear
+        if not ta and not tb:
+            return ()
+        c = _const(b if ta else a)
+        return None if c is None else _scaled(ta or tb, c)
+    if name in _DIV:
+        if _terms(b):
+            return None
+        c = _const(b)
+        return None if not c else _scaled(_terms(a), 1.0 / c)
+    return None
+
+
+class _TapeLoss(torch.Tensor):
+    """A scalar loss value the tape can differentiate (``_terms``)."""
+
+    @classmethod
+    def __torch_function__(cls, func, types, args=(), kwargs=None):
+        kwargs = kwargs or {}
+        name = _func_name(func)
+        with torch._C.DisableTorchFunctionSubclass():
+            out = func(*args, **kwargs)
+        if name in _META or not isinstance(out, torch.Tensor):
+            return out
+        ts = _lin_terms(name, args, kwargs)
+        if ts is None or out.numel() != 1:
+            if isinstance(out, _TapeLoss):  # an in-place op that left the linear family
+                out._terms = None
+            return out.as_subclass(torch.Tensor) if isinstance(out, _TapeLoss) else out
+        res = out if isinstance(out, _TapeLoss) else out.as_subclass(_TapeLoss)
+        res._terms = ts
+        return res
+
+
+def _tape_loss(value, record) -> _TapeLoss:
+    v = torch.as_tensor(value)
+    t = v.as_subclass(_TapeLoss)
+    t._terms = ((record, 1.0),)
+    return t
+
+
+def add_n(inputs):
+    """``tf.add_n``: the sum of a list of (tape) losses, keeping what the tape can differentiate."""
+    inputs = list(inputs)
+    if not inputs:
+        raise ValueError("add_n of an empty list")
+    out = inputs[0]
+    for x in inputs[1:]:
+        out = out + x
+    return out
+
+
+def _param_of(src):
+    p = getattr(src, "param", None)
+    if p is not None:
+        return p
+    if hasattr(src, "offset") and hasattr(src, "grad"):
+        return src  # a Param of the flat store
+    raise TypeError(f"GradientTape.gradient: source {src!r} is not a model variable")
+
+
 class _HeadPred(_Deferred):
     """The prediction of a [..., Dense(relu, big), Dense(N <= 4)] tail under a tape, held at the
     big layer's split-K sums (``_lz``: a :class:`_HeadState`): an MSE loss object called on it runs
@@ -82,6 +205,32 @@ class _HeadState:
         self.state = "pending"  # -> "plain" (unfused tail ran) or "fused" (head_mse ran for the loss)
         self.dz1 = None
         self.loss_obj = None
+        self.record = None  # the tape's _LossRecord of the fused loss call
+
+    def discard(self) -> None:
+        """An abandoned pending prediction (a failed closure, a second forward before the loss):
+        the split-K sums it holds must not leak into the next forward, which adds onto them."""
+        if self.state == "pending":
+            self.acc.zero_()
+            self.state = "dropped"
+
+    def redo_plain(self) -> None:
+        """The fused head ran for a loss, but the tape is asked for the gradient of another target:
+        recompute the big layer's sums (the head consumed them) and run the plain tail instead."""
+        if self.state != "fused":
+            return
+        d1 = self.model.ops[-2]
+        d1.forward_splitk_sums(d1._x, self.model.ws)
+        self.state, self.dz1, self.loss_obj, self.record = "pending", None, None, None
+        self.materialize()
+
+    def scale_grads(self, c: float) -> None:
+        """The target is c x the fused loss: scale what the head kernels produced (dz1 and the
+        Dense2 / Dense1-bias gradients); the backward below is linear in dz1."""
+        d1, d2 = self.model.ops[-2], self.model.ops[-1]
+        self.dz1.mul_(c)
+        for g in (d2.dense.kernel.grad, d2.dense.bias.grad, d1.dense.bias.grad):
+            g.mul_(c)
 
     def materialize(self) -> None:
         """The unfused tail: Dense1 bias + ReLU from the split-K sums (re-zeroing them), Dense2."""
@@ -222,10 +371,57 @@ class GradientTape:
         return False
 
     def record_forward(self, model, out):
-        self.model, self.out = model, out
+        self.model, self.out, self.ret = model, out, out
 
     def record_loss(self, loss_obj, y_true, y_pred, value):
         self.loss_obj, self.y_true = loss_obj, y_true
+        rec = _LossRecord(self, loss_obj, y_true, y_pred)
+        self.records = getattr(self, "records", []) + [rec]
+        return _tape_loss(value, rec)
+
+    def _target_terms(self, target):
+        """Merge the target's terms per loss record; raise for anything the tape cannot differentiate."""
+        ts = getattr(target, "_terms", None) if isinstance(target, _TapeLoss) else None
+        if ts is None:
+            raise ValueError("GradientTape.gradient: the target is not a linear combination of loss values "
+                             "recorded by this tape (loss objects called on the model output inside the "
+                             "`with` block, combined by +, -, * / constant, add_n)")
+        merged: dict = {}
+        for rec, c in ts:
+            if rec.tape is not self:
+                raise ValueError("GradientTape.gradient: the target depends on a loss recorded by another tape")
+            if rec.y_pred is not self.out and rec.y_pred is not self.ret:
+                raise ValueError("GradientTape.gradient: the target depends on a loss of a prediction other than "
+                                 "this tape's last model forward")
+            r0, c0 = merged.get(id(rec), (rec, 0.0))
+            merged[id(rec)] = (rec, c0 + c)
+        return [(r, c) for r, c in merged.values() if c != 0.0]
+
+    @staticmethod
+    def _labels(loss_obj, y_true):
+        from . import losses as LS
+
+        if isinstance(loss_obj, LS.SparseCategoricalCrossentropy):
+            return y_true.to(torch.int32).view(-1).contiguous()
+        yb = y_true.float().contiguous()
+        return yb.view(-1, 1) if yb.dim() == 1 else yb
+
+    def _dpred(self, m, out, terms):
+        """d(target)/d(prediction) = sum of coefficient x the fused loss kernels' output gradients."""
+        stats = torch.zeros(8, dtype=torch.float32, device=out.device)
+        saved_loss = m.loss
+        dpred = None
+        try:
+            for rec, c in terms:
+                m.loss = rec.loss_obj
+                dp = m._loss_grad(out, self._labels(rec.loss_obj, rec.y_true), stats, gscale=c)
+                if dpred is None:
+                    dpred = dp.clone() if len(terms) > 1 else dp  # dp is the model's reused workspace
+                else:
+                    dpred.add_(dp)
+        finally:
+            m.loss = saved_loss
+        return dpred
 
     def gradient(self, target, sources):
         from . import engine as E
@@ -236,38 +432,41 @@ class GradientTape:
         m = self.model
         if m is None or self.loss_obj is None:
             raise RuntimeError("GradientTape.gradient: no model forward / loss recorded")
+        single = not isinstance(sources, (list, tuple))
+        srcs = [sources] if single else list(sources)
+        params = [_param_of(s) for s in srcs]
+        own = {id(p) for p in m.store.params}
+        for p in params:
+            if id(p) not in own:
+                raise ValueError(f"GradientTape.gradient: source {p.name!r} is not a variable of the recorded model")
+        terms = self._target_terms(target)
         flush_lazy(m)
         out = self.out
         last = m._last_op()
-        if isinstance(self.loss_obj, LS.SparseCategoricalCrossentropy) and isinstance(last, E.DenseOp) \
-                and last.act == "softmax" and not last.logits_only:
+        if any(isinstance(r.loss_obj, LS.SparseCategoricalCrossentropy) for r, _ in terms) \
+                and isinstance(last, E.DenseOp) and last.act == "softmax" and not last.logits_only:
             raise RuntimeError("compile() the model with the loss (or build with from_logits) before a tape loop")
         hd = getattr(out, "_lz", None) if isinstance(out, _HeadPred) else None
-        head = hd is not None and hd.state == "fused" and hd.loss_obj is self.loss_obj
+        head = (hd is not None and hd.state == "fused" and len(terms) == 1 and terms[0][0].loss_obj is hd.loss_obj
+                and terms[0][0] is getattr(hd, "record", None))
+        if hd is not None and hd.state == "fused" and not head:
+            hd.redo_plain()  # the fused head's gradients are those of one unscaled loss: run the plain tail
+        if head and terms[0][1] != 1.0:
+            hd.scale_grads(terms[0][1])
         if not head:
-            stats = torch.zeros(8, dtype=torch.float32, device=out.device)
-            saved_loss = m.loss
-            m.loss = self.loss_obj
-            try:
-                yb = self.y_true
-                if isinstance(self.loss_obj, LS.SparseCategoricalCrossentropy):
-                    yb = yb.to(torch.int32).view(-1).contiguous()
-                else:
-                    yb = yb.float().contiguous()
-                    if yb.dim() == 1:
-                        yb = yb.view(-1, 1)
-                m.store.zero_grad()
-                dpred = m._loss_grad(out, yb, stats)
-            finally:
-                m.loss = saved_loss
+            m.store.zero_grad()
+            if not terms:  # e.g. loss - loss: every gradient is zero
+                return self._result([p.grad for p in params], single)
+            dpred = self._dpred(m, out, terms)
         # the same side-stream overlap as fit()'s step (streams.py): every wgrad forks off the dgrad
         # chain and the step's stream joins it before returning, so the gradients handed back are
         # stream-ordered complete, exactly as with the serial backward
         st = getattr(m, "strategy", None) or current_strategy()
         side = S.for_step(m.store, st)
         ready: list = []
-        local = st is None or getattr(st, "world_size", 2) == 1
-        # one local replica (no strategy, or a one-worker parameter server): defer the big Dense dW
+        local = _update_takes_overlap(st)
+        # one local replica whose update consumes the tape's overlap list (no strategy, or a one-worker
+        # parameter server, ps.py _apply_local): defer the big Dense dW
         defer = _DeferDW() if (OVERLAP and LAZY_DW and local) else None
         big = [op for op in m.ops if isinstance(op, E.DenseOp) and op.big] if defer is not None else []
         for op in big:
@@ -305,22 +504,65 @@ class GradientTape:
                 ready.append((p.offset, p.offset + p.numel, None, d))
         m._tape_ready = ready if local else None
         m._pending_grads = True
-        return [grads.get(id(v.param), v.param.grad) for v in sources]
+        return self._result([grads.get(id(p), p.grad) for p in params], single)
+
+    def _result(self, grads, single):
+        self.model._pending_grads = True
+        return grads[0] if single else grads
+
+
+def _update_takes_overlap(st) -> bool:
+    """Whether the update after a tape backward consumes the tape's overlap list (deferred Dense dW
+    fused with Adam, per-range Adam events): with no strategy (apply_gradients runs it) or a
+    one-worker ParameterServerStrategy (ps.py _apply_local).  Any other strategy reads the whole flat
+    gradient buffer, so nothing may be deferred."""
+    if st is None:
+        return True
+    from ..distribute.ps import ParameterServerStrategy
+
+    return isinstance(st, ParameterServerStrategy) and st.world_size == 1
+
+
+def _var_model(v):
+    m = getattr(v, "model", None)
+    if m is None:
+        raise TypeError(f"apply_gradients: {v!r} is not a model variable (model.trainable_variables)")
+    return m
 
 
 def apply_gradients(optimizer, grads_and_vars) -> None:
-    gv = list(grads_and_vars)
+    gv = [(g, v) for g, v in grads_and_vars if g is not None]  # TF skips variables without a gradient
     if not gv:
         return
-    model = gv[0][1].model
+    model = _var_model(gv[0][1])
     from ..distribute import current_strategy
 
     st = getattr(model, "strategy", None) or current_strategy()
     ready = getattr(model, "_tape_ready", None)
     model._tape_ready = None
-    ok = bool(ready) and _overlap_ok(optimizer, gv, ready)
+    params = [_param_of(v) for _, v in gv]
+    subset = {id(p) for p in params} != {id(p) for p in model.store.params}
+    ok = bool(ready) and not subset and _overlap_ok(optimizer, gv, ready)
     if not ok:
         flush_lazy(model)  # the update below reads every gradient from the flat buffer
+        _stage_grads(gv)
+    if subset:
+        # only the listed variables move (and only their optimizer slots)
+        if st is not None and (getattr(st, "world_size", 1) > 1 or st.in_round()):
+            raise NotImplementedError("apply_gradients on a subset of the variables under a distribution "
+                                      "strategy's collective update")
+        if not hasattr(optimizer, "build"):
+            raise NotImplementedError(f"apply_gradients on a subset of the variables with {type(optimizer).__name__}")
+        optimizer.build(model.store)
+        if getattr(optimizer, "dev_state", None) is not None:
+            from ..ops import nn as K
+
+            K.adam_step(optimizer.dev_state, optimizer.learning_rate, optimizer.beta_1, optimizer.beta_2)
+        for lo, hi in _ranges(params):
+            optimizer.apply(model.store, lo=lo, hi=hi, advance=False)
+        optimizer.iterations += 1
+        model._pending_grads = False
+        return
     if st is not None:
         # a one-worker ParameterServerStrategy applies the update itself (possibly at round commit)
         # and takes the overlapped form from here (ps.py _apply_local)
@@ -332,6 +574,34 @@ def apply_gradients(optimizer, grads_and_vars) -> None:
     else:
         optimizer.apply(model.store)
     model._pending_grads = False
+
+
+def _stage_grads(gv) -> None:
+    """Gradients the caller replaced (clipped, scaled, computed elsewhere) go into the flat gradient
+    buffer the fused update reads; the tape's own buffers are already there."""
+    for g, v in gv:
+        p = _param_of(v)
+        if g is p.grad:
+            continue
+        if not isinstance(g, torch.Tensor):
+            g = torch.as_tensor(g, dtype=torch.float32)
+        with torch._C.DisableTorchFunctionSubclass():
+            same = g.device == p.grad.device and g.data_ptr() == p.grad.data_ptr() and g.numel() == p.grad.numel()
+            if not same:
+                if g.numel() != p.grad.numel():
+                    raise ValueError(f"apply_gradients: gradient of {p.name!r} has {g.numel()} elements, "
+                                     f"the variable {p.grad.numel()}")
+                p.grad.copy_(g.reshape(p.grad.shape))
+
+
+def _ranges(params) -> list:
+    out: list = []
+    for a, b in sorted((p.offset, p.offset + p.numel) for p in params):
+        if out and a <= out[-1][1]:
+            out[-1] = (out[-1][0], max(out[-1][1], b))
+        else:
+            out.append((a, b))
+    return out
 
 
 _AUX: dict = {}

@@ -548,3 +548,36 @@ print("RESULT", json.dumps({"retries": co2.retries, "it_ok": o_ok.iterations, "i
     assert v["retries"] == 3 and v["it_ok"] == 6 and v["it_ft"] == 5, v
     assert v["vals"] == [1, 1, 1, 1, "RuntimeError", 1, "StopIteration"], v
     assert v["same_as_skip4"] and v["ran"] == 5, v
+
+
+@pytest.mark.parametrize("mode", ["async", "sync"])
+def test_train_tf_ps_cli_ps_mode(mode, tmp_path):
+    """`train_tf_ps.py --use-ps --ps-mode {async,sync}` (the reference's CSV-MLP driver under
+    ParameterServerStrategy + ClusterCoordinator, train_tf_ps.py:505-510,612-645) on 2 gloo ranks:
+    the strategy runs in the requested mode, the loop trains and the chief saves the model."""
+    script = os.path.join(ROOT, "workloads", "raw-tf", "train_tf_ps.py")
+    body = f"""
+    import runpy, sys, json
+    sys.path.insert(0, {os.path.dirname(script)!r})
+    from pyspark_tf_gke_amd.distribute import ParameterServerStrategy
+    seen = {{}}
+    _init = ParameterServerStrategy.__init__
+    def _spy(self, *a, **k):
+        _init(self, *a, **k)
+        seen["mode"] = self.mode
+    ParameterServerStrategy.__init__ = _spy
+    sys.argv = ["train_tf_ps.py", "--use-ps", "--ps-mode", "{mode}", "--worker-replicas", "2", "--ps-replicas", "1",
+                "--data-path", {os.path.join(ROOT, "tests", "data", "health.csv")!r}, "--epochs", "2",
+                "--batch-size", "512", "--output-dir", {str(tmp_path)!r}, "--chief-addr", "127.0.0.1"]
+    try:
+        runpy.run_path({script!r}, run_name="__main__")
+    except SystemExit as e:
+        assert not e.code, e.code
+    print("RESULT", json.dumps(seen), flush=True)
+    """
+    r = _launch(body, 2, timeout=400)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    res = _results(r.stdout)
+    assert len(res) == 2 and all(v["mode"] == mode for v in res.values()), res
+    assert "Epoch 2 - loss:" in r.stdout
+    assert os.path.exists(os.path.join(str(tmp_path), "model.keras"))

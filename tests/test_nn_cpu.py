@@ -3,6 +3,7 @@ import json
 import zipfile
 
 import numpy as np
+import pytest
 import torch
 
 from pyspark_tf_gke_amd import nn
@@ -320,3 +321,214 @@ def test_ps_one_worker_tape_lazy_path_matches_plain_loop():
     coord.join()
     assert all(seen) and o1.iterations == 4
     assert torch.allclose(m0.store.flat, m1.store.flat, atol=1e-6)
+
+
+# ---------------------------------------------------------------------------------------------
+# GradientTape.gradient(target, sources): the reference's step_fn (train_tf_ps.py:616-631,
+# :738-753) with `loss += tf.add_n(model.losses) if model.losses else 0.0`, scaled targets, sums
+# of recorded losses and subsets of the variables, against torch autograd.
+# ---------------------------------------------------------------------------------------------
+def _mlp_autograd(m, X, y, coef):
+    """d(coef * SCCE(y, softmax(mlp(X)))) / d(params) by torch autograd from the engine's weights."""
+    ps = [p for l in m.layers for p in l.params]
+    ts = [p.data.detach().clone().requires_grad_(True) for p in ps]
+    h = torch.as_tensor(X)
+    for i in range(0, len(ts), 2):
+        h = h @ ts[i].t() + ts[i + 1]
+        if i + 2 < len(ts):
+            h = torch.relu(h)
+    loss = torch.nn.functional.cross_entropy(h, torch.as_tensor(y).long()) * coef
+    loss.backward()
+    return {id(p): t.grad for p, t in zip(ps, ts)}
+
+
+def test_tape_reference_step_fn_scaled_target_matches_autograd():
+    rng = np.random.default_rng(3)
+    X = rng.normal(size=(32, 3)).astype(np.float32)
+    y = rng.integers(0, 5, 32).astype(np.int32)
+    m = build_deep_model(3, 5, device="cpu")
+    loss_obj = nn.losses.SparseCategoricalCrossentropy()
+    ref = _mlp_autograd(m, X, y, 2.5)
+    with nn.GradientTape() as tape:
+        logits = m(X, training=True)
+        loss = loss_obj(y, logits)
+        # Add possible regularization losses (the reference's exact line)
+        loss += nn.add_n(m.losses) if m.losses else 0.0
+        loss = 2.5 * loss
+    vs = m.trainable_variables
+    grads = tape.gradient(loss, vs)
+    for g, v in zip(grads, vs):
+        assert torch.allclose(g, ref[id(v.param)], rtol=1e-4, atol=1e-6), v.name
+    # the loss value follows the arithmetic
+    with nn.GradientTape() as tape:
+        plain = loss_obj(y, m(X, training=True))
+    assert abs(float(loss) - 2.5 * float(plain)) < 1e-5
+
+
+def test_tape_sources_subset_in_caller_order_and_partial_update():
+    rng = np.random.default_rng(4)
+    X = rng.normal(size=(32, 3)).astype(np.float32)
+    y = rng.integers(0, 5, 32).astype(np.int32)
+    m = build_deep_model(3, 5, device="cpu")
+    ref = _mlp_autograd(m, X, y, 1.0)
+    vs = m.trainable_variables
+    sub = [vs[5], vs[0], vs[3]]
+    before = [v.param.data.clone() for v in vs]
+    opt = nn.optimizers.Adam(1e-2)
+    with nn.GradientTape() as tape:
+        loss = nn.losses.SparseCategoricalCrossentropy()(y, m(X, training=True))
+    grads = tape.gradient(loss, sub)
+    assert len(grads) == 3
+    for g, v in zip(grads, sub):
+        assert tuple(g.shape) == tuple(v.param.shape)
+        assert torch.allclose(g, ref[id(v.param)], rtol=1e-4, atol=1e-6), v.name
+    single = None
+    with nn.GradientTape() as tape:
+        loss = nn.losses.SparseCategoricalCrossentropy()(y, m(X, training=True))
+    single = tape.gradient(loss, vs[2])
+    assert torch.allclose(single, ref[id(vs[2].param)], rtol=1e-4, atol=1e-6)
+    with nn.GradientTape() as tape:
+        loss = nn.losses.SparseCategoricalCrossentropy()(y, m(X, training=True))
+    grads = tape.gradient(loss, sub)
+    opt.apply_gradients(zip(grads, sub))
+    moved = {id(v.param) for v in sub}
+    for v, b in zip(vs, before):
+        changed = not torch.equal(v.param.data, b)
+        assert changed == (id(v.param) in moved), v.name
+    assert opt.iterations == 1
+
+
+def test_tape_replaced_gradients_are_applied():
+    """Gradients the caller rescales before apply_gradients are the ones the update uses."""
+    rng = np.random.default_rng(5)
+    X = rng.normal(size=(32, 3)).astype(np.float32)
+    y = rng.integers(0, 5, 32).astype(np.int32)
+    m1 = build_deep_model(3, 5, device="cpu")
+    m2 = build_deep_model(3, 5, device="cpu")
+    m2.set_weights(m1.get_weights())
+    o1, o2 = nn.optimizers.SGD(0.1), nn.optimizers.SGD(0.1)
+    lo = nn.losses.SparseCategoricalCrossentropy()
+    with nn.GradientTape() as tape:
+        l1 = lo(y, m1(X, training=True))
+    g1 = [g * 0.5 for g in tape.gradient(l1, m1.trainable_variables)]
+    o1.apply_gradients(zip(g1, m1.trainable_variables))
+    with nn.GradientTape() as tape:
+        l2 = lo(y, m2(X, training=True)) * 0.5
+    o2.apply_gradients(zip(tape.gradient(l2, m2.trainable_variables), m2.trainable_variables))
+    assert torch.allclose(m1.store.flat, m2.store.flat, atol=1e-6)
+
+
+def test_tape_untracked_target_raises():
+    rng = np.random.default_rng(6)
+    X = rng.normal(size=(16, 3)).astype(np.float32)
+    y = rng.integers(0, 5, 16).astype(np.int32)
+    m = build_deep_model(3, 5, device="cpu")
+    lo = nn.losses.SparseCategoricalCrossentropy()
+    with nn.GradientTape() as tape:
+        loss = lo(y, m(X, training=True))
+    with pytest.raises(ValueError):
+        tape.gradient(loss * loss, m.trainable_variables)  # not linear
+    with pytest.raises(ValueError):
+        tape.gradient(torch.tensor(1.0), m.trainable_variables)  # not a recorded loss
+    with pytest.raises(ValueError):
+        tape.gradient(torch.sqrt(loss), m.trainable_variables)
+    with nn.GradientTape() as other:
+        l2 = lo(y, m(X, training=True))
+    with pytest.raises(ValueError):
+        tape.gradient(l2, m.trainable_variables)  # another tape's loss
+    m2 = build_deep_model(3, 5, device="cpu")
+    with pytest.raises(ValueError):
+        other.gradient(l2, m2.trainable_variables)  # a variable of another model
+
+
+def test_tape_sum_of_losses_on_fused_head_matches_scaled_single():
+    """CNN-B1-shaped model (fused MSE head on the tape): loss_a + 0.5 * loss_b on the same prediction
+    (the head's fused gradients are redone through the plain tail) equals 1.5 * loss_a, and
+    0.25 * loss (scaled fused head) equals loss with a quarter of the gradient."""
+    from pyspark_tf_gke_amd.nn import tape as T
+
+    torch.manual_seed(2)
+    x = torch.rand(4, 32, 40, 3)
+    y = torch.rand(4, 2) * 10
+    m = build_cnn_model((32, 40, 3), flat=True, summary=False, device="cpu")
+    mse = nn.losses.MeanSquaredError()
+    saved = T.LAZY_DW
+    T.LAZY_DW = False  # plain gradient tensors to compare
+    try:
+        def grads(fn):
+            with nn.GradientTape() as tape:
+                pred = m(x, training=True)
+                tgt = fn(pred)
+            return [g.clone() for g in tape.gradient(tgt, m.trainable_variables)]
+
+        g_sum = grads(lambda p: mse(y, p) + 0.5 * mse(y, p))
+        g_15 = grads(lambda p: 1.5 * mse(y, p))
+        g_1 = grads(lambda p: mse(y, p))
+        g_q = grads(lambda p: mse(y, p) * 0.25)
+    finally:
+        T.LAZY_DW = saved
+    def rel(a, b):
+        return float(torch.linalg.vector_norm(a - b) / (torch.linalg.vector_norm(b) + 1e-12))
+
+    # the plain tail and the fused head round dZ / activations to bf16 at different points: compare at
+    # that precision; a power-of-two scale of the fused head is exact
+    for a, b, c, q in zip(g_sum, g_15, g_1, g_q):
+        assert rel(a, 1.5 * c) < 2e-2
+        assert rel(b, 1.5 * c) < 1e-2
+        assert rel(q, 0.25 * c) < 1e-5
+
+
+def test_tape_mwms_one_worker_trains_big_dense_like_fit():
+    """under a one-worker MultiWorkerMirroredStrategy the big Dense kernel's gradient must
+    not be deferred (its update reads the flat buffer): the tape loop equals train_on_batch."""
+    from pyspark_tf_gke_amd import distribute as ds
+
+    torch.manual_seed(0)
+    x = torch.rand(4, 32, 40, 3)
+    y = torch.rand(4, 2)
+    st = ds.MultiWorkerMirroredStrategy()
+    with st.scope():
+        m1 = build_cnn_model((32, 40, 3), flat=True, summary=False, device="cpu")
+        opt = nn.optimizers.Adam(1e-3)
+    m2 = build_cnn_model((32, 40, 3), flat=True, summary=False, device="cpu")
+    m2.set_weights(m1.get_weights())
+    m2.compile(optimizer=nn.optimizers.Adam(1e-3), loss="mse")
+    big = next(l for l in m1.layers if isinstance(l, nn.Dense) and l.units == 2048)
+    w0 = big.kernel.data.clone()
+    from pyspark_tf_gke_amd.nn import tape as T
+
+    saved = T.TAPE_HEAD
+    T.TAPE_HEAD = False  # train_on_batch's unfused CPU tail: the same roundings
+    try:
+        for _ in range(2):
+            with st.scope():
+                _tape_step(m1, opt, x, y)
+            m2.train_on_batch(x, y)
+    finally:
+        T.TAPE_HEAD = saved
+    assert not torch.equal(big.kernel.data, w0), "the big Dense kernel never trained"
+    # (MWMS re-lays the flat store out in buckets: compare per variable)
+    for a, b in zip(m1.get_weights(), m2.get_weights()):
+        assert np.allclose(a, b, atol=1e-5)
+
+
+def test_tape_abandoned_head_prediction_does_not_leak():
+    """a tape forward whose prediction is abandoned (a closure that fails between the
+    forward and the loss) leaves split-K sums behind; the next forward must not add onto them."""
+    from pyspark_tf_gke_amd.nn import tape as T
+
+    torch.manual_seed(3)
+    x = torch.rand(4, 32, 40, 3)
+    y = torch.rand(4, 2)
+    m1 = build_cnn_model((32, 40, 3), flat=True, summary=False, device="cpu")
+    m2 = build_cnn_model((32, 40, 3), flat=True, summary=False, device="cpu")
+    m2.set_weights(m1.get_weights())
+    with nn.GradientTape():
+        p = m1(x, training=True)
+    assert isinstance(p, T._HeadPred) and p._lz.state == "pending"  # the sums are held, never consumed
+    mse = nn.losses.MeanSquaredError()
+    with nn.GradientTape():
+        l1 = mse(y, m1(x, training=True))
+    with nn.GradientTape():
+        l2 = mse(y, m2(x, training=True))
+    assert abs(float(l1) - float(l2)) <= 1e-6 * max(1.0, abs(float(l2)))
