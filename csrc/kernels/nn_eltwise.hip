@@ -693,20 +693,28 @@ __global__ __launch_bounds__(256) void mse_k(const float* __restrict__ pred, con
 // ----------------------------------------------------------------------------------------------
 #define HEAD_RG 4
 template <int N2>
-__global__ __launch_bounds__(256) void head_row_k(const float* __restrict__ acc, const float* __restrict__ b1,
+// nparts > 0: acc holds nparts split-K partial slices [nparts][B][K1] (dense.hip plain-store
+// forward); the row pass sums them, and leaves h = relu(sum + b1) in slice 0 for head_col_k.
+// nparts == 0: acc holds the summed split-K sums (atomic forward) and head_col_k re-zeroes it.
+__global__ __launch_bounds__(256) void head_row_k(float* __restrict__ acc, const float* __restrict__ b1,
                                                   const float* __restrict__ w2, const float* __restrict__ b2,
                                                   const float* __restrict__ tgt, bf16_t* __restrict__ dz1,
                                                   float* __restrict__ dpred, float* __restrict__ rowerr,
-                                                  float* __restrict__ pred_out, int B, int K1, float gscale) {
+                                                  float* __restrict__ pred_out, int B, int K1, float gscale,
+                                                  int nparts) {
   __shared__ float red[4][N2];
   __shared__ float sdp[N2];
   const int m = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const float* arow = acc + (long)m * K1;
+  float* arow = acc + (long)m * K1;
+  const long pstride = (long)B * K1;
   float dot[N2];
 #pragma unroll
   for (int n = 0; n < N2; ++n) dot[n] = 0.f;
   for (int k = tid; k < K1; k += 256) {
-    const float h = fmaxf(arow[k] + b1[k], 0.f);
+    float a = arow[k];
+    for (int p = 1; p < nparts; ++p) a += arow[p * pstride + k];
+    const float h = fmaxf(a + b1[k], 0.f);
+    if (nparts) arow[k] = h;
 #pragma unroll
     for (int n = 0; n < N2; ++n) dot[n] = fmaf(h, w2[(long)n * K1 + k], dot[n]);
   }
@@ -737,7 +745,7 @@ __global__ __launch_bounds__(256) void head_row_k(const float* __restrict__ acc,
 #pragma unroll
   for (int n = 0; n < N2; ++n) dp[n] = sdp[n];
   for (int k = tid; k < K1; k += 256) {
-    const float h = fmaxf(arow[k] + b1[k], 0.f);
+    const float h = nparts ? arow[k] : fmaxf(arow[k] + b1[k], 0.f);  // (this thread's own store above)
     float g = 0.f;
 #pragma unroll
     for (int n = 0; n < N2; ++n) g = fmaf(dp[n], w2[(long)n * K1 + k], g);
@@ -750,7 +758,7 @@ __global__ __launch_bounds__(256) void head_col_k(float* __restrict__ acc, const
                                                   const float* __restrict__ w2, const float* __restrict__ dpred,
                                                   const float* __restrict__ rowerr, float* __restrict__ dw2,
                                                   float* __restrict__ db2, float* __restrict__ db1,
-                                                  float* __restrict__ stats, int B, int K1) {
+                                                  float* __restrict__ stats, int B, int K1, int nparts) {
   const int k = blockIdx.x * 256 + threadIdx.x;
   const int rows = (B + HEAD_RG - 1) / HEAD_RG, m0 = blockIdx.y * rows, m1 = min(B, m0 + rows);
   if (k < K1) {
@@ -761,8 +769,13 @@ __global__ __launch_bounds__(256) void head_col_k(float* __restrict__ acc, const
     float sb = 0.f;
     for (int m = m0; m < m1; ++m) {
       float* ap = acc + (long)m * K1 + k;
-      const float h = fmaxf(*ap + bk, 0.f);
-      *ap = 0.f;
+      float h;
+      if (nparts) {
+        h = *ap;  // head_row_k left relu(sum + b1) here
+      } else {
+        h = fmaxf(*ap + bk, 0.f);
+        *ap = 0.f;
+      }
       float g = 0.f;
 #pragma unroll
       for (int n = 0; n < N2; ++n) {
@@ -1155,16 +1168,16 @@ int ptg_prelu_bwd2(const void* da, const void* z, const float* alpha, void* dz, 
 // on exit.  scratch: fp32 [B * (N2 + 2)] (dpred and per-row errors).
 int ptg_head_mse(void* acc, const float* b1, const float* w2, const float* b2, const float* tgt, void* dz1,
                  float* dw2, float* db2, float* db1, float* stats, float* pred_out, float* scratch, int B, int K1,
-                 int N2, float gscale, hipStream_t s) {
-  if (N2 < 1 || N2 > 4 || B <= 0 || K1 <= 0) return (int)hipErrorInvalidValue;
+                 int N2, float gscale, int nparts, hipStream_t s) {
+  if (N2 < 1 || N2 > 4 || B <= 0 || K1 <= 0 || nparts < 0) return (int)hipErrorInvalidValue;
   float* dpred = scratch;
   float* rowerr = scratch + (long)B * N2;
   const dim3 gc((K1 + 255) / 256, HEAD_RG);
 #define PTG_HEAD(NN)                                                                                          \
-  hipLaunchKernelGGL(head_row_k<NN>, dim3(B), dim3(256), 0, s, (const float*)acc, b1, w2, b2, tgt, (bf16_t*)dz1, \
-                     dpred, rowerr, pred_out, B, K1, gscale);                                                 \
+  hipLaunchKernelGGL(head_row_k<NN>, dim3(B), dim3(256), 0, s, (float*)acc, b1, w2, b2, tgt, (bf16_t*)dz1,       \
+                     dpred, rowerr, pred_out, B, K1, gscale, nparts);                                         \
   hipLaunchKernelGGL(head_col_k<NN>, gc, dim3(256), 0, s, (float*)acc, b1, w2, dpred, rowerr, dw2, db2, db1,    \
-                     stats, B, K1)
+                     stats, B, K1, nparts)
   switch (N2) {
     case 1: PTG_HEAD(1); break;
     case 2: PTG_HEAD(2); break;
@@ -1172,6 +1185,38 @@ int ptg_head_mse(void* acc, const float* b1, const float* w2, const float* b2, c
     default: PTG_HEAD(4); break;
   }
 #undef PTG_HEAD
+  PTG_RETURN_LAUNCH();
+}
+
+// out = act(sum over nparts slices [nparts][M][N] of part + bias[n]) (dense.hip split-K partials);
+// N % 4 == 0, 16-B vectors
+__global__ __launch_bounds__(256) void bias_act_parts_k(const float4* __restrict__ part, const float* __restrict__ bias,
+                                                        uint2* __restrict__ out, float4* __restrict__ out32,
+                                                        long total4, int N, int act, int nparts) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total4; i += (long)gridDim.x * 256) {
+    float4 v = part[i];
+    for (int p = 1; p < nparts; ++p) {
+      const float4 u = part[p * total4 + i];
+      v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
+    }
+    if (bias) {  // (a parameter view of the flat store: not necessarily 16-B aligned)
+      const float* b = bias + (i * 4) % N;
+      v.x += b[0]; v.y += b[1]; v.z += b[2]; v.w += b[3];
+    }
+    if (act == 1) {
+      v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+    }
+    if (out) out[i] = make_uint2(pack_bf(v.x, v.y), pack_bf(v.z, v.w));
+    if (out32) out32[i] = v;
+  }
+}
+
+int ptg_bias_act_parts(const float* part, int nparts, const float* bias, void* out_bf16, float* out32, long M, int N,
+                       int act, hipStream_t s) {
+  if (nparts < 1 || N % 4 || M <= 0) return (int)hipErrorInvalidValue;
+  const long total4 = M * N / 4;
+  hipLaunchKernelGGL(bias_act_parts_k, dim3(grid_for(total4)), dim3(256), 0, s, (const float4*)part, bias,
+                     (uint2*)out_bf16, (float4*)out32, total4, N, act, nparts);
   PTG_RETURN_LAUNCH();
 }
 

@@ -67,6 +67,9 @@ def build_hip(force: bool = False, jobs: int = 8, verbose: bool = True, checked:
     flags = ["--offload-arch=" + ARCH, "-O3", "-fPIC", "-std=c++17", "-munsafe-fp-atomics",
              "-Wno-unused-result", "-I", str(CSRC / "kernels")] + (["-DPTG_CHECKED"] if checked else [])
     flags += [f"-D{d}" for d in defines]
+    if not force and out_lib.exists() and srcs and \
+            out_lib.stat().st_mtime >= max(_newest_dep(s, headers) for s in srcs):
+        return out_lib  # up to date (objects need not exist: a snapshot ships only the library)
     objs, todo = [], []
     for s in srcs:
         o = bdir / (s.stem + ".o")

@@ -109,11 +109,9 @@ _K = [
          "CNN-B1 layers 2-4: PReLU + max-pool backward in the row-pair layout (ppb.hip, dalpha via chunk partials)"),
     Knob("conv1_rec", bool, True, "PTG_CONV1_REC", None, "first conv layer (conv1.hip): forward keeps the pool record, backward needs no recompute (0: recompute z in the backward)"),
     Knob("conv1_fused", bool, True, "PTG_CONV1_FUSED", None, "first conv layer: pooled-only forward + one recomputing backward kernel (conv1.hip)"),
-    Knob("blaslt_dense_fwd", bool, False, "PTG_BLASLT_DENSE_FWD", None,
-         "A/B: the big Dense forward that feeds the fused regression head through hipBLASLt (bf16 in, fp32 out) "
-         "instead of the split-K atomic MFMA GEMM"),
     Knob("dense_fwd_splits", int, 0, "PTG_DENSE_FWD_SPLITS", None,
-         "K-splits of the big Dense forward's atomic MFMA GEMM (0: the default rule, <= 16 and ~512 workgroups)"),
+         "0: the big Dense forward streams its weight through dense.hip (split-K partial slices, plain stores); "
+         ">0: the atomic split-K MFMA GEMM with this many splits (A/B)"),
     Knob("blaslt_dx", bool, True, "PTG_BLASLT_DX", None,
          "big-Dense dX (a plain GEMM) through hipBLASLt instead of the skinny-M MFMA GEMM "
          "(CNN-B1 b256 A/B: 1.642/1.629 vs 1.657/1.650 ms)"),

@@ -457,15 +457,16 @@ class DenseOp(Op):
             acc.add_(x.float() @ self.dense.kernel.bf16.float().t())
             self._x = x
             return acc
-        if BLASLT_DENSE_FWD[0]:
-            # a plain bf16 GEMM with fp32 output: hipBLASLt (the head kernel re-zeroes acc afterwards,
-            # harmless here since the GEMM overwrites it)
-            try:
-                torch.mm(x, self.dense.kernel.bf16.t(), out_dtype=torch.float32, out=acc)
-                self._x = x
-                return acc
-            except (TypeError, RuntimeError):
-                BLASLT_DENSE_FWD[0] = False
+        w = self.dense.kernel.bf16
+        S = K.dense_fwd_splits(B, N, Kd) if (DENSE_FWD_SPLITS <= 0 and x.dtype == torch.bfloat16
+                                             and x.is_contiguous()) else 0
+        if S > 0:
+            # weight-streaming forward: S split-K partial slices with plain stores (no zeroed
+            # accumulator, no atomics); the head / bias pass sums them
+            part = ws.get(self.name + "/headparts", (S, B, N), torch.float32, x.device)
+            K.dense_fwd_parts(x, w, part, S)
+            self._x = x
+            return part
         tiles = -(-B // 128) * -(-N // 128)
         # ~512 workgroups, <= 32 splits of >= 640 (CNN-B1 b32: 32 splits 0.645/0.657 vs 16 splits
         # 0.660/0.667 ms; b256 keeps 16 - 8/12 within noise, 4/6/20/32 slower: r4_ab_dense_fwd_splits.txt)
@@ -560,9 +561,6 @@ class DenseOp(Op):
         return dx
 
 
-# CNN-B1 Dense forward before the fused head (split-K sums in fp32): hipBLASLt with fp32 output
-# instead of our split-K atomic GEMM (A/B option, PTG_BLASLT_DENSE_FWD=1)
-BLASLT_DENSE_FWD = [config.get("blaslt_dense_fwd")]
 DENSE_FWD_SPLITS = config.get("dense_fwd_splits")
 
 

@@ -405,7 +405,7 @@ class Sequential:
         d1, d2 = self.ops[-2], self.ops[-1]
         x = E.run_forward(self.ops[:-2], xb, self.ws, True, pre_op=self._pre_op_hook())
         acc = d1.forward_splitk_sums(x, self.ws)
-        pred = self.ws.get(d2.name + "/tapepred", (acc.shape[0], d2.dense.units), torch.float32, acc.device)
+        pred = self.ws.get(d2.name + "/tapepred", (acc.shape[-2], d2.dense.units), torch.float32, acc.device)
         out = pred.as_subclass(_HeadPred)
         out._lz = self._head_state = _HeadState(self, acc, pred)
         return out
@@ -440,7 +440,7 @@ class Sequential:
             pre(d1)
             pre(d2)
         acc = d1.forward_splitk_sums(x, self.ws)
-        B, K1 = acc.shape
+        B, K1 = acc.shape[-2:]
         dz1 = self.ws.get(d1.name + "/dz", (B, K1), torch.bfloat16, acc.device)
         N2 = d2.dense.units
         scratch = self.ws.get(d1.name + "/headscratch", (B * (N2 + 2),), torch.float32, acc.device)

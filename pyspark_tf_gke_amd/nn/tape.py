@@ -241,7 +241,7 @@ class _HeadState:
         self.state = "plain"
         m = self.model
         d1, d2 = m.ops[-2], m.ops[-1]
-        B, N1 = self.acc.shape
+        B, N1 = self.acc.shape[-2:]
         y1 = m.ws.get(d1.name + "/y", (B, N1), torch.bfloat16, self.acc.device)
         K.bias_act(self.acc, d1.dense.bias.data, "relu", out_bf16=y1, clear=True)
         d1._y = y1
@@ -257,7 +257,7 @@ class _HeadState:
 
         m = self.model
         d1, d2 = m.ops[-2], m.ops[-1]
-        B, K1 = self.acc.shape
+        B, K1 = self.acc.shape[-2:]
         N2 = d2.dense.units
         yb = y_true.float()
         if yb.dim() == 1:

@@ -506,15 +506,52 @@ def gemm(M, N, K, a, lda, a_kcontig, b, ldb, b_kcontig, epi, c, ldc, bias=None, 
         ptr(bias), act, splits)
 
 
+_DFS: dict = {}
+
+
+def dense_fwd_splits(M: int, N: int, K: int) -> int:
+    """K-split count of the weight-streaming forward (dense.hip) for this shape, 0 if it does not
+    apply (M > 256, N % 128, K % 64, ...)."""
+    key = (M, N, K)
+    s = _DFS.get(key)
+    if s is None:
+        from .. import _native
+
+        s = _DFS[key] = int(_native.hip_lib().ptg_dense_fwd_splits(M, N, K))
+    return s
+
+
+def dense_fwd_parts(x, w, part, splits: int):
+    """part[s] (fp32 [S, M, N]) = x[M, K] @ w[N, K]^T over K-split s (dense.hip): every slice is
+    written with plain stores; consumers sum the S slices (head_mse / bias_act on a 3-D tensor)."""
+    M, K = x.shape
+    N = w.shape[0]
+    need(x, torch.bfloat16, "dense_fwd.x")
+    need(w, torch.bfloat16, "dense_fwd.w")
+    assert part.dtype == torch.float32 and part.is_contiguous() and part.numel() >= splits * M * N
+    hip("ptg_dense_fwd_sk", ptr(x), ptr(w), ptr(part), M, N, K, splits)
+    return part
+
+
 def linear_fwd(x, w, bias, act, out, workspace=None, splits: int = 0, workspace_zeroed: bool = False):
-    """out[M,N] bf16 = act(x[M,K] @ w[N,K]^T + bias). Split-K with an fp32 workspace when the
-    output tile grid alone cannot fill the 256 CUs (e.g. M=batch, K=20480).  ``workspace_zeroed``:
-    the workspace holds zeros (a persistent buffer created zeroed): the split-K partial sums land on
-    it directly and the bias/activation pass clears it again for the next call (no fill kernel)."""
+    """out[M,N] bf16 = act(x[M,K] @ w[N,K]^T + bias).  A batch-sized M with a big weight takes the
+    weight-streaming split-K kernel (dense.hip, S partial slices summed by the bias/activation
+    pass); otherwise split-K with an fp32 workspace when the output tile grid alone cannot fill the
+    256 CUs.  ``workspace_zeroed``: the workspace holds zeros (a persistent buffer created zeroed):
+    the atomic split-K sums land on it directly and the bias/activation pass clears it again."""
     if not on_device(x):
         return ref.linear_fwd(x, w, bias, act, out)
     M, K = x.shape
     N = w.shape[0]
+    S = dense_fwd_splits(M, N, K) if (splits == 0 and K >= 4096 and x.dtype == torch.bfloat16
+                                       and w.dtype == torch.bfloat16 and x.is_contiguous()) else 0
+    if S > 0:
+        if workspace is None or workspace.numel() < S * M * N:
+            workspace = torch.empty(S * M * N, device=x.device, dtype=torch.float32)
+        part = workspace[: S * M * N].view(S, M, N)
+        dense_fwd_parts(x, w, part, S)
+        hip("ptg_bias_act_parts", ptr(part), S, ptr(bias), ptr(out), None, M, N, ACT[act])
+        return out
     if splits == 0:
         tiles = math.ceil(M / 128) * math.ceil(N / 128)
         splits = 1 if tiles >= 192 or K < 4096 else min(16, max(1, 512 // max(tiles, 1)), K // 1024)
@@ -598,12 +635,13 @@ def head_mse(acc, b1, w2, b2, tgt, dz1, dw2, db2, db1, stats, pred_out=None, gsc
     re-zeroed): stats / dpred as mse_k, dz1 [B, K1] bf16, dw2 / db2 / db1 accumulated (GPU only)."""
     if not on_device(acc):
         return ref.head_mse(acc, b1, w2, b2, tgt, dz1, dw2, db2, db1, stats, pred_out, gscale)
-    B, K1 = acc.shape
+    B, K1 = acc.shape[-2:]
+    nparts = acc.shape[0] if acc.dim() == 3 else 0  # dense_fwd_parts slices, else atomic sums
     N2 = w2.shape[0]
     if scratch is None or scratch.numel() < B * (N2 + 2):
         scratch = torch.empty(B * (N2 + 2), dtype=torch.float32, device=acc.device)
     hip("ptg_head_mse", ptr(acc), ptr(b1), ptr(w2), ptr(b2), ptr(tgt), ptr(dz1), ptr(dw2), ptr(db2), ptr(db1),
-        ptr(stats), ptr(pred_out), ptr(scratch), B, K1, N2, float(gscale))
+        ptr(stats), ptr(pred_out), ptr(scratch), B, K1, N2, float(gscale), nparts)
 
 
 def col_sum(g, out):
@@ -616,11 +654,16 @@ def col_sum(g, out):
 
 
 def bias_act(acc, bias, act, out_bf16=None, out32=None, clear: bool = False):
-    """act(acc + bias) into out_bf16 / out32; ``clear`` re-zeroes acc (a split-K accumulator)."""
+    """act(acc + bias) into out_bf16 / out32; ``clear`` re-zeroes acc (a split-K accumulator).  A 3-D
+    ``acc`` holds dense_fwd_parts slices [S, M, N], summed here (nothing to clear)."""
     if not on_device(acc):
         ref.bias_act(acc, bias, act, out_bf16, out32)
         if clear:
             acc.zero_()
+        return
+    if acc.dim() == 3:
+        S, M, N = acc.shape
+        hip("ptg_bias_act_parts", ptr(acc), S, ptr(bias), ptr(out_bf16), ptr(out32), M, N, ACT[act])
         return
     M, N = acc.shape
     hip("ptg_bias_act", ptr(acc), ptr(bias), ptr(out_bf16), ptr(out32), M, N, ACT[act], int(clear))
