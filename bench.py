@@ -136,19 +136,15 @@ def _time_steps(model, xs, ys, steps, warmup):
     scope = (torch.cuda.stream(torch.cuda.Stream(priority=prio)) if prio and torch.cuda.is_available()
              else contextlib.nullcontext())
     with scope:
-        # overlapped_steps: a step's big Dense dW+Adam may overlap the next step's conv forward; each
-        # step still launches all of its own kernels, and the scope waits for them before it closes
-        with model.overlapped_steps():
-            for i in range(warmup):
-                model.train_step_fast(xs[i % 2], ys[i % 2], stats)
+        for i in range(warmup):
+            model.train_step_fast(xs[i % 2], ys[i % 2], stats)
         _sync()
         comm.barrier()
         _sync()
         K.fill_(stats, 0.0)
         t0 = time.perf_counter()
-        with model.overlapped_steps():
-            for i in range(steps):
-                model.train_step_fast(xs[i % 2], ys[i % 2], stats)
+        for i in range(steps):
+            model.train_step_fast(xs[i % 2], ys[i % 2], stats)
     _sync()
     comm.barrier()
     _sync()

@@ -242,29 +242,6 @@ int ptg_ipc_close(void* p) { return (int)hipIpcCloseMemHandle(p); }
 int ptg_ipc_free(void* p) { return (int)hipFree(p); }
 int ptg_ipc_handle_bytes() { return (int)sizeof(hipIpcMemHandle_t); }
 
-// A stream whose kernels may only occupy part of the CUs (hipExtStreamCreateWithCUMask): the
-// training step's side stream (weight gradients, the HBM-bound Dense dW+Adam GEMM) can be fenced
-// off so it never takes CUs from the step's dgrad chain.  quarters = 1..4 of the CUs, chosen in
-// blocks of 8 consecutive mask bits (block j kept iff j % 4 < quarters), which spreads them evenly
-// over the 8 XCDs whether the driver numbers CUs XCD-interleaved or XCD-contiguous.
-int ptg_stream_cumask_create(int quarters, void** out) {
-  if (quarters < 1 || quarters > 4) return (int)hipErrorInvalidValue;
-  int dev = 0, ncu = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e != hipSuccess) return (int)e;
-  e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-  if (e != hipSuccess) return (int)e;
-  uint32_t mask[32] = {0};
-  const int words = (ncu + 31) / 32;
-  if (words > 32) return (int)hipErrorInvalidValue;
-  for (int i = 0; i < ncu; ++i)
-    if ((i / 8) % 4 < quarters) mask[i / 32] |= 1u << (i % 32);
-  hipStream_t st = nullptr;
-  e = hipExtStreamCreateWithCUMask(&st, (uint32_t)words, mask);
-  *out = (void*)st;
-  return (int)e;
-}
-
 int ptg_stream_destroy(void* st) { return (int)hipStreamDestroy((hipStream_t)st); }
 
 // in/out: n elements (dtype 0 = fp32, 1 = fp64, 2 = int64); peer_ptrs: host array of world buffer

@@ -31,15 +31,7 @@ namespace ptgc {
 // `z`, shaped like the pooled output) and the argmax position q = 2*dh + dw (uint8, `argout`) -
 // 2.5 bytes per pooled element instead of 8 bytes of z (the first conv layer writes 335 MB less per
 // step at batch 256 and its backward reads 335 MB less).
-enum { EPI_Z = 0, EPI_POOL = 1, EPI_PRELU = 2, EPI_POOLS = 3, EPI_PPB = 4 };
-// EPI_PPB (dgrad of the layer above a Conv + PReLU + MaxPool(2x2) block): the kernel's output is the
-// pooled gradient dA of that block ([N][H][W][Cout], written to z as with EPI_Z), and the epilogue
-// also turns it into the block's pre-activation gradient dZ = d/dz maxpool(prelu(z)) at full
-// resolution ([N][2H][2W][Cout] into aux) from the block's forward z (passed through `argout`,
-// [N][2H][2W][Cout] bf16) and its per-element alpha (`alpha`, [2H][2W][Cout] fp32): the argmax of
-// each window (first maximum in q = 2*dh + dw order) gets dA (times alpha where z <= 0), the rest 0 -
-// exactly prelu_pool_bwd_sg_k's dz, so that kernel leaves the critical path (it still runs on the
-// side stream, without stores, for dalpha / dbias).
+enum { EPI_Z = 0, EPI_POOL = 1, EPI_PRELU = 2, EPI_POOLS = 3 };
 
 template <int C> struct PixPitch { static constexpr int v = C >= 16 ? C + 8 : C; };  // bank-conflict pad (wgrad)
 // forward halo: pixel pitch and per-row pad (elements) chosen with tools/lds_bank_sim.py so the
@@ -303,7 +295,7 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
   // SMAJ (no halo ring, PReLU epilogue): tiles are ordered position-major, sample-minor, so the
   // consecutive tiles of a workgroup share one output position and the per-element PReLU alphas
   // (for CNN-B1 layer 2 16 KB per tile, more than its halo) stay in registers across samples
-  constexpr bool SMAJ = !RING && EPI != EPI_Z && EPI != EPI_PPB;
+  constexpr bool SMAJ = !RING && EPI != EPI_Z;
   // tile t -> (sample n, column strip twi, row tile th); divisions only for a range's first tile,
   // then the next tile is stepped incrementally (each runtime 32-bit division is ~40 scalar and
   // vector instructions, and the tile loop did six of them per tile)
@@ -327,8 +319,7 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
       if (++th_ == tiles_h) { th_ = 0; if (++twi_ == tiles_w) { twi_ = 0; ++n_; } }
     }
   };
-  float4 al[(EPI != EPI_Z && EPI != EPI_PPB) ? FM : 1][NF];
-  const bf16_t* __restrict__ zin = reinterpret_cast<const bf16_t*>(argout);  // EPI_PPB only
+  float4 al[EPI != EPI_Z ? FM : 1][NF];
   __shared__ int s_wq;
   for (int round = 0;; ++round) {
   int t0, t1;
@@ -368,7 +359,7 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
 
     // alpha for this lane's (pixel, 4 channels) of every fragment, needed after the MFMAs
     const int pos = twi * tiles_h + th;
-    if constexpr (EPI != EPI_Z && EPI != EPI_PPB) {
+    if constexpr (EPI != EPI_Z) {
       if (pos != apos) {
         apos = pos;
 #pragma unroll
@@ -548,48 +539,7 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
         const bool in = cval && oh < H && ow < W;
         const long o = (((long)n * H + oh) * W + ow) * Cout + co0;
         if (in) *(U2*)(z + PTG_CHECKED_IDX(o, (long)N * H * W * Cout)) = U2{pack_bf(zr[0], zr[1]), pack_bf(zr[2], zr[3])};
-        if constexpr (EPI == EPI_PPB) {
-          if (in) {
-            // zr = this pooled element's gradient (bf16-rounded, as prelu_pool_bwd_sg_k reads it)
-            // alpha of the 4 window pixels straight from L2 (shared by every sample; caching it in
-            // registers across a position-major tile order cost occupancy)
-            const long W2 = 2L * W, zb = (((long)n * 2 * H + 2 * oh) * W2 + 2 * ow) * Cout + co0;
-            const long ab = ((long)(2 * oh) * W2 + 2 * ow) * Cout + co0;
-            U2 zq[4];
-            float4 aq[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              zq[q] = *(const U2*)(zin + zb + ((q >> 1) * W2 + (q & 1)) * Cout);
-              aq[q] = *(const float4*)(alpha + ab + ((q >> 1) * W2 + (q & 1)) * Cout);
-            }
-            float ov[4][4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              float zv[4], yv[4], av[4];
-#pragma unroll
-              for (int q = 0; q < 4; ++q) {
-                const uint32_t word = (r >> 1) ? zq[q].y : zq[q].x;
-                zv[q] = (r & 1) ? hi_bf(word) : lo_bf(word);
-                av[q] = r == 0 ? aq[q].x : r == 1 ? aq[q].y : r == 2 ? aq[q].z : aq[q].w;
-                yv[q] = zv[q] > 0.f ? zv[q] : av[q] * zv[q];
-              }
-              int am = 0;
-              float best = yv[0];
-#pragma unroll
-              for (int q = 1; q < 4; ++q)
-                if (yv[q] > best) { best = yv[q]; am = q; }  // first maximum in q order
-#pragma unroll
-              for (int q = 0; q < 4; ++q) {
-                const float gq = am == q ? zr[r] : 0.f;
-                ov[q][r] = zv[q] > 0.f ? gq : gq * av[q];
-              }
-            }
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-              *(U2*)(aux + PTG_CHECKED_IDX(zb + ((q >> 1) * W2 + (q & 1)) * Cout, (long)N * 4 * H * W * Cout)) =
-                  U2{pack_bf(ov[q][0], ov[q][1]), pack_bf(ov[q][2], ov[q][3])};
-          }
-        } else if constexpr (EPI != EPI_Z) {
+        if constexpr (EPI != EPI_Z) {
           const float a4[4] = {al[i][j].x, al[i][j].y, al[i][j].z, al[i][j].w};
 #pragma unroll
           for (int r = 0; r < 4; ++r) y[i][r] = zr[r] > 0.f ? zr[r] : a4[r] * zr[r];
@@ -1259,12 +1209,6 @@ static int launch_fwd(const void* x, const void* w, const float* bias, const flo
   if (epi == EPI_POOL) return launch_fwd_e<C, KS, NF, TW, TH, EPI_POOL>(x, w, bias, alpha, z, aux, arg, N, H, W, Cout, pad, s);
   if (epi == EPI_POOLS) return launch_fwd_e<C, KS, NF, TW, TH, EPI_POOLS>(x, w, bias, alpha, z, aux, arg, N, H, W, Cout, pad, s);
   if (epi == EPI_PRELU) return launch_fwd_e<C, KS, NF, TW, TH, EPI_PRELU>(x, w, bias, alpha, z, aux, arg, N, H, W, Cout, pad, s);
-  if (epi == EPI_PPB) {  // instantiated for the dgrads that feed a pooled 5x5 block (CNN-B1 layers 3-5)
-    if constexpr (KS == 5 && C >= 32)
-      return launch_fwd_e<C, KS, NF, TW, TH, EPI_PPB>(x, w, bias, alpha, z, aux, arg, N, H, W, Cout, pad, s);
-    else
-      return (int)hipErrorInvalidValue;
-  }
   return launch_fwd_e<C, KS, NF, TW, TH, EPI_Z>(x, w, bias, alpha, z, aux, arg, N, H, W, Cout, pad, s);
 }
 
@@ -1351,15 +1295,12 @@ extern "C" {
 
 // stride-1 'same'-style conv with halo tiling. C in {4,8,16,32,64}, Cout % 8 == 0 and <= 64, KS in {3,5}.
 // epi: 0 = z only, 1 = z + maxpool2x2(prelu(z)) into aux (H, W even), 2 = z + prelu(z) into aux,
-// 3 = maxpool2x2(prelu(z)) into aux + argmax z into z ([N][H/2][W/2][Cout]) + argmax q into arg,
-// 4 = dgrad into z + the pooled block's dZ into aux ([N][2H][2W][Cout]) from its forward z (`arg`,
-//     bf16 [N][2H][2W][Cout]) and alpha ([2H][2W][Cout]) - EPI_PPB above; KS == 5, C >= 32 only.
+// 3 = maxpool2x2(prelu(z)) into aux + argmax z into z ([N][H/2][W/2][Cout]) + argmax q into arg.
 int ptg_conv2d_fwd_halo(const void* x, const void* w, const float* bias, const float* alpha, void* z, void* aux, void* arg, int N,
                         int H, int W, int C, int Cout, int KS, int pad, int epi, hipStream_t s) {
   if (Cout % 8 || Cout > 64 || !ptg_fits_2g((long)N * H * W * C * 2)) return (int)hipErrorInvalidValue;
   if ((epi == EPI_POOL || epi == EPI_POOLS) && ((H & 1) || (W & 1))) return (int)hipErrorInvalidValue;
-  if (epi == EPI_PPB && (!arg || !aux || !alpha || !ptg_fits_2g((long)N * 4 * H * W * Cout * 2)))
-    return (int)hipErrorInvalidValue;
+  if (epi < EPI_Z || epi > EPI_POOLS) return (int)hipErrorInvalidValue;
   if (C == 4 && Cout == 8 && KS == 5 && (epi == EPI_POOL || epi == EPI_POOLS) && pad == 2 && conv1_pair_enabled()) {
     const auto kern = epi == EPI_POOLS ? conv1_pair_pool_k<5, true> : conv1_pair_pool_k<5, false>;
     static const int res_dense = ptg_resident_blocks((const void*)conv1_pair_pool_k<5, false>);

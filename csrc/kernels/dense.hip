@@ -180,6 +180,185 @@ static int launch_fwd(const bf16_t* x, const bf16_t* w, float* part, int M, int 
   PTG_RETURN_LAUNCH();
 }
 
+
+// ------------------------------------------------------------------------------------------------
+// dX of the big Dense layer: out[M][Kc] (bf16) = dy[M][Nr] . W[Nr][Kc]  (CNN-B1: Nr = 2048 units,
+// Kc = 20480 inputs).  The weight is k-major for this product (W[n][k] with the reduction index n
+// in the rows), the MFMA B operand needs 8 consecutive n per lane: W tiles go through LDS and are
+// read with the transposed LDS read ds_read_b64_tr_b16 (cdna_hip_programming.md T10).
+//   * grid = Kc / 80 workgroups (256 for CNN-B1), each all M rows x 80 output columns over the
+//     whole reduction: every weight byte is read once, no split-K partials.
+//   * 8 waves x 32 rows.  A wave's dy rows are private to it, so its A fragments come straight
+//     from global memory into registers (16 B per lane = one 16x16x32 fragment row, L2 hits: dy is
+//     1 MB), prefetched P K-steps ahead in a register ring; only the shared W tiles use LDS.
+//   * W stage = 64 rows x 80 cols (10 KB) by LDS-DMA, 10 wave-instructions per stage (2 per wave;
+//     the 6 spare ones land OOB zeros in a scratch KB).  Inside each 16-row group the rows are
+//     stored interleaved (global row 8h+r -> LDS row 2r+h) so that the two 4-row blocks a 32-lane
+//     half reads in one transposed read fall on disjoint banks (row stride 160 B = 40 banks).
+//   * per stage per wave 4 A loads + 2 DMA = 6 vector-memory ops in issue order: one counted
+//     s_waitcnt vmcnt(6 (P-1)) + a barrier retires stage t for everyone.
+// ------------------------------------------------------------------------------------------------
+constexpr int DX_KT = 80, DX_BK = 64;
+constexpr int DX_IMG = DX_BK * DX_KT * 2;  // 10 KB
+constexpr int DX_SLOT = DX_IMG + 1024;     // + DMA scratch
+
+// Row placement inside a 64-row W stage (an involution): bit 2 flips with bit 4.  LDS rows 160 B
+// apart start 40 banks apart, so any 8 rows with distinct (row mod 8) start on the 8 distinct 8-bank
+// groups; each transposed read of a 32-lane half covers rows {16g+8s+4h+q} for the half's two lane
+// groups g = 2c, 2c+1 (q = 0..3), which this placement maps to 8 distinct residues mod 8.
+PTG_DEV int dx_lds_row(int k) { return k ^ (((k >> 4) & 1) << 2); }
+PTG_DEV int dx_glb_row(int kk) { return kk ^ (((kk >> 4) & 1) << 2); }
+
+// ds_read_b64_tr_b16 as inline asm: the builtin form carries no alias information, so hipcc
+// drains every LDS-DMA in flight (s_waitcnt vmcnt(0)) before each one, which serialises the
+// weight stream.  The asm result is only valid after an lgkmcnt wait: dx_lgkm_fence() below, whose
+// "+v" operands order every consumer (the MFMAs) after it.
+typedef __attribute__((ext_vector_type(2))) unsigned dx_u2_t;
+PTG_DEV dx_u2_t dx_tr_read(uint32_t lds_addr) {
+  dx_u2_t r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(lds_addr));
+  return r;
+}
+PTG_DEV void dx_lgkm_fence(dx_u2_t (&r)[10]) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]), "+v"(r[6]), "+v"(r[7]),
+                 "+v"(r[8]), "+v"(r[9]));
+}
+PTG_DEV uint32_t dx_lds_addr(const unsigned char* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) unsigned char*)p;
+}
+
+template <int P>
+__global__ __launch_bounds__(512) void dense_dx_k(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ w,
+                                                  bf16_t* __restrict__ out, int M, int Nr, int Kc, uint32_t dybytes,
+                                                  uint32_t wbytes) {
+  constexpr int NS = P + 1;
+  extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int col0 = blockIdx.x * DX_KT;
+  const int nk = Nr / DX_BK;
+  const bool live = wid * 32 < M;  // waves whose rows are all past M only move bytes
+  const uint32_t lds0 = dx_lds_addr(smem);
+
+  const Rsrc rsA = make_rsrc(dy, dybytes), rsB = make_rsrc(w, wbytes);
+  uint32_t aoff[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = wid * 32 + i * 16 + (lane & 15);
+    // lane group g holds k = 16g + 8s .. +7 of a 64-deep stage (s = the 32-deep MFMA step): its two
+    // fragments are 32 contiguous bytes of the dy row
+    aoff[i] = r < M ? (uint32_t)r * (uint32_t)Nr * 2u + 32u * (uint32_t)(lane >> 4) : PTG_OOB;
+  }
+  uint32_t boff[2];
+  int bdst[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int b = wid + 8 * j;
+    if (b < 10) {
+      const int f = b * 64 + lane, kk = f / 10, c8 = f - kk * 10;
+      boff[j] = (uint32_t)dx_glb_row(kk) * (uint32_t)Kc * 2u + (uint32_t)(col0 + c8 * 8) * 2u;
+      bdst[j] = b * 1024;
+    } else {
+      boff[j] = PTG_OOB;
+      bdst[j] = DX_IMG;
+    }
+  }
+  const uint32_t bstep = (uint32_t)DX_BK * (uint32_t)Kc * 2u;
+
+  bf16x8_t areg[NS][2][2];  // [slot][k32 half][row fragment]
+  f32x4_t acc[2][5];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 5; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // tr-read geometry: lane group g = lane>>4 takes k rows 16g+8s .. +7 of MFMA step s (the order of
+  // its A fragment); within the group lane 4q+p addresses row q, columns 4p..4p+3 of the 16-column block
+  const int g = lane >> 4, q = (lane & 15) >> 2, pq = lane & 3;
+  int trow[2][2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) trow[s][h] = dx_lds_row(16 * g + 8 * s + 4 * h + q) * (DX_KT * 2) + pq * 8;
+
+#define DX_ISSUE(T, SL)                                                                                         \
+  {                                                                                                             \
+    const int t_ = (T);                                                                                         \
+    _Pragma("unroll") for (int s_ = 0; s_ < 2; ++s_)                                                            \
+      _Pragma("unroll") for (int i_ = 0; i_ < 2; ++i_)                                                          \
+        areg[SL][s_][i_] = __builtin_bit_cast(bf16x8_t, bload16(rsA, (aoff[i_] == PTG_OOB || t_ >= nk) ? PTG_OOB  \
+                                                                       : aoff[i_] + (uint32_t)(t_ * DX_BK + s_ * 8) * 2u)); \
+    unsigned char* base_ = smem + (SL) * DX_SLOT;                                                               \
+    _Pragma("unroll") for (int j_ = 0; j_ < 2; ++j_)                                                            \
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_t*)(base_ + bdst[j_]), 16,                             \
+                                               boff[j_] == PTG_OOB ? PTG_OOB : boff[j_] + (uint32_t)t_ * bstep, \
+                                               0, 0, 0);                                                        \
+  }
+// Every step issues its 6 loads unconditionally (stages past the end read OOB zeros, steps past the
+// end add zeros): uniform control flow lets hipcc track the register ring's loads exactly; a
+// conditional issue made it wait for the newest loads before every MFMA group.
+#define DX_STEP(T, SL)                                                                                          \
+  {                                                                                                             \
+    wait_vm<6 * (P - 1)>();                                                                                     \
+    __builtin_amdgcn_s_barrier();                                                                               \
+    DX_ISSUE((T) + P, ((SL) + P) % NS)                                                                          \
+    if (live) {                                                                                                 \
+      const uint32_t img_ = lds0 + (SL) * DX_SLOT;                                                              \
+      _Pragma("unroll") for (int s_ = 0; s_ < 2; ++s_) {                                                        \
+        dx_u2_t tr_[10];                                                                                        \
+        _Pragma("unroll") for (int j_ = 0; j_ < 5; ++j_) {                                                      \
+          tr_[2 * j_] = dx_tr_read(img_ + trow[s_][0] + j_ * 32);                                               \
+          tr_[2 * j_ + 1] = dx_tr_read(img_ + trow[s_][1] + j_ * 32);                                           \
+        }                                                                                                       \
+        dx_lgkm_fence(tr_);                                                                                     \
+        bf16x8_t bf_[5];                                                                                        \
+        _Pragma("unroll") for (int j_ = 0; j_ < 5; ++j_) {                                                      \
+          U4 v_;                                                                                                \
+          v_.x = tr_[2 * j_].x; v_.y = tr_[2 * j_].y; v_.z = tr_[2 * j_ + 1].x; v_.w = tr_[2 * j_ + 1].y;       \
+          bf_[j_] = __builtin_bit_cast(bf16x8_t, v_);                                                           \
+        }                                                                                                       \
+        _Pragma("unroll") for (int i_ = 0; i_ < 2; ++i_)                                                        \
+          _Pragma("unroll") for (int j_ = 0; j_ < 5; ++j_)                                                      \
+            acc[i_][j_] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(areg[SL][s_][i_], bf_[j_], acc[i_][j_], 0, 0, 0); \
+      }                                                                                                         \
+    }                                                                                                           \
+  }
+
+#pragma unroll
+  for (int t = 0; t < P; ++t) DX_ISSUE(t, t)
+  for (int t0 = 0; t0 < nk; t0 += NS) {
+    DX_STEP(t0 + 0, 0)
+    if constexpr (NS > 1) { DX_STEP(t0 + 1, 1 % NS) }
+    if constexpr (NS > 2) { DX_STEP(t0 + 2, 2 % NS) }
+    if constexpr (NS > 3) { DX_STEP(t0 + 3, 3 % NS) }
+    if constexpr (NS > 4) { DX_STEP(t0 + 4, 4 % NS) }
+    if constexpr (NS > 5) { DX_STEP(t0 + 5, 5 % NS) }
+  }
+#undef DX_STEP
+#undef DX_ISSUE
+
+  // epilogue: the tile through LDS as bf16 [256][80] (160-B rows), then 16-B coalesced row stores
+  wait_vm<0>();
+  __syncthreads();
+  bf16_t* stile = (bf16_t*)smem;
+  if (live) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 5; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          stile[(wid * 32 + i * 16 + (lane >> 4) * 4 + r) * DX_KT + j * 16 + (lane & 15)] = f2bf(acc[i][j][r]);
+  }
+  __syncthreads();
+  const int rows = min(M, 256);
+  for (int c = tid; c < rows * 10; c += 512) {
+    const int r = c / 10, c8 = c - r * 10;
+    *(U4*)(out + (long)r * Kc + col0 + c8 * 8) = *(const U4*)(stile + r * DX_KT + c8 * 8);
+  }
+}
+
 }  // namespace ptgd
 
 using namespace ptgd;
@@ -212,6 +391,20 @@ int ptg_dense_fwd_sk(const void* x, const void* w, float* part, int M, int N, in
   if (M > 64) return launch_fwd<128>(xb, wb, part, M, N, K, splits, s);
   if (M > 32) return launch_fwd<64>(xb, wb, part, M, N, K, splits, s);
   return launch_fwd<32>(xb, wb, part, M, N, K, splits, s);
+}
+
+
+// dX of a big Dense layer: out[M][Kc] bf16 = dy[M][Nr] . w[Nr][Kc] (w row-major [Nr][Kc], the layer's
+// [units][fan_in] weight).  Requirements (checked): M <= 256, Nr % 64 == 0, Kc % 80 == 0, operands
+// < 2 GiB; `out` rows are Kc apart (16-B aligned rows).
+int ptg_dense_dx(const void* dy, const void* w, void* out, int M, int Nr, int Kc, hipStream_t s) {
+  if (M <= 0 || M > 256 || Nr <= 0 || Nr % DX_BK || Kc <= 0 || Kc % DX_KT) return (int)hipErrorInvalidValue;
+  if (!ptg_fits_2g((long)Nr * Kc * 2) || !ptg_fits_2g((long)M * Nr * 2)) return (int)hipErrorInvalidValue;
+  constexpr int P = 4;
+  const int lds = (P + 1) * DX_SLOT;
+  hipLaunchKernelGGL((dense_dx_k<P>), dim3(Kc / DX_KT), dim3(512), lds, s, (const bf16_t*)dy, (const bf16_t*)w,
+                     (bf16_t*)out, M, Nr, Kc, (uint32_t)((long)M * Nr * 2), (uint32_t)((long)Nr * Kc * 2));
+  PTG_RETURN_LAUNCH();
 }
 
 // measurement variants of the forward at M in (128, 256] (tools/dense_bench.py): mode 1 no MFMA, 2 no

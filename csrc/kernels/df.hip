@@ -1673,44 +1673,14 @@ __global__ __launch_bounds__(256) void sort_count_k(const unsigned long long* __
 
 // vals_in == nullptr: payload = row index (first pass of a fresh sort).  VT = unsigned int when the
 // row count fits 32 bits: 12 instead of 16 bytes per row read and written by every pass.
-// Onesweep status word of (tile, digit): [63:56] pass tag (1..255, so no reset between passes),
-// [55:54] 1 = this tile's count only, 2 = inclusive prefix over tiles 0..t, [53:0] the value.
-#define OS_VAL ((1ULL << 54) - 1ULL)
-PTG_DEV unsigned long long os_pack(unsigned tag, unsigned flag, unsigned long long v) {
-  return ((unsigned long long)tag << 56) | ((unsigned long long)flag << 54) | v;
-}
-
-// exclusive scan of one u64 per thread over the 256 threads (wsum: 4 u64 of LDS)
-PTG_DEV unsigned long long block_excl_scan256_u64(unsigned long long c, unsigned long long* wsum) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  unsigned long long incl = c;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const unsigned long long t = __shfl_up(incl, o, 64);
-    if (lane >= o) incl += t;
-  }
-  if (lane == 63) wsum[w] = incl;
-  __syncthreads();
-  unsigned long long pre = 0;
-  for (int q = 0; q < w; ++q) pre += wsum[q];
-  return pre + incl - c;
-}
-
-// ONESWEEP = false: offs holds every (tile, digit) run's output position (sort_count_k +
-// ptg_digit_offsets).  ONESWEEP = true (no count pass): tiles are taken in ticket order; each
-// publishes its digit counts, then finds its runs' positions by decoupled look-back over the
-// status words of the tiles before it, on top of the pass's global digit starts (the scan of
-// hist_all, counted for every pass by ONE read of the keys in sort_hist_all_k).
-template <typename VT, bool ONESWEEP>
+// offs holds every (tile, digit) run's output position (sort_count_k + ptg_digit_offsets).
+template <typename VT>
 __global__ __launch_bounds__(256) void sort_scatter_k(const unsigned long long* __restrict__ keys_in,
                                                       const VT* __restrict__ vals_in, long n,
                                                       unsigned long long base, int shift, int ntiles,
                                                       const long long* __restrict__ offs,
                                                       unsigned long long* __restrict__ keys_out,
-                                                      VT* __restrict__ vals_out,
-                                                      const unsigned long long* __restrict__ hist_all,
-                                                      unsigned long long* __restrict__ status,
-                                                      unsigned int* __restrict__ ticket, unsigned tag) {
+                                                      VT* __restrict__ vals_out) {
   __shared__ unsigned long long sk[ST];
   __shared__ VT sv[ST];
   __shared__ unsigned char sd[ST];
@@ -1719,19 +1689,9 @@ __global__ __launch_bounds__(256) void sort_scatter_k(const unsigned long long* 
   __shared__ unsigned int lstart[SB];
   __shared__ long long goff[SB];
   __shared__ int wsum[4];
-  __shared__ unsigned long long wsum64[4];
-  __shared__ int s_tile;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  int b;
-  unsigned long long dstart = 0;
-  if constexpr (ONESWEEP) {
-    if (tid == 0) s_tile = (int)atomicAdd(ticket, 1u);
-    dstart = block_excl_scan256_u64(hist_all[tid], wsum64);  // (its barrier publishes s_tile)
-    b = s_tile;
-  } else {
-    b = xcd_tile(blockIdx.x, ntiles);
-    goff[tid] = offs[(long)b * SB + tid];  // tile-major: one coalesced 2 KB row
-  }
+  const int b = xcd_tile(blockIdx.x, ntiles);
+  goff[tid] = offs[(long)b * SB + tid];  // tile-major: one coalesced 2 KB row
   const long s0 = (long)b * ST;
   const int nr = (int)((n - s0) < ST ? (n - s0) : ST);
 #pragma unroll
@@ -1783,28 +1743,6 @@ __global__ __launch_bounds__(256) void sort_scatter_k(const unsigned long long* 
     woff[3][tid] = c0 + c1 + c2;
     running = c0 + c1 + c2 + c3;
   }
-  if constexpr (ONESWEEP) {
-    // thread tid = digit tid: publish this tile's count, then look back for the exclusive prefix
-    unsigned long long* st = status + (long)b * SB + tid;
-    __hip_atomic_store(st, os_pack(tag, 1u, running), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    unsigned long long excl = 0;
-    for (int t = b - 1; t >= 0; --t) {
-      unsigned long long sw;
-      long spins = 0;
-      do {
-        sw = __hip_atomic_load(status + (long)t * SB + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (++spins > (1L << 26)) {  // a predecessor never published: report, never hang the GPU
-          atomicOr(ticket + 1, 1u);
-          sw = os_pack(tag, 2u, 0ULL);
-          break;
-        }
-      } while ((unsigned)(sw >> 56) != tag || ((sw >> 54) & 3ULL) == 0ULL);
-      excl += sw & OS_VAL;
-      if (((sw >> 54) & 3ULL) == 2ULL) break;
-    }
-    __hip_atomic_store(st, os_pack(tag, 2u, excl + running), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    goff[tid] = (long long)(dstart + excl);
-  }
   int total;
   const int ls = block_excl_scan256((int)running, wsum, &total);
   lstart[tid] = (unsigned)ls;
@@ -1820,27 +1758,10 @@ __global__ __launch_bounds__(256) void sort_scatter_k(const unsigned long long* 
   __syncthreads();
   for (int i = tid; i < nr; i += 256) {
     const int dd = sd[i];
-    long long dst = PTG_CHECKED_IDX(goff[dd] + (i - (int)lstart[dd]), n);
-    if constexpr (ONESWEEP) dst = dst < n ? dst : n - 1;  // (only after a reported look-back failure)
+    const long long dst = PTG_CHECKED_IDX(goff[dd] + (i - (int)lstart[dd]), n);
     keys_out[dst] = sk[i];
     vals_out[dst] = sv[i];
   }
-}
-
-// every pass's 256-bin digit histogram in ONE read of the keys (onesweep): hist_all[p][d] (u64)
-__global__ __launch_bounds__(256) void sort_hist_all_k(const unsigned long long* __restrict__ keys, long n,
-                                                       unsigned long long base, int passes,
-                                                       unsigned long long* __restrict__ hist_all) {
-  __shared__ unsigned int h[8][SB];
-  for (int i = threadIdx.x; i < 8 * SB; i += 256) (&h[0][0])[i] = 0;
-  __syncthreads();
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
-    const unsigned long long k = keys[i] - base;
-    for (int p = 0; p < passes; ++p) atomicAdd(&h[p][(unsigned)(k >> (8 * p)) & (SB - 1)], 1u);
-  }
-  __syncthreads();
-  for (int p = 0; p < passes; ++p)
-    if (h[p][threadIdx.x]) atomicAdd(&hist_all[p * SB + threadIdx.x], (unsigned long long)h[p][threadIdx.x]);
 }
 
 // part[i] = number of splitters strictly below keys[i] (unsigned order); counts[dest] += 1
@@ -2324,48 +2245,13 @@ int ptg_sort_scatter(const void* keys_in, const void* vals_in, long n, long base
   if (ntiles <= 0) return 0;
   if (v32 && n > 4294967296L) return (int)hipErrorInvalidValue;
   if (v32)
-    hipLaunchKernelGGL((sort_scatter_k<unsigned int, false>), dim3(ntiles), dim3(256), 0, s,
+    hipLaunchKernelGGL((sort_scatter_k<unsigned int>), dim3(ntiles), dim3(256), 0, s,
                        (const unsigned long long*)keys_in, (const unsigned int*)vals_in, n, (unsigned long long)base,
-                       shift, ntiles, (const long long*)offs, (unsigned long long*)keys_out, (unsigned int*)vals_out,
-                       nullptr, nullptr, nullptr, 0u);
+                       shift, ntiles, (const long long*)offs, (unsigned long long*)keys_out, (unsigned int*)vals_out);
   else
-    hipLaunchKernelGGL((sort_scatter_k<long long, false>), dim3(ntiles), dim3(256), 0, s,
+    hipLaunchKernelGGL((sort_scatter_k<long long>), dim3(ntiles), dim3(256), 0, s,
                        (const unsigned long long*)keys_in, (const long long*)vals_in, n, (unsigned long long)base,
-                       shift, ntiles, (const long long*)offs, (unsigned long long*)keys_out, (long long*)vals_out,
-                       nullptr, nullptr, nullptr, 0u);
-  PTG_RETURN_LAUNCH();
-}
-// onesweep: hist_all u64[passes*256] (zeroed by the caller) <- every pass's digit counts
-int ptg_sort_hist_all(const void* keys, long n, long base, int passes, void* hist_all, hipStream_t s) {
-  if (passes < 1 || passes > 8) return (int)hipErrorInvalidValue;
-  int g = grid_n(n);
-  if (g > 1024) g = 1024;
-  if (n <= 0) return 0;
-  hipLaunchKernelGGL(sort_hist_all_k, dim3(g), dim3(256), 0, s, (const unsigned long long*)keys, n,
-                     (unsigned long long)base, passes, (unsigned long long*)hist_all);
-  PTG_RETURN_LAUNCH();
-}
-// one onesweep pass: hist = this pass's 256 digit counts (u64), status u64[256*ntiles] (tag-versioned,
-// zeroed once when allocated), ticket: 2 zeroed u32 for this pass ([0] tile tickets, [1] error flag:
-// a look-back that timed out), tag in 1..255 (differs from the previous pass on this status buffer)
-int ptg_sort_onesweep(const void* keys_in, const void* vals_in, long n, long base, int shift, const void* hist,
-                      void* status, void* ticket, int tag, void* keys_out, void* vals_out, int v32, hipStream_t s) {
-  const int ntiles = (int)((n + ST - 1) / ST);
-  if (ntiles <= 0) return 0;
-  if (tag < 1 || tag > 255 || n >= (1L << 54)) return (int)hipErrorInvalidValue;
-  if (v32 && n > 4294967296L) return (int)hipErrorInvalidValue;
-  if (v32)
-    hipLaunchKernelGGL((sort_scatter_k<unsigned int, true>), dim3(ntiles), dim3(256), 0, s,
-                       (const unsigned long long*)keys_in, (const unsigned int*)vals_in, n, (unsigned long long)base,
-                       shift, ntiles, nullptr, (unsigned long long*)keys_out, (unsigned int*)vals_out,
-                       (const unsigned long long*)hist, (unsigned long long*)status, (unsigned int*)ticket,
-                       (unsigned)tag);
-  else
-    hipLaunchKernelGGL((sort_scatter_k<long long, true>), dim3(ntiles), dim3(256), 0, s,
-                       (const unsigned long long*)keys_in, (const long long*)vals_in, n, (unsigned long long)base,
-                       shift, ntiles, nullptr, (unsigned long long*)keys_out, (long long*)vals_out,
-                       (const unsigned long long*)hist, (unsigned long long*)status, (unsigned int*)ticket,
-                       (unsigned)tag);
+                       shift, ntiles, (const long long*)offs, (unsigned long long*)keys_out, (long long*)vals_out);
   PTG_RETURN_LAUNCH();
 }
 int ptg_range_partition(const void* keys, long n, const void* split, int nsplit, void* part, void* counts,

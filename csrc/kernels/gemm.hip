@@ -289,10 +289,6 @@ struct EpiBf16 {  // out[m*ldc+n] = act(acc + bias[n]) (+ out if accum) as bf16 
   static constexpr bool STATS = true;
   bf16_t* out; long ldc; const float* bias; int act; float* out32; int accum; float* stats = nullptr;
   const bf16_t* bz = nullptr; const float* bsc = nullptr; const float* bsh = nullptr;
-  // PReLU-backward second output (out2 != nullptr): out2 = d/dz prelu(pz, palpha[n]) applied to the
-  // stored (bf16) value - the data gradient of a Dense layer fed by a PReLU conv block (CNN-B1's
-  // Flatten(conv5) -> Dense) hands that block its dZ, so prelu_bwd's dz pass leaves the step stream
-  bf16_t* out2 = nullptr; const bf16_t* pz = nullptr; const float* palpha = nullptr;
   // backward form: mask v in place with the block's ReLU and return its z values in zz
   PTG_DEV void bwd_prep(int m, int n, float* v, int cnt, float* zz) const {
     const bf16_t* zp = bz + (long)m * ldc + n;
@@ -327,21 +323,6 @@ struct EpiBf16 {  // out[m*ldc+n] = act(acc + bias[n]) (+ out if accum) as bf16 
       for (int j = 0; j < cnt; ++j) out32[(long)m * ldc + n + j] = accum ? v[j] + bf2f(out[(long)m * ldc + n + j]) : v[j];
     }
     bf16_store8(out + (long)m * ldc + n, v, cnt, accum);
-    if (out2) {
-      const bf16_t* zp = pz + (long)m * ldc + n;
-      float zz[8], d[8];
-      if (cnt == 8 && al16(zp)) {
-        unpack8(*(const U4*)zp, zz);
-      } else {
-        for (int j = 0; j < 8; ++j) zz[j] = j < cnt ? bf2f(zp[j]) : 0.f;
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float g = bf2f(f2bf(v[j]));
-        d[j] = j < cnt ? (zz[j] > 0.f ? g : g * palpha[n + j]) : 0.f;
-      }
-      bf16_store8(out2 + (long)m * ldc + n, d, cnt, 0);
-    }
   }
 };
 // Strided scatter (dgrad of a 1x1 stride-s conv): GEMM row m = output pixel (n, oh, ow) lands on
@@ -1245,22 +1226,6 @@ int ptg_gemm_bf16(int M, int N, int K, const void* A, long lda, int a_kcontig, c
     PTG_EPI_SWITCH(la, lb)
   }
 #undef PTG_EPI_SWITCH
-}
-
-// Dense data gradient out[M][K] = dy[M][N] @ w[N][K] (as ptg_gemm_bf16 with a k-contiguous dy and
-// an [N][K] weight), plus out2 = out * prelu'(z) with per-column alpha[K] (EpiBf16 out2 form).
-int ptg_linear_dx_prelu(int M, int N, int K, const void* dy, const void* w, void* out, void* out2, const void* z,
-                        const float* alpha, hipStream_t s) {
-  if (M <= 0 || N <= 0 || K <= 0 || N % 8 || K % 8 || !out2 || !z || !alpha) return (int)hipErrorInvalidValue;
-  if (!fits(matk_bytes(N, M, N)) || !fits(matmn_bytes(K, K, N)) || !fits((long)M * K * 2))
-    return (int)hipErrorInvalidValue;
-  MatK<8> la{(const bf16_t*)dy, N, M, N, (uint32_t)matk_bytes(N, M, N)};
-  MatMN lb{(const bf16_t*)w, K, K, N, (uint32_t)matmn_bytes(K, K, N)};
-  EpiBf16 epi{(bf16_t*)out, K, nullptr, ACT_NONE, nullptr, 0};
-  epi.out2 = (bf16_t*)out2;
-  epi.pz = (const bf16_t*)z;
-  epi.palpha = alpha;
-  return dispatch_gemm(la, lb, epi, M, K, N, 1, s);
 }
 
 // Weight gradient with Adam fused into the epilogue (EpiAdam): G[M][N] = A^T-style product as in

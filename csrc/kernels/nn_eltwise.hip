@@ -753,6 +753,90 @@ __global__ __launch_bounds__(256) void head_row_k(float* __restrict__ acc, const
   }
 }
 
+// head_row_k for split-K partial slices (dense.hip forward), K1 % 4 == 0 and K1 <= 4 * 512: one
+// workgroup per row, one float4 column group per thread, all NP slice loads of a thread issued
+// before the first add (the slices are HBM / Infinity-Cache reads: a load-add-load loop exposes
+// their latency NP times).  Leaves h = relu(sum + b1) in slice 0 for head_col_k.
+template <int N2, int NP>
+__global__ __launch_bounds__(512) void head_row_parts_k(float* __restrict__ acc, const float* __restrict__ b1,
+                                                        const float* __restrict__ w2, const float* __restrict__ b2,
+                                                        const float* __restrict__ tgt, bf16_t* __restrict__ dz1,
+                                                        float* __restrict__ dpred, float* __restrict__ rowerr,
+                                                        float* __restrict__ pred_out, int B, int K1, float gscale,
+                                                        int nparts) {
+  __shared__ float red[8][N2];
+  __shared__ float sdp[N2];
+  const int m = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int k = tid * 4;
+  const bool on = k < K1;
+  float4* arow = (float4*)(acc + (long)m * K1);
+  const long ps4 = (long)B * K1 / 4;
+  float4 h = make_float4(0.f, 0.f, 0.f, 0.f);
+  float dot[N2];
+#pragma unroll
+  for (int n = 0; n < N2; ++n) dot[n] = 0.f;
+  if (on) {
+    float4 u[NP];
+#pragma unroll
+    for (int p = 0; p < NP; ++p) u[p] = p < nparts ? arow[p * ps4 + tid] : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int p = NP; p < nparts; ++p) {  // (more slices than the template holds)
+      const float4 v = arow[p * ps4 + tid];
+      u[0].x += v.x; u[0].y += v.y; u[0].z += v.z; u[0].w += v.w;
+    }
+    float4 a = u[0];
+#pragma unroll
+    for (int p = 1; p < NP; ++p) { a.x += u[p].x; a.y += u[p].y; a.z += u[p].z; a.w += u[p].w; }
+    h.x = fmaxf(a.x + b1[k], 0.f); h.y = fmaxf(a.y + b1[k + 1], 0.f);
+    h.z = fmaxf(a.z + b1[k + 2], 0.f); h.w = fmaxf(a.w + b1[k + 3], 0.f);
+    arow[tid] = h;
+#pragma unroll
+    for (int n = 0; n < N2; ++n) {
+      const float* wn = w2 + (long)n * K1 + k;
+      dot[n] = h.x * wn[0] + h.y * wn[1] + h.z * wn[2] + h.w * wn[3];
+    }
+  }
+#pragma unroll
+  for (int n = 0; n < N2; ++n) {
+    const float v = wave_sum(dot[n]);
+    if (lane == 0) red[w][n] = v;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const float inv = 1.f / (float)(B * N2);
+    float se = 0.f, ae = 0.f;
+#pragma unroll
+    for (int n = 0; n < N2; ++n) {
+      float p = b2[n];
+#pragma unroll
+      for (int ww = 0; ww < 8; ++ww) p += red[ww][n];
+      const float d = p - tgt[(long)m * N2 + n];
+      se += d * d;
+      ae += fabsf(d);
+      sdp[n] = 2.f * d * inv * gscale;
+      dpred[(long)m * N2 + n] = sdp[n];
+      if (pred_out) pred_out[(long)m * N2 + n] = p;
+    }
+    rowerr[2 * m] = se;
+    rowerr[2 * m + 1] = ae;
+  }
+  __syncthreads();
+  if (on) {
+    float g[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int n = 0; n < N2; ++n) {
+      const float d = sdp[n];
+      const float* wn = w2 + (long)n * K1 + k;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) g[j] = fmaf(d, wn[j], g[j]);
+    }
+    const float hv[4] = {h.x, h.y, h.z, h.w};
+    uint2 o;
+    o.x = pack_bf(hv[0] > 0.f ? g[0] : 0.f, hv[1] > 0.f ? g[1] : 0.f);
+    o.y = pack_bf(hv[2] > 0.f ? g[2] : 0.f, hv[3] > 0.f ? g[3] : 0.f);
+    *(uint2*)(dz1 + (long)m * K1 + k) = o;
+  }
+}
+
 template <int N2>
 __global__ __launch_bounds__(256) void head_col_k(float* __restrict__ acc, const float* __restrict__ b1,
                                                   const float* __restrict__ w2, const float* __restrict__ dpred,
@@ -1173,9 +1257,17 @@ int ptg_head_mse(void* acc, const float* b1, const float* w2, const float* b2, c
   float* dpred = scratch;
   float* rowerr = scratch + (long)B * N2;
   const dim3 gc((K1 + 255) / 256, HEAD_RG);
+  const bool vec = nparts > 0 && K1 % 4 == 0 && K1 <= 4 * 512;
 #define PTG_HEAD(NN)                                                                                          \
-  hipLaunchKernelGGL(head_row_k<NN>, dim3(B), dim3(256), 0, s, (float*)acc, b1, w2, b2, tgt, (bf16_t*)dz1,       \
-                     dpred, rowerr, pred_out, B, K1, gscale, nparts);                                         \
+  if (vec && nparts <= 8)                                                                                     \
+    hipLaunchKernelGGL((head_row_parts_k<NN, 8>), dim3(B), dim3(512), 0, s, (float*)acc, b1, w2, b2, tgt,     \
+                       (bf16_t*)dz1, dpred, rowerr, pred_out, B, K1, gscale, nparts);                         \
+  else if (vec)                                                                                               \
+    hipLaunchKernelGGL((head_row_parts_k<NN, 16>), dim3(B), dim3(512), 0, s, (float*)acc, b1, w2, b2, tgt,    \
+                       (bf16_t*)dz1, dpred, rowerr, pred_out, B, K1, gscale, nparts);                         \
+  else                                                                                                        \
+    hipLaunchKernelGGL(head_row_k<NN>, dim3(B), dim3(256), 0, s, (float*)acc, b1, w2, b2, tgt, (bf16_t*)dz1,     \
+                       dpred, rowerr, pred_out, B, K1, gscale, nparts);                                       \
   hipLaunchKernelGGL(head_col_k<NN>, gc, dim3(256), 0, s, (float*)acc, b1, w2, dpred, rowerr, dw2, db2, db1,    \
                      stats, B, K1, nparts)
   switch (N2) {

@@ -52,10 +52,6 @@ _K = [
          "sparse keys at ~64K..1.3M groups: one 512-way hash partition + LDS hash tables (sum/count/avg, <= 2 columns)"),
     Knob("groupby_h9_chunks", int, 4, "PTG_H9_CHUNKS", "spark.ptg.groupby.h9Chunks",
          "row chunks per partition in the 512-way hash aggregation (workgroups = 512 x chunks)"),
-    Knob("sort_onesweep", bool, False, "PTG_SORT_ONESWEEP", "spark.ptg.sort.onesweep",
-         "radix sort passes without a count pass: every pass's digit histogram from one read, tile offsets by "
-         "decoupled look-back (onesweep; 1B rows: 157.6 vs 134.0 ms for count + scatter, the cross-XCD "
-         "coherent look-back polls cost more than the saved key read, so off)"),
     Knob("shuffle_buffer_gb", float, 64.0, "PTG_SHUFFLE_BUFFER_GB", "spark.ptg.shuffle.buffer.gb",
          "HBM staging budget of one all-to-all-v shuffle round"),
     Knob("device", str, "", "PTG_DEVICE", "spark.ptg.device", "executor device: cuda / cpu (default: cuda if present)"),
@@ -63,21 +59,11 @@ _K = [
     Knob("fault_task", int, 0, "PTG_FAULT_TASK", None, "fault injection: fail this many stage-task attempts"),
     # training step
     Knob("fused_adam", bool, True, "PTG_FUSED_ADAM", None, "Adam inside the big Dense weight-gradient GEMM epilogue (1 GPU)"),
-    Knob("defer_dense_update", bool, False, "PTG_DEFER_DENSE_UPDATE", None,
-         "inside fit()/bench step loops: the big Dense dW+Adam GEMM runs under the next step's conv forward "
-         "instead of under this step's backward (A/B on CNN-B1 b256: 1.70-1.71 vs 1.65-1.66 ms, so off)"),
-    Knob("dense_adam_after", int, 0, "PTG_DENSE_ADAM_AFTER", None,
-         "CNN-B1: fork the Dense dW+Adam GEMM after the k-th conv op's backward (0 = right after the Dense dX)"),
     Knob("mlp_fused", bool, True, "PTG_MLP_FUSED", None,
          "a model that is only a small Dense stack (the CSV MLP) runs each training step as ONE kernel (mlp.hip)"),
     Knob("fused_head", bool, True, "PTG_FUSED_HEAD", None, "CNN-B1 Dense(relu)->Dense->MSE head as two kernels"),
     Knob("device_feed", bool, True, "PTG_DEVICE_FEED", None, "fit(): pinned ring + side-stream H2D for host datasets"),
     Knob("side_stream", bool, True, "PTG_SIDE_STREAM", None, "weight gradients on a side HIP stream (1 replica)"),
-    Knob("side_cu_quarters", int, 4, "PTG_SIDE_CU_QUARTERS", None,
-         "side stream confined to 1-3 quarters of the CUs (4 = all): its wgrad / Dense dW+Adam kernels then "
-         "never take CUs from the step's dgrad chain"),
-    Knob("heavy_cu_quarters", int, 4, "PTG_HEAVY_CU_QUARTERS", None,
-         "the Dense dW+Adam GEMM on its own stream confined to 1-3 quarters of the CUs (4 = on the side stream)"),
     Knob("tape_overlap", bool, True, "PTG_TAPE_OVERLAP", None,
          "GradientTape loops: big Dense Adam on an aux stream overlapping the rest of the backward"),
     Knob("tape_fused_head", bool, True, "PTG_TAPE_FUSED_HEAD", None,
@@ -90,12 +76,6 @@ _K = [
     Knob("bn_bwd_epi_stats", bool, True, "PTG_BN_BWD_EPI_STATS", None,
          "ResNet: the BN backward sums of a Conv->BN->ReLU block come from the epilogue of the dgrad that produces its gradient (no bn_bwd_reduce pass)"),
     Knob("bn_epi_stats", bool, True, "PTG_BN_EPI_STATS", None, "ResNet: BN batch statistics from the conv GEMM epilogue (A/B: 9.00k vs 8.78k img/s with the shuffle flush)"),
-    Knob("dense_prelu_dx", bool, False, "PTG_DENSE_PRELU_DX", None,
-         "CNN-B1: the Dense dX epilogue also writes the PReLU conv block's dZ (prelu_bwd runs store-less on the side stream; "
-         "A/B 1.72 vs 1.70 ms: the conv5 dgrad then meets the Adam GEMM and the side-stream reduction, off)"),
-    Knob("ppb_dgrad", bool, False, "PTG_PPB_DGRAD", None,
-         "CNN-B1 layers 3-5: the dgrad epilogue also writes the pooled block's dZ (conv.hip EPI_PPB); the "
-         "PReLU/pool backward moves to the side stream for dalpha/dbias only (A/B: 1.80-1.88 vs 1.65 ms, off)"),
     Knob("conv32", bool, True, "PTG_CONV32", None,
          "5x5 convs with C, Cout in 16..64 (CNN-B1 layers 4-5 and their data gradients, see conv32_min_ch): the "
          "32x32x16-MFMA implicit GEMM of conv32.hip instead of the halo strip kernels (b256 A/B: 1.652/1.649 vs "
@@ -105,16 +85,13 @@ _K = [
     Knob("conv32_min_wg", int, 128, "PTG_CONV32_MINWG", None,
          "conv32 only when its grid (N x H / rows-per-tile workgroups) has at least this many workgroups "
          "(128 since the LDS-staged taps: CNN-B1 b32 0.646/0.638 vs 0.655/0.655 ms at 256)"),
-    Knob("ppb_rows", bool, False, "PTG_PPB_ROWS", None,
-         "CNN-B1 layers 2-4: PReLU + max-pool backward in the row-pair layout (ppb.hip, dalpha via chunk partials)"),
     Knob("conv1_rec", bool, True, "PTG_CONV1_REC", None, "first conv layer (conv1.hip): forward keeps the pool record, backward needs no recompute (0: recompute z in the backward)"),
     Knob("conv1_fused", bool, True, "PTG_CONV1_FUSED", None, "first conv layer: pooled-only forward + one recomputing backward kernel (conv1.hip)"),
     Knob("dense_fwd_splits", int, 0, "PTG_DENSE_FWD_SPLITS", None,
          "0: the big Dense forward streams its weight through dense.hip (split-K partial slices, plain stores); "
          ">0: the atomic split-K MFMA GEMM with this many splits (A/B)"),
-    Knob("blaslt_dx", bool, True, "PTG_BLASLT_DX", None,
-         "big-Dense dX (a plain GEMM) through hipBLASLt instead of the skinny-M MFMA GEMM "
-         "(CNN-B1 b256 A/B: 1.642/1.629 vs 1.657/1.650 ms)"),
+    Knob("blaslt_dx", bool, False, "PTG_BLASLT_DX", None,
+         "A/B only: big-Dense dX through hipBLASLt instead of dense.hip's weight-streaming kernel"),
     Knob("hip_graph", bool, False, "PTG_HIP_GRAPH", None, "capture the training step in a HIP graph (jit_compile)"),
     Knob("host_fp32", bool, False, "PTG_HOST_FP32", None, "CPU tensors: fp32 reference path everywhere"),
     Knob("seed", int, 1337, "PTG_SEED", None, "weight-initialisation seed when none is given"),

@@ -54,16 +54,6 @@ CONV1_FUSED = config.get("conv1_fused")
 # argmax: 3 bytes per pooled element) so the backward kernel needs no conv recompute and no argmax
 # search; PTG_CONV1_REC=0 runs the recomputing backward.
 CONV1_REC = config.get("conv1_rec")
-# PPB_DGRAD: a 5x5 conv over >= 32 channels whose input is the pooled output of a Conv + PReLU +
-# MaxPool block runs its dgrad with the EPI_PPB epilogue (conv.hip): besides dA it writes the
-# block's dZ, so the block's backward skips its PReLU/pool backward on the step's stream (that
-# kernel still runs, on the side stream and without stores, for dalpha / dbias, ahead of the wgrad).
-PPB_DGRAD = config.get("ppb_dgrad")
-# PReLU + 2x2 max-pool backward in the row-pair layout (ppb.hip): coalesced 16-byte z / dz accesses
-PPB_ROWS = config.get("ppb_rows")
-# DENSE_PRELU_DX: a big Dense fed (through Flatten) by a Conv + PReLU block (CNN-B1's last conv) writes
-# that block's dZ in its dX epilogue; the block's prelu_bwd then runs store-less on the side stream
-DENSE_PRELU_DX = config.get("dense_prelu_dx")
 
 
 def host_fp32(enabled: bool | None = None) -> bool:
@@ -263,25 +253,6 @@ class ConvOp(Op):
             return None
         return self.conv.kernel.bf16, self._wflip_buf(ws, self.conv.kernel.bf16.device)
 
-    def _ppb_block(self, dz):
-        """The Conv + PReLU + MaxPool op below this one when this op's dgrad can also produce that
-        block's dZ (EPI_PPB), else None."""
-        blk = getattr(self, "below", None)
-        if not (PPB_DGRAD and dz.is_cuda and isinstance(blk, ConvOp) and blk.prelu is not None
-                and blk.pool is not None and self.conv.kernel_size == (5, 5) and self.conv.out_shape[-1] >= 32
-                and self.conv.out_shape[-1] in (32, 64)):
-            return None
-        if getattr(blk, "_fused1", False) or getattr(blk, "_sel", False) or getattr(blk, "_sparse", True):
-            return None
-        z = getattr(blk, "_z", None)
-        N, H, W, _ = self._x.shape
-        cin = self.conv.cin_p
-        if z is None or tuple(z.shape) != (N, 2 * H, 2 * W, cin) or z.dtype != torch.bfloat16:
-            return None
-        if tuple(blk.prelu.alpha.data.shape) != tuple(z.shape[1:]) or cin % 8 or cin > 64:
-            return None
-        return blk
-
     def _backward_sel(self, x, dy, ws, dev):
         """First layer: sparse record -> dZ record -> weight gradient (no dense z / dZ, no dgrad)."""
         C = self._zshape[-1]
@@ -341,35 +312,14 @@ class ConvOp(Op):
         bias_g = self.conv.bias.grad if self.conv.bias is not None else \
             ws.get(self.name + "/nobias", (zshape[-1],), torch.float32, dev)
         z = self._z if not self._sparse else None
-        pre = getattr(self, "_dz_pre", None)
-        self._dz_pre = None
-        if pre is not None:
-            # dZ came from the dgrad epilogue of the op above (EPI_PPB); dalpha / dbias from the pooled
-            # gradient on the side stream, ordered before this layer's wgrad there
-            dz = pre
-            alpha_g = self.prelu.alpha.grad
-            if self.pool is not None:
-                S.launch(lambda: K.prelu_pool_bwd(dy, z, self.prelu.alpha.data, None, alpha_g, bias_g), dev)
-            else:
-                S.launch(lambda: K.prelu_bwd(dy, z, self.prelu.alpha.data, None, alpha_g, bias_g), dev)
-        elif self._sparse:
+        if self._sparse:
             if self.prelu is not None:
                 dalpha = self.prelu.alpha.grad
             else:
                 dalpha = ws.get(self.name + "/dalpha_dummy", zshape[1:], torch.float32, dev)
             K.prelu_pool_bwd_sparse(dy, self._zs, self._arg, self._pool_alpha(ws, dev), dz, dalpha, bias_g)
         elif self.prelu is not None and self.pool is not None:
-            N_, H_, W_, C_ = z.shape
-            if PPB_ROWS and z.is_cuda and H_ % 2 == 0 and W_ % 2 == 0 and C_ in (8, 16, 32, 64):
-                # row-pair kernel (ppb.hip) + dalpha partials reduced by a second launch
-                key = (N_, H_, W_, C_)
-                if getattr(self, "_ppb_key", None) != key:
-                    self._ppb_key = key
-                    self._ppb_nf = K.ppb_rows_ws_floats(N_, H_, W_, C_, K.ppb_rows_chunks(N_, H_, W_, C_))
-                wsb = ws.get(self.name + "/ppbws", (self._ppb_nf,), torch.float32, dev)
-                K.prelu_pool_bwd_rows(dy, z, self.prelu.alpha.data, dz, self.prelu.alpha.grad, bias_g, ws=wsb)
-            else:
-                K.prelu_pool_bwd(dy, z, self.prelu.alpha.data, dz, self.prelu.alpha.grad, bias_g)
+            K.prelu_pool_bwd(dy, z, self.prelu.alpha.data, dz, self.prelu.alpha.grad, bias_g)
         elif self.prelu is not None:
             K.prelu_bwd(dy, z, self.prelu.alpha.data, dz, self.prelu.alpha.grad, bias_g)
         elif self.pool is not None:
@@ -394,14 +344,7 @@ class ConvOp(Op):
         if self.stride != 1:
             raise NotImplementedError("dgrad for strided convolutions")
         dx = ws.get(self.name + "/dx", x.shape, torch.bfloat16, dev)
-        blk = self._ppb_block(dz) if halo_dgrad and self.pad == 2 else None
-        if blk is not None:
-            wf = self._wflip_buf(ws, dev)
-            dzb = ws.get(blk.name + "/dz", blk._z.shape, torch.bfloat16, dev)
-            K.conv2d_dgrad_halo_ppb(dz, self.conv.kernel.bf16, self.pad, dx, wf, blk._z, blk.prelu.alpha.data, dzb,
-                                    flipped=getattr(self, "_wf_ready", False))
-            blk._dz_pre = dzb
-        elif halo_dgrad:
+        if halo_dgrad:
             wf = self._wflip_buf(ws, dev)
             K.conv2d_dgrad_halo(dz, self.conv.kernel.bf16, self.pad, dx, wf,
                                 flipped=getattr(self, "_wf_ready", False))
@@ -477,37 +420,12 @@ class DenseOp(Op):
         self._x = x
         return acc
 
-    def _prelu_block(self, dz):
-        """The Conv + PReLU (no pool) op feeding this Dense through Flatten, when the dX epilogue can
-        write its dZ (DENSE_PRELU_DX), else None."""
-        fl = getattr(self, "below", None)
-        blk = getattr(fl, "below", None)
-        if not (DENSE_PRELU_DX and dz.is_cuda and self.big and isinstance(fl, FlattenOp) and isinstance(blk, ConvOp)
-                and blk.prelu is not None and blk.pool is None and not blk.first):
-            return None
-        if getattr(blk, "_fused1", False) or getattr(blk, "_sel", False) or getattr(blk, "_sparse", True):
-            return None
-        z = getattr(blk, "_z", None)
-        B = self._x.shape[0]
-        if (z is None or z.dtype != torch.bfloat16 or z.shape[0] != B or z[0].numel() != self.dense.fan_in
-                or tuple(blk.prelu.alpha.data.shape) != tuple(z.shape[1:])):
-            return None
-        return blk
-
     def backward_dz(self, dz, ws):
         """Big Dense backward from the pre-activation gradient dz (bias gradient already summed):
         dX (unless first) then dW, or Adam fused into the dW GEMM."""
         x = self._x
         dx = None
-        blk = None if self.first else self._prelu_block(dz)
-        if blk is not None:
-            dx = ws.get(self.name + "/dx", x.shape, torch.bfloat16, x.device)
-            dzb = ws.get(blk.name + "/dz", blk._z.shape, torch.bfloat16, x.device)
-            B = x.shape[0]
-            K.linear_dx_prelu(dz, self.dense.kernel.bf16, dx, dzb.view(B, -1), blk._z.view(B, -1),
-                              blk.prelu.alpha.data.view(-1))
-            blk._dz_pre = dzb
-        elif not self.first:
+        if not self.first:
             dx = ws.get(self.name + "/dx", x.shape, torch.bfloat16, x.device)
             K.linear_dx(dz, self.dense.kernel.bf16, dx)
         fused = self.fused_update

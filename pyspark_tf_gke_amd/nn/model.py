@@ -38,16 +38,6 @@ from .. import config
 FUSED_ADAM = config.get("fused_adam")
 DEVICE_FEED = config.get("device_feed")
 FUSED_HEAD = config.get("fused_head")
-# Inside a step loop (fit(), bench.py: Model.overlapped_steps) the big Dense layer's fused dW+Adam
-# GEMM of step t is launched after step t's backward and runs on the side stream under step t+1's
-# convolution forward, instead of under step t's dgrad chain, where its ~1.1 GB of Adam traffic
-# slowed every dgrad and PReLU/pool-backward kernel.  Step t+1 waits for it right before the op
-# that overwrites the GEMM's input (and so before the Dense forward reads the updated weights):
-# the same arithmetic in the same order, only the overlap partner changes.
-DEFER_DENSE = config.get("defer_dense_update")
-# Within the backward: the big Dense dW+Adam GEMM is forked onto the side stream after the backward
-# of the k-th conv op from the top (0 = as soon as its inputs exist, right after the Dense dX)
-DENSE_ADAM_AFTER = config.get("dense_adam_after")
 # A model that is only a small Dense stack (the reference's CSV MLP) trains one whole step per launch
 # (mlp.hip): forward, loss, backward and Adam in one workgroup, everything in LDS.
 MLP_FUSED = config.get("mlp_fused")
@@ -160,12 +150,10 @@ class Sequential:
         return []  # no regularizers (reference: `model.losses` is empty, train_tf_ps.py:624)
 
     def get_weights(self):
-        self.wait_deferred()
         self._check_master()
         return [w for l in self.layers for w in l.keras_weights()]
 
     def set_weights(self, ws):
-        self.wait_deferred()
         i = 0
         for l in self.layers:
             n = len(l.keras_weights())
@@ -287,7 +275,6 @@ class Sequential:
     def __call__(self, x, training: bool = False):
         if not self.built:
             self.build()
-        self.wait_deferred()
         xb = self._to_device(x, self._x_dtype(x))
         from .tape import _active_tape
 
@@ -348,7 +335,7 @@ class Sequential:
         else:
             self.optimizer.apply(self.store)
 
-    def _begin_fused_update(self, st, defer: bool = False):
+    def _begin_fused_update(self, st):
         """FusedAdamStep when this step can update big Dense kernels inside their wgrad GEMM: Adam,
         one replica (no gradient collective between backward and update), GPU, PTG_FUSED_ADAM != 0."""
         if not FUSED_ADAM or not isinstance(self.optimizer, OPT.Adam) or not self.store.flat.is_cuda:
@@ -362,7 +349,7 @@ class Sequential:
         ops = self._fusable_ops
         if not ops:
             return None
-        ctx = self.optimizer.begin_fused(self.store, defer=defer)
+        ctx = self.optimizer.begin_fused(self.store)
         for op in ops:
             op.fused_update = ctx
         return ctx
@@ -422,20 +409,7 @@ class Sequential:
         self._drop_pending_head()
         d1, d2 = self.ops[-2], self.ops[-1]
         pre = self._pre_op_hook()
-        if self._deferred_ev is not None:
-            # the previous step's deferred Dense update reads d1's input buffer: wait for it before
-            # the op that rewrites that buffer (the last non-view op before d1)
-            body = self.ops[:-2]
-            prod = next((o for o in reversed(body) if not isinstance(o, E.FlattenOp)), None)
-            inner = pre
-
-            def pre(op, _inner=inner, _prod=prod):
-                if op is _prod:
-                    self.wait_deferred()
-                if _inner is not None:
-                    _inner(op)
         x = E.run_forward(self.ops[:-2], xb, self.ws, True, pre_op=pre)
-        self.wait_deferred()  # (no-op unless the body had no producer op)
         if pre is not None:  # sharded update: the two Dense ops' parameter all-gathers
             pre(d1)
             pre(d2)
@@ -447,9 +421,7 @@ class Sequential:
         K.head_mse(acc, d1.dense.bias.data, d2.dense.kernel.data, d2.dense.bias.data, yb.contiguous(), dz1,
                    d2.dense.kernel.grad, d2.dense.bias.grad, d1.dense.bias.grad, stats, scratch=scratch)
         hook = st.on_op_grads_ready if st is not None else None
-        defer = self._defer_active(acc)
-        late = 0 if defer else DENSE_ADAM_AFTER
-        fused = self._begin_fused_update(st, defer=defer or (late > 0 and acc.is_cuda))
+        fused = self._begin_fused_update(st)
         try:
             with S.active(S.for_step(self.store, st)):
                 if hook is not None:
@@ -457,75 +429,17 @@ class Sequential:
                 dx = d1.backward_dz(dz1, self.ws)
                 if hook is not None:
                     hook(self, d1)
-                done_ops = [0]
-
-                def on_done(op):
-                    if hook is not None:
-                        hook(self, op)
-                    if fused is not None and late > 0 and fused.deferred and isinstance(op, E.ConvOp):
-                        done_ops[0] += 1
-                        if done_ops[0] == late:  # fork the Dense dW+Adam GEMM under the lower layers
-                            for fn in fused.deferred:
-                                S.launch(fn, acc.device)
-                            fused.deferred.clear()
-
-                E.run_backward(self.ops[:-2], dx, self.ws, on_op_done=on_done)
-                if fused is not None and late > 0 and fused.deferred:  # fewer conv ops than `late`
-                    for fn in fused.deferred:
-                        S.launch(fn, acc.device)
-                    fused.deferred.clear()
+                E.run_backward(self.ops[:-2], dx, self.ws, on_op_done=(lambda op: hook(self, op)) if hook else None)
         finally:
             for op in getattr(self, "_fusable_ops", []):
                 op.fused_update = None
         if fused is not None:
             self.optimizer.finish_fused(fused)
-            self._launch_deferred(fused, acc.device)
         elif st is not None:
             st.finish_gradients(self)
             st.apply_update(self)
         else:
             self.optimizer.apply(self.store)
-
-    # ---------------------------------------------------------------- deferred Dense update
-    _defer_ok = False
-    _deferred_ev = None
-
-    @contextlib.contextmanager
-    def overlapped_steps(self):
-        """Step-loop scope (fit(), bench.py): big Dense dW+Adam GEMMs of a step may still be running
-        on the side stream when the step returns; they are waited for inside the next step, and
-        everything is waited for when the scope ends (PTG_DEFER_DENSE_UPDATE=0: never deferred)."""
-        prev = self._defer_ok
-        self._defer_ok = bool(DEFER_DENSE)
-        try:
-            yield self
-        finally:
-            self._defer_ok = prev
-            self.wait_deferred()
-
-    def _defer_active(self, t) -> bool:
-        return (self._defer_ok and t.is_cuda and S.ENABLED
-                and not torch.cuda.is_current_stream_capturing())
-
-    def _launch_deferred(self, fused, dev) -> None:
-        if not fused.deferred:
-            return
-        side = S._stream(dev)
-        side.wait_stream(torch.cuda.current_stream(dev))  # after this step's update pass
-        with torch.cuda.stream(side):
-            for fn in fused.deferred:
-                fn()
-        ev = torch.cuda.Event()
-        ev.record(side)
-        self._deferred_ev = ev
-        fused.deferred.clear()
-
-    def wait_deferred(self) -> None:
-        """Order the current stream after a deferred Dense update (parameter readers call this)."""
-        ev = self._deferred_ev
-        if ev is not None:
-            torch.cuda.current_stream(self.device).wait_event(ev)
-            self._deferred_ev = None
 
     # ---------------------------------------------------------------- fused small-MLP step
     def _mlp_plan(self, st):
@@ -652,7 +566,6 @@ class Sequential:
         if self._head_fusable(xb, st):
             self.store.zero_grad()
             return self._train_step_fused_head(xb, yb, stats, st)
-        self.wait_deferred()
         self.store.zero_grad()
         out = self._run_forward(xb, True)
         dpred = self._loss_grad(out, yb, stats)
@@ -694,7 +607,6 @@ class Sequential:
         self.optimizer.iterations += 1
 
     def train_on_batch(self, x, y, return_dict: bool = False):
-        self.wait_deferred()
         xb, yb = self._prep_batch(x, y)
         stats = self._stats_buf()
         K.fill_(stats, 0.0)
@@ -704,7 +616,6 @@ class Sequential:
         return logs if return_dict else [logs["loss"]] + [logs[m] for m in self.metric_names if m in logs]
 
     def test_step(self, xb, yb, stats) -> None:
-        self.wait_deferred()
         out = self._run_forward(xb, False)
         self._loss_grad(out, yb, stats)
 
@@ -792,42 +703,41 @@ class Sequential:
             else:
                 it = self._iter_batches(x, y, batch_size, shuffle, seed=epoch)
             nsteps = 0
-            with self.overlapped_steps():
-                while steps_per_epoch is None or nsteps < steps_per_epoch:
-                    if mlp_group:
-                        if stash is not None:
-                            (xb, yb, k), stash = stash, None
-                        else:
-                            try:
-                                batch, k = next(it)
-                            except StopIteration:
-                                break
-                            xb, yb = self._prep_batch(batch[0], batch[1])
-                        if steps_per_epoch is not None and nsteps + k > steps_per_epoch:
-                            k1 = steps_per_epoch - nsteps  # the rest of the group opens the next epoch
-                            B = xb.shape[0] // k
-                            stash = (xb[k1 * B:], yb[k1 * B:], k - k1)
-                            xb, yb, k = xb[:k1 * B], yb[:k1 * B], k1
+            while steps_per_epoch is None or nsteps < steps_per_epoch:
+                if mlp_group:
+                    if stash is not None:
+                        (xb, yb, k), stash = stash, None
+                    else:
+                        try:
+                            batch, k = next(it)
+                        except StopIteration:
+                            break
+                        xb, yb = self._prep_batch(batch[0], batch[1])
+                    if steps_per_epoch is not None and nsteps + k > steps_per_epoch:
+                        k1 = steps_per_epoch - nsteps  # the rest of the group opens the next epoch
                         B = xb.shape[0] // k
-                        self._last_batch = int(B)
-                        if self._mlp_fusable(xb[:B], yb[:B], st) is not None:
-                            for _ in range(k):  # fault injection counts every step of the group
-                                _fault.maybe_fail()
-                            _heartbeat.progress(k)
-                            self._train_step_mlp(xb, yb, stats, mlp_group[1], steps=k)
-                        else:
-                            for j in range(k):
-                                self.train_step_fast(xb[j * B:(j + 1) * B], yb[j * B:(j + 1) * B], stats)
-                        nsteps += k
-                        continue
-                    try:
-                        batch = next(it)
-                    except StopIteration:
-                        break
-                    xb, yb = self._prep_batch(batch[0], batch[1])
-                    self._last_batch = int(xb.shape[0])
-                    self.train_step_fast(xb, yb, stats)
-                    nsteps += 1
+                        stash = (xb[k1 * B:], yb[k1 * B:], k - k1)
+                        xb, yb, k = xb[:k1 * B], yb[:k1 * B], k1
+                    B = xb.shape[0] // k
+                    self._last_batch = int(B)
+                    if self._mlp_fusable(xb[:B], yb[:B], st) is not None:
+                        for _ in range(k):  # fault injection counts every step of the group
+                            _fault.maybe_fail()
+                        _heartbeat.progress(k)
+                        self._train_step_mlp(xb, yb, stats, mlp_group[1], steps=k)
+                    else:
+                        for j in range(k):
+                            self.train_step_fast(xb[j * B:(j + 1) * B], yb[j * B:(j + 1) * B], stats)
+                    nsteps += k
+                    continue
+                try:
+                    batch = next(it)
+                except StopIteration:
+                    break
+                xb, yb = self._prep_batch(batch[0], batch[1])
+                self._last_batch = int(xb.shape[0])
+                self.train_step_fast(xb, yb, stats)
+                nsteps += 1
             logs = self._logs_from(stats)
             dt_train = time.perf_counter() - t0  # the logs readback synchronised the device
             self._sync_master()  # every rank is here: the full fp32 master for callbacks / saving
@@ -924,7 +834,6 @@ class Sequential:
         """Keras-3 ``model.export``: write the SavedModel-layout directory (:mod:`.saved_model`)."""
         from . import saved_model
 
-        self.wait_deferred()
         return saved_model.save(self, filepath, assets=assets)
 
     def save(self, filepath: str) -> None:
@@ -932,7 +841,6 @@ class Sequential:
         layouts, keyed ``layers/<name>/vars/<i>``; safetensors instead of HDF5 because h5py is absent)."""
         from safetensors.numpy import save as st_save
 
-        self.wait_deferred()
         st = self._strategy()
         if st is not None and not st.is_chief:
             return

@@ -98,12 +98,12 @@ class Adam(Optimizer):
             self.iterations = step
 
     # ---- fused update: the gradient producer applies Adam in its epilogue (one local replica) ----
-    def begin_fused(self, store, defer: bool = False) -> "FusedAdamStep":
+    def begin_fused(self, store) -> "FusedAdamStep":
         self.build(store)
         ds = getattr(self, "dev_state", None)
         if ds is not None:
             K.adam_step(ds, self.learning_rate, self.beta_1, self.beta_2)
-        return FusedAdamStep(self, store, self.iterations + 1, ds, defer=defer and ds is None)
+        return FusedAdamStep(self, store, self.iterations + 1, ds)
 
     def finish_fused(self, ctx: "FusedAdamStep") -> None:
         """Plain fused-flat Adam over every range no gradient producer has updated."""
@@ -128,13 +128,9 @@ class FusedAdamStep:
     """One training step's Adam state for gradient producers that update their own parameter
     (``DenseOp`` runs :func:`ops.nn.linear_dw_adam`); ``done`` collects the flat ranges they took."""
 
-    def __init__(self, opt: Adam, store, step: int, lr_dev, defer: bool = False):
+    def __init__(self, opt: Adam, store, step: int, lr_dev):
         self.opt, self.store, self.step, self.lr_dev = opt, store, step, lr_dev
         self.done: list = []
-        # defer=True: the producers' launches are collected here instead of issued, and the model
-        # forks them after the step (Sequential._launch_deferred): they then overlap the next step
-        self.defer = defer
-        self.deferred: list = []
 
     def linear_dw(self, dz, x, param) -> None:
         o, n = param.offset, param.numel
@@ -145,10 +141,7 @@ class FusedAdamStep:
         fn = lambda: K.linear_dw_adam(dz, x, st.flat[o:o + n].view(shp), opt.m[o:o + n].view(shp),  # noqa: E731
                                       opt.v[o:o + n].view(shp), st.flat_bf16[o:o + n].view(shp), lr_t,
                                       opt.beta_1, opt.beta_2, opt.epsilon, 1.0, lr_dev=self.lr_dev)
-        if self.defer:
-            self.deferred.append(fn)
-        else:
-            S.launch(fn, dz.device, heavy=True)
+        S.launch(fn, dz.device)
         self.done.append((o, o + n))
 
 

@@ -13,52 +13,19 @@ HIP graph.  Measured on CNN-B1 b256: 2.075 -> 1.91 ms per step (profiles/r2_side
 """
 from __future__ import annotations
 
-import os
-
 import torch
 from .. import config
 
 ENABLED = config.get("side_stream")
-SIDE_CU_QUARTERS = config.get("side_cu_quarters")
-HEAVY_CU_QUARTERS = config.get("heavy_cu_quarters")
 _STREAMS: dict = {}
-_HEAVY: dict = {}
 
 
 def _stream(dev) -> "torch.cuda.Stream":
     dev = torch.device(dev)
     s = _STREAMS.get(dev)
     if s is None:
-        s = _STREAMS[dev] = _new_side_stream(dev)
+        s = _STREAMS[dev] = torch.cuda.Stream(device=dev)
     return s
-
-
-def _heavy_stream(dev):
-    """A third stream confined to PTG_HEAVY_CU_QUARTERS quarters of the CUs for the HBM-bound Dense
-    dW+Adam GEMM, so it cannot take the CUs of the step's dgrad chain (the wgrads keep the side
-    stream on every CU)."""
-    dev = torch.device(dev)
-    s = _HEAVY.get(dev)
-    if s is None:
-        s = _HEAVY[dev] = _new_side_stream(dev, int(HEAVY_CU_QUARTERS))
-    return s
-
-
-def _new_side_stream(dev, quarters=None):
-    """The side stream; PTG_SIDE_CU_QUARTERS < 4 confines it to that many quarters of the CUs
-    (csrc/kernels/comm.hip ptg_stream_cumask_create), so its kernels never occupy the CUs the
-    step's own chain runs on."""
-    q = int(SIDE_CU_QUARTERS if quarters is None else quarters)
-    if q >= 4:
-        return torch.cuda.Stream(device=dev)
-    import ctypes
-
-    from .. import _native
-
-    with torch.cuda.device(dev):
-        h = ctypes.c_void_p()
-        _native.check(_native.hip_lib().ptg_stream_cumask_create(q, ctypes.byref(h)), "ptg_stream_cumask_create")
-        return torch.cuda.ExternalStream(h.value, device=dev)
 
 
 class SideStream:
@@ -104,14 +71,11 @@ def current() -> SideStream | None:
     return _CUR[0]
 
 
-def launch(fn, dev, heavy: bool = False):
+def launch(fn, dev):
     """Weight-gradient (or gradient-collective) launch: forked onto the side stream when a step has
-    one, else inline.  ``heavy`` (the Dense dW+Adam GEMM): onto the CU-fenced stream when
-    PTG_HEAVY_CU_QUARTERS is 1..3.  Returns ``fn()``'s result (e.g. an async collective's handle)."""
+    one, else inline.  Returns ``fn()``'s result (e.g. an async collective's handle)."""
     side = _CUR[0]
     if side is not None and torch.device(dev).type == "cuda":
-        if heavy and 1 <= int(HEAVY_CU_QUARTERS) <= 3:
-            return side.fork(fn, dev, _heavy_stream(dev))
         return side.fork(fn, dev)
     return fn()
 

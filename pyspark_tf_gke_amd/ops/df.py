@@ -877,50 +877,21 @@ def radix_sort_u64(keys: torch.Tensor, vals: torch.Tensor | None = None, lo: int
     vb = torch.empty(n, dtype=vdt, device=dev)
     kc = vc = None
     base = _signed(lo)
-    osw = _onesweep_plan(dev, ntiles, passes) if ONESWEEP else None
-    if osw is not None:
-        hist_all, status, tickets, tags = osw
-        hip("ptg_sort_hist_all", ptr(ka), n, base, passes, ptr(hist_all))
     for p in range(passes):
         shift = 8 * p
-        if osw is not None:  # no count pass: decoupled look-back on the one-read digit histograms
-            hip("ptg_sort_onesweep", ptr(ka), ptr(va), n, base, shift, ptr(hist_all[256 * p:]), ptr(status),
-                ptr(tickets[2 * p:]), tags[p], ptr(kb), ptr(vb), int(v32))
-        else:
-            hip("ptg_sort_count", ptr(ka), n, base, shift, ptr(hist))
-            digit_offsets(hist, ntiles, offs, dbuf)
-            hip("ptg_sort_scatter", ptr(ka), ptr(va), n, base, shift, ptr(offs), ptr(kb), ptr(vb), int(v32))
+        hip("ptg_sort_count", ptr(ka), n, base, shift, ptr(hist))
+        digit_offsets(hist, ntiles, offs, dbuf)
+        hip("ptg_sort_scatter", ptr(ka), ptr(va), n, base, shift, ptr(offs), ptr(kb), ptr(vb), int(v32))
         if kc is None:  # third buffer pair so the caller's keys/vals are never overwritten
             kc = torch.empty(n, dtype=torch.int64, device=dev)
             vc = torch.empty(n, dtype=vdt, device=dev)
             ka, va, kb, vb = kb, vb, kc, vc
         else:
             ka, va, kb, vb = kb, vb, ka, va
-    if osw is not None and int(osw[2][1::2].max().item()) != 0:
-        raise RuntimeError("radix_sort_u64: onesweep look-back timed out (PTG_SORT_ONESWEEP=0 avoids it)")
     if v32:  # u32 row ids (n may reach 2^32) widened to int64 in one pass
         hip("ptg_widen_u32", ptr(va), n, ptr(kb))  # kb: our spare int64 buffer (never the caller's keys)
         va = kb
     return ka, va
-
-
-ONESWEEP = config.get("sort_onesweep")
-_OSW: dict = {}
-
-
-def _onesweep_plan(dev, ntiles: int, passes: int):
-    """(hist_all u64[passes*256] zeroed, status u64[ntiles*256], tickets u32[2*passes] zeroed, tags) of
-    one onesweep sort.  The status buffer is kept per device and versioned by an 8-bit pass tag, so
-    it is zeroed only when it grows or the tag wraps."""
-    st = _OSW.get(dev)
-    if st is None or st["status"].numel() < ntiles * 256 or st["tag"] + passes > 255:
-        st = _OSW[dev] = {"status": torch.zeros(max(ntiles, 1) * 256, dtype=torch.int64, device=dev), "tag": 0}
-    tags = [st["tag"] + 1 + p for p in range(passes)]
-    st["tag"] += passes
-    zeros = torch.zeros(passes * 256 * 2 + 2 * passes, dtype=torch.int32, device=dev)
-    hist_all = zeros[: passes * 512].view(torch.int64)
-    tickets = zeros[passes * 512:]
-    return hist_all, st["status"], tickets, tags
 
 
 def argsort_columns(cols) -> torch.Tensor | None:

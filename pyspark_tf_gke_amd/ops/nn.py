@@ -477,30 +477,6 @@ def conv2d_dgrad_halo(dz, w, pad: int, out, wflip_buf, flipped: bool = False):
     return conv2d_fwd_fused(dz, wflip_buf, None, KS - 1 - pad, out)
 
 
-def conv2d_dgrad_halo_ppb(dz, w, pad: int, out, wflip_buf, z_blk, alpha_blk, dz_blk_out, flipped: bool = False):
-    """conv2d_dgrad_halo whose epilogue also back-propagates through the MaxPool(2x2) + PReLU of the
-    block below (conv.hip EPI_PPB): ``out`` = dA (the block's pooled gradient, [N,H,W,Cin]) and
-    ``dz_blk_out`` = dZ of the block ([N,2H,2W,Cin]) from its forward ``z_blk`` and per-element
-    ``alpha_blk`` ([2H,2W,Cin] fp32) - what prelu_pool_bwd(out, z_blk, alpha_blk, ...) writes as dz.
-    GPU only; 5x5 filters over >= 32 input channels."""
-    if not flipped:
-        conv_flip_weights(w, wflip_buf)
-    KS = w.shape[1]
-    N, H, W, C = dz.shape
-    Cout = wflip_buf.shape[0]
-    assert tuple(out.shape) == (N, H, W, Cout)
-    assert tuple(z_blk.shape) == (N, 2 * H, 2 * W, Cout) and tuple(dz_blk_out.shape) == tuple(z_blk.shape)
-    assert tuple(alpha_blk.shape) == (2 * H, 2 * W, Cout) and alpha_blk.dtype == torch.float32
-    for t, nm in ((dz, "dz"), (wflip_buf, "wflip"), (z_blk, "z_blk"), (dz_blk_out, "dz_blk")):
-        need(t, torch.bfloat16, "conv_ppb." + nm)
-    hip("ptg_conv2d_fwd_halo", ptr(dz), ptr(wflip_buf), None, ptr(alpha_blk.contiguous()), ptr(out), ptr(dz_blk_out),
-        ptr(z_blk), N, H, W, C, Cout, KS, KS - 1 - pad, EPI["ppb"])
-    return out
-
-
-# ----------------------------------------------------------------------------------------------
-# Dense (MFMA GEMM)
-# ----------------------------------------------------------------------------------------------
 def gemm(M, N, K, a, lda, a_kcontig, b, ldb, b_kcontig, epi, c, ldc, bias=None, act=0, splits=1):
     hip("ptg_gemm_bf16", M, N, K, ptr(a), lda, int(a_kcontig), ptr(b), ldb, int(b_kcontig), epi, ptr(c), ldc,
         ptr(bias), act, splits)
@@ -569,9 +545,28 @@ def linear_fwd(x, w, bias, act, out, workspace=None, splits: int = 0, workspace_
     return out
 
 
-# The big Dense layer's dX (M = batch 256, N = 20480, K = 2048) runs on gemm_kernel's skinny-M tiles
-# (256 x 80: the 84 MB weight streamed once, one workgroup per CU); PTG_BLASLT_DX=1 routes it to
-# hipBLASLt for A/B runs only (tools/dense_gemm_bench.py).
+def dense_dx_ok(dy, w, out) -> bool:
+    """Shapes the weight-streaming dX kernel (dense.hip dense_dx_k) takes: batch M <= 256, the
+    reduction (units) a multiple of 64, the input width a multiple of 80, bf16 contiguous."""
+    M, N = dy.shape
+    K = w.shape[1]
+    return (M <= 256 and N % 64 == 0 and K % 80 == 0 and K >= 4096 and dy.dtype == torch.bfloat16
+            and w.dtype == torch.bfloat16 and out.dtype == torch.bfloat16 and dy.is_contiguous()
+            and w.is_contiguous() and out.is_contiguous())
+
+
+def dense_dx(dy, w, out):
+    """out[M,K] bf16 = dy[M,N] @ w[N,K] on dense.hip's weight-streaming kernel (GPU only)."""
+    M, N = dy.shape
+    K = w.shape[1]
+    assert tuple(out.shape) == (M, K) and dense_dx_ok(dy, w, out)
+    hip("ptg_dense_dx", ptr(dy), ptr(w), ptr(out), M, N, K)
+    return out
+
+
+# The big Dense layer's dX (M = batch <= 256, N = 2048 units, K = 20480 inputs) streams the weight
+# through dense.hip (dy fragments straight into registers, W tiles by LDS-DMA + transposed LDS
+# reads); PTG_BLASLT_DX=1 routes it to hipBLASLt for A/B runs only (tools/dense_bench.py).
 BLASLT_DX = config.get("blaslt_dx")
 
 
@@ -585,21 +580,9 @@ def linear_dx(dy, w, out):
             and M <= 512 and K >= 8192:
         torch.matmul(dy, w, out=out)
         return out
+    if dense_dx_ok(dy, w, out):
+        return dense_dx(dy, w, out)
     gemm(M, K, N, dy, N, 1, w, K, 0, 0, out, K)
-    return out
-
-
-def linear_dx_prelu(dy, w, out, out_dz, z, alpha):
-    """linear_dx plus out_dz = out * prelu'(z) with per-column ``alpha`` (gemm.hip EpiBf16 out2): the
-    Dense dX hands the PReLU conv block below it (through Flatten) its dZ.  GPU only; ``z`` / ``out_dz``
-    [M, K] bf16 views of the block's z / dz, ``alpha`` [K] fp32."""
-    M, N = dy.shape
-    K = w.shape[1]
-    assert tuple(out.shape) == (M, K) and tuple(out_dz.shape) == (M, K) and tuple(z.shape) == (M, K)
-    assert alpha.numel() == K and alpha.dtype == torch.float32
-    for t, nm in ((dy, "dy"), (w, "w"), (out, "out"), (out_dz, "out_dz"), (z, "z")):
-        need(t, torch.bfloat16, "linear_dx_prelu." + nm)
-    hip("ptg_linear_dx_prelu", M, N, K, ptr(dy), ptr(w), ptr(out), ptr(out_dz), ptr(z), ptr(alpha.contiguous()))
     return out
 
 
@@ -713,45 +696,12 @@ def prelu_pool_fwd(z, alpha, out):
 
 def prelu_pool_bwd(dp, z, alpha, dz_out, dalpha, dbias, nper: int = 0):
     """dz_out = d/dz of maxpool2x2(prelu(z)); dalpha, dbias accumulate (fp32).  ``nper``: samples
-    per workgroup (0 = auto).  ``dz_out`` None: dalpha / dbias only (dz made by an EPI_PPB dgrad)."""
+    per workgroup (0 = auto).  ``dz_out`` None: dalpha / dbias only."""
     if not on_device(z):
         return ref.prelu_pool_bwd(dp, z, alpha, dz_out, dalpha, dbias)
     N, H, W, C = z.shape
     hip("ptg_prelu_pool_bwd2", ptr(dp), ptr(z), ptr(alpha), ptr(dz_out), ptr(dalpha), ptr(dbias), N, H, W, C, nper)
     return dz_out
-
-
-def ppb_rows_chunks(N: int, H: int, W: int, C: int) -> int:
-    """Sample chunks of the row-pair PReLU+pool backward: ~1280 workgroups in all."""
-    bx = -(-((H // 2) * W * (C // 8)) // 256)
-    return max(1, min(N, -(-1280 // bx)))
-
-
-def ppb_rows_ws_floats(N: int, H: int, W: int, C: int, nchunks: int) -> int:
-    import ctypes
-
-    from .. import _native
-
-    out = ctypes.c_long(0)
-    _native.check(_native.hip_lib().ptg_ppb_rows_ws_floats(N, H, W, C, nchunks, ctypes.byref(out)),
-                  "ptg_ppb_rows_ws_floats")
-    return int(out.value)
-
-
-def prelu_pool_bwd_rows(dp, z, alpha, dz_out, dalpha, dbias, ws=None, nchunks: int = 0):
-    """prelu_pool_bwd with the row-pair kernel (ppb.hip): coalesced 16-byte z / dz accesses, the
-    window partner by lane swizzle, dalpha through per-sample-chunk partials (``ws``, fp32, at
-    least ``ppb_rows_ws_floats`` elements) reduced by a second kernel.  Same dz bits."""
-    if not on_device(z):
-        return ref.prelu_pool_bwd(dp, z, alpha, dz_out, dalpha, dbias)
-    N, H, W, C = z.shape
-    nchunks = nchunks or ppb_rows_chunks(N, H, W, C)
-    need_f = ppb_rows_ws_floats(N, H, W, C, nchunks)
-    if ws is None or ws.numel() < need_f:
-        ws = torch.empty(need_f, dtype=torch.float32, device=z.device)
-    hip("ptg_prelu_pool_bwd_rows", ptr(dp), ptr(z), ptr(alpha), ptr(dz_out), ptr(dalpha), ptr(dbias), N, H, W, C,
-        nchunks, ptr(ws))
-    return ws
 
 
 def prelu_pool_bwd_sparse(dp, zsel, arg, alpha, dz_out, dalpha, dbias, nper: int = 0):
@@ -793,7 +743,7 @@ def prelu_bwd(da, z, alpha, dz_out, dalpha, dbias, nper: int = 0):
         return ref.prelu_bwd(da, z, alpha, dz_out, dalpha, dbias)
     N = z.shape[0]
     C = z.shape[-1]
-    # dz_out None: dalpha / dbias only (dz made by linear_dx_prelu)
+    # dz_out None: dalpha / dbias only
     hip("ptg_prelu_bwd2", ptr(da), ptr(z), ptr(alpha), ptr(dz_out),
         ptr(dalpha), ptr(dbias), N, z[0].numel(), C, nper)
     return dz_out

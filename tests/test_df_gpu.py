@@ -348,29 +348,6 @@ def test_radix_sort_matches_stable_host_sort(hip_built, n, kind, desc):
     assert torch.equal(perm.cpu(), torch.from_numpy(want.astype(np.int64)))
     assert torch.equal(sk.cpu(), kh[torch.from_numpy(want)])
 
-
-@pytest.mark.parametrize("n,kind", [(2049, "f64"), (3_000_000, "i64"), (4_000_000, "small")])
-def test_radix_sort_onesweep_matches_host(hip_built, monkeypatch, n, kind):
-    """The onesweep passes (PTG_SORT_ONESWEEP: one-read digit histograms + decoupled look-back,
-    sort_scatter_k<.., true>; off by default since the look-back lost the 1B-row A/B) give the same
-    stable permutation as numpy, over several sorts on the tag-versioned status buffer."""
-    monkeypatch.setattr(D, "ONESWEEP", True)
-    g = torch.Generator().manual_seed(n + 7)
-    for rep in range(2):
-        if kind == "f64":
-            x = torch.randn(n, generator=g, dtype=torch.float64)
-            x[::13] = math.nan
-        elif kind == "i64":
-            x = torch.randint(-(1 << 62), 1 << 62, (n,), generator=g, dtype=torch.int64)
-        else:
-            x = torch.randint(1000, 1037, (n,), generator=g, dtype=torch.int64)
-        kg, lo, hi = D.sort_key(x.cuda(), False)
-        kh, _, _ = D.sort_key(x, False)
-        sk, perm = D.radix_sort_u64(kg, None, lo, hi)
-        want = np.argsort(kh.numpy().view(np.uint64), kind="stable")
-        assert torch.equal(perm.cpu(), torch.from_numpy(want.astype(np.int64))), rep
-
-
 def test_radix_sort_wide_payload(hip_built):
     """An arbitrary int64 payload (not row ids) keeps the 64-bit scatter path: values above 2^32
     come back intact, in stable key order."""

@@ -216,43 +216,6 @@ def _same_training(m0, m1, init, l0, l1):
                                 1e-12), (p0.name, dd)
 
 
-def test_deferred_dense_update_same_training(hip_built):
-    """overlapped_steps(): the Dense dW+Adam GEMM of step t runs under step t+1's conv forward on the
-    side stream.  Same kernels, same inputs, same order per parameter -> the same weights, Adam
-    moments and per-step losses as the undeferred loop."""
-    from pyspark_tf_gke_amd.nn import model as M
-
-    torch.manual_seed(0)
-    xs = [torch.randint(0, 256, (16, 64, 80, 3), dtype=torch.uint8, device="cuda") for _ in range(2)]
-    ys = [torch.rand(16, 2, device="cuda") * 60 for _ in range(2)]
-
-    def run(defer):
-        torch.manual_seed(1)
-        m = build_cnn_model((64, 80, 3), flat=True, summary=False, device="cuda")
-        init = m.store.flat.clone()
-        st = m._stats_buf()
-        losses = []
-        old = M.DEFER_DENSE
-        M.DEFER_DENSE = defer
-        try:
-            with m.overlapped_steps():
-                for i in range(6):
-                    st.zero_()
-                    m.train_step_fast(xs[i % 2], ys[i % 2], st)
-                    if defer:
-                        assert m._deferred_ev is not None  # the Dense update really was deferred
-                    losses.append(m._logs_from(st)["loss"])
-        finally:
-            M.DEFER_DENSE = old
-        assert m._deferred_ev is None
-        torch.cuda.synchronize()
-        return m, losses, init
-
-    m0, l0, init = run(False)
-    m1, l1, _ = run(True)
-    _same_training(m0, m1, init, l0, l1)
-
-
 def test_persistent_work_queue_mode_matches_static(hip_built):
     """Work-queue mode of the persistent conv kernels (tile chunks claimed from per-stream counters)
     computes the same training step as static per-workgroup ranges, with the side-stream weight
@@ -272,11 +235,10 @@ def test_persistent_work_queue_mode_matches_static(hip_built):
             init = m.store.flat.clone()
             st = m._stats_buf()
             losses = []
-            with m.overlapped_steps():
-                for i in range(5):
-                    st.zero_()
-                    m.train_step_fast(xs[i % 2], ys[i % 2], st)
-                    losses.append(m._logs_from(st)["loss"])
+            for i in range(5):
+                st.zero_()
+                m.train_step_fast(xs[i % 2], ys[i % 2], st)
+                losses.append(m._logs_from(st)["loss"])
             torch.cuda.synchronize()
             return m, losses, init
         finally:
@@ -416,42 +378,6 @@ def test_ps_one_worker_tape_overlap_same_training(hip_built):
             T.OVERLAP, T._apply_overlapped = old, orig
         torch.cuda.synchronize()
         assert opt.iterations == 6 and len(used) == (6 if overlap else 0), used
-        return m, losses, init
-
-    m0, l0, init = run(False)
-    m1, l1, _ = run(True)
-    _same_training(m0, m1, init, l0, l1)
-
-
-@pytest.mark.parametrize("knob", ["heavy", "side"])
-def test_cu_fenced_streams_same_training(hip_built, monkeypatch, knob):
-    """The CU-masked streams (streams.py: the Dense dW+Adam GEMM on a third stream fenced to half the
-    CUs, or the whole side stream fenced) only move kernels between CUs: the same training as the
-    default streams, and the fenced stream really was created through hipExtStreamCreateWithCUMask."""
-    from pyspark_tf_gke_amd.nn import streams as S
-
-    torch.manual_seed(0)
-    xs = [torch.randint(0, 256, (16, 64, 80, 3), dtype=torch.uint8, device="cuda") for _ in range(2)]
-    ys = [torch.rand(16, 2, device="cuda") * 60 for _ in range(2)]
-
-    def run(fenced):
-        if fenced:
-            monkeypatch.setattr(S, "HEAVY_CU_QUARTERS" if knob == "heavy" else "SIDE_CU_QUARTERS", 2)
-            monkeypatch.setattr(S, "_STREAMS", {})
-            monkeypatch.setattr(S, "_HEAVY", {})
-        torch.manual_seed(1)
-        m = build_cnn_model((64, 80, 3), flat=True, summary=False, device="cuda")
-        init = m.store.flat.clone()
-        st = m._stats_buf()
-        losses = []
-        for i in range(6):
-            st.zero_()
-            m.train_step_fast(xs[i % 2], ys[i % 2], st)
-            losses.append(m._logs_from(st)["loss"])
-        torch.cuda.synchronize()
-        if fenced:
-            made = S._HEAVY if knob == "heavy" else S._STREAMS
-            assert made and all(isinstance(s, torch.cuda.ExternalStream) for s in made.values())
         return m, losses, init
 
     m0, l0, init = run(False)

@@ -718,162 +718,6 @@ def test_conv_fwd_gemm256_resnet_layer():
     ref = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), b, padding=1)
     _close(out, ref.permute(0, 2, 3, 1), 2e-2, 2e-2, "conv_fwd_256")
 
-
-@pytest.mark.parametrize("N,H,W,Cin,Co", [(3, 16, 20, 32, 64), (2, 8, 10, 64, 64), (4, 32, 40, 16, 32)])
-def test_dgrad_ppb_epilogue_matches_two_kernels(hip_built, N, H, W, Cin, Co, monkeypatch):
-    """conv.hip EPI_PPB: one dgrad launch writes dA and the pooled block's dZ; both equal the dgrad
-    kernel + prelu_pool_bwd_sg_k pair bit for bit (the halo strip dgrad on both sides: conv32 is
-    switched off), and the store-less prelu_pool_bwd gives the same dalpha / dbias as the storing one."""
-    from pyspark_tf_gke_amd.ops import nn as K
-
-    monkeypatch.setattr(K, "CONV32", False)
-
-    torch.manual_seed(N * H + Cin)
-    dz = (torch.randn(N, H, W, Co) * 0.5).to(torch.bfloat16).cuda()          # this layer's dZ
-    w = (torch.randn(Co, 5, 5, Cin) * 0.05).to(torch.bfloat16).cuda()        # this layer's filter
-    zb = torch.randn(N, 2 * H, 2 * W, Cin).to(torch.bfloat16).cuda()         # block below: forward z
-    zb[:, ::7, ::5, :] = 0.0                                                  # exact ties in some windows
-    ab = (torch.rand(2 * H, 2 * W, Cin) * 0.5 - 0.1).cuda()                  # its per-element alpha
-    wf = torch.empty(Cin, 5, 5, Co, dtype=torch.bfloat16, device="cuda")
-    da_ref = torch.empty(N, H, W, Cin, dtype=torch.bfloat16, device="cuda")
-    K.conv2d_dgrad_halo(dz, w, 2, da_ref, wf)
-    dzb_ref = torch.empty_like(zb)
-    dal_ref = torch.zeros(2 * H, 2 * W, Cin, device="cuda")
-    db_ref = torch.zeros(Cin, device="cuda")
-    K.prelu_pool_bwd(da_ref, zb, ab, dzb_ref, dal_ref, db_ref)
-    da = torch.empty_like(da_ref)
-    dzb = torch.full_like(zb, 7.0)
-    K.conv2d_dgrad_halo_ppb(dz, w, 2, da, wf, zb, ab, dzb, flipped=True)
-    torch.cuda.synchronize()
-    assert torch.equal(da, da_ref)
-    assert torch.equal(dzb, dzb_ref)
-    dal = torch.zeros_like(dal_ref)
-    db = torch.zeros_like(db_ref)
-    K.prelu_pool_bwd(da, zb, ab, None, dal, db)
-    assert torch.allclose(dal, dal_ref, rtol=1e-5, atol=1e-6) and torch.allclose(db, db_ref, rtol=1e-5, atol=1e-5)
-
-
-def test_ppb_dgrad_model_step_matches_two_kernel_path(hip_built):
-    """CNN-B1-shaped model: with PPB_DGRAD the layers 3-5 dgrads also write the block dZ and the
-    PReLU/pool backward runs store-less on the side stream; the training matches the two-kernel path."""
-    from pyspark_tf_gke_amd.models import build_cnn_model
-    from pyspark_tf_gke_amd.nn import engine as E
-
-    torch.manual_seed(0)
-    xs = [torch.randint(0, 256, (32, 128, 160, 3), dtype=torch.uint8, device="cuda") for _ in range(2)]
-    ys = [torch.rand(32, 2, device="cuda") * 100 for _ in range(2)]
-
-    calls = [0]
-    real = E.K.conv2d_dgrad_halo_ppb
-
-    def counting(*a, **k):
-        calls[0] += 1
-        return real(*a, **k)
-
-    def run(on):
-        old = E.PPB_DGRAD
-        E.PPB_DGRAD = on
-        E.K.conv2d_dgrad_halo_ppb = counting
-        try:
-            torch.manual_seed(1)
-            m = build_cnn_model((128, 160, 3), flat=True, summary=False, device="cuda")
-            init = m.store.flat.clone()
-            st = m._stats_buf()
-            losses = []
-            for i in range(5):
-                st.zero_()
-                m.train_step_fast(xs[i % 2], ys[i % 2], st)
-                losses.append(m._logs_from(st)["loss"])
-            torch.cuda.synchronize()
-            used = [getattr(op, "_dz_pre", "unset") for op in m.ops]
-            return m, losses, init, used
-        finally:
-            E.PPB_DGRAD = old
-            E.K.conv2d_dgrad_halo_ppb = real
-
-    m0, l0, init, _ = run(False)
-    assert calls[0] == 0
-    m1, l1, _, _ = run(True)
-    assert calls[0] == 5 * 3  # layers 3, 4 and 5 feed a pooled block in every step
-    np.testing.assert_allclose(l1, l0, rtol=2e-3)
-    d = (m1.store.flat - m0.store.flat).norm().item()
-    u = (m0.store.flat - init).norm().item()
-    assert d <= 0.05 * u, (d, u)
-
-
-def test_linear_dx_prelu_matches_two_kernels(hip_built, monkeypatch):
-    """gemm.hip EpiBf16 out2: the Dense dX also writes the PReLU block's dZ; equal bit for bit to
-    linear_dx (our GEMM, not the hipBLASLt route) + prelu_bwd_sg_k, and the store-less prelu_bwd
-    gives the same dalpha / dbias."""
-    monkeypatch.setattr(K, "BLASLT_DX", False)
-    torch.manual_seed(3)
-    B, N, Kd, C = 64, 256, 16 * 20 * 64, 64
-    dy = (torch.randn(B, N) * 0.1).to(torch.bfloat16).cuda()
-    w = (torch.randn(N, Kd) * 0.02).to(torch.bfloat16).cuda()
-    z = torch.randn(B, 16, 20, C).to(torch.bfloat16).cuda()
-    alpha = (torch.rand(16, 20, C) * 0.5 - 0.1).cuda()
-    da_ref = torch.empty(B, Kd, dtype=torch.bfloat16, device="cuda")
-    K.linear_dx(dy, w, da_ref)
-    dz_ref = torch.empty_like(z)
-    dal_ref = torch.zeros_like(alpha)
-    db_ref = torch.zeros(C, device="cuda")
-    K.prelu_bwd(da_ref.view(B, 16, 20, C), z, alpha, dz_ref, dal_ref, db_ref)
-    da = torch.empty_like(da_ref)
-    dz = torch.full_like(z, 5.0)
-    K.linear_dx_prelu(dy, w, da, dz.view(B, -1), z.view(B, -1), alpha.view(-1))
-    torch.cuda.synchronize()
-    assert torch.equal(da, da_ref) and torch.equal(dz, dz_ref)
-    dal, db = torch.zeros_like(dal_ref), torch.zeros_like(db_ref)
-    K.prelu_bwd(da.view(B, 16, 20, C), z, alpha, None, dal, db)
-    assert torch.allclose(dal, dal_ref, rtol=1e-5, atol=1e-6) and torch.allclose(db, db_ref, rtol=1e-5, atol=1e-5)
-
-
-def test_dense_prelu_dx_model_step_matches(hip_built):
-    """CNN-B1-shaped model with DENSE_PRELU_DX: conv5's dZ comes from the Dense dX epilogue (one
-    call per step) and training matches the separate prelu_bwd path."""
-    from pyspark_tf_gke_amd.models import build_cnn_model
-    from pyspark_tf_gke_amd.nn import engine as E
-
-    torch.manual_seed(0)
-    xs = [torch.randint(0, 256, (32, 128, 160, 3), dtype=torch.uint8, device="cuda") for _ in range(2)]
-    ys = [torch.rand(32, 2, device="cuda") * 100 for _ in range(2)]
-    calls = [0]
-    real = E.K.linear_dx_prelu
-
-    def counting(*a, **k):
-        calls[0] += 1
-        return real(*a, **k)
-
-    def run(on):
-        old = E.DENSE_PRELU_DX
-        E.DENSE_PRELU_DX = on
-        E.K.linear_dx_prelu = counting
-        try:
-            torch.manual_seed(1)
-            m = build_cnn_model((128, 160, 3), flat=True, summary=False, device="cuda")
-            init = m.store.flat.clone()
-            st = m._stats_buf()
-            losses = []
-            for i in range(5):
-                st.zero_()
-                m.train_step_fast(xs[i % 2], ys[i % 2], st)
-                losses.append(m._logs_from(st)["loss"])
-            torch.cuda.synchronize()
-            return m, losses, init
-        finally:
-            E.DENSE_PRELU_DX = old
-            E.K.linear_dx_prelu = real
-
-    m0, l0, init = run(False)
-    assert calls[0] == 0
-    m1, l1, _ = run(True)
-    assert calls[0] == 5
-    np.testing.assert_allclose(l1, l0, rtol=2e-3)
-    d = (m1.store.flat - m0.store.flat).norm().item()
-    u = (m0.store.flat - init).norm().item()
-    assert d <= 0.05 * u, (d, u)
-
-
 @pytest.mark.parametrize("n", [64, 300_000])
 def test_metric_update_kernel_matches_torch(n):
     """nn/metrics.py one-launch updates (metric_update_k) == the fp64 torch formulas: Mean of a
