@@ -20,6 +20,8 @@
 //     regression head, or bias_act) sums the S slices in its own pass, so no fill and no atomics.
 #include "common.h"
 
+#include <cstdlib>
+
 namespace ptgd {
 
 constexpr int BK = 64;   // K per stage (one 128-B row per operand row)
@@ -359,6 +361,143 @@ __global__ __launch_bounds__(512) void dense_dx_k(const bf16_t* __restrict__ dy,
   }
 }
 
+// dX, all-LDS form: both operands by LDS-DMA.  Measured on the dense_dx_k form above (dy fragments
+// loaded straight into registers): its 16-rows-x-64-B loads cost the texture addresser two line
+// lookups per 128 B (TA busy 78 %, stalled by the L1 15.8 M cycles, 4.0 M L2 requests for 352 MB,
+// 52 us), so here dy goes through LDS as whole 128-B rows like the forward's activations, and the
+// 80-column W tiles of neighbouring workgroups (which share 128-B lines) run on one XCD.
+//   stage = dy [256 rows][64 k] (32 KB, the forward's swizzled row image, 4 DMA per wave) + W [64 n][80]
+//   (10 KB + 1 KB DMA scratch, 2 DMA per wave); 3-deep ring (129 KB), counted vmcnt(6) per stage.
+PTG_DEV int dx2_lds_row(int k) { return (k & ~15) | ((k & 7) << 1) | ((k >> 3) & 1); }
+PTG_DEV int dx2_glb_row(int kk) { return (kk & ~15) | ((kk & 1) << 3) | ((kk >> 1) & 7); }
+constexpr int DX2_A = 256 * 128;              // dy image bytes per stage
+constexpr int DX2_SLOT = DX2_A + DX_SLOT;      // + W image + scratch
+constexpr int DX2_NS = 3;
+
+__global__ __launch_bounds__(512) void dense_dx2_k(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ w,
+                                                   bf16_t* __restrict__ out, int M, int Nr, int Kc, uint32_t dybytes,
+                                                   uint32_t wbytes) {
+  extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int col0 = xcd_remap(blockIdx.x, gridDim.x) * DX_KT;  // neighbouring tiles share an L2
+  const int nk = Nr / DX_BK;
+  const bool live = wid * 32 < M;
+  const uint32_t lds0 = dx_lds_addr(smem);
+  const Rsrc rsA = make_rsrc(dy, dybytes), rsB = make_rsrc(w, wbytes);
+
+  // 6 DMA per wave per stage: j = 0..3 the dy blocks wid + 8j (rows 8b..8b+7), j = 4, 5 the W blocks
+  uint32_t goff[6];
+  int dst[6];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int b = wid + 8 * j, row = b * 8 + (lane >> 3);
+    const int chunk = (lane & 7) ^ ((row >> 1) & 7);
+    goff[j] = row < M ? (uint32_t)row * (uint32_t)Nr * 2u + (uint32_t)chunk * 16u : PTG_OOB;
+    dst[j] = b * 1024;
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int b = wid + 8 * j;
+    if (b < 10) {
+      const int f = b * 64 + lane, kk = f / 10, c8 = f - kk * 10;
+      goff[4 + j] = (uint32_t)dx2_glb_row(kk) * (uint32_t)Kc * 2u + (uint32_t)(col0 + c8 * 8) * 2u;
+      dst[4 + j] = DX2_A + b * 1024;
+    } else {
+      goff[4 + j] = PTG_OOB;
+      dst[4 + j] = DX2_A + DX_IMG;
+    }
+  }
+  const uint32_t astep = DX_BK * 2u, bstep = (uint32_t)DX_BK * (uint32_t)Kc * 2u;
+  auto issue = [&](int t) {
+    unsigned char* base = smem + (t % DX2_NS) * DX2_SLOT;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_t*)(base + dst[j]), 16,
+                                               goff[j] == PTG_OOB ? PTG_OOB : goff[j] + (uint32_t)t * astep, 0, 0, 0);
+#pragma unroll
+    for (int j = 4; j < 6; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_t*)(base + dst[j]), 16,
+                                               goff[j] == PTG_OOB ? PTG_OOB : goff[j] + (uint32_t)t * bstep, 0, 0, 0);
+  };
+
+  // A fragment (16 rows, 16-B chunk cbase + lane>>4 of the swizzled 128-B row): lane group g holds
+  // k = 8g..8g+7 of MFMA step s (cbase = 4s); B: the same k through two transposed reads
+  const int fr = lane & 15, fc = lane >> 4;
+  const int g = lane >> 4, q = (lane & 15) >> 2, pq = lane & 3;
+  int trow[2][2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) trow[s][h] = DX2_A + dx2_lds_row(s * 32 + 8 * g + 4 * h + q) * (DX_KT * 2) + pq * 8;
+
+  f32x4_t acc[2][5];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 5; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int t = 0; t < DX2_NS - 1; ++t)
+    if (t < nk) issue(t);
+  for (int t = 0; t < nk; ++t) {
+    if (t + DX2_NS - 2 < nk) wait_vm<6 * (DX2_NS - 2)>();
+    else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    if (t + DX2_NS - 1 < nk) issue(t + DX2_NS - 1);
+    if (!live) continue;
+    const int slot = (t % DX2_NS) * DX2_SLOT;
+    const unsigned char* sA = smem + slot;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      dx_u2_t tr[10];
+#pragma unroll
+      for (int j = 0; j < 5; ++j) {
+        tr[2 * j] = dx_tr_read(lds0 + slot + trow[s][0] + j * 32);
+        tr[2 * j + 1] = dx_tr_read(lds0 + slot + trow[s][1] + j * 32);
+      }
+      bf16x8_t af[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int r = wid * 32 + i * 16 + fr;
+        const int pos = (4 * s + fc) ^ ((r >> 1) & 7);
+        af[i] = __builtin_bit_cast(bf16x8_t, *(const U4*)(sA + r * 128 + pos * 16));
+      }
+      dx_lgkm_fence(tr);
+      bf16x8_t bf[5];
+#pragma unroll
+      for (int j = 0; j < 5; ++j) {
+        U4 v;
+        v.x = tr[2 * j].x; v.y = tr[2 * j].y; v.z = tr[2 * j + 1].x; v.w = tr[2 * j + 1].y;
+        bf[j] = __builtin_bit_cast(bf16x8_t, v);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 5; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
+  }
+
+  wait_vm<0>();
+  __syncthreads();
+  bf16_t* stile = (bf16_t*)smem;
+  if (live) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 5; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          stile[(wid * 32 + i * 16 + (lane >> 4) * 4 + r) * DX_KT + j * 16 + (lane & 15)] = f2bf(acc[i][j][r]);
+  }
+  __syncthreads();
+  const int rows = min(M, 256);
+  for (int c = tid; c < rows * 10; c += 512) {
+    const int r = c / 10, c8 = c - r * 10;
+    *(U4*)(out + (long)r * Kc + col0 + c8 * 8) = *(const U4*)(stile + r * DX_KT + c8 * 8);
+  }
+}
+
 }  // namespace ptgd
 
 using namespace ptgd;
@@ -400,10 +539,23 @@ int ptg_dense_fwd_sk(const void* x, const void* w, float* part, int M, int N, in
 int ptg_dense_dx(const void* dy, const void* w, void* out, int M, int Nr, int Kc, hipStream_t s) {
   if (M <= 0 || M > 256 || Nr <= 0 || Nr % DX_BK || Kc <= 0 || Kc % DX_KT) return (int)hipErrorInvalidValue;
   if (!ptg_fits_2g((long)Nr * Kc * 2) || !ptg_fits_2g((long)M * Nr * 2)) return (int)hipErrorInvalidValue;
-  constexpr int P = 4;
-  const int lds = (P + 1) * DX_SLOT;
-  hipLaunchKernelGGL((dense_dx_k<P>), dim3(Kc / DX_KT), dim3(512), lds, s, (const bf16_t*)dy, (const bf16_t*)w,
-                     (bf16_t*)out, M, Nr, Kc, (uint32_t)((long)M * Nr * 2), (uint32_t)((long)Nr * Kc * 2));
+  static int variant = -1;
+  if (variant < 0) {
+    const char* e = getenv("PTG_DENSE_DX_REG");  // A/B: 1 = dy fragments straight into registers
+    variant = e && e[0] == '1' ? 1 : 0;
+    (void)hipFuncSetAttribute((const void*)dense_dx2_k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              DX2_NS * DX2_SLOT);
+  }
+  if (variant == 1) {
+    constexpr int P = 4;
+    hipLaunchKernelGGL((dense_dx_k<P>), dim3(Kc / DX_KT), dim3(512), (P + 1) * DX_SLOT, s, (const bf16_t*)dy,
+                       (const bf16_t*)w, (bf16_t*)out, M, Nr, Kc, (uint32_t)((long)M * Nr * 2),
+                       (uint32_t)((long)Nr * Kc * 2));
+  } else {
+    hipLaunchKernelGGL(dense_dx2_k, dim3(Kc / DX_KT), dim3(512), DX2_NS * DX2_SLOT, s, (const bf16_t*)dy,
+                       (const bf16_t*)w, (bf16_t*)out, M, Nr, Kc, (uint32_t)((long)M * Nr * 2),
+                       (uint32_t)((long)Nr * Kc * 2));
+  }
   PTG_RETURN_LAUNCH();
 }
 
