@@ -30,6 +30,11 @@
 #define PTG_ADAM_NT 1
 #endif
 
+// p/m/v groups of 8 whose loads the fused-Adam epilogue issues before its first update (per thread)
+#ifndef PTG_ADAM_PRE
+#define PTG_ADAM_PRE 4
+#endif
+
 #include <cstdlib>
 #include <type_traits>
 #include <utility>
@@ -382,7 +387,7 @@ struct EpiAdam {
   static constexpr bool VEC = true;
   // the kernel issues PRE lanes' worth of p/m/v loads before any update is stored (the epilogue's
   // stores could alias later loads, so the compiler would otherwise serialise 8 HBM round trips)
-  static constexpr int PRE = 4;
+  static constexpr int PRE = PTG_ADAM_PRE;
   struct Pre { float4 P[2], Mm[2], V[2]; };
   float* p; float* mo; float* ve; bf16_t* pbf; long ldc; float lr_t, b1, b2, eps, gscale; const float* lr_dev;
   PTG_DEV float lr() const { return lr_dev ? lr_dev[1] : lr_t; }

@@ -99,6 +99,9 @@ _K = [
     Knob("dist_backend", str, "", "PTG_DIST_BACKEND", None, "torch.distributed backend override (default nccl=RCCL / gloo)"),
     Knob("force_pg", bool, False, "PTG_FORCE_PG", None,
          "create the process group even for one rank (a 1-rank RCCL group: the collective code paths run for real)"),
+    Knob("collectives_world1", bool, False, "PTG_COLLECTIVES_WORLD1", None,
+         "with a 1-rank process group (PTG_FORCE_PG): take the multi-rank code paths, so every collective "
+         "(shuffles, range sort, PS rounds, KMeans sums, string unification) runs through the backend"),
     Knob("shard_world1", bool, False, "PTG_SHARD_WORLD1", None,
          "MWMS on one rank with a process group: build the sharded update anyway (RCCL reduce-scatter / all-gather "
          "of one rank through the side streams; a test of the N>1 path on one GPU)"),

@@ -311,7 +311,7 @@ class ClusterCoordinator:
 
         st = self.strategy
         world, rank = st.world_size, st.rank
-        if world == 1:
+        if not comm.distributed():
             self._join_local()
             return
         while self._queue:

@@ -670,7 +670,7 @@ class ParameterServerStrategy(Strategy):
             self._defer(model, optimizer)
             return
         opt = optimizer or model.optimizer
-        if self.world_size == 1:
+        if not comm.distributed():
             self._apply_local(model, opt)
         elif self.is_async:
             self._push_async(model, opt)
@@ -682,7 +682,7 @@ class ParameterServerStrategy(Strategy):
         if sum(bool(c) for c in contributed) == 0:
             self._pending = None
             return
-        if self.world_size == 1:
+        if not comm.distributed():
             self._apply_local(model, opt)
         else:
             self._push_apply_sync(model, opt, contributed)
@@ -716,7 +716,7 @@ class ParameterServerStrategy(Strategy):
         """Collective: the full fp32 values on every rank (after bf16 pulls only the fp32 pieces are)."""
         plan = getattr(model, "_ps_plan", None)
         st = model.store
-        if plan is None or self.world_size == 1 or not getattr(st, "master_stale", False):
+        if plan is None or not comm.distributed() or not getattr(st, "master_stale", False):
             return
         if plan.window is not None:
             self.wait_all_applied()
@@ -729,7 +729,7 @@ class ParameterServerStrategy(Strategy):
         every rank, so checkpoints are stored per parameter name."""
         plan = getattr(model, "_ps_plan", None)
         opt = model.optimizer
-        if plan is None or self.world_size == 1:
+        if plan is None or not comm.distributed():
             return
         model.store.master_stale = True
         self.synchronize_master(model)

@@ -73,7 +73,7 @@ class Strategy:
     def register_model(self, model) -> None:
         self.models.append(model)
         model.strategy = self
-        if self.world_size > 1:
+        if comm.distributed():
             comm.broadcast_(model.store.flat, 0)
             model.store.refresh_bf16()
 
@@ -91,7 +91,7 @@ class Strategy:
         return dataset.shard(self.world_size, self.rank) if self.world_size > 1 else dataset
 
     def all_reduce_sum(self, t: torch.Tensor) -> torch.Tensor:
-        if self.world_size == 1:
+        if not comm.distributed():
             return t
         dev_t = t.to(self.device) if comm.is_initialized() and torch.distributed.get_backend() == "nccl" else t.cpu()
         dev_t = dev_t.clone()

@@ -35,7 +35,7 @@ _ITER_BATCH = 4  # Lloyd iterations queued between two reads of the device conve
 
 def _gather_rows_all(t: torch.Tensor, Dm: int) -> np.ndarray:
     """Every rank's rows of a [m, Dm] float tensor, in rank order (one tensor all-gather)."""
-    parts = comm.all_gather_v(t.contiguous()) if comm.world_size() > 1 else [t]
+    parts = comm.all_gather_v(t.contiguous()) if comm.distributed() else [t]
     return np.concatenate([p.cpu().numpy().reshape(-1, Dm) for p in parts]).astype(np.float32)
 
 
@@ -115,7 +115,7 @@ class KMeans(Estimator, MLWritable, MLReadable):
         while launched < max_iter:
             for _ in range(min(_ITER_BATCH, max_iter - launched)):
                 D.kmeans_assign_accum(X, C, sums=sums, counts=counts, cn=cn, done=state)
-                if comm.world_size() > 1:
+                if comm.distributed():
                     # sums || counts all-reduced as one tensor (a converged fit reduces zeros: every
                     # rank holds the same flag, so the collective sequence stays identical)
                     buf = torch.cat([sums.view(-1), counts]).contiguous()

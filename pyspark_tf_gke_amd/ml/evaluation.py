@@ -31,7 +31,7 @@ class ClusteringEvaluator(Params):
         k_loc = int(a.max().item()) + 1 if a.numel() else 0
         k = comm.all_reduce_int([k_loc], op=torch.distributed.ReduceOp.MAX)[0]
         S, Q, cnt = D.silhouette_sum(X, a, k)
-        if comm.world_size() > 1:
+        if comm.distributed():
             buf = torch.cat([S.view(-1), Q, cnt]).contiguous()
             comm.all_reduce_(buf)
             kd = S.numel()

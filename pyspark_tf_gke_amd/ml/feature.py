@@ -27,7 +27,7 @@ from .base import Estimator, MLReadable, MLWritable, Model, Transformer, read_da
 
 
 def _all_reduce_counts(counts: torch.Tensor) -> torch.Tensor:
-    if comm.world_size() == 1:
+    if not comm.distributed():
         return counts
     return comm.all_reduce_tensor_(counts.clone())
 

@@ -81,6 +81,15 @@ def world_size() -> int:
     return dist.get_world_size() if is_initialized() else 1
 
 
+def distributed() -> bool:
+    """Whether the multi-rank code paths run: a process group of >1 ranks, or a 1-rank group with
+    PTG_COLLECTIVES_WORLD1=1 (every collective site then runs through the real backend - RCCL on
+    the GPU - against itself: the test of the N > 1 paths on one GPU)."""
+    if not is_initialized():
+        return False
+    return dist.get_world_size() > 1 or bool(config.get("collectives_world1"))
+
+
 def barrier() -> None:
     if is_initialized():
         if dist.get_backend() == "nccl":
@@ -90,7 +99,7 @@ def barrier() -> None:
 
 
 def all_reduce_(t: torch.Tensor, op=dist.ReduceOp.SUM, async_op: bool = False):
-    if not is_initialized() or dist.get_world_size() == 1:
+    if not distributed():
         return None
     return dist.all_reduce(t, op=op, async_op=async_op)
 
@@ -105,7 +114,7 @@ def all_reduce_max_scalar(x: float) -> float:
 
 
 def broadcast_(t: torch.Tensor, src: int = 0):
-    if is_initialized() and dist.get_world_size() > 1:
+    if distributed():
         dist.broadcast(t, src)
     return t
 
@@ -121,7 +130,7 @@ def all_gather_flat(full: torch.Tensor, shard: torch.Tensor, async_op=False):
 def all_to_all_v(send: torch.Tensor, send_counts: list[int], recv_counts: list[int] | None = None) -> torch.Tensor:
     """Variable all-to-all of rows (dim 0).  Size exchange first (one int64 all_to_all), then the
     payload with split sizes: the two-phase shuffle of SURVEY §5.8 / M12."""
-    if not is_initialized() or dist.get_world_size() == 1:
+    if not distributed():
         return send
     world = dist.get_world_size()
     dev = send.device
@@ -148,7 +157,7 @@ def _ctl_device() -> torch.device:
 def all_reduce_int(values, op=dist.ReduceOp.SUM) -> list:
     """All-reduce a short list of Python ints (int64) -> list of ints."""
     vals = [int(v) for v in values]
-    if not is_initialized() or dist.get_world_size() == 1:
+    if not distributed():
         return vals
     t = torch.tensor(vals, dtype=torch.int64, device=_ctl_device())
     dist.all_reduce(t, op=op)
@@ -158,7 +167,7 @@ def all_reduce_int(values, op=dist.ReduceOp.SUM) -> list:
 def all_reduce_float(values, op=dist.ReduceOp.SUM) -> list:
     """All-reduce a short list of Python floats (fp64) -> list of floats."""
     vals = [float(v) for v in values]
-    if not is_initialized() or dist.get_world_size() == 1:
+    if not distributed():
         return vals
     t = torch.tensor(vals, dtype=torch.float64, device=_ctl_device())
     dist.all_reduce(t, op=op)
@@ -167,7 +176,7 @@ def all_reduce_float(values, op=dist.ReduceOp.SUM) -> list:
 
 def all_gather_int(value: int) -> list:
     """Every rank's int (one int64 all-gather) -> list in rank order."""
-    if not is_initialized() or dist.get_world_size() == 1:
+    if not distributed():
         return [int(value)]
     dev = _ctl_device()
     t = torch.tensor([int(value)], dtype=torch.int64, device=dev)
@@ -179,7 +188,7 @@ def all_gather_int(value: int) -> list:
 def all_reduce_tensor_(t: torch.Tensor, op=dist.ReduceOp.SUM) -> torch.Tensor:
     """In-place all-reduce of a tensor on whatever device it lives (staged through the control
     device when the backend cannot reach it, e.g. CPU tensors under RCCL)."""
-    if not is_initialized() or dist.get_world_size() == 1:
+    if not distributed():
         return t
     if op == dist.ReduceOp.SUM and t.is_cuda:
         from . import ipc
@@ -200,7 +209,7 @@ def all_reduce_tensor_(t: torch.Tensor, op=dist.ReduceOp.SUM) -> torch.Tensor:
 def check_fast_paths() -> None:
     """Fail loudly if a one-shot IPC all-reduce issued so far timed out (its error word is only read
     every few calls, so a consumer calls this before it trusts the reduced values)."""
-    if not is_initialized() or dist.get_world_size() == 1:
+    if not distributed():
         return
     from . import ipc
 
@@ -210,7 +219,7 @@ def check_fast_paths() -> None:
 def all_gather_v(t: torch.Tensor) -> list:
     """Variable-length all-gather along dim 0 -> list of per-rank tensors (on ``t``'s device).
     One int64 all-gather of the lengths, then one all_gather_into_tensor of the padded rows."""
-    if not is_initialized() or dist.get_world_size() == 1:
+    if not distributed():
         return [t]
     world = dist.get_world_size()
     dev = _ctl_device()
@@ -244,7 +253,7 @@ def all_gather_unique(t: torch.Tensor) -> torch.Tensor:
 def all_gather_bytes(blobs: list) -> list:
     """Every rank's list of byte strings, in rank order: one all_gather_v of the int64 lengths and
     one of the concatenated uint8 payload (tensors only, nothing pickled)."""
-    if not is_initialized() or dist.get_world_size() == 1:
+    if not distributed():
         return [list(blobs)]
     lens = torch.tensor([len(b) for b in blobs], dtype=torch.int64)
     raw = b"".join(blobs)
@@ -273,7 +282,7 @@ def union_strings(strings: list) -> list:
     Tensor control plane: one all_gather_v of 64-bit string hashes decides which rank first holds
     each distinct string, then only those strings' UTF-8 bytes travel (all_gather_bytes)."""
     strings = list(strings)
-    if not is_initialized() or dist.get_world_size() == 1:
+    if not distributed():
         seen, out = set(), []
         for x in strings:
             if x not in seen:
@@ -301,7 +310,7 @@ def union_strings(strings: list) -> list:
 
 
 def all_gather_object(obj):
-    if not is_initialized() or dist.get_world_size() == 1:
+    if not distributed():
         return [obj]
     out = [None] * dist.get_world_size()
     dist.all_gather_object(out, obj)

@@ -52,7 +52,7 @@ def run(total_rows: int = 1_000_000_000, num_keys: int = 1_000_000, steps: int =
     dt = comm.all_reduce_max_scalar(time.perf_counter() - t0)
     groups = out.count()
     total_c = int(out._t.column("c").data.sum().item())
-    if world > 1:
+    if comm.distributed():
         total_c = int(comm.all_reduce_int([total_c])[0])
     ok = total_c == n * world
     # value checksums against the input columns (reduced by a different kernel, in another order):

@@ -369,7 +369,7 @@ class DataFrame:
 
     def collect(self) -> list:
         names = self.columns
-        t = _gather_table_all(self._t) if comm.world_size() > 1 else self._t
+        t = _gather_table_all(self._t) if comm.distributed() else self._t
         return [Row._make(names, r) for r in t.rows()]
 
     def take(self, num: int) -> list:
@@ -475,7 +475,7 @@ class DataFrame:
             specs.append((c, bool(a)))
         t = self._t
         world = comm.world_size()
-        if world > 1:
+        if comm.distributed():
             from . import shuffle as SH
 
             t = SH._unify_strings(t)
@@ -550,7 +550,7 @@ class DataFrame:
         t = self._t
         if cols:
             key = _group_keys(self, [_to_col(c) for c in cols])[0]
-            if world > 1:
+            if comm.distributed():
                 pieces, sizes = [], []
                 for _, pt in bucket_exchange(t, key, n, coalesce=False):
                     pieces.append(pt)
@@ -561,7 +561,7 @@ class DataFrame:
                 table = t.take(perm)
                 sizes = [int(x) for x in counts.cpu().tolist()]
         else:
-            table = round_robin_shuffle(t) if world > 1 else t
+            table = round_robin_shuffle(t) if comm.distributed() else t
             mine = len(range(rank, n, world))
             sizes = [table.num_rows * (i + 1) // mine - table.num_rows * i // mine for i in range(mine)]
         d = self._new(table)
@@ -743,7 +743,7 @@ def _parse_sql_predicate(s: str) -> Column:
 def _global_stats(cv: ColumnVector):
     s, c, mn, mx, nul = D.reduce_stats(cv.data if cv.data.dtype != torch.bool else cv.data.to(torch.uint8),
                                        cv.valid_u8(), skip_nan=True)
-    if comm.world_size() > 1:
+    if comm.distributed():
         s, c, nul = comm.all_reduce_float([s, c, nul])
         mx, neg_mn = comm.all_reduce_float([mx, -mn], op=torch.distributed.ReduceOp.MAX)
         mn = -neg_mn
@@ -860,17 +860,17 @@ def _count_distinct(cv: ColumnVector) -> int:
         if ok is not None:
             u = D.gather_rows(u, D.compact(ok))
         uk = D.distinct_raw(u)
-        if world > 1:
+        if comm.distributed():
             uk = D.distinct_raw(torch.cat(comm.all_gather_v(uk)))
         return int(uk.numel())
     k, null = _key_of(cv)
     ok = cv.valid_bool() if null is None else (cv.valid_bool() & ~null)
     loc = torch.unique(k[ok])
-    return int(comm.all_gather_unique(loc).numel()) if world > 1 else int(loc.numel())
+    return int(comm.all_gather_unique(loc).numel()) if comm.distributed() else int(loc.numel())
 
 
 def _any_rank(flag: bool) -> bool:
-    if comm.world_size() == 1:
+    if not comm.distributed():
         return flag
     return bool(comm.all_reduce_int([int(flag)])[0])
 
@@ -900,7 +900,7 @@ def _group_keys_device(srcs: list):
         cols.append({"name": name, "cv": cv, "u": u, "ok": ok, "lut": None, "type": kt})
     st = [x & ((1 << 64) - 1) for x in stats.cpu().tolist()]  # u64 bit patterns
     world = comm.world_size()
-    if world > 1:  # orderable u64 -> signed order for the int64 collectives
+    if comm.distributed():  # orderable u64 -> signed order for the int64 collectives
         sg = lambda x: x - (1 << 63)  # noqa: E731
         mins = comm.all_reduce_int([sg(st[3 * j]) for j in range(nc)], op=dist.ReduceOp.MIN)
         maxs = comm.all_reduce_int([sg(st[3 * j + 1]) for j in range(nc)], op=dist.ReduceOp.MAX)
@@ -930,7 +930,7 @@ def _group_keys_device(srcs: list):
         if c["ok"] is not None:
             raw = D.gather_rows(raw, D.compact(c["ok"]))
         raw = D.distinct_raw(raw)
-        if world > 1:
+        if comm.distributed():
             raw = D.distinct_raw(torch.cat(comm.all_gather_v(raw)))
         lut = D.sorted_orderable(raw, c["type"])
         c["lut"], c["lo"], c["nvals"] = lut, 0, int(lut.numel())
@@ -987,7 +987,7 @@ def _group_keys(df: "DataFrame", cols: list):
     for _, cv, k, null in keyed:
         has_null = _any_rank(null is not None)
         kv = k if null is None else k[~null]
-        if comm.world_size() > 1:
+        if comm.distributed():
             # globally consistent dense codes: union of distinct keys across ranks
             glob = comm.all_gather_unique(torch.unique(kv))
         else:
@@ -1241,7 +1241,7 @@ class GroupedData:
         vdata = [_num(cv) for cv in value_cols]
         vvalid = [cv.valid_u8() for cv in value_cols]
         ukeys, rows, outs = _hash_agg_all(key, vdata, vvalid, need_minmax)
-        if world > 1:
+        if comm.distributed():
             # shuffle the partials to the key owners in spark.sql.shuffle.partitions hash buckets, one
             # reduce partition per round (RCCL all-to-all-v), and merge each received bucket as its
             # own reduce task: staging per round ~ 1/buckets of the partials
@@ -1355,7 +1355,7 @@ class GroupedData:
         df = self.df
         t = df._t
         key, _ = _group_keys(df, self.cols)
-        if comm.world_size() > 1:
+        if comm.distributed():
             t = _shuffle_by_key(t, key)
             df = df._new(t)
             key, _ = _group_keys(df, self.cols)

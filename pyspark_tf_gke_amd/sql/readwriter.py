@@ -40,7 +40,7 @@ from .table import ColumnVector, Table, column_from_python
 def unify_dictionary(cv: ColumnVector) -> ColumnVector:
     """Make a string column's dictionary identical on every rank (union in rank order) and remap
     local codes — required before codes can be compared, shuffled or grouped across ranks."""
-    if comm.world_size() == 1 or not isinstance(cv.dtype, T.StringType):
+    if not comm.distributed() or not isinstance(cv.dtype, T.StringType):
         return cv
     merged = comm.union_strings(cv.dictionary or [])  # tensor collectives: hashes, then new strings' bytes
     idx = {s: i for i, s in enumerate(merged)}
@@ -86,7 +86,7 @@ def _parse_csv_bytes(buf: bytes, header: bool, infer: bool, sep: str, device, sc
     if isinstance(schema, T.StructType):
         names = schema.names
     total = len(data_starts)
-    if rank_split and comm.world_size() > 1:
+    if rank_split and comm.distributed():
         w, r = comm.world_size(), comm.rank()
         data_starts = data_starts[total * r // w: total * (r + 1) // w]
     st = np.ascontiguousarray(data_starts)
@@ -105,7 +105,7 @@ def _parse_csv_bytes(buf: bytes, header: bool, infer: bool, sep: str, device, sc
         tcode = ctypes.c_int(5)
         lib.ptgh_csv_infer(cbuf, p(fs), p(fl), p(fq), m, Cn, j, ctypes.byref(tcode))
         types.append(tcode.value)
-    if infer and comm.world_size() > 1 and not isinstance(schema, T.StructType):
+    if infer and comm.distributed() and not isinstance(schema, T.StructType):
         allt = [row.tolist() for row in comm.all_gather_v(torch.tensor([types], dtype=torch.int64))[0:]]
         allt = [r[0] for r in allt]
         merged = []
@@ -218,7 +218,7 @@ class DataFrameReader:
         for pth in paths:
             with open(pth, "r", encoding="utf-8", errors="replace") as fh:
                 lines += [fh.read()] if wholetext else fh.read().splitlines()
-        if comm.world_size() > 1:
+        if comm.distributed():
             w, r = comm.world_size(), comm.rank()
             lines = lines[len(lines) * r // w: len(lines) * (r + 1) // w]
         cv = unify_dictionary(column_from_python(lines, T.StringType(), self._s.device))

@@ -190,7 +190,7 @@ class SparkSession:
             schema = schema or names
         elif rows and isinstance(rows[0], Row) and rows[0].__fields__ and schema is None:
             schema = list(rows[0].__fields__)
-        if not _local and comm.world_size() > 1:
+        if not _local and comm.distributed():
             w, r = comm.world_size(), comm.rank()
             lo, hi = len(rows) * r // w, len(rows) * (r + 1) // w
             rows = rows[lo:hi]
@@ -216,7 +216,7 @@ class SparkSession:
             if dt is None:
                 # infer over the global data so every rank agrees on the type
                 dt = infer_python_type(vals)
-                if comm.world_size() > 1 and not _local:
+                if comm.distributed() and not _local:
                     names_ = ["BooleanType", "IntegerType", "LongType", "DoubleType", "StringType"]
                     code = names_.index(type(dt).__name__) if type(dt).__name__ in names_ else len(names_)
                     kinds = {names_[c] if c < len(names_) else "other" for c in comm.all_gather_int(code)}

@@ -69,7 +69,7 @@ def shuffle_table(t: Table, perm: torch.Tensor, counts: torch.Tensor, budget: in
     """Send rows ``perm[start_d : start_d + counts[d]]`` to rank d (perm groups rows by destination)
     and return the rows this rank receives, ordered by source rank."""
     world = comm.world_size()
-    if world == 1:
+    if not comm.distributed():
         return t.take(perm)
     budget = budget or budget_bytes()
     t = _unify_strings(t)

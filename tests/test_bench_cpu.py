@@ -37,3 +37,26 @@ def test_bench_three_ranks():
     one = _run("--gpus", "1", "--workload", "mlp", "--batch-size", "96", "--steps", "3", "--warmup", "1")
     assert three["n_gpus"] == 3
     assert abs(three["config"]["final_loss"] - one["config"]["final_loss"]) <= 1e-5 * abs(one["config"]["final_loss"])
+
+
+def test_bench_eight_ranks_driver_launch():
+    """The driver's own N=8 command line (torch.distributed.run, one rank per 'GPU', 127.0.0.1
+    rendezvous) rehearsed on gloo: eight weak-scaled ranks give the 1-rank run at the global batch,
+    rank 0 alone prints the one JSON line, and the gradient buckets were all-reduced."""
+    env = dict(os.environ)
+    env.update({"PTG_DEVICE": "cpu", "OMP_NUM_THREADS": "1"})
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8", "--master-addr",
+           "127.0.0.1", "--master-port", "29741", "bench.py", "--gpus", "8", "--workload", "mlp", "--batch-size", "16",
+           "--steps", "3", "--warmup", "1"]
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    eight = json.loads(lines[0])
+    one = _run("--gpus", "1", "--workload", "mlp", "--batch-size", "128", "--steps", "3", "--warmup", "1")
+    assert eight["n_gpus"] == 8 and eight["config"]["global_batch"] == 128 and eight["scaling"] == "weak"
+    assert eight["config"]["parallelism"].startswith("dp8")
+    assert eight["comm"]["buckets"] >= 1
+    assert abs(eight["config"]["final_loss"] - one["config"]["final_loss"]) <= 1e-5 * abs(one["config"]["final_loss"])

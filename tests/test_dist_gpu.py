@@ -307,3 +307,106 @@ def test_tape_overlap_with_fresh_adam_matches_serial(hip_built):
     a, b = flats
     assert torch.isfinite(a).all()
     assert float((a - b).abs().max()) <= 1e-4 * max(1.0, float(b.abs().max()))
+
+
+SITES_BODY = """
+import json, os, numpy as np, torch
+import torch.distributed as dist
+from pyspark_tf_gke_amd import nn
+from pyspark_tf_gke_amd.parallel import comm
+from pyspark_tf_gke_amd.ops import df as D
+from pyspark_tf_gke_amd.sql import SparkSession, functions as F, types as T
+from pyspark_tf_gke_amd.sql.dataframe import DataFrame
+from pyspark_tf_gke_amd.sql.table import ColumnVector, Table
+from pyspark_tf_gke_amd.ml import KMeans, VectorAssembler
+from pyspark_tf_gke_amd.cli.train import _ps_loop, make_parameter_server_strategy
+from pyspark_tf_gke_amd.data import Dataset
+from pyspark_tf_gke_amd.models import build_deep_model
+
+calls = {}
+def counting(name, fn):
+    def f(*a, **k):
+        calls[name] = calls.get(name, 0) + 1
+        return fn(*a, **k)
+    return f
+for nm in ("all_to_all_single", "all_reduce", "all_gather_into_tensor", "reduce_scatter_tensor", "broadcast"):
+    setattr(dist, nm, counting(nm, getattr(dist, nm)))
+
+comm.init()
+spark = SparkSession.builder.master("mi355x").getOrCreate()
+dev = torch.device("cuda", 0)
+def run(forced):
+    os.environ["PTG_COLLECTIVES_WORLD1"] = "1" if forced else "0"
+    calls.clear()
+    out = {}
+    n = 2_000_000
+    k, v = D.fill_synthetic_kv(n, 50_000, dev, seed=9)
+    df = DataFrame(Table({"key": ColumnVector(k, T.LongType()), "value": ColumnVector(v, T.DoubleType())}, n, dev), spark)
+    g = df.groupBy("key").agg(F.sum("value").alias("s"), F.count("*").alias("c"))
+    gk = g._t.column("key").data
+    order = torch.argsort(gk)
+    out["gb_keys"] = int(gk.numel()); out["gb_unique"] = int(torch.unique(gk).numel())
+    out["gb_cnt"] = int(g._t.column("c").data.sum()); out["gb_sum"] = float(g._t.column("s").data.sum())
+    out["gb_first"] = [float(x) for x in g._t.column("s").data[order][:5].cpu()]
+    calls_gb = dict(calls)
+    o = df.orderBy(F.col("value").desc())
+    col = o._t.column("value").data
+    out["ob_sorted"] = bool((col[1:] <= col[:-1]).all()); out["ob_n"] = int(col.numel())
+    out["ob_head"] = [float(x) for x in col[:3].cpu()]
+    rng = np.random.default_rng(3)
+    import pandas as pd
+    pdf = pd.DataFrame({"a": rng.normal(size=4000), "b": rng.normal(size=4000), "c": rng.normal(size=4000),
+                        "name": rng.choice(["x", "y", "z"], 4000)})
+    sdf = spark.createDataFrame(pdf)
+    X = VectorAssembler(inputCols=["a", "b", "c"], outputCol="features").transform(sdf)
+    km = KMeans(k=4, seed=1, maxIter=10).fit(X)
+    out["km_cost"] = float(km.summary.trainingCost)
+    out["strings"] = comm.union_strings(["b", "a", "b", "c"])
+    ps = make_parameter_server_strategy(1, 1, chief_addr="127.0.0.1")
+    Xc = rng.normal(size=(512, 3)).astype(np.float32); yc = (Xc[:, 0] > 0).astype(np.int32)
+    def ds_fn(ctx=None):
+        return Dataset.from_tensor_slices((Xc, yc)).shuffle(100, seed=1).batch(32).repeat()
+    with ps.scope():
+        torch.manual_seed(0)
+        mm = build_deep_model(3, 2, device=dev)
+        opt = nn.optimizers.Adam(1e-2)
+        metrics = [nn.metrics.Mean("loss"), nn.metrics.SparseCategoricalAccuracy("accuracy")]
+    h = _ps_loop(mm, ps, ds_fn, 4, 2, nn.losses.SparseCategoricalCrossentropy(), opt, metrics, lambda e, v: str(v))
+    out["ps_loss"] = h["loss"]; out["ps_sum"] = float(sum(float(np.asarray(w, dtype=np.float64).sum()) for w in mm.get_weights()))
+    torch.cuda.synchronize()
+    out["calls_groupby"] = calls_gb; out["calls"] = dict(calls)
+    return out
+
+a = run(True)
+b = run(False)
+print("RESULT", json.dumps({"backend": dist.get_backend(), "world": dist.get_world_size(), "forced": a, "plain": b}),
+      flush=True)
+"""
+
+
+def test_single_rank_rccl_every_collective_site(hip_built):
+    """every multi-rank code path through a real 1-rank RCCL group (PTG_FORCE_PG +
+    PTG_COLLECTIVES_WORLD1): the groupBy all-to-all-v shuffle, the range-shuffled orderBy, the KMeans
+    sums all-reduce, all_gather_v string unification and the sync parameter-server round (push /
+    apply / pull) - each gives the single-process result, and the collectives really ran."""
+    env = dict(os.environ)
+    env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    env.update({"PTG_FORCE_PG": "1", "RANK": "0", "WORLD_SIZE": "1", "LOCAL_RANK": "0", "LOCAL_WORLD_SIZE": "1",
+                "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": "29657"})
+    env.pop("PTG_DIST_BACKEND", None)
+    r = subprocess.run([sys.executable, "-c", textwrap.dedent(SITES_BODY)], env=env, capture_output=True, text=True,
+                       timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    v = [json.loads(line.split("RESULT ", 1)[1]) for line in r.stdout.splitlines() if "RESULT " in line][0]
+    assert v["backend"] == "nccl" and v["world"] == 1, v
+    a, b = v["forced"], v["plain"]
+    assert a["calls_groupby"].get("all_to_all_single", 0) >= 2, a["calls_groupby"]  # counts + payload
+    assert a["calls"].get("all_reduce", 0) > 0 and a["calls"].get("all_gather_into_tensor", 0) > 0, a["calls"]
+    assert not b["calls"].get("all_to_all_single"), b["calls"]
+    assert a["gb_keys"] == a["gb_unique"] == b["gb_keys"] and a["gb_cnt"] == b["gb_cnt"] == 2_000_000
+    assert abs(a["gb_sum"] - b["gb_sum"]) <= 1e-9 * b["gb_sum"]
+    assert a["gb_first"] == pytest.approx(b["gb_first"], rel=1e-12)
+    assert a["ob_sorted"] and a["ob_n"] == b["ob_n"] and a["ob_head"] == b["ob_head"]
+    assert a["km_cost"] == pytest.approx(b["km_cost"], rel=1e-5)
+    assert a["strings"] == b["strings"] == ["b", "a", "c"]
+    assert a["ps_loss"] == pytest.approx(b["ps_loss"], rel=1e-5) and a["ps_sum"] == pytest.approx(b["ps_sum"], rel=1e-6)
