@@ -991,6 +991,60 @@ __global__ __launch_bounds__(256) void adam_k(float* __restrict__ p, float* __re
   }
 }
 
+// Adam over up to 4 disjoint [lo, hi) ranges of the flat store in ONE launch (the ranges a fused
+// step's gradient producers did not update: the conv / PReLU block before a big Dense and the
+// tail after it), optionally writing the flipped bf16 dgrad filters of up to 4 conv kernels that lie
+// inside those ranges: wf[ci][KS-1-kh][KS-1-kw][co] = bf16(new W[co][kh][kw][ci]).  The next
+// backward's halo dgrad then reads them as they are (no conv_flip4_k launch on its critical path).
+struct AdamRanges { long lo[4]; long pre[5]; int nr; };
+struct AdamFlips { bf16_t* wf[4]; long off[4]; int n[4], Cout[4], KS[4], Cin[4]; int nf; };
+__global__ __launch_bounds__(256) void adam_multi_k(float* __restrict__ p, float* __restrict__ g,
+                                                    float* __restrict__ m, float* __restrict__ v,
+                                                    bf16_t* __restrict__ pbf, AdamRanges R, AdamFlips F, float lr_t,
+                                                    float b1, float b2, float eps, float gscale,
+                                                    const float* __restrict__ lr_dev, int clear) {
+  if (lr_dev) lr_t = lr_dev[1];
+  const long tot = R.pre[R.nr];
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < tot; i += (long)gridDim.x * 256) {
+    int r = 0;
+    while (r + 1 < R.nr && i >= R.pre[r + 1]) ++r;
+    const long e = R.lo[r] + 4 * (i - R.pre[r]);  // first element of this float4
+    const long q = e >> 2;
+    float4 pp = ((float4*)p)[q];
+    const float4 gg = ((const float4*)g)[q];
+    if (clear) ((float4*)g)[q] = float4{0.f, 0.f, 0.f, 0.f};
+    float4 mm = ((float4*)m)[q], vv = ((float4*)v)[q];
+    float* P = &pp.x; const float* G = &gg.x; float* Mm = &mm.x; float* V = &vv.x;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float gj = G[j] * gscale;
+      Mm[j] = b1 * Mm[j] + (1.f - b1) * gj;
+      V[j] = b2 * V[j] + (1.f - b2) * gj * gj;
+      P[j] -= lr_t * Mm[j] / (sqrtf(V[j]) + eps);
+    }
+    ((float4*)p)[q] = pp; ((float4*)m)[q] = mm; ((float4*)v)[q] = vv;
+    if (pbf) {
+      U2 o; o.x = pack_bf(pp.x, pp.y); o.y = pack_bf(pp.z, pp.w);
+      ((U2*)pbf)[q] = o;
+    }
+    for (int j = 0; j < F.nf; ++j) {
+      const long d0 = e - F.off[j];
+      if (d0 < 0 || d0 >= F.n[j]) continue;
+      const int Cin = F.Cin[j], KS = F.KS[j], Cout = F.Cout[j];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int d = (int)d0 + t;
+        const int ci = d % Cin;
+        int rest = d / Cin;
+        const int kw = rest % KS;
+        rest /= KS;
+        const int kh = rest % KS, co = rest / KS;
+        F.wf[j][((ci * KS + (KS - 1 - kh)) * KS + (KS - 1 - kw)) * Cout + co] = f2bf(P[t]);
+      }
+    }
+  }
+}
+
 // Fused flat SGD (+momentum, optional Nesterov), Keras convention:
 //   v = momentum*v - lr*g ; p += v            (nesterov: p += momentum*v - lr*g)
 __global__ __launch_bounds__(256) void sgd_k(float* __restrict__ p, float* __restrict__ g,
@@ -1417,6 +1471,41 @@ int ptg_adam(float* p, float* g, float* m, float* v, void* pbf, long n, float lr
   const long n4 = n / 4;
   hipLaunchKernelGGL(adam_k, dim3(grid_for(n4)), dim3(256), 0, s, p, g, m, v, (bf16_t*)pbf, n4, lr_t, b1, b2,
                      eps, gscale, lr_dev, clear);
+  PTG_RETURN_LAUNCH();
+}
+
+// ranges: nr (<= 4) pairs (lo, hi) of element offsets from p (multiples of 4, disjoint); flips: nf
+// (<= 4) records (wf pointer, element offset of the conv kernel from p, Cout, KS, Cin), each kernel
+// wholly inside one range.
+int ptg_adam_multi(float* p, float* g, float* m, float* v, void* pbf, int nr, const long* ranges, float lr_t,
+                   float b1, float b2, float eps, float gscale, const float* lr_dev, int clear, int nf,
+                   const long* flips, hipStream_t s) {
+  if (nr < 1 || nr > 4 || nf < 0 || nf > 4) return (int)hipErrorInvalidValue;
+  AdamRanges R{};
+  R.nr = nr;
+  R.pre[0] = 0;
+  for (int r = 0; r < nr; ++r) {
+    const long lo = ranges[2 * r], hi = ranges[2 * r + 1];
+    if (lo < 0 || hi < lo || lo % 4 || hi % 4) return (int)hipErrorInvalidValue;
+    R.lo[r] = lo;
+    R.pre[r + 1] = R.pre[r] + (hi - lo) / 4;
+  }
+  AdamFlips F{};
+  F.nf = nf;
+  for (int j = 0; j < nf; ++j) {
+    const long* f = flips + 5 * j;
+    F.wf[j] = (bf16_t*)f[0];
+    F.off[j] = f[1]; F.Cout[j] = (int)f[2]; F.KS[j] = (int)f[3]; F.Cin[j] = (int)f[4];
+    const long n = f[2] * f[3] * f[3] * f[4];
+    if (!F.wf[j] || F.off[j] % 4 || n % 4 || n >= (1L << 31)) return (int)hipErrorInvalidValue;
+    F.n[j] = (int)n;
+    bool inside = false;
+    for (int r = 0; r < nr; ++r) inside |= F.off[j] >= ranges[2 * r] && F.off[j] + n <= ranges[2 * r + 1];
+    if (!inside) return (int)hipErrorInvalidValue;
+  }
+  if (R.pre[nr] == 0) return 0;
+  hipLaunchKernelGGL(adam_multi_k, dim3(grid_for(R.pre[nr])), dim3(256), 0, s, p, g, m, v, (bf16_t*)pbf, R, F, lr_t,
+                     b1, b2, eps, gscale, lr_dev, clear);
   PTG_RETURN_LAUNCH();
 }
 

@@ -59,6 +59,9 @@ _K = [
     Knob("fault_task", int, 0, "PTG_FAULT_TASK", None, "fault injection: fail this many stage-task attempts"),
     # training step
     Knob("fused_adam", bool, True, "PTG_FUSED_ADAM", None, "Adam inside the big Dense weight-gradient GEMM epilogue (1 GPU)"),
+    Knob("flip_in_adam", bool, True, "PTG_FLIP_IN_ADAM", None,
+         "the fused step's Adam pass writes the conv layers' flipped dgrad filters for the next backward "
+         "(no flip kernel in the step); 0 = flip at the start of every backward"),
     Knob("mlp_fused", bool, True, "PTG_MLP_FUSED", None,
          "a model that is only a small Dense stack (the CSV MLP) runs each training step as ONE kernel (mlp.hip)"),
     Knob("fused_head", bool, True, "PTG_FUSED_HEAD", None, "CNN-B1 Dense(relu)->Dense->MSE head as two kernels"),

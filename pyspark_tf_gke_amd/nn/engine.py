@@ -244,14 +244,32 @@ class ConvOp(Op):
         return p
 
     def _wflip_buf(self, ws, dev):
+        """This op's flipped dgrad filter [Cin][KS][KS][Cout] (bf16): owned by the op, not the
+        workspace, so a fused Adam step can write it for the next backward (``flip_spec``)."""
         KS, Co = self.conv.kernel_size[0], self.conv.out_shape[-1]
-        return ws.get(self.name + "/wflip", (self.conv.cin_p, KS, KS, Co), torch.bfloat16, dev)
+        shp = (self.conv.cin_p, KS, KS, Co)
+        b = getattr(self, "_wf_buf", None)
+        if b is None or tuple(b.shape) != shp or b.device != torch.device(dev):
+            b = self._wf_buf = torch.empty(shp, dtype=torch.bfloat16, device=dev)
+        return b
+
+    def _flips(self) -> bool:
+        return not self.first and self.stride == 1 and self.conv.kernel.bf16.is_cuda and self._halo()[1]
 
     def dgrad_flip_job(self, ws):
         """(weights, flip buffer) when this op's backward runs the halo dgrad on the GPU, else None."""
-        if self.first or self.stride != 1 or not self.conv.kernel.bf16.is_cuda or not self._halo()[1]:
+        if not self._flips():
             return None
         return self.conv.kernel.bf16, self._wflip_buf(ws, self.conv.kernel.bf16.device)
+
+    def flip_spec(self):
+        """(flip buffer, flat offset, Cout, KS, Cin) for an optimizer pass that writes this op's
+        flipped dgrad filter from the updated weights (ops.nn.adam_multi), else None."""
+        if not self._flips():
+            return None
+        k = self.conv.kernel
+        Cout, KS, _, Cin = k.shape
+        return self._wflip_buf(None, k.bf16.device), k.offset, Cout, KS, Cin
 
     def _backward_sel(self, x, dy, ws, dev):
         """First layer: sparse record -> dZ record -> weight gradient (no dense z / dZ, no dgrad)."""
@@ -341,6 +359,9 @@ class ConvOp(Op):
             S.launch(lambda: K.conv2d_wgrad(x, dz, self.stride, self.pad, g, accumulate=True), dev)
         if self.first:
             return None
+        return self._dgrad(x, dz, ws, dev, halo_dgrad)
+
+    def _dgrad(self, x, dz, ws, dev, halo_dgrad):
         if self.stride != 1:
             raise NotImplementedError("dgrad for strided convolutions")
         dx = ws.get(self.name + "/dx", x.shape, torch.bfloat16, dev)
@@ -631,15 +652,16 @@ def run_forward(ops, x, ws, training=True, pre_op=None):
     return x
 
 
-def run_backward(ops, dy, ws, on_op_done=None):
+def run_backward(ops, dy, ws, on_op_done=None, flips_ready=()):
     # every halo dgrad filter of this pass flipped by one launch up front (weights are fixed until
-    # the optimizer step that follows the backward)
+    # the optimizer step that follows the backward); ``flips_ready``: ops whose flipped filter the
+    # last optimizer pass already wrote from these very weights (ops.nn.adam_multi)
     jobs = []
     for op in ops:
         if isinstance(op, ConvOp):
             job = op.dgrad_flip_job(ws)
             op._wf_ready = job is not None
-            if job is not None:
+            if job is not None and op.name not in flips_ready:
                 jobs.append(job)
     if jobs:
         K.conv_flip_weights_multi(jobs)

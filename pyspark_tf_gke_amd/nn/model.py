@@ -38,6 +38,7 @@ from .. import config
 FUSED_ADAM = config.get("fused_adam")
 DEVICE_FEED = config.get("device_feed")
 FUSED_HEAD = config.get("fused_head")
+FLIP_IN_ADAM = config.get("flip_in_adam")
 # A model that is only a small Dense stack (the reference's CSV MLP) trains one whole step per launch
 # (mlp.hip): forward, loss, backward and Adam in one workgroup, everything in LDS.
 MLP_FUSED = config.get("mlp_fused")
@@ -220,7 +221,14 @@ class Sequential:
                                "first (fit() and train_on_batch() do it for you)")
 
     def _run_backward(self, dpred, on_op_done=None):
-        return E.run_backward(self.ops, dpred, self.ws, on_op_done=on_op_done)
+        return E.run_backward(self.ops, dpred, self.ws, on_op_done=on_op_done, flips_ready=self._flips_ready())
+
+    def _flips_ready(self) -> frozenset:
+        """Conv ops whose flipped dgrad filter the last update wrote from the current weights."""
+        st, opt = self.store, getattr(self, "optimizer", None)
+        if opt is None or st.flip_token is None or st.flip_token != (id(opt), opt.iterations):
+            return frozenset()
+        return st.flip_names
 
     def _last_op(self):
         return self.ops[-1]
@@ -352,6 +360,11 @@ class Sequential:
         ctx = self.optimizer.begin_fused(self.store)
         for op in ops:
             op.fused_update = ctx
+        if FLIP_IN_ADAM:
+            for op in all_ops:
+                spec = op.flip_spec() if isinstance(op, E.ConvOp) else None
+                if spec is not None:
+                    ctx.flips.append((op.name, spec))
         return ctx
 
     def _head_fusable(self, xb, st) -> bool:
@@ -429,7 +442,8 @@ class Sequential:
                 dx = d1.backward_dz(dz1, self.ws)
                 if hook is not None:
                     hook(self, d1)
-                E.run_backward(self.ops[:-2], dx, self.ws, on_op_done=(lambda op: hook(self, op)) if hook else None)
+                E.run_backward(self.ops[:-2], dx, self.ws, on_op_done=(lambda op: hook(self, op)) if hook else None,
+                               flips_ready=self._flips_ready())
         finally:
             for op in getattr(self, "_fusable_ops", []):
                 op.fused_update = None

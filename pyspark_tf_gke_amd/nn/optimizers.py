@@ -106,12 +106,28 @@ class Adam(Optimizer):
         return FusedAdamStep(self, store, self.iterations + 1, ds)
 
     def finish_fused(self, ctx: "FusedAdamStep") -> None:
-        """Plain fused-flat Adam over every range no gradient producer has updated."""
-        lo = 0
-        for a, b in sorted(ctx.done) + [(ctx.store.total, ctx.store.total)]:
+        """Plain fused-flat Adam over every range no gradient producer has updated: one launch for
+        all the gaps, which also writes the flipped dgrad filters of the conv kernels in them
+        (``ctx.flips``) so the next backward skips its flip pass."""
+        st = ctx.store
+        lo, gaps = 0, []
+        for a, b in sorted(ctx.done) + [(st.total, st.total)]:
             if a > lo:
-                self.apply(ctx.store, lo=lo, hi=a, advance=False)
+                gaps.append((lo, a))
             lo = max(lo, b)
+        flips = [(nm, f) for nm, f in ctx.flips if any(a <= f[1] and f[1] + f[2] * f[3] * f[3] * f[4] <= b
+                                                       for a, b in gaps)]
+        if gaps and st.flat.is_cuda and len(gaps) <= 4 and len(flips) <= 4:
+            self.build(st)
+            K.adam_multi(st.flat, st.flat_grad, self.m, self.v, st.flat_bf16, gaps, self.lr_t(ctx.step), self.beta_1,
+                         self.beta_2, self.epsilon, 1.0, lr_dev=getattr(self, "dev_state", None), clear_grad=True,
+                         flips=[f for _, f in flips])
+            st.flip_token = (id(self), ctx.step) if flips else None
+            st.flip_names = frozenset(nm for nm, _ in flips)
+        else:
+            for a, b in gaps:
+                self.apply(st, lo=a, hi=b, advance=False)
+            st.flip_token = None
         # the gaps were cleared by their updates; the fused producers' ranges were never written
         ctx.store.grad_clean = True
         self.iterations = ctx.step
@@ -131,6 +147,7 @@ class FusedAdamStep:
     def __init__(self, opt: Adam, store, step: int, lr_dev):
         self.opt, self.store, self.step, self.lr_dev = opt, store, step, lr_dev
         self.done: list = []
+        self.flips: list = []  # (op name, ConvOp.flip_spec()) the finishing pass may write
 
     def linear_dw(self, dz, x, param) -> None:
         o, n = param.offset, param.numel

@@ -71,6 +71,10 @@ class ParamStore:
     total: int = 0
     device: torch.device | None = None
     _zero_ranges: list = field(default_factory=list)
+    # (id(optimizer), iterations) after an update that also wrote the conv ops' flipped dgrad
+    # filters (nn.optimizers.Adam.finish_fused); any other write to the weights clears it
+    flip_token: tuple | None = None
+    flip_names: frozenset = frozenset()
 
     def add(self, name: str, shape, init, overwrite_grad=False, logical_numel=None, mask_fn=None) -> Param:
         p = Param(name, tuple(int(s) for s in shape), init, overwrite_grad, logical_numel, len(self.params),
@@ -156,6 +160,7 @@ class ParamStore:
         return ranges
 
     def _bind_views(self) -> None:
+        self.flip_token = None
         for p in self.params:
             sl = slice(p.offset, p.offset + p.numel)
             p.data = self.flat[sl].view(p.shape)
@@ -177,6 +182,7 @@ class ParamStore:
     def refresh_bf16(self) -> None:
         from ..ops import nn as K
 
+        self.flip_token = None
         if self.flat.is_cuda and self.flat_bf16.dtype == torch.bfloat16:
             K.cast_f32_bf16(self.flat, self.flat_bf16)
         else:

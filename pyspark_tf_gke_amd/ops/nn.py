@@ -799,6 +799,36 @@ def adam(p, g, m, v, pbf, lr_t: float, b1: float, b2: float, eps: float, gscale:
         float(eps), float(gscale), ptr(lr_dev), int(clear_grad))
 
 
+def adam_multi(p, g, m, v, pbf, ranges, lr_t: float, b1: float, b2: float, eps: float, gscale: float = 1.0,
+               lr_dev=None, clear_grad: bool = False, flips=()):
+    """:func:`adam` over several [lo, hi) ranges of flat 1-D tensors in ONE launch (<= 4 ranges).
+    ``flips``: (wf, offset, Cout, KS, Cin) records of conv kernels inside the ranges whose flipped
+    bf16 dgrad filter ``wf`` [Cin][KS][KS][Cout] is written from the updated weights (what
+    :func:`conv_flip_weights` would make of the new bf16 mirror)."""
+    ranges = [(int(lo), int(hi)) for lo, hi in ranges if hi > lo]
+    flips = list(flips)
+    if not ranges:
+        return
+    if not on_device(p) or len(ranges) > 4 or len(flips) > 4:
+        for lo, hi in ranges:
+            adam(p[lo:hi], g[lo:hi], m[lo:hi], v[lo:hi], None if pbf is None else pbf[lo:hi], lr_t, b1, b2, eps,
+                 gscale, lr_dev=lr_dev, clear_grad=clear_grad)
+        for wf, off, Cout, KS, Cin in flips:
+            n = Cout * KS * KS * Cin
+            conv_flip_weights(pbf[off:off + n].view(Cout, KS, KS, Cin), wf)
+        return
+    import ctypes
+
+    rr = (ctypes.c_long * (2 * len(ranges)))(*[x for r in ranges for x in r])
+    ff = (ctypes.c_long * max(1, 5 * len(flips)))(*[int(x) for wf, off, co, ks, ci in flips
+                                                    for x in (wf.data_ptr(), off, co, ks, ci)])
+    for wf, off, co, ks, ci in flips:
+        need(wf, torch.bfloat16, "adam_multi.wf")
+        assert wf.numel() == co * ks * ks * ci
+    hip("ptg_adam_multi", ptr(p), ptr(g), ptr(m), ptr(v), ptr(pbf), len(ranges), rr, float(lr_t), float(b1),
+        float(b2), float(eps), float(gscale), ptr(lr_dev), int(clear_grad), len(flips), ff)
+
+
 def _mlp_desc(dims, acts, woffs, boffs):
     import ctypes
 

@@ -124,3 +124,4 @@ def test_dense_dx_vs_fp32(M, N, Kd):
     K.linear_dx(dy.to(DEV), w.to(DEV), out2)
     torch.cuda.synchronize()
     assert torch.equal(out2.cpu(), out.cpu())
+

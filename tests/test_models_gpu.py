@@ -383,3 +383,50 @@ def test_ps_one_worker_tape_overlap_same_training(hip_built):
     m0, l0, init = run(False)
     m1, l1, _ = run(True)
     _same_training(m0, m1, init, l0, l1)
+
+
+def test_flip_in_adam_matches_flip_kernel(hip_built, monkeypatch):
+    """The fused step's Adam pass writes the conv layers' flipped dgrad filters (adam_multi_k): after
+    the first step no flip kernel runs, and five CNN-B1 steps train as with the per-backward flip.
+    A weight write outside the optimizer (set_weights) invalidates the written filters."""
+    from pyspark_tf_gke_amd.nn import model as M
+    from pyspark_tf_gke_amd.nn import engine as E
+    from pyspark_tf_gke_amd.ops import nn as K
+
+    torch.manual_seed(0)
+    xs = [torch.randint(0, 256, (32, 128, 160, 3), dtype=torch.uint8, device="cuda") for _ in range(2)]
+    ys = [torch.rand(32, 2, device="cuda") * 100 for _ in range(2)]
+    calls = []
+    orig = K.conv_flip_weights_multi
+    monkeypatch.setattr(K, "conv_flip_weights_multi", lambda jobs: (calls.append(len(jobs)), orig(jobs)))
+
+    def run(flag):
+        monkeypatch.setattr(M, "FLIP_IN_ADAM", flag)
+        calls.clear()
+        torch.manual_seed(1)
+        m = build_cnn_model((128, 160, 3), flat=True, summary=False, device="cuda")
+        init = m.store.flat.clone()
+        st = m._stats_buf()
+        losses = []
+        for i in range(5):
+            st.zero_()
+            m.train_step_fast(xs[i % 2], ys[i % 2], st)
+            losses.append(m._logs_from(st)["loss"])
+        torch.cuda.synchronize()
+        return m, losses, init, list(calls)
+
+    m0, l0, init, c0 = run(False)
+    m1, l1, _, c1 = run(True)
+    assert len(c0) == 5 and all(c == 4 for c in c0), c0
+    assert c1 == [4], c1  # only the first backward flips; every later one reads the Adam-written filters
+    _same_training(m0, m1, init, l0, l1)
+    # the written filters are exactly what the flip kernel makes of the current bf16 weights
+    for op in m1.ops:
+        if isinstance(op, E.ConvOp) and op.flip_spec() is not None:
+            ref = torch.empty_like(op._wf_buf)
+            K.conv_flip_weights(op.conv.kernel.bf16, ref)
+            torch.cuda.synchronize()
+            assert torch.equal(ref, op._wf_buf), op.name
+    assert m1._flips_ready()
+    m1.set_weights(m1.get_weights())
+    assert not m1._flips_ready()

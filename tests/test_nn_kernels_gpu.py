@@ -749,3 +749,33 @@ def test_metric_update_kernel_matches_torch(n):
     acc.update_state(lab.cuda(), logits.cuda())
     want = float((logits.argmax(-1) == lab.long()).double().mean())
     assert abs(float(acc.result()) - want) <= 1e-6
+
+
+def test_adam_multi_ranges_and_flips():
+    """adam_multi_k: several ranges in one launch == adam_k per range (bitwise), untouched elements
+    stay untouched, and the flipped filters equal conv_flip_weights of the updated bf16 mirror."""
+    n = 4096 + 3 * 5 * 5 * 8 + 16 * 5 * 5 * 8
+    g0 = torch.randn(n)
+    p0, m0, v0 = torch.randn(n), torch.randn(n) * 0.01, torch.rand(n) * 0.01
+    ranges = [(0, 1024), (1536, n)]
+    flips = [(1536, 3, 5, 8), (1536 + 3 * 200, 16, 5, 8)]
+    outs = []
+    for multi in (True, False):
+        p, g, m, v = (t.clone().to(DEV) for t in (p0, g0, m0, v0))
+        pb = torch.zeros(n, device=DEV, dtype=torch.bfloat16)
+        wfs = [torch.zeros(ci, ks, ks, co, device=DEV, dtype=torch.bfloat16) for _, co, ks, ci in flips]
+        if multi:
+            K.adam_multi(p, g, m, v, pb, ranges, 1e-3, 0.9, 0.999, 1e-7, 0.5, clear_grad=True,
+                         flips=[(wf, off, co, ks, ci) for wf, (off, co, ks, ci) in zip(wfs, flips)])
+        else:
+            for lo, hi in ranges:
+                K.adam(p[lo:hi], g[lo:hi], m[lo:hi], v[lo:hi], pb[lo:hi], 1e-3, 0.9, 0.999, 1e-7, 0.5,
+                       clear_grad=True)
+            for wf, (off, co, ks, ci) in zip(wfs, flips):
+                K.conv_flip_weights(pb[off:off + co * ks * ks * ci].view(co, ks, ks, ci), wf)
+        torch.cuda.synchronize()
+        outs.append([t.cpu() for t in (p, g, m, v, pb, *wfs)])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    assert torch.equal(outs[0][0][1024:1536], p0[1024:1536]) and torch.equal(outs[0][1][1024:1536], g0[1024:1536])
+    assert outs[0][1][:1024].abs().max() == 0

@@ -39,7 +39,7 @@ def main():
     t = timed(lambda: K.adam(p, g, m, v, pb, 1e-3, 0.9, 0.999, 1e-7), flush)
     res["adam_k_us"] = round(t, 1)
     res["adam_k_TBs"] = round(30 * n / t / 1e6, 2)
-    for B in (32, 256):
+    for B in (32, 64, 128, 256):
         dz = torch.randn(B, N, device=dev).bfloat16()
         x = torch.randn(B, Kd, device=dev).bfloat16()
         t = timed(lambda: K.linear_dw_adam(dz, x, p.view(N, Kd), m.view(N, Kd), v.view(N, Kd), pb.view(N, Kd),
