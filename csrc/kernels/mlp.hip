@@ -12,9 +12,12 @@
 // Per step: forward, fused softmax + cross-entropy (or MSE) producing dlogits, then per layer from
 // the top: dX for the layer below (with the ReLU mask) from the pre-update LDS weights, a barrier,
 // then each parameter's gradient followed immediately by its Adam update straight into the flat
-// master / m / v / bf16 copy in HBM and into the LDS weights in place (no gradient buffer is
-// written).  Every matrix product is a register-tiled LDS GEMM (tile_gemm: up to 4 x 4 outputs per
-// thread, so a few LDS reads feed many independent FMA chains).  ``steps`` > 1 runs consecutive
+// master / m / v / bf16 copy in HBM and into the LDS weights (no gradient buffer is written).  Every
+// matrix product runs on the matrix cores (v_mfma_f32_16x16x4_f32: fp32 products and sums, one LDS
+// float per lane per operand) - the register-tiled FMA form before it moved 8x the LDS bytes and
+// made the step LDS-bound; the bias gradient is one more column of the weight-gradient GEMM (each
+// activation row carries a constant 1), and the barriers only wait for LDS (tools/mlp_phases.py
+// times the phases of the PTG_MLP_PROF build).  ``steps`` > 1 runs consecutive
 // batches of a device-resident dataset in the same launch (Keras' steps_per_execution): each step
 // is still a full forward / backward / Adam step.  Metric sums are kept in registers and added to
 // `stats` once (the layouts of softmax_xent_k / mse_k).
@@ -23,6 +26,14 @@
 #include "common.h"
 
 namespace ptgm {
+
+#ifdef PTG_MLP_PROF  // phase timestamps of the first step (A/B build: tools/mlp_phases.py)
+__device__ long long g_mlp_prof[32];
+#define MLP_T(i) \
+  if (threadIdx.x == 0 && st == 0) g_mlp_prof[i] = wall_clock64();
+#else
+#define MLP_T(i)
+#endif
 
 constexpr int MAXL = 6;
 #ifndef PTG_MLP_NT
@@ -42,9 +53,17 @@ struct MlpDesc {
   int lg0, lg1, gs;             // the two gradient buffers (row stride gs, odd) and red scratch
   int lred;
   int lg;                       // lanes per row of the softmax loss (16 / 32 / 64; 0: one thread per row)
+  int ly;                       // LDS float offset of the step's labels / targets
   float lr, b1, b2, eps;
   int t0;                       // optimizer steps taken before this launch
 };
+
+// Workgroup barrier for LDS only.  __syncthreads() also waits for this wave's outstanding GLOBAL
+// stores (its release fence covers global memory): after every dW+Adam phase that is a full HBM
+// write round trip (~2.5 us of a 3.3 us phase, tools/mlp_phases.py).  Nothing in the step reads back
+// the p / m / v / bf16 values it stores (the next launch is ordered by the kernel boundary), so the
+// step's barriers only wait for LDS traffic.
+PTG_DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 PTG_DEV float sum_block(float v, float* red) {
   v = wave_sum(v);
@@ -58,56 +77,44 @@ PTG_DEV float sum_block(float v, float* red) {
   return r;
 }
 
-// out(i, j) = sum_k P[i*pi + k*pk] * Q[j*qj + k*qk] for i < M, j < N, all operands in LDS.  Each
-// thread owns a TM x TN register tile: TM + TN LDS reads feed TM*TN independent FMA chains (the
-// step is latency-bound on one CU, so the ILP is what matters).  Out-of-range rows / columns read
-// the last valid one and are dropped at the epilogue.
-template <int TM, int TN, class Epi>
-PTG_DEV void tile_gemm(int M, int N, int K, const float* P, int pi, int pk, const float* Q, int qj, int qk,
-                       Epi epi) {
-  const int tm = (M + TM - 1) / TM, tn = (N + TN - 1) / TN;
-  for (int t = threadIdx.x; t < tm * tn; t += NT) {
-    const int i0 = (t / tn) * TM, j0 = (t - (t / tn) * tn) * TN;
-    const float* pr[TM];
-    const float* qr[TN];
-#pragma unroll
-    for (int a = 0; a < TM; ++a) pr[a] = P + min(i0 + a, M - 1) * pi;
-#pragma unroll
-    for (int b = 0; b < TN; ++b) qr[b] = Q + min(j0 + b, N - 1) * qj;
-    float acc[TM][TN];
-#pragma unroll
-    for (int a = 0; a < TM; ++a)
-#pragma unroll
-      for (int b = 0; b < TN; ++b) acc[a][b] = 0.f;
-#pragma unroll 8
-    for (int k = 0; k < K; ++k) {  // unrolled: several k's LDS loads in flight at once
-      float av[TM], bv[TN];
-#pragma unroll
-      for (int a = 0; a < TM; ++a) av[a] = pr[a][k * pk];
-#pragma unroll
-      for (int b = 0; b < TN; ++b) bv[b] = qr[b][k * qk];
-#pragma unroll
-      for (int a = 0; a < TM; ++a)
-#pragma unroll
-        for (int b = 0; b < TN; ++b) acc[a][b] = fmaf(av[a], bv[b], acc[a][b]);
-    }
-#pragma unroll
-    for (int a = 0; a < TM; ++a)
-#pragma unroll
-      for (int b = 0; b < TN; ++b)
-        if (i0 + a < M && j0 + b < N) epi(i0 + a, j0 + b, acc[a][b]);
+// out(i, j) = sum_k P[i*pi + k*pk] * Q[j*qj + k*qk] for i < M, j < N, all operands in LDS, on the
+// matrix cores: each wave takes 16 x 16 output tiles and runs v_mfma_f32_16x16x4_f32 (fp32 products,
+// fp32 sums) over K in steps of 4, every operand one LDS float per lane (lane l: A row l % 16 / B column
+// l % 16 at k = l / 16).  The scalar register-tiled form this replaced moved 8x the LDS bytes per FMA
+// and made the step LDS-bound (25 us of a 30 us step at batch 32).  Two accumulators split the k
+// steps (even / odd) so consecutive MFMAs do not wait on each other.  Out-of-range rows / columns read
+// the last valid one and are dropped at the epilogue; k >= K reads zero.
+PTG_DEV f32x4_t mfma_dot(int K, const float* pa, int pk, const float* qb, int qk, int kq) {
+  f32x4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  int k0 = 0;
+  for (; k0 + 8 <= K; k0 += 8) {
+    const float a0 = pa[(k0 + kq) * pk], b0 = qb[(k0 + kq) * qk];
+    const float a1 = pa[(k0 + 4 + kq) * pk], b1 = qb[(k0 + 4 + kq) * qk];
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, acc1, 0, 0, 0);
   }
+  for (; k0 < K; k0 += 4) {
+    const int k = k0 + kq;
+    const float a = k < K ? pa[k * pk] : 0.f, b = k < K ? qb[k * qk] : 0.f;
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc0, 0, 0, 0);
+  }
+  return acc0 + acc1;
 }
 
-// the largest register tile that still gives every thread at least one tile
 template <class Epi>
 PTG_DEV void gemm(int M, int N, int K, const float* P, int pi, int pk, const float* Q, int qj, int qk, Epi epi) {
-  const int outs = M * N;
-  if (outs >= 16 * NT) tile_gemm<4, 4>(M, N, K, P, pi, pk, Q, qj, qk, epi);
-  else if (outs >= 8 * NT) tile_gemm<2, 4>(M, N, K, P, pi, pk, Q, qj, qk, epi);
-  else if (outs >= 4 * NT) tile_gemm<2, 2>(M, N, K, P, pi, pk, Q, qj, qk, epi);
-  else if (outs >= 2 * NT) tile_gemm<1, 2>(M, N, K, P, pi, pk, Q, qj, qk, epi);
-  else tile_gemm<1, 1>(M, N, K, P, pi, pk, Q, qj, qk, epi);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int r16 = lane & 15, kq = lane >> 4;
+  const int tm = (M + 15) / 16, tn = (N + 15) / 16;
+  for (int t = wid; t < tm * tn; t += NT / 64) {
+    const int i0 = (t / tn) * 16, j0 = (t - (t / tn) * tn) * 16;
+    const f32x4_t acc = mfma_dot(K, P + min(i0 + r16, M - 1) * pi, pk, Q + min(j0 + r16, N - 1) * qj, qk, kq);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = i0 + 4 * kq + r, j = j0 + r16;
+      if (i < M && j < N) epi(i, j, acc[r]);
+    }
+  }
 }
 
 // tstep (nullable): the optimizer step counter on the device (read for Adam's bias correction and
@@ -123,7 +130,9 @@ struct AdamArgs {
 PTG_DEV float adam_update(const AdamArgs& o, long idx, float g, float p0, float m0, float v0) {
   const float mm = o.b1 * m0 + (1.f - o.b1) * g;
   const float vv = o.b2 * v0 + (1.f - o.b2) * g * g;
-  const float pp = p0 - o.lr_t * mm / (sqrtf(vv) + o.eps);
+  // v_sqrt_f32 / v_rcp_f32 (1 ulp) instead of the IEEE sequences: ~25 fewer dependent VALU ops per
+  // element on this latency-bound single-workgroup step
+  const float pp = p0 - o.lr_t * mm * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vv) + o.eps);
   o.m[idx] = mm;
   o.v[idx] = vv;
   o.p[idx] = pp;
@@ -131,67 +140,42 @@ PTG_DEV float adam_update(const AdamArgs& o, long idx, float g, float p0, float 
   return pp;
 }
 
-// dW[i][j] = sum_k P[i*pi + k*pk] Q[j*qj + k*qk] (i < M output units, j < N inputs) with Adam on
-// element wo + i*N + j: the thread's p / m / v are loaded BEFORE its GEMM loop, so the HBM latency
-// hides under the FMAs instead of following each output; the updated weight also goes to LDS W.
-template <int TM, int TN>
-PTG_DEV void dw_adam_tile(int M, int N, int K, const float* P, int pi, int pk, const float* Q, int qj, int qk,
-                          const AdamArgs& o, long wo, float* Wl, int S) {
-  const int tm = (M + TM - 1) / TM, tn = (N + TN - 1) / TN;
-  for (int t = threadIdx.x; t < tm * tn; t += NT) {
-    const int i0 = (t / tn) * TM, j0 = (t - (t / tn) * tn) * TN;
-    float p0[TM][TN], m0[TM][TN], v0[TM][TN];
+// dW[i][j] = sum_k P[i*pi + k*pk] Q[j*qj + k*qk] (i < M output units, j < Nw inputs) with Adam on
+// element wo + i*Nw + j, on the matrix cores as gemm().  With a bias (bo >= 0) the GEMM has one more
+// column j = Nw whose Q entries are the constant-1 column every activation row carries at index Nw, so
+// the same MFMAs produce db[i] = sum_k P[i][k] (Adam on element bo + i, LDS copy Bl / Bc) - no serial
+// per-unit reduction over the batch.  A lane's four outputs have their p / m / v read BEFORE the MFMAs
+// (from HBM: the latency hides under the k loop; the weight itself from its current LDS copy Wc / Bc);
+// the updated value also goes to the LDS copy Wl / Bl.
+PTG_DEV void dw_adam(int M, int Nw, int K, const float* P, int pi, int pk, const float* Q, int qj, int qk,
+                     const AdamArgs& o, long wo, long bo, float* Wl, int S, const float* Wc, float* Bl,
+                     const float* Bc) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int r16 = lane & 15, kq = lane >> 4;
+  const int N = Nw + (bo >= 0 ? 1 : 0);
+  const int tm = (M + 15) / 16, tn = (N + 15) / 16;
+  for (int t = wid; t < tm * tn; t += NT / 64) {
+    const int i0 = (t / tn) * 16, j0 = (t - (t / tn) * tn) * 16;
+    float p0[4], m0[4], v0[4];
 #pragma unroll
-    for (int a = 0; a < TM; ++a)
-#pragma unroll
-      for (int b = 0; b < TN; ++b) {
-        const long idx = wo + (long)min(i0 + a, M - 1) * N + min(j0 + b, N - 1);
-        p0[a][b] = o.p[idx];
-        m0[a][b] = o.m[idx];
-        v0[a][b] = o.v[idx];
-      }
-    const float* pr[TM];
-    const float* qr[TN];
-#pragma unroll
-    for (int a = 0; a < TM; ++a) pr[a] = P + min(i0 + a, M - 1) * pi;
-#pragma unroll
-    for (int b = 0; b < TN; ++b) qr[b] = Q + min(j0 + b, N - 1) * qj;
-    float acc[TM][TN];
-#pragma unroll
-    for (int a = 0; a < TM; ++a)
-#pragma unroll
-      for (int b = 0; b < TN; ++b) acc[a][b] = 0.f;
-#pragma unroll 8
-    for (int k = 0; k < K; ++k) {  // unrolled: several k's LDS loads in flight at once
-      float av[TM], bv[TN];
-#pragma unroll
-      for (int a = 0; a < TM; ++a) av[a] = pr[a][k * pk];
-#pragma unroll
-      for (int b = 0; b < TN; ++b) bv[b] = qr[b][k * qk];
-#pragma unroll
-      for (int a = 0; a < TM; ++a)
-#pragma unroll
-        for (int b = 0; b < TN; ++b) acc[a][b] = fmaf(av[a], bv[b], acc[a][b]);
+    for (int r = 0; r < 4; ++r) {
+      const int i = min(i0 + 4 * kq + r, M - 1), j = min(j0 + r16, N - 1);
+      const bool isb = j == Nw;
+      const long idx = isb ? bo + i : wo + (long)i * Nw + j;
+      p0[r] = isb ? Bc[i] : Wc[i * S + j];
+      m0[r] = o.m[idx];
+      v0[r] = o.v[idx];
     }
+    const f32x4_t acc = mfma_dot(K, P + min(i0 + r16, M - 1) * pi, pk, Q + min(j0 + r16, N - 1) * qj, qk, kq);
 #pragma unroll
-    for (int a = 0; a < TM; ++a)
-#pragma unroll
-      for (int b = 0; b < TN; ++b)
-        if (i0 + a < M && j0 + b < N) {
-          const int i = i0 + a, j = j0 + b;
-          Wl[i * S + j] = adam_update(o, wo + (long)i * N + j, acc[a][b], p0[a][b], m0[a][b], v0[a][b]);
-        }
+    for (int r = 0; r < 4; ++r) {
+      const int i = i0 + 4 * kq + r, j = j0 + r16;
+      if (i < M && j < N) {
+        if (j == Nw) Bl[i] = adam_update(o, bo + i, acc[r], p0[r], m0[r], v0[r]);
+        else Wl[i * S + j] = adam_update(o, wo + (long)i * Nw + j, acc[r], p0[r], m0[r], v0[r]);
+      }
+    }
   }
-}
-
-PTG_DEV void dw_adam(int M, int N, int K, const float* P, int pi, int pk, const float* Q, int qj, int qk,
-                     const AdamArgs& o, long wo, float* Wl, int S) {
-  const int outs = M * N;
-  if (outs >= 16 * NT) dw_adam_tile<4, 4>(M, N, K, P, pi, pk, Q, qj, qk, o, wo, Wl, S);
-  else if (outs >= 8 * NT) dw_adam_tile<2, 4>(M, N, K, P, pi, pk, Q, qj, qk, o, wo, Wl, S);
-  else if (outs >= 4 * NT) dw_adam_tile<2, 2>(M, N, K, P, pi, pk, Q, qj, qk, o, wo, Wl, S);
-  else if (outs >= 2 * NT) dw_adam_tile<1, 2>(M, N, K, P, pi, pk, Q, qj, qk, o, wo, Wl, S);
-  else dw_adam_tile<1, 1>(M, N, K, P, pi, pk, Q, qj, qk, o, wo, Wl, S);
 }
 
 // max / first-argmax / sum over the `g` lanes of a row group (g = 16 / 32 / 64, aligned in the wave)
@@ -216,6 +200,21 @@ __global__ __launch_bounds__(NT) void mlp_train_k(const float* __restrict__ x, c
   const int tid = threadIdx.x;
   const int L = D.L, B = D.B;
   const int t0 = tstep ? (int)tstep[0] : D.t0;
+  // step 0's inputs and labels: loads issued first, stored to LDS after the weight loads (one HBM
+  // round trip for the whole prologue instead of two)
+  const int K0 = D.d[0], C = D.d[L];
+  const int nx = B * K0, ny = D.loss == 0 ? B : B * C;
+  constexpr int PX = 2;
+  float xr[PX], yr[PX];
+  const bool xpre = nx <= PX * NT && ny <= PX * NT;
+  if (xpre) {
+#pragma unroll
+    for (int u = 0; u < PX; ++u) {
+      const int i = tid + u * NT;
+      xr[u] = i < nx ? x[i] : 0.f;
+      yr[u] = i < ny ? (D.loss == 0 ? __int_as_float(((const int*)y)[i]) : ((const float*)y)[i]) : 0.f;
+    }
+  }
   // weights + biases -> LDS (the Adam epilogues keep them current in place)
   for (int l = 0; l < L; ++l) {
     const int K = D.d[l], N = D.d[l + 1], S = D.ws[l];
@@ -225,18 +224,37 @@ __global__ __launch_bounds__(NT) void mlp_train_k(const float* __restrict__ x, c
       if (D.dbl && D.boff[l] < 0) sm[D.wtot + D.lb[l] + n] = 0.f;  // bias-less: zeros in both copies
     }
   }
+  if (xpre) {
+#pragma unroll
+    for (int u = 0; u < PX; ++u) {
+      const int i = tid + u * NT;
+      if (i < nx) sm[D.la[0] + (i / K0) * D.as[0] + i % K0] = xr[u];
+      if (i < ny) sm[D.ly + i] = yr[u];
+    }
+  }
   float s_loss = 0.f, s_a = 0.f, s_b = 0.f;
-  const int C = D.d[L];
+#ifdef PTG_MLP_PROF
+  if (tid == 0) g_mlp_prof[0] = wall_clock64();
+#endif
   // with two weight copies a step reads one and its Adam epilogues write the other, so a layer's dX
   // and its weight update share one phase; otherwise the update is in place after a barrier
+  // every activation row carries a constant 1 at column d[l] (its row stride leaves room): the
+  // weight-gradient GEMM's extra column that yields the bias gradient
+  for (int l = 0; l < L; ++l)
+    for (int r = tid; r < B; r += NT) sm[D.la[l] + r * D.as[l] + D.d[l]] = 1.f;
   int wcur = 0;
   for (int st = 0; st < D.steps; ++st) {
     const int wnxt = D.dbl ? D.wtot - wcur : wcur;
-    // ---- input batch
-    const int K0 = D.d[0];
-    const float* xs = x + (long)st * B * K0;
-    for (int i = tid; i < B * K0; i += NT) sm[D.la[0] + (i / K0) * D.as[0] + i % K0] = xs[i];
-    __syncthreads();
+    // ---- input batch, with its labels / targets (their HBM latency is paid once, not again in the
+    // loss phase); step 0's came with the prologue
+    if (st > 0 || !xpre) {
+      const float* xs = x + (long)st * nx;
+      for (int i = tid; i < nx; i += NT) sm[D.la[0] + (i / K0) * D.as[0] + i % K0] = xs[i];
+      for (int i = tid; i < ny; i += NT)
+        sm[D.ly + i] = D.loss == 0 ? __int_as_float(((const int*)y)[(long)st * B + i]) : ((const float*)y)[(long)st * ny + i];
+    }
+    lds_barrier();
+    MLP_T(1)
     // ---- forward: O[r][n] = act(b[n] + A[r] . W[n])
     for (int l = 0; l < L; ++l) {
       const int K = D.d[l], N = D.d[l + 1], SO = D.as[l + 1];
@@ -247,7 +265,8 @@ __global__ __launch_bounds__(NT) void mlp_train_k(const float* __restrict__ x, c
         acc += bias[n];
         O[r * SO + n] = relu ? fmaxf(acc, 0.f) : acc;
       });
-      __syncthreads();
+      lds_barrier();
+      MLP_T(2 + l)
     }
     // ---- loss: dlogits into gradient buffer 0
     float* G = sm + D.lg0;
@@ -255,7 +274,7 @@ __global__ __launch_bounds__(NT) void mlp_train_k(const float* __restrict__ x, c
     const int SZ = D.as[L];
     if (D.loss == 0 && D.lg) {
       // D.lg lanes per row: lane c holds logit c; max / argmax / sum by lane shuffles
-      const int* lab = (const int*)y + (long)st * B;
+      const int* lab = (const int*)(sm + D.ly);
       const float scale = 1.f / (float)B;
       const int g = D.lg, c = tid & (g - 1), rpp = NT / g;
       for (int r0 = 0; r0 < B; r0 += rpp) {  // uniform trip count: every lane joins the shuffles
@@ -278,7 +297,7 @@ __global__ __launch_bounds__(NT) void mlp_train_k(const float* __restrict__ x, c
         }
       }
     } else if (D.loss == 0) {
-      const int* lab = (const int*)y + (long)st * B;
+      const int* lab = (const int*)(sm + D.ly);
       const float scale = 1.f / (float)B;
       for (int r = tid; r < B; r += NT) {
         const float* z = Z + r * SZ;
@@ -296,7 +315,7 @@ __global__ __launch_bounds__(NT) void mlp_train_k(const float* __restrict__ x, c
         s_a += am == t ? 1.f : 0.f;
       }
     } else {
-      const float* tg = (const float*)y + (long)st * B * C;
+      const float* tg = sm + D.ly;
       const float inv = 1.f / (float)(B * C);
       for (int i = tid; i < B * C; i += NT) {
         const int r = i / C, c = i - r * C;
@@ -307,7 +326,8 @@ __global__ __launch_bounds__(NT) void mlp_train_k(const float* __restrict__ x, c
         s_b += d * d;
       }
     }
-    __syncthreads();
+    lds_barrier();
+    MLP_T(9)
     // ---- backward, per layer: dX for the layer below from the pre-update LDS weights, a barrier,
     // then each weight gradient with its Adam update into HBM and into the LDS weights in place
     const float t = (float)(t0 + st + 1);
@@ -327,42 +347,23 @@ __global__ __launch_bounds__(NT) void mlp_train_k(const float* __restrict__ x, c
           if (mask && !(A[r * SA + k] > 0.f)) s = 0.f;
           Gn[r * gs + k] = s;
         });
-        if (!D.dbl) __syncthreads();  // every dX read of W_l before the in-place update below
+        if (!D.dbl) lds_barrier();  // every dX read of W_l before the in-place update below
       }
-      // bias gradients of this layer: their p / m / v loads are issued first (consumed after the dW GEMM)
-      const bool hasb = D.boff[l] >= 0;
-      const int bn0 = tid, bn1 = tid + NT;
-      float bp[2] = {0.f, 0.f}, bm[2] = {0.f, 0.f}, bvv[2] = {0.f, 0.f};
-      if (hasb) {
-        if (bn0 < N) { const long q = D.boff[l] + bn0; bp[0] = p[q]; bm[0] = m[q]; bvv[0] = v[q]; }
-        if (bn1 < N) { const long q = D.boff[l] + bn1; bp[1] = p[q]; bm[1] = m[q]; bvv[1] = v[q]; }
-      }
-      // dW[n][k] = sum_r G[r][n] A[r][k], Adam straight from the register
-      dw_adam(N, K, B, Gc, 1, D.gs, A, 1, SA, ad, D.woff[l], sm + wnxt + D.lw[l], S);
-      if (hasb) {
-        float* bnl = sm + wnxt + D.lb[l];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const int n = u ? bn1 : bn0;
-          if (n < N) {
-            float g = 0.f;
-            for (int r = 0; r < B; ++r) g += Gc[r * D.gs + n];
-            bnl[n] = adam_update(ad, D.boff[l] + n, g, bp[u], bm[u], bvv[u]);
-          }
-        }
-        for (int n = tid + 2 * NT; n < N; n += NT) {  // (layers wider than 2 x NT units)
-          float g = 0.f;
-          for (int r = 0; r < B; ++r) g += Gc[r * D.gs + n];
-          const long q = D.boff[l] + n;
-          bnl[n] = adam_update(ad, q, g, p[q], m[q], v[q]);
-        }
-      }
-      __syncthreads();
+      MLP_T(10 + 2 * (L - 1 - l))
+      // dW[n][k] = sum_r G[r][n] A[r][k] and db[n] = sum_r G[r][n] (A's constant-1 column), Adam
+      // straight from the register
+      dw_adam(N, K, B, Gc, 1, D.gs, A, 1, SA, ad, D.woff[l], D.boff[l], sm + wnxt + D.lw[l], S, sm + wcur + D.lw[l],
+              sm + wnxt + D.lb[l], sm + wcur + D.lb[l]);
+      lds_barrier();
+      MLP_T(11 + 2 * (L - 1 - l))
       const int tmp = cur; cur = nxt; nxt = tmp;
     }
     wcur = wnxt;  // (the next step's input barrier orders the new copy before any forward read)
   }
   float* red = sm + D.lred;
+#ifdef PTG_MLP_PROF
+  if (tid == 0) g_mlp_prof[30] = wall_clock64();
+#endif
   const float tl = sum_block(s_loss, red);
   const float ta = sum_block(s_a, red);
   const float tb = sum_block(s_b, red);
@@ -408,18 +409,19 @@ static long mlp_plan(const long* hdesc, int L, int B, ptgm::MlpDesc* D) {
     D->lb[l] = off; off += D->d[l + 1];
   }
   for (int l = 0; l <= L; ++l) {
-    D->as[l] = odd(D->d[l]);
+    D->as[l] = odd(D->d[l] + 1);  // room for the constant-1 bias column at d[l]
     D->la[l] = off; off += B * D->as[l];
   }
   D->gs = odd(dmax);
   D->lg0 = off; off += B * D->gs;
   D->lg1 = off; off += B * D->gs;
   D->lred = off; off += 16;
+  D->ly = off; off += B * D->d[L];  // labels (B ints) or MSE targets (B x C)
   D->wtot = D->la[0];
   D->dbl = (long)(off + D->wtot) * 4 <= 160 * 1024;
   if (D->dbl) {  // the second weight copy goes right after the first: shift everything behind it
     for (int l = 0; l <= L; ++l) D->la[l] += D->wtot;
-    D->lg0 += D->wtot; D->lg1 += D->wtot; D->lred += D->wtot;
+    D->lg0 += D->wtot; D->lg1 += D->wtot; D->lred += D->wtot; D->ly += D->wtot;
     off += D->wtot;
   }
   // softmax loss with one row per lane group (PTG_MLP_LOSS_LANES=0: one thread per row)
@@ -493,6 +495,12 @@ int ptg_mlp_ctx_run(void* ctx, const void* x, const void* y, int steps, hipStrea
                      c->v, c->pbf, c->stats, c->tstep, D);
   return (int)hipGetLastError();
 }
+
+#ifdef PTG_MLP_PROF
+int ptg_mlp_prof_read(long long* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(ptgm::g_mlp_prof), sizeof(long long) * 32);
+}
+#endif
 
 int ptg_mlp_ctx_free(void* ctx) {
   delete (MlpCtx*)ctx;

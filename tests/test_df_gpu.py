@@ -780,3 +780,63 @@ def test_groupby_more_than_four_value_columns(spark_gpu):
         for name, ref in (("s1", grp["value"].sum()), ("a2", grp["lower_ci"].mean()), ("m3", grp["upper_ci"].max()),
                           ("s4", grp["lower_ci"].sum()), ("a5", grp["value"].mean()), ("m6", grp["value"].max())):
             assert math.isclose(r[name], ref, rel_tol=1e-9, abs_tol=1e-9), (st, name, r[name], ref)
+
+
+def _spec_launches():
+    import ctypes
+
+    from pyspark_tf_gke_amd import _native
+
+    v = ctypes.c_long(0)
+    _native.hip_lib().ptg_expr_spec_launches(ctypes.byref(v))
+    return v.value
+
+
+def test_specialised_expressions_match_vm(spark_gpu, monkeypatch):
+    """expr_affine_k (one column, one constant, one op, optional int cast, or a comparison) gives
+    bit-identical values and null masks to the expression VM, including NaN / inf / out-of-range
+    casts and an odd-length tail, for every column and output type; other shapes stay on the VM."""
+    from pyspark_tf_gke_amd.sql import types as T
+    from pyspark_tf_gke_amd.sql.dataframe import DataFrame
+    from pyspark_tf_gke_amd.sql.functions import col
+    from pyspark_tf_gke_amd.sql.table import ColumnVector, Table
+
+    n = 100_003
+    g = torch.Generator().manual_seed(5)
+    v = torch.randn(n, generator=g, dtype=torch.float64) * 1e3
+    v[::97] = float("nan")
+    v[::101] = float("inf")
+    v[::103] = 3e12
+    cols = {"v": ColumnVector(v.cuda(), T.DoubleType()),
+            "f": ColumnVector(v.float().cuda(), T.FloatType()),
+            "i": ColumnVector((torch.randint(-1000, 1000, (n,), generator=g)).int().cuda(), T.IntegerType()),
+            "l": ColumnVector((torch.randint(-10**12, 10**12, (n,), generator=g)).cuda(), T.LongType())}
+    df = DataFrame(Table(cols, n, torch.device("cuda")), spark_gpu)
+    exprs = {"a": (col("v") * 4).cast("int"), "b": col("v") + 1.5, "c": 3 - col("v"), "d": col("v") / 2,
+             "e": (col("f") * 0.5).cast("long"), "g": (col("i") - 7).cast("int"), "h": col("l") * 3,
+             "k": col("v").cast("int"), "m": col("i") * 2.5, "p": col("v") > 0.5, "q": col("i") == 7,
+             "r": 10 <= col("l"), "s": col("v") * col("f")}  # (s: two columns -> the VM)
+
+    def run(flag):
+        monkeypatch.setenv("PTG_EXPR_SPECIALIZE", flag)
+        out = df.select(*[e.alias(k) for k, e in exprs.items()])
+        res = {}
+        for k in exprs:
+            cv = out._t.column(k)
+            res[k] = (cv.data.cpu(), None if cv.valid is None else cv.valid.cpu())
+        f = df.filter(col("v") >= 100.0)
+        res["filter"] = (f._t.column("l").data.cpu(), None)
+        torch.cuda.synchronize()
+        return res
+
+    before = _spec_launches()
+    spec = run("1")
+    used = _spec_launches() - before
+    vm = run("0")
+    assert _spec_launches() - before == used
+    assert used >= len(exprs) - 1, used  # every single-column shape took the specialised kernels
+    for k in spec:
+        a, b = spec[k], vm[k]
+        assert a[0].dtype == b[0].dtype, k
+        assert torch.equal(a[0].contiguous().view(torch.uint8), b[0].contiguous().view(torch.uint8)), k  # NaN bits too
+        assert (a[1] is None) == (b[1] is None) and (a[1] is None or torch.equal(a[1], b[1])), k
