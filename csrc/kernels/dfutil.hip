@@ -323,6 +323,34 @@ __global__ __launch_bounds__(512) void colapply_k(const unsigned int* __restrict
   }
 }
 
+
+// Small device utilities the DataFrame operators use instead of torch's fill / arange / bitwise
+// kernels (the operator profile carries only framework kernels): a typed fill, an int64 iota and the
+// inverse of the orderable sort-key transform.
+__global__ __launch_bounds__(256) void fill_bytes_k(void* __restrict__ p, long n, int esize, unsigned long long pat) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    switch (esize) {
+      case 1: ((uint8_t*)p)[i] = (uint8_t)pat; break;
+      case 2: ((uint16_t*)p)[i] = (uint16_t)pat; break;
+      case 4: ((uint32_t*)p)[i] = (uint32_t)pat; break;
+      default: ((unsigned long long*)p)[i] = pat; break;
+    }
+  }
+}
+__global__ __launch_bounds__(256) void iota_i64_k(long long* __restrict__ out, long n, long long start) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) out[i] = start + i;
+}
+// orderable u64 (sort_key) -> signed integer value: flip (descending), then the sign bit back
+__global__ __launch_bounds__(256) void sort_key_decode_k(const long long* __restrict__ sk, long n, int desc, int out32,
+                                                         void* __restrict__ out) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const unsigned long long u = (unsigned long long)sk[i];
+    const long long x = (long long)((desc ? ~u : u) ^ 0x8000000000000000ULL);
+    if (out32) ((int*)out)[i] = (int)x;
+    else ((long long*)out)[i] = x;
+  }
+}
+
 extern "C" {
 
 // out[0..n) = exclusive prefix sum of in (int32 when in64 == 0, else int64); total (optional) =
@@ -501,4 +529,26 @@ int ptg_gather_fixed(const void* src, const void* idx, int idx32, long m, int ro
   PTG_RETURN_LAUNCH();
 }
 
+
+int ptg_fill_bytes(void* p, long n, int esize, long pat, hipStream_t s) {
+  if (n <= 0) return 0;
+  if (esize != 1 && esize != 2 && esize != 4 && esize != 8) return (int)hipErrorInvalidValue;
+  const long g = std::min<long>(4096, (n + 255) / 256);
+  hipLaunchKernelGGL(fill_bytes_k, dim3((unsigned)g), dim3(256), 0, s, p, n, esize, (unsigned long long)pat);
+  PTG_RETURN_LAUNCH();
+}
+
+int ptg_iota_i64(void* out, long n, long start, hipStream_t s) {
+  if (n <= 0) return 0;
+  const long g = std::min<long>(4096, (n + 255) / 256);
+  hipLaunchKernelGGL(iota_i64_k, dim3((unsigned)g), dim3(256), 0, s, (long long*)out, n, (long long)start);
+  PTG_RETURN_LAUNCH();
+}
+
+int ptg_sort_key_decode(const void* sk, long n, int desc, int out32, void* out, hipStream_t s) {
+  if (n <= 0) return 0;
+  const long g = std::min<long>(4096, (n + 255) / 256);
+  hipLaunchKernelGGL(sort_key_decode_k, dim3((unsigned)g), dim3(256), 0, s, (const long long*)sk, n, desc, out32, out);
+  PTG_RETURN_LAUNCH();
+}
 }  // extern "C"

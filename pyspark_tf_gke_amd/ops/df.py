@@ -56,6 +56,45 @@ def expr_eval(prog: bytes, n: int, out, out_valid=None):
 
 
 # ------------------------------------------------------------------------------------------------
+# Device fills / iota (dfutil.hip): the operators use these instead of torch.zeros / ones / full /
+# arange, so a DataFrame query launches only framework kernels.
+def fill(t: torch.Tensor, value) -> torch.Tensor:
+    """t[:] = value (contiguous t; bool / int / float of 1, 2, 4 or 8 bytes)."""
+    if not on_device(t) or not t.is_contiguous():
+        return t.fill_(value)
+    es = t.element_size()
+    if t.dtype == torch.float64:
+        pat = int(np.array(value, dtype=np.float64).view(np.int64))
+    elif t.dtype == torch.float32:
+        pat = int(np.array(value, dtype=np.float32).view(np.int32))
+    else:
+        pat = int(value)
+    pat &= (1 << (8 * es)) - 1
+    if pat >= 1 << 63:
+        pat -= 1 << 64
+    hip("ptg_fill_bytes", ptr(t), t.numel(), es, pat)
+    return t
+
+
+def full(n: int, value, dtype, device) -> torch.Tensor:
+    return fill(torch.empty(n, dtype=dtype, device=device), value)
+
+
+def zeros(n: int, dtype, device) -> torch.Tensor:
+    return full(n, 0, dtype, device)
+
+
+def arange(start: int, stop: int, device) -> torch.Tensor:
+    """int64 [start, stop)."""
+    n = max(0, stop - start)
+    out = torch.empty(n, dtype=torch.int64, device=device)
+    if not on_device(out):
+        return torch.arange(start, start + n, dtype=torch.int64)
+    hip("ptg_iota_i64", ptr(out), n, int(start))
+    return out
+
+
+# ------------------------------------------------------------------------------------------------
 def compact(mask: torch.Tensor) -> torch.Tensor:
     """Ascending int64 indices of the non-zero entries of a uint8/bool mask."""
     n = mask.numel()
@@ -66,7 +105,7 @@ def compact(mask: torch.Tensor) -> torch.Tensor:
     dev = mask.device
     bc = torch.empty(nb, dtype=torch.int32, device=dev)
     bo = torch.empty(nb, dtype=torch.int64, device=dev)
-    tot = torch.zeros(1, dtype=torch.int64, device=dev)
+    tot = zeros(1, torch.int64, dev)
     hip("ptg_compact", ptr(m), n, ptr(bc), ptr(bo), ptr(tot), None)
     total = int(tot.item())
     idx = torch.empty(total, dtype=torch.int64, device=dev)
@@ -265,7 +304,7 @@ def hash_agg(keys: torch.Tensor, vals: list, valids: list, want_minmax: bool = F
     cap = _pow2(2 * (cap_hint if cap_hint else min(n, 1 << 22)) + 16)
     gkeys = torch.empty(cap, dtype=torch.int64, device=dev)
     gtab = torch.empty((1 + 4 * nv) * cap, dtype=torch.float64, device=dev)
-    overflow = torch.zeros(1, dtype=torch.int32, device=dev)
+    overflow = zeros(1, torch.int32, dev)
     hip("ptg_hash_table_init", ptr(gkeys), ptr(gtab), cap, nv)
     vptrs = (ctypes.c_void_p * 4)(*[v.data_ptr() for v in vals])
     vvals = (ctypes.c_void_p * 4)(*[(vd.data_ptr() if vd is not None else 0) for vd in valids])
@@ -280,12 +319,12 @@ def hash_agg(keys: torch.Tensor, vals: list, valids: list, want_minmax: bool = F
 
 def _extract(gkeys, gtab, cap, nv):
     dev = gkeys.device
-    mcount = torch.zeros(1, dtype=torch.int64, device=dev)
+    mcount = zeros(1, torch.int64, dev)
     hip("ptg_hash_extract", ptr(gkeys), ptr(gtab), cap, nv, None, None, 0, ptr(mcount))
     m = int(mcount.item())
     ok = torch.empty(m, dtype=torch.int64, device=dev)
     ot = torch.empty((1 + 4 * nv) * max(m, 1), dtype=torch.float64, device=dev)
-    mcount.zero_()
+    fill(mcount, 0)
     hip("ptg_hash_extract", ptr(gkeys), ptr(gtab), cap, nv, ptr(ok), ptr(ot), m, ptr(mcount))
     ot = ot.view(1 + 4 * nv, max(m, 1))[:, :m]
     outs = [(ot[1 + 4 * j], ot[2 + 4 * j], ot[3 + 4 * j], ot[4 + 4 * j]) for j in range(nv)]
@@ -819,6 +858,10 @@ def sort_key(col: torch.Tensor, desc: bool = False):
 
 def decode_sort_key(sk: torch.Tensor, dtype, desc: bool) -> torch.Tensor:
     """Inverse of :func:`sort_key` for integer columns: orderable u64 bit patterns -> values."""
+    if on_device(sk) and dtype in (torch.int64, torch.int32) and sk.is_contiguous():
+        out = torch.empty(sk.numel(), dtype=dtype, device=sk.device)
+        hip("ptg_sort_key_decode", ptr(sk), sk.numel(), int(desc), int(dtype == torch.int32), ptr(out))
+        return out
     u = ~sk if desc else sk
     x = u ^ torch.iinfo(torch.int64).min  # flip the sign bit back
     return x if dtype == torch.int64 else x.to(dtype)

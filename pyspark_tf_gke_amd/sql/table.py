@@ -44,7 +44,9 @@ class ColumnVector:
 
     def valid_bool(self) -> torch.Tensor:
         if self.valid is None:
-            return torch.ones(len(self), dtype=torch.bool, device=self.device)
+            return D.full(len(self), 1, torch.bool, self.device)
+        if self.valid.dtype == torch.uint8 and self.valid.is_contiguous():
+            return self.valid.view(torch.bool)  # (0 / 1 bytes: the same storage, no conversion kernel)
         return self.valid.bool()
 
     def null_mask(self) -> torch.Tensor:
@@ -64,7 +66,7 @@ class ColumnVector:
 
     def to_pylist(self) -> list:
         data = self.data.detach().cpu()
-        valid = self.valid_bool().cpu().numpy()
+        valid = np.ones(len(self), dtype=bool) if self.valid is None else self.valid_bool().cpu().numpy()
         if isinstance(self.dtype, T.StringType):
             codes = data.numpy()
             d = self.dictionary or []
@@ -153,7 +155,7 @@ class Table:
         return Table({n: c.take(idx) for n, c in self.columns.items()}, int(idx.numel()), self.device)
 
     def slice(self, start: int, stop: int) -> "Table":
-        idx = torch.arange(start, min(stop, self.num_rows), dtype=torch.int64, device=self.device)
+        idx = D.arange(start, min(stop, self.num_rows), self.device)
         return self.take(idx)
 
     def with_column(self, name: str, cv: ColumnVector) -> "Table":
