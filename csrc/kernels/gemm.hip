@@ -185,77 +185,6 @@ struct ConvWgradB {
 };
 
 // ------------------------------------------------------------------------------------------
-// BatchNormalization + ReLU folded into an operand load (ResNet: the BN of a conv whose only
-// consumer is the next conv).  The stored tensor is the previous conv's z; the GEMM sees
-// y = relu(z * scale[c] + shift[c]) rounded to bf16 - exactly what bn_apply_k would have written -
-// and elements the base loader returns as padding (offset out of range) stay zero.  The previous
-// BN's y is then never materialised: its apply pass (read z, write y) disappears and this conv's
-// forward A operand and weight-gradient B operand read z instead of y.
-// ------------------------------------------------------------------------------------------
-struct BnT { const float* scale; const float* shift; };
-
-// 8 consecutive channels c..c+7: unpack, one FMA each, round to bf16, ReLU on the bf16 bit patterns
-// (v_pk_max_i16 with 0: a set sign bit is a negative int16)
-PTG_DEV U4 bn_relu8(U4 v, const BnT& bn, int c) {
-  const float4 s0 = *(const float4*)(bn.scale + c), s1 = *(const float4*)(bn.scale + c + 4);
-  const float4 h0 = *(const float4*)(bn.shift + c), h1 = *(const float4*)(bn.shift + c + 4);
-  float f[8];
-  unpack8(v, f);
-  f[0] = fmaf(f[0], s0.x, h0.x); f[1] = fmaf(f[1], s0.y, h0.y); f[2] = fmaf(f[2], s0.z, h0.z); f[3] = fmaf(f[3], s0.w, h0.w);
-  f[4] = fmaf(f[4], s1.x, h1.x); f[5] = fmaf(f[5], s1.y, h1.y); f[6] = fmaf(f[6], s1.z, h1.z); f[7] = fmaf(f[7], s1.w, h1.w);
-  U4 o = pack8(f);
-  typedef __attribute__((ext_vector_type(2))) short s16x2_t;
-  const s16x2_t z2 = {0, 0};
-  auto relu2 = [&](uint32_t w) {
-    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(s16x2_t, w), z2));
-  };
-  o.x = relu2(o.x); o.y = relu2(o.y); o.z = relu2(o.z); o.w = relu2(o.w);
-  return o;
-}
-
-template <class L> struct BnLoad;
-// 1x1 conv forward A: element (pixel r, channel k..k+7)
-template <> struct BnLoad<MatK<8>> : MatK<8> {
-  static constexpr bool DMA16 = false;  // the transform needs the register path (no LDS-DMA kernel)
-  BnT bn;
-  PTG_DEV U4 load(Rsrc rs, const Ctx& c, int k) const {
-    const uint32_t off = k < K ? c.row + 2u * k : OOB;
-    const U4 v = bload16(rs, off);
-    return off < OOB ? bn_relu8(v, bn, k) : v;
-  }
-};
-// KxK conv forward A (implicit im2col): channel = k mod C
-template <> struct BnLoad<ConvFwdA<8>> : ConvFwdA<8> {
-  static constexpr bool DMA16 = false;
-  BnT bn;
-  PTG_DEV U4 load(Rsrc rs, const Ctx& c, int k) const {
-    const uint32_t off = at(c, k);
-    const U4 v = bload16(rs, off);
-    return off < OOB ? bn_relu8(v, bn, k & (C - 1)) : v;
-  }
-};
-// 1x1 conv weight-gradient B = x^T: rows r0..r0+7 are channels of pixel k
-template <> struct BnLoad<MatMN> : MatMN {
-  BnT bn;
-  PTG_DEV U4 load(Rsrc rs, const Ctx& c, int k) const {
-    const uint32_t off = k < K ? c.col + (uint32_t)(k * ld) * 2u : OOB;
-    const U4 v = bload16(rs, off);
-    return off < OOB ? bn_relu8(v, bn, (int)(c.col >> 1)) : v;
-  }
-};
-// KxK conv weight-gradient B (im2col^T): rows kc = (kh, kw, ci0..ci0+7) of output pixel k
-template <> struct BnLoad<ConvWgradB<8>> : ConvWgradB<8> {
-  BnT bn;
-  PTG_DEV U4 load(Rsrc rs, const Ctx& c, int k) const {
-    const int ohw = OH * OW;
-    const int n = (int)fOHW.div(k), rem = k - n * ohw, oh = (int)fOW.div(rem), ow = rem - oh * OW;
-    const uint32_t off = at(k, n, oh, ow, c.dh0, c.dw0, c.ci0);
-    const U4 v = bload16(rs, off);
-    return off < OOB ? bn_relu8(v, bn, (int)(c.ci0 >> 1)) : v;
-  }
-};
-
-// ------------------------------------------------------------------------------------------
 // Epilogues: called per accumulator element (m, n) inside bounds.
 // ------------------------------------------------------------------------------------------
 enum { ACT_NONE = 0, ACT_RELU = 1 };
@@ -1357,70 +1286,33 @@ int ptg_conv2d_wgrad(const void* x, const void* dz, float* dw, int N, int H, int
   }
 }
 
-// ---- BatchNormalization folded into the conv GEMMs (ResNet, graph_ops.ConvBNOp) ---------------
-// in_scale / in_shift (fp32 [C], both or neither): the conv's INPUT is relu(x * scale + shift) of
-// the stored tensor x (the previous BatchNormalization + ReLU, applied in the operand loader).
+// ---- BatchNormalization statistics from the conv GEMMs (ResNet, graph_ops.ConvBNOp) --------------
 // stats (fp32 [64][2][Cout], accumulated into): batch statistics of the bf16 output z for the
 // following BatchNormalization, produced in the epilogue.
 int ptg_conv_bn_fwd(const void* x, const void* w, const float* bias, void* z, int N, int H, int W, int C, int Cout,
-                    int KH, int KW, int stride, int pad, int OH, int OW, const float* in_scale, const float* in_shift,
-                    float* stats, hipStream_t s) {
-  if (!is_pow2(C) || C < 4 || Cout % 8 || (stats && Cout >= 4096) || (in_scale && C % 8)) return (int)hipErrorInvalidValue;
+                    int KH, int KW, int stride, int pad, int OH, int OW, float* stats, hipStream_t s) {
+  if (!is_pow2(C) || C < 4 || Cout % 8 || (stats && Cout >= 4096)) return (int)hipErrorInvalidValue;
   const int M = N * OH * OW, Kc = KH * KW * C;
   if (!fits((long)N * H * W * C * 2) || !fits((long)M * Cout * 2) || !fits((long)Cout * Kc * 2))
     return (int)hipErrorInvalidValue;
   EpiBf16 epi{(bf16_t*)z, Cout, bias, ACT_NONE, nullptr, 0, stats};
-  const BnT bn{in_scale, in_shift};
   const bf16_t* xb = (const bf16_t*)x;
   if (KH == 1 && KW == 1 && stride == 1 && pad == 0) {  // plain GEMM over the NHWC pixel rows
+    if (C % 8) return (int)hipErrorInvalidValue;
     MatK<8> la{xb, C, M, C, (uint32_t)matk_bytes(C, M, C)};
     MatK<8> lb{(const bf16_t*)w, C, Cout, C, (uint32_t)matk_bytes(C, Cout, C)};
-    if (C % 8) return (int)hipErrorInvalidValue;
-    if (in_scale) return dispatch_gemm(BnLoad<MatK<8>>{la, bn}, lb, epi, M, Cout, C, 1, s);
     return dispatch_gemm(la, lb, epi, M, Cout, C, 1, s);
   }
   if (C % 8 == 0) {
     ConvFwdA<8> la{xb, H, W, C, ilog2(C), OH, OW, KW, stride, pad, M, Kc};
     la.init();
     MatK<8> lb{(const bf16_t*)w, Kc, Cout, Kc, (uint32_t)matk_bytes(Kc, Cout, Kc)};
-    if (in_scale) return dispatch_gemm(BnLoad<ConvFwdA<8>>{la, bn}, lb, epi, M, Cout, Kc, 1, s);
     return dispatch_gemm(la, lb, epi, M, Cout, Kc, 1, s);
   }
   ConvFwdA<4> la{xb, H, W, C, ilog2(C), OH, OW, KW, stride, pad, M, Kc};
   la.init();
   MatK<4> lb{(const bf16_t*)w, Kc, Cout, Kc, (uint32_t)matk_bytes(Kc, Cout, Kc)};
   return dispatch_gemm(la, lb, epi, M, Cout, Kc, 1, s);
-}
-
-// Weight gradient of a conv whose input is relu(x * in_scale + in_shift) (see ptg_conv_bn_fwd):
-// dw (fp32 [Cout][KH][KW][C], accumulated into with split-K atomics) from the stored x and dz.
-int ptg_conv_bn_wgrad(const void* x, const void* dz, float* dw, int N, int H, int W, int C, int Cout, int KH, int KW,
-                      int stride, int pad, int OH, int OW, int splits, const float* in_scale, const float* in_shift,
-                      hipStream_t s) {
-  if (!in_scale || !in_shift || C % 8 || Cout % 8 || !is_pow2(C)) return (int)hipErrorInvalidValue;
-  const int P = N * OH * OW, Kc = KH * KW * C;
-  if (!fits((long)N * H * W * C * 2) || !fits((long)P * Cout * 2)) return (int)hipErrorInvalidValue;
-  const BnT bn{in_scale, in_shift};
-  MatMN la{(const bf16_t*)dz, Cout, Cout, P, (uint32_t)matmn_bytes(Cout, Cout, P)};
-  if (KH == 1 && KW == 1 && stride == 1 && pad == 0) {  // dw[co][ci] = dz^T x over the pixel rows
-    const int tiles = ptg_ceil_div(Cout, 128) * ptg_ceil_div(C, 128);
-    if (splits <= 0) {
-      splits = ptg_ceil_div(512, tiles);
-      if (splits > P / 512) splits = P / 512;
-      if (splits < 1) splits = 1;
-    }
-    MatMN lb{(const bf16_t*)x, C, C, P, (uint32_t)matmn_bytes(C, C, P)};
-    return dispatch_gemm(la, BnLoad<MatMN>{lb, bn}, EpiAtomic{dw, C}, Cout, C, P, splits, s);
-  }
-  if (splits <= 0) {
-    const int tiles = ptg_ceil_div(Cout, Cout <= 16 ? 16 : (Cout <= 32 ? 32 : 64)) * ptg_ceil_div(Kc, 128);
-    splits = ptg_ceil_div(512, tiles);
-    const int max_splits = ptg_ceil_div(P, 4 * BK);
-    if (splits > max_splits) splits = max_splits;
-  }
-  ConvWgradB<8> lb{(const bf16_t*)x, H, W, C, ilog2(C), OH, OW, KW, stride, pad, P, Kc};
-  lb.init();
-  return dispatch_gemm_narrow_m(la, BnLoad<ConvWgradB<8>>{lb, bn}, EpiAtomic{dw, Kc}, Cout, Kc, P, splits, s);
 }
 
 }  // extern "C"

@@ -216,8 +216,6 @@ def _lower(nodes: list, input_idx: int) -> list:
         if inner is None:
             raise NotImplementedError(f"functional lowering of {type(layer).__name__}")
         ops.append(G.Adapter(inner(layer), [src(ins[0])], k))
-    if G.BN_FUSE:
-        _fuse_bn_links(ops)
     _bn_bwd_links(ops)
     # dense relu-mask hand-off as in the Sequential engine
     for a, b in zip(ops, ops[1:]):
@@ -227,29 +225,6 @@ def _lower(nodes: list, input_idx: int) -> list:
             ib.mask_for_prev, ib._prev_big, ib._prev_op = True, ia.big, ia
             ia.grad_masked_by_next = True
     return ops
-
-
-def _fuse_bn_links(ops) -> None:
-    """Conv -> BN -> ReLU feeding exactly one Conv -> BN op (a ResNet bottleneck's 1x1 -> 3x3 -> 1x1
-    chain): the producer skips its BN apply and the consumer applies it in its operand loaders."""
-    uses: dict = {}
-    for op in ops:
-        for i in op.inputs:
-            uses.setdefault(i, []).append(op)
-    for a in ops:
-        pa = getattr(a, "op", None)
-        if not isinstance(pa, G.ConvBNOp) or not pa.relu or pa.residual:
-            continue
-        cons = uses.get(a.output, [])
-        if len(cons) != 1 or not isinstance(getattr(cons[0], "op", None), G.ConvBNOp):
-            continue
-        b = cons[0]
-        if b.inputs[0] != a.output or a.output in b.inputs[1:] or b.op.in_bn_op is not None:
-            continue
-        if not G.bn_input_ok(b.op.conv, b.op.pad):
-            continue
-        pa.defer = True
-        b.op.in_bn_op = pa
 
 
 def _bn_bwd_links(ops) -> None:

@@ -99,11 +99,9 @@ class GraphOp:
 # implicit-GEMM path is faster, so graph ops use the halo kernels for 5x5 only.
 HALO_KS = (5,)
 # BatchNormalization fusion: every ConvBNOp's batch statistics come out of its conv GEMM's epilogue
-# (PTG_BN_EPI_STATS; no bn_stats pass over z), and (PTG_BN_FUSE) a Conv -> BN -> ReLU whose only consumer is
-# another ConvBNOp leaves its BN + ReLU to that consumer's operand loaders (forward A operand and
-# weight-gradient B operand read the stored z and apply relu(z*scale + shift) in registers), so its
-# apply pass and its y tensor disappear (gemm.hip BnLoad / EpiBf16 stats).
-BN_FUSE = config.get("bn_fuse")
+# (PTG_BN_EPI_STATS; no bn_stats pass over z; gemm.hip EpiBf16 stats).  (Applying the previous BN + ReLU
+# in the next conv's operand loaders instead of a bn_apply pass measured slower - 8.04k vs 8.75k img/s
+# - and was removed in round 5.)
 BN_EPI_STATS = config.get("bn_epi_stats")
 # Backward: a Conv -> BN -> ReLU block whose output feeds exactly one ConvBNOp gets its BN backward
 # sums (sum g, sum g*z) from the epilogue of that consumer's dgrad GEMM, which also applies the ReLU
@@ -116,28 +114,17 @@ def _pow2(v):
     return v > 0 and (v & (v - 1)) == 0
 
 
-def bn_input_ok(conv: L.Conv2D, pad: int) -> bool:
-    """A conv that can apply its producer's BN + ReLU in its loaders (implicit-GEMM / 1x1 GEMM path)."""
-    C, KH = conv.cin_p, conv.kernel_size[0]
-    same = pad == KH // 2 and conv.kernel_size[0] == conv.kernel_size[1] and conv.strides[0] == 1
-    halo = KH in HALO_KS and K.halo_eligible(C, conv.out_shape[-1], KH, conv.strides[0], same)
-    return C % 8 == 0 and _pow2(C) and not halo and conv.out_shape[-1] % 8 == 0
-
-
-def conv_forward(x, w, bias, stride, pad, z, in_bn=None, stats=None) -> bool:
-    """z = conv(x) (+ bias).  ``in_bn``: (scale, shift) of the producer's BN + ReLU to apply to x on
-    load; ``stats``: [64,2,Cout] partial sums for this op's BN, filled by the conv epilogue when it
-    can.  Returns True when ``stats`` were produced."""
+def conv_forward(x, w, bias, stride, pad, z, stats=None) -> bool:
+    """z = conv(x) (+ bias).  ``stats``: [64,2,Cout] partial sums for this op's BN, filled by the conv
+    epilogue when it can.  Returns True when ``stats`` were produced."""
     N, H, W, C = x.shape
     Co, KH, KW, _ = w.shape
-    if in_bn is not None or stats is not None:
+    if stats is not None:
         same = pad == KH // 2 and KH == KW and stride == 1
         halo = KH in HALO_KS and K.halo_eligible(C, Co, KH, stride, same)
-        if not halo and _pow2(C) and C >= 4 and (in_bn is None or C % 8 == 0) and Co % 8 == 0:
-            K.conv_bn_fwd(x, w, bias, stride, pad, z, in_bn, stats)
-            return stats is not None
-        if in_bn is not None:
-            raise RuntimeError("conv_forward: BN-on-load input for a conv outside the implicit-GEMM path")
+        if not halo and _pow2(C) and C >= 4 and Co % 8 == 0:
+            K.conv_bn_fwd(x, w, bias, stride, pad, z, stats)
+            return True
     if not K.on_device(x):
         K.conv2d_fwd(x, w, bias, stride, pad, z, None)
         return False
@@ -153,13 +140,11 @@ def conv_forward(x, w, bias, stride, pad, z, in_bn=None, stats=None) -> bool:
     return False
 
 
-def conv_wgrad(x, dz, stride, pad, dw, in_bn=None):
-    """dw (fp32, already zeroed by the store) += d(conv)/dw; ``in_bn`` as in :func:`conv_forward`."""
+def conv_wgrad(x, dz, stride, pad, dw):
+    """dw (fp32, already zeroed by the store) += d(conv)/dw."""
     N, H, W, C = x.shape
     _, OH, OW, Co = dz.shape
     _, KH, KW, _ = dw.shape
-    if in_bn is not None:
-        return K.conv_bn_wgrad(x, dz, stride, pad, dw, in_bn)
     if not K.on_device(x):
         return K.conv2d_wgrad(x, dz, stride, pad, dw, accumulate=True)
     if KH == KW == 1 and stride == 1 and pad == 0:
@@ -254,10 +239,6 @@ class ConvBNOp:
         self.pad = conv.pad_amount() + extra_pad
         self.name = conv.name
         self.state = _BNState(bn, conv.name)
-        # set by the graph lowering (functional._fuse_bn_links): defer = our BN + ReLU is applied by
-        # our single consumer's loaders; in_bn_op = the producer whose BN + ReLU we apply on load
-        self.defer = False
-        self.in_bn_op = None
         # the Conv -> BN -> ReLU producer whose BN backward sums our dgrad epilogue computes (set by
         # functional._bn_bwd_links); _bwd_stats_done marks a step in which it did
         self.bwd_bn_op = None
@@ -276,16 +257,8 @@ class ConvBNOp:
         xi[..., : x.shape[-1]] = x
         return xi
 
-    def _in_bn(self, ws, dev):
-        """(scale, shift) of the producer's BN when its apply is folded into our loads."""
-        p = self.in_bn_op
-        if p is None:
-            return None
-        _, scale, shift, _, _, _ = p.state.bufs(ws, p.conv.out_shape[-1], dev)
-        return scale, shift
-
     def forward(self, xs, ws, training):
-        x = xs[0] if self.in_bn_op is not None else self._prep_input(xs[0], ws)
+        x = self._prep_input(xs[0], ws)
         res = xs[1] if self.residual else None
         if res is not None:
             res = _bf16(res, ws, self.name + "/res16")
@@ -294,14 +267,9 @@ class ConvBNOp:
         dev = x.device
         z = ws.get(self.name + "/z", (B, OH, OW, Co), torch.bfloat16, dev)
         b = self.conv.bias.data if self.conv.bias is not None else None
-        in_bn = self._in_bn(ws, dev)
         part = self.state.bufs(ws, Co, dev)[0] if (training and BN_EPI_STATS) else None
-        stats_done = conv_forward(x, self.conv.kernel.bf16, b, self.stride, self.pad, z, in_bn, part)
-        self._x, self._z, self._in_bn_t = x, z, in_bn
-        if self.defer:
-            self.state.forward(z, None, self.relu, None, ws, training, stats_done, apply=False)
-            self._y = None
-            return z  # the consumer applies relu(z*scale + shift) itself
+        stats_done = conv_forward(x, self.conv.kernel.bf16, b, self.stride, self.pad, z, part)
+        self._x, self._z = x, z
         y = ws.get(self.name + "/y", z.shape, torch.bfloat16, dev)
         self.state.forward(z, res, self.relu, y, ws, training, stats_done)
         self._y = y
@@ -316,8 +284,7 @@ class ConvBNOp:
         done, self._bwd_stats_done = self._bwd_stats_done, False
         self.state.backward(dy, y, z, self.relu, dz, dres, ws, stats_done=done)
         g = self.conv.kernel.grad
-        in_bn = self._in_bn_t
-        S.launch(lambda: conv_wgrad(x, dz, self.stride, self.pad, g, in_bn), dev)
+        S.launch(lambda: conv_wgrad(x, dz, self.stride, self.pad, g), dev)
         dx = None
         if not self.first:
             ex = existing[0]

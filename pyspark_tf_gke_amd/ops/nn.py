@@ -276,12 +276,6 @@ def conv2d_wgrad_halo_sparse(x, dzsel, arg, pad: int, out, zeroed: bool = False)
     return out
 
 
-def bn_relu_host(x, in_bn):
-    """relu(x * scale + shift) rounded to x's dtype: the host form of the BN-on-load operand."""
-    sc, sh = in_bn
-    return torch.relu(x.float() * sc.float() + sh.float()).to(x.dtype)
-
-
 def _conv_shape(x, w, stride, pad):
     N, H, W, C = x.shape
     Co, KH, KW, Cw = w.shape
@@ -289,44 +283,26 @@ def _conv_shape(x, w, stride, pad):
     return N, H, W, C, Co, KH, KW, (H + 2 * pad - KH) // stride + 1, (W + 2 * pad - KW) // stride + 1
 
 
-def conv_bn_fwd(x, w, bias, stride: int, pad: int, z, in_bn=None, stats=None):
-    """z = conv(x', w) + bias (implicit-GEMM MFMA conv, gemm.hip ptg_conv_bn_fwd) where x' = x, or
-    relu(x * scale + shift) with ``in_bn = (scale, shift)`` - the previous BatchNormalization + ReLU
-    applied inside the operand loader, so its output is never written.  ``stats`` ([64, 2, Cout]
-    fp32): the batch statistics (sum, sum of squares) of the stored z are added in the epilogue."""
+def conv_bn_fwd(x, w, bias, stride: int, pad: int, z, stats=None):
+    """z = conv(x, w) + bias (implicit-GEMM MFMA conv, gemm.hip ptg_conv_bn_fwd); ``stats`` ([64, 2,
+    Cout] fp32): the batch statistics (sum, sum of squares) of the stored z are added in the epilogue."""
     N, H, W, C, Co, KH, KW, OH, OW = _conv_shape(x, w, stride, pad)
     assert tuple(z.shape) == (N, OH, OW, Co), (z.shape, (N, OH, OW, Co))
     if not on_device(x):
-        xin = bn_relu_host(x, in_bn) if in_bn is not None else x
-        ref.conv2d_fwd(xin, w, bias, stride, pad, z, None)
+        ref.conv2d_fwd(x, w, bias, stride, pad, z, None)
         if stats is not None:
             zf = z.float().reshape(-1, Co)
             stats[0, 0] += zf.sum(0)
             stats[0, 1] += (zf * zf).sum(0)
         return z
     need(x, torch.bfloat16, "conv_bn.x"); need(w, torch.bfloat16, "conv_bn.w"); need(z, torch.bfloat16, "conv_bn.z")
-    sc, sh = in_bn if in_bn is not None else (None, None)
     if stats is not None:
         need(stats, torch.float32, "conv_bn.stats")
         assert tuple(stats.shape) == (64, 2, Co), stats.shape
-    hip("ptg_conv_bn_fwd", ptr(x), ptr(w), ptr(bias), ptr(z), N, H, W, C, Co, KH, KW, stride, pad, OH, OW, ptr(sc),
-        ptr(sh), ptr(stats))
+    hip("ptg_conv_bn_fwd", ptr(x), ptr(w), ptr(bias), ptr(z), N, H, W, C, Co, KH, KW, stride, pad, OH, OW,
+        ptr(stats))
     return z
 
-
-def conv_bn_wgrad(x, dz, stride: int, pad: int, dw, in_bn, splits: int = 0):
-    """dw (fp32, accumulated into) = d(conv)/dw of a conv whose input was relu(x * scale + shift)
-    (``in_bn = (scale, shift)``, see :func:`conv_bn_fwd`); x is the stored pre-BN tensor."""
-    if not on_device(x):
-        return ref.conv2d_wgrad(bn_relu_host(x, in_bn), dz, stride, pad, dw, accumulate=True)
-    N, H, W, C = x.shape
-    _, OH, OW, Co = dz.shape
-    _, KH, KW, _ = dw.shape
-    need(dw, torch.float32, "conv_bn_wgrad.dw")
-    sc, sh = in_bn
-    hip("ptg_conv_bn_wgrad", ptr(x), ptr(dz), ptr(dw), N, H, W, C, Co, KH, KW, stride, pad, OH, OW, splits, ptr(sc),
-        ptr(sh))
-    return dw
 
 
 def _conv1_check(x, w, alpha, N, H, W):

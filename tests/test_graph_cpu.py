@@ -65,36 +65,6 @@ def test_resnet_small_grads_match_autograd(blocks, fp32_host):
         assert _rel(eg, rg) < 1e-3, (name, _rel(eg, rg))
 
 
-def test_bn_fusion_defers_bottleneck_links(fp32_host, monkeypatch):
-    """PTG_BN_FUSE lowering: in every bottleneck the 1x1 -> 3x3 and 3x3 -> 1x1 links keep their BN +
-    ReLU for the consumer's loaders (no y tensor), block outputs (residual) are never deferred, and
-    gradients equal the unfused plan's."""
-    from pyspark_tf_gke_amd.nn import graph_ops as G
-
-    torch.manual_seed(0)
-    x = torch.rand(4, 32, 32, 3)
-    y = torch.randint(0, 10, (4,))
-    grads = {}
-    for fuse in (False, True):
-        monkeypatch.setattr(G, "BN_FUSE", fuse)
-        monkeypatch.setattr(G, "BN_EPI_STATS", fuse)
-        torch.manual_seed(1)
-        m = ResNet((2, 1), input_shape=(32, 32, 3), classes=10, width=8, device="cpu")
-        m.compile(optimizer=nn.optimizers.SGD(0.0), loss="sparse_categorical_crossentropy")
-        convbn = [op.op for op in m.ops if isinstance(getattr(op, "op", None), G.ConvBNOp)]
-        deferred = [o.name for o in convbn if o.defer]
-        if fuse:
-            assert sorted(deferred) == sorted(n for n in (o.name for o in convbn) if n.endswith(("_1_conv", "_2_conv")))
-            assert all(o.in_bn_op is not None for o in convbn if o.name.endswith(("_2_conv", "_3_conv")))
-            assert not any(o.defer for o in convbn if o.residual)
-        else:
-            assert not deferred
-        grads[fuse] = _engine_grads(m, x, y)
-    assert abs(grads[True][0] - grads[False][0]) < 1e-5
-    for name, g0 in grads[False][1].items():
-        assert _rel(grads[True][1][name], g0) < 1e-4, name
-
-
 def test_resnet_small_bf16_close_to_autograd():
     """The real (bf16-activation) host path: same directions, bf16-level deviations."""
     torch.manual_seed(0)
