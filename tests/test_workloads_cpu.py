@@ -149,3 +149,14 @@ def test_model_checker_writes_plots(tmp_path):
                "--device", "cpu")
     assert out.count("predicted (x=") == 2
     assert sorted(os.listdir(mdir / "plots")) == ["spot0.png", "spot1.png"]
+
+
+def test_train_tf_ps_use_ps_async(tmp_path):
+    """The reference driver's parameter-server path in asynchronous mode
+    (`train_tf_ps.py --use-ps --ps-mode async`, train_tf_ps.py:505-510,612-645): one process, the
+    coordinator loop trains two epochs and the chief saves the model."""
+    out = _run(os.path.join(TF, "train_tf_ps.py"), "--use-ps", "--ps-mode", "async", "--worker-replicas", "1",
+               "--ps-replicas", "1", "--data-path", HEALTH, "--epochs", "2", "--batch-size", "512", "--output-dir",
+               str(tmp_path), "--chief-addr", "127.0.0.1", env={"PTG_PS_MODE": "sync"})  # the flag wins
+    assert "Epoch 2" in out and "loss:" in out, out[-2000:]
+    assert os.path.exists(os.path.join(str(tmp_path), "model.keras"))
