@@ -1,7 +1,8 @@
 #!/usr/bin/env python
 """Per-kernel roofline of one CNN-B1 training step (train_tf_ps.py:346-378, flat=True, 256x320x3,
-batch B) from a rocprofv3 kernel trace, for the round-4 kernel set (uint8 input read by the first
-layer's kernels, fused head, fused Dense dW + Adam).
+batch B) from a rocprofv3 kernel trace, for the round-4 / round-5 kernel sets (uint8 input read by the
+first layer's kernels, fused head, fused Dense dW + Adam; round 5: dense.hip forward / dX, the
+multi-range Adam that also writes the flipped dgrad filters).
 
 Each kernel of one steady-state step (between two consecutive conv1_fwd_rec_k launches) is mapped by
 NAME to the op it implements; the three prelu_pool_bwd launches are told apart by their order (layers
@@ -47,7 +48,7 @@ def ops(B):
     o["head (Dense2 + MSE, fwd+bwd)"] = (8.0 * B * 2048, B * 2048 * f32 * 2)
     o["Dense dX"] = (2.0 * B * F * 2048, B * 2048 * bf + 2048 * F * bf + B * F * bf)
     o["Dense dW + Adam"] = (2.0 * B * F * 2048, B * 2048 * bf + B * F * bf + 2048 * F * (3 * f32 + 3 * f32 + bf))
-    o["Adam (small params)"] = (0.0, 1.42e6 * 26)
+    o["Adam (small params)"] = (0.0, 1.42e6 * 34)  # p, g, m, v read; p, m, v, bf16 p, g = 0 written
     o["dgrad filter flips"] = (0.0, 2 * 2 * 25 * (8 * 16 + 16 * 32 + 32 * 64 + 64 * 64))
     return o
 
@@ -80,6 +81,12 @@ def classify(name, ppb_seen):
         return "L1 bwd (recompute, dW, dalpha, dbias)"
     if "EpiAdam" in name:
         return "Dense dW + Adam"
+    if "dense_fwd_sk_k" in name:
+        return "Dense fwd (split-K)"
+    if "dense_dx" in name:
+        return "Dense dX"
+    if name.startswith("adam_multi_k"):
+        return "Adam (small params)"
     if "EpiAtomic" in name:
         return "Dense fwd (split-K)"
     if "gemm_kernel<256, 80" in name or "gemm_kernel<256, 64" in name or "Cijk" in name:
