@@ -234,10 +234,23 @@ st = ParameterServerStrategy(mode="async", variable_partitioner=MinSizePartition
 m, o = make(st, lr=5e-3)
 ref, ro = make(st, lr=5e-3)
 co = ClusterCoordinator(st)
+# rank 1 arrives late: it joins only after rank 0 has run every closure (a flag file written by the
+# 8th closure, not a sleep, so a loaded machine cannot let it draw one); its service thread applies
+# its shards meanwhile
+flag = f"/tmp/ptg_ps_seq_{os.environ['MASTER_PORT']}.done"
+ran = [0]
+def fn(m, o, i):
+    out = step_fn(m, o, i)
+    ran[0] += 1
+    if ran[0] == 8:
+        open(flag, "w").close()
+    return out
 for i in range(8):
-    co.schedule(step_fn, args=(m, o, i))
+    co.schedule(fn, args=(m, o, i))
 if st.rank == 1:
-    time.sleep(1.5)
+    t_end = time.time() + 120
+    while not os.path.exists(flag) and time.time() < t_end:
+        time.sleep(0.05)
 co.join()
 st.synchronize_master(m)
 from pyspark_tf_gke_amd.nn import engine as E
