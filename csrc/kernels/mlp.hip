@@ -27,6 +27,8 @@
 
 namespace ptgm {
 
+typedef __attribute__((address_space(3))) void lds_t;
+
 #ifdef PTG_MLP_PROF  // phase timestamps of the first step (A/B build: tools/mlp_phases.py)
 __device__ long long g_mlp_prof[32];
 #define MLP_T(i) \
@@ -56,6 +58,10 @@ struct MlpDesc {
   int ly;                       // LDS float offset of the step's labels / targets
   float lr, b1, b2, eps;
   int t0;                       // optimizer steps taken before this launch
+  // LDS-resident Adam state (res): the flat span [lo, lo + rn) of p / m / v covering every layer is
+  // copied into LDS by the prologue's LDS-DMA loads (p staged at lps, m / v live at lpm / lpv)
+  int res, rn, lps, lpm, lpv;
+  long lo;
 };
 
 // Workgroup barrier for LDS only.  __syncthreads() also waits for this wave's outstanding GLOBAL
@@ -127,16 +133,22 @@ struct AdamArgs {
   float lr_t, b1, b2, eps;
 };
 
-PTG_DEV float adam_update(const AdamArgs& o, long idx, float g, float p0, float m0, float v0) {
+// Adam on one element; m0 / v0 come back updated.  The HBM copies are written when `store`: every
+// step, or only the launch's last step when the moments live in LDS.
+PTG_DEV float adam_update(const AdamArgs& o, long idx, float g, float p0, float& m0, float& v0, bool store) {
   const float mm = o.b1 * m0 + (1.f - o.b1) * g;
   const float vv = o.b2 * v0 + (1.f - o.b2) * g * g;
   // v_sqrt_f32 / v_rcp_f32 (1 ulp) instead of the IEEE sequences: ~25 fewer dependent VALU ops per
   // element on this latency-bound single-workgroup step
   const float pp = p0 - o.lr_t * mm * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vv) + o.eps);
-  o.m[idx] = mm;
-  o.v[idx] = vv;
-  o.p[idx] = pp;
-  if (o.pbf) o.pbf[idx] = f2bf(pp);
+  m0 = mm;
+  v0 = vv;
+  if (store) {
+    o.m[idx] = mm;
+    o.v[idx] = vv;
+    o.p[idx] = pp;
+    if (o.pbf) o.pbf[idx] = f2bf(pp);
+  }
   return pp;
 }
 
@@ -145,11 +157,16 @@ PTG_DEV float adam_update(const AdamArgs& o, long idx, float g, float p0, float 
 // column j = Nw whose Q entries are the constant-1 column every activation row carries at index Nw, so
 // the same MFMAs produce db[i] = sum_k P[i][k] (Adam on element bo + i, LDS copy Bl / Bc) - no serial
 // per-unit reduction over the batch.  A lane's four outputs have their p / m / v read BEFORE the MFMAs
-// (from HBM: the latency hides under the k loop; the weight itself from its current LDS copy Wc / Bc);
-// the updated value also goes to the LDS copy Wl / Bl.
+// (the weight itself from its current LDS copy Wc / Bc; the moments from the LDS-resident copies
+// Ml / Vl at element - lo, or else from HBM, whose latency then partly hides under the k loop); the
+// updated value also goes to the LDS copy Wl / Bl.
+// RES is a template argument so that the resident form has no global load at all: a run-time select
+// between the LDS and HBM pointers compiles to FLAT loads, whose vmcnt waits then also wait for every
+// earlier global store of the phase.
+template <bool RES>
 PTG_DEV void dw_adam(int M, int Nw, int K, const float* P, int pi, int pk, const float* Q, int qj, int qk,
                      const AdamArgs& o, long wo, long bo, float* Wl, int S, const float* Wc, float* Bl,
-                     const float* Bc) {
+                     const float* Bc, float* Ml, float* Vl, long lo, bool store) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int r16 = lane & 15, kq = lane >> 4;
   const int N = Nw + (bo >= 0 ? 1 : 0);
@@ -163,16 +180,24 @@ PTG_DEV void dw_adam(int M, int Nw, int K, const float* P, int pi, int pk, const
       const bool isb = j == Nw;
       const long idx = isb ? bo + i : wo + (long)i * Nw + j;
       p0[r] = isb ? Bc[i] : Wc[i * S + j];
-      m0[r] = o.m[idx];
-      v0[r] = o.v[idx];
+      if constexpr (RES) {
+        m0[r] = Ml[idx - lo];
+        v0[r] = Vl[idx - lo];
+      } else {
+        m0[r] = o.m[idx];
+        v0[r] = o.v[idx];
+      }
     }
     const f32x4_t acc = mfma_dot(K, P + min(i0 + r16, M - 1) * pi, pk, Q + min(j0 + r16, N - 1) * qj, qk, kq);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int i = i0 + 4 * kq + r, j = j0 + r16;
       if (i < M && j < N) {
-        if (j == Nw) Bl[i] = adam_update(o, bo + i, acc[r], p0[r], m0[r], v0[r]);
-        else Wl[i * S + j] = adam_update(o, wo + (long)i * Nw + j, acc[r], p0[r], m0[r], v0[r]);
+        const long idx = j == Nw ? bo + i : wo + (long)i * Nw + j;
+        const float pp = adam_update(o, idx, acc[r], p0[r], m0[r], v0[r], store);
+        if (j == Nw) Bl[i] = pp;
+        else Wl[i * S + j] = pp;
+        if constexpr (RES) { Ml[idx - lo] = m0[r]; Vl[idx - lo] = v0[r]; }
       }
     }
   }
@@ -199,6 +224,9 @@ __global__ __launch_bounds__(NT) void mlp_train_k(const float* __restrict__ x, c
   extern __shared__ __align__(16) float sm[];
   const int tid = threadIdx.x;
   const int L = D.L, B = D.B;
+#ifdef PTG_MLP_PROF
+  if (tid == 0) g_mlp_prof[31] = wall_clock64();
+#endif
   const int t0 = tstep ? (int)tstep[0] : D.t0;
   // step 0's inputs and labels: loads issued first, stored to LDS after the weight loads (one HBM
   // round trip for the whole prologue instead of two)
@@ -215,13 +243,39 @@ __global__ __launch_bounds__(NT) void mlp_train_k(const float* __restrict__ x, c
       yr[u] = i < ny ? (D.loss == 0 ? __int_as_float(((const int*)y)[i]) : ((const float*)y)[i]) : 0.f;
     }
   }
-  // weights + biases -> LDS (the Adam epilogues keep them current in place)
-  for (int l = 0; l < L; ++l) {
-    const int K = D.d[l], N = D.d[l + 1], S = D.ws[l];
-    for (int i = tid; i < N * K; i += NT) sm[D.lw[l] + (i / K) * S + i % K] = p[D.woff[l] + i];
-    for (int n = tid; n < N; n += NT) {
-      sm[D.lb[l] + n] = D.boff[l] >= 0 ? p[D.boff[l] + n] : 0.f;
-      if (D.dbl && D.boff[l] < 0) sm[D.wtot + D.lb[l] + n] = 0.f;  // bias-less: zeros in both copies
+  // weights + biases -> LDS (the Adam epilogues keep them current in place).  res: one LDS-DMA
+  // burst brings the p / m / v span (1 KB per wave instruction, all in flight together), then p is
+  // spread into the padded weight layout LDS -> LDS; otherwise per-element loads.
+  if (D.res) {
+    const int lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t bytes = (uint32_t)D.rn * 4u;
+    const Rsrc rp = make_rsrc(p + D.lo, bytes), rm = make_rsrc(m + D.lo, bytes), rv = make_rsrc(v + D.lo, bytes);
+    unsigned char* sb = (unsigned char*)sm;
+    for (int c = wid; c * 256 < D.rn; c += NT / 64) {
+      const uint32_t off = (uint32_t)c * 1024u + (uint32_t)lane * 16u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rp, (lds_t*)(sb + D.lps * 4 + c * 1024), 16, off, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rm, (lds_t*)(sb + D.lpm * 4 + c * 1024), 16, off, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, (lds_t*)(sb + D.lpv * 4 + c * 1024), 16, off, 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const float* ps = sm + D.lps - D.lo;
+    for (int l = 0; l < L; ++l) {
+      const int K = D.d[l], N = D.d[l + 1], S = D.ws[l];
+      for (int i = tid; i < N * K; i += NT) sm[D.lw[l] + (i / K) * S + i % K] = ps[D.woff[l] + i];
+      for (int n = tid; n < N; n += NT) {
+        sm[D.lb[l] + n] = D.boff[l] >= 0 ? ps[D.boff[l] + n] : 0.f;
+        if (D.dbl && D.boff[l] < 0) sm[D.wtot + D.lb[l] + n] = 0.f;
+      }
+    }
+  } else {
+    for (int l = 0; l < L; ++l) {
+      const int K = D.d[l], N = D.d[l + 1], S = D.ws[l];
+      for (int i = tid; i < N * K; i += NT) sm[D.lw[l] + (i / K) * S + i % K] = p[D.woff[l] + i];
+      for (int n = tid; n < N; n += NT) {
+        sm[D.lb[l] + n] = D.boff[l] >= 0 ? p[D.boff[l] + n] : 0.f;
+        if (D.dbl && D.boff[l] < 0) sm[D.wtot + D.lb[l] + n] = 0.f;  // bias-less: zeros in both copies
+      }
     }
   }
   if (xpre) {
@@ -333,6 +387,7 @@ __global__ __launch_bounds__(NT) void mlp_train_k(const float* __restrict__ x, c
     const float t = (float)(t0 + st + 1);
     const float lr_t = D.lr * sqrtf(1.f - powf(D.b2, t)) / (1.f - powf(D.b1, t));
     const AdamArgs ad{p, m, v, pbf, lr_t, D.b1, D.b2, D.eps};
+    const bool store = !D.res || st == D.steps - 1;  // LDS-resident state: HBM copies at the end only
     int cur = D.lg0, nxt = D.lg1;
     for (int l = L - 1; l >= 0; --l) {
       const int K = D.d[l], N = D.d[l + 1], S = D.ws[l], SA = D.as[l];
@@ -352,8 +407,12 @@ __global__ __launch_bounds__(NT) void mlp_train_k(const float* __restrict__ x, c
       MLP_T(10 + 2 * (L - 1 - l))
       // dW[n][k] = sum_r G[r][n] A[r][k] and db[n] = sum_r G[r][n] (A's constant-1 column), Adam
       // straight from the register
-      dw_adam(N, K, B, Gc, 1, D.gs, A, 1, SA, ad, D.woff[l], D.boff[l], sm + wnxt + D.lw[l], S, sm + wcur + D.lw[l],
-              sm + wnxt + D.lb[l], sm + wcur + D.lb[l]);
+      if (D.res)
+        dw_adam<true>(N, K, B, Gc, 1, D.gs, A, 1, SA, ad, D.woff[l], D.boff[l], sm + wnxt + D.lw[l], S,
+                      sm + wcur + D.lw[l], sm + wnxt + D.lb[l], sm + wcur + D.lb[l], sm + D.lpm, sm + D.lpv, D.lo, store);
+      else
+        dw_adam<false>(N, K, B, Gc, 1, D.gs, A, 1, SA, ad, D.woff[l], D.boff[l], sm + wnxt + D.lw[l], S,
+                       sm + wcur + D.lw[l], sm + wnxt + D.lb[l], sm + wcur + D.lb[l], nullptr, nullptr, 0, true);
       lds_barrier();
       MLP_T(11 + 2 * (L - 1 - l))
       const int tmp = cur; cur = nxt; nxt = tmp;
@@ -423,6 +482,33 @@ static long mlp_plan(const long* hdesc, int L, int B, ptgm::MlpDesc* D) {
     for (int l = 0; l <= L; ++l) D->la[l] += D->wtot;
     D->lg0 += D->wtot; D->lg1 += D->wtot; D->lred += D->wtot; D->ly += D->wtot;
     off += D->wtot;
+  }
+  // LDS-resident Adam state: the 16-B aligned span of every W / b, three copies (p staging, m, v) in
+  // whole 1 KB DMA chunks, when it fits next to the rest (PTG_MLP_RES=0: per-element HBM moments)
+  D->res = 0;
+  {
+    long lo = D->woff[0], hi = 0, used = 0;
+    for (int l = 0; l < L; ++l) {
+      const long nw = (long)D->d[l] * D->d[l + 1];
+      lo = lo < D->woff[l] ? lo : D->woff[l];
+      hi = hi > D->woff[l] + nw ? hi : D->woff[l] + nw;
+      used += nw;
+      if (D->boff[l] >= 0) {
+        lo = lo < D->boff[l] ? lo : D->boff[l];
+        hi = hi > D->boff[l] + D->d[l + 1] ? hi : D->boff[l] + D->d[l + 1];
+        used += D->d[l + 1];
+      }
+    }
+    lo &= ~3L;
+    const long rn = hi - lo, rpad = (rn + 255) / 256 * 256;
+    const char* re = getenv("PTG_MLP_RES");
+    const bool want = !(re && re[0] == '0');
+    int o4 = (off + 3) & ~3;  // 16-B aligned regions
+    if (want && rn <= 4 * used + 256 && (long)(o4 + 3 * rpad) * 4 <= 160 * 1024) {
+      D->res = 1; D->lo = lo; D->rn = (int)rn;
+      D->lps = o4; D->lpm = o4 + (int)rpad; D->lpv = o4 + 2 * (int)rpad;
+      off = o4 + 3 * (int)rpad;
+    }
   }
   // softmax loss with one row per lane group (PTG_MLP_LOSS_LANES=0: one thread per row)
   const char* lz = getenv("PTG_MLP_LOSS_LANES");

@@ -59,6 +59,33 @@ def test_mlp_tracks_reference(hip_built):
         assert abs(a["accuracy"] - b["accuracy"]) < 1e-6
 
 
+def test_mlp_lds_resident_adam_state_matches_hbm(hip_built, monkeypatch):
+    """mlp.hip with the p / m / v span brought into LDS by one DMA burst (and the HBM copies written
+    only at a launch's last step) == the per-element HBM path, bit for bit, over single- and
+    multi-step launches at batch 32 and 64."""
+    from pyspark_tf_gke_amd.nn import optimizers
+
+    for B in (32, 64):
+        g = torch.Generator().manual_seed(B)
+        x = torch.randn(8 * B, 3, generator=g).cuda()
+        y = torch.randint(0, 15, (8 * B,), generator=g, dtype=torch.int32).cuda()
+        out = []
+        for res in ("1", "0"):
+            monkeypatch.setenv("PTG_MLP_RES", res)
+            torch.manual_seed(0)
+            m = build_deep_model(3, 15, device="cuda")
+            m.compile(optimizer=optimizers.Adam(1e-2), loss=m.loss, metrics=m.metric_names)
+            st = m._stats_buf()
+            plan = m._mlp_fusable(x[:B], y[:B], m._strategy())
+            assert plan is not None
+            for steps, r0 in ((4, 0), (1, 4), (3, 5)):
+                m._train_step_mlp(x[r0 * B:(r0 + steps) * B], y[r0 * B:(r0 + steps) * B], st, plan, steps=steps)
+            torch.cuda.synchronize()
+            out.append((m.store.flat.clone(), m.optimizer.m.clone(), m.optimizer.v.clone(), st.clone()))
+        for a, b in zip(out[0], out[1]):
+            assert torch.equal(a, b), (B, (a - b).abs().max().item())
+
+
 def test_mnist_cnn_learns(hip_built):
     torch.manual_seed(0)
     m = build_mnist_cnn(device="cuda")

@@ -25,7 +25,7 @@ x = torch.randn(B, 3, device=dev)
 y = torch.randint(0, 15, (B,), device=dev).to(torch.int32)
 st = m._stats_buf()
 lib = _native.hip_lib()
-names = {0: "prologue", 1: "input", 9: "loss", 30: "end"}
+names = {31: "kernel_start", 0: "prologue", 1: "input", 9: "loss", 30: "end"}
 for l in range(4):
     names[2 + l] = f"fwd{l}"
     names[10 + 2 * l] = f"bwd{3 - l}_dx"
