@@ -244,6 +244,21 @@ int ptg_ipc_handle_bytes() { return (int)sizeof(hipIpcMemHandle_t); }
 
 int ptg_stream_destroy(void* st) { return (int)hipStreamDestroy((hipStream_t)st); }
 
+// Cross-stream fork / join events of the training step's side stream (nn/streams.py).  A default HIP
+// event record ends with a SYSTEM-scope release (cache writeback + invalidate, so the host could read
+// device memory): on the step's stream that stalled the next kernel ~6.5 us per fork
+// (profiles/r5_cnn_b1_b256_gantt.txt gaps).  The two streams share one device, so a device-scope
+// release is all the ordering needs (hipEventDisableSystemFence).
+int ptg_event_create_device(void** out) {
+  hipEvent_t e;
+  const hipError_t rc = hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventDisableSystemFence);
+  *out = rc == hipSuccess ? (void*)e : nullptr;
+  return (int)rc;
+}
+int ptg_event_destroy(void* e) { return (int)hipEventDestroy((hipEvent_t)e); }
+int ptg_event_record(void* e, hipStream_t s) { return (int)hipEventRecord((hipEvent_t)e, s); }
+int ptg_stream_wait_event(void* e, hipStream_t s) { return (int)hipStreamWaitEvent(s, (hipEvent_t)e, 0); }
+
 // in/out: n elements (dtype 0 = fp32, 1 = fp64, 2 = int64); peer_ptrs: host array of world buffer
 // base addresses (this rank's own buffer at index rank); in may equal out.
 int ptg_ipc_allreduce(const void* in, void* out, long n, int dtype, const void* peer_ptrs, int world,

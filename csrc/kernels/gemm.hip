@@ -194,6 +194,10 @@ enum { ACT_NONE = 0, ACT_RELU = 1 };
 // consecutive outputs: 16-byte stores instead of 2-byte ones).
 PTG_DEV bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
+// PTG_EPI_NT (A/B build): the bf16 epilogue outputs written with nontemporal stores
+#ifndef PTG_EPI_NT
+#define PTG_EPI_NT 0
+#endif
 PTG_DEV void bf16_store8(bf16_t* p, float* v, int cnt, bool accum) {
   if (cnt == 8 && al16(p)) {
     if (accum) {
@@ -202,7 +206,13 @@ PTG_DEV void bf16_store8(bf16_t* p, float* v, int cnt, bool accum) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] += e[j];
     }
+#if PTG_EPI_NT
+    typedef unsigned int u4nt __attribute__((ext_vector_type(4)));
+    const U4 w = pack8(v);
+    __builtin_nontemporal_store(u4nt{w.x, w.y, w.z, w.w}, (u4nt*)p);
+#else
     *(U4*)p = pack8(v);
+#endif
     return;
   }
   for (int j = 0; j < cnt; ++j) p[j] = f2bf(accum ? v[j] + bf2f(p[j]) : v[j]);

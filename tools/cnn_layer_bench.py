@@ -95,6 +95,11 @@ def main():
             if ops.conv32_supported(H, W, C, Co, 5, 2, epi):
                 ops_[f"fwd32_{li}"] = (lambda x=x, w=w, b=b, z=z, al=al, aux=aux, epi=epi: ops.conv32(
                     x, w, b, z, al, aux, epi), x.numel() * 2 + z.numel() * 2 + aux.numel() * 2)
+            # the implicit-GEMM weight gradient of gemm.hip (split-K over the pixels, fp32 atomics)
+            dwg = torch.zeros_like(dw)
+            for sp in (0, 8, 32, 128):
+                ops_[f"wgradG{li}_s{sp}"] = (lambda x=x, dz=dz, dwg=dwg, sp=sp: ops.conv2d_wgrad(x, dz, 1, 2, dwg, splits=sp),
+                                             x.numel() * 2 + dz.numel() * 2)
             # the implicit-GEMM path of gemm.hip for the same dgrad / forward (A/B reference)
             ops_[f"dgradG{li}"] = (lambda dz=dz, w=w, dx=dx: ops.conv2d_dgrad(dz, w, 2, dx),
                                    dz.numel() * 2 + dx.numel() * 2)
