@@ -194,9 +194,11 @@ enum { ACT_NONE = 0, ACT_RELU = 1 };
 // consecutive outputs: 16-byte stores instead of 2-byte ones).
 PTG_DEV bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
-// PTG_EPI_NT (A/B build): the bf16 epilogue outputs written with nontemporal stores
+// PTG_EPI_NT: the bf16 epilogue outputs (conv / GEMM activations, read back only by a later kernel)
+// written with nontemporal stores: ResNet-50 b128 14.02 / 13.99 -> 13.93 / 13.87 ms, CNN-B1 b256
+// 1.546 / 1.531 -> 1.536 / 1.530 ms (profiles/r5_ab_epi_nt.txt); -DPTG_EPI_NT=0 for the A/B
 #ifndef PTG_EPI_NT
-#define PTG_EPI_NT 0
+#define PTG_EPI_NT 1
 #endif
 PTG_DEV void bf16_store8(bf16_t* p, float* v, int cnt, bool accum) {
   if (cnt == 8 && al16(p)) {

@@ -60,24 +60,6 @@ def main():
         if pool:
             ops_[f"ppbwd{li}"] = (lambda dp=dp, z=z, al=al, dz=dz, da=da, db=db: ops.prelu_pool_bwd(dp, z, al, dz, da, db),
                                   dp.numel() * 2 + z.numel() * 4)
-            if C % 8 == 0 or Co % 8 == 0:
-                wsr = [None]
-
-                def ppbr(dp=dp, z=z, al=al, dz=dz, da=da, db=db, wsr=wsr):
-                    wsr[0] = ops.prelu_pool_bwd_rows(dp, z, al, dz, da, db, ws=wsr[0])
-                ops_[f"ppbrows{li}"] = (ppbr, dp.numel() * 2 + z.numel() * 4)
-                # numerics: the row-pair kernel gives the same dz bits, dalpha / dbias within fp32 rounding
-                z.copy_(torch.randn(z.shape, device=dev, generator=g).bfloat16())
-                dz1, dz2 = torch.empty_like(z), torch.empty_like(z)
-                da1, da2 = torch.zeros_like(al), torch.zeros_like(al)
-                db1, db2 = torch.zeros(Co, device=dev), torch.zeros(Co, device=dev)
-                al2 = (torch.rand(al.shape, device=dev, generator=g) * 0.5)
-                ops.prelu_pool_bwd(dp, z, al2, dz1, da1, db1)
-                ops.prelu_pool_bwd_rows(dp, z, al2, dz2, da2, db2)
-                torch.cuda.synchronize()
-                print(json.dumps({"check": f"ppbrows{li}", "dz_equal": bool(torch.equal(dz1, dz2)),
-                                  "dalpha_maxrel": float(((da1 - da2).abs() / (da1.abs() + 1e-3)).max()),
-                                  "dbias_maxrel": float(((db1 - db2).abs() / (db1.abs() + 1e-3)).max())}), flush=True)
         else:
             ops_[f"pbwd{li}"] = (lambda dp=dp, z=z, al=al, dz=dz, da=da, db=db: ops.prelu_bwd(dp, z, al, dz, da, db),
                                  dp.numel() * 2 + z.numel() * 4)
