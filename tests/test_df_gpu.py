@@ -361,10 +361,14 @@ def test_radix_sort_wide_payload(hip_built):
     assert torch.equal(sv.cpu(), pay[torch.from_numpy(order)])
 
 
+@pytest.mark.parametrize("payload", ["1", "0"])
 @pytest.mark.parametrize("dtype,asc", [(torch.int64, True), (torch.int64, False), (torch.int32, True)])
-def test_orderby_integer_key_output_keys(spark_gpu, dtype, asc):
+def test_orderby_integer_key_output_keys(spark_gpu, dtype, asc, payload, monkeypatch):
     """Single null-free integer sort column: the sorted key column is decoded from the radix
-    sort's own output keys (not gathered); the result equals a stable host sort, ties included."""
+    sort's own output keys (not gathered); the result equals a stable host sort, ties included.
+    payload=1: the one value column rides through the radix passes as the payload; 0: row-id
+    payload + gather."""
+    monkeypatch.setenv("PTG_SORT_VALUE_PAYLOAD", payload)
     from pyspark_tf_gke_amd.sql import types as T
     from pyspark_tf_gke_amd.sql.dataframe import DataFrame
     from pyspark_tf_gke_amd.sql.table import ColumnVector, Table
