@@ -1732,7 +1732,7 @@ __global__ __launch_bounds__(256) void sort_key_prep_k(const void* __restrict__ 
   unsigned long long mn = ~0ULL, mx = 0ULL;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
     const unsigned long long u = orderable_key(col, type, i, desc);
-    out[i] = u;
+    if (out) out[i] = u;  // null: range only (the first radix pass applies the transform itself)
     mn = u < mn ? u : mn;
     mx = u > mx ? u : mx;
   }
@@ -1744,9 +1744,11 @@ __global__ __launch_bounds__(256) void sort_key_prep_k(const void* __restrict__ 
   }
 }
 
+// xin: XOR mask applied to every key as it is read (int64 column -> orderable u64 in the first pass:
+// sign bit for ascending, its complement for descending; 0 = keys already orderable)
 __global__ __launch_bounds__(256) void sort_count_k(const unsigned long long* __restrict__ keys, long n,
                                                     unsigned long long base, int shift, int ntiles,
-                                                    unsigned int* __restrict__ hist) {
+                                                    unsigned int* __restrict__ hist, unsigned long long xin) {
   __shared__ unsigned int h[4][SB];
   const int tid = threadIdx.x, w = tid >> 6, b = blockIdx.x;
 #pragma unroll
@@ -1756,7 +1758,7 @@ __global__ __launch_bounds__(256) void sort_count_k(const unsigned long long* __
 #pragma unroll
   for (int j = 0; j < SRPT; ++j) {
     const long i = s0 + j * 256 + tid;
-    k[j] = i < n ? keys[i] : 0ULL;
+    k[j] = i < n ? keys[i] ^ xin : 0ULL;
   }
   __syncthreads();
 #pragma unroll
@@ -1776,7 +1778,10 @@ __global__ __launch_bounds__(256) void sort_scatter_k(const unsigned long long* 
                                                       unsigned long long base, int shift, int ntiles,
                                                       const long long* __restrict__ offs,
                                                       unsigned long long* __restrict__ keys_out,
-                                                      VT* __restrict__ vals_out) {
+                                                      VT* __restrict__ vals_out, unsigned long long xin,
+                                                      unsigned long long xout) {
+  // xin: XOR mask on the keys as read (sort_count_k); xout: on the keys as written (the last pass
+  // writes the decoded column values: the same XOR mask undoes the orderable transform)
   __shared__ unsigned long long sk[ST];
   __shared__ VT sv[ST];
   __shared__ unsigned char sd[ST];
@@ -1805,7 +1810,7 @@ __global__ __launch_bounds__(256) void sort_scatter_k(const unsigned long long* 
     const int i = w * (ST / 4) + j * 64 + lane;
     d[j] = -1;
     if (i < nr) {
-      k[j] = keys_in[s0 + i];
+      k[j] = keys_in[s0 + i] ^ xin;
       v[j] = vals_in ? vals_in[s0 + i] : (VT)(s0 + i);
       d[j] = (int)((k[j] - base) >> shift) & (SB - 1);
     }
@@ -1855,7 +1860,7 @@ __global__ __launch_bounds__(256) void sort_scatter_k(const unsigned long long* 
   for (int i = tid; i < nr; i += 256) {
     const int dd = sd[i];
     const long long dst = PTG_CHECKED_IDX(goff[dd] + (i - (int)lstart[dd]), n);
-    keys_out[dst] = sk[i];
+    keys_out[dst] = sk[i] ^ xout;
     vals_out[dst] = sv[i];
   }
 }
@@ -2427,27 +2432,29 @@ int ptg_sort_key_prep(const void* col, int type, long n, int desc, void* out, vo
 }
 int ptg_sort_tile_rows() { return ST; }
 // one LSD pass: hist u32[256*ntiles] (digit-major) -> offs i64[256*ntiles] (exclusive scan, host/torch)
-int ptg_sort_count(const void* keys, long n, long base, int shift, void* hist, hipStream_t s) {
+int ptg_sort_count(const void* keys, long n, long base, int shift, void* hist, long xin, hipStream_t s) {
   const int ntiles = (int)((n + ST - 1) / ST);
   if (ntiles <= 0) return 0;
   hipLaunchKernelGGL(sort_count_k, dim3(ntiles), dim3(256), 0, s, (const unsigned long long*)keys, n,
-                     (unsigned long long)base, shift, ntiles, (unsigned int*)hist);
+                     (unsigned long long)base, shift, ntiles, (unsigned int*)hist, (unsigned long long)xin);
   PTG_RETURN_LAUNCH();
 }
 // v32: payload is u32 (requires n <= 2^32) instead of i64
 int ptg_sort_scatter(const void* keys_in, const void* vals_in, long n, long base, int shift, const void* offs,
-                     void* keys_out, void* vals_out, int v32, hipStream_t s) {
+                     void* keys_out, void* vals_out, int v32, long xin, long xout, hipStream_t s) {
   const int ntiles = (int)((n + ST - 1) / ST);
   if (ntiles <= 0) return 0;
   if (v32 && n > 4294967296L) return (int)hipErrorInvalidValue;
   if (v32)
     hipLaunchKernelGGL((sort_scatter_k<unsigned int>), dim3(ntiles), dim3(256), 0, s,
                        (const unsigned long long*)keys_in, (const unsigned int*)vals_in, n, (unsigned long long)base,
-                       shift, ntiles, (const long long*)offs, (unsigned long long*)keys_out, (unsigned int*)vals_out);
+                       shift, ntiles, (const long long*)offs, (unsigned long long*)keys_out, (unsigned int*)vals_out,
+                       (unsigned long long)xin, (unsigned long long)xout);
   else
     hipLaunchKernelGGL((sort_scatter_k<long long>), dim3(ntiles), dim3(256), 0, s,
                        (const unsigned long long*)keys_in, (const long long*)vals_in, n, (unsigned long long)base,
-                       shift, ntiles, (const long long*)offs, (unsigned long long*)keys_out, (long long*)vals_out);
+                       shift, ntiles, (const long long*)offs, (unsigned long long*)keys_out, (long long*)vals_out,
+                       (unsigned long long)xin, (unsigned long long)xout);
   PTG_RETURN_LAUNCH();
 }
 int ptg_range_partition(const void* keys, long n, const void* split, int nsplit, void* part, void* counts,

@@ -69,6 +69,8 @@ _K = [
     Knob("side_stream", bool, True, "PTG_SIDE_STREAM", None, "weight gradients on a side HIP stream (1 replica)"),
     Knob("sort_value_payload", bool, True, "PTG_SORT_VALUE_PAYLOAD", None,
          "orderBy of a (key, one 8-byte column) table carries the column through the radix passes"),
+    Knob("sort_fused_keys", bool, True, "PTG_SORT_FUSED_KEYS", None,
+         "orderBy on an int64 column: orderable-key transform inside the first / last radix pass"),
     Knob("fork_device_events", bool, True, "PTG_FORK_DEVICE_EVENTS", None,
          "side-stream fork/join through device-scope events (no system-scope cache flush per fork)"),
     Knob("tape_overlap", bool, True, "PTG_TAPE_OVERLAP", None,

@@ -839,21 +839,28 @@ def _orderable_np(x: torch.Tensor, desc: bool) -> np.ndarray:
     return ~u if desc else u
 
 
-def sort_key(col: torch.Tensor, desc: bool = False):
+def sort_key(col: torch.Tensor, desc: bool = False, write: bool = True):
     """Column -> (int64 tensor holding unsigned-orderable u64 keys, lo, hi) with lo/hi the key range
-    as Python ints in [0, 2^64)."""
+    as Python ints in [0, 2^64).  ``write=False`` (device): the range only, keys None (an int64
+    column then goes into :func:`radix_sort_u64` raw, with ``xin = orderable_mask(desc)``)."""
     n = col.numel()
     if not on_device(col):
         u = _orderable_np(col.contiguous(), desc)
         lo, hi = (int(u.min()), int(u.max())) if n else (0, 0)
         return torch.from_numpy(u.view(np.int64).copy()), lo, hi
     c = col.view(torch.uint8) if col.dtype == torch.bool else col.contiguous()
-    out = torch.empty(n, dtype=torch.int64, device=col.device)
+    out = torch.empty(n, dtype=torch.int64, device=col.device) if write else None
     rng = torch.tensor([-1, 0], dtype=torch.int64, device=col.device)
     if n:
         hip("ptg_sort_key_prep", ptr(c), TORCH_CT[c.dtype], n, int(desc), ptr(out), ptr(rng))
     lo, hi = (x & _U64 for x in rng.cpu().tolist())
     return out, (lo if n else 0), (hi if n else 0)
+
+
+def orderable_mask(desc: bool) -> int:
+    """XOR mask taking an int64 value to its unsigned-orderable key (and back): the sign bit for
+    ascending order, its complement for descending (as a signed int64)."""
+    return _signed((1 << 63) if not desc else (1 << 63) - 1)
 
 
 def decode_sort_key(sk: torch.Tensor, dtype, desc: bool) -> torch.Tensor:
@@ -885,21 +892,28 @@ def digit_offsets(hist: torch.Tensor, ntiles: int, offs: torch.Tensor, buf) -> t
 
 
 def radix_sort_u64(keys: torch.Tensor, vals: torch.Tensor | None = None, lo: int = 0, hi: int = _U64,
-                   row_payload: bool = False):
+                   row_payload: bool = False, xin: int = 0, xout: int = 0):
     """Stable sort of u64 keys (held in an int64 tensor) with an int64 payload (default: the row
     index, i.e. the result payload is the sorting permutation).  Only the significant bits of
     hi - lo are sorted: ceil(bits / 8) LSD passes of sort_count_k + sort_scatter_k.
-    ``row_payload``: ``vals`` holds row ids < 2^32 (a permutation), so it may travel as u32."""
+    ``row_payload``: ``vals`` holds row ids < 2^32 (a permutation), so it may travel as u32.
+    ``xin`` / ``xout``: XOR masks the first pass applies to the keys as read and the last pass as
+    written (:func:`orderable_mask`: raw int64 column in, decoded column values out - no separate
+    key prep / decode passes); with no pass at all (one distinct key) they must be equal."""
     n = keys.numel()
     if not on_device(keys):
-        u = keys.numpy().view(np.uint64)
+        k = keys ^ xin if xin else keys
+        u = k.numpy().view(np.uint64)
         order = np.argsort(u, kind="stable")
         v = torch.from_numpy(order.astype(np.int64)) if vals is None else vals[torch.from_numpy(order)]
-        return keys[torch.from_numpy(order)], v
+        ko = k[torch.from_numpy(order)]
+        return (ko ^ xout if xout else ko), v
     dev = keys.device
     bits = (hi - lo).bit_length()
     passes = (bits + 7) // 8
     if n == 0 or passes == 0:
+        if xin != xout:
+            keys = keys ^ (xin ^ xout)
         return keys, (torch.arange(n, dtype=torch.int64, device=dev) if vals is None else vals)
     ntiles = -(-n // _native.hip_lib().ptg_sort_tile_rows())
     hist = torch.empty(256 * ntiles, dtype=torch.int32, device=dev)
@@ -922,9 +936,11 @@ def radix_sort_u64(keys: torch.Tensor, vals: torch.Tensor | None = None, lo: int
     base = _signed(lo)
     for p in range(passes):
         shift = 8 * p
-        hip("ptg_sort_count", ptr(ka), n, base, shift, ptr(hist))
+        pin = xin if p == 0 else 0
+        pout = xout if p == passes - 1 else 0
+        hip("ptg_sort_count", ptr(ka), n, base, shift, ptr(hist), pin)
         digit_offsets(hist, ntiles, offs, dbuf)
-        hip("ptg_sort_scatter", ptr(ka), ptr(va), n, base, shift, ptr(offs), ptr(kb), ptr(vb), int(v32))
+        hip("ptg_sort_scatter", ptr(ka), ptr(va), n, base, shift, ptr(offs), ptr(kb), ptr(vb), int(v32), pin, pout)
         if kc is None:  # third buffer pair so the caller's keys/vals are never overwritten
             kc = torch.empty(n, dtype=torch.int64, device=dev)
             vc = torch.empty(n, dtype=vdt, device=dev)

@@ -500,23 +500,29 @@ class DataFrame:
             name = t.resolve(specs[0][0].node[1])
             cv = t.column(name)
             if cv.valid is None and cv.data.dtype in (torch.int64, torch.int32) and not isinstance(cv.dtype, T.StringType):
-                k, lo, hi = D.sort_key(cv.data, desc=not specs[0][1])
+                desc = not specs[0][1]
+                # int64 on the GPU: the first radix pass reads the raw column and the last writes the
+                # decoded values (XOR masks), so there is no key-prep write nor decode pass
+                fused = cv.data.dtype == torch.int64 and cv.data.is_cuda and config.get("sort_fused_keys")
+                k, lo, hi = D.sort_key(cv.data, desc=desc, write=not fused)
+                rs = dict(xin=D.orderable_mask(desc), xout=D.orderable_mask(desc)) if fused else {}
+                src = cv.data.contiguous() if fused else k
                 others = [n for n in t.columns if n != name]
                 oc = t.column(others[0]) if len(others) == 1 else None
-                if (oc is not None and config.get("sort_value_payload") and oc.valid is None and oc.data.dim() == 1 and oc.data.element_size() == 8
-                        and not isinstance(oc.dtype, T.StringType) and oc.data.is_cuda):
+                if (oc is not None and config.get("sort_value_payload") and oc.valid is None and oc.data.dim() == 1
+                        and oc.data.element_size() == 8 and not isinstance(oc.dtype, T.StringType) and oc.data.is_cuda):
                     # exactly one other (8-byte, null-free) column: it rides through the radix passes as
                     # the payload (16 instead of 12 bytes per row per pass) instead of a row-id payload
                     # plus a random-access gather of the column by the permutation afterwards
-                    sk, sv = D.radix_sort_u64(k, oc.data.contiguous().view(torch.int64), lo, hi)
-                    cols = {n: (ColumnVector(D.decode_sort_key(sk, cv.data.dtype, not specs[0][1]), cv.dtype, None,
-                                             cv.dictionary) if n == name else
+                    sk, sv = D.radix_sort_u64(src, oc.data.contiguous().view(torch.int64), lo, hi, **rs)
+                    kcol = sk if fused else D.decode_sort_key(sk, cv.data.dtype, desc)
+                    cols = {n: (ColumnVector(kcol, cv.dtype, None, cv.dictionary) if n == name else
                                 ColumnVector(sv.view(oc.data.dtype), oc.dtype, None, oc.dictionary))
                             for n in t.columns}
                     return self._new(Table(cols, t.num_rows, t.device))
-                sk, perm = D.radix_sort_u64(k, None, lo, hi, row_payload=True)
-                cols = {n: (ColumnVector(D.decode_sort_key(sk, cv.data.dtype, not specs[0][1]), cv.dtype, None,
-                                         cv.dictionary) if n == name else c.take(perm))
+                sk, perm = D.radix_sort_u64(src, None, lo, hi, row_payload=True, **rs)
+                kcol = sk if fused else D.decode_sort_key(sk, cv.data.dtype, desc)
+                cols = {n: (ColumnVector(kcol, cv.dtype, None, cv.dictionary) if n == name else c.take(perm))
                         for n, c in t.columns.items()}
                 return self._new(Table(cols, t.num_rows, t.device))
         df_t = DataFrame(t, self.sparkSession)

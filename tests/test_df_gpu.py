@@ -361,14 +361,16 @@ def test_radix_sort_wide_payload(hip_built):
     assert torch.equal(sv.cpu(), pay[torch.from_numpy(order)])
 
 
-@pytest.mark.parametrize("payload", ["1", "0"])
+@pytest.mark.parametrize("payload,fused", [("1", "1"), ("0", "1"), ("1", "0"), ("0", "0")])
 @pytest.mark.parametrize("dtype,asc", [(torch.int64, True), (torch.int64, False), (torch.int32, True)])
-def test_orderby_integer_key_output_keys(spark_gpu, dtype, asc, payload, monkeypatch):
+def test_orderby_integer_key_output_keys(spark_gpu, dtype, asc, payload, fused, monkeypatch):
     """Single null-free integer sort column: the sorted key column is decoded from the radix
     sort's own output keys (not gathered); the result equals a stable host sort, ties included.
     payload=1: the one value column rides through the radix passes as the payload; 0: row-id
-    payload + gather."""
+    payload + gather.  fused=1 (int64): the first radix pass reads the raw column and the last writes
+    the decoded values (no key prep write, no decode pass)."""
     monkeypatch.setenv("PTG_SORT_VALUE_PAYLOAD", payload)
+    monkeypatch.setenv("PTG_SORT_FUSED_KEYS", fused)
     from pyspark_tf_gke_amd.sql import types as T
     from pyspark_tf_gke_amd.sql.dataframe import DataFrame
     from pyspark_tf_gke_amd.sql.table import ColumnVector, Table
