@@ -1693,7 +1693,14 @@ __global__ __launch_bounds__(1024) void hash9_merge_k(const long long* __restric
 #endif
 #define ST PTG_ST        // rows per sort tile
 #define SB 256           // digit bins (8 bits per pass)
-#define SRPT (ST / 256)
+// threads per sort tile workgroup (A/B build: 512 with 8192-row tiles keeps 16 rows per thread and the
+// same 8 waves per CU as two 256-thread 4096-row tiles, with digit runs twice as long)
+#ifndef PTG_SORT_NTH
+#define PTG_SORT_NTH 256
+#endif
+#define SNT PTG_SORT_NTH
+#define SNW (SNT / 64)
+#define SRPT (ST / SNT)
 
 PTG_DEV unsigned long long orderable_key(const void* col, int type, long i, int desc) {
   unsigned long long u;
@@ -1746,26 +1753,30 @@ __global__ __launch_bounds__(256) void sort_key_prep_k(const void* __restrict__ 
 
 // xin: XOR mask applied to every key as it is read (int64 column -> orderable u64 in the first pass:
 // sign bit for ascending, its complement for descending; 0 = keys already orderable)
-__global__ __launch_bounds__(256) void sort_count_k(const unsigned long long* __restrict__ keys, long n,
+__global__ __launch_bounds__(SNT) void sort_count_k(const unsigned long long* __restrict__ keys, long n,
                                                     unsigned long long base, int shift, int ntiles,
                                                     unsigned int* __restrict__ hist, unsigned long long xin) {
-  __shared__ unsigned int h[4][SB];
+  __shared__ unsigned int h[SNW][SB];
   const int tid = threadIdx.x, w = tid >> 6, b = blockIdx.x;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) h[q][tid] = 0;
+  for (int t = tid; t < SNW * SB; t += SNT) (&h[0][0])[t] = 0;
   const long s0 = (long)b * ST;
   unsigned long long k[SRPT];
 #pragma unroll
   for (int j = 0; j < SRPT; ++j) {
-    const long i = s0 + j * 256 + tid;
+    const long i = s0 + j * SNT + tid;
     k[j] = i < n ? keys[i] ^ xin : 0ULL;
   }
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < SRPT; ++j)
-    if (s0 + j * 256 + tid < n) atomicAdd(&h[w][(unsigned)((k[j] - base) >> shift) & (SB - 1)], 1u);
+    if (s0 + j * SNT + tid < n) atomicAdd(&h[w][(unsigned)((k[j] - base) >> shift) & (SB - 1)], 1u);
   __syncthreads();
-  hist[(long)b * SB + tid] = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
+  if (tid < SB) {
+    unsigned c = 0;
+#pragma unroll
+    for (int q = 0; q < SNW; ++q) c += h[q][tid];
+    hist[(long)b * SB + tid] = c;
+  }
   (void)ntiles;
 }
 
@@ -1773,7 +1784,7 @@ __global__ __launch_bounds__(256) void sort_count_k(const unsigned long long* __
 // row count fits 32 bits: 12 instead of 16 bytes per row read and written by every pass.
 // offs holds every (tile, digit) run's output position (sort_count_k + ptg_digit_offsets).
 template <typename VT>
-__global__ __launch_bounds__(256) void sort_scatter_k(const unsigned long long* __restrict__ keys_in,
+__global__ __launch_bounds__(SNT) void sort_scatter_k(const unsigned long long* __restrict__ keys_in,
                                                       const VT* __restrict__ vals_in, long n,
                                                       unsigned long long base, int shift, int ntiles,
                                                       const long long* __restrict__ offs,
@@ -1785,18 +1796,17 @@ __global__ __launch_bounds__(256) void sort_scatter_k(const unsigned long long* 
   __shared__ unsigned long long sk[ST];
   __shared__ VT sv[ST];
   __shared__ unsigned char sd[ST];
-  __shared__ unsigned int wc[4][SB];
-  __shared__ unsigned int woff[4][SB];
+  __shared__ unsigned int wc[SNW][SB];
+  __shared__ unsigned int woff[SNW][SB];
   __shared__ unsigned int lstart[SB];
   __shared__ long long goff[SB];
-  __shared__ int wsum[4];
+  __shared__ int wsum[SNW];
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int b = xcd_tile(blockIdx.x, ntiles);
-  goff[tid] = offs[(long)b * SB + tid];  // tile-major: one coalesced 2 KB row
+  if (tid < SB) goff[tid] = offs[(long)b * SB + tid];  // tile-major: one coalesced 2 KB row
   const long s0 = (long)b * ST;
   const int nr = (int)((n - s0) < ST ? (n - s0) : ST);
-#pragma unroll
-  for (int q = 0; q < 4; ++q) wc[q][tid] = 0;
+  for (int t = tid; t < SNW * SB; t += SNT) (&wc[0][0])[t] = 0;
   // Wave-contiguous rows: wave w owns tile rows [w*ST/4, (w+1)*ST/4), 64 consecutive rows per round
   // (coalesced loads), so the stable order inside the tile is (wave, round, lane).  Ranks come from
   // a wave-private running count per digit (wc[w]): no block barrier per round, only the one
@@ -1807,7 +1817,7 @@ __global__ __launch_bounds__(256) void sort_scatter_k(const unsigned long long* 
   int d[SRPT], r[SRPT];
 #pragma unroll
   for (int j = 0; j < SRPT; ++j) {
-    const int i = w * (ST / 4) + j * 64 + lane;
+    const int i = w * (ST / SNW) + j * 64 + lane;
     d[j] = -1;
     if (i < nr) {
       k[j] = keys_in[s0 + i] ^ xin;
@@ -1835,18 +1845,17 @@ __global__ __launch_bounds__(256) void sort_scatter_k(const unsigned long long* 
     r[j] = (int)old + rank_w;
   }
   __syncthreads();
-  unsigned int running;
-  {  // thread tid owns digit tid: per-wave offsets inside the digit's run, and the tile total
-    const unsigned c0 = wc[0][tid], c1 = wc[1][tid], c2 = wc[2][tid], c3 = wc[3][tid];
-    woff[0][tid] = 0;
-    woff[1][tid] = c0;
-    woff[2][tid] = c0 + c1;
-    woff[3][tid] = c0 + c1 + c2;
-    running = c0 + c1 + c2 + c3;
+  unsigned int running = 0;
+  if (tid < SB) {  // thread tid owns digit tid: per-wave offsets inside the digit's run, and the tile total
+#pragma unroll
+    for (int q = 0; q < SNW; ++q) {
+      woff[q][tid] = running;
+      running += wc[q][tid];
+    }
   }
   int total;
-  const int ls = block_excl_scan256((int)running, wsum, &total);
-  lstart[tid] = (unsigned)ls;
+  const int ls = block_excl_scan256((int)running, wsum, &total);  // threads >= SB add 0 after digit 255
+  if (tid < SB) lstart[tid] = (unsigned)ls;
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < SRPT; ++j) {
@@ -1857,7 +1866,7 @@ __global__ __launch_bounds__(256) void sort_scatter_k(const unsigned long long* 
     sd[pos] = (unsigned char)d[j];
   }
   __syncthreads();
-  for (int i = tid; i < nr; i += 256) {
+  for (int i = tid; i < nr; i += SNT) {
     const int dd = sd[i];
     const long long dst = PTG_CHECKED_IDX(goff[dd] + (i - (int)lstart[dd]), n);
     keys_out[dst] = sk[i] ^ xout;
@@ -2435,7 +2444,7 @@ int ptg_sort_tile_rows() { return ST; }
 int ptg_sort_count(const void* keys, long n, long base, int shift, void* hist, long xin, hipStream_t s) {
   const int ntiles = (int)((n + ST - 1) / ST);
   if (ntiles <= 0) return 0;
-  hipLaunchKernelGGL(sort_count_k, dim3(ntiles), dim3(256), 0, s, (const unsigned long long*)keys, n,
+  hipLaunchKernelGGL(sort_count_k, dim3(ntiles), dim3(SNT), 0, s, (const unsigned long long*)keys, n,
                      (unsigned long long)base, shift, ntiles, (unsigned int*)hist, (unsigned long long)xin);
   PTG_RETURN_LAUNCH();
 }
@@ -2446,12 +2455,12 @@ int ptg_sort_scatter(const void* keys_in, const void* vals_in, long n, long base
   if (ntiles <= 0) return 0;
   if (v32 && n > 4294967296L) return (int)hipErrorInvalidValue;
   if (v32)
-    hipLaunchKernelGGL((sort_scatter_k<unsigned int>), dim3(ntiles), dim3(256), 0, s,
+    hipLaunchKernelGGL((sort_scatter_k<unsigned int>), dim3(ntiles), dim3(SNT), 0, s,
                        (const unsigned long long*)keys_in, (const unsigned int*)vals_in, n, (unsigned long long)base,
                        shift, ntiles, (const long long*)offs, (unsigned long long*)keys_out, (unsigned int*)vals_out,
                        (unsigned long long)xin, (unsigned long long)xout);
   else
-    hipLaunchKernelGGL((sort_scatter_k<long long>), dim3(ntiles), dim3(256), 0, s,
+    hipLaunchKernelGGL((sort_scatter_k<long long>), dim3(ntiles), dim3(SNT), 0, s,
                        (const unsigned long long*)keys_in, (const long long*)vals_in, n, (unsigned long long)base,
                        shift, ntiles, (const long long*)offs, (unsigned long long*)keys_out, (long long*)vals_out,
                        (unsigned long long)xin, (unsigned long long)xout);
