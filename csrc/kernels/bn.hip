@@ -88,6 +88,30 @@ PTG_DEV void bn_part_sums(float* part, int C, int c, double& s, double& q) {
   }
 }
 
+// ReLU masks as bits (residual BNs): bit j of byte i = (y[8i + j] > 0), written by bn_apply_k from
+// the stored bf16 outputs, so the backward passes read 1 bit instead of the 16-bit y per element.
+// relu mode 3 of the backward kernels: the mask byte expands to a bf16x8 vector of 1.0 / 0.0 that
+// takes y's place in the mode-1 code path.
+PTG_DEV unsigned relu_bits(const U4& y) {
+  const uint32_t w[4] = {y.x, y.y, y.z, y.w};
+  unsigned b = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t lo = w[k] & 0xFFFFu, hi = w[k] >> 16;
+    b |= (unsigned)(lo != 0u && lo <= 0x7F80u) << (2 * k);  // > 0: positive, nonzero (+inf included)
+    b |= (unsigned)(hi != 0u && hi <= 0x7F80u) << (2 * k + 1);
+  }
+  return b;
+}
+PTG_DEV U4 mask_u4(unsigned b) {
+  U4 v;
+  v.x = ((b & 1u) ? 0x3F80u : 0u) | ((b & 2u) ? 0x3F800000u : 0u);
+  v.y = ((b & 4u) ? 0x3F80u : 0u) | ((b & 8u) ? 0x3F800000u : 0u);
+  v.z = ((b & 16u) ? 0x3F80u : 0u) | ((b & 32u) ? 0x3F800000u : 0u);
+  v.w = ((b & 64u) ? 0x3F80u : 0u) | ((b & 128u) ? 0x3F800000u : 0u);
+  return v;
+}
+
 }  // namespace
 
 __global__ __launch_bounds__(256) void bn_stats_k(const bf16_t* __restrict__ z, long M, int C, int rpb, int cs,
@@ -160,7 +184,8 @@ __global__ __launch_bounds__(256) void bn_finalize_k(float* __restrict__ part, i
 
 __global__ __launch_bounds__(256) void bn_apply_k(const bf16_t* __restrict__ z, const float* __restrict__ scale,
                                                   const float* __restrict__ shift, const bf16_t* __restrict__ res,
-                                                  int relu, bf16_t* __restrict__ y, long n8, int C) {
+                                                  int relu, bf16_t* __restrict__ y, long n8, int C,
+                                                  uint8_t* __restrict__ mask) {
   const long stride = (long)gridDim.x * 256;
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n8; i += stride) {
     const int c0 = (int)((i * 8) % C);
@@ -177,23 +202,28 @@ __global__ __launch_bounds__(256) void bn_apply_k(const bf16_t* __restrict__ z, 
       if (res) v += r[j];
       f[j] = relu ? fmaxf(v, 0.f) : v;
     }
-    *(U4*)(y + i * 8) = pack8(f);
+    const U4 yv = pack8(f);
+    *(U4*)(y + i * 8) = yv;
+    if (mask) mask[i] = (uint8_t)relu_bits(yv);
   }
 }
 
 // relu: 0 = none, 1 = ReLU mask from the stored output y, 2 = mask recomputed from z as
 // fmaf(z, scale, shift) > 0 - exactly the forward's pre-activation when no residual was added, so
-// the y tensor is not read at all (a third less traffic for those BatchNormalizations).
+// the y tensor is not read at all (a third less traffic for those BatchNormalizations); 3 = mask
+// from the bit mask bn_apply_k wrote (residual BNs: 1 bit instead of 16 per element).
 __global__ __launch_bounds__(256) void bn_bwd_reduce_k(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
                                                        const bf16_t* __restrict__ z, long M, int C, int rpb, int cs,
                                                        int relu, float* __restrict__ part,
-                                                       const float* __restrict__ scale, const float* __restrict__ shift) {
+                                                       const float* __restrict__ scale, const float* __restrict__ shift,
+                                                       const uint8_t* __restrict__ mask) {
   __shared__ float red[2][256][8];
   const int tid = threadIdx.x, cpt = cs >> 3, rpi = 256 / cpt, cbase = blockIdx.y * cs;
   const int slot = tid % cpt, rsub = tid / cpt;
   dy += cbase;
   z += cbase;
   if (y) y += cbase;
+  if (mask) mask += cbase >> 3;
   float s[8], q[8], sc[8], sh[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) { s[j] = 0.f; q[j] = 0.f; sc[j] = 0.f; sh[j] = 0.f; }
@@ -206,7 +236,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_k(const bf16_t* __restrict_
     float g[8], zz[8];
     unpack8(vd, g);
     unpack8(vz, zz);
-    if (relu == 1) {
+    if (relu == 1 || relu == 3) {
       float yy[8];
       unpack8(vy, yy);
 #pragma unroll
@@ -227,7 +257,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_k(const bf16_t* __restrict_
         const long off = (r + (long)u * rpi) * C + slot * 8;
         vd[u] = *(const U4*)(dy + off);
         vz[u] = *(const U4*)(z + off);
-        vy[u] = relu == 1 ? *(const U4*)(y + off) : vd[u];
+        vy[u] = relu == 1 ? *(const U4*)(y + off) : relu == 3 ? mask_u4(mask[off >> 3]) : vd[u];
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) acc_row(vd[u], vz[u], vy[u]);
@@ -235,7 +265,8 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_k(const bf16_t* __restrict_
     for (; r < r1; r += rpi) {
       const long off = r * C + slot * 8;
       const U4 vd = *(const U4*)(dy + off);
-      acc_row(vd, *(const U4*)(z + off), relu == 1 ? *(const U4*)(y + off) : vd);
+      acc_row(vd, *(const U4*)(z + off),
+              relu == 1 ? *(const U4*)(y + off) : relu == 3 ? mask_u4(mask[off >> 3]) : vd);
     }
   }
   bn_flush(red, s, q, tid, cpt, rpi, part, C, cbase);
@@ -275,19 +306,20 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(const bf16_t* __restrict__
                                                       const bf16_t* __restrict__ z, const float* __restrict__ coef,
                                                       int relu, bf16_t* __restrict__ dz, bf16_t* __restrict__ dres,
                                                       long n8, int C, const float* __restrict__ scale,
-                                                      const float* __restrict__ shift) {
+                                                      const float* __restrict__ shift,
+                                                      const uint8_t* __restrict__ mask) {
   const long stride = (long)gridDim.x * 256;
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n8; i += stride) {
     const int c0 = (int)((i * 8) % C);
     const U4 vd = *(const U4*)(dy + i * 8), vz = *(const U4*)(z + i * 8);
-    const U4 vy = relu == 1 ? *(const U4*)(y + i * 8) : vd;
+    const U4 vy = relu == 1 ? *(const U4*)(y + i * 8) : relu == 3 ? mask_u4(mask[i]) : vd;
     float g[8], zz[8], a[8], c1[8], c0v[8];
     unpack8(vd, g);
     unpack8(vz, zz);
     load8f(coef + c0, a);
     load8f(coef + C + c0, c1);
     load8f(coef + 2 * C + c0, c0v);
-    if (relu == 1) {
+    if (relu == 1 || relu == 3) {
       float yy[8];
       unpack8(vy, yy);
 #pragma unroll
@@ -432,23 +464,26 @@ int ptg_bn_finalize(float* part, int C, long M, const float* gamma, const float*
   PTG_RETURN_LAUNCH();
 }
 
+// mask (nullable, u8[M*C/8]): the ReLU bit mask of y for the backward's relu mode 3
 int ptg_bn_apply(const void* z, const float* scale, const float* shift, const void* res, int relu, void* y,
-                 long M, int C, hipStream_t s) {
+                 long M, int C, void* mask, hipStream_t s) {
   if (C % 8) return (int)hipErrorInvalidValue;
   const long n8 = M * C / 8;
   hipLaunchKernelGGL(bn_apply_k, dim3(ew_grid(n8)), dim3(256), 0, s, (const bf16_t*)z, scale, shift,
-                     (const bf16_t*)res, relu, (bf16_t*)y, n8, C);
+                     (const bf16_t*)res, relu, (bf16_t*)y, n8, C, (uint8_t*)mask);
   PTG_RETURN_LAUNCH();
 }
 
 int ptg_bn_bwd_reduce(const void* dy, const void* y, const void* z, long M, int C, int relu, float* part,
-                      const float* scale, const float* shift, hipStream_t s) {
+                      const float* scale, const float* shift, const void* mask, hipStream_t s) {
   if (relu == 2 && (!scale || !shift)) return (int)hipErrorInvalidValue;
+  if (relu == 3 && !mask) return (int)hipErrorInvalidValue;
   if (C % 8 || C > 2048 || M <= 0) return (int)hipErrorInvalidValue;
   const int cs = bn_slice(C), rpi = 256 / (cs / 8);
   const int rpb = bn_rows_per_block(M, rpi, C / cs);
   hipLaunchKernelGGL(bn_bwd_reduce_k, dim3(ptg_ceil_div(M, rpb), C / cs), dim3(256), 0, s, (const bf16_t*)dy,
-                     (const bf16_t*)y, (const bf16_t*)z, M, C, rpb, cs, relu, part, scale, shift);
+                     (const bf16_t*)y, (const bf16_t*)z, M, C, rpb, cs, relu, part, scale, shift,
+                     (const uint8_t*)mask);
   PTG_RETURN_LAUNCH();
 }
 
@@ -460,12 +495,14 @@ int ptg_bn_bwd_finalize(float* part, int C, long M, const float* gamma, const fl
 }
 
 int ptg_bn_bwd_apply(const void* dy, const void* y, const void* z, const float* coef, int relu, void* dz, void* dres,
-                     long M, int C, const float* scale, const float* shift, hipStream_t s) {
+                     long M, int C, const float* scale, const float* shift, const void* mask, hipStream_t s) {
   if (relu == 2 && (!scale || !shift)) return (int)hipErrorInvalidValue;
+  if (relu == 3 && !mask) return (int)hipErrorInvalidValue;
   if (C % 8) return (int)hipErrorInvalidValue;
   const long n8 = M * C / 8;
   hipLaunchKernelGGL(bn_bwd_apply_k, dim3(ew_grid(n8)), dim3(256), 0, s, (const bf16_t*)dy, (const bf16_t*)y,
-                     (const bf16_t*)z, coef, relu, (bf16_t*)dz, (bf16_t*)dres, n8, C, scale, shift);
+                     (const bf16_t*)z, coef, relu, (bf16_t*)dz, (bf16_t*)dres, n8, C, scale, shift,
+                     (const uint8_t*)mask);
   PTG_RETURN_LAUNCH();
 }
 

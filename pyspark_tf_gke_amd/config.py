@@ -81,6 +81,8 @@ _K = [
          "GradientTape loops: big Dense dW deferred to apply_gradients and fused with Adam (computed on first read)"),
     Knob("raw_u8_input", bool, True, "PTG_RAW_U8_INPUT", None, "first conv reads the uint8 image batch directly"),
     Knob("sparse_first", bool, True, "PTG_SPARSE_FIRST", None, "first conv layer keeps a sparse pool record"),
+    Knob("bn_relu_bits", bool, True, "PTG_BN_RELU_BITS", None,
+         "residual BN + ReLU: the backward reads a 1-bit ReLU mask written by the forward instead of y"),
     Knob("bn_bwd_epi_stats", bool, True, "PTG_BN_BWD_EPI_STATS", None,
          "ResNet: the BN backward sums of a Conv->BN->ReLU block come from the epilogue of the dgrad that produces its gradient (no bn_bwd_reduce pass)"),
     Knob("bn_epi_stats", bool, True, "PTG_BN_EPI_STATS", None, "ResNet: BN batch statistics from the conv GEMM epilogue (A/B: 9.00k vs 8.78k img/s with the shuffle flush)"),

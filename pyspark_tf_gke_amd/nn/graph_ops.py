@@ -108,6 +108,9 @@ BN_EPI_STATS = config.get("bn_epi_stats")
 # mask to the gradient it stores (gemm.hip EpiBf16 backward form): the bn_bwd_reduce pass over dy and
 # z disappears.  PTG_BN_BWD_EPI_STATS=0 keeps the separate reduction.
 BN_BWD_EPI = config.get("bn_bwd_epi_stats")
+# Residual BN + ReLU: bn_apply_k also writes a 1-bit ReLU mask of y; the backward reads it instead of
+# y (PTG_BN_RELU_BITS=0: read y).
+RELU_BITS = config.get("bn_relu_bits")
 
 
 def _pow2(v):
@@ -207,7 +210,13 @@ class _BNState:
             part.zero_()
         if not apply:
             return z
-        return KB.bn_apply(z, scale, shift, res, relu, y)
+        # residual + ReLU on the GPU: the backward's ReLU mask comes from a bit mask written here
+        # (1 bit instead of re-reading the 16-bit y in bn_bwd_reduce and bn_bwd_apply)
+        mask = None
+        if relu and res is not None and K.on_device(z) and RELU_BITS:
+            mask = ws.get(self.name + "/relu_bits", (z.numel() // 8,), torch.uint8, z.device)
+        self._mask = mask
+        return KB.bn_apply(z, scale, shift, res, relu, y, mask)
 
     def backward(self, dy, y, z, relu, dz, dres, ws, stats_done=False):
         bn = self.bn
@@ -216,14 +225,15 @@ class _BNState:
         part, scale, shift, mean, rstd, coef = self.bufs(ws, C, z.device)
         # no residual was added before the ReLU: its mask is z*scale+shift > 0, y need not be read
         sc, sh = (scale, shift) if (relu and dres is None) else (None, None)
+        mask = getattr(self, "_mask", None) if (relu and dres is not None) else None
         if not stats_done:  # else: the producing dgrad's epilogue summed (g, g*z) into part already
-            KB.bn_bwd_reduce(dy, y, z, relu, part, sc, sh)
+            KB.bn_bwd_reduce(dy, y, z, relu, part, sc, sh, mask)
         KB.bn_bwd_finalize(part, M, bn.gamma.data if bn.gamma is not None else None, mean, rstd,
                            bn.gamma.grad if bn.gamma is not None else None,
                            bn.beta.grad if bn.beta is not None else None, coef)
         if not K.on_device(z):
             part.zero_()
-        return KB.bn_bwd_apply(dy, y, z, coef, relu, dz, dres, sc, sh)
+        return KB.bn_bwd_apply(dy, y, z, coef, relu, dz, dres, sc, sh, mask)
 
 
 class ConvBNOp:

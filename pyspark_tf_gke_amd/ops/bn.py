@@ -62,7 +62,9 @@ def bn_finalize(part, M: int, gamma, beta, eps: float, momentum: float, mmean, m
         ptr(mvar), ptr(scale), ptr(shift), ptr(mean_out), ptr(rstd_out), int(training))
 
 
-def bn_apply(z, scale, shift, res, relu: bool, y):
+def bn_apply(z, scale, shift, res, relu: bool, y, mask=None):
+    """``mask`` (device, uint8 [M*C/8]): also write the ReLU bit mask of y (bit j of byte i: y[8i+j] >
+    0) for :func:`bn_bwd_reduce` / :func:`bn_bwd_apply` ``mask=`` (1 bit read instead of 16)."""
     C = z.shape[-1]
     M = z.numel() // C
     if not on_device(z):
@@ -73,7 +75,7 @@ def bn_apply(z, scale, shift, res, relu: bool, y):
             v = torch.relu(v)
         y.copy_(v.to(y.dtype))
         return y
-    hip("ptg_bn_apply", ptr(z), ptr(scale), ptr(shift), ptr(res), int(relu), ptr(y), M, C)
+    hip("ptg_bn_apply", ptr(z), ptr(scale), ptr(shift), ptr(res), int(relu), ptr(y), M, C, ptr(mask))
     return y
 
 
@@ -85,7 +87,7 @@ def _relu_mask(y, z, scale, shift, M, C):
     return y.float().reshape(M, C) > 0
 
 
-def bn_bwd_reduce(dy, y, z, relu: bool, part, scale=None, shift=None):
+def bn_bwd_reduce(dy, y, z, relu: bool, part, scale=None, shift=None, mask=None):
     """part += (sum g, sum g*z) with g = dy masked by the ReLU.  With ``scale``/``shift`` (a BN with
     no residual input) the mask is recomputed from z and ``y`` is not read."""
     C = z.shape[-1]
@@ -97,8 +99,8 @@ def bn_bwd_reduce(dy, y, z, relu: bool, part, scale=None, shift=None):
         part[0, 0] += g.sum(0)
         part[0, 1] += (g * z.float().reshape(M, C)).sum(0)
         return part
-    mode = 0 if not relu else (2 if scale is not None else 1)
-    hip("ptg_bn_bwd_reduce", ptr(dy), ptr(y), ptr(z), M, C, mode, ptr(part), ptr(scale), ptr(shift))
+    mode = 0 if not relu else (2 if scale is not None else (3 if mask is not None else 1))
+    hip("ptg_bn_bwd_reduce", ptr(dy), ptr(y), ptr(z), M, C, mode, ptr(part), ptr(scale), ptr(shift), ptr(mask))
     return part
 
 
@@ -125,7 +127,7 @@ def bn_bwd_finalize(part, M: int, gamma, mean, rstd, dgamma, dbeta, coef):
     return coef
 
 
-def bn_bwd_apply(dy, y, z, coef, relu: bool, dz, dres=None, scale=None, shift=None):
+def bn_bwd_apply(dy, y, z, coef, relu: bool, dz, dres=None, scale=None, shift=None, mask=None):
     C = z.shape[-1]
     M = z.numel() // C
     if not on_device(z):
@@ -136,9 +138,9 @@ def bn_bwd_apply(dy, y, z, coef, relu: bool, dz, dres=None, scale=None, shift=No
             dres.copy_(g.to(dres.dtype))
         dz.copy_((coef[0] * g + coef[1] * z.float() + coef[2]).to(dz.dtype))
         return dz
-    mode = 0 if not relu else (2 if scale is not None else 1)
+    mode = 0 if not relu else (2 if scale is not None else (3 if mask is not None else 1))
     hip("ptg_bn_bwd_apply", ptr(dy), ptr(y), ptr(z), ptr(coef), mode, ptr(dz), ptr(dres), M, C, ptr(scale),
-        ptr(shift))
+        ptr(shift), ptr(mask))
     return dz
 
 

@@ -83,6 +83,40 @@ def test_bn_backward_mask_from_z(M, C):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("M,C", [(4096, 64), (1000, 256), (392, 2048), (300, 96)])
+def test_bn_backward_relu_bits(M, C):
+    """Residual BN + ReLU: the backward with the 1-bit ReLU mask bn_apply wrote (relu mode 3) gives
+    the same bits as with the mask from y (mode 1); the mask bits are y > 0."""
+    torch.manual_seed(6)
+    z = (torch.randn(M, C) * 2 + 0.3).to(torch.bfloat16).to(DEV)
+    res = torch.randn(M, C).to(torch.bfloat16).to(DEV)
+    res[0, :8] = 0.0  # exact zeros through the ReLU
+    dy = torch.randn(M, C).to(torch.bfloat16).to(DEV)
+    gamma, beta = (torch.rand(C) + 0.5).to(DEV), torch.randn(C).to(DEV)
+    f = lambda: torch.empty(C, device=DEV)  # noqa: E731
+    part = KB.part_buffer(C, DEV)
+    scale, shift, mean, rstd = f(), f(), f(), f()
+    KB.bn_stats(z, part)
+    KB.bn_finalize(part, M, gamma, beta, 1e-3, -1.0, None, None, scale, shift, mean, rstd, True)
+    y = torch.empty_like(z)
+    bits = torch.empty(M * C // 8, dtype=torch.uint8, device=DEV)
+    KB.bn_apply(z, scale, shift, res, True, y, bits)
+    want = (y.float() > 0).reshape(-1, 8).cpu()
+    got = ((bits.cpu().long().unsqueeze(1) >> torch.arange(8)) & 1).bool()
+    assert torch.equal(got, want)
+    outs = []
+    for m in (None, bits):
+        coef = torch.empty(3, C, device=DEV)
+        dg, db = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+        KB.bn_bwd_reduce(dy, y if m is None else None, z, True, part, mask=m)
+        KB.bn_bwd_finalize(part, M, gamma, mean, rstd, dg, db, coef)
+        dz, dres = torch.empty_like(z), torch.empty_like(z)
+        KB.bn_bwd_apply(dy, y if m is None else None, z, coef, True, dz, dres, mask=m)
+        outs.append((dz.cpu(), dres.cpu(), dg.cpu(), db.cpu()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("shape,k,s,p", [((2, 112, 112, 64), 3, 2, 1), ((3, 17, 19, 16), 3, 2, 0),
                                          ((2, 32, 40, 8), 2, 2, 0)])
 def test_maxpool(shape, k, s, p):
