@@ -130,11 +130,17 @@ def check(rc: int, name: str) -> None:
         raise RuntimeError(f"native kernel {name} failed: hipError_t={rc}")
 
 
+_FNS: dict = {}  # bound entry points by name (a ctypes attribute lookup per launch was measurable)
+
+
 def call(name: str, *args) -> None:
     """Invoke a HIP entry point and raise on error."""
-    lib = hip_lib()
-    fn = getattr(lib, name)
-    check(fn(*args), name)
+    fn = _FNS.get(name)
+    if fn is None:
+        fn = _FNS[name] = getattr(hip_lib(), name)
+    rc = fn(*args)
+    if rc:
+        check(rc, name)
     if CHECKED:
         check_kernels(name)
 

@@ -12,7 +12,17 @@ def ptr(t: torch.Tensor | None) -> int | None:
     return t.data_ptr()
 
 
+# The current stream's raw handle straight from the C++ stream state (torch.cuda.current_stream()
+# builds a Stream object through several Python device-index lookups: ~5 us per kernel launch, which
+# made the CNN-B1 b32 step host-bound, tools/host_profile.py).  Same answer: torch.cuda.stream()
+# contexts set that C++ state.
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+_CUR_DEVICE = getattr(torch._C, "_cuda_getDevice", None)
+
+
 def stream_handle() -> int:
+    if _RAW_STREAM is not None and _CUR_DEVICE is not None:
+        return _RAW_STREAM(_CUR_DEVICE())
     return torch.cuda.current_stream().cuda_stream
 
 

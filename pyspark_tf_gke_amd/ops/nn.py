@@ -15,7 +15,7 @@ import numpy as np
 import torch
 
 from . import reference as ref
-from ._util import hip, need, on_device, ptr
+from ._util import hip, need, on_device, ptr, stream_handle
 from .. import config
 
 # prelu+pool backward kernel: "sg" = sample-parallel blocks with an in-LDS dalpha reduction
@@ -884,7 +884,7 @@ class MlpStep:
         """``steps`` fused steps on x (steps*B rows, fp32) / y; ``t0`` = optimizer steps so far."""
         if t0 != self.t:  # the host counter moved (set_iterations, a checkpoint): resync the device one
             self.tstep.fill_(float(t0))
-        rc = self.lib.ptg_mlp_ctx_run(self.h, x.data_ptr(), y.data_ptr(), steps, torch.cuda.current_stream().cuda_stream)
+        rc = self.lib.ptg_mlp_ctx_run(self.h, x.data_ptr(), y.data_ptr(), steps, stream_handle())
         if rc:
             raise RuntimeError(f"native kernel ptg_mlp_ctx_run failed: hipError_t={rc}")
         self.t = t0 + steps
