@@ -1780,6 +1780,68 @@ __global__ __launch_bounds__(SNT) void sort_count_k(const unsigned long long* __
   (void)ntiles;
 }
 
+// The key range and the first radix pass's histogram in ONE read of the keys (an int64 column read raw,
+// XOR xin -> orderable): per tile the 256-bin histogram of the RAW low byte (the pass-0 digit
+// (k - base) & 255 is that byte rotated by base & 255; ptg_digit_offsets rot) and the tile's
+// min / max into tmm[2 * tile], reduced by sort_range_reduce_k.  Replaces sort_key_prep_k's range pass
+// and pass 0's sort_count_k.
+__global__ __launch_bounds__(SNT) void sort_range_count_k(const unsigned long long* __restrict__ keys, long n,
+                                                          unsigned long long xin, unsigned int* __restrict__ hist,
+                                                          unsigned long long* __restrict__ tmm) {
+  __shared__ unsigned int h[SNW][SB];
+  __shared__ unsigned long long wmn[SNW], wmx[SNW];
+  const int tid = threadIdx.x, w = tid >> 6, b = blockIdx.x;
+  for (int t = tid; t < SNW * SB; t += SNT) (&h[0][0])[t] = 0;
+  const long s0 = (long)b * ST;
+  unsigned long long k[SRPT];
+  unsigned long long mn = ~0ULL, mx = 0ULL;
+#pragma unroll
+  for (int j = 0; j < SRPT; ++j) {
+    const long i = s0 + j * SNT + tid;
+    k[j] = i < n ? keys[i] ^ xin : 0ULL;
+    if (i < n) { mn = k[j] < mn ? k[j] : mn; mx = k[j] > mx ? k[j] : mx; }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < SRPT; ++j)
+    if (s0 + j * SNT + tid < n) atomicAdd(&h[w][(unsigned)k[j] & (SB - 1)], 1u);
+  mn = wave_min_u64(mn);
+  mx = wave_max_u64(mx);
+  if ((tid & 63) == 0) { wmn[w] = mn; wmx[w] = mx; }
+  __syncthreads();
+  if (tid < SB) {
+    unsigned c = 0;
+#pragma unroll
+    for (int q = 0; q < SNW; ++q) c += h[q][tid];
+    hist[(long)b * SB + tid] = c;
+  }
+  if (tid == 0) {
+#pragma unroll
+    for (int q = 1; q < SNW; ++q) { mn = wmn[q] < mn ? wmn[q] : mn; mx = wmx[q] > mx ? wmx[q] : mx; }
+    mn = wmn[0] < mn ? wmn[0] : mn;
+    mx = wmx[0] > mx ? wmx[0] : mx;
+    tmm[2L * b] = mn;
+    tmm[2L * b + 1] = mx;
+  }
+}
+
+// range[0] = min, range[1] = max over the tiles' (min, max) pairs (range initialised to ~0 / 0)
+__global__ __launch_bounds__(256) void sort_range_reduce_k(const unsigned long long* __restrict__ tmm, int ntiles,
+                                                           unsigned long long* __restrict__ range) {
+  unsigned long long mn = ~0ULL, mx = 0ULL;
+  for (int t = blockIdx.x * 256 + threadIdx.x; t < ntiles; t += gridDim.x * 256) {
+    const unsigned long long a = tmm[2L * t], c = tmm[2L * t + 1];
+    mn = a < mn ? a : mn;
+    mx = c > mx ? c : mx;
+  }
+  mn = wave_min_u64(mn);
+  mx = wave_max_u64(mx);
+  if ((threadIdx.x & 63) == 0) {
+    atomicMin(&range[0], mn);
+    atomicMax(&range[1], mx);
+  }
+}
+
 // vals_in == nullptr: payload = row index (first pass of a fresh sort).  VT = unsigned int when the
 // row count fits 32 bits: 12 instead of 16 bytes per row read and written by every pass.
 // offs holds every (tile, digit) run's output position (sort_count_k + ptg_digit_offsets).
@@ -2440,6 +2502,19 @@ int ptg_sort_key_prep(const void* col, int type, long n, int desc, void* out, vo
   PTG_RETURN_LAUNCH();
 }
 int ptg_sort_tile_rows() { return ST; }
+// hist u32[256 * ntiles] (raw low-byte counts per tile), tmm u64[2 * ntiles] scratch, range u64[2]
+// (initialised to ~0 / 0 by the caller)
+int ptg_sort_range_count(const void* keys, long n, long xin, void* hist, void* tmm, void* range, hipStream_t s) {
+  const int ntiles = (int)((n + ST - 1) / ST);
+  if (ntiles <= 0) return 0;
+  hipLaunchKernelGGL(sort_range_count_k, dim3(ntiles), dim3(SNT), 0, s, (const unsigned long long*)keys, n,
+                     (unsigned long long)xin, (unsigned int*)hist, (unsigned long long*)tmm);
+  int g = (ntiles + 255) / 256;
+  if (g > 256) g = 256;
+  hipLaunchKernelGGL(sort_range_reduce_k, dim3(g), dim3(256), 0, s, (const unsigned long long*)tmm, ntiles,
+                     (unsigned long long*)range);
+  PTG_RETURN_LAUNCH();
+}
 // one LSD pass: hist u32[256*ntiles] (digit-major) -> offs i64[256*ntiles] (exclusive scan, host/torch)
 int ptg_sort_count(const void* keys, long n, long base, int shift, void* hist, long xin, hipStream_t s) {
   const int ntiles = (int)((n + ST - 1) / ST);

@@ -295,26 +295,30 @@ inline int grid_for(long n, int cap = 4096) {
 constexpr int DO_BINS = 256;
 
 // blockDim.x = number of digits (256, or 512 for the 9-bit hash partition of ptg_hash9_*)
+// rot: digit c's counts sit in column (c + rot) % bins of hist (a histogram of raw low key bytes when
+// the radix digit is (key - base) & 255: sort_range_count_k)
 __global__ __launch_bounds__(512) void colsum_k(const unsigned int* __restrict__ hist, int ntiles, int tpc,
-                                                long long* __restrict__ csum, int nch) {
+                                                long long* __restrict__ csum, int nch, int rot) {
   const int c = threadIdx.x, ch = blockIdx.x, bins = blockDim.x;
+  const int hc = (c + rot) & (bins - 1);
   const int t0 = ch * tpc, t1 = min(ntiles, t0 + tpc);
   long long s = 0;
 #pragma unroll 8
-  for (int t = t0; t < t1; ++t) s += hist[(long)t * bins + c];
+  for (int t = t0; t < t1; ++t) s += hist[(long)t * bins + hc];
   csum[(long)c * nch + ch] = s;
 }
 
 __global__ __launch_bounds__(512) void colapply_k(const unsigned int* __restrict__ hist, int ntiles, int tpc,
                                                   const long long* __restrict__ cbase, int nch,
-                                                  long long* __restrict__ offs) {
+                                                  long long* __restrict__ offs, int rot) {
   const int c = threadIdx.x, ch = blockIdx.x, bins = blockDim.x;
+  const int hc = (c + rot) & (bins - 1);
   const int t0 = ch * tpc, t1 = min(ntiles, t0 + tpc);
   long long run = cbase[(long)c * nch + ch];
   for (int t0b = t0; t0b < t1; t0b += 8) {  // 8 loads in flight, then the dependent running sum
     unsigned int h[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) h[u] = t0b + u < t1 ? hist[(long)(t0b + u) * bins + c] : 0u;
+    for (int u = 0; u < 8; ++u) h[u] = t0b + u < t1 ? hist[(long)(t0b + u) * bins + hc] : 0u;
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       if (t0b + u < t1) offs[(long)(t0b + u) * bins + c] = run;
@@ -360,20 +364,20 @@ extern "C" {
 // phase 0 = colsum (csum i64[256*nch]), phase 1 = colapply (cbase = scanned csum).  tpc = tiles per chunk.
 // bins: 256 (radix / range passes) or 512 (ptg_hash9_*); hist / offs rows are `bins` wide.
 int ptg_digit_offsets_b(int phase, const void* hist, int ntiles, int tpc, void* csum_or_cbase, int nch, void* offs,
-                        int bins, hipStream_t s) {
+                        int bins, int rot, hipStream_t s) {
   if (ntiles <= 0 || tpc <= 0 || nch != (ntiles + tpc - 1) / tpc || (bins != DO_BINS && bins != 2 * DO_BINS))
     return (int)hipErrorInvalidValue;
   if (phase == 0)
     hipLaunchKernelGGL(colsum_k, dim3(nch), dim3(bins), 0, s, (const unsigned int*)hist, ntiles, tpc,
-                       (long long*)csum_or_cbase, nch);
+                       (long long*)csum_or_cbase, nch, rot);
   else
     hipLaunchKernelGGL(colapply_k, dim3(nch), dim3(bins), 0, s, (const unsigned int*)hist, ntiles, tpc,
-                       (const long long*)csum_or_cbase, nch, (long long*)offs);
+                       (const long long*)csum_or_cbase, nch, (long long*)offs, rot);
   PTG_RETURN_LAUNCH();
 }
 int ptg_digit_offsets(int phase, const void* hist, int ntiles, int tpc, void* csum_or_cbase, int nch, void* offs,
-                      hipStream_t s) {
-  return ptg_digit_offsets_b(phase, hist, ntiles, tpc, csum_or_cbase, nch, offs, DO_BINS, s);
+                      int rot, hipStream_t s) {
+  return ptg_digit_offsets_b(phase, hist, ntiles, tpc, csum_or_cbase, nch, offs, DO_BINS, rot, s);
 }
 
 int ptg_scan_excl(const void* in, int in64, long n, void* out, void* total, void* bsum, hipStream_t s) {

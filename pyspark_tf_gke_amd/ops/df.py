@@ -645,9 +645,9 @@ def hash_agg_h9(keys: torch.Tensor, pay: list, buf, nv: int, est_keys: int):
     nch = -(-ntiles // tpc)
     csum = buf("h9_csum", (H9_BINS * nch,), torch.int64)
     cbase = buf("h9_cbase", (H9_BINS * nch,), torch.int64)
-    hip("ptg_digit_offsets_b", 0, ptr(hist), ntiles, tpc, ptr(csum), nch, None, H9_BINS)
+    hip("ptg_digit_offsets_b", 0, ptr(hist), ntiles, tpc, ptr(csum), nch, None, H9_BINS, 0)
     scan_excl(csum, out=cbase, total=offs[H9_BINS * ntiles:])
-    hip("ptg_digit_offsets_b", 1, ptr(hist), ntiles, tpc, ptr(cbase), nch, ptr(offs), H9_BINS)
+    hip("ptg_digit_offsets_b", 1, ptr(hist), ntiles, tpc, ptr(cbase), nch, ptr(offs), H9_BINS, 0)
     okeys = buf("h9okeys", (max(n, 1),), torch.int64)[:n]
     ovals = [buf(f"h9ov{j}", (max(n, 1),), torch.float64)[:n] for j in range(nv)]
     pin, pout = _pay_in(pay), _pay_out(ovals)
@@ -857,6 +857,20 @@ def sort_key(col: torch.Tensor, desc: bool = False, write: bool = True):
     return out, (lo if n else 0), (hi if n else 0)
 
 
+def sort_range_count(keys: torch.Tensor, xin: int):
+    """(lo, hi, hist0) of the orderable keys ``keys ^ xin`` in one read (device int64 column): the key
+    range and every sort tile's 256-bin histogram of the raw low byte, which
+    :func:`radix_sort_u64` (``hist0=``) uses as its first pass's counts."""
+    n = keys.numel()
+    ntiles = -(-n // _native.hip_lib().ptg_sort_tile_rows())
+    hist = torch.empty(256 * ntiles, dtype=torch.int32, device=keys.device)
+    tmm = torch.empty(2 * ntiles, dtype=torch.int64, device=keys.device)
+    rng = torch.tensor([-1, 0], dtype=torch.int64, device=keys.device)
+    hip("ptg_sort_range_count", ptr(keys), n, xin, ptr(hist), ptr(tmm), ptr(rng))
+    lo, hi = (x & _U64 for x in rng.cpu().tolist())
+    return lo, hi, hist
+
+
 def orderable_mask(desc: bool) -> int:
     """XOR mask taking an int64 value to its unsigned-orderable key (and back): the sign bit for
     ascending order, its complement for descending (as a signed int64)."""
@@ -877,29 +891,32 @@ def decode_sort_key(sk: torch.Tensor, dtype, desc: bool) -> torch.Tensor:
 DIGIT_OFFS_TPC = 64  # tiles per column-scan chunk (ptg_digit_offsets)
 
 
-def digit_offsets(hist: torch.Tensor, ntiles: int, offs: torch.Tensor, buf) -> torch.Tensor:
+def digit_offsets(hist: torch.Tensor, ntiles: int, offs: torch.Tensor, buf, rot: int = 0) -> torch.Tensor:
     """offs[t*256 + d] (int64, tile-major) = the stable output position of tile t's digit-d run, i.e.
     the digit-major exclusive scan of the tile-major [ntiles][256] counts ``hist``; offs[256*ntiles]
-    = total.  ``buf(name, shape, dtype)`` supplies workspace."""
+    = total.  ``buf(name, shape, dtype)`` supplies workspace.  ``rot``: digit d's counts are in column
+    (d + rot) % 256 of ``hist``."""
     tpc = DIGIT_OFFS_TPC
     nch = -(-ntiles // tpc)
     csum = buf("do_csum", (256 * nch,), torch.int64)
     cbase = buf("do_cbase", (256 * nch,), torch.int64)
-    hip("ptg_digit_offsets", 0, ptr(hist), ntiles, tpc, ptr(csum), nch, None)
+    hip("ptg_digit_offsets", 0, ptr(hist), ntiles, tpc, ptr(csum), nch, None, rot)
     scan_excl(csum, out=cbase, total=offs[256 * ntiles: 256 * ntiles + 1])
-    hip("ptg_digit_offsets", 1, ptr(hist), ntiles, tpc, ptr(cbase), nch, ptr(offs))
+    hip("ptg_digit_offsets", 1, ptr(hist), ntiles, tpc, ptr(cbase), nch, ptr(offs), rot)
     return offs
 
 
 def radix_sort_u64(keys: torch.Tensor, vals: torch.Tensor | None = None, lo: int = 0, hi: int = _U64,
-                   row_payload: bool = False, xin: int = 0, xout: int = 0):
+                   row_payload: bool = False, xin: int = 0, xout: int = 0, hist0: torch.Tensor | None = None):
     """Stable sort of u64 keys (held in an int64 tensor) with an int64 payload (default: the row
     index, i.e. the result payload is the sorting permutation).  Only the significant bits of
     hi - lo are sorted: ceil(bits / 8) LSD passes of sort_count_k + sort_scatter_k.
     ``row_payload``: ``vals`` holds row ids < 2^32 (a permutation), so it may travel as u32.
     ``xin`` / ``xout``: XOR masks the first pass applies to the keys as read and the last pass as
     written (:func:`orderable_mask`: raw int64 column in, decoded column values out - no separate
-    key prep / decode passes); with no pass at all (one distinct key) they must be equal."""
+    key prep / decode passes); with no pass at all (one distinct key) they must be equal.
+    ``hist0``: the first pass's per-tile raw low-byte counts from :func:`sort_range_count` (no
+    first count pass)."""
     n = keys.numel()
     if not on_device(keys):
         k = keys ^ xin if xin else keys
@@ -916,7 +933,7 @@ def radix_sort_u64(keys: torch.Tensor, vals: torch.Tensor | None = None, lo: int
             keys = keys ^ (xin ^ xout)
         return keys, (torch.arange(n, dtype=torch.int64, device=dev) if vals is None else vals)
     ntiles = -(-n // _native.hip_lib().ptg_sort_tile_rows())
-    hist = torch.empty(256 * ntiles, dtype=torch.int32, device=dev)
+    hist = hist0 if hist0 is not None else torch.empty(256 * ntiles, dtype=torch.int32, device=dev)
     offs = torch.empty(256 * ntiles + 1, dtype=torch.int64, device=dev)
     dws: dict = {}
 
@@ -938,8 +955,11 @@ def radix_sort_u64(keys: torch.Tensor, vals: torch.Tensor | None = None, lo: int
         shift = 8 * p
         pin = xin if p == 0 else 0
         pout = xout if p == passes - 1 else 0
-        hip("ptg_sort_count", ptr(ka), n, base, shift, ptr(hist), pin)
-        digit_offsets(hist, ntiles, offs, dbuf)
+        if p == 0 and hist0 is not None:
+            digit_offsets(hist, ntiles, offs, dbuf, rot=lo & 255)
+        else:
+            hip("ptg_sort_count", ptr(ka), n, base, shift, ptr(hist), pin)
+            digit_offsets(hist, ntiles, offs, dbuf)
         hip("ptg_sort_scatter", ptr(ka), ptr(va), n, base, shift, ptr(offs), ptr(kb), ptr(vb), int(v32), pin, pout)
         if kc is None:  # third buffer pair so the caller's keys/vals are never overwritten
             kc = torch.empty(n, dtype=torch.int64, device=dev)

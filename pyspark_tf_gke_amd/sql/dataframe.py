@@ -504,9 +504,13 @@ class DataFrame:
                 # int64 on the GPU: the first radix pass reads the raw column and the last writes the
                 # decoded values (XOR masks), so there is no key-prep write nor decode pass
                 fused = cv.data.dtype == torch.int64 and cv.data.is_cuda and config.get("sort_fused_keys")
-                k, lo, hi = D.sort_key(cv.data, desc=desc, write=not fused)
-                rs = dict(xin=D.orderable_mask(desc), xout=D.orderable_mask(desc)) if fused else {}
-                src = cv.data.contiguous() if fused else k
+                if fused:  # one read of the column: key range + the first radix pass's counts
+                    src = cv.data.contiguous()
+                    lo, hi, h0 = D.sort_range_count(src, D.orderable_mask(desc))
+                    rs = dict(xin=D.orderable_mask(desc), xout=D.orderable_mask(desc), hist0=h0)
+                else:
+                    k, lo, hi = D.sort_key(cv.data, desc=desc)
+                    src, rs = k, {}
                 others = [n for n in t.columns if n != name]
                 oc = t.column(others[0]) if len(others) == 1 else None
                 if (oc is not None and config.get("sort_value_payload") and oc.valid is None and oc.data.dim() == 1

@@ -361,6 +361,27 @@ def test_radix_sort_wide_payload(hip_built):
     assert torch.equal(sv.cpu(), pay[torch.from_numpy(order)])
 
 
+@pytest.mark.parametrize("n", [1, 4095, 4096 * 3 + 17])
+def test_sort_range_count(hip_built, n):
+    """df.hip sort_range_count_k: the orderable key range and each tile's raw low-byte histogram in
+    one read; the first radix pass's digit counts are that histogram rotated by lo & 255."""
+    from pyspark_tf_gke_amd.ops import df as D
+
+    g = torch.Generator().manual_seed(n)
+    k = torch.randint(-(1 << 62), 1 << 62, (n,), generator=g, dtype=torch.int64)
+    for desc in (False, True):
+        m = D.orderable_mask(desc)
+        lo, hi, h = D.sort_range_count(k.cuda(), m)
+        u = (k ^ m).numpy().view(np.uint64)
+        assert lo == int(u.min()) and hi == int(u.max())
+        ST = D._native.hip_lib().ptg_sort_tile_rows()
+        nt = -(-n // ST)
+        want = np.zeros((nt, 256), np.int64)
+        for t in range(nt):
+            want[t] = np.bincount((u[t * ST:(t + 1) * ST] & np.uint64(255)).astype(np.int64), minlength=256)
+        assert np.array_equal(h.cpu().numpy().reshape(nt, 256), want)
+
+
 @pytest.mark.parametrize("payload,fused", [("1", "1"), ("0", "1"), ("1", "0"), ("0", "0")])
 @pytest.mark.parametrize("dtype,asc", [(torch.int64, True), (torch.int64, False), (torch.int32, True)])
 def test_orderby_integer_key_output_keys(spark_gpu, dtype, asc, payload, fused, monkeypatch):
@@ -691,9 +712,9 @@ def test_digit_offsets_512_bins(ntiles):
     csum = torch.empty(B * nch, dtype=torch.int64, device="cuda")
     cbase = torch.empty_like(csum)
     offs = torch.full((B * ntiles + 1,), -7, dtype=torch.int64, device="cuda")
-    hip("ptg_digit_offsets_b", 0, ptr(hg), ntiles, tpc, ptr(csum), nch, None, B)
+    hip("ptg_digit_offsets_b", 0, ptr(hg), ntiles, tpc, ptr(csum), nch, None, B, 0)
     D.scan_excl(csum, out=cbase, total=offs[B * ntiles:])
-    hip("ptg_digit_offsets_b", 1, ptr(hg), ntiles, tpc, ptr(cbase), nch, ptr(offs), B)
+    hip("ptg_digit_offsets_b", 1, ptr(hg), ntiles, tpc, ptr(cbase), nch, ptr(offs), B, 0)
     out = offs.cpu()
     assert torch.equal(out[:-1], ref)
     assert int(out[-1]) == int(hist.long().sum())
