@@ -127,6 +127,9 @@ _K = [
     Knob("coord_dead_s", float, 60.0, "PTG_COORD_DEAD_S", None,
          "async ClusterCoordinator: a worker whose liveness beat is this old has its drawn-but-unfinished "
          "closures re-queued for the others"),
+    Knob("coord_stall_s", float, 0.0, "PTG_COORD_STALL_S", None,
+         "async ClusterCoordinator: fail every rank's join when no closure finished and no live worker ran "
+         "one for this long (0: PTG_PG_TIMEOUT)"),
     Knob("ipc_allreduce", bool, False, "PTG_IPC_ALLREDUCE", None, "one-shot IPC all-reduce for small messages"),
     Knob("fault_rank", str, "", "PTG_FAULT_RANK", None, "fault injection: rank to kill"),
     Knob("fault_step", int, 1, "PTG_FAULT_STEP", None, "fault injection: step at which fault_rank dies"),

@@ -197,7 +197,7 @@ class ClusterCoordinator:
         dead_mask = [0]  # ranks found dead by this rank's scans
         seen_nfin = [-1]
         skipped: list = []  # retry entries this rank was excluded from (claimable once the others die)
-        deadline_s = float(config.get("pg_timeout_s"))
+        deadline_s = float(config.get("coord_stall_s")) or float(config.get("pg_timeout_s"))
         cursor, fresh_done, last_scan, last_progress = 0, False, time.time(), time.time()
         try:
             while True:
@@ -226,11 +226,17 @@ class ClusterCoordinator:
                     if now - last_scan > min(1.0, dead_s / 4):
                         last_scan = now
                         dead_mask[0] |= self._rescue_dead(store, pre, n, world, rank, dead_s, requeue)
-                        if nfin != seen_nfin[0]:
+                        self._check_abort(store, pre)
+                        if nfin != seen_nfin[0] or self._live_busy(store, pre, world, rank, dead_mask[0], now, dead_s):
+                            # progress, or a live worker is inside a closure (a first-call native build
+                            # or an epoch-sized closure is not a stall)
                             seen_nfin[0], last_progress = nfin, now
                         elif now - last_progress > deadline_s:
-                            raise RuntimeError(f"ClusterCoordinator.join: no closure finished for {deadline_s:.0f} s "
-                                               f"({nfin}/{n} done; PTG_PG_TIMEOUT)")
+                            msg = (f"ClusterCoordinator.join: no closure finished for {deadline_s:.0f} s and no "
+                                   f"live worker is running one ({nfin}/{n} done; PTG_COORD_STALL_S), seen by "
+                                   f"worker {rank}")
+                            store.set(pre + "/abort", msg)  # every rank's loop fails with it, not just ours
+                            raise RuntimeError(msg)
                     for k, (j, i, tries, excl) in enumerate(skipped):
                         if (excl | dead_mask[0]) == every:
                             del skipped[k]
@@ -243,6 +249,7 @@ class ClusterCoordinator:
                 last_progress = time.time()
                 i, tries, excl = job
                 store.set(f"{pre}/own/{i}", str(rank))
+                store.set(f"{pre}/busy/{rank}", "1")
                 fn, args, kwargs, rv, _ = queue[i]
                 st._closure_pushed = False
                 try:
@@ -266,7 +273,9 @@ class ClusterCoordinator:
                     if finalize(i, f"V:{vt}:{x!r}"):
                         rv._set(value)
                         self.closures_run += 1
+                store.set(f"{pre}/busy/{rank}", "0")
                 heartbeat.progress()
+                self._check_abort(store, pre)
         finally:
             stop.set()
             hb.join(timeout=5)
@@ -275,6 +284,23 @@ class ClusterCoordinator:
             if not rv._done and rv._error is None:
                 rv._remote_key = f"{pre}/rv/{i}"  # ran elsewhere: resolved on fetch()
         comm.barrier()
+
+    @staticmethod
+    def _check_abort(store, pre) -> None:
+        """Fail this rank's join too once any rank declared the round stalled."""
+        if store.check([pre + "/abort"]):
+            raise RuntimeError(store.get(pre + "/abort").decode())
+
+    @staticmethod
+    def _live_busy(store, pre, world, rank, dead_mask, now, dead_s) -> bool:
+        """Whether another worker whose liveness beat is fresh is running a closure right now."""
+        for r in range(world):
+            if r == rank or dead_mask & (1 << r):
+                continue
+            bk, hk = f"{pre}/busy/{r}", f"{pre}/hb/{r}"
+            if store.check([bk, hk]) and store.get(bk) == b"1" and now - float(store.get(hk).decode()) <= dead_s:
+                return True
+        return False
 
     @staticmethod
     def _rescue_dead(store, pre, n, world, rank, dead_s, requeue) -> None:

@@ -118,6 +118,8 @@ def _lin_terms(name: str, args, kwargs):
     a = args[0] if args else None
     b = args[1] if len(args) > 1 else kwargs.get("other")
     alpha = kwargs.get("alpha", 1)
+    if any(isinstance(x, _TapeLoss) and getattr(x, "_terms", ()) is None for x in (a, b)):
+        return None  # an operand an in-place op already took out of the linear family
     if name in _SAME:
         return _terms(a)
     if name in _NEG:
@@ -519,8 +521,12 @@ def _update_takes_overlap(st) -> bool:
     if st is None:
         return True
     from ..distribute.ps import ParameterServerStrategy
+    from ..parallel import comm
 
-    return isinstance(st, ParameterServerStrategy) and st.world_size == 1
+    # the same gate as ps.py's apply_update / commit_round: a one-worker group that still runs its
+    # collectives (PTG_FORCE_PG + PTG_COLLECTIVES_WORLD1) pushes the flat gradient buffer, so a
+    # deferred Dense dW would be pushed before it exists
+    return isinstance(st, ParameterServerStrategy) and not comm.distributed()
 
 
 def _var_model(v):

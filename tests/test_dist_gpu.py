@@ -219,6 +219,7 @@ RCCL_BODY = """
 import json, torch
 from pyspark_tf_gke_amd.distribute import MultiWorkerMirroredStrategy
 from pyspark_tf_gke_amd.models import build_cnn_model
+from pyspark_tf_gke_amd.nn import model as M
 from pyspark_tf_gke_amd.parallel import comm
 import torch.distributed as dist
 st_s = MultiWorkerMirroredStrategy(sharded_update=True, bucket_mb=1.0)
@@ -228,10 +229,11 @@ g = torch.Generator().manual_seed(11)
 X = torch.rand(4, 16, 64, 80, 3, generator=g)
 Y = torch.rand(4, 16, 2, generator=g) * 60
 models = {}
-for name, st in (("sharded", st_s), ("plain", st_p)):
+for name, st in (("sharded", st_s), ("unfused", st_p), ("plain", st_p)):
     with st.scope():
         models[name] = build_cnn_model((64, 80, 3), flat=True, summary=False, device=dev)
-ms, mp = models["sharded"], models["plain"]
+ms, mu, mp = models["sharded"], models["unfused"], models["plain"]
+init = {p.name: p.data.clone() for p in mp.store.params}
 calls = {"rs": 0, "ag": 0}
 orig_rs, orig_ag = comm.reduce_scatter_flat, comm.all_gather_flat
 def rs(*a, **k):
@@ -242,26 +244,66 @@ def ag(*a, **k):
     calls["ag"] += 1
     return orig_ag(*a, **k)
 comm.reduce_scatter_flat, comm.all_gather_flat = rs, ag
+# the gradients each optimizer consumes: the sharded path's reduce-scattered bucket shards (world 1:
+# a shard is the whole bucket) and the replicated path's flat_grad with the Dense Adam NOT fused
+# into its dW GEMM (so every gradient is materialised)
+gs = torch.zeros(ms.store.total, device=dev)
+gu = torch.zeros(mu.store.total, device=dev)
+o_shard, o_apply = ms.optimizer.apply_shard, mu.optimizer.apply
+def apply_shard(store, gsh, lo, hi, gscale=1.0, advance=True):
+    gs[lo:hi] = gsh * gscale
+    return o_shard(store, gsh, lo, hi, gscale=gscale, advance=advance)
+def apply(store, gscale=1.0, lo=0, hi=None, advance=True):
+    h = store.total if hi is None else hi
+    gu[lo:h] = store.flat_grad[lo:h] * gscale
+    return o_apply(store, gscale=gscale, lo=lo, hi=hi, advance=advance)
+ms.optimizer.apply_shard, mu.optimizer.apply = apply_shard, apply
+grad_rel, losses = [], []
 for i in range(4):
-    for m in (ms, mp):
+    step_loss = []
+    for m in (ms, mu, mp):
         xb, yb = m._prep_batch(X[i], Y[i])
         stats = m._stats_buf()
         stats.zero_()
-        m.train_step_fast(xb, yb, stats)
+        old = M.FUSED_ADAM
+        M.FUSED_ADAM = old and m is not mu
+        try:
+            m.train_step_fast(xb, yb, stats)
+        finally:
+            M.FUSED_ADAM = old
+        step_loss.append(float(stats[0] / stats[4]))
+    losses.append(step_loss)
+    worst = 0.0
+    for p in mu.store.params:
+        q = ms.store.by_name(p.name)
+        a = gu[p.offset:p.offset + p.numel]
+        b = gs[q.offset:q.offset + q.numel]
+        worst = max(worst, float((a - b).norm()) / max(float(a.norm()), 1e-12))
+    grad_rel.append(worst)
 st_s.synchronize_master(ms)
 torch.cuda.synchronize()
-diff = max(float((p.data - mp.store.by_name(p.name).data).abs().max()) for p in ms.store.params)
-scale = max(float(p.data.abs().max()) for p in mp.store.params)
+# Adam turns a gradient at atomic-order noise level into a full +-lr step, so an element whose
+# gradient nearly cancels can land on either side (measured: one dense/kernel element moves 1.24e-3
+# either way in both the sharded AND the replicated path, tools/diag_shard_repeat.py): compare each
+# parameter's whole update instead - a stale, skipped or doubled bucket differs by its whole size
+upd = {}
+for p in ms.store.params:
+    q = mp.store.by_name(p.name)
+    upd[p.name] = (float((p.data - q.data).norm()), float((q.data - init[p.name]).norm()),
+                   float((p.data - q.data).abs().max()))
 print("RESULT", json.dumps({"backend": dist.get_backend(), "world": dist.get_world_size(), "sharded": st_s.sharded_update,
-                            "buckets": len(ms._shard_plan.buckets), "calls": calls, "diff": diff, "scale": scale}),
-      flush=True)
+                            "buckets": len(ms._shard_plan.buckets), "calls": calls, "grad_rel": grad_rel,
+                            "losses": losses, "upd": upd}), flush=True)
 """
 
 
 def test_single_rank_rccl_sharded_update_matches_replicated(hip_built):
     """A real 1-rank RCCL group (PTG_FORCE_PG, backend nccl): the sharded update's per-bucket
-    reduce-scatters (async, from the side stream) and bf16 / fp32 all-gathers run as RCCL kernels,
-    and four CNN steps give the replicated update's parameters."""
+    reduce-scatters (async, from the side stream) and bf16 / fp32 all-gathers run as RCCL kernels.
+    Over four CNN steps the gradients every bucket's shard update consumes equal the replicated
+    path's (relative L2 per parameter; a bucket reduce-scattered before its side-stream wgrads
+    finished, or read stale, is off by O(1)), the losses agree, and every parameter's update matches
+    the replicated (fused-Adam) path's to 5% of its size."""
     env = dict(os.environ)
     env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
     env.update({"PTG_FORCE_PG": "1", "PTG_SHARD_WORLD1": "1", "RANK": "0", "WORLD_SIZE": "1", "LOCAL_RANK": "0",
@@ -273,7 +315,14 @@ def test_single_rank_rccl_sharded_update_matches_replicated(hip_built):
     v = [json.loads(line.split("RESULT ", 1)[1]) for line in r.stdout.splitlines() if "RESULT " in line][0]
     assert v["backend"] == "nccl" and v["world"] == 1 and v["sharded"] and v["buckets"] > 2, v
     assert v["calls"]["rs"] >= 4 * v["buckets"] and v["calls"]["ag"] >= 4 * v["buckets"], v
-    assert v["diff"] <= 1e-4 * max(1.0, v["scale"]), v
+    # step 0 starts from identical parameters: only fp32 atomic-order noise (measured ~5e-7); later
+    # steps start from parameters that differ by that noise amplified as above.  A bucket read before
+    # its wgrads landed, zero or doubled is off by O(1)
+    assert v["grad_rel"][0] <= 1e-4 and max(v["grad_rel"]) <= 1e-2, v["grad_rel"]
+    for ls in v["losses"]:
+        assert max(ls) - min(ls) <= 1e-4 * max(1.0, abs(ls[-1])), v["losses"]
+    for name, (d, u, dmax) in v["upd"].items():
+        assert u > 0 and d <= 0.05 * u, (name, d, u, dmax)
 
 
 @pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
@@ -294,6 +343,7 @@ def test_tape_overlap_with_fresh_adam_matches_serial(hip_built):
         try:
             torch.manual_seed(3)
             m = build_cnn_model((64, 80, 3), flat=True, summary=False, device="cuda")
+            init = m.store.flat.clone()
             opt = nn.optimizers.Adam(1e-3)  # unbuilt: its first apply allocates m / v
             loss_fn = nn.losses.MeanSquaredError()
             for i in range(3):
@@ -306,7 +356,11 @@ def test_tape_overlap_with_fresh_adam_matches_serial(hip_built):
             T.OVERLAP = True
     a, b = flats
     assert torch.isfinite(a).all()
-    assert float((a - b).abs().max()) <= 1e-4 * max(1.0, float(b.abs().max()))
+    # whole-update comparison (see test_single_rank_rccl_sharded_update_matches_replicated): Adam
+    # moves an element whose gradient is at atomic-order noise by +-lr, so elementwise max-abs is not
+    # a sound test of two runs; a missed or stale moment build differs by the whole update
+    d, u = float((a - b).norm()), float((b - init).norm())
+    assert u > 0 and d <= 0.05 * u, (d, u, float((a - b).abs().max()))
 
 
 SITES_BODY = """

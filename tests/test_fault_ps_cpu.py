@@ -594,3 +594,46 @@ def test_train_tf_ps_cli_ps_mode(mode, tmp_path):
     assert len(res) == 2 and all(v["mode"] == mode for v in res.values()), res
     assert "Epoch 2 - loss:" in r.stdout
     assert os.path.exists(os.path.join(str(tmp_path), "model.keras"))
+
+
+def test_async_coordinator_long_closure_is_not_a_stall_and_stall_aborts_all():
+    """a closure longer than the stall deadline on a live worker is progress (its busy
+    mark and fresh liveness beat), not a stall; a real stall (here: the busy check stubbed out) is
+    declared by the idle rank in the store, and the busy rank's join fails with the same message as
+    soon as its closure returns, instead of walking into the collective tail."""
+    body = COMMON + """
+import sys, time
+C = sys.modules["pyspark_tf_gke_amd.distribute.coordinator"]
+st = ParameterServerStrategy(mode="async")
+def run(stub):
+    co = ClusterCoordinator(st)
+    if stub:
+        C.ClusterCoordinator._live_busy = staticmethod(lambda *a: False)
+    def closure(i):
+        if st.rank == 1:
+            time.sleep(4.0)        # 2 x PTG_COORD_STALL_S
+        return i
+    if st.rank == 0:
+        time.sleep(0.5)            # rank 1 draws closure 0 first
+    rvs = [co.schedule(closure, args=(i,)) for i in range(2)]
+    try:
+        co.join()
+        return [rv.fetch() for rv in rvs]
+    except RuntimeError as e:
+        return "ERR:" + str(e)[:60]
+ok = run(False)
+bad = run(True)
+print("RESULT", json.dumps({"ok": ok, "bad": bad}), flush=True)
+from pyspark_tf_gke_amd.distribute.ps import _store
+_store().set(f"test/done/{st.rank}", "1")
+if st.rank == 0:
+    _store().wait(["test/done/1"])
+os._exit(0)
+"""
+    r = _launch(body, 2, extra_env={"PTG_COORD_STALL_S": "2"})
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    res = _results(r.stdout)
+    assert sorted(res) == [0, 1], r.stdout[-3000:] + r.stderr[-3000:]
+    for v in res.values():
+        assert v["ok"] == [0, 1], v
+        assert v["bad"].startswith("ERR:ClusterCoordinator.join: no closure finished"), v

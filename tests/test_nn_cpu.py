@@ -432,6 +432,10 @@ def test_tape_untracked_target_raises():
         tape.gradient(torch.tensor(1.0), m.trainable_variables)  # not a recorded loss
     with pytest.raises(ValueError):
         tape.gradient(torch.sqrt(loss), m.trainable_variables)
+    alias = loss
+    loss.clamp_(max=1e9)  # in place: every reference to this loss leaves the linear family
+    with pytest.raises(ValueError):
+        tape.gradient(alias + 1, m.trainable_variables)  # was a TypeError
     with nn.GradientTape() as other:
         l2 = lo(y, m(X, training=True))
     with pytest.raises(ValueError):

@@ -59,7 +59,7 @@ def test_gemm_splitk_atomic_and_bias_relu():
 def test_linear_dx_dw(M, N, Kd, bn, monkeypatch):
     """dX on gemm_kernel: the CNN-B1 shape (M = 256, K = 20480) on the skinny-M 256x80 tiles (bn -1),
     forced 256x64 tiles, a ragged M with 256x64, and the 128x128 tiling (bn 0); the hipBLASLt route
-    (the default for this plain GEMM) is switched off so our kernel is the one checked."""
+    (an off-by-default A/B knob, PTG_BLASLT_DX) is pinned off so our kernel is the one checked."""
     from pyspark_tf_gke_amd import _native
 
     monkeypatch.setattr(K, "BLASLT_DX", False)
