@@ -209,6 +209,33 @@ def bench_train(args, strategy, rank, world):
     return res
 
 
+def bench_mlp_fit(B: int, steps_per_epoch: int = 2048, epochs: int = 3) -> dict:
+    """The reference's CSV-MLP ``model.fit`` loop (train_tf_ps.py:651-672) at batch B over a column
+    dataset: fit() keeps the columns in HBM and runs groups of 64 consecutive batches per launch of
+    the fused step (mlp.hip).  Every batch is a full forward/backward/Adam step; the time covers
+    whole epochs (including each epoch's metric readback), divided by the number of steps."""
+    import numpy as np
+
+    from pyspark_tf_gke_amd.data.dataset import Dataset
+    from pyspark_tf_gke_amd.models import build_deep_model
+
+    rng = np.random.default_rng(7)
+    X = rng.normal(size=(B * steps_per_epoch, 3)).astype(np.float32)
+    y = rng.integers(0, 15, B * steps_per_epoch).astype(np.int32)
+    ds = Dataset.from_tensor_slices((X, y)).batch(B)
+    model = build_deep_model(3, 15)
+    model.fit(ds, epochs=1, verbose=0)  # columns to HBM, plan + launch descriptors built
+    _sync()
+    t0 = time.perf_counter()
+    model.fit(ds, epochs=epochs, verbose=0)
+    _sync()
+    dt = time.perf_counter() - t0
+    n = steps_per_epoch * epochs
+    return {"value": round(B * n / dt, 2), "unit": "samples/s", "ms_per_step": round(dt / n * 1e3, 5),
+            "per_gpu_batch": B, "steps": n, "grouped": model._mlp_fit_plan(ds, None, None) is not None,
+            "model": "CSV-MLP 3->16->32->64->15 via model.fit over a Dataset (grouped fused steps)"}
+
+
 def bench_groupby(args, strategy, rank, world):
     from pyspark_tf_gke_amd.sql import bench_groupby as bg
 
@@ -269,6 +296,9 @@ def main():
                 extra[f"mlp_b{b}"] = {"value": r2["value"], "unit": "samples/s", "ms_per_step": r2["ms_per_step"],
                                       "per_gpu_batch": b, "global_batch": b * world,
                                       "model": "CSV-MLP 3->16->32->64->15 (train_tf_ps.py:328-343), Adam, fp32"}
+            if torch.cuda.is_available():
+                for b in [int(x) for x in args.mlp_batches.split(",") if x.strip()]:
+                    extra[f"mlp_fit_b{b}"] = bench_mlp_fit(b)
         if args.workload == "cnn_b1" and args.sim_world > 1 and world == 1 and torch.cuda.is_available():
             # the N>1 compute path on one GPU: dW into flat_grad, per-bucket reduce-scatter stand-in,
             # shard Adam, all-gather stand-in + bf16 re-cast (MultiWorkerMirroredStrategy sim mode)

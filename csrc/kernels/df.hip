@@ -1290,60 +1290,102 @@ __global__ __launch_bounds__(256) void range2_agg_k(const unsigned short* __rest
 
 // ---- tiny key ranges (max - min < ~4K): no partitioning at all ---------------------------------
 // Every workgroup holds the WHOLE key range as a direct-indexed LDS table (index = key - lo: no
-// hashing, probing or CAS), aggregates a contiguous chunk of rows with 4 rows' loads in flight, and
-// writes a dense partial table; the host sums the partials.  One read of the data (the LDS hash
-// table path, hash_agg_lds_k, ran 41-51 ms per 1B rows at 1K keys).
-template <int NV>
+// hashing, probing or CAS), aggregates a contiguous chunk of rows, and writes a dense partial table;
+// dense_extract sums the partials.  One read of the data (the LDS hash table path, hash_agg_lds_k,
+// ran 41-51 ms per 1B rows at 1K keys).
+//  * the key window [lo, lo + W) comes from a strided sample, not a full min/max pass: a key outside
+//    it sets *err and is skipped, and the host re-plans with the exact range (the sample costs 64K
+//    loads instead of a second 8 GB read of the key column at 1B rows);
+//  * per row: one u32 LDS atomic (row count) + one f64 LDS atomic per value column; the per-column
+//    value count is rows - nulls, so the null-count atomic runs only for a null / NaN value;
+//  * FAST (every value column plain f64 without a validity mask): rows go two per thread as 16-byte
+//    loads of two keys and two values, UNR pairs in flight per thread, no per-element type switch
+//    (the generic loader's switch serialised the unrolled loads behind vmcnt(0) waits).
+template <int NV, bool FAST>
 __global__ __launch_bounds__(256) void small_range_agg_k(const long long* __restrict__ keys, long n, long long lo, int W,
                                                          PayIn pin, long rows_per_block, unsigned int* __restrict__ prow,
-                                                         double* __restrict__ psum) {
+                                                         double* __restrict__ psum, int* __restrict__ err) {
   constexpr int NVS = NV > 0 ? NV : 1;
+  constexpr int UNR = 4;
   extern __shared__ __align__(16) unsigned char lds_raw[];
   double* lsum = (double*)lds_raw;                            // [NV][W]
-  unsigned int* lrow = (unsigned int*)(lsum + (long)NV * W);  // [1 + NV][W]
+  unsigned int* lrow = (unsigned int*)(lsum + (long)NV * W);  // [1 + NV][W]: rows, then nulls per column
   for (int t = threadIdx.x; t < W; t += 256) {
     lrow[t] = 0;
 #pragma unroll
     for (int j = 0; j < NV; ++j) { lsum[j * W + t] = 0.0; lrow[(1 + j) * W + t] = 0; }
   }
   __syncthreads();
+  bool bad = false;
   auto add = [&](long long k, const double* v) {
-    const int i = (int)(k - lo);  // lo / W are the exact key range (host: aminmax)
+    const unsigned long long i = (unsigned long long)(k - lo);
+    if (i >= (unsigned long long)W) { bad = true; return; }
     atomicAdd(&lrow[i], 1u);
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
-      if (v[j] != v[j]) continue;  // null / NaN
+      if (v[j] != v[j]) { atomicAdd(&lrow[(1 + j) * W + i], 1u); continue; }  // null / NaN
       atomicAdd(&lsum[j * W + i], v[j]);
-      atomicAdd(&lrow[(1 + j) * W + i], 1u);
     }
   };
   const long r0 = (long)blockIdx.x * rows_per_block, r1 = min(n, r0 + rows_per_block);
-  long i = r0 + threadIdx.x;
-  for (; i + 3 * 256 < r1; i += 4 * 256) {
-    long long k4[4];
-    double v4[4][NVS];
+  long i = r0;
+  if (FAST) {
+    // r0 is a multiple of 2 * 256 * UNR (host): pairs of rows are 16-byte aligned
+    const double* const* vals = (const double* const*)pin.vals;
+    for (; i + 2 * 256 * UNR <= r1; i += 2 * 256 * UNR) {
+      longlong2 k2[UNR];
+      double2 v2[UNR][NVS];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      k4[u] = keys[i + u * 256];
+      for (int u = 0; u < UNR; ++u) {
+        const long e = i + 2 * (u * 256 + threadIdx.x);
+        k2[u] = *(const longlong2*)(keys + e);
 #pragma unroll
-      for (int j = 0; j < NV; ++j) v4[u][j] = load_pay(pin, j, i + u * 256);
+        for (int j = 0; j < NV; ++j) v2[u][j] = *(const double2*)(vals[j] + e);
+      }
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        double a[NVS], b[NVS];
+#pragma unroll
+        for (int j = 0; j < NV; ++j) { a[j] = v2[u][j].x; b[j] = v2[u][j].y; }
+        add(k2[u].x, a);
+        add(k2[u].y, b);
+      }
     }
+    for (i += threadIdx.x; i < r1; i += 256) {
+      double v1[NVS];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) add(k4[u], v4[u]);
-  }
-  for (; i < r1; i += 256) {
-    double v1[NVS];
+      for (int j = 0; j < NV; ++j) v1[j] = vals[j][i];
+      add(keys[i], v1);
+    }
+  } else {
+    for (i += threadIdx.x; i + 3 * 256 < r1; i += 4 * 256) {
+      long long k4[4];
+      double v4[4][NVS];
 #pragma unroll
-    for (int j = 0; j < NV; ++j) v1[j] = load_pay(pin, j, i);
-    add(keys[i], v1);
+      for (int u = 0; u < 4; ++u) {
+        k4[u] = keys[i + u * 256];
+#pragma unroll
+        for (int j = 0; j < NV; ++j) v4[u][j] = load_pay(pin, j, i + u * 256);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) add(k4[u], v4[u]);
+    }
+    for (; i < r1; i += 256) {
+      double v1[NVS];
+#pragma unroll
+      for (int j = 0; j < NV; ++j) v1[j] = load_pay(pin, j, i);
+      add(keys[i], v1);
+    }
   }
+  if (bad) atomicOr(err, 1);
   __syncthreads();
   const long b = blockIdx.x;
   for (int t = threadIdx.x; t < W; t += 256) {
-    prow[(b * (1 + NV)) * W + t] = lrow[t];
+    const unsigned int rows = lrow[t];
+    prow[(b * (1 + NV)) * W + t] = rows;
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
-      prow[(b * (1 + NV) + 1 + j) * W + t] = lrow[(1 + j) * W + t];
+      prow[(b * (1 + NV) + 1 + j) * W + t] = rows - lrow[(1 + j) * W + t];
       psum[(b * NV + j) * W + t] = lsum[j * W + t];
     }
   }
@@ -2469,26 +2511,34 @@ int ptg_range_agg(const void* okeys, const void* const* vals, int nv, int minmax
 #undef PTG_RAG
   PTG_RETURN_LAUNCH();
 }
-// tiny key range: prow u32[blocks][1+nv][W], psum f64[blocks][nv][W]; every key in [lo, lo + W)
+// tiny key range: prow u32[blocks][1+nv][W], psum f64[blocks][nv][W]; a key outside [lo, lo + W)
+// sets *err (int, host-zeroed) and is left out.  fast: every value column plain f64 without a
+// validity mask (rows_per_block then a multiple of 2048, see small_range_agg_k)
 int ptg_small_range_agg(const void* keys, long n, long lo, int W, const void* pin_p, int nv, long rows_per_block,
-                        int blocks, void* prow, void* psum, hipStream_t s) {
+                        int blocks, void* prow, void* psum, void* err, int fast, hipStream_t s) {
   const size_t lds = (size_t)W * (4 + (size_t)nv * 12);
   if (nv < 0 || nv > PAY_MAX || W <= 0 || blocks <= 0 || lds > 150 * 1024) return (int)hipErrorInvalidValue;
+  if (fast && (rows_per_block % 2048 || ((uintptr_t)keys & 15))) return (int)hipErrorInvalidValue;
   PayIn pin;
   memcpy(&pin, pin_p, sizeof(PayIn));
-#define PTG_SRA(NV)                                                                                          \
+#define PTG_SRA(NV, F)                                                                                       \
   {                                                                                                          \
     static bool attr = false;                                                                                \
     if (!attr) {                                                                                             \
-      (void)hipFuncSetAttribute((const void*)small_range_agg_k<NV>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+      (void)hipFuncSetAttribute((const void*)small_range_agg_k<NV, F>, hipFuncAttributeMaxDynamicSharedMemorySize, \
                                 150 * 1024);                                                                 \
       attr = true;                                                                                           \
     }                                                                                                        \
-    hipLaunchKernelGGL((small_range_agg_k<NV>), dim3(blocks), dim3(256), lds, s, (const long long*)keys, n,     \
-                       (long long)lo, W, pin, rows_per_block, (unsigned int*)prow, (double*)psum);          \
+    hipLaunchKernelGGL((small_range_agg_k<NV, F>), dim3(blocks), dim3(256), lds, s, (const long long*)keys, n,  \
+                       (long long)lo, W, pin, rows_per_block, (unsigned int*)prow, (double*)psum, (int*)err); \
   }
-  switch (nv) { case 0: PTG_SRA(0) break; case 1: PTG_SRA(1) break; case 2: PTG_SRA(2) break;
-                case 3: PTG_SRA(3) break; default: PTG_SRA(4) break; }
+  if (fast) {
+    switch (nv) { case 1: PTG_SRA(1, true) break; case 2: PTG_SRA(2, true) break;
+                  case 3: PTG_SRA(3, true) break; case 4: PTG_SRA(4, true) break; default: PTG_SRA(0, false) break; }
+  } else {
+    switch (nv) { case 0: PTG_SRA(0, false) break; case 1: PTG_SRA(1, false) break; case 2: PTG_SRA(2, false) break;
+                  case 3: PTG_SRA(3, false) break; default: PTG_SRA(4, false) break; }
+  }
 #undef PTG_SRA
   PTG_RETURN_LAUNCH();
 }

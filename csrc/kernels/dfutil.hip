@@ -409,6 +409,43 @@ int ptg_minmax_i64(const void* p, long n, long stride, int off_min, int off_max,
   PTG_RETURN_LAUNCH();
 }
 
+// fold the C partial tables of a direct-indexed aggregation into ceil(C / F) tables (sums of F
+// consecutive chunks, in chunk order): dense_count_k / dense_write_k parallelise over keys only, so
+// with a narrow key range (W ~ 1K: one workgroup) and many chunks (small_range_agg_k: one per
+// workgroup of the pass) their per-key loop over C partials was a latency-bound serial tail.
+// grid (ceil(W / 256), ceil(C / F)); prow u32[C][1+nv][W], psum f64[C][nv][W] -> orow / osum.
+__global__ __launch_bounds__(256) void dense_fold_k(const unsigned int* __restrict__ prow, const double* __restrict__ psum,
+                                                    int C, int nv, long W, int F, unsigned int* __restrict__ orow,
+                                                    double* __restrict__ osum) {
+  const long w = (long)blockIdx.x * 256 + threadIdx.x;
+  if (w >= W) return;
+  const int c2 = blockIdx.y, k0 = c2 * F, k1 = min(C, k0 + F);
+  for (int q = 0; q <= nv; ++q) {
+    unsigned int acc[4] = {0u, 0u, 0u, 0u};
+    int k = k0;
+    for (; k + 4 <= k1; k += 4) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[u] += prow[((long)(k + u) * (1 + nv) + q) * W + w];
+    }
+    for (; k < k1; ++k) acc[0] += prow[((long)k * (1 + nv) + q) * W + w];
+    orow[((long)c2 * (1 + nv) + q) * W + w] = acc[0] + acc[1] + acc[2] + acc[3];
+  }
+  for (int v = 0; v < nv; ++v) {
+    double acc = 0.0;  // one accumulator in chunk order: the same sum as the unfolded extract
+    for (int k = k0; k < k1; ++k) acc += psum[((long)k * nv + v) * W + w];
+    osum[((long)c2 * nv + v) * W + w] = acc;
+  }
+}
+
+int ptg_dense_fold(const void* prow, const void* psum, int C, int nv, long W, int F, void* orow, void* osum,
+                   hipStream_t s) {
+  if (nv < 0 || nv > 4 || C < 1 || F < 1 || W <= 0) return (int)hipErrorInvalidValue;
+  const dim3 grid((unsigned)((W + 255) / 256), (unsigned)((C + F - 1) / F));
+  hipLaunchKernelGGL(dense_fold_k, grid, dim3(256), 0, s, (const unsigned int*)prow, (const double*)psum, C, nv, W, F,
+                     (unsigned int*)orow, (double*)osum);
+  PTG_RETURN_LAUNCH();
+}
+
 // dense-key groups: see DenseOut.  Pass 1 (counts=1): block counts of occupied keys -> bcount
 // (int32[nb]), boff (int64[nb]) scanned, total (int64[1]).  Pass 2 (counts=0): writes the outputs
 // (capacity = total; the host allocates after reading total).  outs: host array of 2 + 4 * 4 device

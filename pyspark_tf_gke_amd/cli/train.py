@@ -302,12 +302,53 @@ def _plot_mae(history: dict, path: str) -> None:
         matplotlib.use("Agg")
         import matplotlib.pyplot as plt
 
-        plt.plot(history.get("mae", []))
+        for k in ("mae", "val_mae"):
+            if history.get(k):
+                plt.plot(range(1, len(history[k]) + 1), history[k], label=k)
         plt.xlabel("epoch")
+        plt.ylabel("MAE (px)")
+        plt.yscale("log")
+        plt.legend()
         plt.savefig(path)
         plt.close()
+    except ImportError:
+        _plot_curves_pil({k: history[k] for k in ("mae", "val_mae") if history.get(k)}, path)
     except Exception as e:  # noqa: BLE001
         print(f"plot skipped: {e}")
+
+
+def _plot_curves_pil(curves: dict, path: str, size=(640, 400)) -> None:
+    """Line plot of per-epoch curves with PIL only (matplotlib is not in the image): log-scale y,
+    axes with min / max labels, one colour per curve and a legend."""
+    from PIL import Image, ImageDraw
+
+    import math
+
+    W, H = size
+    L, R, T, B = 60, 20, 20, 40
+    img = Image.new("RGB", size, "white")
+    d = ImageDraw.Draw(img)
+    vals = [v for c in curves.values() for v in c if v > 0]
+    if not vals:
+        return
+    lo, hi = math.log10(min(vals)), math.log10(max(vals))
+    hi = hi if hi > lo else lo + 1.0
+    n = max(len(c) for c in curves.values())
+    d.rectangle([L, T, W - R, H - B], outline="black")
+    for frac, v in ((0.0, lo), (1.0, hi)):
+        y = H - B - frac * (H - T - B)
+        d.text((4, y - 6), f"{10 ** v:.3g}", fill="black")
+    d.text((L, H - B + 6), "1", fill="black")
+    d.text((W - R - 30, H - B + 6), str(n), fill="black")
+    d.text(((W - L) // 2, H - B + 20), "epoch", fill="black")
+    colours = ["#1f77b4", "#d62728", "#2ca02c", "#9467bd"]
+    for k, (name, c) in enumerate(curves.items()):
+        pts = [(L + (i / max(n - 1, 1)) * (W - L - R), H - B - (math.log10(max(v, 1e-12)) - lo) / (hi - lo) * (H - T - B))
+               for i, v in enumerate(c)]
+        if len(pts) > 1:
+            d.line(pts, fill=colours[k % len(colours)], width=2)
+        d.text((W - R - 120, T + 6 + 14 * k), name, fill=colours[k % len(colours)])
+    img.save(path)
 
 
 def main(argv: Optional[List[str]] = None) -> int:

@@ -44,6 +44,8 @@ _K = [
     # data engine
     Knob("groupby_range", bool, True, "PTG_GROUPBY_RANGE", "spark.ptg.groupby.range",
          "dense small-range integer keys take the one-pass range partition + direct LDS aggregation"),
+    Knob("groupby_small_blocks", int, 1024, "PTG_GROUPBY_SMALL_BLOCKS", None,
+         "workgroups of the tiny-key-range groupBy pass (small_range_agg_k; each writes one dense partial table)"),
     Knob("groupby_range2", bool, True, "PTG_GROUPBY_RANGE2", "spark.ptg.groupby.range2",
          "dense integer keys spanning 2^20..2^28 values: two 256-way range partitioning passes + direct LDS aggregation"),
     Knob("groupby_range_chunks", int, 8, "PTG_RANGE_CHUNKS", "spark.ptg.groupby.rangeChunks",

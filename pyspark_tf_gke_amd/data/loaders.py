@@ -186,20 +186,30 @@ def _resident_image_dataset(paths, targets, img_h, img_w, batch_size, shuffle, i
     return ds
 
 
-def write_synthetic_image_dataset(out_dir: str, n: int = 64, size=(256, 320), seed: int = 0) -> str:
-    """A laser-spot-like dataset: dark noisy frames with one bright red spot at a random pixel."""
-    from PIL import Image
-
-    os.makedirs(out_dir, exist_ok=True)
+def synthetic_laser_spots(n: int, size=(256, 320), seed: int = 0):
+    """Yield ``n`` (uint8 [H, W, 3] frame, (x_px, y_px)) laser-spot-like samples: a dark noisy frame
+    with one bright red Gaussian spot (sigma 3 px) at a uniform random position >= 10 px from the
+    border - the shape of the reference's laser-spot dataset (clean_labels.jsonl, train_tf_ps.py:
+    234-268), which is not shipped with it."""
     rng = np.random.default_rng(seed)
     h, w = size
     yy, xx = np.mgrid[0:h, 0:w]
+    for _ in range(n):
+        x, y = float(rng.uniform(10, w - 10)), float(rng.uniform(10, h - 10))
+        img = rng.integers(0, 40, (h, w, 3), dtype=np.uint8)
+        spot = np.exp(-((xx - x) ** 2 + (yy - y) ** 2) / 18.0)
+        img[..., 0] = np.clip(img[..., 0] + 215 * spot, 0, 255).astype(np.uint8)
+        yield img, (x, y)
+
+
+def write_synthetic_image_dataset(out_dir: str, n: int = 64, size=(256, 320), seed: int = 0) -> str:
+    """A laser-spot-like dataset on disk (PNG frames + clean_labels.jsonl): :func:`synthetic_laser_spots`."""
+    from PIL import Image
+
+    os.makedirs(out_dir, exist_ok=True)
+    h, w = size
     with open(os.path.join(out_dir, "clean_labels.jsonl"), "w") as fh:
-        for i in range(n):
-            x, y = float(rng.uniform(10, w - 10)), float(rng.uniform(10, h - 10))
-            img = rng.integers(0, 40, (h, w, 3), dtype=np.uint8)
-            spot = np.exp(-((xx - x) ** 2 + (yy - y) ** 2) / 18.0)
-            img[..., 0] = np.clip(img[..., 0] + 215 * spot, 0, 255).astype(np.uint8)
+        for i, (img, (x, y)) in enumerate(synthetic_laser_spots(n, size, seed)):
             name = f"img_{i:05d}.png"
             Image.fromarray(img).save(os.path.join(out_dir, name))
             fh.write(json.dumps({"image": name, "point": {"x_px": x, "y_px": y},

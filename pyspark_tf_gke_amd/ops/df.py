@@ -114,11 +114,16 @@ def compact(mask: torch.Tensor) -> torch.Tensor:
     return idx
 
 
-def gather_rows(t: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
-    if not on_device(t):
-        return t.index_select(0, idx)
+def gather_rows(t: torch.Tensor, idx: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """t[idx] along dim 0; ``out`` (contiguous, [idx.numel(), *t.shape[1:]]) receives the rows in place
+    of a new tensor (a shuffle writes its local rows straight into their final output slice)."""
     m = idx.numel()
-    out = torch.empty((m, *t.shape[1:]), dtype=t.dtype, device=t.device)
+    if out is not None and (tuple(out.shape) != (m, *t.shape[1:]) or out.dtype != t.dtype or not out.is_contiguous()):
+        raise ValueError(f"gather_rows: out {tuple(out.shape)} {out.dtype} does not fit {m} rows of {tuple(t.shape)}")
+    if not on_device(t):
+        return torch.index_select(t, 0, idx, out=out) if out is not None else t.index_select(0, idx)
+    if out is None:
+        out = torch.empty((m, *t.shape[1:]), dtype=t.dtype, device=t.device)
     if m == 0:
         return out
     row_bytes = t[0].numel() * t.element_size() if t.dim() > 0 and t.shape[0] > 0 else t.element_size()
@@ -243,7 +248,9 @@ def _pow2(x: int) -> int:
 
 def _small_range_agg(keys, vals, valids):
     """Keys spanning < ~4K values (small_range_agg_k): the whole range is one direct-indexed LDS
-    table per workgroup, one pass over the rows; None when the span is wider."""
+    table per workgroup, one pass over the rows; None when the span is wider.  The key window comes
+    from a strided sample (64K loads); a key outside it makes the kernel flag an error and the pass
+    is re-run on the exact range (one full min/max read of the keys, only then)."""
     n = keys.numel()
     nv = len(vals)
     keys = keys.contiguous()
@@ -252,24 +259,46 @@ def _small_range_agg(keys, vals, valids):
     slo, shi = minmax_i64(keys, n=(n + st - 1) // st, stride=st)
     if shi - slo >= wmax:
         return None
-    lo, hi = minmax_i64(keys)
-    W = hi - lo + 1
-    if W > wmax:
-        return None
     pay = []
     for v, vd in zip(vals, valids):
         v = v.view(torch.uint8) if v.dtype == torch.bool else v.contiguous()
         if vd is not None and vd.dtype == torch.bool:
             vd = vd.view(torch.uint8)
         pay.append((v, vd))
-    G = 1024
-    rpb = -(-n // G)
+    fast = nv > 0 and all(v.dtype == torch.float64 and vd is None and v.data_ptr() % 16 == 0 for v, vd in pay) \
+        and keys.data_ptr() % 16 == 0
+    pin = _pay_in(pay)
+    err = zeros(1, torch.int32, keys.device)
+    # a little headroom around the sampled range: a key the sample missed just outside it still fits
+    span = shi - slo + 1
+    pad = min((wmax - span) // 2, span // 16 + 8)
+    lo, W = slo - pad, span + 2 * pad
+    G = int(config.get("groupby_small_blocks"))
+    quant = 2048 if fast else 1
+    rpb = -(-(-(-n // G)) // quant) * quant
     G = -(-n // rpb)
     prow = torch.empty((G, 1 + nv, W), dtype=torch.int32, device=keys.device)
     psum = torch.empty((G, max(nv, 1), W), dtype=torch.float64, device=keys.device)
-    pin = _pay_in(pay)
     hip("ptg_small_range_agg", ptr(keys), n, lo, W, ctypes.addressof(pin), nv, rpb, G, ptr(prow),
-        ptr(psum))
+        ptr(psum), ptr(err), int(fast))
+    if int(err.item()):
+        lo, hi = minmax_i64(keys)  # the sample missed keys: exact range
+        W = hi - lo + 1
+        if W > wmax:
+            return None
+        prow = torch.empty((G, 1 + nv, W), dtype=torch.int32, device=keys.device)
+        psum = torch.empty((G, max(nv, 1), W), dtype=torch.float64, device=keys.device)
+        fill(err, 0)
+        hip("ptg_small_range_agg", ptr(keys), n, lo, W, ctypes.addressof(pin), nv, rpb, G, ptr(prow),
+            ptr(psum), ptr(err), int(fast))
+    if G > 64:
+        # fold the per-workgroup partials 32 at a time first: the extract parallelises over keys only
+        F = 32
+        G2 = -(-G // F)
+        prow2 = torch.empty((G2, 1 + nv, W), dtype=torch.int32, device=keys.device)
+        psum2 = torch.empty((G2, max(nv, 1), W), dtype=torch.float64, device=keys.device)
+        hip("ptg_dense_fold", ptr(prow), ptr(psum), G, nv, W, F, ptr(prow2), ptr(psum2))
+        prow, psum, G = prow2, psum2, G2
     return _dense_extract(prow, psum, None, G, nv, W, lo, keys.device)
 
 
@@ -609,7 +638,10 @@ def hash_agg_range2(keys: torch.Tensor, pay: list, buf, nv: int, sample_lohi: tu
 
 
 H9_BINS = 512
-H9_MIN_KEYS = 1 << 16  # below this the recursive path needs one 64-way level: the same passes
+# the recursive path runs two 64-way levels for any >= 1M-row input (partition parallelism), so one
+# 512-way hash9 pass wins from the smallest cardinality the LDS-table path hands over (4096 keys,
+# sql/dataframe.py _RADIX_MIN_KEYS): 4K sparse keys over 1B rows took 82.7 ms on the two levels
+H9_MIN_KEYS = 1 << 12
 
 
 def _h9_table_slots(est_keys: int, nv: int) -> int | None:

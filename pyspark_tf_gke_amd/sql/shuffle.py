@@ -2,12 +2,15 @@
 RCCL all-to-all-v between the GPUs of one node (the reference's Spark workers move
 these blocks over the pod network, spark_session.py:80-83 sizes their memory).
 
-* one device-side count exchange (a single int64 all_to_all), never pickled;
+* one device-side count exchange (a single int64 all-gather of every rank's count vector, so every
+  rank knows the whole count matrix and the round count without another collective), never pickled;
 * rows are gathered per destination straight from the source columns (no permuted copy of the
   whole table), in as many rounds as the staging budget requires — ``spark.ptg.shuffle.buffer.gb``
   (deploy/node.yaml) bounds the bytes staged per direction per round, and every rank runs the same
   number of rounds (one all-reduce MAX of the round count);
-* received chunks land directly in their final place of the output columns;
+* every column and validity mask of a round goes out in one grouped point-to-point launch, and the
+  backend writes each received chunk straight into its final slice of the output column (no
+  receive staging, no copy after the collective); a rank's own rows are gathered into place;
 * ``spark.sql.shuffle.partitions`` (spark_installation_check.py:16) is the number of hash buckets of
   a keyed shuffle (:func:`bucket_exchange`): bucket b belongs to rank b % world and the exchange
   runs one reduce partition per round (round r moves bucket r * world + d to rank d), so each round
@@ -41,15 +44,27 @@ def budget_bytes() -> int:
     return max(1, int(gb * (1 << 30)))
 
 
-def exchange_counts(send_counts: torch.Tensor) -> list:
-    """send_counts int64[world] (rows this rank sends to each rank) -> rows it receives from each."""
+def count_matrix(send_counts) -> list:
+    """Every rank's send counts (int64[world], on the device or host) -> the full matrix
+    M[src][dst] of rows, identical on every rank: ONE all-gather of the count vectors and ONE
+    device-to-host copy.  Rank r receives column r; every rank derives the same round count."""
     world = comm.world_size()
     dev = comm._ctl_device()
-    sc = send_counts.to(device=dev, dtype=torch.int64).contiguous()
-    rc = torch.empty(world, dtype=torch.int64, device=dev)
-    torch.distributed.all_to_all_single(rc, sc)
+    if isinstance(send_counts, torch.Tensor):
+        sc = send_counts.to(device=dev, dtype=torch.int64).contiguous()
+    else:
+        sc = torch.tensor([int(x) for x in send_counts], dtype=torch.int64, device=dev)
+    mat = torch.empty(world * world, dtype=torch.int64, device=dev)
+    torch.distributed.all_gather_into_tensor(mat, sc)
     STATS["count_exchanges"] += 1
-    return [int(x) for x in rc.cpu().tolist()]
+    flat = mat.cpu().tolist()
+    return [flat[s * world:(s + 1) * world] for s in range(world)]
+
+
+def exchange_counts(send_counts: torch.Tensor) -> list:
+    """send_counts int64[world] (rows this rank sends to each rank) -> rows it receives from each."""
+    m = count_matrix(send_counts)
+    return [m[s][comm.rank()] for s in range(comm.world_size())]
 
 
 def _row_bytes(cv: ColumnVector) -> int:
@@ -65,50 +80,97 @@ def _unify_strings(t: Table) -> Table:
     return Table(cols, t.num_rows, t.device)
 
 
-def shuffle_table(t: Table, perm: torch.Tensor, counts: torch.Tensor, budget: int | None = None) -> Table:
+def _seg_range(segs: list, lo: int, hi: int) -> list:
+    """Views of the index segments ``segs`` (concatenated) covering positions [lo, hi)."""
+    out, base = [], 0
+    for sg in segs:
+        n = sg.numel()
+        a, b = max(lo, base), min(hi, base + n)
+        if a < b:
+            out.append(sg[a - base:b - base])
+        base += n
+        if base >= hi:
+            break
+    return out
+
+
+def shuffle_table(t: Table, perm: torch.Tensor, counts, budget: int | None = None) -> Table:
     """Send rows ``perm[start_d : start_d + counts[d]]`` to rank d (perm groups rows by destination)
     and return the rows this rank receives, ordered by source rank."""
-    world = comm.world_size()
     if not comm.distributed():
         return t.take(perm)
+    world = comm.world_size()
+    mat = count_matrix(counts)
+    sc = mat[comm.rank()]
+    starts = [sum(sc[:d]) for d in range(world)]
+    segs = [[perm[starts[d]:starts[d] + sc[d]]] for d in range(world)]
+    return exchange(t, segs, mat, budget)
+
+
+def exchange(t: Table, segs: list, mat: list, budget: int | None = None) -> Table:
+    """The shuffle proper.  ``segs[d]``: index tensors (views) of the rows this rank sends to rank d,
+    in order; ``mat``: the count matrix of :func:`count_matrix` (every rank's sends).
+
+    Per round, every column and validity mask goes out in ONE grouped point-to-point launch
+    (``batch_isend_irecv``: RCCL runs a round's sends and receives as one ncclGroup); each received
+    chunk is written by the backend straight into its final slice of the output column (rows from
+    source s at ``sum(rc[:s]) + rc[s] * r // rounds``), and this rank's own rows are gathered
+    directly into theirs — no receive staging and no copy after the collective.  The only staging
+    is the per-destination send gather, bounded by the budget per round."""
+    world, rank = comm.world_size(), comm.rank()
     budget = budget or budget_bytes()
     t = _unify_strings(t)
-    sc = [int(x) for x in counts.cpu().tolist()]
-    rc = exchange_counts(counts)
+    sc = mat[rank]
+    rc = [mat[s][rank] for s in range(world)]
     row_bytes = sum(_row_bytes(cv) for cv in t.columns.values()) or 1
-    need = max(sum(sc), sum(rc)) * row_bytes
+    # every rank computes the same round count from the same matrix (no extra collective)
+    need = max(max(sum(mat[r]), sum(mat[s][r] for s in range(world))) for r in range(world)) * row_bytes
     rounds = max(1, math.ceil(need / budget))
-    rounds = comm.all_reduce_int([rounds], op=torch.distributed.ReduceOp.MAX)[0]
     dev = t.device
-    send_start = [sum(sc[:d]) for d in range(world)]
     recv_start = [sum(rc[:s]) for s in range(world)]
     n_out = sum(rc)
-    out = {}
+    out, srcs = {}, []
     for n, cv in t.columns.items():
         data = torch.empty((n_out, *cv.data.shape[1:]), dtype=cv.data.dtype, device=dev)
         valid = torch.empty(n_out, dtype=torch.uint8, device=dev) if cv.valid is not None else None
         out[n] = (data, valid)
+        srcs.append((cv.data.contiguous(), data))
+        if valid is not None:
+            srcs.append((cv.valid_u8().contiguous(), valid))
     peak = 0
     for r in range(rounds):
-        c = [sc[d] * (r + 1) // rounds - sc[d] * r // rounds for d in range(world)]
-        q = [rc[s] * (r + 1) // rounds - rc[s] * r // rounds for s in range(world)]
-        parts = [perm[send_start[d] + sc[d] * r // rounds: send_start[d] + sc[d] * r // rounds + c[d]]
-                 for d in range(world)]
-        idx = torch.cat(parts) if parts else perm[:0]
-        for n, cv in t.columns.items():
-            for src_t, dst_t in ((cv.data, out[n][0]), (cv.valid_u8(), out[n][1])):
-                if src_t is None:
+        ops, keep, staged = [], [], 0
+        for d in range(world):
+            lo, hi = sc[d] * r // rounds, sc[d] * (r + 1) // rounds
+            s_lo, s_hi = rc[d] * r // rounds, rc[d] * (r + 1) // rounds
+            parts = _seg_range(segs[d], lo, hi) if hi > lo else []
+            for src, dst in srcs:
+                if d == rank:
+                    o = recv_start[d] + lo
+                    for pt in parts:  # own rows: gathered straight into their output slice
+                        D.gather_rows(src, pt, out=dst[o:o + pt.numel()])
+                        o += pt.numel()
                     continue
-                send = D.gather_rows(src_t.contiguous(), idx)
-                recv = comm.all_to_all_v(send, c, q)
-                peak = max(peak, send.numel() * send.element_size() + recv.numel() * recv.element_size())
-                off = 0
-                for s in range(world):
-                    if q[s]:
-                        o = recv_start[s] + rc[s] * r // rounds
-                        dst_t[o: o + q[s]].copy_(recv[off: off + q[s]])
-                    off += q[s]
-                del send, recv
+                if hi > lo:
+                    if len(parts) == 1:
+                        buf = D.gather_rows(src, parts[0])
+                    else:
+                        buf = torch.empty((hi - lo, *src.shape[1:]), dtype=src.dtype, device=src.device)
+                        o = 0
+                        for pt in parts:
+                            D.gather_rows(src, pt, out=buf[o:o + pt.numel()])
+                            o += pt.numel()
+                    keep.append(buf)
+                    staged += buf.numel() * buf.element_size()
+                    ops.append(torch.distributed.P2POp(torch.distributed.isend, buf, d))
+                if s_hi > s_lo:
+                    o = recv_start[d] + s_lo
+                    ops.append(torch.distributed.P2POp(torch.distributed.irecv, dst[o:o + (s_hi - s_lo)], d))
+        if ops:
+            for req in torch.distributed.batch_isend_irecv(ops):
+                req.wait()
+        peak = max(peak, staged)
+        del keep
     STATS["peak_staging_bytes"] = peak
     STATS["rounds"] = rounds
     cols = {n: ColumnVector(out[n][0], cv.dtype, out[n][1], cv.dictionary) for n, cv in t.columns.items()}
@@ -203,15 +265,15 @@ def bucket_exchange(t: Table, key: torch.Tensor, nbuckets: int, budget: int | No
     for g in groups:
         sel, sc = [], []
         for d in range(world):
-            n_d = 0
+            n_d, segs = 0, []
             for rr in g:
                 b = rr * world + d
                 if b < nbuckets and ch[b]:
-                    sel.append(perm[starts[b]: starts[b] + ch[b]])
+                    segs.append(perm[starts[b]: starts[b] + ch[b]])
                     n_d += ch[b]
+            sel.append(segs)
             sc.append(n_d)
-        idx = torch.cat(sel) if sel else perm[:0]
-        out = shuffle_table(t, idx, torch.tensor(sc, dtype=torch.int64), budget)
+        out = exchange(t, sel, count_matrix(sc), budget)
         peak = max(peak, STATS["peak_staging_bytes"])
         STATS["reduce_tasks"] += 1
         mine = [rr * world + rank for rr in g if rr * world + rank < nbuckets]

@@ -16,7 +16,15 @@ from torch.utils._python_dispatch import TorchDispatchMode  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--rows", type=int, default=2_000_000)
+ap.add_argument("--multirank", action="store_true",
+                help="the multi-rank path on one GPU: a 1-rank RCCL group with PTG_COLLECTIVES_WORLD1, so the "
+                     "groupBy / orderBy shuffles (count matrix, p2p exchange, range split) run; only the "
+                     "single-int64-key groupBy and the orderBy are recorded")
 a = ap.parse_args()
+if a.multirank:
+    os.environ.update({"PTG_FORCE_PG": "1", "PTG_COLLECTIVES_WORLD1": "1", "RANK": "0", "WORLD_SIZE": "1",
+                       "LOCAL_RANK": "0", "LOCAL_WORLD_SIZE": "1", "MASTER_ADDR": "127.0.0.1",
+                       "MASTER_PORT": os.environ.get("MASTER_PORT", "29671")})
 
 SKIP = ("view", "_unsafe_view", "alias", "empty", "empty_strided", "as_strided", "detach", "t", "transpose",
         "permute", "expand", "slice", "select", "unsqueeze", "squeeze", "reshape", "_reshape_alias", "split",
@@ -59,6 +67,23 @@ k, v = D.fill_synthetic_kv(a.rows, 1000, "cuda")
 big = DataFrame(Table({"k": ColumnVector(k, T.LongType()), "v": ColumnVector(v, T.DoubleType())}, a.rows, k.device),
                 spark)
 torch.cuda.synchronize()
+if a.multirank:
+    from pyspark_tf_gke_amd.parallel import comm  # noqa: E402
+
+    comm.init()
+    assert comm.distributed()
+    big.groupBy("k").agg(count("*").alias("n"), fsum("v").alias("s"))._t.num_rows  # warm (plans, buffers)
+    torch.cuda.synchronize()
+    with Rec():
+        g = big.groupBy("k").agg(count("*").alias("n"), fsum("v").alias("s"))
+        g._t.num_rows
+        o = big.orderBy(col("v").desc())
+        o._t.num_rows
+    torch.cuda.synchronize()
+    print(json.dumps({"multirank": True, "groups": int(g._t.num_rows), "sorted_rows": int(o._t.num_rows)}))
+    for (name, site), c in counts.most_common():
+        print(json.dumps({"op": name, "count": c, "site": site}))
+    sys.exit(0)
 with Rec():
     df.groupBy("measure_name", "subpopulation").agg(count("*").alias("n"), avg("value").alias("m"),
                                                     fsum("value").alias("s"), fmax("upper_ci").alias("hi")).collect()
