@@ -31,6 +31,12 @@
 #endif
 
 // p/m/v groups of 8 whose loads the fused-Adam epilogue issues before its first update (per thread)
+#ifndef PTG_ADAM_V4
+#define PTG_ADAM_V4 0
+#endif
+#ifndef PTG_ADAM_PRE4
+#define PTG_ADAM_PRE4 8
+#endif
 #ifndef PTG_ADAM_PRE
 #define PTG_ADAM_PRE 4
 #endif
@@ -393,6 +399,34 @@ struct EpiAdam {
     st4(ve + i, r.V[0]); st4(ve + i + 4, r.V[1]);
     st16(pbf + i, pack8(o));
   }
+#if PTG_ADAM_V4
+  // 4 columns per lane (PTG_ADAM_V4): 32 lanes cover a 128-column row, so every load / store
+  // instruction of a wave is two fully contiguous 512-byte runs (the 8-column form issues each
+  // instruction as 64 16-byte pieces at a 32-byte stride, every line touched by two instructions)
+  static constexpr int PRE4 = PTG_ADAM_PRE4;
+  struct Pre4 { float4 P, Mm, V; };
+  PTG_DEV void preload4(int m, int n, int cnt, Pre4& r) const {
+    const long i = (long)m * ldc + n;
+    if (cnt != 4 || (i & 3)) return;
+    r.P = ld4(p + i); r.Mm = ld4(mo + i); r.V = ld4(ve + i);
+  }
+  PTG_DEV void vec4_pre(int m, int n, const float* v, int cnt, Pre4& r) const {
+    const long i = (long)m * ldc + n;
+    if (cnt != 4 || (i & 3)) {
+      for (int j = 0; j < cnt; ++j) (*this)(m, n + j, v[j]);
+      return;
+    }
+    const float l = lr();
+    float* pp = &r.P.x; float* mm = &r.Mm.x; float* vv = &r.V.x;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) upd(pp[j], mm[j], vv[j], v[j], l);
+    st4(p + i, r.P); st4(mo + i, r.Mm); st4(ve + i, r.V);
+    U2 b;
+    b.x = pack_bf(pp[0], pp[1]);
+    b.y = pack_bf(pp[2], pp[3]);
+    *(U2*)(pbf + i) = b;
+  }
+#endif
   PTG_DEV void vec8(int m, int n, float* v, int cnt) const {
     Pre r;
     preload(m, n, cnt, r);
@@ -401,6 +435,8 @@ struct EpiAdam {
 };
 template <class E, class = void> struct EpiPre { static constexpr int v = 0; };
 template <class E> struct EpiPre<E, std::void_t<decltype(E::PRE)>> { static constexpr int v = E::PRE; };
+template <class E, class = void> struct EpiPre4 { static constexpr int v = 0; };
+template <class E> struct EpiPre4<E, std::void_t<decltype(E::PRE4)>> { static constexpr int v = E::PRE4; };
 struct EpiAtomic {  // split-K: out[m*ldc+n] += acc  (device-scope fp32 atomic, no return)
   static constexpr bool VEC = false;  // lane-consecutive atomics coalesce; 8-per-lane runs do not
   float* out; long ldc;
@@ -701,7 +737,32 @@ __global__ __launch_bounds__(256) void gemm_kernel(LA la, LB lb, EPI epi, int M,
         cs[(wm * WTM + i * 16 + (lane >> 4) * 4 + r) * CP + wn * WTN + j * 16 + (lane & 15)] = acc[i][j][r];
   __syncthreads();
   constexpr int NV = BM * BN / 8;
-  if constexpr (EpiPre<EPI>::v > 0 && NV % 256 == 0) {
+  if constexpr (EpiPre4<EPI>::v > 0 && (BM * BN / 4) % 256 == 0) {
+    // read-modify-write epilogue, 4 consecutive columns per lane (EpiAdam with PTG_ADAM_V4)
+    constexpr int NIT = BM * BN / 4 / 256, B = EpiPre4<EPI>::v < NIT ? EpiPre4<EPI>::v : NIT;
+#pragma unroll
+    for (int b0 = 0; b0 < NIT; b0 += B) {
+      typename EPI::Pre4 pre[B];
+      int mm[B], nn[B];
+#pragma unroll
+      for (int u = 0; u < B; ++u) {
+        const int v = (b0 + u) * 256 + tid;
+        const int row = v / (BN / 4), c4 = v - row * (BN / 4);
+        mm[u] = m0 + row; nn[u] = n0 + c4 * 4;
+        if (mm[u] < M && nn[u] < N) epi.preload4(mm[u], nn[u], min(4, N - nn[u]), pre[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < B; ++u) {
+        if (mm[u] >= M || nn[u] >= N) continue;
+        const int v = (b0 + u) * 256 + tid;
+        const int row = v / (BN / 4), c4 = v - row * (BN / 4);
+        const float4 a = *(const float4*)(cs + row * CP + c4 * 4);
+        const float vals[4] = {a.x, a.y, a.z, a.w};
+        epi.vec4_pre(mm[u], nn[u], vals, min(4, N - nn[u]), pre[u]);
+      }
+    }
+    return;
+  } else if constexpr (EpiPre<EPI>::v > 0 && NV % 256 == 0) {
     // read-modify-write epilogue: a batch of lanes' operand loads first, then the updates
     constexpr int NIT = NV / 256, B = EpiPre<EPI>::v < NIT ? EpiPre<EPI>::v : NIT;
 #pragma unroll

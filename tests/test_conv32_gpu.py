@@ -16,10 +16,10 @@ CASES = [(64, 80, 16, 32, "pool"), (32, 40, 32, 64, "pool"), (16, 20, 64, 64, "p
 
 
 @pytest.mark.skipif(not torch.cuda.is_available(), reason="needs a GPU")
+@pytest.mark.parametrize("N", [3, 160])  # 160: 320-pixel tiles (C = 64: two half-channel passes); 3: 160-pixel tiles
 @pytest.mark.parametrize("H,W,C,Co,epi", CASES)
-def test_conv32_matches_fp32_reference(hip_built, H, W, C, Co, epi):
+def test_conv32_matches_fp32_reference(hip_built, H, W, C, Co, epi, N):
     g = torch.Generator(device="cuda").manual_seed(H * 100 + C + Co)
-    N = 3
     x = (torch.randn((N, H, W, C), device="cuda", generator=g)).bfloat16()
     w = (torch.randn((Co, 5, 5, C), device="cuda", generator=g) * 0.05).bfloat16()
     b = torch.randn(Co, device="cuda", generator=g) * 0.1 if epi else None

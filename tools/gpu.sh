@@ -45,7 +45,7 @@ for task in "$@"; do
     prof)
       wl=${arg:-cnn_b1}
       timeout -k 10 $STEP_T rocprofv3 --kernel-trace --stats --output-format csv -d "gpurun_out/prof_$wl" -o run -- \
-        python bench.py --workload "$wl" --steps ${PROF_STEPS:-10} --warmup 3 --groupby-extra 0 --extra-batches "" --sim-world 0 \
+        python bench.py --workload "$wl" --steps ${PROF_STEPS:-10} --warmup 3 --groupby-extra 0 --extra-batches "" --mlp-batches "" --sim-world 0 \
         $BENCH_ARGS > "gpurun_out/prof_$wl.log" 2>&1 || fail prof "gpurun_out/prof_$wl.log"
       grep metric "gpurun_out/prof_$wl.log" | cut -c1-200
       python tools/prof_summary.py "gpurun_out/prof_$wl/run_kernel_stats.csv" $(( ${PROF_STEPS:-10} + 3 )) > "gpurun_out/prof_${wl}_summary.txt" 2>&1 || true
@@ -54,20 +54,20 @@ for task in "$@"; do
       wl=${arg:-cnn_b1}
       timeout -s KILL 150 rocprofv3 --kernel-trace --pmc SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS \
         SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU SQ_INSTS_VMEM SQ_WAVE_CYCLES SQ_WAIT_ANY GRBM_GUI_ACTIVE --output-format csv \
-        -d "gpurun_out/pmc_${wl}_a" -o run -- python bench.py --workload "$wl" --steps 2 --warmup 1 --groupby-extra 0 --sim-world 0 \
+        -d "gpurun_out/pmc_${wl}_a" -o run -- python bench.py --workload "$wl" --steps 2 --warmup 1 --groupby-extra 0 --mlp-batches "" --sim-world 0 \
         --extra-batches "" $BENCH_ARGS > "gpurun_out/pmc_${wl}_a.log" 2>&1 || fail pmc_a "gpurun_out/pmc_${wl}_a.log"
       timeout -s KILL 150 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d "gpurun_out/pmc_${wl}_b" \
-        -o run -- python bench.py --workload "$wl" --steps 2 --warmup 1 --groupby-extra 0 --extra-batches "" --sim-world 0 \
+        -o run -- python bench.py --workload "$wl" --steps 2 --warmup 1 --groupby-extra 0 --extra-batches "" --mlp-batches "" --sim-world 0 \
         $BENCH_ARGS > "gpurun_out/pmc_${wl}_b.log" 2>&1 || fail pmc_b "gpurun_out/pmc_${wl}_b.log"
       python tools/pmc_report.py "gpurun_out/pmc_${wl}_a" "gpurun_out/pmc_${wl}_b" > "gpurun_out/pmc_${wl}_report.txt" \
         2>&1 || true
       head -30 "gpurun_out/pmc_${wl}_report.txt" ;;
     ab)
       for i in 1 2; do
-        timeout -k 10 $STEP_T python bench.py --groupby-extra 0 --extra-batches "" --sim-world 0 $BENCH_ARGS > gpurun_out/ab_a$i.json \
+        timeout -k 10 $STEP_T python bench.py --groupby-extra 0 --extra-batches "" --mlp-batches "" --sim-world 0 $BENCH_ARGS > gpurun_out/ab_a$i.json \
           2> gpurun_out/ab_a.err || fail ab_a gpurun_out/ab_a.err
         echo "A $(cut -c1-160 gpurun_out/ab_a$i.json)"
-        timeout -k 10 $STEP_T env $AB_ENV python bench.py --groupby-extra 0 --extra-batches "" --sim-world 0 $BENCH_ARGS \
+        timeout -k 10 $STEP_T env $AB_ENV python bench.py --groupby-extra 0 --extra-batches "" --mlp-batches "" --sim-world 0 $BENCH_ARGS \
           > gpurun_out/ab_b$i.json 2> gpurun_out/ab_b.err || fail ab_b gpurun_out/ab_b.err
         echo "B $(cut -c1-160 gpurun_out/ab_b$i.json)"
       done ;;
@@ -77,7 +77,7 @@ for task in "$@"; do
       IFS=';' read -ra sets <<< "${ABM_ENVS:-}"
       for i in 1 2; do
         for e in "${sets[@]}" ""; do
-          timeout -k 10 $STEP_T env $e python bench.py --workload "$wl" --groupby-extra 0 --extra-batches "" --sim-world 0 \
+          timeout -k 10 $STEP_T env $e python bench.py --workload "$wl" --groupby-extra 0 --extra-batches "" --mlp-batches "" --sim-world 0 \
             $BENCH_ARGS > gpurun_out/abm.json 2> gpurun_out/abm.err || fail abm gpurun_out/abm.err
           echo "[${e:-default}] $(python -c "import json; d = json.load(open('gpurun_out/abm.json')); print(d['value'], d['ms_per_step'], 'final_loss', d['config'].get('final_loss'))")"
         done
@@ -85,7 +85,7 @@ for task in "$@"; do
     abvar)
       for i in 1 2; do
         for lib in "" "libptg_hip_$arg.so"; do
-          PTG_HIP_LIB=$lib timeout -k 10 $STEP_T python bench.py --groupby-extra 0 --extra-batches "" --sim-world 0 $BENCH_ARGS \
+          PTG_HIP_LIB=$lib timeout -k 10 $STEP_T python bench.py --groupby-extra 0 --extra-batches "" --mlp-batches "" --sim-world 0 $BENCH_ARGS \
             > gpurun_out/abvar.json 2> gpurun_out/abvar.err || fail abvar gpurun_out/abvar.err
           echo "${lib:-default} $(cut -c1-160 gpurun_out/abvar.json)"
         done
