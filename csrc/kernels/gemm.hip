@@ -32,7 +32,7 @@
 
 // p/m/v groups of 8 whose loads the fused-Adam epilogue issues before its first update (per thread)
 #ifndef PTG_ADAM_V4
-#define PTG_ADAM_V4 0
+#define PTG_ADAM_V4 1
 #endif
 #ifndef PTG_ADAM_PRE4
 #define PTG_ADAM_PRE4 8
@@ -400,9 +400,12 @@ struct EpiAdam {
     st16(pbf + i, pack8(o));
   }
 #if PTG_ADAM_V4
-  // 4 columns per lane (PTG_ADAM_V4): 32 lanes cover a 128-column row, so every load / store
-  // instruction of a wave is two fully contiguous 512-byte runs (the 8-column form issues each
-  // instruction as 64 16-byte pieces at a 32-byte stride, every line touched by two instructions)
+  // 4 columns per lane (PTG_ADAM_V4, default): 32 lanes cover a 128-column row, so every load /
+  // store instruction of a wave is two fully contiguous 512-byte runs (the 8-column form issues each
+  // instruction as 64 16-byte pieces at a 32-byte stride, every line touched by two instructions).
+  // CNN-B1 step: b256 1.555 -> 1.527 ms, b32 0.619 -> 0.600 ms (profiles/r6_ab_adam_v4.txt); an
+  // 8-deep preload batch (PTG_ADAM_PRE4) beat 4.  A one-stage / half-tile-staging low-LDS form of
+  // this GEMM lost at b256 (profiles/r6_ab_adam_lowlds_rejected.txt) and was removed.
   static constexpr int PRE4 = PTG_ADAM_PRE4;
   struct Pre4 { float4 P, Mm, V; };
   PTG_DEV void preload4(int m, int n, int cnt, Pre4& r) const {
