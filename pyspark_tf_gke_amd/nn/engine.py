@@ -95,6 +95,17 @@ class Op:
         raise NotImplementedError
 
 
+def _const_buf(ws, key, shape, value, dev):
+    """A workspace buffer filled with ``value`` once per (re)allocation (the per-element alphas of a
+    ReLU / identity layer run through the PReLU kernels): the fill used to run at every forward and
+    backward - a framework fill kernel per call in the MNIST step."""
+    t = ws.get(key, shape, torch.float32, dev)
+    if getattr(t, "_ptg_const", None) != value:
+        K.fill_(t, value)
+        t._ptg_const = value
+    return t
+
+
 def _bf16(x, ws, key):
     if x.dtype == torch.bfloat16 or (_HOST_FP32[0] and x.device.type == "cpu"):
         return x
@@ -147,9 +158,7 @@ class ConvOp(Op):
 
     def _alpha_const(self, ws, value, dev):
         key = self.name + ("/ones" if value else "/zeros")
-        t = ws.get(key, self.conv.out_shape, torch.float32, dev)
-        t.fill_(value)
-        return t
+        return _const_buf(ws, key, self.conv.out_shape, value, dev)
 
     def _raw_u8_ok(self, x) -> bool:
         """Raw uint8 images straight into the sparse first-layer kernels (same size, no resize)."""
@@ -221,8 +230,7 @@ class ConvOp(Op):
             a = ws.get(self.name + "/a", (B, OH, OW, Co), torch.bfloat16, dev)
             return K.prelu_fwd(z, self.prelu.alpha.data, a)
         if self.pool is not None:
-            ones = ws.get(self.name + "/ones", (OH, OW, Co), torch.float32, dev)
-            ones.fill_(1.0)
+            ones = _const_buf(ws, self.name + "/ones", (OH, OW, Co), 1.0, dev)
             p = ws.get(self.name + "/p", (B, OH // 2, OW // 2, Co), torch.bfloat16, dev)
             return K.prelu_pool_fwd(z, ones, p)
         return z
@@ -562,8 +570,7 @@ class PoolOp(Op):
         x = _bf16(x, ws, self.name + "/x16")
         self._z = x
         B, H, W, C = x.shape
-        ones = ws.get(self.name + "/ones", (H, W, C), torch.float32, x.device)
-        ones.fill_(1.0)
+        ones = _const_buf(ws, self.name + "/ones", (H, W, C), 1.0, x.device)
         p = ws.get(self.name + "/p", (B, H // 2, W // 2, C), torch.bfloat16, x.device)
         return K.prelu_pool_fwd(x, ones, p)
 

@@ -841,7 +841,7 @@ def hash_partition(keys: torch.Tensor, P: int):
         return torch.from_numpy(perm.astype(np.int64)), torch.from_numpy(counts.astype(np.int64))
     dev = keys.device
     part = torch.empty(n, dtype=torch.int32, device=dev)
-    counts = torch.zeros(P, dtype=torch.int64, device=dev)
+    counts = zeros(P, torch.int64, dev)
     hip("ptg_hash_partition", ptr(keys), n, P, ptr(part), ptr(counts))
     return partition_perm(part, counts), counts
 
@@ -1032,7 +1032,7 @@ def range_partition(keys: torch.Tensor, splitters: torch.Tensor, P: int):
         part = np.searchsorted(sp, u, side="left").astype(np.int32)
         return torch.from_numpy(part), torch.from_numpy(np.bincount(part, minlength=P).astype(np.int64))
     part = torch.empty(n, dtype=torch.int32, device=keys.device)
-    counts = torch.zeros(P, dtype=torch.int64, device=keys.device)
+    counts = zeros(P, torch.int64, keys.device)
     sp = splitters.to(keys.device).contiguous()
     hip("ptg_range_partition", ptr(keys), n, ptr(sp), ns, ptr(part), ptr(counts))
     return part, counts

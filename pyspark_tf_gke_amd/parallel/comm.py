@@ -227,14 +227,45 @@ def all_gather_v(t: torch.Tensor) -> list:
     ns = torch.empty(world, dtype=torch.int64, device=dev)
     dist.all_gather_into_tensor(ns, n)
     lens = [int(x) for x in ns.cpu().tolist()]
+    out, mx = _all_gather_padded(t, lens, dev)
+    return [out[r * mx: r * mx + lens[r]].to(t.device) for r in range(world)]
+
+
+def _all_gather_padded(t: torch.Tensor, lens: list, dev) -> tuple:
+    """All-gather of every rank's rows padded to the longest (the pad rows are never read, so they
+    are not initialised): -> (out [world * mx, ...] on ``dev``, mx)."""
+    world = len(lens)
     mx = max(lens)
     row = t.shape[1:]
-    src = torch.zeros((mx, *row), dtype=t.dtype, device=dev)
-    if t.shape[0]:
-        src[: t.shape[0]] = t.to(dev)
+    if t.shape[0] == mx and t.device == torch.device(dev) and t.is_contiguous():
+        src = t
+    else:
+        src = torch.empty((mx, *row), dtype=t.dtype, device=dev)
+        if t.shape[0]:
+            src[: t.shape[0]].copy_(t)
     out = torch.empty((world * mx, *row), dtype=t.dtype, device=dev)
     dist.all_gather_into_tensor(out, src)
-    return [out[r * mx: r * mx + lens[r]].to(t.device) for r in range(world)]
+    return out, mx
+
+
+def all_gather_v_host(t: torch.Tensor):
+    """:func:`all_gather_v` concatenated in rank order as ONE host numpy array (one device-to-host
+    copy of the padded gather, the concatenation done on the host)."""
+    import numpy as np
+
+    if not distributed():
+        return t.cpu().numpy()
+    world = dist.get_world_size()
+    dev = _ctl_device()
+    n = torch.tensor([t.shape[0]], dtype=torch.int64, device=dev)
+    ns = torch.empty(world, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(ns, n)
+    lens = [int(x) for x in ns.cpu().tolist()]
+    if max(lens) == 0:
+        return t.cpu().numpy()[:0]
+    out, mx = _all_gather_padded(t, lens, dev)
+    h = out.cpu().numpy()
+    return np.concatenate([h[r * mx: r * mx + lens[r]] for r in range(world)])
 
 
 def all_gather_unique(t: torch.Tensor) -> torch.Tensor:

@@ -818,8 +818,8 @@ def _range_splitters(keys: torch.Tensor, world: int, per_rank: int = 4096) -> to
     """world-1 splitters (u64 bit patterns in int64) from a strided sample of every rank's keys."""
     n = keys.numel()
     step = max(1, n // per_rank)
-    sample = keys[::step][:per_rank].contiguous()
-    allk = torch.cat(comm.all_gather_v(sample)).cpu().numpy().view(np.uint64)
+    sample = D.strided_sample(keys.contiguous(), step, min(per_rank, -(-n // step)))
+    allk = comm.all_gather_v_host(sample).view(np.uint64)
     allk.sort()
     if allk.size == 0:
         return torch.zeros(world - 1, dtype=torch.int64)
@@ -860,8 +860,12 @@ def _decode_key(k: torch.Tensor, src: ColumnVector, null: torch.Tensor | None = 
     """Inverse of :func:`_key_of`: group key (+ null flag) -> key column value (so grouped outputs
     need no representative-row lookup)."""
     valid = None if null is None or not bool(null.any()) else (~null).to(torch.uint8)
-    if null is None:
-        null = torch.zeros_like(k, dtype=torch.bool)
+    if valid is None:  # no null group: the key is the value (no where / zeros kernels)
+        if isinstance(src.dtype, T.StringType):
+            return ColumnVector(k.to(torch.int32), src.dtype, None, src.dictionary)
+        if src.data.dtype in (torch.float64, torch.float32):
+            return ColumnVector(k.view(torch.float64).to(src.data.dtype), src.dtype, None)
+        return ColumnVector(k.to(src.data.dtype), src.dtype, None)
     if isinstance(src.dtype, T.StringType):
         return ColumnVector(torch.where(null, torch.full_like(k, -1), k).to(torch.int32), src.dtype, None,
                             src.dictionary)
@@ -1291,7 +1295,9 @@ class GroupedData:
                 rs.append(o2[0][0])
                 os_.append([(o2[1 + 4 * j][0], o2[2 + 4 * j][0], o2[3 + 4 * j][2], o2[4 + 4 * j][3])
                             for j in range(len(outs))])
-            if ks:
+            if len(ks) == 1:  # one reduce task (the usual case after adaptive coalescing): no copies
+                ukeys, rows, outs = ks[0], rs[0], os_[0]
+            elif ks:
                 ukeys, rows = torch.cat(ks), torch.cat(rs)
                 outs = [tuple(torch.cat([o[j][q] for o in os_]) for q in range(4)) for j in range(len(outs))]
             else:
