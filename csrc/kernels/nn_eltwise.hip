@@ -914,36 +914,44 @@ __global__ __launch_bounds__(256) void softmax_xent_k(const float* __restrict__ 
                                                       const int* __restrict__ labels,
                                                       float* __restrict__ dlogits, float* __restrict__ stats,
                                                       int B, int C, float gscale) {
-  const int lane = threadIdx.x & 63;
-  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (b >= B) return;
-  const float* r = logits + (long)b * C;
-  float mx = -INFINITY;
-  int am = 0x7fffffff;
-  for (int c = lane; c < C; c += 64) {
-    const float v = r[c];
-    if (v > mx) { mx = v; am = c; }
-  }
+  // one wave per row, grid-strided; the loss / correct / count sums go through LDS to ONE set of
+  // three atomics per workgroup (one per row contended on the same three words: 23 us at B = 512)
+  __shared__ float red[4][3];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float loss = 0.f, hit = 0.f, cnt = 0.f;
+  for (int b = blockIdx.x * 4 + w; b < B; b += gridDim.x * 4) {
+    const float* r = logits + (long)b * C;
+    float mx = -INFINITY;
+    int am = 0x7fffffff;
+    for (int c = lane; c < C; c += 64) {
+      const float v = r[c];
+      if (v > mx) { mx = v; am = c; }
+    }
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {  // arg-max, lowest index on ties
-    const float om = __shfl_xor(mx, o, 64);
-    const int oa = __shfl_xor(am, o, 64);
-    if (om > mx || (om == mx && oa < am)) { mx = om; am = oa; }
-  }
-  float s = 0.f;
-  for (int c = lane; c < C; c += 64) s += __expf(r[c] - mx);
-  s = wave_sum(s);
-  const int lab = labels[b];
-  const float inv = 1.f / s, scale = gscale / (float)B;
-  for (int c = lane; c < C; c += 64) {
-    const float pr = __expf(r[c] - mx) * inv;
-    dlogits[(long)b * C + c] = (pr - (c == lab ? 1.f : 0.f)) * scale;
-  }
-  if (lane == 0) {
+    for (int o = 32; o > 0; o >>= 1) {  // arg-max, lowest index on ties
+      const float om = __shfl_xor(mx, o, 64);
+      const int oa = __shfl_xor(am, o, 64);
+      if (om > mx || (om == mx && oa < am)) { mx = om; am = oa; }
+    }
+    float s = 0.f;
+    for (int c = lane; c < C; c += 64) s += __expf(r[c] - mx);
+    s = wave_sum(s);
+    const int lab = labels[b];
+    const float inv = 1.f / s, scale = gscale / (float)B;
+    for (int c = lane; c < C; c += 64) {
+      const float pr = __expf(r[c] - mx) * inv;
+      dlogits[(long)b * C + c] = (pr - (c == lab ? 1.f : 0.f)) * scale;
+    }
     const float pl = fminf(fmaxf(__expf(r[lab] - mx) * inv, 1e-7f), 1.f - 1e-7f);
-    atomicAdd(stats + 0, -__logf(pl));
-    atomicAdd(stats + 1, am == lab ? 1.f : 0.f);
-    atomicAdd(stats + 4, 1.f);
+    loss += -__logf(pl);
+    hit += am == lab ? 1.f : 0.f;
+    cnt += 1.f;
+  }
+  if (lane == 0) { red[w][0] = loss; red[w][1] = hit; red[w][2] = cnt; }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    const float t = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    if (t != 0.f) atomicAdd(stats + (threadIdx.x == 2 ? 4 : threadIdx.x), t);
   }
 }
 
@@ -1460,7 +1468,8 @@ int ptg_mse(const float* pred, const float* y, float* dpred, float* stats, int B
 
 int ptg_softmax_xent(const float* logits, const int* labels, float* dlogits, float* stats, int B, int C,
                      float gscale, hipStream_t s) {
-  hipLaunchKernelGGL(softmax_xent_k, dim3(ptg_ceil_div(B, 4)), dim3(256), 0, s, logits, labels, dlogits, stats, B, C,
+  const int g = ptg_ceil_div(B, 16) < 256 ? ptg_ceil_div(B, 16) : 256;  // ~4 rows per wave, <= 256 workgroups
+  hipLaunchKernelGGL(softmax_xent_k, dim3(g > 0 ? g : 1), dim3(256), 0, s, logits, labels, dlogits, stats, B, C,
                      gscale);
   PTG_RETURN_LAUNCH();
 }

@@ -127,8 +127,10 @@ class ConvOp(Op):
         self.name = conv.name
         if conv.activation not in ("linear", None, "relu"):
             raise NotImplementedError(f"Conv2D activation {conv.activation}")
-        if conv.activation == "relu" and (prelu or pool):
-            raise NotImplementedError("Conv2D(activation='relu') followed by PReLU/pool")
+        if conv.activation == "relu" and prelu:
+            raise NotImplementedError("Conv2D(activation='relu') followed by PReLU")
+        # Conv2D(activation='relu') -> MaxPooling2D fuses as PReLU with alpha 0 + pool (the MNIST
+        # convnet): the pooled output comes out of the conv epilogue, its backward is one kernel
 
     def _prep_input(self, x, ws):
         cp = self.conv.cin_p
@@ -349,9 +351,10 @@ class ConvOp(Op):
         elif self.prelu is not None:
             K.prelu_bwd(dy, z, self.prelu.alpha.data, dz, self.prelu.alpha.grad, bias_g)
         elif self.pool is not None:
-            ones = ws.get(self.name + "/ones", z.shape[1:], torch.float32, dev)
+            # identity (alpha 1) or ReLU (alpha 0: z is pre-activation on the halo path, post-ReLU on the
+            # generic one - the same mask and argmax either way)
             dummy = ws.get(self.name + "/dalpha_dummy", z.shape[1:], torch.float32, dev)
-            K.prelu_pool_bwd(dy, z, ones, dz, dummy, bias_g)
+            K.prelu_pool_bwd(dy, z, self._pool_alpha(ws, dev), dz, dummy, bias_g)
         elif self.conv.activation == "relu":
             zeros = ws.get(self.name + "/zeros", z.shape[1:], torch.float32, dev, zero=True)
             dummy = ws.get(self.name + "/dalpha_dummy", z.shape[1:], torch.float32, dev)
@@ -612,7 +615,8 @@ def lower(layers: list) -> list:
             j = i + 1
             if j < len(seq) and isinstance(seq[j], L.PReLU) and l.activation in ("linear", None):
                 prelu = seq[j]; j += 1
-            if j < len(seq) and isinstance(seq[j], L.MaxPooling2D) and l.activation in ("linear", None):
+            if j < len(seq) and isinstance(seq[j], L.MaxPooling2D) and l.activation in ("linear", None, "relu") \
+                    and tuple(seq[j].pool_size) == (2, 2) and tuple(seq[j].strides) == (2, 2):
                 pool = seq[j]; j += 1
             ops.append(ConvOp(l, prelu, pool))
             i = j

@@ -86,6 +86,24 @@ def test_mlp_lds_resident_adam_state_matches_hbm(hip_built, monkeypatch):
             assert torch.equal(a, b), (B, (a - b).abs().max().item())
 
 
+def test_mnist_cnn_tracks_reference(hip_built):
+    """The MNIST convnet (Conv(relu) -> MaxPool fused into one ConvOp: PReLU alpha 0 + pool epilogue,
+    one-kernel backward) vs the fp32 CPU reference path: losses, accuracy and parameters."""
+    from pyspark_tf_gke_amd.nn import engine as E
+
+    torch.manual_seed(0)
+    x = torch.rand(64, 28, 28, 1)
+    y = torch.randint(0, 10, (64,), dtype=torch.int32)
+    mg = build_mnist_cnn(device="cuda")
+    mc = build_mnist_cnn(device="cpu")
+    assert sum(isinstance(op, E.ConvOp) and op.pool is not None for op in mg.ops) == 2
+    lg, lc = _steps(mg, x, y, 4), _steps(mc, x, y, 4)
+    for a, b in zip(lg, lc):
+        assert abs(a["loss"] - b["loss"]) <= 0.02 * abs(b["loss"]) + 1e-3, (a, b)
+    pg, pc = mg.store.flat.cpu(), mc.store.flat
+    assert torch.allclose(pg, pc, atol=5e-3, rtol=5e-2), float((pg - pc).abs().max())
+
+
 def test_mnist_cnn_learns(hip_built):
     torch.manual_seed(0)
     m = build_mnist_cnn(device="cuda")
