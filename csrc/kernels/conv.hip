@@ -1264,14 +1264,33 @@ static int launch_wgrad(const void* x, const void* dz, float* dw, int N, int H, 
   PTG_RETURN_LAUNCH();
 }
 
+// C = 32 / 64 weight gradients at small batch (<= WG_SMALL_N samples): wider tiles (16 x 8 and 20 x 16
+// pixels instead of 8 x 8 and 4 x 16).  Every workgroup flushes its 64 x (64 * NB) partial sums with
+// one fp32 atomic each, and with few samples a workgroup owns ~one small tile, so the flush dominated:
+// CNN-B1 b32 L4 / L5 wgrad 37.2 / 37.6 -> 30.5 / 23.3 us; at b256 the small tiles stay faster
+// (82.8 / 71.8 vs 111.6 / 91.3 us, profiles/r6_ab_wgrad_tiles.txt).
+static int wg_small_n() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("PTG_WG_SMALL_N");
+    v = e && *e ? atoi(e) : 64;
+  }
+  return v;
+}
 template <int C, int KS, int MF, bool SPARSE>
 static int wgrad_by_c(const void* x, const void* dz, float* dw, int N, int H, int W, int Cout, int pad, hipStream_t s,
                       const void* argq) {
+  const bool small = N <= wg_small_n();
   if constexpr (C == 4) return launch_wgrad<C, KS, 64, 4, MF, SPARSE>(x, dz, dw, N, H, W, Cout, pad, s, argq);
   else if constexpr (C == 8) return launch_wgrad<C, KS, 32, 8, MF, SPARSE>(x, dz, dw, N, H, W, Cout, pad, s, argq);
   else if constexpr (C == 16) return launch_wgrad<C, KS, 16, 8, MF, SPARSE>(x, dz, dw, N, H, W, Cout, pad, s, argq);
-  else if constexpr (C == 32) return launch_wgrad<C, KS, 8, 8, MF, SPARSE>(x, dz, dw, N, H, W, Cout, pad, s, argq);
-  else return launch_wgrad<C, KS, 4, 16, MF, SPARSE>(x, dz, dw, N, H, W, Cout, pad, s, argq);
+  else if constexpr (C == 32) {
+    if (small) return launch_wgrad<C, KS, 16, 8, MF, SPARSE>(x, dz, dw, N, H, W, Cout, pad, s, argq);
+    return launch_wgrad<C, KS, 8, 8, MF, SPARSE>(x, dz, dw, N, H, W, Cout, pad, s, argq);
+  } else {
+    if (small) return launch_wgrad<C, KS, 20, 16, MF, SPARSE>(x, dz, dw, N, H, W, Cout, pad, s, argq);
+    return launch_wgrad<C, KS, 4, 16, MF, SPARSE>(x, dz, dw, N, H, W, Cout, pad, s, argq);
+  }
 }
 
 template <int KS, int MF, bool SPARSE = false>
