@@ -319,7 +319,26 @@ def main():
                 _cfg._cli.pop("sim_world", None)
         if args.workload == "cnn_b1" and args.groupby_extra and torch.cuda.is_available():
             # second half of BASELINE.json's metric ("rows/sec Spark groupBy + samples/sec TF CNN
-            # train"); timed separately, after the CNN steps, so it cannot perturb them
+            # train"); timed separately, after the CNN steps, so it cannot perturb them.  With N > 1
+            # ranks the shuffle's collectives run here for the first time in the job: a watchdog
+            # prints the headline line without the groupBy extra and ends the process if they hang
+            # (PTG_BENCH_EXTRA_TIMEOUT seconds), so a stuck extra can never take the CNN number down.
+            watchdog = None
+            if world > 1:
+                import threading
+
+                done = threading.Event()
+
+                def _expire(limit=float(os.environ.get("PTG_BENCH_EXTRA_TIMEOUT", "240"))):
+                    if done.wait(limit):
+                        return
+                    extra["groupby"] = {"error": f"multi-rank groupBy extra did not finish in {limit:.0f} s"}
+                    if rank == 0:
+                        print(json.dumps(_bench_line(res, extra, world, args, dtype, data)), flush=True)
+                    os._exit(0)
+
+                watchdog = threading.Thread(target=_expire, daemon=True)
+                watchdog.start()
             try:
                 import gc
 
@@ -347,6 +366,16 @@ def main():
                                            "groups_check": gs["config"]["groups_check"], "dtype": "fp64"}
             except Exception as e:  # noqa: BLE001 - never lose the headline line
                 extra["groupby"] = {"error": repr(e)[:300]}
+            if watchdog is not None:
+                done.set()
+    out = _bench_line(res, extra, world, args, dtype, data)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    comm.destroy()
+    return 0
+
+
+def _bench_line(res, extra, world, args, dtype, data) -> dict:
     out = {"metric": res["metric"], "value": res["value"], "unit": res["unit"], "n_gpus": world,
            "steps": args.steps, "warmup": args.warmup, "ms_per_step": res["ms_per_step"],
            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": dtype, "data": data,
@@ -354,11 +383,8 @@ def main():
     if "comm" in res:
         out["comm"] = res["comm"]
     if extra:
-        out["extra"] = extra
-    if rank == 0:
-        print(json.dumps(out), flush=True)
-    comm.destroy()
-    return 0
+        out["extra"] = dict(extra)
+    return out
 
 
 if __name__ == "__main__":
