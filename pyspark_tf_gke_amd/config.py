@@ -69,6 +69,8 @@ _K = [
     Knob("fused_head", bool, True, "PTG_FUSED_HEAD", None, "CNN-B1 Dense(relu)->Dense->MSE head as two kernels"),
     Knob("device_feed", bool, True, "PTG_DEVICE_FEED", None, "fit(): pinned ring + side-stream H2D for host datasets"),
     Knob("side_stream", bool, True, "PTG_SIDE_STREAM", None, "weight gradients on a side HIP stream (1 replica)"),
+    Knob("adam_stream", bool, True, "PTG_ADAM_STREAM", None,
+         "the big Dense dW+Adam on a second side stream (the conv weight gradients do not queue behind it)"),
     Knob("sort_value_payload", bool, True, "PTG_SORT_VALUE_PAYLOAD", None,
          "orderBy of a (key, one 8-byte column) table carries the column through the radix passes"),
     Knob("sort_fused_keys", bool, True, "PTG_SORT_FUSED_KEYS", None,

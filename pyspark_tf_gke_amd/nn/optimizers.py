@@ -158,7 +158,7 @@ class FusedAdamStep:
         fn = lambda: K.linear_dw_adam(dz, x, st.flat[o:o + n].view(shp), opt.m[o:o + n].view(shp),  # noqa: E731
                                       opt.v[o:o + n].view(shp), st.flat_bf16[o:o + n].view(shp), lr_t,
                                       opt.beta_1, opt.beta_2, opt.epsilon, 1.0, lr_dev=self.lr_dev)
-        S.launch(fn, dz.device)
+        S.launch(fn, dz.device, aux=True)
         self.done.append((o, o + n))
 
 

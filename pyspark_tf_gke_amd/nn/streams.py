@@ -70,11 +70,12 @@ def _wait(waiter, producer, used: list) -> None:
         waiter.wait_stream(producer)
 
 
-def _stream(dev) -> "torch.cuda.Stream":
+def _stream(dev, k: int = 0) -> "torch.cuda.Stream":
+    """Side stream ``k`` of ``dev`` (0: weight gradients; 1: the big Dense dW+Adam, see launch())."""
     dev = torch.device(dev)
-    s = _STREAMS.get(dev)
+    s = _STREAMS.get((dev, k))
     if s is None:
-        s = _STREAMS[dev] = torch.cuda.Stream(device=dev)
+        s = _STREAMS[(dev, k)] = torch.cuda.Stream(device=dev)
     return s
 
 
@@ -132,12 +133,19 @@ def current() -> SideStream | None:
     return _CUR[0]
 
 
-def launch(fn, dev):
+# PTG_ADAM_STREAM: the big Dense dW+Adam GEMM forks onto a second side stream.  On the shared side
+# stream it ran first (the largest side kernel, ~0.25-0.36 ms) and every conv weight gradient queued
+# behind it, so the last one (layer 2) still ran after the main stream's backward had finished.
+ADAM_STREAM = config.get("adam_stream")
+
+
+def launch(fn, dev, aux: bool = False):
     """Weight-gradient (or gradient-collective) launch: forked onto the side stream when a step has
-    one, else inline.  Returns ``fn()``'s result (e.g. an async collective's handle)."""
+    one, else inline.  ``aux``: the second side stream (PTG_ADAM_STREAM).  Returns ``fn()``'s result
+    (e.g. an async collective's handle)."""
     side = _CUR[0]
     if side is not None and torch.device(dev).type == "cuda":
-        return side.fork(fn, dev)
+        return side.fork(fn, dev, stream=_stream(dev, 1) if aux and ADAM_STREAM else None)
     return fn()
 
 
