@@ -96,9 +96,10 @@ _K = [
          "1.657/1.650 ms; on layer 3 as well: 1.80 ms)"),
     Knob("conv32_min_ch", int, 32, "PTG_CONV32_MINCH", None,
          "conv32 only where min(C, Cout) >= this (layer bench: it wins on CNN-B1 layers 4-5, loses the 32->16 dgrad)"),
-    Knob("conv32_min_wg", int, 128, "PTG_CONV32_MINWG", None,
+    Knob("conv32_min_wg", int, 64, "PTG_CONV32_MINWG", None,
          "conv32 only when its grid (N x H / rows-per-tile workgroups) has at least this many workgroups "
-         "(128 since the LDS-staged taps: CNN-B1 b32 0.646/0.638 vs 0.655/0.655 ms at 256)"),
+         "(64 since the 160-px small-grid tiles: CNN-B1 b64 0.7057/0.7058 vs 0.7214/0.7106 ms at 128, which "
+         "keeps layer 5 on the strip kernel; b32 at 0 loses, 0.562/0.559 vs 0.556/0.554 ms)"),
     Knob("conv1_rec", bool, True, "PTG_CONV1_REC", None, "first conv layer (conv1.hip): forward keeps the pool record, backward needs no recompute (0: recompute z in the backward)"),
     Knob("conv1_fused", bool, True, "PTG_CONV1_FUSED", None, "first conv layer: pooled-only forward + one recomputing backward kernel (conv1.hip)"),
     Knob("dense_fwd_splits", int, 0, "PTG_DENSE_FWD_SPLITS", None,
