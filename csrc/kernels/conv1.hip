@@ -739,10 +739,35 @@ PTG_DEV void conv_tile_r(const bf16_t* hb, const int* boff, const bf16x8_t* wreg
 // sample): goff = byte offset of the pixel pair inside one image (~0u: padding), loff = LDS element
 // offset (~0u: slot past the halo).
 template <bool U8>
+struct HaloSlot {  // one sample's halo in registers (a prefetch ring entry)
+  U4 pf[U8 ? 1 : WPF];
+  U8Pair pu[U8 ? WPF : 1];
+};
+template <bool U8>
 struct WaveHaloR {
   uint32_t goff[WPF], loff[WPF];
   U4 pf[U8 ? 1 : WPF];
   U8Pair pu[U8 ? WPF : 1];
+  PTG_DEV void load_to(HaloSlot<U8>& s, const Rsrc& xr, uint32_t img_bytes, int n) const {
+    const uint32_t base = (uint32_t)n * img_bytes;
+#pragma unroll
+    for (int p = 0; p < WPF; ++p) {
+      const bool ok = goff[p] != ~0u;
+      if constexpr (U8) s.pu[p] = u8pair_load(xr, base + goff[p], ok);
+      else s.pf[p] = bload16(xr, ok ? base + goff[p] : PTG_OOB);
+    }
+  }
+  PTG_DEV void store_from(const HaloSlot<U8>& s, bf16_t* buf) const {
+#pragma unroll
+    for (int p = 0; p < WPF; ++p) {
+      if (loff[p] != ~0u) {
+        U4 v;
+        if constexpr (U8) v = u8pair_to_bf16x8_int(s.pu[p]);
+        else v = s.pf[p];
+        *(U4*)(buf + loff[p]) = v;
+      }
+    }
+  }
   PTG_DEV void init(int H, int W, int ih0, int iw0, int lane) {
 #pragma unroll
     for (int p = 0; p < WPF; ++p) {
@@ -775,8 +800,22 @@ struct WaveHaloR {
   }
 };
 
-template <bool U8>
-__global__ __launch_bounds__(256) void conv1_fwd_rec_k(const void* __restrict__ x, const bf16_t* __restrict__ w,
+// lanes 0-31: the value of lane + 32 (v_permlane32_swap, one VALU op instead of an LDS-routed
+// ds_bpermute per __shfl_xor(v, 32)); lanes 32-63 keep their own value
+PTG_DEV float hi_half(float v) {
+  return __uint_as_float(__builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false)[1]);
+}
+// v_permlane32_swap(a, b): lanes 32-63 of a trade places with lanes 0-31 of b, so
+//   lo = lanes < 32: own a,           lanes >= 32: b of lane - 32
+//   hi = lanes < 32: a of lane + 32,  lanes >= 32: own b
+PTG_DEV void swap32(float a, float b, float& lo, float& hi) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  lo = __uint_as_float(r[0]);
+  hi = __uint_as_float(r[1]);
+}
+
+template <bool U8, int PD>
+__global__ __launch_bounds__(256, PD == 1 ? 5 : 4) void conv1_fwd_rec_k(const void* __restrict__ x, const bf16_t* __restrict__ w,
                                                        const float* __restrict__ bias, const float* __restrict__ alpha,
                                                        bf16_t* __restrict__ pooled, bf16_t* __restrict__ zsel,
                                                        uint8_t* __restrict__ argq, int N, int H, int W, int tiles_h,
@@ -806,57 +845,80 @@ __global__ __launch_bounds__(256) void conv1_fwd_rec_k(const void* __restrict__ 
   }
   const int PH = H >> 1, PW = W >> 1;
   const int ph = (it.oh0 >> 1) + rp, pw = (it.ow0 >> 1) + hf * 16 + px;
-  const bool store_lane = g < 2 && ph < PH && pw < PW;
-  const long pstep = (long)PH * PW * COUT, pbase = ((long)ph * PW + pw) * COUT + cc;
+  const bool store_lane = ph < PH && pw < PW;
+  // the lane's 2 pooled channels after the window exchange: 4 * (g & 1) + 2 * (g >> 1) + {0, 1}
+  const long pstep = (long)PH * PW * COUT, pbase = ((long)ph * PW + pw) * COUT + cc + 2 * (g >> 1);
   const Rsrc xr = x_rsrc<U8>(x, N, H, W);
   const uint32_t img_bytes = (uint32_t)(H * W) * (U8 ? 3u : 8u);
   int boff[KSTEPS];
   conv_boffs(px, g, boff);
   WaveHaloR<U8> hl;
   hl.init(H, W, it.oh0 + 2 * rp - PAD, it.ow0 + hf * WTW - PAD, lane);
-  hl.load(xr, img_bytes, it.n0);
-  hl.store(wr);
+  // register prefetch ring: sample s lives in ring[(s - n0) % PD] from its load until it is copied
+  // to the LDS double buffer, so PD samples' halos are in flight while one computes (the step is
+  // bound by loads in flight per CU, not by the MFMAs: 4 waves x 864 B per SIMD at PD = 1)
+  HaloSlot<U8> ring[PD];
+#pragma unroll
+  for (int u = 0; u < PD; ++u)
+    if (it.n0 + u < it.n1) hl.load_to(ring[u], xr, img_bytes, it.n0 + u);
+  hl.store_from(ring[0], wr);
   wave_lds_sync();
-  for (int n = it.n0; n < it.n1; ++n) {
+  if (it.n0 + PD < it.n1) hl.load_to(ring[0], xr, img_bytes, it.n0 + PD);
+  for (int nb = it.n0; nb < it.n1; nb += PD)
+#pragma unroll
+  for (int u = 0; u < PD; ++u) {
+    const int n = nb + u;
+    if (n >= it.n1) break;
     const int b = (n - it.n0) & 1;
     const bool has_next = n + 1 < it.n1;
-    if (has_next) hl.load(xr, img_bytes, n + 1);
     f32x4_t acc[2];
     conv_tile_r(wr + b * WHB, boff, wreg, acc);
-    float pm[4], zs[4];
+    float zv[2][4], yv[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        zv[i][r] = bf2f(f2bf(fmaf(acc[i][r], XS, bv[r])));
+        yv[i][r] = zv[i][r] > 0.f ? zv[i][r] : al[i][r] * zv[i][r];
+      }
+    // 2x2 windows: lane l < 32 holds the dw = 0 pixel, lane l + 32 the dw = 1 pixel of the same
+    // pooled column, 4 channels each.  One v_permlane32_swap per (r, r + 2) pair leaves every lane
+    // with BOTH columns of 2 channels - lanes < 32 channels r = 0, 1, lanes >= 32 channels 2, 3 - in
+    // (dw 0, dw 1) order, so all 64 lanes pool 2 windows (no half-wave of discarded pool math)
+    float pm[2], zs[2];
     uint32_t qs = 0;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float y[2], zr[2];
+    for (int k = 0; k < 2; ++k) {
+      float y0[2], y1[2], z0[2], z1[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        zr[i] = bf2f(f2bf(fmaf(acc[i][r], XS, bv[r])));
-        y[i] = zr[i] > 0.f ? zr[i] : al[i][r] * zr[i];
+        swap32(yv[i][k], yv[i][k + 2], y0[i], y1[i]);
+        swap32(zv[i][k], zv[i][k + 2], z0[i], z1[i]);
       }
-      // window (dh, dw) in q = 2*dh + dw order: only the dw = 0 lanes (g < 2) store, so the window is
-      // assembled in their order (own pixel = dw 0, lane ^ 32 = dw 1); the dw = 1 lanes' result is unused
-      const float py0 = __shfl_xor(y[0], 32, 64), py1 = __shfl_xor(y[1], 32, 64);
-      const float pz0 = __shfl_xor(zr[0], 32, 64), pz1 = __shfl_xor(zr[1], 32, 64);
-      const float yq[4] = {y[0], py0, y[1], py1};
-      const float zq[4] = {zr[0], pz0, zr[1], pz1};
+      const float yq[4] = {y0[0], y1[0], y0[1], y1[1]};  // q = 2*dh + dw
+      const float zq[4] = {z0[0], z1[0], z0[1], z1[1]};
       float bm = yq[0], bz = zq[0];
       uint32_t a = 0;
 #pragma unroll
       for (int q = 1; q < 4; ++q)
         if (yq[q] > bm) { bm = yq[q]; bz = zq[q]; a = q; }  // first maximum in q order
-      pm[r] = bm;
-      zs[r] = bz;
-      qs |= a << (8 * r);
+      pm[k] = bm;
+      zs[k] = bz;
+      qs |= a << (8 * k);
+    }
+    // the next halo goes to LDS BEFORE this sample's global stores: vmcnt counts loads and stores
+    // in issue order, so waiting for the prefetch behind (conditional) stores waited for their
+    // write acknowledgements too (s_waitcnt vmcnt(0) each sample)
+    if (has_next) {
+      hl.store_from(ring[(u + 1) % PD], wr + (b ^ 1) * WHB);
+      wave_lds_sync();
+      if (n + 1 + PD < it.n1) hl.load_to(ring[(u + 1) % PD], xr, img_bytes, n + 1 + PD);
     }
     if (store_lane) {
       const long po = (long)n * pstep + pbase;
-      *(U2*)(pooled + po) = U2{pack_bf(pm[0], pm[1]), pack_bf(pm[2], pm[3])};
-      *(U2*)(zsel + po) = U2{pack_bf(zs[0], zs[1]), pack_bf(zs[2], zs[3])};
-      *(uint32_t*)(argq + po) = qs;
-    }
-    if (has_next) {
-      hl.store(wr + (b ^ 1) * WHB);
-      wave_lds_sync();
+      *(uint32_t*)(pooled + po) = pack_bf(pm[0], pm[1]);
+      *(uint32_t*)(zsel + po) = pack_bf(zs[0], zs[1]);
+      *(uint16_t*)(argq + po) = (uint16_t)qs;
     }
   }
 }
@@ -1040,6 +1102,19 @@ static bool conv1_wave() {
   return on;
 }
 
+// samples in flight per wave in the record forward (PTG_CONV1_PD = 1 or 2).  Measured at b256
+// (rocprof, kernel us in the step): PD 1 148.5, 2 146.7, 3 167.6, 4 167.6 - the extra ring registers
+// cost occupancy (3 waves per SIMD at PD >= 3) and the kernel is issue-bound, not load-latency-bound,
+// so PD 1 at 5 waves per SIMD (launch bounds) is the default.
+static int conv1_pd() {
+  static const int pd = [] {
+    const char* e = getenv("PTG_CONV1_PD");
+    const int v = e ? atoi(e) : 1;
+    return v < 1 ? 1 : v > 2 ? 2 : v;
+  }();
+  return pd;
+}
+
 static int conv1_chunks(int N, long npos, const void* kern, const char* env) {
   long slots = ptg_resident_blocks(kern);
   if (const char* e = getenv(env)) {
@@ -1107,7 +1182,9 @@ int ptg_conv1_fwd_rec(const void* x, int u8, const void* w, const float* bias, c
       !ptg_fits_2g((long)N * H * W * 4))
     return (int)hipErrorInvalidValue;
   const int th = (H + TH - 1) / TH, tw = (W + TW - 1) / TW;
-  const auto kern = u8 ? conv1_fwd_rec_k<true> : conv1_fwd_rec_k<false>;
+  const int pd = conv1_pd();
+  const auto kern = pd >= 2 ? (u8 ? conv1_fwd_rec_k<true, 2> : conv1_fwd_rec_k<false, 2>)
+                            : (u8 ? conv1_fwd_rec_k<true, 1> : conv1_fwd_rec_k<false, 1>);
   const int nch = conv1_chunks(N, (long)th * tw, (const void*)kern, "PTG_CONV1_FWD_PER_CU");
   const long items = (long)th * tw * nch;
   if (items > 0x7fffffff) return (int)hipErrorInvalidValue;

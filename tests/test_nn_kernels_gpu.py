@@ -360,10 +360,12 @@ def test_conv1_fused_matches_sparse_record_pipeline(N, H, W, u8):
 
 
 @pytest.mark.parametrize("N,H,W,u8", [(3, 12, 140, True), (2, 14, 64, False), (5, 20, 70, False),
-                                      (7, 256, 320, True)])
+                                      (7, 256, 320, True), (24, 256, 320, True)])
 def test_conv1_record_kernels_vs_reference(N, H, W, u8):
     """conv1.hip record pipeline: the forward's pooled output / z at the argmax / argmax vs the fp32
-    reference, and the backward from the GPU's own record vs the reference backward of that record."""
+    reference, and the backward from the GPU's own record vs the reference backward of that record.
+    N = 24 gives every work item several samples, so the forward's prefetch ring (PTG_CONV1_PD deep)
+    wraps and ends mid-ring."""
     x, w, b, alpha, dp = _conv1_inputs(N, H, W, u8)
     shp = (N, H // 2, W // 2, 8)
     p = torch.empty(shp, dtype=torch.bfloat16, device=DEV)
