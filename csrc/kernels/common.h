@@ -89,6 +89,12 @@ PTG_DEV U2 bload8(Rsrc r, uint32_t off) {
   return __builtin_bit_cast(U2, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
 }
 PTG_DEV uint32_t bload4(Rsrc r, uint32_t off) { return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0); }
+// vector buffer stores (offsets >= the descriptor's byte count are dropped by the range check)
+typedef __attribute__((ext_vector_type(2))) unsigned int ptg_vu2_t;
+PTG_DEV void bstore8(Rsrc r, uint32_t off, U2 v) {
+  __builtin_amdgcn_raw_buffer_store_b64(ptg_vu2_t{v.x, v.y}, r, off, 0, 0);
+}
+PTG_DEV void bstore4(Rsrc r, uint32_t off, uint32_t v) { __builtin_amdgcn_raw_buffer_store_b32(v, r, off, 0, 0); }
 static inline bool ptg_fits_2g(long bytes) { return bytes > 0 && bytes < (long)PTG_OOB; }
 
 static inline int ptg_ceil_div(long a, long b) { return (int)((a + b - 1) / b); }

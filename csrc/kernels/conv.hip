@@ -288,6 +288,23 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
     }
   }
 
+  // tile-invariant parts of each fragment's output offsets (elements): full-resolution planes (lf)
+  // and, for the pool-window leaders (even row and column), the pooled planes (lp; others ~0u)
+  uint32_t lf[FM], lp[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    lf[i] = (uint32_t)(f_r[i] * W + f_c[i]) * (uint32_t)Cout + (uint32_t)(cb + g * 4);
+    const bool lead = ((f_r[i] | f_c[i]) & 1) == 0;
+    lp[i] = lead ? (uint32_t)((f_r[i] >> 1) * (W >> 1) + (f_c[i] >> 1)) * (uint32_t)Cout + (uint32_t)(cb + g * 4) : ~0u;
+  }
+  // pooled-plane element offset of fragment i's window for co fragment j, or PTG_OOB / 2 (dropped)
+  // when the lane does not lead a window or the window / channel is outside the output
+  auto pool_off = [&](int i, int j, bool cval, uint32_t tpool, uint32_t ppl, int oh0_, int ow0_) -> uint32_t {
+    const int ph = (oh0_ + f_r[i]) >> 1, pw = (ow0_ + f_c[i]) >> 1;
+    const bool ok = cval && lp[i] != ~0u && ph < (H >> 1) && pw < (W >> 1);
+    return ok ? (uint32_t)PTG_CHECKED_IDX(tpool + lp[i] + j * 16, (long)ppl) : PTG_OOB / 2;
+  };
+
   // Tile ranges, strip-major: static (this workgroup's contiguous 1/nblk of the tiles) or, with a
   // work queue `wq`, chunks of `wchunk` tiles claimed until none is left - a workgroup that starts
   // late (CUs held by a concurrent RCCL kernel) then takes less work instead of a full range.
@@ -471,10 +488,23 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
     if (has_next) store_rows(nrows2, slot2);
 
     // ---- epilogue from registers ----
+    // Stores go through per-tile buffer descriptors over sample n's output planes: the 64-bit plane
+    // base is uniform (scalar math once per tile) and each lane adds a 32-bit offset = the tile's
+    // uniform offset + its precomputed fragment offset (lf / lp), instead of 64-bit per-fragment
+    // index arithmetic (v_mul_lo_u32 / v_mad_u64_u32: ~100 VALU ops of a ~360-op tile on layer 2).
+    // Lanes outside the image / channel range or not leading a pool window store at PTG_OOB, which
+    // the descriptor's range check drops - no exec-mask branches.
+    const uint32_t zpl = (uint32_t)(EPI == EPI_POOLS ? PH * PW : H * W) * (uint32_t)Cout;  // elements
+    const uint32_t ppl = (uint32_t)(PH * PW) * (uint32_t)Cout;
+    const Rsrc rz = make_rsrc(z + (long)n * zpl, zpl * 2u);
+    const Rsrc ra = make_rsrc(aux + (long)n * (EPI == EPI_PRELU ? zpl : ppl), (EPI == EPI_PRELU ? zpl : ppl) * 2u);
+    const uint32_t tfull = (uint32_t)(oh0 * W + ow0) * (uint32_t)Cout;
+    const uint32_t tpool = (uint32_t)((oh0 >> 1) * PW + (ow0 >> 1)) * (uint32_t)Cout;
     if constexpr (EPI == EPI_POOLS) {
       // sparse pool record, one vertical fragment pair (WIDE) / one fragment at a time to keep the
       // live register set small; the first maximum in q order (0,1,2,3) wins, as in the dense
       // backward
+      const Rsrc rq = make_rsrc(argout + (long)n * ppl, ppl);
       constexpr int STEP = WIDE ? 2 : 1;
 #pragma unroll
       for (int j = 0; j < NF; ++j) {
@@ -512,16 +542,10 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
             pz[r] = down ? zb : zz[0][r];
             pq[r] = down ? qb + 2.f : qq[0][r];
           }
-          const int rr = f_r[i], cc = f_c[i];
-          const bool lead = ((cc & 1) == 0) && ((rr & 1) == 0);
-          const int ph = (oh0 + rr) >> 1, pw = (ow0 + cc) >> 1;
-          if (cval && lead && ph < PH && pw < PW) {
-            const long po = PTG_CHECKED_IDX((((long)n * PH + ph) * PW + pw) * Cout + co0, (long)N * PH * PW * Cout);
-            *(U2*)(aux + po) = U2{pack_bf(pm[0], pm[1]), pack_bf(pm[2], pm[3])};
-            *(U2*)(z + po) = U2{pack_bf(pz[0], pz[1]), pack_bf(pz[2], pz[3])};
-            *(uint32_t*)(argout + po) = (uint32_t)pq[0] | ((uint32_t)pq[1] << 8) | ((uint32_t)pq[2] << 16) |
-                                        ((uint32_t)pq[3] << 24);
-          }
+          const uint32_t po = pool_off(i, j, cval, tpool, ppl, oh0, ow0);
+          bstore8(ra, 2u * po, U2{pack_bf(pm[0], pm[1]), pack_bf(pm[2], pm[3])});
+          bstore8(rz, 2u * po, U2{pack_bf(pz[0], pz[1]), pack_bf(pz[2], pz[3])});
+          bstore4(rq, po, (uint32_t)pq[0] | ((uint32_t)pq[1] << 8) | ((uint32_t)pq[2] << 16) | ((uint32_t)pq[3] << 24));
         }
       }
     } else
@@ -532,20 +556,17 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
       float y[FM][4];
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
-        const int oh = oh0 + f_r[i], ow = ow0 + f_c[i];
         float zr[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) zr[r] = bf2f(f2bf(res[i][j][r] + bv[j][r]));
-        const bool in = cval && oh < H && ow < W;
-        const long o = (((long)n * H + oh) * W + ow) * Cout + co0;
-        if (in) *(U2*)(z + PTG_CHECKED_IDX(o, (long)N * H * W * Cout)) = U2{pack_bf(zr[0], zr[1]), pack_bf(zr[2], zr[3])};
+        const bool in = cval && oh0 + f_r[i] < H && ow0 + f_c[i] < W;
+        const uint32_t o = in ? (uint32_t)PTG_CHECKED_IDX(tfull + lf[i] + j * 16, (long)zpl) : PTG_OOB / 2;
+        bstore8(rz, 2u * o, U2{pack_bf(zr[0], zr[1]), pack_bf(zr[2], zr[3])});
         if constexpr (EPI != EPI_Z) {
           const float a4[4] = {al[i][j].x, al[i][j].y, al[i][j].z, al[i][j].w};
 #pragma unroll
           for (int r = 0; r < 4; ++r) y[i][r] = zr[r] > 0.f ? zr[r] : a4[r] * zr[r];
-          if constexpr (EPI == EPI_PRELU) {
-            if (in) *(U2*)(aux + o) = U2{pack_bf(y[i][0], y[i][1]), pack_bf(y[i][2], y[i][3])};
-          }
+          if constexpr (EPI == EPI_PRELU) bstore8(ra, 2u * o, U2{pack_bf(y[i][0], y[i][1]), pack_bf(y[i][2], y[i][3])});
         }
       }
       if constexpr (EPI == EPI_POOL) {
@@ -562,12 +583,7 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
             if constexpr (WIDE) pm[r] = fmaxf(y[i][r], y[i + 1][r]);
             else pm[r] = fmaxf(y[i][r], row_shl<(WIDE ? 1 : TW)>(y[i][r]));
           }
-          const int rr = f_r[i], cc = f_c[i];
-          const bool lead = ((cc & 1) == 0) && ((rr & 1) == 0);
-          const int ph = (oh0 + rr) >> 1, pw = (ow0 + cc) >> 1;
-          if (cval && lead && ph < PH && pw < PW)
-            *(U2*)(aux + PTG_CHECKED_IDX((((long)n * PH + ph) * PW + pw) * Cout + co0, (long)N * PH * PW * Cout)) =
-                U2{pack_bf(pm[0], pm[1]), pack_bf(pm[2], pm[3])};
+          bstore8(ra, 2u * pool_off(i, j, cval, tpool, ppl, oh0, ow0), U2{pack_bf(pm[0], pm[1]), pack_bf(pm[2], pm[3])});
         }
       }
     }
