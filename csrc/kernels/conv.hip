@@ -288,6 +288,19 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
     }
   }
 
+  // KUNROLL: the K loop fully unrolled with each lane's halo offset per k-step precomputed here
+  // (tile-invariant; -1: k group past KTOT).  Rolled, every k-step spent ~14 VALU ops on the
+  // (kh, kw, ci) division and waited for its LDS read right before its MFMA.
+  constexpr bool KUNROLL = !WREG && !KSPLIT && KSTEPS <= 16;
+  int koffs[KUNROLL ? KSTEPS : 1];
+  if constexpr (KUNROLL) {
+#pragma unroll
+    for (int ks = 0; ks < KSTEPS; ++ks) {
+      const int kf = ks * 32 + 8 * g;
+      const int kh = kf / KROW, rem = kf - kh * KROW, kw = rem / C, ci = rem - kw * C;
+      koffs[ks] = kf < KTOT ? kh * ROWE + kw * PIX + ci : -1;
+    }
+  }
   // tile-invariant parts of each fragment's output offsets (elements): full-resolution planes (lf)
   // and, for the pool-window leaders (even row and column), the pooled planes (lp; others ~0u)
   uint32_t lf[FM], lp[FM];
@@ -412,7 +425,7 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
 #pragma unroll
       for (int j = 0; j < NF; ++j) wnext[j] = load_w(ks_begin, j);
     }
-#pragma unroll(WREG ? KSTEPS : 1)
+#pragma unroll((WREG || KUNROLL) ? KSTEPS : 1)
     for (int ks = ks_begin; ks < KSTEPS; ks += KSTEP) {
       bf16x8_t wf[NF];
       if constexpr (WREG) {
@@ -426,11 +439,18 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
           for (int j = 0; j < NF; ++j) wnext[j] = load_w(ks + KSTEP, j);
         }
       }
-      const int kf = ks * 32 + 8 * g;
-      const bool kval = kf < KTOT;
-      const int kh = kf / KROW, rem = kf - kh * KROW;
-      const int kw = rem / C, ci = rem - kw * C;
-      const int koff = kh * ROWE + kw * PIX + ci;
+      int koff;
+      bool kval;
+      if constexpr (KUNROLL) {
+        koff = koffs[KUNROLL ? ks : 0];
+        kval = koff >= 0;
+      } else {
+        const int kf = ks * 32 + 8 * g;
+        kval = kf < KTOT;
+        const int kh = kf / KROW, rem = kf - kh * KROW;
+        const int kw = rem / C, ci = rem - kw * C;
+        koff = kh * ROWE + kw * PIX + ci;
+      }
 #pragma unroll
       for (int i = 0; i < AF; ++i) {
         bf16x8_t xf;
