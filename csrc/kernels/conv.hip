@@ -291,7 +291,7 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
   // KUNROLL: the K loop fully unrolled with each lane's halo offset per k-step precomputed here
   // (tile-invariant; -1: k group past KTOT).  Rolled, every k-step spent ~14 VALU ops on the
   // (kh, kw, ci) division and waited for its LDS read right before its MFMA.
-  constexpr bool KUNROLL = !WREG && !KSPLIT && KSTEPS <= 16;
+  constexpr bool KUNROLL = !WREG && !KSPLIT && KSTEPS <= 32;
   int koffs[KUNROLL ? KSTEPS : 1];
   if constexpr (KUNROLL) {
 #pragma unroll
