@@ -126,11 +126,33 @@ PTG_DEV float row_shl(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), 0x100 | NSH, 0xF, 0xF, false));
 }
 
+// 8 bf16 channels of a sparse pool record, kept where their argmax byte (a) equals the pixel's window
+// position q, zero elsewhere: x ^ (q * 0x01010101) has a zero byte exactly at the matching channels
+PTG_DEV vu4_t sparse_select(vu4_t v, U2 a, uint32_t q) {
+  const uint32_t rep = q * 0x01010101u, x0 = a.x ^ rep, x1 = a.y ^ rep;
+  auto m = [](uint32_t x, int sh) -> uint32_t {
+    return (((x >> sh) & 0xffu) == 0u ? 0x0000ffffu : 0u) | (((x >> (sh + 8)) & 0xffu) == 0u ? 0xffff0000u : 0u);
+  };
+  vu4_t o;
+  o.x = v.x & m(x0, 0);
+  o.y = v.y & m(x0, 16);
+  o.z = v.z & m(x1, 0);
+  o.w = v.w & m(x1, 16);
+  return o;
+}
+PTG_DEV vu2_t sparse_select(vu2_t v, U2, uint32_t) { return v; }  // (C == 4: never instantiated with SPIN)
+
 // WLDS: the block's weight slice [NF*16 co][KSTEPS*32 k] is staged in LDS once (persistent
 // workgroup) and every A fragment is an LDS read instead of a per-wave global load per k-step
 // (for C >= 16 those loads were L2-latency bound).  COS > 1 splits Cout over COS workgroup groups
 // (blockIdx % COS), each holding NF*16 channels, when the whole filter does not fit LDS.
-template <int C, int KS, int NF, int TW, int TH, int EPI, bool RING, bool KSPLIT, bool WLDS = false, int COS = 1>
+// SPIN (data gradients of a pooled layer, EPI_Z only): the input is the layer's sparse dZ record -
+// x = dzsel [N][H/2][W/2][C] (dZ at each 2x2 window's argmax) and argout = argq (the argmax q = 2*dh
+// + dw per channel, same shape) - and the halo loader expands it: halo pixel (ih, iw) keeps channel
+// c of its window's dzsel where argq == 2*(ih & 1) + (iw & 1), zero elsewhere.  The full-resolution
+// dZ is never written or read (4x fewer bytes than the dense dZ, plus the argq byte).
+template <int C, int KS, int NF, int TW, int TH, int EPI, bool RING, bool KSPLIT, bool WLDS = false, int COS = 1,
+          bool SPIN = false>
 __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
                                                         const float* __restrict__ bias, const float* __restrict__ alpha,
                                                         bf16_t* __restrict__ z, bf16_t* __restrict__ aux,
@@ -166,6 +188,7 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
   constexpr int WP = KSTEPS * 32 + 8;                  // LDS weight row pitch: odd multiple of 16 B
   constexpr int WL_ELEMS = WLDS ? NF * 16 * WP : 8;
   static_assert(!WLDS || (C >= 8 && !KSPLIT), "WLDS: contiguous filter rows, no k-split");
+  static_assert(!SPIN || (EPI == EPI_Z && C >= 8), "sparse-record input: data gradient (EPI_Z), 8-channel vectors");
   __shared__ __attribute__((aligned(16))) bf16_t smem[HALO_ELEMS + 8];
   __shared__ __attribute__((aligned(16))) float4 sred[RED_F4];
   __shared__ __attribute__((aligned(16))) bf16_t wlds[WL_ELEMS];
@@ -239,15 +262,32 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
     pr_l[p] = pr_c[p] * PIX + vv * VE;   // LDS offset inside a halo row
   }
   VT pf[PFN];
+  U2 pa[SPIN ? PFN : 1];        // SPIN: the argq bytes of each slot's 8 channels
+  uint32_t pq[SPIN ? PFN : 1];  // SPIN: the slot pixel's window position q
   // halo loads: buffer loads, the zero padding / rows past the image come back as 0 (PTG_OOB)
-  const Rsrc xr = make_rsrc(x, (uint32_t)((long)N * H * W * C * 2));
+  const int SPH = H >> 1, SPW = W >> 1;
+  const Rsrc xr = make_rsrc(x, SPIN ? (uint32_t)((long)N * SPH * SPW * C * 2) : (uint32_t)((long)N * H * W * C * 2));
+  const Rsrc ar = make_rsrc(argout, SPIN ? (uint32_t)((long)N * SPH * SPW * C) : 0u);
   auto load_rows = [&](int n, int iw0, int ih_first, int nrows) {
-    const uint32_t img = (uint32_t)(n * H * W * C) * 2u;
+    if constexpr (SPIN) {
+      const uint32_t img = (uint32_t)(n * SPH * SPW * C);
 #pragma unroll
-    for (int p = 0; p < PFN; ++p) {
-      const int ih = ih_first + pr_r[p], iw = iw0 + pr_c[p];
-      const bool ok = pr_r[p] < nrows && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
-      pf[p] = bload_vt<VT>(xr, ok ? img + (uint32_t)((ih * W + iw) * C + (pr_l[p] - pr_c[p] * PIX)) * 2u : PTG_OOB);
+      for (int p = 0; p < PFN; ++p) {
+        const int ih = ih_first + pr_r[p], iw = iw0 + pr_c[p];
+        const bool ok = pr_r[p] < nrows && (unsigned)ih < (unsigned)(2 * SPH) && (unsigned)iw < (unsigned)(2 * SPW);
+        const uint32_t e = img + (uint32_t)(((ih >> 1) * SPW + (iw >> 1)) * C + (pr_l[p] - pr_c[p] * PIX));
+        pf[p] = bload_vt<VT>(xr, ok ? 2u * e : PTG_OOB);
+        pa[p] = bload8(ar, ok ? e : PTG_OOB);
+        pq[p] = (uint32_t)(((ih & 1) << 1) | (iw & 1));
+      }
+    } else {
+      const uint32_t img = (uint32_t)(n * H * W * C) * 2u;
+#pragma unroll
+      for (int p = 0; p < PFN; ++p) {
+        const int ih = ih_first + pr_r[p], iw = iw0 + pr_c[p];
+        const bool ok = pr_r[p] < nrows && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+        pf[p] = bload_vt<VT>(xr, ok ? img + (uint32_t)((ih * W + iw) * C + (pr_l[p] - pr_c[p] * PIX)) * 2u : PTG_OOB);
+      }
     }
   };
   auto store_rows = [&](int nrows, int slot_first) {
@@ -257,8 +297,10 @@ __global__ __launch_bounds__(256) void conv_fwd_strip_k(const bf16_t* __restrict
         int slot = slot_first + pr_r[p];
         if constexpr (RING) slot = slot >= HR ? slot - HR : slot;
         bf16_t* dst = smem + slot * ROWE + pr_l[p];
-        *(VT*)dst = pf[p];
-        if constexpr (RING) *(VT*)(dst + HR * ROWE) = pf[p];
+        VT v = pf[p];
+        if constexpr (SPIN) v = sparse_select(v, pa[p], pq[p]);
+        *(VT*)dst = v;
+        if constexpr (RING) *(VT*)(dst + HR * ROWE) = v;
       }
     }
   };
@@ -1179,14 +1221,14 @@ static int wq_chunk(long tiles, int groups) {
   return (int)(c < 4 ? 4 : c);
 }
 
-template <int C, int KS, int NF, int TW, int TH, int E, bool WLDS, int COS>
+template <int C, int KS, int NF, int TW, int TH, int E, bool WLDS, int COS, bool SPIN = false>
 static int launch_fwd_k(const void* x, const void* w, const float* bias, const float* alpha, void* z, void* aux, void* arg,
                         int N, int H, int W, int Cout, int pad, hipStream_t s) {
   constexpr bool RING = TH < 2 * (KS - 1);
   constexpr int KTOT = KS * Kwp<C, KS>::v * C, KSTEPS = (KTOT + 31) / 32, MFR = TH * TW / 16;
   constexpr bool WREG = KSTEPS * NF <= 8;
   constexpr bool KSPLIT = !WLDS && !WREG && MFR / 4 <= 2 && MFR * NF <= 16;
-  const auto kern = conv_fwd_strip_k<C, KS, NF, TW, TH, E, RING, KSPLIT, WLDS, COS>;
+  const auto kern = conv_fwd_strip_k<C, KS, NF, TW, TH, E, RING, KSPLIT, WLDS, COS, SPIN>;
   static const int resident = ptg_resident_blocks((const void*)kern);
   const int th = (H + TH - 1) / TH, tw = (W + TW - 1) / TW;
   const long tiles = (long)N * tw * th;
@@ -1217,7 +1259,7 @@ static bool conv_wlds_enabled() {
   return on;
 }
 
-template <int C, int KS, int NF, int TW, int TH, int E>
+template <int C, int KS, int NF, int TW, int TH, int E, bool SPIN = false>
 static int launch_fwd_e(const void* x, const void* w, const float* bias, const float* alpha, void* z, void* aux, void* arg, int N,
                         int H, int W, int Cout, int pad, hipStream_t s) {
   constexpr int KTOT = KS * Kwp<C, KS>::v * C, KSTEPS = (KTOT + 31) / 32;
@@ -1231,12 +1273,12 @@ static int launch_fwd_e(const void* x, const void* w, const float* bias, const f
     constexpr int WB = NF * 16 * (KSTEPS * 32 + 8) * 2;
     if (conv_wlds_enabled()) {
       if constexpr (HALO_B + WB <= 150 * 1024)
-        return launch_fwd_k<C, KS, NF, TW, TH, E, true, 1>(x, w, bias, alpha, z, aux, arg, N, H, W, Cout, pad, s);
+        return launch_fwd_k<C, KS, NF, TW, TH, E, true, 1, SPIN>(x, w, bias, alpha, z, aux, arg, N, H, W, Cout, pad, s);
       else if constexpr (NF % 2 == 0 && HALO_B + WB / 2 <= 150 * 1024)
-        return launch_fwd_k<C, KS, NF / 2, TW, TH, E, true, 2>(x, w, bias, alpha, z, aux, arg, N, H, W, Cout, pad, s);
+        return launch_fwd_k<C, KS, NF / 2, TW, TH, E, true, 2, SPIN>(x, w, bias, alpha, z, aux, arg, N, H, W, Cout, pad, s);
     }
   }
-  return launch_fwd_k<C, KS, NF, TW, TH, E, false, 1>(x, w, bias, alpha, z, aux, arg, N, H, W, Cout, pad, s);
+  return launch_fwd_k<C, KS, NF, TW, TH, E, false, 1, SPIN>(x, w, bias, alpha, z, aux, arg, N, H, W, Cout, pad, s);
 }
 
 template <int C, int KS, int NF, int TW, int TH>
@@ -1371,6 +1413,29 @@ int ptg_conv2d_fwd_halo(const void* x, const void* w, const float* bias, const f
   }
   if (KS == 5) return fwd_by_cin<5>(x, w, bias, alpha, z, aux, arg, N, H, W, C, Cout, pad, epi, s);
   if (KS == 3) return fwd_by_cin<3>(x, w, bias, alpha, z, aux, arg, N, H, W, C, Cout, pad, epi, s);
+  return (int)hipErrorInvalidValue;
+}
+
+// Data gradient of a 5x5 'same' conv whose output was 2x2-pooled, from its SPARSE dZ record:
+// dzsel / argq [N][H/2][W/2][C] (dZ at each window's argmax, the argmax q); wf = the flipped filter
+// [Cout][5][5][C]; dx [N][H][W][Cout] (bf16).  C in {16, 32} (CNN-B1 layers 2 / 3), Cout <= 64.
+int ptg_conv2d_dgrad_halo_sparse(const void* dzsel, const void* argq, const void* wf, void* dx, int N, int H, int W,
+                                 int C, int Cout, int KS, int pad, hipStream_t s) {
+  if (KS != 5 || (H & 1) || (W & 1) || Cout % 8 || Cout > 64 || !ptg_fits_2g((long)N * H * W * Cout * 2))
+    return (int)hipErrorInvalidValue;
+  const int NF = Cout <= 16 ? 1 : (Cout <= 32 ? 2 : 4);
+#define PTG_SPD(CV, TWV, THV)                                                                                        \
+  {                                                                                                                  \
+    if (NF == 1) return launch_fwd_e<CV, 5, 1, TWV, THV, EPI_Z, true>(dzsel, wf, nullptr, nullptr, dx, nullptr,       \
+                                                                      (void*)argq, N, H, W, Cout, pad, s);          \
+    if (NF == 2) return launch_fwd_e<CV, 5, 2, TWV, THV, EPI_Z, true>(dzsel, wf, nullptr, nullptr, dx, nullptr,       \
+                                                                      (void*)argq, N, H, W, Cout, pad, s);          \
+    return launch_fwd_e<CV, 5, 4, TWV, THV, EPI_Z, true>(dzsel, wf, nullptr, nullptr, dx, nullptr, (void*)argq, N, H, \
+                                                         W, Cout, pad, s);                                          \
+  }
+  if (C == 16) PTG_SPD(16, 16, 8)
+  if (C == 32) PTG_SPD(32, 8, 16)
+#undef PTG_SPD
   return (int)hipErrorInvalidValue;
 }
 

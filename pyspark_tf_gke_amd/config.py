@@ -85,6 +85,13 @@ _K = [
          "GradientTape loops: big Dense dW deferred to apply_gradients and fused with Adam (computed on first read)"),
     Knob("raw_u8_input", bool, True, "PTG_RAW_U8_INPUT", None, "first conv reads the uint8 image batch directly"),
     Knob("sparse_first", bool, True, "PTG_SPARSE_FIRST", None, "first conv layer keeps a sparse pool record"),
+    Knob("sparse_pool", bool, True, "PTG_SPARSE_POOL", None,
+         "pooled 5x5 conv layers after the first (CNN-B1 layers 2-3) keep only the sparse pool record: the "
+         "forward writes z at the window argmax + the argmax, the PReLU/pool backward writes dZ at the argmax, "
+         "and the weight and data gradients expand it in their halo loaders (no full-resolution z or dZ). "
+         "b256 A/B: 1.4044/1.4018 vs 1.4300/1.4257 ms (profiles/r6_ab_sparse_pool_record.txt)"),
+    Knob("sparse_pool_min_batch", int, 128, "PTG_SPARSE_POOL_MIN_BATCH", None,
+         "sparse_pool only from this batch size (b64: 0.6958/0.6841 vs 0.6848/0.6801 ms, b32 within noise)"),
     Knob("bn_relu_bits", bool, True, "PTG_BN_RELU_BITS", None,
          "residual BN + ReLU: the backward reads a 1-bit ReLU mask written by the forward instead of y"),
     Knob("bn_bwd_epi_stats", bool, True, "PTG_BN_BWD_EPI_STATS", None,

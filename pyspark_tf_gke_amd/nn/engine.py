@@ -39,6 +39,10 @@ _HOST_FP32 = [config.get("host_fp32")]
 # LDS, so the full-resolution z and dZ (335 MB each for CNN-B1 at batch 256) never exist.  Measured
 # on CNN-B1 b256: 118.6k vs 116.6k samples/s with the dense first-layer record.
 SPARSE_FIRST = config.get("sparse_first")
+# Pooled layers after the first: sparse pool record end to end (forward record, sparse dZ record,
+# weight and data gradients expanding it in their loaders) - no full-resolution z / dZ in HBM.
+SPARSE_POOL = config.get("sparse_pool")
+SPARSE_POOL_MIN_BATCH = config.get("sparse_pool_min_batch")
 # That first layer reads the raw uint8 [N,H,W,3] image batch itself (conv.hip U8 loaders: /255 and
 # the zero 4th channel applied in registers) in both its forward and its weight gradient, so the
 # packed bf16 copy of the input (pack_u8rgb4_k: 3 B read + 8 B written per pixel, 8 B read twice
@@ -211,8 +215,15 @@ class ConvOp(Op):
         OH, OW, Co = self.conv.out_shape
         dev = x.device
         b = self.conv.bias.data if self.conv.bias is not None else None
-        self._sparse = False
+        self._sparse = self._sp2 = False
         halo_ok = self._halo()[0] and not (self.pool is not None and (OH % 2 or OW % 2))
+        if (SPARSE_POOL and B >= SPARSE_POOL_MIN_BATCH and halo_ok and self.pool is not None and x.is_cuda
+                and not self.first and self.stride == 1
+                and self.conv.kernel_size == (5, 5) and self._halo()[1]
+                and K.dgrad_sparse_supported(Co, self.conv.cin_p, 5)):
+            self._sel, self._sp2 = False, True
+            self._x = x
+            return self._forward_pool_sparse(x, b, ws, B, OH, OW, Co, dev)
         self._sel = halo_ok and self.pool is not None and x.is_cuda and self.first and SPARSE_FIRST \
             and self.conv.kernel_size[0] == 5
         if halo_ok and self.pool is not None and x.is_cuda and self._sel:
@@ -293,6 +304,24 @@ class ConvOp(Op):
         K.conv2d_wgrad_halo_sparse(x, dzs, self._arg, self.pad, self.conv.kernel.grad, zeroed=True)
         return None
 
+    def _backward_sparse_record(self, x, dy, ws, dev):
+        """Pooled layer with a sparse record (SPARSE_POOL): dZ at each window's argmax, then the
+        weight gradient (side stream) and the data gradient both expand it in their loaders."""
+        C = self._zshape[-1]
+        bias_g = self.conv.bias.grad if self.conv.bias is not None else \
+            ws.get(self.name + "/nobias", (C,), torch.float32, dev)
+        dalpha = self.prelu.alpha.grad if self.prelu is not None else \
+            ws.get(self.name + "/dalpha_dummy", self._zshape[1:], torch.float32, dev)
+        dzs = ws.get(self.name + "/dzsel", self._zs.shape, torch.bfloat16, dev)
+        arg = self._arg
+        K.prelu_pool_bwd_sel(dy, self._zs, arg, self._pool_alpha(ws, dev), dzs, dalpha, bias_g)
+        g = self.conv.kernel.grad
+        S.launch(lambda: K.conv2d_wgrad_halo_sparse(x, dzs, arg, self.pad, g, zeroed=True), dev)
+        dx = ws.get(self.name + "/dx", x.shape, torch.bfloat16, dev)
+        K.conv2d_dgrad_halo_sparse(dzs, arg, self.conv.kernel.bf16, self.pad, dx, self._wflip_buf(ws, dev),
+                                   flipped=getattr(self, "_wf_ready", False))
+        return dx
+
     def _backward_fused1(self, x, dy, ws, dev):
         """First layer, conv1.hip: one kernel from the pooled gradient to dW / dalpha / dbias."""
         OH, OW, Co = self.conv.out_shape
@@ -335,6 +364,8 @@ class ConvOp(Op):
             return self._backward_fused1(x, dy, ws, dev)
         if getattr(self, "_sel", False):
             return self._backward_sel(x, dy, ws, dev)
+        if getattr(self, "_sp2", False):
+            return self._backward_sparse_record(x, dy, ws, dev)
         zshape = self._zshape if self._sparse else self._z.shape
         dz = ws.get(self.name + "/dz", zshape, torch.bfloat16, dev)
         bias_g = self.conv.bias.grad if self.conv.bias is not None else \

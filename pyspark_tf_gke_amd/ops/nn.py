@@ -453,6 +453,30 @@ def conv2d_dgrad_halo(dz, w, pad: int, out, wflip_buf, flipped: bool = False):
     return conv2d_fwd_fused(dz, wflip_buf, None, KS - 1 - pad, out)
 
 
+def conv2d_dgrad_halo_sparse(dzsel, arg, w, pad: int, out, wflip_buf, flipped: bool = False):
+    """dx = d(conv)/dx (stride-1 'same', 5x5) of a layer whose output was 2x2-pooled, with dZ given
+    as its sparse pool record (dzsel / arg [N,H/2,W/2,Cout], see conv2d_wgrad_halo_sparse): the halo
+    loader of the strip kernel expands it, so the full-resolution dZ is never materialised."""
+    N, H, W, Cin = out.shape
+    Cout, KS, _, Cw = w.shape
+    assert Cw == Cin and tuple(dzsel.shape) == (N, H // 2, W // 2, Cout) and tuple(arg.shape) == tuple(dzsel.shape)
+    if not on_device(dzsel):
+        dz = ref.expand_pool_record(dzsel, arg, (N, H, W, Cout)).to(dzsel.dtype)
+        return ref.conv2d_dgrad(dz, w, pad, out)
+    need(dzsel, torch.bfloat16, "dgrad_sparse.dzsel"); need(arg, torch.uint8, "dgrad_sparse.arg")
+    need(out, torch.bfloat16, "dgrad_sparse.out")
+    if not flipped:
+        conv_flip_weights(w, wflip_buf)
+    hip("ptg_conv2d_dgrad_halo_sparse", ptr(dzsel), ptr(arg), ptr(wflip_buf), ptr(out), N, H, W, Cout, Cin, KS,
+        KS - 1 - pad)
+    return out
+
+
+def dgrad_sparse_supported(Cout: int, Cin: int, KS: int) -> bool:
+    """ptg_conv2d_dgrad_halo_sparse covers this layer (dZ channels Cout, dx channels Cin)."""
+    return KS == 5 and Cout in (16, 32) and Cin % 8 == 0 and Cin <= 64
+
+
 def gemm(M, N, K, a, lda, a_kcontig, b, ldb, b_kcontig, epi, c, ldc, bias=None, act=0, splits=1):
     hip("ptg_gemm_bf16", M, N, K, ptr(a), lda, int(a_kcontig), ptr(b), ldb, int(b_kcontig), epi, ptr(c), ldc,
         ptr(bias), act, splits)

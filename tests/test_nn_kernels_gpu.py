@@ -781,3 +781,53 @@ def test_adam_multi_ranges_and_flips():
         assert torch.equal(a, b)
     assert torch.equal(outs[0][0][1024:1536], p0[1024:1536]) and torch.equal(outs[0][1][1024:1536], g0[1024:1536])
     assert outs[0][1][:1024].abs().max() == 0
+
+
+@pytest.mark.parametrize("N,H,W,Co,Ci", [(3, 16, 40, 16, 8), (2, 32, 48, 32, 16), (5, 12, 20, 16, 16)])
+def test_dgrad_halo_sparse_matches_dense(N, H, W, Co, Ci):
+    """conv.hip SPIN loader: the data gradient from the sparse pool record (dzsel / argq, expanded in
+    the halo loader) equals the dense data gradient of the expanded dZ - the same MFMA math on the
+    same values, so the outputs are identical - and both match the fp32 reference."""
+    torch.manual_seed(7)
+    shp = (N, H // 2, W // 2, Co)
+    dzs = rnd(*shp)
+    arg = torch.randint(0, 4, shp, dtype=torch.uint8)
+    w = rnd(Co, 5, 5, Ci, scale=0.1)
+    dz = R.expand_pool_record(dzs.float(), arg, (N, H, W, Co)).bfloat16()
+    d_dense = torch.empty(N, H, W, Ci, dtype=torch.bfloat16, device=DEV)
+    d_sparse = torch.empty_like(d_dense)
+    wf = torch.empty(Ci, 5, 5, Co, dtype=torch.bfloat16, device=DEV)
+    K.conv2d_dgrad_halo(dz.to(DEV), w.to(DEV), 2, d_dense, wf)
+    K.conv2d_dgrad_halo_sparse(dzs.to(DEV), arg.to(DEV), w.to(DEV), 2, d_sparse, wf, flipped=True)
+    torch.cuda.synchronize()
+    assert torch.equal(d_sparse.cpu(), d_dense.cpu()), "sparse-record dgrad differs from the dense one"
+    ref = torch.empty(N, H, W, Ci)
+    R.conv2d_dgrad(dz.float(), w.float(), 2, ref)
+    _close(d_sparse, ref, 2e-2, 2e-2, "dgrad_sparse")
+
+
+def test_sparse_pool_record_model_grads(monkeypatch):
+    """CNN-B1-shaped model with the sparse pool record on layers 2-3 (engine.SPARSE_POOL) vs the dense
+    z / dZ path: the same argmaxes and dZ values, so every parameter gradient agrees up to summation
+    order."""
+    from pyspark_tf_gke_amd.models import build_cnn_model
+    from pyspark_tf_gke_amd.nn import engine as E
+
+    torch.manual_seed(5)
+    x = torch.rand(4, 64, 80, 3)
+    y = torch.rand(4, 2) * 50
+    grads = {}
+    for mode in (False, True):
+        monkeypatch.setattr(E, "SPARSE_POOL", mode)
+        monkeypatch.setattr(E, "SPARSE_POOL_MIN_BATCH", 1)
+        m = build_cnn_model((64, 80, 3), flat=True, summary=False, device=DEV)
+        xb, yb = m._prep_batch(x, y)
+        m.store.zero_grad()
+        out = m._run_forward(xb, True)
+        d = m._loss_grad(out, yb, m._stats_buf())
+        m._run_backward(d)
+        torch.cuda.synchronize()
+        assert sum(bool(getattr(op, "_sp2", False)) for op in m.ops) == (2 if mode else 0)
+        grads[mode] = {p.name: p.grad.detach().float().cpu().clone() for p in m.store.params}
+    for name, g in grads[False].items():
+        _close(grads[True][name], g, 1e-2, 1e-4, "sparse_pool_grad_" + name)
