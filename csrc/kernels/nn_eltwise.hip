@@ -1271,13 +1271,13 @@ int ptg_prelu_pool_bwd_sel(const void* dp, const void* zs, const void* arg, cons
   if (C % 8 || C > 256 || (H & 1) || (W & 1) || H < 2 || W < 2) return (int)hipErrorInvalidValue;
   const int npos = (H / 2) * (W / 2) * (C / 8);
   const int bx = (npos + 15) / 16;
-  if (nper <= 0) {  // >= 64 samples per chunk (4 chunks of 64 samples for the first layer were slower:
-    //                 173 vs 134 us, dalpha atomics), and at most one wave of resident workgroups: a
-    //                 second, partial wave (CNN-B1 layer 3 at b256: 1280 blocks for 1024 slots) ran the
-    //                 latency-bound tail at a quarter occupancy (PTG_SEL_FILL=0: the old >= 1024 rule)
-    static const int res = ptg_resident_blocks((const void*)prelu_pool_bwd_sel_k);
-    static const bool fill = [] { const char* e = getenv("PTG_SEL_FILL"); return !(e && e[0] == '0'); }();
-    int chunks = fill ? res / bx : (1024 + bx - 1) / bx;
+  if (nper <= 0) {  // samples per chunk: a block's fixed cost (alpha loads, the dalpha reduction over
+    //                 its sample groups, one RMW / atomic per (position, channel, q)) is amortised over
+    //                 nper samples, so few chunks - ~400 blocks - beat filling the device
+    //                 (tools/sel_bench.py, b256, us by nper: layer 2 64: 101.5, 128: 88.6, 256: 67.1;
+    //                 layer 3 64: 59.8, 128: 43.1, 256: 45.9; layer 4 64: 38.6, 128: 31.2, 256: 41.6),
+    //                 and >= 64 samples per chunk (the first layer: 173 vs 134 us at 4 chunks of 64)
+    int chunks = std::max(1, 400 / bx);
     chunks = std::max(1, std::min(chunks, N / 64));
     nper = (N + chunks - 1) / chunks;
   }
