@@ -25,6 +25,9 @@ L = [(256, 320, 3, 8, True), (128, 160, 8, 16, True), (64, 80, 16, 32, True), (3
      (16, 20, 64, 64, False)]
 
 
+SPARSE: set = set()  # conv layers (2..5) running the sparse pool record (--sparse-layers)
+
+
 def ops(B):
     bf, f32 = 2, 4
     o = {}
@@ -39,6 +42,12 @@ def ops(B):
     for i in range(1, 5):
         H, W, ci, co, pool = L[i]
         out_hw = (H // 2) * (W // 2) if pool else H * W
+        if i + 1 in SPARSE:  # sparse pool record (engine SPARSE_POOL): no full-resolution z / dZ
+            o[f"L{i + 1} fwd"] = (cf(i), B * H * W * ci * bf + B * out_hw * co * (bf + bf + 1))
+            o[f"L{i + 1} dgrad"] = (cf(i), B * out_hw * co * (bf + 1) + B * H * W * ci * bf)
+            o[f"L{i + 1} wgrad"] = (cf(i), B * H * W * ci * bf + B * out_hw * co * (bf + 1))
+            o[f"L{i + 1} PReLU+pool bwd"] = (0.0, B * out_hw * co * (bf + bf + 1 + bf))
+            continue
         o[f"L{i + 1} fwd"] = (cf(i), B * H * W * ci * bf + B * H * W * co * bf + B * out_hw * co * bf)
         o[f"L{i + 1} dgrad"] = (cf(i), B * H * W * co * bf + B * H * W * ci * bf)
         o[f"L{i + 1} wgrad"] = (cf(i), B * H * W * ci * bf + B * H * W * co * bf)
@@ -57,7 +66,7 @@ def classify(name, ppb_seen):
     m = re.search(r"conv_fwd_strip_k<(\d+), 5, (\d+), \d+, \d+, (\d+)", name)
     if m:
         C, NF, E = int(m.group(1)), int(m.group(2)), int(m.group(3))
-        if E in (1, 2):
+        if E in (1, 2, 3):
             return {8: "L2 fwd", 16: "L3 fwd", 32: "L4 fwd", 64: "L5 fwd"}.get(C)
         return {16: "L2 dgrad", 32: "L3 dgrad", 64: "L4 dgrad" if NF == 2 else "L5 dgrad"}.get(C)
     m = re.search(r"conv32_k<(\d+), (\d+), (\d+)", name)
@@ -106,7 +115,11 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--step", type=int, default=-2)
     ap.add_argument("--serial", action="store_true", help="label: the trace is of a serialized run (PTG_SIDE_STREAM=0)")
+    ap.add_argument("--sparse-layers", default=None,
+                    help="conv layers on the sparse pool record (default: 2,3 from batch 128, as the engine)")
     a = ap.parse_args()
+    sl = a.sparse_layers if a.sparse_layers is not None else ("2,3" if a.batch >= 128 else "")
+    SPARSE.update(int(v) for v in sl.split(",") if v)
     rows = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r["Start_Timestamp"]))
     starts = [i for i, r in enumerate(rows) if "conv1_fwd" in r["Kernel_Name"]]
     s, e = starts[a.step - 1], starts[a.step]
