@@ -722,6 +722,12 @@ __global__ __launch_bounds__(256) void conv_wgrad_strip_k(const bf16_t* __restri
   for (int i = 0; i < MF; ++i)
 #pragma unroll
     for (int j = 0; j < NB; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  // KSEP (32 % TW == 0): a k0 block of 32 pixels starts a tile row, so the pixel of a lane's
+  // tr-read rows splits into k0's rows (compile-time) + the lane's own (row, column) below
+  constexpr bool KSEP = 32 % TW == 0;
+  const int lp0 = 8 * g + q, lp1 = lp0 + 4;
+  const int hl0 = ((lp0 / TW) * HC + lp0 % TW) * PIX, hl1 = ((lp1 / TW) * HC + lp1 % TW) * PIX;
+  const int dl0 = lp0 * DPITCH, dl1 = lp1 * DPITCH;
 
   // halo slots of this thread
   int pr_r[PFN], pr_c[PFN], pr_l[PFN];
@@ -861,6 +867,45 @@ __global__ __launch_bounds__(256) void conv_wgrad_strip_k(const bf16_t* __restri
     if (has_next) load_tile(n2, twi2, th2, nrows2, ih2);
 
     const int wrow = RING ? (th * TH) % HR : 0;
+    if constexpr (KSEP) {
+      // fully unrolled: every read address = a per-tile base (lane + ring row) + a compile-time
+      // offset of k0, so the loop is tr-reads and MFMAs only (the rolled form spent ~40 VALU ops per
+      // 4 MFMAs on addresses and selects, and rotated the accumulators through AGPR moves)
+      const int hw = wrow * HC * PIX;
+      const bf16_t* hb0[NB];
+      const bf16_t* hb1[NB];
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        hb0[j] = smem + hw + hl0 + boff[j];
+        hb1[j] = smem + hw + hl1 + boff[j];
+      }
+#pragma unroll
+      for (int k0 = 0; k0 < M; k0 += 32) {
+        const int kr = (k0 / TW) * HC * PIX;  // compile-time after unrolling
+        // (columns past KF read real halo data through boff's kk = 0 fallback: their outputs are
+        // never flushed, see the epilogue)
+        bf16x8_t af[MF];
+#pragma unroll
+        for (int i = 0; i < MF; ++i) {
+          const int co = i * 16 + 4 * p;
+          const s16x4_t lo = tr_read(ds + dl0 + k0 * DPITCH + co);
+          const s16x4_t hi = tr_read(ds + dl1 + k0 * DPITCH + co);
+          const U2 a = __builtin_bit_cast(U2, lo), b = __builtin_bit_cast(U2, hi);
+          U4 v; v.x = a.x; v.y = a.y; v.z = b.x; v.w = b.y;
+          af[i] = __builtin_bit_cast(bf16x8_t, v);
+        }
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          const s16x4_t lo = tr_read(hb0[j] + kr);
+          const s16x4_t hi = tr_read(hb1[j] + kr);
+          const U2 a = __builtin_bit_cast(U2, lo), b = __builtin_bit_cast(U2, hi);
+          U4 v; v.x = a.x; v.y = a.y; v.z = b.x; v.w = b.y;
+          const bf16x8_t bfr = __builtin_bit_cast(bf16x8_t, v);
+#pragma unroll
+          for (int i = 0; i < MF; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[i][j], 0, 0, 0);
+        }
+      }
+    } else
 #pragma unroll 2
     for (int k0 = 0; k0 < M; k0 += 32) {
       // rows of the two tr-reads of this lane group: pixels k0 + 8g + q and k0 + 8g + 4 + q
