@@ -1396,7 +1396,8 @@ static int wg_small_n() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("PTG_WG_SMALL_N");
-    v = e && *e ? atoi(e) : 64;
+    v = e && *e ? atoi(e) : 0;  // 0 since the unrolled (KSEP) loop: the large-batch tiles win at
+    //                              b32 / b64 too (profiles/r6_ab_wgrad_small_tiles_after_unroll.txt)
   }
   return v;
 }
