@@ -536,3 +536,25 @@ def test_tape_abandoned_head_prediction_does_not_leak():
     with nn.GradientTape():
         l2 = mse(y, m2(x, training=True))
     assert abs(float(l1) - float(l2)) <= 1e-6 * max(1.0, abs(float(l2)))
+
+
+def test_sparse_pool_record_dgrad_cpu_fallback_matches_dense():
+    """ops.nn.conv2d_dgrad_halo_sparse off the GPU: the data gradient of the expanded sparse pool
+    record equals the dense data gradient (the reference the GPU kernel is tested against)."""
+    from pyspark_tf_gke_amd.ops import nn as K
+    from pyspark_tf_gke_amd.ops import reference as R
+
+    torch.manual_seed(3)
+    N, H, W, Co, Ci = 2, 8, 12, 16, 8
+    dzs = torch.randn(N, H // 2, W // 2, Co).bfloat16()
+    arg = torch.randint(0, 4, (N, H // 2, W // 2, Co), dtype=torch.uint8)
+    w = (torch.randn(Co, 5, 5, Ci) * 0.1).bfloat16()
+    out = torch.empty(N, H, W, Ci)
+    K.conv2d_dgrad_halo_sparse(dzs, arg, w, 2, out, None)
+    ref = torch.empty(N, H, W, Ci)
+    R.conv2d_dgrad(R.expand_pool_record(dzs, arg, (N, H, W, Co)), w, 2, ref)
+    assert torch.allclose(out, ref, atol=1e-5)
+    # the record keeps exactly one value per window and channel
+    dense = R.expand_pool_record(dzs, arg, (N, H, W, Co))
+    win = dense.reshape(N, H // 2, 2, W // 2, 2, Co)
+    assert int((win != 0).sum(dim=(2, 4)).max()) <= 1
