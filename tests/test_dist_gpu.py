@@ -375,8 +375,9 @@ from pyspark_tf_gke_amd.sql.table import ColumnVector, Table
 from pyspark_tf_gke_amd.ml import KMeans, VectorAssembler
 from pyspark_tf_gke_amd.cli.train import _ps_loop, make_parameter_server_strategy
 from pyspark_tf_gke_amd.data import Dataset
-from pyspark_tf_gke_amd.models import build_deep_model
+from pyspark_tf_gke_amd.models import build_cnn_model, build_deep_model
 
+UPD = {}
 calls = {}
 def counting(name, fn):
     def f(*a, **k):
@@ -427,14 +428,35 @@ def run(forced):
         metrics = [nn.metrics.Mean("loss"), nn.metrics.SparseCategoricalAccuracy("accuracy")]
     h = _ps_loop(mm, ps, ds_fn, 4, 2, nn.losses.SparseCategoricalCrossentropy(), opt, metrics, lambda e, v: str(v))
     out["ps_loss"] = h["loss"]; out["ps_sum"] = float(sum(float(np.asarray(w, dtype=np.float64).sum()) for w in mm.get_weights()))
+    # a big-Dense CNN through the same one-worker PS tape loop (ADVICE r5): with the collectives forced
+    # the tape must not defer the Dense dW (the push would copy it before it exists)
+    ps2 = make_parameter_server_strategy(1, 1, chief_addr="127.0.0.1")
+    rng2 = np.random.default_rng(5)
+    Xi = rng2.random((32, 64, 80, 3)).astype(np.float32); yi = (rng2.random((32, 2)) * 50).astype(np.float32)
+    def ds2(ctx=None):
+        return Dataset.from_tensor_slices((Xi, yi)).batch(8).repeat()
+    with ps2.scope():
+        torch.manual_seed(0)
+        cm = build_cnn_model((64, 80, 3), flat=True, summary=False, device=dev)
+        copt = nn.optimizers.Adam(1e-3)
+        cmet = [nn.metrics.Mean("loss")]
+    big0 = np.asarray(max(cm.get_weights(), key=lambda w: np.asarray(w).size), dtype=np.float64).copy()
+    h2 = _ps_loop(cm, ps2, ds2, 2, 2, nn.losses.MeanSquaredError(), copt, cmet, lambda e, v: str(v))
+    ps2.synchronize_master(cm)  # the forced path keeps only the bf16 copy of the big segment current
+    big1 = np.asarray(max(cm.get_weights(), key=lambda w: np.asarray(w).size), dtype=np.float64)
+    UPD[forced] = (big1 - big0).ravel()
+    out["cnn_loss"] = h2["loss"]
     torch.cuda.synchronize()
     out["calls_groupby"] = calls_gb; out["calls"] = dict(calls)
     return out
 
 a = run(True)
 b = run(False)
-print("RESULT", json.dumps({"backend": dist.get_backend(), "world": dist.get_world_size(), "forced": a, "plain": b}),
-      flush=True)
+ua, ub = UPD[True], UPD[False]
+upd = {"norm_forced": float(np.linalg.norm(ua)), "norm_plain": float(np.linalg.norm(ub)),
+       "cos": float(ua @ ub / (np.linalg.norm(ua) * np.linalg.norm(ub) + 1e-30))}
+print("RESULT", json.dumps({"backend": dist.get_backend(), "world": dist.get_world_size(), "forced": a, "plain": b,
+                            "dense_update": upd}), flush=True)
 """
 
 
@@ -466,3 +488,9 @@ def test_single_rank_rccl_every_collective_site(hip_built):
     assert a["km_cost"] == pytest.approx(b["km_cost"], rel=1e-5)
     assert a["strings"] == b["strings"] == ["b", "a", "c"]
     assert a["ps_loss"] == pytest.approx(b["ps_loss"], rel=1e-5) and a["ps_sum"] == pytest.approx(b["ps_sum"], rel=1e-6)
+    # big-Dense CNN through the PS tape loop: the forced-collectives run (no deferred Dense dW) updates
+    # the Dense kernel like the local run (a pushed-before-computed gradient would leave it at zero /
+    # stale - cosine far below 1)
+    u = v["dense_update"]
+    assert u["norm_forced"] > 0 and u["norm_plain"] > 0 and u["cos"] > 0.9, u
+    assert a["cnn_loss"] == pytest.approx(b["cnn_loss"], rel=1e-2), (a["cnn_loss"], b["cnn_loss"])
