@@ -330,7 +330,8 @@ static int launch(const void* x, const void* w, const float* bias, const float* 
   const int mode = c32_mode();
   constexpr int CH2 = C >= 64 ? C / 2 : C;
   // 160-pixel tiles when the 320-pixel grid would not give every CU two workgroups
-  const bool small = mode != 0 && (320 / (W > 0 ? W : 1)) > 0 && (long)N * (H / (320 / W)) < 512 &&
+  // (PTG_C32_SPLIT=2: 160-pixel tiles at every grid size, A/B)
+  const bool small = mode != 0 && (320 / (W > 0 ? W : 1)) > 0 && (mode == 2 || (long)N * (H / (320 / W)) < 512) &&
                      W <= 160 && 160 % W == 0 && H % (160 / W) == 0 && (EPI != EPI_POOL || ((160 / W) % 2 == 0));
   if (mode == 0) return launch_t<C, CO, EPI, C, 2>(x, w, bias, alpha, z, aux, N, H, W, Cout, s);
   if (small) return launch_t<C, CO, EPI, CH2, 1>(x, w, bias, alpha, z, aux, N, H, W, Cout, s);
